@@ -1,0 +1,546 @@
+"""ORACLE (test infrastructure only) — CPU fp32 restatement of Swin + Mask2Former.
+
+The whole model of the north-star path, written against the oracle ops in
+`oracle/ref_ops.py`.  Parameter names follow the build's canonical layout (the one the
+product model in `vision-instance-seg_amd/visionseg/model.py` also uses), so one state
+dict drives both.  Every block cites the HF oracle line it restates (transformers
+5.15.0, see oracle/__init__.py).  It is the parity oracle on the GPU box and the timed
+`cpu_baseline` of bench.py; it is never on the product path.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, asdict
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ref_ops as R
+
+
+@dataclass
+class RefConfig:
+    embed_dim: int = 96
+    depths: tuple = (2, 2, 6, 2)
+    num_heads: tuple = (3, 6, 12, 24)
+    window_size: int = 7
+    mlp_ratio: float = 4.0
+    feature_size: int = 256
+    mask_feature_size: int = 256
+    hidden_dim: int = 256
+    enc_ffn: int = 1024
+    dec_ffn: int = 2048
+    dec_heads: int = 8
+    enc_layers: int = 6
+    dec_layers: int = 10          # HF counts the initial prediction (decoder has dec_layers-1 layers)
+    num_queries: int = 100
+    num_labels: int = 1
+    n_points: int = 4
+    n_levels: int = 3
+    # criterion (HF:m2f-cfg defaults)
+    no_object_weight: float = 0.1
+    class_weight: float = 2.0
+    mask_weight: float = 5.0
+    dice_weight: float = 5.0
+    train_num_points: int = 12544
+    oversample_ratio: float = 3.0
+    importance_sample_ratio: float = 0.75
+
+    @staticmethod
+    def from_dict(d):
+        d = dict(d)
+        for k in ("depths", "num_heads"):
+            if k in d:
+                d[k] = tuple(d[k])
+        return RefConfig(**{k: v for k, v in d.items() if k in RefConfig.__dataclass_fields__})
+
+    def to_dict(self):
+        d = asdict(self)
+        d["depths"] = list(self.depths)
+        d["num_heads"] = list(self.num_heads)
+        return d
+
+
+# ----------------------------------------------------------------------------------
+# Swin backbone (HF:swin)
+# ----------------------------------------------------------------------------------
+
+
+def _partition(x, ws, shift):
+    """torch form of ref_ops.window_partition_np (autograd-capable)."""
+    B, H, W, C = x.shape
+    Hp, Wp = R.padded_size(H, ws), R.padded_size(W, ws)
+    x = F.pad(x, (0, 0, 0, Wp - W, 0, Hp - H))
+    if shift > 0:
+        x = torch.roll(x, shifts=(-shift, -shift), dims=(1, 2))
+    x = x.view(B, Hp // ws, ws, Wp // ws, ws, C).transpose(2, 3)
+    return x.reshape(-1, ws * ws, C)
+
+
+def _reverse(win, B, H, W, ws, shift):
+    C = win.shape[-1]
+    Hp, Wp = R.padded_size(H, ws), R.padded_size(W, ws)
+    x = win.view(B, Hp // ws, Wp // ws, ws, ws, C).transpose(2, 3).reshape(B, Hp, Wp, C)
+    if shift > 0:
+        x = torch.roll(x, shifts=(shift, shift), dims=(1, 2))
+    return x[:, :H, :W].contiguous()
+
+
+class RefWindowAttention(nn.Module):
+    """HF:swin:401-468 with q/k/v fused into one `qkv` Linear (rows q;k;v)."""
+
+    def __init__(self, dim, heads, ws):
+        super().__init__()
+        self.heads, self.ws = heads, ws
+        self.qkv = nn.Linear(dim, 3 * dim)
+        self.proj = nn.Linear(dim, dim)
+        self.rel_table = nn.Parameter(torch.zeros((2 * ws - 1) ** 2, heads))
+
+
+class RefMlp(nn.Module):
+    """HF:swin:471-483 (GELU, exact erf form)."""
+
+    def __init__(self, dim, hidden, act="gelu"):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+    def forward(self, x):
+        return self.fc2(F.gelu(self.fc1(x)))
+
+
+class RefSwinBlock(nn.Module):
+    """HF:swin:508-574 (SwinLayer.forward, always_partition=True)."""
+
+    def __init__(self, dim, heads, ws, shift, mlp_ratio):
+        super().__init__()
+        self.ws, self.shift = ws, shift
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn = RefWindowAttention(dim, heads, ws)
+        self.norm2 = nn.LayerNorm(dim)
+        self.mlp = RefMlp(dim, int(dim * mlp_ratio))
+
+    def forward(self, x, H, W):
+        B, L, C = x.shape
+        ws, shift, heads = self.ws, self.shift, self.attn.heads
+        shortcut = x
+        h = self.norm1(x).view(B, H, W, C)
+        win = _partition(h, ws, shift)                               # HF:swin:546-551
+        Bw, N, _ = win.shape
+        qkv = self.attn.qkv(win).view(Bw, N, 3, heads, C // heads).permute(2, 0, 3, 1, 4)
+        mask = None
+        if shift > 0:
+            Hp, Wp = R.padded_size(H, ws), R.padded_size(W, ws)
+            mask = torch.from_numpy(R.shift_attn_mask_np(Hp, Wp, ws, shift))
+        o = R.window_attention_ref(qkv[0], qkv[1], qkv[2], self.attn.rel_table, ws, mask)
+        o = self.attn.proj(o)
+        o = _reverse(o, B, H, W, ws, shift)                          # HF:swin:558-566
+        x = shortcut + o.view(B, H * W, C)
+        return x + self.mlp(self.norm2(x))                           # HF:swin:569-572
+
+
+class RefPatchMerging(nn.Module):
+    """HF:swin:289-326."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.norm = nn.LayerNorm(4 * dim)
+        self.reduction = nn.Linear(4 * dim, 2 * dim, bias=False)
+
+    def forward(self, x, H, W):
+        B, L, C = x.shape
+        x = x.view(B, H, W, C)
+        if H % 2 == 1 or W % 2 == 1:
+            x = F.pad(x, (0, 0, 0, W % 2, 0, H % 2))
+        x = torch.cat([x[:, r::2, c::2, :] for c in range(2) for r in range(2)], dim=-1)
+        x = x.view(B, -1, 4 * C)
+        return self.reduction(self.norm(x))
+
+
+class RefStage(nn.Module):
+    def __init__(self, dim, depth, heads, ws, mlp_ratio, downsample):
+        super().__init__()
+        self.blocks = nn.ModuleList(
+            [RefSwinBlock(dim, heads, ws, 0 if i % 2 == 0 else ws // 2, mlp_ratio) for i in range(depth)])
+        self.merge = RefPatchMerging(dim) if downsample else None
+
+
+class RefPatchEmbed(nn.Module):
+    """HF:swin:247-286 + HF:swin:219-245 (norm)."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.proj = nn.Conv2d(3, dim, kernel_size=4, stride=4)
+        self.norm = nn.LayerNorm(dim)
+
+
+class RefSwin(nn.Module):
+    """HF:swin:1070-1140 (SwinBackbone.forward, always_partition, pre-downsample maps)."""
+
+    def __init__(self, cfg: RefConfig):
+        super().__init__()
+        C = cfg.embed_dim
+        self.patch_embed = RefPatchEmbed(C)
+        n = len(cfg.depths)
+        self.stages = nn.ModuleList([
+            RefStage(C * 2 ** i, cfg.depths[i], cfg.num_heads[i], cfg.window_size, cfg.mlp_ratio, i < n - 1)
+            for i in range(n)])
+        self.out_norms = nn.ModuleList([nn.LayerNorm(C * 2 ** i) for i in range(n)])
+
+    def forward(self, pixel_values):
+        x = pixel_values
+        H, W = x.shape[-2:]
+        if W % 4:
+            x = F.pad(x, (0, 4 - W % 4))
+        if H % 4:
+            x = F.pad(x, (0, 0, 0, 4 - H % 4))
+        x = self.patch_embed.proj(x)
+        B, C, H, W = x.shape
+        x = self.patch_embed.norm(x.flatten(2).transpose(1, 2))
+        feats = []
+        for i, st in enumerate(self.stages):
+            for blk in st.blocks:
+                x = blk(x, H, W)
+            f = self.out_norms[i](x)
+            feats.append(f.view(B, H, W, -1).permute(0, 3, 1, 2).contiguous())
+            if st.merge is not None:
+                x = st.merge(x, H, W)
+                H, W = (H + 1) // 2, (W + 1) // 2
+        return feats
+
+
+# ----------------------------------------------------------------------------------
+# Pixel decoder (HF:m2f:919-1419)
+# ----------------------------------------------------------------------------------
+
+
+class RefMSDeformAttn(nn.Module):
+    """HF:m2f:919-1014 (value/offset/weight projections + sampling + output_proj)."""
+
+    def __init__(self, d, heads, levels, points):
+        super().__init__()
+        self.d, self.heads, self.levels, self.points = d, heads, levels, points
+        self.sampling_offsets = nn.Linear(d, heads * levels * points * 2)
+        self.attention_weights = nn.Linear(d, heads * levels * points)
+        self.value_proj = nn.Linear(d, d)
+        self.output_proj = nn.Linear(d, d)
+
+    def forward(self, h, pos, ref, shapes):
+        B, S, _ = h.shape
+        q = h + pos
+        value = self.value_proj(h).view(B, S, self.heads, self.d // self.heads)
+        off = self.sampling_offsets(q).view(B, S, self.heads, self.levels, self.points, 2)
+        aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
+        aw = F.softmax(aw, -1).view(B, S, self.heads, self.levels, self.points)
+        norm = torch.tensor([[w, hh] for hh, w in shapes], dtype=torch.long)
+        loc = ref[:, :, None, :, None, :] + off / norm[None, None, None, :, None, :]
+        out = R.msda_ref(value, shapes, loc, aw)
+        return self.output_proj(out)
+
+
+class RefEncoderLayer(nn.Module):
+    """HF:m2f:1017-1103 (post-norm, ReLU FFN)."""
+
+    def __init__(self, d, ffn, heads, levels, points):
+        super().__init__()
+        self.attn = RefMSDeformAttn(d, heads, levels, points)
+        self.norm1 = nn.LayerNorm(d)
+        self.fc1 = nn.Linear(d, ffn)
+        self.fc2 = nn.Linear(ffn, d)
+        self.norm2 = nn.LayerNorm(d)
+
+    def forward(self, h, pos, ref, shapes):
+        h = self.norm1(h + self.attn(h, pos, ref, shapes))
+        return self.norm2(h + self.fc2(F.relu(self.fc1(h))))
+
+
+class ConvGN(nn.Module):
+    def __init__(self, cin, cout, k, bias):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, kernel_size=k, padding=k // 2, bias=bias)
+        self.gn = nn.GroupNorm(32, cout)
+
+    def forward(self, x):
+        return self.gn(self.conv(x))
+
+
+class RefPixelDecoder(nn.Module):
+    """HF:m2f:1236-1419 (3 MSDA levels, one FPN level at stride 4)."""
+
+    def __init__(self, cfg: RefConfig, channels):
+        super().__init__()
+        F_ = cfg.feature_size
+        self.cfg = cfg
+        self.input_proj = nn.ModuleList([ConvGN(c, F_, 1, True) for c in channels[::-1][:3]])
+        self.level_embed = nn.Parameter(torch.zeros(3, F_))
+        self.encoder = nn.ModuleList([RefEncoderLayer(F_, cfg.enc_ffn, cfg.dec_heads, 3, cfg.n_points)
+                                      for _ in range(cfg.enc_layers)])
+        self.lateral = ConvGN(channels[0], F_, 1, False)
+        self.output = ConvGN(F_, F_, 3, False)
+        self.mask_proj = nn.Conv2d(F_, cfg.mask_feature_size, kernel_size=1)
+
+    def forward(self, feats):
+        F_ = self.cfg.feature_size
+        embeds, pos = [], []
+        for lvl, x in enumerate(feats[::-1][:3]):                     # HF:m2f:1328-1332
+            embeds.append(self.input_proj[lvl](x))
+            pos.append(R.sine_pos_embed(x.shape[0], x.shape[2], x.shape[3], F_ // 2))
+        shapes = [(e.shape[2], e.shape[3]) for e in embeds]
+        h = torch.cat([e.flatten(2).transpose(1, 2) for e in embeds], 1)
+        p = torch.cat([q.flatten(2).transpose(1, 2) + self.level_embed[i].view(1, 1, -1)
+                       for i, q in enumerate(pos)], 1)
+        B = h.shape[0]
+        ref = R.reference_points(shapes, B)
+        for layer in self.encoder:
+            h = layer(h, p, ref, shapes)
+        outs, s = [], 0
+        for (Hl, Wl) in shapes:                                       # HF:m2f:1378-1391
+            outs.append(h[:, s:s + Hl * Wl].transpose(1, 2).reshape(B, -1, Hl, Wl))
+            s += Hl * Wl
+        cur = self.lateral(feats[0])                                  # HF:m2f:1394-1405
+        y = cur + F.interpolate(outs[-1], size=cur.shape[-2:], mode="bilinear", align_corners=False)
+        y = F.relu(self.output(y))
+        return self.mask_proj(y), outs
+
+
+# ----------------------------------------------------------------------------------
+# Masked-attention transformer decoder (HF:m2f:1451-2129)
+# ----------------------------------------------------------------------------------
+
+
+class RefCrossAttn(nn.Module):
+    """nn.MultiheadAttention parameters as HF:m2f:1618 registers them."""
+
+    def __init__(self, d):
+        super().__init__()
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d))
+        self.in_proj_bias = nn.Parameter(torch.zeros(3 * d))
+        self.out_proj = nn.Linear(d, d)
+
+
+class RefSelfAttn(nn.Module):
+    """HF:m2f:1451-1584 (Mask2FormerAttention)."""
+
+    def __init__(self, d):
+        super().__init__()
+        self.q_proj = nn.Linear(d, d)
+        self.k_proj = nn.Linear(d, d)
+        self.v_proj = nn.Linear(d, d)
+        self.out_proj = nn.Linear(d, d)
+
+
+class RefDecoderLayer(nn.Module):
+    """HF:m2f:1627-1684 (forward_post)."""
+
+    def __init__(self, d, ffn, heads):
+        super().__init__()
+        self.heads = heads
+        self.cross_attn = RefCrossAttn(d)
+        self.norm_cross = nn.LayerNorm(d)
+        self.self_attn = RefSelfAttn(d)
+        self.norm_self = nn.LayerNorm(d)
+        self.fc1 = nn.Linear(d, ffn)
+        self.fc2 = nn.Linear(ffn, d)
+        self.norm_ffn = nn.LayerNorm(d)
+
+    def forward(self, h, qpos, mem, mpos, blocked):
+        B, Q, D = h.shape
+        S = mem.shape[1]
+        H, d = self.heads, D // self.heads
+        W, b = self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias
+        q = F.linear(h + qpos, W[:D], b[:D]).view(B, Q, H, d).transpose(1, 2)
+        k = F.linear(mem + mpos, W[D:2 * D], b[D:2 * D]).view(B, S, H, d).transpose(1, 2)
+        v = F.linear(mem, W[2 * D:], b[2 * D:]).view(B, S, H, d).transpose(1, 2)
+        o = R.masked_attention_ref(q, k, v, blocked)
+        h = self.norm_cross(h + self.cross_attn.out_proj(o))
+        sa = self.self_attn                                           # HF:m2f:1488-1584
+        qs = sa.q_proj(h + qpos) * (d ** -0.5)
+        ks = sa.k_proj(h + qpos)
+        vs = sa.v_proj(h)
+        qs = qs.view(B, Q, H, d).transpose(1, 2)
+        ks = ks.view(B, Q, H, d).transpose(1, 2)
+        vs = vs.view(B, Q, H, d).transpose(1, 2)
+        att = torch.softmax(qs @ ks.transpose(-1, -2), -1) @ vs
+        h = self.norm_self(h + sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)))
+        return self.norm_ffn(h + self.fc2(F.relu(self.fc1(h))))
+
+
+class RefDecoder(nn.Module):
+    """HF:m2f:1801-1960 + HF:m2f:2059-2129 + mask predictor HF:m2f:2018-2056."""
+
+    def __init__(self, cfg: RefConfig):
+        super().__init__()
+        d = cfg.hidden_dim
+        self.cfg = cfg
+        self.query_feat = nn.Embedding(cfg.num_queries, d)
+        self.query_embed = nn.Embedding(cfg.num_queries, d)
+        self.level_embed = nn.Embedding(3, d)
+        self.layers = nn.ModuleList([RefDecoderLayer(d, cfg.dec_ffn, cfg.dec_heads)
+                                     for _ in range(cfg.dec_layers - 1)])
+        self.norm = nn.LayerNorm(d)
+        self.mask_embed = nn.ModuleList([nn.Linear(d, d), nn.Linear(d, d), nn.Linear(d, cfg.mask_feature_size)])
+
+    def predict(self, h, mask_features, target_hw):
+        x = self.norm(h)
+        e = F.relu(self.mask_embed[0](x))
+        e = F.relu(self.mask_embed[1](e))
+        e = self.mask_embed[2](e)
+        logits, blocked = R.mask_head_ref(e, mask_features, target_hw)
+        return x, logits, blocked
+
+    def forward(self, ms_feats, mask_features):
+        d = self.cfg.hidden_dim
+        B = mask_features.shape[0]
+        mems, mposs, sizes = [], [], []
+        for i in range(3):
+            f = ms_feats[i]
+            sizes.append(tuple(f.shape[-2:]))
+            mposs.append(R.sine_pos_embed(B, f.shape[2], f.shape[3], d // 2).flatten(2).transpose(1, 2))
+            mems.append((f.flatten(2) + self.level_embed.weight[i][None, :, None]).transpose(1, 2))
+        qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
+        h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
+        inter, logits, blocked = self.predict(h, mask_features, sizes[0])
+        inters, masks = [inter], [logits]
+        for idx, layer in enumerate(self.layers):
+            lvl = idx % 3
+            blocked = R.unblock_full_rows(blocked)
+            h = layer(h, qpos, mems[lvl], mposs[lvl], blocked)
+            inter, logits, blocked = self.predict(h, mask_features, sizes[(idx + 1) % 3])
+            inters.append(inter)
+            masks.append(logits)
+        return inters, masks
+
+
+class RefMask2Former(nn.Module):
+    """Mask2FormerForUniversalSegmentation forward (HF:m2f:2332-2480) without the loss."""
+
+    def __init__(self, cfg: RefConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.backbone = RefSwin(cfg)
+        chans = [cfg.embed_dim * 2 ** i for i in range(len(cfg.depths))]
+        self.pixel_decoder = RefPixelDecoder(cfg, chans)
+        self.decoder = RefDecoder(cfg)
+        self.class_head = nn.Linear(cfg.hidden_dim, cfg.num_labels + 1)
+
+    def forward(self, pixel_values):
+        feats = self.backbone(pixel_values)
+        mask_features, ms = self.pixel_decoder(feats)
+        inters, masks = self.decoder(ms, mask_features)
+        classes = [self.class_head(x) for x in inters]
+        return masks, classes
+
+
+# ----------------------------------------------------------------------------------
+# Criterion (HF:m2f:245-794), RNG draws in HF's order so a seeded run matches HF
+# ----------------------------------------------------------------------------------
+
+
+def _sample_point(feat, coords):
+    """HF:m2f:245-275."""
+    add = False
+    if coords.dim() == 3:
+        add = True
+        coords = coords.unsqueeze(2)
+    out = F.grid_sample(feat, 2.0 * coords - 1.0, align_corners=False)
+    return out.squeeze(3) if add else out
+
+
+def _pair_bce(inputs, labels):
+    """HF:m2f:350-374."""
+    hw = inputs.shape[1]
+    pos = F.binary_cross_entropy_with_logits(inputs, torch.ones_like(inputs), reduction="none")
+    neg = F.binary_cross_entropy_with_logits(inputs, torch.zeros_like(inputs), reduction="none")
+    return (pos / hw) @ labels.T + (neg / hw) @ (1 - labels).T
+
+
+def _pair_dice(inputs, labels):
+    """HF:m2f:328-347."""
+    inputs = inputs.sigmoid().flatten(1)
+    num = 2 * inputs @ labels.T
+    den = inputs.sum(-1)[:, None] + labels.sum(-1)[None, :]
+    return 1 - (num + 1) / (den + 1)
+
+
+class RefCriterion:
+    """HF:m2f:378-794 with scipy's linear_sum_assignment (CPU)."""
+
+    def __init__(self, cfg: RefConfig):
+        self.cfg = cfg
+        self.empty_weight = torch.ones(cfg.num_labels + 1)
+        self.empty_weight[-1] = cfg.no_object_weight
+
+    def match(self, masks, classes, mask_labels, class_labels):
+        from scipy.optimize import linear_sum_assignment
+        c = self.cfg
+        out = []
+        for i in range(masks.shape[0]):
+            probs = classes[i].softmax(-1)
+            cost_class = -probs[:, class_labels[i]]
+            tgt = mask_labels[i].to(masks)[:, None]
+            pred = masks[i][:, None]
+            pts = torch.rand(1, c.train_num_points, 2, device=pred.device)
+            tgt = _sample_point(tgt, pts.repeat(tgt.shape[0], 1, 1)).squeeze(1)
+            pred = _sample_point(pred, pts.repeat(pred.shape[0], 1, 1)).squeeze(1)
+            cost = c.mask_weight * _pair_bce(pred, tgt) + c.class_weight * cost_class + \
+                c.dice_weight * _pair_dice(pred, tgt)
+            cost = torch.minimum(cost, torch.tensor(1e10))
+            cost = torch.maximum(cost, torch.tensor(-1e10))
+            cost = torch.nan_to_num(cost, 0)
+            a, b = linear_sum_assignment(cost.cpu())
+            out.append((torch.as_tensor(a, dtype=torch.int64), torch.as_tensor(b, dtype=torch.int64)))
+        return out
+
+    def _points(self, logits):
+        """HF:m2f:671-724."""
+        c = self.cfg
+        nb = logits.shape[0]
+        ns = int(c.train_num_points * c.oversample_ratio)
+        coords = torch.rand(nb, ns, 2, device=logits.device)
+        unc = -torch.abs(_sample_point(logits, coords))
+        nu = int(c.importance_sample_ratio * c.train_num_points)
+        nr = c.train_num_points - nu
+        idx = torch.topk(unc[:, 0, :], k=nu, dim=1)[1]
+        idx = idx + (ns * torch.arange(nb, dtype=torch.long, device=logits.device))[:, None]
+        coords = coords.view(-1, 2)[idx.view(-1), :].view(nb, nu, 2)
+        if nr > 0:
+            coords = torch.cat([coords, torch.rand(nb, nr, 2, device=logits.device)], dim=1)
+        return coords
+
+    def single(self, masks, classes, mask_labels, class_labels):
+        c = self.cfg
+        idx = self.match(masks, classes, mask_labels, class_labels)
+        nm = torch.clamp(torch.as_tensor(float(sum(len(x) for x in class_labels))), min=1)
+        bi = torch.cat([torch.full_like(s, i) for i, (s, _) in enumerate(idx)])
+        si = torch.cat([s for s, _ in idx])
+        ti = torch.cat([t for _, t in idx])
+        pred = masks[(bi, si)][:, None]
+        # HF pads targets to the batch max (HF:m2f:529-542); equal sizes here
+        tgt = torch.cat([mask_labels[i][t] for i, (_, t) in enumerate(idx)]).to(masks)[:, None]
+        with torch.no_grad():
+            pts = self._points(pred)
+            plab = _sample_point(tgt, pts).squeeze(1)
+        plog = _sample_point(pred, pts).squeeze(1)
+        loss_mask = F.binary_cross_entropy_with_logits(plog, plab, reduction="none").mean(1).sum() / nm
+        pr = plog.sigmoid().flatten(1)
+        loss_dice = (1 - (2 * (pr * plab).sum(-1) + 1) / (pr.sum(-1) + plab.sum(-1) + 1)).sum() / nm
+        tc = torch.full(classes.shape[:2], c.num_labels, dtype=torch.int64)
+        tc[(bi, si)] = torch.cat([class_labels[i][t] for i, (_, t) in enumerate(idx)])
+        loss_ce = F.cross_entropy(classes.transpose(1, 2), tc, weight=self.empty_weight)
+        return {"loss_mask": loss_mask, "loss_dice": loss_dice, "loss_cross_entropy": loss_ce}
+
+    def __call__(self, masks, classes, mask_labels, class_labels):
+        """HF:m2f:726-779 + weighting HF:m2f:2312-2321; final prediction first, then aux."""
+        c = self.cfg
+        losses = dict(self.single(masks[-1], classes[-1], mask_labels, class_labels))
+        for i, (m, cl) in enumerate(zip(masks[:-1], classes[:-1])):
+            for k, v in self.single(m, cl, mask_labels, class_labels).items():
+                losses[f"{k}_{i}"] = v
+        w = {"loss_cross_entropy": c.class_weight, "loss_mask": c.mask_weight, "loss_dice": c.dice_weight}
+        for k in list(losses):
+            for key, wt in w.items():
+                if key in k:
+                    losses[k] = losses[k] * wt
+        return sum(losses.values()), losses

@@ -1,0 +1,275 @@
+"""Generate the golden vectors that pin the oracle (run in the build container only).
+
+Source of truth: the in-container third-party implementation transformers 5.15.0
+(HF:swin = transformers/models/swin/modeling_swin.py, HF:m2f =
+transformers/models/mask2former/modeling_mask2former.py).  The reference repository
+holds no implementation of this path, so its arithmetic is pinned
+to the HF implementation the survey designates as the oracle.  Only the resulting
+arrays are committed (`tests/golden/*.npz`); nothing from HF travels to the GPU box.
+
+    python tests/golden/gen_golden.py          # rewrites tests/golden/*.npz
+
+Model weights are not stored: they are regenerated from a seed by
+`oracle.detinit.det_init` both here and in the tests.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "vision-instance-seg_amd"))
+
+from oracle.detinit import det_init  # noqa: E402
+from oracle.ref_model import RefConfig, RefMask2Former  # noqa: E402
+from visionseg.convert import to_hf_state_dict, from_hf_state_dict  # noqa: E402
+
+from transformers import Mask2FormerConfig, SwinConfig, Mask2FormerForUniversalSegmentation  # noqa: E402
+from transformers.models.swin import modeling_swin as HS  # noqa: E402
+from transformers.models.mask2former import modeling_mask2former as HM  # noqa: E402
+
+TINY = dict(embed_dim=32, depths=[2, 2, 2, 2], num_heads=[1, 2, 4, 8], window_size=7, mlp_ratio=4.0,
+            feature_size=64, mask_feature_size=64, hidden_dim=64, enc_ffn=128, dec_ffn=128, dec_heads=2,
+            enc_layers=2, dec_layers=4, num_queries=10, num_labels=1, train_num_points=256)
+WEIGHT_SEED = 1234
+
+
+def hf_model(c: dict):
+    sw = SwinConfig(embed_dim=c["embed_dim"], depths=c["depths"], num_heads=c["num_heads"],
+                    window_size=c["window_size"], mlp_ratio=c["mlp_ratio"], drop_path_rate=0.0,
+                    hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0,
+                    out_features=["stage1", "stage2", "stage3", "stage4"])
+    sw._attn_implementation = "eager"
+    cfg = Mask2FormerConfig(backbone_config=sw, num_labels=c["num_labels"], num_queries=c["num_queries"],
+                            feature_size=c["feature_size"], mask_feature_size=c["mask_feature_size"],
+                            hidden_dim=c["hidden_dim"], encoder_feedforward_dim=c["enc_ffn"],
+                            dim_feedforward=c["dec_ffn"], num_attention_heads=c["dec_heads"],
+                            encoder_layers=c["enc_layers"], decoder_layers=c["dec_layers"],
+                            train_num_points=c["train_num_points"], dropout=0.0)
+    m = Mask2FormerForUniversalSegmentation(cfg)
+    m.model.pixel_level_module.encoder.config._attn_implementation = "eager"
+    return m
+
+
+def synth_targets(B, H, W, seed):
+    """1..3 thin random-polygon-ish instances per image, class 0 (single class)."""
+    g = np.random.default_rng(seed)
+    masks, classes = [], []
+    yy, xx = np.mgrid[0:H, 0:W]
+    for _ in range(B):
+        k = int(g.integers(1, 4))
+        m = np.zeros((k, H, W), dtype=np.float32)
+        for j in range(k):
+            cy, cx = g.uniform(0.2, 0.8) * H, g.uniform(0.2, 0.8) * W
+            ry, rx = g.uniform(0.05, 0.25) * H, g.uniform(0.05, 0.25) * W
+            m[j] = (((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2 <= 1).astype(np.float32)
+        masks.append(m)
+        classes.append(np.zeros(k, dtype=np.int64))
+    return masks, classes
+
+
+def gen_model(out):
+    cfg = RefConfig.from_dict(TINY)
+    shapes = {k: v.shape for k, v in RefMask2Former(cfg).state_dict().items()}
+    sd = det_init(shapes, WEIGHT_SEED)
+    m = hf_model(TINY)
+    hsd = to_hf_state_dict(sd, TINY["num_labels"])
+    missing, unexpected = m.load_state_dict(hsd, strict=False)
+    missing = [k for k in missing if not k.endswith("relative_position_index") and ".swin.layernorm." not in k]
+    assert not missing and not unexpected, (missing, unexpected)
+    back = from_hf_state_dict(m.state_dict())
+    assert set(back) == set(sd) and all(torch.equal(back[k], sd[k]) for k in sd)
+    m.eval()
+    res = {"config": np.array(json.dumps(TINY)), "weight_seed": np.array(WEIGHT_SEED)}
+    for tag, (B, H, W) in {"a": (2, 128, 128), "b": (1, 96, 160)}.items():
+        g = torch.Generator().manual_seed(7 if tag == "a" else 8)
+        px = torch.randn(B, 3, H, W, generator=g)
+        with torch.no_grad():
+            o = m(pixel_values=px, output_auxiliary_logits=True, output_hidden_states=True)
+        masks = [a["masks_queries_logits"] for a in o.auxiliary_logits] + [o.masks_queries_logits]
+        classes = [a["class_queries_logits"] for a in o.auxiliary_logits] + [o.class_queries_logits]
+        res[f"{tag}_pixel_values"] = px.numpy()
+        for i, x in enumerate(o.encoder_hidden_states):
+            res[f"{tag}_backbone_{i}"] = x.numpy()
+        res[f"{tag}_mask_features"] = o.pixel_decoder_last_hidden_state.numpy()
+        res[f"{tag}_masks"] = torch.stack(masks).numpy()
+        res[f"{tag}_classes"] = torch.stack(classes).numpy()
+        if tag == "a":
+            ml, cl = synth_targets(B, H // 4 * 4, W // 4 * 4, 11)
+            mlt = [torch.from_numpy(x) for x in ml]
+            clt = [torch.from_numpy(x) for x in cl]
+            aux = [{"masks_queries_logits": a, "class_queries_logits": b} for a, b in zip(masks[:-1], classes[:-1])]
+            torch.manual_seed(99)
+            with torch.no_grad():
+                ld = m.get_loss_dict(masks[-1], classes[-1], mlt, clt, aux)
+            res["a_loss_total"] = np.array(float(sum(ld.values())))
+            res["a_loss_keys"] = np.array(json.dumps(sorted(ld)))
+            res["a_loss_vals"] = np.array([float(ld[k]) for k in sorted(ld)], dtype=np.float64)
+            for i, (x, y) in enumerate(zip(ml, cl)):
+                res[f"a_target_masks_{i}"] = x.astype(np.uint8)
+                res[f"a_target_classes_{i}"] = y
+    np.savez_compressed(os.path.join(HERE, "model_tiny.npz"), **res)
+    out.append("model_tiny.npz")
+
+
+def gen_window(out):
+    """a2/a3/a4: window partition/reverse, shift mask, relative index (bit-exact)."""
+    res = {}
+    cases = [(2, 10, 13, 8, 7, 3), (1, 9, 9, 4, 4, 2), (1, 14, 7, 5, 7, 0), (3, 4, 4, 6, 7, 3), (1, 24, 24, 3, 12, 6)]
+    for ci, (B, H, W, C, ws, shift) in enumerate(cases):
+        sw = SwinConfig(embed_dim=C, window_size=ws)
+        layer = HS.SwinLayer(sw, C, (H, W), 1, shift_size=shift)
+        x = torch.randn(B, H, W, C, generator=torch.Generator().manual_seed(ci))
+        xp, _ = layer.maybe_pad(x, H, W)
+        Hp, Wp = xp.shape[1:3]
+        win = HS.window_partition(layer.cyclic_shift(xp), ws).reshape(-1, ws * ws, C)
+        back = layer.cyclic_shift(HS.window_reverse(win.view(-1, ws, ws, C), ws, Hp, Wp), reverse=True)[:, :H, :W]
+        assert torch.equal(back, x)
+        am = layer.get_attn_mask(Hp, Wp, torch.float32, "cpu")
+        rpb = HS.SwinRelativePositionBias(1, (ws, ws))
+        res[f"c{ci}_meta"] = np.array([B, H, W, C, ws, shift])
+        res[f"c{ci}_x"] = x.numpy()
+        res[f"c{ci}_windows"] = win.numpy()
+        res[f"c{ci}_rel_index"] = rpb.relative_position_index.numpy()
+        if am is not None:
+            res[f"c{ci}_attn_mask"] = am.numpy()
+    np.savez_compressed(os.path.join(HERE, "window_ops.npz"), **res)
+    out.append("window_ops.npz")
+
+
+def gen_swin_attention(out):
+    """a5: SwinAttention on partitioned windows (with and without the shift mask)."""
+    res = {}
+    for ci, (B, H, W, C, heads, ws, shift) in enumerate([(2, 10, 13, 64, 2, 7, 3), (1, 14, 14, 32, 1, 7, 0),
+                                                         (1, 12, 12, 96, 3, 12, 6)]):
+        torch.manual_seed(100 + ci)
+        sw = SwinConfig(embed_dim=C, window_size=ws)
+        sw._attn_implementation = "eager"
+        layer = HS.SwinLayer(sw, C, (H, W), heads, shift_size=shift)
+        with torch.no_grad():
+            for p in layer.parameters():
+                p.add_(0.2 * torch.randn_like(p))
+        layer.eval()
+        x = torch.randn(B, H * W, C)
+        with torch.no_grad():
+            y, _ = layer(x, (H, W), always_partition=True)
+        sd = {k: v for k, v in layer.state_dict().items() if "relative_position_index" not in k}
+        res[f"c{ci}_meta"] = np.array([B, H, W, C, heads, ws, shift])
+        res[f"c{ci}_x"] = x.numpy()
+        res[f"c{ci}_y"] = y.numpy()
+        for k, v in sd.items():
+            res[f"c{ci}_w_{k}"] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, "swin_layer.npz"), **res)
+    out.append("swin_layer.npz")
+
+
+def gen_msda(out):
+    """a8: multi_scale_deformable_attention incl. borders, pixel centres, half-integers,
+    outside points; gradients through autograd."""
+    res = {}
+    g = torch.Generator().manual_seed(21)
+    shapes = [(6, 7), (3, 4), (2, 2)]
+    B, H, D, Q, L, P = 2, 2, 32, 11, 3, 4
+    S = sum(h * w for h, w in shapes)
+    value = torch.randn(B, S, H, D, generator=g)
+    loc = torch.rand(B, Q, H, L, P, 2, generator=g) * 1.4 - 0.2
+    # special positions on level-specific grids
+    for l, (hl, wl) in enumerate(shapes):
+        loc[0, 0, 0, l, 0] = torch.tensor([0.5 / wl, 0.5 / hl])        # pixel centre (0,0)
+        loc[0, 0, 1, l, 1] = torch.tensor([1.0, 1.0])                  # far border
+        loc[0, 1, 0, l, 2] = torch.tensor([0.0, 0.0])                  # near border
+        loc[0, 1, 1, l, 3] = torch.tensor([2.0 / wl, 1.0 / hl])        # half-integer h/w
+        loc[1, 2, 0, l, 0] = torch.tensor([-0.5, 0.3])                 # fully outside
+        loc[1, 2, 1, l, 1] = torch.tensor([0.3, 1.5])                  # fully outside
+        loc[1, 3, 0, l, 2] = torch.tensor([-0.5 / wl, 0.5])            # exactly -1 in w
+        loc[1, 3, 1, l, 3] = torch.tensor([(wl - 0.5) / wl, (hl - 0.5) / hl])  # last pixel centre
+    w = torch.softmax(torch.randn(B, Q, H, L * P, generator=g), -1).view(B, Q, H, L, P)
+    value.requires_grad_(True)
+    loc.requires_grad_(True)
+    w.requires_grad_(True)
+    o = HM.multi_scale_deformable_attention(value, shapes, loc, w)
+    go = torch.randn(o.shape, generator=g)
+    o.backward(go)
+    res.update(shapes=np.array(shapes), value=value.detach().numpy(), loc=loc.detach().numpy(),
+               weights=w.detach().numpy(), out=o.detach().numpy(), grad_out=go.numpy(),
+               grad_value=value.grad.numpy(), grad_loc=loc.grad.numpy(), grad_weights=w.grad.numpy())
+    np.savez_compressed(os.path.join(HERE, "msda.npz"), **res)
+    out.append("msda.npz")
+
+
+def gen_mask_head(out):
+    """a11: Mask2FormerMaskPredictor (MLP + einsum + resize/threshold)."""
+    res = {}
+    torch.manual_seed(31)
+    D, heads, Q, B = 32, 2, 6, 2
+    mp = HM.Mask2FormerMaskPredictor(D, heads, D)
+    with torch.no_grad():
+        for p in mp.parameters():
+            p.copy_(torch.randn_like(p) / 3)
+    h = torch.randn(Q, B, D)
+    pix = torch.randn(B, D, 16, 16)
+    for ti, tgt in enumerate([(2, 2), (4, 4), (8, 8), (16, 16)]):
+        with torch.no_grad():
+            lo, am = mp(h, pix, tgt)
+        res[f"t{ti}_size"] = np.array(tgt)
+        res[f"t{ti}_logits"] = lo.numpy()
+        res[f"t{ti}_mask"] = am.numpy()
+    res["h"] = h.numpy()
+    res["pix"] = pix.numpy()
+    for k, v in mp.state_dict().items():
+        res["w_" + k] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, "mask_head.npz"), **res)
+    out.append("mask_head.npz")
+
+
+def gen_masked_attn(out):
+    """a10: the decoder's nn.MultiheadAttention with a boolean mask after the
+    fully-blocked-row fix (HF:m2f:1912-1914, 1644-1650)."""
+    res = {}
+    torch.manual_seed(41)
+    D, heads, Q, S, B = 64, 2, 7, 40, 2
+    mha = torch.nn.MultiheadAttention(D, heads)
+    with torch.no_grad():
+        mha.in_proj_bias.copy_(torch.randn(3 * D) * 0.1)
+    q = torch.randn(Q, B, D)
+    k = torch.randn(S, B, D)
+    v = torch.randn(S, B, D)
+    blocked = torch.rand(B * heads, Q, S) < 0.6
+    blocked = blocked.view(B, heads, Q, S)[:, :1].expand(B, heads, Q, S).reshape(B * heads, Q, S).clone()
+    blocked[0, 3] = True      # fully blocked rows -> unblocked by the fix
+    blocked[1, 3] = True
+    blocked[2, 0] = True
+    blocked[3, 0] = True
+    where = (blocked.sum(-1) != blocked.shape[-1]).to(blocked.dtype)
+    fixed = blocked * where.unsqueeze(-1)
+    with torch.no_grad():
+        o, _ = mha(q, k, v, attn_mask=fixed, key_padding_mask=None)
+    res.update(q=q.numpy(), k=k.numpy(), v=v.numpy(), blocked_raw=blocked.numpy(), blocked_fixed=fixed.numpy(),
+               out=o.numpy(), **{"w_" + kk: vv.numpy() for kk, vv in mha.state_dict().items()})
+    np.savez_compressed(os.path.join(HERE, "masked_attn.npz"), **res)
+    out.append("masked_attn.npz")
+
+
+def gen_misc(out):
+    res = {}
+    pe = HM.Mask2FormerSinePositionEmbedding(num_position_features=32, normalize=True)
+    res["pos_2x64x5x7"] = pe((2, 64, 5, 7), "cpu", torch.float32).numpy()
+    shapes = [(4, 5), (2, 3), (1, 1)]
+    vr = torch.ones(2, 3, 2)
+    res["refpts"] = HM.Mask2FormerPixelDecoderEncoderOnly.get_reference_points(shapes, vr, "cpu").numpy()
+    np.savez_compressed(os.path.join(HERE, "misc.npz"), **res)
+    out.append("misc.npz")
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    done = []
+    for fn in (gen_window, gen_swin_attention, gen_msda, gen_mask_head, gen_masked_attn, gen_misc, gen_model):
+        fn(done)
+        print("wrote", done[-1])
