@@ -1,0 +1,102 @@
+/*
+ * visionseg.h — C ABI of libvisionseg_hip.so, the MI355X (gfx950) kernels of the
+ * Swin + Mask2Former training hot path.
+ *
+ * Boundary.  The reference (Wlsghdh/VISION-Instance-Seg) reaches this path only
+ * through upstream Python/C++ extensions that are not vendored:
+ *   - MSDeformAttn CUDA extension `MultiScaleDeformableAttention.ms_deform_attn_forward/
+ *     backward(value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
+ *     im2col_step)` called by MaskDINO/Mask2Former `MSDeformAttnFunction`
+ *     (upstream ops/functions/ms_deform_attn_func.py); in-container oracle equivalent
+ *     HF:m2f:798-837 `multi_scale_deformable_attention`.
+ *   - Swin `window_partition` / `window_reverse` + `torch.roll` + `F.pad`
+ *     (HF:swin:486-505, 546-566, 609-626) and the window attention core
+ *     (HF:swin:373-398, 401-468).
+ *   - the mask head einsum + attention-mask derivation (HF:m2f:2040-2056).
+ *   - the masked cross-attention core of `nn.MultiheadAttention` as the decoder calls
+ *     it (HF:m2f:1644-1650, fully-blocked-row fix HF:m2f:1912-1914).
+ * Callers: training/train_template.py `train_maskdino(...)` and
+ * labeling_server/ai_segmentation.py `AISegmentationModel.predict(...)` reach these
+ * entry points through the Python package `visionseg`.
+ *
+ * Conventions.
+ *   - Every pointer named *without* a `_host` suffix is DEVICE memory; all tensors are
+ *     dense row-major (C-contiguous) in the layout documented per function.
+ *   - `dtype` selects the storage type of the activation tensors: VS_F32 or VS_BF16.
+ *     Coordinates, attention weights, statistics and gradient accumulators are f32.
+ *     Arithmetic is always f32 (MFMA accumulate in f32).
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  Every call is
+ *     asynchronous on that stream; no call allocates device memory or synchronises,
+ *     so calls are hipGraph-capturable.
+ *   - Return value: VS_OK (0) or a negative error code; vs_last_error() returns a
+ *     thread-local message for the last failure (mirrors TORCH_CHECK -> RuntimeError
+ *     in the upstream extension).
+ */
+#ifndef VISIONSEG_H_
+#define VISIONSEG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VS_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define VS_API __attribute__((visibility("default")))
+#else
+#define VS_API
+#endif
+
+enum vs_dtype { VS_F32 = 0, VS_BF16 = 1 };
+enum vs_status { VS_OK = 0, VS_ERR_INVALID = -1, VS_ERR_HIP = -2, VS_ERR_UNSUPPORTED = -3 };
+
+VS_API int vs_abi_version(void);
+VS_API const char* vs_last_error(void);
+
+/* ---- a8: multi-scale deformable attention sampling -------------------------------
+ * value       [B, S, H, 32]            dtype      (S = sum_l H_l*W_l, head dim 32)
+ * spatial_shapes_host  int64 [L, 2]    HOST       (H_l, W_l), L <= 4
+ * level_start_host     int64 [L]       HOST       start of level l inside S
+ * sampling_loc f32 [B, Q, H, L, P, 2]  (x, y) normalised to [0,1]
+ * attn_weight  f32 [B, Q, H, L, P]
+ * out         [B, Q, H*32]             dtype
+ * Sampling: h = y*H_l - 0.5, w = x*W_l - 0.5, bilinear, zeros outside (upstream
+ * ms_deform_attn_im2col_bilinear == grid_sample(align_corners=False, zeros)).
+ * Replaces ms_deform_attn_forward.  im2col_step of the upstream API has no meaning
+ * here (the whole batch is one launch) and is not part of the ABI. */
+VS_API int vs_msda_forward(int dtype, const void* value, const int64_t* spatial_shapes_host,
+                    const int64_t* level_start_host, const float* sampling_loc,
+                    const float* attn_weight, void* out, int batch, int spatial_size,
+                    int num_heads, int channels, int num_levels, int num_query,
+                    int num_point, void* stream);
+
+/* Replaces ms_deform_attn_backward.  grad_out [B, Q, H*32] dtype.  Outputs (all f32,
+ * overwritten): grad_value [B, S, H, 32], grad_loc [B, Q, H, L, P, 2],
+ * grad_attn [B, Q, H, L, P]. */
+VS_API int vs_msda_backward(int dtype, const void* value, const int64_t* spatial_shapes_host,
+                     const int64_t* level_start_host, const float* sampling_loc,
+                     const float* attn_weight, const void* grad_out, float* grad_value,
+                     float* grad_loc, float* grad_attn, int batch, int spatial_size,
+                     int num_heads, int channels, int num_levels, int num_query,
+                     int num_point, void* stream);
+
+/* ---- a2: Swin pad + cyclic shift + window partition / its inverse ---------------
+ * window_partition: x [B, H, W, C] -> windows [B*nWh*nWw, ws*ws, C] where
+ * Hp = ceil(H/ws)*ws, nWh = Hp/ws (same for W); windows[(b,wy,wx), (ty,tx)] =
+ * xpad[b, (wy*ws+ty+shift) % Hp, (wx*ws+tx+shift) % Wp] with zero padding.
+ * Bit-exact data movement for any element size (esize = bytes per element).
+ * window_reverse is the exact inverse on the un-padded region (crop) — it is also the
+ * backward of window_partition, and window_partition is the backward of
+ * window_reverse. */
+VS_API int vs_window_partition(const void* x, void* windows, int esize, int batch, int height,
+                        int width, int channels, int window, int shift, void* stream);
+VS_API int vs_window_reverse(const void* windows, void* x, int esize, int batch, int height,
+                      int width, int channels, int window, int shift, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VISIONSEG_H_ */

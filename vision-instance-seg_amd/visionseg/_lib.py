@@ -1,0 +1,80 @@
+"""ctypes binding of libvisionseg_hip.so (the C ABI declared in include/visionseg.h).
+
+The library is built in-tree by `make -C vision-instance-seg_amd` (or
+`__graft_entry__.build()`).  There is no fallback: if the library is missing or a
+tensor is not on a HIP device, the ops raise — the product path never silently runs
+something else.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # load torch (and its HIP runtime) before the kernels library
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvisionseg_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "visionseg.h")
+
+VS_F32, VS_BF16 = 0, 1
+
+_c_int, _c_void_p, _c_float = ctypes.c_int, ctypes.c_void_p, ctypes.c_float
+_P = _c_void_p
+
+# name -> argtypes (restype int unless noted); keep in sync with include/visionseg.h
+SIGNATURES = {
+    "vs_abi_version": [],
+    "vs_last_error": [],
+    "vs_msda_forward": [_c_int, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
+    "vs_msda_backward": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
+    "vs_window_partition": [_P, _P] + [_c_int] * 7 + [_P],
+    "vs_window_reverse": [_P, _P] + [_c_int] * 7 + [_P],
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is not built: run `make -C vision-instance-seg_amd` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, args in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_char_p if name == "vs_last_error" else _c_int
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().vs_last_error().decode(errors="replace")
+        raise RuntimeError(f"visionseg {what} failed (status {rc}): {msg}")
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return VS_F32
+    if t.dtype == torch.bfloat16:
+        return VS_BF16
+    raise TypeError(f"visionseg kernels take float32 or bfloat16 activations, got {t.dtype}")
+
+
+def require_hip(*ts: torch.Tensor):
+    for t in ts:
+        if not t.is_cuda:
+            raise RuntimeError("visionseg ops run only on a HIP device (no CPU fallback); "
+                               f"got a tensor on {t.device}")
+
+
+def ptr(t: torch.Tensor):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream(t: torch.Tensor | None = None):
+    dev = t.device if t is not None else None
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
