@@ -95,6 +95,61 @@ VS_API int vs_window_partition(const void* x, void* windows, int esize, int batc
 VS_API int vs_window_reverse(const void* windows, void* x, int esize, int batch, int height,
                       int width, int channels, int window, int shift, void* stream);
 
+
+/* ---- a3/a4/a5: Swin (shifted-)window attention core ------------------------------
+ * qkv   [Bw, N, 3, heads, 32] dtype   fused q;k;v projection of the partitioned windows
+ *                                     (N = window^2, Bw = batch * nwin_h * nwin_w)
+ * rel_table f32 [(2*window-1)^2, heads]   relative position bias table
+ * out   [Bw, N, heads*32] dtype;  lse f32 [Bw, heads, N] (saved for backward)
+ * S_ij = q_i.k_j*scale + table[rel(i,j)] + (shift>0 && region_i != region_j ? -100 : 0);
+ * region ids are computed from the padded-grid position (nwin_h*window rows), exactly as
+ * HF:swin:584-607 builds its mask.  f32 softmax. */
+VS_API int vs_window_attn_forward(int dtype, const void* qkv, const float* rel_table, void* out,
+                                  float* lse, int num_windows, int heads, int window, int shift,
+                                  int nwin_h, int nwin_w, float scale, void* stream);
+
+/* grad_out [Bw, N, heads*32] dtype -> grad_qkv [Bw, N, 3, heads, 32] dtype (overwritten),
+ * grad_table_partial f32 [Bw, heads, (2*window-1)^2]: per-window partial sums of the
+ * bias-table gradient; the caller reduces over Bw (deterministic, no global atomics). */
+VS_API int vs_window_attn_backward(int dtype, const void* qkv, const float* rel_table,
+                                   const void* out, const float* lse, const void* grad_out,
+                                   void* grad_qkv, float* grad_table_partial, int num_windows,
+                                   int heads, int window, int shift, int nwin_h, int nwin_w,
+                                   float scale, void* stream);
+
+
+/* ---- a11: mask head -----------------------------------------------------------------
+ * logits f32 [B, Q, H*W] = E [B, Q, C] x P[b]^T, with the pixel embedding P
+ * channels-last [B, H*W, C] (HF:m2f:2051 einsum 'bqc,bchw->bqhw').  dtype of E and P:
+ * bf16 (v_mfma_f32_32x32x16_bf16) or f32 (v_mfma_f32_32x32x2_f32, exact f32 products). */
+VS_API int vs_mask_head_forward(int dtype, const void* mask_embed, const void* pixel_embed_nhwc,
+                                float* logits, int batch, int num_query, int channels, int height,
+                                int width, void* stream);
+
+/* Attention bitmask of the next decoder layer (HF:m2f:2049-2055 + row fix 1912-1914):
+ * bilinear (align_corners=False) resize of each logits row [H, W] to [th, tw], key k
+ * blocked iff sigmoid(v) < 0.5, stored as bit k%32 of words[row, k/32]
+ * (words u32 [rows, ceil(th*tw/32)], rows = B*Q); a row blocked at every key is
+ * written all-zero (un-blocked). */
+VS_API int vs_attn_bitmask(const float* logits, uint32_t* words, int rows, int height, int width,
+                           int target_h, int target_w, void* stream);
+
+/* ---- a10: masked cross-attention core ------------------------------------------------
+ * q [B, Q, heads*32], k/v [B, S, heads*32] (dtype), words u32 [B, Q, ceil(S/32)] from
+ * vs_attn_bitmask, out [B, Q, heads*32] dtype, lse f32 [B, heads, Q].
+ * workspace: device scratch of vs_masked_attn_workspace_bytes(B, Q, S, heads) bytes. */
+VS_API long long vs_masked_attn_workspace_bytes(int batch, int num_query, int num_keys, int heads);
+VS_API int vs_masked_attn_forward(int dtype, const void* q, const void* k, const void* v,
+                                  const uint32_t* words, void* out, float* lse, void* workspace,
+                                  int batch, int num_query, int num_keys, int heads, float scale,
+                                  void* stream);
+/* grad_out [B, Q, heads*32] -> grad_q, grad_k, grad_v (dtype, overwritten). */
+VS_API int vs_masked_attn_backward(int dtype, const void* q, const void* k, const void* v,
+                                   const uint32_t* words, const void* out, const float* lse,
+                                   const void* grad_out, void* grad_q, void* grad_k, void* grad_v,
+                                   void* workspace, int batch, int num_query, int num_keys,
+                                   int heads, float scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,7 +12,7 @@ from visionseg import _lib as L
 
 def declared_symbols():
     txt = open(L.HEADER_PATH).read()
-    return sorted(set(re.findall(r"VS_API\s+(?:const\s+)?\w+\*?\s+(vs_\w+)\s*\(", txt)))
+    return sorted(set(re.findall(r"VS_API\s+[\w ]+?\*?\s*\b(vs_\w+)\s*\(", txt)))
 
 
 def test_header_declares_entry_points():

@@ -134,3 +134,180 @@ def test_msda_rejects_bad_shapes():
     w = torch.zeros(1, 2, 1, 1, 1, device=DEV)
     with pytest.raises(ValueError):
         ops.ms_deform_attn(v, [(3, 3)], loc, w)
+
+
+# ------------------------------------------------------------------ window attention
+def _win_attn_ref(qkv, table, heads, ws, shift, nWh, nWw):
+    Bw, N, C3 = qkv.shape
+    q, k, v = qkv.view(Bw, N, 3, heads, 32).permute(2, 0, 3, 1, 4)
+    mask = torch.from_numpy(R.shift_attn_mask_np(nWh * ws, nWw * ws, ws, shift)) if shift else None
+    return R.window_attention_ref(q, k, v, table, ws, mask)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(B=2, nWh=2, nWw=3, heads=2, ws=7, shift=3),
+    dict(B=1, nWh=2, nWw=2, heads=1, ws=7, shift=0),
+    dict(B=1, nWh=3, nWw=2, heads=3, ws=12, shift=6),
+    dict(B=1, nWh=37, nWw=37, heads=3, ws=7, shift=3),    # Swin-T stage 1 @ 1024^2, one image
+])
+def test_window_attention_fp32_vs_oracle(cfg):
+    ops = _ops()
+    Bw = cfg["B"] * cfg["nWh"] * cfg["nWw"]
+    N, C = cfg["ws"] ** 2, cfg["heads"] * 32
+    g = torch.Generator().manual_seed(3)
+    qkv = torch.randn(Bw, N, 3 * C, generator=g)
+    table = torch.randn((2 * cfg["ws"] - 1) ** 2, cfg["heads"], generator=g)
+    qr, tr = qkv.clone().requires_grad_(True), table.clone().requires_grad_(True)
+    ref = _win_attn_ref(qr, tr, cfg["heads"], cfg["ws"], cfg["shift"], cfg["nWh"], cfg["nWw"])
+    go = torch.randn(ref.shape, generator=g)
+    ref.backward(go)
+    qd, td = qkv.to(DEV).requires_grad_(True), table.to(DEV).requires_grad_(True)
+    out = ops.window_attention(qd, td, cfg["heads"], cfg["ws"], cfg["shift"], cfg["nWh"], cfg["nWw"])
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), atol=1e-5, rtol=0)
+    out.backward(go.to(DEV))
+    np.testing.assert_allclose(qd.grad.cpu().numpy(), qr.grad.numpy(), atol=5e-5, rtol=0)
+    gt = tr.grad.numpy()
+    np.testing.assert_allclose(td.grad.cpu().numpy(), gt, atol=1e-4 * max(1.0, np.abs(gt).max()), rtol=1e-5)
+
+
+def test_window_attention_bf16_vs_oracle():
+    ops = _ops()
+    B, nWh, nWw, heads, ws, shift = 2, 4, 4, 3, 7, 3
+    Bw, N, C = B * nWh * nWw, ws * ws, heads * 32
+    g = torch.Generator().manual_seed(4)
+    qkv = torch.randn(Bw, N, 3 * C, generator=g).to(torch.bfloat16)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g)
+    ref = _win_attn_ref(qkv.float(), table, heads, ws, shift, nWh, nWw)
+    out = ops.window_attention(qkv.to(DEV), table.to(DEV), heads, ws, shift, nWh, nWw)
+    err = (out.float().cpu() - ref).abs()
+    assert bool((err <= ref.abs() * 2 ** -8 + 2e-3).all()), float(err.max())
+
+
+# ------------------------------------------------------------------ mask head + bitmask
+def test_mask_head_golden(golden):
+    """MLP on host-side torch, einsum + mask on the kernels vs the HF predictor fixture."""
+    ops = _ops()
+    d = golden("mask_head.npz")
+    h = torch.from_numpy(d["h"]).transpose(0, 1)
+    pix = torch.from_numpy(d["pix"])
+    lin = [(torch.from_numpy(d[f"w_mask_embedder.{i}.0.weight"]), torch.from_numpy(d[f"w_mask_embedder.{i}.0.bias"]))
+           for i in range(3)]
+    e = torch.relu(torch.nn.functional.linear(h, *lin[0]))
+    e = torch.relu(torch.nn.functional.linear(e, *lin[1]))
+    e = torch.nn.functional.linear(e, *lin[2])
+    B, C, H, W = pix.shape
+    nhwc = pix.permute(0, 2, 3, 1).reshape(B, H * W, C)
+    lo = ops.mask_head(e.to(DEV), nhwc.to(DEV), H, W)
+    for ti in range(4):
+        tgt = tuple(d[f"t{ti}_size"].tolist())
+        np.testing.assert_allclose(lo.cpu().numpy(), d[f"t{ti}_logits"], atol=1e-5, rtol=0)
+        words = ops.attn_bitmask(lo, tgt)
+        blocked = ops.unpack_bitmask(words, tgt[0] * tgt[1]).cpu()
+        exp = R.unblock_full_rows(torch.from_numpy(d[f"t{ti}_mask"]).view(B, 2, -1, tgt[0] * tgt[1])[:, 0])
+        assert torch.equal(blocked, exp), ti
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 100, 256, 64, 64), (1, 300, 256, 32, 48), (4, 100, 256, 256, 256)])
+def test_mask_head_vs_oracle(dtype, shape):
+    ops = _ops()
+    B, Q, C, H, W = shape
+    g = torch.Generator().manual_seed(12)
+    E = (torch.randn(B, Q, C, generator=g) / 8).to(dtype)
+    P = torch.randn(B, H * W, C, generator=g).to(dtype)
+    Ed, Pd = E.to(DEV), P.to(DEV)
+    lo = ops.mask_head(Ed, Pd, H, W)
+    # oracle on the same (rounded) inputs in f32; bf16 products are exact in f32
+    for b in range(B):
+        ref = torch.einsum("qc,nc->qn", E[b].float(), P[b].float()).view(Q, H, W)
+        np.testing.assert_allclose(lo[b].cpu().numpy(), ref.numpy(), atol=2e-5 if dtype == torch.float32 else 1e-4,
+                                   rtol=1e-5)
+        if B * H * W > 65536 and b > 0:
+            break
+
+
+def test_attn_bitmask_vs_oracle():
+    ops = _ops()
+    g = torch.Generator().manual_seed(13)
+    lo = torch.randn(2, 7, 64, 64, generator=g) * 3
+    lo[0, 2] = -5.0          # fully blocked row -> un-blocked by the fix
+    for tgt in [(8, 8), (16, 16), (32, 32), (64, 64), (5, 7)]:
+        words = ops.attn_bitmask(lo.to(DEV), tgt)
+        am = torch.nn.functional.interpolate(lo, size=tgt, mode="bilinear", align_corners=False)
+        exp = R.unblock_full_rows(am.sigmoid().flatten(2) < 0.5)
+        got = ops.unpack_bitmask(words, tgt[0] * tgt[1]).cpu()
+        assert torch.equal(got, exp), tgt
+        assert not got[0, 2].any()
+
+
+# ------------------------------------------------------------------ masked cross-attention
+def _xattn_case(B, Q, S, heads, seed, dtype=torch.float32, p_block=0.7):
+    g = torch.Generator().manual_seed(seed)
+    C = heads * 32
+    q = torch.randn(B, Q, C, generator=g).to(dtype)
+    k = torch.randn(B, S, C, generator=g).to(dtype)
+    v = torch.randn(B, S, C, generator=g).to(dtype)
+    blocked = torch.rand(B, Q, S, generator=g) < p_block
+    blocked[0, 0] = True                  # fully blocked -> fixed
+    blocked = R.unblock_full_rows(blocked)
+    nw = (S + 31) // 32
+    pad = torch.zeros(B, Q, nw * 32, dtype=torch.bool)
+    pad[..., :S] = blocked
+    bits = (pad.view(B, Q, nw, 32).to(torch.int64) << torch.arange(32)).sum(-1)
+    words = torch.where(bits >= 2 ** 31, bits - 2 ** 32, bits).to(torch.int32)
+    return q, k, v, blocked, words
+
+
+@pytest.mark.parametrize("cfg", [dict(B=2, Q=7, S=40, heads=2), dict(B=2, Q=100, S=1024, heads=8),
+                                 dict(B=1, Q=100, S=16384, heads=8), dict(B=1, Q=300, S=4096, heads=8)])
+def test_masked_attention_fp32_vs_oracle(cfg):
+    ops = _ops()
+    q, k, v, blocked, words = _xattn_case(cfg["B"], cfg["Q"], cfg["S"], cfg["heads"], seed=21)
+    assert torch.equal(ops.unpack_bitmask(words, cfg["S"]), blocked)
+    H = cfg["heads"]
+    qr, kr, vr = (t.clone().requires_grad_(True) for t in (q, k, v))
+    B, Q, C = q.shape
+    S = k.shape[1]
+    ref = R.masked_attention_ref(qr.view(B, Q, H, 32).transpose(1, 2), kr.view(B, S, H, 32).transpose(1, 2),
+                                 vr.view(B, S, H, 32).transpose(1, 2), blocked)
+    go = torch.randn(ref.shape, generator=torch.Generator().manual_seed(22))
+    ref.backward(go)
+    qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
+    out = ops.masked_attention(qd, kd, vd, words.to(DEV), H)
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), atol=1e-5, rtol=0)
+    out.backward(go.to(DEV))
+    for a, r_ in ((qd, qr), (kd, kr), (vd, vr)):
+        np.testing.assert_allclose(a.grad.cpu().numpy(), r_.grad.numpy(), atol=5e-5, rtol=0)
+
+
+def test_masked_attention_golden(golden):
+    ops = _ops()
+    d = golden("masked_attn.npz")
+    D, heads = 64, 2
+    W = torch.from_numpy(d["w_in_proj_weight"])
+    b = torch.from_numpy(d["w_in_proj_bias"])
+    q = torch.nn.functional.linear(torch.from_numpy(d["q"]).transpose(0, 1), W[:D], b[:D])
+    k = torch.nn.functional.linear(torch.from_numpy(d["k"]).transpose(0, 1), W[D:2 * D], b[D:2 * D])
+    v = torch.nn.functional.linear(torch.from_numpy(d["v"]).transpose(0, 1), W[2 * D:], b[2 * D:])
+    B, Q, S = q.shape[0], q.shape[1], k.shape[1]
+    blocked = torch.from_numpy(d["blocked_fixed"]).view(B, heads, Q, S)[:, 0]
+    nw = (S + 31) // 32
+    pad = torch.zeros(B, Q, nw * 32, dtype=torch.bool)
+    pad[..., :S] = blocked
+    bits = (pad.view(B, Q, nw, 32).to(torch.int64) << torch.arange(32)).sum(-1)
+    words = torch.where(bits >= 2 ** 31, bits - 2 ** 32, bits).to(torch.int32)
+    o = ops.masked_attention(q.to(DEV), k.to(DEV), v.to(DEV), words.to(DEV), heads).cpu()
+    o = torch.nn.functional.linear(o, torch.from_numpy(d["w_out_proj.weight"]), torch.from_numpy(d["w_out_proj.bias"]))
+    np.testing.assert_allclose(o.transpose(0, 1).numpy(), d["out"], atol=1e-5, rtol=0)
+
+
+def test_masked_attention_bf16_vs_oracle():
+    ops = _ops()
+    q, k, v, blocked, words = _xattn_case(2, 100, 4096, 8, seed=23, dtype=torch.bfloat16)
+    B, Q, C = q.shape
+    S = k.shape[1]
+    ref = R.masked_attention_ref(q.float().view(B, Q, 8, 32).transpose(1, 2), k.float().view(B, S, 8, 32).transpose(1, 2),
+                                 v.float().view(B, S, 8, 32).transpose(1, 2), blocked)
+    out = ops.masked_attention(q.to(DEV), k.to(DEV), v.to(DEV), words.to(DEV), 8)
+    err = (out.float().cpu() - ref).abs()
+    assert bool((err <= ref.abs() * 2 ** -8 + 1e-3).all()), float(err.max())

@@ -1,0 +1,186 @@
+// Mask head: logits[b,q,n] = sum_c E[b,q,c] * P[b,n,c]  (HF:m2f:2040-2051 einsum
+// 'bqc,bchw->bqhw' with the pixel embedding kept channels-last, P = [B, H*W, C]),
+// and the masked-attention bitmask derived from it (HF:m2f:2049-2055, row fix
+// HF:m2f:1912-1914).
+//
+// GEMM: per batch M = Q (queries, <=128 per workgroup z-slice), N = H*W pixels,
+// K = C.  Both operands are K-contiguous (E row-major, P channels-last), so every MFMA
+// fragment is a contiguous 16-B (bf16) / 4-B (f32) read: E for the workgroup's 128
+// query rows is staged once in LDS (rows padded by 16 B -> conflict-free ds_read_b128),
+// P fragments are loaded straight from HBM (each pixel row is read exactly once per
+// launch: the kernel is HBM-bound, AI ~ 2Q flop per 4+2C/Q bytes).  bf16 path:
+// v_mfma_f32_32x32x16_bf16; f32 path (parity mode): v_mfma_f32_32x32x2_f32 (exact
+// f32 products, k-ordered f32 accumulation).  4 waves per workgroup, one 32-pixel
+// column tile per wave per iteration, 4 query tiles of 32 per wave (64 acc VGPRs).
+//
+// Bitmask: one workgroup per (b, q): bilinear (align_corners=False, PyTorch's
+// area_pixel_compute_source_index rule) resize of the logits row to (th, tw), blocked
+// bit = sigmoid(v) < 0.5, 32 keys per u32 word (bit k%32 of word k/32); a row blocked
+// at every key is written as all-zero (un-blocked), so the consumer needs no fix-up.
+#include "common.h"
+
+namespace vs {
+namespace {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+constexpr int kQT = 4;          // 32-row query tiles per workgroup (128 rows)
+constexpr int kWaves = 4;
+
+template <typename T>
+__global__ void __launch_bounds__(256) mask_head_fwd_kernel(const T* __restrict__ E, const T* __restrict__ P,
+                                                            float* __restrict__ out, int Q, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* sE = reinterpret_cast<T*>(smem_raw);
+  const int ldE = K + 16 / (int)sizeof(T);  // pad each row by 16 bytes
+  const int b = blockIdx.y;
+  const int q0 = blockIdx.z * 32 * kQT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  // ---- stage E rows [q0, q0+128) of batch b into LDS (zero rows past Q)
+  {
+    constexpr int V = 16 / sizeof(T);
+    const int chunks = K / V;
+    for (int idx = threadIdx.x; idx < 32 * kQT * chunks; idx += blockDim.x) {
+      const int row = idx / chunks, c = (idx % chunks) * V;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (q0 + row < Q) v = *reinterpret_cast<const uint4*>(E + ((size_t)b * Q + q0 + row) * K + c);
+      *reinterpret_cast<uint4*>(sE + row * ldE + c) = v;
+    }
+  }
+  __syncthreads();
+  const T* Pb = P + (size_t)b * N * K;
+  float* Ob = out + (size_t)b * Q * N;
+  const int tiles = (N + 31) / 32;
+  for (int tile = blockIdx.x * kWaves + wave; tile < tiles; tile += gridDim.x * kWaves) {
+    const int n0 = tile * 32;
+    const int n = n0 + r;
+    const bool nvalid = n < N;
+    f32x16_t acc[kQT];
+#pragma unroll
+    for (int t = 0; t < kQT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    const T* prow = Pb + (size_t)(nvalid ? n : 0) * K;
+    if constexpr (sizeof(T) == 2) {
+      for (int k0 = 0; k0 < K; k0 += 16) {
+        bf16x8_t bfrag = *reinterpret_cast<const bf16x8_t*>(prow + k0 + 8 * hh);
+        if (!nvalid) bfrag = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < kQT; ++t) {
+          const bf16x8_t afrag = *reinterpret_cast<const bf16x8_t*>(sE + (32 * t + r) * ldE + k0 + 8 * hh);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag, bfrag, acc[t], 0, 0, 0);
+        }
+      }
+    } else {
+      for (int k0 = 0; k0 < K; k0 += 2) {
+        float bv = nvalid ? (float)prow[k0 + hh] : 0.f;
+#pragma unroll
+        for (int t = 0; t < kQT; ++t) {
+          const float av = (float)sE[(32 * t + r) * ldE + k0 + hh];
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    if (nvalid) {
+#pragma unroll
+      for (int t = 0; t < kQT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = q0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (row < Q) Ob[(size_t)row * N + n] = acc[t][i];
+        }
+    }
+  }
+}
+
+// PyTorch upsample_bilinear2d (align_corners=False) source index for one axis.
+__device__ __forceinline__ void src_index(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  const float scale = (float)in / (float)out;
+  float s = scale * ((float)dst + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = s - (float)i0;
+  l0 = 1.f - l1;
+}
+
+__global__ void __launch_bounds__(256) attn_bitmask_kernel(const float* __restrict__ logits,
+                                                           uint32_t* __restrict__ words, int H, int W,
+                                                           int th, int tw, int nwords) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sw[];
+  __shared__ int s_count;
+  const long long row = blockIdx.x;  // (b, q)
+  const float* src = logits + row * (long long)H * W;
+  if (threadIdx.x == 0) s_count = 0;
+  for (int i = threadIdx.x; i < nwords; i += blockDim.x) sw[i] = 0u;
+  __syncthreads();
+  const int total = th * tw;
+  int local = 0;
+  for (int k = threadIdx.x; k < total; k += blockDim.x) {
+    const int y = k / tw, x = k - y * tw;
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    src_index(y, H, th, y0, y1, ly0, ly1);
+    src_index(x, W, tw, x0, x1, lx0, lx1);
+    const float v = ly0 * (lx0 * src[y0 * W + x0] + lx1 * src[y0 * W + x1]) +
+                    ly1 * (lx0 * src[y1 * W + x0] + lx1 * src[y1 * W + x1]);
+    const float sg = 1.f / (1.f + expf(-v));
+    if (sg < 0.5f) {
+      atomicOr(&sw[k >> 5], 1u << (k & 31));
+      ++local;
+    }
+  }
+  atomicAdd(&s_count, local);
+  __syncthreads();
+  const bool full = s_count == total;
+  uint32_t* dst = words + row * nwords;
+  for (int i = threadIdx.x; i < nwords; i += blockDim.x) dst[i] = full ? 0u : sw[i];
+}
+
+}  // namespace
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" int vs_mask_head_forward(int dtype, const void* E, const void* P, float* logits, int B, int Q,
+                                    int C, int H, int W, void* stream) {
+  VS_CHECK(E && P && logits, "null pointer");
+  VS_CHECK(B > 0 && Q > 0 && C > 0 && H > 0 && W > 0, "bad sizes");
+  const int N = H * W;
+  hipStream_t st = (hipStream_t)stream;
+  const int qz = (Q + 32 * kQT - 1) / (32 * kQT);
+  const int tiles = (N + 31) / 32;
+  int gx = (tiles + kWaves - 1) / kWaves;
+  const int cap = (2048 + B * qz - 1) / (B * qz);
+  if (gx > cap) gx = cap;
+  dim3 grid(gx, B, qz);
+  if (dtype == VS_BF16) {
+    VS_CHECK(C % 16 == 0 && C <= 512, "bf16 mask head needs C % 16 == 0, C <= 512");
+    const size_t lds = (size_t)32 * kQT * (C + 8) * 2;
+    hipLaunchKernelGGL(mask_head_fwd_kernel<bf16>, grid, dim3(256), lds, st, (const bf16*)E, (const bf16*)P,
+                       logits, Q, N, C);
+  } else if (dtype == VS_F32) {
+    VS_CHECK(C % 4 == 0 && C <= 256, "f32 mask head needs C % 4 == 0, C <= 256");
+    const size_t lds = (size_t)32 * kQT * (C + 4) * 4;
+    hipLaunchKernelGGL(mask_head_fwd_kernel<float>, grid, dim3(256), lds, st, (const float*)E, (const float*)P,
+                       logits, Q, N, C);
+  } else {
+    VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
+  }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_attn_bitmask(const float* logits, uint32_t* words, int rows, int H, int W, int th, int tw,
+                               void* stream) {
+  VS_CHECK(logits && words, "null pointer");
+  VS_CHECK(rows > 0 && H > 0 && W > 0 && th > 0 && tw > 0, "bad sizes");
+  const int nwords = (th * tw + 31) / 32;
+  VS_CHECK(nwords * 4 <= 64 * 1024, "target too large");
+  hipLaunchKernelGGL(attn_bitmask_kernel, dim3(rows), dim3(256), nwords * 4, (hipStream_t)stream, logits, words,
+                     H, W, th, tw, nwords);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

@@ -1,0 +1,418 @@
+// Masked cross-attention core of the Mask2Former decoder (HF:m2f:1644-1650: an
+// nn.MultiheadAttention with a boolean attn_mask, True = blocked; rows blocked at
+// every key are un-blocked before use, HF:m2f:1912-1914 — the bitmask producer
+// (vs_attn_bitmask) already wrote such rows as all-zero).
+//
+//   O_i = softmax_{j unblocked}( (q_i . k_j) * scale ) V      per (batch, head)
+//
+// Layout: q [B, Q, heads*32], k/v [B, S, heads*32] (batch-first in_proj outputs),
+// words u32 [B, Q, ceil(S/32)] (bit j%32 of word j/32 = key j blocked, shared by all
+// heads), out [B, Q, heads*32], lse f32 [B, heads, Q].
+//
+// Forward = split-K ("flash-decoding"): the keys are cut into chunks so the grid has
+// ~B*heads*32 workgroups even though Q is only 100; each workgroup stages its K/V
+// chunk in LDS (128 keys per stage, f32) and gives one lane per query (two-pass max
+// then exp-sum/PV per chunk, blocked keys skipped); a combine kernel merges the chunk
+// partials (m, l, o) into O and the log-sum-exp.  Backward: dQ per chunk (lane per
+// query, P recomputed from the saved lse, partials summed over chunks by a combine
+// kernel — deterministic) and dK/dV with one lane per key over all queries staged in
+// LDS.  Scalar f32 FMA datapath (first correct path; MFMA version is the next step).
+#include "common.h"
+
+namespace vs {
+namespace {
+
+constexpr int kD = 32;
+constexpr int kStage = 128;   // keys per LDS stage
+constexpr int kQTile = 128;   // queries per workgroup (lanes)
+
+__device__ __forceinline__ float dot32_lds(const float* a, const float* b_lds) {
+  float s = 0.f;
+  const float4* b4 = reinterpret_cast<const float4*>(b_lds);
+#pragma unroll
+  for (int c = 0; c < kD / 4; ++c) {
+    const float4 b = b4[c];
+    s = fmaf(a[4 * c + 0], b.x, s);
+    s = fmaf(a[4 * c + 1], b.y, s);
+    s = fmaf(a[4 * c + 2], b.z, s);
+    s = fmaf(a[4 * c + 3], b.w, s);
+  }
+  return s;
+}
+
+template <typename T>
+__device__ __forceinline__ void load_head_row(const T* src, float* dst) {
+  constexpr int V = Vec16<T>::N;
+#pragma unroll
+  for (int c = 0; c < kD; c += V) Vec16<T>::load(src + c, dst + c);
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_kv(const T* base, int C, int h, int j0, int n, float* dst) {
+  constexpr int V = Vec16<T>::N;
+  constexpr int CH = kD / V;
+  for (int idx = threadIdx.x; idx < kStage * CH; idx += blockDim.x) {
+    const int t = idx / CH, c = (idx % CH) * V;
+    float tmp[V];
+    if (t < n) {
+      Vec16<T>::load(base + (size_t)(j0 + t) * C + h * kD + c, tmp);
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) tmp[e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) dst[t * kD + c + e] = tmp[e];
+  }
+}
+
+struct XGeom {
+  int B, Q, S, heads, nw, chunk, nchunk;
+  float scale;
+};
+
+// partial layout: po [B, heads, nchunk, Q, 32], pml [B, heads, nchunk, Q, 2]
+template <typename T>
+__global__ void __launch_bounds__(kQTile) xattn_fwd_partial(const T* __restrict__ q, const T* __restrict__ k,
+                                                            const T* __restrict__ v, const uint32_t* __restrict__ words,
+                                                            float* __restrict__ po, float* __restrict__ pml, XGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sk = smem;
+  float* sv = sk + kStage * kD;
+  const int chunk = blockIdx.x, h = blockIdx.y;
+  const int qg = blockIdx.z % ((g.Q + kQTile - 1) / kQTile);
+  const int b = blockIdx.z / ((g.Q + kQTile - 1) / kQTile);
+  const int C = g.heads * kD;
+  const int i = qg * kQTile + threadIdx.x;
+  const bool active = i < g.Q;
+  float qi[kD];
+  if (active) {
+    load_head_row(q + ((size_t)b * g.Q + i) * C + h * kD, qi);
+#pragma unroll
+    for (int c = 0; c < kD; ++c) qi[c] *= g.scale;
+  }
+  const uint32_t* wrow = words + ((size_t)b * g.Q + (active ? i : 0)) * g.nw;
+  const int jbeg = chunk * g.chunk;
+  const int jend = min(g.S, jbeg + g.chunk);
+  const T* kb = k + (size_t)b * g.S * C;
+  const T* vb = v + (size_t)b * g.S * C;
+  float m = -INFINITY, l = 0.f;
+  float o[kD];
+#pragma unroll
+  for (int c = 0; c < kD; ++c) o[c] = 0.f;
+  for (int j0 = jbeg; j0 < jend; j0 += kStage) {
+    const int n = min(kStage, jend - j0);
+    __syncthreads();
+    stage_kv(kb, C, h, j0, n, sk);
+    stage_kv(vb, C, h, j0, n, sv);
+    __syncthreads();
+    if (!active) continue;
+    // pass 1: stage max (the running max only grows; rescale once per stage)
+    float ms = -INFINITY;
+    for (int t = 0; t < n; ++t) {
+      const int j = j0 + t;
+      if ((wrow[j >> 5] >> (j & 31)) & 1u) continue;
+      ms = fmaxf(ms, dot32_lds(qi, sk + t * kD));
+    }
+    if (ms == -INFINITY) continue;
+    const float mn = fmaxf(m, ms);
+    const float alpha = __expf(m - mn);  // m = -inf -> 0
+    l *= alpha;
+#pragma unroll
+    for (int c = 0; c < kD; ++c) o[c] *= alpha;
+    m = mn;
+    for (int t = 0; t < n; ++t) {
+      const int j = j0 + t;
+      if ((wrow[j >> 5] >> (j & 31)) & 1u) continue;
+      const float p = __expf(dot32_lds(qi, sk + t * kD) - m);
+      l += p;
+      const float4* v4 = reinterpret_cast<const float4*>(sv + t * kD);
+#pragma unroll
+      for (int c = 0; c < kD / 4; ++c) {
+        const float4 vv = v4[c];
+        o[4 * c + 0] = fmaf(p, vv.x, o[4 * c + 0]);
+        o[4 * c + 1] = fmaf(p, vv.y, o[4 * c + 1]);
+        o[4 * c + 2] = fmaf(p, vv.z, o[4 * c + 2]);
+        o[4 * c + 3] = fmaf(p, vv.w, o[4 * c + 3]);
+      }
+    }
+  }
+  if (!active) return;
+  const size_t prow = (((size_t)b * g.heads + h) * g.nchunk + chunk) * g.Q + i;
+  float4* dst = reinterpret_cast<float4*>(po + prow * kD);
+#pragma unroll
+  for (int c = 0; c < kD / 4; ++c) dst[c] = make_float4(o[4 * c], o[4 * c + 1], o[4 * c + 2], o[4 * c + 3]);
+  pml[prow * 2 + 0] = m;
+  pml[prow * 2 + 1] = l;
+}
+
+// one lane per (b, h, q, channel-quad): merge chunk partials
+template <typename T>
+__global__ void __launch_bounds__(256) xattn_fwd_combine(const float* __restrict__ po, const float* __restrict__ pml,
+                                                         T* __restrict__ out, float* __restrict__ lse, XGeom g) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long rows = (long long)g.B * g.heads * g.Q;
+  if (gid >= rows * 8) return;
+  const int quad = (int)(gid & 7);
+  const long long row = gid >> 3;  // (b, h, q)
+  const int i = (int)(row % g.Q);
+  const long long bh = row / g.Q;
+  const int h = (int)(bh % g.heads);
+  const long long b = bh / g.heads;
+  float M = -INFINITY;
+  for (int c = 0; c < g.nchunk; ++c) M = fmaxf(M, pml[((bh * g.nchunk + c) * g.Q + i) * 2]);
+  float lsum = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < g.nchunk; ++c) {
+    const size_t pr = (bh * g.nchunk + c) * g.Q + i;
+    const float mc = pml[pr * 2];
+    if (mc == -INFINITY) continue;
+    const float w = __expf(mc - M);
+    lsum += w * pml[pr * 2 + 1];
+    const float4 v = reinterpret_cast<const float4*>(po + pr * kD)[quad];
+    acc[0] += w * v.x; acc[1] += w * v.y; acc[2] += w * v.z; acc[3] += w * v.w;
+  }
+  const float inv = 1.f / lsum;
+  T* dst = out + ((size_t)b * g.Q + i) * (g.heads * kD) + h * kD + quad * 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) dst[e] = from_f32<T>(acc[e] * inv);
+  if (quad == 0) lse[row] = M + __logf(lsum);
+}
+
+// dQ partials per key chunk (lane = query) + D_i = dO_i . O_i (written by chunk 0)
+template <typename T>
+__global__ void __launch_bounds__(kQTile) xattn_bwd_dq_partial(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ words,
+    const T* __restrict__ out, const float* __restrict__ lse, const T* __restrict__ gout, float* __restrict__ pdq,
+    float* __restrict__ Dbuf, XGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sk = smem;
+  float* sv = sk + kStage * kD;
+  const int chunk = blockIdx.x, h = blockIdx.y;
+  const int nqg = (g.Q + kQTile - 1) / kQTile;
+  const int qg = blockIdx.z % nqg, b = blockIdx.z / nqg;
+  const int C = g.heads * kD;
+  const int i = qg * kQTile + threadIdx.x;
+  const bool active = i < g.Q;
+  float qi[kD], di[kD], dq[kD];
+  float Li = 0.f, Di = 0.f;
+  if (active) {
+    float oi[kD];
+    load_head_row(q + ((size_t)b * g.Q + i) * C + h * kD, qi);
+    load_head_row(gout + ((size_t)b * g.Q + i) * C + h * kD, di);
+    load_head_row(out + ((size_t)b * g.Q + i) * C + h * kD, oi);
+#pragma unroll
+    for (int c = 0; c < kD; ++c) { Di = fmaf(di[c], oi[c], Di); qi[c] *= g.scale; dq[c] = 0.f; }
+    Li = lse[((size_t)b * g.heads + h) * g.Q + i];
+    if (chunk == 0) Dbuf[((size_t)b * g.heads + h) * g.Q + i] = Di;
+  }
+  const uint32_t* wrow = words + ((size_t)b * g.Q + (active ? i : 0)) * g.nw;
+  const int jbeg = chunk * g.chunk, jend = min(g.S, jbeg + g.chunk);
+  const T* kb = k + (size_t)b * g.S * C;
+  const T* vb = v + (size_t)b * g.S * C;
+  for (int j0 = jbeg; j0 < jend; j0 += kStage) {
+    const int n = min(kStage, jend - j0);
+    __syncthreads();
+    stage_kv(kb, C, h, j0, n, sk);
+    stage_kv(vb, C, h, j0, n, sv);
+    __syncthreads();
+    if (!active) continue;
+    for (int t = 0; t < n; ++t) {
+      const int j = j0 + t;
+      if ((wrow[j >> 5] >> (j & 31)) & 1u) continue;
+      const float p = __expf(dot32_lds(qi, sk + t * kD) - Li);
+      const float ds = p * (dot32_lds(di, sv + t * kD) - Di);
+      const float4* k4 = reinterpret_cast<const float4*>(sk + t * kD);
+#pragma unroll
+      for (int c = 0; c < kD / 4; ++c) {
+        const float4 kk = k4[c];
+        dq[4 * c + 0] = fmaf(ds, kk.x, dq[4 * c + 0]);
+        dq[4 * c + 1] = fmaf(ds, kk.y, dq[4 * c + 1]);
+        dq[4 * c + 2] = fmaf(ds, kk.z, dq[4 * c + 2]);
+        dq[4 * c + 3] = fmaf(ds, kk.w, dq[4 * c + 3]);
+      }
+    }
+  }
+  if (!active) return;
+  const size_t prow = (((size_t)b * g.heads + h) * g.nchunk + chunk) * g.Q + i;
+  float4* dst = reinterpret_cast<float4*>(pdq + prow * kD);
+#pragma unroll
+  for (int c = 0; c < kD / 4; ++c)
+    dst[c] = make_float4(dq[4 * c] * g.scale, dq[4 * c + 1] * g.scale, dq[4 * c + 2] * g.scale, dq[4 * c + 3] * g.scale);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) xattn_bwd_dq_combine(const float* __restrict__ pdq, T* __restrict__ gq, XGeom g) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)g.B * g.heads * g.Q * kD;
+  if (gid >= total) return;
+  const int c = (int)(gid % kD);
+  const long long row = gid / kD;  // (b, h, q)
+  const int i = (int)(row % g.Q);
+  const long long bh = row / g.Q;
+  const int h = (int)(bh % g.heads);
+  const long long b = bh / g.heads;
+  float s = 0.f;
+  for (int ch = 0; ch < g.nchunk; ++ch) s += pdq[((bh * g.nchunk + ch) * g.Q + i) * kD + c];
+  gq[((size_t)b * g.Q + i) * (g.heads * kD) + h * kD + c] = from_f32<T>(s);
+}
+
+// dK, dV: lane = key; all queries of (b, h) staged in LDS
+template <typename T>
+__global__ void __launch_bounds__(256) xattn_bwd_dkdv(const T* __restrict__ q, const T* __restrict__ k,
+                                                      const T* __restrict__ v, const uint32_t* __restrict__ words,
+                                                      const float* __restrict__ lse, const float* __restrict__ Dbuf,
+                                                      const T* __restrict__ gout, T* __restrict__ gk,
+                                                      T* __restrict__ gv, XGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Q = g.Q;
+  float* sq = smem;               // [Q][32] (pre-scaled)
+  float* sdo = sq + Q * kD;       // [Q][32]
+  float* sl = sdo + Q * kD;       // [Q]
+  float* sD = sl + Q;             // [Q]
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int C = g.heads * kD;
+  {
+    constexpr int V = Vec16<T>::N;
+    constexpr int CH = kD / V;
+    for (int idx = threadIdx.x; idx < Q * CH; idx += blockDim.x) {
+      const int t = idx / CH, c = (idx % CH) * V;
+      float a[V], d[V];
+      Vec16<T>::load(q + ((size_t)b * Q + t) * C + h * kD + c, a);
+      Vec16<T>::load(gout + ((size_t)b * Q + t) * C + h * kD + c, d);
+#pragma unroll
+      for (int e = 0; e < V; ++e) { sq[t * kD + c + e] = a[e] * g.scale; sdo[t * kD + c + e] = d[e]; }
+    }
+    for (int t = threadIdx.x; t < Q; t += blockDim.x) {
+      sl[t] = lse[((size_t)b * g.heads + h) * Q + t];
+      sD[t] = Dbuf[((size_t)b * g.heads + h) * Q + t];
+    }
+  }
+  __syncthreads();
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= g.S) return;
+  float kj[kD], vj[kD], dk[kD], dv[kD];
+  load_head_row(k + ((size_t)b * g.S + j) * C + h * kD, kj);
+  load_head_row(v + ((size_t)b * g.S + j) * C + h * kD, vj);
+#pragma unroll
+  for (int c = 0; c < kD; ++c) { dk[c] = 0.f; dv[c] = 0.f; }
+  const uint32_t* wcol = words + (size_t)b * Q * g.nw + (j >> 5);
+  const uint32_t bit = 1u << (j & 31);
+  for (int i = 0; i < Q; ++i) {
+    if (wcol[(size_t)i * g.nw] & bit) continue;
+    const float p = __expf(dot32_lds(kj, sq + i * kD) - sl[i]);
+    const float ds = p * (dot32_lds(vj, sdo + i * kD) - sD[i]);
+    const float4* q4 = reinterpret_cast<const float4*>(sq + i * kD);
+    const float4* d4 = reinterpret_cast<const float4*>(sdo + i * kD);
+#pragma unroll
+    for (int c = 0; c < kD / 4; ++c) {
+      const float4 qq = q4[c];
+      const float4 dd = d4[c];
+      dk[4 * c + 0] = fmaf(ds, qq.x, dk[4 * c + 0]);
+      dk[4 * c + 1] = fmaf(ds, qq.y, dk[4 * c + 1]);
+      dk[4 * c + 2] = fmaf(ds, qq.z, dk[4 * c + 2]);
+      dk[4 * c + 3] = fmaf(ds, qq.w, dk[4 * c + 3]);
+      dv[4 * c + 0] = fmaf(p, dd.x, dv[4 * c + 0]);
+      dv[4 * c + 1] = fmaf(p, dd.y, dv[4 * c + 1]);
+      dv[4 * c + 2] = fmaf(p, dd.z, dv[4 * c + 2]);
+      dv[4 * c + 3] = fmaf(p, dd.w, dv[4 * c + 3]);
+    }
+  }
+  // sq was pre-scaled, so dk already carries the 'scale' factor of dS/dK
+  constexpr int V = Vec16<T>::N;
+#pragma unroll
+  for (int c = 0; c < kD; c += V) {
+    Vec16<T>::store(gk + ((size_t)b * g.S + j) * C + h * kD + c, dk + c);
+    Vec16<T>::store(gv + ((size_t)b * g.S + j) * C + h * kD + c, dv + c);
+  }
+}
+
+XGeom make_geom(int B, int Q, int S, int heads, float scale) {
+  XGeom g;
+  g.B = B; g.Q = Q; g.S = S; g.heads = heads; g.scale = scale;
+  g.nw = (S + 31) / 32;
+  // ~32 key chunks per (b, head) on long maps, at least one 128-key stage per chunk
+  int chunk = (S + 31) / 32;
+  chunk = ((chunk + kStage - 1) / kStage) * kStage;
+  if (chunk < kStage) chunk = kStage;
+  g.chunk = chunk;
+  g.nchunk = (S + chunk - 1) / chunk;
+  return g;
+}
+
+}  // namespace
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" long long vs_masked_attn_workspace_bytes(int B, int Q, int S, int heads) {
+  XGeom g = make_geom(B, Q, S, heads, 1.f);
+  const long long rows = (long long)B * heads * g.nchunk * Q;
+  return rows * (kD + 2) * 4 + (long long)B * heads * Q * 4 + 256;
+}
+
+extern "C" int vs_masked_attn_forward(int dtype, const void* q, const void* k, const void* v,
+                                      const uint32_t* words, void* out, float* lse, void* workspace,
+                                      int B, int Q, int S, int heads, float scale, void* stream) {
+  VS_CHECK(q && k && v && words && out && lse && workspace, "null pointer");
+  VS_CHECK(B > 0 && Q > 0 && S > 0 && heads > 0, "bad sizes");
+  XGeom g = make_geom(B, Q, S, heads, scale);
+  float* po = (float*)workspace;
+  float* pml = po + (size_t)B * heads * g.nchunk * Q * kD;
+  hipStream_t st = (hipStream_t)stream;
+  const int nqg = (Q + kQTile - 1) / kQTile;
+  dim3 grid(g.nchunk, heads, B * nqg);
+  const size_t lds = 2 * kStage * kD * sizeof(float);
+  const long long crows = (long long)B * heads * Q * 8;
+  const int cgrid = (int)((crows + 255) / 256);
+  if (dtype == VS_BF16) {
+    hipLaunchKernelGGL(xattn_fwd_partial<bf16>, grid, dim3(kQTile), lds, st, (const bf16*)q, (const bf16*)k,
+                       (const bf16*)v, words, po, pml, g);
+    hipLaunchKernelGGL(xattn_fwd_combine<bf16>, dim3(cgrid), dim3(256), 0, st, po, pml, (bf16*)out, lse, g);
+  } else if (dtype == VS_F32) {
+    hipLaunchKernelGGL(xattn_fwd_partial<float>, grid, dim3(kQTile), lds, st, (const float*)q, (const float*)k,
+                       (const float*)v, words, po, pml, g);
+    hipLaunchKernelGGL(xattn_fwd_combine<float>, dim3(cgrid), dim3(256), 0, st, po, pml, (float*)out, lse, g);
+  } else {
+    VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
+  }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_masked_attn_backward(int dtype, const void* q, const void* k, const void* v,
+                                       const uint32_t* words, const void* out, const float* lse,
+                                       const void* grad_out, void* grad_q, void* grad_k, void* grad_v,
+                                       void* workspace, int B, int Q, int S, int heads, float scale,
+                                       void* stream) {
+  VS_CHECK(q && k && v && words && out && lse && grad_out && grad_q && grad_k && grad_v && workspace,
+           "null pointer");
+  VS_CHECK(B > 0 && Q > 0 && S > 0 && heads > 0, "bad sizes");
+  XGeom g = make_geom(B, Q, S, heads, scale);
+  const size_t lds_dkdv = (2 * (size_t)Q * kD + 2 * Q) * sizeof(float);
+  VS_CHECK(lds_dkdv <= 160 * 1024, "too many queries for the dK/dV kernel");
+  float* pdq = (float*)workspace;
+  float* Dbuf = pdq + (size_t)B * heads * g.nchunk * Q * kD + (size_t)B * heads * g.nchunk * Q * 2;
+  hipStream_t st = (hipStream_t)stream;
+  const int nqg = (Q + kQTile - 1) / kQTile;
+  dim3 grid(g.nchunk, heads, B * nqg);
+  const size_t lds = 2 * kStage * kD * sizeof(float);
+  const long long total = (long long)B * heads * Q * kD;
+  const int cgrid = (int)((total + 255) / 256);
+  dim3 kgrid((S + 255) / 256, heads, B);
+  if (dtype == VS_BF16) {
+    hipLaunchKernelGGL(xattn_bwd_dq_partial<bf16>, grid, dim3(kQTile), lds, st, (const bf16*)q, (const bf16*)k,
+                       (const bf16*)v, words, (const bf16*)out, lse, (const bf16*)grad_out, pdq, Dbuf, g);
+    hipLaunchKernelGGL(xattn_bwd_dq_combine<bf16>, dim3(cgrid), dim3(256), 0, st, pdq, (bf16*)grad_q, g);
+    hipLaunchKernelGGL(xattn_bwd_dkdv<bf16>, kgrid, dim3(256), lds_dkdv, st, (const bf16*)q, (const bf16*)k,
+                       (const bf16*)v, words, lse, Dbuf, (const bf16*)grad_out, (bf16*)grad_k, (bf16*)grad_v, g);
+  } else if (dtype == VS_F32) {
+    hipLaunchKernelGGL(xattn_bwd_dq_partial<float>, grid, dim3(kQTile), lds, st, (const float*)q, (const float*)k,
+                       (const float*)v, words, (const float*)out, lse, (const float*)grad_out, pdq, Dbuf, g);
+    hipLaunchKernelGGL(xattn_bwd_dq_combine<float>, dim3(cgrid), dim3(256), 0, st, pdq, (float*)grad_q, g);
+    hipLaunchKernelGGL(xattn_bwd_dkdv<float>, kgrid, dim3(256), lds_dkdv, st, (const float*)q, (const float*)k,
+                       (const float*)v, words, lse, Dbuf, (const float*)grad_out, (float*)grad_k, (float*)grad_v, g);
+  } else {
+    VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
+  }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

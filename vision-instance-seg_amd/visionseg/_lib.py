@@ -29,7 +29,15 @@ SIGNATURES = {
     "vs_msda_backward": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_window_partition": [_P, _P] + [_c_int] * 7 + [_P],
     "vs_window_reverse": [_P, _P] + [_c_int] * 7 + [_P],
+    "vs_window_attn_forward": [_c_int, _P, _P, _P, _P] + [_c_int] * 6 + [_c_float, _P],
+    "vs_window_attn_backward": [_c_int, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 6 + [_c_float, _P],
+    "vs_mask_head_forward": [_c_int, _P, _P, _P] + [_c_int] * 5 + [_P],
+    "vs_attn_bitmask": [_P, _P] + [_c_int] * 5 + [_P],
+    "vs_masked_attn_workspace_bytes": [_c_int] * 4,
+    "vs_masked_attn_forward": [_c_int, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 4 + [_c_float, _P],
+    "vs_masked_attn_backward": [_c_int] + [_P] * 11 + [_c_int] * 4 + [_c_float, _P],
 }
+RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
 
@@ -45,7 +53,7 @@ def lib():
         for name, args in SIGNATURES.items():
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = ctypes.c_char_p if name == "vs_last_error" else _c_int
+            fn.restype = RESTYPES.get(name, _c_int)
         _lib = L
     return _lib
 

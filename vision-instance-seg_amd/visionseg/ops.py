@@ -155,3 +155,162 @@ def window_partition(x, window: int, shift: int = 0):
 def window_reverse(windows, batch: int, height: int, width: int, window: int, shift: int = 0):
     """Inverse of window_partition: [B*nW, window^2, C] -> [B,H,W,C] (HF:swin:558-566)."""
     return _WindowReverse.apply(windows, int(batch), int(height), int(width), int(window), int(shift))
+
+
+class WindowAttentionFunction(torch.autograd.Function):
+    """Swin window attention core with the relative-position bias and the shifted-window
+    mask fused (HF:swin:373-398, 418-468, 584-607).
+
+    qkv [Bw, N, 3*C] (fused q;k;v Linear output of the partitioned windows, C =
+    heads*32), rel_table [(2ws-1)^2, heads] -> [Bw, N, C]."""
+
+    @staticmethod
+    def forward(ctx, qkv, rel_table, heads, window, shift, nwin_h, nwin_w, scale):
+        L.require_hip(qkv, rel_table)
+        qkv = qkv.contiguous()
+        table = rel_table.float().contiguous()
+        Bw, N, C3 = qkv.shape
+        C = C3 // 3
+        if C != heads * 32 or N != window * window:
+            raise ValueError(f"qkv {tuple(qkv.shape)} does not match heads={heads} (x32) window={window}")
+        out = torch.empty(Bw, N, C, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(Bw, heads, N, device=qkv.device, dtype=torch.float32)
+        with timed("window_attn_fwd", qkv):
+            L.check(L.lib().vs_window_attn_forward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
+                                                   L.ptr(lse), Bw, heads, window, shift, nwin_h, nwin_w,
+                                                   float(scale), L.stream(qkv)), "window_attn_forward")
+        ctx.meta = (heads, window, shift, nwin_h, nwin_w, float(scale), rel_table.dtype)
+        ctx.save_for_backward(qkv, table, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        qkv, table, out, lse = ctx.saved_tensors
+        heads, window, shift, nwin_h, nwin_w, scale, tdtype = ctx.meta
+        Bw, N, C3 = qkv.shape
+        g = grad_out.to(qkv.dtype).contiguous()
+        gqkv = torch.empty_like(qkv)
+        T2 = (2 * window - 1) ** 2
+        part = torch.empty(Bw, heads, T2, device=qkv.device, dtype=torch.float32)
+        with timed("window_attn_bwd", qkv):
+            L.check(L.lib().vs_window_attn_backward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
+                                                    L.ptr(lse), L.ptr(g), L.ptr(gqkv), L.ptr(part), Bw, heads,
+                                                    window, shift, nwin_h, nwin_w, scale, L.stream(qkv)),
+                    "window_attn_backward")
+        gtable = part.sum(0).t().contiguous().to(tdtype)
+        return gqkv, gtable, None, None, None, None, None, None
+
+
+def window_attention(qkv, rel_table, heads: int, window: int, shift: int, nwin_h: int, nwin_w: int,
+                     scale: float | None = None):
+    if scale is None:
+        scale = 32 ** -0.5
+    return WindowAttentionFunction.apply(qkv, rel_table, int(heads), int(window), int(shift), int(nwin_h),
+                                         int(nwin_w), float(scale))
+
+
+class MaskHeadFunction(torch.autograd.Function):
+    """logits [B,Q,H,W] f32 = einsum('bqc,bchw->bqhw') with the pixel embedding given
+    channels-last (HF:m2f:2051).  Forward: hand-written MFMA kernel.  Backward: the two
+    operand gradients are plain GEMMs (dE = dL.P, dP = dL^T.E) and go to hipBLASLt via
+    torch.matmul."""
+
+    @staticmethod
+    def forward(ctx, mask_embed, pixel_nhwc, height, width):
+        L.require_hip(mask_embed, pixel_nhwc)
+        E = mask_embed.contiguous()
+        P = pixel_nhwc.to(E.dtype).contiguous()
+        B, Q, C = E.shape
+        if P.shape != (B, height * width, C):
+            raise ValueError(f"pixel embedding {tuple(P.shape)} != {(B, height * width, C)}")
+        out = torch.empty(B, Q, height, width, device=E.device, dtype=torch.float32)
+        with timed("mask_head_fwd", E):
+            L.check(L.lib().vs_mask_head_forward(L.dtype_code(E), L.ptr(E), L.ptr(P), L.ptr(out), B, Q, C, height,
+                                                 width, L.stream(E)), "mask_head_forward")
+        ctx.save_for_backward(E, P)
+        ctx.pdtype = pixel_nhwc.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        E, P = ctx.saved_tensors
+        B, Q, C = E.shape
+        gl = g.reshape(B, Q, -1).to(E.dtype)
+        gE = torch.bmm(gl, P) if ctx.needs_input_grad[0] else None
+        gP = torch.bmm(gl.transpose(1, 2), E).to(ctx.pdtype) if ctx.needs_input_grad[1] else None
+        return gE, gP, None, None
+
+
+def mask_head(mask_embed, pixel_nhwc, height: int, width: int):
+    return MaskHeadFunction.apply(mask_embed, pixel_nhwc, int(height), int(width))
+
+
+def attn_bitmask(logits, target_hw):
+    """Blocked-key bitmask of the next decoder layer from mask logits [B,Q,H,W]
+    (HF:m2f:2049-2055 + the fully-blocked-row fix HF:m2f:1912-1914) -> int32 words
+    [B, Q, ceil(th*tw/32)] (bit k%32 of word k/32 set = key k blocked)."""
+    L.require_hip(logits)
+    lg = logits.detach().float().contiguous()
+    B, Q, H, W = lg.shape
+    th, tw = int(target_hw[0]), int(target_hw[1])
+    words = torch.empty(B, Q, (th * tw + 31) // 32, device=lg.device, dtype=torch.int32)
+    with timed("attn_bitmask", lg):
+        L.check(L.lib().vs_attn_bitmask(L.ptr(lg), L.ptr(words), B * Q, H, W, th, tw, L.stream(lg)), "attn_bitmask")
+    return words
+
+
+def unpack_bitmask(words, n_keys: int):
+    """[..., nwords] int32 -> bool [..., n_keys] (True = blocked); test/debug helper."""
+    w = words.to(torch.int64) & 0xFFFFFFFF
+    bits = (w.unsqueeze(-1) >> torch.arange(32, device=w.device)) & 1
+    return bits.flatten(-2)[..., :n_keys].bool()
+
+
+class MaskedAttentionFunction(torch.autograd.Function):
+    """softmax over unblocked keys of (q.k)*scale, times V (HF:m2f:1644-1650 core).
+    q [B,Q,heads*32], k/v [B,S,heads*32], words from `attn_bitmask` -> [B,Q,heads*32]."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, words, heads, scale):
+        L.require_hip(q, k, v, words)
+        q, k, v = q.contiguous(), k.to(q.dtype).contiguous(), v.to(q.dtype).contiguous()
+        B, Q, C = q.shape
+        S = k.shape[1]
+        if C != heads * 32 or k.shape != (B, S, C) or v.shape != (B, S, C):
+            raise ValueError("masked attention shape mismatch")
+        if words.shape != (B, Q, (S + 31) // 32):
+            raise ValueError(f"bitmask {tuple(words.shape)} does not cover {S} keys")
+        out = torch.empty_like(q)
+        lse = torch.empty(B, heads, Q, device=q.device, dtype=torch.float32)
+        ws = torch.empty(int(L.lib().vs_masked_attn_workspace_bytes(B, Q, S, heads)), device=q.device,
+                         dtype=torch.uint8)
+        with timed("masked_attn_fwd", q):
+            L.check(L.lib().vs_masked_attn_forward(L.dtype_code(q), L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(words),
+                                                   L.ptr(out), L.ptr(lse), L.ptr(ws), B, Q, S, heads, float(scale),
+                                                   L.stream(q)), "masked_attn_forward")
+        ctx.meta = (heads, float(scale))
+        ctx.save_for_backward(q, k, v, words, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        q, k, v, words, out, lse = ctx.saved_tensors
+        heads, scale = ctx.meta
+        B, Q, C = q.shape
+        S = k.shape[1]
+        g = g.to(q.dtype).contiguous()
+        gq, gk, gv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        ws = torch.empty(int(L.lib().vs_masked_attn_workspace_bytes(B, Q, S, heads)), device=q.device,
+                         dtype=torch.uint8)
+        with timed("masked_attn_bwd", q):
+            L.check(L.lib().vs_masked_attn_backward(L.dtype_code(q), L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(words),
+                                                    L.ptr(out), L.ptr(lse), L.ptr(g), L.ptr(gq), L.ptr(gk),
+                                                    L.ptr(gv), L.ptr(ws), B, Q, S, heads, scale, L.stream(q)),
+                    "masked_attn_backward")
+        return gq, gk, gv, None, None, None
+
+
+def masked_attention(q, k, v, words, heads: int, scale: float | None = None):
+    if scale is None:
+        scale = 32 ** -0.5
+    return MaskedAttentionFunction.apply(q, k, v, words, int(heads), float(scale))
