@@ -1,0 +1,177 @@
+"""Training-throughput benchmark of the MI355X Swin + Mask2Former path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model swin_t] [--batch 4] [--size 1024]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric (BASELINE.json): images/sec at 1024^2, Swin-T Mask2Former, 1/2/4/8 GPUs.  A step
+is one full training iteration (bf16 autocast forward, set criterion with Hungarian
+matching, backward, RCCL gradient all-reduce when N>1, per-parameter grad clip, AdamW)
+on a synthetic COCO-format defect batch of `--batch` images per GPU, resident in HBM
+before the timed region.  Weak scaling: per-GPU batch fixed.  Rank 0 prints ONE JSON
+line; `roofline` covers the dominant hand-written kernel (HIP events on its launch
+stream, algorithmic bytes/flops per launch); `cpu_baseline` times the oracle CPU
+restatement (fp32, fwd+loss+bwd) on the host cores on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "vision-instance-seg_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA spec
+VALU_F32_PEAK_TFS = 157.3    # f32 vector / f32 MFMA spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="swin_t")
+    ap.add_argument("--batch", type=int, default=4, help="images per GPU")
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--queries", type=int, default=100)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=2)
+    ap.add_argument("--kernel-timing", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
+    return ap.parse_args()
+
+
+def kernel_roofline(summary):
+    """Pick the hand-written kernel with the largest total time and price it against the
+    roofline of its regime (HBM bytes for gather/copy kernels, matrix FLOP/s otherwise)."""
+    if not summary:
+        return None, {}
+    name = max(summary, key=lambda k: summary[k]["total_ms"])
+    s = summary[name]
+    t = s["mean_ms"] / 1e3
+    hbm_kernels = {"msda_fwd", "msda_bwd", "window_partition", "window_reverse", "attn_bitmask", "mask_head_fwd"}
+    if name in hbm_kernels:
+        ach = s["bytes"] / t / 1e9
+        roof = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=None, kernel=name,
+                    algorithmic_bytes_per_launch=int(s["bytes"]), mean_launch_ms=round(s["mean_ms"], 4),
+                    launches=s["launches"])
+    else:
+        ach = s["flops"] / t / 1e12
+        roof = dict(bound="mfma", achieved=round(ach, 2), peak=MFMA_BF16_PEAK_TFS, unit="TFLOP/s",
+                    frac=round(ach / MFMA_BF16_PEAK_TFS, 5), traffic=None, kernel=name,
+                    algorithmic_flops_per_launch=int(s["flops"]), mean_launch_ms=round(s["mean_ms"], 4),
+                    launches=s["launches"])
+    table = {k: dict(launches=v["launches"], total_ms=round(v["total_ms"], 3), mean_ms=round(v["mean_ms"], 4),
+                     gbs=round(v["bytes"] / (v["mean_ms"] / 1e3) / 1e9, 1) if v["bytes"] else None,
+                     tflops=round(v["flops"] / (v["mean_ms"] / 1e3) / 1e12, 2) if v["flops"] else None)
+             for k, v in summary.items()}
+    return roof, table
+
+
+def cpu_baseline(model_name, size, iters, queries):
+    """Oracle CPU restatement (fp32), 1 image, forward + loss + backward, median of `iters`
+    after one warm-up; images/s on this host's cores."""
+    from oracle.ref_model import RefConfig, RefMask2Former, RefCriterion
+    from visionseg.model import M2FConfig
+    from visionseg.data import synthetic_batch
+    mc = M2FConfig.preset(model_name, num_queries=queries)
+    cfg = RefConfig.from_dict(mc.to_dict())
+    torch.manual_seed(0)
+    m = RefMask2Former(cfg)
+    crit = RefCriterion(cfg)
+    imgs, ml, cl = synthetic_batch(1, size, seed=42)
+    ml = [x.float() for x in ml]
+    ts = []
+    for i in range(iters + 1):
+        t0 = time.perf_counter()
+        masks, classes = m(imgs)
+        loss, _ = crit(masks, classes, ml, cl)
+        loss.backward()
+        m.zero_grad(set_to_none=True)
+        if i > 0:
+            ts.append(time.perf_counter() - t0)
+    ts.sort()
+    med = ts[len(ts) // 2]
+    return dict(value=round(1.0 / med, 4), unit="images/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"1x3x{size}^2 {model_name} Mask2Former fp32 fwd+loss+bwd (oracle CPU restatement), "
+                       f"median of {iters} iters after 1 warm-up, {med:.1f} s/iter")
+
+
+def main():
+    a = parse()
+    from visionseg.train import init_distributed, Trainer, SolverConfig
+    from visionseg.model import M2FConfig, Mask2Former
+    from visionseg.criterion import SetCriterion
+    from visionseg.data import synthetic_batch
+    from visionseg.profiling import KernelTimer
+
+    rank, local, world = init_distributed()
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = M2FConfig.preset(a.model, num_queries=a.queries)
+    model = Mask2Former(cfg).init_weights(seed=0)
+    trainer = Trainer(model, SetCriterion(cfg), SolverConfig(), device=dev)
+    images, ml, cl = synthetic_batch(a.batch, a.size, seed=42 + rank, device=dev)
+    torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        trainer.step(images, ml, cl)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer = KernelTimer() if a.kernel_timing else None
+    if timer:
+        timer.__enter__()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = trainer.step(images, ml, cl)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if timer:
+        timer.__exit__(None, None, None)
+    t = torch.tensor([elapsed], device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms = elapsed / a.steps * 1e3
+    value = a.batch * world * a.steps / elapsed
+    if rank == 0:
+        roof, table = kernel_roofline(timer.summary()) if timer else (None, {})
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            torch.set_num_threads(min(16, os.cpu_count() or 1))
+            cpu = cpu_baseline(a.model, a.size, a.cpu_iters, a.queries)
+        line = {
+            "metric": "images/sec @1024^2 Swin-T Mask2Former training (fwd+loss+bwd+AdamW)",
+            "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic COCO-format defect batches (random-init weights)",
+            "config": {"workload": f"C2: {a.model} + Mask2Former, {a.batch}x3x{a.size}^2 per GPU, "
+                                   f"{cfg.num_queries} queries, bf16 autocast, 1 class",
+                       "model": f"{a.model}_mask2former", "global_batch": a.batch * world, "image_size": a.size,
+                       "parallelism": f"dp{world}"},
+            "final_loss": round(float(loss.item()), 4),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "kernels": table,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

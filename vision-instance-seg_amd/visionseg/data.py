@@ -1,0 +1,175 @@
+"""COCO-format instance data for the training path.
+
+* `synthetic_batch` — BASELINE's synthetic "COCO-format defect" batches:
+  uint8 images ~ U[0,255], 1..3 thin "thunderbolt"-like polygon instances per image,
+  single class 0 (the reference remaps category 1 -> 0 for detectron2,
+  scripts/data_utils/fix_category_ids.py:25-36), masks rasterised to bool.
+* `write_coco_dataset` / `CocoInstanceDataset` — the on-disk format the reference's
+  callers hand over (`train_dir/annotations.json` + images; guide.md:144-161,
+  training/train_template.py:188-194), mapped the way the reference's
+  MaskDINODatasetMapper does (training/maskdino/train_full.py:69-147): polygon ->
+  bitmask, ResizeShortestEdge, random horizontal flip, class ids kept.
+* `normalize` — ImageNet pixel mean/std (detectron2 PIXEL_MEAN/STD in RGB order).
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import torch
+from PIL import Image, ImageDraw
+
+PIXEL_MEAN = (123.675, 116.28, 103.53)
+PIXEL_STD = (58.395, 57.12, 57.375)
+
+
+def normalize(images_u8: torch.Tensor) -> torch.Tensor:
+    """uint8 [B,3,H,W] -> float32 normalised."""
+    m = torch.tensor(PIXEL_MEAN, device=images_u8.device).view(1, 3, 1, 1)
+    s = torch.tensor(PIXEL_STD, device=images_u8.device).view(1, 3, 1, 1)
+    return (images_u8.float() - m) / s
+
+
+def thunderbolt_polygon(rng: np.random.Generator, H: int, W: int) -> list:
+    """A thin zig-zag stroke as a closed polygon (8..16 vertices), area ~0.5-5% of the image."""
+    n = int(rng.integers(4, 9))                 # polyline joints -> 2n polygon vertices
+    L = rng.uniform(0.25, 0.6) * min(H, W)
+    ang = rng.uniform(0, 2 * np.pi)
+    cx, cy = rng.uniform(0.2, 0.8) * W, rng.uniform(0.2, 0.8) * H
+    t = np.linspace(-0.5, 0.5, n) * L
+    zig = rng.uniform(0.03, 0.09) * L * np.where(np.arange(n) % 2 == 0, 1.0, -1.0)
+    px = cx + t * np.cos(ang) - zig * np.sin(ang)
+    py = cy + t * np.sin(ang) + zig * np.cos(ang)
+    wid = rng.uniform(0.012, 0.04) * min(H, W)
+    nx, ny = -np.sin(ang) * wid, np.cos(ang) * wid
+    left = list(zip(px + nx, py + ny))
+    right = list(zip(px - nx, py - ny))[::-1]
+    pts = np.clip(np.array(left + right), 0, [W - 1, H - 1])
+    return pts.reshape(-1).tolist()
+
+
+def rasterize(poly_flat: list, H: int, W: int) -> np.ndarray:
+    img = Image.new("1", (W, H), 0)
+    ImageDraw.Draw(img).polygon([(poly_flat[i], poly_flat[i + 1]) for i in range(0, len(poly_flat), 2)], fill=1)
+    return np.array(img, dtype=bool)
+
+
+def synthetic_sample(rng: np.random.Generator, H: int, W: int):
+    img = rng.integers(0, 256, size=(3, H, W), dtype=np.uint8)
+    k = int(rng.integers(1, 4))
+    polys = [thunderbolt_polygon(rng, H, W) for _ in range(k)]
+    masks = np.stack([rasterize(p, H, W) for p in polys])
+    return img, masks, np.zeros(k, dtype=np.int64), polys
+
+
+def synthetic_batch(batch: int, size: int, seed: int = 42, device="cpu"):
+    """-> (images float [B,3,S,S] normalised, [masks bool [K_i,S,S]], [classes int64 [K_i]])."""
+    rng = np.random.default_rng(seed)
+    imgs, masks, classes = [], [], []
+    for _ in range(batch):
+        im, m, c, _ = synthetic_sample(rng, size, size)
+        imgs.append(torch.from_numpy(im))
+        masks.append(torch.from_numpy(m).to(device))
+        classes.append(torch.from_numpy(c).to(device))
+    images = normalize(torch.stack(imgs).to(device))
+    return images, masks, classes
+
+
+def write_coco_dataset(root: str, n_images: int, size: int, seed: int = 42, category: str = "thunderbolt"):
+    """Write `root/annotations.json` + `root/images/*.png` in the reference's COCO layout."""
+    os.makedirs(os.path.join(root, "images"), exist_ok=True)
+    rng = np.random.default_rng(seed)
+    images, anns = [], []
+    aid = 1
+    for i in range(n_images):
+        im, masks, _, polys = synthetic_sample(rng, size, size)
+        fn = f"{i:06d}.png"
+        Image.fromarray(np.transpose(im, (1, 2, 0))).save(os.path.join(root, "images", fn))
+        images.append({"id": i, "file_name": fn, "height": size, "width": size})
+        for m, p in zip(masks, polys):
+            ys, xs = np.nonzero(m)
+            bbox = [float(xs.min()), float(ys.min()), float(xs.max() - xs.min() + 1), float(ys.max() - ys.min() + 1)] \
+                if len(xs) else [0.0, 0.0, 0.0, 0.0]
+            anns.append({"id": aid, "image_id": i, "category_id": 0, "segmentation": [p], "area": float(m.sum()),
+                         "bbox": bbox, "iscrowd": 0})
+            aid += 1
+    coco = {"images": images, "annotations": anns, "categories": [{"id": 0, "name": category}]}
+    with open(os.path.join(root, "annotations.json"), "w") as f:
+        json.dump(coco, f)
+    return coco
+
+
+class CocoInstanceDataset:
+    """Reads a COCO instance json (+ images) -> (uint8 image [3,H,W], bool masks [K,H,W],
+    int64 classes [K]) per image, with the reference mapper's train augmentations."""
+
+    def __init__(self, root: str, ann_file: str = "annotations.json", image_dir: str | None = None,
+                 min_size=(480, 512, 544, 576, 608, 640), max_size=800, train=True, fixed_size: int | None = None,
+                 seed: int = 42):
+        with open(os.path.join(root, ann_file)) as f:
+            coco = json.load(f)
+        self.root = root
+        self.image_dir = image_dir or (os.path.join(root, "images") if os.path.isdir(os.path.join(root, "images")) else root)
+        self.images = coco["images"]
+        self.by_img = {}
+        for a in coco.get("annotations", []):
+            self.by_img.setdefault(a["image_id"], []).append(a)
+        cats = sorted(c["id"] for c in coco.get("categories", [{"id": 0}]))
+        self.cat_to_label = {c: i for i, c in enumerate(cats)}
+        self.min_size, self.max_size, self.train, self.fixed_size = min_size, max_size, train, fixed_size
+        self.rng = np.random.default_rng(seed)
+
+    def __len__(self):
+        return len(self.images)
+
+    def _target_size(self, h, w):
+        if self.fixed_size:
+            return self.fixed_size, self.fixed_size
+        s = int(self.rng.choice(self.min_size)) if self.train else int(self.min_size[-1])
+        scale = s / min(h, w)
+        if max(h, w) * scale > self.max_size:
+            scale = self.max_size / max(h, w)
+        return int(round(h * scale)), int(round(w * scale))
+
+    def __getitem__(self, i):
+        info = self.images[i]
+        img = Image.open(os.path.join(self.image_dir, info["file_name"])).convert("RGB")
+        w0, h0 = img.size
+        H, W = self._target_size(h0, w0)
+        sx, sy = W / w0, H / h0
+        img = img.resize((W, H), Image.BILINEAR)
+        masks, classes = [], []
+        for a in self.by_img.get(info["id"], []):
+            if a.get("iscrowd", 0):
+                continue
+            m = np.zeros((H, W), dtype=bool)
+            for poly in a["segmentation"]:
+                p = np.array(poly, dtype=np.float64).reshape(-1, 2) * [sx, sy]
+                m |= rasterize(p.reshape(-1).tolist(), H, W)
+            masks.append(m)
+            classes.append(self.cat_to_label[a["category_id"]])
+        arr = np.asarray(img, dtype=np.uint8).transpose(2, 0, 1)
+        if self.train and self.rng.random() < 0.5:
+            arr = arr[:, :, ::-1]
+            masks = [m[:, ::-1] for m in masks]
+        m = np.stack(masks) if masks else np.zeros((0, H, W), dtype=bool)
+        return (torch.from_numpy(np.ascontiguousarray(arr)), torch.from_numpy(np.ascontiguousarray(m)),
+                torch.tensor(classes, dtype=torch.int64))
+
+
+def collate_padded(samples, size_divisibility: int = 32, device="cpu"):
+    """Pad a list of samples to a common size divisible by 32 (detectron2 ImageList)."""
+    H = max(s[0].shape[1] for s in samples)
+    W = max(s[0].shape[2] for s in samples)
+    H = (H + size_divisibility - 1) // size_divisibility * size_divisibility
+    W = (W + size_divisibility - 1) // size_divisibility * size_divisibility
+    imgs = torch.zeros(len(samples), 3, H, W, dtype=torch.float32, device=device)
+    masks, classes = [], []
+    for i, (im, m, c) in enumerate(samples):
+        imgs[i, :, :im.shape[1], :im.shape[2]] = normalize(im[None].to(device))[0]   # pad after normalising
+        mm = torch.zeros(m.shape[0], H, W, dtype=torch.bool)
+        mm[:, :m.shape[1], :m.shape[2]] = m
+        masks.append(mm.to(device))
+        classes.append(c.to(device))
+    return imgs, masks, classes

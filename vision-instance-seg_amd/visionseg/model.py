@@ -1,0 +1,481 @@
+"""Swin + Mask2Former on the MI355X kernels.
+
+Same module tree and parameter names as the oracle restatement (oracle/ref_model.py)
+so one state dict drives both; `visionseg.convert.from_hf_state_dict` loads HF /
+upstream-layout checkpoints.  The hot path runs on the hand-written HIP kernels:
+
+  Swin block      LN -> window_partition (pad+roll+partition, HIP) -> fused qkv Linear
+                  -> window_attention (rel-bias + shift mask in-kernel, HIP) -> proj
+                  -> window_reverse (HIP) -> residual -> MLP            (HF:swin:508-574)
+  pixel decoder   6 x MSDeformAttn encoder layers, sampling on the HIP gather kernel
+                  (HF:m2f:919-1103); FPN tail on MIOpen convs (HF:m2f:1394-1419)
+  decoder         9 x [masked cross-attn (HIP) -> self-attn -> FFN]; every mask
+                  prediction = query MLP -> mask_head MFMA kernel -> attn_bitmask kernel
+                  (HF:m2f:1801-1960, 2018-2056)
+
+Plain Linear / LayerNorm / conv / GroupNorm stay on hipBLASLt / MIOpen through torch.
+Under torch.autocast(bfloat16) the kernels run their bf16 path (f32 accumulate); in
+fp32 they run the exact-f32 path used by the parity tests.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, asdict
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+
+@dataclass
+class M2FConfig:
+    embed_dim: int = 96
+    depths: tuple = (2, 2, 6, 2)
+    num_heads: tuple = (3, 6, 12, 24)
+    window_size: int = 7
+    mlp_ratio: float = 4.0
+    feature_size: int = 256
+    mask_feature_size: int = 256
+    hidden_dim: int = 256
+    enc_ffn: int = 1024
+    dec_ffn: int = 2048
+    dec_heads: int = 8
+    enc_layers: int = 6
+    dec_layers: int = 10
+    num_queries: int = 100
+    num_labels: int = 1
+    n_points: int = 4
+    n_levels: int = 3
+    no_object_weight: float = 0.1
+    class_weight: float = 2.0
+    mask_weight: float = 5.0
+    dice_weight: float = 5.0
+    train_num_points: int = 12544
+    oversample_ratio: float = 3.0
+    importance_sample_ratio: float = 0.75
+
+    @staticmethod
+    def preset(name: str, **kw) -> "M2FConfig":
+        """Backbone presets of BASELINE.json's configs (upstream Mask2Former Swin configs)."""
+        p = {
+            "swin_t": dict(embed_dim=96, depths=(2, 2, 6, 2), num_heads=(3, 6, 12, 24), window_size=7),
+            "swin_s": dict(embed_dim=96, depths=(2, 2, 18, 2), num_heads=(3, 6, 12, 24), window_size=7),
+            "swin_b": dict(embed_dim=128, depths=(2, 2, 18, 2), num_heads=(4, 8, 16, 32), window_size=12),
+            "swin_l": dict(embed_dim=192, depths=(2, 2, 18, 2), num_heads=(6, 12, 24, 48), window_size=12),
+        }[name]
+        p.update(kw)
+        return M2FConfig(**p)
+
+    @staticmethod
+    def from_dict(d):
+        d = dict(d)
+        for k in ("depths", "num_heads"):
+            if k in d:
+                d[k] = tuple(d[k])
+        return M2FConfig(**{k: v for k, v in d.items() if k in M2FConfig.__dataclass_fields__})
+
+    def to_dict(self):
+        d = asdict(self)
+        d["depths"] = list(self.depths)
+        d["num_heads"] = list(self.num_heads)
+        return d
+
+
+def _padded(n, ws):
+    return n + (ws - n % ws) % ws
+
+
+def _compute_dtype(t):
+    return torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled() else t.dtype
+
+
+# ----------------------------------------------------------------------------------
+# Swin backbone
+# ----------------------------------------------------------------------------------
+
+
+class WindowAttention(nn.Module):
+    def __init__(self, dim, heads, ws):
+        super().__init__()
+        if dim != heads * 32:
+            raise ValueError("the window-attention kernel needs head_dim == 32")
+        self.heads, self.ws = heads, ws
+        self.qkv = nn.Linear(dim, 3 * dim)
+        self.proj = nn.Linear(dim, dim)
+        self.rel_table = nn.Parameter(torch.zeros((2 * ws - 1) ** 2, heads))
+
+
+class Mlp(nn.Module):
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+    def forward(self, x):
+        return self.fc2(F.gelu(self.fc1(x)))
+
+
+class SwinBlock(nn.Module):
+    def __init__(self, dim, heads, ws, shift, mlp_ratio):
+        super().__init__()
+        self.ws, self.shift = ws, shift
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn = WindowAttention(dim, heads, ws)
+        self.norm2 = nn.LayerNorm(dim)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+
+    def forward(self, x, H, W):
+        B, L, C = x.shape
+        ws, shift = self.ws, self.shift
+        h = self.norm1(x).view(B, H, W, C)
+        win = ops.window_partition(h.to(_compute_dtype(h)), ws, shift)   # cast first: half the bytes moved
+        qkv = self.attn.qkv(win)
+        o = ops.window_attention(qkv, self.attn.rel_table, self.attn.heads, ws, shift,
+                                 _padded(H, ws) // ws, _padded(W, ws) // ws)
+        o = ops.window_reverse(o, B, H, W, ws, shift)                 # per-token proj commutes with crop
+        o = self.attn.proj(o.view(B, H * W, C))
+        x = x + o
+        return x + self.mlp(self.norm2(x))
+
+
+class PatchMerging(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.norm = nn.LayerNorm(4 * dim)
+        self.reduction = nn.Linear(4 * dim, 2 * dim, bias=False)
+
+    def forward(self, x, H, W):
+        B, L, C = x.shape
+        x = x.view(B, H, W, C)
+        if H % 2 == 1 or W % 2 == 1:
+            x = F.pad(x, (0, 0, 0, W % 2, 0, H % 2))
+        x = torch.cat([x[:, r::2, c::2, :] for c in range(2) for r in range(2)], dim=-1)
+        return self.reduction(self.norm(x.reshape(B, -1, 4 * C)))
+
+
+class Stage(nn.Module):
+    def __init__(self, dim, depth, heads, ws, mlp_ratio, downsample):
+        super().__init__()
+        self.blocks = nn.ModuleList(
+            [SwinBlock(dim, heads, ws, 0 if i % 2 == 0 else ws // 2, mlp_ratio) for i in range(depth)])
+        self.merge = PatchMerging(dim) if downsample else None
+
+
+class PatchEmbed(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.proj = nn.Conv2d(3, dim, kernel_size=4, stride=4)
+        self.norm = nn.LayerNorm(dim)
+
+
+class SwinBackbone(nn.Module):
+    """Returns per-stage NCHW feature maps (pre-downsample, out-norm applied)."""
+
+    def __init__(self, cfg: M2FConfig):
+        super().__init__()
+        C = cfg.embed_dim
+        n = len(cfg.depths)
+        self.patch_embed = PatchEmbed(C)
+        self.stages = nn.ModuleList([
+            Stage(C * 2 ** i, cfg.depths[i], cfg.num_heads[i], cfg.window_size, cfg.mlp_ratio, i < n - 1)
+            for i in range(n)])
+        self.out_norms = nn.ModuleList([nn.LayerNorm(C * 2 ** i) for i in range(n)])
+
+    def forward(self, px):
+        H, W = px.shape[-2:]
+        if W % 4:
+            px = F.pad(px, (0, 4 - W % 4))
+        if H % 4:
+            px = F.pad(px, (0, 0, 0, 4 - H % 4))
+        x = self.patch_embed.proj(px)
+        B, C, H, W = x.shape
+        x = self.patch_embed.norm(x.flatten(2).transpose(1, 2))
+        feats = []
+        for i, st in enumerate(self.stages):
+            for blk in st.blocks:
+                x = blk(x, H, W)
+            f = self.out_norms[i](x)
+            feats.append(f.view(B, H, W, -1).permute(0, 3, 1, 2))     # NCHW view, channels-last memory
+            if st.merge is not None:
+                x = st.merge(x, H, W)
+                H, W = (H + 1) // 2, (W + 1) // 2
+        return feats
+
+
+# ----------------------------------------------------------------------------------
+# Pixel decoder
+# ----------------------------------------------------------------------------------
+
+
+def sine_pos_embed(B, H, W, num_feats, device, dtype=torch.float32, temperature=10000, scale=2 * math.pi):
+    """Normalised sine embedding (HF:m2f:864-904), [B, 2*num_feats, H, W]."""
+    y = torch.arange(1, H + 1, dtype=dtype, device=device)[None, :, None].expand(B, H, W)
+    x = torch.arange(1, W + 1, dtype=dtype, device=device)[None, None, :].expand(B, H, W)
+    eps = 1e-6
+    y = y / (y[:, -1:, :] + eps) * scale
+    x = x / (x[:, :, -1:] + eps) * scale
+    dim_t = torch.arange(num_feats, dtype=torch.int64, device=device).to(dtype)
+    dim_t = temperature ** (2 * torch.div(dim_t, 2, rounding_mode="floor") / num_feats)
+    px = x[:, :, :, None] / dim_t
+    py = y[:, :, :, None] / dim_t
+    px = torch.stack((px[:, :, :, 0::2].sin(), px[:, :, :, 1::2].cos()), dim=4).flatten(3)
+    py = torch.stack((py[:, :, :, 0::2].sin(), py[:, :, :, 1::2].cos()), dim=4).flatten(3)
+    return torch.cat((py, px), dim=3).permute(0, 3, 1, 2)
+
+
+def reference_points(shapes, B, device, dtype=torch.float32):
+    """HF:m2f:1127-1156 with valid ratios 1 -> [B, S, L, 2]."""
+    refs = []
+    for (Hl, Wl) in shapes:
+        ry, rx = torch.meshgrid(torch.linspace(0.5, Hl - 0.5, Hl, dtype=dtype, device=device),
+                                torch.linspace(0.5, Wl - 0.5, Wl, dtype=dtype, device=device), indexing="ij")
+        refs.append(torch.stack((rx.reshape(-1)[None] / Wl, ry.reshape(-1)[None] / Hl), -1))
+    r = torch.cat(refs, 1)
+    return r[:, :, None].expand(B, -1, len(shapes), -1)
+
+
+class MSDeformAttn(nn.Module):
+    def __init__(self, d, heads, levels, points):
+        super().__init__()
+        self.d, self.heads, self.levels, self.points = d, heads, levels, points
+        self.sampling_offsets = nn.Linear(d, heads * levels * points * 2)
+        self.attention_weights = nn.Linear(d, heads * levels * points)
+        self.value_proj = nn.Linear(d, d)
+        self.output_proj = nn.Linear(d, d)
+
+    def forward(self, h, pos, ref, shapes, norm):
+        B, S, _ = h.shape
+        q = h + pos
+        value = self.value_proj(h).view(B, S, self.heads, self.d // self.heads)
+        off = self.sampling_offsets(q).view(B, S, self.heads, self.levels, self.points, 2)
+        aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
+        aw = F.softmax(aw.float(), -1).view(B, S, self.heads, self.levels, self.points)
+        loc = ref[:, :, None, :, None, :] + off.float() / norm           # HF:m2f:994-1002
+        out = ops.ms_deform_attn(value, shapes, loc, aw)
+        return self.output_proj(out)
+
+
+class EncoderLayer(nn.Module):
+    def __init__(self, d, ffn, heads, levels, points):
+        super().__init__()
+        self.attn = MSDeformAttn(d, heads, levels, points)
+        self.norm1 = nn.LayerNorm(d)
+        self.fc1 = nn.Linear(d, ffn)
+        self.fc2 = nn.Linear(ffn, d)
+        self.norm2 = nn.LayerNorm(d)
+
+    def forward(self, h, pos, ref, shapes, norm):
+        h = self.norm1(h + self.attn(h, pos, ref, shapes, norm))
+        return self.norm2(h + self.fc2(F.relu(self.fc1(h))))
+
+
+class ConvGN(nn.Module):
+    def __init__(self, cin, cout, k, bias):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, kernel_size=k, padding=k // 2, bias=bias)
+        self.gn = nn.GroupNorm(32, cout)
+
+    def forward(self, x):
+        return self.gn(self.conv(x))
+
+
+class PixelDecoder(nn.Module):
+    def __init__(self, cfg: M2FConfig, channels):
+        super().__init__()
+        Fd = cfg.feature_size
+        self.cfg = cfg
+        self.input_proj = nn.ModuleList([ConvGN(c, Fd, 1, True) for c in channels[::-1][:3]])
+        self.level_embed = nn.Parameter(torch.zeros(3, Fd))
+        self.encoder = nn.ModuleList([EncoderLayer(Fd, cfg.enc_ffn, cfg.dec_heads, 3, cfg.n_points)
+                                      for _ in range(cfg.enc_layers)])
+        self.lateral = ConvGN(channels[0], Fd, 1, False)
+        self.output = ConvGN(Fd, Fd, 3, False)
+        self.mask_proj = nn.Conv2d(Fd, cfg.mask_feature_size, kernel_size=1)
+
+    def forward(self, feats):
+        Fd = self.cfg.feature_size
+        dev = feats[0].device
+        embeds, pos = [], []
+        for lvl, x in enumerate(feats[::-1][:3]):
+            e = self.input_proj[lvl](x)
+            embeds.append(e)
+            pos.append(sine_pos_embed(x.shape[0], x.shape[2], x.shape[3], Fd // 2, dev))
+        shapes = [(int(e.shape[2]), int(e.shape[3])) for e in embeds]
+        B = embeds[0].shape[0]
+        h = torch.cat([e.flatten(2).transpose(1, 2) for e in embeds], 1)
+        p = torch.cat([q.flatten(2).transpose(1, 2) + self.level_embed[i].view(1, 1, -1)
+                       for i, q in enumerate(pos)], 1)
+        ref = reference_points(shapes, B, dev)
+        norm = torch.tensor([[w, hh] for hh, w in shapes], device=dev, dtype=torch.float32)[None, None, None, :, None, :]
+        for layer in self.encoder:
+            h = layer(h, p, ref, shapes, norm)
+        outs, s = [], 0
+        for (Hl, Wl) in shapes:
+            outs.append(h[:, s:s + Hl * Wl].transpose(1, 2).reshape(B, -1, Hl, Wl))
+            s += Hl * Wl
+        cur = self.lateral(feats[0])
+        y = cur + F.interpolate(outs[-1].to(cur.dtype), size=cur.shape[-2:], mode="bilinear", align_corners=False)
+        y = F.relu(self.output(y))
+        return self.mask_proj(y), outs
+
+
+# ----------------------------------------------------------------------------------
+# Masked-attention decoder
+# ----------------------------------------------------------------------------------
+
+
+class CrossAttn(nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d))
+        self.in_proj_bias = nn.Parameter(torch.zeros(3 * d))
+        self.out_proj = nn.Linear(d, d)
+
+
+class SelfAttn(nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.q_proj = nn.Linear(d, d)
+        self.k_proj = nn.Linear(d, d)
+        self.v_proj = nn.Linear(d, d)
+        self.out_proj = nn.Linear(d, d)
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, d, ffn, heads):
+        super().__init__()
+        self.heads = heads
+        self.cross_attn = CrossAttn(d)
+        self.norm_cross = nn.LayerNorm(d)
+        self.self_attn = SelfAttn(d)
+        self.norm_self = nn.LayerNorm(d)
+        self.fc1 = nn.Linear(d, ffn)
+        self.fc2 = nn.Linear(ffn, d)
+        self.norm_ffn = nn.LayerNorm(d)
+
+    def forward(self, h, qpos, mem, mpos, words):
+        B, Q, D = h.shape
+        H, d = self.heads, D // self.heads
+        W, b = self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias
+        q = F.linear(h + qpos, W[:D], b[:D])
+        k = F.linear(mem + mpos, W[D:2 * D], b[D:2 * D])
+        v = F.linear(mem, W[2 * D:], b[2 * D:])
+        o = ops.masked_attention(q, k, v, words, H, d ** -0.5)
+        h = self.norm_cross(h + self.cross_attn.out_proj(o))
+        sa = self.self_attn
+        qs = sa.q_proj(h + qpos).view(B, Q, H, d).transpose(1, 2)
+        ks = sa.k_proj(h + qpos).view(B, Q, H, d).transpose(1, 2)
+        vs = sa.v_proj(h).view(B, Q, H, d).transpose(1, 2)
+        att = F.scaled_dot_product_attention(qs, ks, vs)
+        h = self.norm_self(h + sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)))
+        return self.norm_ffn(h + self.fc2(F.relu(self.fc1(h))))
+
+
+class Decoder(nn.Module):
+    def __init__(self, cfg: M2FConfig):
+        super().__init__()
+        d = cfg.hidden_dim
+        self.cfg = cfg
+        self.query_feat = nn.Embedding(cfg.num_queries, d)
+        self.query_embed = nn.Embedding(cfg.num_queries, d)
+        self.level_embed = nn.Embedding(3, d)
+        self.layers = nn.ModuleList([DecoderLayer(d, cfg.dec_ffn, cfg.dec_heads) for _ in range(cfg.dec_layers - 1)])
+        self.norm = nn.LayerNorm(d)
+        self.mask_embed = nn.ModuleList([nn.Linear(d, d), nn.Linear(d, d), nn.Linear(d, cfg.mask_feature_size)])
+
+    def predict(self, h, mf_nhwc, Hm, Wm, target_hw):
+        x = self.norm(h)
+        e = F.relu(self.mask_embed[0](x))
+        e = F.relu(self.mask_embed[1](e))
+        e = self.mask_embed[2](e)
+        e = e.to(mf_nhwc.dtype)
+        logits = ops.mask_head(e, mf_nhwc, Hm, Wm)
+        words = ops.attn_bitmask(logits, target_hw) if target_hw is not None else None
+        return x, logits, words
+
+    def forward(self, ms_feats, mask_features):
+        d = self.cfg.hidden_dim
+        B, _, Hm, Wm = mask_features.shape
+        dev = mask_features.device
+        mf = mask_features.to(_compute_dtype(mask_features)).permute(0, 2, 3, 1).reshape(B, Hm * Wm, -1).contiguous()
+        mems, mposs, sizes = [], [], []
+        for i in range(3):
+            f = ms_feats[i]
+            sizes.append((int(f.shape[2]), int(f.shape[3])))
+            mposs.append(sine_pos_embed(B, f.shape[2], f.shape[3], d // 2, dev).flatten(2).transpose(1, 2))
+            mems.append((f.flatten(2) + self.level_embed.weight[i][None, :, None]).transpose(1, 2))
+        qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
+        h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
+        n = len(self.layers)
+        inter, logits, words = self.predict(h, mf, Hm, Wm, sizes[0] if n else None)
+        inters, masks = [inter], [logits]
+        for idx, layer in enumerate(self.layers):
+            lvl = idx % 3
+            h = layer(h, qpos, mems[lvl], mposs[lvl], words)
+            nxt = sizes[(idx + 1) % 3] if idx + 1 < n else None
+            inter, logits, words = self.predict(h, mf, Hm, Wm, nxt)
+            inters.append(inter)
+            masks.append(logits)
+        return inters, masks
+
+
+class Mask2Former(nn.Module):
+    """Swin + Mask2Former forward: returns (mask logits per decoder step [B,Q,H/4,W/4]
+    f32, class logits per step [B,Q,num_labels+1])."""
+
+    def __init__(self, cfg: M2FConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.backbone = SwinBackbone(cfg)
+        chans = [cfg.embed_dim * 2 ** i for i in range(len(cfg.depths))]
+        self.pixel_decoder = PixelDecoder(cfg, chans)
+        self.decoder = Decoder(cfg)
+        self.class_head = nn.Linear(cfg.hidden_dim, cfg.num_labels + 1)
+
+    def forward(self, pixel_values):
+        feats = self.backbone(pixel_values)
+        mask_features, ms = self.pixel_decoder(feats)
+        inters, masks = self.decoder(ms, mask_features)
+        classes = [self.class_head(x) for x in inters]
+        return masks, classes
+
+    @torch.no_grad()
+    def init_weights(self, seed: int = 0):
+        """Training init in the spirit of upstream Mask2Former (trunc-normal Linear,
+        xavier decoder projections, Deformable-DETR MSDA init, zero rel-bias)."""
+        g = torch.Generator().manual_seed(seed)
+        for name, m in self.named_modules():
+            if isinstance(m, nn.Linear):
+                w = torch.empty_like(m.weight, device="cpu")
+                nn.init.trunc_normal_(w, std=0.02, generator=g)
+                m.weight.copy_(w)
+                if m.bias is not None:
+                    m.bias.zero_()
+            elif isinstance(m, nn.LayerNorm):
+                m.weight.fill_(1.0)
+                m.bias.zero_()
+            elif isinstance(m, CrossAttn):
+                w = torch.empty_like(m.in_proj_weight, device="cpu")
+                nn.init.xavier_uniform_(w, generator=g)
+                m.in_proj_weight.copy_(w)
+                m.in_proj_bias.zero_()
+            elif isinstance(m, nn.Embedding):
+                w = torch.empty_like(m.weight, device="cpu")
+                nn.init.normal_(w, generator=g)
+                m.weight.copy_(w)
+        for m in self.modules():
+            if isinstance(m, MSDeformAttn):
+                m.sampling_offsets.weight.zero_()
+                th = torch.arange(m.heads, dtype=torch.float32) * (2.0 * math.pi / m.heads)
+                grid = torch.stack([th.cos(), th.sin()], -1)
+                grid = (grid / grid.abs().max(-1, keepdim=True)[0]).view(m.heads, 1, 1, 2).repeat(1, m.levels, m.points, 1)
+                for i in range(m.points):
+                    grid[:, :, i, :] *= i + 1
+                m.sampling_offsets.bias.copy_(grid.view(-1))
+                m.attention_weights.weight.zero_()
+                m.attention_weights.bias.zero_()
+            elif isinstance(m, WindowAttention):
+                m.rel_table.zero_()
+        return self

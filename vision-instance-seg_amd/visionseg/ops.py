@@ -59,7 +59,8 @@ class MSDeformAttnFunction(torch.autograd.Function):
         sh, st, tot = _level_arrays(shapes)
         if tot != S:
             raise ValueError(f"spatial shapes cover {tot} positions, value has {S}")
-        with timed("msda_fwd", value):
+        nb = (value.numel() + out.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 4
+        with timed("msda_fwd", value, bytes_=nb, flops=2.0 * aw.numel() * (4 * D + D)):
             L.check(L.lib().vs_msda_forward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
                                             L.ptr(out), B, S, H, D, Lv, Q, P, L.stream(value)), "msda_forward")
         ctx.shapes = shapes
@@ -76,7 +77,8 @@ class MSDeformAttnFunction(torch.autograd.Function):
         gl = torch.empty_like(loc)
         ga = torch.empty_like(aw)
         sh, st, _ = _level_arrays(ctx.shapes)
-        with timed("msda_bwd", value):
+        nb = (value.numel() + g.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 8 + gv.numel() * 4
+        with timed("msda_bwd", value, bytes_=nb, flops=2.0 * aw.numel() * 10 * D):
             L.check(L.lib().vs_msda_backward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
                                              L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga), B, S, H, D, Lv, Q, P,
                                              L.stream(value)), "msda_backward")
@@ -101,7 +103,7 @@ class _WindowPartition(torch.autograd.Function):
         B, H, W, C = x.shape
         Hp, Wp = _padded(H, ws), _padded(W, ws)
         out = torch.empty(B * (Hp // ws) * (Wp // ws), ws * ws, C, device=x.device, dtype=x.dtype)
-        with timed("window_partition", x):
+        with timed("window_partition", x, bytes_=(x.numel() + out.numel()) * x.element_size()):
             L.check(L.lib().vs_window_partition(L.ptr(x), L.ptr(out), x.element_size(), B, H, W, C, ws, shift,
                                                 L.stream(x)), "window_partition")
         ctx.meta = (B, H, W, C, ws, shift)
@@ -115,7 +117,7 @@ class _WindowPartition(torch.autograd.Function):
 
 def _window_reverse_raw(win, B, H, W, C, ws, shift):
     out = torch.empty(B, H, W, C, device=win.device, dtype=win.dtype)
-    with timed("window_reverse", win):
+    with timed("window_reverse", win, bytes_=(win.numel() + out.numel()) * win.element_size()):
         L.check(L.lib().vs_window_reverse(L.ptr(win), L.ptr(out), win.element_size(), B, H, W, C, ws, shift,
                                           L.stream(win)), "window_reverse")
     return out
@@ -125,7 +127,7 @@ def _window_partition_raw(x, ws, shift):
     B, H, W, C = x.shape
     Hp, Wp = _padded(H, ws), _padded(W, ws)
     out = torch.empty(B * (Hp // ws) * (Wp // ws), ws * ws, C, device=x.device, dtype=x.dtype)
-    with timed("window_partition", x):
+    with timed("window_partition", x, bytes_=(x.numel() + out.numel()) * x.element_size()):
         L.check(L.lib().vs_window_partition(L.ptr(x), L.ptr(out), x.element_size(), B, H, W, C, ws, shift,
                                             L.stream(x)), "window_partition")
     return out
@@ -175,7 +177,8 @@ class WindowAttentionFunction(torch.autograd.Function):
             raise ValueError(f"qkv {tuple(qkv.shape)} does not match heads={heads} (x32) window={window}")
         out = torch.empty(Bw, N, C, device=qkv.device, dtype=qkv.dtype)
         lse = torch.empty(Bw, heads, N, device=qkv.device, dtype=torch.float32)
-        with timed("window_attn_fwd", qkv):
+        with timed("window_attn_fwd", qkv, bytes_=(qkv.numel() + out.numel()) * qkv.element_size() + lse.numel() * 4,
+                   flops=4.0 * Bw * heads * N * N * 32):
             L.check(L.lib().vs_window_attn_forward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
                                                    L.ptr(lse), Bw, heads, window, shift, nwin_h, nwin_w,
                                                    float(scale), L.stream(qkv)), "window_attn_forward")
@@ -192,7 +195,8 @@ class WindowAttentionFunction(torch.autograd.Function):
         gqkv = torch.empty_like(qkv)
         T2 = (2 * window - 1) ** 2
         part = torch.empty(Bw, heads, T2, device=qkv.device, dtype=torch.float32)
-        with timed("window_attn_bwd", qkv):
+        with timed("window_attn_bwd", qkv, bytes_=(3 * qkv.numel() + 2 * out.numel()) * qkv.element_size(),
+                   flops=10.0 * Bw * heads * N * N * 32):
             L.check(L.lib().vs_window_attn_backward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
                                                     L.ptr(lse), L.ptr(g), L.ptr(gqkv), L.ptr(part), Bw, heads,
                                                     window, shift, nwin_h, nwin_w, scale, L.stream(qkv)),
@@ -224,7 +228,8 @@ class MaskHeadFunction(torch.autograd.Function):
         if P.shape != (B, height * width, C):
             raise ValueError(f"pixel embedding {tuple(P.shape)} != {(B, height * width, C)}")
         out = torch.empty(B, Q, height, width, device=E.device, dtype=torch.float32)
-        with timed("mask_head_fwd", E):
+        with timed("mask_head_fwd", E, bytes_=(E.numel() + P.numel()) * E.element_size() + out.numel() * 4,
+                   flops=2.0 * B * Q * C * height * width):
             L.check(L.lib().vs_mask_head_forward(L.dtype_code(E), L.ptr(E), L.ptr(P), L.ptr(out), B, Q, C, height,
                                                  width, L.stream(E)), "mask_head_forward")
         ctx.save_for_backward(E, P)
@@ -254,7 +259,7 @@ def attn_bitmask(logits, target_hw):
     B, Q, H, W = lg.shape
     th, tw = int(target_hw[0]), int(target_hw[1])
     words = torch.empty(B, Q, (th * tw + 31) // 32, device=lg.device, dtype=torch.int32)
-    with timed("attn_bitmask", lg):
+    with timed("attn_bitmask", lg, bytes_=min(lg.numel(), B * Q * th * tw * 4) * 4 + words.numel() * 4):
         L.check(L.lib().vs_attn_bitmask(L.ptr(lg), L.ptr(words), B * Q, H, W, th, tw, L.stream(lg)), "attn_bitmask")
     return words
 
@@ -284,7 +289,8 @@ class MaskedAttentionFunction(torch.autograd.Function):
         lse = torch.empty(B, heads, Q, device=q.device, dtype=torch.float32)
         ws = torch.empty(int(L.lib().vs_masked_attn_workspace_bytes(B, Q, S, heads)), device=q.device,
                          dtype=torch.uint8)
-        with timed("masked_attn_fwd", q):
+        nb = (q.numel() * 2 + k.numel() + v.numel()) * q.element_size() + words.numel() * 4
+        with timed("masked_attn_fwd", q, bytes_=nb, flops=4.0 * B * heads * Q * S * 32):
             L.check(L.lib().vs_masked_attn_forward(L.dtype_code(q), L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(words),
                                                    L.ptr(out), L.ptr(lse), L.ptr(ws), B, Q, S, heads, float(scale),
                                                    L.stream(q)), "masked_attn_forward")
@@ -302,7 +308,8 @@ class MaskedAttentionFunction(torch.autograd.Function):
         gq, gk, gv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         ws = torch.empty(int(L.lib().vs_masked_attn_workspace_bytes(B, Q, S, heads)), device=q.device,
                          dtype=torch.uint8)
-        with timed("masked_attn_bwd", q):
+        nb = (q.numel() * 4 + 2 * k.numel() + 2 * v.numel()) * q.element_size() + words.numel() * 4
+        with timed("masked_attn_bwd", q, bytes_=nb, flops=10.0 * B * heads * Q * S * 32):
             L.check(L.lib().vs_masked_attn_backward(L.dtype_code(q), L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(words),
                                                     L.ptr(out), L.ptr(lse), L.ptr(g), L.ptr(gq), L.ptr(gk),
                                                     L.ptr(gv), L.ptr(ws), B, Q, S, heads, scale, L.stream(q)),

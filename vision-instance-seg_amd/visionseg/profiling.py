@@ -1,9 +1,10 @@
 """Per-kernel HIP-event timing of the hand-written ops (used by bench.py's roofline).
 
-`timed(name, tensor)` brackets one C-ABI launch with two `torch.cuda.Event`s recorded
-on the stream the kernel is launched on (the inputs' current stream — the same stream
-the ops pass to the C ABI).  Disabled (zero overhead beyond a flag check) unless a
-`KernelTimer` is active.
+`timed(name, tensor, bytes_=, flops=)` brackets one C-ABI launch with two
+`torch.cuda.Event`s recorded on the stream the kernel is launched on (the inputs'
+current stream — the same stream the ops pass to the C ABI) and records the launch's
+ALGORITHMIC work (compulsory HBM bytes and/or useful flops, computed from the shapes).
+Disabled (one global check) unless a `KernelTimer` is active.
 """
 from __future__ import annotations
 
@@ -31,16 +32,23 @@ class KernelTimer:
         return False
 
     def summary(self):
-        """{name: (launches, total_ms, mean_ms)} — call after synchronising."""
+        """{name: dict(launches, total_ms, mean_ms, bytes, flops)} — call after a sync.
+        bytes/flops are per-launch averages of the algorithmic work."""
         out = {}
         for name, evs in self.events.items():
-            ts = [a.elapsed_time(b) for a, b in evs]
-            out[name] = (len(ts), sum(ts), sum(ts) / max(1, len(ts)))
+            ts = [a.elapsed_time(b) for a, b, _, _ in evs]
+            n = len(ts)
+            out[name] = dict(launches=n, total_ms=sum(ts), mean_ms=sum(ts) / max(1, n),
+                             bytes=sum(x[2] for x in evs) / max(1, n), flops=sum(x[3] for x in evs) / max(1, n))
         return out
 
 
+def enabled() -> bool:
+    return _active is not None
+
+
 @contextlib.contextmanager
-def timed(name: str, like: torch.Tensor):
+def timed(name: str, like: torch.Tensor, bytes_: float = 0.0, flops: float = 0.0):
     t = _active
     if t is None:
         yield
@@ -53,4 +61,4 @@ def timed(name: str, like: torch.Tensor):
         yield
     finally:
         b.record(s)
-        t.events[name].append((a, b))
+        t.events[name].append((a, b, float(bytes_), float(flops)))
