@@ -26,6 +26,26 @@ for _p in (ROOT, os.path.join(ROOT, "vision-instance-seg_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
+# Vendor-GEMM solution table (PyTorch TunableOp over hipBLASLt/rocBLAS, incl. split-K for
+# the tall-K weight-gradient GEMMs), tuned on MI355X for this workload and shipped
+# in-tree; read-only unless --gemm-tuning tune.  Must be set before torch loads.
+_TUNE_FILE = os.path.join(ROOT, "vision-instance-seg_amd", "visionseg", "tuning", "tunableop_mi355x.csv")
+_gt = "file"
+for _i, _a in enumerate(sys.argv):
+    if _a == "--gemm-tuning" and _i + 1 < len(sys.argv):
+        _gt = sys.argv[_i + 1]
+    elif _a.startswith("--gemm-tuning="):
+        _gt = _a.split("=", 1)[1]
+if _gt == "file" and os.path.exists(_TUNE_FILE):
+    os.environ.setdefault("PYTORCH_TUNABLEOP_ENABLED", "1")
+    os.environ.setdefault("PYTORCH_TUNABLEOP_TUNING", "0")
+    os.environ.setdefault("PYTORCH_TUNABLEOP_FILENAME", _TUNE_FILE)
+elif _gt == "tune":
+    os.environ.setdefault("PYTORCH_TUNABLEOP_ENABLED", "1")
+    os.environ.setdefault("PYTORCH_TUNABLEOP_TUNING", "1")
+    os.environ.setdefault("PYTORCH_TUNABLEOP_FILENAME", os.path.join(ROOT, "gpurun_out", "tunableop_results%d.csv"))
+    os.environ.setdefault("PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS", "20")
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -46,6 +66,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=2)
     ap.add_argument("--kernel-timing", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
+    ap.add_argument("--gemm-tuning", default="file", choices=["file", "tune", "off"],
+                    help="vendor GEMM solution table: in-tree TunableOp file (default), re-tune, or heuristics")
     return ap.parse_args()
 
 
@@ -164,6 +186,7 @@ def main():
                        "model": f"{a.model}_mask2former", "global_batch": a.batch * world, "image_size": a.size,
                        "parallelism": f"dp{world}"},
             "final_loss": round(float(loss.item()), 4),
+            "gemm_tuning": a.gemm_tuning,
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels": table,

@@ -82,6 +82,18 @@ VS_API int vs_msda_backward(int dtype, const void* value, const int64_t* spatial
                      int num_heads, int channels, int num_levels, int num_query,
                      int num_point, void* stream);
 
+/* Encoder self-attention backward (the pixel decoder's case: the queries ARE the value
+ * grid, Q == S, level-major).  Same tensors as vs_msda_backward with num_query = S;
+ * grad_value is produced by destination bands in LDS (no global atomics except for
+ * taps more than 4 rows from their query's mapped row).  Same results up to f32
+ * summation order. */
+VS_API int vs_msda_backward_encoder(int dtype, const void* value, const int64_t* spatial_shapes_host,
+                                    const int64_t* level_start_host, const float* sampling_loc,
+                                    const float* attn_weight, const void* grad_out, float* grad_value,
+                                    float* grad_loc, float* grad_attn, int batch, int spatial_size,
+                                    int num_heads, int channels, int num_levels, int num_point,
+                                    void* stream);
+
 /* ---- a2: Swin pad + cyclic shift + window partition / its inverse ---------------
  * window_partition: x [B, H, W, C] -> windows [B*nWh*nWw, ws*ws, C] where
  * Hp = ceil(H/ws)*ws, nWh = Hp/ws (same for W); windows[(b,wy,wx), (ty,tx)] =
@@ -125,6 +137,16 @@ VS_API int vs_window_attn_backward(int dtype, const void* qkv, const float* rel_
 VS_API int vs_mask_head_forward(int dtype, const void* mask_embed, const void* pixel_embed_nhwc,
                                 float* logits, int batch, int num_query, int channels, int height,
                                 int width, void* stream);
+
+/* Backward of vs_mask_head_forward, bf16 path (Q <= 128, C in {128, 256}):
+ * grad_logits f32 [B, Q, H*W] -> grad_E [B, Q, C], grad_P [B, H*W, C] (bf16, overwritten).
+ * workspace: vs_mask_head_backward_workspace_bytes(B, Q, C) bytes of device scratch
+ * (per-workgroup f32 partials of grad_E, reduced in a fixed order: deterministic). */
+VS_API long long vs_mask_head_backward_workspace_bytes(int batch, int num_query, int channels);
+VS_API int vs_mask_head_backward(int dtype, const float* grad_logits, const void* mask_embed,
+                                 const void* pixel_embed_nhwc, void* grad_mask_embed,
+                                 void* grad_pixel_embed, void* workspace, int batch, int num_query,
+                                 int channels, int height, int width, void* stream);
 
 /* Attention bitmask of the next decoder layer (HF:m2f:2049-2055 + row fix 1912-1914):
  * bilinear (align_corners=False) resize of each logits row [H, W] to [th, tw], key k

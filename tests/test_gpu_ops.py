@@ -311,3 +311,69 @@ def test_masked_attention_bf16_vs_oracle():
     out = ops.masked_attention(q.to(DEV), k.to(DEV), v.to(DEV), words.to(DEV), 8)
     err = (out.float().cpu() - ref).abs()
     assert bool((err <= ref.abs() * 2 ** -8 + 1e-3).all()), float(err.max())
+
+
+@pytest.mark.parametrize("shape", [(2, 100, 256, 64, 64), (4, 100, 256, 256, 256), (1, 37, 128, 20, 30)])
+def test_mask_head_backward_bf16_vs_oracle(shape):
+    """Fused bf16 backward vs f32 GEMMs on the same bf16-rounded operands (dL rounded to
+    bf16 as the MFMA consumes it): accumulation-order differences only."""
+    ops = _ops()
+    B, Q, C, H, W = shape
+    g = torch.Generator().manual_seed(14)
+    E = (torch.randn(B, Q, C, generator=g) / 8).to(torch.bfloat16)
+    P = torch.randn(B, H * W, C, generator=g).to(torch.bfloat16)
+    gl = torch.randn(B, Q, H, W, generator=g)
+    Ed, Pd = E.to(DEV).requires_grad_(True), P.to(DEV).requires_grad_(True)
+    lo = ops.mask_head(Ed, Pd, H, W)
+    lo.backward(gl.to(DEV))
+    glb = gl.to(torch.bfloat16).float().view(B, Q, H * W)
+    for b in range(min(B, 2)):
+        refE = glb[b] @ P[b].float()
+        refP = glb[b].t() @ E[b].float()
+        gE = Ed.grad[b].float().cpu()
+        gP = Pd.grad[b].float().cpu()
+        assert float((gE - refE).abs().max()) <= 2 ** -7 * float(refE.abs().max()) + 1e-3
+        assert float((gP - refP).abs().max()) <= 2 ** -7 * float(refP.abs().max()) + 1e-3
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(B=2, shapes=[(6, 7), (3, 4), (2, 2)], H=2, spread=2.0),
+    dict(B=1, shapes=[(32, 32), (64, 64), (128, 128)], H=8, spread=4.0),     # 1024^2 pixel decoder, init-like
+    dict(B=1, shapes=[(16, 16), (32, 32), (64, 64)], H=8, spread=12.0),      # many far taps (atomic path)
+    dict(B=2, shapes=[(12, 20), (24, 40), (48, 80)], H=8, spread=3.0),       # non-square (tiny fixture 'b' like)
+])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_msda_encoder_backward_vs_oracle(cfg, dtype):
+    """Encoder mode (queries = value grid): band kernel + far-tap atomics vs the oracle."""
+    ops = _ops()
+    shapes, B, H, L, P = cfg["shapes"], cfg["B"], cfg["H"], len(cfg["shapes"]), 4
+    S = sum(h * w for h, w in shapes)
+    g = torch.Generator().manual_seed(31)
+    ref = R.reference_points(shapes, B)                                          # [B,S,L,2]
+    off = (torch.rand(B, S, H, L, P, 2, generator=g) * 2 - 1) * cfg["spread"]
+    norm = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32)[None, None, None, :, None, :]
+    loc = ref[:, :, None, :, None, :] + off / norm
+    value = torch.randn(B, S, H, 32, generator=g).to(dtype)
+    w = torch.softmax(torch.randn(B, S, H, L * P, generator=g), -1).view(B, S, H, L, P)
+    vr, lr, wr = value.float().clone().requires_grad_(True), loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    out_r = R.msda_ref(vr, shapes, lr, wr)
+    go = torch.randn(out_r.shape, generator=g)
+    go_q = go.to(dtype).float()
+    out_r.backward(go_q)
+    vd, ld, wd = value.to(DEV).requires_grad_(True), loc.to(DEV).requires_grad_(True), w.to(DEV).requires_grad_(True)
+    out = ops.ms_deform_attn(vd, shapes, ld, wd, encoder=True)
+    out.backward(go.to(dtype).to(DEV))
+    tol = 2e-5 if dtype == torch.float32 else None
+    if dtype == torch.float32:
+        np.testing.assert_allclose(vd.grad.cpu().numpy(), vr.grad.numpy(), atol=tol, rtol=0)
+        np.testing.assert_allclose(wd.grad.cpu().numpy(), wr.grad.numpy(), atol=tol, rtol=0)
+    else:
+        gvr = vr.grad
+        err = (vd.grad.float().cpu() - gvr).abs()
+        assert bool((err <= gvr.abs() * 2 ** -8 + 1e-4).all()), float(err.max())
+    # encoder mode and the general (all-atomic) path agree
+    vd2 = value.to(DEV).requires_grad_(True)
+    out2 = ops.ms_deform_attn(vd2, shapes, loc.to(DEV), w.to(DEV), encoder=False)
+    out2.backward(go.to(dtype).to(DEV))
+    d = (vd2.grad.float() - vd.grad.float()).abs().max().item()
+    assert d <= (1e-5 if dtype == torch.float32 else 2 ** -7 * float(vd.grad.float().abs().max())), d

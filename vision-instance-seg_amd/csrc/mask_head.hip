@@ -95,6 +95,144 @@ __global__ void __launch_bounds__(256) mask_head_fwd_kernel(const T* __restrict_
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// Backward (bf16): one pass over the logits gradient produces both operand grads.
+//   dP[b,n,:] = sum_q gL[b,q,n] E[b,q,:]          (M = pixels, N = C, K = Q)
+//   dE[b,q,:] = sum_n gL[b,q,n] P[b,n,:]          (M = Q, N = C, K = pixels: split-K)
+// A workgroup (4 waves) keeps E^T [C][Q] in LDS and walks 32-pixel tiles of one image:
+// each tile's gL block is staged twice as bf16 (pixel-major for dP's A operand,
+// query-major for dE's A operand) and its P block transposed ([C][32]) for dE's B
+// operand, so every MFMA fragment is one contiguous 16-B LDS read (row strides padded
+// by 16 B: conflict-free ds_read_b128).  dE accumulates in registers across the
+// workgroup's tiles (4 q-tiles x C/128 c-tiles per wave) and is written once as a
+// per-workgroup f32 partial; `mask_head_bwd_reduce` sums the partials (deterministic).
+// HBM traffic per call: gL (f32) + P read once, dP written once.
+template <int CT>  // c-tiles (of 32) per wave; C = 128 * CT
+__global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restrict__ gL, const bf16* __restrict__ E,
+                                                            const bf16* __restrict__ P, bf16* __restrict__ dP,
+                                                            float* __restrict__ dEpart, int Q, int N) {
+  constexpr int C = 128 * CT;
+  constexpr int QP = 128 + 8;     // padded q stride
+  constexpr int TN = 32;
+  constexpr int NP = TN + 8;      // padded n stride
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* sET = reinterpret_cast<bf16*>(smem_raw);   // [C][QP]
+  bf16* sGT = sET + C * QP;                          // [TN][QP]
+  bf16* sGN = sGT + TN * QP;                         // [128][NP]
+  bf16* sPT = sGN + 128 * NP;                        // [C][NP]
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const bf16 zero = __float2bfloat16(0.f);
+  for (int idx = threadIdx.x; idx < 128 * C; idx += blockDim.x) {
+    const int q = idx / C, c = idx - q * C;
+    sET[c * QP + q] = q < Q ? E[((size_t)b * Q + q) * C + c] : zero;
+  }
+  f32x16_t accE[4][CT];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < CT; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) accE[t][u][i] = 0.f;
+  const float* gLb = gL + (size_t)b * Q * N;
+  const bf16* Pb = P + (size_t)b * N * C;
+  bf16* dPb = dP + (size_t)b * N * C;
+  const int tiles = (N + TN - 1) / TN;
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int n0 = tile * TN;
+    __syncthreads();
+    {  // gL tile: thread -> (q = tid/2, 16 pixels)
+      const int q = threadIdx.x >> 1, nh = (threadIdx.x & 1) * 16;
+      float v[16];
+      if (q < Q && n0 + nh + 16 <= N) {
+        const float4* src = reinterpret_cast<const float4*>(gLb + (size_t)q * N + n0 + nh);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 t4 = src[i];
+          v[4 * i] = t4.x; v[4 * i + 1] = t4.y; v[4 * i + 2] = t4.z; v[4 * i + 3] = t4.w;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = (q < Q && n0 + nh + i < N) ? gLb[(size_t)q * N + n0 + nh + i] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const bf16 x = __float2bfloat16(v[i]);
+        sGN[q * NP + nh + i] = x;
+        sGT[(nh + i) * QP + q] = x;
+      }
+    }
+    {  // P tile: 32 rows x C, 16-B chunks, stored transposed [C][NP]
+      constexpr int CH = C / 8;
+      for (int idx = threadIdx.x; idx < TN * CH; idx += blockDim.x) {
+        const int n = idx / CH, c0 = (idx - n * CH) * 8;
+        uint4 u = make_uint4(0, 0, 0, 0);
+        if (n0 + n < N) u = *reinterpret_cast<const uint4*>(Pb + (size_t)(n0 + n) * C + c0);
+        const bf16* e = reinterpret_cast<const bf16*>(&u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sPT[(c0 + i) * NP + n] = e[i];
+      }
+    }
+    __syncthreads();
+    // ---- dP tile [32 n][C]: wave owns c-tiles {wave*CT .. wave*CT+CT-1}
+#pragma unroll
+    for (int u = 0; u < CT; ++u) {
+      const int c0 = (wave * CT + u) * 32;
+      f32x16_t acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sGT + r * QP + 16 * s + 8 * hh);
+        const bf16x8_t bb = *reinterpret_cast<const bf16x8_t*>(sET + (c0 + r) * QP + 16 * s + 8 * hh);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int n = n0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        if (n < N) dPb[(size_t)n * C + c0 + r] = __float2bfloat16(acc[i]);
+      }
+    }
+    // ---- dE partial [128 q][C] += gL_tile [128 x 32] . P_tile [32 x C]
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t bfr[CT];
+#pragma unroll
+      for (int u = 0; u < CT; ++u)
+        bfr[u] = *reinterpret_cast<const bf16x8_t*>(sPT + ((wave * CT + u) * 32 + r) * NP + 16 * s + 8 * hh);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sGN + (32 * t + r) * NP + 16 * s + 8 * hh);
+#pragma unroll
+        for (int u = 0; u < CT; ++u) accE[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[u], accE[t][u], 0, 0, 0);
+      }
+    }
+  }
+  float* part = dEpart + ((size_t)blockIdx.x * gridDim.y + b) * Q * C;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < CT; ++u) {
+      const int c = (wave * CT + u) * 32 + r;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int q = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        if (q < Q) part[(size_t)q * C + c] = accE[t][u][i];
+      }
+    }
+}
+
+__global__ void __launch_bounds__(256) mask_head_bwd_reduce(const float* __restrict__ part, bf16* __restrict__ dE,
+                                                            int nparts, long long per_part) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per_part) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(size_t)p * per_part + i];
+  dE[i] = __float2bfloat16(s);
+}
+
 // PyTorch upsample_bilinear2d (align_corners=False) source index for one axis.
 __device__ __forceinline__ void src_index(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
   const float scale = (float)in / (float)out;
@@ -181,6 +319,42 @@ extern "C" int vs_attn_bitmask(const float* logits, uint32_t* words, int rows, i
   VS_CHECK(nwords * 4 <= 64 * 1024, "target too large");
   hipLaunchKernelGGL(attn_bitmask_kernel, dim3(rows), dim3(256), nwords * 4, (hipStream_t)stream, logits, words,
                      H, W, th, tw, nwords);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+static int mask_head_bwd_parts(int B) { return B >= 64 ? 1 : (256 + B - 1) / B; }
+
+extern "C" long long vs_mask_head_backward_workspace_bytes(int B, int Q, int C) {
+  return (long long)mask_head_bwd_parts(B) * B * Q * C * 4;
+}
+
+extern "C" int vs_mask_head_backward(int dtype, const float* grad_logits, const void* E, const void* P, void* grad_E,
+                                     void* grad_P, void* workspace, int B, int Q, int C, int H, int W,
+                                     void* stream) {
+  VS_CHECK(grad_logits && E && P && grad_E && grad_P && workspace, "null pointer");
+  VS_CHECK(dtype == VS_BF16, "the fused mask-head backward is the bf16 path (f32 parity mode uses vendor GEMMs)");
+  VS_CHECK(B > 0 && Q > 0 && Q <= 128 && H > 0 && W > 0, "need 0 < Q <= 128");
+  VS_CHECK(C == 128 || C == 256, "channels must be 128 or 256");
+  const int N = H * W;
+  const int parts = mask_head_bwd_parts(B);
+  const int tiles = (N + 31) / 32;
+  const int gx = parts < tiles ? parts : tiles;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = ((size_t)C * 136 + 32 * 136 + 128 * 40 + (size_t)C * 40) * 2;
+  float* part = (float*)workspace;
+  if (gx < parts) VS_HIP(hipMemsetAsync(part + (size_t)gx * B * Q * C, 0, (size_t)(parts - gx) * B * Q * C * 4, st));
+  if (C == 256) {
+    hipLaunchKernelGGL(mask_head_bwd_kernel<2>, dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
+                       (const bf16*)P, (bf16*)grad_P, part, Q, N);
+  } else {
+    hipLaunchKernelGGL(mask_head_bwd_kernel<1>, dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
+                       (const bf16*)P, (bf16*)grad_P, part, Q, N);
+  }
+  VS_LAUNCH_CHECK();
+  const long long per = (long long)B * Q * C;
+  hipLaunchKernelGGL(mask_head_bwd_reduce, dim3((int)((per + 255) / 256)), dim3(256), 0, st, part, (bf16*)grad_E,
+                     parts, per);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

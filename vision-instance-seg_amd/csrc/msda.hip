@@ -10,10 +10,20 @@
 // one 16-B load per lane, adjacent lanes read adjacent bytes; the group's loc/attn
 // rows (96 B / 48 B, 16-B aligned) are read as float4.  Accumulation in f32.
 //
-// Backward: one lane per channel (32 lanes = one group, 2 groups per wave) so every
-// grad_value atomic wave-instruction is two contiguous 128-B row segments (the shape
-// the f32 atomic path runs at full rate, MI355X_MICROARCH §Global float atomics);
-// grad_loc / grad_attn are 32-lane shuffle reductions, written by lane 0.
+// Backward, general queries (decoder cross-attention): one lane per channel (32 lanes =
+// one group, 2 groups per wave) so every grad_value atomic wave-instruction is two
+// contiguous 128-B row segments (the shape the f32 atomic path runs at full rate,
+// MI355X_MICROARCH §Global float atomics); grad_loc / grad_attn are 32-lane shuffle
+// reductions, written by lane 0.  That path is atomic-bound: 4 corners x 32 channels
+// x 4 B per tap (4.2 GB per pixel-decoder layer at 4x1024^2).
+//
+// Backward, encoder self-attention (queries ARE the value grid, Q == S): grad_value is
+// produced by destination instead.  msda_bwd_band_kernel owns a band of value rows of
+// one (image, head, level) in LDS and gathers every tap landing there from the queries
+// whose mapped row is within kBandR rows (LDS float atomics, then one plain coalesced
+// store per element: no global atomics); the query kernel computes grad_loc /
+// grad_attn and atomically adds only the "far" corners (row beyond the margin), which
+// the shared integer predicate `near_row` assigns to exactly one of the two kernels.
 #include "common.h"
 
 namespace vs {
@@ -27,6 +37,45 @@ struct Levels {
   int w[kMaxLevels];
   int start[kMaxLevels];
 };
+
+
+// ---- backward helpers shared by the band and query kernels (must stay identical:
+// a corner is accumulated by exactly one of them, decided by `near_row`).
+constexpr int kBandR = 4;      // row margin (level-l rows) of the band kernel's query scan; covers the
+                               // Deformable-DETR init offsets (|off| <= 4 px); farther taps go atomic
+constexpr int kBandMaxRows = 8;     // value rows per band workgroup (fewer if the level is wide)
+constexpr int kBandThreads = 512;   // 16 query slots of 32 channel-lanes
+
+struct Tap {
+  int h0, w0;
+  float lh, lw, hh, hw;
+  bool inside;
+};
+
+__device__ __forceinline__ Tap tap_geom(float x, float y, int Hl, int Wl) {
+  Tap t;
+  const float him = __fmaf_rn(y, (float)Hl, -0.5f);
+  const float wim = __fmaf_rn(x, (float)Wl, -0.5f);
+  t.inside = him > -1.f && wim > -1.f && him < (float)Hl && wim < (float)Wl;
+  const float fh0 = floorf(him), fw0 = floorf(wim);
+  t.h0 = (int)fh0;
+  t.w0 = (int)fw0;
+  t.lh = him - fh0;
+  t.lw = wim - fw0;
+  t.hh = 1.f - t.lh;
+  t.hw = 1.f - t.lw;
+  return t;
+}
+
+// Row of level l (height Hl) onto which query row yq of level lq (height Hq) maps:
+// floor(((yq + 0.5) * Hl / Hq) - 0.5), integer arithmetic (exact, no fp ambiguity).
+__device__ __forceinline__ int mapped_row(int yq, int Hq, int Hl) {
+  const int num = (2 * yq + 1) * Hl - Hq;
+  const int den = 2 * Hq;
+  return num >= 0 ? num / den : -((-num + den - 1) / den);
+}
+
+__device__ __forceinline__ bool near_row(int cy, int m) { return cy >= m - kBandR && cy <= m + kBandR + 1; }
 
 template <typename T>
 __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ value,
@@ -93,18 +142,30 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ val
   }
 }
 
-template <typename T>
+template <typename T, bool ENC>
 __global__ void __launch_bounds__(256) msda_bwd_kernel(
     const T* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attw,
     const T* __restrict__ gout, float* __restrict__ gvalue, float* __restrict__ gloc,
     float* __restrict__ gattw, Levels lv, int S, int Hh, int Q, int L, int P, long long groups) {
+  // lane = channel, 32 lanes per (b, q, head).  ENC: queries are the value grid itself
+  // (encoder self-attention, Q == S level-major): near corners are accumulated by
+  // msda_bwd_band_kernel, only far corners (|row - mapped row| beyond the margin) are
+  // added here with atomics.  !ENC: every corner is an atomic add.
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long grp = gid >> 5;
   const int c = (int)(gid & 31);
   if (grp >= groups) return;  // uniform per 32-lane half-wave
   const int LP = L * P;
   const int h = (int)(grp % Hh);
-  const long long b = grp / Hh / Q;
+  const long long bq = grp / Hh;
+  const int q = (int)(bq % Q);
+  const long long b = bq / Q;
+  int lq = 0, yq = 0, Hq = 1;
+  if (ENC) {
+    while (lq + 1 < L && q >= lv.start[lq + 1]) ++lq;
+    yq = (q - lv.start[lq]) / lv.w[lq];
+    Hq = lv.h[lq];
+  }
   const float* lp = loc + grp * LP * 2;
   const float* wp = attw + grp * LP;
   const size_t rowstride = (size_t)Hh * kD;
@@ -114,40 +175,38 @@ __global__ void __launch_bounds__(256) msda_bwd_kernel(
     const int Hl = lv.h[l], Wl = lv.w[l];
     const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
     const float fH = (float)Hl, fW = (float)Wl;
+    const int m = ENC ? mapped_row(yq, Hq, Hl) : 0;
     for (int p = 0; p < P; ++p) {
       const int tap = l * P + p;
-      const float x = lp[tap * 2 + 0];
-      const float y = lp[tap * 2 + 1];
       const float a = wp[tap];
-      const float him = y * fH - 0.5f;
-      const float wim = x * fW - 0.5f;
+      const Tap t = tap_geom(lp[tap * 2 + 0], lp[tap * 2 + 1], Hl, Wl);
       float r_w = 0.f, r_x = 0.f, r_y = 0.f;
-      if (him > -1.f && wim > -1.f && him < fH && wim < fW) {
-        const float fh0 = floorf(him), fw0 = floorf(wim);
-        const int h0 = (int)fh0, w0 = (int)fw0;
-        const float lh = him - fh0, lw = wim - fw0;
-        const float hh = 1.f - lh, hw = 1.f - lw;
+      if (t.inside) {
+        const int h0 = t.h0, w0 = t.w0;
+        const float lh = t.lh, lw = t.lw, hh = t.hh, hw = t.hw;
         const float ga = g * a;
         float v1 = 0.f, v2 = 0.f, v3 = 0.f, v4 = 0.f;
+        const bool far0 = !ENC || !near_row(h0, m);
+        const bool far1 = !ENC || !near_row(h0 + 1, m);
         if (h0 >= 0 && w0 >= 0) {
           const size_t o = lbase + (size_t)(h0 * Wl + w0) * rowstride;
           v1 = to_f32(value[o]);
-          atomicAdd(gvalue + o, hh * hw * ga);
+          if (far0) atomicAdd(gvalue + o, hh * hw * ga);
         }
         if (h0 >= 0 && w0 + 1 <= Wl - 1) {
           const size_t o = lbase + (size_t)(h0 * Wl + w0 + 1) * rowstride;
           v2 = to_f32(value[o]);
-          atomicAdd(gvalue + o, hh * lw * ga);
+          if (far0) atomicAdd(gvalue + o, hh * lw * ga);
         }
         if (h0 + 1 <= Hl - 1 && w0 >= 0) {
           const size_t o = lbase + (size_t)((h0 + 1) * Wl + w0) * rowstride;
           v3 = to_f32(value[o]);
-          atomicAdd(gvalue + o, lh * hw * ga);
+          if (far1) atomicAdd(gvalue + o, lh * hw * ga);
         }
         if (h0 + 1 <= Hl - 1 && w0 + 1 <= Wl - 1) {
           const size_t o = lbase + (size_t)((h0 + 1) * Wl + w0 + 1) * rowstride;
           v4 = to_f32(value[o]);
-          atomicAdd(gvalue + o, lh * lw * ga);
+          if (far1) atomicAdd(gvalue + o, lh * lw * ga);
         }
         const float val = hh * hw * v1 + hh * lw * v2 + lh * hw * v3 + lh * lw * v4;
         r_w = g * val;
@@ -168,6 +227,82 @@ __global__ void __launch_bounds__(256) msda_bwd_kernel(
         gloc[(grp * LP + tap) * 2 + 1] = r_y;
       }
     }
+  }
+}
+
+// grad_value by destination band (encoder mode).  One workgroup = (band of kBandRows
+// rows of level lb, head h, image b); the band's [rows][W][32] f32 accumulator lives in
+// LDS.  The workgroup scans every query (of every level) whose mapped row on level lb
+// lies within kBandR of the band, evaluates its taps on level lb, and adds the corners
+// that fall in the band AND are `near` their query (the complement of the query
+// kernel's far set) with LDS float atomics; the band is then written with plain
+// coalesced stores.  Waves walk queries; lane = channel; 2 queries per wave.
+template <typename T>
+__global__ void __launch_bounds__(kBandThreads) msda_bwd_band_kernel(
+    const float* __restrict__ loc, const float* __restrict__ attw, const T* __restrict__ gout,
+    float* __restrict__ gvalue, Levels lv, int S, int Hh, int L, int P, int band_rows) {
+  extern __shared__ __attribute__((aligned(16))) float sacc[];
+  // decode (level, band) from blockIdx.x
+  int bx = blockIdx.x, lb = 0;
+  while (lb + 1 < L && bx >= (lv.h[lb] + band_rows - 1) / band_rows) { bx -= (lv.h[lb] + band_rows - 1) / band_rows; ++lb; }
+  const int h = blockIdx.y;
+  const long long b = blockIdx.z;
+  const int Hl = lv.h[lb], Wl = lv.w[lb];
+  const int y0 = bx * band_rows;
+  const int y1 = min(Hl, y0 + band_rows);  // exclusive
+  const int nrows = y1 - y0;
+  const int LP = L * P;
+  for (int i = threadIdx.x; i < nrows * Wl * kD; i += blockDim.x) sacc[i] = 0.f;
+  __syncthreads();
+  const int c = threadIdx.x & 31;
+  const int slot = threadIdx.x >> 5;          // 16 query slots per workgroup
+  constexpr int kSlots = kBandThreads / 32;
+  for (int lq = 0; lq < L; ++lq) {
+    const int Hq = lv.h[lq], Wq = lv.w[lq];
+    // query rows whose mapped row m satisfies y0-R-1 <= m <= y1-1+R (m monotone in yq)
+    int ylo = 0, yhi = -1;
+    {
+      int lo = Hq, hi = -1;
+      for (int yq = 0; yq < Hq; ++yq) {
+        const int m = mapped_row(yq, Hq, Hl);
+        if (m >= y0 - kBandR - 1 && m <= y1 - 1 + kBandR) { lo = min(lo, yq); hi = max(hi, yq); }
+      }
+      ylo = lo; yhi = hi;
+    }
+    if (yhi < ylo) continue;
+    const int nq = (yhi - ylo + 1) * Wq;
+    const int qbase = lv.start[lq] + ylo * Wq;
+    for (int qi = slot; qi < nq; qi += kSlots) {
+      const int q = qbase + qi;
+      const int yq = ylo + qi / Wq;
+      const int m = mapped_row(yq, Hq, Hl);
+      const long long grp = (b * S + q) * Hh + h;
+      const float g = to_f32(gout[grp * kD + c]);
+      const float* lp = loc + grp * LP * 2 + lb * P * 2;
+      const float* wp = attw + grp * LP + lb * P;
+      for (int p = 0; p < P; ++p) {
+        const Tap t = tap_geom(lp[2 * p], lp[2 * p + 1], Hl, Wl);
+        if (!t.inside) continue;
+        const float ga = g * wp[p];
+        const int h0 = t.h0, w0 = t.w0;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) {
+          const int cy = h0 + dy;
+          if (cy < y0 || cy >= y1 || cy > Hl - 1 || !near_row(cy, m)) continue;
+          const float wy = dy ? t.lh : t.hh;
+          float* row = sacc + ((cy - y0) * Wl) * kD + c;
+          if (w0 >= 0) atomicAdd(row + w0 * kD, wy * t.hw * ga);
+          if (w0 + 1 <= Wl - 1) atomicAdd(row + (w0 + 1) * kD, wy * t.lw * ga);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const size_t rowstride = (size_t)Hh * kD;
+  float* dst = gvalue + ((size_t)b * S * Hh + h) * kD + (size_t)(lv.start[lb] + y0 * Wl) * rowstride;
+  for (int i = threadIdx.x; i < nrows * Wl * kD; i += blockDim.x) {
+    const int px = i / kD, cc = i - px * kD;
+    dst[(size_t)px * rowstride + cc] = sacc[i];
   }
 }
 
@@ -217,32 +352,72 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
   return VS_OK;
 }
 
-extern "C" int vs_msda_backward(int dtype, const void* value, const int64_t* shapes,
-                                const int64_t* starts, const float* loc, const float* attw,
-                                const void* gout, float* gvalue, float* gloc, float* gattw,
-                                int B, int S, int Hh, int D, int L, int Q, int P, void* stream) {
+static int msda_backward_impl(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
+                              const float* loc, const float* attw, const void* gout, float* gvalue, float* gloc,
+                              float* gattw, int B, int S, int Hh, int D, int L, int Q, int P, void* stream,
+                              bool encoder) {
   VS_CHECK(D == kD, "channels per head must be 32");
   VS_CHECK(L >= 1 && L <= kMaxLevels, "1..4 levels supported");
   VS_CHECK(B > 0 && S > 0 && Hh > 0 && Q >= 0 && P > 0, "bad sizes");
   VS_CHECK(value && loc && attw && gout && gvalue && gloc && gattw && shapes && starts, "null pointer");
   Levels lv;
   VS_CHECK(fill_levels(&lv, shapes, starts, L, S), "spatial shapes / level starts inconsistent with S");
+  VS_CHECK(!encoder || Q == S, "encoder mode needs the queries to be the value grid (Q == S)");
   hipStream_t st = (hipStream_t)stream;
-  VS_HIP(hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * Hh * kD, st));
-  if (Q == 0) return VS_OK;
   const long long groups = (long long)B * Q * Hh;
   const int block = 256;
   const long long threads = groups * 32;
   const int grid = (int)((threads + block - 1) / block);
+  if (encoder) {
+    int maxw = 0, bands = 0;
+    for (int l = 0; l < L; ++l) maxw = max(maxw, lv.w[l]);
+    const int band_rows = min(kBandMaxRows, (int)((160 * 1024) / ((size_t)maxw * kD * sizeof(float))));
+    VS_CHECK(band_rows >= 1, "level too wide for the band kernel");
+    for (int l = 0; l < L; ++l) bands += (lv.h[l] + band_rows - 1) / band_rows;
+    const size_t lds = (size_t)band_rows * maxw * kD * sizeof(float);
+    dim3 bgrid(bands, Hh, B);
+    if (dtype == VS_BF16) {
+      hipLaunchKernelGGL(msda_bwd_band_kernel<bf16>, bgrid, dim3(kBandThreads), lds, st, loc, attw, (const bf16*)gout,
+                         gvalue, lv, S, Hh, L, P, band_rows);
+      hipLaunchKernelGGL((msda_bwd_kernel<bf16, true>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, attw,
+                         (const bf16*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
+    } else if (dtype == VS_F32) {
+      hipLaunchKernelGGL(msda_bwd_band_kernel<float>, bgrid, dim3(kBandThreads), lds, st, loc, attw,
+                         (const float*)gout, gvalue, lv, S, Hh, L, P, band_rows);
+      hipLaunchKernelGGL((msda_bwd_kernel<float, true>), dim3(grid), dim3(block), 0, st, (const float*)value, loc,
+                         attw, (const float*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
+    } else {
+      VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
+    }
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
+  VS_HIP(hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * Hh * kD, st));
+  if (Q == 0) return VS_OK;
   if (dtype == VS_BF16) {
-    hipLaunchKernelGGL(msda_bwd_kernel<bf16>, dim3(grid), dim3(block), 0, st, (const bf16*)value,
-                       loc, attw, (const bf16*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
+    hipLaunchKernelGGL((msda_bwd_kernel<bf16, false>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, attw,
+                       (const bf16*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
   } else if (dtype == VS_F32) {
-    hipLaunchKernelGGL(msda_bwd_kernel<float>, dim3(grid), dim3(block), 0, st, (const float*)value,
-                       loc, attw, (const float*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
+    hipLaunchKernelGGL((msda_bwd_kernel<float, false>), dim3(grid), dim3(block), 0, st, (const float*)value, loc,
+                       attw, (const float*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
   } else {
     VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
   }
   VS_LAUNCH_CHECK();
   return VS_OK;
+}
+
+extern "C" int vs_msda_backward(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
+                                const float* loc, const float* attw, const void* gout, float* gvalue, float* gloc,
+                                float* gattw, int B, int S, int Hh, int D, int L, int Q, int P, void* stream) {
+  return msda_backward_impl(dtype, value, shapes, starts, loc, attw, gout, gvalue, gloc, gattw, B, S, Hh, D, L, Q,
+                            P, stream, false);
+}
+
+extern "C" int vs_msda_backward_encoder(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
+                                        const float* loc, const float* attw, const void* gout, float* gvalue,
+                                        float* gloc, float* gattw, int B, int S, int Hh, int D, int L, int P,
+                                        void* stream) {
+  return msda_backward_impl(dtype, value, shapes, starts, loc, attw, gout, gvalue, gloc, gattw, B, S, Hh, D, L, S,
+                            P, stream, true);
 }

@@ -27,17 +27,21 @@ SIGNATURES = {
     "vs_last_error": [],
     "vs_msda_forward": [_c_int, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_msda_backward": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
+    "vs_msda_backward_encoder": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 6 + [_P],
     "vs_window_partition": [_P, _P] + [_c_int] * 7 + [_P],
     "vs_window_reverse": [_P, _P] + [_c_int] * 7 + [_P],
     "vs_window_attn_forward": [_c_int, _P, _P, _P, _P] + [_c_int] * 6 + [_c_float, _P],
     "vs_window_attn_backward": [_c_int, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 6 + [_c_float, _P],
     "vs_mask_head_forward": [_c_int, _P, _P, _P] + [_c_int] * 5 + [_P],
+    "vs_mask_head_backward_workspace_bytes": [_c_int] * 3,
+    "vs_mask_head_backward": [_c_int] + [_P] * 6 + [_c_int] * 5 + [_P],
     "vs_attn_bitmask": [_P, _P] + [_c_int] * 5 + [_P],
     "vs_masked_attn_workspace_bytes": [_c_int] * 4,
     "vs_masked_attn_forward": [_c_int, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 4 + [_c_float, _P],
     "vs_masked_attn_backward": [_c_int] + [_P] * 11 + [_c_int] * 4 + [_c_float, _P],
 }
-RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": ctypes.c_longlong}
+RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": ctypes.c_longlong,
+            "vs_mask_head_backward_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
 

@@ -253,7 +253,7 @@ class MSDeformAttn(nn.Module):
         aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
         aw = F.softmax(aw.float(), -1).view(B, S, self.heads, self.levels, self.points)
         loc = ref[:, :, None, :, None, :] + off.float() / norm           # HF:m2f:994-1002
-        out = ops.ms_deform_attn(value, shapes, loc, aw)
+        out = ops.ms_deform_attn(value, shapes, loc, aw, encoder=True)
         return self.output_proj(out)
 
 

@@ -47,7 +47,7 @@ class MSDeformAttnFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, value, spatial_shapes, level_start_index, sampling_locations, attention_weights,
-                im2col_step=64):
+                im2col_step=64, encoder=False):
         shapes = _shapes_list(spatial_shapes)
         L.require_hip(value, sampling_locations, attention_weights)
         value = value.contiguous()
@@ -64,6 +64,7 @@ class MSDeformAttnFunction(torch.autograd.Function):
             L.check(L.lib().vs_msda_forward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
                                             L.ptr(out), B, S, H, D, Lv, Q, P, L.stream(value)), "msda_forward")
         ctx.shapes = shapes
+        ctx.encoder = bool(encoder) and Q == S
         ctx.save_for_backward(value, loc, aw)
         return out
 
@@ -79,16 +80,23 @@ class MSDeformAttnFunction(torch.autograd.Function):
         sh, st, _ = _level_arrays(ctx.shapes)
         nb = (value.numel() + g.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 8 + gv.numel() * 4
         with timed("msda_bwd", value, bytes_=nb, flops=2.0 * aw.numel() * 10 * D):
-            L.check(L.lib().vs_msda_backward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
-                                             L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga), B, S, H, D, Lv, Q, P,
-                                             L.stream(value)), "msda_backward")
-        return gv.to(value.dtype), None, None, gl, ga, None
+            if ctx.encoder:
+                L.check(L.lib().vs_msda_backward_encoder(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc),
+                                                         L.ptr(aw), L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga), B, S,
+                                                         H, D, Lv, P, L.stream(value)), "msda_backward_encoder")
+            else:
+                L.check(L.lib().vs_msda_backward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
+                                                 L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga), B, S, H, D, Lv, Q, P,
+                                                 L.stream(value)), "msda_backward")
+        return gv.to(value.dtype), None, None, gl, ga, None, None
 
 
-def ms_deform_attn(value, spatial_shapes, sampling_locations, attention_weights):
-    """Functional form with the oracle's argument order (HF:m2f:798)."""
+def ms_deform_attn(value, spatial_shapes, sampling_locations, attention_weights, encoder: bool = False):
+    """Functional form with the oracle's argument order (HF:m2f:798).  `encoder=True`
+    declares that the queries are the value grid itself (pixel-decoder self-attention,
+    Q == S): the backward then builds grad_value by destination band, without atomics."""
     shapes = _shapes_list(spatial_shapes)
-    return MSDeformAttnFunction.apply(value, shapes, None, sampling_locations, attention_weights, 64)
+    return MSDeformAttnFunction.apply(value, shapes, None, sampling_locations, attention_weights, 64, encoder)
 
 
 def _padded(n, ws):
@@ -215,9 +223,9 @@ def window_attention(qkv, rel_table, heads: int, window: int, shift: int, nwin_h
 
 class MaskHeadFunction(torch.autograd.Function):
     """logits [B,Q,H,W] f32 = einsum('bqc,bchw->bqhw') with the pixel embedding given
-    channels-last (HF:m2f:2051).  Forward: hand-written MFMA kernel.  Backward: the two
-    operand gradients are plain GEMMs (dE = dL.P, dP = dL^T.E) and go to hipBLASLt via
-    torch.matmul."""
+    channels-last (HF:m2f:2051).  Forward: hand-written MFMA kernel.  Backward (bf16):
+    one fused MFMA kernel producing dE = dL.P and dP = dL^T.E in a single pass over dL;
+    f32 parity mode uses vendor GEMMs for the backward."""
 
     @staticmethod
     def forward(ctx, mask_embed, pixel_nhwc, height, width):
@@ -240,6 +248,20 @@ class MaskHeadFunction(torch.autograd.Function):
     def backward(ctx, g):
         E, P = ctx.saved_tensors
         B, Q, C = E.shape
+        N = P.shape[1]
+        if E.dtype == torch.bfloat16 and Q <= 128 and C in (128, 256):
+            g = g.float().contiguous()
+            gE = torch.empty_like(E)
+            gP = torch.empty_like(P)
+            ws = torch.empty(int(L.lib().vs_mask_head_backward_workspace_bytes(B, Q, C)), device=E.device,
+                             dtype=torch.uint8)
+            nb = g.numel() * 4 + (E.numel() * 2 + P.numel() * 2) * 2
+            with timed("mask_head_bwd", E, bytes_=nb, flops=4.0 * B * Q * C * N):
+                L.check(L.lib().vs_mask_head_backward(L.dtype_code(E), L.ptr(g), L.ptr(E), L.ptr(P), L.ptr(gE),
+                                                      L.ptr(gP), L.ptr(ws), B, Q, C, N, 1, L.stream(E)),
+                        "mask_head_backward")
+            return gE, gP.to(ctx.pdtype), None, None
+        # f32 parity mode (and shapes outside the fused kernel): vendor GEMMs
         gl = g.reshape(B, Q, -1).to(E.dtype)
         gE = torch.bmm(gl, P) if ctx.needs_input_grad[0] else None
         gP = torch.bmm(gl.transpose(1, 2), E).to(ctx.pdtype) if ctx.needs_input_grad[1] else None
