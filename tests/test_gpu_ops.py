@@ -363,10 +363,12 @@ def test_msda_encoder_backward_vs_oracle(cfg, dtype):
     vd, ld, wd = value.to(DEV).requires_grad_(True), loc.to(DEV).requires_grad_(True), w.to(DEV).requires_grad_(True)
     out = ops.ms_deform_attn(vd, shapes, ld, wd, encoder=True)
     out.backward(go.to(dtype).to(DEV))
-    tol = 2e-5 if dtype == torch.float32 else None
     if dtype == torch.float32:
-        np.testing.assert_allclose(vd.grad.cpu().numpy(), vr.grad.numpy(), atol=tol, rtol=0)
-        np.testing.assert_allclose(wd.grad.cpu().numpy(), wr.grad.numpy(), atol=tol, rtol=0)
+        # f32: the coordinate x*W-0.5 carries ~|xW|*2^-24 rounding (fma vs mul+sub), scaled
+        # by the channel sums -> tolerance relative to the gradient magnitude
+        for got, exp in ((vd.grad, vr.grad), (wd.grad, wr.grad)):
+            e = exp.numpy()
+            np.testing.assert_allclose(got.cpu().numpy(), e, atol=2e-5 * max(1.0, float(np.abs(e).max())), rtol=0)
     else:
         gvr = vr.grad
         err = (vd.grad.float().cpu() - gvr).abs()

@@ -1,0 +1,105 @@
+"""Per-kernel microbenchmark at the C2 training shapes (Swin-T M2F, 4 x 1024^2, bf16).
+
+    python tools/kbench.py [--only msda,mask,win,xattn] [--iters 20]
+
+Times each hand-written op (forward and backward separately) with HIP events on the
+current stream, interleaving variants in one process, and prints ms / GB/s / TF/s from
+the same algorithmic byte and flop counts bench.py's roofline uses.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "vision-instance-seg_amd"))
+
+import torch  # noqa: E402
+
+from visionseg import ops  # noqa: E402
+from visionseg.profiling import KernelTimer  # noqa: E402
+
+
+def run(name, fn, iters, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    with KernelTimer() as t:
+        for _ in range(iters):
+            fn()
+    torch.cuda.synchronize()
+    for k, v in sorted(t.summary().items()):
+        gbs = v["bytes"] / (v["mean_ms"] / 1e3) / 1e9 if v["bytes"] else 0
+        tfs = v["flops"] / (v["mean_ms"] / 1e3) / 1e12 if v["flops"] else 0
+        print(f"{name:28s} {k:18s} {v['mean_ms']:8.4f} ms  {gbs:8.1f} GB/s  {tfs:8.2f} TF/s  x{v['launches'] // iters}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="msda,mask,win,xattn")
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    dev = "cuda"
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    B = 4
+    if "msda" in a.only:
+        shapes = [(32, 32), (64, 64), (128, 128)]
+        S = sum(h * w for h, w in shapes)
+        H, L, P = 8, 3, 4
+        ys = [torch.linspace(0.5, h - 0.5, h, device=dev) / h for h, w in shapes]
+        xs = [torch.linspace(0.5, w - 0.5, w, device=dev) / w for h, w in shapes]
+        ref = torch.cat([torch.stack(torch.meshgrid(x, y, indexing="xy"), -1).reshape(-1, 2) for x, y in zip(xs, ys)])
+        norm = torch.tensor([[w, h] for h, w in shapes], device=dev, dtype=torch.float32)
+        off = (torch.rand(B, S, H, L, P, 2, device=dev, generator=g) * 2 - 1) * 4
+        loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
+        w = torch.softmax(torch.randn(B, S, H, L * P, device=dev, generator=g), -1).view(B, S, H, L, P)
+        v = torch.randn(B, S, H, 32, device=dev, generator=g).to(bf).requires_grad_(True)
+        go = torch.randn(B, S, H * 32, device=dev, generator=g).to(bf)
+        locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
+        for enc in (True, False):
+            def fb(enc=enc):
+                o = ops.ms_deform_attn(v, shapes, locr, wr, encoder=enc)
+                o.backward(go)
+            run(f"msda encoder={enc}", fb, a.iters)
+    if "mask" in a.only:
+        Q, C, Hm = 100, 256, 256
+        E = torch.randn(B, Q, C, device=dev, generator=g).to(bf).requires_grad_(True)
+        Pm = torch.randn(B, Hm * Hm, C, device=dev, generator=g).to(bf).requires_grad_(True)
+        gl = torch.randn(B, Q, Hm, Hm, device=dev, generator=g)
+
+        def mh():
+            lo = ops.mask_head(E, Pm, Hm, Hm)
+            lo.backward(gl)
+            ops.attn_bitmask(lo.detach(), (128, 128))
+        run("mask head 4x100x256x256^2", mh, a.iters)
+    if "win" in a.only:
+        for (nW, heads, tag) in ((37, 3, "stage1"), (19, 6, "stage2"), (10, 12, "stage3"), (5, 24, "stage4")):
+            Bw = B * nW * nW
+            qkv = torch.randn(Bw, 49, 3 * heads * 32, device=dev, generator=g).to(bf).requires_grad_(True)
+            tab = torch.randn(169, heads, device=dev, generator=g).requires_grad_(True)
+            gout = torch.randn(Bw, 49, heads * 32, device=dev, generator=g).to(bf)
+
+            def wa(qkv=qkv, tab=tab, gout=gout, heads=heads, nW=nW):
+                o = ops.window_attention(qkv, tab, heads, 7, 3, nW, nW)
+                o.backward(gout)
+            run(f"window attn {tag}", wa, a.iters)
+    if "xattn" in a.only:
+        for S in (1024, 4096, 16384):
+            q = torch.randn(B, 100, 256, device=dev, generator=g).to(bf).requires_grad_(True)
+            k = torch.randn(B, S, 256, device=dev, generator=g).to(bf).requires_grad_(True)
+            vv = torch.randn(B, S, 256, device=dev, generator=g).to(bf).requires_grad_(True)
+            lo = torch.randn(B, 100, int(S ** 0.5), int(S ** 0.5), device=dev, generator=g)
+            words = ops.attn_bitmask(lo, (int(S ** 0.5), int(S ** 0.5)))
+            go = torch.randn(B, 100, 256, device=dev, generator=g).to(bf)
+
+            def xa(q=q, k=k, vv=vv, words=words, go=go):
+                o = ops.masked_attention(q, k, vv, words, 8)
+                o.backward(go)
+            run(f"masked xattn S={S}", xa, a.iters)
+
+
+if __name__ == "__main__":
+    main()

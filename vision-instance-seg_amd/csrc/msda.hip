@@ -44,7 +44,8 @@ struct Levels {
 constexpr int kBandR = 4;      // row margin (level-l rows) of the band kernel's query scan; covers the
                                // Deformable-DETR init offsets (|off| <= 4 px); farther taps go atomic
 constexpr int kBandMaxRows = 8;     // value rows per band workgroup (fewer if the level is wide)
-constexpr int kBandThreads = 512;   // 16 query slots of 32 channel-lanes
+constexpr int kBandThreads = 1024;  // 32 query slots of 32 channel-lanes
+constexpr int kBandUnroll = 4;      // queries in flight per slot (loads hoisted ahead of the LDS adds)
 
 struct Tap {
   int h0, w0;
@@ -272,27 +273,42 @@ __global__ void __launch_bounds__(kBandThreads) msda_bwd_band_kernel(
     if (yhi < ylo) continue;
     const int nq = (yhi - ylo + 1) * Wq;
     const int qbase = lv.start[lq] + ylo * Wq;
-    for (int qi = slot; qi < nq; qi += kSlots) {
-      const int q = qbase + qi;
-      const int yq = ylo + qi / Wq;
-      const int m = mapped_row(yq, Hq, Hl);
-      const long long grp = (b * S + q) * Hh + h;
-      const float g = to_f32(gout[grp * kD + c]);
-      const float* lp = loc + grp * LP * 2 + lb * P * 2;
-      const float* wp = attw + grp * LP + lb * P;
-      for (int p = 0; p < P; ++p) {
-        const Tap t = tap_geom(lp[2 * p], lp[2 * p + 1], Hl, Wl);
-        if (!t.inside) continue;
-        const float ga = g * wp[p];
-        const int h0 = t.h0, w0 = t.w0;
+    for (int q0 = slot * kBandUnroll; q0 < nq; q0 += kSlots * kBandUnroll) {
+      float4 la[kBandUnroll], lb4[kBandUnroll], wv[kBandUnroll];
+      float gg[kBandUnroll];
+      int mm[kBandUnroll];
 #pragma unroll
-        for (int dy = 0; dy < 2; ++dy) {
-          const int cy = h0 + dy;
-          if (cy < y0 || cy >= y1 || cy > Hl - 1 || !near_row(cy, m)) continue;
-          const float wy = dy ? t.lh : t.hh;
-          float* row = sacc + ((cy - y0) * Wl) * kD + c;
-          if (w0 >= 0) atomicAdd(row + w0 * kD, wy * t.hw * ga);
-          if (w0 + 1 <= Wl - 1) atomicAdd(row + (w0 + 1) * kD, wy * t.lw * ga);
+      for (int u = 0; u < kBandUnroll; ++u) {
+        const int qi = min(q0 + u, nq - 1);
+        const int q = qbase + qi;
+        mm[u] = mapped_row(ylo + qi / Wq, Hq, Hl);
+        const long long grp = (b * S + q) * Hh + h;
+        const float4* lp4 = reinterpret_cast<const float4*>(loc + grp * LP * 2 + lb * P * 2);
+        la[u] = lp4[0];
+        lb4[u] = lp4[1];
+        wv[u] = *reinterpret_cast<const float4*>(attw + grp * LP + lb * P);
+        gg[u] = (q0 + u < nq) ? to_f32(gout[grp * kD + c]) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kBandUnroll; ++u) {
+        const float xs[4] = {la[u].x, la[u].z, lb4[u].x, lb4[u].z};
+        const float ys[4] = {la[u].y, la[u].w, lb4[u].y, lb4[u].w};
+        const float ws4[4] = {wv[u].x, wv[u].y, wv[u].z, wv[u].w};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const Tap t = tap_geom(xs[p], ys[p], Hl, Wl);
+          if (!t.inside) continue;
+          const float ga = gg[u] * ws4[p];
+          const int h0 = t.h0, w0 = t.w0;
+#pragma unroll
+          for (int dy = 0; dy < 2; ++dy) {
+            const int cy = h0 + dy;
+            if (cy < y0 || cy >= y1 || cy > Hl - 1 || !near_row(cy, mm[u])) continue;
+            const float wy = dy ? t.lh : t.hh;
+            float* row = sacc + ((cy - y0) * Wl) * kD + c;
+            if (w0 >= 0) atomicAdd(row + w0 * kD, wy * t.hw * ga);
+            if (w0 + 1 <= Wl - 1) atomicAdd(row + (w0 + 1) * kD, wy * t.lw * ga);
+          }
         }
       }
     }
@@ -363,6 +379,7 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   Levels lv;
   VS_CHECK(fill_levels(&lv, shapes, starts, L, S), "spatial shapes / level starts inconsistent with S");
   VS_CHECK(!encoder || Q == S, "encoder mode needs the queries to be the value grid (Q == S)");
+  VS_CHECK(!encoder || P == 4, "encoder-mode backward is specialised for 4 sampling points");
   hipStream_t st = (hipStream_t)stream;
   const long long groups = (long long)B * Q * Hh;
   const int block = 256;
