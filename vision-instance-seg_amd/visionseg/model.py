@@ -240,6 +240,7 @@ class MSDeformAttn(nn.Module):
     def __init__(self, d, heads, levels, points):
         super().__init__()
         self.d, self.heads, self.levels, self.points = d, heads, levels, points
+        self.band_backward = False   # opt-in destination-band grad_value (see csrc/msda.hip)
         self.sampling_offsets = nn.Linear(d, heads * levels * points * 2)
         self.attention_weights = nn.Linear(d, heads * levels * points)
         self.value_proj = nn.Linear(d, d)
@@ -253,7 +254,7 @@ class MSDeformAttn(nn.Module):
         aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
         aw = F.softmax(aw.float(), -1).view(B, S, self.heads, self.levels, self.points)
         loc = ref[:, :, None, :, None, :] + off.float() / norm           # HF:m2f:994-1002
-        out = ops.ms_deform_attn(value, shapes, loc, aw, encoder=True)
+        out = ops.ms_deform_attn(value, shapes, loc, aw, encoder=self.band_backward)
         return self.output_proj(out)
 
 
