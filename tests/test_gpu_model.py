@@ -90,3 +90,27 @@ def test_bf16_training_step():
     for p in m.parameters():
         assert torch.isfinite(p).all()
     print("bf16 losses", losses)
+
+
+def test_train_template_seam_and_inference_seam(tmp_path):
+    """train_template.train_maskdino(...) contract (metrics dict, results, checkpoint) and
+    the ai_segmentation init_detector / inference_detector contract on the trained model."""
+    from visionseg.adapters import train_maskdino
+    from visionseg.data import write_coco_dataset
+    from visionseg.inference import init_detector, inference_detector
+    write_coco_dataset(str(tmp_path / "train"), 4, 128, seed=1)
+    write_coco_dataset(str(tmp_path / "val"), 2, 128, seed=2)
+    hp = dict(epochs=2, batch_size=2, img_size=128, save_period=1, warmup_epochs=0)
+    r = train_maskdino("exp_test", tmp_path / "train", tmp_path / "val", tmp_path / "out", hp)
+    assert set(r) == {"mAP50", "mAP75", "mAP", "precision", "recall"}
+    assert all(0.0 <= v <= 1.0 for v in r.values())
+    assert (tmp_path / "out" / "model_final.pth").exists() and (tmp_path / "out" / "model_epoch0002.pth").exists()
+    assert train_maskdino("missing", tmp_path / "nope", tmp_path / "val", tmp_path / "out2", hp) is None
+    det = init_detector("swin_t", str(tmp_path / "out" / "model_final.pth"), device="cuda:0")
+    img = (np.random.default_rng(0).integers(0, 256, (100, 140, 3))).astype(np.uint8)
+    res = inference_detector(det, img)
+    pi = res.pred_instances
+    assert len(pi) == 100 and pi.masks.shape == (100, 100, 140) and pi.masks.dtype == torch.bool
+    best = int(pi.scores.cpu().numpy().argmax())                  # the caller's selection (ai_segmentation.py:83-88)
+    mask = pi.masks[best].cpu().numpy()
+    assert mask.shape == img.shape[:2] and int(pi.labels[best]) == 0

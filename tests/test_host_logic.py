@@ -1,0 +1,99 @@
+"""Host-side logic on CPU: COCO data path, mask-AP evaluator, state-dict conversion,
+LR schedule, instance post-processing."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from visionseg.data import write_coco_dataset, CocoInstanceDataset, collate_padded, synthetic_batch, normalize
+from visionseg.evaluate import MaskAPEvaluator
+from visionseg.convert import from_hf_state_dict, to_hf_state_dict
+from visionseg.model import M2FConfig, Mask2Former
+from visionseg.train import SolverConfig, _lr_lambda
+from visionseg.inference import instance_inference
+
+
+def test_coco_roundtrip(tmp_path):
+    coco = write_coco_dataset(str(tmp_path), n_images=3, size=96, seed=1)
+    assert set(coco) == {"images", "annotations", "categories"}
+    ds = CocoInstanceDataset(str(tmp_path), train=False, keep_size=True)
+    assert len(ds) == 3
+    img, m, c = ds[0]
+    assert img.dtype == torch.uint8 and img.shape == (3, 96, 96)
+    assert m.dtype == torch.bool and m.shape[1:] == (96, 96) and m.shape[0] == c.shape[0] >= 1
+    assert (c == 0).all()
+    # annotation areas match the rasterised masks
+    areas = [a["area"] for a in coco["annotations"] if a["image_id"] == 0]
+    assert np.allclose(sorted(areas), sorted(m.flatten(1).sum(1).tolist()))
+    ds2 = CocoInstanceDataset(str(tmp_path), min_size=(64,), max_size=80, train=True, seed=0)
+    batch = collate_padded([ds2[0], ds2[1]])
+    assert batch[0].shape[-1] % 32 == 0 and batch[0].shape[-2] % 32 == 0
+    assert batch[1][0].shape[-2:] == batch[0].shape[-2:]
+
+
+def test_synthetic_batch_shapes():
+    imgs, ml, cl = synthetic_batch(2, 128, seed=42)
+    assert imgs.shape == (2, 3, 128, 128) and imgs.dtype == torch.float32
+    for m, c in zip(ml, cl):
+        assert 1 <= m.shape[0] <= 3 and m.shape[0] == c.shape[0]
+        frac = m.float().mean((1, 2))
+        assert bool(((frac > 0.001) & (frac < 0.2)).all())
+    n = normalize(torch.full((1, 3, 2, 2), 128, dtype=torch.uint8))[0, :, 0, 0]
+    assert torch.allclose(n, torch.tensor([(128 - 123.675) / 58.395, (128 - 116.28) / 57.12, (128 - 103.53) / 57.375]))
+
+
+def test_mask_ap_evaluator():
+    g = torch.Generator().manual_seed(0)
+    gt = torch.zeros(3, 32, 32, dtype=torch.bool)
+    gt[0, 2:10, 2:10] = True
+    gt[1, 15:30, 5:12] = True
+    gt[2, 20:25, 20:31] = True
+    lab = torch.zeros(3, dtype=torch.int64)
+    ev = MaskAPEvaluator(1)
+    ev.add(torch.tensor([0.9, 0.8, 0.7]), lab, gt.clone(), gt, lab)
+    r = ev.summarize()
+    assert r["mAP"] == pytest.approx(1.0) and r["mAP50"] == pytest.approx(1.0)
+    assert r["precision"] == 1.0 and r["recall"] == 1.0
+    ev = MaskAPEvaluator(1)
+    pred = gt.clone()
+    pred[0] = False
+    pred[0, 2:10, 2:7] = True            # IoU 5/8 = 0.625
+    ev.add(torch.tensor([0.9, 0.8, 0.7]), lab, pred, gt, lab)
+    r = ev.summarize()
+    assert r["mAP50"] == pytest.approx(1.0)
+    assert r["mAP75"] < 1.0 and 0.5 < r["mAP"] < 1.0
+    ev = MaskAPEvaluator(1)
+    ev.add(torch.zeros(0), torch.zeros(0, dtype=torch.int64), torch.zeros(0, 32, 32, dtype=torch.bool), gt, lab)
+    assert ev.summarize()["mAP"] == 0.0
+
+
+def test_state_dict_conversion_roundtrip():
+    cfg = M2FConfig(embed_dim=32, depths=(2, 2, 2, 2), num_heads=(1, 2, 4, 8), feature_size=64, mask_feature_size=64,
+                    hidden_dim=64, enc_ffn=128, dec_ffn=128, dec_heads=2, enc_layers=2, dec_layers=4, num_queries=10)
+    sd = Mask2Former(cfg).init_weights(0).state_dict()
+    hf = to_hf_state_dict(sd)
+    assert any(k.endswith("attention.q_proj.weight") for k in hf)
+    back = from_hf_state_dict(hf)
+    assert set(back) == set(sd) and all(torch.equal(back[k], sd[k]) for k in sd)
+
+
+def test_lr_schedules():
+    f = _lr_lambda(SolverConfig(warmup_iters=200, steps=(3500, 4500)))
+    assert f(0) == pytest.approx(0.001) and f(200) == 1.0 and f(3600) == pytest.approx(0.1) and f(4600) == pytest.approx(0.01)
+    c = _lr_lambda(SolverConfig(warmup_iters=0, schedule="cosine", max_iter=100))
+    assert c(0) == 1.0 and c(50) == pytest.approx(0.5) and c(100) == pytest.approx(0.0, abs=1e-12)
+
+
+def test_instance_inference():
+    Q, K = 4, 1
+    ml = torch.full((Q, 8, 8), -5.0)
+    ml[1, 2:6, 2:6] = 5.0
+    cl = torch.tensor([[0.0, 3.0], [4.0, 0.0], [0.0, 0.0], [-2.0, 2.0]])
+    s, lab, m = instance_inference(ml, cl, (32, 32))
+    assert m.shape == (4, 32, 32) and m.dtype == torch.bool
+    best = int(torch.argmax(s))
+    assert m[best].sum() > 0 and (lab == 0).all()
+    assert float(s.max()) > 0.9

@@ -1,0 +1,117 @@
+"""Training seam of training/train_template.py.
+
+The reference dispatches `--model` to `train_<model>(exp_name, train_dir, test_dir,
+output_dir, hyperparams) -> dict` (training/train_template.py:104, 197-205) and writes
+the returned metrics (`mAP50, mAP75, mAP, precision, recall`, :139-145) plus
+exp_name / model_type / hyperparams to `output_dir/results.json` (:207-214).  Its
+MaskDINO slot is a stub returning zeros (:104-145).  `train_mask2former` is a working
+implementation of that contract on the MI355X path (Swin + Mask2Former, COCO json in
+`train_dir/annotations.json`, evaluation on `test_dir`); `train_maskdino` is the same
+function under the reference's name (the MaskDINO decoder itself is the next row of the
+plan).  Missing annotations -> None, as the caller expects (:188-194).
+
+Multi-GPU: run the caller under torchrun; images are sharded by rank, gradients are
+all-reduced by the Trainer (RCCL), rank 0 writes checkpoints and evaluates.
+"""
+from __future__ import annotations
+
+import math
+import os
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .criterion import SetCriterion
+from .data import CocoInstanceDataset, collate_padded
+from .evaluate import MaskAPEvaluator
+from .inference import Predictor
+from .model import M2FConfig, Mask2Former
+from .train import SolverConfig, Trainer, init_distributed
+
+HYPERPARAMS = {   # defaults of training/train_template.py:45-57
+    "epochs": 100, "batch_size": 8, "learning_rate": 1e-4, "weight_decay": 1e-4, "optimizer": "AdamW",
+    "lr_scheduler": "cosine", "warmup_epochs": 5, "img_size": 640, "random_seed": 42,
+    "early_stopping_patience": 15, "save_period": 10,
+}
+
+
+def evaluate_dir(model: Mask2Former, test_dir, img_size: int = 640, device="cuda", max_images: int | None = None):
+    """COCO mask AP of `model` on `test_dir/annotations.json` (original resolution)."""
+    test_dir = Path(test_dir)
+    if not (test_dir / "annotations.json").exists():
+        return None
+    ds = CocoInstanceDataset(str(test_dir), train=False, keep_size=True)
+    pred = Predictor(model, device=device, min_size=img_size, max_size=int(round(img_size * 1.25)))
+    ev = MaskAPEvaluator(num_classes=model.cfg.num_labels)
+    n = len(ds) if max_images is None else min(len(ds), max_images)
+    for i in range(n):
+        img, masks, classes = ds[i]
+        bgr = img.permute(1, 2, 0).numpy()[:, :, ::-1]
+        r = pred(np.ascontiguousarray(bgr)).pred_instances
+        ev.add(r.scores, r.labels, r.masks, masks.to(r.masks.device), classes)
+    model.train()
+    return ev.summarize()
+
+
+def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, backbone: str = "swin_t",
+                      device=None, max_iters: int | None = None):
+    hp = dict(HYPERPARAMS)
+    hp.update(hyperparams or {})
+    train_dir, output_dir = Path(train_dir), Path(output_dir)
+    if not (train_dir / "annotations.json").exists():
+        print(f"annotations not found: {train_dir / 'annotations.json'}")
+        return None
+    rank, local, world = init_distributed()
+    if device is None:
+        device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    seed = int(hp["random_seed"])
+    torch.manual_seed(seed + rank)
+    img = int(hp["img_size"])
+    ds = CocoInstanceDataset(str(train_dir), min_size=(img,), max_size=int(round(img * 1.25)), train=True,
+                             seed=seed + rank)
+    cfg = M2FConfig.preset(backbone, num_labels=max(1, len(ds.cat_to_label)))
+    model = Mask2Former(cfg).init_weights(seed)
+    bs = int(hp["batch_size"])
+    per_rank = max(1, bs // world)
+    iters_per_epoch = max(1, math.ceil(len(ds) / (per_rank * world)))
+    total = iters_per_epoch * int(hp["epochs"])
+    if max_iters is not None:
+        total = min(total, max_iters)
+    solver = SolverConfig(lr=float(hp["learning_rate"]), weight_decay=float(hp["weight_decay"]),
+                          schedule="cosine" if hp.get("lr_scheduler") == "cosine" else "multistep",
+                          warmup_iters=int(hp.get("warmup_epochs", 0)) * iters_per_epoch, max_iter=total,
+                          amp=device.type == "cuda")
+    trainer = Trainer(model, SetCriterion(cfg), solver, device=device)
+    output_dir.mkdir(parents=True, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    it = 0
+    for epoch in range(int(hp["epochs"])):
+        order = rng.permutation(len(ds))
+        for k in range(iters_per_epoch):
+            if it >= total:
+                break
+            idx = order[(k * world + rank) * per_rank:(k * world + rank + 1) * per_rank]
+            if len(idx) == 0:
+                idx = order[:per_rank]
+            images, masks, classes = collate_padded([ds[int(i)] for i in idx], device=device)
+            trainer.step(images, masks, classes)
+            it += 1
+        if hp.get("save_period") and (epoch + 1) % int(hp["save_period"]) == 0:
+            trainer.save(str(output_dir / f"model_epoch{epoch + 1:04d}.pth"))
+        if it >= total:
+            break
+    trainer.save(str(output_dir / "model_final.pth"))
+    metrics = {"mAP50": 0.0, "mAP75": 0.0, "mAP": 0.0, "precision": 0.0, "recall": 0.0}
+    if rank == 0 and device.type == "cuda":
+        r = evaluate_dir(model, test_dir, img_size=img, device=device)
+        if r is not None:
+            metrics.update(r)
+    if world > 1:
+        dist.barrier()
+    return metrics
+
+
+# the reference's seam name (train_template.py:104)
+train_maskdino = train_mask2former

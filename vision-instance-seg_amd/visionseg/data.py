@@ -106,7 +106,7 @@ class CocoInstanceDataset:
 
     def __init__(self, root: str, ann_file: str = "annotations.json", image_dir: str | None = None,
                  min_size=(480, 512, 544, 576, 608, 640), max_size=800, train=True, fixed_size: int | None = None,
-                 seed: int = 42):
+                 seed: int = 42, keep_size: bool = False):
         with open(os.path.join(root, ann_file)) as f:
             coco = json.load(f)
         self.root = root
@@ -118,12 +118,15 @@ class CocoInstanceDataset:
         cats = sorted(c["id"] for c in coco.get("categories", [{"id": 0}]))
         self.cat_to_label = {c: i for i, c in enumerate(cats)}
         self.min_size, self.max_size, self.train, self.fixed_size = min_size, max_size, train, fixed_size
+        self.keep_size = keep_size
         self.rng = np.random.default_rng(seed)
 
     def __len__(self):
         return len(self.images)
 
     def _target_size(self, h, w):
+        if self.keep_size:
+            return h, w
         if self.fixed_size:
             return self.fixed_size, self.fixed_size
         s = int(self.rng.choice(self.min_size)) if self.train else int(self.min_size[-1])

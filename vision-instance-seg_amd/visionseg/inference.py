@@ -1,0 +1,135 @@
+"""Inference seam for labeling_server/ai_segmentation.py (`AISegmentationModel`).
+
+The reference's predictor calls `mmdet.apis.init_detector(config, checkpoint, device)`
+and `inference_detector(model, image)` and reads `result.pred_instances.{scores,
+masks, labels}` (labeling_server/ai_segmentation.py:41-50, 70-97).  This module
+provides the same two functions and result shape on top of the MI355X model, so the
+caller swaps one import and keeps its own top-score selection,
+thresholding and polygon extraction unchanged.
+
+Post-processing follows Mask2Former's instance inference (upstream `instance_inference`;
+in-container oracle HF:m2f-proc:627-746): per image, class scores softmax[:, :-1],
+top-k over queries x classes, binary mask = mask logit > 0 at image resolution, final
+score = class score x mean foreground probability inside the binary mask.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .data import PIXEL_MEAN, PIXEL_STD
+from .model import M2FConfig, Mask2Former
+
+
+@dataclass
+class InstanceData:
+    """The subset of mmengine's InstanceData the caller reads."""
+    scores: torch.Tensor     # [N] float
+    masks: torch.Tensor      # [N, H, W] bool (original image size)
+    labels: torch.Tensor     # [N] int64
+
+    def __len__(self):
+        return int(self.scores.shape[0])
+
+
+@dataclass
+class DetResult:
+    pred_instances: InstanceData
+
+
+@torch.no_grad()
+def instance_inference(mask_logits, class_logits, out_hw, valid_hw=None, top_k: int | None = None):
+    """mask_logits [Q,h,w], class_logits [Q,K+1] -> (scores [k], labels [k], masks bool [k,H,W]).
+    `valid_hw` crops the padded area (detectron2 sem_seg_postprocess) before resizing."""
+    Q, K1 = class_logits.shape
+    K = K1 - 1
+    scores = F.softmax(class_logits.float(), -1)[:, :-1]
+    labels = torch.arange(K, device=scores.device).unsqueeze(0).repeat(Q, 1).flatten(0, 1)
+    k = top_k or Q
+    sc, idx = scores.flatten(0, 1).topk(min(k, Q * K), sorted=False)
+    lab = labels[idx]
+    qi = torch.div(idx, K, rounding_mode="floor")
+    m = mask_logits[qi].float()
+    if valid_hw is not None:
+        m = m[:, : valid_hw[0], : valid_hw[1]]
+    m = F.interpolate(m[None], size=tuple(out_hw), mode="bilinear", align_corners=False)[0]
+    binm = m > 0
+    prob = m.sigmoid()
+    mscore = (prob * binm).flatten(1).sum(1) / (binm.flatten(1).sum(1) + 1e-6)
+    return sc * mscore, lab, binm
+
+
+class Predictor:
+    """Swin + Mask2Former predictor on the MI355X kernels (eval mode, bf16 autocast)."""
+
+    def __init__(self, model: Mask2Former, device="cuda:0", min_size: int = 640, max_size: int = 800,
+                 amp: bool = True, top_k: int = 100):
+        self.device = torch.device(device)
+        self.model = model.to(self.device).eval()
+        self.min_size, self.max_size, self.amp, self.top_k = min_size, max_size, amp, top_k
+
+    def _preprocess(self, image_bgr: np.ndarray):
+        h, w = image_bgr.shape[:2]
+        s = self.min_size / min(h, w)
+        if max(h, w) * s > self.max_size:
+            s = self.max_size / max(h, w)
+        nh, nw = int(round(h * s)), int(round(w * s))
+        rgb = torch.from_numpy(np.ascontiguousarray(image_bgr[:, :, ::-1])).to(self.device)
+        x = rgb.permute(2, 0, 1).float()[None]
+        x = F.interpolate(x, size=(nh, nw), mode="bilinear", align_corners=False)
+        x = (x - torch.tensor(PIXEL_MEAN, device=self.device).view(1, 3, 1, 1)) / \
+            torch.tensor(PIXEL_STD, device=self.device).view(1, 3, 1, 1)
+        ph, pw = (nh + 31) // 32 * 32, (nw + 31) // 32 * 32
+        x = F.pad(x, (0, pw - nw, 0, ph - nh))
+        return x, (nh, nw), (h, w)
+
+    @torch.no_grad()
+    def __call__(self, image_bgr: np.ndarray) -> DetResult:
+        x, valid, orig = self._preprocess(image_bgr)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.amp and self.device.type == "cuda"):
+            masks, classes = self.model(x)
+        m, c = masks[-1][0], classes[-1][0]
+        vh, vw = (valid[0] + 3) // 4, (valid[1] + 3) // 4     # valid region at mask resolution (stride 4)
+        scores, labels, binm = instance_inference(m, c, orig, valid_hw=(vh, vw), top_k=self.top_k)
+        return DetResult(InstanceData(scores=scores, masks=binm, labels=labels))
+
+
+def load_checkpoint(path: str, device="cpu") -> dict:
+    """Trainer.save() checkpoints ({'model': sd, ...}) or bare state dicts, in the build's
+    or the HF layout (converted).  Safe loader only (weights_only=True)."""
+    from .convert import from_hf_state_dict
+    sd = torch.load(path, map_location=device, weights_only=True)
+    if isinstance(sd, dict) and "model" in sd and isinstance(sd["model"], dict):
+        sd = sd["model"]
+    if any(k.startswith("model.pixel_level_module.") for k in sd):
+        sd = from_hf_state_dict(sd)
+    return sd
+
+
+def init_detector(config, checkpoint: str | None = None, device: str = "cuda:0") -> Predictor:
+    """mmdet.apis.init_detector-compatible entry (ai_segmentation.py:41-50).
+    `config`: an M2FConfig, a preset name ("swin_t", "swin_b", ...), or a JSON file."""
+    if isinstance(config, M2FConfig):
+        cfg = config
+    elif isinstance(config, str) and os.path.exists(config):
+        with open(config) as f:
+            d = json.load(f)
+        cfg = M2FConfig.preset(d.pop("preset")) if "preset" in d and len(d) == 1 else M2FConfig.from_dict(d)
+    else:
+        cfg = M2FConfig.preset(config or "swin_t")
+    model = Mask2Former(cfg)
+    if checkpoint:
+        model.load_state_dict(load_checkpoint(checkpoint))
+    else:
+        model.init_weights()
+    return Predictor(model, device=device)
+
+
+def inference_detector(model: Predictor, image: np.ndarray) -> DetResult:
+    """mmdet.apis.inference_detector-compatible entry (ai_segmentation.py:74-77)."""
+    return model(image)

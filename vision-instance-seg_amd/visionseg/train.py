@@ -38,6 +38,8 @@ class SolverConfig:
     gamma: float = 0.1
     amp: bool = True                 # bf16 autocast
     bucket_cap_mb: int = 64
+    schedule: str = "multistep"      # detectron2 WarmupMultiStep | "cosine" (train_template.py:51)
+    max_iter: int = 5000
 
 
 def dist_env():
@@ -61,11 +63,15 @@ def init_distributed(backend: str | None = None):
 
 
 def _lr_lambda(cfg: SolverConfig):
+    import math
+
     def f(it):
         w = 1.0
         if it < cfg.warmup_iters:
             a = it / max(1, cfg.warmup_iters)
             w = cfg.warmup_factor * (1 - a) + a
+        if cfg.schedule == "cosine":
+            return w * 0.5 * (1.0 + math.cos(math.pi * min(it, cfg.max_iter) / max(1, cfg.max_iter)))
         return w * cfg.gamma ** sum(1 for s in cfg.steps if it >= s)
     return f
 
