@@ -55,7 +55,7 @@ def _worker(rank, world, port, data, out_q):
     # criterion num_masks is the global mean over ranks (upstream SetCriterion semantics)
     crit = SetCriterion(M2FConfig(num_queries=5))
     n = crit._num_masks([torch.zeros(rank + 1)], torch.device("cpu"))
-    out_q.put((rank, flat, float(n)))
+    out_q.put((rank, flat.numpy().copy(), float(n)))   # by value: no shared-memory tensor handles
     dist.barrier()
     dist.destroy_process_group()
 
@@ -71,11 +71,12 @@ def test_ddp_matches_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, data, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in range(world)])
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     (_, f0, n0), (_, f1, n1) = res
+    f0, f1 = torch.from_numpy(f0), torch.from_numpy(f1)
     assert torch.equal(f0, f1), "replicas diverged"
     assert n0 == n1 == pytest.approx(1.5)
     # single process, global batch of 2: mean-reduced loss over per-image terms = DDP average
