@@ -388,6 +388,9 @@ class RefDecoder(nn.Module):
         e = F.relu(self.mask_embed[1](e))
         e = self.mask_embed[2](e)
         logits, blocked = R.mask_head_ref(e, mask_features, target_hw)
+        if getattr(self, "record", False):     # test hook: the decisions and what they were made on
+            am = F.interpolate(logits, size=target_hw, mode="bilinear", align_corners=False).flatten(2)
+            self.trace.append((R.unblock_full_rows(blocked), am))
         return x, logits, blocked
 
     def forward(self, ms_feats, mask_features):
@@ -401,6 +404,7 @@ class RefDecoder(nn.Module):
             mems.append((f.flatten(2) + self.level_embed.weight[i][None, :, None]).transpose(1, 2))
         qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
         h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
+        self.trace = []
         inter, logits, blocked = self.predict(h, mask_features, sizes[0])
         inters, masks = [inter], [logits]
         for idx, layer in enumerate(self.layers):
@@ -472,7 +476,9 @@ class RefCriterion:
         self.empty_weight = torch.ones(cfg.num_labels + 1)
         self.empty_weight[-1] = cfg.no_object_weight
 
+    @torch.no_grad()
     def match(self, masks, classes, mask_labels, class_labels):
+        """HF:m2f:413-481 (no_grad, as HF)."""
         from scipy.optimize import linear_sum_assignment
         c = self.cfg
         out = []

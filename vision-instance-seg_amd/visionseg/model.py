@@ -385,6 +385,11 @@ class Decoder(nn.Module):
         self.layers = nn.ModuleList([DecoderLayer(d, cfg.dec_ffn, cfg.dec_heads) for _ in range(cfg.dec_layers - 1)])
         self.norm = nn.LayerNorm(d)
         self.mask_embed = nn.ModuleList([nn.Linear(d, d), nn.Linear(d, d), nn.Linear(d, cfg.mask_feature_size)])
+        # Parity-test hook ("teacher forcing"): a list of bool [B,Q,h*w] blocked masks, one per
+        # decoder layer, used instead of the masks this decoder derives itself.  Lets a test
+        # separate threshold-decision flips (sigmoid(x) < 0.5 at |x| ~ rounding) from arithmetic.
+        self.mask_override = None
+        self.record = False
 
     def predict(self, h, mf_nhwc, Hm, Wm, target_hw):
         x = self.norm(h)
@@ -412,14 +417,29 @@ class Decoder(nn.Module):
         n = len(self.layers)
         inter, logits, words = self.predict(h, mf, Hm, Wm, sizes[0] if n else None)
         inters, masks = [inter], [logits]
+        self.trace = []
         for idx, layer in enumerate(self.layers):
             lvl = idx % 3
+            if self.record:
+                self.trace.append(words)
+            if self.mask_override is not None:
+                words = pack_bitmask(self.mask_override[idx].to(dev))
             h = layer(h, qpos, mems[lvl], mposs[lvl], words)
             nxt = sizes[(idx + 1) % 3] if idx + 1 < n else None
             inter, logits, words = self.predict(h, mf, Hm, Wm, nxt)
             inters.append(inter)
             masks.append(logits)
         return inters, masks
+
+
+def pack_bitmask(blocked: torch.Tensor) -> torch.Tensor:
+    """bool [B,Q,K] (True = blocked) -> int32 words [B,Q,ceil(K/32)] in the kernels' format."""
+    B, Q, K = blocked.shape
+    nw = (K + 31) // 32
+    pad = torch.zeros(B, Q, nw * 32, dtype=torch.int64, device=blocked.device)
+    pad[..., :K] = blocked.to(torch.int64)
+    bits = (pad.view(B, Q, nw, 32) << torch.arange(32, device=blocked.device)).sum(-1)
+    return torch.where(bits >= 2 ** 31, bits - 2 ** 32, bits).to(torch.int32)
 
 
 class Mask2Former(nn.Module):
@@ -480,3 +500,10 @@ class Mask2Former(nn.Module):
             elif isinstance(m, WindowAttention):
                 m.rel_table.zero_()
         return self
+
+
+def unpack_bitmask_like(words: torch.Tensor, n_keys: int) -> torch.Tensor:
+    """int32 words [B,Q,nw] -> bool [B,Q,n_keys] (True = blocked)."""
+    w = words.to(torch.int64) & 0xFFFFFFFF
+    bits = (w.unsqueeze(-1) >> torch.arange(32, device=w.device)) & 1
+    return bits.flatten(-2)[..., :n_keys].bool()
