@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=2)
     ap.add_argument("--kernel-timing", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "amp"],
+                    help="bf16: bf16 params/activations + f32 master weights; amp: f32 params + bf16 autocast")
     ap.add_argument("--gemm-tuning", default="file", choices=["file", "tune", "off"],
                     help="vendor GEMM solution table: in-tree TunableOp file (default), re-tune, or heuristics")
     return ap.parse_args()
@@ -143,7 +145,7 @@ def main():
     dev = torch.device("cuda", local)
     cfg = M2FConfig.preset(a.model, num_queries=a.queries)
     model = Mask2Former(cfg).init_weights(seed=0)
-    trainer = Trainer(model, SetCriterion(cfg), SolverConfig(), device=dev)
+    trainer = Trainer(model, SetCriterion(cfg), SolverConfig(precision=a.precision), device=dev)
     images, ml, cl = synthetic_batch(a.batch, a.size, seed=42 + rank, device=dev)
     torch.cuda.synchronize()
 
@@ -187,6 +189,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "final_loss": round(float(loss.item()), 4),
             "gemm_tuning": a.gemm_tuning,
+            "precision": a.precision,
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels": table,

@@ -302,11 +302,11 @@ class PixelDecoder(nn.Module):
         for lvl, x in enumerate(feats[::-1][:3]):
             e = self.input_proj[lvl](x)
             embeds.append(e)
-            pos.append(sine_pos_embed(x.shape[0], x.shape[2], x.shape[3], Fd // 2, dev))
+            pos.append(sine_pos_embed(x.shape[0], x.shape[2], x.shape[3], Fd // 2, dev).to(e.dtype))
         shapes = [(int(e.shape[2]), int(e.shape[3])) for e in embeds]
         B = embeds[0].shape[0]
         h = torch.cat([e.flatten(2).transpose(1, 2) for e in embeds], 1)
-        p = torch.cat([q.flatten(2).transpose(1, 2) + self.level_embed[i].view(1, 1, -1)
+        p = torch.cat([q.flatten(2).transpose(1, 2) + self.level_embed[i].view(1, 1, -1).to(q.dtype)
                        for i, q in enumerate(pos)], 1)
         ref = reference_points(shapes, B, dev)
         norm = torch.tensor([[w, hh] for hh, w in shapes], device=dev, dtype=torch.float32)[None, None, None, :, None, :]
@@ -410,8 +410,8 @@ class Decoder(nn.Module):
         for i in range(3):
             f = ms_feats[i]
             sizes.append((int(f.shape[2]), int(f.shape[3])))
-            mposs.append(sine_pos_embed(B, f.shape[2], f.shape[3], d // 2, dev).flatten(2).transpose(1, 2))
-            mems.append((f.flatten(2) + self.level_embed.weight[i][None, :, None]).transpose(1, 2))
+            mposs.append(sine_pos_embed(B, f.shape[2], f.shape[3], d // 2, dev).to(f.dtype).flatten(2).transpose(1, 2))
+            mems.append((f.flatten(2) + self.level_embed.weight[i][None, :, None].to(f.dtype)).transpose(1, 2))
         qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
         h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
         n = len(self.layers)
@@ -456,7 +456,8 @@ class Mask2Former(nn.Module):
         self.class_head = nn.Linear(cfg.hidden_dim, cfg.num_labels + 1)
 
     def forward(self, pixel_values):
-        feats = self.backbone(pixel_values)
+        # pure-bf16 mode (bf16 parameters): feed the backbone in the parameter dtype
+        feats = self.backbone(pixel_values.to(self.backbone.patch_embed.proj.weight.dtype))
         mask_features, ms = self.pixel_decoder(feats)
         inters, masks = self.decoder(ms, mask_features)
         classes = [self.class_head(x) for x in inters]

@@ -36,7 +36,9 @@ class SolverConfig:
     warmup_factor: float = 0.001     # detectron2 SOLVER.WARMUP_FACTOR, linear warmup
     steps: tuple = (3500, 4500)
     gamma: float = 0.1
-    amp: bool = True                 # bf16 autocast
+    amp: bool = True                 # bf16 compute on a cuda device (see `precision`)
+    precision: str = "bf16"          # "bf16": bf16 params/activations + f32 master weights in the
+                                     # optimizer; "amp": f32 params + bf16 autocast; "fp32"
     bucket_cap_mb: int = 64
     schedule: str = "multistep"      # detectron2 WarmupMultiStep | "cosine" (train_template.py:51)
     max_iter: int = 5000
@@ -87,6 +89,12 @@ class Trainer:
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
         self.model = model.to(self.device)
         self.criterion = criterion
+        s = self.solver
+        self.mode = "fp32"
+        if s.amp and self.device.type == "cuda":
+            self.mode = s.precision
+        if self.mode == "bf16":
+            self.model.to(torch.bfloat16)
         if distributed is None:
             distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self.distributed = distributed
@@ -98,9 +106,14 @@ class Trainer:
         else:
             self.net = self.model
         params = [p for p in self.model.parameters() if p.requires_grad]
-        self.params = params
+        self.model_params = params
+        if self.mode == "bf16":
+            # f32 master copy owned by the optimiser; the model keeps bf16 working weights
+            self.params = [p.detach().float().clone() for p in params]
+        else:
+            self.params = params
         fused = self.device.type == "cuda"
-        self.opt = torch.optim.AdamW(params, lr=self.solver.lr, betas=self.solver.betas,
+        self.opt = torch.optim.AdamW(self.params, lr=self.solver.lr, betas=self.solver.betas,
                                      weight_decay=self.solver.weight_decay, fused=fused, foreach=None if fused else True)
         self.sched = torch.optim.lr_scheduler.LambdaLR(self.opt, _lr_lambda(self.solver))
         self.iter = 0
@@ -120,8 +133,7 @@ class Trainer:
         torch._foreach_mul_(grads, scales)
 
     def forward_loss(self, images, mask_labels, class_labels):
-        use_amp = self.solver.amp and self.device.type == "cuda"
-        with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=use_amp):
+        with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.mode == "amp"):
             masks, classes = self.net(images)
         masks = [m.float() for m in masks]
         classes = [c.float() for c in classes]
@@ -130,16 +142,32 @@ class Trainer:
     def step(self, images, mask_labels, class_labels):
         """One optimisation step; returns the (device) loss tensor, no host sync."""
         self.opt.zero_grad(set_to_none=True)
+        for p in self.model_params:
+            p.grad = None
         loss, _ = self.forward_loss(images, mask_labels, class_labels)
         loss.backward()
+        if self.mode == "bf16":
+            # (DDP has already averaged the bf16 grads) -> f32 master grads
+            grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.model_params]
+            for m, g in zip(self.params, grads):
+                m.grad = g.float()
         self.clip_gradients()
         self.opt.step()
+        if self.mode == "bf16":
+            with torch.no_grad():
+                torch._foreach_copy_(self.model_params, self.params)
         self.sched.step()
         self.iter += 1
         return loss.detach()
 
     def state_dict(self):
-        return {"model": self.model.state_dict(), "optimizer": self.opt.state_dict(),
+        if self.mode == "bf16":   # checkpoint the f32 master weights under the model's names
+            names = [n for n, p in self.model.named_parameters() if p.requires_grad]
+            sd = {k: v.float() for k, v in self.model.state_dict().items()}
+            sd.update({n: m.detach().clone() for n, m in zip(names, self.params)})
+        else:
+            sd = self.model.state_dict()
+        return {"model": sd, "optimizer": self.opt.state_dict(),
                 "scheduler": self.sched.state_dict(), "iter": self.iter}
 
     def save(self, path):
@@ -150,6 +178,11 @@ class Trainer:
     def load(self, path):
         sd = torch.load(path, map_location=self.device, weights_only=True)
         self.model.load_state_dict(sd["model"])
+        if self.mode == "bf16":
+            names = [n for n, p in self.model.named_parameters() if p.requires_grad]
+            with torch.no_grad():
+                for n, m in zip(names, self.params):
+                    m.copy_(sd["model"][n])
         self.opt.load_state_dict(sd["optimizer"])
         self.sched.load_state_dict(sd["scheduler"])
         self.iter = int(sd["iter"])
