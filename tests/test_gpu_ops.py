@@ -379,3 +379,64 @@ def test_msda_encoder_backward_vs_oracle(cfg, dtype):
     out2.backward(go.to(dtype).to(DEV))
     d = (vd2.grad.float() - vd.grad.float()).abs().max().item()
     assert d <= (1e-5 if dtype == torch.float32 else 2 ** -7 * float(vd.grad.float().abs().max())), d
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("K", [40000, 70756])
+def test_token_linear_split_k_grads(dtype, K):
+    """Split-K weight gradient (visionseg.linear) vs an f64 reference of dY^T X; the
+    K remainder (K not a multiple of the chunk) is covered by 70756 = 69*1025 + 1031."""
+    from visionseg.linear import TokenLinear, split_count
+    g = torch.Generator(device="cuda").manual_seed(0)
+    lin = TokenLinear(192, 576).to(DEV, dtype)
+    x = torch.randn(2, K // 2, 192, device=DEV, generator=g).to(dtype).requires_grad_(True)
+    gy = torch.randn(2, K // 2, 576, device=DEV, generator=g).to(dtype)
+    assert split_count(K, 576, 192) > 1
+    y = lin(x)
+    np.testing.assert_array_equal(y.detach().float().cpu(), torch.nn.functional.linear(x, lin.weight, lin.bias).detach().float().cpu())
+    y.backward(gy)
+    x2, gy2 = x.detach().double().reshape(-1, 192), gy.double().reshape(-1, 576)
+    ew, eb, ex = gy2.t() @ x2, gy2.sum(0), gy2 @ lin.weight.detach().double()
+    tol = 1e-5 if dtype == torch.float32 else 8e-3
+    for got, exp in ((lin.weight.grad, ew), (lin.bias.grad, eb), (x.grad.reshape(-1, 192), ex)):
+        rel = float((got.double() - exp).abs().max() / exp.abs().max())
+        assert rel <= tol, rel
+
+
+def _encoder_like_inputs(B, shapes, H, P, seed, jitter):
+    """Queries = every pixel of every level (encoder self-attention), sampling points =
+    reference point + a smooth per-head offset field + `jitter` (pixels) of noise."""
+    g = torch.Generator().manual_seed(seed)
+    S = sum(h * w for h, w in shapes)
+    L = len(shapes)
+    ref = R.reference_points(shapes, B)                                 # [B,S,L,2]
+    base = torch.randn(1, 1, H, L, P, 2, generator=g) * 2.0             # pixels, shared by all queries
+    ramp = torch.linspace(0, 1.5, S)[None, :, None, None, None, None]   # slow drift along the query order
+    off = base + ramp * torch.randn(1, 1, H, L, P, 2, generator=g) + jitter * torch.randn(B, S, H, L, P, 2, generator=g)
+    norm = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32)[None, None, None, :, None, :]
+    loc = ref[:, :, None, :, None, :] + off / norm
+    value = torch.randn(B, S, H, 32, generator=g)
+    w = torch.softmax(torch.randn(B, S, H, L * P, generator=g), -1).view(B, S, H, L, P)
+    return value, loc, w
+
+
+@pytest.mark.parametrize("run", ["32", "7", "0"])
+@pytest.mark.parametrize("jitter", [0.0, 0.3, 3.0])
+def test_msda_carry_backward_vs_oracle(monkeypatch, run, jitter):
+    """Register-carry grad_value (csrc/msda.hip msda_bwd_carry_kernel) on encoder-shaped
+    queries, runs of 32 / 7 (ragged) queries and the plain kernel (0), vs the oracle."""
+    monkeypatch.setenv("VS_MSDA_RUN", run)
+    ops = _ops()
+    shapes = [(8, 8), (16, 16), (32, 32)]
+    value, loc, w = _encoder_like_inputs(2, shapes, 4, 4, seed=11, jitter=jitter)
+    vr, lr, wr = (t.clone().requires_grad_(True) for t in (value, loc, w))
+    ref = R.msda_ref(vr, shapes, lr, wr)
+    go = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3))
+    ref.backward(go)
+    vd, ld, wd = (t.to(DEV).requires_grad_(True) for t in (value, loc, w))
+    out = ops.ms_deform_attn(vd, shapes, ld, wd)
+    out.backward(go.to(DEV))
+    np.testing.assert_allclose(vd.grad.cpu().numpy(), vr.grad.numpy(), atol=2e-5, rtol=0)
+    np.testing.assert_allclose(wd.grad.cpu().numpy(), wr.grad.numpy(), atol=2e-5, rtol=0)
+    gl = lr.grad.numpy()
+    np.testing.assert_allclose(ld.grad.cpu().numpy(), gl, atol=2e-5 * max(1.0, np.abs(gl).max()), rtol=0)

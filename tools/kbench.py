@@ -53,17 +53,26 @@ def main():
         xs = [torch.linspace(0.5, w - 0.5, w, device=dev) / w for h, w in shapes]
         ref = torch.cat([torch.stack(torch.meshgrid(x, y, indexing="xy"), -1).reshape(-1, 2) for x, y in zip(xs, ys)])
         norm = torch.tensor([[w, h] for h, w in shapes], device=dev, dtype=torch.float32)
-        off = (torch.rand(B, S, H, L, P, 2, device=dev, generator=g) * 2 - 1) * 4
-        loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
         w = torch.softmax(torch.randn(B, S, H, L * P, device=dev, generator=g), -1).view(B, S, H, L, P)
         v = torch.randn(B, S, H, 32, device=dev, generator=g).to(bf).requires_grad_(True)
         go = torch.randn(B, S, H * 32, device=dev, generator=g).to(bf)
-        locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
-        for enc in (True, False):
-            def fb(enc=enc):
-                o = ops.ms_deform_attn(v, shapes, locr, wr, encoder=enc)
-                o.backward(go)
-            run(f"msda encoder={enc}", fb, a.iters)
+        # offsets (pixels of the sampled level): iid uniform +-4 px per query (worst case for
+        # the register carry) and a smooth field (per-head pattern + 0.3 px jitter), which is
+        # what the encoder's Linear(query) offsets look like between neighbouring pixels
+        offs = {"iid4px": (torch.rand(B, S, H, L, P, 2, device=dev, generator=g) * 2 - 1) * 4,
+                "smooth": (torch.randn(1, 1, H, L, P, 2, device=dev, generator=g) * 2
+                           + 0.3 * torch.randn(B, S, H, L, P, 2, device=dev, generator=g))}
+        for oname, off in offs.items():
+            loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
+            locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
+            for mode in ("carry32", "carry16", "carry8", "plain", "band"):
+                os.environ["VS_MSDA_RUN"] = {"carry32": "32", "carry16": "16", "carry8": "8"}.get(mode, "0")
+
+                def fb(enc=mode == "band"):
+                    o = ops.ms_deform_attn(v, shapes, locr, wr, encoder=enc)
+                    o.backward(go)
+                run(f"msda {oname} {mode}", fb, a.iters)
+            os.environ.pop("VS_MSDA_RUN")
     if "mask" in a.only:
         Q, C, Hm = 100, 256, 256
         E = torch.randn(B, Q, C, device=dev, generator=g).to(bf).requires_grad_(True)

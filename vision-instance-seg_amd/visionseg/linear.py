@@ -1,0 +1,80 @@
+"""Token-major Linear with a split-K weight gradient.
+
+The backbone and pixel-decoder Linears see tens to hundreds of thousands of tokens
+(Swin-T stage 1 at 1024^2, batch 4: K = 268k) but only a few hundred output features,
+so the weight gradient dW[out,in] = dY^T X is a tall-K GEMM whose M x N is a handful
+of macro-tiles: one launch of the library kernel fills ~10 of the 256 CUs.  Here the
+K (token) axis is cut into S chunks and run as one batched GEMM with f32 outputs
+[S, out, in] (every CU busy), then reduced over S in f32 and rounded once.  Forward and
+dX are the plain library GEMMs.  Parameter names are nn.Linear's, so checkpoints and
+visionseg.convert are unaffected.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+# split when K is at least this many tokens; chunks never drop below MIN_CHUNK rows
+MIN_TOKENS = 32768
+MIN_CHUNK = 1024
+TARGET_TILES = 768          # aim for this many 128x128 output tiles over all chunks
+
+
+def split_count(K: int, M: int, N: int) -> int:
+    tiles = max(1, -(-M // 128) * -(-N // 128))
+    s = max(1, TARGET_TILES // tiles)
+    return max(1, min(s, K // MIN_CHUNK))
+
+
+def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+    """dW = gy^T x for gy [K, M], x [K, N] -> [M, N] (out_dtype), f32 accumulation."""
+    K, M = gy.shape
+    N = x.shape[1]
+    S = split_count(K, M, N)
+    if S <= 1:
+        return (gy.t() @ x).to(out_dtype)
+    chunk = K // S
+    main = chunk * S
+    part = torch.bmm(gy[:main].view(S, chunk, M).transpose(1, 2), x[:main].view(S, chunk, N),
+                     out_dtype=torch.float32)
+    acc = part.sum(0)
+    if main < K:
+        acc += torch.mm(gy[main:].t(), x[main:], out_dtype=torch.float32)
+    return acc.to(out_dtype)
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy2 = gy.reshape(-1, gy.shape[-1])
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = (gy2 @ weight.to(gy2.dtype)).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            gw = weight_grad(gy2, x.reshape(-1, x.shape[-1]).to(gy2.dtype), weight.dtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy2.sum(0, dtype=torch.float32).to(weight.dtype)
+        return gx, gw, gb
+
+
+class TokenLinear(nn.Linear):
+    """nn.Linear whose backward splits the token axis of dW (see module docstring)."""
+
+    def forward(self, x):
+        tokens = x.numel() // max(1, x.shape[-1])
+        if not (x.is_cuda and torch.is_grad_enabled() and self.weight.requires_grad and tokens >= MIN_TOKENS):
+            return F.linear(x, self.weight, self.bias)
+        w, b = self.weight, self.bias
+        if torch.is_autocast_enabled():
+            dt = torch.get_autocast_dtype("cuda")
+            with torch.autocast("cuda", enabled=False):
+                return _LinearFn.apply(x.to(dt), w.to(dt), None if b is None else b.to(dt))
+        return _LinearFn.apply(x, w, b)

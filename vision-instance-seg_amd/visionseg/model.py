@@ -27,6 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from .linear import TokenLinear
 
 
 @dataclass
@@ -102,16 +103,16 @@ class WindowAttention(nn.Module):
         if dim != heads * 32:
             raise ValueError("the window-attention kernel needs head_dim == 32")
         self.heads, self.ws = heads, ws
-        self.qkv = nn.Linear(dim, 3 * dim)
-        self.proj = nn.Linear(dim, dim)
+        self.qkv = TokenLinear(dim, 3 * dim)
+        self.proj = TokenLinear(dim, dim)
         self.rel_table = nn.Parameter(torch.zeros((2 * ws - 1) ** 2, heads))
 
 
 class Mlp(nn.Module):
     def __init__(self, dim, hidden):
         super().__init__()
-        self.fc1 = nn.Linear(dim, hidden)
-        self.fc2 = nn.Linear(hidden, dim)
+        self.fc1 = TokenLinear(dim, hidden)
+        self.fc2 = TokenLinear(hidden, dim)
 
     def forward(self, x):
         return self.fc2(F.gelu(self.fc1(x)))
@@ -144,7 +145,7 @@ class PatchMerging(nn.Module):
     def __init__(self, dim):
         super().__init__()
         self.norm = nn.LayerNorm(4 * dim)
-        self.reduction = nn.Linear(4 * dim, 2 * dim, bias=False)
+        self.reduction = TokenLinear(4 * dim, 2 * dim, bias=False)
 
     def forward(self, x, H, W):
         B, L, C = x.shape
@@ -241,10 +242,10 @@ class MSDeformAttn(nn.Module):
         super().__init__()
         self.d, self.heads, self.levels, self.points = d, heads, levels, points
         self.band_backward = False   # opt-in destination-band grad_value (see csrc/msda.hip)
-        self.sampling_offsets = nn.Linear(d, heads * levels * points * 2)
-        self.attention_weights = nn.Linear(d, heads * levels * points)
-        self.value_proj = nn.Linear(d, d)
-        self.output_proj = nn.Linear(d, d)
+        self.sampling_offsets = TokenLinear(d, heads * levels * points * 2)
+        self.attention_weights = TokenLinear(d, heads * levels * points)
+        self.value_proj = TokenLinear(d, d)
+        self.output_proj = TokenLinear(d, d)
 
     def forward(self, h, pos, ref, shapes, norm):
         B, S, _ = h.shape
@@ -263,8 +264,8 @@ class EncoderLayer(nn.Module):
         super().__init__()
         self.attn = MSDeformAttn(d, heads, levels, points)
         self.norm1 = nn.LayerNorm(d)
-        self.fc1 = nn.Linear(d, ffn)
-        self.fc2 = nn.Linear(ffn, d)
+        self.fc1 = TokenLinear(d, ffn)
+        self.fc2 = TokenLinear(ffn, d)
         self.norm2 = nn.LayerNorm(d)
 
     def forward(self, h, pos, ref, shapes, norm):

@@ -128,9 +128,10 @@ class Trainer:
             torch.nn.utils.clip_grad_norm_(self.params, s.clip_value)
             return
         # detectron2 "norm": clip_grad_norm_(p, clip_value) for every parameter, fused
-        norms = torch._foreach_norm(grads)
-        scales = [torch.clamp(s.clip_value / (n + 1e-6), max=1.0) for n in norms]
-        torch._foreach_mul_(grads, scales)
+        # (one stacked scale vector: a handful of launches instead of several per parameter)
+        norms = torch.stack(torch._foreach_norm(grads))
+        scales = (s.clip_value / (norms + 1e-6)).clamp_(max=1.0)
+        torch._foreach_mul_(grads, list(scales.unbind(0)))
 
     def forward_loss(self, images, mask_labels, class_labels):
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.mode == "amp"):
@@ -141,16 +142,20 @@ class Trainer:
 
     def step(self, images, mask_labels, class_labels):
         """One optimisation step; returns the (device) loss tensor, no host sync."""
-        self.opt.zero_grad(set_to_none=True)
+        if self.mode != "bf16":
+            self.opt.zero_grad(set_to_none=True)
         for p in self.model_params:
             p.grad = None
         loss, _ = self.forward_loss(images, mask_labels, class_labels)
         loss.backward()
         if self.mode == "bf16":
-            # (DDP has already averaged the bf16 grads) -> f32 master grads
+            # (DDP has already averaged the bf16 grads) -> persistent f32 master grads, one
+            # multi-tensor cast-copy
+            if self.params[0].grad is None:
+                for m in self.params:
+                    m.grad = torch.empty_like(m)
             grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.model_params]
-            for m, g in zip(self.params, grads):
-                m.grad = g.float()
+            torch._foreach_copy_([m.grad for m in self.params], grads)
         self.clip_gradients()
         self.opt.step()
         if self.mode == "bf16":
