@@ -172,6 +172,26 @@ VS_API int vs_masked_attn_backward(int dtype, const void* q, const void* k, cons
                                    void* workspace, int batch, int num_query, int num_keys,
                                    int heads, float scale, void* stream);
 
+/* ---- Token-major LayerNorm and column sums (csrc/norm.hip) --------------------------
+ * Replaces torch.nn.LayerNorm on the Swin blocks / patch merging / out-norms
+ * (HF modeling_swin SwinLayer.layernorm_before/after, SwinPatchMerging.norm; reference
+ * training/maskdino/train_full.py:166-175 builds that backbone) and the pixel-decoder
+ * encoder norms (HF:m2f Mask2FormerPixelDecoderEncoderLayer.self_attn_layer_norm /
+ * final_layer_norm), plus the bias gradient of their Linears.  Semantics of
+ * torch.nn.functional.layer_norm over the last dim.  x, w, b, y in `dtype`; mean / rstd
+ * f32 [M]; C a multiple of 8, <= 2048. */
+VS_API int vs_layer_norm_forward(int dtype, const void* x, const void* weight, const void* bias, void* y,
+                                 float* mean, float* rstd, int rows, int cols, float eps, void* stream);
+VS_API long long vs_layer_norm_backward_workspace_bytes(int rows, int cols);
+/* grad_y [M, C] -> grad_x [M, C], grad_weight / grad_bias [C] (dtype, overwritten). */
+VS_API int vs_layer_norm_backward(int dtype, const void* grad_y, const void* x, const void* weight,
+                                  const float* mean, const float* rstd, void* grad_x, void* grad_weight,
+                                  void* grad_bias, void* workspace, int rows, int cols, void* stream);
+VS_API long long vs_column_sum_workspace_bytes(int rows, int cols);
+/* out[n] = sum_m x[m, n] (f32 accumulation, fixed order); N a multiple of 8, <= 2048. */
+VS_API int vs_column_sum(int dtype, const void* x, void* out, void* workspace, int rows, int cols,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

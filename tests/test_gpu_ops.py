@@ -440,3 +440,41 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, jitter):
     np.testing.assert_allclose(wd.grad.cpu().numpy(), wr.grad.numpy(), atol=2e-5, rtol=0)
     gl = lr.grad.numpy()
     np.testing.assert_allclose(ld.grad.cpu().numpy(), gl, atol=2e-5 * max(1.0, np.abs(gl).max()), rtol=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,C", [(1, 96), (1000, 96), (4099, 192), (777, 256), (2048, 384), (513, 768), (65, 1536),
+                                 (33, 2048), (0, 96)])
+def test_layer_norm_vs_torch(dtype, M, C):
+    """HIP LayerNorm (csrc/norm.hip) forward + backward vs torch f64 on the same inputs."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(M * 7 + C)
+    x = (torch.randn(M, C, generator=g) * 3 + 0.5).to(dtype)
+    w = (1 + 0.1 * torch.randn(C, generator=g)).to(dtype)
+    b = (0.1 * torch.randn(C, generator=g)).to(dtype)
+    gy = torch.randn(M, C, generator=g).to(dtype)
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (C,), wr, br, 1e-5)
+    yr.backward(gy.double())
+    xd, wd, bd = (t.to(DEV).requires_grad_(True) for t in (x, w, b))
+    y = ops.layer_norm(xd, wd, bd, 1e-5)
+    assert y.dtype == dtype
+    y.backward(gy.to(DEV))
+    tol = 2e-5 if dtype == torch.float32 else 2 ** -7
+    for got, exp in ((y, yr), (xd.grad, xr.grad)):
+        err = (got.detach().double().cpu() - exp.detach()).abs()
+        assert float(err.max() if err.numel() else 0) <= tol * max(1.0, float(exp.detach().abs().max() if exp.numel() else 1))
+    for got, exp in ((wd.grad, wr.grad), (bd.grad, br.grad)):
+        err = float((got.double().cpu() - exp).abs().max())
+        assert err <= (1e-4 if dtype == torch.float32 else 2 ** -7) * max(1.0, float(exp.abs().max())), err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N", [(262144, 96), (86016, 256), (5, 384), (0, 64), (1023, 2048)])
+def test_column_sum_vs_torch(dtype, M, N):
+    ops = _ops()
+    x = torch.randn(M, N, generator=torch.Generator().manual_seed(N)).to(dtype)
+    exp = x.double().sum(0)
+    got = ops.column_sum(x.to(DEV)).double().cpu()
+    tol = 1e-5 if dtype == torch.float32 else 2 ** -8
+    assert float((got - exp).abs().max()) <= tol * max(1.0, float(exp.abs().max())) + 1e-3 * (M ** 0.5) * (dtype != torch.float32)

@@ -1,0 +1,399 @@
+// Token-major LayerNorm (forward + backward) and column sums (Linear bias gradients).
+//
+// Swin and the pixel-decoder encoder normalise [M, C] activations with M = 16k..270k
+// tokens and short rows (C = 96..768 for Swin-T).  PyTorch's kernels spend a workgroup
+// per row and run these far below the HBM roofline (10.8 ms of LayerNorm per C2 step for
+// < 1 GB of traffic).  Here a row belongs to a GROUP of G lanes (G = 4..64, a power of
+// two) and each lane owns K 16-byte chunks of the row, so a wave normalises 64/G rows
+// with 16-B loads/stores; statistics in f32 (two-pass in registers), one read and one
+// write per element.  Semantics: torch.nn.functional.layer_norm (biased variance,
+// y = (x - mean) * rsqrt(var + eps) * w + b).
+//
+// Backward: dx per row from the saved mean / rstd (xhat recomputed); dw / db are
+// accumulated per lane in registers over a grid-stride sweep of rows, reduced across the
+// workgroup's groups in LDS and written as one f32 partial row per workgroup, then
+// summed over workgroups by `colsum_partials_kernel` (deterministic, no atomics).
+//
+// Column sum (bias gradient of a token-major Linear, sum over M of dY [M, N]): same
+// partial-row scheme.
+#include "common.h"
+
+namespace vs {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxPartials = 512;    // workgroups of a backward / column-sum sweep
+
+// lanes of one group: shuffle-reduce within G lanes (G a power of two, <= 64)
+__device__ __forceinline__ float group_sum(float x, int G) {
+  for (int s = G >> 1; s >= 1; s >>= 1) x += __shfl_xor(x, s, G);
+  return x;
+}
+
+template <typename T>
+__device__ __forceinline__ void load_chunk(const T* p, float* out) {
+  Vec16<T>::load(p, out);
+  if constexpr (Vec16<T>::N == 4) Vec16<T>::load(p + 4, out + 4);
+}
+
+template <typename T>
+__device__ __forceinline__ void store_chunk(T* p, const float* v) {
+  Vec16<T>::store(p, v);
+  if constexpr (Vec16<T>::N == 4) Vec16<T>::store(p + 4, v + 4);
+}
+
+// chunk = 8 elements (one 16-B load for bf16, two for f32); C % 8 == 0
+template <typename T, int K>
+__global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                          const T* __restrict__ b, T* __restrict__ y,
+                                                          float* __restrict__ mean, float* __restrict__ rstd,
+                                                          int M, int C, float eps, int G) {
+  const int nch = C >> 3;
+  const int lane = threadIdx.x & (G - 1);
+  const int rows_per_block = kThreads / G;
+  const float invC = 1.f / (float)C;
+  for (long long row = (long long)blockIdx.x * rows_per_block + threadIdx.x / G; row < M;
+       row += (long long)gridDim.x * rows_per_block) {
+    const T* xr = x + row * C;
+    float v[K][8];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = lane + k * G;
+      if (j < nch) {
+        load_chunk(xr + j * 8, v[k]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += v[k][i];
+      }
+    }
+    const float mu = group_sum(s, G) * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = lane + k * G;
+      if (j < nch) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float d = v[k][i] - mu;
+          q += d * d;
+        }
+      }
+    }
+    const float rs = rsqrtf(group_sum(q, G) * invC + eps);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = lane + k * G;
+      if (j < nch) {
+        float wv[8], bv[8], o[8];
+        load_chunk(w + j * 8, wv);
+        load_chunk(b + j * 8, bv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mu) * rs * wv[i] + bv[i];
+        store_chunk(y + row * C + j * 8, o);
+      }
+    }
+    if (lane == 0) {
+      mean[row] = mu;
+      rstd[row] = rs;
+    }
+  }
+}
+
+// dx, plus per-workgroup partial dw / db rows (f32) in part[blockIdx][2][C]
+template <typename T, int K>
+__global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const T* __restrict__ w, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, T* __restrict__ dx,
+                                                          float* __restrict__ part, int M, int C, int G) {
+  extern __shared__ float red[];             // [groups][2][C]
+  const int nch = C >> 3;
+  const int lane = threadIdx.x & (G - 1);
+  const int grp = threadIdx.x / G;
+  const int rows_per_block = kThreads / G;
+  const float invC = 1.f / (float)C;
+  float dw[K][8], db[K][8], wv[K][8];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int j = lane + k * G;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dw[k][i] = db[k][i] = wv[k][i] = 0.f;   // masked chunks must hold 0, not garbage
+    if (j < nch) load_chunk(w + j * 8, wv[k]);
+  }
+  // U rows per iteration, all loads issued before the math (memory-level parallelism)
+  constexpr int U = K <= 2 ? 2 : 1;
+  const long long stride = (long long)gridDim.x * rows_per_block;
+  for (long long row0 = (long long)blockIdx.x * rows_per_block + grp; row0 < M; row0 += U * stride) {
+    float xv[U][K][8], dv[U][K][8], mu[U], rs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = row0 + u * stride;
+      const bool ok = row < M;
+      mu[u] = ok ? mean[row] : 0.f;
+      rs[u] = ok ? rstd[row] : 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int j = lane + k * G;
+        if (ok && j < nch) {
+          load_chunk(x + row * C + j * 8, xv[u][k]);
+          load_chunk(dy + row * C + j * 8, dv[u][k]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) xv[u][k][i] = dv[u][k][i] = 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = row0 + u * stride;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float xh = (xv[u][k][i] - mu[u]) * rs[u];   // masked chunks / rows have dv = 0: no effect
+          const float g = dv[u][k][i] * wv[k][i];
+          s1 += g;
+          s2 += g * xh;
+          dw[k][i] += dv[u][k][i] * xh;
+          db[k][i] += dv[u][k][i];
+          xv[u][k][i] = xh;                                  // keep xhat, reuse dv for g
+          dv[u][k][i] = g;
+        }
+      }
+      s1 = group_sum(s1, G) * invC;
+      s2 = group_sum(s2, G) * invC;
+      if (row < M) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int j = lane + k * G;
+          if (j < nch) {
+            float o[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = rs[u] * (dv[u][k][i] - s1 - xv[u][k][i] * s2);
+            store_chunk(dx + row * C + j * 8, o);
+          }
+        }
+      }
+    }
+  }
+  // reduce the groups' dw / db in LDS -> one partial row pair per workgroup
+  float* mine = red + (size_t)grp * 2 * C;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int j = lane + k * G;
+    if (j < nch) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        mine[j * 8 + i] = dw[k][i];
+        mine[C + j * 8 + i] = db[k][i];
+      }
+    }
+  }
+  __syncthreads();
+  const int groups = kThreads / G;
+  for (int c = threadIdx.x; c < 2 * C; c += kThreads) {
+    float acc = 0.f;
+    for (int gi = 0; gi < groups; ++gi) acc += red[(size_t)gi * 2 * C + c];
+    part[(size_t)blockIdx.x * 2 * C + c] = acc;
+  }
+}
+
+// column sums of x [M, N] -> part[blockIdx][N] (f32); a thread owns one 8-column chunk
+// and a subset of rows
+template <typename T>
+__global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ x, float* __restrict__ part, int M,
+                                                          int N) {
+  extern __shared__ float red[];             // [rowsets][N]
+  const int nch = N >> 3;
+  const int rowsets = kThreads / nch;        // nch <= 256
+  const int ch = threadIdx.x % nch;
+  const int rs = threadIdx.x / nch;
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  if (rs < rowsets) {
+    const long long stride = (long long)gridDim.x * rowsets;
+    for (long long row = (long long)blockIdx.x * rowsets + rs; row < M; row += 4 * stride) {
+      float v[4][8];                            // 4 rows' loads in flight
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (row + u * stride < M) {
+          load_chunk(x + (row + u * stride) * N + ch * 8, v[u]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += v[u][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[(size_t)rs * N + ch * 8 + i] = acc[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += kThreads) {
+    float a = 0.f;
+    for (int r = 0; r < rowsets; ++r) a += red[(size_t)r * N + c];
+    part[(size_t)blockIdx.x * N + c] = a;
+  }
+}
+
+// out[c] = sum_b part[b][c] (b < nb) in a fixed order; columns [0, split) go to out0,
+// [split, N) to out1.  A block = 32 columns x 8 row slices, 4 independent accumulators
+// per thread (memory-level parallelism), slices combined in LDS.
+template <typename T>
+__global__ void __launch_bounds__(kThreads) colsum_partials_kernel(const float* __restrict__ part, T* __restrict__ out0,
+                                                                   T* __restrict__ out1, int nb, int N, int split) {
+  __shared__ float red[8][33];
+  const int lane = threadIdx.x & 31;
+  const int sl = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < N) {
+    int r = sl;
+    for (; r + 24 < nb; r += 32) {
+      a0 += part[(size_t)r * N + col];
+      a1 += part[(size_t)(r + 8) * N + col];
+      a2 += part[(size_t)(r + 16) * N + col];
+      a3 += part[(size_t)(r + 24) * N + col];
+    }
+    for (; r < nb; r += 8) a0 += part[(size_t)r * N + col];
+  }
+  red[sl][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sl == 0 && col < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][lane];
+    if (col < split) out0[col] = from_f32<T>(t);
+    else out1[col - split] = from_f32<T>(t);
+  }
+}
+
+// pick (G, K): smallest K whose power-of-two group fits in 16 lanes, else 64 lanes
+bool pick_gk(int nch, int kmax, int* G, int* K) {
+  static const int ks[] = {1, 2, 3, 4};
+  for (int lim : {16, 64}) {
+    for (int k : ks) {
+      if (k > kmax) break;
+      int g = 4;
+      while (g * k < nch) g <<= 1;
+      if (g <= lim) {
+        *G = g;
+        *K = k;
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
+int blocks_for(long long M, int rows_per_block, int cap) {
+  long long nb = (M + rows_per_block - 1) / rows_per_block;
+  return (int)std::max<long long>(1, std::min<long long>(nb, cap));
+}
+
+}  // namespace
+}  // namespace vs
+
+using namespace vs;
+
+#define VS_LN_K(KK, ...)           \
+  switch (KK) {                    \
+    case 1: __VA_ARGS__(1); break; \
+    case 2: __VA_ARGS__(2); break; \
+    case 3: __VA_ARGS__(3); break; \
+    default: __VA_ARGS__(4); break; \
+  }
+
+// at most 4 chunks of 8 per lane (register budget of the backward): C <= 64 * 32 = 2048
+static int ln_kmax(int) { return 4; }
+
+extern "C" int vs_layer_norm_forward(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
+                                     float* rstd, int M, int C, float eps, void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
+  VS_CHECK(w && b && (M == 0 || (x && y && mean && rstd)), "null pointer");
+  int G, K;
+  VS_CHECK(pick_gk(C / 8, ln_kmax(dtype), &G, &K), "row too long for the LayerNorm kernel (C <= 2048)");
+  if (M == 0) return VS_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = blocks_for(M, kThreads / G, 256 * 32);
+#define VS_LNF(KK)                                                                                          \
+  if (dtype == VS_BF16)                                                                                     \
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK>), dim3(grid), dim3(kThreads), 0, st, (const bf16*)x,        \
+                       (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G);                 \
+  else                                                                                                      \
+    hipLaunchKernelGGL((ln_fwd_kernel<float, KK>), dim3(grid), dim3(kThreads), 0, st, (const float*)x,      \
+                       (const float*)w, (const float*)b, (float*)y, mean, rstd, M, C, eps, G)
+  VS_LN_K(K, VS_LNF)
+#undef VS_LNF
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" long long vs_layer_norm_backward_workspace_bytes(int M, int C) {
+  return (long long)kMaxPartials * 2 * C * sizeof(float);
+}
+
+extern "C" int vs_layer_norm_backward(int dtype, const void* dy, const void* x, const void* w, const float* mean,
+                                      const float* rstd, void* dx, void* dw, void* db, void* ws, int M, int C,
+                                      void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
+  VS_CHECK(w && dw && db && ws && (M == 0 || (dy && x && mean && rstd && dx)), "null pointer");
+  int G, K;
+  VS_CHECK(pick_gk(C / 8, ln_kmax(dtype), &G, &K), "row too long for the LayerNorm kernel (C <= 2048)");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  const int grid = blocks_for(M, kThreads / G, kMaxPartials);
+  const size_t lds = (size_t)(kThreads / G) * 2 * C * sizeof(float);
+  VS_CHECK(lds <= 64 * 1024, "LayerNorm backward LDS budget exceeded");
+#define VS_LNB(KK)                                                                                            \
+  if (dtype == VS_BF16)                                                                                       \
+    hipLaunchKernelGGL((ln_bwd_kernel<bf16, KK>), dim3(grid), dim3(kThreads), lds, st, (const bf16*)dy,       \
+                       (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, C, G);                 \
+  else                                                                                                        \
+    hipLaunchKernelGGL((ln_bwd_kernel<float, KK>), dim3(grid), dim3(kThreads), lds, st, (const float*)dy,     \
+                       (const float*)x, (const float*)w, mean, rstd, (float*)dx, part, M, C, G)
+  VS_LN_K(K, VS_LNB)
+#undef VS_LNB
+  // dw = column sums of the partial rows' first halves, db of the second halves
+  const int rgrid = (2 * C + 31) / 32;
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3(rgrid), dim3(kThreads), 0, st, part, (bf16*)dw, (bf16*)db,
+                       grid, 2 * C, C);
+  else
+    hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3(rgrid), dim3(kThreads), 0, st, part, (float*)dw,
+                       (float*)db, grid, 2 * C, C);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" long long vs_column_sum_workspace_bytes(int M, int N) {
+  return (long long)kMaxPartials * N * sizeof(float);
+}
+
+extern "C" int vs_column_sum(int dtype, const void* x, void* out, void* ws, int M, int N, void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(M >= 0 && N > 0 && N % 8 == 0 && N / 8 <= kThreads, "N must be a multiple of 8, <= 2048");
+  VS_CHECK(out && ws && (M == 0 || x), "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  const int rowsets = kThreads / (N / 8);
+  const int grid = blocks_for(M, rowsets * 16, kMaxPartials);
+  const size_t lds = (size_t)rowsets * N * sizeof(float);
+  if (dtype == VS_BF16) {
+    hipLaunchKernelGGL(colsum_kernel<bf16>, dim3(grid), dim3(kThreads), lds, st, (const bf16*)x, part, M, N);
+    hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part, (bf16*)out,
+                       (bf16*)nullptr, grid, N, N);
+  } else {
+    hipLaunchKernelGGL(colsum_kernel<float>, dim3(grid), dim3(kThreads), lds, st, (const float*)x, part, M, N);
+    hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part,
+                       (float*)out, (float*)nullptr, grid, N, N);
+  }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

@@ -15,6 +15,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import ops
+
 # split when K is at least this many tokens; chunks never drop below MIN_CHUNK rows
 MIN_TOKENS = 32768
 MIN_CHUNK = 1024
@@ -61,8 +63,23 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gw = weight_grad(gy2, x.reshape(-1, x.shape[-1]).to(gy2.dtype), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = gy2.sum(0, dtype=torch.float32).to(weight.dtype)
+            if gy2.shape[1] % 8 == 0 and gy2.shape[1] <= 2048:
+                gb = ops.column_sum(gy2).to(weight.dtype)          # HIP column sum, f32 accumulation
+            else:
+                gb = gy2.sum(0, dtype=torch.float32).to(weight.dtype)
         return gx, gw, gb
+
+
+class TokenLayerNorm(nn.LayerNorm):
+    """nn.LayerNorm on the HIP row kernel (csrc/norm.hip) for f32 / bf16 device tensors
+    whose weight shares their dtype; anything else (autocast's f32 LayerNorm, CPU
+    tensors, rows > 2048) is torch's own layer_norm."""
+
+    def forward(self, x):
+        if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
+                and not torch.is_autocast_enabled():
+            return ops.layer_norm(x, self.weight, self.bias, self.eps)
+        return F.layer_norm(x, self.normalized_shape, self.weight, self.bias, self.eps)
 
 
 class TokenLinear(nn.Linear):

@@ -27,7 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .linear import TokenLinear
+from .linear import TokenLayerNorm, TokenLinear
 
 
 @dataclass
@@ -122,9 +122,9 @@ class SwinBlock(nn.Module):
     def __init__(self, dim, heads, ws, shift, mlp_ratio):
         super().__init__()
         self.ws, self.shift = ws, shift
-        self.norm1 = nn.LayerNorm(dim)
+        self.norm1 = TokenLayerNorm(dim)
         self.attn = WindowAttention(dim, heads, ws)
-        self.norm2 = nn.LayerNorm(dim)
+        self.norm2 = TokenLayerNorm(dim)
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
 
     def forward(self, x, H, W):
@@ -144,7 +144,7 @@ class SwinBlock(nn.Module):
 class PatchMerging(nn.Module):
     def __init__(self, dim):
         super().__init__()
-        self.norm = nn.LayerNorm(4 * dim)
+        self.norm = TokenLayerNorm(4 * dim)
         self.reduction = TokenLinear(4 * dim, 2 * dim, bias=False)
 
     def forward(self, x, H, W):
@@ -168,7 +168,7 @@ class PatchEmbed(nn.Module):
     def __init__(self, dim):
         super().__init__()
         self.proj = nn.Conv2d(3, dim, kernel_size=4, stride=4)
-        self.norm = nn.LayerNorm(dim)
+        self.norm = TokenLayerNorm(dim)
 
 
 class SwinBackbone(nn.Module):
@@ -182,7 +182,7 @@ class SwinBackbone(nn.Module):
         self.stages = nn.ModuleList([
             Stage(C * 2 ** i, cfg.depths[i], cfg.num_heads[i], cfg.window_size, cfg.mlp_ratio, i < n - 1)
             for i in range(n)])
-        self.out_norms = nn.ModuleList([nn.LayerNorm(C * 2 ** i) for i in range(n)])
+        self.out_norms = nn.ModuleList([TokenLayerNorm(C * 2 ** i) for i in range(n)])
 
     def forward(self, px):
         H, W = px.shape[-2:]
@@ -263,10 +263,10 @@ class EncoderLayer(nn.Module):
     def __init__(self, d, ffn, heads, levels, points):
         super().__init__()
         self.attn = MSDeformAttn(d, heads, levels, points)
-        self.norm1 = nn.LayerNorm(d)
+        self.norm1 = TokenLayerNorm(d)
         self.fc1 = TokenLinear(d, ffn)
         self.fc2 = TokenLinear(ffn, d)
-        self.norm2 = nn.LayerNorm(d)
+        self.norm2 = TokenLayerNorm(d)
 
     def forward(self, h, pos, ref, shapes, norm):
         h = self.norm1(h + self.attn(h, pos, ref, shapes, norm))

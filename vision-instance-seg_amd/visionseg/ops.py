@@ -343,3 +343,66 @@ def masked_attention(q, k, v, words, heads: int, scale: float | None = None):
     if scale is None:
         scale = 32 ** -0.5
     return MaskedAttentionFunction.apply(q, k, v, words, int(heads), float(scale))
+
+
+# ------------------------------------------------------------------ LayerNorm / bias grad
+class LayerNormFunction(torch.autograd.Function):
+    """F.layer_norm over the last dim of a token-major [..., C] tensor (csrc/norm.hip);
+    x, weight, bias share one dtype (f32 or bf16)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        L.require_hip(x, weight, bias)
+        C = x.shape[-1]
+        xc = x.contiguous()
+        M = xc.numel() // C
+        y = torch.empty_like(xc)
+        mean = torch.empty(M, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(M, device=x.device, dtype=torch.float32)
+        with timed("layer_norm_fwd", xc, bytes_=2 * xc.numel() * xc.element_size()):
+            L.check(L.lib().vs_layer_norm_forward(L.dtype_code(xc), L.ptr(xc), L.ptr(weight), L.ptr(bias), L.ptr(y),
+                                                  L.ptr(mean), L.ptr(rstd), M, C, float(eps), L.stream(xc)),
+                    "layer_norm_forward")
+        ctx.save_for_backward(xc, weight, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, weight, mean, rstd = ctx.saved_tensors
+        C = xc.shape[-1]
+        M = xc.numel() // C
+        gy = gy.to(xc.dtype).contiguous()
+        gx = torch.empty_like(xc)
+        gw = torch.empty_like(weight)
+        gb = torch.empty_like(weight)
+        ws = torch.empty(int(L.lib().vs_layer_norm_backward_workspace_bytes(M, C)), device=xc.device,
+                         dtype=torch.uint8)
+        with timed("layer_norm_bwd", xc, bytes_=3 * xc.numel() * xc.element_size()):
+            L.check(L.lib().vs_layer_norm_backward(L.dtype_code(xc), L.ptr(gy), L.ptr(xc), L.ptr(weight), L.ptr(mean),
+                                                   L.ptr(rstd), L.ptr(gx), L.ptr(gw), L.ptr(gb), L.ptr(ws), M, C,
+                                                   L.stream(xc)), "layer_norm_backward")
+        return gx, gw, gb, None
+
+
+def layer_norm(x, weight, bias, eps: float = 1e-5):
+    return LayerNormFunction.apply(x, weight, bias, eps)
+
+
+def layer_norm_supported(x, weight) -> bool:
+    C = x.shape[-1]
+    return (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and weight.dtype == x.dtype
+            and C % 8 == 0 and C <= 2048)
+
+
+def column_sum(x2d):
+    """x [M, N] -> [N] (x's dtype, f32 accumulation): the bias gradient of a token-major
+    Linear (csrc/norm.hip)."""
+    L.require_hip(x2d)
+    x2d = x2d.contiguous()
+    M, N = x2d.shape
+    out = torch.empty(N, device=x2d.device, dtype=x2d.dtype)
+    ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=x2d.device, dtype=torch.uint8)
+    with timed("column_sum", x2d, bytes_=x2d.numel() * x2d.element_size()):
+        L.check(L.lib().vs_column_sum(L.dtype_code(x2d), L.ptr(x2d), L.ptr(out), L.ptr(ws), M, N, L.stream(x2d)),
+                "column_sum")
+    return out
