@@ -192,6 +192,16 @@ VS_API long long vs_column_sum_workspace_bytes(int rows, int cols);
 VS_API int vs_column_sum(int dtype, const void* x, void* out, void* workspace, int rows, int cols,
                          void* stream);
 
+/* ---- Per-parameter gradient clipping (csrc/optim.hip) --------------------------------
+ * detectron2 "norm" clipping (reference training/maskdino/train_full.py:266-271:
+ * clip_grad_norm_(p, 0.01) for every parameter p) over a flat f32 gradient buffer whose
+ * parameters start 16-B aligned.  table: device int32 [num_chunks][4] = {start, len,
+ * first chunk of the parameter, chunks of the parameter}, chunks of one parameter
+ * consecutive.  g *= min(1, max_norm / (||g_param||_2 + eps)), deterministic. */
+VS_API long long vs_segment_clip_workspace_bytes(int num_chunks);
+VS_API int vs_segment_clip(float* data, const int* table, int num_chunks, float max_norm, float eps,
+                           void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,9 +37,11 @@ def main():
     rows.sort()
     opt = [i for i, r in enumerate(rows) if "multi_tensor_apply_kernel" in r[2]]
     # group optimizer launches into bursts
+    # bursts separated by the forward/backward: split at gaps above half the largest gap
+    thr = max(b - a for a, b in zip(opt, opt[1:])) // 2
     bursts, cur = [], [opt[0]]
     for i in opt[1:]:
-        if i - cur[-1] <= 3500:
+        if i - cur[-1] <= thr:
             cur.append(i)
         else:
             bursts.append(cur)

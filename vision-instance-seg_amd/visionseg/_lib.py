@@ -44,11 +44,14 @@ SIGNATURES = {
     "vs_layer_norm_backward": [_c_int] + [_P] * 9 + [_c_int] * 2 + [_P],
     "vs_column_sum_workspace_bytes": [_c_int] * 2,
     "vs_column_sum": [_c_int] + [_P] * 3 + [_c_int] * 2 + [_P],
+    "vs_segment_clip_workspace_bytes": [_c_int],
+    "vs_segment_clip": [_P, _P, _c_int, _c_float, _c_float, _P, _P],
 }
 RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": ctypes.c_longlong,
             "vs_mask_head_backward_workspace_bytes": ctypes.c_longlong,
             "vs_layer_norm_backward_workspace_bytes": ctypes.c_longlong,
-            "vs_column_sum_workspace_bytes": ctypes.c_longlong}
+            "vs_column_sum_workspace_bytes": ctypes.c_longlong,
+            "vs_segment_clip_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
 

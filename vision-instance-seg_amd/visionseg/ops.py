@@ -406,3 +406,47 @@ def column_sum(x2d):
         L.check(L.lib().vs_column_sum(L.dtype_code(x2d), L.ptr(x2d), L.ptr(out), L.ptr(ws), M, N, L.stream(x2d)),
                 "column_sum")
     return out
+
+
+# ------------------------------------------------------------------ per-parameter clip
+class FlatParams:
+    """f32 parameters (or gradients) packed into one flat device buffer, each starting
+    16-B aligned, with the chunk table of csrc/optim.hip for per-parameter clipping."""
+
+    CHUNK = 1 << 16
+
+    def __init__(self, shapes, device):
+        self.shapes = [tuple(s) for s in shapes]
+        self.offsets, off = [], 0
+        for s in self.shapes:
+            n = 1
+            for d in s:
+                n *= int(d)
+            self.offsets.append((off, n))
+            off += (n + 3) // 4 * 4
+        self.total = off
+        rows = []
+        for (o, n) in self.offsets:
+            first = len(rows)
+            count = max(1, (n + self.CHUNK - 1) // self.CHUNK)
+            for c in range(count):
+                rows.append([o + c * self.CHUNK, max(0, min(self.CHUNK, n - c * self.CHUNK)), first, count])
+        self.num_chunks = len(rows)
+        self.table = torch.tensor(rows, dtype=torch.int32).to(device)
+        self.device = torch.device(device)
+        self.ws = torch.empty(int(L.lib().vs_segment_clip_workspace_bytes(self.num_chunks)) if self.device.type == "cuda"
+                              else 0, device=device, dtype=torch.uint8)
+
+    def buffer(self):
+        return torch.zeros(self.total, device=self.device, dtype=torch.float32)
+
+    def views(self, flat):
+        return [flat[o:o + n].view(s) for (o, n), s in zip(self.offsets, self.shapes)]
+
+    def clip_(self, flat, max_norm: float, eps: float = 1e-6):
+        """In place: every parameter's slice scaled to L2 norm <= max_norm (clip_grad_norm_
+        per parameter, detectron2 "norm")."""
+        L.require_hip(flat)
+        with timed("segment_clip", flat, bytes_=3 * self.total * 4):
+            L.check(L.lib().vs_segment_clip(L.ptr(flat), L.ptr(self.table), self.num_chunks, float(max_norm),
+                                            float(eps), L.ptr(self.ws), L.stream(flat)), "segment_clip")

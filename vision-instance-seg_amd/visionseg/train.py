@@ -107,9 +107,21 @@ class Trainer:
             self.net = self.model
         params = [p for p in self.model.parameters() if p.requires_grad]
         self.model_params = params
+        self.flat = None
         if self.mode == "bf16":
-            # f32 master copy owned by the optimiser; the model keeps bf16 working weights
-            self.params = [p.detach().float().clone() for p in params]
+            # f32 master copy owned by the optimiser, packed in one flat buffer (and the f32
+            # master grads in another) so the per-parameter clip is two kernels; the model
+            # keeps bf16 working weights
+            from .ops import FlatParams
+            self.flat = FlatParams([p.shape for p in params], self.device)
+            self.flat_master, self.flat_grad = self.flat.buffer(), self.flat.buffer()
+            self.params = []
+            with torch.no_grad():
+                for v, g, p in zip(self.flat.views(self.flat_master), self.flat.views(self.flat_grad), params):
+                    v.copy_(p.detach().float())
+                    m = torch.nn.Parameter(v)
+                    m.grad = g
+                    self.params.append(m)
         else:
             self.params = params
         fused = self.device.type == "cuda"
@@ -126,6 +138,9 @@ class Trainer:
             return
         if s.clip_type == "full_model":
             torch.nn.utils.clip_grad_norm_(self.params, s.clip_value)
+            return
+        if self.flat is not None and self.device.type == "cuda":
+            self.flat.clip_(self.flat_grad, s.clip_value)      # csrc/optim.hip, 2 launches
             return
         # detectron2 "norm": clip_grad_norm_(p, clip_value) for every parameter, fused
         # (one stacked scale vector: a handful of launches instead of several per parameter)
@@ -149,11 +164,8 @@ class Trainer:
         loss, _ = self.forward_loss(images, mask_labels, class_labels)
         loss.backward()
         if self.mode == "bf16":
-            # (DDP has already averaged the bf16 grads) -> persistent f32 master grads, one
+            # (DDP has already averaged the bf16 grads) -> the flat f32 master grads, one
             # multi-tensor cast-copy
-            if self.params[0].grad is None:
-                for m in self.params:
-                    m.grad = torch.empty_like(m)
             grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.model_params]
             torch._foreach_copy_([m.grad for m in self.params], grads)
         self.clip_gradients()
