@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=4, help="images per GPU")
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--queries", type=int, default=100)
+    ap.add_argument("--matcher", default="device", choices=["device", "host"],
+                    help="Hungarian matching on the device (csrc/match.hip) or scipy on the host")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=2)
     ap.add_argument("--kernel-timing", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
@@ -145,7 +147,7 @@ def main():
     dev = torch.device("cuda", local)
     cfg = M2FConfig.preset(a.model, num_queries=a.queries)
     model = Mask2Former(cfg).init_weights(seed=0)
-    trainer = Trainer(model, SetCriterion(cfg), SolverConfig(precision=a.precision), device=dev)
+    trainer = Trainer(model, SetCriterion(cfg, matcher=a.matcher), SolverConfig(precision=a.precision), device=dev)
     images, ml, cl = synthetic_batch(a.batch, a.size, seed=42 + rank, device=dev)
     torch.cuda.synchronize()
 
@@ -190,6 +192,7 @@ def main():
             "final_loss": round(float(loss.item()), 4),
             "gemm_tuning": a.gemm_tuning,
             "precision": a.precision,
+            "matcher": a.matcher,
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels": table,

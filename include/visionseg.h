@@ -202,6 +202,19 @@ VS_API long long vs_segment_clip_workspace_bytes(int num_chunks);
 VS_API int vs_segment_clip(float* data, const int* table, int num_chunks, float max_norm, float eps,
                            void* workspace, void* stream);
 
+/* ---- Hungarian matching on the device (csrc/match.hip) -------------------------------
+ * Replaces scipy.optimize.linear_sum_assignment(cost.cpu()) of the set-criterion matcher
+ * (HF:m2f:489-491; upstream Mask2Former/MaskDINO matcher.py), batched over decoder steps
+ * and images.  cost: device f32 [steps, batch, queries, max_targets] (problem (s, b) uses
+ * its first targets_per_image[b] target columns); targets_per_image: HOST int [batch].
+ * assign: device int32 [steps, batch, max_targets] = the query matched to each target
+ * (-1 past the image's target count).  Minimum-total-cost assignment of every target to
+ * a distinct query (targets <= queries <= 1024).  vs_lsa_max_targets(Q) = the largest
+ * per-image target count the kernel accepts for Q queries. */
+VS_API int vs_lsa_max_targets(int num_queries);
+VS_API int vs_lsa_batch(const float* cost, const int* targets_per_image, int num_steps, int batch,
+                        int num_queries, int max_targets, int* assign, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,8 @@ SIGNATURES = {
     "vs_column_sum": [_c_int] + [_P] * 3 + [_c_int] * 2 + [_P],
     "vs_segment_clip_workspace_bytes": [_c_int],
     "vs_segment_clip": [_P, _P, _c_int, _c_float, _c_float, _P, _P],
+    "vs_lsa_max_targets": [_c_int],
+    "vs_lsa_batch": [_P, _P] + [_c_int] * 4 + [_P, _P],
 }
 RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": ctypes.c_longlong,
             "vs_mask_head_backward_workspace_bytes": ctypes.c_longlong,

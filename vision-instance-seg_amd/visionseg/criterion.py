@@ -7,13 +7,17 @@ uniformly sampled points; class 2 / mask 5 / dice 5; every decoder step supervis
 restructured for the device:
 
 * the matching costs of ALL decoder steps and ALL images are computed in a few
-  batched kernels and copied to the host in ONE transfer (the reference's per-image,
-  per-layer `linear_sum_assignment(cost.cpu())` is 10 x B host syncs per step);
-* the mask/dice/CE losses of all decoder steps are evaluated as one batch.
+  batched kernels, and the assignments are solved ON THE DEVICE (csrc/match.hip, one
+  wave per (step, image) Hungarian problem): the reference's per-image, per-layer
+  `linear_sum_assignment(cost.cpu())` is 10 x B host syncs per step, here there is none,
+  so the host keeps enqueueing the loss and the backward while the GPU runs the forward;
+* the mask/dice/CE losses of all decoder steps are evaluated as one batch over the
+  matched (query, target) pairs, ordered by target.
 
-The assignment itself is scipy's `linear_sum_assignment` (the reference's choice).  The
-random points come from the device generator, so a GPU loss is not bit-comparable
-with the CPU oracle's (documented in DESIGN.md; the oracle's loss is pinned to HF).
+`matcher="host"` keeps scipy's `linear_sum_assignment` (the reference's choice); both
+return the same optimum (unique for generic costs).  The random points come from the
+device generator, so a GPU loss is not bit-comparable with the CPU oracle's (documented
+in DESIGN.md; the oracle's loss is pinned to HF).
 """
 from __future__ import annotations
 
@@ -22,6 +26,8 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
+from . import ops
+
 
 def _sample(feat, coords):
     """point_sample (HF:m2f:245-275): feat [N,1,H,W], coords [N,P,2] in [0,1] -> [N,P]."""
@@ -29,15 +35,21 @@ def _sample(feat, coords):
 
 
 class SetCriterion:
-    def __init__(self, cfg):
+    def __init__(self, cfg, matcher: str = "device"):
+        """matcher: "device" (csrc/match.hip, no host sync) or "host" (scipy, the
+        reference's linear_sum_assignment)."""
+        if matcher not in ("device", "host"):
+            raise ValueError(matcher)
         self.cfg = cfg
         self.num_labels = cfg.num_labels
+        self.matcher = matcher
+        self._pairs = {}
 
     # --------------------------------------------------------------- matching
     @torch.no_grad()
     def match(self, masks_list, classes, mask_labels, class_labels):
-        """masks_list: S x [B,Q,H,W] (S decoder steps), classes [S,B,Q,K+1] -> per step, per
-        image (src_idx, tgt_idx) int64 CPU tensors."""
+        """masks_list: S x [B,Q,H,W] (S decoder steps), classes [S,B,Q,K+1] -> int32
+        [S, B, Kmax] on the device: the query matched to each target (-1 padding)."""
         c = self.cfg
         S = len(masks_list)
         B, Q = masks_list[0].shape[:2]
@@ -64,21 +76,25 @@ class SetCriterion:
             cc = -probs[:, i][:, :, class_labels[i]]
             cost[:, i, :, :K] = c.mask_weight * cm + c.class_weight * cc + c.dice_weight * cd
         cost = torch.nan_to_num(cost.clamp(-1e10, 1e10), 0.0)
-        host = cost.cpu().numpy()                                                         # the one host sync
+        ks = [int(t.shape[0]) for t in class_labels]
+        if any(k > Q for k in ks):
+            raise ValueError(f"an image has more targets ({max(ks)}) than queries ({Q})")
+        if self.matcher == "device" and cost.is_cuda and max(ks) <= ops.lsa_max_targets(Q):
+            return ops.linear_sum_assignment_batch(cost, ks)           # csrc/match.hip, no host sync
+        # scipy on the host (the reference's matcher): one device->host sync
+        host = cost.cpu().numpy()
         from scipy.optimize import linear_sum_assignment
-        out = []
+        out = np.full((S, B, kmax), -1, dtype=np.int32)
         for s in range(S):
-            per = []
             for i in range(B):
-                K = int(class_labels[i].shape[0])
-                a, b = linear_sum_assignment(host[s, i, :, :K]) if K else (np.zeros(0, np.int64), np.zeros(0, np.int64))
-                per.append((torch.as_tensor(a, dtype=torch.int64), torch.as_tensor(b, dtype=torch.int64)))
-            out.append(per)
-        return out
+                if ks[i]:
+                    a, b = linear_sum_assignment(host[s, i, :, :ks[i]])
+                    out[s, i, b] = a
+        return torch.from_numpy(out).to(dev)
 
     # --------------------------------------------------------------- losses
     def _num_masks(self, class_labels, device):
-        n = torch.as_tensor(float(sum(int(t.shape[0]) for t in class_labels)), device=device)
+        n = torch.full((), float(sum(int(t.shape[0]) for t in class_labels)), device=device)   # fill, no copy
         ws = 1
         if dist.is_available() and dist.is_initialized():
             dist.all_reduce(n)
@@ -93,22 +109,24 @@ class SetCriterion:
         classes = torch.stack(classes_list)      # [S,B,Q,K+1]
         S, B, Q = classes.shape[:3]
         dev = classes.device
-        idx = self.match([m.detach() for m in masks_list], classes.detach(), mask_labels, class_labels)
+        assign = self.match([m.detach() for m in masks_list], classes.detach(), mask_labels, class_labels)
         nm = self._num_masks(class_labels, dev)
-        # gather matched predictions and their targets for every step: [S, N, H, W]
-        bsel, qsel, tgts = [], [], []
-        offs = np.cumsum([0] + [int(t.shape[0]) for t in class_labels])
-        tgt_all = torch.cat([m.float() for m in mask_labels], 0) if offs[-1] else None
-        for s in range(S):
-            bsel.append(torch.cat([torch.full_like(a, i) for i, (a, _) in enumerate(idx[s])]))
-            qsel.append(torch.cat([a for a, _ in idx[s]]))
-            tgts.append(torch.cat([b + int(offs[i]) for i, (_, b) in enumerate(idx[s])]))
-        N = int(offs[-1])
-        tc = torch.full((S, B, Q), self.num_labels, dtype=torch.int64)
-        for s in range(S):
-            if N:
-                tc[s, bsel[s], qsel[s]] = torch.cat([class_labels[i].cpu()[b] for i, (_, b) in enumerate(idx[s])])
-        tc = tc.to(dev, non_blocking=True)
+        # matched pairs of every step, ordered by target t (image-major): image bs[t], the
+        # target's index k within its image, its query qs[s, t]; all on the device
+        ks = tuple(int(t.shape[0]) for t in class_labels)
+        N = sum(ks)
+        if (ks, dev) not in self._pairs:
+            img = [torch.full((k,), i, device=dev, dtype=torch.int64) for i, k in enumerate(ks) if k]
+            kin = [torch.arange(k, device=dev) for k in ks if k]
+            self._pairs[(ks, dev)] = (torch.cat(img), torch.cat(kin)) if N else (None, None)
+        bt, kt = self._pairs[(ks, dev)]
+        tgt_all = torch.cat([m.float() for m in mask_labels], 0) if N else None
+        tc = torch.full((S, B, Q), self.num_labels, dtype=torch.int64, device=dev)
+        if N:
+            qs = assign[:, bt, kt].long()                                                  # [S, N]
+            bs = bt.expand(S, N)
+            cls_all = torch.cat([t.to(dev) for t in class_labels]).long()
+            tc[torch.arange(S, device=dev)[:, None], bs, qs] = cls_all.expand(S, N)
         ew = torch.ones(self.num_labels + 1, device=dev)
         ew[-1] = c.no_object_weight
         ce = F.cross_entropy(classes.float().reshape(S * B, Q, -1).transpose(1, 2), tc.view(S * B, Q),
@@ -117,9 +135,6 @@ class SetCriterion:
         wsum = ew[tc.view(S * B, Q)].view(S, B * Q).sum(-1)
         loss_ce = ce.view(S, B * Q).sum(-1) / wsum                                         # [S]
         if N:
-            bs = torch.stack(bsel).to(dev)
-            qs = torch.stack(qsel).to(dev)
-            ts = torch.stack(tgts).to(dev)
             pred = torch.stack([masks_list[k][bs[k], qs[k]] for k in range(S)])           # [S,N,H,W]
             H, W = pred.shape[-2:]
             pred = pred.reshape(S * N, 1, H, W)
@@ -134,13 +149,10 @@ class SetCriterion:
                 if npts - nu > 0:
                     coords = torch.cat([coords, torch.rand(S * N, npts - nu, 2, device=dev)], 1)
                 # sample each full-resolution target once, with the coordinates of the S
-                # predictions it is matched to (every target is matched once per step)
-                inv = torch.empty_like(ts)
-                inv.scatter_(1, ts, torch.arange(N, device=dev).expand(S, N).contiguous())
-                cs = coords.view(S, N, npts, 2)
-                by_t = cs[torch.arange(S, device=dev)[None, :], inv.t()]                      # [N,S,P,2]
+                # predictions it is matched to (pairs are target-ordered in every step)
+                by_t = coords.view(S, N, npts, 2).transpose(0, 1)                          # [N,S,P,2]
                 lab_t = _sample(tgt_all[:, None], by_t.reshape(N, S * npts, 2)).view(N, S, npts)
-                plab = lab_t[ts, torch.arange(S, device=dev)[:, None]].reshape(S * N, npts)
+                plab = lab_t.transpose(0, 1).reshape(S * N, npts)
             plog = _sample(pred.float(), coords)
             bce = F.binary_cross_entropy_with_logits(plog, plab, reduction="none").mean(1)  # [S*N]
             loss_mask = bce.view(S, N).sum(-1) / nm

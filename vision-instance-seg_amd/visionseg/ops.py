@@ -450,3 +450,23 @@ class FlatParams:
         with timed("segment_clip", flat, bytes_=3 * self.total * 4):
             L.check(L.lib().vs_segment_clip(L.ptr(flat), L.ptr(self.table), self.num_chunks, float(max_norm),
                                             float(eps), L.ptr(self.ws), L.stream(flat)), "segment_clip")
+
+
+# ------------------------------------------------------------------ matching
+def lsa_max_targets(num_queries: int) -> int:
+    return int(L.lib().vs_lsa_max_targets(int(num_queries)))
+
+
+def linear_sum_assignment_batch(cost, targets_per_image):
+    """cost [S, B, Q, Kmax] f32 (device) + per-image target counts (host ints) ->
+    int32 [S, B, Kmax]: the query matched to each target, -1 past the count
+    (csrc/match.hip; scipy linear_sum_assignment semantics per (step, image))."""
+    import ctypes
+    L.require_hip(cost)
+    c = cost.float().contiguous()
+    S, B, Q, K = c.shape
+    ks = (ctypes.c_int * B)(*[int(k) for k in targets_per_image])
+    out = torch.empty(S, B, K, device=c.device, dtype=torch.int32)
+    with timed("lsa", c, bytes_=c.numel() * 4):
+        L.check(L.lib().vs_lsa_batch(L.ptr(c), ks, S, B, Q, K, L.ptr(out), L.stream(c)), "lsa_batch")
+    return out
