@@ -180,7 +180,8 @@ def test_window_attention_bf16_vs_oracle():
     ref = _win_attn_ref(qkv.float(), table, heads, ws, shift, nWh, nWw)
     out = ops.window_attention(qkv.to(DEV), table.to(DEV), heads, ws, shift, nWh, nWw)
     err = (out.float().cpu() - ref).abs()
-    assert bool((err <= ref.abs() * 2 ** -8 + 2e-3).all()), float(err.max())
+    # the MFMA path rounds P to bf16 for the P.V product (flash-attention practice)
+    assert bool((err <= ref.abs() * 2 ** -7 + 4e-3).all()), float(err.max())
 
 
 # ------------------------------------------------------------------ mask head + bitmask
@@ -498,3 +499,31 @@ def test_segment_clip_vs_clip_grad_norm():
         p.grad = gr.double().clone()
         torch.nn.utils.clip_grad_norm_([p], 0.01)
         np.testing.assert_allclose(v.cpu().double().numpy(), p.grad.numpy(), rtol=2e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("shift", [0, 3])
+@pytest.mark.parametrize("heads,nWh,nWw", [(3, 4, 4), (6, 3, 5), (12, 2, 2)])
+@pytest.mark.parametrize("kernel", ["mfma", "scalar"])
+def test_window_attention_bf16_fwd_bwd_vs_oracle(monkeypatch, shift, heads, nWh, nWw, kernel):
+    """bf16 window attention forward + backward (MFMA path for ws=7, and the scalar path
+    via VS_WIN_ATTN_SCALAR=1) vs the f32 oracle on the same bf16-rounded inputs."""
+    if kernel == "scalar":
+        monkeypatch.setenv("VS_WIN_ATTN_SCALAR", "1")
+    ops = _ops()
+    B, ws = 2, 7
+    Bw, N, C = B * nWh * nWw, ws * ws, heads * 32
+    g = torch.Generator().manual_seed(heads * 10 + shift)
+    qkv = torch.randn(Bw, N, 3 * C, generator=g).to(torch.bfloat16)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g)
+    qr, tr = qkv.float().requires_grad_(True), table.clone().requires_grad_(True)
+    ref = _win_attn_ref(qr, tr, heads, ws, shift, nWh, nWw)
+    go = torch.randn(ref.shape, generator=g).to(torch.bfloat16)
+    ref.backward(go.float())
+    qd, td = qkv.to(DEV).requires_grad_(True), table.to(DEV).requires_grad_(True)
+    out = ops.window_attention(qd, td, heads, ws, shift, nWh, nWw)
+    err = (out.float().cpu() - ref.detach()).abs()
+    assert bool((err <= ref.detach().abs() * 2 ** -7 + 4e-3).all()), float(err.max())
+    out.backward(go.to(DEV))
+    for got, exp in ((qd.grad, qr.grad), (td.grad, tr.grad)):
+        e = float((got.float().cpu() - exp).abs().max())
+        assert e <= 2e-2 * float(exp.abs().max()), (e, float(exp.abs().max()))

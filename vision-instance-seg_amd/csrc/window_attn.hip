@@ -280,6 +280,418 @@ __global__ void __launch_bounds__(256) win_attn_bwd_kernel(
   for (int t = threadIdx.x; t < T2; t += blockDim.x) gp[t] = sbins[t];
 }
 
+// ---------------------------------------------------------------------------------------
+// bf16 MFMA path (windows of N <= 64 tokens, e.g. Swin ws = 7): one wave per (window,
+// head).  v_mfma_f32_32x32x16_bf16 fragments (lane l: r = l & 31, hh = l >> 5):
+//   A: row r, k = 8hh + j;  B: col r, k = 8hh + j;  C/D: col r, row (i&3) + 8(i>>2) + 4hh.
+// Forward: S^T = K Q^T (keys on rows, 2x2 tiles over the 64-padded window), so a lane
+// holds 32 keys of ONE query: the softmax is in-register plus one lane^32 exchange.  Then
+// O^T = V^T P^T takes P^T straight from the accumulators: the MFMA's k index is mapped to
+// keys in the C layout's row order (k = 8hh + j  <->  key 16t + (j&3) + 8(j>>2) + 4hh) and
+// the A operand (V^T, staged in LDS) is read in that same order, so P never leaves
+// registers.  Backward: dP^T = V dO^T (same layout), dV = P^T dO and dK = dS^T Q through
+// one LDS copy of P^T / dS^T, dQ^T = K^T dS^T again straight from registers; the bias
+// gradient is binned per window in LDS (as the scalar path).
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxT2 = 225;       // (2*8-1)^2
+constexpr int kPadK = 72;         // LDS row pitch (shorts) of the 64-token operands
+
+__device__ __forceinline__ short bf16_bits(float x) {
+  const bf16 b = __float2bfloat16(x);
+  return *reinterpret_cast<const short*>(&b);
+}
+
+__device__ __forceinline__ bf16x8_t ld8(const bf16* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+
+__device__ __forceinline__ bf16x8_t pack8(const f32x16_t& a, int base) {
+  bf16x8_t v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf16_bits(a[base + j]);
+  return v;
+}
+
+// A operand in the permuted key order from an LDS row [.. keys ..]: keys base+0..3, base+8..11
+__device__ __forceinline__ bf16x8_t ld_perm(const short* row, int base) {
+  const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(row + base);
+  const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(row + base + 8);
+  bf16x8_t v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// token metadata of the window: ty | tx << 8 | region << 16
+__device__ __forceinline__ void window_tokens(const WinGeom& g, int bw, int lane, int* tok) {
+  const int ws = g.ws;
+  const int wl = bw % (g.nWh * g.nWw);
+  const int wy = wl / g.nWw, wx = wl % g.nWw;
+  const int Hp = g.nWh * ws, Wp = g.nWw * ws;
+  const int t = lane;
+  if (t < g.N) {
+    const int ty = t / ws, tx = t % ws;
+    const int reg = g.shift > 0 ? region_of(wy * ws + ty, Hp, ws, g.shift) * 3 + region_of(wx * ws + tx, Wp, ws, g.shift) : 0;
+    tok[t] = ty | (tx << 8) | (reg << 16);
+  } else {
+    tok[t] = 0;
+  }
+}
+
+// scaled logits + bias + shift mask for the S^T accumulators of one (kt, qt) tile
+__device__ __forceinline__ void logits_tile(f32x16_t& s, const WinGeom& g, const int* tok, const float* bias, int kt,
+                                            int qt, int r, int hh) {
+  const int q = 32 * qt + r;
+  const int tq = tok[q];
+  const int tyq = tq & 255, txq = (tq >> 8) & 255, rq = tq >> 16;
+  const int tw = 2 * g.ws - 1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh;
+    if (k < g.N) {
+      const int tk = tok[k];
+      const int rel = (tyq - (tk & 255) + g.ws - 1) * tw + (txq - ((tk >> 8) & 255) + g.ws - 1);
+      float v = s[i] * g.scale + bias[rel];
+      if ((tk >> 16) != rq) v += -100.f;
+      s[i] = v;
+    } else {
+      s[i] = -INFINITY;
+    }
+  }
+}
+
+constexpr int kFwdWaves = 4;
+
+__global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* __restrict__ qkv,
+                                                                    const float* __restrict__ table,
+                                                                    bf16* __restrict__ out, float* __restrict__ lse,
+                                                                    WinGeom g, int items) {
+  __shared__ __attribute__((aligned(16))) short sVt[kFwdWaves][32 * kPadK];   // V^T [d][key]
+  __shared__ float sBias[kFwdWaves][kMaxT2];
+  __shared__ int sTok[kFwdWaves][64];
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int item = blockIdx.x * kFwdWaves + wave;
+  if (item >= items) return;                  // wave-uniform; only wave-level syncs below
+  const int h = item % g.heads, bw = item / g.heads;
+  const int N = g.N, C = g.heads * kD, C3 = 3 * C;
+  const bf16* win = qkv + (size_t)bw * N * C3;
+  short* vt = sVt[wave];
+  float* bias = sBias[wave];
+  int* tok = sTok[wave];
+  window_tokens(g, bw, l, tok);
+  for (int t = l; t < g.T2; t += 64) bias[t] = table[t * g.heads + h];
+  {  // V^T: lane = key
+    const int key = l;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bf16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (key < N) v = ld8(win + (size_t)key * C3 + 2 * C + h * kD + 8 * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vt[(8 * c + j) * kPadK + key] = v[j];
+    }
+  }
+  // S^T = K Q^T
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    bf16x8_t ka[2], qb[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int row = 32 * t + r;
+      const bf16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+      ka[t] = row < N ? ld8(win + (size_t)row * C3 + C + h * kD + 16 * st + 8 * hh) : z;
+      qb[t] = row < N ? ld8(win + (size_t)row * C3 + h * kD + 16 * st + 8 * hh) : z;
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+        acc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kt], qb[qt], acc[kt][qt], 0, 0, 0);
+  }
+  wave_sync();                                // tok / bias / V^T visible to the whole wave
+  float inv[2], lq[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    logits_tile(acc[0][qt], g, tok, bias, 0, qt, r, hh);
+    logits_tile(acc[1][qt], g, tok, bias, 1, qt, r, hh);
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m = fmaxf(m, fmaxf(acc[0][qt][i], acc[1][qt][i]));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      acc[0][qt][i] = __expf(acc[0][qt][i] - m);
+      acc[1][qt][i] = __expf(acc[1][qt][i] - m);
+      sum += acc[0][qt][i] + acc[1][qt][i];
+    }
+    sum += __shfl_xor(sum, 32, 64);
+    inv[qt] = 1.f / sum;
+    lq[qt] = m + __logf(sum);
+  }
+  // O^T = V^T P^T
+  f32x16_t o[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[qt][i] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int kt = t >> 1, th = t & 1;
+    const bf16x8_t a = ld_perm(vt + r * kPadK, 32 * kt + 16 * th + 4 * hh);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+      o[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pack8(acc[kt][qt], 8 * th), o[qt], 0, 0, 0);
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = 32 * qt + r;
+    if (q < N) {
+      bf16* dst = out + ((size_t)bw * N + q) * C + h * kD;
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        bf16x4_t v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[qt][4 * grp + e] * inv[qt]);
+        *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+      }
+      if (hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = lq[qt];
+    }
+  }
+}
+
+constexpr int kBwdWaves = 2;
+
+__global__ void __launch_bounds__(64 * kBwdWaves) win_attn_bwd_mfma(
+    const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
+    const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
+    float* __restrict__ gtable_part, WinGeom g, int items) {
+  __shared__ __attribute__((aligned(16))) short sT[kBwdWaves][64 * kPadK];    // P^T, then dS^T [key][q]
+  __shared__ __attribute__((aligned(16))) short sDoT[kBwdWaves][32 * kPadK];  // dO^T [d][q]
+  __shared__ __attribute__((aligned(16))) short sQT[kBwdWaves][32 * kPadK];   // Q^T [d][q]
+  __shared__ __attribute__((aligned(16))) short sKT[kBwdWaves][32 * kPadK];   // K^T [d][key]
+  __shared__ float sBias[kBwdWaves][kMaxT2];
+  __shared__ float sBins[kBwdWaves][kMaxT2];
+  __shared__ int sTok[kBwdWaves][64];
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int item = blockIdx.x * kBwdWaves + wave;
+  if (item >= items) return;
+  const int h = item % g.heads, bw = item / g.heads;
+  const int N = g.N, C = g.heads * kD, C3 = 3 * C;
+  const bf16* win = qkv + (size_t)bw * N * C3;
+  const bf16* gwin_o = gout + (size_t)bw * N * C + h * kD;
+  short* pt = sT[wave];
+  short* dot_ = sDoT[wave];
+  short* qt_ = sQT[wave];
+  short* kt_ = sKT[wave];
+  float* bias = sBias[wave];
+  float* bins = sBins[wave];
+  int* tok = sTok[wave];
+  window_tokens(g, bw, l, tok);
+  for (int t = l; t < g.T2; t += 64) {
+    bias[t] = table[t * g.heads + h];
+    bins[t] = 0.f;
+  }
+  {  // transposed copies, lane = token
+    const int t = l;
+    const bf16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8_t q = t < N ? ld8(win + (size_t)t * C3 + h * kD + 8 * c) : z;
+      const bf16x8_t k = t < N ? ld8(win + (size_t)t * C3 + C + h * kD + 8 * c) : z;
+      const bf16x8_t d = t < N ? ld8(gwin_o + (size_t)t * C + 8 * c) : z;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        qt_[(8 * c + j) * kPadK + t] = q[j];
+        kt_[(8 * c + j) * kPadK + t] = k[j];
+        dot_[(8 * c + j) * kPadK + t] = d[j];
+      }
+    }
+  }
+  // S^T = K Q^T and dP^T = V dO^T
+  f32x16_t sacc[2][2], dacc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[a][b][i] = dacc[a][b][i] = 0.f;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    bf16x8_t ka[2], va[2], qb[2], db[2];
+    const bf16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int row = 32 * t + r;
+      const int off = 16 * st + 8 * hh;
+      ka[t] = row < N ? ld8(win + (size_t)row * C3 + C + h * kD + off) : z;
+      va[t] = row < N ? ld8(win + (size_t)row * C3 + 2 * C + h * kD + off) : z;
+      qb[t] = row < N ? ld8(win + (size_t)row * C3 + h * kD + off) : z;
+      db[t] = row < N ? ld8(gwin_o + (size_t)row * C + off) : z;
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        sacc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kt], qb[qt], sacc[kt][qt], 0, 0, 0);
+        dacc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[kt], db[qt], dacc[kt][qt], 0, 0, 0);
+      }
+  }
+  // D_q = dO_q . O_q  and the saved log-sum-exp, per query column
+  float Dq[2], Lq[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = 32 * qt + r;
+    float d = 0.f;
+    Lq[qt] = 0.f;
+    if (q < N) {
+      const bf16* orow = out + ((size_t)bw * N + q) * C + h * kD + 16 * hh;
+      const bf16* grow = gwin_o + (size_t)q * C + 16 * hh;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const bf16x8_t ov = ld8(orow + 8 * c), gv = ld8(grow + 8 * c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += bf16_bits_to_f32((unsigned short)ov[j]) * bf16_bits_to_f32((unsigned short)gv[j]);
+      }
+      Lq[qt] = lse[((size_t)bw * g.heads + h) * N + q];
+    }
+    Dq[qt] = d + __shfl_xor(d, 32, 64);
+  }
+  wave_sync();
+  // P^T = exp(logits - lse); P^T -> LDS [key][q] (bf16)
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      logits_tile(sacc[kt][qt], g, tok, bias, kt, qt, r, hh);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = (32 * qt + r) < N ? __expf(sacc[kt][qt][i] - Lq[qt]) : 0.f;
+        sacc[kt][qt][i] = p;
+        pt[(32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh) * kPadK + 32 * qt + r] = bf16_bits(p);
+      }
+    }
+  wave_sync();
+  // dV = P^T dO  (rows = keys, cols = d; k over queries)
+  f32x16_t dv[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dv[kt][i] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(dot_ + r * kPadK + 16 * t + 8 * hh);
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(pt + (32 * kt + r) * kPadK + 16 * t + 8 * hh);
+      dv[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, dv[kt], 0, 0, 0);
+    }
+  }
+  bf16* gw = gqkv + (size_t)bw * N * C3 + h * kD;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      if (key < N) gw[(size_t)key * C3 + 2 * C + r] = __float2bfloat16(dv[kt][i]);
+    }
+  // dS^T = P^T (dP^T - D_q); bias-gradient bins
+  const int tw = 2 * g.ws - 1;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = 32 * qt + r;
+    const int tq = tok[q];
+    const int tyq = tq & 255, txq = (tq >> 8) & 255;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        const float ds = sacc[kt][qt][i] * (dacc[kt][qt][i] - Dq[qt]);
+        dacc[kt][qt][i] = ds;
+        if (key < N && q < N) {
+          const int tk = tok[key];
+          atomicAdd(&bins[(tyq - (tk & 255) + g.ws - 1) * tw + (txq - ((tk >> 8) & 255) + g.ws - 1)], ds);
+        }
+      }
+  }
+  wave_sync();                                // every lane has read P^T for dV
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        pt[(32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh) * kPadK + 32 * qt + r] = bf16_bits(dacc[kt][qt][i]);
+  wave_sync();
+  // dK = scale * dS^T Q
+  f32x16_t dk[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[kt][i] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(qt_ + r * kPadK + 16 * t + 8 * hh);
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(pt + (32 * kt + r) * kPadK + 16 * t + 8 * hh);
+      dk[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, dk[kt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      if (key < N) gw[(size_t)key * C3 + C + r] = __float2bfloat16(dk[kt][i] * g.scale);
+    }
+  // dQ^T = scale * K^T dS^T  (dS^T straight from registers, K^T read in the permuted key order)
+  f32x16_t dq[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[qt][i] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int kt = t >> 1, th = t & 1;
+    const bf16x8_t a = ld_perm(kt_ + r * kPadK, 32 * kt + 16 * th + 4 * hh);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+      dq[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pack8(dacc[kt][qt], 8 * th), dq[qt], 0, 0, 0);
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = 32 * qt + r;
+    if (q < N) {
+      bf16* dst = gw + (size_t)q * C3;
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        bf16x4_t v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = bf16_bits(dq[qt][4 * grp + e] * g.scale);
+        *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+      }
+    }
+  }
+  wave_sync();
+  float* gp = gtable_part + ((size_t)bw * g.heads + h) * g.T2;
+  for (int t = l; t < g.T2; t += 64) gp[t] = bins[t];
+}
+
 int check_geom(WinGeom& g, int Bw, int heads, int ws, int shift, int nWh, int nWw, float scale) {
   g.heads = heads; g.ws = ws; g.shift = shift; g.nWh = nWh; g.nWw = nWw; g.scale = scale;
   g.N = ws * ws;
@@ -293,6 +705,12 @@ int check_geom(WinGeom& g, int Bw, int heads, int ws, int shift, int nWh, int nW
 
 using namespace vs;
 
+// VS_WIN_ATTN_SCALAR=1 selects the scalar-FMA kernels for bf16 too (A/B and debugging)
+static bool use_mfma() {
+  const char* e = getenv("VS_WIN_ATTN_SCALAR");
+  return !(e && atoi(e) != 0);
+}
+
 extern "C" int vs_window_attn_forward(int dtype, const void* qkv, const float* table, void* out,
                                       float* lse, int Bw, int heads, int ws, int shift, int nWh,
                                       int nWw, float scale, void* stream) {
@@ -304,7 +722,11 @@ extern "C" int vs_window_attn_forward(int dtype, const void* qkv, const float* t
   const size_t lds = sizeof(float) * (2 * g.N * kD + g.T2);
   dim3 grid(Bw, heads);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VS_BF16) {
+  if (dtype == VS_BF16 && g.N <= 64 && use_mfma()) {
+    const int items = Bw * heads;
+    hipLaunchKernelGGL(win_attn_fwd_mfma, dim3((items + kFwdWaves - 1) / kFwdWaves), dim3(64 * kFwdWaves), 0, st,
+                       (const bf16*)qkv, table, (bf16*)out, lse, g, items);
+  } else if (dtype == VS_BF16) {
     hipLaunchKernelGGL(win_attn_fwd_kernel<bf16>, grid, dim3(threads), lds, st, (const bf16*)qkv, table,
                        (bf16*)out, lse, g);
   } else if (dtype == VS_F32) {
@@ -330,7 +752,12 @@ extern "C" int vs_window_attn_backward(int dtype, const void* qkv, const float* 
   VS_CHECK(lds <= 160 * 1024, "window too large for LDS");
   dim3 grid(Bw, heads);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VS_BF16) {
+  if (dtype == VS_BF16 && g.N <= 64 && use_mfma()) {
+    const int items = Bw * heads;
+    hipLaunchKernelGGL(win_attn_bwd_mfma, dim3((items + kBwdWaves - 1) / kBwdWaves), dim3(64 * kBwdWaves), 0, st,
+                       (const bf16*)qkv, table, (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv,
+                       grad_table_partial, g, items);
+  } else if (dtype == VS_BF16) {
     hipLaunchKernelGGL(win_attn_bwd_kernel<bf16>, grid, dim3(threads), lds, st, (const bf16*)qkv, table,
                        (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, grad_table_partial, g);
   } else if (dtype == VS_F32) {
