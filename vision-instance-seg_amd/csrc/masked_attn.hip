@@ -17,7 +17,9 @@
 // query, P recomputed from the saved lse, partials summed over chunks by a combine
 // kernel — deterministic) and dK/dV with one lane per key over all queries staged in
 // LDS.  Scalar f32 FMA datapath (first correct path; MFMA version is the next step).
-#include "common.h"
+#include "mfma_util.h"
+
+#include <algorithm>
 
 namespace vs {
 namespace {
@@ -325,6 +327,256 @@ __global__ void __launch_bounds__(256) xattn_bwd_dkdv(const T* __restrict__ q, c
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// bf16 MFMA path (32x32x16 bf16 tiles, helpers in mfma_util.h).
+//
+// Forward: workgroup = (256-key chunk, head, image x 128-query group), 4 waves = 4 query
+// tiles of 32.  V^T of the chunk is staged once in LDS.  Per 32-key tile a wave computes
+// S^T = K Q^T (keys on rows: a lane holds 16 keys of ONE query, the other 16 in lane^32),
+// applies the blocked-key bits (one 32-bit word per lane per tile), runs the online
+// softmax in registers and accumulates O^T += V^T P^T with P^T taken straight from the
+// accumulators (permuted k).  Chunk partials (o, m, l) go to xattn_fwd_combine.
+//
+// Backward: workgroup = (128-key chunk, head, image), all queries (<= 128, padded) in
+// the workgroup, wave w owns keys 32w..32w+31.  S = Q K^T and dP = dO V^T with QUERIES on
+// rows, so dV^T = dO^T P and dK^T = scale Q^T dS take P / dS straight from registers
+// (dO^T, Q^T read from LDS in the permuted query order); dS goes to LDS once so that
+// wave w can form the chunk's dQ partial for query tile w (dQ = scale dS K), summed over
+// chunks by xattn_bwd_dq_combine.
+constexpr int kFChunk = 256;
+constexpr int kFPad = kFChunk + 8;
+constexpr int kBChunk = 128;
+constexpr int kBQ = 128;
+constexpr int kBPadQ = kBQ + 8;
+constexpr int kBPadK = kBChunk + 8;
+
+__global__ void __launch_bounds__(256) xattn_fwd_mfma(const bf16* __restrict__ q, const bf16* __restrict__ k,
+                                                      const bf16* __restrict__ v, const uint32_t* __restrict__ words,
+                                                      float* __restrict__ po, float* __restrict__ pml, XGeom g) {
+  __shared__ __attribute__((aligned(16))) short sVt[32 * kFPad];
+  const int chunk = blockIdx.x, h = blockIdx.y;
+  const int nqg = (g.Q + 127) / 128;
+  const int qg = blockIdx.z % nqg, b = blockIdx.z / nqg;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int C = g.heads * kD;
+  const int jbeg = chunk * kFChunk;
+  const int n = min(kFChunk, g.S - jbeg);
+  const bf16* kb = k + ((size_t)b * g.S + jbeg) * C + h * kD;
+  const bf16* vb = v + ((size_t)b * g.S + jbeg) * C + h * kD;
+  for (int key = threadIdx.x; key < kFChunk; key += 256) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8_t v8 = key < n ? ld8(vb + (size_t)key * C + 8 * c) : zero8();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sVt[(8 * c + j) * kFPad + key] = v8[j];
+    }
+  }
+  __syncthreads();
+  const int qi = qg * 128 + wave * 32 + r;
+  const bool qok = qi < g.Q;
+  bf16x8_t qf[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) qf[st] = qok ? ld8(q + ((size_t)b * g.Q + qi) * C + h * kD + 16 * st + 8 * hh) : zero8();
+  const uint32_t* wrow = words + ((size_t)b * g.Q + (qok ? qi : 0)) * g.nw + (jbeg >> 5);
+  float m = -INFINITY, lsum = 0.f;
+  f32x16_t o;
+  zero16(o);
+  const int ntiles = (n + 31) / 32;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    f32x16_t sc;
+    zero16(sc);
+    const int key = kt * 32 + r;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8_t a = key < n ? ld8(kb + (size_t)key * C + 16 * st + 8 * hh) : zero8();
+      sc = mfma16(a, qf[st], sc);
+    }
+    const uint32_t w = qok ? wrow[kt] : 0xffffffffu;
+    float mt = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kl = crow(i, hh);
+      const bool blocked = (kt * 32 + kl >= n) || ((w >> kl) & 1u);
+      sc[i] = blocked ? -INFINITY : sc[i] * g.scale;
+      mt = fmaxf(mt, sc[i]);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float safe = mn == -INFINITY ? 0.f : mn;
+    const float alpha = __expf(m - safe);
+    lsum *= alpha;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[i] *= alpha;
+      sc[i] = __expf(sc[i] - safe);
+      lsum += sc[i];
+    }
+    m = mn;
+#pragma unroll
+    for (int th = 0; th < 2; ++th) o = mfma16(ld_perm(sVt + r * kFPad, kt * 32 + 16 * th + 4 * hh), pack8(sc, 8 * th), o);
+  }
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (qok) {
+    const size_t prow = (((size_t)b * g.heads + h) * g.nchunk + chunk) * g.Q + qi;
+    float* dst = po + prow * kD;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp)
+      *reinterpret_cast<float4*>(dst + 8 * grp + 4 * hh) =
+          make_float4(o[4 * grp], o[4 * grp + 1], o[4 * grp + 2], o[4 * grp + 3]);
+    if (hh == 0) {
+      pml[prow * 2 + 0] = m;
+      pml[prow * 2 + 1] = lsum;
+    }
+  }
+}
+
+// D_i = dO_i . O_i per (b, h, q)
+template <typename T>
+__global__ void __launch_bounds__(256) xattn_bwd_prep(const T* __restrict__ out, const T* __restrict__ gout,
+                                                      float* __restrict__ Dbuf, XGeom g) {
+  const long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // (b, h, q)
+  if (row >= (long long)g.B * g.heads * g.Q) return;
+  const int i = (int)(row % g.Q);
+  const long long bh = row / g.Q;
+  const int h = (int)(bh % g.heads);
+  const long long b = bh / g.heads;
+  float o[kD], d[kD];
+  load_head_row(out + ((size_t)b * g.Q + i) * (g.heads * kD) + h * kD, o);
+  load_head_row(gout + ((size_t)b * g.Q + i) * (g.heads * kD) + h * kD, d);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < kD; ++c) s = fmaf(o[c], d[c], s);
+  Dbuf[row] = s;
+}
+
+__global__ void __launch_bounds__(256) xattn_bwd_mfma(const bf16* __restrict__ q, const bf16* __restrict__ k,
+                                                      const bf16* __restrict__ v, const uint32_t* __restrict__ words,
+                                                      const float* __restrict__ lse, const float* __restrict__ Dbuf,
+                                                      const bf16* __restrict__ gout, bf16* __restrict__ gk,
+                                                      bf16* __restrict__ gv, float* __restrict__ pdq, XGeom g) {
+  __shared__ __attribute__((aligned(16))) short sQT[32 * kBPadQ];    // Q^T [d][q]
+  __shared__ __attribute__((aligned(16))) short sDoT[32 * kBPadQ];   // dO^T [d][q]
+  __shared__ __attribute__((aligned(16))) short sKT[32 * kBPadK];    // K^T [d][key]
+  __shared__ __attribute__((aligned(16))) short sDS[kBQ * kBPadK];   // dS [q][key]
+  __shared__ float sL[kBQ], sD[kBQ];
+  __shared__ uint32_t sW[kBQ][kBChunk / 32];
+  const int chunk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int C = g.heads * kD, Q = g.Q;
+  const int jbeg = chunk * kBChunk;
+  const int n = min(kBChunk, g.S - jbeg);
+  const bf16* qb = q + (size_t)b * Q * C + h * kD;
+  const bf16* ob = gout + (size_t)b * Q * C + h * kD;
+  const bf16* kb = k + ((size_t)b * g.S + jbeg) * C + h * kD;
+  const bf16* vb = v + ((size_t)b * g.S + jbeg) * C + h * kD;
+  {
+    const int t = threadIdx.x & 127;
+    const bool second = threadIdx.x >= 128;
+    // Q^T / dO^T (threads 0..127 / 128..255, one query each)
+    const bf16* src = second ? ob : qb;
+    short* dstT = second ? sDoT : sQT;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8_t x = t < Q ? ld8(src + (size_t)t * C + 8 * c) : zero8();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dstT[(8 * c + j) * kBPadQ + t] = x[j];
+    }
+    if (!second) {   // K^T, one key each
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bf16x8_t x = t < n ? ld8(kb + (size_t)t * C + 8 * c) : zero8();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sKT[(8 * c + j) * kBPadK + t] = x[j];
+      }
+      sL[t] = t < Q ? lse[((size_t)b * g.heads + h) * Q + t] : 0.f;
+      sD[t] = t < Q ? Dbuf[((size_t)b * g.heads + h) * Q + t] : 0.f;
+    } else {
+#pragma unroll
+      for (int c = 0; c < kBChunk / 32; ++c) {
+        const int wi = (jbeg >> 5) + c;
+        sW[t][c] = (t < Q && wi < g.nw) ? words[((size_t)b * Q + t) * g.nw + wi] : 0xffffffffu;
+      }
+    }
+  }
+  __syncthreads();
+  // S = Q K^T and dP = dO V^T for queries (rows, 4 tiles) x this wave's 32 keys (cols)
+  const int kl = wave * 32 + r;                 // key within the chunk (this lane's column)
+  const bool kok = kl < n;
+  f32x16_t sacc[4], dacc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    zero16(sacc[t]);
+    zero16(dacc[t]);
+  }
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const bf16x8_t kf = kok ? ld8(kb + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
+    const bf16x8_t vf = kok ? ld8(vb + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      const int qr = 32 * qt + r;
+      const bf16x8_t qa = qr < Q ? ld8(qb + (size_t)qr * C + 16 * st + 8 * hh) : zero8();
+      const bf16x8_t da = qr < Q ? ld8(ob + (size_t)qr * C + 16 * st + 8 * hh) : zero8();
+      sacc[qt] = mfma16(qa, kf, sacc[qt]);
+      dacc[qt] = mfma16(da, vf, dacc[qt]);
+    }
+  }
+  // P and dS (queries on rows)
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qr = 32 * qt + crow(i, hh);
+      const bool ok = kok && qr < Q && !((sW[qr][wave] >> r) & 1u);
+      const float p = ok ? __expf(sacc[qt][i] * g.scale - sL[qr]) : 0.f;
+      sacc[qt][i] = p;
+      dacc[qt][i] = p * (dacc[qt][i] - sD[qr]);
+      sDS[qr * kBPadK + kl] = bf16_bits(dacc[qt][i]);
+    }
+  // dV^T = dO^T P, dK^T = Q^T dS (k over queries, permuted order)
+  f32x16_t dv, dk;
+  zero16(dv);
+  zero16(dk);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int qt = t >> 1, th = t & 1;
+    const int base = 32 * qt + 16 * th + 4 * hh;
+    dv = mfma16(ld_perm(sDoT + r * kBPadQ, base), pack8(sacc[qt], 8 * th), dv);
+    dk = mfma16(ld_perm(sQT + r * kBPadQ, base), pack8(dacc[qt], 8 * th), dk);
+  }
+  if (kok) {
+    bf16* gvr = gv + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
+    bf16* gkr = gk + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      bf16x4_t a, c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = bf16_bits(dv[4 * grp + e]);
+        c[e] = bf16_bits(dk[4 * grp + e] * g.scale);
+      }
+      *reinterpret_cast<bf16x4_t*>(gvr + 8 * grp + 4 * hh) = a;
+      *reinterpret_cast<bf16x4_t*>(gkr + 8 * grp + 4 * hh) = c;
+    }
+  }
+  __syncthreads();                               // every wave's dS is in LDS
+  // dQ partial of query tile `wave`: dQ = scale * dS K (k over the chunk's keys)
+  f32x16_t dq;
+  zero16(dq);
+#pragma unroll
+  for (int t = 0; t < kBChunk / 16; ++t) {
+    const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sDS + (wave * 32 + r) * kBPadK + 16 * t + 8 * hh);
+    const bf16x8_t bb = *reinterpret_cast<const bf16x8_t*>(sKT + r * kBPadK + 16 * t + 8 * hh);
+    dq = mfma16(a, bb, dq);
+  }
+  const size_t prow0 = (((size_t)b * g.heads + h) * g.nchunk + chunk) * Q;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int qr = wave * 32 + crow(i, hh);
+    if (qr < Q) pdq[(prow0 + qr) * kD + r] = dq[i] * g.scale;
+  }
+}
+
 XGeom make_geom(int B, int Q, int S, int heads, float scale) {
   XGeom g;
   g.B = B; g.Q = Q; g.S = S; g.heads = heads; g.scale = scale;
@@ -343,9 +595,24 @@ XGeom make_geom(int B, int Q, int S, int heads, float scale) {
 
 using namespace vs;
 
+// chunking of the bf16 MFMA kernels (forward 256 keys, backward 128 keys per workgroup)
+static XGeom mfma_geom(int B, int Q, int S, int heads, float scale, int chunk) {
+  XGeom g = make_geom(B, Q, S, heads, scale);
+  g.chunk = chunk;
+  g.nchunk = (S + chunk - 1) / chunk;
+  return g;
+}
+
+// VS_XATTN_SCALAR=1 selects the scalar-FMA kernels for bf16 too
+static bool xattn_use_mfma() {
+  const char* e = getenv("VS_XATTN_SCALAR");
+  return !(e && atoi(e) != 0);
+}
+
 extern "C" long long vs_masked_attn_workspace_bytes(int B, int Q, int S, int heads) {
   XGeom g = make_geom(B, Q, S, heads, 1.f);
-  const long long rows = (long long)B * heads * g.nchunk * Q;
+  const int nchunk = std::max(g.nchunk, (S + kBChunk - 1) / kBChunk);
+  const long long rows = (long long)B * heads * nchunk * Q;
   return rows * (kD + 2) * 4 + (long long)B * heads * Q * 4 + 256;
 }
 
@@ -354,6 +621,20 @@ extern "C" int vs_masked_attn_forward(int dtype, const void* q, const void* k, c
                                       int B, int Q, int S, int heads, float scale, void* stream) {
   VS_CHECK(q && k && v && words && out && lse && workspace, "null pointer");
   VS_CHECK(B > 0 && Q > 0 && S > 0 && heads > 0, "bad sizes");
+  if (dtype == VS_BF16 && xattn_use_mfma()) {
+    XGeom g = mfma_geom(B, Q, S, heads, scale, kFChunk);
+    float* po = (float*)workspace;
+    float* pml = po + (size_t)B * heads * g.nchunk * Q * kD;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid(g.nchunk, heads, B * ((Q + 127) / 128));
+    hipLaunchKernelGGL(xattn_fwd_mfma, grid, dim3(256), 0, st, (const bf16*)q, (const bf16*)k, (const bf16*)v, words,
+                       po, pml, g);
+    const long long crows = (long long)B * heads * Q * 8;
+    hipLaunchKernelGGL(xattn_fwd_combine<bf16>, dim3((int)((crows + 255) / 256)), dim3(256), 0, st, po, pml,
+                       (bf16*)out, lse, g);
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
   XGeom g = make_geom(B, Q, S, heads, scale);
   float* po = (float*)workspace;
   float* pml = po + (size_t)B * heads * g.nchunk * Q * kD;
@@ -386,6 +667,22 @@ extern "C" int vs_masked_attn_backward(int dtype, const void* q, const void* k, 
   VS_CHECK(q && k && v && words && out && lse && grad_out && grad_q && grad_k && grad_v && workspace,
            "null pointer");
   VS_CHECK(B > 0 && Q > 0 && S > 0 && heads > 0, "bad sizes");
+  if (dtype == VS_BF16 && Q <= kBQ && xattn_use_mfma()) {
+    XGeom g = mfma_geom(B, Q, S, heads, scale, kBChunk);
+    float* pdq = (float*)workspace;
+    float* Dbuf = pdq + (size_t)B * heads * g.nchunk * Q * kD + (size_t)B * heads * g.nchunk * Q * 2;
+    hipStream_t st = (hipStream_t)stream;
+    const long long rows = (long long)B * heads * Q;
+    hipLaunchKernelGGL(xattn_bwd_prep<bf16>, dim3((int)((rows + 255) / 256)), dim3(256), 0, st, (const bf16*)out,
+                       (const bf16*)grad_out, Dbuf, g);
+    hipLaunchKernelGGL(xattn_bwd_mfma, dim3(g.nchunk, heads, B), dim3(256), 0, st, (const bf16*)q, (const bf16*)k,
+                       (const bf16*)v, words, lse, Dbuf, (const bf16*)grad_out, (bf16*)grad_k, (bf16*)grad_v, pdq, g);
+    const long long total = rows * kD;
+    hipLaunchKernelGGL(xattn_bwd_dq_combine<bf16>, dim3((int)((total + 255) / 256)), dim3(256), 0, st, pdq,
+                       (bf16*)grad_q, g);
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
   XGeom g = make_geom(B, Q, S, heads, scale);
   const size_t lds_dkdv = (2 * (size_t)Q * kD + 2 * Q) * sizeof(float);
   VS_CHECK(lds_dkdv <= 160 * 1024, "too many queries for the dK/dV kernel");

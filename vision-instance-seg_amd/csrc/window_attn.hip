@@ -21,7 +21,7 @@
 // pass for dK/dV, recomputing P from the saved log-sum-exp.  The per-window bias
 // gradient partials are written to [Bw, heads, (2ws-1)^2] and summed by the caller
 // (deterministic, no cross-workgroup atomics on a 169-entry table).
-#include "common.h"
+#include "mfma_util.h"
 
 namespace vs {
 namespace {
@@ -292,42 +292,8 @@ __global__ void __launch_bounds__(256) win_attn_bwd_kernel(
 // registers.  Backward: dP^T = V dO^T (same layout), dV = P^T dO and dK = dS^T Q through
 // one LDS copy of P^T / dS^T, dQ^T = K^T dS^T again straight from registers; the bias
 // gradient is binned per window in LDS (as the scalar path).
-typedef short bf16x8_t __attribute__((ext_vector_type(8)));
-typedef short bf16x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x16_t __attribute__((ext_vector_type(16)));
-
 constexpr int kMaxT2 = 225;       // (2*8-1)^2
 constexpr int kPadK = 72;         // LDS row pitch (shorts) of the 64-token operands
-
-__device__ __forceinline__ short bf16_bits(float x) {
-  const bf16 b = __float2bfloat16(x);
-  return *reinterpret_cast<const short*>(&b);
-}
-
-__device__ __forceinline__ bf16x8_t ld8(const bf16* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
-
-__device__ __forceinline__ bf16x8_t pack8(const f32x16_t& a, int base) {
-  bf16x8_t v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = bf16_bits(a[base + j]);
-  return v;
-}
-
-// A operand in the permuted key order from an LDS row [.. keys ..]: keys base+0..3, base+8..11
-__device__ __forceinline__ bf16x8_t ld_perm(const short* row, int base) {
-  const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(row + base);
-  const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(row + base + 8);
-  bf16x8_t v;
-  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-  return v;
-}
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // token metadata of the window: ty | tx << 8 | region << 16
 __device__ __forceinline__ void window_tokens(const WinGeom& g, int bw, int lane, int* tok) {
