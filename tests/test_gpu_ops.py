@@ -344,8 +344,11 @@ def test_mask_head_backward_bf16_vs_oracle(shape):
     dict(B=2, shapes=[(12, 20), (24, 40), (48, 80)], H=8, spread=3.0),       # non-square (tiny fixture 'b' like)
 ])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_msda_encoder_backward_vs_oracle(cfg, dtype):
-    """Encoder mode (queries = value grid): band kernel + far-tap atomics vs the oracle."""
+@pytest.mark.parametrize("pull_r", ["5", "0"])
+def test_msda_encoder_backward_vs_oracle(monkeypatch, cfg, dtype, pull_r):
+    """Encoder mode (queries = value grid): destination pull kernel + far-tap atomics vs
+    the oracle; R0 = 0 sends nearly every tap through the far (atomic) path."""
+    monkeypatch.setenv("VS_MSDA_PULL_R", pull_r)
     ops = _ops()
     shapes, B, H, L, P = cfg["shapes"], cfg["B"], cfg["H"], len(cfg["shapes"]), 4
     S = sum(h * w for h, w in shapes)

@@ -65,14 +65,16 @@ def main():
         for oname, off in offs.items():
             loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
             locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
-            for mode in ("carry32", "carry16", "carry8", "plain", "band"):
-                os.environ["VS_MSDA_RUN"] = {"carry32": "32", "carry16": "16", "carry8": "8"}.get(mode, "0")
+            for mode in ("carry32", "plain", "pull3", "pull5", "pull8"):
+                os.environ["VS_MSDA_RUN"] = {"carry32": "32"}.get(mode, "0")
+                os.environ["VS_MSDA_PULL_R"] = mode[4:] if mode.startswith("pull") else "5"
 
-                def fb(enc=mode == "band"):
+                def fb(enc=mode.startswith("pull")):
                     o = ops.ms_deform_attn(v, shapes, locr, wr, encoder=enc)
                     o.backward(go)
                 run(f"msda {oname} {mode}", fb, a.iters)
             os.environ.pop("VS_MSDA_RUN")
+            os.environ.pop("VS_MSDA_PULL_R")
     if "mask" in a.only:
         Q, C, Hm = 100, 256, 256
         E = torch.randn(B, Q, C, device=dev, generator=g).to(bf).requires_grad_(True)

@@ -10,24 +10,26 @@
 // one 16-B load per lane, adjacent lanes read adjacent bytes; the group's loc/attn
 // rows (96 B / 48 B, 16-B aligned) are read as float4.  Accumulation in f32.
 //
-// Backward, general queries (decoder cross-attention): one lane per channel (32 lanes =
-// one group, 2 groups per wave) so every grad_value atomic wave-instruction is two
-// contiguous 128-B row segments (the shape the f32 atomic path runs at full rate,
-// MI355X_MICROARCH §Global float atomics); grad_loc / grad_attn are 32-lane shuffle
-// reductions, written by lane 0.  That path is atomic-bound: 4 corners x 32 channels
-// x 4 B per tap (4.2 GB per pixel-decoder layer at 4x1024^2).
+// Backward, general queries (decoder cross-attention, or whenever the encoder path
+// does not apply): grad_loc / grad_attn from a gather kernel (msda_bwd_geom_kernel) and
+// grad_value from a scatter kernel with a register carry (msda_bwd_scatter_kernel; see
+// there).  Small problems use the single fused kernel (msda_bwd_kernel, one f32 atomic
+// per corner).  grad_value is bound by the float-atomic rate (~1.3 TB/s of added bytes,
+// MI355X_MICROARCH §Global float atomics).
 //
-// Backward, encoder self-attention (queries ARE the value grid, Q == S): grad_value is
-// produced by destination instead.  msda_bwd_band_kernel owns a band of value rows of
-// one (image, head, level) in LDS and gathers every tap landing there from the queries
-// whose mapped row is within kBandR rows (LDS float atomics, then one plain coalesced
-// store per element: no global atomics); the query kernel computes grad_loc /
-// grad_attn and atomically adds only the "far" corners (row beyond the margin), which
-// the shared integer predicate `near_row` assigns to exactly one of the two kernels.
-// Measured on MI355X (4x1024^2, 8 heads, tools/kbench.py): band 7.65 ms + query 1.24 ms
-// vs 3.08 ms for the all-atomic path — LDS float atomics (ds_add_f32) on this access
-// pattern cost ~6 ms (a non-atomic LDS RMW probe: ~0.2 ms), the latency-bound scan the
-// other ~1.3 ms.  The band path is therefore opt-in (encoder=True) until it wins.
+// Backward, encoder self-attention (queries ARE the value grid, Q == S, level-major),
+// opt-in (encoder=True): grad_value is first PULLED by destination
+// (msda_bwd_pull_kernel): a wave owns a 4x16 block of value cells of one (image, head,
+// level l), enumerates the queries of levels not finer than l whose reference point
+// maps within R0 cells of the block (an implicit inverse index: the queries are the
+// grid), stages their taps and grad_out rows in LDS and accumulates each cell's 32
+// channels in registers; every grad_value element is written once with a plain store.
+// The carry scatter kernel then adds every other tap (finer query levels, or farther
+// than R0 cells) with atomics; pull_tap() assigns each tap to exactly one of the two.
+// Measured at 4x1024^2 (tools/msda_probe.py, smooth offsets, R0 = 5): pull 0.9 ms +
+// scatter 2.1 ms + geom 0.36 ms, against geom + carry scatter ~2.0 ms for the default
+// path — the remaining atomics pile onto the small coarse levels and the per-query level
+// decode costs integer divisions — so the model uses the default path.
 #include "common.h"
 
 namespace vs {
@@ -43,13 +45,10 @@ struct Levels {
 };
 
 
-// ---- backward helpers shared by the band and query kernels (must stay identical:
-// a corner is accumulated by exactly one of them, decided by `near_row`).
-constexpr int kBandR = 4;      // row margin (level-l rows) of the band kernel's query scan; covers the
-                               // Deformable-DETR init offsets (|off| <= 4 px); farther taps go atomic
-constexpr int kBandMaxRows = 8;     // value rows per band workgroup (fewer if the level is wide)
-constexpr int kBandThreads = 1024;  // 32 query slots of 32 channel-lanes
-constexpr int kBandUnroll = 4;      // queries in flight per slot (loads hoisted ahead of the LDS adds)
+// ---- backward helpers shared by the pull and geom kernels (must stay identical: a
+// tap is accumulated by exactly one of them, decided by `near_tap`).
+constexpr int kPullR = 5;           // default cell margin R0 of the pull kernel (VS_MSDA_PULL_R)
+constexpr int kPullRows = 4, kPullCols = 16;   // value cells per wave of the pull kernel
 
 struct Tap {
   int h0, w0;
@@ -72,15 +71,29 @@ __device__ __forceinline__ Tap tap_geom(float x, float y, int Hl, int Wl) {
   return t;
 }
 
-// Row of level l (height Hl) onto which query row yq of level lq (height Hq) maps:
-// floor(((yq + 0.5) * Hl / Hq) - 0.5), integer arithmetic (exact, no fp ambiguity).
-__device__ __forceinline__ int mapped_row(int yq, int Hq, int Hl) {
-  const int num = (2 * yq + 1) * Hl - Hq;
-  const int den = 2 * Hq;
+// Cell of level l (extent nl) onto which query coordinate xq of level lq (extent nq)
+// maps: floor((xq + 0.5) * nl / nq - 0.5), integer arithmetic (exact, no fp ambiguity).
+__host__ __device__ __forceinline__ int mapped_cell(int xq, int nq, int nl) {
+  const int num = (2 * xq + 1) * nl - nq;
+  const int den = 2 * nq;
   return num >= 0 ? num / den : -((-num + den - 1) / den);
 }
 
-__device__ __forceinline__ bool near_row(int cy, int m) { return cy >= m - kBandR && cy <= m + kBandR + 1; }
+// a tap belongs to the pull kernel iff its query's level lq is not finer than the tap's
+// level l, it is inside, and its top-left cell is within R0 cells (both axes) of the
+// query's mapped cell on level l
+__device__ __forceinline__ bool pull_tap(const Tap& t, int lq, int l, int mcy, int mcx, int R0) {
+  return lq <= l && t.inside && abs(t.h0 - mcy) <= R0 && abs(t.w0 - mcx) <= R0;
+}
+
+__device__ __forceinline__ int ceil_div(int a, int b) { return a >= 0 ? (a + b - 1) / b : -((-a) / b); }
+
+// exact range of query coordinates x (level extent nq) whose mapped cell on a level of
+// extent nl lies in [lo, hi]:  mapped_cell(x) >= lo  <=>  x >= ceil(((2lo+1)nq - nl) / 2nl)
+__device__ __forceinline__ void mapped_range(int lo, int hi, int nq, int nl, int* xa, int* xb) {
+  *xa = max(0, ceil_div((2 * lo + 1) * nq - nl, 2 * nl));
+  *xb = min(nq - 1, ceil_div((2 * hi + 3) * nq - nl, 2 * nl) - 1);
+}
 
 template <typename T>
 __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ value,
@@ -147,15 +160,12 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ val
   }
 }
 
-template <typename T, bool ENC>
+template <typename T>
 __global__ void __launch_bounds__(256) msda_bwd_kernel(
     const T* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attw,
     const T* __restrict__ gout, float* __restrict__ gvalue, float* __restrict__ gloc,
     float* __restrict__ gattw, Levels lv, int S, int Hh, int Q, int L, int P, long long groups) {
-  // lane = channel, 32 lanes per (b, q, head).  ENC: queries are the value grid itself
-  // (encoder self-attention, Q == S level-major): near corners are accumulated by
-  // msda_bwd_band_kernel, only far corners (|row - mapped row| beyond the margin) are
-  // added here with atomics.  !ENC: every corner is an atomic add.
+  // lane = channel, 32 lanes per (b, q, head); every corner is one f32 atomic add
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long grp = gid >> 5;
   const int c = (int)(gid & 31);
@@ -163,14 +173,7 @@ __global__ void __launch_bounds__(256) msda_bwd_kernel(
   const int LP = L * P;
   const int h = (int)(grp % Hh);
   const long long bq = grp / Hh;
-  const int q = (int)(bq % Q);
   const long long b = bq / Q;
-  int lq = 0, yq = 0, Hq = 1;
-  if (ENC) {
-    while (lq + 1 < L && q >= lv.start[lq + 1]) ++lq;
-    yq = (q - lv.start[lq]) / lv.w[lq];
-    Hq = lv.h[lq];
-  }
   const float* lp = loc + grp * LP * 2;
   const float* wp = attw + grp * LP;
   const size_t rowstride = (size_t)Hh * kD;
@@ -180,7 +183,6 @@ __global__ void __launch_bounds__(256) msda_bwd_kernel(
     const int Hl = lv.h[l], Wl = lv.w[l];
     const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
     const float fH = (float)Hl, fW = (float)Wl;
-    const int m = ENC ? mapped_row(yq, Hq, Hl) : 0;
     for (int p = 0; p < P; ++p) {
       const int tap = l * P + p;
       const float a = wp[tap];
@@ -191,27 +193,25 @@ __global__ void __launch_bounds__(256) msda_bwd_kernel(
         const float lh = t.lh, lw = t.lw, hh = t.hh, hw = t.hw;
         const float ga = g * a;
         float v1 = 0.f, v2 = 0.f, v3 = 0.f, v4 = 0.f;
-        const bool far0 = !ENC || !near_row(h0, m);
-        const bool far1 = !ENC || !near_row(h0 + 1, m);
         if (h0 >= 0 && w0 >= 0) {
           const size_t o = lbase + (size_t)(h0 * Wl + w0) * rowstride;
           v1 = to_f32(value[o]);
-          if (far0) atomicAdd(gvalue + o, hh * hw * ga);
+          atomicAdd(gvalue + o, hh * hw * ga);
         }
         if (h0 >= 0 && w0 + 1 <= Wl - 1) {
           const size_t o = lbase + (size_t)(h0 * Wl + w0 + 1) * rowstride;
           v2 = to_f32(value[o]);
-          if (far0) atomicAdd(gvalue + o, hh * lw * ga);
+          atomicAdd(gvalue + o, hh * lw * ga);
         }
         if (h0 + 1 <= Hl - 1 && w0 >= 0) {
           const size_t o = lbase + (size_t)((h0 + 1) * Wl + w0) * rowstride;
           v3 = to_f32(value[o]);
-          if (far1) atomicAdd(gvalue + o, lh * hw * ga);
+          atomicAdd(gvalue + o, lh * hw * ga);
         }
         if (h0 + 1 <= Hl - 1 && w0 + 1 <= Wl - 1) {
           const size_t o = lbase + (size_t)((h0 + 1) * Wl + w0 + 1) * rowstride;
           v4 = to_f32(value[o]);
-          if (far1) atomicAdd(gvalue + o, lh * lw * ga);
+          atomicAdd(gvalue + o, lh * lw * ga);
         }
         const float val = hh * hw * v1 + hh * lw * v2 + lh * hw * v3 + lh * lw * v4;
         r_w = g * val;
@@ -327,10 +327,12 @@ __global__ void __launch_bounds__(256) msda_bwd_geom_kernel(
 
 constexpr int kScatterRun = 32;        // queries per half-wave run (LDS staging is sized for it)
 
-template <typename T, int L, int P>
+// ENC (encoder mode, Q == S level-major): taps owned by the pull kernel (pull_tap) are
+// skipped here; the pull kernel has already written every grad_value element.
+template <typename T, int L, int P, bool ENC>
 __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
     const float* __restrict__ loc, const float* __restrict__ attw, const T* __restrict__ gout,
-    float* __restrict__ gvalue, Levels lv, int S, int Hh, int Q, int R, int nrun, long long halfwaves) {
+    float* __restrict__ gvalue, Levels lv, int S, int Hh, int Q, int R, int nrun, long long halfwaves, int R0) {
   constexpr int LP = L * P;
   // per half-wave staging: loc [R][LP][2], attn [R][LP], grad_out [R][32] (f32)
   constexpr int kStage = kScatterRun * (LP * 3 + kD);
@@ -376,6 +378,13 @@ __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
   };
   for (int i = 0; i < nq; ++i) {
     const float g = sg[i * kD + c];
+    int lq = 0, yq = 0, xq = 0;
+    if (ENC) {
+      const int q = q0 + i;
+      while (lq + 1 < L && q >= lv.start[lq + 1]) ++lq;
+      yq = (q - lv.start[lq]) / lv.w[lq];
+      xq = (q - lv.start[lq]) % lv.w[lq];
+    }
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       const int Hl = lv.h[l], Wl = lv.w[l];
@@ -385,6 +394,7 @@ __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
         const int t = l * P + p;
         const Tap tg = tap_geom(sl[(i * LP + t) * 2 + 0], sl[(i * LP + t) * 2 + 1], Hl, Wl);
         if (!tg.inside) continue;             // no contribution; the held block stays
+        if (ENC && pull_tap(tg, lq, l, mapped_cell(yq, lv.h[lq], Hl), mapped_cell(xq, lv.w[lq], Wl), R0)) continue;
         const float ga = g * sw[i * LP + t];
         const int dy = tg.h0 - ph[t], dx = tg.w0 - pw[t];
         // held corner k = (cy, cx) survives iff (cy - dy, cx - dx) lies in the new block
@@ -421,94 +431,116 @@ __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
   }
 }
 
-// grad_value by destination band (encoder mode).  One workgroup = (band of kBandRows
-// rows of level lb, head h, image b); the band's [rows][W][32] f32 accumulator lives in
-// LDS.  The workgroup scans every query (of every level) whose mapped row on level lb
-// lies within kBandR of the band, evaluates its taps on level lb, and adds the corners
-// that fall in the band AND are `near` their query (the complement of the query
-// kernel's far set) with LDS float atomics; the band is then written with plain
-// coalesced stores.  Waves walk queries; lane = channel; 2 queries per wave.
+// grad_value by destination (encoder mode; see the header).  Block = (16x16 cell tile
+// of level l, head, image), wave w = cell rows 4w..4w+3 of the tile, lane = one cell.
+// For each source level lq the wave enumerates the rectangle of queries whose mapped
+// cell on level l lies in [region - R0 - 1, region + R0] (both axes), 64 at a time:
+// every lane stages one query's 4 taps on level l (top-left cell packed, fractions,
+// attention weight; non-near taps get a sentinel cell) and its grad_out row (f32) in LDS,
+// then every lane walks the 64 x 4 staged taps and accumulates those whose 2x2 corner
+// block contains its cell.
 template <typename T>
-__global__ void __launch_bounds__(kBandThreads) msda_bwd_band_kernel(
-    const float* __restrict__ loc, const float* __restrict__ attw, const T* __restrict__ gout,
-    float* __restrict__ gvalue, Levels lv, int S, int Hh, int L, int P, int band_rows) {
-  extern __shared__ __attribute__((aligned(16))) float sacc[];
-  // decode (level, band) from blockIdx.x
-  int bx = blockIdx.x, lb = 0;
-  while (lb + 1 < L && bx >= (lv.h[lb] + band_rows - 1) / band_rows) { bx -= (lv.h[lb] + band_rows - 1) / band_rows; ++lb; }
-  const int h = blockIdx.y;
-  const long long b = blockIdx.z;
-  const int Hl = lv.h[lb], Wl = lv.w[lb];
-  const int y0 = bx * band_rows;
-  const int y1 = min(Hl, y0 + band_rows);  // exclusive
-  const int nrows = y1 - y0;
+__global__ void __launch_bounds__(256) msda_bwd_pull_kernel(const float* __restrict__ loc,
+                                                            const float* __restrict__ attw,
+                                                            const T* __restrict__ gout, float* __restrict__ gvalue,
+                                                            Levels lv, int S, int Hh, int L, int R0, int tiles0,
+                                                            int tiles1, int tiles2) {
+  constexpr int P = 4;
+  __shared__ int sCell[4][64][P];
+  __shared__ float4 sW[4][64][P / 2];               // (lh, lw) pairs per tap, 2 taps per float4
+  __shared__ float sA[4][64][P];
+  __shared__ __attribute__((aligned(16))) float sG[4][64][kD];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = blockIdx.y, b = blockIdx.z;
+  // tile -> (level, tile row, tile col)
+  int t = blockIdx.x, l = 0;
+  const int tl[3] = {tiles0, tiles1, tiles2};
+  while (l < L - 1 && l < 3 && t >= tl[l]) { t -= tl[l]; ++l; }
+  const int Hl = lv.h[l], Wl = lv.w[l];
+  const int tx_n = (Wl + 15) / 16;
+  const int y0 = (t / tx_n) * 16 + wave * kPullRows, x0 = (t % tx_n) * 16;
+  const int cy = y0 + lane / kPullCols, cx = x0 + lane % kPullCols;
   const int LP = L * P;
-  for (int i = threadIdx.x; i < nrows * Wl * kD; i += blockDim.x) sacc[i] = 0.f;
-  __syncthreads();
-  const int c = threadIdx.x & 31;
-  const int slot = threadIdx.x >> 5;          // 16 query slots per workgroup
-  constexpr int kSlots = kBandThreads / 32;
-  for (int lq = 0; lq < L; ++lq) {
+  float acc[kD];
+#pragma unroll
+  for (int c = 0; c < kD; ++c) acc[c] = 0.f;
+  int* cell = &sCell[wave][0][0];
+  float4* wts = &sW[wave][0][0];
+  float* aw = &sA[wave][0][0];
+  float* gg = &sG[wave][0][0];
+  for (int lq = 0; lq <= l; ++lq) {           // source levels not finer than l
     const int Hq = lv.h[lq], Wq = lv.w[lq];
-    // query rows whose mapped row m satisfies y0-R-1 <= m <= y1-1+R (m monotone in yq)
-    int ylo = 0, yhi = -1;
-    {
-      int lo = Hq, hi = -1;
-      for (int yq = 0; yq < Hq; ++yq) {
-        const int m = mapped_row(yq, Hq, Hl);
-        if (m >= y0 - kBandR - 1 && m <= y1 - 1 + kBandR) { lo = min(lo, yq); hi = max(hi, yq); }
+    // query rectangle: mapped cell within [y0 - R0 - 1, y0 + rows - 1 + R0] x [...]
+    const int lo_y = y0 - R0 - 1, hi_y = y0 + kPullRows - 1 + R0;
+    const int lo_x = x0 - R0 - 1, hi_x = x0 + kPullCols - 1 + R0;
+    int ya, yb, xa, xb;
+    mapped_range(lo_y, hi_y, Hq, Hl, &ya, &yb);
+    mapped_range(lo_x, hi_x, Wq, Wl, &xa, &xb);
+    if (ya > yb || xa > xb) continue;
+    const int nx = xb - xa + 1;
+    const int ncand = (yb - ya + 1) * nx;
+    for (int base = 0; base < ncand; base += 64) {
+      const int i = base + lane;
+      if (i < ncand) {
+        const int yq = ya + i / nx, xq = xa + i % nx;
+        const long long grp = ((long long)b * S + lv.start[lq] + yq * Wq + xq) * Hh + h;
+        const int mcy = mapped_cell(yq, Hq, Hl), mcx = mapped_cell(xq, Wq, Wl);
+        const float4* lp4 = reinterpret_cast<const float4*>(loc + (grp * LP + l * P) * 2);
+        const float4 a4 = *reinterpret_cast<const float4*>(attw + grp * LP + l * P);
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+        for (int pp = 0; pp < P / 2; ++pp) {
+          const float4 xy = lp4[pp];
+          const Tap t0 = tap_geom(xy.x, xy.y, Hl, Wl);
+          const Tap t1 = tap_geom(xy.z, xy.w, Hl, Wl);
+          cell[lane * P + 2 * pp] = pull_tap(t0, lq, l, mcy, mcx, R0) ? ((t0.h0 << 16) | (t0.w0 & 0xffff)) : (int)0x80008000;
+          cell[lane * P + 2 * pp + 1] = pull_tap(t1, lq, l, mcy, mcx, R0) ? ((t1.h0 << 16) | (t1.w0 & 0xffff)) : (int)0x80008000;
+          wts[lane * 2 + pp] = make_float4(t0.lh, t0.lw, t1.lh, t1.lw);
+        }
+#pragma unroll
+        for (int pp = 0; pp < P; ++pp) aw[lane * P + pp] = av[pp];
+        float gv[kD];
+        constexpr int V = Vec16<T>::N;
+#pragma unroll
+        for (int c = 0; c < kD; c += V) Vec16<T>::load(gout + grp * kD + c, gv + c);
+#pragma unroll
+        for (int c = 0; c < kD; c += 4)
+          *reinterpret_cast<float4*>(gg + lane * kD + c) = make_float4(gv[c], gv[c + 1], gv[c + 2], gv[c + 3]);
       }
-      ylo = lo; yhi = hi;
-    }
-    if (yhi < ylo) continue;
-    const int nq = (yhi - ylo + 1) * Wq;
-    const int qbase = lv.start[lq] + ylo * Wq;
-    for (int q0 = slot * kBandUnroll; q0 < nq; q0 += kSlots * kBandUnroll) {
-      float4 la[kBandUnroll], lb4[kBandUnroll], wv[kBandUnroll];
-      float gg[kBandUnroll];
-      int mm[kBandUnroll];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int cnt = min(64, ncand - base);
+      for (int j = 0; j < cnt; ++j) {
 #pragma unroll
-      for (int u = 0; u < kBandUnroll; ++u) {
-        const int qi = min(q0 + u, nq - 1);
-        const int q = qbase + qi;
-        mm[u] = mapped_row(ylo + qi / Wq, Hq, Hl);
-        const long long grp = (b * S + q) * Hh + h;
-        const float4* lp4 = reinterpret_cast<const float4*>(loc + grp * LP * 2 + lb * P * 2);
-        la[u] = lp4[0];
-        lb4[u] = lp4[1];
-        wv[u] = *reinterpret_cast<const float4*>(attw + grp * LP + lb * P);
-        gg[u] = (q0 + u < nq) ? to_f32(gout[grp * kD + c]) : 0.f;
-      }
+        for (int pp = 0; pp < P; ++pp) {
+          const int packed = cell[j * P + pp];
+          const int dy = cy - (packed >> 16), dx = cx - (short)(packed & 0xffff);
+          if ((unsigned)dy <= 1u && (unsigned)dx <= 1u) {
+            const float4 w4 = wts[j * 2 + (pp >> 1)];
+            const float lh = (pp & 1) ? w4.z : w4.x, lw = (pp & 1) ? w4.w : w4.y;
+            const float wgt = (dy ? lh : 1.f - lh) * (dx ? lw : 1.f - lw) * aw[j * P + pp];
+            const float4* g4 = reinterpret_cast<const float4*>(gg + j * kD);
 #pragma unroll
-      for (int u = 0; u < kBandUnroll; ++u) {
-        const float xs[4] = {la[u].x, la[u].z, lb4[u].x, lb4[u].z};
-        const float ys[4] = {la[u].y, la[u].w, lb4[u].y, lb4[u].w};
-        const float ws4[4] = {wv[u].x, wv[u].y, wv[u].z, wv[u].w};
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const Tap t = tap_geom(xs[p], ys[p], Hl, Wl);
-          if (!t.inside) continue;
-          const float ga = gg[u] * ws4[p];
-          const int h0 = t.h0, w0 = t.w0;
-#pragma unroll
-          for (int dy = 0; dy < 2; ++dy) {
-            const int cy = h0 + dy;
-            if (cy < y0 || cy >= y1 || cy > Hl - 1 || !near_row(cy, mm[u])) continue;
-            const float wy = dy ? t.lh : t.hh;
-            float* row = sacc + ((cy - y0) * Wl) * kD + c;
-            if (w0 >= 0) atomicAdd(row + w0 * kD, wy * t.hw * ga);
-            if (w0 + 1 <= Wl - 1) atomicAdd(row + (w0 + 1) * kD, wy * t.lw * ga);
+            for (int c = 0; c < kD / 4; ++c) {
+              const float4 v = g4[c];
+              acc[4 * c + 0] = fmaf(wgt, v.x, acc[4 * c + 0]);
+              acc[4 * c + 1] = fmaf(wgt, v.y, acc[4 * c + 1]);
+              acc[4 * c + 2] = fmaf(wgt, v.z, acc[4 * c + 2]);
+              acc[4 * c + 3] = fmaf(wgt, v.w, acc[4 * c + 3]);
+            }
           }
         }
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
-  __syncthreads();
-  const size_t rowstride = (size_t)Hh * kD;
-  float* dst = gvalue + ((size_t)b * S * Hh + h) * kD + (size_t)(lv.start[lb] + y0 * Wl) * rowstride;
-  for (int i = threadIdx.x; i < nrows * Wl * kD; i += blockDim.x) {
-    const int px = i / kD, cc = i - px * kD;
-    dst[(size_t)px * rowstride + cc] = sacc[i];
+  if (cy < Hl && cx < Wl) {
+    float4* dst = reinterpret_cast<float4*>(gvalue + (((size_t)b * S + lv.start[l] + cy * Wl + cx) * Hh + h) * kD);
+#pragma unroll
+    for (int c = 0; c < kD / 4; ++c) dst[c] = make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
   }
 }
 
@@ -558,6 +590,44 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
   return VS_OK;
 }
 
+static void launch_geom(int dtype, const void* value, const float* loc, const float* attw, const void* gout,
+                        float* gloc, float* gattw, const Levels& lv, int S, int Hh, int Q, int L, int P,
+                        long long groups, hipStream_t st) {
+  const int lpg = dtype == VS_BF16 ? 4 : 8;
+  const int ggrid = (int)((groups * lpg + 255) / 256);
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(msda_bwd_geom_kernel<bf16>, dim3(ggrid), dim3(256), 0, st, (const bf16*)value, loc, attw,
+                       (const bf16*)gout, gloc, gattw, lv, S, Hh, Q, L, P, groups);
+  else
+    hipLaunchKernelGGL(msda_bwd_geom_kernel<float>, dim3(ggrid), dim3(256), 0, st, (const float*)value, loc, attw,
+                       (const float*)gout, gloc, gattw, lv, S, Hh, Q, L, P, groups);
+}
+
+template <bool ENC>
+static void launch_scatter(int dtype, const float* loc, const float* attw, const void* gout, float* gvalue,
+                           const Levels& lv, int B, int S, int Hh, int Q, int L, int run, int R0, hipStream_t st) {
+  const int nrun = (Q + run - 1) / run;
+  const long long hws = (long long)B * nrun * Hh;
+  const int sgrid = (int)((hws + 7) / 8);
+#define VS_SCATTER(TT, LL)                                                                                   \
+  hipLaunchKernelGGL((msda_bwd_scatter_kernel<TT, LL, 4, ENC>), dim3(sgrid), dim3(256), 0, st, loc, attw,     \
+                     (const TT*)gout, gvalue, lv, S, Hh, Q, run, nrun, hws, R0)
+#define VS_SCATTER_L(TT)                \
+  switch (L) {                          \
+    case 1: VS_SCATTER(TT, 1); break;   \
+    case 2: VS_SCATTER(TT, 2); break;   \
+    case 3: VS_SCATTER(TT, 3); break;   \
+    default: VS_SCATTER(TT, 4); break;  \
+  }
+  if (dtype == VS_BF16) {
+    VS_SCATTER_L(bf16)
+  } else {
+    VS_SCATTER_L(float)
+  }
+#undef VS_SCATTER_L
+#undef VS_SCATTER
+}
+
 static int msda_backward_impl(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
                               const float* loc, const float* attw, const void* gout, float* gvalue, float* gloc,
                               float* gattw, int B, int S, int Hh, int D, int L, int Q, int P, void* stream,
@@ -566,42 +636,43 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   VS_CHECK(L >= 1 && L <= kMaxLevels, "1..4 levels supported");
   VS_CHECK(B > 0 && S > 0 && Hh > 0 && Q >= 0 && P > 0, "bad sizes");
   VS_CHECK(value && loc && attw && gout && gvalue && gloc && gattw && shapes && starts, "null pointer");
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   Levels lv;
   VS_CHECK(fill_levels(&lv, shapes, starts, L, S), "spatial shapes / level starts inconsistent with S");
   VS_CHECK(!encoder || Q == S, "encoder mode needs the queries to be the value grid (Q == S)");
   VS_CHECK(!encoder || P == 4, "encoder-mode backward is specialised for 4 sampling points");
   hipStream_t st = (hipStream_t)stream;
   const long long groups = (long long)B * Q * Hh;
-  const int block = 256;
-  const long long threads = groups * 32;
-  const int grid = (int)((threads + block - 1) / block);
   if (encoder) {
-    int maxw = 0, bands = 0;
-    for (int l = 0; l < L; ++l) maxw = max(maxw, lv.w[l]);
-    const int band_rows = min(kBandMaxRows, (int)((160 * 1024) / ((size_t)maxw * kD * sizeof(float))));
-    VS_CHECK(band_rows >= 1, "level too wide for the band kernel");
-    for (int l = 0; l < L; ++l) bands += (lv.h[l] + band_rows - 1) / band_rows;
-    const size_t lds = (size_t)band_rows * maxw * kD * sizeof(float);
-    dim3 bgrid(bands, Hh, B);
-    if (dtype == VS_BF16) {
-      hipLaunchKernelGGL(msda_bwd_band_kernel<bf16>, bgrid, dim3(kBandThreads), lds, st, loc, attw, (const bf16*)gout,
-                         gvalue, lv, S, Hh, L, P, band_rows);
-      hipLaunchKernelGGL((msda_bwd_kernel<bf16, true>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, attw,
-                         (const bf16*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
-    } else if (dtype == VS_F32) {
-      hipLaunchKernelGGL(msda_bwd_band_kernel<float>, bgrid, dim3(kBandThreads), lds, st, loc, attw,
-                         (const float*)gout, gvalue, lv, S, Hh, L, P, band_rows);
-      hipLaunchKernelGGL((msda_bwd_kernel<float, true>), dim3(grid), dim3(block), 0, st, (const float*)value, loc,
-                         attw, (const float*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
-    } else {
-      VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
+    // pull (plain stores of every grad_value element: the taps of coarser-or-equal query
+    // levels landing within R0 cells), then the carry scatter adds every other tap, and
+    // the geom kernel computes grad_loc / grad_attn
+    int R0 = kPullR;
+    if (const char* e = getenv("VS_MSDA_PULL_R")) R0 = atoi(e);
+    VS_CHECK(R0 >= 0 && R0 <= 64, "VS_MSDA_PULL_R out of range");
+    int tiles[4] = {0, 0, 0, 0}, ntiles = 0;
+    for (int l = 0; l < L; ++l) {
+      tiles[l] = ((lv.h[l] + 15) / 16) * ((lv.w[l] + 15) / 16);
+      ntiles += tiles[l];
     }
+    // VS_MSDA_SKIP (profiling only): bit 0 skips the pull, bit 1 the scatter, bit 2 geom
+    int skip = 0;
+    if (const char* e = getenv("VS_MSDA_SKIP")) skip = atoi(e);
+    if (!(skip & 1)) {
+      if (dtype == VS_BF16)
+        hipLaunchKernelGGL(msda_bwd_pull_kernel<bf16>, dim3(ntiles, Hh, B), dim3(256), 0, st, loc, attw,
+                           (const bf16*)gout, gvalue, lv, S, Hh, L, R0, tiles[0], tiles[1], tiles[2]);
+      else
+        hipLaunchKernelGGL(msda_bwd_pull_kernel<float>, dim3(ntiles, Hh, B), dim3(256), 0, st, loc, attw,
+                           (const float*)gout, gvalue, lv, S, Hh, L, R0, tiles[0], tiles[1], tiles[2]);
+    }
+    if (!(skip & 2)) launch_scatter<true>(dtype, loc, attw, gout, gvalue, lv, B, S, Hh, Q, L, kScatterRun, R0, st);
+    if (!(skip & 4)) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
   VS_HIP(hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * Hh * kD, st));
   if (Q == 0) return VS_OK;
-  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   // geom + register-carry scatter when there are enough queries for runs to fill the chip
   // (VS_MSDA_RUN=n forces runs of n <= 32 queries at any size, 0 the single kernel)
   int run = kScatterRun;
@@ -612,46 +683,18 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   }
   if (split && P == 4) {
     VS_CHECK(run <= kScatterRun, "VS_MSDA_RUN must be <= 32");
-    const int lpg = dtype == VS_BF16 ? 4 : 8;
-    const int ggrid = (int)((groups * lpg + block - 1) / block);
-    if (dtype == VS_BF16)
-      hipLaunchKernelGGL(msda_bwd_geom_kernel<bf16>, dim3(ggrid), dim3(block), 0, st, (const bf16*)value, loc,
-                         attw, (const bf16*)gout, gloc, gattw, lv, S, Hh, Q, L, P, groups);
-    else
-      hipLaunchKernelGGL(msda_bwd_geom_kernel<float>, dim3(ggrid), dim3(block), 0, st, (const float*)value, loc,
-                         attw, (const float*)gout, gloc, gattw, lv, S, Hh, Q, L, P, groups);
-    const int nrun = (Q + run - 1) / run;
-    const long long hws = (long long)B * nrun * Hh;
-    const int sgrid = (int)((hws + 7) / 8);
-#define VS_SCATTER(TT, LL)                                                                                 \
-  hipLaunchKernelGGL((msda_bwd_scatter_kernel<TT, LL, 4>), dim3(sgrid), dim3(block), 0, st, loc, attw,      \
-                     (const TT*)gout, gvalue, lv, S, Hh, Q, run, nrun, hws)
-#define VS_SCATTER_L(TT)                \
-  switch (L) {                          \
-    case 1: VS_SCATTER(TT, 1); break;   \
-    case 2: VS_SCATTER(TT, 2); break;   \
-    case 3: VS_SCATTER(TT, 3); break;   \
-    default: VS_SCATTER(TT, 4); break;  \
-  }
-    if (dtype == VS_BF16) {
-      VS_SCATTER_L(bf16)
-    } else {
-      VS_SCATTER_L(float)
-    }
-#undef VS_SCATTER_L
-#undef VS_SCATTER
+    launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
+    launch_scatter<false>(dtype, loc, attw, gout, gvalue, lv, B, S, Hh, Q, L, run, 0, st);
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
-  if (dtype == VS_BF16) {
-    hipLaunchKernelGGL((msda_bwd_kernel<bf16, false>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, attw,
+  const int grid = (int)((groups * 32 + 255) / 256);
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL((msda_bwd_kernel<bf16>), dim3(grid), dim3(256), 0, st, (const bf16*)value, loc, attw,
                        (const bf16*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
-  } else if (dtype == VS_F32) {
-    hipLaunchKernelGGL((msda_bwd_kernel<float, false>), dim3(grid), dim3(block), 0, st, (const float*)value, loc,
-                       attw, (const float*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
-  } else {
-    VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
-  }
+  else
+    hipLaunchKernelGGL((msda_bwd_kernel<float>), dim3(grid), dim3(256), 0, st, (const float*)value, loc, attw,
+                       (const float*)gout, gvalue, gloc, gattw, lv, S, Hh, Q, L, P, groups);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

@@ -241,7 +241,10 @@ class MSDeformAttn(nn.Module):
     def __init__(self, d, heads, levels, points):
         super().__init__()
         self.d, self.heads, self.levels, self.points = d, heads, levels, points
-        self.band_backward = False   # opt-in destination-band grad_value (see csrc/msda.hip)
+        # True: encoder-mode backward (destination pull + carry scatter, csrc/msda.hip);
+        # measured slower than the general register-carry path at C2 (3.0 vs 2.0 ms per
+        # layer), so opt-in
+        self.encoder_backward = False
         self.sampling_offsets = TokenLinear(d, heads * levels * points * 2)
         self.attention_weights = TokenLinear(d, heads * levels * points)
         self.value_proj = TokenLinear(d, d)
@@ -255,7 +258,7 @@ class MSDeformAttn(nn.Module):
         aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
         aw = F.softmax(aw.float(), -1).view(B, S, self.heads, self.levels, self.points)
         loc = ref[:, :, None, :, None, :] + off.float() / norm           # HF:m2f:994-1002
-        out = ops.ms_deform_attn(value, shapes, loc, aw, encoder=self.band_backward)
+        out = ops.ms_deform_attn(value, shapes, loc, aw, encoder=self.encoder_backward)
         return self.output_proj(out)
 
 

@@ -64,7 +64,7 @@ class MSDeformAttnFunction(torch.autograd.Function):
             L.check(L.lib().vs_msda_forward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
                                             L.ptr(out), B, S, H, D, Lv, Q, P, L.stream(value)), "msda_forward")
         ctx.shapes = shapes
-        ctx.encoder = bool(encoder) and Q == S
+        ctx.encoder = bool(encoder) and Q == S and P == 4
         ctx.save_for_backward(value, loc, aw)
         return out
 
