@@ -46,6 +46,14 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return __f
 // bf16 bit pattern <-> f32 without a library call (exact widening).
 __device__ __forceinline__ float bf16_bits_to_f32(uint32_t u16) { return __uint_as_float(u16 << 16); }
 
+// XCD-aware workgroup remap (cdna_hip_programming.md T1, bijective form): the dispatcher
+// round-robins consecutive workgroups over the 8 XCDs, each with its own L2; this gives
+// every XCD a contiguous range of logical workgroup ids instead.  Speed only.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 // 16-byte vector of T (8 bf16 or 4 f32) loaded/stored in one instruction.
 template <typename T> struct Vec16;
 template <> struct Vec16<float> {

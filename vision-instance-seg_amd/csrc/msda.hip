@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ val
                                                         long long groups) {
   constexpr int V = Vec16<T>::N;       // channels per lane
   constexpr int LPG = kD / V;          // lanes per group
-  long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long gid = (long long)xcd_swizzle(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   long long stride = (long long)gridDim.x * blockDim.x;
   const int LP = L * P;
   for (; gid < groups * LPG; gid += stride) {
@@ -267,11 +267,17 @@ __global__ void __launch_bounds__(256) msda_bwd_geom_kernel(
     int Hh, int Q, int L, int P, long long groups) {
   constexpr int V = Vec16<T>::N;       // channels per lane
   constexpr int LPG = kD / V;          // lanes per group (4 bf16, 8 f32), a power of two
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int kGroups = 256 / LPG;   // groups per workgroup (consecutive)
+  constexpr int kMaxLP = 16;
+  __shared__ float s_w[kGroups * kMaxLP], s_xy[kGroups * kMaxLP * 2];
+  const long long blk = xcd_swizzle(blockIdx.x, gridDim.x);
+  const long long gid = blk * blockDim.x + threadIdx.x;
+  const long long grp0 = blk * kGroups;
   const long long grp = gid / LPG;
   const int sub = (int)(gid % LPG);
-  if (grp >= groups) return;           // groups are aligned to LPG lanes: uniform per group
   const int LP = L * P;
+  const bool staged = LP <= kMaxLP;    // outputs staged in LDS and written coalesced
+  if (grp < groups) {
   const int h = (int)(grp % Hh);
   const long long b = grp / Hh / Q;
   const float* lp = loc + grp * LP * 2;
@@ -317,11 +323,25 @@ __global__ void __launch_bounds__(256) msda_bwd_geom_kernel(
         r_y += __shfl_xor(r_y, s, LPG);
       }
       if (sub == 0) {
-        gattw[grp * LP + t] = r_w;
-        gloc[(grp * LP + t) * 2 + 0] = r_x;
-        gloc[(grp * LP + t) * 2 + 1] = r_y;
+        if (staged) {
+          const int gl = (int)(grp - grp0);
+          s_w[gl * LP + t] = r_w;
+          s_xy[(gl * LP + t) * 2 + 0] = r_x;
+          s_xy[(gl * LP + t) * 2 + 1] = r_y;
+        } else {
+          gattw[grp * LP + t] = r_w;
+          gloc[(grp * LP + t) * 2 + 0] = r_x;
+          gloc[(grp * LP + t) * 2 + 1] = r_y;
+        }
       }
     }
+  }
+  }
+  if (staged) {
+    __syncthreads();
+    const int ng = (int)min((long long)kGroups, groups - grp0);
+    for (int i = threadIdx.x; i < ng * LP; i += 256) gattw[grp0 * LP + i] = s_w[i];
+    for (int i = threadIdx.x; i < ng * LP * 2; i += 256) gloc[grp0 * LP * 2 + i] = s_xy[i];
   }
 }
 
