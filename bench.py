@@ -75,6 +75,38 @@ def parse():
     return ap.parse_args()
 
 
+# HBM traffic per op launch from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; KiB,
+# FETCH x2 on gfx950 -- tools/pmc_traffic.py), committed under profiles/; the kernels
+# each timed op dispatches once per launch
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+OP_KERNELS = {
+    "msda_bwd": ["msda_bwd_geom_kernel", "msda_bwd_scatter_kernel"],
+    "msda_fwd": ["msda_fwd_kernel"],
+    "window_attn_fwd": ["win_attn_fwd_mfma"],
+    "window_attn_bwd": ["win_attn_bwd_mfma"],
+    "mask_head_fwd": ["mask_head_fwd_kernel"],
+    "mask_head_bwd": ["mask_head_bwd_kernel", "mask_head_bwd_reduce"],
+    "masked_attn_fwd": ["xattn_fwd_mfma", "xattn_fwd_combine"],
+    "masked_attn_bwd": ["xattn_bwd_prep", "xattn_bwd_mfma", "xattn_bwd_dq_combine"],
+}
+
+
+def pmc_traffic(op):
+    """(bytes per launch, kernels counted) of `op` from the committed PMC profile, or None."""
+    if op not in OP_KERNELS or not os.path.exists(PMC_FILE):
+        return None, None
+    rows = json.load(open(PMC_FILE))
+    tot, used = 0.0, []
+    for pat in OP_KERNELS[op]:
+        hits = [(k, v) for k, v in rows.items() if pat + "<" in k or pat + "(" in k]
+        if not hits:
+            return None, None
+        for k, v in hits:
+            tot += v["fetch_bytes"] + v["write_bytes"]
+            used.append(k.split("(")[0][:80])
+    return int(tot), used
+
+
 def kernel_roofline(summary):
     """Pick the hand-written kernel with the largest total time and price it against the
     roofline of its regime (HBM bytes for gather/copy kernels, matrix FLOP/s otherwise)."""
@@ -86,14 +118,18 @@ def kernel_roofline(summary):
     hbm_kernels = {"msda_fwd", "msda_bwd", "window_partition", "window_reverse", "attn_bitmask", "mask_head_fwd"}
     if name in hbm_kernels:
         ach = s["bytes"] / t / 1e9
+        traffic, kernels = pmc_traffic(name)
         roof = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=None, kernel=name,
+                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, kernel=name,
+                    traffic_source=(f"profiles/{os.path.basename(PMC_FILE)}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) "
+                                    f"+ WRITE_SIZE per launch of {kernels}") if traffic else None,
                     algorithmic_bytes_per_launch=int(s["bytes"]), mean_launch_ms=round(s["mean_ms"], 4),
                     launches=s["launches"])
     else:
         ach = s["flops"] / t / 1e12
+        traffic, kernels = pmc_traffic(name)
         roof = dict(bound="mfma", achieved=round(ach, 2), peak=MFMA_BF16_PEAK_TFS, unit="TFLOP/s",
-                    frac=round(ach / MFMA_BF16_PEAK_TFS, 5), traffic=None, kernel=name,
+                    frac=round(ach / MFMA_BF16_PEAK_TFS, 5), traffic=traffic, kernel=name,
                     algorithmic_flops_per_launch=int(s["flops"]), mean_launch_ms=round(s["mean_ms"], 4),
                     launches=s["launches"])
     table = {k: dict(launches=v["launches"], total_ms=round(v["total_ms"], 3), mean_ms=round(v["mean_ms"], 4),
