@@ -17,8 +17,10 @@ import torch.nn.functional as F
 
 from . import ops
 
+import os
+
 # split when K is at least this many tokens; chunks never drop below MIN_CHUNK rows
-MIN_TOKENS = 32768
+MIN_TOKENS = int(os.environ.get("VS_SPLITK_MIN_TOKENS", "16384"))
 MIN_CHUNK = 1024
 TARGET_TILES = 768          # aim for this many 128x128 output tiles over all chunks
 
@@ -82,16 +84,20 @@ class TokenLayerNorm(nn.LayerNorm):
         return F.layer_norm(x, self.normalized_shape, self.weight, self.bias, self.eps)
 
 
+def linear_tokens(x, w, b=None):
+    """F.linear with the split-K weight gradient when x carries many tokens."""
+    tokens = x.numel() // max(1, x.shape[-1])
+    if not (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and tokens >= MIN_TOKENS):
+        return F.linear(x, w, b)
+    if torch.is_autocast_enabled():
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return _LinearFn.apply(x.to(dt), w.to(dt), None if b is None else b.to(dt))
+    return _LinearFn.apply(x, w, b)
+
+
 class TokenLinear(nn.Linear):
     """nn.Linear whose backward splits the token axis of dW (see module docstring)."""
 
     def forward(self, x):
-        tokens = x.numel() // max(1, x.shape[-1])
-        if not (x.is_cuda and torch.is_grad_enabled() and self.weight.requires_grad and tokens >= MIN_TOKENS):
-            return F.linear(x, self.weight, self.bias)
-        w, b = self.weight, self.bias
-        if torch.is_autocast_enabled():
-            dt = torch.get_autocast_dtype("cuda")
-            with torch.autocast("cuda", enabled=False):
-                return _LinearFn.apply(x.to(dt), w.to(dt), None if b is None else b.to(dt))
-        return _LinearFn.apply(x, w, b)
+        return linear_tokens(x, self.weight, self.bias)

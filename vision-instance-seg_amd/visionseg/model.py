@@ -27,7 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .linear import TokenLayerNorm, TokenLinear
+from .linear import TokenLayerNorm, TokenLinear, linear_tokens
 
 
 @dataclass
@@ -360,13 +360,14 @@ class DecoderLayer(nn.Module):
         self.fc2 = nn.Linear(ffn, d)
         self.norm_ffn = nn.LayerNorm(d)
 
-    def forward(self, h, qpos, mem, mpos, words):
+    def forward(self, h, qpos, mem, mem_pos, words):
+        """mem: level memory [B, hw, D] (contiguous), mem_pos = mem + its position embedding."""
         B, Q, D = h.shape
         H, d = self.heads, D // self.heads
         W, b = self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias
         q = F.linear(h + qpos, W[:D], b[:D])
-        k = F.linear(mem + mpos, W[D:2 * D], b[D:2 * D])
-        v = F.linear(mem, W[2 * D:], b[2 * D:])
+        k = linear_tokens(mem_pos, W[D:2 * D], b[D:2 * D])
+        v = linear_tokens(mem, W[2 * D:], b[2 * D:])
         o = ops.masked_attention(q, k, v, words, H, d ** -0.5)
         h = self.norm_cross(h + self.cross_attn.out_proj(o))
         sa = self.self_attn
@@ -410,12 +411,15 @@ class Decoder(nn.Module):
         B, _, Hm, Wm = mask_features.shape
         dev = mask_features.device
         mf = mask_features.to(_compute_dtype(mask_features)).permute(0, 2, 3, 1).reshape(B, Hm * Wm, -1).contiguous()
-        mems, mposs, sizes = [], [], []
+        mems, mem_pos, sizes = [], [], []
         for i in range(3):
+            # once per level (shared by the decoder rounds): token-major memory and memory + pos
             f = ms_feats[i]
             sizes.append((int(f.shape[2]), int(f.shape[3])))
-            mposs.append(sine_pos_embed(B, f.shape[2], f.shape[3], d // 2, dev).to(f.dtype).flatten(2).transpose(1, 2))
-            mems.append((f.flatten(2) + self.level_embed.weight[i][None, :, None].to(f.dtype)).transpose(1, 2))
+            pos = sine_pos_embed(B, f.shape[2], f.shape[3], d // 2, dev).to(f.dtype).flatten(2).transpose(1, 2)
+            m = (f.flatten(2) + self.level_embed.weight[i][None, :, None].to(f.dtype)).transpose(1, 2).contiguous()
+            mems.append(m)
+            mem_pos.append(m + pos)
         qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
         h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
         n = len(self.layers)
@@ -428,7 +432,7 @@ class Decoder(nn.Module):
                 self.trace.append(words)
             if self.mask_override is not None:
                 words = pack_bitmask(self.mask_override[idx].to(dev))
-            h = layer(h, qpos, mems[lvl], mposs[lvl], words)
+            h = layer(h, qpos, mems[lvl], mem_pos[lvl], words)
             nxt = sizes[(idx + 1) % 3] if idx + 1 < n else None
             inter, logits, words = self.predict(h, mf, Hm, Wm, nxt)
             inters.append(inter)
