@@ -57,14 +57,19 @@ class SetCriterion:
         kmax = max(1, max(int(t.shape[0]) for t in class_labels))
         cost = torch.zeros(S, B, Q, kmax, device=dev)
         probs = classes.float().softmax(-1)
+        # one uniform point set per image, shared by its queries and the S decoder steps:
+        # the queries are grid_sample CHANNELS, so one call per step samples all B x Q masks
+        P = c.train_num_points
+        grid = (2.0 * torch.rand(B, P, 2, device=dev) - 1.0).unsqueeze(2)              # [B,P,1,2]
+        pp_all = torch.stack([F.grid_sample(m.float(), grid, align_corners=False).squeeze(3)
+                              for m in masks_list])                                      # [S,B,Q,P]
         for i in range(B):
             K = int(class_labels[i].shape[0])
             if K == 0:
                 continue
-            # one uniform point set per image, shared by the S decoder steps
-            pts = torch.rand(1, c.train_num_points, 2, device=dev)
-            tp = _sample(mask_labels[i].float()[:, None], pts.expand(K, -1, -1))[None].expand(S, -1, -1)
-            pp = torch.stack([_sample(m[i].float()[:, None], pts.expand(Q, -1, -1)) for m in masks_list])  # [S,Q,P]
+            tp = F.grid_sample(mask_labels[i].float()[None], grid[i:i + 1], align_corners=False)
+            tp = tp.squeeze(3)[0][None].expand(S, -1, -1)                                  # [S,K,P]
+            pp = pp_all[:, i]                                                            # [S,Q,P]
             P = pp.shape[-1]
             pos = F.softplus(-pp)          # BCE(x, 1)
             neg = F.softplus(pp)           # BCE(x, 0)
