@@ -215,6 +215,22 @@ VS_API int vs_lsa_max_targets(int num_queries);
 VS_API int vs_lsa_batch(const float* cost, const int* targets_per_image, int num_steps, int batch,
                         int num_queries, int max_targets, int* assign, void* stream);
 
+/* ---- GroupNorm over channels-last activations (csrc/groupnorm.hip) -------------------
+ * The pixel decoder's Conv2d + GroupNorm(32) blocks (upstream MSDeformAttnPixelDecoder
+ * input projections / lateral / output convs; HF:m2f Mask2FormerPixelDecoder) on MIOpen's
+ * channels-last outputs.  x, y: [B, HW, C] (NHWC), groups of exactly 8 channels
+ * (C = 8 G); weight/bias [C] in dtype; mean/rstd f32 [B, G]; relu != 0 fuses a ReLU
+ * after the affine (the backward recomputes its mask from x).  torch.nn.functional.
+ * group_norm semantics (biased variance). */
+VS_API long long vs_group_norm_workspace_bytes(int batch, int hw, int channels, int groups);
+VS_API int vs_group_norm_forward(int dtype, const void* x, const void* weight, const void* bias, void* y,
+                                 float* mean, float* rstd, void* workspace, int batch, int hw, int channels,
+                                 int groups, float eps, int relu, void* stream);
+VS_API int vs_group_norm_backward(int dtype, const void* grad_y, const void* x, const void* weight,
+                                  const void* bias, const float* mean, const float* rstd, void* grad_x,
+                                  void* grad_weight, void* grad_bias, void* workspace, int batch, int hw,
+                                  int channels, int groups, int relu, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

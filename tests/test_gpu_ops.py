@@ -557,3 +557,45 @@ def test_masked_attention_bf16_fwd_bwd_vs_oracle(monkeypatch, kernel, B, Q, S):
     for got, exp in ((qd.grad, qr.grad), (kd.grad, kr.grad), (vd.grad, vr.grad)):
         e = float((got.float().cpu() - exp).abs().max())
         assert e <= 2e-2 * float(exp.abs().max()) + 1e-4, (e, float(exp.abs().max()))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("shape,groups,cl", [((2, 256, 64, 64), 32, True), ((2, 256, 17, 23), 32, True),
+                                             ((1, 64, 5, 7), 8, False), ((1, 256, 256, 256), 32, True)])
+def test_group_norm_nhwc_vs_torch(dtype, relu, shape, groups, cl):
+    """Channels-last GroupNorm (+ReLU) forward/backward (csrc/groupnorm.hip) vs torch f64.
+    With the ReLU, a pre-activation within rounding of 0 may be masked differently by
+    the kernel (f32 statistics) and the f64 reference: every such disagreement must sit at
+    |pre-activation| < 1e-4, and the gradients are compared against the reference using
+    the kernel's own mask (decisions separated from arithmetic)."""
+    ops = _ops()
+    B, C, H, W = shape
+    g = torch.Generator().manual_seed(C + H)
+    x = (torch.randn(shape, generator=g) * 2 + 0.3).to(dtype)
+    w = (1 + 0.2 * torch.randn(C, generator=g)).to(dtype)
+    b = (0.2 * torch.randn(C, generator=g)).to(dtype)
+    gy = torch.randn(shape, generator=g).to(dtype)
+    xd = x.to(DEV)
+    if cl:
+        xd = xd.contiguous(memory_format=torch.channels_last)
+    xd, wd, bd = xd.requires_grad_(True), w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    y = ops.group_norm_nhwc(xd, wd, bd, groups, 1e-5, relu)
+    y.backward(gy.to(DEV))
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+    pre = torch.nn.functional.group_norm(xr, groups, wr, br, 1e-5)
+    yr = pre
+    if relu:
+        mask = (y.detach().cpu() > 0)
+        ref_mask = pre.detach() > 0
+        flips = mask != ref_mask
+        if flips.any():
+            assert float(pre.detach()[flips].abs().max()) < 1e-4
+        yr = pre * mask.double()
+    yr.backward(gy.double())
+    tol = 3e-5 if dtype == torch.float32 else 2 ** -7
+    e = (y.detach().double().cpu() - (torch.relu(pre) if relu else pre).detach()).abs().max()
+    assert float(e) <= tol * max(1.0, float(pre.detach().abs().max()))
+    for name, got, exp in (("dx", xd.grad, xr.grad), ("dw", wd.grad, wr.grad), ("db", bd.grad, br.grad)):
+        e = float((got.detach().double().cpu() - exp.detach()).abs().max())
+        assert e <= tol * max(1.0, float(exp.detach().abs().max())), (name, e, float(exp.detach().abs().max()))

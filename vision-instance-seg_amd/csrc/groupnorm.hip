@@ -1,0 +1,366 @@
+// GroupNorm over channels-last activations (NHWC memory), forward + backward, optional
+// fused ReLU.
+//
+// The pixel decoder's ConvGN blocks (upstream MSDeformAttnPixelDecoder: Conv2d + GroupNorm
+// (32 groups), HF:m2f Mask2FormerPixelDecoder lateral / output convs, input projections)
+// see MIOpen's channels-last conv outputs; torch's GroupNorm first copies them to NCHW.
+// Here x is [B, HW, C] with groups of exactly 8 channels (C = 8 G): one 16-B bf16 chunk
+// (two float4 for f32) per (row, group), so a thread owns one group of one row at a time.
+//
+// Forward: (1) per (chunk of rows, image) partial sum / sum of squares per group (f32),
+// (2) finalize mean / rstd per (image, group) in f64, (3) normalise (+ ReLU).
+// Backward: (1) per chunk partials of sum(g) and sum(g * xhat) per group and of
+// sum(dy * xhat), sum(dy) per channel (g = dy * w, masked by the recomputed ReLU),
+// (2) finalize the group coefficients and reduce dw / db over chunks (fixed order),
+// (3) dx = rstd (g - mean(g) - xhat mean(g xhat)).  Semantics of
+// torch.nn.functional.group_norm (biased variance) followed by relu when requested.
+#include "common.h"
+
+#include <algorithm>
+
+namespace vs {
+namespace {
+
+constexpr int kT = 256;
+constexpr int kMinRows = 256;      // rows per chunk: max(kMinRows, HW / kMaxChunks)
+constexpr int kMaxChunks = 64;
+
+template <typename T>
+__device__ __forceinline__ void ld8f(const T* p, float* v) {
+  Vec16<T>::load(p, v);
+  if constexpr (Vec16<T>::N == 4) Vec16<T>::load(p + 4, v + 4);
+}
+
+template <typename T>
+__device__ __forceinline__ void st8f(T* p, const float* v) {
+  Vec16<T>::store(p, v);
+  if constexpr (Vec16<T>::N == 4) Vec16<T>::store(p + 4, v + 4);
+}
+
+// partials: part[b][chunk][g][2] = (sum, sumsq) over the chunk's rows and the group's 8 ch
+template <typename T>
+__global__ void __launch_bounds__(kT) gn_stats_kernel(const T* __restrict__ x, float* __restrict__ part, int HW, int G,
+                                                      int nchunk, int rpc) {
+  extern __shared__ float red[];             // [rowlanes][G][2]
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int rowlanes = kT / G;               // threads per group column (G <= 256)
+  const int g = threadIdx.x % G, rl = threadIdx.x / G;
+  const int C = 8 * G;
+  const int r0 = chunk * rpc, r1 = min(HW, r0 + rpc);
+  float s = 0.f, q = 0.f;
+  if (rl < rowlanes) {
+    const T* xb = x + (size_t)b * HW * C + g * 8;
+    for (int r = r0 + rl; r < r1; r += 4 * rowlanes) {
+      float v[4][8];                          // 4 rows' loads in flight
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (r + u * rowlanes < r1) {
+          ld8f(xb + (size_t)(r + u * rowlanes) * C, v[u]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s += v[u][i];
+          q += v[u][i] * v[u][i];
+        }
+    }
+    red[(rl * G + g) * 2 + 0] = s;
+    red[(rl * G + g) * 2 + 1] = q;
+  }
+  __syncthreads();
+  for (int gg = threadIdx.x; gg < G; gg += kT) {
+    float a = 0.f, c = 0.f;
+    for (int k = 0; k < rowlanes; ++k) {
+      a += red[(k * G + gg) * 2 + 0];
+      c += red[(k * G + gg) * 2 + 1];
+    }
+    float* o = part + (((size_t)b * nchunk + chunk) * G + gg) * 2;
+    o[0] = a;
+    o[1] = c;
+  }
+}
+
+__global__ void __launch_bounds__(kT) gn_finalize_kernel(const float* __restrict__ part, float* __restrict__ mean,
+                                                         float* __restrict__ rstd, int B, int HW, int G, int nchunk,
+                                                         float eps) {
+  const int i = blockIdx.x * kT + threadIdx.x;   // (b, g)
+  if (i >= B * G) return;
+  const int b = i / G, g = i % G;
+  double s = 0.0, q = 0.0;
+  for (int c = 0; c < nchunk; ++c) {
+    const float* p = part + (((size_t)b * nchunk + c) * G + g) * 2;
+    s += p[0];
+    q += p[1];
+  }
+  const double n = (double)HW * 8.0;
+  const double m = s / n;
+  const double var = fmax(q / n - m * m, 0.0);
+  mean[i] = (float)m;
+  rstd[i] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+template <typename T, bool RELU>
+__global__ void __launch_bounds__(kT) gn_apply_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                      const T* __restrict__ bias, const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd, T* __restrict__ y, int B, int HW,
+                                                      int G) {
+  const long long n = (long long)B * HW * G;     // (row, group) chunks
+  for (long long i = (long long)blockIdx.x * kT + threadIdx.x; i < n; i += (long long)gridDim.x * kT) {
+    const int g = (int)(i % G);
+    const long long row = i / G;
+    const int b = (int)(row / HW);
+    const float m = mean[b * G + g], rs = rstd[b * G + g];
+    float v[8], wv[8], bv[8];
+    ld8f(x + i * 8, v);
+    ld8f(w + g * 8, wv);
+    ld8f(bias + g * 8, bv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float o = (v[k] - m) * rs * wv[k] + bv[k];
+      v[k] = RELU ? fmaxf(o, 0.f) : o;
+    }
+    st8f(y + i * 8, v);
+  }
+}
+
+// backward partials: gpart[b][chunk][g][2] = (sum g, sum g*xhat); cpart[b*nchunk+chunk][C][2]
+// = (sum dy*xhat, sum dy) with dy masked by the ReLU
+template <typename T, bool RELU>
+__global__ void __launch_bounds__(kT) gn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const T* __restrict__ w, const T* __restrict__ bias,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, float* __restrict__ gpart,
+                                                          float* __restrict__ cpart, int HW, int G, int nchunk,
+                                                          int rpc) {
+  extern __shared__ float red[];             // [rowlanes][G][2 + 16]
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int rowlanes = kT / G;
+  const int g = threadIdx.x % G, rl = threadIdx.x / G;
+  const int C = 8 * G;
+  const int r0 = chunk * rpc, r1 = min(HW, r0 + rpc);
+  constexpr int W = 2 + 16;
+  float s1 = 0.f, s2 = 0.f, cw[8], cb[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) cw[k] = cb[k] = 0.f;
+  if (rl < rowlanes) {
+    const float m = mean[b * G + g], rs = rstd[b * G + g];
+    float wv[8], bv[8];
+    ld8f(w + g * 8, wv);
+    ld8f(bias + g * 8, bv);
+    const size_t base = (size_t)b * HW * C + g * 8;
+    for (int r = r0 + rl; r < r1; r += 2 * rowlanes) {
+      float xv[2][8], dv[2][8];               // 2 rows' loads in flight
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (r + u * rowlanes < r1) {
+          ld8f(x + base + (size_t)(r + u * rowlanes) * C, xv[u]);
+          ld8f(dy + base + (size_t)(r + u * rowlanes) * C, dv[u]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) xv[u][k] = dv[u][k] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (xv[u][k] - m) * rs;
+        float d = dv[u][k];
+        if (RELU && xh * wv[k] + bv[k] <= 0.f) d = 0.f;
+        const float gg = d * wv[k];
+        s1 += gg;
+        s2 += gg * xh;
+        cw[k] += d * xh;
+        cb[k] += d;
+      }
+    }
+    float* o = red + (rl * G + g) * W;
+    o[0] = s1;
+    o[1] = s2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o[2 + k] = cw[k];
+      o[10 + k] = cb[k];
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < G * W; j += kT) {
+    const int gg = j / W, f = j % W;
+    float a = 0.f;
+    for (int k = 0; k < rowlanes; ++k) a += red[(k * G + gg) * W + f];
+    if (f < 2) {
+      gpart[(((size_t)b * nchunk + chunk) * G + gg) * 2 + f] = a;
+    } else {
+      const int ch = gg * 8 + (f - 2) % 8;
+      const int which = (f - 2) / 8;    // 0: dw, 1: db
+      cpart[(((size_t)b * nchunk + chunk) * C + ch) * 2 + which] = a;
+    }
+  }
+}
+
+// group coefficients c1 = mean(g), c2 = mean(g xhat) per (b, g)
+__global__ void __launch_bounds__(kT) gn_bwd_finalize_kernel(const float* __restrict__ gpart, float* __restrict__ c12,
+                                                             int B, int HW, int G, int nchunk) {
+  const int i = blockIdx.x * kT + threadIdx.x;
+  if (i >= B * G) return;
+  const int b = i / G, g = i % G;
+  double a = 0.0, c = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    const float* p = gpart + (((size_t)b * nchunk + k) * G + g) * 2;
+    a += p[0];
+    c += p[1];
+  }
+  const double n = (double)HW * 8.0;
+  c12[i * 2 + 0] = (float)(a / n);
+  c12[i * 2 + 1] = (float)(c / n);
+}
+
+// dw / db: sum of the per-chunk channel partials in a fixed order; a block = 32 (channel,
+// which) columns x 8 part slices, 4 independent accumulators, slices combined in LDS
+template <typename T>
+__global__ void __launch_bounds__(kT) gn_bwd_wb_kernel(const float* __restrict__ cpart, T* __restrict__ dw,
+                                                       T* __restrict__ db, int nparts, int C) {
+  __shared__ float red[8][33];
+  const int lane = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const int j = blockIdx.x * 32 + lane;          // (channel, which) = cpart column
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (j < 2 * C) {
+    int k = sl;
+    for (; k + 24 < nparts; k += 32) {
+      a0 += cpart[(size_t)k * 2 * C + j];
+      a1 += cpart[(size_t)(k + 8) * 2 * C + j];
+      a2 += cpart[(size_t)(k + 16) * 2 * C + j];
+      a3 += cpart[(size_t)(k + 24) * 2 * C + j];
+    }
+    for (; k < nparts; k += 8) a0 += cpart[(size_t)k * 2 * C + j];
+  }
+  red[sl][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sl == 0 && j < 2 * C) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][lane];
+    ((j & 1) ? db : dw)[j >> 1] = from_f32<T>(t);
+  }
+}
+
+template <typename T, bool RELU>
+__global__ void __launch_bounds__(kT) gn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const T* __restrict__ w, const T* __restrict__ bias,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          const float* __restrict__ c12, T* __restrict__ dx, int B,
+                                                          int HW, int G) {
+  const long long n = (long long)B * HW * G;
+  for (long long i = (long long)blockIdx.x * kT + threadIdx.x; i < n; i += (long long)gridDim.x * kT) {
+    const int g = (int)(i % G);
+    const int b = (int)((i / G) / HW);
+    const int bg = b * G + g;
+    const float m = mean[bg], rs = rstd[bg], c1 = c12[bg * 2], c2 = c12[bg * 2 + 1];
+    float xv[8], dv[8], wv[8], bv[8];
+    ld8f(x + i * 8, xv);
+    ld8f(dy + i * 8, dv);
+    ld8f(w + g * 8, wv);
+    ld8f(bias + g * 8, bv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float xh = (xv[k] - m) * rs;
+      float d = dv[k];
+      if (RELU && xh * wv[k] + bv[k] <= 0.f) d = 0.f;
+      xv[k] = rs * (d * wv[k] - c1 - xh * c2);
+    }
+    st8f(dx + i * 8, xv);
+  }
+}
+
+int rows_per_chunk(int HW) { return std::max(kMinRows, (HW + kMaxChunks - 1) / kMaxChunks); }
+
+int chunks_for(int HW) { return (HW + rows_per_chunk(HW) - 1) / rows_per_chunk(HW); }
+
+int apply_grid(long long n) { return (int)std::min<long long>((n + kT - 1) / kT, 256 * 32); }
+
+}  // namespace
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" long long vs_group_norm_workspace_bytes(int B, int HW, int C, int G) {
+  const long long nchunk = chunks_for(HW);
+  // forward: group partials; backward: group partials + channel partials + c12
+  return (long long)B * nchunk * G * 2 * 4 + (long long)B * nchunk * C * 2 * 4 + (long long)B * G * 2 * 4 + 256;
+}
+
+#define VS_GN_CHECK()                                                                           \
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");             \
+  VS_CHECK(B > 0 && HW > 0 && G > 0 && G <= kT && C == 8 * G, "groups of exactly 8 channels"); \
+  VS_CHECK(kT % G == 0, "G must divide 256")
+
+extern "C" int vs_group_norm_forward(int dtype, const void* x, const void* weight, const void* bias, void* y,
+                                     float* mean, float* rstd, void* workspace, int B, int HW, int C, int G,
+                                     float eps, int relu, void* stream) {
+  VS_GN_CHECK();
+  VS_CHECK(x && weight && bias && y && mean && rstd && workspace, "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int nchunk = chunks_for(HW);
+  float* part = (float*)workspace;
+  const size_t lds = (size_t)kT * 2 * sizeof(float);
+  const long long n = (long long)B * HW * G;
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(gn_stats_kernel<bf16>, dim3(nchunk, B), dim3(kT), lds, st, (const bf16*)x, part, HW, G, nchunk,
+                       rows_per_chunk(HW));
+  else
+    hipLaunchKernelGGL(gn_stats_kernel<float>, dim3(nchunk, B), dim3(kT), lds, st, (const float*)x, part, HW, G,
+                       nchunk, rows_per_chunk(HW));
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * G + kT - 1) / kT), dim3(kT), 0, st, part, mean, rstd, B, HW, G,
+                     nchunk, eps);
+#define VS_GN_APPLY(TT, R)                                                                                    \
+  hipLaunchKernelGGL((gn_apply_kernel<TT, R>), dim3(apply_grid(n)), dim3(kT), 0, st, (const TT*)x,           \
+                     (const TT*)weight, (const TT*)bias, mean, rstd, (TT*)y, B, HW, G)
+  if (dtype == VS_BF16) {
+    if (relu) VS_GN_APPLY(bf16, true); else VS_GN_APPLY(bf16, false);
+  } else {
+    if (relu) VS_GN_APPLY(float, true); else VS_GN_APPLY(float, false);
+  }
+#undef VS_GN_APPLY
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_group_norm_backward(int dtype, const void* grad_y, const void* x, const void* weight,
+                                      const void* bias, const float* mean, const float* rstd, void* grad_x,
+                                      void* grad_weight, void* grad_bias, void* workspace, int B, int HW, int C,
+                                      int G, int relu, void* stream) {
+  VS_GN_CHECK();
+  VS_CHECK(grad_y && x && weight && bias && mean && rstd && grad_x && grad_weight && grad_bias && workspace,
+           "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int nchunk = chunks_for(HW);
+  float* gpart = (float*)workspace;
+  float* cpart = gpart + (size_t)B * nchunk * G * 2;
+  float* c12 = cpart + (size_t)B * nchunk * C * 2;
+  const size_t lds = (size_t)kT * 18 * sizeof(float);
+  const long long n = (long long)B * HW * G;
+#define VS_GN_BWD(TT, R)                                                                                          \
+  hipLaunchKernelGGL((gn_bwd_stats_kernel<TT, R>), dim3(nchunk, B), dim3(kT), lds, st, (const TT*)grad_y,         \
+                     (const TT*)x, (const TT*)weight, (const TT*)bias, mean, rstd, gpart, cpart, HW, G, nchunk,    \
+                     rows_per_chunk(HW));                                                                         \
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3((B * G + kT - 1) / kT), dim3(kT), 0, st, gpart, c12, B, HW, G,   \
+                     nchunk);                                                                                     \
+  hipLaunchKernelGGL((gn_bwd_wb_kernel<TT>), dim3((2 * C + 31) / 32), dim3(kT), 0, st, cpart, (TT*)grad_weight,    \
+                     (TT*)grad_bias, B * nchunk, C);                                                              \
+  hipLaunchKernelGGL((gn_bwd_apply_kernel<TT, R>), dim3(apply_grid(n)), dim3(kT), 0, st, (const TT*)grad_y,       \
+                     (const TT*)x, (const TT*)weight, (const TT*)bias, mean, rstd, c12, (TT*)grad_x, B, HW, G)
+  if (dtype == VS_BF16) {
+    if (relu) { VS_GN_BWD(bf16, true); } else { VS_GN_BWD(bf16, false); }
+  } else {
+    if (relu) { VS_GN_BWD(float, true); } else { VS_GN_BWD(float, false); }
+  }
+#undef VS_GN_BWD
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

@@ -470,3 +470,52 @@ def linear_sum_assignment_batch(cost, targets_per_image):
     with timed("lsa", c, bytes_=c.numel() * 4):
         L.check(L.lib().vs_lsa_batch(L.ptr(c), ks, S, B, Q, K, L.ptr(out), L.stream(c)), "lsa_batch")
     return out
+
+
+# ------------------------------------------------------------------ GroupNorm (channels-last)
+class GroupNormNHWCFunction(torch.autograd.Function):
+    """group_norm (+ optional ReLU) of an NCHW tensor stored channels-last, groups of 8
+    channels (csrc/groupnorm.hip); returns a channels-last NCHW tensor."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps, relu):
+        L.require_hip(x, weight, bias)
+        B, C, H, W = x.shape
+        xt = x.permute(0, 2, 3, 1)
+        if not xt.is_contiguous():
+            xt = xt.contiguous()
+        y = torch.empty_like(xt)
+        mean = torch.empty(B * groups, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        ws = torch.empty(int(L.lib().vs_group_norm_workspace_bytes(B, H * W, C, groups)), device=x.device,
+                         dtype=torch.uint8)
+        with timed("group_norm_fwd", xt, bytes_=3 * xt.numel() * xt.element_size()):
+            L.check(L.lib().vs_group_norm_forward(L.dtype_code(xt), L.ptr(xt), L.ptr(weight), L.ptr(bias), L.ptr(y),
+                                                  L.ptr(mean), L.ptr(rstd), L.ptr(ws), B, H * W, C, groups,
+                                                  float(eps), int(relu), L.stream(xt)), "group_norm_forward")
+        ctx.save_for_backward(xt, weight, bias, mean, rstd)
+        ctx.cfg = (groups, bool(relu))
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xt, weight, bias, mean, rstd = ctx.saved_tensors
+        groups, relu = ctx.cfg
+        B, H, W, C = xt.shape
+        gyt = gy.permute(0, 2, 3, 1).to(xt.dtype)
+        if not gyt.is_contiguous():
+            gyt = gyt.contiguous()
+        gx = torch.empty_like(xt)
+        gw, gb = torch.empty_like(weight), torch.empty_like(bias)
+        ws = torch.empty(int(L.lib().vs_group_norm_workspace_bytes(B, H * W, C, groups)), device=xt.device,
+                         dtype=torch.uint8)
+        with timed("group_norm_bwd", xt, bytes_=5 * xt.numel() * xt.element_size()):
+            L.check(L.lib().vs_group_norm_backward(L.dtype_code(xt), L.ptr(gyt), L.ptr(xt), L.ptr(weight), L.ptr(bias),
+                                                   L.ptr(mean), L.ptr(rstd), L.ptr(gx), L.ptr(gw), L.ptr(gb),
+                                                   L.ptr(ws), B, H * W, C, groups, int(relu), L.stream(xt)),
+                    "group_norm_backward")
+        return gx.permute(0, 3, 1, 2), gw, gb, None, None, None
+
+
+def group_norm_nhwc(x, weight, bias, groups: int, eps: float = 1e-5, relu: bool = False):
+    return GroupNormNHWCFunction.apply(x, weight, bias, int(groups), float(eps), bool(relu))
