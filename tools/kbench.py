@@ -65,8 +65,8 @@ def main():
         for oname, off in offs.items():
             loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
             locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
-            for mode in ("carry32", "plain", "pull3", "pull5", "pull8"):
-                os.environ["VS_MSDA_RUN"] = {"carry32": "32"}.get(mode, "0")
+            for mode in ("carry16", "plain", "pull5"):
+                os.environ["VS_MSDA_RUN"] = {"carry16": "16"}.get(mode, "0")
                 os.environ["VS_MSDA_PULL_R"] = mode[4:] if mode.startswith("pull") else "5"
 
                 def fb(enc=mode.startswith("pull")):

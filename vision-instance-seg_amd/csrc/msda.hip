@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(256) msda_bwd_geom_kernel(
   }
 }
 
-constexpr int kScatterRun = 32;        // queries per half-wave run (LDS staging is sized for it)
+constexpr int kScatterRun = 16;        // queries per half-wave run (LDS staging is sized for it)
 
 // ENC (encoder mode, Q == S level-major): taps owned by the pull kernel (pull_tap) are
 // skipped here; the pull kernel has already written every grad_value element.
@@ -694,7 +694,7 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   VS_HIP(hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * Hh * kD, st));
   if (Q == 0) return VS_OK;
   // geom + register-carry scatter when there are enough queries for runs to fill the chip
-  // (VS_MSDA_RUN=n forces runs of n <= 32 queries at any size, 0 the single kernel)
+  // (VS_MSDA_RUN=n forces runs of n <= kScatterRun queries at any size, 0 the single kernel)
   int run = kScatterRun;
   bool split = (long long)B * Q * Hh >= (long long)kScatterRun * 8192;
   if (const char* e = getenv("VS_MSDA_RUN")) {
@@ -702,7 +702,7 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     split = run >= 1;
   }
   if (split && P == 4) {
-    VS_CHECK(run <= kScatterRun, "VS_MSDA_RUN must be <= 32");
+    VS_CHECK(run <= kScatterRun, "VS_MSDA_RUN must not exceed the LDS-staged run (16)");
     launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
     launch_scatter<false>(dtype, loc, attw, gout, gvalue, lv, B, S, Hh, Q, L, run, 0, st);
     VS_LAUNCH_CHECK();

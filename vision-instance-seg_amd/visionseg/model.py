@@ -243,9 +243,9 @@ class MSDeformAttn(nn.Module):
         super().__init__()
         self.d, self.heads, self.levels, self.points = d, heads, levels, points
         # True: encoder-mode backward (destination pull + carry scatter, csrc/msda.hip);
-        # measured slower than the general register-carry path at C2 (3.0 vs 2.0 ms per
-        # layer), so opt-in
-        self.encoder_backward = False
+        # opt-in (VS_MSDA_ENCODER=1): faster on uncorrelated offsets, slower than the
+        # general register-carry path on the smooth offsets of the C2 bench
+        self.encoder_backward = os.environ.get("VS_MSDA_ENCODER", "0") == "1"
         self.sampling_offsets = TokenLinear(d, heads * levels * points * 2)
         self.attention_weights = TokenLinear(d, heads * levels * points)
         self.value_proj = TokenLinear(d, d)
