@@ -231,6 +231,13 @@ VS_API int vs_group_norm_backward(int dtype, const void* grad_y, const void* x, 
                                   void* grad_weight, void* grad_bias, void* workspace, int batch, int hw,
                                   int channels, int groups, int relu, void* stream);
 
+/* ---- split-K epilogue (csrc/norm.hip) -------------------------------------------------
+ * out[i] = sum_{s < num_parts} partials[s * n + i] (+ extra[i] when extra != NULL), f32
+ * accumulation in a fixed order, out in dtype: the weight gradient of a token-major
+ * Linear computed as a batched GEMM over token chunks (visionseg/linear.py).  n % 4 == 0. */
+VS_API int vs_splitk_sum(int dtype, const float* partials, int num_parts, long long n, const float* extra,
+                         void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,8 @@
 // partial-row scheme.
 #include "common.h"
 
+#include <algorithm>
+
 namespace vs {
 namespace {
 
@@ -272,6 +274,38 @@ __global__ void __launch_bounds__(kThreads) colsum_partials_kernel(const float* 
   }
 }
 
+// split-K epilogue: out[i] = sum_{s < S} part[s][i] (+ extra[i]), f32 accumulation in a
+// fixed order, written in the output dtype; 4 elements per thread (float4), 4 partial
+// rows in flight
+template <typename T>
+__global__ void __launch_bounds__(kThreads) splitk_sum_kernel(const float* __restrict__ part,
+                                                              const float* __restrict__ extra, T* __restrict__ out,
+                                                              int S, long long n4) {
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
+    float4 a = extra ? reinterpret_cast<const float4*>(extra)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 b = make_float4(0.f, 0.f, 0.f, 0.f), c = b, d = b;
+    const float4* p = reinterpret_cast<const float4*>(part) + i;
+    int s = 0;
+    for (; s + 3 < S; s += 4) {
+      const float4 v0 = p[(size_t)s * n4], v1 = p[(size_t)(s + 1) * n4], v2 = p[(size_t)(s + 2) * n4],
+                   v3 = p[(size_t)(s + 3) * n4];
+      a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+      b.x += v1.x; b.y += v1.y; b.z += v1.z; b.w += v1.w;
+      c.x += v2.x; c.y += v2.y; c.z += v2.z; c.w += v2.w;
+      d.x += v3.x; d.y += v3.y; d.z += v3.z; d.w += v3.w;
+    }
+    for (; s < S; ++s) {
+      const float4 v = p[(size_t)s * n4];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    const float r[4] = {(a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
+                        (a.w + b.w) + (c.w + d.w)};
+    T* o = out + i * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = from_f32<T>(r[k]);
+  }
+}
+
 // pick (G, K): smallest K whose power-of-two group fits in 16 lanes, else 64 lanes
 bool pick_gk(int nch, int kmax, int* G, int* K) {
   static const int ks[] = {1, 2, 3, 4};
@@ -394,6 +428,25 @@ extern "C" int vs_column_sum(int dtype, const void* x, void* out, void* ws, int 
     hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part,
                        (float*)out, (float*)nullptr, grid, N, N);
   }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_splitk_sum(int dtype, const float* partials, int num_parts, long long n, const float* extra,
+                             void* out, void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(num_parts >= 0 && n >= 0 && n % 4 == 0, "n must be a multiple of 4");
+  VS_CHECK(out && (num_parts == 0 || partials), "null pointer");
+  if (n == 0) return VS_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const long long n4 = n / 4;
+  const int grid = (int)std::min<long long>((n4 + kThreads - 1) / kThreads, 256 * 16);
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(splitk_sum_kernel<bf16>, dim3(grid), dim3(kThreads), 0, st, partials, extra, (bf16*)out,
+                       num_parts, n4);
+  else
+    hipLaunchKernelGGL(splitk_sum_kernel<float>, dim3(grid), dim3(kThreads), 0, st, partials, extra, (float*)out,
+                       num_parts, n4);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

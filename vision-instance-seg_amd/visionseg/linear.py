@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _lib as L
 from . import ops
 
 import os
@@ -32,20 +33,23 @@ def split_count(K: int, M: int, N: int) -> int:
 
 
 def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
-    """dW = gy^T x for gy [K, M], x [K, N] -> [M, N] (out_dtype), f32 accumulation."""
+    """dW = gy^T x for gy [K, M], x [K, N] -> [M, N] (out_dtype), f32 accumulation: a
+    batched GEMM over S token chunks with f32 outputs, then one HIP epilogue that sums
+    the chunks (+ the remainder rows' product) and rounds once (csrc/norm.hip)."""
     K, M = gy.shape
     N = x.shape[1]
     S = split_count(K, M, N)
-    if S <= 1:
+    if S <= 1 or (M * N) % 4 or out_dtype not in (torch.float32, torch.bfloat16):
         return (gy.t() @ x).to(out_dtype)
     chunk = K // S
     main = chunk * S
     part = torch.bmm(gy[:main].view(S, chunk, M).transpose(1, 2), x[:main].view(S, chunk, N),
                      out_dtype=torch.float32)
-    acc = part.sum(0)
-    if main < K:
-        acc += torch.mm(gy[main:].t(), x[main:], out_dtype=torch.float32)
-    return acc.to(out_dtype)
+    extra = torch.mm(gy[main:].t(), x[main:], out_dtype=torch.float32) if main < K else None
+    out = torch.empty(M, N, device=gy.device, dtype=out_dtype)
+    L.check(L.lib().vs_splitk_sum(L.dtype_code(out), L.ptr(part), S, M * N, L.ptr(extra) if extra is not None else None,
+                                  L.ptr(out), L.stream(out)), "splitk_sum")
+    return out
 
 
 class _LinearFn(torch.autograd.Function):
