@@ -100,34 +100,61 @@ __global__ void __launch_bounds__(256) mask_head_fwd_kernel(const T* __restrict_
 // Backward (bf16): one pass over the logits gradient produces both operand grads.
 //   dP[b,n,:] = sum_q gL[b,q,n] E[b,q,:]          (M = pixels, N = C, K = Q)
 //   dE[b,q,:] = sum_n gL[b,q,n] P[b,n,:]          (M = Q, N = C, K = pixels: split-K)
-// A workgroup (4 waves) keeps E^T [C][Q] in LDS and walks 32-pixel tiles of one image:
-// each tile's gL block is staged twice as bf16 (pixel-major for dP's A operand,
-// query-major for dE's A operand) and its P block transposed ([C][32]) for dE's B
-// operand, so every MFMA fragment is one contiguous 16-B LDS read (row strides padded
-// by 16 B: conflict-free ds_read_b128).  dE accumulates in registers across the
-// workgroup's tiles (4 q-tiles x C/128 c-tiles per wave) and is written once as a
-// per-workgroup f32 partial; `mask_head_bwd_reduce` sums the partials (deterministic).
+// A workgroup (4 waves) walks 32-pixel tiles of one image.  Everything is staged in LDS
+// in its NATURAL layout with 16-B stores (E [q][C] once, the gL tile [q][32] as bf16,
+// the P tile [32][C]); operands that the MFMA needs in the other orientation (gL^T and E
+// for dP, P for dE) are read with the gfx950 transpose read ds_read_b64_tr_b16
+// (cdna_hip_programming.md T10): a 16-lane group reads a 4-row x 16-column block and
+// each lane receives one column.  Row pitches of 64 B mod 256 keep those reads in
+// distinct banks.  The next tile's gL / P are loaded into registers while the current
+// tile computes (one barrier pair per tile).  dE accumulates in registers across the
+// workgroup's tiles and is written once as a per-workgroup f32 partial;
+// `mask_head_bwd_reduce` sums the partials (deterministic).
 // HBM traffic per call: gL (f32) + P read once, dP written once.
+typedef short bf16x4v_t __attribute__((ext_vector_type(4)));
+
+// MFMA operand (8 k-values of one column) from an LDS image whose ROWS are the k index:
+// rows k0 + 8hh + {0..3} and k0 + 8hh + 4 + {0..3}, column cbase + (lane & 31)
+__device__ __forceinline__ bf16x8_t tr_operand(const bf16* img, int pitch, int k0, int cbase, int lane) {
+  const int hh = lane >> 5;
+  const int row = k0 + 8 * hh + ((lane & 15) >> 2);
+  const int col = cbase + (lane & 16) + 4 * (lane & 3);
+  typedef __attribute__((address_space(3))) bf16x4v_t lds_v4;
+  const bf16x4v_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + row * pitch + col));
+  const bf16x4v_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + (row + 4) * pitch + col));
+  bf16x8_t v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const bf16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  return (uint32_t)(*reinterpret_cast<const uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<const uint16_t*>(&y)) << 16);
+}
+
 template <int CT>  // c-tiles (of 32) per wave; C = 128 * CT
 __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restrict__ gL, const bf16* __restrict__ E,
                                                             const bf16* __restrict__ P, bf16* __restrict__ dP,
                                                             float* __restrict__ dEpart, int Q, int N) {
   constexpr int C = 128 * CT;
-  constexpr int QP = 128 + 8;     // padded q stride
   constexpr int TN = 32;
-  constexpr int NP = TN + 8;      // padded n stride
+  constexpr int EP = C + 32;      // E / P row pitch (elements): 2*EP bytes = 64 mod 256
+  constexpr int GP = TN;          // gL tile row pitch: 64 B
+  constexpr int CH = C / 8;       // 16-B chunks per P row
+  constexpr int PCH = TN * CH / 256;  // P chunks per thread per tile
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  bf16* sET = reinterpret_cast<bf16*>(smem_raw);   // [C][QP]
-  bf16* sGT = sET + C * QP;                          // [TN][QP]
-  bf16* sGN = sGT + TN * QP;                         // [128][NP]
-  bf16* sPT = sGN + 128 * NP;                        // [C][NP]
+  bf16* sE = reinterpret_cast<bf16*>(smem_raw);      // [128][EP]
+  bf16* sG = sE + 128 * EP;                          // [128][GP]
+  bf16* sP = sG + 128 * GP;                          // [TN][EP]
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const bf16 zero = __float2bfloat16(0.f);
-  for (int idx = threadIdx.x; idx < 128 * C; idx += blockDim.x) {
-    const int q = idx / C, c = idx - q * C;
-    sET[c * QP + q] = q < Q ? E[((size_t)b * Q + q) * C + c] : zero;
+  for (int idx = threadIdx.x; idx < 128 * CH; idx += 256) {
+    const int q = idx / CH, c0 = (idx - q * CH) * 8;
+    uint4 u = make_uint4(0, 0, 0, 0);
+    if (q < Q) u = *reinterpret_cast<const uint4*>(E + ((size_t)b * Q + q) * C + c0);
+    *reinterpret_cast<uint4*>(sE + q * EP + c0) = u;
   }
   f32x16_t accE[4][CT];
 #pragma unroll
@@ -140,43 +167,53 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
   const bf16* Pb = P + (size_t)b * N * C;
   bf16* dPb = dP + (size_t)b * N * C;
   const int tiles = (N + TN - 1) / TN;
-  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const int n0 = tile * TN;
-    __syncthreads();
-    {  // gL tile: thread -> (q = tid/2, 16 pixels)
-      const int q = threadIdx.x >> 1, nh = (threadIdx.x & 1) * 16;
+  // register staging of one tile: gL row q = tid/2, 16 pixels; PCH P chunks
+  const int gq = threadIdx.x >> 1, gh = (threadIdx.x & 1) * 16;
+  float4 rg[4];
+  uint4 rp[PCH];
+  auto load_tile = [&](int n0) {
+    if (gq < Q && n0 + gh + 16 <= N && (N & 3) == 0) {
+      const float4* src = reinterpret_cast<const float4*>(gLb + (size_t)gq * N + n0 + gh);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rg[i] = src[i];
+    } else {
       float v[16];
-      if (q < Q && n0 + nh + 16 <= N) {
-        const float4* src = reinterpret_cast<const float4*>(gLb + (size_t)q * N + n0 + nh);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float4 t4 = src[i];
-          v[4 * i] = t4.x; v[4 * i + 1] = t4.y; v[4 * i + 2] = t4.z; v[4 * i + 3] = t4.w;
-        }
-      } else {
+      for (int i = 0; i < 16; ++i) v[i] = (gq < Q && n0 + gh + i < N) ? gLb[(size_t)gq * N + n0 + gh + i] : 0.f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = (q < Q && n0 + nh + i < N) ? gLb[(size_t)q * N + n0 + nh + i] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const bf16 x = __float2bfloat16(v[i]);
-        sGN[q * NP + nh + i] = x;
-        sGT[(nh + i) * QP + q] = x;
-      }
+      for (int i = 0; i < 4; ++i) rg[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
     }
-    {  // P tile: 32 rows x C, 16-B chunks, stored transposed [C][NP]
-      constexpr int CH = C / 8;
-      for (int idx = threadIdx.x; idx < TN * CH; idx += blockDim.x) {
-        const int n = idx / CH, c0 = (idx - n * CH) * 8;
-        uint4 u = make_uint4(0, 0, 0, 0);
-        if (n0 + n < N) u = *reinterpret_cast<const uint4*>(Pb + (size_t)(n0 + n) * C + c0);
-        const bf16* e = reinterpret_cast<const bf16*>(&u);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sPT[(c0 + i) * NP + n] = e[i];
-      }
+    for (int k = 0; k < PCH; ++k) {
+      const int idx = threadIdx.x + k * 256;
+      const int n = idx / CH, c0 = (idx - n * CH) * 8;
+      rp[k] = (n0 + n < N) ? *reinterpret_cast<const uint4*>(Pb + (size_t)(n0 + n) * C + c0) : make_uint4(0, 0, 0, 0);
     }
+  };
+  auto store_tile = [&]() {
+    uint4 w0, w1;
+    w0.x = pack_bf16x2(rg[0].x, rg[0].y); w0.y = pack_bf16x2(rg[0].z, rg[0].w);
+    w0.z = pack_bf16x2(rg[1].x, rg[1].y); w0.w = pack_bf16x2(rg[1].z, rg[1].w);
+    w1.x = pack_bf16x2(rg[2].x, rg[2].y); w1.y = pack_bf16x2(rg[2].z, rg[2].w);
+    w1.z = pack_bf16x2(rg[3].x, rg[3].y); w1.w = pack_bf16x2(rg[3].z, rg[3].w);
+    *reinterpret_cast<uint4*>(sG + gq * GP + gh) = w0;
+    *reinterpret_cast<uint4*>(sG + gq * GP + gh + 8) = w1;
+#pragma unroll
+    for (int k = 0; k < PCH; ++k) {
+      const int idx = threadIdx.x + k * 256;
+      const int n = idx / CH, c0 = (idx - n * CH) * 8;
+      *reinterpret_cast<uint4*>(sP + n * EP + c0) = rp[k];
+    }
+  };
+  int tile = blockIdx.x;
+  if (tile < tiles) load_tile(tile * TN);
+  for (; tile < tiles; tile += gridDim.x) {
+    const int n0 = tile * TN;
+    __syncthreads();                 // previous tile's LDS reads are done
+    store_tile();
     __syncthreads();
-    // ---- dP tile [32 n][C]: wave owns c-tiles {wave*CT .. wave*CT+CT-1}
+    if (tile + gridDim.x < tiles) load_tile((tile + gridDim.x) * TN);   // in flight during the MFMAs
+    // ---- dP tile [32 n][C]: A = gL^T (rows n, k = q), B = E (k = q, cols c)
 #pragma unroll
     for (int u = 0; u < CT; ++u) {
       const int c0 = (wave * CT + u) * 32;
@@ -185,8 +222,8 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
       for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sGT + r * QP + 16 * s + 8 * hh);
-        const bf16x8_t bb = *reinterpret_cast<const bf16x8_t*>(sET + (c0 + r) * QP + 16 * s + 8 * hh);
+        const bf16x8_t a = tr_operand(sG, GP, 16 * s, 0, lane);
+        const bf16x8_t bb = tr_operand(sE, EP, 16 * s, c0, lane);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
       }
 #pragma unroll
@@ -200,11 +237,10 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
     for (int s = 0; s < 2; ++s) {
       bf16x8_t bfr[CT];
 #pragma unroll
-      for (int u = 0; u < CT; ++u)
-        bfr[u] = *reinterpret_cast<const bf16x8_t*>(sPT + ((wave * CT + u) * 32 + r) * NP + 16 * s + 8 * hh);
+      for (int u = 0; u < CT; ++u) bfr[u] = tr_operand(sP, EP, 16 * s, (wave * CT + u) * 32, lane);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sGN + (32 * t + r) * NP + 16 * s + 8 * hh);
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sG + (32 * t + r) * GP + 16 * s + 8 * hh);
 #pragma unroll
         for (int u = 0; u < CT; ++u) accE[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[u], accE[t][u], 0, 0, 0);
       }
@@ -341,7 +377,7 @@ extern "C" int vs_mask_head_backward(int dtype, const float* grad_logits, const 
   const int tiles = (N + 31) / 32;
   const int gx = parts < tiles ? parts : tiles;
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = ((size_t)C * 136 + 32 * 136 + 128 * 40 + (size_t)C * 40) * 2;
+  const size_t lds = ((size_t)128 * (C + 32) + 128 * 32 + (size_t)32 * (C + 32)) * 2;
   float* part = (float*)workspace;
   if (gx < parts) VS_HIP(hipMemsetAsync(part + (size_t)gx * B * Q * C, 0, (size_t)(parts - gx) * B * Q * C * 4, st));
   if (C == 256) {
