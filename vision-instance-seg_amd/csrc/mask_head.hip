@@ -28,9 +28,10 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 constexpr int kQT = 4;          // 32-row query tiles per workgroup (128 rows)
 constexpr int kWaves = 4;
 
-template <typename T>
+template <typename T, int KC>  // KC: compile-time channel count (0 = runtime K)
 __global__ void __launch_bounds__(256) mask_head_fwd_kernel(const T* __restrict__ E, const T* __restrict__ P,
-                                                            float* __restrict__ out, int Q, int N, int K) {
+                                                            float* __restrict__ out, int Q, int N, int Kr) {
+  const int K = KC > 0 ? KC : Kr;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   T* sE = reinterpret_cast<T*>(smem_raw);
   const int ldE = K + 16 / (int)sizeof(T);  // pad each row by 16 bytes
@@ -41,12 +42,24 @@ __global__ void __launch_bounds__(256) mask_head_fwd_kernel(const T* __restrict_
   // ---- stage E rows [q0, q0+128) of batch b into LDS (zero rows past Q)
   {
     constexpr int V = 16 / sizeof(T);
+    constexpr int kBatch = 8;   // loads in flight per thread before their LDS stores
     const int chunks = K / V;
-    for (int idx = threadIdx.x; idx < 32 * kQT * chunks; idx += blockDim.x) {
-      const int row = idx / chunks, c = (idx % chunks) * V;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (q0 + row < Q) v = *reinterpret_cast<const uint4*>(E + ((size_t)b * Q + q0 + row) * K + c);
-      *reinterpret_cast<uint4*>(sE + row * ldE + c) = v;
+    const int total = 32 * kQT * chunks;
+    for (int base = 0; base < total; base += 256 * kBatch) {
+      uint4 v[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        const int idx = base + threadIdx.x + 256 * k;
+        const int row = idx / chunks, c = (idx % chunks) * V;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (idx < total && q0 + row < Q) v[k] = *reinterpret_cast<const uint4*>(E + ((size_t)b * Q + q0 + row) * K + c);
+      }
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        const int idx = base + threadIdx.x + 256 * k;
+        const int row = idx / chunks, c = (idx % chunks) * V;
+        if (idx < total) *reinterpret_cast<uint4*>(sE + row * ldE + c) = v[k];
+      }
     }
   }
   __syncthreads();
@@ -96,6 +109,85 @@ __global__ void __launch_bounds__(256) mask_head_fwd_kernel(const T* __restrict_
 }
 
 
+// bf16 forward with a compile-time channel count: each wave streams its pixel tiles with
+// the NEXT tile's P fragments (KC/16 x 16 B per lane) in flight while the current tile's
+// MFMAs run, so at one wave per SIMD the HBM latency stays hidden.
+template <int KC>
+__global__ void __launch_bounds__(256) mask_head_fwd_bf16_kernel(const bf16* __restrict__ E, const bf16* __restrict__ P,
+                                                                 float* __restrict__ out, int Q, int N) {
+  constexpr int S = KC / 16;
+  constexpr int ldE = KC + 8;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* sE = reinterpret_cast<bf16*>(smem_raw);
+  const int b = blockIdx.y;
+  const int q0 = blockIdx.z * 32 * kQT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  {
+    constexpr int CH = KC / 8;
+    constexpr int EC = 32 * kQT * CH / 256;
+    uint4 v[EC];
+#pragma unroll
+    for (int k = 0; k < EC; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int row = idx / CH, c = (idx % CH) * 8;
+      v[k] = q0 + row < Q ? *reinterpret_cast<const uint4*>(E + ((size_t)b * Q + q0 + row) * KC + c) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < EC; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int row = idx / CH, c = (idx % CH) * 8;
+      *reinterpret_cast<uint4*>(sE + row * ldE + c) = v[k];
+    }
+  }
+  __syncthreads();
+  const bf16* Pb = P + (size_t)b * N * KC;
+  float* Ob = out + (size_t)b * Q * N;
+  const int tiles = (N + 31) / 32;
+  const int stride = gridDim.x * kWaves;
+  bf16x8_t cur[S], nxt[S];
+  auto load = [&](bf16x8_t* f, int tile) {
+    const int n = tile * 32 + r;
+    const bf16* prow = Pb + (size_t)(n < N ? n : 0) * KC + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < S; ++s) f[s] = *reinterpret_cast<const bf16x8_t*>(prow + 16 * s);
+  };
+  int tile = blockIdx.x * kWaves + wave;
+  if (tile < tiles) load(cur, tile);
+  for (; tile < tiles; tile += stride) {
+    if (tile + stride < tiles) load(nxt, tile + stride);
+    const int n = tile * 32 + r;
+    const bool nvalid = n < N;
+    f32x16_t acc[kQT];
+#pragma unroll
+    for (int t = 0; t < kQT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8_t bfrag = nvalid ? cur[s] : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int t = 0; t < kQT; ++t) {
+        const bf16x8_t afrag = *reinterpret_cast<const bf16x8_t*>(sE + (32 * t + r) * ldE + 16 * s + 8 * hh);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag, bfrag, acc[t], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (nvalid) {
+#pragma unroll
+      for (int t = 0; t < kQT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = q0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (row < Q) Ob[(size_t)row * N + n] = acc[t][i];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) cur[s] = nxt[s];
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // Backward (bf16): one pass over the logits gradient produces both operand grads.
 //   dP[b,n,:] = sum_q gL[b,q,n] E[b,q,:]          (M = pixels, N = C, K = Q)
@@ -133,14 +225,14 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return (uint32_t)(*reinterpret_cast<const uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<const uint16_t*>(&y)) << 16);
 }
 
-template <int CT>  // c-tiles (of 32) per wave; C = 128 * CT
+template <int CT, int TN>  // c-tiles (of 32) per wave (C = 128 * CT); pixels per tile (32 or 64)
 __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restrict__ gL, const bf16* __restrict__ E,
                                                             const bf16* __restrict__ P, bf16* __restrict__ dP,
-                                                            float* __restrict__ dEpart, int Q, int N) {
+                                                            float* __restrict__ dEpart, int Q, int N, int exp) {
   constexpr int C = 128 * CT;
-  constexpr int TN = 32;
+  constexpr int NT = TN / 32;
   constexpr int EP = C + 32;      // E / P row pitch (elements): 2*EP bytes = 64 mod 256
-  constexpr int GP = TN;          // gL tile row pitch: 64 B
+  constexpr int GP = TN == 32 ? 32 : 96;   // gL tile row pitch: 64 / 192 B (4 rows -> distinct banks)
   constexpr int CH = C / 8;       // 16-B chunks per P row
   constexpr int PCH = TN * CH / 256;  // P chunks per thread per tile
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -150,11 +242,21 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  for (int idx = threadIdx.x; idx < 128 * CH; idx += 256) {
-    const int q = idx / CH, c0 = (idx - q * CH) * 8;
-    uint4 u = make_uint4(0, 0, 0, 0);
-    if (q < Q) u = *reinterpret_cast<const uint4*>(E + ((size_t)b * Q + q) * C + c0);
-    *reinterpret_cast<uint4*>(sE + q * EP + c0) = u;
+  {  // all of this thread's E chunks in flight at once, then the LDS stores
+    constexpr int EC = 128 * CH / 256;
+    uint4 ue[EC];
+#pragma unroll
+    for (int k = 0; k < EC; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int q = idx / CH, c0 = (idx - q * CH) * 8;
+      ue[k] = q < Q ? *reinterpret_cast<const uint4*>(E + ((size_t)b * Q + q) * C + c0) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < EC; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int q = idx / CH, c0 = (idx - q * CH) * 8;
+      *reinterpret_cast<uint4*>(sE + q * EP + c0) = ue[k];
+    }
   }
   f32x16_t accE[4][CT];
 #pragma unroll
@@ -167,21 +269,27 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
   const bf16* Pb = P + (size_t)b * N * C;
   bf16* dPb = dP + (size_t)b * N * C;
   const int tiles = (N + TN - 1) / TN;
-  // register staging of one tile: gL row q = tid/2, 16 pixels; PCH P chunks
-  const int gq = threadIdx.x >> 1, gh = (threadIdx.x & 1) * 16;
-  float4 rg[4];
+  // register staging of one tile: gL row q = tid/2, TN/2 pixels; PCH P chunks
+  constexpr int GH = TN / 2;
+  const int gq = threadIdx.x >> 1, gh = (threadIdx.x & 1) * GH;
+  float4 rg[GH / 4];
   uint4 rp[PCH];
   auto load_tile = [&](int n0) {
-    if (gq < Q && n0 + gh + 16 <= N && (N & 3) == 0) {
+    if (gq < Q && n0 + gh + GH <= N && (N & 3) == 0) {
       const float4* src = reinterpret_cast<const float4*>(gLb + (size_t)gq * N + n0 + gh);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) rg[i] = src[i];
+      for (int i = 0; i < GH / 4; ++i) rg[i] = src[i];
     } else {
-      float v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = (gq < Q && n0 + gh + i < N) ? gLb[(size_t)gq * N + n0 + gh + i] : 0.f;
+      for (int i = 0; i < GH / 4; ++i) {
+        float v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) rg[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + gh + 4 * i + j;
+          v[j] = (gq < Q && n < N) ? gLb[(size_t)gq * N + n] : 0.f;
+        }
+        rg[i] = make_float4(v[0], v[1], v[2], v[3]);
+      }
     }
 #pragma unroll
     for (int k = 0; k < PCH; ++k) {
@@ -191,13 +299,13 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
     }
   };
   auto store_tile = [&]() {
-    uint4 w0, w1;
-    w0.x = pack_bf16x2(rg[0].x, rg[0].y); w0.y = pack_bf16x2(rg[0].z, rg[0].w);
-    w0.z = pack_bf16x2(rg[1].x, rg[1].y); w0.w = pack_bf16x2(rg[1].z, rg[1].w);
-    w1.x = pack_bf16x2(rg[2].x, rg[2].y); w1.y = pack_bf16x2(rg[2].z, rg[2].w);
-    w1.z = pack_bf16x2(rg[3].x, rg[3].y); w1.w = pack_bf16x2(rg[3].z, rg[3].w);
-    *reinterpret_cast<uint4*>(sG + gq * GP + gh) = w0;
-    *reinterpret_cast<uint4*>(sG + gq * GP + gh + 8) = w1;
+#pragma unroll
+    for (int i = 0; i < GH / 8; ++i) {
+      uint4 w;
+      w.x = pack_bf16x2(rg[2 * i].x, rg[2 * i].y); w.y = pack_bf16x2(rg[2 * i].z, rg[2 * i].w);
+      w.z = pack_bf16x2(rg[2 * i + 1].x, rg[2 * i + 1].y); w.w = pack_bf16x2(rg[2 * i + 1].z, rg[2 * i + 1].w);
+      *reinterpret_cast<uint4*>(sG + gq * GP + gh + 8 * i) = w;
+    }
 #pragma unroll
     for (int k = 0; k < PCH; ++k) {
       const int idx = threadIdx.x + k * 256;
@@ -212,61 +320,126 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
     __syncthreads();                 // previous tile's LDS reads are done
     store_tile();
     __syncthreads();
-    if (tile + gridDim.x < tiles) load_tile((tile + gridDim.x) * TN);   // in flight during the MFMAs
-    // ---- dP tile [32 n][C]: A = gL^T (rows n, k = q), B = E (k = q, cols c)
+    if (!(exp & 8) && tile + gridDim.x < tiles) load_tile((tile + gridDim.x) * TN);   // in flight during the MFMAs
+    // ---- dP tile [TN n][C]: A = gL^T (rows n, k = q), B = E (k = q, cols c).  The
+    // fragments of k-step s+1 are read before the MFMAs of step s issue (one wave per
+    // SIMD: nothing else hides the LDS latency); CT x NT independent accumulators.
+    if (!(exp & 16)) {
+      f32x16_t acc[CT][NT];
 #pragma unroll
-    for (int u = 0; u < CT; ++u) {
-      const int c0 = (wave * CT + u) * 32;
-      f32x16_t acc;
+      for (int u = 0; u < CT; ++u)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        for (int m = 0; m < NT; ++m)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[u][m][i] = 0.f;
+      bf16x8_t fa[2][NT], fb[2][CT];
+#pragma unroll
+      for (int m = 0; m < NT; ++m) fa[0][m] = tr_operand(sG, GP, 0, 32 * m, lane);
+#pragma unroll
+      for (int u = 0; u < CT; ++u) fb[0][u] = tr_operand(sE, EP, 0, (wave * CT + u) * 32, lane);
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        const bf16x8_t a = tr_operand(sG, GP, 16 * s, 0, lane);
-        const bf16x8_t bb = tr_operand(sE, EP, 16 * s, c0, lane);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
-      }
+        const int cur = s & 1, nxt = cur ^ 1;
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < 8) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int n = n0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        if (n < N) dPb[(size_t)n * C + c0 + r] = __float2bfloat16(acc[i]);
+          for (int m = 0; m < NT; ++m) fa[nxt][m] = tr_operand(sG, GP, 16 * (s + 1), 32 * m, lane);
+#pragma unroll
+          for (int u = 0; u < CT; ++u) fb[nxt][u] = tr_operand(sE, EP, 16 * (s + 1), (wave * CT + u) * 32, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep the next step's reads ahead of these MFMAs
+#pragma unroll
+        for (int u = 0; u < CT; ++u)
+#pragma unroll
+          for (int m = 0; m < NT; ++m)
+            acc[u][m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[cur][u], fa[cur][m], acc[u][m], 0, 0, 0);
+      }
+      // acc[u][m] is the dP^T tile: lane column = pixel n0 + 32m + r, rows = channels
+      // c0 + (i & 3) + 8 (i >> 2) + 4 hh -> four consecutive channels per 8-B store
+#pragma unroll
+      for (int m = 0; m < NT; ++m) {
+        const int n = n0 + 32 * m + r;
+        if (n < N && !(exp & 1)) {
+          bf16* dst = dPb + (size_t)n * C + wave * CT * 32 + 4 * hh;
+#pragma unroll
+          for (int u = 0; u < CT; ++u)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              uint2 w;
+              w.x = pack_bf16x2(acc[u][m][4 * g], acc[u][m][4 * g + 1]);
+              w.y = pack_bf16x2(acc[u][m][4 * g + 2], acc[u][m][4 * g + 3]);
+              *reinterpret_cast<uint2*>(dst + 32 * u + 8 * g) = w;
+            }
+        }
       }
     }
-    // ---- dE partial [128 q][C] += gL_tile [128 x 32] . P_tile [32 x C]
+    // ---- dE partial [128 q][C] += gL_tile [128 x TN] . P_tile [TN x C]
+    if (!(exp & 2)) {
+      bf16x8_t fa[2][4], fb[2][CT];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8_t bfr[CT];
+      for (int t = 0; t < 4; ++t) fa[0][t] = *reinterpret_cast<const bf16x8_t*>(sG + (32 * t + r) * GP + 8 * hh);
 #pragma unroll
-      for (int u = 0; u < CT; ++u) bfr[u] = tr_operand(sP, EP, 16 * s, (wave * CT + u) * 32, lane);
+      for (int u = 0; u < CT; ++u) fb[0][u] = tr_operand(sP, EP, 0, (wave * CT + u) * 32, lane);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sG + (32 * t + r) * GP + 16 * s + 8 * hh);
+      for (int s = 0; s < 2 * NT; ++s) {
+        const int cur = s & 1, nxt = cur ^ 1;
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < 2 * NT) {
 #pragma unroll
-        for (int u = 0; u < CT; ++u) accE[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[u], accE[t][u], 0, 0, 0);
+          for (int t = 0; t < 4; ++t)
+            fa[nxt][t] = *reinterpret_cast<const bf16x8_t*>(sG + (32 * t + r) * GP + 16 * (s + 1) + 8 * hh);
+#pragma unroll
+          for (int u = 0; u < CT; ++u) fb[nxt][u] = tr_operand(sP, EP, 16 * (s + 1), (wave * CT + u) * 32, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int u = 0; u < CT; ++u)
+            accE[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[cur][u], fa[cur][t], accE[t][u], 0, 0, 0);
       }
     }
   }
+  // accE[t][u] is the dE^T tile: lane column = query 32t + r, rows = channels
+  // (wave * CT + u) * 32 + (i & 3) + 8 (i >> 2) + 4 hh -> 16-B stores of 4 channels
   float* part = dEpart + ((size_t)blockIdx.x * gridDim.y + b) * Q * C;
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < 4; ++t) {
+    const int q = 32 * t + r;
+    if (q < Q) {
 #pragma unroll
-    for (int u = 0; u < CT; ++u) {
-      const int c = (wave * CT + u) * 32 + r;
+      for (int u = 0; u < CT; ++u)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int q = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        if (q < Q) part[(size_t)q * C + c] = accE[t][u][i];
-      }
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(part + (size_t)q * C + (wave * CT + u) * 32 + 8 * g + 4 * hh) =
+              make_float4(accE[t][u][4 * g], accE[t][u][4 * g + 1], accE[t][u][4 * g + 2], accE[t][u][4 * g + 3]);
     }
+  }
 }
 
 __global__ void __launch_bounds__(256) mask_head_bwd_reduce(const float* __restrict__ part, bf16* __restrict__ dE,
                                                             int nparts, long long per_part) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  // 4 consecutive elements per thread (per_part % 4 == 0: C is a multiple of 128), 8 parts
+  // in flight; parts summed in index order (deterministic)
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= per_part) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(size_t)p * per_part + i];
-  dE[i] = __float2bfloat16(s);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  int p = 0;
+  for (; p + 8 <= nparts; p += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(part + (size_t)(p + k) * per_part + i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
+  }
+  for (; p < nparts; ++p) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (size_t)p * per_part + i);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  uint2 w;
+  w.x = pack_bf16x2(s.x, s.y);
+  w.y = pack_bf16x2(s.z, s.w);
+  *reinterpret_cast<uint2*>(dE + i) = w;
 }
 
 // PyTorch upsample_bilinear2d (align_corners=False) source index for one axis.
@@ -333,12 +506,23 @@ extern "C" int vs_mask_head_forward(int dtype, const void* E, const void* P, flo
   if (dtype == VS_BF16) {
     VS_CHECK(C % 16 == 0 && C <= 512, "bf16 mask head needs C % 16 == 0, C <= 512");
     const size_t lds = (size_t)32 * kQT * (C + 8) * 2;
-    hipLaunchKernelGGL(mask_head_fwd_kernel<bf16>, grid, dim3(256), lds, st, (const bf16*)E, (const bf16*)P,
-                       logits, Q, N, C);
+    // pipelined kernel: one workgroup per CU (1 wave/SIMD by registers), tiles streamed
+    dim3 pgrid(grid);
+    const int pcap = (256 + B * qz - 1) / (B * qz);
+    if ((int)pgrid.x > pcap) pgrid.x = pcap;
+    if (C == 256)
+      hipLaunchKernelGGL((mask_head_fwd_bf16_kernel<256>), pgrid, dim3(256), lds, st, (const bf16*)E,
+                         (const bf16*)P, logits, Q, N);
+    else if (C == 128)
+      hipLaunchKernelGGL((mask_head_fwd_bf16_kernel<128>), pgrid, dim3(256), lds, st, (const bf16*)E,
+                         (const bf16*)P, logits, Q, N);
+    else
+      hipLaunchKernelGGL((mask_head_fwd_kernel<bf16, 0>), grid, dim3(256), lds, st, (const bf16*)E,
+                         (const bf16*)P, logits, Q, N, C);
   } else if (dtype == VS_F32) {
     VS_CHECK(C % 4 == 0 && C <= 256, "f32 mask head needs C % 4 == 0, C <= 256");
     const size_t lds = (size_t)32 * kQT * (C + 4) * 4;
-    hipLaunchKernelGGL(mask_head_fwd_kernel<float>, grid, dim3(256), lds, st, (const float*)E, (const float*)P,
+    hipLaunchKernelGGL((mask_head_fwd_kernel<float, 0>), grid, dim3(256), lds, st, (const float*)E, (const float*)P,
                        logits, Q, N, C);
   } else {
     VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
@@ -359,6 +543,8 @@ extern "C" int vs_attn_bitmask(const float* logits, uint32_t* words, int rows, i
   return VS_OK;
 }
 
+#include <cstdlib>
+static int mh_exp_flags() { const char* e = getenv("VS_MH_EXP"); return e ? atoi(e) : 0; }
 static int mask_head_bwd_parts(int B) { return B >= 64 ? 1 : (256 + B - 1) / B; }
 
 extern "C" long long vs_mask_head_backward_workspace_bytes(int B, int Q, int C) {
@@ -374,22 +560,24 @@ extern "C" int vs_mask_head_backward(int dtype, const float* grad_logits, const 
   VS_CHECK(C == 128 || C == 256, "channels must be 128 or 256");
   const int N = H * W;
   const int parts = mask_head_bwd_parts(B);
-  const int tiles = (N + 31) / 32;
+  constexpr int TN = 64;
+  const int mh_exp = mh_exp_flags();
+  const int tiles = (N + TN - 1) / TN;
   const int gx = parts < tiles ? parts : tiles;
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = ((size_t)128 * (C + 32) + 128 * 32 + (size_t)32 * (C + 32)) * 2;
+  const size_t lds = ((size_t)128 * (C + 32) + 128 * 96 + (size_t)TN * (C + 32)) * 2;
   float* part = (float*)workspace;
   if (gx < parts) VS_HIP(hipMemsetAsync(part + (size_t)gx * B * Q * C, 0, (size_t)(parts - gx) * B * Q * C * 4, st));
   if (C == 256) {
-    hipLaunchKernelGGL(mask_head_bwd_kernel<2>, dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
-                       (const bf16*)P, (bf16*)grad_P, part, Q, N);
+    hipLaunchKernelGGL((mask_head_bwd_kernel<2, TN>), dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
+                       (const bf16*)P, (bf16*)grad_P, part, Q, N, mh_exp);
   } else {
-    hipLaunchKernelGGL(mask_head_bwd_kernel<1>, dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
-                       (const bf16*)P, (bf16*)grad_P, part, Q, N);
+    hipLaunchKernelGGL((mask_head_bwd_kernel<1, TN>), dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
+                       (const bf16*)P, (bf16*)grad_P, part, Q, N, mh_exp);
   }
   VS_LAUNCH_CHECK();
   const long long per = (long long)B * Q * C;
-  hipLaunchKernelGGL(mask_head_bwd_reduce, dim3((int)((per + 255) / 256)), dim3(256), 0, st, part, (bf16*)grad_E,
+  hipLaunchKernelGGL(mask_head_bwd_reduce, dim3((int)((per / 4 + 255) / 256)), dim3(256), 0, st, part, (bf16*)grad_E,
                      parts, per);
   VS_LAUNCH_CHECK();
   return VS_OK;
