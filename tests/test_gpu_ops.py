@@ -232,7 +232,7 @@ def test_attn_bitmask_vs_oracle():
     g = torch.Generator().manual_seed(13)
     lo = torch.randn(2, 7, 64, 64, generator=g) * 3
     lo[0, 2] = -5.0          # fully blocked row -> un-blocked by the fix
-    for tgt in [(8, 8), (16, 16), (32, 32), (64, 64), (5, 7)]:
+    for tgt in [(8, 8), (16, 16), (32, 32), (64, 64), (5, 7), (37, 61), (128, 128), (1, 1)]:
         words = ops.attn_bitmask(lo.to(DEV), tgt)
         am = torch.nn.functional.interpolate(lo, size=tgt, mode="bilinear", align_corners=False)
         exp = R.unblock_full_rows(am.sigmoid().flatten(2) < 0.5)

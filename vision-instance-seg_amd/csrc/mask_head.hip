@@ -228,7 +228,7 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 template <int CT, int TN>  // c-tiles (of 32) per wave (C = 128 * CT); pixels per tile (32 or 64)
 __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restrict__ gL, const bf16* __restrict__ E,
                                                             const bf16* __restrict__ P, bf16* __restrict__ dP,
-                                                            float* __restrict__ dEpart, int Q, int N, int exp) {
+                                                            float* __restrict__ dEpart, int Q, int N) {
   constexpr int C = 128 * CT;
   constexpr int NT = TN / 32;
   constexpr int EP = C + 32;      // E / P row pitch (elements): 2*EP bytes = 64 mod 256
@@ -320,11 +320,11 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
     __syncthreads();                 // previous tile's LDS reads are done
     store_tile();
     __syncthreads();
-    if (!(exp & 8) && tile + gridDim.x < tiles) load_tile((tile + gridDim.x) * TN);   // in flight during the MFMAs
+    if (tile + gridDim.x < tiles) load_tile((tile + gridDim.x) * TN);   // in flight during the MFMAs
     // ---- dP tile [TN n][C]: A = gL^T (rows n, k = q), B = E (k = q, cols c).  The
     // fragments of k-step s+1 are read before the MFMAs of step s issue (one wave per
     // SIMD: nothing else hides the LDS latency); CT x NT independent accumulators.
-    if (!(exp & 16)) {
+    {
       f32x16_t acc[CT][NT];
 #pragma unroll
       for (int u = 0; u < CT; ++u)
@@ -359,7 +359,7 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
 #pragma unroll
       for (int m = 0; m < NT; ++m) {
         const int n = n0 + 32 * m + r;
-        if (n < N && !(exp & 1)) {
+        if (n < N) {
           bf16* dst = dPb + (size_t)n * C + wave * CT * 32 + 4 * hh;
 #pragma unroll
           for (int u = 0; u < CT; ++u)
@@ -374,7 +374,7 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
       }
     }
     // ---- dE partial [128 q][C] += gL_tile [128 x TN] . P_tile [TN x C]
-    if (!(exp & 2)) {
+    {
       bf16x8_t fa[2][4], fb[2][CT];
 #pragma unroll
       for (int t = 0; t < 4; ++t) fa[0][t] = *reinterpret_cast<const bf16x8_t*>(sG + (32 * t + r) * GP + 8 * hh);
@@ -453,37 +453,48 @@ __device__ __forceinline__ void src_index(int dst, int in, int out, int& i0, int
   l0 = 1.f - l1;
 }
 
-__global__ void __launch_bounds__(256) attn_bitmask_kernel(const float* __restrict__ logits,
-                                                           uint32_t* __restrict__ words, int H, int W,
-                                                           int th, int tw, int nwords) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t sw[];
+__global__ void __launch_bounds__(1024) attn_bitmask_kernel(const float* __restrict__ logits,
+                                                            uint32_t* __restrict__ words, int H, int W,
+                                                            int th, int tw, int nwords) {
+  // one workgroup (16 waves) per (b, q) row; a wave evaluates 64 consecutive keys and
+  // its ballot IS two output words (bit k % 32 of word k / 32), written directly
   __shared__ int s_count;
-  const long long row = blockIdx.x;  // (b, q)
+  const long long row = blockIdx.x;
   const float* src = logits + row * (long long)H * W;
+  uint32_t* dst = words + row * nwords;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_count = 0;
-  for (int i = threadIdx.x; i < nwords; i += blockDim.x) sw[i] = 0u;
   __syncthreads();
   const int total = th * tw;
   int local = 0;
-  for (int k = threadIdx.x; k < total; k += blockDim.x) {
-    const int y = k / tw, x = k - y * tw;
-    int y0, y1, x0, x1;
-    float ly0, ly1, lx0, lx1;
-    src_index(y, H, th, y0, y1, ly0, ly1);
-    src_index(x, W, tw, x0, x1, lx0, lx1);
-    const float v = ly0 * (lx0 * src[y0 * W + x0] + lx1 * src[y0 * W + x1]) +
-                    ly1 * (lx0 * src[y1 * W + x0] + lx1 * src[y1 * W + x1]);
-    const float sg = 1.f / (1.f + expf(-v));
-    if (sg < 0.5f) {
-      atomicOr(&sw[k >> 5], 1u << (k & 31));
-      ++local;
+  for (int base = wave * 64; base < total; base += 1024) {
+    const int k = base + lane;
+    bool blocked = false;
+    if (k < total) {
+      const int y = k / tw, x = k - y * tw;
+      int y0, y1, x0, x1;
+      float ly0, ly1, lx0, lx1;
+      src_index(y, H, th, y0, y1, ly0, ly1);
+      src_index(x, W, tw, x0, x1, lx0, lx1);
+      const float v = ly0 * (lx0 * src[y0 * W + x0] + lx1 * src[y0 * W + x1]) +
+                      ly1 * (lx0 * src[y1 * W + x0] + lx1 * src[y1 * W + x1]);
+      const float sg = 1.f / (1.f + expf(-v));
+      blocked = sg < 0.5f;
+    }
+    const unsigned long long m = __ballot(blocked);
+    if (lane == 0) {
+      const int w0 = base >> 5;
+      dst[w0] = (uint32_t)m;
+      if (w0 + 1 < nwords) dst[w0 + 1] = (uint32_t)(m >> 32);
+      local += __popcll(m);
     }
   }
-  atomicAdd(&s_count, local);
+  if (lane == 0) atomicAdd(&s_count, local);
   __syncthreads();
-  const bool full = s_count == total;
-  uint32_t* dst = words + row * nwords;
-  for (int i = threadIdx.x; i < nwords; i += blockDim.x) dst[i] = full ? 0u : sw[i];
+  // a row blocked at every key is written un-blocked (HF:m2f:1912-1914); words past the
+  // last key (nwords * 32 > total) were written by the wave that covers them
+  if (s_count == total)
+    for (int i = threadIdx.x; i < nwords; i += blockDim.x) dst[i] = 0u;
 }
 
 }  // namespace
@@ -537,14 +548,12 @@ extern "C" int vs_attn_bitmask(const float* logits, uint32_t* words, int rows, i
   VS_CHECK(rows > 0 && H > 0 && W > 0 && th > 0 && tw > 0, "bad sizes");
   const int nwords = (th * tw + 31) / 32;
   VS_CHECK(nwords * 4 <= 64 * 1024, "target too large");
-  hipLaunchKernelGGL(attn_bitmask_kernel, dim3(rows), dim3(256), nwords * 4, (hipStream_t)stream, logits, words,
+  hipLaunchKernelGGL(attn_bitmask_kernel, dim3(rows), dim3(1024), 0, (hipStream_t)stream, logits, words,
                      H, W, th, tw, nwords);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
 
-#include <cstdlib>
-static int mh_exp_flags() { const char* e = getenv("VS_MH_EXP"); return e ? atoi(e) : 0; }
 static int mask_head_bwd_parts(int B) { return B >= 64 ? 1 : (256 + B - 1) / B; }
 
 extern "C" long long vs_mask_head_backward_workspace_bytes(int B, int Q, int C) {
@@ -561,7 +570,6 @@ extern "C" int vs_mask_head_backward(int dtype, const float* grad_logits, const 
   const int N = H * W;
   const int parts = mask_head_bwd_parts(B);
   constexpr int TN = 64;
-  const int mh_exp = mh_exp_flags();
   const int tiles = (N + TN - 1) / TN;
   const int gx = parts < tiles ? parts : tiles;
   hipStream_t st = (hipStream_t)stream;
@@ -570,10 +578,10 @@ extern "C" int vs_mask_head_backward(int dtype, const float* grad_logits, const 
   if (gx < parts) VS_HIP(hipMemsetAsync(part + (size_t)gx * B * Q * C, 0, (size_t)(parts - gx) * B * Q * C * 4, st));
   if (C == 256) {
     hipLaunchKernelGGL((mask_head_bwd_kernel<2, TN>), dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
-                       (const bf16*)P, (bf16*)grad_P, part, Q, N, mh_exp);
+                       (const bf16*)P, (bf16*)grad_P, part, Q, N);
   } else {
     hipLaunchKernelGGL((mask_head_bwd_kernel<1, TN>), dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
-                       (const bf16*)P, (bf16*)grad_P, part, Q, N, mh_exp);
+                       (const bf16*)P, (bf16*)grad_P, part, Q, N);
   }
   VS_LAUNCH_CHECK();
   const long long per = (long long)B * Q * C;
