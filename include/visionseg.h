@@ -231,6 +231,19 @@ VS_API int vs_group_norm_backward(int dtype, const void* grad_y, const void* x, 
                                   void* grad_weight, void* grad_bias, void* workspace, int batch, int hw,
                                   int channels, int groups, int relu, void* stream);
 
+/* ---- GroupNorm over NCHW-contiguous activations (csrc/groupnorm.hip) ----------------
+ * Same op as above for MIOpen's NCHW conv outputs (the 1/4-resolution lateral and output
+ * ConvGN blocks of the pixel decoder, HF:m2f Mask2FormerPixelDecoder): x, y [B, C, HW],
+ * any C % G == 0; each group is C/G contiguous channel planes, so no layout copies. */
+VS_API long long vs_group_norm_nchw_workspace_bytes(int batch, int channels, int groups);
+VS_API int vs_group_norm_nchw_forward(int dtype, const void* x, const void* weight, const void* bias, void* y,
+                                      float* mean, float* rstd, void* workspace, int batch, int channels, int hw,
+                                      int groups, float eps, int relu, void* stream);
+VS_API int vs_group_norm_nchw_backward(int dtype, const void* grad_y, const void* x, const void* weight,
+                                       const void* bias, const float* mean, const float* rstd, void* grad_x,
+                                       void* grad_weight, void* grad_bias, void* workspace, int batch,
+                                       int channels, int hw, int groups, int relu, void* stream);
+
 /* ---- split-K epilogue (csrc/norm.hip) -------------------------------------------------
  * out[i] = sum_{s < num_parts} partials[s * n + i] (+ extra[i] when extra != NULL), f32
  * accumulation in a fixed order, out in dtype: the weight gradient of a token-major

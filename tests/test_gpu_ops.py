@@ -569,7 +569,20 @@ def test_group_norm_nhwc_vs_torch(dtype, relu, shape, groups, cl):
     the kernel (f32 statistics) and the f64 reference: every such disagreement must sit at
     |pre-activation| < 1e-4, and the gradients are compared against the reference using
     the kernel's own mask (decisions separated from arithmetic)."""
-    ops = _ops()
+    _check_group_norm(_ops().group_norm_nhwc, dtype, relu, shape, groups, cl)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("shape,groups", [((2, 256, 64, 64), 32), ((2, 96, 17, 23), 32), ((1, 64, 5, 7), 8),
+                                          ((3, 48, 9, 8), 16), ((1, 256, 256, 256), 32)])
+def test_group_norm_nchw_vs_torch(dtype, relu, shape, groups):
+    """NCHW GroupNorm (+ReLU) kernels, incl. groups of 3 channels and HW % 8 != 0 (scalar
+    path), same checks as the channels-last test."""
+    _check_group_norm(_ops().group_norm_nchw, dtype, relu, shape, groups, False)
+
+
+def _check_group_norm(fn, dtype, relu, shape, groups, cl):
     B, C, H, W = shape
     g = torch.Generator().manual_seed(C + H)
     x = (torch.randn(shape, generator=g) * 2 + 0.3).to(dtype)
@@ -580,7 +593,7 @@ def test_group_norm_nhwc_vs_torch(dtype, relu, shape, groups, cl):
     if cl:
         xd = xd.contiguous(memory_format=torch.channels_last)
     xd, wd, bd = xd.requires_grad_(True), w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
-    y = ops.group_norm_nhwc(xd, wd, bd, groups, 1e-5, relu)
+    y = fn(xd, wd, bd, groups, 1e-5, relu)
     y.backward(gy.to(DEV))
     xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
     pre = torch.nn.functional.group_norm(xr, groups, wr, br, 1e-5)

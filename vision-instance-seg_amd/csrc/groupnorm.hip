@@ -278,6 +278,270 @@ __global__ void __launch_bounds__(kT) gn_bwd_apply_kernel(const T* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------
+// NCHW layout: a group is Cg = C / G consecutive channel planes of HW contiguous elements,
+// so every pass is a contiguous stream.  One block per (b, c) plane for the statistics.
+template <typename T, bool VEC>
+__device__ __forceinline__ void plane_load8(const T* p, long long j, float* v) {
+  if constexpr (VEC) {
+    ld8f(p + 8 * j, v);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = to_f32(p[8 * j + k]);
+  }
+}
+
+__device__ __forceinline__ void block_sum2(float& a, float& b, float* sh) {
+  for (int o = 32; o >= 1; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) {
+    sh[2 * w] = a;
+    sh[2 * w + 1] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float x = 0.f, y = 0.f;
+    for (int i = 0; i < kT / 64; ++i) {
+      x += sh[2 * i];
+      y += sh[2 * i + 1];
+    }
+    sh[2 * (kT / 64)] = x;
+    sh[2 * (kT / 64) + 1] = y;
+  }
+  __syncthreads();
+  a = sh[2 * (kT / 64)];
+  b = sh[2 * (kT / 64) + 1];
+}
+
+// cpart[b*C + c] = (sum, sumsq) of the plane
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(kT) gn_nchw_stats_kernel(const T* __restrict__ x, float* __restrict__ cpart, int HW) {
+  __shared__ float sh[2 * (kT / 64) + 2];
+  const int plane = blockIdx.x;
+  const T* p = x + (size_t)plane * HW;
+  float s = 0.f, q = 0.f;
+  const int nv = HW / 8;
+  int j = threadIdx.x;
+  for (; j + 3 * kT < nv; j += 4 * kT) {
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) plane_load8<T, VEC>(p, j + u * kT, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s += v[u][k];
+        q += v[u][k] * v[u][k];
+      }
+  }
+  for (; j < nv; j += kT) {
+    float v[8];
+    plane_load8<T, VEC>(p, j, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s += v[k];
+      q += v[k] * v[k];
+    }
+  }
+  for (int i = nv * 8 + threadIdx.x; i < HW; i += kT) {
+    const float v = to_f32(p[i]);
+    s += v;
+    q += v * v;
+  }
+  block_sum2(s, q, sh);
+  if (threadIdx.x == 0) {
+    cpart[plane * 2] = s;
+    cpart[plane * 2 + 1] = q;
+  }
+}
+
+__global__ void __launch_bounds__(kT) gn_nchw_finalize_kernel(const float* __restrict__ cpart, float* __restrict__ mean,
+                                                              float* __restrict__ rstd, int B, int HW, int C, int G,
+                                                              float eps) {
+  const int i = blockIdx.x * kT + threadIdx.x;   // (b, g)
+  if (i >= B * G) return;
+  const int Cg = C / G;
+  double s = 0.0, q = 0.0;
+  for (int c = 0; c < Cg; ++c) {
+    s += cpart[((size_t)i * Cg + c) * 2];
+    q += cpart[((size_t)i * Cg + c) * 2 + 1];
+  }
+  const double n = (double)HW * Cg;
+  const double m = s / n;
+  const double var = fmax(q / n - m * m, 0.0);
+  mean[i] = (float)m;
+  rstd[i] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+template <typename T, bool RELU, bool VEC>
+__global__ void __launch_bounds__(kT) gn_nchw_apply_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                           const T* __restrict__ bias, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, T* __restrict__ y, int B,
+                                                           int HW, int C, int G) {
+  const int Cg = C / G;
+  if constexpr (VEC) {
+    const long long n = (long long)B * C * HW / 8;
+    for (long long i = (long long)blockIdx.x * kT + threadIdx.x; i < n; i += (long long)gridDim.x * kT) {
+      const int plane = (int)(i * 8 / HW);
+      const int c = plane % C, bg = plane / Cg;      // plane = b*C + c, group index b*G + c/Cg
+      const float m = mean[bg], rs = rstd[bg], wv = to_f32(w[c]), bv = to_f32(bias[c]);
+      float v[8];
+      ld8f(x + i * 8, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float o = (v[k] - m) * rs * wv + bv;
+        v[k] = RELU ? fmaxf(o, 0.f) : o;
+      }
+      st8f(y + i * 8, v);
+    }
+  } else {
+    const long long n = (long long)B * C * HW;
+    for (long long i = (long long)blockIdx.x * kT + threadIdx.x; i < n; i += (long long)gridDim.x * kT) {
+      const int plane = (int)(i / HW);
+      const int c = plane % C, bg = plane / Cg;
+      const float o = (to_f32(x[i]) - mean[bg]) * rstd[bg] * to_f32(w[c]) + to_f32(bias[c]);
+      y[i] = from_f32<T>(RELU ? fmaxf(o, 0.f) : o);
+    }
+  }
+}
+
+// cpart[b*C + c] = (sum dy*xhat, sum dy) with dy masked by the recomputed ReLU
+template <typename T, bool RELU, bool VEC>
+__global__ void __launch_bounds__(kT) gn_nchw_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               const T* __restrict__ w, const T* __restrict__ bias,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               float* __restrict__ cpart, int HW, int C, int G) {
+  __shared__ float sh[2 * (kT / 64) + 2];
+  const int plane = blockIdx.x;
+  const int c = plane % C, bg = plane / (C / G);
+  const float m = mean[bg], rs = rstd[bg], wv = to_f32(w[c]), bv = to_f32(bias[c]);
+  const T* px = x + (size_t)plane * HW;
+  const T* pd = dy + (size_t)plane * HW;
+  float sw = 0.f, sb = 0.f;
+  const int nv = HW / 8;
+  int j = threadIdx.x;
+  for (; j + kT < nv; j += 2 * kT) {
+    float xv[2][8], dv[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      plane_load8<T, VEC>(px, j + u * kT, xv[u]);
+      plane_load8<T, VEC>(pd, j + u * kT, dv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (xv[u][k] - m) * rs;
+        float d = dv[u][k];
+        if (RELU && xh * wv + bv <= 0.f) d = 0.f;
+        sw += d * xh;
+        sb += d;
+      }
+  }
+  for (; j < nv; j += kT) {
+    float xv[8], dv[8];
+    plane_load8<T, VEC>(px, j, xv);
+    plane_load8<T, VEC>(pd, j, dv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float xh = (xv[k] - m) * rs;
+      float d = dv[k];
+      if (RELU && xh * wv + bv <= 0.f) d = 0.f;
+      sw += d * xh;
+      sb += d;
+    }
+  }
+  for (int i = nv * 8 + threadIdx.x; i < HW; i += kT) {
+    const float xh = (to_f32(px[i]) - m) * rs;
+    float d = to_f32(pd[i]);
+    if (RELU && xh * wv + bv <= 0.f) d = 0.f;
+    sw += d * xh;
+    sb += d;
+  }
+  block_sum2(sw, sb, sh);
+  if (threadIdx.x == 0) {
+    cpart[plane * 2] = sw;
+    cpart[plane * 2 + 1] = sb;
+  }
+}
+
+// c12[b*G + g] = (mean over the group of w*dy, mean of w*dy*xhat) from the channel sums;
+// dw[c] / db[c] = sums over the batch (fixed order)
+template <typename T>
+__global__ void __launch_bounds__(kT) gn_nchw_bwd_finalize_kernel(const float* __restrict__ cpart,
+                                                                  const T* __restrict__ w, float* __restrict__ c12,
+                                                                  T* __restrict__ dw, T* __restrict__ db, int B,
+                                                                  int HW, int C, int G) {
+  const int i = blockIdx.x * kT + threadIdx.x;
+  const int Cg = C / G;
+  if (i < B * G) {
+    double a = 0.0, c = 0.0;
+    for (int k = 0; k < Cg; ++k) {
+      const int ch = (i % G) * Cg + k;
+      const double wv = (double)to_f32(w[ch]);
+      a += wv * cpart[((size_t)i * Cg + k) * 2 + 1];
+      c += wv * cpart[((size_t)i * Cg + k) * 2];
+    }
+    const double n = (double)HW * Cg;
+    c12[i * 2] = (float)(a / n);
+    c12[i * 2 + 1] = (float)(c / n);
+  }
+  if (i < C) {
+    float sw = 0.f, sb = 0.f;
+    for (int b = 0; b < B; ++b) {
+      sw += cpart[((size_t)b * C + i) * 2];
+      sb += cpart[((size_t)b * C + i) * 2 + 1];
+    }
+    dw[i] = from_f32<T>(sw);
+    db[i] = from_f32<T>(sb);
+  }
+}
+
+template <typename T, bool RELU, bool VEC>
+__global__ void __launch_bounds__(kT) gn_nchw_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               const T* __restrict__ w, const T* __restrict__ bias,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               const float* __restrict__ c12, T* __restrict__ dx,
+                                                               int B, int HW, int C, int G) {
+  const int Cg = C / G;
+  if constexpr (VEC) {
+    const long long n = (long long)B * C * HW / 8;
+    for (long long i = (long long)blockIdx.x * kT + threadIdx.x; i < n; i += (long long)gridDim.x * kT) {
+      const int plane = (int)(i * 8 / HW);
+      const int c = plane % C, bg = plane / Cg;
+      const float m = mean[bg], rs = rstd[bg], c1 = c12[bg * 2], c2 = c12[bg * 2 + 1];
+      const float wv = to_f32(w[c]), bv = to_f32(bias[c]);
+      float xv[8], dv[8];
+      ld8f(x + i * 8, xv);
+      ld8f(dy + i * 8, dv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (xv[k] - m) * rs;
+        float d = dv[k];
+        if (RELU && xh * wv + bv <= 0.f) d = 0.f;
+        xv[k] = rs * (d * wv - c1 - xh * c2);
+      }
+      st8f(dx + i * 8, xv);
+    }
+  } else {
+    const long long n = (long long)B * C * HW;
+    for (long long i = (long long)blockIdx.x * kT + threadIdx.x; i < n; i += (long long)gridDim.x * kT) {
+      const int plane = (int)(i / HW);
+      const int c = plane % C, bg = plane / Cg;
+      const float m = mean[bg], rs = rstd[bg], wv = to_f32(w[c]), bv = to_f32(bias[c]);
+      const float xh = (to_f32(x[i]) - m) * rs;
+      float d = to_f32(dy[i]);
+      if (RELU && xh * wv + bv <= 0.f) d = 0.f;
+      dx[i] = from_f32<T>(rs * (d * wv - c12[bg * 2] - xh * c12[bg * 2 + 1]));
+    }
+  }
+}
+
 int rows_per_chunk(int HW) { return std::max(kMinRows, (HW + kMaxChunks - 1) / kMaxChunks); }
 
 int chunks_for(int HW) { return (HW + rows_per_chunk(HW) - 1) / rows_per_chunk(HW); }
@@ -361,6 +625,75 @@ extern "C" int vs_group_norm_backward(int dtype, const void* grad_y, const void*
     if (relu) { VS_GN_BWD(float, true); } else { VS_GN_BWD(float, false); }
   }
 #undef VS_GN_BWD
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+// ------------------------------------------------------------------------ NCHW entry points
+extern "C" long long vs_group_norm_nchw_workspace_bytes(int B, int C, int G) {
+  return (long long)B * C * 2 * 4 + (long long)B * G * 2 * 4 + 256;
+}
+
+#define VS_GN_NCHW_CHECK()                                                                        \
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");               \
+  VS_CHECK(B > 0 && HW > 0 && G > 0 && C > 0 && C % G == 0, "channels must be a multiple of groups")
+
+extern "C" int vs_group_norm_nchw_forward(int dtype, const void* x, const void* weight, const void* bias, void* y,
+                                          float* mean, float* rstd, void* workspace, int B, int C, int HW, int G,
+                                          float eps, int relu, void* stream) {
+  VS_GN_NCHW_CHECK();
+  VS_CHECK(x && weight && bias && y && mean && rstd && workspace, "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  float* cpart = (float*)workspace;
+  const bool vec = HW % 8 == 0;
+  const long long n = (long long)B * C * HW / (vec ? 8 : 1);
+#define VS_GN_NCHW_FWD(TT, R, V)                                                                                  \
+  hipLaunchKernelGGL((gn_nchw_stats_kernel<TT, V>), dim3(B * C), dim3(kT), 0, st, (const TT*)x, cpart, HW);         \
+  hipLaunchKernelGGL(gn_nchw_finalize_kernel, dim3((B * G + kT - 1) / kT), dim3(kT), 0, st, cpart, mean, rstd, B, \
+                     HW, C, G, eps);                                                                              \
+  hipLaunchKernelGGL((gn_nchw_apply_kernel<TT, R, V>), dim3(apply_grid(n)), dim3(kT), 0, st, (const TT*)x,        \
+                     (const TT*)weight, (const TT*)bias, mean, rstd, (TT*)y, B, HW, C, G)
+  if (dtype == VS_BF16) {
+    if (vec) { if (relu) { VS_GN_NCHW_FWD(bf16, true, true); } else { VS_GN_NCHW_FWD(bf16, false, true); } }
+    else { if (relu) { VS_GN_NCHW_FWD(bf16, true, false); } else { VS_GN_NCHW_FWD(bf16, false, false); } }
+  } else {
+    if (vec) { if (relu) { VS_GN_NCHW_FWD(float, true, true); } else { VS_GN_NCHW_FWD(float, false, true); } }
+    else { if (relu) { VS_GN_NCHW_FWD(float, true, false); } else { VS_GN_NCHW_FWD(float, false, false); } }
+  }
+#undef VS_GN_NCHW_FWD
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_group_norm_nchw_backward(int dtype, const void* grad_y, const void* x, const void* weight,
+                                           const void* bias, const float* mean, const float* rstd, void* grad_x,
+                                           void* grad_weight, void* grad_bias, void* workspace, int B, int C, int HW,
+                                           int G, int relu, void* stream) {
+  VS_GN_NCHW_CHECK();
+  VS_CHECK(grad_y && x && weight && bias && mean && rstd && grad_x && grad_weight && grad_bias && workspace,
+           "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  float* cpart = (float*)workspace;
+  float* c12 = cpart + (size_t)B * C * 2;
+  const bool vec = HW % 8 == 0;
+  const long long n = (long long)B * C * HW / (vec ? 8 : 1);
+  const int fin = (std::max(B * G, C) + kT - 1) / kT;
+#define VS_GN_NCHW_BWD(TT, R, V)                                                                                   \
+  hipLaunchKernelGGL((gn_nchw_bwd_stats_kernel<TT, R, V>), dim3(B * C), dim3(kT), 0, st, (const TT*)grad_y,        \
+                     (const TT*)x, (const TT*)weight, (const TT*)bias, mean, rstd, cpart, HW, C, G);               \
+  hipLaunchKernelGGL((gn_nchw_bwd_finalize_kernel<TT>), dim3(fin), dim3(kT), 0, st, cpart, (const TT*)weight, c12, \
+                     (TT*)grad_weight, (TT*)grad_bias, B, HW, C, G);                                               \
+  hipLaunchKernelGGL((gn_nchw_bwd_apply_kernel<TT, R, V>), dim3(apply_grid(n)), dim3(kT), 0, st,                   \
+                     (const TT*)grad_y, (const TT*)x, (const TT*)weight, (const TT*)bias, mean, rstd, c12,         \
+                     (TT*)grad_x, B, HW, C, G)
+  if (dtype == VS_BF16) {
+    if (vec) { if (relu) { VS_GN_NCHW_BWD(bf16, true, true); } else { VS_GN_NCHW_BWD(bf16, false, true); } }
+    else { if (relu) { VS_GN_NCHW_BWD(bf16, true, false); } else { VS_GN_NCHW_BWD(bf16, false, false); } }
+  } else {
+    if (vec) { if (relu) { VS_GN_NCHW_BWD(float, true, true); } else { VS_GN_NCHW_BWD(float, false, true); } }
+    else { if (relu) { VS_GN_NCHW_BWD(float, true, false); } else { VS_GN_NCHW_BWD(float, false, false); } }
+  }
+#undef VS_GN_NCHW_BWD
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

@@ -52,13 +52,17 @@ SIGNATURES = {
     "vs_group_norm_forward": [_c_int] + [_P] * 7 + [_c_int] * 4 + [_c_float, _c_int, _P],
     "vs_group_norm_backward": [_c_int] + [_P] * 10 + [_c_int] * 5 + [_P],
     "vs_splitk_sum": [_c_int, _P, _c_int, ctypes.c_longlong, _P, _P, _P],
+    "vs_group_norm_nchw_workspace_bytes": [_c_int] * 3,
+    "vs_group_norm_nchw_forward": [_c_int] + [_P] * 7 + [_c_int] * 4 + [_c_float, _c_int, _P],
+    "vs_group_norm_nchw_backward": [_c_int] + [_P] * 10 + [_c_int] * 5 + [_P],
 }
 RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": ctypes.c_longlong,
             "vs_mask_head_backward_workspace_bytes": ctypes.c_longlong,
             "vs_layer_norm_backward_workspace_bytes": ctypes.c_longlong,
             "vs_column_sum_workspace_bytes": ctypes.c_longlong,
             "vs_segment_clip_workspace_bytes": ctypes.c_longlong,
-            "vs_group_norm_workspace_bytes": ctypes.c_longlong}
+            "vs_group_norm_workspace_bytes": ctypes.c_longlong,
+            "vs_group_norm_nchw_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
 

@@ -76,6 +76,81 @@ class _LinearFn(torch.autograd.Function):
         return gx, gw, gb
 
 
+class _PlaneProjectionFn(torch.autograd.Function):
+    """1x1 convolution from NCHW planes to token-major output: out[b, p, o] = sum_i
+    W[o, i] y[b, i, p] + bias[o].  Both GEMMs read y in place (its [C, HW] planes are a
+    column-major [HW, C] operand), so neither direction needs a layout copy."""
+
+    @staticmethod
+    def forward(ctx, y, weight, bias):
+        B, Ci, H, W = y.shape
+        Co = weight.shape[0]
+        y3 = y.contiguous().view(B, Ci, H * W)
+        w2 = weight.view(Co, Ci)
+        wt = w2.t().unsqueeze(0).expand(B, Ci, Co)
+        if bias is not None:
+            out = torch.baddbmm(bias.view(1, 1, Co).expand(B, H * W, Co), y3.transpose(1, 2), wt)
+        else:
+            out = torch.bmm(y3.transpose(1, 2), wt)
+        ctx.save_for_backward(y3, weight)
+        ctx.has_bias = bias is not None
+        ctx.hw = (H, W)
+        return out
+
+    @staticmethod
+    def backward(ctx, gp):
+        y3, weight = ctx.saved_tensors
+        B, Ci, HW = y3.shape
+        Co = weight.shape[0]
+        H, W = ctx.hw
+        gp = gp.contiguous()
+        w2 = weight.view(Co, Ci).to(gp.dtype)
+        gy = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gy = torch.bmm(w2.t().unsqueeze(0).expand(B, Ci, Co), gp.transpose(1, 2)).view(B, Ci, H, W)
+        if ctx.needs_input_grad[1]:
+            gw = _plane_weight_grad(gp, y3.to(gp.dtype), weight.dtype).view_as(weight)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            g2 = gp.view(-1, Co)
+            gb = (ops.column_sum(g2) if Co % 8 == 0 and Co <= 2048 else g2.sum(0, dtype=torch.float32))
+            gb = gb.to(weight.dtype)
+        return gy, gw, gb
+
+
+def _plane_weight_grad(gp, y3, out_dtype):
+    """dW[o, i] = sum_b gp[b]^T y[b]^T with K = HW per image: each image's pixel axis is
+    cut into chunks run as one f32 batched GEMM (y's chunk is a column-major operand
+    in place), all partials summed once by the split-K epilogue."""
+    B, HW, Co = gp.shape
+    Ci = y3.shape[1]
+    per = max(1, split_count(B * HW, Co, Ci) // B)
+    while per > 1 and HW % per:
+        per -= 1
+    if per <= 1 or (Co * Ci) % 4 or out_dtype not in (torch.float32, torch.bfloat16):
+        return torch.einsum("bpo,bip->oi", gp.float(), y3.float()).to(out_dtype)
+    c = HW // per
+    parts = [torch.bmm(gp[b].view(per, c, Co).transpose(1, 2), y3[b].view(Ci, per, c).permute(1, 2, 0),
+                       out_dtype=torch.float32) for b in range(B)]
+    part = torch.cat(parts, 0)
+    out = torch.empty(Co, Ci, device=gp.device, dtype=out_dtype)
+    L.check(L.lib().vs_splitk_sum(L.dtype_code(out), L.ptr(part), B * per, Co * Ci, None, L.ptr(out),
+                                  L.stream(out)), "splitk_sum")
+    return out
+
+
+def plane_projection(y, weight, bias=None):
+    """nn.Conv2d(k=1) of an NCHW tensor returned as a channels-last NCHW view (memory
+    [B, H, W, Co]): the mask projection whose output the mask head reads token-major."""
+    B, _, H, W = y.shape
+    if torch.is_autocast_enabled():
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            out = _PlaneProjectionFn.apply(y.to(dt), weight.to(dt), None if bias is None else bias.to(dt))
+    else:
+        out = _PlaneProjectionFn.apply(y, weight, bias)
+    return out.view(B, H, W, -1).permute(0, 3, 1, 2)
+
+
 class TokenLayerNorm(nn.LayerNorm):
     """nn.LayerNorm on the HIP row kernel (csrc/norm.hip) for f32 / bf16 device tensors
     whose weight shares their dtype; anything else (autocast's f32 LayerNorm, CPU

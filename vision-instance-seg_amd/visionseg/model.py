@@ -28,7 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .linear import TokenLayerNorm, TokenLinear, linear_tokens
+from .linear import TokenLayerNorm, TokenLinear, linear_tokens, plane_projection
 
 
 @dataclass
@@ -278,28 +278,37 @@ class EncoderLayer(nn.Module):
 
 
 _TORCH_GN = os.environ.get("VS_TORCH_GROUPNORM", "0") == "1"     # A/B switch
+_PIXDEC_NCHW = os.environ.get("VS_PIXDEC_NCHW", "1") == "1"    # A/B switch: NCHW 1/4-res blocks
 
 
 class ConvGN(nn.Module):
-    """Conv2d + GroupNorm(32) (+ ReLU when relu=True).  On the device with channels-last
-    activations, groups of 8 channels and matching dtypes the norm runs on the HIP
-    channels-last kernel (csrc/groupnorm.hip, ReLU fused); otherwise torch's."""
+    """Conv2d + GroupNorm(32) (+ ReLU when relu=True), the norm on the HIP kernels
+    (csrc/groupnorm.hip, ReLU fused) for device tensors of matching dtype, torch's
+    otherwise.  nchw=False: the conv sees channels-last activations (Swin features) and
+    the output stays channels-last (the encoder flattens it token-major for free).
+    nchw=True: the 1/4-resolution blocks run NCHW end to end (MIOpen's NCHW 3x3 conv
+    kernels are the fast ones there; the NCHW GroupNorm needs no layout copy)."""
 
-    def __init__(self, cin, cout, k, bias, relu=False):
+    def __init__(self, cin, cout, k, bias, relu=False, nchw=False):
         super().__init__()
         self.conv = nn.Conv2d(cin, cout, kernel_size=k, padding=k // 2, bias=bias)
         self.gn = nn.GroupNorm(32, cout)
         self.relu = relu
+        self.nchw = nchw
 
     def forward(self, x):
-        y = self.conv(x)
         gn = self.gn
-        if (y.is_cuda and y.shape[1] == 8 * gn.num_groups and y.dtype in (torch.float32, torch.bfloat16)
-                and gn.weight.dtype == y.dtype and not torch.is_autocast_enabled() and not _TORCH_GN):
-            # NCHW-contiguous output: MIOpen's NCHW kernels for the following 3x3 conv (and
-            # its backward) beat the channels-last ones at 1/4 resolution (71.1 vs 76-84
-            # ms/step measured), worth the transpose copy
-            return ops.group_norm_nhwc(y, gn.weight, gn.bias, gn.num_groups, gn.eps, self.relu).contiguous()
+        hip = (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and gn.weight.dtype == x.dtype
+               and not torch.is_autocast_enabled() and not _TORCH_GN)
+        if hip and self.nchw and _PIXDEC_NCHW:
+            y = self.conv(x.contiguous())
+            if y.is_contiguous():
+                return ops.group_norm_nchw(y, gn.weight, gn.bias, gn.num_groups, gn.eps, self.relu)
+        else:
+            y = self.conv(x)
+        if hip and y.shape[1] == 8 * gn.num_groups and y.is_contiguous(memory_format=torch.channels_last):
+            out = ops.group_norm_nhwc(y, gn.weight, gn.bias, gn.num_groups, gn.eps, self.relu)
+            return out if _PIXDEC_NCHW else out.contiguous()
         y = gn(y)
         return F.relu(y) if self.relu else y
 
@@ -313,8 +322,8 @@ class PixelDecoder(nn.Module):
         self.level_embed = nn.Parameter(torch.zeros(3, Fd))
         self.encoder = nn.ModuleList([EncoderLayer(Fd, cfg.enc_ffn, cfg.dec_heads, 3, cfg.n_points)
                                       for _ in range(cfg.enc_layers)])
-        self.lateral = ConvGN(channels[0], Fd, 1, False)
-        self.output = ConvGN(Fd, Fd, 3, False, relu=True)
+        self.lateral = ConvGN(channels[0], Fd, 1, False, nchw=True)
+        self.output = ConvGN(Fd, Fd, 3, False, relu=True, nchw=True)
         self.mask_proj = nn.Conv2d(Fd, cfg.mask_feature_size, kernel_size=1)
 
     def forward(self, feats):
@@ -341,6 +350,9 @@ class PixelDecoder(nn.Module):
         cur = self.lateral(feats[0])
         y = cur + F.interpolate(outs[-1].to(cur.dtype), size=cur.shape[-2:], mode="bilinear", align_corners=False)
         y = self.output(y)
+        if y.is_cuda and _PIXDEC_NCHW:
+            # token-major mask features straight from the NCHW planes (channels-last view)
+            return plane_projection(y, self.mask_proj.weight, self.mask_proj.bias), outs
         return self.mask_proj(y), outs
 
 

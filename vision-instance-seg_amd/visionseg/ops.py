@@ -519,3 +519,48 @@ class GroupNormNHWCFunction(torch.autograd.Function):
 
 def group_norm_nhwc(x, weight, bias, groups: int, eps: float = 1e-5, relu: bool = False):
     return GroupNormNHWCFunction.apply(x, weight, bias, int(groups), float(eps), bool(relu))
+
+
+class GroupNormNCHWFunction(torch.autograd.Function):
+    """group_norm (+ optional ReLU) of an NCHW-contiguous tensor (csrc/groupnorm.hip NCHW
+    kernels: a group is C/G contiguous channel planes); returns an NCHW-contiguous tensor."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps, relu):
+        L.require_hip(x, weight, bias)
+        B, C, H, W = x.shape
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        mean = torch.empty(B * groups, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        ws = torch.empty(int(L.lib().vs_group_norm_nchw_workspace_bytes(B, C, groups)), device=x.device,
+                         dtype=torch.uint8)
+        with timed("group_norm_nchw_fwd", x, bytes_=3 * x.numel() * x.element_size()):
+            L.check(L.lib().vs_group_norm_nchw_forward(L.dtype_code(x), L.ptr(x), L.ptr(weight), L.ptr(bias),
+                                                       L.ptr(y), L.ptr(mean), L.ptr(rstd), L.ptr(ws), B, C, H * W,
+                                                       groups, float(eps), int(relu), L.stream(x)),
+                    "group_norm_nchw_forward")
+        ctx.save_for_backward(x, weight, bias, mean, rstd)
+        ctx.cfg = (groups, bool(relu))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        groups, relu = ctx.cfg
+        B, C, H, W = x.shape
+        gy = gy.to(x.dtype).contiguous()
+        gx = torch.empty_like(x)
+        gw, gb = torch.empty_like(weight), torch.empty_like(bias)
+        ws = torch.empty(int(L.lib().vs_group_norm_nchw_workspace_bytes(B, C, groups)), device=x.device,
+                         dtype=torch.uint8)
+        with timed("group_norm_nchw_bwd", x, bytes_=5 * x.numel() * x.element_size()):
+            L.check(L.lib().vs_group_norm_nchw_backward(L.dtype_code(x), L.ptr(gy), L.ptr(x), L.ptr(weight),
+                                                        L.ptr(bias), L.ptr(mean), L.ptr(rstd), L.ptr(gx), L.ptr(gw),
+                                                        L.ptr(gb), L.ptr(ws), B, C, H * W, groups, int(relu),
+                                                        L.stream(x)), "group_norm_nchw_backward")
+        return gx, gw, gb, None, None, None
+
+
+def group_norm_nchw(x, weight, bias, groups: int, eps: float = 1e-5, relu: bool = False):
+    return GroupNormNCHWFunction.apply(x, weight, bias, int(groups), float(eps), bool(relu))
