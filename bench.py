@@ -67,7 +67,10 @@ def parse():
                     help="Hungarian matching on the device (csrc/match.hip) or scipy on the host")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=2)
-    ap.add_argument("--kernel-timing", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
+    ap.add_argument("--kernel-timing", type=int, default=1,
+                    help="HIP-event per-kernel timing (graphs: over --timing-steps eager steps after the timed region)")
+    ap.add_argument("--graphs", type=int, default=1, help="replay the step as HIP graphs (Trainer(graphs=True))")
+    ap.add_argument("--timing-steps", type=int, default=2, help="eager steps for per-kernel timing in graph mode")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "amp"],
                     help="bf16: bf16 params/activations + f32 master weights; amp: f32 params + bf16 autocast")
     ap.add_argument("--gemm-tuning", default="file", choices=["file", "tune", "off"],
@@ -183,17 +186,21 @@ def main():
     dev = torch.device("cuda", local)
     cfg = M2FConfig.preset(a.model, num_queries=a.queries)
     model = Mask2Former(cfg).init_weights(seed=0)
-    trainer = Trainer(model, SetCriterion(cfg, matcher=a.matcher), SolverConfig(precision=a.precision), device=dev)
+    trainer = Trainer(model, SetCriterion(cfg, matcher=a.matcher), SolverConfig(precision=a.precision), device=dev,
+                      graphs=bool(a.graphs))
+    graphs = trainer.graphs
     images, ml, cl = synthetic_batch(a.batch, a.size, seed=42 + rank, device=dev)
     torch.cuda.synchronize()
 
+    if graphs:    # the eager warm-ups of the trainer and the capture stay out of the timed region
+        a.warmup = max(a.warmup, trainer.graph_warmup + 1)
     for _ in range(a.warmup):
         trainer.step(images, ml, cl)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     timer = KernelTimer() if a.kernel_timing else None
-    if timer:
+    if timer and not graphs:
         timer.__enter__()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -202,6 +209,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if timer and graphs:
+        # a graph replay carries no event timestamps: time the kernels over eager steps
+        # of the same workload right after the timed region (outside it)
+        timer.__enter__()
+        for _ in range(max(1, a.timing_steps)):
+            trainer._eager_split_step(images, ml, cl) if trainer.split else trainer._eager_bf16_step(images, ml, cl)
+        torch.cuda.synchronize()
     if timer:
         timer.__exit__(None, None, None)
     t = torch.tensor([elapsed], device=dev)
@@ -229,6 +243,9 @@ def main():
             "gemm_tuning": a.gemm_tuning,
             "precision": a.precision,
             "matcher": a.matcher,
+            "graphs": graphs,
+            "kernel_timing": ("HIP events over %d eager steps after the timed region" % max(1, a.timing_steps))
+            if graphs else "HIP events over the timed region",
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels": table,

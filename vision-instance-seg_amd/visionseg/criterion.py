@@ -44,6 +44,7 @@ class SetCriterion:
         self.num_labels = cfg.num_labels
         self.matcher = matcher
         self._pairs = {}
+        self._ew = {}
 
     # --------------------------------------------------------------- matching
     @torch.no_grad()
@@ -99,6 +100,10 @@ class SetCriterion:
 
     # --------------------------------------------------------------- losses
     def _num_masks(self, class_labels, device):
+        tot = getattr(self, "num_masks_total", None)
+        if tot is not None:       # global count supplied by the trainer (graph-replayed steps)
+            ws = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+            return torch.clamp(tot / ws, min=1)
         n = torch.full((), float(sum(int(t.shape[0]) for t in class_labels)), device=device)   # fill, no copy
         ws = 1
         if dist.is_available() and dist.is_initialized():
@@ -132,8 +137,11 @@ class SetCriterion:
             bs = bt.expand(S, N)
             cls_all = torch.cat([t.to(dev) for t in class_labels]).long()
             tc[torch.arange(S, device=dev)[:, None], bs, qs] = cls_all.expand(S, N)
-        ew = torch.ones(self.num_labels + 1, device=dev)
-        ew[-1] = c.no_object_weight
+        ew = self._ew.get(dev)
+        if ew is None:        # made once: a scalar store is a host->device copy (not capturable)
+            ew = torch.ones(self.num_labels + 1, device=dev)
+            ew[-1] = c.no_object_weight
+            self._ew[dev] = ew
         ce = F.cross_entropy(classes.float().reshape(S * B, Q, -1).transpose(1, 2), tc.view(S * B, Q),
                              weight=ew, reduction="none")                                  # [S*B, Q]
         # weighted mean per step, as nn.CrossEntropyLoss(weight) does

@@ -325,6 +325,7 @@ class PixelDecoder(nn.Module):
         self.lateral = ConvGN(channels[0], Fd, 1, False, nchw=True)
         self.output = ConvGN(Fd, Fd, 3, False, relu=True, nchw=True)
         self.mask_proj = nn.Conv2d(Fd, cfg.mask_feature_size, kernel_size=1)
+        self._norm_cache = {}
 
     def forward(self, feats):
         Fd = self.cfg.feature_size
@@ -340,7 +341,11 @@ class PixelDecoder(nn.Module):
         p = torch.cat([q.flatten(2).transpose(1, 2) + self.level_embed[i].view(1, 1, -1).to(q.dtype)
                        for i, q in enumerate(pos)], 1)
         ref = reference_points(shapes, B, dev)
-        norm = torch.tensor([[w, hh] for hh, w in shapes], device=dev, dtype=torch.float32)[None, None, None, :, None, :]
+        key = (tuple(shapes), dev)
+        norm = self._norm_cache.get(key)
+        if norm is None:      # made once per shape set: no host->device copy inside a graph capture
+            norm = torch.tensor([[w, hh] for hh, w in shapes], device=dev, dtype=torch.float32)[None, None, None, :, None, :]
+            self._norm_cache[key] = norm
         for layer in self.encoder:
             h = layer(h, p, ref, shapes, norm)
         outs, s = [], 0

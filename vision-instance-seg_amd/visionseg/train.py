@@ -83,7 +83,7 @@ class Trainer:
     criterion: callable(masks, classes, mask_labels, class_labels) -> (loss, parts)."""
 
     def __init__(self, model, criterion, solver: SolverConfig | None = None, device=None,
-                 distributed: bool | None = None):
+                 distributed: bool | None = None, graphs: bool = False, graph_warmup: int = 2):
         self.solver = solver or SolverConfig()
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
@@ -98,7 +98,19 @@ class Trainer:
         if distributed is None:
             distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self.distributed = distributed
-        if distributed:
+        # HIP-graph replay of the whole step (bf16 mode on a device; see step()): with
+        # several ranks the gradient all-reduce stays an eager RCCL call between two
+        # graphs (no collective inside a capture), so DDP's hooks are not used
+        self.graphs = bool(graphs) and self.device.type == "cuda" and self.mode == "bf16"
+        self.split = self.graphs and distributed
+        self.graph_warmup = max(1, int(graph_warmup))
+        self._graph_states, self._eager_seen = {}, {}
+        if self.split:
+            self.net = self.model
+            with torch.no_grad():                       # DDP's start-up broadcast from rank 0
+                for t in list(self.model.parameters()) + list(self.model.buffers()):
+                    dist.broadcast(t, 0)
+        elif distributed:
             kw = dict(bucket_cap_mb=self.solver.bucket_cap_mb, gradient_as_bucket_view=True, broadcast_buffers=False)
             if self.device.type == "cuda":
                 kw["device_ids"] = [self.device.index]
@@ -125,9 +137,23 @@ class Trainer:
         else:
             self.params = params
         fused = self.device.type == "cuda"
-        self.opt = torch.optim.AdamW(self.params, lr=self.solver.lr, betas=self.solver.betas,
-                                     weight_decay=self.solver.weight_decay, fused=fused, foreach=None if fused else True)
+        okw = dict(fused=fused, foreach=None if fused else True)
+        lr = self.solver.lr
+        if self.graphs:
+            # device-side step count and a tensor lr: replays see the scheduler's updates
+            okw["capturable"] = True
+            lr = torch.tensor(lr, device=self.device, dtype=torch.float32)
+        self.opt = torch.optim.AdamW(self.params, lr=lr, betas=self.solver.betas,
+                                     weight_decay=self.solver.weight_decay, **okw)
+        if self.split:
+            self.flat_g16 = torch.zeros(self.flat.total, device=self.device, dtype=torch.bfloat16)
+            self.g16_views = self.flat.views(self.flat_g16)
+            self.num_masks_total = torch.zeros((), device=self.device, dtype=torch.float32)
         self.sched = torch.optim.lr_scheduler.LambdaLR(self.opt, _lr_lambda(self.solver))
+        if self.graphs:
+            # float bases: the scheduler then fills the lr tensor from a host float (a tensor
+            # base would make it read the value back, one host sync per step)
+            self.sched.base_lrs = [float(self.solver.lr) for _ in self.opt.param_groups]
         self.iter = 0
 
     @torch.no_grad()
@@ -155,8 +181,105 @@ class Trainer:
         classes = [c.float() for c in classes]
         return self.criterion(masks, classes, mask_labels, class_labels)
 
+    # ----------------------------------------------------------- graph-replayed step
+    def _phase1(self, images, mask_labels, class_labels):
+        """Forward + loss + backward, then the gradients into the flat buffer of the next
+        phase (f32 master grads; bf16 all-reduce buffer when split)."""
+        for p in self.model_params:
+            p.grad = None
+        loss, _ = self.forward_loss(images, mask_labels, class_labels)
+        loss.backward()
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.model_params]
+        with torch.no_grad():
+            torch._foreach_copy_(self.g16_views if self.split else [m.grad for m in self.params], grads)
+        return loss.detach()
+
+    @torch.no_grad()
+    def _phase2(self):
+        """(split: averaged bf16 grads -> f32 master grads) clip, AdamW, master -> bf16."""
+        if self.split:
+            torch._foreach_copy_([m.grad for m in self.params], self.g16_views)
+            self.flat_grad.mul_(1.0 / dist.get_world_size())
+        self.clip_gradients()
+        self.opt.step()
+        torch._foreach_copy_(self.model_params, self.params)
+
+    def _set_num_masks(self, class_labels):
+        """split mode: the criterion's global target count, all-reduced eagerly (it is a
+        graph input, not a collective inside the capture)."""
+        self.num_masks_total.fill_(float(sum(int(t.shape[0]) for t in class_labels)))
+        dist.all_reduce(self.num_masks_total)
+        self.criterion.num_masks_total = self.num_masks_total
+
+    def _eager_split_step(self, images, mask_labels, class_labels):
+        self._set_num_masks(class_labels)
+        loss = self._phase1(images, mask_labels, class_labels)
+        dist.all_reduce(self.flat_g16)
+        self._phase2()
+        return loss
+
+    def _capture(self, images, mask_labels, class_labels):
+        st = {"images": images.clone(), "ml": [m.clone() for m in mask_labels],
+              "cl": [c.clone() for c in class_labels], "graphs": []}
+        torch.cuda.synchronize(self.device)
+        pool = torch.cuda.graph_pool_handle()
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, pool=pool):
+            st["loss"] = self._phase1(st["images"], st["ml"], st["cl"])
+            if not self.split:
+                self._phase2()
+        st["graphs"].append(g1)
+        if self.split:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=pool):
+                self._phase2()
+            st["graphs"].append(g2)
+        torch.cuda.synchronize(self.device)
+        return st
+
+    def _graph_step(self, images, mask_labels, class_labels):
+        key = (tuple(images.shape), images.dtype, tuple((tuple(m.shape), m.dtype) for m in mask_labels),
+               tuple((tuple(c.shape), c.dtype) for c in class_labels))
+        st = self._graph_states.get(key)
+        if st is None:
+            seen = self._eager_seen.get(key, 0)
+            if seen < self.graph_warmup:
+                # eager steps first: lazy library state and the optimiser's moments exist
+                # before the capture (a capture records launches, it runs nothing)
+                self._eager_seen[key] = seen + 1
+                return self._eager_split_step(images, mask_labels, class_labels) if self.split else \
+                    self._eager_bf16_step(images, mask_labels, class_labels)
+            st = self._graph_states[key] = self._capture(images, mask_labels, class_labels)
+        with torch.no_grad():
+            st["images"].copy_(images)
+            for d, x in zip(st["ml"], mask_labels):
+                d.copy_(x)
+            for d, x in zip(st["cl"], class_labels):
+                d.copy_(x)
+        if self.split:
+            self._set_num_masks(class_labels)
+            st["graphs"][0].replay()
+            dist.all_reduce(self.flat_g16)
+            st["graphs"][1].replay()
+        else:
+            st["graphs"][0].replay()
+        return st["loss"].clone()
+
+    def _eager_bf16_step(self, images, mask_labels, class_labels):
+        loss = self._phase1(images, mask_labels, class_labels)
+        self._phase2()
+        return loss
+
     def step(self, images, mask_labels, class_labels):
-        """One optimisation step; returns the (device) loss tensor, no host sync."""
+        """One optimisation step; returns the (device) loss tensor, no host sync.  With
+        graphs=True the step is captured once per input-shape signature (after
+        `graph_warmup` eager steps of that signature) and replayed: one launch per graph
+        instead of ~3200 per step."""
+        if self.graphs:
+            loss = self._graph_step(images, mask_labels, class_labels)
+            self.sched.step()
+            self.iter += 1
+            return loss
         if self.mode != "bf16":
             self.opt.zero_grad(set_to_none=True)
         for p in self.model_params:
