@@ -244,6 +244,16 @@ VS_API int vs_group_norm_nchw_backward(int dtype, const void* grad_y, const void
                                        void* grad_weight, void* grad_bias, void* workspace, int batch,
                                        int channels, int hw, int groups, int relu, void* stream);
 
+/* ---- small-token Linear weight / bias gradient (csrc/small_linear.hip) ------------
+ * Replaces the backward GEMM + bias reduction autograd runs for the masked-attention
+ * decoder's Linears (HF:m2f Mask2FormerMaskedAttentionDecoderLayer q/k/v/out projections
+ * and FFN, Mask2FormerMLPPredictionHead; B x Q = 400 tokens): grad_w[o, i] = sum_t
+ * grad_y[t, o] x[t, i], grad_b[o] = sum_t grad_y[t, o] (grad_b may be NULL), f32
+ * accumulation, bf16 in / out.  grad_y [tokens, out], x [tokens, in], grad_w [out, in],
+ * out and in multiples of 64. */
+VS_API int vs_small_linear_wgrad(int dtype, const void* grad_y, const void* x, void* grad_w, void* grad_b,
+                                 int tokens, int out_features, int in_features, void* stream);
+
 /* ---- split-K epilogue (csrc/norm.hip) -------------------------------------------------
  * out[i] = sum_{s < num_parts} partials[s * n + i] (+ extra[i] when extra != NULL), f32
  * accumulation in a fixed order, out in dtype: the weight gradient of a token-major

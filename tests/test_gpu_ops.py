@@ -612,3 +612,45 @@ def _check_group_norm(fn, dtype, relu, shape, groups, cl):
     for name, got, exp in (("dx", xd.grad, xr.grad), ("dw", wd.grad, wr.grad), ("db", bd.grad, br.grad)):
         e = float((got.detach().double().cpu() - exp.detach()).abs().max())
         assert e <= tol * max(1.0, float(exp.detach().abs().max())), (name, e, float(exp.detach().abs().max()))
+
+
+# ------------------------------------------------------------------ small-token Linear
+@pytest.mark.parametrize("T,I,O,bias", [(400, 256, 256, True), (400, 256, 2048, True), (400, 2048, 256, True),
+                                        (1, 64, 128, True), (1000, 128, 64, False), (64, 256, 256, True),
+                                        (0, 64, 64, True)])
+def test_small_linear_grads_vs_torch(T, I, O, bias):
+    """csrc/small_linear.hip dW / db (+ library dX) vs torch f64 on the same bf16 operands."""
+    from visionseg.linear import small_linear
+    g = torch.Generator().manual_seed(T + I + O)
+    x = torch.randn(T, I, generator=g).to(torch.bfloat16)
+    w = (torch.randn(O, I, generator=g) / I ** 0.5).to(torch.bfloat16)
+    b = torch.randn(O, generator=g).to(torch.bfloat16) if bias else None
+    gy = torch.randn(T, O, generator=g).to(torch.bfloat16)
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    bd = b.to(DEV).requires_grad_(True) if bias else None
+    y = small_linear(xd, wd, bd)
+    y.backward(gy.to(DEV))
+    xr, wr = x.double().requires_grad_(True), w.double().requires_grad_(True)
+    br = b.double().requires_grad_(True) if bias else None
+    torch.nn.functional.linear(xr, wr, br).backward(gy.double())
+    pairs = [("dx", xd.grad, xr.grad), ("dw", wd.grad, wr.grad)] + ([("db", bd.grad, br.grad)] if bias else [])
+    for name, got, exp in pairs:
+        e = float((got.double().cpu() - exp).abs().max()) if exp.numel() else 0.0
+        scale = float(exp.abs().max()) if exp.numel() else 0.0
+        assert e <= 2 ** -7 * max(1.0, scale) + 1e-3, (name, e, scale)
+
+
+def test_small_linear_weight_slice():
+    """A weight slice (the decoder's cross-attention q rows of in_proj_weight) gets its
+    gradient rows back through autograd's slice."""
+    from visionseg.linear import small_linear
+    g = torch.Generator().manual_seed(5)
+    W = (torch.randn(768, 256, generator=g) / 16).to(torch.bfloat16).to(DEV).requires_grad_(True)
+    bb = torch.randn(768, generator=g).to(torch.bfloat16).to(DEV).requires_grad_(True)
+    x = torch.randn(4, 100, 256, generator=g).to(torch.bfloat16).to(DEV)
+    small_linear(x, W[:256], bb[:256]).float().sum().backward()
+    assert float(W.grad[256:].abs().max()) == 0.0 and float(bb.grad[256:].abs().max()) == 0.0
+    ref = x.double().reshape(-1, 256).sum(0)
+    assert torch.allclose(W.grad[0].double().cpu(), ref.cpu(), rtol=2 ** -7, atol=1e-2)
+    assert abs(float(bb.grad[0]) - 400.0) <= 2.0

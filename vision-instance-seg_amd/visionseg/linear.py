@@ -151,6 +151,58 @@ def plane_projection(y, weight, bias=None):
     return out.view(B, H, W, -1).permute(0, 3, 1, 2)
 
 
+SMALL_MAX_TOKENS = 4096
+_SMALL = os.environ.get("VS_SMALL_LINEAR", "1") == "1"      # A/B switch
+
+
+class _SmallLinearFn(torch.autograd.Function):
+    """Linear over a few hundred tokens: forward / dX are library GEMMs, dW and db one HIP
+    launch (csrc/small_linear.hip) instead of a single-tile GEMM plus a reduction."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        O, I = weight.shape
+        gy2 = gy.reshape(-1, O).contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = (gy2 @ weight).view(x.shape)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            x2 = x.reshape(-1, I).contiguous()
+            gw = torch.empty(O, I, device=gy2.device, dtype=torch.bfloat16)
+            gb = torch.empty(O, device=gy2.device, dtype=torch.bfloat16) if ctx.has_bias else None
+            L.check(L.lib().vs_small_linear_wgrad(L.dtype_code(gw), L.ptr(gy2), L.ptr(x2), L.ptr(gw),
+                                                  L.ptr(gb) if gb is not None else None, gy2.shape[0], O, I,
+                                                  L.stream(gy2)), "small_linear_wgrad")
+            if not ctx.needs_input_grad[1]:
+                gw = None
+        return gx, gw, gb
+
+
+def small_linear(x, w, b=None):
+    """F.linear with the one-launch weight/bias gradient for small bf16 token counts."""
+    tokens = x.numel() // max(1, x.shape[-1])
+    O, I = w.shape
+    if (_SMALL and x.is_cuda and torch.is_grad_enabled() and w.requires_grad and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and (b is None or b.dtype == torch.bfloat16)
+            and tokens <= SMALL_MAX_TOKENS and O % 64 == 0 and I % 64 == 0 and not torch.is_autocast_enabled()):
+        return _SmallLinearFn.apply(x, w, b)
+    return F.linear(x, w, b)
+
+
+class SmallLinear(nn.Linear):
+    """nn.Linear for the decoder's B x Q tokens (see small_linear)."""
+
+    def forward(self, x):
+        return small_linear(x, self.weight, self.bias)
+
+
 class TokenLayerNorm(nn.LayerNorm):
     """nn.LayerNorm on the HIP row kernel (csrc/norm.hip) for f32 / bf16 device tensors
     whose weight shares their dtype; anything else (autocast's f32 LayerNorm, CPU

@@ -28,7 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .linear import TokenLayerNorm, TokenLinear, linear_tokens, plane_projection
+from .linear import SmallLinear, TokenLayerNorm, TokenLinear, linear_tokens, plane_projection, small_linear
 
 
 @dataclass
@@ -371,16 +371,16 @@ class CrossAttn(nn.Module):
         super().__init__()
         self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d))
         self.in_proj_bias = nn.Parameter(torch.zeros(3 * d))
-        self.out_proj = nn.Linear(d, d)
+        self.out_proj = SmallLinear(d, d)
 
 
 class SelfAttn(nn.Module):
     def __init__(self, d):
         super().__init__()
-        self.q_proj = nn.Linear(d, d)
-        self.k_proj = nn.Linear(d, d)
-        self.v_proj = nn.Linear(d, d)
-        self.out_proj = nn.Linear(d, d)
+        self.q_proj = SmallLinear(d, d)
+        self.k_proj = SmallLinear(d, d)
+        self.v_proj = SmallLinear(d, d)
+        self.out_proj = SmallLinear(d, d)
 
 
 class DecoderLayer(nn.Module):
@@ -391,8 +391,8 @@ class DecoderLayer(nn.Module):
         self.norm_cross = nn.LayerNorm(d)
         self.self_attn = SelfAttn(d)
         self.norm_self = nn.LayerNorm(d)
-        self.fc1 = nn.Linear(d, ffn)
-        self.fc2 = nn.Linear(ffn, d)
+        self.fc1 = SmallLinear(d, ffn)
+        self.fc2 = SmallLinear(ffn, d)
         self.norm_ffn = nn.LayerNorm(d)
 
     def forward(self, h, qpos, mem, mem_pos, words):
@@ -400,7 +400,7 @@ class DecoderLayer(nn.Module):
         B, Q, D = h.shape
         H, d = self.heads, D // self.heads
         W, b = self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias
-        q = F.linear(h + qpos, W[:D], b[:D])
+        q = small_linear(h + qpos, W[:D], b[:D])
         k = linear_tokens(mem_pos, W[D:2 * D], b[D:2 * D])
         v = linear_tokens(mem, W[2 * D:], b[2 * D:])
         o = ops.masked_attention(q, k, v, words, H, d ** -0.5)
@@ -424,7 +424,7 @@ class Decoder(nn.Module):
         self.level_embed = nn.Embedding(3, d)
         self.layers = nn.ModuleList([DecoderLayer(d, cfg.dec_ffn, cfg.dec_heads) for _ in range(cfg.dec_layers - 1)])
         self.norm = nn.LayerNorm(d)
-        self.mask_embed = nn.ModuleList([nn.Linear(d, d), nn.Linear(d, d), nn.Linear(d, cfg.mask_feature_size)])
+        self.mask_embed = nn.ModuleList([SmallLinear(d, d), SmallLinear(d, d), SmallLinear(d, cfg.mask_feature_size)])
         # Parity-test hook ("teacher forcing"): a list of bool [B,Q,h*w] blocked masks, one per
         # decoder layer, used instead of the masks this decoder derives itself.  Lets a test
         # separate threshold-decision flips (sigmoid(x) < 0.5 at |x| ~ rounding) from arithmetic.
