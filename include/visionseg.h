@@ -94,6 +94,19 @@ VS_API int vs_msda_backward_encoder(int dtype, const void* value, const int64_t*
                                     int num_heads, int channels, int num_levels, int num_point,
                                     void* stream);
 
+/* Backward with grad_value built by destination after a counting sort of the corner
+ * contributions (any queries; no float atomics): grad_value [B, S, H, 32] is written in
+ * the value dtype (every row once), grad_loc / grad_attn as in vs_msda_backward.  Same
+ * results up to f32 summation order.  workspace >= vs_msda_backward_sorted_workspace_bytes. */
+VS_API long long vs_msda_backward_sorted_workspace_bytes(int batch, int spatial_size, int num_heads, int num_query,
+                                                         int num_levels, int num_point);
+VS_API int vs_msda_backward_sorted(int dtype, const void* value, const int64_t* spatial_shapes_host,
+                                   const int64_t* level_start_host, const float* sampling_loc,
+                                   const float* attn_weight, const void* grad_out, void* grad_value,
+                                   float* grad_loc, float* grad_attn, void* workspace, int batch, int spatial_size,
+                                   int num_heads, int channels, int num_levels, int num_query, int num_point,
+                                   void* stream);
+
 /* ---- a2: Swin pad + cyclic shift + window partition / its inverse ---------------
  * window_partition: x [B, H, W, C] -> windows [B*nWh*nWw, ws*ws, C] where
  * Hp = ceil(H/ws)*ws, nWh = Hp/ws (same for W); windows[(b,wy,wx), (ty,tx)] =

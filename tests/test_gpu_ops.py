@@ -350,6 +350,7 @@ def test_msda_encoder_backward_vs_oracle(monkeypatch, cfg, dtype, pull_r):
     the oracle; R0 = 0 sends nearly every tap through the far (atomic) path."""
     monkeypatch.setenv("VS_MSDA_PULL_R", pull_r)
     ops = _ops()
+    monkeypatch.setattr(ops, "_MSDA_SORTED", False)          # the atomic scatter paths
     shapes, B, H, L, P = cfg["shapes"], cfg["B"], cfg["H"], len(cfg["shapes"]), 4
     S = sum(h * w for h, w in shapes)
     g = torch.Generator().manual_seed(31)
@@ -431,6 +432,7 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, jitter):
     queries, runs of 16 / 7 (ragged) queries and the plain kernel (0), vs the oracle."""
     monkeypatch.setenv("VS_MSDA_RUN", run)
     ops = _ops()
+    monkeypatch.setattr(ops, "_MSDA_SORTED", False)
     shapes = [(8, 8), (16, 16), (32, 32)]
     value, loc, w = _encoder_like_inputs(2, shapes, 4, 4, seed=11, jitter=jitter)
     vr, lr, wr = (t.clone().requires_grad_(True) for t in (value, loc, w))
@@ -444,6 +446,46 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, jitter):
     np.testing.assert_allclose(wd.grad.cpu().numpy(), wr.grad.numpy(), atol=2e-5, rtol=0)
     gl = lr.grad.numpy()
     np.testing.assert_allclose(ld.grad.cpu().numpy(), gl, atol=2e-5 * max(1.0, np.abs(gl).max()), rtol=0)
+
+
+@pytest.mark.parametrize("case", [
+    dict(B=2, shapes=[(8, 8), (16, 16), (32, 32)], H=4, jitter=0.0, Q=None),
+    dict(B=2, shapes=[(8, 8), (16, 16), (32, 32)], H=4, jitter=3.0, Q=None),
+    dict(B=1, shapes=[(32, 32), (64, 64), (128, 128)], H=8, jitter=0.3, Q=None),     # 1024^2 encoder, one image
+    dict(B=1, shapes=[(16, 16), (32, 32), (64, 64)], H=8, jitter=12.0, Q=None),      # far taps, many off-grid
+    dict(B=2, shapes=[(12, 20), (24, 40), (48, 80), (6, 10)], H=8, jitter=1.0, Q=300),  # decoder-like, 4 levels
+    dict(B=1, shapes=[(5, 7)], H=2, jitter=1.0, Q=0),                                  # no queries
+])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_msda_sorted_backward_vs_oracle(monkeypatch, case, dtype):
+    """grad_value by destination after a counting sort (vs_msda_backward_sorted, opt-in
+    path) vs the oracle; bf16: grad_value is produced in bf16 from f32 sums."""
+    ops = _ops()
+    monkeypatch.setattr(ops, "_MSDA_SORTED", True)
+    shapes, B, H = case["shapes"], case["B"], case["H"]
+    value, loc, w = _encoder_like_inputs(B, shapes, H, 4, seed=21, jitter=case["jitter"])
+    if case["Q"] is not None:
+        g = torch.Generator().manual_seed(4)
+        idx = torch.randint(0, loc.shape[1], (case["Q"],), generator=g)
+        loc, w = loc[:, idx].contiguous(), w[:, idx].contiguous()
+    value = value.to(dtype)
+    vr, lr, wr = value.float().clone().requires_grad_(True), loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    ref = R.msda_ref(vr, shapes, lr, wr)
+    go = torch.randn(ref.shape, generator=torch.Generator().manual_seed(8)).to(dtype)
+    ref.backward(go.float())
+    vd, ld, wd = value.to(DEV).requires_grad_(True), loc.to(DEV).requires_grad_(True), w.to(DEV).requires_grad_(True)
+    out = ops.ms_deform_attn(vd, shapes, ld, wd)
+    out.backward(go.to(DEV))
+    assert vd.grad.dtype == dtype
+    if dtype == torch.float32:
+        np.testing.assert_allclose(vd.grad.cpu().numpy(), vr.grad.numpy(), atol=2e-5, rtol=0)
+    else:
+        err = (vd.grad.float().cpu() - vr.grad).abs()
+        assert bool((err <= vr.grad.abs() * 2 ** -8 + 1e-4).all()), float(err.max())
+    if loc.shape[1]:
+        e = wr.grad.numpy()
+        np.testing.assert_allclose(wd.grad.cpu().numpy(), e, atol=2e-5 * max(1.0, np.abs(e).max()) * (
+            1 if dtype == torch.float32 else 400), rtol=0 if dtype == torch.float32 else 2 ** -6)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -564,6 +564,195 @@ __global__ void __launch_bounds__(256) msda_bwd_pull_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------
+// grad_value by destination after a counting sort of the corner contributions (no float
+// atomics).  key(b, cell, h) = (b * S + cell) * Hh + h: the grad_value row of that
+// head, so keys in order are the output in order.
+//   count:  per valid corner of every tap, count[key] += 1 (int atomics)
+//   scan:   offset(key) = exclusive prefix of count (1024-key blocks + block prefix)
+//   fill:   slot = offset(key) + (atomicSub(count[key], 1) - 1): record {query, weight}
+//           (count returns to 0)
+//   pull:   a group of lanes per key sums weight * grad_out[b, query, h, :] over its
+//           records in f32 and writes the row once, in the value dtype
+// The contributions reaching one row come from the queries whose taps land next to it;
+// their grad_out rows are re-read from L2 / MALL, not HBM.
+constexpr int kScanBlock = 1024;
+
+__device__ __forceinline__ void corner_keys(const Tap& tg, int Wl, int Hl, long long rowbase, int Hh, long long* key,
+                                            float* wk) {
+  const int h0 = tg.h0, w0 = tg.w0;
+  const bool ok[4] = {h0 >= 0 && w0 >= 0, h0 >= 0 && w0 + 1 <= Wl - 1, h0 + 1 <= Hl - 1 && w0 >= 0,
+                      h0 + 1 <= Hl - 1 && w0 + 1 <= Wl - 1};
+  const int off[4] = {h0 * Wl + w0, h0 * Wl + w0 + 1, (h0 + 1) * Wl + w0, (h0 + 1) * Wl + w0 + 1};
+  wk[0] = tg.hh * tg.hw;
+  wk[1] = tg.hh * tg.lw;
+  wk[2] = tg.lh * tg.hw;
+  wk[3] = tg.lh * tg.lw;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) key[k] = ok[k] ? (rowbase + off[k]) * Hh : -1;
+}
+
+// one thread per tap (b, q, h, l, p); FILL = false: count, true: write records
+template <bool FILL>
+__global__ void __launch_bounds__(256) msda_sort_kernel(const float* __restrict__ loc, const float* __restrict__ attw,
+                                                        int* __restrict__ count, const int* __restrict__ local,
+                                                        const int* __restrict__ bprefix, int2* __restrict__ rec,
+                                                        Levels lv, int S, int Hh, int Q, int L, int P, long long taps) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= taps) return;
+  const int LP = L * P;
+  const int t = (int)(i % LP);
+  const long long grp = i / LP;
+  const int h = (int)(grp % Hh);
+  const long long bq = grp / Hh;
+  const int q = (int)(bq % Q);
+  const long long b = bq / Q;
+  const int l = t / P;
+  const int Hl = lv.h[l], Wl = lv.w[l];
+  const float2 xy = reinterpret_cast<const float2*>(loc)[i];
+  const Tap tg = tap_geom(xy.x, xy.y, Hl, Wl);
+  if (!tg.inside) return;
+  long long key[4];
+  float wk[4];
+  corner_keys(tg, Wl, Hl, b * S + lv.start[l], Hh, key, wk);
+  if (!FILL) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (key[k] >= 0) atomicAdd(count + key[k] + h, 1);
+  } else {
+    const float a = attw[i];
+    int slot[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) slot[k] = key[k] >= 0 ? atomicSub(count + key[k] + h, 1) - 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (key[k] >= 0) {
+        const long long kk = key[k] + h;
+        rec[local[kk] + bprefix[kk / kScanBlock] + slot[k]] = make_int2(q, __float_as_int(a * wk[k]));
+      }
+  }
+}
+
+// block-local exclusive scan of count (kScanBlock keys per block) + block totals
+__global__ void __launch_bounds__(256) sort_scan_local_kernel(const int* __restrict__ count, int* __restrict__ local,
+                                                              int* __restrict__ bsum, long long n) {
+  __shared__ int sw[4];
+  const long long base = (long long)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  int v[4], s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = base + k < n ? count[base + k] : 0;
+    s += v[k];
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = s;                                   // inclusive scan of s over the wave
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) sw[wave] = incl;
+  __syncthreads();
+  int wpre = 0;
+  for (int w = 0; w < wave; ++w) wpre += sw[w];
+  int run = wpre + incl - s;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (base + k < n) local[base + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 255) bsum[blockIdx.x] = wpre + incl;
+}
+
+// exclusive scan of the block totals (one workgroup, any count); bprefix[nb] = total
+__global__ void __launch_bounds__(1024) sort_scan_blocks_kernel(const int* __restrict__ bsum, int* __restrict__ bprefix,
+                                                                int nb) {
+  __shared__ int sw[16];
+  __shared__ int carry;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < nb; base += 1024) {
+    const int i = base + threadIdx.x;
+    const int s = i < nb ? bsum[i] : 0;
+    int incl = s;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) sw[wave] = incl;
+    __syncthreads();
+    int wpre = 0;
+    for (int w = 0; w < wave; ++w) wpre += sw[w];
+    const int c0 = carry;
+    if (i < nb) bprefix[i] = c0 + wpre + incl - s;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = c0 + wpre + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bprefix[nb] = carry;
+}
+
+// one group of LPG lanes per key (grad_value row of one head), V channels per lane
+template <typename T>
+__global__ void __launch_bounds__(256) msda_pull_sorted_kernel(const int* __restrict__ local,
+                                                               const int* __restrict__ bprefix,
+                                                               const int2* __restrict__ rec, const T* __restrict__ gout,
+                                                               T* __restrict__ gvalue, int S, int Hh, int Q,
+                                                               long long nkeys) {
+  constexpr int V = Vec16<T>::N;
+  constexpr int LPG = kD / V;
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long key = gid / LPG;
+  const int sub = (int)(gid % LPG);
+  if (key >= nkeys) return;
+  const int r0 = local[key] + bprefix[key / kScanBlock];
+  const int r1 = key + 1 < nkeys ? local[key + 1] + bprefix[(key + 1) / kScanBlock] : bprefix[(nkeys - 1) / kScanBlock + 1];
+  const int h = (int)(key % Hh);
+  const long long b = key / Hh / S;
+  const T* gb = gout + ((size_t)b * Q * Hh + h) * kD + sub * V;
+  const size_t qstride = (size_t)Hh * kD;
+  float acc[V];
+#pragma unroll
+  for (int c = 0; c < V; ++c) acc[c] = 0.f;
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {            // 4 records' gathers in flight
+    int2 e[4];
+    float g[4][V];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) e[u] = rec[r + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) Vec16<T>::load(gb + (size_t)e[u].x * qstride, g[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float w = __int_as_float(e[u].y);
+#pragma unroll
+      for (int c = 0; c < V; ++c) acc[c] = __fmaf_rn(w, g[u][c], acc[c]);
+    }
+  }
+  for (; r < r1; ++r) {
+    const int2 e = rec[r];
+    float g[V];
+    Vec16<T>::load(gb + (size_t)e.x * qstride, g);
+    const float w = __int_as_float(e.y);
+#pragma unroll
+    for (int c = 0; c < V; ++c) acc[c] = __fmaf_rn(w, g[c], acc[c]);
+  }
+  Vec16<T>::store(gvalue + key * kD + sub * V, acc);
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// workspace: count [nkeys] | local [nkeys] | bsum [nb] | bprefix [nb + 1] | records
+void sorted_layout(long long nkeys, long long maxrec, size_t* off) {
+  const long long nb = (nkeys + kScanBlock - 1) / kScanBlock;
+  off[0] = 0;
+  off[1] = align256(off[0] + nkeys * 4);
+  off[2] = align256(off[1] + nkeys * 4);
+  off[3] = align256(off[2] + nb * 4);
+  off[4] = align256(off[3] + (nb + 1) * 4);
+  off[5] = align256(off[4] + (size_t)maxrec * 8);
+}
+
 int fill_levels(Levels* lv, const int64_t* shapes, const int64_t* starts, int L, int S) {
   long long tot = 0;
   for (int l = 0; l < L; ++l) {
@@ -588,10 +777,11 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
   VS_CHECK(D == kD, "channels per head must be 32");
   VS_CHECK(L >= 1 && L <= kMaxLevels, "1..4 levels supported");
   VS_CHECK(B > 0 && S > 0 && Hh > 0 && Q >= 0 && P > 0, "bad sizes");
-  VS_CHECK(value && loc && attw && out && shapes && starts, "null pointer");
+  VS_CHECK(value && shapes && starts, "null pointer");
   Levels lv;
   VS_CHECK(fill_levels(&lv, shapes, starts, L, S), "spatial shapes / level starts inconsistent with S");
   if (Q == 0) return VS_OK;
+  VS_CHECK(loc && attw && out, "null pointer");
   hipStream_t st = (hipStream_t)stream;
   const long long groups = (long long)B * Q * Hh;
   const int block = 256;
@@ -732,4 +922,61 @@ extern "C" int vs_msda_backward_encoder(int dtype, const void* value, const int6
                                         void* stream) {
   return msda_backward_impl(dtype, value, shapes, starts, loc, attw, gout, gvalue, gloc, gattw, B, S, Hh, D, L, S,
                             P, stream, true);
+}
+
+extern "C" long long vs_msda_backward_sorted_workspace_bytes(int B, int S, int Hh, int Q, int L, int P) {
+  size_t off[6];
+  sorted_layout((long long)B * S * Hh, 4LL * B * Q * Hh * L * P, off);
+  return (long long)off[5];
+}
+
+extern "C" int vs_msda_backward_sorted(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
+                                       const float* loc, const float* attw, const void* gout, void* gvalue,
+                                       float* gloc, float* gattw, void* workspace, int B, int S, int Hh, int D, int L,
+                                       int Q, int P, void* stream) {
+  VS_CHECK(D == kD, "channels per head must be 32");
+  VS_CHECK(L >= 1 && L <= kMaxLevels, "1..4 levels supported");
+  VS_CHECK(B > 0 && S > 0 && Hh > 0 && Q >= 0 && P > 0, "bad sizes");
+  VS_CHECK(value && gvalue && shapes && starts && workspace, "null pointer");
+  VS_CHECK(Q == 0 || (loc && attw && gout && gloc && gattw), "null pointer");
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  Levels lv;
+  VS_CHECK(fill_levels(&lv, shapes, starts, L, S), "spatial shapes / level starts inconsistent with S");
+  const long long nkeys = (long long)B * S * Hh;
+  const long long taps = (long long)B * Q * Hh * L * P;
+  VS_CHECK(4 * taps < (1LL << 31), "too many corner contributions for 32-bit record offsets");
+  hipStream_t st = (hipStream_t)stream;
+  size_t off[6];
+  sorted_layout(nkeys, 4 * taps, off);
+  char* ws = (char*)workspace;
+  int* count = (int*)(ws + off[0]);
+  int* local = (int*)(ws + off[1]);
+  int* bsum = (int*)(ws + off[2]);
+  int* bprefix = (int*)(ws + off[3]);
+  int2* rec = (int2*)(ws + off[4]);
+  const int nb = (int)((nkeys + kScanBlock - 1) / kScanBlock);
+  VS_HIP(hipMemsetAsync(count, 0, (size_t)nkeys * 4, st));
+  if (Q > 0) {
+    const int tgrid = (int)((taps + 255) / 256);
+    hipLaunchKernelGGL(msda_sort_kernel<false>, dim3(tgrid), dim3(256), 0, st, loc, attw, count, local, bprefix, rec,
+                       lv, S, Hh, Q, L, P, taps);
+  }
+  hipLaunchKernelGGL(sort_scan_local_kernel, dim3(nb), dim3(256), 0, st, count, local, bsum, nkeys);
+  hipLaunchKernelGGL(sort_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, bsum, bprefix, nb);
+  if (Q > 0) {
+    const int tgrid = (int)((taps + 255) / 256);
+    hipLaunchKernelGGL(msda_sort_kernel<true>, dim3(tgrid), dim3(256), 0, st, loc, attw, count, local, bprefix, rec,
+                       lv, S, Hh, Q, L, P, taps);
+  }
+  const int lpg = dtype == VS_BF16 ? 4 : 8;
+  const int pgrid = (int)((nkeys * lpg + 255) / 256);
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(msda_pull_sorted_kernel<bf16>, dim3(pgrid), dim3(256), 0, st, local, bprefix, rec,
+                       (const bf16*)gout, (bf16*)gvalue, S, Hh, Q, nkeys);
+  else
+    hipLaunchKernelGGL(msda_pull_sorted_kernel<float>, dim3(pgrid), dim3(256), 0, st, local, bprefix, rec,
+                       (const float*)gout, (float*)gvalue, S, Hh, Q, nkeys);
+  if (Q > 0) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, (long long)B * Q * Hh, st);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
 }
