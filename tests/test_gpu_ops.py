@@ -342,13 +342,14 @@ def test_mask_head_backward_bf16_vs_oracle(shape):
     dict(B=1, shapes=[(32, 32), (64, 64), (128, 128)], H=8, spread=4.0),     # 1024^2 pixel decoder, init-like
     dict(B=1, shapes=[(16, 16), (32, 32), (64, 64)], H=8, spread=12.0),      # many far taps (atomic path)
     dict(B=2, shapes=[(12, 20), (24, 40), (48, 80)], H=8, spread=3.0),       # non-square (tiny fixture 'b' like)
+    dict(B=2, shapes=[(48, 80), (24, 40), (12, 20), (6, 10)], H=4, spread=3.0),  # 4 levels, finest first
 ])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("pull_r", ["5", "0"])
-def test_msda_encoder_backward_vs_oracle(monkeypatch, cfg, dtype, pull_r):
-    """Encoder mode (queries = value grid): destination pull kernel + far-tap atomics vs
-    the oracle; R0 = 0 sends nearly every tap through the far (atomic) path."""
-    monkeypatch.setenv("VS_MSDA_PULL_R", pull_r)
+@pytest.mark.parametrize("near_r", ["5", "0", "9"])
+def test_msda_encoder_backward_vs_oracle(monkeypatch, cfg, dtype, near_r):
+    """Encoder mode (queries = value grid): LDS destination-tile kernel (near taps) +
+    far-tap atomics vs the oracle; R0 = 0 sends most taps through the far (atomic) path."""
+    monkeypatch.setenv("VS_MSDA_NEAR_R", near_r)
     ops = _ops()
     monkeypatch.setattr(ops, "_MSDA_SORTED", False)          # the atomic scatter paths
     shapes, B, H, L, P = cfg["shapes"], cfg["B"], cfg["H"], len(cfg["shapes"]), 4

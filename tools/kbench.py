@@ -68,14 +68,14 @@ def main():
             for mode in ("sorted", "carry16", "plain", "pull5"):
                 ops._MSDA_SORTED = mode == "sorted"
                 os.environ["VS_MSDA_RUN"] = {"carry16": "16"}.get(mode, "0")
-                os.environ["VS_MSDA_PULL_R"] = mode[4:] if mode.startswith("pull") else "5"
+                os.environ["VS_MSDA_NEAR_R"] = mode[4:] if mode.startswith("pull") else "5"
 
                 def fb(enc=mode.startswith("pull")):
                     o = ops.ms_deform_attn(v, shapes, locr, wr, encoder=enc)
                     o.backward(go)
                 run(f"msda {oname} {mode}", fb, a.iters)
             os.environ.pop("VS_MSDA_RUN")
-            os.environ.pop("VS_MSDA_PULL_R")
+            os.environ.pop("VS_MSDA_NEAR_R")
     if "mask" in a.only:
         Q, C, Hm = 100, 256, 256
         E = torch.randn(B, Q, C, device=dev, generator=g).to(bf).requires_grad_(True)

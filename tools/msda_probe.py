@@ -1,4 +1,4 @@
-"""Per-sub-kernel timing of the encoder-mode MSDA backward (pull / scatter / geom) on
+"""Per-sub-kernel timing of the encoder-mode MSDA backward (tile / scatter / geom) on
 smooth and iid offsets at several R0, via VS_MSDA_SKIP (C2 shapes, bf16)."""
 import os
 import sys
@@ -29,8 +29,8 @@ def main():
         loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
         locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
         for r0 in ("0", "3", "5"):
-            for skip, what in (("6", "pull"), ("5", "scatter"), ("3", "geom"), ("0", "all")):
-                os.environ["VS_MSDA_PULL_R"], os.environ["VS_MSDA_SKIP"] = r0, skip
+            for skip, what in (("6", "tile"), ("5", "scatter"), ("3", "geom"), ("0", "all")):
+                os.environ["VS_MSDA_NEAR_R"], os.environ["VS_MSDA_SKIP"] = r0, skip
 
                 def fb():
                     o = ops.ms_deform_attn(v, shapes, locr, wr, encoder=True)

@@ -45,10 +45,9 @@ struct Levels {
 };
 
 
-// ---- backward helpers shared by the pull and geom kernels (must stay identical: a
+// ---- backward helpers shared by the tile and scatter kernels (must stay identical: a
 // tap is accumulated by exactly one of them, decided by `near_tap`).
-constexpr int kPullR = 5;           // default cell margin R0 of the pull kernel (VS_MSDA_PULL_R)
-constexpr int kPullRows = 4, kPullCols = 16;   // value cells per wave of the pull kernel
+constexpr int kNearR = 5;           // default near margin R0 of the tile kernel (VS_MSDA_NEAR_R)
 
 struct Tap {
   int h0, w0;
@@ -79,11 +78,11 @@ __host__ __device__ __forceinline__ int mapped_cell(int xq, int nq, int nl) {
   return num >= 0 ? num / den : -((-num + den - 1) / den);
 }
 
-// a tap belongs to the pull kernel iff its query's level lq is not finer than the tap's
-// level l, it is inside, and its top-left cell is within R0 cells (both axes) of the
-// query's mapped cell on level l
-__device__ __forceinline__ bool pull_tap(const Tap& t, int lq, int l, int mcy, int mcx, int R0) {
-  return lq <= l && t.inside && abs(t.h0 - mcy) <= R0 && abs(t.w0 - mcx) <= R0;
+// a tap belongs to the tile kernel ("near") iff it is inside and its top-left cell is
+// within R0 cells (both axes) of the query's mapped cell on the tap's level; every other
+// tap is added by the scatter kernel
+__device__ __forceinline__ bool near_tap(const Tap& t, int mcy, int mcx, int R0) {
+  return t.inside && abs(t.h0 - mcy) <= R0 && abs(t.w0 - mcx) <= R0;
 }
 
 __device__ __forceinline__ int ceil_div(int a, int b) { return a >= 0 ? (a + b - 1) / b : -((-a) / b); }
@@ -347,8 +346,8 @@ __global__ void __launch_bounds__(256) msda_bwd_geom_kernel(
 
 constexpr int kScatterRun = 16;        // queries per half-wave run (LDS staging is sized for it)
 
-// ENC (encoder mode, Q == S level-major): taps owned by the pull kernel (pull_tap) are
-// skipped here; the pull kernel has already written every grad_value element.
+// ENC (encoder mode, Q == S level-major): near taps (near_tap) are skipped here; the
+// tile kernel has already written every grad_value element.
 template <typename T, int L, int P, bool ENC>
 __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
     const float* __restrict__ loc, const float* __restrict__ attw, const T* __restrict__ gout,
@@ -414,7 +413,7 @@ __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
         const int t = l * P + p;
         const Tap tg = tap_geom(sl[(i * LP + t) * 2 + 0], sl[(i * LP + t) * 2 + 1], Hl, Wl);
         if (!tg.inside) continue;             // no contribution; the held block stays
-        if (ENC && pull_tap(tg, lq, l, mapped_cell(yq, lv.h[lq], Hl), mapped_cell(xq, lv.w[lq], Wl), R0)) continue;
+        if (ENC && near_tap(tg, mapped_cell(yq, lv.h[lq], Hl), mapped_cell(xq, lv.w[lq], Wl), R0)) continue;
         const float ga = g * sw[i * LP + t];
         const int dy = tg.h0 - ph[t], dx = tg.w0 - pw[t];
         // held corner k = (cy, cx) survives iff (cy - dy, cx - dx) lies in the new block
@@ -451,116 +450,160 @@ __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
   }
 }
 
-// grad_value by destination (encoder mode; see the header).  Block = (16x16 cell tile
-// of level l, head, image), wave w = cell rows 4w..4w+3 of the tile, lane = one cell.
-// For each source level lq the wave enumerates the rectangle of queries whose mapped
-// cell on level l lies in [region - R0 - 1, region + R0] (both axes), 64 at a time:
-// every lane stages one query's 4 taps on level l (top-left cell packed, fractions,
-// attention weight; non-near taps get a sentinel cell) and its grad_out row (f32) in LDS,
-// then every lane walks the 64 x 4 staged taps and accumulates those whose 2x2 corner
-// block contains its cell.
+// grad_value by destination tile (encoder mode; see the header).  Block = (16x16 cell
+// tile of level l, head, image); the tile's 256 cells x 32 channels are accumulated in
+// LDS (32 KB f32).  For every query level lq the block enumerates the rectangle of
+// queries whose mapped cell on level l lies within R0 cells of a corner block touching
+// the tile (mapped_range), 16 queries per wave at a time: lane = (query, point) computes
+// the tap on level l, keeps it if near_tap() and one of its four corners is in the tile,
+// and the kept taps are compacted (wave ballot) into a per-wave list with the query's
+// grad_out row staged in LDS.  Then the two half-waves walk the list with lane = channel
+// and add weight * grad_out into the tile with LDS float atomics (32 consecutive floats
+// per half-wave: conflict-free).  Far taps are left to the scatter kernel.  Finally every
+// cell of the tile is stored once (plain f32 stores; the scatter adds on top).
+//
+// Work per tile grows with the number of queries mapping into its window, so coarse
+// levels (whose window holds the finer levels' queries) cost more per tile: the block
+// order is tile-major with the coarsest level first (longest jobs start first), and the
+// heads of one (tile, image) are consecutive workgroups of one XCD (their loc / grad_out
+// rows share cache lines).
+constexpr int kTile = 16;
+
+struct TileOrder {
+  int level[kMaxLevels];      // levels by ascending cell count (coarsest first)
+  int prefix[kMaxLevels + 1]; // tile-slot prefix over that order (slots = tiles x images)
+  int slots;                  // total (tile, image) slots
+};
+
 template <typename T>
-__global__ void __launch_bounds__(256) msda_bwd_pull_kernel(const float* __restrict__ loc,
+__global__ void __launch_bounds__(256) msda_bwd_tile_kernel(const float* __restrict__ loc,
                                                             const float* __restrict__ attw,
                                                             const T* __restrict__ gout, float* __restrict__ gvalue,
-                                                            Levels lv, int S, int Hh, int L, int R0, int tiles0,
-                                                            int tiles1, int tiles2) {
+                                                            Levels lv, int S, int Hh, int B, int L, int R0,
+                                                            TileOrder to) {
   constexpr int P = 4;
-  __shared__ int sCell[4][64][P];
-  __shared__ float4 sW[4][64][P / 2];               // (lh, lw) pairs per tap, 2 taps per float4
-  __shared__ float sA[4][64][P];
-  __shared__ __attribute__((aligned(16))) float sG[4][64][kD];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int h = blockIdx.y, b = blockIdx.z;
-  // tile -> (level, tile row, tile col)
-  int t = blockIdx.x, l = 0;
-  const int tl[3] = {tiles0, tiles1, tiles2};
-  while (l < L - 1 && l < 3 && t >= tl[l]) { t -= tl[l]; ++l; }
+  __shared__ __attribute__((aligned(16))) float sAcc[kTile * kTile * kD];
+  __shared__ int4 sCell[4][64];
+  __shared__ float4 sWgt[4][64];
+  __shared__ int sQ[4][64];
+  __shared__ __attribute__((aligned(16))) float sG[4][16][kD];
+  // physical id -> (slot, head): workgroup i runs on XCD i % 8; heads of one slot are
+  // consecutive workgroups of that XCD, slots advance in order (coarsest level first)
+  const int i = blockIdx.x;
+  const int xcd = i & 7, j = i >> 3;
+  const int h = j % Hh;
+  const int slot = (j / Hh) * 8 + xcd;
+  if (slot >= to.slots) return;                     // padding (uniform per block)
+  int oi = 0;
+  while (oi + 1 < L && slot >= to.prefix[oi + 1]) ++oi;
+  const int l = to.level[oi];
+  const int local = slot - to.prefix[oi];
+  const int b = local % B, t = local / B;
   const int Hl = lv.h[l], Wl = lv.w[l];
-  const int tx_n = (Wl + 15) / 16;
-  const int y0 = (t / tx_n) * 16 + wave * kPullRows, x0 = (t % tx_n) * 16;
-  const int cy = y0 + lane / kPullCols, cx = x0 + lane % kPullCols;
+  const int txn = (Wl + kTile - 1) / kTile;
+  const int ty0 = (t / txn) * kTile, tx0 = (t % txn) * kTile;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int LP = L * P;
-  float acc[kD];
-#pragma unroll
-  for (int c = 0; c < kD; ++c) acc[c] = 0.f;
-  int* cell = &sCell[wave][0][0];
-  float4* wts = &sW[wave][0][0];
-  float* aw = &sA[wave][0][0];
-  float* gg = &sG[wave][0][0];
-  for (int lq = 0; lq <= l; ++lq) {           // source levels not finer than l
+
+  for (int k = tid; k < kTile * kTile * kD / 4; k += 256)
+    reinterpret_cast<float4*>(sAcc)[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+
+  const int half = lane >> 5, c = lane & 31;
+  for (int lq = 0; lq < L; ++lq) {
     const int Hq = lv.h[lq], Wq = lv.w[lq];
-    // query rectangle: mapped cell within [y0 - R0 - 1, y0 + rows - 1 + R0] x [...]
-    const int lo_y = y0 - R0 - 1, hi_y = y0 + kPullRows - 1 + R0;
-    const int lo_x = x0 - R0 - 1, hi_x = x0 + kPullCols - 1 + R0;
+    // a near tap's top-left cell is within R0 of the query's mapped cell; its corner
+    // block touches the tile iff the top-left cell is in [tile0 - 1, tile0 + 15]
     int ya, yb, xa, xb;
-    mapped_range(lo_y, hi_y, Hq, Hl, &ya, &yb);
-    mapped_range(lo_x, hi_x, Wq, Wl, &xa, &xb);
+    mapped_range(ty0 - 1 - R0, ty0 + kTile - 1 + R0, Hq, Hl, &ya, &yb);
+    mapped_range(tx0 - 1 - R0, tx0 + kTile - 1 + R0, Wq, Wl, &xa, &xb);
     if (ya > yb || xa > xb) continue;
     const int nx = xb - xa + 1;
     const int ncand = (yb - ya + 1) * nx;
-    for (int base = 0; base < ncand; base += 64) {
-      const int i = base + lane;
-      if (i < ncand) {
-        const int yq = ya + i / nx, xq = xa + i % nx;
-        const long long grp = ((long long)b * S + lv.start[lq] + yq * Wq + xq) * Hh + h;
+    for (int base = wave * 16; base < ncand; base += 64) {
+      // ---- geometry: lane = (query base + lane/4, point lane%4)
+      const int qi = base + (lane >> 2), p = lane & 3;
+      int4 cell = make_int4(-1, -1, -1, -1);
+      float4 wgt = make_float4(0.f, 0.f, 0.f, 0.f);
+      bool keep = false;
+      long long grp = 0;
+      if (qi < ncand) {
+        const int yq = ya + qi / nx, xq = xa + qi % nx;
+        grp = ((long long)b * S + lv.start[lq] + yq * Wq + xq) * Hh + h;
         const int mcy = mapped_cell(yq, Hq, Hl), mcx = mapped_cell(xq, Wq, Wl);
-        const float4* lp4 = reinterpret_cast<const float4*>(loc + (grp * LP + l * P) * 2);
-        const float4 a4 = *reinterpret_cast<const float4*>(attw + grp * LP + l * P);
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-        for (int pp = 0; pp < P / 2; ++pp) {
-          const float4 xy = lp4[pp];
-          const Tap t0 = tap_geom(xy.x, xy.y, Hl, Wl);
-          const Tap t1 = tap_geom(xy.z, xy.w, Hl, Wl);
-          cell[lane * P + 2 * pp] = pull_tap(t0, lq, l, mcy, mcx, R0) ? ((t0.h0 << 16) | (t0.w0 & 0xffff)) : (int)0x80008000;
-          cell[lane * P + 2 * pp + 1] = pull_tap(t1, lq, l, mcy, mcx, R0) ? ((t1.h0 << 16) | (t1.w0 & 0xffff)) : (int)0x80008000;
-          wts[lane * 2 + pp] = make_float4(t0.lh, t0.lw, t1.lh, t1.lw);
+        const float2 xy = *reinterpret_cast<const float2*>(loc + (grp * LP + l * P + p) * 2);
+        const float a = attw[grp * LP + l * P + p];
+        const Tap tg = tap_geom(xy.x, xy.y, Hl, Wl);
+        if (near_tap(tg, mcy, mcx, R0)) {
+          const int ry0 = tg.h0 - ty0, rx0 = tg.w0 - tx0;
+          const bool y0in = (unsigned)ry0 < (unsigned)kTile && tg.h0 >= 0;
+          const bool y1in = (unsigned)(ry0 + 1) < (unsigned)kTile && tg.h0 + 1 < Hl;
+          const bool x0in = (unsigned)rx0 < (unsigned)kTile && tg.w0 >= 0;
+          const bool x1in = (unsigned)(rx0 + 1) < (unsigned)kTile && tg.w0 + 1 < Wl;
+          const int base_cell = (ry0 * kTile + rx0) * kD;
+          cell.x = y0in && x0in ? base_cell : -1;
+          cell.y = y0in && x1in ? base_cell + kD : -1;
+          cell.z = y1in && x0in ? base_cell + kTile * kD : -1;
+          cell.w = y1in && x1in ? base_cell + (kTile + 1) * kD : -1;
+          wgt = make_float4(tg.hh * tg.hw * a, tg.hh * tg.lw * a, tg.lh * tg.hw * a, tg.lh * tg.lw * a);
+          keep = cell.x >= 0 || cell.y >= 0 || cell.z >= 0 || cell.w >= 0;
         }
+      }
+      // ---- grad_out rows of the wave's 16 queries -> LDS (lane = query lane/4, 8 channels)
+      {
+        const int qg = lane >> 2, c8 = (lane & 3) * 8;
+        const int qn = base + qg;
+        float gv[8];
+        if (qn < ncand) {
+          const int yq = ya + qn / nx, xq = xa + qn % nx;
+          const long long g2 = ((long long)b * S + lv.start[lq] + yq * Wq + xq) * Hh + h;
+          Vec16<T>::load(gout + g2 * kD + c8, gv);
+          if constexpr (Vec16<T>::N == 4) Vec16<T>::load(gout + g2 * kD + c8 + 4, gv + 4);
+        } else {
 #pragma unroll
-        for (int pp = 0; pp < P; ++pp) aw[lane * P + pp] = av[pp];
-        float gv[kD];
-        constexpr int V = Vec16<T>::N;
-#pragma unroll
-        for (int c = 0; c < kD; c += V) Vec16<T>::load(gout + grp * kD + c, gv + c);
-#pragma unroll
-        for (int c = 0; c < kD; c += 4)
-          *reinterpret_cast<float4*>(gg + lane * kD + c) = make_float4(gv[c], gv[c + 1], gv[c + 2], gv[c + 3]);
+          for (int k = 0; k < 8; ++k) gv[k] = 0.f;
+        }
+        float4* dst = reinterpret_cast<float4*>(&sG[wave][qg][c8]);
+        dst[0] = make_float4(gv[0], gv[1], gv[2], gv[3]);
+        dst[1] = make_float4(gv[4], gv[5], gv[6], gv[7]);
+      }
+      // ---- compact the kept taps
+      const unsigned long long mask = __ballot(keep);
+      const int n = __popcll(mask);
+      if (keep) {
+        const int pos = __popcll(mask & ((1ull << lane) - 1ull));
+        sCell[wave][pos] = cell;
+        sWgt[wave][pos] = wgt;
+        sQ[wave][pos] = lane >> 2;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int cnt = min(64, ncand - base);
-      for (int j = 0; j < cnt; ++j) {
-#pragma unroll
-        for (int pp = 0; pp < P; ++pp) {
-          const int packed = cell[j * P + pp];
-          const int dy = cy - (packed >> 16), dx = cx - (short)(packed & 0xffff);
-          if ((unsigned)dy <= 1u && (unsigned)dx <= 1u) {
-            const float4 w4 = wts[j * 2 + (pp >> 1)];
-            const float lh = (pp & 1) ? w4.z : w4.x, lw = (pp & 1) ? w4.w : w4.y;
-            const float wgt = (dy ? lh : 1.f - lh) * (dx ? lw : 1.f - lw) * aw[j * P + pp];
-            const float4* g4 = reinterpret_cast<const float4*>(gg + j * kD);
-#pragma unroll
-            for (int c = 0; c < kD / 4; ++c) {
-              const float4 v = g4[c];
-              acc[4 * c + 0] = fmaf(wgt, v.x, acc[4 * c + 0]);
-              acc[4 * c + 1] = fmaf(wgt, v.y, acc[4 * c + 1]);
-              acc[4 * c + 2] = fmaf(wgt, v.z, acc[4 * c + 2]);
-              acc[4 * c + 3] = fmaf(wgt, v.w, acc[4 * c + 3]);
-            }
-          }
-        }
+      // ---- add: half-wave per list entry, lane = channel
+      for (int e = half; e < n; e += 2) {
+        const int4 ce = sCell[wave][e];
+        const float4 we = sWgt[wave][e];
+        const float g = sG[wave][sQ[wave][e]][c];
+        if (ce.x >= 0) atomicAdd(&sAcc[ce.x + c], we.x * g);
+        if (ce.y >= 0) atomicAdd(&sAcc[ce.y + c], we.y * g);
+        if (ce.z >= 0) atomicAdd(&sAcc[ce.z + c], we.z * g);
+        if (ce.w >= 0) atomicAdd(&sAcc[ce.w + c], we.w * g);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
-  if (cy < Hl && cx < Wl) {
-    float4* dst = reinterpret_cast<float4*>(gvalue + (((size_t)b * S + lv.start[l] + cy * Wl + cx) * Hh + h) * kD);
-#pragma unroll
-    for (int c = 0; c < kD / 4; ++c) dst[c] = make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
+  __syncthreads();
+  // ---- store the tile: 8 consecutive lanes per cell (128 B), every cell once
+  const size_t rowstride = (size_t)Hh * kD;
+  float* gl = gvalue + (((size_t)b * S + lv.start[l]) * Hh + h) * kD;
+  for (int k = tid; k < kTile * kTile * 8; k += 256) {
+    const int cl = k >> 3, part = k & 7;
+    const int cy = ty0 + cl / kTile, cx = tx0 + cl % kTile;
+    if (cy < Hl && cx < Wl)
+      *reinterpret_cast<float4*>(gl + (size_t)(cy * Wl + cx) * rowstride + part * 4) =
+          reinterpret_cast<const float4*>(sAcc)[k];
   }
 }
 
@@ -854,27 +897,43 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   hipStream_t st = (hipStream_t)stream;
   const long long groups = (long long)B * Q * Hh;
   if (encoder) {
-    // pull (plain stores of every grad_value element: the taps of coarser-or-equal query
-    // levels landing within R0 cells), then the carry scatter adds every other tap, and
-    // the geom kernel computes grad_loc / grad_attn
-    int R0 = kPullR;
-    if (const char* e = getenv("VS_MSDA_PULL_R")) R0 = atoi(e);
-    VS_CHECK(R0 >= 0 && R0 <= 64, "VS_MSDA_PULL_R out of range");
-    int tiles[4] = {0, 0, 0, 0}, ntiles = 0;
-    for (int l = 0; l < L; ++l) {
-      tiles[l] = ((lv.h[l] + 15) / 16) * ((lv.w[l] + 15) / 16);
-      ntiles += tiles[l];
+    // tile kernel (plain stores of every grad_value element: all near taps, LDS
+    // accumulation), then the carry scatter adds the far taps, and the geom kernel
+    // computes grad_loc / grad_attn
+    int R0 = kNearR;
+    if (const char* e = getenv("VS_MSDA_NEAR_R")) R0 = atoi(e);
+    VS_CHECK(R0 >= 0 && R0 <= 64, "VS_MSDA_NEAR_R out of range");
+    TileOrder to;
+    int ord[kMaxLevels];
+    for (int l = 0; l < L; ++l) ord[l] = l;
+    for (int a = 0; a < L; ++a)                 // ascending cell count (stable)
+      for (int c2 = a + 1; c2 < L; ++c2)
+        if ((long long)lv.h[ord[c2]] * lv.w[ord[c2]] < (long long)lv.h[ord[a]] * lv.w[ord[a]]) {
+          const int tmp = ord[a];
+          ord[a] = ord[c2];
+          ord[c2] = tmp;
+        }
+    to.prefix[0] = 0;
+    for (int k = 0; k < kMaxLevels; ++k) to.level[k] = k < L ? ord[k] : 0;
+    for (int k = 0; k < L; ++k) {
+      const int l = ord[k];
+      const int tiles = ((lv.h[l] + kTile - 1) / kTile) * ((lv.w[l] + kTile - 1) / kTile);
+      to.prefix[k + 1] = to.prefix[k] + tiles * B;
     }
-    // VS_MSDA_SKIP (profiling only): bit 0 skips the pull, bit 1 the scatter, bit 2 geom
+    for (int k = L; k < kMaxLevels; ++k) to.prefix[k + 1] = to.prefix[L];
+    to.slots = to.prefix[L];
+    const long long nblk = (long long)((to.slots + 7) / 8) * 8 * Hh;
+    VS_CHECK(nblk < (1LL << 31), "too many tiles");
+    // VS_MSDA_SKIP (profiling only): bit 0 skips the tile kernel, bit 1 the scatter, bit 2 geom
     int skip = 0;
     if (const char* e = getenv("VS_MSDA_SKIP")) skip = atoi(e);
     if (!(skip & 1)) {
       if (dtype == VS_BF16)
-        hipLaunchKernelGGL(msda_bwd_pull_kernel<bf16>, dim3(ntiles, Hh, B), dim3(256), 0, st, loc, attw,
-                           (const bf16*)gout, gvalue, lv, S, Hh, L, R0, tiles[0], tiles[1], tiles[2]);
+        hipLaunchKernelGGL(msda_bwd_tile_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0, st, loc, attw,
+                           (const bf16*)gout, gvalue, lv, S, Hh, B, L, R0, to);
       else
-        hipLaunchKernelGGL(msda_bwd_pull_kernel<float>, dim3(ntiles, Hh, B), dim3(256), 0, st, loc, attw,
-                           (const float*)gout, gvalue, lv, S, Hh, L, R0, tiles[0], tiles[1], tiles[2]);
+        hipLaunchKernelGGL(msda_bwd_tile_kernel<float>, dim3((unsigned)nblk), dim3(256), 0, st, loc, attw,
+                           (const float*)gout, gvalue, lv, S, Hh, B, L, R0, to);
     }
     if (!(skip & 2)) launch_scatter<true>(dtype, loc, attw, gout, gvalue, lv, B, S, Hh, Q, L, kScatterRun, R0, st);
     if (!(skip & 4)) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
