@@ -227,6 +227,12 @@ VS_API int vs_segment_clip(float* data, const int* table, int num_chunks, float 
 VS_API int vs_lsa_max_targets(int num_queries);
 VS_API int vs_lsa_batch(const float* cost, const int* targets_per_image, int num_steps, int batch,
                         int num_queries, int max_targets, int* assign, void* stream);
+/* Same, with the per-image target counts in DEVICE memory (int32 [batch], clamped to
+ * [0, max_targets]): the launch does not depend on the counts, so a captured HIP graph
+ * serves every batch whose largest count is <= max_targets (padded targets, see
+ * visionseg/criterion.py PaddedTargets). */
+VS_API int vs_lsa_batch_device_counts(const float* cost, const int* targets_per_image_dev, int num_steps,
+                                      int batch, int num_queries, int max_targets, int* assign, void* stream);
 
 /* ---- GroupNorm over channels-last activations (csrc/groupnorm.hip) -------------------
  * The pixel decoder's Conv2d + GroupNorm(32) blocks (upstream MSDeformAttnPixelDecoder

@@ -44,7 +44,7 @@ def _worker(rank, world, port, data, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     from visionseg.train import Trainer, SolverConfig, init_distributed
-    from visionseg.criterion import SetCriterion
+    from visionseg.criterion import SetCriterion, PaddedTargets
     from visionseg.model import M2FConfig
     init_distributed("gloo")
     x = data[rank:rank + 1]
@@ -54,7 +54,9 @@ def _worker(rank, world, port, data, out_q):
     flat = torch.cat([p.detach().flatten() for p in tr.model.parameters()])
     # criterion num_masks is the global mean over ranks (upstream SetCriterion semantics)
     crit = SetCriterion(M2FConfig(num_queries=5))
-    n = crit._num_masks([torch.zeros(rank + 1)], torch.device("cpu"))
+    tg = PaddedTargets.from_lists([torch.zeros(rank + 1, 4, 4, dtype=torch.bool)],
+                                  [torch.zeros(rank + 1, dtype=torch.int64)], device="cpu")
+    n = crit._num_masks(tg, torch.device("cpu"))
     out_q.put((rank, flat.numpy().copy(), float(n)))   # by value: no shared-memory tensor handles
     dist.barrier()
     dist.destroy_process_group()

@@ -83,6 +83,31 @@ def test_graph_new_signature_recaptures():
     assert len(tb._graph_states) == 2
 
 
+def test_graph_same_capacity_replays():
+    """Batches whose per-image target counts differ but whose largest count is the same
+    replay ONE graph (targets padded into its static buffers) and track the eager step."""
+    from visionseg.data import synthetic_batch
+    from visionseg.train import Trainer
+    cfg, model, crit, b1, _ = _setup()
+    kc = max(int(c.shape[0]) for c in b1[2])
+    b4 = None
+    for seed in range(20, 60):
+        cand = synthetic_batch(2, 256, seed=seed, device=DEV)
+        ks = [int(c.shape[0]) for c in cand[2]]
+        if max(ks) == kc and ks != [int(c.shape[0]) for c in b1[2]]:
+            b4 = cand
+            break
+    if b4 is None:
+        pytest.skip("no batch with the same capacity and other counts")
+    ta = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV)
+    tb = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV, graphs=True, graph_warmup=1)
+    batches = [b1, b1, b4, b1, b4]
+    la = _run(ta, batches)
+    lb = _run(tb, batches)
+    assert len(tb._graph_states) == 1
+    _compare(ta, tb, la, lb)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -35,6 +35,26 @@ def test_lsa_matches_scipy(Q, ks):
             np.testing.assert_array_equal(got[s, b, :k], exp)
 
 
+@pytest.mark.parametrize("Q,ks,kc", [(100, [7, 0, 1, 50], 50), (100, [3, 2], 8), (20, [20, 0, 5], 20)])
+def test_lsa_device_counts_matches_scipy(Q, ks, kc):
+    """Counts read from device memory (graph-replayable launch): same assignments as scipy
+    on each image's first count columns, -1 past them, whatever the padded capacity."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(Q + kc)
+    S, B = 2, len(ks)
+    cost = torch.randn(S, B, Q, kc, generator=g) * 3
+    got = ops.linear_sum_assignment_padded(cost.to(DEV), torch.tensor(ks, dtype=torch.int32, device=DEV)).cpu().numpy()
+    assert got.shape == (S, B, kc)
+    for s in range(S):
+        for b, k in enumerate(ks):
+            assert (got[s, b, k:] == -1).all()
+            if k:
+                r, cidx = linear_sum_assignment(cost[s, b, :, :k].double().numpy())
+                exp = np.full(k, -1)
+                exp[cidx] = r
+                np.testing.assert_array_equal(got[s, b, :k], exp)
+
+
 def test_lsa_ties_reach_the_optimum():
     """Duplicate target columns make the optimum non-unique: the total cost must still be
     scipy's minimum and the assignment a valid matching."""

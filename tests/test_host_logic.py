@@ -97,3 +97,57 @@ def test_instance_inference():
     best = int(torch.argmax(s))
     assert m[best].sum() > 0 and (lab == 0).all()
     assert float(s.max()) > 0.9
+
+
+def _pair_independent_rand(monkeypatch):
+    """torch.rand whose point draws depend only on the point index, not on the number of
+    (step, image, target) pairs: a loss over padded pairs is then comparable bit for bit
+    with a loss over fewer pairs."""
+    base = torch.rand(200000, 2, generator=torch.Generator().manual_seed(9))
+
+    def fake_rand(*shape, device=None, generator=None, **kw):
+        if len(shape) == 1 and isinstance(shape[0], (tuple, list)):
+            shape = tuple(shape[0])
+        n = shape[-2]
+        return base[:n].expand(*shape[:-2], n, 2).clone().to(device if device is not None else "cpu")
+    monkeypatch.setattr(torch, "rand", fake_rand)
+
+
+@pytest.mark.parametrize("ks", [[2, 0, 3], [1, 1], [0, 0], [3, 1, 2, 0]])
+def test_criterion_padding_invariance(monkeypatch, ks):
+    """Padded targets (criterion.PaddedTargets, what a graph-replayed step feeds the
+    criterion) give the same matching, loss and gradients whatever the padded capacity,
+    and the same as the reference's per-image lists (HF:m2f:378-794 semantics)."""
+    from visionseg.criterion import SetCriterion, PaddedTargets
+    cfg = M2FConfig.preset("swin_t", num_queries=12, train_num_points=256)
+    g = torch.Generator().manual_seed(sum(ks) + len(ks))
+    S, B, Q, H = 3, len(ks), 12, 32
+    masks = [torch.randn(B, Q, H, H, generator=g, requires_grad=True) for _ in range(S)]
+    classes = [torch.randn(B, Q, 2, generator=g, requires_grad=True) for _ in range(S)]
+    ml = [torch.rand(k, 96, 96, generator=g) > 0.7 for k in ks]
+    cl = [torch.zeros(k, dtype=torch.int64) for k in ks]
+    _pair_independent_rand(monkeypatch)
+    res = []
+    for tg in ((ml, cl), (PaddedTargets.from_lists(ml, cl), None), (PaddedTargets.from_lists(ml, cl, kc=5), None)):
+        crit = SetCriterion(cfg, matcher="host")
+        assign = crit.match([m.detach() for m in masks], torch.stack(classes).detach(), *tg)
+        loss, parts = crit(masks, classes, *tg)
+        grads = torch.autograd.grad(loss, masks + classes)
+        res.append((assign, loss.detach(), grads))
+    kmax = max(ks)
+    for i, (assign, loss, grads) in enumerate(res[1:]):
+        assert torch.equal(assign[..., :kmax], res[0][0][..., :kmax])
+        assert (assign[..., kmax:] == -1).all()
+        if i == 0:      # same capacity: bit-identical
+            assert torch.equal(loss, res[0][1])
+            assert all(torch.equal(a, b) for a, b in zip(grads, res[0][2]))
+        else:           # extra zero pairs change only the summation tree
+            assert abs(float(loss) - float(res[0][1])) <= 1e-6 * abs(float(res[0][1]))
+            for a, b in zip(grads, res[0][2]):
+                assert float((a - b).abs().max()) <= 1e-6 * max(1e-6, float(b.abs().max()))
+    # every valid target matched to a distinct query
+    a = res[0][0]
+    for s in range(S):
+        for b, k in enumerate(ks):
+            q = a[s, b, :k].tolist()
+            assert len(set(q)) == k and all(0 <= x < Q for x in q)

@@ -35,12 +35,14 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// cost [S*B][Q][Kmax] f32 -> assign [S*B][Kmax] int32 (query of target k, -1 padding)
+// cost [S*B][Q][Kmax] f32 -> assign [S*B][Kmax] int32 (query of target k, -1 padding).
+// Per-image target counts by value (cc) or, when dcounts is set, read from device memory
+// (clamped to [0, Kmax]): a graph-replayed step then serves any counts up to Kmax.
 __global__ void __launch_bounds__(64) lsa_kernel(const float* __restrict__ cost, int* __restrict__ assign, int B,
-                                                 int Q, int Kmax, ColCounts cc) {
+                                                 int Q, int Kmax, ColCounts cc, const int* __restrict__ dcounts) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int prob = blockIdx.x;
-  const int K = cc.k[prob % B];
+  const int K = dcounts ? min(max(dcounts[prob % B], 0), min(Kmax, Q)) : cc.k[prob % B];
   const int lane = threadIdx.x;
   int* out = assign + (size_t)prob * Kmax;
   for (int k = lane; k < Kmax; k += 64) out[k] = -1;
@@ -168,7 +170,23 @@ extern "C" int vs_lsa_batch(const float* cost, const int* targets_per_image, int
   if (num_steps == 0) return VS_OK;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(lsa_kernel, dim3(num_steps * batch), dim3(64), lds, st, cost, assign, batch, num_queries,
-                     max_targets, cc);
+                     max_targets, cc, (const int*)nullptr);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_lsa_batch_device_counts(const float* cost, const int* targets_per_image_dev, int num_steps,
+                                          int batch, int num_queries, int max_targets, int* assign, void* stream) {
+  VS_CHECK(num_steps >= 0 && batch > 0, "batch must be positive");
+  VS_CHECK(num_queries > 0 && num_queries <= kMaxQ, "1 <= queries <= 1024");
+  VS_CHECK(max_targets > 0 && max_targets <= num_queries, "1 <= max_targets <= queries");
+  VS_CHECK(cost && targets_per_image_dev && assign, "null pointer");
+  const size_t lds = lsa_lds_bytes(max_targets, num_queries);
+  VS_CHECK(lds <= 64 * 1024, "cost matrix too large for the device matcher (see vs_lsa_max_targets)");
+  if (num_steps == 0) return VS_OK;
+  ColCounts cc = {};
+  hipLaunchKernelGGL(lsa_kernel, dim3(num_steps * batch), dim3(64), lds, (hipStream_t)stream, cost, assign, batch,
+                     num_queries, max_targets, cc, targets_per_image_dev);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

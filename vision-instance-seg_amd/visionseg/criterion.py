@@ -12,7 +12,12 @@ restructured for the device:
   `linear_sum_assignment(cost.cpu())` is 10 x B host syncs per step, here there is none,
   so the host keeps enqueueing the loss and the backward while the GPU runs the forward;
 * the mask/dice/CE losses of all decoder steps are evaluated as one batch over the
-  matched (query, target) pairs, ordered by target.
+  matched (query, target) pairs;
+* targets are carried PADDED (`PaddedTargets`: masks [B, Kc, H, W], classes [B, Kc],
+  per-image counts [B] on the device, Kc = the batch's largest count): no shape or launch
+  depends on the individual counts, so a captured HIP graph of the training step
+  (train.Trainer(graphs=True)) serves every batch with the same Kc, and the padded
+  columns / pairs are masked out of the matching and the losses.
 
 `matcher="host"` keeps scipy's `linear_sum_assignment` (the reference's choice); both
 return the same optimum (unique for generic costs).  The random points come from the
@@ -34,6 +39,61 @@ def _sample(feat, coords):
     return F.grid_sample(feat, 2.0 * coords.unsqueeze(2) - 1.0, align_corners=False).squeeze(3).squeeze(1)
 
 
+class PaddedTargets:
+    """Per-image instance targets padded to the batch's largest count Kc.
+
+    masks [B, Kc, H, W] (bool/uint8, zero past the count), classes int64 [B, Kc] (0 past
+    the count), counts int32 [B] on the device.  `kc` is a host int (a shape); the counts
+    themselves never reach the host."""
+
+    def __init__(self, masks, classes, counts):
+        self.masks, self.classes, self.counts = masks, classes, counts
+        self.kc = int(classes.shape[1])
+
+    @classmethod
+    def from_lists(cls, mask_labels, class_labels, kc=None, device=None):
+        """The reference's per-image lists ([K_i, H, W] masks, [K_i] classes) -> padded."""
+        B = len(class_labels)
+        ks = [int(t.shape[0]) for t in class_labels]
+        kc = max(ks + [0]) if kc is None else int(kc)
+        if any(k > kc for k in ks):
+            raise ValueError(f"an image has {max(ks)} targets, more than the padded capacity {kc}")
+        dev = device if device is not None else (mask_labels[0].device if B else "cpu")
+        H, W = (int(mask_labels[0].shape[-2]), int(mask_labels[0].shape[-1])) if B else (0, 0)
+        masks = torch.zeros(B, kc, H, W, dtype=torch.bool, device=dev)
+        classes = torch.zeros(B, kc, dtype=torch.int64, device=dev)
+        for i, (m, c) in enumerate(zip(mask_labels, class_labels)):
+            if ks[i]:
+                masks[i, :ks[i]] = m.to(dev)
+                classes[i, :ks[i]] = c.to(dev)
+        counts = torch.tensor(ks, dtype=torch.int32).to(dev)
+        return cls(masks, classes, counts)
+
+    def copy_from_lists(self, mask_labels, class_labels):
+        """Refill in place (static buffers of a captured graph): eager copies, no reallocation."""
+        ks = [int(t.shape[0]) for t in class_labels]
+        if len(ks) != self.masks.shape[0] or max(ks + [0]) > self.kc:
+            raise ValueError("targets do not fit the padded buffers")
+        with torch.no_grad():
+            self.masks.zero_()
+            self.classes.zero_()
+            for i, (m, c) in enumerate(zip(mask_labels, class_labels)):
+                if ks[i]:
+                    self.masks[i, :ks[i]].copy_(m)
+                    self.classes[i, :ks[i]].copy_(c)
+            self.counts.copy_(torch.tensor(ks, dtype=torch.int32), non_blocking=False)
+
+    def valid(self):
+        """bool [B, Kc]: target k of image b exists."""
+        return torch.arange(self.kc, device=self.counts.device)[None, :] < self.counts[:, None]
+
+
+def as_padded(mask_labels, class_labels, device):
+    if isinstance(mask_labels, PaddedTargets):
+        return mask_labels
+    return PaddedTargets.from_lists(mask_labels, class_labels, device=device)
+
+
 class SetCriterion:
     def __init__(self, cfg, matcher: str = "device"):
         """matcher: "device" (csrc/match.hip, no host sync) or "host" (scipy, the
@@ -43,54 +103,54 @@ class SetCriterion:
         self.cfg = cfg
         self.num_labels = cfg.num_labels
         self.matcher = matcher
-        self._pairs = {}
         self._ew = {}
 
     # --------------------------------------------------------------- matching
     @torch.no_grad()
-    def match(self, masks_list, classes, mask_labels, class_labels):
-        """masks_list: S x [B,Q,H,W] (S decoder steps), classes [S,B,Q,K+1] -> int32
-        [S, B, Kmax] on the device: the query matched to each target (-1 padding)."""
+    def match(self, masks_list, classes, mask_labels, class_labels=None):
+        """masks_list: S x [B,Q,H,W] (S decoder steps), classes [S,B,Q,K+1], targets as
+        lists or PaddedTargets -> int32 [S, B, Kc] on the device: the query matched to
+        each target (-1 past the image's count).  Costs as HF:m2f:434-481 (HungarianMatcher:
+        class -prob, sigmoid-BCE and dice on `train_num_points` uniform points)."""
         c = self.cfg
         S = len(masks_list)
         B, Q = masks_list[0].shape[:2]
         dev = masks_list[0].device
-        kmax = max(1, max(int(t.shape[0]) for t in class_labels))
-        cost = torch.zeros(S, B, Q, kmax, device=dev)
-        probs = classes.float().softmax(-1)
-        # one uniform point set per image, shared by its queries and the S decoder steps:
-        # the queries are grid_sample CHANNELS, so one call per step samples all B x Q masks
+        tg = as_padded(mask_labels, class_labels, dev)
+        Kc = max(1, tg.kc)
+        if tg.kc > Q:
+            raise ValueError(f"an image has more targets ({tg.kc}) than queries ({Q})")
+        probs = classes.float().softmax(-1)                                              # [S,B,Q,C+1]
+        # one uniform point set per image, shared by its queries, targets and the S steps:
+        # queries / targets are grid_sample CHANNELS (one call per step, one for all targets)
         P = c.train_num_points
         grid = (2.0 * torch.rand(B, P, 2, device=dev) - 1.0).unsqueeze(2)              # [B,P,1,2]
-        pp_all = torch.stack([F.grid_sample(m.float(), grid, align_corners=False).squeeze(3)
-                              for m in masks_list])                                      # [S,B,Q,P]
-        for i in range(B):
-            K = int(class_labels[i].shape[0])
-            if K == 0:
-                continue
-            tp = F.grid_sample(mask_labels[i].float()[None], grid[i:i + 1], align_corners=False)
-            tp = tp.squeeze(3)[0][None].expand(S, -1, -1)                                  # [S,K,P]
-            pp = pp_all[:, i]                                                            # [S,Q,P]
-            P = pp.shape[-1]
-            pos = F.softplus(-pp)          # BCE(x, 1)
-            neg = F.softplus(pp)           # BCE(x, 0)
-            cm = torch.bmm(pos / P, tp.transpose(1, 2)) + torch.bmm(neg / P, (1 - tp).transpose(1, 2))
-            sg = pp.sigmoid()
-            num = 2 * torch.bmm(sg, tp.transpose(1, 2))
-            den = sg.sum(-1)[:, :, None] + tp.sum(-1)[:, None, :]
-            cd = 1 - (num + 1) / (den + 1)
-            cc = -probs[:, i][:, :, class_labels[i]]
-            cost[:, i, :, :K] = c.mask_weight * cm + c.class_weight * cc + c.dice_weight * cd
+        pp = torch.stack([F.grid_sample(m.float(), grid, align_corners=False).squeeze(3)
+                          for m in masks_list])                                          # [S,B,Q,P]
+        if tg.kc:
+            tp = F.grid_sample(tg.masks.float(), grid, align_corners=False).squeeze(3)  # [B,Kc,P]
+        else:
+            tp = torch.zeros(B, 1, P, device=dev)
+        tpt = tp.transpose(1, 2)[None]                                                   # [1,B,P,Kc]
+        Pn = pp.shape[-1]
+        pos = F.softplus(-pp)          # BCE(x, 1)
+        neg = F.softplus(pp)           # BCE(x, 0)
+        cm = torch.matmul(pos / Pn, tpt) + torch.matmul(neg / Pn, 1 - tpt)              # [S,B,Q,Kc]
+        sg = pp.sigmoid()
+        num = 2 * torch.matmul(sg, tpt)
+        den = sg.sum(-1)[..., None] + tp.sum(-1)[None, :, None, :]
+        cd = 1 - (num + 1) / (den + 1)
+        cls = (tg.classes if tg.kc else torch.zeros(B, 1, dtype=torch.int64, device=dev))
+        cc = -torch.gather(probs, 3, cls[None, :, None, :].expand(S, B, Q, Kc))
+        cost = c.mask_weight * cm + c.class_weight * cc + c.dice_weight * cd
         cost = torch.nan_to_num(cost.clamp(-1e10, 1e10), 0.0)
-        ks = [int(t.shape[0]) for t in class_labels]
-        if any(k > Q for k in ks):
-            raise ValueError(f"an image has more targets ({max(ks)}) than queries ({Q})")
-        if self.matcher == "device" and cost.is_cuda and max(ks) <= ops.lsa_max_targets(Q):
-            return ops.linear_sum_assignment_batch(cost, ks)           # csrc/match.hip, no host sync
+        if self.matcher == "device" and cost.is_cuda and Kc <= ops.lsa_max_targets(Q):
+            return ops.linear_sum_assignment_padded(cost, tg.counts)                    # csrc/match.hip, no sync
         # scipy on the host (the reference's matcher): one device->host sync
         host = cost.cpu().numpy()
+        ks = tg.counts.cpu().tolist()
         from scipy.optimize import linear_sum_assignment
-        out = np.full((S, B, kmax), -1, dtype=np.int32)
+        out = np.full((S, B, Kc), -1, dtype=np.int32)
         for s in range(S):
             for i in range(B):
                 if ks[i]:
@@ -99,79 +159,83 @@ class SetCriterion:
         return torch.from_numpy(out).to(dev)
 
     # --------------------------------------------------------------- losses
-    def _num_masks(self, class_labels, device):
+    def _num_masks(self, tg, device):
         tot = getattr(self, "num_masks_total", None)
         if tot is not None:       # global count supplied by the trainer (graph-replayed steps)
             ws = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
             return torch.clamp(tot / ws, min=1)
-        n = torch.full((), float(sum(int(t.shape[0]) for t in class_labels)), device=device)   # fill, no copy
+        n = tg.counts.sum().float()                                   # on the device, no sync
         ws = 1
         if dist.is_available() and dist.is_initialized():
             dist.all_reduce(n)
             ws = dist.get_world_size()
         return torch.clamp(n / ws, min=1)
 
-    def __call__(self, masks_list, classes_list, mask_labels, class_labels):
-        """masks_list: per decoder step [B,Q,H,W] logits; classes_list: per step [B,Q,K+1].
-        Returns (total loss, dict of weighted components; keys as HF: final step
-        un-suffixed, aux steps `_{i}`)."""
+    def __call__(self, masks_list, classes_list, mask_labels, class_labels=None):
+        """masks_list: per decoder step [B,Q,H,W] logits; classes_list: per step [B,Q,K+1];
+        targets as the reference's per-image lists or a PaddedTargets.  Returns (total
+        loss, dict of weighted components; keys as HF: final step un-suffixed, aux steps
+        `_{i}`)."""
         c = self.cfg
         classes = torch.stack(classes_list)      # [S,B,Q,K+1]
         S, B, Q = classes.shape[:3]
         dev = classes.device
-        assign = self.match([m.detach() for m in masks_list], classes.detach(), mask_labels, class_labels)
-        nm = self._num_masks(class_labels, dev)
-        # matched pairs of every step, ordered by target t (image-major): image bs[t], the
-        # target's index k within its image, its query qs[s, t]; all on the device
-        ks = tuple(int(t.shape[0]) for t in class_labels)
-        N = sum(ks)
-        if (ks, dev) not in self._pairs:
-            img = [torch.full((k,), i, device=dev, dtype=torch.int64) for i, k in enumerate(ks) if k]
-            kin = [torch.arange(k, device=dev) for k in ks if k]
-            self._pairs[(ks, dev)] = (torch.cat(img), torch.cat(kin)) if N else (None, None)
-        bt, kt = self._pairs[(ks, dev)]
-        tgt_all = torch.cat([m.float() for m in mask_labels], 0) if N else None
-        tc = torch.full((S, B, Q), self.num_labels, dtype=torch.int64, device=dev)
-        if N:
-            qs = assign[:, bt, kt].long()                                                  # [S, N]
-            bs = bt.expand(S, N)
-            cls_all = torch.cat([t.to(dev) for t in class_labels]).long()
-            tc[torch.arange(S, device=dev)[:, None], bs, qs] = cls_all.expand(S, N)
+        tg = as_padded(mask_labels, class_labels, dev)
+        Kc = tg.kc
+        assign = self.match([m.detach() for m in masks_list], classes.detach(), tg)
+        nm = self._num_masks(tg, dev)
         ew = self._ew.get(dev)
         if ew is None:        # made once: a scalar store is a host->device copy (not capturable)
             ew = torch.ones(self.num_labels + 1, device=dev)
             ew[-1] = c.no_object_weight
             self._ew[dev] = ew
+        # target class per query (no-object where unmatched): matched pairs scatter their
+        # class; padded pairs go to a spare column Q that is dropped
+        tc = torch.full((S, B, Q + 1), self.num_labels, dtype=torch.int64, device=dev)
+        if Kc:
+            valid = tg.valid()                                                           # [B,Kc]
+            qs = assign[..., :Kc].long()                                                 # [S,B,Kc]
+            qidx = torch.where(valid[None] & (qs >= 0), qs, torch.full_like(qs, Q))
+            tc.scatter_(2, qidx, tg.classes[None].expand(S, B, Kc))
+        tc = tc[..., :Q].contiguous()
         ce = F.cross_entropy(classes.float().reshape(S * B, Q, -1).transpose(1, 2), tc.view(S * B, Q),
                              weight=ew, reduction="none")                                  # [S*B, Q]
         # weighted mean per step, as nn.CrossEntropyLoss(weight) does
         wsum = ew[tc.view(S * B, Q)].view(S, B * Q).sum(-1)
         loss_ce = ce.view(S, B * Q).sum(-1) / wsum                                         # [S]
-        if N:
-            pred = torch.stack([masks_list[k][bs[k], qs[k]] for k in range(S)])           # [S,N,H,W]
+        if Kc:
+            # every (step, image, target slot) pair; padded slots point at query 0 and are
+            # masked out of the sums
+            qsel = qidx.clamp(max=Q - 1)                                                 # [S,B,Kc]
+            bidx = torch.arange(B, device=dev)[:, None].expand(B, Kc)
+            pred = torch.stack([masks_list[k][bidx, qsel[k]] for k in range(S)])          # [S,B,Kc,H,W]
             H, W = pred.shape[-2:]
-            pred = pred.reshape(S * N, 1, H, W)
+            NP = B * Kc
+            pred = pred.reshape(S * NP, 1, H, W)
             with torch.no_grad():
                 npts = c.train_num_points
                 ns = int(npts * c.oversample_ratio)
                 nu = int(c.importance_sample_ratio * npts)
-                coords = torch.rand(S * N, ns, 2, device=dev)
+                coords = torch.rand(S * NP, ns, 2, device=dev)
                 unc = -torch.abs(_sample(pred.detach().float(), coords))
                 top = torch.topk(unc, k=nu, dim=1)[1]
                 coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
                 if npts - nu > 0:
-                    coords = torch.cat([coords, torch.rand(S * N, npts - nu, 2, device=dev)], 1)
+                    coords = torch.cat([coords, torch.rand(S * NP, npts - nu, 2, device=dev)], 1)
                 # sample each full-resolution target once, with the coordinates of the S
-                # predictions it is matched to (pairs are target-ordered in every step)
-                by_t = coords.view(S, N, npts, 2).transpose(0, 1)                          # [N,S,P,2]
-                lab_t = _sample(tgt_all[:, None], by_t.reshape(N, S * npts, 2)).view(N, S, npts)
-                plab = lab_t.transpose(0, 1).reshape(S * N, npts)
+                # predictions it is matched to
+                by_t = coords.view(S, NP, npts, 2).transpose(0, 1)                         # [NP,S,P,2]
+                tgt = tg.masks.reshape(NP, 1, *tg.masks.shape[-2:]).float()
+                lab_t = _sample(tgt, by_t.reshape(NP, S * npts, 2)).view(NP, S, npts)
+                plab = lab_t.transpose(0, 1).reshape(S * NP, npts)
             plog = _sample(pred.float(), coords)
-            bce = F.binary_cross_entropy_with_logits(plog, plab, reduction="none").mean(1)  # [S*N]
-            loss_mask = bce.view(S, N).sum(-1) / nm
+            keep = valid.reshape(1, NP).expand(S, NP).reshape(S * NP)
+            bce = F.binary_cross_entropy_with_logits(plog, plab, reduction="none").mean(1)  # [S*NP]
+            zero = torch.zeros((), device=dev)
+            loss_mask = torch.where(keep, bce, zero).view(S, NP).sum(-1) / nm
             pr = plog.sigmoid()
             dice = 1 - (2 * (pr * plab).sum(-1) + 1) / (pr.sum(-1) + plab.sum(-1) + 1)
-            loss_dice = dice.view(S, N).sum(-1) / nm
+            loss_dice = torch.where(keep, dice, zero).view(S, NP).sum(-1) / nm
         else:
             loss_mask = sum(m.sum() for m in masks_list) * 0.0 + torch.zeros(S, device=dev)
             loss_dice = torch.zeros(S, device=dev)

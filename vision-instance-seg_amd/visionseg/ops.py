@@ -493,6 +493,23 @@ def linear_sum_assignment_batch(cost, targets_per_image):
     return out
 
 
+def linear_sum_assignment_padded(cost, counts):
+    """cost [S, B, Q, K] f32 (device) + per-image target counts int32 [B] ON THE DEVICE ->
+    int32 [S, B, K] (-1 past each count).  The launch does not depend on the counts, so a
+    captured graph serves any counts <= K (csrc/match.hip vs_lsa_batch_device_counts)."""
+    L.require_hip(cost, counts)
+    c = cost.float().contiguous()
+    S, B, Q, K = c.shape
+    cnt = counts.to(torch.int32).contiguous()
+    if cnt.numel() != B:
+        raise ValueError(f"counts has {cnt.numel()} entries for a batch of {B}")
+    out = torch.empty(S, B, K, device=c.device, dtype=torch.int32)
+    with timed("lsa", c, bytes_=c.numel() * 4):
+        L.check(L.lib().vs_lsa_batch_device_counts(L.ptr(c), L.ptr(cnt), S, B, Q, K, L.ptr(out), L.stream(c)),
+                "lsa_batch_device_counts")
+    return out
+
+
 # ------------------------------------------------------------------ GroupNorm (channels-last)
 class GroupNormNHWCFunction(torch.autograd.Function):
     """group_norm (+ optional ReLU) of an NCHW tensor stored channels-last, groups of 8

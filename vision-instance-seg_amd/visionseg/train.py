@@ -218,14 +218,17 @@ class Trainer:
         self._phase2()
         return loss
 
-    def _capture(self, images, mask_labels, class_labels):
-        st = {"images": images.clone(), "ml": [m.clone() for m in mask_labels],
-              "cl": [c.clone() for c in class_labels], "graphs": []}
+    def _capture(self, images, mask_labels, class_labels, kc):
+        # static inputs: the image batch and the targets padded to kc (criterion.PaddedTargets),
+        # so every batch with the same image shape and largest target count replays this graph
+        from .criterion import PaddedTargets
+        st = {"images": images.clone(), "tg": PaddedTargets.from_lists(mask_labels, class_labels, kc=kc,
+                                                                       device=self.device), "graphs": []}
         torch.cuda.synchronize(self.device)
         pool = torch.cuda.graph_pool_handle()
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=pool):
-            st["loss"] = self._phase1(st["images"], st["ml"], st["cl"])
+            st["loss"] = self._phase1(st["images"], st["tg"], None)
             if not self.split:
                 self._phase2()
         st["graphs"].append(g1)
@@ -238,8 +241,8 @@ class Trainer:
         return st
 
     def _graph_step(self, images, mask_labels, class_labels):
-        key = (tuple(images.shape), images.dtype, tuple((tuple(m.shape), m.dtype) for m in mask_labels),
-               tuple((tuple(c.shape), c.dtype) for c in class_labels))
+        kc = max([int(c.shape[0]) for c in class_labels] + [0])
+        key = (tuple(images.shape), images.dtype, kc, tuple(mask_labels[0].shape[-2:]) if mask_labels else ())
         st = self._graph_states.get(key)
         if st is None:
             seen = self._eager_seen.get(key, 0)
@@ -249,13 +252,10 @@ class Trainer:
                 self._eager_seen[key] = seen + 1
                 return self._eager_split_step(images, mask_labels, class_labels) if self.split else \
                     self._eager_bf16_step(images, mask_labels, class_labels)
-            st = self._graph_states[key] = self._capture(images, mask_labels, class_labels)
+            st = self._graph_states[key] = self._capture(images, mask_labels, class_labels, kc)
         with torch.no_grad():
             st["images"].copy_(images)
-            for d, x in zip(st["ml"], mask_labels):
-                d.copy_(x)
-            for d, x in zip(st["cl"], class_labels):
-                d.copy_(x)
+            st["tg"].copy_from_lists(mask_labels, class_labels)
         if self.split:
             self._set_num_masks(class_labels)
             st["graphs"][0].replay()
@@ -272,9 +272,10 @@ class Trainer:
 
     def step(self, images, mask_labels, class_labels):
         """One optimisation step; returns the (device) loss tensor, no host sync.  With
-        graphs=True the step is captured once per input-shape signature (after
-        `graph_warmup` eager steps of that signature) and replayed: one launch per graph
-        instead of ~3200 per step."""
+        graphs=True the step is captured once per signature (image shape, largest target
+        count of the batch; after `graph_warmup` eager steps of it) and replayed with the
+        batch's targets padded into static buffers: one launch per graph instead of ~3200
+        per step."""
         if self.graphs:
             loss = self._graph_step(images, mask_labels, class_labels)
             self.sched.step()
