@@ -171,6 +171,41 @@ def cpu_baseline(model_name, size, iters, queries):
                        f"median of {iters} iters after 1 warm-up, {med:.1f} s/iter")
 
 
+def parity_check(model_name, size, queries, dev):
+    """BASELINE metric, second half: mask-logit max-abs-err of the GPU path (fp32 kernel
+    mode) vs the oracle CPU restatement on one `size`^2 image, same weights (init_weights
+    + perturbed tables/offsets so every path carries signal), every decoder step.  The
+    decoder's attention masks are threshold decisions; the number of mask bits that
+    differ from the oracle's (all at near-zero logits, tests/test_gpu_model.py) is reported."""
+    from oracle.ref_model import RefConfig, RefMask2Former
+    from visionseg.model import M2FConfig, Mask2Former, unpack_bitmask_like
+    cfg = M2FConfig.preset(model_name, num_queries=queries)
+    m = Mask2Former(cfg).init_weights(0)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "rel_table" in n or "attention_weights" in n or "level_embed" in n:
+                p.add_(0.3 * torch.randn(p.shape, generator=g))
+    ref = RefMask2Former(RefConfig.from_dict(cfg.to_dict()))
+    ref.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
+    m = m.to(dev).eval()
+    ref.eval()
+    px = torch.randn(1, 3, size, size, generator=torch.Generator().manual_seed(5))
+    with torch.no_grad():
+        ref.decoder.record = True
+        rmasks, _ = ref(px)
+        m.decoder.record = True
+        masks, _ = m(px.to(dev))
+        err = max(float((a.cpu() - b).abs().max()) for a, b in zip(masks, rmasks))
+        flips = sum(int((unpack_bitmask_like(w, rb.shape[-1]).cpu() != rb).sum())
+                    for (rb, _), w in zip(ref.decoder.trace, m.decoder.trace))
+    del m, ref
+    torch.cuda.empty_cache()
+    return dict(mask_logit_max_abs_err=float(f"{err:.3e}"), tolerance=1e-3, attention_mask_bit_flips=flips,
+                sample=f"1x3x{size}^2 {model_name} Mask2Former, {queries} queries, fp32 kernel mode vs the oracle "
+                       f"CPU restatement, all {cfg.dec_layers} decoder steps")
+
+
 def main():
     a = parse()
     from visionseg.train import init_distributed, Trainer, SolverConfig
@@ -226,10 +261,11 @@ def main():
     value = a.batch * world * a.steps / elapsed
     if rank == 0:
         roof, table = kernel_roofline(timer.summary()) if timer else (None, {})
-        cpu = None
+        cpu, parity = None, None
         if world == 1 and not a.no_cpu_baseline:
             torch.set_num_threads(min(16, os.cpu_count() or 1))
             cpu = cpu_baseline(a.model, a.size, a.cpu_iters, a.queries)
+            parity = parity_check(a.model, a.size, a.queries, dev)
         line = {
             "metric": "images/sec @1024^2 Swin-T Mask2Former training (fwd+loss+bwd+AdamW)",
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -248,6 +284,7 @@ def main():
             if graphs else "HIP events over the timed region",
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
             "kernels": table,
         }
         print(json.dumps(line), flush=True)
