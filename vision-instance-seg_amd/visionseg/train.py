@@ -105,6 +105,7 @@ class Trainer:
         self.split = self.graphs and distributed
         self.graph_warmup = max(1, int(graph_warmup))
         self._graph_states, self._eager_seen = {}, {}
+        self._pool = None
         if self.split:
             self.net = self.model
             with torch.no_grad():                       # DDP's start-up broadcast from rank 0
@@ -225,7 +226,15 @@ class Trainer:
         st = {"images": images.clone(), "tg": PaddedTargets.from_lists(mask_labels, class_labels, kc=kc,
                                                                        device=self.device), "graphs": []}
         torch.cuda.synchronize(self.device)
-        pool = torch.cuda.graph_pool_handle()
+        # one private pool per trainer, shared by all its captures (replays are serial);
+        # the BLAS workspace cached per (handle, capture stream) is dropped before and
+        # after every capture, so each graph allocates its own inside the pool instead of
+        # reusing one that lives in another graph's pool (torch/_inductor/cudagraph_trees.py
+        # clear_cublass_cache does the same)
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        pool = self._pool
+        torch._C._cuda_clearCublasWorkspaces()
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=pool):
             st["loss"] = self._phase1(st["images"], st["tg"], None)
@@ -238,6 +247,7 @@ class Trainer:
                 self._phase2()
             st["graphs"].append(g2)
         torch.cuda.synchronize(self.device)
+        torch._C._cuda_clearCublasWorkspaces()
         return st
 
     def _graph_step(self, images, mask_labels, class_labels):
