@@ -106,7 +106,7 @@ def pmc_traffic(op):
             return None, None
         for k, v in hits:
             tot += v["fetch_bytes"] + v["write_bytes"]
-            used.append(k.split("(")[0][:80])
+            used.append(pat)
     return int(tot), used
 
 

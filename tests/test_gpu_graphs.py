@@ -57,9 +57,9 @@ def test_graph_step_matches_eager():
     from visionseg.train import Trainer
     cfg, model, crit, b1, b2 = _setup()
     ta = Trainer(copy.deepcopy(model), crit, device=DEV)
-    tb = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV, graphs=True, graph_warmup=1)
+    tb = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV, graphs=True, graph_warmup=2)
     before = [p.detach().clone() for p in tb.params]
-    batches = [b1, b1, b2, b1, b2]
+    batches = [b1, b1, b1, b2, b1, b2]
     la = _run(ta, batches)
     lb = _run(tb, batches)
     assert len(tb._graph_states) == 1
@@ -74,11 +74,11 @@ def test_graph_new_signature_recaptures():
     from visionseg.data import synthetic_batch
     from visionseg.train import Trainer
     cfg, model, crit, b1, _ = _setup()
-    tb = Trainer(copy.deepcopy(model), crit, device=DEV, graphs=True, graph_warmup=1)
+    tb = Trainer(copy.deepcopy(model), crit, device=DEV, graphs=True, graph_warmup=2)
     b3 = synthetic_batch(2, 256, seed=7, device=DEV)
     if [int(c.shape[0]) for c in b3[2]] == [int(c.shape[0]) for c in b1[2]]:
         pytest.skip("seed gave the same target counts")
-    losses = _run(tb, [b1, b1, b3, b3, b1])
+    losses = _run(tb, [b1, b1, b1, b3, b3, b3, b1])
     assert all(torch.isfinite(torch.tensor(losses)))
     assert len(tb._graph_states) == 2
 
@@ -100,8 +100,8 @@ def test_graph_same_capacity_replays():
     if b4 is None:
         pytest.skip("no batch with the same capacity and other counts")
     ta = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV)
-    tb = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV, graphs=True, graph_warmup=1)
-    batches = [b1, b1, b4, b1, b4]
+    tb = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV, graphs=True, graph_warmup=2)
+    batches = [b1, b1, b1, b4, b1, b4]
     la = _run(ta, batches)
     lb = _run(tb, batches)
     assert len(tb._graph_states) == 1
@@ -125,9 +125,9 @@ def test_split_graph_step_one_rank():
                             device_id=DEV)
     try:
         tb = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV, distributed=True, graphs=True,
-                     graph_warmup=1)
+                     graph_warmup=2)
         assert tb.split
-        batches = [b1, b1, b2, b1]
+        batches = [b1, b1, b1, b2, b1]
         la = _run(ta, batches)
         lb = _run(tb, batches)
         _compare(ta, tb, la, lb)

@@ -103,7 +103,10 @@ class Trainer:
         # graphs (no collective inside a capture), so DDP's hooks are not used
         self.graphs = bool(graphs) and self.device.type == "cuda" and self.mode == "bf16"
         self.split = self.graphs and distributed
-        self.graph_warmup = max(1, int(graph_warmup))
+        # at least two eager steps of a signature before its capture: captures after a
+        # single eager step of a fresh process faulted on their first replay on MI355X
+        # (tools/graph_diag.py), two (the bench's setting) have always replayed cleanly
+        self.graph_warmup = max(2, int(graph_warmup))
         self._graph_states, self._eager_seen = {}, {}
         self._pool = None
         if self.split:
