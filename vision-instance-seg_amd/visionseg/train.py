@@ -108,7 +108,6 @@ class Trainer:
         # (tools/graph_diag.py), two (the bench's setting) have always replayed cleanly
         self.graph_warmup = max(2, int(graph_warmup))
         self._graph_states, self._eager_seen = {}, {}
-        self._pool = None
         if self.split:
             self.net = self.model
             with torch.no_grad():                       # DDP's start-up broadcast from rank 0
@@ -229,14 +228,14 @@ class Trainer:
         st = {"images": images.clone(), "tg": PaddedTargets.from_lists(mask_labels, class_labels, kc=kc,
                                                                        device=self.device), "graphs": []}
         torch.cuda.synchronize(self.device)
-        # one private pool per trainer, shared by all its captures (replays are serial);
-        # the BLAS workspace cached per (handle, capture stream) is dropped before and
-        # after every capture, so each graph allocates its own inside the pool instead of
-        # reusing one that lives in another graph's pool (torch/_inductor/cudagraph_trees.py
-        # clear_cublass_cache does the same)
-        if self._pool is None:
-            self._pool = torch.cuda.graph_pool_handle()
-        pool = self._pool
+        # one live graph per trainer: the previous signature's graphs are destroyed before
+        # a new capture (replaying a graph captured BEFORE another capture faulted on
+        # MI355X, tools/graph_diag.py --variant recapture), and a returning signature is
+        # captured again.  The BLAS workspace cached per (handle, capture stream) is
+        # dropped before and after every capture, so each graph allocates its own inside
+        # its pool (torch/_inductor/cudagraph_trees.py clear_cublass_cache does the same)
+        self._drop_graphs()
+        pool = torch.cuda.graph_pool_handle()
         torch._C._cuda_clearCublasWorkspaces()
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=pool):
@@ -252,6 +251,17 @@ class Trainer:
         torch.cuda.synchronize(self.device)
         torch._C._cuda_clearCublasWorkspaces()
         return st
+
+    def _drop_graphs(self):
+        if not self._graph_states:
+            return
+        for p in self.model_params:          # gradients living in the old graph's pool
+            p.grad = None
+        for st in self._graph_states.values():
+            for g in st["graphs"]:
+                g.reset()
+        self._graph_states.clear()
+        torch.cuda.synchronize(self.device)
 
     def _graph_step(self, images, mask_labels, class_labels):
         kc = max([int(c.shape[0]) for c in class_labels] + [0])
@@ -285,10 +295,11 @@ class Trainer:
 
     def step(self, images, mask_labels, class_labels):
         """One optimisation step; returns the (device) loss tensor, no host sync.  With
-        graphs=True the step is captured once per signature (image shape, largest target
-        count of the batch; after `graph_warmup` eager steps of it) and replayed with the
-        batch's targets padded into static buffers: one launch per graph instead of ~3200
-        per step."""
+        graphs=True the step is captured per signature (image shape, largest target count
+        of the batch; after `graph_warmup` eager steps of it) and replayed with the batch's
+        targets padded into static buffers: one launch per graph instead of ~3200 per
+        step.  One signature's graph lives at a time: another signature destroys it and is
+        captured in its place."""
         if self.graphs:
             loss = self._graph_step(images, mask_labels, class_labels)
             self.sched.step()
