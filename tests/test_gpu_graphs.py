@@ -78,9 +78,9 @@ def test_graph_new_signature_recaptures():
     b3 = synthetic_batch(2, 256, seed=7, device=DEV)
     if [int(c.shape[0]) for c in b3[2]] == [int(c.shape[0]) for c in b1[2]]:
         pytest.skip("seed gave the same target counts")
-    # b1 captured; b3 eager twice with a b1 replay between; b3 captured (b1's graph
-    # dropped); b1 captured again and replayed
-    seq = [b1, b1, b1, b3, b1, b3, b3, b1, b1]
+    # b1 captured; b3 arrives: b1's graph dropped, b3 eager twice then captured; b1
+    # returns: b3's graph dropped, b1 captured again (seen twice already) and replayed
+    seq = [b1, b1, b1, b3, b3, b3, b1, b1]
     ta = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV)
     la = _run(ta, seq)
     lb = _run(tb, seq)

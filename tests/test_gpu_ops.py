@@ -575,6 +575,35 @@ def test_window_attention_bf16_fwd_bwd_vs_oracle(monkeypatch, shift, heads, nWh,
         assert e <= 2e-2 * float(exp.abs().max()), (e, float(exp.abs().max()))
 
 
+@pytest.mark.parametrize("ws,shift,heads,nWh,nWw", [(12, 0, 4, 2, 3), (12, 6, 4, 3, 3), (12, 6, 8, 2, 2),
+                                                    (9, 4, 2, 2, 2), (10, 5, 3, 3, 2), (11, 0, 1, 2, 2)])
+def test_window_attention_bf16_large_windows_vs_oracle(ws, shift, heads, nWh, nWw):
+    """bf16 MFMA window attention for 64 < N <= 160 (Swin-B/L ws 12: N = 144; one wave per
+    32-query tile, csrc/window_attn.hip win_attn_*_mfma_big) vs the f32 oracle on the same
+    bf16-rounded inputs; tolerances as the N <= 64 path."""
+    ops = _ops()
+    B = 2
+    Bw, N, C = B * nWh * nWw, ws * ws, heads * 32
+    g = torch.Generator().manual_seed(ws * 100 + shift * 10 + heads)
+    qkv = torch.randn(Bw, N, 3 * C, generator=g).to(torch.bfloat16)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g)
+    qr, tr = qkv.float().requires_grad_(True), table.clone().requires_grad_(True)
+    ref = _win_attn_ref(qr, tr, heads, ws, shift, nWh, nWw)
+    go = torch.randn(ref.shape, generator=g).to(torch.bfloat16)
+    ref.backward(go.float())
+    qd, td = qkv.to(DEV).requires_grad_(True), table.to(DEV).requires_grad_(True)
+    out = ops.window_attention(qd, td, heads, ws, shift, nWh, nWw)
+    err = (out.float().cpu() - ref.detach()).abs()
+    assert bool((err <= ref.detach().abs() * 2 ** -7 + 4e-3).all()), float(err.max())
+    out.backward(go.to(DEV))
+    gq, gr = qd.grad.float().cpu().view(Bw, N, 3, C), qr.grad.view(Bw, N, 3, C)
+    for part in range(3):      # q, k, v gradients separately (each scaled to its own range)
+        e = float((gq[:, :, part] - gr[:, :, part]).abs().max())
+        assert e <= 2e-2 * float(gr[:, :, part].abs().max()), (part, e)
+    e = float((td.grad.cpu() - tr.grad).abs().max())
+    assert e <= 2e-2 * float(tr.grad.abs().max()), e
+
+
 @pytest.mark.parametrize("kernel", ["mfma", "scalar"])
 @pytest.mark.parametrize("B,Q,S", [(2, 100, 4096), (1, 100, 1000), (2, 7, 300), (1, 128, 16384), (1, 130, 512)])
 def test_masked_attention_bf16_fwd_bwd_vs_oracle(monkeypatch, kernel, B, Q, S):

@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(256) win_attn_bwd_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// bf16 MFMA path (windows of N <= 64 tokens, e.g. Swin ws = 7): one wave per (window,
+// bf16 MFMA path (windows of N <= 64 tokens, e.g. Swin ws = 7; N <= 160 below): one wave per (window,
 // head).  v_mfma_f32_32x32x16_bf16 fragments (lane l: r = l & 31, hh = l >> 5):
 //   A: row r, k = 8hh + j;  B: col r, k = 8hh + j;  C/D: col r, row (i&3) + 8(i>>2) + 4hh.
 // Forward: S^T = K Q^T (keys on rows, 2x2 tiles over the 64-padded window), so a lane
@@ -658,6 +658,292 @@ __global__ void __launch_bounds__(64 * kBwdWaves) win_attn_bwd_mfma(
   for (int t = l; t < g.T2; t += 64) gp[t] = bins[t];
 }
 
+// ---------------------------------------------------------------------------------------
+// bf16 MFMA path for windows of 64 < N <= 32*NT tokens (Swin-B/L ws = 12: N = 144, NT = 5).
+// One workgroup per (window, head), one wave per 32-query tile; fragments as above.
+// Forward: K (natural [key][d]) and V^T ([d][key]) of the window staged once in LDS; a
+// wave forms S^T for all NT key tiles of its queries (NT accumulators), softmax in
+// registers, and O^T = V^T P^T with P^T straight from the accumulators (permuted k).
+// Backward: a wave forms S^T and dP^T for its queries (2 NT accumulators) and writes P^T
+// to a shared [key][q] LDS tile (which aliases the K/V staging); after a block barrier
+// wave w computes dV of key tile w over all queries; the tile is then overwritten with
+// dS^T for dK of key tile w; dQ^T of the wave's queries comes from registers as above.
+constexpr int kMaxT2Big = 529;    // (2*12-1)^2
+
+template <int NT>
+__device__ __forceinline__ void window_tokens_blk(const WinGeom& g, int bw, int* tok) {
+  const int ws = g.ws;
+  const int wl = bw % (g.nWh * g.nWw);
+  const int wy = wl / g.nWw, wx = wl % g.nWw;
+  const int Hp = g.nWh * ws, Wp = g.nWw * ws;
+  for (int t = threadIdx.x; t < 32 * NT; t += blockDim.x) {
+    if (t < g.N) {
+      const int ty = t / ws, tx = t % ws;
+      const int reg = g.shift > 0 ? region_of(wy * ws + ty, Hp, ws, g.shift) * 3 + region_of(wx * ws + tx, Wp, ws, g.shift) : 0;
+      tok[t] = ty | (tx << 8) | (reg << 16);
+    } else {
+      tok[t] = 0;
+    }
+  }
+}
+
+template <int NT>
+__global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __restrict__ qkv,
+                                                                 const float* __restrict__ table,
+                                                                 bf16* __restrict__ out, float* __restrict__ lse,
+                                                                 WinGeom g) {
+  constexpr int NP = 32 * NT, PT = NP + 8, PK = 40;
+  __shared__ __attribute__((aligned(16))) short sK[NP * PK];   // K [key][d]
+  __shared__ __attribute__((aligned(16))) short sVt[32 * PT];  // V^T [d][key]
+  __shared__ float sBias[kMaxT2Big];
+  __shared__ int sTok[NP];
+  const int bw = blockIdx.x, h = blockIdx.y;
+  const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int N = g.N, C = g.heads * kD, C3 = 3 * C;
+  const bf16* win = qkv + (size_t)bw * N * C3;
+  window_tokens_blk<NT>(g, bw, sTok);
+  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
+  for (int p = threadIdx.x; p < NP * 4; p += blockDim.x) {
+    const int t = p >> 2, c = p & 3;
+    bf16x8_t k = zero8(), v = zero8();
+    if (t < N) {
+      k = ld8(win + (size_t)t * C3 + C + h * kD + 8 * c);
+      v = ld8(win + (size_t)t * C3 + 2 * C + h * kD + 8 * c);
+    }
+    *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = k;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sVt[(8 * c + j) * PT + t] = v[j];
+  }
+  bf16x8_t qb[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const int row = 32 * qt + r;
+    qb[st] = row < N ? ld8(win + (size_t)row * C3 + h * kD + 16 * st + 8 * hh) : zero8();
+  }
+  __syncthreads();
+  // S^T = K Q^T for every key tile of this wave's queries
+  f32x16_t acc[NT];
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) zero16(acc[kt]);
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(sK + (32 * kt + r) * PK + 16 * st + 8 * hh);
+      acc[kt] = mfma16(ka, qb[st], acc[kt]);
+    }
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) {
+    logits_tile(acc[kt], g, sTok, sBias, kt, qt, r, hh);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m = fmaxf(m, acc[kt][i]);
+  }
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      acc[kt][i] = __expf(acc[kt][i] - m);
+      sum += acc[kt][i];
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum, lq = m + __logf(sum);
+  // O^T = V^T P^T
+  f32x16_t o;
+  zero16(o);
+#pragma unroll
+  for (int t = 0; t < 2 * NT; ++t) {
+    const int kt = t >> 1, th = t & 1;
+    const bf16x8_t a = ld_perm(sVt + r * PT, 32 * kt + 16 * th + 4 * hh);
+    o = mfma16(a, pack8(acc[kt], 8 * th), o);
+  }
+  const int q = 32 * qt + r;
+  if (q < N) {
+    bf16* dst = out + ((size_t)bw * N + q) * C + h * kD;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      bf16x4_t v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[4 * grp + e] * inv);
+      *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+    }
+    if (hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = lq;
+  }
+}
+
+template <int NT>
+__global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
+    const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
+    const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
+    float* __restrict__ gtable_part, WinGeom g) {
+  constexpr int NP = 32 * NT, PT = NP + 8, PK = 40;
+  constexpr int kNat = NP * PK, kTB = NP * PT;
+  constexpr int kU = 2 * kNat > kTB ? 2 * kNat : kTB;
+  __shared__ __attribute__((aligned(16))) short sU[kU];        // K, V [token][d]; then P^T / dS^T [key][q]
+  __shared__ __attribute__((aligned(16))) short sQT[32 * PT];  // Q^T [d][q]
+  __shared__ __attribute__((aligned(16))) short sKT[32 * PT];  // K^T [d][key]
+  __shared__ __attribute__((aligned(16))) short sDoT[32 * PT]; // dO^T [d][q]
+  __shared__ float sBias[kMaxT2Big];
+  __shared__ float sBins[kMaxT2Big];
+  __shared__ int sTok[NP];
+  short* sK = sU;
+  short* sV = sU + kNat;
+  short* sT = sU;
+  const int bw = blockIdx.x, h = blockIdx.y;
+  const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int N = g.N, C = g.heads * kD, C3 = 3 * C;
+  const bf16* win = qkv + (size_t)bw * N * C3;
+  const bf16* gwin_o = gout + (size_t)bw * N * C + h * kD;
+  window_tokens_blk<NT>(g, bw, sTok);
+  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) {
+    sBias[t] = table[t * g.heads + h];
+    sBins[t] = 0.f;
+  }
+  for (int p = threadIdx.x; p < NP * 4; p += blockDim.x) {
+    const int t = p >> 2, c = p & 3;
+    bf16x8_t q = zero8(), k = zero8(), v = zero8(), d = zero8();
+    if (t < N) {
+      q = ld8(win + (size_t)t * C3 + h * kD + 8 * c);
+      k = ld8(win + (size_t)t * C3 + C + h * kD + 8 * c);
+      v = ld8(win + (size_t)t * C3 + 2 * C + h * kD + 8 * c);
+      d = ld8(gwin_o + (size_t)t * C + 8 * c);
+    }
+    *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = k;
+    *reinterpret_cast<bf16x8_t*>(sV + t * PK + 8 * c) = v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sQT[(8 * c + j) * PT + t] = q[j];
+      sKT[(8 * c + j) * PT + t] = k[j];
+      sDoT[(8 * c + j) * PT + t] = d[j];
+    }
+  }
+  const int q = 32 * qt + r;
+  bf16x8_t qb[2], db[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const int off = 16 * st + 8 * hh;
+    qb[st] = q < N ? ld8(win + (size_t)q * C3 + h * kD + off) : zero8();
+    db[st] = q < N ? ld8(gwin_o + (size_t)q * C + off) : zero8();
+  }
+  // D_q = dO_q . O_q and the saved log-sum-exp of this lane's query
+  float Dq = 0.f, Lq = 0.f;
+  if (q < N) {
+    const bf16* orow = out + ((size_t)bw * N + q) * C + h * kD + 16 * hh;
+    const bf16* grow = gwin_o + (size_t)q * C + 16 * hh;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const bf16x8_t ov = ld8(orow + 8 * c), gv = ld8(grow + 8 * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Dq += bf16_bits_to_f32((unsigned short)ov[j]) * bf16_bits_to_f32((unsigned short)gv[j]);
+    }
+    Lq = lse[((size_t)bw * g.heads + h) * N + q];
+  }
+  Dq += __shfl_xor(Dq, 32, 64);
+  __syncthreads();
+  // S^T = K Q^T and dP^T = V dO^T for every key tile of this wave's queries
+  f32x16_t sacc[NT], dacc[NT];
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) {
+    zero16(sacc[kt]);
+    zero16(dacc[kt]);
+  }
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      const int o = (32 * kt + r) * PK + 16 * st + 8 * hh;
+      sacc[kt] = mfma16(*reinterpret_cast<const bf16x8_t*>(sK + o), qb[st], sacc[kt]);
+      dacc[kt] = mfma16(*reinterpret_cast<const bf16x8_t*>(sV + o), db[st], dacc[kt]);
+    }
+  __syncthreads();                            // K / V staging is overwritten by P^T below
+  const int tw = 2 * g.ws - 1;
+  const int tq = sTok[q];
+  const int tyq = tq & 255, txq = (tq >> 8) & 255;
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) {
+    logits_tile(sacc[kt], g, sTok, sBias, kt, qt, r, hh);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = 32 * kt + crow(i, hh);
+      const float p = q < N ? __expf(sacc[kt][i] - Lq) : 0.f;
+      sT[key * PT + q] = bf16_bits(p);
+      const float ds = p * (dacc[kt][i] - Dq);
+      dacc[kt][i] = ds;
+      if (key < N && q < N) {
+        const int tk = sTok[key];
+        atomicAdd(&sBins[(tyq - (tk & 255) + g.ws - 1) * tw + (txq - ((tk >> 8) & 255) + g.ws - 1)], ds);
+      }
+    }
+  }
+  __syncthreads();
+  // dV = P^T dO for key tile kw = wave (k over all queries)
+  const int kw = qt;
+  bf16* gw = gqkv + (size_t)bw * N * C3 + h * kD;
+  {
+    f32x16_t dv;
+    zero16(dv);
+#pragma unroll
+    for (int t = 0; t < 2 * NT; ++t) {
+      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(sDoT + r * PT + 16 * t + 8 * hh);
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sT + (32 * kw + r) * PT + 16 * t + 8 * hh);
+      dv = mfma16(a, b, dv);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = 32 * kw + crow(i, hh);
+      if (key < N) gw[(size_t)key * C3 + 2 * C + r] = __float2bfloat16(dv[i]);
+    }
+  }
+  __syncthreads();                            // every wave has read P^T
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sT[(32 * kt + crow(i, hh)) * PT + q] = bf16_bits(dacc[kt][i]);
+  __syncthreads();
+  // dK = scale * dS^T Q for key tile kw
+  {
+    f32x16_t dk;
+    zero16(dk);
+#pragma unroll
+    for (int t = 0; t < 2 * NT; ++t) {
+      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(sQT + r * PT + 16 * t + 8 * hh);
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sT + (32 * kw + r) * PT + 16 * t + 8 * hh);
+      dk = mfma16(a, b, dk);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = 32 * kw + crow(i, hh);
+      if (key < N) gw[(size_t)key * C3 + C + r] = __float2bfloat16(dk[i] * g.scale);
+    }
+  }
+  // dQ^T = scale * K^T dS^T for this wave's queries (dS^T from registers)
+  {
+    f32x16_t dq;
+    zero16(dq);
+#pragma unroll
+    for (int t = 0; t < 2 * NT; ++t) {
+      const int kt = t >> 1, th = t & 1;
+      const bf16x8_t a = ld_perm(sKT + r * PT, 32 * kt + 16 * th + 4 * hh);
+      dq = mfma16(a, pack8(dacc[kt], 8 * th), dq);
+    }
+    if (q < N) {
+      bf16* dst = gw + (size_t)q * C3;
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        bf16x4_t v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = bf16_bits(dq[4 * grp + e] * g.scale);
+        *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+      }
+    }
+  }
+  __syncthreads();
+  float* gp = gtable_part + ((size_t)bw * g.heads + h) * g.T2;
+  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) gp[t] = sBins[t];
+}
+
 int check_geom(WinGeom& g, int Bw, int heads, int ws, int shift, int nWh, int nWw, float scale) {
   g.heads = heads; g.ws = ws; g.shift = shift; g.nWh = nWh; g.nWw = nWw; g.scale = scale;
   g.N = ws * ws;
@@ -692,6 +978,14 @@ extern "C" int vs_window_attn_forward(int dtype, const void* qkv, const float* t
     const int items = Bw * heads;
     hipLaunchKernelGGL(win_attn_fwd_mfma, dim3((items + kFwdWaves - 1) / kFwdWaves), dim3(64 * kFwdWaves), 0, st,
                        (const bf16*)qkv, table, (bf16*)out, lse, g, items);
+  } else if (dtype == VS_BF16 && g.N <= 160 && use_mfma()) {
+    const int nt = (g.N + 31) / 32;
+    if (nt == 3)
+      hipLaunchKernelGGL(win_attn_fwd_mfma_big<3>, grid, dim3(192), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
+    else if (nt == 4)
+      hipLaunchKernelGGL(win_attn_fwd_mfma_big<4>, grid, dim3(256), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
+    else
+      hipLaunchKernelGGL(win_attn_fwd_mfma_big<5>, grid, dim3(320), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
   } else if (dtype == VS_BF16) {
     hipLaunchKernelGGL(win_attn_fwd_kernel<bf16>, grid, dim3(threads), lds, st, (const bf16*)qkv, table,
                        (bf16*)out, lse, g);
@@ -723,6 +1017,18 @@ extern "C" int vs_window_attn_backward(int dtype, const void* qkv, const float* 
     hipLaunchKernelGGL(win_attn_bwd_mfma, dim3((items + kBwdWaves - 1) / kBwdWaves), dim3(64 * kBwdWaves), 0, st,
                        (const bf16*)qkv, table, (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv,
                        grad_table_partial, g, items);
+  } else if (dtype == VS_BF16 && g.N <= 160 && use_mfma()) {
+    const int nt = (g.N + 31) / 32;
+#define VS_WIN_BWD_BIG(NT_)                                                                                       \
+  hipLaunchKernelGGL(win_attn_bwd_mfma_big<NT_>, grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,            \
+                     (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, grad_table_partial, g)
+    if (nt == 3)
+      VS_WIN_BWD_BIG(3);
+    else if (nt == 4)
+      VS_WIN_BWD_BIG(4);
+    else
+      VS_WIN_BWD_BIG(5);
+#undef VS_WIN_BWD_BIG
   } else if (dtype == VS_BF16) {
     hipLaunchKernelGGL(win_attn_bwd_kernel<bf16>, grid, dim3(threads), lds, st, (const bf16*)qkv, table,
                        (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, grad_table_partial, g);

@@ -228,13 +228,10 @@ class Trainer:
         st = {"images": images.clone(), "tg": PaddedTargets.from_lists(mask_labels, class_labels, kc=kc,
                                                                        device=self.device), "graphs": []}
         torch.cuda.synchronize(self.device)
-        # one live graph per trainer: the previous signature's graphs are destroyed before
-        # a new capture (replaying a graph captured BEFORE another capture faulted on
-        # MI355X, tools/graph_diag.py --variant recapture), and a returning signature is
-        # captured again.  The BLAS workspace cached per (handle, capture stream) is
-        # dropped before and after every capture, so each graph allocates its own inside
-        # its pool (torch/_inductor/cudagraph_trees.py clear_cublass_cache does the same)
-        self._drop_graphs()
+        # one live graph per trainer (see _graph_step).  The BLAS workspace cached per
+        # (handle, capture stream) is dropped before and after every capture, so each
+        # graph allocates its own inside its pool (torch/_inductor/cudagraph_trees.py
+        # clear_cublass_cache does the same)
         pool = torch.cuda.graph_pool_handle()
         torch._C._cuda_clearCublasWorkspaces()
         g1 = torch.cuda.CUDAGraph()
@@ -268,6 +265,10 @@ class Trainer:
         key = (tuple(images.shape), images.dtype, kc, tuple(mask_labels[0].shape[-2:]) if mask_labels else ())
         st = self._graph_states.get(key)
         if st is None:
+            # another signature's graph is destroyed BEFORE any eager work of this one: a
+            # graph replayed after eager steps of a different signature faulted on MI355X
+            # (tools/graph_diag.py); a returning signature is captured again
+            self._drop_graphs()
             seen = self._eager_seen.get(key, 0)
             if seen < self.graph_warmup:
                 # eager steps first: lazy library state and the optimiser's moments exist
