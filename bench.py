@@ -21,6 +21,9 @@ import os
 import sys
 import time
 
+# before HIP initialises (see visionseg/__init__.py)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, "vision-instance-seg_amd")):
     if _p not in sys.path:

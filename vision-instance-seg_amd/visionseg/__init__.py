@@ -7,3 +7,13 @@ plus the model, criterion, data-parallel trainer and the adapters the reference'
 callers use (`train_template.train_maskdino`, `AISegmentationModel`).
 """
 __version__ = "0.1.0"
+
+import os as _os
+
+# HIP graphs (Trainer(graphs=True)): ROCm's graph packet capture (kernel packets and
+# kernel arguments of a graph exec recorded once at instantiation) replayed graphs with
+# the wrong kernel arguments after another graph was captured or destroyed -- illegal
+# memory accesses on MI355X (tools/graph_diag.py --variant recapture).  Plain per-node
+# graph launches cost nothing measurable here (59.2 vs 59.0 ms/step).  The runtime reads
+# the flag once, at HIP initialisation: import visionseg before touching the device.
+_os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")

@@ -103,9 +103,8 @@ class Trainer:
         # graphs (no collective inside a capture), so DDP's hooks are not used
         self.graphs = bool(graphs) and self.device.type == "cuda" and self.mode == "bf16"
         self.split = self.graphs and distributed
-        # at least two eager steps of a signature before its capture: captures after a
-        # single eager step of a fresh process faulted on their first replay on MI355X
-        # (tools/graph_diag.py), two (the bench's setting) have always replayed cleanly
+        # at least two eager steps of a signature before its capture (lazy library state
+        # and the optimiser's moments exist before the capture records anything)
         self.graph_warmup = max(2, int(graph_warmup))
         self._graph_states, self._eager_seen = {}, {}
         if self.split:
@@ -265,9 +264,10 @@ class Trainer:
         key = (tuple(images.shape), images.dtype, kc, tuple(mask_labels[0].shape[-2:]) if mask_labels else ())
         st = self._graph_states.get(key)
         if st is None:
-            # another signature's graph is destroyed BEFORE any eager work of this one: a
-            # graph replayed after eager steps of a different signature faulted on MI355X
-            # (tools/graph_diag.py); a returning signature is captured again
+            # one live graph per trainer (bounded pool memory): another signature's graph
+            # is destroyed before any eager work of this one, and a returning signature is
+            # captured again.  (Replays that faulted after a recapture were ROCm's graph
+            # packet capture, disabled in visionseg/__init__.py; tools/graph_diag.py.)
             self._drop_graphs()
             seen = self._eager_seen.get(key, 0)
             if seen < self.graph_warmup:
