@@ -52,6 +52,7 @@ elif _gt == "tune":
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+MODEL_NAMES = {"swin_t": "Swin-T", "swin_s": "Swin-S", "swin_b": "Swin-B", "swin_l": "Swin-L"}
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA spec
 VALU_F32_PEAK_TFS = 157.3    # f32 vector / f32 MFMA spec
@@ -209,6 +210,12 @@ def parity_check(model_name, size, queries, dev):
                        f"CPU restatement, all {cfg.dec_layers} decoder steps")
 
 
+def _config_tag(model, size):
+    """BASELINE.json config the run corresponds to (C2 is the headline workload)."""
+    return {("swin_t", 1024): "C2", ("swin_b", 1024): "C3 (per-GPU share)",
+            ("swin_l", 1536): "C5 (per-GPU share, bf16)"}.get((model, size), "custom")
+
+
 def main():
     a = parse()
     from visionseg.train import init_distributed, Trainer, SolverConfig
@@ -270,11 +277,12 @@ def main():
             cpu = cpu_baseline(a.model, a.size, a.cpu_iters, a.queries)
             parity = parity_check(a.model, a.size, a.queries, dev)
         line = {
-            "metric": "images/sec @1024^2 Swin-T Mask2Former training (fwd+loss+bwd+AdamW)",
+            "metric": f"images/sec @{a.size}^2 {MODEL_NAMES.get(a.model, a.model)} Mask2Former training "
+                      "(fwd+loss+bwd+AdamW)",
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic COCO-format defect batches (random-init weights)",
-            "config": {"workload": f"C2: {a.model} + Mask2Former, {a.batch}x3x{a.size}^2 per GPU, "
+            "config": {"workload": f"{_config_tag(a.model, a.size)}: {a.model} + Mask2Former, {a.batch}x3x{a.size}^2 per GPU, "
                                    f"{cfg.num_queries} queries, bf16 autocast, 1 class",
                        "model": f"{a.model}_mask2former", "global_batch": a.batch * world, "image_size": a.size,
                        "parallelism": f"dp{world}"},
