@@ -107,6 +107,22 @@ VS_API int vs_msda_backward_sorted(int dtype, const void* value, const int64_t* 
                                    int num_heads, int channels, int num_levels, int num_query, int num_point,
                                    void* stream);
 
+/* Default backward (replaces MSDeformAttnFunction.backward / ms_deform_attn_backward,
+ * upstream ms_deform_attn_cuda.cu, behind HF:m2f:798-837): grad_value by destination tiles
+ * (image, head, level, te x te cells), each owned by one wave that accumulates its
+ * corner contributions with plain LDS read-modify-write -- no float atomics, no memset;
+ * grad_value [B, S, H, 32] is written once, in the value dtype.  grad_loc / grad_attn as
+ * in vs_msda_backward.  Any queries.  workspace >=
+ * vs_msda_backward_tiled_workspace_bytes (spatial_shapes_host as below; -1 on bad sizes). */
+VS_API long long vs_msda_backward_tiled_workspace_bytes(int batch, int num_heads, int num_levels, int num_query,
+                                                        int num_point, const int64_t* spatial_shapes_host);
+VS_API int vs_msda_backward_tiled(int dtype, const void* value, const int64_t* spatial_shapes_host,
+                                  const int64_t* level_start_host, const float* sampling_loc,
+                                  const float* attn_weight, const void* grad_out, void* grad_value,
+                                  float* grad_loc, float* grad_attn, void* workspace, int batch, int spatial_size,
+                                  int num_heads, int channels, int num_levels, int num_query, int num_point,
+                                  void* stream);
+
 /* ---- a2: Swin pad + cyclic shift + window partition / its inverse ---------------
  * window_partition: x [B, H, W, C] -> windows [B*nWh*nWw, ws*ws, C] where
  * Hp = ceil(H/ws)*ws, nWh = Hp/ws (same for W); windows[(b,wy,wx), (ty,tx)] =

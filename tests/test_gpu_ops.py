@@ -352,6 +352,7 @@ def test_msda_encoder_backward_vs_oracle(monkeypatch, cfg, dtype, near_r):
     monkeypatch.setenv("VS_MSDA_NEAR_R", near_r)
     ops = _ops()
     monkeypatch.setattr(ops, "_MSDA_SORTED", False)          # the atomic scatter paths
+    monkeypatch.setattr(ops, "_MSDA_BWD", "carry")
     shapes, B, H, L, P = cfg["shapes"], cfg["B"], cfg["H"], len(cfg["shapes"]), 4
     S = sum(h * w for h, w in shapes)
     g = torch.Generator().manual_seed(31)
@@ -434,6 +435,7 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, jitter):
     monkeypatch.setenv("VS_MSDA_RUN", run)
     ops = _ops()
     monkeypatch.setattr(ops, "_MSDA_SORTED", False)
+    monkeypatch.setattr(ops, "_MSDA_BWD", "carry")
     shapes = [(8, 8), (16, 16), (32, 32)]
     value, loc, w = _encoder_like_inputs(2, shapes, 4, 4, seed=11, jitter=jitter)
     vr, lr, wr = (t.clone().requires_grad_(True) for t in (value, loc, w))
@@ -458,11 +460,14 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, jitter):
     dict(B=1, shapes=[(5, 7)], H=2, jitter=1.0, Q=0),                                  # no queries
 ])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_msda_sorted_backward_vs_oracle(monkeypatch, case, dtype):
-    """grad_value by destination after a counting sort (vs_msda_backward_sorted, opt-in
-    path) vs the oracle; bf16: grad_value is produced in bf16 from f32 sums."""
+@pytest.mark.parametrize("mode", ["tiled", "sorted"])
+def test_msda_destination_backward_vs_oracle(monkeypatch, case, dtype, mode):
+    """grad_value by destination -- tiles owned by one wave (vs_msda_backward_tiled, the
+    default) or after a per-cell counting sort (vs_msda_backward_sorted, opt-in) -- vs the
+    oracle; bf16: grad_value is produced in bf16 from f32 sums."""
     ops = _ops()
-    monkeypatch.setattr(ops, "_MSDA_SORTED", True)
+    monkeypatch.setattr(ops, "_MSDA_SORTED", mode == "sorted")
+    monkeypatch.setattr(ops, "_MSDA_BWD", mode)
     shapes, B, H = case["shapes"], case["B"], case["H"]
     value, loc, w = _encoder_like_inputs(B, shapes, H, 4, seed=21, jitter=case["jitter"])
     if case["Q"] is not None:

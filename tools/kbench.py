@@ -65,8 +65,9 @@ def main():
         for oname, off in offs.items():
             loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
             locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
-            for mode in ("sorted", "carry16", "plain", "pull5"):
+            for mode in ("tiled", "carry16", "sorted", "pull5"):
                 ops._MSDA_SORTED = mode == "sorted"
+                ops._MSDA_BWD = {"tiled": "tiled", "sorted": "sorted"}.get(mode, "carry")
                 os.environ["VS_MSDA_RUN"] = {"carry16": "16"}.get(mode, "0")
                 os.environ["VS_MSDA_NEAR_R"] = mode[4:] if mode.startswith("pull") else "5"
 

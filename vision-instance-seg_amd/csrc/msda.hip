@@ -783,6 +783,177 @@ __global__ void __launch_bounds__(256) msda_pull_sorted_kernel(const int* __rest
   Vec16<T>::store(gvalue + key * kD + sub * V, acc);
 }
 
+// ---------------------------------------------------------------------------------
+// grad_value by destination TILES, without float atomics (default backward).
+//
+// gfx950 measurement (tools/micro/lds_atomic_bench.hip): LDS float atomics (ds_add_f32)
+// retire ~0.33 lane-ops/clk/CU -- slower than global f32 atomics (~1.1 TB/s of added
+// bytes) and ~18x slower than a plain LDS read-modify-write -- which is why every earlier
+// LDS-atomic variant (bands, destination tiles) lost to the global-atomic carry scatter.
+// This path has ONE wave own each destination tile, so its accumulation is plain LDS
+// read-modify-write:
+//   count:  per tap (natural order), the distinct tiles its valid corners fall in (1, 2
+//           or 4) -> count[tile] += 1, one atomic per distinct tile per wave (ballot)
+//   scan:   offset(tile) = exclusive prefix of count (the sort_scan kernels)
+//   fill:   records[offset(tile) + rank] = q * P + p   (4 B; geometry is recomputed)
+//   accum:  one wave per tile: per record, lanes = 2 corner rows x 32 channels add
+//           w * attw * grad_out[q, h, c] into the tile's te x te x 32 f32 LDS block
+//           (rows (y, y+1) land in opposite LDS bank halves), then every cell of the
+//           tile is written once, in the value dtype.  No memset, no float atomics.
+// A tile is (image, head, level, te x te cells), te chosen per level so that tiles carry
+// about the same number of taps (te = 8 / 4 / 2 for ~5 / 21 / 84 taps per cell).
+constexpr int kTileMaxEdge = 8;
+
+struct TileGeo {
+  int sh[kMaxLevels];     // log2(te) per level
+  int ntx[kMaxLevels];    // tiles per row
+  int nty[kMaxLevels];    // tile rows
+  int base[kMaxLevels + 1];
+  int per_bh;             // tiles per (image, head)
+};
+
+// distinct tiles of a tap's valid corners, -1 padded (the tap must be inside)
+__device__ __forceinline__ void tap_tiles(const TileGeo& tg, int l, const Tap& t, int Hl, int Wl, int* id) {
+  const int sh = tg.sh[l];
+  const int ya = t.h0 >= 0 ? t.h0 : t.h0 + 1, yb = t.h0 + 1 <= Hl - 1 ? t.h0 + 1 : t.h0;
+  const int xa = t.w0 >= 0 ? t.w0 : t.w0 + 1, xb = t.w0 + 1 <= Wl - 1 ? t.w0 + 1 : t.w0;
+  const int ty0 = ya >> sh, ty1 = yb >> sh, tx0 = xa >> sh, tx1 = xb >> sh;
+  const int nx = tg.ntx[l], b0 = tg.base[l];
+  id[0] = b0 + ty0 * nx + tx0;
+  id[1] = tx1 != tx0 ? b0 + ty0 * nx + tx1 : -1;
+  id[2] = ty1 != ty0 ? b0 + ty1 * nx + tx0 : -1;
+  id[3] = (ty1 != ty0 && tx1 != tx0) ? b0 + ty1 * nx + tx1 : -1;
+}
+
+// ctr[id] += 1 for every lane with id >= 0, one atomic per distinct id of the wave;
+// returns this lane's slot (value before its own increment).  Wave-uniform call.
+__device__ __forceinline__ int wave_agg_inc(int* ctr, int id) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long pend = __ballot(id >= 0);
+  int mine = 0;
+  while (pend) {
+    const int leader = __ffsll((long long)pend) - 1;
+    const int lid = __shfl(id, leader, 64);
+    const unsigned long long m = __ballot(id == lid) & pend;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(ctr + lid, (int)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if ((m >> lane) & 1ull) mine = base + (int)__popcll(m & ((1ull << lane) - 1ull));
+    pend &= ~m;
+  }
+  return mine;
+}
+
+// FILL = false: count;  FILL = true: write records.  One thread per tap, natural order.
+template <bool FILL>
+__global__ void __launch_bounds__(256) msda_tile_bucket_kernel(const float* __restrict__ loc, int* __restrict__ ctr,
+                                                               const int* __restrict__ local,
+                                                               const int* __restrict__ bprefix, int* __restrict__ rec,
+                                                               Levels lv, TileGeo tg, int Hh, int Q, int L, int P,
+                                                               long long taps) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int id[4] = {-1, -1, -1, -1};
+  int q = 0, lp = 0;
+  if (i < taps) {
+    const int LP = L * P;
+    lp = (int)(i % LP);
+    const long long grp = i / LP;
+    const int h = (int)(grp % Hh);
+    const long long bq = grp / Hh;
+    q = (int)(bq % Q);
+    const long long b = bq / Q;
+    const int l = lp / P;
+    const int Hl = lv.h[l], Wl = lv.w[l];
+    const float2 xy = reinterpret_cast<const float2*>(loc)[i];
+    const Tap t = tap_geom(xy.x, xy.y, Hl, Wl);
+    if (t.inside) {
+      tap_tiles(tg, l, t, Hl, Wl, id);
+      const int off = (int)((b * Hh + h) * tg.per_bh);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (id[k] >= 0) id[k] += off;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int slot = wave_agg_inc(ctr, id[k]);
+    if (FILL && id[k] >= 0) rec[local[id[k]] + bprefix[id[k] / kScanBlock] + slot] = q * P + (lp % P);
+  }
+}
+
+// one wave per tile (4 tiles per workgroup); grad_value written in the value dtype
+template <typename T>
+__global__ void __launch_bounds__(256) msda_tile_accum_kernel(const float* __restrict__ loc,
+                                                              const float* __restrict__ attw,
+                                                              const T* __restrict__ gout, const int* __restrict__ local,
+                                                              const int* __restrict__ bprefix,
+                                                              const int* __restrict__ rec, T* __restrict__ gvalue,
+                                                              Levels lv, TileGeo tg, int S, int Hh, int Q, int L, int P,
+                                                              int ntiles) {
+  constexpr int kCells = kTileMaxEdge * (kTileMaxEdge + 1);
+  __shared__ __attribute__((aligned(16))) float sAcc[4][kCells * kD];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, c = lane & 31;
+  const int tile = blockIdx.x * 4 + wave;
+  if (tile >= ntiles) return;                      // wave-uniform; no block barriers below
+  const int bh = tile / tg.per_bh, lt = tile % tg.per_bh;
+  const int h = bh % Hh, b = bh / Hh;
+  int l = 0;
+  while (l + 1 < L && lt >= tg.base[l + 1]) ++l;
+  const int tl = lt - tg.base[l];
+  const int sh = tg.sh[l], te = 1 << sh, tp = te + 1;
+  const int ty0 = (tl / tg.ntx[l]) << sh, tx0 = (tl % tg.ntx[l]) << sh;
+  const int Hl = lv.h[l], Wl = lv.w[l];
+  float* acc = sAcc[wave];
+  for (int k = lane; k < te * tp * kD; k += 64) acc[k] = 0.f;
+  const int r0 = local[tile] + bprefix[tile / kScanBlock];
+  const int r1 = tile + 1 < ntiles ? local[tile + 1] + bprefix[(tile + 1) / kScanBlock]
+                                  : bprefix[(ntiles - 1) / kScanBlock + 1];
+  const int LP = L * P;
+  const long long gbase = (long long)b * Q * Hh + h;    // (b, q=0, h) group index
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr int U = 4;
+  for (int r = r0; r < r1; r += U) {
+    float2 xy[U];
+    float a[U], g[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = rec[r + u < r1 ? r + u : r];
+      const int q = e / P, p = e - q * P;
+      const long long grp = gbase + (long long)q * Hh;
+      const long long ti = grp * LP + l * P + p;
+      xy[u] = reinterpret_cast<const float2*>(loc)[ti];
+      a[u] = r + u < r1 ? attw[ti] : 0.f;
+      g[u] = to_f32(gout[grp * kD + c]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const Tap t = tap_geom(xy[u].x, xy[u].y, Hl, Wl);
+      const int y = t.h0 + half;
+      const int ly = y - ty0, lx = t.w0 - tx0;
+      const float gw = g[u] * a[u] * (half ? t.lh : t.hh);
+      if (r + u < r1 && t.inside && ly >= 0 && ly < te && y < Hl) {
+        float* row = acc + (ly * tp) * kD + c;
+        if (lx >= 0 && lx < te && t.w0 >= 0) row[lx * kD] += gw * t.hw;
+        if (lx + 1 >= 0 && lx + 1 < te && t.w0 + 1 < Wl) row[(lx + 1) * kD] += gw * t.lw;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const size_t rowstride = (size_t)Hh * kD;
+  T* gb = gvalue + (((size_t)b * S + lv.start[l]) * Hh + h) * kD + c;
+  for (int cell = half; cell < te * te; cell += 2) {
+    const int y = cell >> sh, x = cell & (te - 1);
+    if (ty0 + y < Hl && tx0 + x < Wl) {
+      const float v = acc[(y * tp + x) * kD + c];
+      gb[((size_t)(ty0 + y) * Wl + tx0 + x) * rowstride] = from_f32<T>(v);
+    }
+  }
+}
+
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // workspace: count [nkeys] | local [nkeys] | bsum [nb] | bprefix [nb + 1] | records
@@ -1035,6 +1206,116 @@ extern "C" int vs_msda_backward_sorted(int dtype, const void* value, const int64
   else
     hipLaunchKernelGGL(msda_pull_sorted_kernel<float>, dim3(pgrid), dim3(256), 0, st, local, bprefix, rec,
                        (const float*)gout, (float*)gvalue, S, Hh, Q, nkeys);
+  if (Q > 0) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, (long long)B * Q * Hh, st);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+
+// ---- tiled grad_value (default backward; see msda_tile_accum_kernel) ----------------
+static void tile_geo(TileGeo* tg, const int* hs, const int* ws, int L, int Q, int P) {
+  int base = 0;
+  for (int l = 0; l < kMaxLevels; ++l) {
+    tg->sh[l] = 3;
+    tg->ntx[l] = tg->nty[l] = 0;
+    tg->base[l] = base;
+    if (l >= L) continue;
+    const double density = (double)Q * P / ((double)hs[l] * ws[l]);
+    const int sh = density <= 8.0 ? 3 : density <= 32.0 ? 2 : 1;
+    const int te = 1 << sh;
+    tg->sh[l] = sh;
+    tg->ntx[l] = (ws[l] + te - 1) / te;
+    tg->nty[l] = (hs[l] + te - 1) / te;
+    base += tg->ntx[l] * tg->nty[l];
+  }
+  tg->base[kMaxLevels] = base;
+  tg->per_bh = base;
+}
+
+// workspace: ctr [T] | local [T] | bsum [nb] | bprefix [nb + 1] | records [4 * taps]
+static void tiled_layout(long long ntiles, long long taps, size_t* off) {
+  const long long nb = (ntiles + kScanBlock - 1) / kScanBlock;
+  off[0] = 0;
+  off[1] = align256(off[0] + ntiles * 4);
+  off[2] = align256(off[1] + ntiles * 4);
+  off[3] = align256(off[2] + nb * 4);
+  off[4] = align256(off[3] + (nb + 1) * 4);
+  off[5] = align256(off[4] + (size_t)taps * 4 * 4);
+}
+
+static int tiled_sizes(const int64_t* shapes, int B, int Hh, int L, int Q, int P, TileGeo* tg, long long* ntiles,
+                       long long* taps) {
+  int hs[kMaxLevels], ws[kMaxLevels];
+  for (int l = 0; l < L; ++l) {
+    hs[l] = (int)shapes[2 * l];
+    ws[l] = (int)shapes[2 * l + 1];
+    if (hs[l] <= 0 || ws[l] <= 0) return 0;
+  }
+  tile_geo(tg, hs, ws, L, Q, P);
+  *ntiles = (long long)B * Hh * tg->per_bh;
+  *taps = (long long)B * Q * Hh * L * P;
+  return *ntiles < (1LL << 30) && *taps * 4 < (1LL << 31);
+}
+
+extern "C" long long vs_msda_backward_tiled_workspace_bytes(int B, int Hh, int L, int Q, int P,
+                                                            const int64_t* shapes) {
+  if (B <= 0 || Hh <= 0 || L < 1 || L > kMaxLevels || Q < 0 || P <= 0 || !shapes) return -1;
+  TileGeo tg;
+  long long ntiles, taps;
+  if (!tiled_sizes(shapes, B, Hh, L, Q, P, &tg, &ntiles, &taps)) return -1;
+  size_t off[6];
+  tiled_layout(ntiles, taps, off);
+  return (long long)off[5];
+}
+
+extern "C" int vs_msda_backward_tiled(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
+                                      const float* loc, const float* attw, const void* gout, void* gvalue,
+                                      float* gloc, float* gattw, void* workspace, int B, int S, int Hh, int D, int L,
+                                      int Q, int P, void* stream) {
+  VS_CHECK(D == kD, "channels per head must be 32");
+  VS_CHECK(L >= 1 && L <= kMaxLevels, "1..4 levels supported");
+  VS_CHECK(B > 0 && S > 0 && Hh > 0 && Q >= 0 && P > 0, "bad sizes");
+  VS_CHECK(value && gvalue && shapes && starts && workspace, "null pointer");
+  VS_CHECK(Q == 0 || (loc && attw && gout && gloc && gattw), "null pointer");
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  Levels lv;
+  VS_CHECK(fill_levels(&lv, shapes, starts, L, S), "spatial shapes / level starts inconsistent with S");
+  TileGeo tg;
+  long long ntiles, taps;
+  VS_CHECK(tiled_sizes(shapes, B, Hh, L, Q, P, &tg, &ntiles, &taps), "problem too large for the tiled backward");
+  hipStream_t st = (hipStream_t)stream;
+  size_t off[6];
+  tiled_layout(ntiles, taps, off);
+  unsigned char* ws = (unsigned char*)workspace;
+  int* ctr = (int*)(ws + off[0]);
+  int* local = (int*)(ws + off[1]);
+  int* bsum = (int*)(ws + off[2]);
+  int* bprefix = (int*)(ws + off[3]);
+  int* rec = (int*)(ws + off[4]);
+  const int nb = (int)((ntiles + kScanBlock - 1) / kScanBlock);
+  VS_HIP(hipMemsetAsync(ctr, 0, (size_t)ntiles * 4, st));
+  if (taps > 0) {
+    const int tgrid = (int)((taps + 255) / 256);
+    hipLaunchKernelGGL(msda_tile_bucket_kernel<false>, dim3(tgrid), dim3(256), 0, st, loc, ctr, (const int*)nullptr,
+                       (const int*)nullptr, (int*)nullptr, lv, tg, Hh, Q, L, P, taps);
+  }
+  hipLaunchKernelGGL(sort_scan_local_kernel, dim3(nb), dim3(256), 0, st, (const int*)ctr, local, bsum, ntiles);
+  hipLaunchKernelGGL(sort_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, (const int*)bsum, bprefix, nb);
+  if (taps > 0) {
+    VS_HIP(hipMemsetAsync(ctr, 0, (size_t)ntiles * 4, st));
+    const int tgrid = (int)((taps + 255) / 256);
+    hipLaunchKernelGGL(msda_tile_bucket_kernel<true>, dim3(tgrid), dim3(256), 0, st, loc, ctr, (const int*)local,
+                       (const int*)bprefix, rec, lv, tg, Hh, Q, L, P, taps);
+  }
+  const int agrid = (int)((ntiles + 3) / 4);
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(msda_tile_accum_kernel<bf16>, dim3(agrid), dim3(256), 0, st, loc, attw, (const bf16*)gout,
+                       (const int*)local, (const int*)bprefix, (const int*)rec, (bf16*)gvalue, lv, tg, S, Hh, Q, L, P,
+                       (int)ntiles);
+  else
+    hipLaunchKernelGGL(msda_tile_accum_kernel<float>, dim3(agrid), dim3(256), 0, st, loc, attw, (const float*)gout,
+                       (const int*)local, (const int*)bprefix, (const int*)rec, (float*)gvalue, lv, tg, S, Hh, Q, L,
+                       P, (int)ntiles);
   if (Q > 0) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, (long long)B * Q * Hh, st);
   VS_LAUNCH_CHECK();
   return VS_OK;

@@ -30,6 +30,8 @@ SIGNATURES = {
     "vs_msda_backward_encoder": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 6 + [_P],
     "vs_msda_backward_sorted_workspace_bytes": [_c_int] * 6,
     "vs_msda_backward_sorted": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
+    "vs_msda_backward_tiled_workspace_bytes": [_c_int] * 5 + [_P],
+    "vs_msda_backward_tiled": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_window_partition": [_P, _P] + [_c_int] * 7 + [_P],
     "vs_window_reverse": [_P, _P] + [_c_int] * 7 + [_P],
     "vs_window_attn_forward": [_c_int, _P, _P, _P, _P] + [_c_int] * 6 + [_c_float, _P],
@@ -67,7 +69,8 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_segment_clip_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_nchw_workspace_bytes": ctypes.c_longlong,
-            "vs_msda_backward_sorted_workspace_bytes": ctypes.c_longlong}
+            "vs_msda_backward_sorted_workspace_bytes": ctypes.c_longlong,
+            "vs_msda_backward_tiled_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
 

@@ -43,10 +43,12 @@ def _level_arrays(shapes):
     return sh, starts, s
 
 
-# opt-in: grad_value by destination after a counting sort (no float atomics).  Measured
-# slower than the register-carry scatter at 4x1024^2 (count 1.2 + fill 1.4 + pull 0.3 ms vs
-# 1.5 ms): 33M scattered int atomics run at ~27 G/s against the carry's coalesced adds.
-_MSDA_SORTED = os.environ.get("VS_MSDA_SORTED", "0") == "1"
+# MSDA backward variant (A/B switch, VS_MSDA_BWD): "tiled" (default; grad_value by
+# destination tiles with plain LDS read-modify-write, no float atomics, written once in the
+# value dtype), "carry" (register-carry scatter with f32 global atomics, then a cast),
+# "sorted" (per-cell counting sort: 33M scattered int atomics, measured slower).
+_MSDA_BWD = os.environ.get("VS_MSDA_BWD", "tiled")
+_MSDA_SORTED = os.environ.get("VS_MSDA_SORTED", "0") == "1" or _MSDA_BWD == "sorted"
 
 
 class MSDeformAttnFunction(torch.autograd.Function):
@@ -85,6 +87,21 @@ class MSDeformAttnFunction(torch.autograd.Function):
         gl = torch.empty_like(loc)
         ga = torch.empty_like(aw)
         sh, st, _ = _level_arrays(ctx.shapes)
+        if _MSDA_BWD == "tiled" and not _MSDA_SORTED and not ctx.encoder:
+            # grad_value by destination tiles (csrc/msda.hip msda_tile_*): atomic-free,
+            # written once in value's dtype
+            gv = torch.empty_like(value)
+            nbytes = int(L.lib().vs_msda_backward_tiled_workspace_bytes(B, H, Lv, Q, P, sh))
+            if nbytes < 0:
+                raise ValueError("bad sizes for the tiled MSDA backward")
+            ws = torch.empty(nbytes, device=value.device, dtype=torch.uint8)
+            nb = (2 * value.numel() + g.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 8
+            with timed("msda_bwd", value, bytes_=nb, flops=2.0 * aw.numel() * 10 * D):
+                L.check(L.lib().vs_msda_backward_tiled(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc),
+                                                       L.ptr(aw), L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga),
+                                                       L.ptr(ws), B, S, H, D, Lv, Q, P, L.stream(value)),
+                        "msda_backward_tiled")
+            return gv, None, None, gl, ga, None, None
         if _MSDA_SORTED:
             # grad_value by destination after a counting sort (csrc/msda.hip): no float
             # atomics, written once in value's dtype
