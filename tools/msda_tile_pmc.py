@@ -1,6 +1,7 @@
 """Encoder-mode MSDA backward sub-kernels at the C2 shapes (const offsets), few
 iterations: a short program for rocprofv3 --pmc / --kernel-trace passes.
-    python tools/msda_tile_pmc.py [R0] [skip]"""
+    python tools/msda_tile_pmc.py [R0] [skip] [encoder 0/1]
+(VS_MSDA_BWD=tiled|carry|sorted selects the general-path variant when encoder=0)"""
 import os
 import sys
 
@@ -13,6 +14,7 @@ from visionseg import ops  # noqa: E402
 def main():
     r0 = sys.argv[1] if len(sys.argv) > 1 else "5"
     skip = sys.argv[2] if len(sys.argv) > 2 else "6"
+    enc = (sys.argv[3] if len(sys.argv) > 3 else "1") == "1"
     os.environ["VS_MSDA_NEAR_R"], os.environ["VS_MSDA_SKIP"] = r0, skip
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -30,7 +32,7 @@ def main():
     loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
     locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
     for _ in range(4):
-        o = ops.ms_deform_attn(v, shapes, locr, wr, encoder=True)
+        o = ops.ms_deform_attn(v, shapes, locr, wr, encoder=enc)
         o.backward(go)
     torch.cuda.synchronize()
     print("done", flush=True)

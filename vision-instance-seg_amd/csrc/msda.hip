@@ -881,7 +881,11 @@ __global__ void __launch_bounds__(256) msda_tile_bucket_kernel(const float* __re
   }
 }
 
-// one wave per tile (4 tiles per workgroup); grad_value written in the value dtype
+// one wave per tile (4 tiles per workgroup); grad_value written in the value dtype.
+// Records are taken 64 at a time: lane j loads record j's tap (loc, attw) and its
+// grad_out row (64 B of bf16 / 128 B of f32) into LDS, so every global load of the chunk
+// is in flight at once; the accumulation then walks the chunk with the tap geometry read
+// by v_readlane (wave-uniform) and grad_out from LDS.
 template <typename T>
 __global__ void __launch_bounds__(256) msda_tile_accum_kernel(const float* __restrict__ loc,
                                                               const float* __restrict__ attw,
@@ -892,6 +896,7 @@ __global__ void __launch_bounds__(256) msda_tile_accum_kernel(const float* __res
                                                               int ntiles) {
   constexpr int kCells = kTileMaxEdge * (kTileMaxEdge + 1);
   __shared__ __attribute__((aligned(16))) float sAcc[4][kCells * kD];
+  __shared__ __attribute__((aligned(16))) float sG[4][64 * (kD + 1)];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, c = lane & 31;
   const int tile = blockIdx.x * 4 + wave;
   if (tile >= ntiles) return;                      // wave-uniform; no block barriers below
@@ -904,45 +909,59 @@ __global__ void __launch_bounds__(256) msda_tile_accum_kernel(const float* __res
   const int ty0 = (tl / tg.ntx[l]) << sh, tx0 = (tl % tg.ntx[l]) << sh;
   const int Hl = lv.h[l], Wl = lv.w[l];
   float* acc = sAcc[wave];
+  float* sg = sG[wave];
   for (int k = lane; k < te * tp * kD; k += 64) acc[k] = 0.f;
   const int r0 = local[tile] + bprefix[tile / kScanBlock];
   const int r1 = tile + 1 < ntiles ? local[tile + 1] + bprefix[(tile + 1) / kScanBlock]
                                   : bprefix[(ntiles - 1) / kScanBlock + 1];
   const int LP = L * P;
   const long long gbase = (long long)b * Q * Hh + h;    // (b, q=0, h) group index
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  constexpr int U = 4;
-  for (int r = r0; r < r1; r += U) {
-    float2 xy[U];
-    float a[U], g[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = rec[r + u < r1 ? r + u : r];
+  for (int r = r0; r < r1; r += 64) {
+    const int n = min(64, r1 - r);
+    // ---- lane j: record r + j -> tap geometry (registers) and grad_out row (LDS)
+    int h0 = -(1 << 20), w0 = -(1 << 20);
+    float lh = 0.f, lw = 0.f, a = 0.f;
+    if (lane < n) {
+      const int e = rec[r + lane];
       const int q = e / P, p = e - q * P;
       const long long grp = gbase + (long long)q * Hh;
       const long long ti = grp * LP + l * P + p;
-      xy[u] = reinterpret_cast<const float2*>(loc)[ti];
-      a[u] = r + u < r1 ? attw[ti] : 0.f;
-      g[u] = to_f32(gout[grp * kD + c]);
-    }
+      const float2 xy = reinterpret_cast<const float2*>(loc)[ti];
+      a = attw[ti];
+      const Tap t = tap_geom(xy.x, xy.y, Hl, Wl);
+      h0 = t.h0;
+      w0 = t.w0;
+      lh = t.lh;
+      lw = t.lw;
+      const T* grow = gout + grp * kD;
+      constexpr int V = Vec16<T>::N;
+      float gv[kD];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const Tap t = tap_geom(xy[u].x, xy[u].y, Hl, Wl);
-      const int y = t.h0 + half;
-      const int ly = y - ty0, lx = t.w0 - tx0;
-      const float gw = g[u] * a[u] * (half ? t.lh : t.hh);
-      if (r + u < r1 && t.inside && ly >= 0 && ly < te && y < Hl) {
+      for (int k = 0; k < kD; k += V) Vec16<T>::load(grow + k, gv + k);
+#pragma unroll
+      for (int k = 0; k < kD; ++k) sg[lane * (kD + 1) + k] = gv[k] * a;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- walk the chunk: half 0 adds corner row h0, half 1 row h0 + 1 (distinct rows)
+    for (int j = 0; j < n; ++j) {
+      const int jh0 = __builtin_amdgcn_readlane(h0, j), jw0 = __builtin_amdgcn_readlane(w0, j);
+      const float jlh = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lh), j));
+      const float jlw = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lw), j));
+      const int y = jh0 + half;
+      const int ly = y - ty0, lx = jw0 - tx0;
+      if (ly >= 0 && ly < te && y < Hl) {
+        const float gw = sg[j * (kD + 1) + c] * (half ? jlh : 1.f - jlh);
         float* row = acc + (ly * tp) * kD + c;
-        if (lx >= 0 && lx < te && t.w0 >= 0) row[lx * kD] += gw * t.hw;
-        if (lx + 1 >= 0 && lx + 1 < te && t.w0 + 1 < Wl) row[(lx + 1) * kD] += gw * t.lw;
+        if (lx >= 0 && lx < te && jw0 >= 0) row[lx * kD] += gw * (1.f - jlw);
+        if (lx + 1 < te && lx + 1 >= 0 && jw0 + 1 < Wl) row[(lx + 1) * kD] += gw * jlw;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const size_t rowstride = (size_t)Hh * kD;
   T* gb = gvalue + (((size_t)b * S + lv.start[l]) * Hh + h) * kD + c;
   for (int cell = half; cell < te * te; cell += 2) {

@@ -43,11 +43,14 @@ def _level_arrays(shapes):
     return sh, starts, s
 
 
-# MSDA backward variant (A/B switch, VS_MSDA_BWD): "tiled" (default; grad_value by
-# destination tiles with plain LDS read-modify-write, no float atomics, written once in the
-# value dtype), "carry" (register-carry scatter with f32 global atomics, then a cast),
-# "sorted" (per-cell counting sort: 33M scattered int atomics, measured slower).
-_MSDA_BWD = os.environ.get("VS_MSDA_BWD", "tiled")
+# MSDA backward variant (A/B switch, VS_MSDA_BWD): "carry" (default; register-carry scatter
+# with f32 global atomics, then a cast), "tiled" (grad_value by destination tiles with plain
+# LDS read-modify-write, no float atomics, written once in the value dtype), "sorted"
+# (per-cell counting sort).  Both destination variants pay for building the inverse index
+# with integer atomics (~30 G/s on gfx950): at 4x1024^2 (tools/kbench.py --only msda,
+# smooth offsets) carry 2.1 ms, tiled 4.4 ms (count 1.1 + fill 1.6 + accumulate 1.7),
+# sorted 3.1 ms.
+_MSDA_BWD = os.environ.get("VS_MSDA_BWD", "carry")
 _MSDA_SORTED = os.environ.get("VS_MSDA_SORTED", "0") == "1" or _MSDA_BWD == "sorted"
 
 
