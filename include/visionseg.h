@@ -107,8 +107,8 @@ VS_API int vs_msda_backward_sorted(int dtype, const void* value, const int64_t* 
                                    int num_heads, int channels, int num_levels, int num_query, int num_point,
                                    void* stream);
 
-/* Default backward (replaces MSDeformAttnFunction.backward / ms_deform_attn_backward,
- * upstream ms_deform_attn_cuda.cu, behind HF:m2f:798-837): grad_value by destination tiles
+/* Opt-in backward (VS_MSDA_BWD=tiled; replaces ms_deform_attn_backward like the others):
+ * grad_value by destination tiles
  * (image, head, level, te x te cells), each owned by one wave that accumulates its
  * corner contributions with plain LDS read-modify-write -- no float atomics, no memset;
  * grad_value [B, S, H, 32] is written once, in the value dtype.  grad_loc / grad_attn as
@@ -247,6 +247,19 @@ VS_API int vs_lsa_batch(const float* cost, const int* targets_per_image, int num
  * [0, max_targets]): the launch does not depend on the counts, so a captured HIP graph
  * serves every batch whose largest count is <= max_targets (padded targets, see
  * visionseg/criterion.py PaddedTargets). */
+/* Matcher cost matrix for every decoder step at once (HungarianMatcher, HF:m2f:413-481,
+ * replacing its point_sample + pair-wise sigmoid-BCE / dice matmuls + class cost):
+ * mask_logits = host array of num_steps device pointers, each f32 [B, Q, H, W];
+ * class_probs f32 [S, B, Q, C+1] (softmax); target_classes int64 [B, Kc] (padded);
+ * points f32 [B, P, 2] in [-1, 1] (grid_sample order x, y; align_corners=False, zero
+ * padding); target_point_labels f32 [B, Kc, P]  ->  cost f32 [S, B, Q, Kc]
+ * (= wm * BCE + wc * (-prob) + wd * dice, clamped to +-1e10, NaN -> 0).  S <= 16, Kc <= 16. */
+VS_API int vs_match_cost(const float* const* mask_logits, int num_steps, const float* class_probs,
+                         int num_classes_plus1, const long long* target_classes, const float* points,
+                         const float* target_point_labels, float* cost, int batch, int num_queries, int height,
+                         int width, int num_points, int max_targets, float mask_weight, float class_weight,
+                         float dice_weight, void* stream);
+
 VS_API int vs_lsa_batch_device_counts(const float* cost, const int* targets_per_image_dev, int num_steps,
                                       int batch, int num_queries, int max_targets, int* assign, void* stream);
 

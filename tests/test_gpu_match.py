@@ -98,3 +98,28 @@ def test_criterion_device_matcher_equals_scipy_matcher():
     a_host = SetCriterion(cfg, matcher="host").match(masks, torch.stack(classes), ml, cl).cpu()
     assert torch.equal(a_dev, a_host)
     assert abs(out[0][1] - out[1][1]) <= 1e-4 * abs(out[1][1])
+
+
+@pytest.mark.parametrize("Kc", [1, 3, 9])
+def test_match_cost_kernel_vs_torch(Kc):
+    """Fused matcher cost (csrc/match.hip match_cost_kernel) vs the torch formulation of
+    HF:m2f:413-481 on the same points (some outside the map: zero padding)."""
+    import torch.nn.functional as F
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(Kc)
+    S, B, Q, H, W, P = 3, 2, 20, 32, 48, 777
+    masks = [torch.randn(B, Q, H, W, device=DEV, generator=g) * 3 for _ in range(S)]
+    probs = torch.softmax(torch.randn(S, B, Q, 3, device=DEV, generator=g), -1)
+    tcls = torch.randint(0, 3, (B, Kc), device=DEV, generator=g)
+    pts = torch.rand(B, P, 2, device=DEV, generator=g) * 2.2 - 1.1
+    tmask = (torch.rand(B, Kc, 64, 96, device=DEV, generator=g) > 0.5).float()
+    tp = F.grid_sample(tmask, pts.unsqueeze(2), align_corners=False).squeeze(3)
+    got = ops.match_cost(masks, probs, tcls, pts, tp, 5.0, 2.0, 5.0)
+    pp = torch.stack([F.grid_sample(m, pts.unsqueeze(2), align_corners=False).squeeze(3) for m in masks])
+    tpt = tp.transpose(1, 2)[None]
+    cm = torch.matmul(F.softplus(-pp) / P, tpt) + torch.matmul(F.softplus(pp) / P, 1 - tpt)
+    sg = pp.sigmoid()
+    cd = 1 - (2 * torch.matmul(sg, tpt) + 1) / (sg.sum(-1)[..., None] + tp.sum(-1)[None, :, None, :] + 1)
+    cc = -torch.gather(probs, 3, tcls[None, :, None, :].expand(S, B, Q, Kc))
+    exp = 5.0 * cm + 2.0 * cc + 5.0 * cd
+    torch.testing.assert_close(got, exp, atol=3e-5, rtol=1e-5)

@@ -139,6 +139,108 @@ size_t lsa_lds_bytes(int K, int Q) {
   return (((size_t)K * Q * 4 + 7) & ~(size_t)7) + (size_t)(K + 1) * 8 + (size_t)(Q + 1) * (8 + 8 + 4 + 4 + 1);
 }
 
+// ---------------------------------------------------------------------------------
+// Matcher cost matrix (HungarianMatcher, HF:m2f:413-481) for all decoder steps at once.
+// For every (step s, image b, query q) one wave walks the image's P uniform points:
+//   v      = bilinear sample of mask logits[s][b, q] at the point (grid_sample,
+//            align_corners=False, zero padding -- the same arithmetic as ATen's kernel)
+//   A_k   += softplus(-v) t_k + softplus(v) (1 - t_k)      (pair-wise sigmoid BCE, :350-374)
+//   N_k   += sigmoid(v) t_k ;  Ssg += sigmoid(v) ;  T_k += t_k   (dice, :328-347)
+// with t_k = the target point labels [B, Kc, P] (sampled once by the caller), then
+//   cost[s,b,q,k] = wm A_k / P + wc (-prob[s,b,q,cls_k]) + wd (1 - (2 N_k + 1) / (Ssg + T_k + 1))
+// clamped to +-1e10 and NaN -> 0 as the reference.  Replaces S grid_sample launches over
+// the [B, Q, H, W] logit maps (one thread per point looping over the Q channels: 100
+// strided reads per thread) and the pos/neg/sigmoid matmuls with K = P.
+constexpr int kMaxSteps = 16;
+constexpr int kMaxKc = 16;
+
+struct MaskPtrs {
+  const float* p[kMaxSteps];
+};
+
+__device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+template <int KC>
+__global__ void __launch_bounds__(256) match_cost_kernel(MaskPtrs masks, const float* __restrict__ probs, int C1,
+                                                         const long long* __restrict__ tcls,
+                                                         const float* __restrict__ grid, const float* __restrict__ tp,
+                                                         float* __restrict__ cost, int S, int B, int Q, int H, int W,
+                                                         int P, int Kc, float wm, float wc, float wd) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long item = (long long)blockIdx.x * 4 + wave;       // (s, b, q)
+  if (item >= (long long)S * B * Q) return;
+  const int q = (int)(item % Q);
+  const int b = (int)((item / Q) % B);
+  const int s = (int)(item / ((long long)Q * B));
+  const float* map = masks.p[s] + ((size_t)b * Q + q) * H * W;
+  const float* g2 = grid + (size_t)b * P * 2;
+  const float* tb = tp + (size_t)b * Kc * P;
+  float A[KC], N[KC], T[KC], ssg = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) A[k] = N[k] = T[k] = 0.f;
+  for (int p = lane; p < P; p += 64) {
+    const float gx = g2[2 * p], gy = g2[2 * p + 1];
+    // ATen grid_sampler_compute_source_index (zeros padding, align_corners=False)
+    const float ix = ((gx + 1.f) * W - 1.f) / 2.f;
+    const float iy = ((gy + 1.f) * H - 1.f) / 2.f;
+    const float ix_nw = floorf(ix), iy_nw = floorf(iy);
+    const float ix_ne = ix_nw + 1.f, iy_ne = iy_nw;
+    const float ix_sw = ix_nw, iy_sw = iy_nw + 1.f;
+    const float ix_se = ix_nw + 1.f, iy_se = iy_nw + 1.f;
+    const float nw = (ix_se - ix) * (iy_se - iy);
+    const float ne = (ix - ix_sw) * (iy_sw - iy);
+    const float sw = (ix_ne - ix) * (iy - iy_ne);
+    const float se = (ix - ix_nw) * (iy - iy_nw);
+    const int x0 = (int)ix_nw, y0 = (int)iy_nw;
+    float v = 0.f;
+    const bool xin0 = x0 >= 0 && x0 < W, xin1 = x0 + 1 >= 0 && x0 + 1 < W;
+    const bool yin0 = y0 >= 0 && y0 < H, yin1 = y0 + 1 >= 0 && y0 + 1 < H;
+    if (yin0 && xin0) v += map[(size_t)y0 * W + x0] * nw;
+    if (yin0 && xin1) v += map[(size_t)y0 * W + x0 + 1] * ne;
+    if (yin1 && xin0) v += map[(size_t)(y0 + 1) * W + x0] * sw;
+    if (yin1 && xin1) v += map[(size_t)(y0 + 1) * W + x0 + 1] * se;
+    const float pos = softplus_f(-v), neg = softplus_f(v);
+    const float sg = 1.f / (1.f + expf(-v));
+    ssg += sg;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      if (k < Kc) {
+        const float t = tb[(size_t)k * P + p];
+        A[k] += pos * t + neg * (1.f - t);
+        N[k] += sg * t;
+        T[k] += t;
+      }
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    ssg += __shfl_xor(ssg, o, 64);
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      A[k] += __shfl_xor(A[k], o, 64);
+      N[k] += __shfl_xor(N[k], o, 64);
+      T[k] += __shfl_xor(T[k], o, 64);
+    }
+  }
+  if (lane < Kc) {
+    float a = 0.f, n = 0.f, t = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+      if (k == lane) {
+        a = A[k];
+        n = N[k];
+        t = T[k];
+      }
+    const long long cls = tcls[(size_t)b * Kc + lane];
+    const float prob = probs[(((size_t)s * B + b) * Q + q) * C1 + (int)cls];
+    const float cm = a / (float)P;
+    const float cd = 1.f - (2.f * n + 1.f) / (ssg + t + 1.f);
+    float cst = wm * cm + wc * (-prob) + wd * cd;
+    cst = fminf(fmaxf(cst, -1e10f), 1e10f);
+    if (cst != cst) cst = 0.f;
+    cost[(((size_t)s * B + b) * Q + q) * Kc + lane] = cst;
+  }
+}
+
 }  // namespace
 }  // namespace vs
 
@@ -187,6 +289,39 @@ extern "C" int vs_lsa_batch_device_counts(const float* cost, const int* targets_
   ColCounts cc = {};
   hipLaunchKernelGGL(lsa_kernel, dim3(num_steps * batch), dim3(64), lds, (hipStream_t)stream, cost, assign, batch,
                      num_queries, max_targets, cc, targets_per_image_dev);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_match_cost(const float* const* mask_logits, int num_steps, const float* class_probs,
+                             int num_classes_plus1, const long long* target_classes, const float* points,
+                             const float* target_point_labels, float* cost, int batch, int num_queries, int height,
+                             int width, int num_points, int max_targets, float mask_weight, float class_weight,
+                             float dice_weight, void* stream) {
+  VS_CHECK(num_steps >= 1 && num_steps <= kMaxSteps, "1 <= decoder steps <= 16");
+  VS_CHECK(max_targets >= 1 && max_targets <= kMaxKc, "1 <= padded targets <= 16");
+  VS_CHECK(batch > 0 && num_queries > 0 && height > 0 && width > 0 && num_points > 0 && num_classes_plus1 > 0,
+           "bad sizes");
+  VS_CHECK(mask_logits && class_probs && target_classes && points && target_point_labels && cost, "null pointer");
+  MaskPtrs mp = {};
+  for (int s = 0; s < num_steps; ++s) {
+    VS_CHECK(mask_logits[s], "null mask-logit pointer");
+    mp.p[s] = mask_logits[s];
+  }
+  const long long items = (long long)num_steps * batch * num_queries;
+  const int grid = (int)((items + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+#define VS_MC(KC_)                                                                                            \
+  hipLaunchKernelGGL(match_cost_kernel<KC_>, dim3(grid), dim3(256), 0, st, mp, class_probs, num_classes_plus1, \
+                     target_classes, points, target_point_labels, cost, num_steps, batch, num_queries, height,   \
+                     width, num_points, max_targets, mask_weight, class_weight, dice_weight)
+  if (max_targets <= 4)
+    VS_MC(4);
+  else if (max_targets <= 8)
+    VS_MC(8);
+  else
+    VS_MC(16);
+#undef VS_MC
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

@@ -53,6 +53,7 @@ SIGNATURES = {
     "vs_lsa_max_targets": [_c_int],
     "vs_lsa_batch": [_P, _P] + [_c_int] * 4 + [_P, _P],
     "vs_lsa_batch_device_counts": [_P, _P] + [_c_int] * 4 + [_P, _P],
+    "vs_match_cost": [_P, _c_int, _P, _c_int, _P, _P, _P, _P] + [_c_int] * 6 + [_c_float] * 3 + [_P],
     "vs_group_norm_workspace_bytes": [_c_int] * 4,
     "vs_group_norm_forward": [_c_int] + [_P] * 7 + [_c_int] * 4 + [_c_float, _c_int, _P],
     "vs_group_norm_backward": [_c_int] + [_P] * 10 + [_c_int] * 5 + [_P],

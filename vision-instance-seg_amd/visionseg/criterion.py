@@ -26,12 +26,18 @@ in DESIGN.md; the oracle's loss is pinned to HF).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import ops
+
+
+# A/B switch: the fused matcher-cost kernel (default) or the torch formulation below it
+_FUSED_COST = os.environ.get("VS_MATCH_FUSED", "1") == "1"
 
 
 def _sample(feat, coords):
@@ -125,6 +131,13 @@ class SetCriterion:
         # queries / targets are grid_sample CHANNELS (one call per step, one for all targets)
         P = c.train_num_points
         grid = (2.0 * torch.rand(B, P, 2, device=dev) - 1.0).unsqueeze(2)              # [B,P,1,2]
+        if (self.matcher == "device" and dev.type == "cuda" and 1 <= tg.kc <= 16 and S <= 16
+                and Kc <= ops.lsa_max_targets(Q) and _FUSED_COST):
+            # one kernel: point-sampled logits, BCE / dice / class costs (csrc/match.hip)
+            tp = F.grid_sample(tg.masks.float(), grid, align_corners=False).squeeze(3)  # [B,Kc,P]
+            cost = ops.match_cost(masks_list, probs, tg.classes, grid.squeeze(2), tp, c.mask_weight,
+                                  c.class_weight, c.dice_weight)
+            return ops.linear_sum_assignment_padded(cost, tg.counts)
         pp = torch.stack([F.grid_sample(m.float(), grid, align_corners=False).squeeze(3)
                           for m in masks_list])                                          # [S,B,Q,P]
         if tg.kc:

@@ -530,6 +530,30 @@ def linear_sum_assignment_padded(cost, counts):
     return out
 
 
+def match_cost(masks_list, probs, target_classes, points, target_labels, mask_weight, class_weight, dice_weight):
+    """Hungarian-matcher cost for all decoder steps (csrc/match.hip match_cost_kernel).
+    masks_list: S x f32 [B,Q,H,W]; probs f32 [S,B,Q,C+1]; target_classes int64 [B,Kc];
+    points f32 [B,P,2] in [-1,1]; target_labels f32 [B,Kc,P] -> cost f32 [S,B,Q,Kc]."""
+    ms = [m.float().contiguous() for m in masks_list]
+    L.require_hip(*ms, probs, target_classes, points, target_labels)
+    S = len(ms)
+    B, Q, H, W = ms[0].shape
+    pr = probs.float().contiguous()
+    tc = target_classes.to(torch.int64).contiguous()
+    pts = points.float().contiguous()
+    tl = target_labels.float().contiguous()
+    Kc, P = int(tl.shape[1]), int(tl.shape[2])
+    if tuple(pts.shape) != (B, P, 2) or tuple(tc.shape) != (B, Kc) or tuple(pr.shape[:3]) != (S, B, Q):
+        raise ValueError("match_cost: inconsistent shapes")
+    cost = torch.empty(S, B, Q, Kc, device=pr.device, dtype=torch.float32)
+    ptrs = (ctypes.c_void_p * S)(*[m.data_ptr() for m in ms])
+    with timed("match_cost", pr, bytes_=sum(m.numel() for m in ms) * 4):
+        L.check(L.lib().vs_match_cost(ptrs, S, L.ptr(pr), int(pr.shape[3]), L.ptr(tc), L.ptr(pts), L.ptr(tl),
+                                      L.ptr(cost), B, Q, H, W, P, Kc, float(mask_weight), float(class_weight),
+                                      float(dice_weight), L.stream(pr)), "match_cost")
+    return cost
+
+
 # ------------------------------------------------------------------ GroupNorm (channels-last)
 class GroupNormNHWCFunction(torch.autograd.Function):
     """group_norm (+ optional ReLU) of an NCHW tensor stored channels-last, groups of 8
