@@ -16,6 +16,7 @@ kernels library is missing or an input is on the CPU.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
