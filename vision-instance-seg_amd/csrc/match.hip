@@ -160,15 +160,18 @@ struct MaskPtrs {
 
 __device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
 
+// One workgroup per (s, b, q); its 4 waves take contiguous quarters of the points (the
+// caller orders the points by pixel row, so a wave's taps share cache lines and every
+// logit map streams through L2 about once) and combine their sums through LDS.
 template <int KC>
 __global__ void __launch_bounds__(256) match_cost_kernel(MaskPtrs masks, const float* __restrict__ probs, int C1,
                                                          const long long* __restrict__ tcls,
                                                          const float* __restrict__ grid, const float* __restrict__ tp,
                                                          float* __restrict__ cost, int S, int B, int Q, int H, int W,
                                                          int P, int Kc, float wm, float wc, float wd) {
+  __shared__ float red[4][3 * KC + 1];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long long item = (long long)blockIdx.x * 4 + wave;       // (s, b, q)
-  if (item >= (long long)S * B * Q) return;
+  const long long item = blockIdx.x;                              // (s, b, q)
   const int q = (int)(item % Q);
   const int b = (int)((item / Q) % B);
   const int s = (int)(item / ((long long)Q * B));
@@ -178,11 +181,13 @@ __global__ void __launch_bounds__(256) match_cost_kernel(MaskPtrs masks, const f
   float A[KC], N[KC], T[KC], ssg = 0.f;
 #pragma unroll
   for (int k = 0; k < KC; ++k) A[k] = N[k] = T[k] = 0.f;
-  for (int p = lane; p < P; p += 64) {
-    const float gx = g2[2 * p], gy = g2[2 * p + 1];
+  const int per = (P + 3) / 4;
+  const int p0 = wave * per, p1 = min(P, p0 + per);
+  for (int p = p0 + lane; p < p1; p += 64) {
+    const float2 gxy = *reinterpret_cast<const float2*>(g2 + 2 * p);
     // ATen grid_sampler_compute_source_index (zeros padding, align_corners=False)
-    const float ix = ((gx + 1.f) * W - 1.f) / 2.f;
-    const float iy = ((gy + 1.f) * H - 1.f) / 2.f;
+    const float ix = ((gxy.x + 1.f) * W - 1.f) / 2.f;
+    const float iy = ((gxy.y + 1.f) * H - 1.f) / 2.f;
     const float ix_nw = floorf(ix), iy_nw = floorf(iy);
     const float ix_ne = ix_nw + 1.f, iy_ne = iy_nw;
     const float ix_sw = ix_nw, iy_sw = iy_nw + 1.f;
@@ -221,23 +226,30 @@ __global__ void __launch_bounds__(256) match_cost_kernel(MaskPtrs masks, const f
       T[k] += __shfl_xor(T[k], o, 64);
     }
   }
-  if (lane < Kc) {
-    float a = 0.f, n = 0.f, t = 0.f;
+  if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < KC; ++k)
-      if (k == lane) {
-        a = A[k];
-        n = N[k];
-        t = T[k];
-      }
-    const long long cls = tcls[(size_t)b * Kc + lane];
+    for (int k = 0; k < KC; ++k) {
+      red[wave][k] = A[k];
+      red[wave][KC + k] = N[k];
+      red[wave][2 * KC + k] = T[k];
+    }
+    red[wave][3 * KC] = ssg;
+  }
+  __syncthreads();
+  if (threadIdx.x < Kc) {
+    const int k = threadIdx.x;
+    const float a = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+    const float n = (red[0][KC + k] + red[1][KC + k]) + (red[2][KC + k] + red[3][KC + k]);
+    const float t = (red[0][2 * KC + k] + red[1][2 * KC + k]) + (red[2][2 * KC + k] + red[3][2 * KC + k]);
+    const float sgt = (red[0][3 * KC] + red[1][3 * KC]) + (red[2][3 * KC] + red[3][3 * KC]);
+    const long long cls = tcls[(size_t)b * Kc + k];
     const float prob = probs[(((size_t)s * B + b) * Q + q) * C1 + (int)cls];
     const float cm = a / (float)P;
-    const float cd = 1.f - (2.f * n + 1.f) / (ssg + t + 1.f);
+    const float cd = 1.f - (2.f * n + 1.f) / (sgt + t + 1.f);
     float cst = wm * cm + wc * (-prob) + wd * cd;
     cst = fminf(fmaxf(cst, -1e10f), 1e10f);
     if (cst != cst) cst = 0.f;
-    cost[(((size_t)s * B + b) * Q + q) * Kc + lane] = cst;
+    cost[(((size_t)s * B + b) * Q + q) * Kc + k] = cst;
   }
 }
 
@@ -309,7 +321,8 @@ extern "C" int vs_match_cost(const float* const* mask_logits, int num_steps, con
     mp.p[s] = mask_logits[s];
   }
   const long long items = (long long)num_steps * batch * num_queries;
-  const int grid = (int)((items + 3) / 4);
+  VS_CHECK(items < (1LL << 31), "too many (step, image, query) items");
+  const int grid = (int)items;
   hipStream_t st = (hipStream_t)stream;
 #define VS_MC(KC_)                                                                                            \
   hipLaunchKernelGGL(match_cost_kernel<KC_>, dim3(grid), dim3(256), 0, st, mp, class_probs, num_classes_plus1, \

@@ -133,7 +133,12 @@ class SetCriterion:
         grid = (2.0 * torch.rand(B, P, 2, device=dev) - 1.0).unsqueeze(2)              # [B,P,1,2]
         if (self.matcher == "device" and dev.type == "cuda" and 1 <= tg.kc <= 16 and S <= 16
                 and Kc <= ops.lsa_max_targets(Q) and _FUSED_COST):
-            # one kernel: point-sampled logits, BCE / dice / class costs (csrc/match.hip)
+            # one kernel: point-sampled logits, BCE / dice / class costs (csrc/match.hip).
+            # The points are taken in pixel-row order (the cost sums over them): each
+            # wave's taps then share cache lines and a logit map streams through L2 once
+            H, W = masks_list[0].shape[-2:]
+            key = (((grid[..., 0, 1] + 1) * (H / 2)).floor() * W + ((grid[..., 0, 0] + 1) * (W / 2)).floor())
+            grid = torch.gather(grid, 1, key.argsort(dim=1)[:, :, None, None].expand(B, P, 1, 2))
             tp = F.grid_sample(tg.masks.float(), grid, align_corners=False).squeeze(3)  # [B,Kc,P]
             cost = ops.match_cost(masks_list, probs, tg.classes, grid.squeeze(2), tp, c.mask_weight,
                                   c.class_weight, c.dice_weight)
