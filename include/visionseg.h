@@ -211,6 +211,17 @@ VS_API int vs_masked_attn_backward(int dtype, const void* q, const void* k, cons
  * f32 [M]; C a multiple of 8, <= 2048. */
 VS_API int vs_layer_norm_forward(int dtype, const void* x, const void* weight, const void* bias, void* y,
                                  float* mean, float* rstd, int rows, int cols, float eps, void* stream);
+/* Residual add fused into the LayerNorm that follows it (Swin blocks HF:swin:672-684,
+ * pixel-decoder encoder layers HF:m2f:1016-1045): s = x + r rounded to dtype (written),
+ * y = LN(s); replaces the separate torch add + layer_norm.  Same tensors as
+ * vs_layer_norm_forward plus r [M, C] and s [M, C]. */
+VS_API int vs_add_layer_norm_forward(int dtype, const void* x, const void* r, const void* w, const void* b, void* s,
+                                     void* y, float* mean, float* rstd, int M, int C, float eps, void* stream);
+/* vs_layer_norm_backward with dx += dres (the gradient reaching the LayerNorm input
+ * through the residual path; autograd's separate accumulation add). */
+VS_API int vs_layer_norm_backward_add(int dtype, const void* dy, const void* x, const void* w, const float* mean,
+                                      const float* rstd, const void* dres, void* dx, void* dw, void* db, void* ws,
+                                      int M, int C, void* stream);
 VS_API long long vs_layer_norm_backward_workspace_bytes(int rows, int cols);
 /* grad_y [M, C] -> grad_x [M, C], grad_weight / grad_bias [C] (dtype, overwritten). */
 VS_API int vs_layer_norm_backward(int dtype, const void* grad_y, const void* x, const void* weight,

@@ -522,6 +522,40 @@ def test_layer_norm_vs_torch(dtype, M, C):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,C", [(1000, 96), (4099, 192), (2048, 384), (65, 768), (0, 96)])
+@pytest.mark.parametrize("use_s", [True, False])
+def test_add_layer_norm_vs_torch(dtype, M, C, use_s):
+    """Fused residual add + LayerNorm (ops.add_layer_norm, csrc/norm.hip RES / ADD
+    variants): s = x + r (rounded to dtype) and y = LN(s) vs torch f64 on the rounded s;
+    gradients of x and r = LN backward + the gradient of s (when s is used downstream)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(M * 11 + C)
+    x = (torch.randn(M, C, generator=g) * 3 + 0.5).to(dtype)
+    r = torch.randn(M, C, generator=g).to(dtype)
+    w = (1 + 0.1 * torch.randn(C, generator=g)).to(dtype)
+    b = (0.1 * torch.randn(C, generator=g)).to(dtype)
+    gy = torch.randn(M, C, generator=g).to(dtype)
+    gs = torch.randn(M, C, generator=g).to(dtype)
+    s_ref = (x.float() + r.float()).to(dtype)
+    sr, wr, br = (t.double().requires_grad_(True) for t in (s_ref, w, b))
+    yr = torch.nn.functional.layer_norm(sr, (C,), wr, br, 1e-5)
+    yr.backward(gy.double())
+    gx_exp = sr.grad + (gs.double() if use_s else 0)
+    xd, rd, wd, bd = (t.to(DEV).requires_grad_(True) for t in (x, r, w, b))
+    s, y = ops.add_layer_norm(xd, rd, wd, bd, 1e-5)
+    assert torch.equal(s.detach().cpu(), s_ref)
+    loss = (y * gy.to(DEV)).sum() + ((s * gs.to(DEV)).sum() if use_s else 0)
+    loss.backward()
+    tol = 2e-5 if dtype == torch.float32 else 2 ** -7
+    for got, exp in ((y, yr), (xd.grad, gx_exp), (rd.grad, gx_exp)):
+        err = (got.detach().double().cpu() - exp.detach()).abs()
+        assert float(err.max() if err.numel() else 0) <= tol * max(1.0, float(exp.detach().abs().max() if exp.numel() else 1))
+    for got, exp in ((wd.grad, wr.grad), (bd.grad, br.grad)):
+        err = float((got.double().cpu() - exp).abs().max())
+        assert err <= (1e-4 if dtype == torch.float32 else 2 ** -7) * max(1.0, float(exp.abs().max())), err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N", [(262144, 96), (86016, 256), (5, 384), (0, 64), (1023, 2048)])
 def test_column_sum_vs_torch(dtype, M, N):
     ops = _ops()

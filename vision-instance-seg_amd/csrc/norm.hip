@@ -45,11 +45,15 @@ __device__ __forceinline__ void store_chunk(T* p, const float* v) {
 }
 
 // chunk = 8 elements (one 16-B load for bf16, two for f32); C % 8 == 0
-template <typename T, int K>
+// RES: y = LN(s) with s = x + r rounded to T (the residual add of a pre-/post-norm block,
+// written to s_out): one pass instead of an add kernel plus a LayerNorm.
+template <typename T, int K, bool RES = false>
 __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                           const T* __restrict__ b, T* __restrict__ y,
                                                           float* __restrict__ mean, float* __restrict__ rstd,
-                                                          int M, int C, float eps, int G) {
+                                                          int M, int C, float eps, int G,
+                                                          const T* __restrict__ r = nullptr,
+                                                          T* __restrict__ s_out = nullptr) {
   const int nch = C >> 3;
   const int lane = threadIdx.x & (G - 1);
   const int rows_per_block = kThreads / G;
@@ -64,6 +68,13 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ 
       const int j = lane + k * G;
       if (j < nch) {
         load_chunk(xr + j * 8, v[k]);
+        if constexpr (RES) {
+          float rv[8];
+          load_chunk(r + row * C + j * 8, rv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[k][i] = to_f32(from_f32<T>(v[k][i] + rv[i]));
+          store_chunk(s_out + row * C + j * 8, v[k]);
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) s += v[k][i];
       }
@@ -102,11 +113,14 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ 
 }
 
 // dx, plus per-workgroup partial dw / db rows (f32) in part[blockIdx][2][C]
-template <typename T, int K>
+// ADD: dx += dres (the gradient reaching the LayerNorm input through the residual path),
+// accumulated in f32 and rounded once.
+template <typename T, int K, bool ADD = false>
 __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const T* __restrict__ w, const float* __restrict__ mean,
                                                           const float* __restrict__ rstd, T* __restrict__ dx,
-                                                          float* __restrict__ part, int M, int C, int G) {
+                                                          float* __restrict__ part, int M, int C, int G,
+                                                          const T* __restrict__ dres = nullptr) {
   extern __shared__ float red[];             // [groups][2][C]
   const int nch = C >> 3;
   const int lane = threadIdx.x & (G - 1);
@@ -172,6 +186,12 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
             float o[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) o[i] = rs[u] * (dv[u][k][i] - s1 - xv[u][k][i] * s2);
+            if constexpr (ADD) {
+              float rv[8];
+              load_chunk(dres + row * C + j * 8, rv);
+#pragma unroll
+              for (int i = 0; i < 8; ++i) o[i] += rv[i];
+            }
             store_chunk(dx + row * C + j * 8, o);
           }
         }
@@ -368,13 +388,56 @@ extern "C" int vs_layer_norm_forward(int dtype, const void* x, const void* w, co
   return VS_OK;
 }
 
+extern "C" int vs_add_layer_norm_forward(int dtype, const void* x, const void* r, const void* w, const void* b,
+                                         void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
+                                         void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
+  VS_CHECK(w && b && (M == 0 || (x && r && s && y && mean && rstd)), "null pointer");
+  int G, K;
+  VS_CHECK(pick_gk(C / 8, ln_kmax(dtype), &G, &K), "row too long for the LayerNorm kernel (C <= 2048)");
+  if (M == 0) return VS_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = blocks_for(M, kThreads / G, 256 * 32);
+#define VS_ALNF(KK)                                                                                           \
+  if (dtype == VS_BF16)                                                                                       \
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, true>), dim3(grid), dim3(kThreads), 0, st, (const bf16*)x,    \
+                       (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G, (const bf16*)r,    \
+                       (bf16*)s);                                                                             \
+  else                                                                                                        \
+    hipLaunchKernelGGL((ln_fwd_kernel<float, KK, true>), dim3(grid), dim3(kThreads), 0, st, (const float*)x,  \
+                       (const float*)w, (const float*)b, (float*)y, mean, rstd, M, C, eps, G, (const float*)r, \
+                       (float*)s)
+  VS_LN_K(K, VS_ALNF)
+#undef VS_ALNF
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
 extern "C" long long vs_layer_norm_backward_workspace_bytes(int M, int C) {
   return (long long)kMaxPartials * 2 * C * sizeof(float);
 }
 
+static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, const void* w, const float* mean,
+                                    const float* rstd, const void* dres, void* dx, void* dw, void* db, void* ws, int M,
+                                    int C, void* stream);
+
 extern "C" int vs_layer_norm_backward(int dtype, const void* dy, const void* x, const void* w, const float* mean,
                                       const float* rstd, void* dx, void* dw, void* db, void* ws, int M, int C,
                                       void* stream) {
+  return layer_norm_backward_impl(dtype, dy, x, w, mean, rstd, nullptr, dx, dw, db, ws, M, C, stream);
+}
+
+extern "C" int vs_layer_norm_backward_add(int dtype, const void* dy, const void* x, const void* w, const float* mean,
+                                          const float* rstd, const void* dres, void* dx, void* dw, void* db, void* ws,
+                                          int M, int C, void* stream) {
+  VS_CHECK(M == 0 || dres, "null pointer");
+  return layer_norm_backward_impl(dtype, dy, x, w, mean, rstd, dres, dx, dw, db, ws, M, C, stream);
+}
+
+static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, const void* w, const float* mean,
+                                    const float* rstd, const void* dres, void* dx, void* dw, void* db, void* ws, int M,
+                                    int C, void* stream) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && dw && db && ws && (M == 0 || (dy && x && mean && rstd && dx)), "null pointer");
@@ -386,12 +449,19 @@ extern "C" int vs_layer_norm_backward(int dtype, const void* dy, const void* x, 
   const size_t lds = (size_t)(kThreads / G) * 2 * C * sizeof(float);
   VS_CHECK(lds <= 64 * 1024, "LayerNorm backward LDS budget exceeded");
 #define VS_LNB(KK)                                                                                            \
-  if (dtype == VS_BF16)                                                                                       \
+  if (dtype == VS_BF16 && dres)                                                                               \
+    hipLaunchKernelGGL((ln_bwd_kernel<bf16, KK, true>), dim3(grid), dim3(kThreads), lds, st, (const bf16*)dy, \
+                       (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, C, G, (const bf16*)dres); \
+  else if (dtype == VS_BF16)                                                                                  \
     hipLaunchKernelGGL((ln_bwd_kernel<bf16, KK>), dim3(grid), dim3(kThreads), lds, st, (const bf16*)dy,       \
-                       (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, C, G);                 \
+                       (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, C, G, nullptr);        \
+  else if (dres)                                                                                              \
+    hipLaunchKernelGGL((ln_bwd_kernel<float, KK, true>), dim3(grid), dim3(kThreads), lds, st,                 \
+                       (const float*)dy, (const float*)x, (const float*)w, mean, rstd, (float*)dx, part, M, C, \
+                       G, (const float*)dres);                                                                \
   else                                                                                                        \
     hipLaunchKernelGGL((ln_bwd_kernel<float, KK>), dim3(grid), dim3(kThreads), lds, st, (const float*)dy,     \
-                       (const float*)x, (const float*)w, mean, rstd, (float*)dx, part, M, C, G)
+                       (const float*)x, (const float*)w, mean, rstd, (float*)dx, part, M, C, G, nullptr)
   VS_LN_K(K, VS_LNB)
 #undef VS_LNB
   // dw = column sums of the partial rows' first halves, db of the second halves

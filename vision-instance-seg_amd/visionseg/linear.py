@@ -214,6 +214,15 @@ class TokenLayerNorm(nn.LayerNorm):
             return ops.layer_norm(x, self.weight, self.bias, self.eps)
         return F.layer_norm(x, self.normalized_shape, self.weight, self.bias, self.eps)
 
+    def add_forward(self, x, r):
+        """(x + r, LN(x + r)): the residual add fused into the norm on the HIP kernel
+        (ops.add_layer_norm) where the plain norm would run there too."""
+        if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
+                and r.shape == x.shape and r.dtype == x.dtype and not torch.is_autocast_enabled():
+            return ops.add_layer_norm(x, r, self.weight, self.bias, self.eps)
+        s = x + r
+        return s, self(s)
+
 
 def linear_tokens(x, w, b=None):
     """F.linear with the split-K weight gradient when x carries many tokens."""

@@ -128,18 +128,25 @@ class SwinBlock(nn.Module):
         self.norm2 = TokenLayerNorm(dim)
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
 
-    def forward(self, x, H, W):
+    def forward(self, x, H, W, res=None):
+        """x: residual stream; res: the previous block's pending MLP branch (added to x
+        inside this block's first LayerNorm).  Returns (stream, pending MLP branch): the
+        caller adds the branch in the next norm (ops.add_layer_norm)."""
         B, L, C = x.shape
         ws, shift = self.ws, self.shift
-        h = self.norm1(x).view(B, H, W, C)
+        if res is None:
+            h = self.norm1(x)
+        else:
+            x, h = self.norm1.add_forward(x, res)
+        h = h.view(B, H, W, C)
         win = ops.window_partition(h.to(_compute_dtype(h)), ws, shift)   # cast first: half the bytes moved
         qkv = self.attn.qkv(win)
         o = ops.window_attention(qkv, self.attn.rel_table, self.attn.heads, ws, shift,
                                  _padded(H, ws) // ws, _padded(W, ws) // ws)
         o = ops.window_reverse(o, B, H, W, ws, shift)                 # per-token proj commutes with crop
         o = self.attn.proj(o.view(B, H * W, C))
-        x = x + o
-        return x + self.mlp(self.norm2(x))
+        x, h2 = self.norm2.add_forward(x, o)
+        return x, self.mlp(h2)
 
 
 class PatchMerging(nn.Module):
@@ -196,9 +203,10 @@ class SwinBackbone(nn.Module):
         x = self.patch_embed.norm(x.flatten(2).transpose(1, 2))
         feats = []
         for i, st in enumerate(self.stages):
+            res = None
             for blk in st.blocks:
-                x = blk(x, H, W)
-            f = self.out_norms[i](x)
+                x, res = blk(x, H, W, res)
+            x, f = self.out_norms[i].add_forward(x, res)     # stream + last MLP branch, stage norm
             feats.append(f.view(B, H, W, -1).permute(0, 3, 1, 2))     # NCHW view, channels-last memory
             if st.merge is not None:
                 x = st.merge(x, H, W)
@@ -273,8 +281,9 @@ class EncoderLayer(nn.Module):
         self.norm2 = TokenLayerNorm(d)
 
     def forward(self, h, pos, ref, shapes, norm):
-        h = self.norm1(h + self.attn(h, pos, ref, shapes, norm))
-        return self.norm2(h + self.fc2(F.relu(self.fc1(h))))
+        _, h = self.norm1.add_forward(h, self.attn(h, pos, ref, shapes, norm))     # post-norm, fused add
+        _, h = self.norm2.add_forward(h, self.fc2(F.relu(self.fc1(h))))
+        return h
 
 
 _TORCH_GN = os.environ.get("VS_TORCH_GROUPNORM", "0") == "1"     # A/B switch

@@ -426,6 +426,59 @@ class LayerNormFunction(torch.autograd.Function):
         return gx, gw, gb, None
 
 
+class AddLayerNormFunction(torch.autograd.Function):
+    """(s, y) = (x + r, layer_norm(x + r)) in one pass (csrc/norm.hip, RES variant); the
+    backward adds the gradient of s (residual path) inside the LayerNorm backward."""
+
+    @staticmethod
+    def forward(ctx, x, r, weight, bias, eps):
+        L.require_hip(x, r, weight, bias)
+        C = x.shape[-1]
+        xc, rc = x.contiguous(), r.to(x.dtype).contiguous()
+        M = xc.numel() // C
+        s = torch.empty_like(xc)
+        y = torch.empty_like(xc)
+        mean = torch.empty(M, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(M, device=x.device, dtype=torch.float32)
+        with timed("add_layer_norm_fwd", xc, bytes_=4 * xc.numel() * xc.element_size()):
+            L.check(L.lib().vs_add_layer_norm_forward(L.dtype_code(xc), L.ptr(xc), L.ptr(rc), L.ptr(weight),
+                                                      L.ptr(bias), L.ptr(s), L.ptr(y), L.ptr(mean), L.ptr(rstd), M,
+                                                      C, float(eps), L.stream(xc)), "add_layer_norm_forward")
+        ctx.save_for_backward(s, weight, mean, rstd)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, gs, gy):
+        s, weight, mean, rstd = ctx.saved_tensors
+        C = s.shape[-1]
+        M = s.numel() // C
+        if gy is None:
+            gy = torch.zeros_like(s)
+        gy = gy.to(s.dtype).contiguous()
+        gx = torch.empty_like(s)
+        gw = torch.empty_like(weight)
+        gb = torch.empty_like(weight)
+        ws = torch.empty(int(L.lib().vs_layer_norm_backward_workspace_bytes(M, C)), device=s.device,
+                         dtype=torch.uint8)
+        with timed("layer_norm_bwd", s, bytes_=(3 + (gs is not None)) * s.numel() * s.element_size()):
+            if gs is None:
+                L.check(L.lib().vs_layer_norm_backward(L.dtype_code(s), L.ptr(gy), L.ptr(s), L.ptr(weight),
+                                                       L.ptr(mean), L.ptr(rstd), L.ptr(gx), L.ptr(gw), L.ptr(gb),
+                                                       L.ptr(ws), M, C, L.stream(s)), "layer_norm_backward")
+            else:
+                gsc = gs.to(s.dtype).contiguous()
+                L.check(L.lib().vs_layer_norm_backward_add(L.dtype_code(s), L.ptr(gy), L.ptr(s), L.ptr(weight),
+                                                           L.ptr(mean), L.ptr(rstd), L.ptr(gsc), L.ptr(gx),
+                                                           L.ptr(gw), L.ptr(gb), L.ptr(ws), M, C, L.stream(s)),
+                        "layer_norm_backward_add")
+        return gx, gx, gw, gb, None
+
+
+def add_layer_norm(x, r, weight, bias, eps: float = 1e-5):
+    """(x + r, layer_norm(x + r)) for token-major [..., C] tensors (see AddLayerNormFunction)."""
+    return AddLayerNormFunction.apply(x, r, weight, bias, eps)
+
+
 def layer_norm(x, weight, bias, eps: float = 1e-5):
     return LayerNormFunction.apply(x, weight, bias, eps)
 
