@@ -292,6 +292,27 @@ __global__ void __launch_bounds__(256) win_attn_bwd_kernel(
 // registers.  Backward: dP^T = V dO^T (same layout), dV = P^T dO and dK = dS^T Q through
 // one LDS copy of P^T / dS^T, dQ^T = K^T dS^T again straight from registers; the bias
 // gradient is binned per window in LDS (as the scalar path).
+// Relative-position bias gradient of one (window, head) from its dS^T tile in LDS
+// ([key][query] bf16, row pitch `pitch`): bin t = (dy, dx) gets the sum of dS over the
+// pairs with ty_q - ty_k = dy, tx_q - tx_k = dx (HF:swin:350-365 index), each bin
+// summed by one thread in a fixed order (deterministic).  Threads `tid` of `nthreads`.
+__device__ __forceinline__ void bias_grad_bins(const short* dst, int pitch, const WinGeom& g, int tid, int nthreads,
+                                               float* out) {
+  const int ws = g.ws, tw = 2 * ws - 1;
+  for (int t = tid; t < g.T2; t += nthreads) {
+    const int dy = t / tw - (ws - 1), dx = t % tw - (ws - 1);
+    const int qy0 = dy > 0 ? dy : 0, qy1 = dy < 0 ? ws + dy : ws;
+    const int qx0 = dx > 0 ? dx : 0, qx1 = dx < 0 ? ws + dx : ws;
+    float acc = 0.f;
+    for (int qy = qy0; qy < qy1; ++qy)
+      for (int qx = qx0; qx < qx1; ++qx) {
+        const int q = qy * ws + qx, k = (qy - dy) * ws + (qx - dx);
+        acc += bf16_bits_to_f32((unsigned short)dst[k * pitch + q]);
+      }
+    out[t] = acc;
+  }
+}
+
 constexpr int kMaxT2 = 225;       // (2*8-1)^2
 constexpr int kPadK = 72;         // LDS row pitch (shorts) of the 64-token operands
 
@@ -450,7 +471,6 @@ __global__ void __launch_bounds__(64 * kBwdWaves) win_attn_bwd_mfma(
   __shared__ __attribute__((aligned(16))) short sQT[kBwdWaves][32 * kPadK];   // Q^T [d][q]
   __shared__ __attribute__((aligned(16))) short sKT[kBwdWaves][32 * kPadK];   // K^T [d][key]
   __shared__ float sBias[kBwdWaves][kMaxT2];
-  __shared__ float sBins[kBwdWaves][kMaxT2];
   __shared__ int sTok[kBwdWaves][64];
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int item = blockIdx.x * kBwdWaves + wave;
@@ -464,13 +484,9 @@ __global__ void __launch_bounds__(64 * kBwdWaves) win_attn_bwd_mfma(
   short* qt_ = sQT[wave];
   short* kt_ = sKT[wave];
   float* bias = sBias[wave];
-  float* bins = sBins[wave];
   int* tok = sTok[wave];
   window_tokens(g, bw, l, tok);
-  for (int t = l; t < g.T2; t += 64) {
-    bias[t] = table[t * g.heads + h];
-    bins[t] = 0.f;
-  }
+  for (int t = l; t < g.T2; t += 64) bias[t] = table[t * g.heads + h];
   {  // transposed copies, lane = token
     const int t = l;
     const bf16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -574,24 +590,15 @@ __global__ void __launch_bounds__(64 * kBwdWaves) win_attn_bwd_mfma(
       const int key = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh;
       if (key < N) gw[(size_t)key * C3 + 2 * C + r] = __float2bfloat16(dv[kt][i]);
     }
-  // dS^T = P^T (dP^T - D_q); bias-gradient bins
-  const int tw = 2 * g.ws - 1;
+  // dS^T = P^T (dP^T - D_q)
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    const int q = 32 * qt + r;
-    const int tq = tok[q];
-    const int tyq = tq & 255, txq = (tq >> 8) & 255;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int key = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh;
         const float ds = sacc[kt][qt][i] * (dacc[kt][qt][i] - Dq[qt]);
         dacc[kt][qt][i] = ds;
-        if (key < N && q < N) {
-          const int tk = tok[key];
-          atomicAdd(&bins[(tyq - (tk & 255) + g.ws - 1) * tw + (txq - ((tk >> 8) & 255) + g.ws - 1)], ds);
-        }
       }
   }
   wave_sync();                                // every lane has read P^T for dV
@@ -654,8 +661,9 @@ __global__ void __launch_bounds__(64 * kBwdWaves) win_attn_bwd_mfma(
     }
   }
   wave_sync();
-  float* gp = gtable_part + ((size_t)bw * g.heads + h) * g.T2;
-  for (int t = l; t < g.T2; t += 64) gp[t] = bins[t];
+  // bias gradient: bin (dy, dx) sums dS over the query/key pairs at that offset, read
+  // back from the dS^T tile (no LDS float atomics: ~0.33 lane-ops/clk/CU on gfx950)
+  bias_grad_bins(pt, kPadK, g, l, 64, gtable_part + ((size_t)bw * g.heads + h) * g.T2);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -786,7 +794,6 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
   __shared__ __attribute__((aligned(16))) short sKT[32 * PT];  // K^T [d][key]
   __shared__ __attribute__((aligned(16))) short sDoT[32 * PT]; // dO^T [d][q]
   __shared__ float sBias[kMaxT2Big];
-  __shared__ float sBins[kMaxT2Big];
   __shared__ int sTok[NP];
   short* sK = sU;
   short* sV = sU + kNat;
@@ -797,10 +804,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
   const bf16* win = qkv + (size_t)bw * N * C3;
   const bf16* gwin_o = gout + (size_t)bw * N * C + h * kD;
   window_tokens_blk<NT>(g, bw, sTok);
-  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) {
-    sBias[t] = table[t * g.heads + h];
-    sBins[t] = 0.f;
-  }
+  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
   for (int p = threadIdx.x; p < NP * 4; p += blockDim.x) {
     const int t = p >> 2, c = p & 3;
     bf16x8_t q = zero8(), k = zero8(), v = zero8(), d = zero8();
@@ -858,9 +862,6 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
       dacc[kt] = mfma16(*reinterpret_cast<const bf16x8_t*>(sV + o), db[st], dacc[kt]);
     }
   __syncthreads();                            // K / V staging is overwritten by P^T below
-  const int tw = 2 * g.ws - 1;
-  const int tq = sTok[q];
-  const int tyq = tq & 255, txq = (tq >> 8) & 255;
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
     logits_tile(sacc[kt], g, sTok, sBias, kt, qt, r, hh);
@@ -869,12 +870,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
       const int key = 32 * kt + crow(i, hh);
       const float p = q < N ? __expf(sacc[kt][i] - Lq) : 0.f;
       sT[key * PT + q] = bf16_bits(p);
-      const float ds = p * (dacc[kt][i] - Dq);
-      dacc[kt][i] = ds;
-      if (key < N && q < N) {
-        const int tk = sTok[key];
-        atomicAdd(&sBins[(tyq - (tk & 255) + g.ws - 1) * tw + (txq - ((tk >> 8) & 255) + g.ws - 1)], ds);
-      }
+      dacc[kt][i] = p * (dacc[kt][i] - Dq);
     }
   }
   __syncthreads();
@@ -939,9 +935,8 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
       }
     }
   }
-  __syncthreads();
-  float* gp = gtable_part + ((size_t)bw * g.heads + h) * g.T2;
-  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) gp[t] = sBins[t];
+  __syncthreads();                            // (sT still holds dS^T)
+  bias_grad_bins(sT, PT, g, threadIdx.x, blockDim.x, gtable_part + ((size_t)bw * g.heads + h) * g.T2);
 }
 
 int check_geom(WinGeom& g, int Bw, int heads, int ws, int shift, int nWh, int nWw, float scale) {
