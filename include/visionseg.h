@@ -176,6 +176,12 @@ VS_API int vs_mask_head_backward(int dtype, const float* grad_logits, const void
                                  const void* pixel_embed_nhwc, void* grad_mask_embed,
                                  void* grad_pixel_embed, void* workspace, int batch, int num_query,
                                  int channels, int height, int width, void* stream);
+/* vs_mask_head_backward with accumulate_grad_P != 0: grad_P += dL^T.E (bf16, in place),
+ * so the decoder's mask-head calls sum their pixel-embedding gradient into one buffer
+ * (replaces autograd's accumulation of one [B, HW, C] gradient per call). */
+VS_API int vs_mask_head_backward_ex(int dtype, const float* grad_logits, const void* E, const void* P, void* grad_E,
+                                    void* grad_P, void* workspace, int batch, int num_queries, int channels,
+                                    int height, int width, int accumulate_grad_P, void* stream);
 
 /* Attention bitmask of the next decoder layer (HF:m2f:2049-2055 + row fix 1912-1914):
  * bilinear (align_corners=False) resize of each logits row [H, W] to [th, tw], key k

@@ -185,6 +185,33 @@ def test_window_attention_bf16_vs_oracle():
 
 
 # ------------------------------------------------------------------ mask head + bitmask
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_mask_head_grad_sink_sums_calls(dtype):
+    """Several mask-head calls sharing one pixel embedding through ops.GradSink: the
+    embedding gradient (accumulated in place by the backward kernel) equals autograd's sum
+    of the per-call gradients; the mask-embedding gradients are unchanged."""
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(0)
+    B, Q, C, H, W, calls = 2, 100, 256, 32, 48, 4
+    P = (torch.randn(B, H * W, C, device=DEV, generator=g)).to(dtype)
+    Es = [torch.randn(B, Q, C, device=DEV, generator=g).to(dtype) for _ in range(calls)]
+    gls = [torch.randn(B, Q, H, W, device=DEV, generator=g) for _ in range(calls)]
+    outs = []
+    for use_sink in (False, True):
+        p = P.clone().requires_grad_(True)
+        es = [e.clone().requires_grad_(True) for e in Es]
+        sink = ops.GradSink() if use_sink else None
+        src = sink.source(p) if use_sink else p
+        loss = sum((ops.mask_head(e, src, H, W, sink=sink) * gl).sum() for e, gl in zip(es, gls))
+        loss.backward()
+        outs.append((p.grad.float(), [e.grad.float() for e in es]))
+    (pa, ea), (pb, eb) = outs
+    tol = 1e-5 if dtype == torch.float32 else 2 ** -6
+    assert float((pa - pb).abs().max()) <= tol * float(pa.abs().max())
+    for x, y in zip(ea, eb):
+        assert torch.equal(x, y)
+
+
 def test_mask_head_golden(golden):
     """MLP on host-side torch, einsum + mask on the kernels vs the HF predictor fixture."""
     ops = _ops()

@@ -225,7 +225,9 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return (uint32_t)(*reinterpret_cast<const uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<const uint16_t*>(&y)) << 16);
 }
 
-template <int CT, int TN>  // c-tiles (of 32) per wave (C = 128 * CT); pixels per tile (32 or 64)
+// ACC: dP += (the pixel-embedding gradient summed over the decoder's mask-head calls in
+// place, instead of autograd adding 10 [B, HW, C] tensors)
+template <int CT, int TN, bool ACC = false>  // c-tiles (of 32) per wave (C = 128 * CT); pixels per tile (32 or 64)
 __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restrict__ gL, const bf16* __restrict__ E,
                                                             const bf16* __restrict__ P, bf16* __restrict__ dP,
                                                             float* __restrict__ dEpart, int Q, int N) {
@@ -365,9 +367,18 @@ __global__ void __launch_bounds__(256) mask_head_bwd_kernel(const float* __restr
           for (int u = 0; u < CT; ++u)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
+              float a0 = acc[u][m][4 * g], a1 = acc[u][m][4 * g + 1], a2 = acc[u][m][4 * g + 2],
+                    a3 = acc[u][m][4 * g + 3];
+              if constexpr (ACC) {
+                const uint2 o = *reinterpret_cast<const uint2*>(dst + 32 * u + 8 * g);
+                a0 += __uint_as_float(o.x << 16);
+                a1 += __uint_as_float(o.x & 0xffff0000u);
+                a2 += __uint_as_float(o.y << 16);
+                a3 += __uint_as_float(o.y & 0xffff0000u);
+              }
               uint2 w;
-              w.x = pack_bf16x2(acc[u][m][4 * g], acc[u][m][4 * g + 1]);
-              w.y = pack_bf16x2(acc[u][m][4 * g + 2], acc[u][m][4 * g + 3]);
+              w.x = pack_bf16x2(a0, a1);
+              w.y = pack_bf16x2(a2, a3);
               *reinterpret_cast<uint2*>(dst + 32 * u + 8 * g) = w;
             }
         }
@@ -560,9 +571,26 @@ extern "C" long long vs_mask_head_backward_workspace_bytes(int B, int Q, int C) 
   return (long long)mask_head_bwd_parts(B) * B * Q * C * 4;
 }
 
+static int mask_head_backward_impl(int dtype, const float* grad_logits, const void* E, const void* P, void* grad_E,
+                                   void* grad_P, void* workspace, int B, int Q, int C, int H, int W, bool acc,
+                                   void* stream);
+
 extern "C" int vs_mask_head_backward(int dtype, const float* grad_logits, const void* E, const void* P, void* grad_E,
                                      void* grad_P, void* workspace, int B, int Q, int C, int H, int W,
                                      void* stream) {
+  return mask_head_backward_impl(dtype, grad_logits, E, P, grad_E, grad_P, workspace, B, Q, C, H, W, false, stream);
+}
+
+extern "C" int vs_mask_head_backward_ex(int dtype, const float* grad_logits, const void* E, const void* P,
+                                        void* grad_E, void* grad_P, void* workspace, int B, int Q, int C, int H, int W,
+                                        int accumulate_grad_P, void* stream) {
+  return mask_head_backward_impl(dtype, grad_logits, E, P, grad_E, grad_P, workspace, B, Q, C, H, W,
+                                 accumulate_grad_P != 0, stream);
+}
+
+static int mask_head_backward_impl(int dtype, const float* grad_logits, const void* E, const void* P, void* grad_E,
+                                   void* grad_P, void* workspace, int B, int Q, int C, int H, int W, bool acc,
+                                   void* stream) {
   VS_CHECK(grad_logits && E && P && grad_E && grad_P && workspace, "null pointer");
   VS_CHECK(dtype == VS_BF16, "the fused mask-head backward is the bf16 path (f32 parity mode uses vendor GEMMs)");
   VS_CHECK(B > 0 && Q > 0 && Q <= 128 && H > 0 && W > 0, "need 0 < Q <= 128");
@@ -576,13 +604,18 @@ extern "C" int vs_mask_head_backward(int dtype, const float* grad_logits, const 
   const size_t lds = ((size_t)128 * (C + 32) + 128 * 96 + (size_t)TN * (C + 32)) * 2;
   float* part = (float*)workspace;
   if (gx < parts) VS_HIP(hipMemsetAsync(part + (size_t)gx * B * Q * C, 0, (size_t)(parts - gx) * B * Q * C * 4, st));
-  if (C == 256) {
-    hipLaunchKernelGGL((mask_head_bwd_kernel<2, TN>), dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
-                       (const bf16*)P, (bf16*)grad_P, part, Q, N);
-  } else {
-    hipLaunchKernelGGL((mask_head_bwd_kernel<1, TN>), dim3(gx, B), dim3(256), lds, st, grad_logits, (const bf16*)E,
-                       (const bf16*)P, (bf16*)grad_P, part, Q, N);
-  }
+#define VS_MHB(CT_, ACC_)                                                                                 \
+  hipLaunchKernelGGL((mask_head_bwd_kernel<CT_, TN, ACC_>), dim3(gx, B), dim3(256), lds, st, grad_logits, \
+                     (const bf16*)E, (const bf16*)P, (bf16*)grad_P, part, Q, N)
+  if (C == 256 && acc)
+    VS_MHB(2, true);
+  else if (C == 256)
+    VS_MHB(2, false);
+  else if (acc)
+    VS_MHB(1, true);
+  else
+    VS_MHB(1, false);
+#undef VS_MHB
   VS_LAUNCH_CHECK();
   const long long per = (long long)B * Q * C;
   hipLaunchKernelGGL(mask_head_bwd_reduce, dim3((int)((per / 4 + 255) / 256)), dim3(256), 0, st, part, (bf16*)grad_E,

@@ -24,7 +24,7 @@ namespace vs {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kMaxPartials = 512;    // workgroups of a backward / column-sum sweep
+constexpr int kMaxPartials = 2048;   // workgroups of a backward / column-sum sweep
 
 // lanes of one group: shuffle-reduce within G lanes (G a power of two, <= 64)
 __device__ __forceinline__ float group_sum(float x, int G) {
@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
                                                           const float* __restrict__ rstd, T* __restrict__ dx,
                                                           float* __restrict__ part, int M, int C, int G,
                                                           const T* __restrict__ dres = nullptr) {
-  extern __shared__ float red[];             // [groups][2][C]
+  extern __shared__ float red[];             // [4 waves][2][C]
   const int nch = C >> 3;
   const int lane = threadIdx.x & (G - 1);
   const int grp = threadIdx.x / G;
@@ -198,24 +198,35 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
       }
     }
   }
-  // reduce the groups' dw / db in LDS -> one partial row pair per workgroup
-  float* mine = red + (size_t)grp * 2 * C;
+  // reduce the wave's groups with shuffles (lanes holding the same chunks), then the 4
+  // waves in LDS -> one partial row pair per workgroup
+  for (int o = G; o < 64; o <<= 1) {
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int j = lane + k * G;
-    if (j < nch) {
+    for (int k = 0; k < K; ++k)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        mine[j * 8 + i] = dw[k][i];
-        mine[C + j * 8 + i] = db[k][i];
+        dw[k][i] += __shfl_xor(dw[k][i], o, 64);
+        db[k][i] += __shfl_xor(db[k][i], o, 64);
+      }
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < G) {
+    float* mine = red + (size_t)wave * 2 * C;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = lane + k * G;
+      if (j < nch) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          mine[j * 8 + i] = dw[k][i];
+          mine[C + j * 8 + i] = db[k][i];
+        }
       }
     }
   }
   __syncthreads();
-  const int groups = kThreads / G;
   for (int c = threadIdx.x; c < 2 * C; c += kThreads) {
-    float acc = 0.f;
-    for (int gi = 0; gi < groups; ++gi) acc += red[(size_t)gi * 2 * C + c];
+    const float acc = (red[c] + red[2 * C + c]) + (red[4 * C + c] + red[6 * C + c]);
     part[(size_t)blockIdx.x * 2 * C + c] = acc;
   }
 }
@@ -446,7 +457,7 @@ static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, co
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   const int grid = blocks_for(M, kThreads / G, kMaxPartials);
-  const size_t lds = (size_t)(kThreads / G) * 2 * C * sizeof(float);
+  const size_t lds = (size_t)(kThreads / 64) * 2 * C * sizeof(float);
   VS_CHECK(lds <= 64 * 1024, "LayerNorm backward LDS budget exceeded");
 #define VS_LNB(KK)                                                                                            \
   if (dtype == VS_BF16 && dres)                                                                               \

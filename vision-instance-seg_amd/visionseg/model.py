@@ -440,13 +440,13 @@ class Decoder(nn.Module):
         self.mask_override = None
         self.record = False
 
-    def predict(self, h, mf_nhwc, Hm, Wm, target_hw):
+    def predict(self, h, mf_nhwc, Hm, Wm, target_hw, sink=None):
         x = self.norm(h)
         e = F.relu(self.mask_embed[0](x))
         e = F.relu(self.mask_embed[1](e))
         e = self.mask_embed[2](e)
         e = e.to(mf_nhwc.dtype)
-        logits = ops.mask_head(e, mf_nhwc, Hm, Wm)
+        logits = ops.mask_head(e, mf_nhwc, Hm, Wm, sink=sink)
         words = ops.attn_bitmask(logits, target_hw) if target_hw is not None else None
         return x, logits, words
 
@@ -455,6 +455,10 @@ class Decoder(nn.Module):
         B, _, Hm, Wm = mask_features.shape
         dev = mask_features.device
         mf = mask_features.to(_compute_dtype(mask_features)).permute(0, 2, 3, 1).reshape(B, Hm * Wm, -1).contiguous()
+        # the mask-head calls sum their pixel-embedding gradient in one buffer (ops.GradSink)
+        sink = ops.GradSink() if (mf.requires_grad and torch.is_grad_enabled() and mf.is_cuda) else None
+        if sink is not None:
+            mf = sink.source(mf)
         mems, mem_pos, sizes = [], [], []
         for i in range(3):
             # once per level (shared by the decoder rounds): token-major memory and memory + pos
@@ -467,7 +471,7 @@ class Decoder(nn.Module):
         qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
         h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
         n = len(self.layers)
-        inter, logits, words = self.predict(h, mf, Hm, Wm, sizes[0] if n else None)
+        inter, logits, words = self.predict(h, mf, Hm, Wm, sizes[0] if n else None, sink)
         inters, masks = [inter], [logits]
         self.trace = []
         for idx, layer in enumerate(self.layers):
@@ -478,7 +482,7 @@ class Decoder(nn.Module):
                 words = pack_bitmask(self.mask_override[idx].to(dev))
             h = layer(h, qpos, mems[lvl], mem_pos[lvl], words)
             nxt = sizes[(idx + 1) % 3] if idx + 1 < n else None
-            inter, logits, words = self.predict(h, mf, Hm, Wm, nxt)
+            inter, logits, words = self.predict(h, mf, Hm, Wm, nxt, sink)
             inters.append(inter)
             masks.append(logits)
         return inters, masks

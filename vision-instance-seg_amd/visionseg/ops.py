@@ -270,8 +270,9 @@ class MaskHeadFunction(torch.autograd.Function):
     f32 parity mode uses vendor GEMMs for the backward."""
 
     @staticmethod
-    def forward(ctx, mask_embed, pixel_nhwc, height, width):
+    def forward(ctx, mask_embed, pixel_nhwc, height, width, sink=None):
         L.require_hip(mask_embed, pixel_nhwc)
+        ctx.sink = sink
         E = mask_embed.contiguous()
         P = pixel_nhwc.to(E.dtype).contiguous()
         B, Q, C = E.shape
@@ -291,27 +292,67 @@ class MaskHeadFunction(torch.autograd.Function):
         E, P = ctx.saved_tensors
         B, Q, C = E.shape
         N = P.shape[1]
+        sink = ctx.sink
         if E.dtype == torch.bfloat16 and Q <= 128 and C in (128, 256):
             g = g.float().contiguous()
             gE = torch.empty_like(E)
-            gP = torch.empty_like(P)
+            acc = sink is not None and sink.buf is not None
+            if sink is not None and not acc:
+                sink.buf = torch.empty_like(P)
+            gP = sink.buf if sink is not None else torch.empty_like(P)
             ws = torch.empty(int(L.lib().vs_mask_head_backward_workspace_bytes(B, Q, C)), device=E.device,
                              dtype=torch.uint8)
-            nb = g.numel() * 4 + (E.numel() * 2 + P.numel() * 2) * 2
+            nb = g.numel() * 4 + (E.numel() * 2 + P.numel() * 2) * 2 + (P.numel() * 2 if acc else 0)
             with timed("mask_head_bwd", E, bytes_=nb, flops=4.0 * B * Q * C * N):
-                L.check(L.lib().vs_mask_head_backward(L.dtype_code(E), L.ptr(g), L.ptr(E), L.ptr(P), L.ptr(gE),
-                                                      L.ptr(gP), L.ptr(ws), B, Q, C, N, 1, L.stream(E)),
+                L.check(L.lib().vs_mask_head_backward_ex(L.dtype_code(E), L.ptr(g), L.ptr(E), L.ptr(P), L.ptr(gE),
+                                                         L.ptr(gP), L.ptr(ws), B, Q, C, N, 1, int(acc), L.stream(E)),
                         "mask_head_backward")
-            return gE, gP.to(ctx.pdtype), None, None
+            if sink is not None:
+                return gE, None, None, None, None
+            return gE, gP.to(ctx.pdtype), None, None, None
         # f32 parity mode (and shapes outside the fused kernel): vendor GEMMs
         gl = g.reshape(B, Q, -1).to(E.dtype)
         gE = torch.bmm(gl, P) if ctx.needs_input_grad[0] else None
         gP = torch.bmm(gl.transpose(1, 2), E).to(ctx.pdtype) if ctx.needs_input_grad[1] else None
-        return gE, gP, None, None
+        if sink is not None and gP is not None:
+            sink.buf = gP if sink.buf is None else sink.buf + gP
+            gP = None
+        return gE, gP, None, None, None
 
 
-def mask_head(mask_embed, pixel_nhwc, height: int, width: int):
-    return MaskHeadFunction.apply(mask_embed, pixel_nhwc, int(height), int(width))
+def mask_head(mask_embed, pixel_nhwc, height: int, width: int, sink=None):
+    """sink (GradSink): the pixel-embedding gradient of every call sharing the sink is
+    summed in one buffer inside the backward kernel (pass `pixel_nhwc` through
+    `sink.source(...)` once); without a sink each call returns its own gradient."""
+    return MaskHeadFunction.apply(mask_embed, pixel_nhwc, int(height), int(width), sink)
+
+
+class _SinkSource(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, sink):
+        ctx.sink = sink
+        ctx.set_materialize_grads(False)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        # runs after every consumer of the output: their in-place sum is in sink.buf
+        buf, ctx.sink.buf = ctx.sink.buf, None
+        if g is not None:
+            buf = g if buf is None else buf + g
+        return buf, None
+
+
+class GradSink:
+    """Gradient side channel for a tensor consumed by several mask-head calls: the calls
+    accumulate its gradient into `buf` in place (csrc/mask_head.hip ACC mode) and return
+    none; the source node hands the sum to autograd once."""
+
+    def __init__(self):
+        self.buf = None
+
+    def source(self, x):
+        return _SinkSource.apply(x, self)
 
 
 def attn_bitmask(logits, target_hw):
