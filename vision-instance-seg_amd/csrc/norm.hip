@@ -24,7 +24,7 @@ namespace vs {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kMaxPartials = 2048;   // workgroups of a backward / column-sum sweep
+constexpr int kMaxPartials = 512;    // workgroups of a backward / column-sum sweep
 
 // lanes of one group: shuffle-reduce within G lanes (G a power of two, <= 64)
 __device__ __forceinline__ float group_sum(float x, int G) {
