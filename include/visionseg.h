@@ -326,6 +326,19 @@ VS_API int vs_small_linear_wgrad(int dtype, const void* grad_y, const void* x, v
 VS_API int vs_splitk_sum(int dtype, const float* partials, int num_parts, long long n, const float* extra,
                          void* out, void* stream);
 
+/* ---- a9: pixel-decoder FPN merge ----------------------------------------------------
+ * out[B, C, H, W] = cur + bilinear_upsample(src) (align_corners=False, HF:m2f:1405-1413),
+ * cur / out NCHW, src token-major [B, Hs*Ws, C] with batch stride src_batch_stride
+ * (elements; token stride C); upsampling factor in [1, 2], C % 32 == 0.  The upsampled
+ * value is rounded to dtype before the add (as F.interpolate + add). */
+VS_API int vs_upsample_add_forward(int dtype, const void* cur, const void* src, void* out, int batch, int channels,
+                                   int height, int width, int src_height, int src_width, long long src_batch_stride,
+                                   void* stream);
+/* grad_src [B, Hs*Ws, C] (contiguous, overwritten) = adjoint of the upsample applied to
+ * grad_out [B, C, H, W]; fixed-order gather, no atomics. */
+VS_API int vs_upsample_backward(int dtype, const void* grad_out, void* grad_src, int batch, int channels, int height,
+                                int width, int src_height, int src_width, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

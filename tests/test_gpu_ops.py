@@ -7,6 +7,7 @@ tolerance stated per test (bf16 output rounding, 2^-8 relative).
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from oracle import ref_ops as R
 
@@ -792,3 +793,32 @@ def test_small_linear_weight_slice():
     ref = x.double().reshape(-1, 256).sum(0)
     assert torch.allclose(W.grad[0].double().cpu(), ref.cpu(), rtol=2 ** -7, atol=1e-2)
     assert abs(float(bb.grad[0]) - 400.0) <= 2.0
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,Hs,Ws,H,W", [(2, 256, 16, 16, 32, 32), (1, 64, 128, 128, 256, 256),
+                                           (2, 32, 13, 21, 25, 42), (1, 32, 7, 9, 7, 9), (1, 96, 40, 70, 64, 100)])
+def test_upsample_add_vs_torch(dtype, B, C, Hs, Ws, H, W):
+    """FPN merge (csrc/upsample.hip): cur + bilinear upsample of a token-major level vs
+    F.interpolate(align_corners=False) + add (up rounded to dtype first, as the unfused
+    graph), and the source gradient vs autograd of F.interpolate."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(C + H)
+    cur = torch.randn(B, C, H, W, generator=g).to(dtype)
+    big = torch.randn(B, Hs * Ws + 37, C, generator=g).to(dtype)    # the level is a slice of a longer sequence
+    go = torch.randn(B, C, H, W, generator=g).to(dtype)
+    src = big[:, 5:5 + Hs * Ws]
+    sr = src.double().clone().requires_grad_(True)
+    up = F.interpolate(sr.transpose(1, 2).reshape(B, C, Hs, Ws), size=(H, W), mode="bilinear", align_corners=False)
+    exp = (cur.double() + up.to(dtype).double()).to(dtype)
+    up.backward(go.double())
+    bd = big.to(DEV).requires_grad_(True)
+    out = ops.upsample_add(cur.to(DEV), bd[:, 5:5 + Hs * Ws], Hs, Ws)
+    err = (out.double().cpu() - exp.double()).abs().max()
+    tol = 1e-5 if dtype == torch.float32 else 2 ** -7
+    assert float(err) <= tol * max(1.0, float(exp.double().abs().max())), float(err)
+    out.backward(go.to(DEV))
+    gsrc = bd.grad[:, 5:5 + Hs * Ws].double().cpu()
+    e2 = float((gsrc - sr.grad).abs().max())
+    assert e2 <= (1e-5 if dtype == torch.float32 else 2 ** -7) * max(1.0, float(sr.grad.abs().max())), e2
+    assert float(bd.grad[:, :5].abs().max()) == 0.0 and float(bd.grad[:, 5 + Hs * Ws:].abs().max()) == 0.0

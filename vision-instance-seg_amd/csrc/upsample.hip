@@ -1,0 +1,182 @@
+// Pixel-decoder FPN merge: out = cur + upsample_bilinear(src)  (HF:m2f:1405-1413,
+// `F.interpolate(..., mode="bilinear", align_corners=False)` added to the lateral
+// branch), and its backward for src.
+//
+// cur / out are NCHW planes [B, C, H, W] (the 1/4-resolution blocks run NCHW for
+// MIOpen's 3x3 conv); src is the encoder's token-major level [B, Hs*Ws, C] (a view of
+// the encoder output, batch stride given).  The torch composition is an NHWC upsample
+// (its input is a channels-last view), an add of an NHWC and an NCHW tensor that falls
+// off the vectorised path, and a scatter-style upsample backward: ~1 ms per step.  Here:
+//   forward:  block = (64 output columns, one output row, 32 channels, image); the two
+//             source rows' needed tokens are staged in LDS (64-B channel runs, coalesced),
+//             outputs written along x (coalesced NCHW).  up is rounded to the dtype before
+//             the add, as the unfused graph does.
+//   backward: block = (32 source columns, one source row, 32 channels, image); the output
+//             rows/columns whose bilinear taps reach them are staged from dL/dout and
+//             every source element is a fixed-order gather (no atomics), written once,
+//             token-major.
+// Source index: ATen area_pixel_compute_source_index (align_corners=False):
+// s = (in/out) * (dst + 0.5) - 0.5, clamped at 0; i1 = min(i0 + 1, in - 1).
+#include "common.h"
+
+namespace vs {
+namespace {
+
+constexpr int kCB = 32;    // channels per block
+
+__device__ __forceinline__ void up_index(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  const float scale = (float)in / (float)out;
+  float s = scale * ((float)dst + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = s - (float)i0;
+  l0 = 1.f - l1;
+}
+
+// grid (ceil(W / 64), H, B * C / 32), 256 threads
+template <typename T>
+__global__ void __launch_bounds__(256) upsample_add_fwd_kernel(const T* __restrict__ cur, const T* __restrict__ src,
+                                                               T* __restrict__ out, int C, int H, int W, int Hs,
+                                                               int Ws, long long src_bstride) {
+  constexpr int kMaxCols = 2 * 64 + 4;        // source columns a 64-wide output tile can touch (scale <= 2)
+  __shared__ float sS[2][kMaxCols][kCB + 1];
+  const int x0 = blockIdx.x * 64, y = blockIdx.y;
+  const int cb = blockIdx.z % (C / kCB), b = blockIdx.z / (C / kCB);
+  const int c0 = cb * kCB;
+  int ya, yb, xa_, xb_;
+  float ly0, ly1, lxa, lxb;
+  up_index(y, Hs, H, ya, yb, ly0, ly1);
+  up_index(x0, Ws, W, xa_, xb_, lxa, lxb);
+  const int xlast = min(W, x0 + 64) - 1;
+  int xl0, xl1;
+  up_index(xlast, Ws, W, xl0, xl1, lxa, lxb);
+  const int sx0 = xa_, ncols = xl1 - sx0 + 1;  // source columns [sx0, xl1]
+  const T* sb = src + (size_t)b * src_bstride + c0;
+  for (int i = threadIdx.x; i < 2 * ncols * kCB; i += 256) {
+    const int c = i % kCB, col = (i / kCB) % ncols, r = i / (kCB * ncols);
+    const int sy = r ? yb : ya;
+    sS[r][col][c] = to_f32(sb[((size_t)sy * Ws + sx0 + col) * C + c]);
+  }
+  __syncthreads();
+  const int xi = threadIdx.x & 63;
+  const int x = x0 + xi;
+  if (x >= W) return;
+  int xs0, xs1;
+  float lx0, lx1;
+  up_index(x, Ws, W, xs0, xs1, lx0, lx1);
+  xs0 -= sx0;
+  xs1 -= sx0;
+  for (int c = threadIdx.x >> 6; c < kCB; c += 4) {
+    const float up = ly0 * (lx0 * sS[0][xs0][c] + lx1 * sS[0][xs1][c]) +
+                     ly1 * (lx0 * sS[1][xs0][c] + lx1 * sS[1][xs1][c]);
+    const size_t o = (((size_t)b * C + c0 + c) * H + y) * W + x;
+    out[o] = from_f32<T>(to_f32(cur[o]) + to_f32(from_f32<T>(up)));
+  }
+}
+
+// grid (ceil(Ws / 32), Hs, B * C / 32), 256 threads; dsrc [B, Hs*Ws, C] contiguous
+template <typename T>
+__global__ void __launch_bounds__(256) upsample_bwd_kernel(const T* __restrict__ dout, T* __restrict__ dsrc, int C,
+                                                           int H, int W, int Hs, int Ws) {
+  constexpr int kMaxRows = 8, kMaxCols = 72;   // output rows / columns reaching a source row / 32 columns (scale <= 2)
+  __shared__ float sD[kCB][kMaxRows][kMaxCols + 1];
+  __shared__ float sWy[kMaxRows];
+  __shared__ int sRow[kMaxRows];
+  const int sx0 = blockIdx.x * 32, sy = blockIdx.y;
+  const int cb = blockIdx.z % (C / kCB), b = blockIdx.z / (C / kCB);
+  const int c0 = cb * kCB;
+  // output rows whose taps touch source row sy (scan a conservative window)
+  const float sc_y = (float)H / (float)Hs;
+  const int ylo = max(0, (int)floorf((sy - 1) * sc_y) - 2), yhi = min(H - 1, (int)ceilf((sy + 2) * sc_y) + 2);
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int y = ylo; y <= yhi && n < kMaxRows; ++y) {
+      int y0, y1;
+      float l0, l1;
+      up_index(y, Hs, H, y0, y1, l0, l1);
+      const float w = (y0 == sy ? l0 : 0.f) + (y1 == sy ? l1 : 0.f);
+      if (w != 0.f) {
+        sRow[n] = y;
+        sWy[n] = w;
+        ++n;
+      }
+    }
+    for (int k = n; k < kMaxRows; ++k) {
+      sRow[k] = -1;
+      sWy[k] = 0.f;
+    }
+  }
+  // output columns reaching source columns [sx0, sx0 + 32)
+  const float sc_x = (float)W / (float)Ws;
+  const int xlo = max(0, (int)floorf((sx0 - 1) * sc_x) - 2);
+  const int xhi = min(W - 1, min(xlo + kMaxCols - 1, (int)ceilf((sx0 + 33) * sc_x) + 2));
+  const int ncols = xhi - xlo + 1;
+  __syncthreads();
+  for (int i = threadIdx.x; i < kCB * kMaxRows * ncols; i += 256) {
+    const int xx = i % ncols, r = (i / ncols) % kMaxRows, c = i / (ncols * kMaxRows);
+    const int y = sRow[r];
+    sD[c][r][xx] = y >= 0 ? to_f32(dout[(((size_t)b * C + c0 + c) * H + y) * W + xlo + xx]) : 0.f;
+  }
+  __syncthreads();
+  const int c = threadIdx.x & 31;
+  for (int sxi = threadIdx.x >> 5; sxi < 32; sxi += 8) {
+    const int sx = sx0 + sxi;
+    if (sx >= Ws) break;
+    float acc = 0.f;
+    for (int xx = 0; xx < ncols; ++xx) {
+      int x0_, x1_;
+      float l0, l1;
+      up_index(xlo + xx, Ws, W, x0_, x1_, l0, l1);
+      const float wx = (x0_ == sx ? l0 : 0.f) + (x1_ == sx ? l1 : 0.f);
+      if (wx != 0.f) {
+        float col = 0.f;
+#pragma unroll
+        for (int r = 0; r < kMaxRows; ++r) col += sWy[r] * sD[c][r][xx];
+        acc += wx * col;
+      }
+    }
+    dsrc[((size_t)b * Hs * Ws + (size_t)sy * Ws + sx) * C + c0 + c] = from_f32<T>(acc);
+  }
+}
+
+}  // namespace
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" int vs_upsample_add_forward(int dtype, const void* cur, const void* src, void* out, int B, int C, int H,
+                                       int W, int Hs, int Ws, long long src_batch_stride, void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(B > 0 && C > 0 && C % kCB == 0 && H > 0 && W > 0 && Hs > 0 && Ws > 0, "bad sizes (C % 32 == 0)");
+  VS_CHECK(Hs <= H && Ws <= W && 2 * Hs >= H && 2 * Ws >= W, "upsampling factor must lie in [1, 2]");
+  VS_CHECK(cur && src && out, "null pointer");
+  dim3 grid((W + 63) / 64, H, B * (C / kCB));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(upsample_add_fwd_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)cur, (const bf16*)src,
+                       (bf16*)out, C, H, W, Hs, Ws, src_batch_stride);
+  else
+    hipLaunchKernelGGL(upsample_add_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)cur, (const float*)src,
+                       (float*)out, C, H, W, Hs, Ws, src_batch_stride);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_upsample_backward(int dtype, const void* grad_out, void* grad_src, int B, int C, int H, int W,
+                                    int Hs, int Ws, void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(B > 0 && C > 0 && C % kCB == 0 && H > 0 && W > 0 && Hs > 0 && Ws > 0, "bad sizes (C % 32 == 0)");
+  VS_CHECK(Hs <= H && Ws <= W && 2 * Hs >= H && 2 * Ws >= W, "upsampling factor must lie in [1, 2]");
+  VS_CHECK(grad_out && grad_src, "null pointer");
+  dim3 grid((Ws + 31) / 32, Hs, B * (C / kCB));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(upsample_bwd_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)grad_out, (bf16*)grad_src, C,
+                       H, W, Hs, Ws);
+  else
+    hipLaunchKernelGGL(upsample_bwd_kernel<float>, grid, dim3(256), 0, st, (const float*)grad_out, (float*)grad_src,
+                       C, H, W, Hs, Ws);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

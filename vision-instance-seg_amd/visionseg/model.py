@@ -357,12 +357,18 @@ class PixelDecoder(nn.Module):
             self._norm_cache[key] = norm
         for layer in self.encoder:
             h = layer(h, p, ref, shapes, norm)
-        outs, s = [], 0
-        for (Hl, Wl) in shapes:
-            outs.append(h[:, s:s + Hl * Wl].transpose(1, 2).reshape(B, -1, Hl, Wl))
-            s += Hl * Wl
+        # encoder levels, token-major [B, H_l*W_l, C] (split: one concatenating backward
+        # instead of a zero-filled full-size gradient per slice)
+        toks = torch.split(h, [Hl * Wl for (Hl, Wl) in shapes], dim=1)
+        outs = [(t, hw) for t, hw in zip(toks, shapes)]
         cur = self.lateral(feats[0])
-        y = cur + F.interpolate(outs[-1].to(cur.dtype), size=cur.shape[-2:], mode="bilinear", align_corners=False)
+        Hs, Ws = shapes[-1]
+        if (cur.is_cuda and _PIXDEC_NCHW and cur.shape[1] % 32 == 0 and cur.shape[2] <= 2 * Hs
+                and cur.shape[3] <= 2 * Ws and not torch.is_autocast_enabled()):
+            y = ops.upsample_add(cur, toks[-1], Hs, Ws)                  # csrc/upsample.hip
+        else:
+            lvl = toks[-1].transpose(1, 2).reshape(B, -1, Hs, Ws)
+            y = cur + F.interpolate(lvl.to(cur.dtype), size=cur.shape[-2:], mode="bilinear", align_corners=False)
         y = self.output(y)
         if y.is_cuda and _PIXDEC_NCHW:
             # token-major mask features straight from the NCHW planes (channels-last view)
@@ -462,10 +468,10 @@ class Decoder(nn.Module):
         mems, mem_pos, sizes = [], [], []
         for i in range(3):
             # once per level (shared by the decoder rounds): token-major memory and memory + pos
-            f = ms_feats[i]
-            sizes.append((int(f.shape[2]), int(f.shape[3])))
-            pos = sine_pos_embed(B, f.shape[2], f.shape[3], d // 2, dev).to(f.dtype).flatten(2).transpose(1, 2)
-            m = (f.flatten(2) + self.level_embed.weight[i][None, :, None].to(f.dtype)).transpose(1, 2).contiguous()
+            f, (Hl, Wl) = ms_feats[i]                       # token-major [B, Hl*Wl, C]
+            sizes.append((int(Hl), int(Wl)))
+            pos = sine_pos_embed(B, Hl, Wl, d // 2, dev).to(f.dtype).flatten(2).transpose(1, 2)
+            m = f + self.level_embed.weight[i][None, None, :].to(f.dtype)
             mems.append(m)
             mem_pos.append(m + pos)
         qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)

@@ -741,3 +741,42 @@ class GroupNormNCHWFunction(torch.autograd.Function):
 
 def group_norm_nchw(x, weight, bias, groups: int, eps: float = 1e-5, relu: bool = False):
     return GroupNormNCHWFunction.apply(x, weight, bias, int(groups), float(eps), bool(relu))
+
+
+# ------------------------------------------------------------------ FPN merge (upsample + add)
+class UpsampleAddFunction(torch.autograd.Function):
+    """out = cur + bilinear_upsample(src) (csrc/upsample.hip): cur NCHW [B,C,H,W]
+    contiguous, src token-major [B, Hs*Ws, C] (rows contiguous, any batch stride)."""
+
+    @staticmethod
+    def forward(ctx, cur, src, Hs, Ws):
+        L.require_hip(cur, src)
+        B, C, H, W = cur.shape
+        cur = cur.contiguous()
+        src = src.to(cur.dtype)
+        if src.stride(2) != 1 or src.stride(1) != C:
+            src = src.contiguous()
+        if tuple(src.shape) != (B, Hs * Ws, C):
+            raise ValueError(f"src {tuple(src.shape)} != {(B, Hs * Ws, C)}")
+        out = torch.empty_like(cur)
+        with timed("upsample_add", cur, bytes_=(2 * cur.numel() + src.numel()) * cur.element_size()):
+            L.check(L.lib().vs_upsample_add_forward(L.dtype_code(cur), L.ptr(cur), L.ptr(src), L.ptr(out), B, C, H,
+                                                    W, int(Hs), int(Ws), src.stride(0), L.stream(cur)),
+                    "upsample_add_forward")
+        ctx.geom = (B, C, H, W, int(Hs), int(Ws))
+        ctx.src_dtype = src.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, C, H, W, Hs, Ws = ctx.geom
+        g = g.contiguous()
+        gs = torch.empty(B, Hs * Ws, C, device=g.device, dtype=g.dtype)
+        with timed("upsample_bwd", g, bytes_=(g.numel() + gs.numel()) * g.element_size()):
+            L.check(L.lib().vs_upsample_backward(L.dtype_code(g), L.ptr(g), L.ptr(gs), B, C, H, W, Hs, Ws,
+                                                 L.stream(g)), "upsample_backward")
+        return g, gs.to(ctx.src_dtype), None, None
+
+
+def upsample_add(cur, src_tokens, Hs: int, Ws: int):
+    return UpsampleAddFunction.apply(cur, src_tokens, int(Hs), int(Ws))
