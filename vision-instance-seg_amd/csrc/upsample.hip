@@ -79,8 +79,8 @@ __global__ void __launch_bounds__(256) upsample_add_fwd_kernel(const T* __restri
 template <typename T>
 __global__ void __launch_bounds__(256) upsample_bwd_kernel(const T* __restrict__ dout, T* __restrict__ dsrc, int C,
                                                            int H, int W, int Hs, int Ws) {
-  constexpr int kMaxRows = 8, kMaxCols = 72;   // output rows / columns reaching a source row / 32 columns (scale <= 2)
-  __shared__ float sD[kCB][kMaxRows][kMaxCols + 1];
+  constexpr int kMaxRows = 5, kMaxCols = 72;   // output rows (nonzero weight) / columns reaching a source row / 32 columns (scale <= 2)
+  __shared__ float sD[kMaxRows][kMaxCols][kCB + 1];     // [row][column][channel]: lanes = channels
   __shared__ float sWy[kMaxRows];
   __shared__ int sRow[kMaxRows];
   const int sx0 = blockIdx.x * 32, sy = blockIdx.y;
@@ -113,10 +113,18 @@ __global__ void __launch_bounds__(256) upsample_bwd_kernel(const T* __restrict__
   const int xhi = min(W - 1, min(xlo + kMaxCols - 1, (int)ceilf((sx0 + 33) * sc_x) + 2));
   const int ncols = xhi - xlo + 1;
   __syncthreads();
-  for (int i = threadIdx.x; i < kCB * kMaxRows * ncols; i += 256) {
-    const int xx = i % ncols, r = (i / ncols) % kMaxRows, c = i / (ncols * kMaxRows);
-    const int y = sRow[r];
-    sD[c][r][xx] = y >= 0 ? to_f32(dout[(((size_t)b * C + c0 + c) * H + y) * W + xlo + xx]) : 0.f;
+  int nr = 0;
+  while (nr < kMaxRows && sRow[nr] >= 0) ++nr;
+  // stage the valid rows only; 4 consecutive columns per thread
+  const int nq = (ncols + 3) >> 2;
+  for (int i = threadIdx.x; i < kCB * nr * nq; i += 256) {
+    const int xq = i % nq, r = (i / nq) % nr, c = i / (nq * nr);
+    const T* row = dout + (((size_t)b * C + c0 + c) * H + sRow[r]) * W + xlo;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int xx = 4 * xq + k;
+      if (xx < ncols) sD[r][xx][c] = to_f32(row[xx]);
+    }
   }
   __syncthreads();
   const int c = threadIdx.x & 31;
@@ -124,15 +132,17 @@ __global__ void __launch_bounds__(256) upsample_bwd_kernel(const T* __restrict__
     const int sx = sx0 + sxi;
     if (sx >= Ws) break;
     float acc = 0.f;
-    for (int xx = 0; xx < ncols; ++xx) {
+    // only the few output columns whose taps can reach sx (~2 per unit of scale)
+    const int xb = max(xlo, (int)floorf((sx - 1) * sc_x) - 1);
+    const int xe = min(xhi, (int)ceilf((sx + 2) * sc_x) + 1);
+    for (int x = xb; x <= xe; ++x) {
       int x0_, x1_;
       float l0, l1;
-      up_index(xlo + xx, Ws, W, x0_, x1_, l0, l1);
+      up_index(x, Ws, W, x0_, x1_, l0, l1);
       const float wx = (x0_ == sx ? l0 : 0.f) + (x1_ == sx ? l1 : 0.f);
       if (wx != 0.f) {
         float col = 0.f;
-#pragma unroll
-        for (int r = 0; r < kMaxRows; ++r) col += sWy[r] * sD[c][r][xx];
+        for (int r = 0; r < nr; ++r) col += sWy[r] * sD[r][x - xlo][c];
         acc += wx * col;
       }
     }
