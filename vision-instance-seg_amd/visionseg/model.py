@@ -403,12 +403,12 @@ class DecoderLayer(nn.Module):
         super().__init__()
         self.heads = heads
         self.cross_attn = CrossAttn(d)
-        self.norm_cross = nn.LayerNorm(d)
+        self.norm_cross = TokenLayerNorm(d)
         self.self_attn = SelfAttn(d)
-        self.norm_self = nn.LayerNorm(d)
+        self.norm_self = TokenLayerNorm(d)
         self.fc1 = SmallLinear(d, ffn)
         self.fc2 = SmallLinear(ffn, d)
-        self.norm_ffn = nn.LayerNorm(d)
+        self.norm_ffn = TokenLayerNorm(d)
 
     def forward(self, h, qpos, mem, mem_pos, words):
         """mem: level memory [B, hw, D] (contiguous), mem_pos = mem + its position embedding."""
@@ -419,14 +419,15 @@ class DecoderLayer(nn.Module):
         k = linear_tokens(mem_pos, W[D:2 * D], b[D:2 * D])
         v = linear_tokens(mem, W[2 * D:], b[2 * D:])
         o = ops.masked_attention(q, k, v, words, H, d ** -0.5)
-        h = self.norm_cross(h + self.cross_attn.out_proj(o))
+        _, h = self.norm_cross.add_forward(h, self.cross_attn.out_proj(o))       # post-norm, fused add
         sa = self.self_attn
         qs = sa.q_proj(h + qpos).view(B, Q, H, d).transpose(1, 2)
         ks = sa.k_proj(h + qpos).view(B, Q, H, d).transpose(1, 2)
         vs = sa.v_proj(h).view(B, Q, H, d).transpose(1, 2)
         att = F.scaled_dot_product_attention(qs, ks, vs)
-        h = self.norm_self(h + sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)))
-        return self.norm_ffn(h + self.fc2(F.relu(self.fc1(h))))
+        _, h = self.norm_self.add_forward(h, sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)))
+        _, h = self.norm_ffn.add_forward(h, self.fc2(F.relu(self.fc1(h))))
+        return h
 
 
 class Decoder(nn.Module):
@@ -438,7 +439,7 @@ class Decoder(nn.Module):
         self.query_embed = nn.Embedding(cfg.num_queries, d)
         self.level_embed = nn.Embedding(3, d)
         self.layers = nn.ModuleList([DecoderLayer(d, cfg.dec_ffn, cfg.dec_heads) for _ in range(cfg.dec_layers - 1)])
-        self.norm = nn.LayerNorm(d)
+        self.norm = TokenLayerNorm(d)
         self.mask_embed = nn.ModuleList([SmallLinear(d, d), SmallLinear(d, d), SmallLinear(d, cfg.mask_feature_size)])
         # Parity-test hook ("teacher forcing"): a list of bool [B,Q,h*w] blocked masks, one per
         # decoder layer, used instead of the masks this decoder derives itself.  Lets a test
