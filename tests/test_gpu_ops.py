@@ -455,17 +455,23 @@ def _encoder_like_inputs(B, shapes, H, P, seed, jitter):
     return value, loc, w
 
 
-@pytest.mark.parametrize("run", ["16", "7", "0"])
+@pytest.mark.parametrize("run,win", [("16", "1"), ("16", "0"), ("7", "0"), ("0", "0"), ("16", "sub")])
 @pytest.mark.parametrize("jitter", [0.0, 0.3, 3.0])
-def test_msda_carry_backward_vs_oracle(monkeypatch, run, jitter):
-    """Register-carry grad_value (csrc/msda.hip msda_bwd_carry_kernel) on encoder-shaped
-    queries, runs of 16 / 7 (ragged) queries and the plain kernel (0), vs the oracle."""
+def test_msda_carry_backward_vs_oracle(monkeypatch, run, win, jitter):
+    """Atomic-scatter grad_value on encoder-shaped queries vs the oracle: the query-tile
+    LDS-window kernel (csrc/msda.hip msda_bwd_window_kernel; 4x4 grid tiles, or runs of
+    16 queries for a query subset "sub"), the register-carry kernel with runs of 16 / 7
+    (ragged) queries, and the plain kernel (run 0)."""
     monkeypatch.setenv("VS_MSDA_RUN", run)
+    monkeypatch.setenv("VS_MSDA_WIN", "0" if win == "0" else "1")
     ops = _ops()
     monkeypatch.setattr(ops, "_MSDA_SORTED", False)
     monkeypatch.setattr(ops, "_MSDA_BWD", "carry")
     shapes = [(8, 8), (16, 16), (32, 32)]
     value, loc, w = _encoder_like_inputs(2, shapes, 4, 4, seed=11, jitter=jitter)
+    if win == "sub":                                   # Q != S: windows over runs of 16 queries
+        idx = torch.randperm(loc.shape[1], generator=torch.Generator().manual_seed(5))[:700].sort().values
+        loc, w = loc[:, idx].contiguous(), w[:, idx].contiguous()
     vr, lr, wr = (t.clone().requires_grad_(True) for t in (value, loc, w))
     ref = R.msda_ref(vr, shapes, lr, wr)
     go = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3))

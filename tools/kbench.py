@@ -65,10 +65,11 @@ def main():
         for oname, off in offs.items():
             loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
             locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
-            for mode in ("tiled", "carry16", "sorted", "pull5"):
+            for mode in ("window", "carry16", "tiled", "sorted"):
                 ops._MSDA_SORTED = mode == "sorted"
                 ops._MSDA_BWD = {"tiled": "tiled", "sorted": "sorted"}.get(mode, "carry")
-                os.environ["VS_MSDA_RUN"] = {"carry16": "16"}.get(mode, "0")
+                os.environ["VS_MSDA_RUN"] = {"carry16": "16", "window": "16"}.get(mode, "0")
+                os.environ["VS_MSDA_WIN"] = "1" if mode == "window" else "0"
                 os.environ["VS_MSDA_NEAR_R"] = mode[4:] if mode.startswith("pull") else "5"
 
                 def fb(enc=mode.startswith("pull")):
@@ -76,6 +77,7 @@ def main():
                     o.backward(go)
                 run(f"msda {oname} {mode}", fb, a.iters)
             os.environ.pop("VS_MSDA_RUN")
+            os.environ.pop("VS_MSDA_WIN")
             os.environ.pop("VS_MSDA_NEAR_R")
     if "mask" in a.only:
         Q, C, Hm = 100, 256, 256
