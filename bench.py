@@ -87,7 +87,7 @@ def parse():
 # each timed op dispatches once per launch
 PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
 OP_KERNELS = {
-    "msda_bwd": ["msda_bwd_geom_kernel", "msda_bwd_scatter_kernel"],
+    "msda_bwd": ["msda_bwd_geom_kernel", "msda_bwd_window_kernel"],
     "msda_fwd": ["msda_fwd_kernel"],
     "window_attn_fwd": ["win_attn_fwd_mfma"],
     "window_attn_bwd": ["win_attn_bwd_mfma"],
