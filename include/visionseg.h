@@ -123,6 +123,28 @@ VS_API int vs_msda_backward_tiled(int dtype, const void* value, const int64_t* s
                                   int num_heads, int channels, int num_levels, int num_query, int num_point,
                                   void* stream);
 
+/* ---- a7: MSDeformAttn prologue (csrc/msda_prep.hip) ---------------------------------
+ * Replaces the reference path's `sampling_offsets(q) / offset_normalizer + reference_points`
+ * and `softmax(attention_weights(q))` (HF:m2f:994-1002; upstream MSDeformAttn.forward,
+ * reached from training/maskdino/train_full.py:308-310 through the pixel decoder):
+ *   loc[b,q,h,l,p,:] = ref[b,q,l,:] + offsets[b,q,h,l,p,:] / (W_l, H_l)      (f32 out)
+ *   attw[b,q,h,:]    = softmax_{L*P}(logits[b,q,h,:])                        (f32 out)
+ * offsets [B,Q,H*L*P*2] / logits [B,Q,H*L*P] in dtype with row strides (elements) >= a
+ * row (views of one fused projection allowed); ref f32 [B,Q,L,2] with rows contiguous
+ * and batch stride ref_batch_stride (0: shared by the batch); loc / attw contiguous.
+ * L <= 4, L*P <= 32. */
+VS_API int vs_msda_prep_forward(int dtype, const void* offsets, long long offsets_row_stride, const void* logits,
+                                long long logits_row_stride, const float* ref, long long ref_batch_stride,
+                                const int64_t* spatial_shapes_host, float* loc, float* attw, int batch,
+                                int num_query, int num_heads, int num_levels, int num_point, void* stream);
+/* Adjoint: grad_offsets = grad_loc / (W_l, H_l), grad_logits = attw * (g - <g, attw>)
+ * (attw = the forward's output), both rounded to dtype and written with the given row
+ * strides. */
+VS_API int vs_msda_prep_backward(int dtype, const float* grad_loc, const float* grad_attw, const float* attw,
+                                 const int64_t* spatial_shapes_host, void* grad_offsets,
+                                 long long grad_offsets_row_stride, void* grad_logits, long long grad_logits_row_stride,
+                                 int batch, int num_query, int num_heads, int num_levels, int num_point, void* stream);
+
 /* ---- a2: Swin pad + cyclic shift + window partition / its inverse ---------------
  * window_partition: x [B, H, W, C] -> windows [B*nWh*nWw, ws*ws, C] where
  * Hp = ceil(H/ws)*ws, nWh = Hp/ws (same for W); windows[(b,wy,wx), (ty,tx)] =

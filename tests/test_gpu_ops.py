@@ -828,3 +828,58 @@ def test_upsample_add_vs_torch(dtype, B, C, Hs, Ws, H, W):
     e2 = float((gsrc - sr.grad).abs().max())
     assert e2 <= (1e-5 if dtype == torch.float32 else 2 ** -7) * max(1.0, float(sr.grad.abs().max())), e2
     assert float(bd.grad[:, :5].abs().max()) == 0.0 and float(bd.grad[:, 5 + Hs * Ws:].abs().max()) == 0.0
+
+
+# ------------------------------------------------------------------ MSDA prologue
+def _prep_ref(off, lg, ref, shapes, H, P):
+    """The oracle's composition (oracle/ref_model.py:234-238, HF:m2f:994-1002) in f32 on
+    the CPU, from the same (dtype-rounded) projections."""
+    B, Q, nl = off.shape[0], off.shape[1], len(shapes)
+    norm = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32)
+    o = off.float().cpu().reshape(B, Q, H, nl, P, 2)
+    a = F.softmax(lg.float().cpu().reshape(B, Q, H, nl * P), -1).view(B, Q, H, nl, P)
+    loc = ref.float().cpu()[:, :, None, :, None, :] + o / norm[None, None, None, :, None, :]
+    return loc, a
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(2, 37, 8, [(4, 5), (2, 3), (1, 1)], 4, "fused"), (1, 300, 8, [(10, 30)] * 4, 4, "plain"),
+                                  (3, 5, 2, [(7, 3)], 1, "plain"), (2, 0, 8, [(2, 2)] * 3, 4, "plain"),
+                                  (1, 64, 3, [(8, 8), (4, 4)], 8, "fused")])
+def test_msda_prep_vs_torch(case, dtype):
+    """csrc/msda_prep.hip (sampling locations + softmax weights and their adjoint) vs the
+    f32 torch composition: loc / weights <= 1e-6 abs (f32 math on identical inputs), input
+    grads within one output-dtype rounding (f32 1e-6, bf16 2^-8 relative); batch-shared
+    reference points (batch stride 0), projections as views of one fused row (row stride
+    > row), ragged Q, one level, Q = 0."""
+    ops = _ops()
+    B, Q, H, shapes, P, layout = case
+    nl = len(shapes)
+    g = torch.Generator().manual_seed(Q + H)
+    if layout == "fused":
+        proj = (torch.randn(B, Q, H * nl * P * 3 + 5, generator=g) * 3).to(dtype).to(DEV)
+        off, lg = proj[..., :H * nl * P * 2], proj[..., H * nl * P * 2:H * nl * P * 3]
+    else:
+        off = (torch.randn(B, Q, H * nl * P * 2, generator=g) * 3).to(dtype).to(DEV)
+        lg = (torch.randn(B, Q, H * nl * P, generator=g) * 3).to(dtype).to(DEV)
+    ref = torch.rand(1, Q, nl, 2, generator=g).expand(B, -1, -1, -1).to(DEV)
+    offr, lgr = off.detach().clone().requires_grad_(True), lg.detach().clone().requires_grad_(True)
+    loc, aw = ops.msda_prep(offr, lgr, ref, shapes, H, P)
+    eloc, eaw = _prep_ref(off, lg, ref, shapes, H, P)
+    assert loc.dtype == torch.float32 and aw.dtype == torch.float32
+    assert loc.shape == eloc.shape and aw.shape == eaw.shape
+    torch.testing.assert_close(loc.cpu(), eloc, atol=1e-6, rtol=1e-6)
+    torch.testing.assert_close(aw.cpu(), eaw, atol=1e-6, rtol=1e-5)
+    if Q == 0:
+        return
+    gl = torch.randn(loc.shape, generator=g)
+    ga = torch.randn(aw.shape, generator=g)
+    torch.autograd.backward((loc, aw), (gl.to(DEV), ga.to(DEV)))
+    o32 = off.float().cpu().requires_grad_(True)
+    l32 = lg.float().cpu().requires_grad_(True)
+    e1, e2 = _prep_ref(o32, l32, ref, shapes, H, P)
+    torch.autograd.backward((e1, e2), (gl, ga))
+    tol = dict(atol=1e-6, rtol=1e-5) if dtype == torch.float32 else dict(atol=1e-6, rtol=2 ** -8)
+    assert offr.grad.dtype == dtype and lgr.grad.dtype == dtype
+    torch.testing.assert_close(offr.grad.float().cpu(), o32.grad, **tol)
+    torch.testing.assert_close(lgr.grad.float().cpu(), l32.grad, **tol)

@@ -1004,7 +1004,10 @@ void sorted_layout(long long nkeys, long long maxrec, size_t* off) {
 // Smoothly varying encoder offsets put a tile's taps of one level into a few dozen
 // cells, so the global atomics fall several-fold against one per corner per tap
 // (measured: pixel-decoder layer backward 1.74 -> 1.10 ms at C2).
-constexpr int kWinCells = 96;            // LDS window capacity (cells x 16 ch f32 = 6 KB)
+#ifndef VS_MSDA_WIN_CELLS
+#define VS_MSDA_WIN_CELLS 96
+#endif
+constexpr int kWinCells = VS_MSDA_WIN_CELLS;   // LDS window capacity (cells x 16 ch f32 = 6 KB)
 constexpr int kTE = 4, kTQ = kTE * kTE;  // query tile edge / queries per tile
 constexpr int kWinC = 16;                // channels per workgroup (a head's 32 split over two)
 
@@ -1041,7 +1044,11 @@ __device__ __forceinline__ int wave_max(int v) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(64) msda_bwd_window_kernel(const float* __restrict__ loc,
+__global__ void __launch_bounds__(64)
+#ifdef VS_MSDA_WIN_WPE
+__attribute__((amdgpu_waves_per_eu(VS_MSDA_WIN_WPE)))
+#endif
+msda_bwd_window_kernel(const float* __restrict__ loc,
                                                              const float* __restrict__ attw,
                                                              const T* __restrict__ gout, float* __restrict__ gvalue,
                                                              Levels lv, QueryTiles qt, int S, int Hh, int Q, int L,

@@ -32,6 +32,10 @@ SIGNATURES = {
     "vs_msda_backward_sorted": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_msda_backward_tiled_workspace_bytes": [_c_int] * 5 + [_P],
     "vs_msda_backward_tiled": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
+    "vs_msda_prep_forward": [_c_int, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P, _P,
+                             _P] + [_c_int] * 5 + [_P],
+    "vs_msda_prep_backward": [_c_int, _P, _P, _P, _P, _P, ctypes.c_longlong, _P, ctypes.c_longlong] + [_c_int] * 5
+                             + [_P],
     "vs_window_partition": [_P, _P] + [_c_int] * 7 + [_P],
     "vs_window_reverse": [_P, _P] + [_c_int] * 7 + [_P],
     "vs_window_attn_forward": [_c_int, _P, _P, _P, _P] + [_c_int] * 6 + [_c_float, _P],

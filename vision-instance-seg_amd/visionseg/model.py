@@ -246,6 +246,9 @@ def reference_points(shapes, B, device, dtype=torch.float32):
     return r[:, :, None].expand(B, -1, len(shapes), -1)
 
 
+_MSDA_PREP = os.environ.get("VS_MSDA_PREP", "1") == "1"          # A/B switch: fused prologue
+
+
 class MSDeformAttn(nn.Module):
     def __init__(self, d, heads, levels, points):
         super().__init__()
@@ -263,10 +266,14 @@ class MSDeformAttn(nn.Module):
         B, S, _ = h.shape
         q = h + pos
         value = self.value_proj(h).view(B, S, self.heads, self.d // self.heads)
-        off = self.sampling_offsets(q).view(B, S, self.heads, self.levels, self.points, 2)
-        aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
-        aw = F.softmax(aw.float(), -1).view(B, S, self.heads, self.levels, self.points)
-        loc = ref[:, :, None, :, None, :] + off.float() / norm           # HF:m2f:994-1002
+        if _MSDA_PREP:                       # one HIP kernel each way (csrc/msda_prep.hip)
+            loc, aw = ops.msda_prep(self.sampling_offsets(q), self.attention_weights(q), ref, shapes,
+                                    self.heads, self.points)
+        else:
+            off = self.sampling_offsets(q).view(B, S, self.heads, self.levels, self.points, 2)
+            aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
+            aw = F.softmax(aw.float(), -1).view(B, S, self.heads, self.levels, self.points)
+            loc = ref[:, :, None, :, None, :] + off.float() / norm           # HF:m2f:994-1002
         out = ops.ms_deform_attn(value, shapes, loc, aw, encoder=self.encoder_backward)
         return self.output_proj(out)
 

@@ -141,6 +141,69 @@ def ms_deform_attn(value, spatial_shapes, sampling_locations, attention_weights,
     return MSDeformAttnFunction.apply(value, shapes, None, sampling_locations, attention_weights, 64, encoder)
 
 
+class MSDAPrepFunction(torch.autograd.Function):
+    """(offsets [B,Q,H*L*P*2], logits [B,Q,H*L*P], ref [B,Q,L,2] f32) -> (sampling
+    locations [B,Q,H,L,P,2] f32, attention weights [B,Q,H,L,P] f32) as
+    `ref + offsets.float() / (W_l, H_l)` and `softmax(logits.float())` over L*P
+    (HF:m2f:994-1002; csrc/msda_prep.hip).  ref gets no gradient (a buffer)."""
+
+    @staticmethod
+    def forward(ctx, off, logits, ref, shapes, heads, points):
+        L.require_hip(off, logits, ref)
+        B, Q = off.shape[0], off.shape[1]
+        nl = len(shapes)
+        lp = nl * points
+        if off.dtype != logits.dtype:
+            raise ValueError("offsets / logits dtypes differ")
+        if off.shape[-1] != heads * lp * 2 or logits.shape[-1] != heads * lp:
+            raise ValueError(f"projection widths {off.shape[-1]}, {logits.shape[-1]} != {heads * lp * 2}, "
+                             f"{heads * lp}")
+        n_off, n_lg = heads * lp * 2, heads * lp
+        off2 = off.reshape(B * Q, n_off) if off.stride(-1) == 1 else off.contiguous().view(B * Q, n_off)
+        lg2 = logits.reshape(B * Q, n_lg) if logits.stride(-1) == 1 else logits.contiguous().view(B * Q, n_lg)
+        if B * Q and (off2.stride(1) != 1 or lg2.stride(1) != 1 or off2.stride(0) < n_off or lg2.stride(0) < n_lg):
+            off2, lg2 = off2.contiguous(), lg2.contiguous()
+        ref = ref.float()
+        if tuple(ref.shape) != (B, Q, nl, 2):
+            raise ValueError(f"reference points {tuple(ref.shape)} != {(B, Q, nl, 2)}")
+        if ref.stride(3) != 1 or ref.stride(2) != 2 or ref.stride(1) != 2 * nl:
+            ref = ref.contiguous()
+        loc = torch.empty(B, Q, heads, nl, points, 2, device=off.device, dtype=torch.float32)
+        aw = torch.empty(B, Q, heads, nl, points, device=off.device, dtype=torch.float32)
+        sh, _, _ = _level_arrays(shapes)
+        with timed("msda_prep_fwd", off, bytes_=(off.numel() + logits.numel()) * off.element_size()
+                   + (loc.numel() + aw.numel()) * 4):
+            L.check(L.lib().vs_msda_prep_forward(L.dtype_code(off), L.ptr(off2), max(off2.stride(0), n_off),
+                                                 L.ptr(lg2), max(lg2.stride(0), n_lg), L.ptr(ref), ref.stride(0), sh, L.ptr(loc), L.ptr(aw),
+                                                 B, Q, heads, nl, points, L.stream(off)), "msda_prep_forward")
+        ctx.save_for_backward(aw)
+        ctx.geom = (B, Q, heads, nl, points, off.dtype, tuple(shapes))
+        return loc, aw
+
+    @staticmethod
+    def backward(ctx, gloc, gaw):
+        (aw,) = ctx.saved_tensors
+        B, Q, heads, nl, points, dt, shapes = ctx.geom
+        lp = nl * points
+        gloc = aw.new_zeros(*aw.shape, 2) if gloc is None else gloc.float().contiguous()
+        gaw = torch.zeros_like(aw) if gaw is None else gaw.float().contiguous()
+        goff = torch.empty(B, Q, heads * lp * 2, device=aw.device, dtype=dt)
+        glg = torch.empty(B, Q, heads * lp, device=aw.device, dtype=dt)
+        sh, _, _ = _level_arrays(shapes)
+        with timed("msda_prep_bwd", aw, bytes_=(gloc.numel() + gaw.numel() + aw.numel()) * 4
+                   + (goff.numel() + glg.numel()) * goff.element_size()):
+            L.check(L.lib().vs_msda_prep_backward(L.dtype_code(goff), L.ptr(gloc), L.ptr(gaw), L.ptr(aw), sh,
+                                                  L.ptr(goff), goff.shape[-1], L.ptr(glg), glg.shape[-1], B, Q, heads,
+                                                  nl, points, L.stream(aw)), "msda_prep_backward")
+        return goff, glg, None, None, None, None
+
+
+def msda_prep(offsets, logits, ref, spatial_shapes, heads: int, points: int):
+    """Sampling locations and attention weights of MSDeformAttn from its two projections
+    (see MSDAPrepFunction)."""
+    return MSDAPrepFunction.apply(offsets, logits, ref, _shapes_list(spatial_shapes), int(heads), int(points))
+
+
 def _padded(n, ws):
     return n + (ws - n % ws) % ws
 
