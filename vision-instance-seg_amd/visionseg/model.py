@@ -267,8 +267,12 @@ class MSDeformAttn(nn.Module):
         q = h + pos
         value = self.value_proj(h).view(B, S, self.heads, self.d // self.heads)
         if _MSDA_PREP:                       # one HIP kernel each way (csrc/msda_prep.hip)
-            loc, aw = ops.msda_prep(self.sampling_offsets(q), self.attention_weights(q), ref, shapes,
-                                    self.heads, self.points)
+            # both projections of q as one GEMM (q read once, one dX GEMM, no add of
+            # their input gradients); the prologue reads the two column ranges as views
+            so, at = self.sampling_offsets, self.attention_weights
+            proj = linear_tokens(q, torch.cat((so.weight, at.weight)), torch.cat((so.bias, at.bias)))
+            n_off = so.out_features
+            loc, aw = ops.msda_prep(proj[..., :n_off], proj[..., n_off:], ref, shapes, self.heads, self.points)
         else:
             off = self.sampling_offsets(q).view(B, S, self.heads, self.levels, self.points, 2)
             aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
