@@ -131,7 +131,8 @@ VS_API int vs_msda_backward_tiled(int dtype, const void* value, const int64_t* s
  *   attw[b,q,h,:]    = softmax_{L*P}(logits[b,q,h,:])                        (f32 out)
  * offsets [B,Q,H*L*P*2] / logits [B,Q,H*L*P] in dtype with row strides (elements) >= a
  * row (views of one fused projection allowed); ref f32 [B,Q,L,2] with rows contiguous
- * and batch stride ref_batch_stride (0: shared by the batch); loc / attw contiguous.
+ * and batch stride ref_batch_stride (even; 0: shared by the batch); loc / attw contiguous;
+ * ref, loc (and, backward, grad_loc) 8-byte aligned.
  * L <= 4, L*P <= 32. */
 VS_API int vs_msda_prep_forward(int dtype, const void* offsets, long long offsets_row_stride, const void* logits,
                                 long long logits_row_stride, const float* ref, long long ref_batch_stride,

@@ -44,14 +44,15 @@ __global__ void __launch_bounds__(256) msda_prep_fwd_kernel(const T* __restrict_
   const int c0 = (int)(e0 - bq0 * rowe);
   const long long b0 = bq0 / Q;
   const int q0 = (int)(bq0 - b0 * Q);
-  for (int e = threadIdx.x; e < ng * LP * 2; e += 256) {
+  for (int e = 2 * threadIdx.x; e < ng * LP * 2; e += 512) {     // one (x, y) pair per thread
     const int t = c0 + e;
     const int dr = t / rowe, c = t - dr * rowe;
     const int qq = q0 + dr;
     const int db = qq / Q, q = qq - db * Q;
-    const int xy = c & 1, l = (c >> 1) / P % L;
-    const float r = ref[(b0 + db) * ref_bs + ((long long)q * L + l) * 2 + xy];
-    loc[e0 + e] = r + to_f32(off[(bq0 + dr) * off_rs + c]) / (xy ? gm.h[l] : gm.w[l]);
+    const int l = (c >> 1) / P % L;
+    const float2 r = *reinterpret_cast<const float2*>(ref + (b0 + db) * ref_bs + ((long long)q * L + l) * 2);
+    const T* o = off + (bq0 + dr) * off_rs + c;
+    *reinterpret_cast<float2*>(loc + e0 + e) = make_float2(r.x + to_f32(o[0]) / gm.w[l], r.y + to_f32(o[1]) / gm.h[l]);
   }
   // softmax weights
   const int rowl = Hh * LP;
@@ -95,11 +96,14 @@ __global__ void __launch_bounds__(256) msda_prep_bwd_kernel(const float* __restr
   const long long e0 = g0 * LP * 2;
   const long long bq0 = e0 / rowe;
   const int c0 = (int)(e0 - bq0 * rowe);
-  for (int e = threadIdx.x; e < ng * LP * 2; e += 256) {
+  for (int e = 2 * threadIdx.x; e < ng * LP * 2; e += 512) {     // one (x, y) pair per thread
     const int t = c0 + e;
     const int dr = t / rowe, c = t - dr * rowe;
-    const int xy = c & 1, l = (c >> 1) / P % L;
-    goff[(bq0 + dr) * goff_rs + c] = from_f32<T>(gloc[e0 + e] / (xy ? gm.h[l] : gm.w[l]));
+    const int l = (c >> 1) / P % L;
+    const float2 gv = *reinterpret_cast<const float2*>(gloc + e0 + e);
+    T* o = goff + (bq0 + dr) * goff_rs + c;
+    o[0] = from_f32<T>(gv.x / gm.w[l]);
+    o[1] = from_f32<T>(gv.y / gm.h[l]);
   }
   const long long f0 = g0 * LP;
   for (int e = threadIdx.x; e < ng * LP; e += 256) {
@@ -153,6 +157,8 @@ extern "C" int vs_msda_prep_forward(int dtype, const void* offsets, long long of
   const long long groups = (long long)B * Q * Hh;
   if (groups == 0) return VS_OK;
   VS_CHECK(offsets && logits && ref && loc && attw, "null pointer");
+  VS_CHECK(((uintptr_t)ref & 7) == 0 && ref_batch_stride % 2 == 0 && ((uintptr_t)loc & 7) == 0,
+           "ref / loc must be 8-byte aligned with an even batch stride");
   hipStream_t st = (hipStream_t)stream;
   const int grid = (int)((groups + kGroups - 1) / kGroups);
   if (dtype == VS_BF16)
@@ -182,6 +188,7 @@ extern "C" int vs_msda_prep_backward(int dtype, const float* grad_loc, const flo
   const long long groups = (long long)B * Q * Hh;
   if (groups == 0) return VS_OK;
   VS_CHECK(grad_loc && grad_attw && attw && grad_offsets && grad_logits, "null pointer");
+  VS_CHECK(((uintptr_t)grad_loc & 7) == 0, "grad_loc must be 8-byte aligned");
   hipStream_t st = (hipStream_t)stream;
   const int grid = (int)((groups + kGroups - 1) / kGroups);
   if (dtype == VS_BF16)

@@ -166,7 +166,8 @@ class MSDAPrepFunction(torch.autograd.Function):
         ref = ref.float()
         if tuple(ref.shape) != (B, Q, nl, 2):
             raise ValueError(f"reference points {tuple(ref.shape)} != {(B, Q, nl, 2)}")
-        if ref.stride(3) != 1 or ref.stride(2) != 2 or ref.stride(1) != 2 * nl:
+        if (ref.stride(3) != 1 or ref.stride(2) != 2 or ref.stride(1) != 2 * nl or ref.stride(0) % 2
+                or ref.data_ptr() % 8):
             ref = ref.contiguous()
         loc = torch.empty(B, Q, heads, nl, points, 2, device=off.device, dtype=torch.float32)
         aw = torch.empty(B, Q, heads, nl, points, device=off.device, dtype=torch.float32)
