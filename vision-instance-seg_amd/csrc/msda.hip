@@ -1008,7 +1008,15 @@ void sorted_layout(long long nkeys, long long maxrec, size_t* off) {
 #define VS_MSDA_WIN_CELLS 96
 #endif
 constexpr int kWinCells = VS_MSDA_WIN_CELLS;   // LDS window capacity (cells x 16 ch f32 = 6 KB)
-constexpr int kTE = 4, kTQ = kTE * kTE;  // query tile edge / queries per tile
+#ifndef VS_MSDA_TX
+#define VS_MSDA_TX 4
+#endif
+#ifndef VS_MSDA_TY
+#define VS_MSDA_TY 4
+#endif
+constexpr int kTX = VS_MSDA_TX, kTY = VS_MSDA_TY;   // query tile width / height (grid mode)
+constexpr int kTQ = kTX * kTY;                      // queries per tile (a power of two <= 64)
+static_assert((kTQ & (kTQ - 1)) == 0 && kTQ >= 4 && kTQ <= 64, "query tile must hold 4..64 queries, a power of 2");
 constexpr int kWinC = 16;                // channels per workgroup (a head's 32 split over two)
 
 struct QueryTiles {
@@ -1027,7 +1035,7 @@ __device__ __forceinline__ int tile_query(const QueryTiles& qt, const Levels& lv
   int lq = 0;
   while (lq + 1 < L && tile >= qt.prefix[lq + 1]) ++lq;
   const int t = tile - qt.prefix[lq];
-  const int y = (t / qt.ntx[lq]) * kTE + idx / kTE, x = (t % qt.ntx[lq]) * kTE + idx % kTE;
+  const int y = (t / qt.ntx[lq]) * kTY + idx / kTX, x = (t % qt.ntx[lq]) * kTX + idx % kTX;
   return (y < lv.h[lq] && x < lv.w[lq]) ? lv.start[lq] + y * lv.w[lq] + x : -1;
 }
 
@@ -1351,8 +1359,8 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     qt.prefix[0] = 0;
     for (int l = 0; l < kMaxLevels; ++l) {
       const bool on = qt.mode == 1 && l < L;
-      qt.ntx[l] = on ? (lv.w[l] + kTE - 1) / kTE : 1;
-      qt.prefix[l + 1] = qt.prefix[l] + (on ? ((lv.h[l] + kTE - 1) / kTE) * qt.ntx[l] : 0);
+      qt.ntx[l] = on ? (lv.w[l] + kTX - 1) / kTX : 1;
+      qt.prefix[l + 1] = qt.prefix[l] + (on ? ((lv.h[l] + kTY - 1) / kTY) * qt.ntx[l] : 0);
     }
     qt.per_image = qt.mode == 1 ? qt.prefix[L] : (Q + kTQ - 1) / kTQ;
     const long long nblk = 2LL * B * qt.per_image * Hh;
