@@ -5,13 +5,18 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Metric (BASELINE.json): images/sec at 1024^2, Swin-T Mask2Former, 1/2/4/8 GPUs.  A step
-is one full training iteration (bf16 autocast forward, set criterion with Hungarian
-matching, backward, RCCL gradient all-reduce when N>1, per-parameter grad clip, AdamW)
+is one full training iteration (bf16 forward with bf16 parameters and f32 master weights,
+set criterion with device Hungarian matching, backward, bucketed f32 RCCL gradient
+all-reduce overlapped with backward when N>1, per-parameter grad clip, SGD momentum --
+the reference's detectron2 solver)
 on a synthetic COCO-format defect batch of `--batch` images per GPU, resident in HBM
 before the timed region.  Weak scaling: per-GPU batch fixed.  Rank 0 prints ONE JSON
 line; `roofline` covers the dominant hand-written kernel (HIP events on its launch
-stream, algorithmic bytes/flops per launch); `cpu_baseline` times the oracle CPU
-restatement (fp32, fwd+loss+bwd) on the host cores on a bounded sample.
+stream, algorithmic bytes/flops per launch), `step_roofline` the whole step against the
+bf16 MFMA peak (algorithmic training FLOPs per image); `cpu_baseline`
+times the oracle CPU restatement (fp32) on the host cores on a bounded sample
+(BASELINE.md §3); `parity` is the mask-logit error vs the oracle in fp32 kernel mode and
+on the production bf16 path.
 """
 from __future__ import annotations
 
@@ -70,22 +75,32 @@ def parse():
     ap.add_argument("--matcher", default="device", choices=["device", "host"],
                     help="Hungarian matching on the device (csrc/match.hip) or scipy on the host")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=2)
+    ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--kernel-timing", type=int, default=1,
                     help="HIP-event per-kernel timing (graphs: over --timing-steps eager steps after the timed region)")
     ap.add_argument("--graphs", type=int, default=1, help="replay the step as HIP graphs (Trainer(graphs=True))")
     ap.add_argument("--timing-steps", type=int, default=2, help="eager steps for per-kernel timing in graph mode")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "amp"],
                     help="bf16: bf16 params/activations + f32 master weights; amp: f32 params + bf16 autocast")
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adamw"],
+                    help="sgd: the reference's detectron2 DefaultTrainer solver; adamw: upstream train_net")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--gemm-tuning", default="file", choices=["file", "tune", "off"],
                     help="vendor GEMM solution table: in-tree TunableOp file (default), re-tune, or heuristics")
     return ap.parse_args()
 
 
 # HBM traffic per op launch from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; KiB,
-# FETCH x2 on gfx950 -- tools/pmc_traffic.py), committed under profiles/; the kernels
-# each timed op dispatches once per launch
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+# FETCH x2 on gfx950 -- tools/pmc_traffic.py), committed under profiles/ PER CONFIG
+# (profiles/pmc_traffic_<model>_<size>.json); the kernels each timed op dispatches once
+# per launch.  No file for the config -> traffic null.
+PMC_DIR = os.path.join(ROOT, "profiles")
+
+
+def pmc_file(model, size):
+    return os.path.join(PMC_DIR, f"pmc_traffic_{model}_{size}.json")
+
+
 OP_KERNELS = {
     "msda_bwd": ["msda_bwd_geom_kernel", "msda_bwd_window_kernel"],
     "msda_fwd": ["msda_fwd_kernel"],
@@ -98,11 +113,11 @@ OP_KERNELS = {
 }
 
 
-def pmc_traffic(op):
+def pmc_traffic(op, path):
     """(bytes per launch, kernels counted) of `op` from the committed PMC profile, or None."""
-    if op not in OP_KERNELS or not os.path.exists(PMC_FILE):
+    if op not in OP_KERNELS or not os.path.exists(path):
         return None, None
-    rows = json.load(open(PMC_FILE))
+    rows = json.load(open(path))
     tot, used = 0.0, []
     for pat in OP_KERNELS[op]:
         hits = [(k, v) for k, v in rows.items() if pat + "<" in k or pat + "(" in k]
@@ -114,7 +129,7 @@ def pmc_traffic(op):
     return int(tot), used
 
 
-def kernel_roofline(summary):
+def kernel_roofline(summary, pmc_path):
     """Pick the hand-written kernel with the largest total time and price it against the
     roofline of its regime (HBM bytes for gather/copy kernels, matrix FLOP/s otherwise)."""
     if not summary:
@@ -125,16 +140,16 @@ def kernel_roofline(summary):
     hbm_kernels = {"msda_fwd", "msda_bwd", "window_partition", "window_reverse", "attn_bitmask", "mask_head_fwd"}
     if name in hbm_kernels:
         ach = s["bytes"] / t / 1e9
-        traffic, kernels = pmc_traffic(name)
+        traffic, kernels = pmc_traffic(name, pmc_path)
         roof = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, kernel=name,
-                    traffic_source=(f"profiles/{os.path.basename(PMC_FILE)}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) "
+                    traffic_source=(f"profiles/{os.path.basename(pmc_path)}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) "
                                     f"+ WRITE_SIZE per launch of {kernels}") if traffic else None,
                     algorithmic_bytes_per_launch=int(s["bytes"]), mean_launch_ms=round(s["mean_ms"], 4),
                     launches=s["launches"])
     else:
         ach = s["flops"] / t / 1e12
-        traffic, kernels = pmc_traffic(name)
+        traffic, kernels = pmc_traffic(name, pmc_path)
         roof = dict(bound="mfma", achieved=round(ach, 2), peak=MFMA_BF16_PEAK_TFS, unit="TFLOP/s",
                     frac=round(ach / MFMA_BF16_PEAK_TFS, 5), traffic=traffic, kernel=name,
                     algorithmic_flops_per_launch=int(s["flops"]), mean_launch_ms=round(s["mean_ms"], 4),
@@ -146,41 +161,85 @@ def kernel_roofline(summary):
     return roof, table
 
 
+def _cpu_model_name():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(model_name, size, iters, queries):
-    """Oracle CPU restatement (fp32), 1 image, forward + loss + backward, median of `iters`
-    after one warm-up; images/s on this host's cores."""
+    """the oracle CPU restatement (fp32) on this host's cores, median of
+    `iters` after one warm-up, images/s, for (a) C1 = 2x512^2 forward+loss and (b) one
+    `size`^2 image forward+loss+backward (the like-for-like training sample; its rate is
+    `value`).  Threads = the CPUs this process may run on (its affinity set: the box's CPU
+    share), reported with os.cpu_count() and the CPU model."""
     from oracle.ref_model import RefConfig, RefMask2Former, RefCriterion
     from visionseg.model import M2FConfig
     from visionseg.data import synthetic_batch
-    mc = M2FConfig.preset(model_name, num_queries=queries)
-    cfg = RefConfig.from_dict(mc.to_dict())
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    cfg = RefConfig.from_dict(M2FConfig.preset(model_name, num_queries=queries).to_dict())
     torch.manual_seed(0)
     m = RefMask2Former(cfg)
     crit = RefCriterion(cfg)
-    imgs, ml, cl = synthetic_batch(1, size, seed=42)
-    ml = [x.float() for x in ml]
-    ts = []
-    for i in range(iters + 1):
-        t0 = time.perf_counter()
-        masks, classes = m(imgs)
-        loss, _ = crit(masks, classes, ml, cl)
-        loss.backward()
-        m.zero_grad(set_to_none=True)
-        if i > 0:
-            ts.append(time.perf_counter() - t0)
-    ts.sort()
-    med = ts[len(ts) // 2]
-    return dict(value=round(1.0 / med, 4), unit="images/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"1x3x{size}^2 {model_name} Mask2Former fp32 fwd+loss+bwd (oracle CPU restatement), "
-                       f"median of {iters} iters after 1 warm-up, {med:.1f} s/iter")
+
+    def run(batch, sz, backward):
+        imgs, ml, cl = synthetic_batch(batch, sz, seed=42)
+        ml = [x.float() for x in ml]
+        ts = []
+        for i in range(iters + 1):
+            t0 = time.perf_counter()
+            if backward:
+                masks, classes = m(imgs)
+                loss, _ = crit(masks, classes, ml, cl)
+                loss.backward()
+                m.zero_grad(set_to_none=True)
+            else:
+                with torch.no_grad():
+                    masks, classes = m(imgs)
+                    crit(masks, classes, ml, cl)
+            if i > 0:
+                ts.append(time.perf_counter() - t0)
+        ts.sort()
+        med = ts[len(ts) // 2]
+        return batch / med, med
+
+    c1, c1_t = run(2, 512, False)
+    v, t = run(1, size, True)
+    torch.set_num_threads(prev)
+    return dict(value=round(v, 4), unit="images/s", cores=threads, kind="port",
+                sample=f"1x3x{size}^2 {model_name} Mask2Former fp32 forward+loss+backward (oracle CPU restatement), "
+                       f"median of {iters} iters after 1 warm-up, {t:.2f} s/iter",
+                c1_forward_loss=dict(value=round(c1, 4), unit="images/s",
+                                     sample=f"C1: 2x3x512^2 forward+loss, median of {iters} after 1 warm-up, "
+                                            f"{c1_t:.2f} s/iter"),
+                host=dict(cpu_model=_cpu_model_name(), os_cpu_count=os.cpu_count(), threads_used=threads))
+
+
+def _bf16_round_(model):
+    with torch.no_grad():
+        for p in model.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    return model
 
 
 def parity_check(model_name, size, queries, dev):
-    """BASELINE metric, second half: mask-logit max-abs-err of the GPU path (fp32 kernel
-    mode) vs the oracle CPU restatement on one `size`^2 image, same weights (init_weights
-    + perturbed tables/offsets so every path carries signal), every decoder step.  The
-    decoder's attention masks are threshold decisions; the number of mask bits that
-    differ from the oracle's (all at near-zero logits, tests/test_gpu_model.py) is reported."""
+    """BASELINE metric, second half: mask-logit max-abs-err vs the oracle CPU restatement
+    on one `size`^2 image, every decoder step, weights = init_weights + perturbed
+    tables/offsets (every path carries signal) rounded to bf16 so ONE oracle forward
+    serves both checks:
+      fp32: the GPU path in fp32 kernel mode, free-running (the decoder's attention masks
+            are threshold decisions; the mask bits that differ from the oracle's, all at
+            near-zero logits (tests/test_gpu_model.py), are counted);
+      bf16: the production path (bf16 parameters and activations, MFMA window and masked
+            attention, bf16 mask head) with the oracle's attention masks forced in (a
+            near-zero logit flips freely in bf16), error absolute and relative to the
+            step's max |logit|."""
     from oracle.ref_model import RefConfig, RefMask2Former
     from visionseg.model import M2FConfig, Mask2Former, unpack_bitmask_like
     cfg = M2FConfig.preset(model_name, num_queries=queries)
@@ -190,24 +249,48 @@ def parity_check(model_name, size, queries, dev):
         for n, p in m.named_parameters():
             if "rel_table" in n or "attention_weights" in n or "level_embed" in n:
                 p.add_(0.3 * torch.randn(p.shape, generator=g))
+    _bf16_round_(m)
     ref = RefMask2Former(RefConfig.from_dict(cfg.to_dict()))
     ref.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
     m = m.to(dev).eval()
     ref.eval()
-    px = torch.randn(1, 3, size, size, generator=torch.Generator().manual_seed(5))
+    px = torch.randn(1, 3, size, size, generator=torch.Generator().manual_seed(5)).to(torch.bfloat16).float()
     with torch.no_grad():
         ref.decoder.record = True
+        t0 = time.perf_counter()
         rmasks, _ = ref(px)
+        t_ref = time.perf_counter() - t0
         m.decoder.record = True
         masks, _ = m(px.to(dev))
         err = max(float((a.cpu() - b).abs().max()) for a, b in zip(masks, rmasks))
         flips = sum(int((unpack_bitmask_like(w, rb.shape[-1]).cpu() != rb).sum())
                     for (rb, _), w in zip(ref.decoder.trace, m.decoder.trace))
-    del m, ref
+        del masks
+        m = m.to(torch.bfloat16)
+        m.decoder.record = False
+        m.decoder.mask_override = [rb for rb, _ in ref.decoder.trace]
+        bmasks, _ = m(px.to(dev).to(torch.bfloat16))
+        abs_err = [float((a.float().cpu() - b).abs().max()) for a, b in zip(bmasks, rmasks)]
+        rel_err = [e / float(b.abs().max()) for e, b in zip(abs_err, rmasks)]
+        mean_err = max(float((a.float().cpu() - b).abs().mean()) for a, b in zip(bmasks, rmasks))
+        scale = max(float(b.abs().max()) for b in rmasks)
+    del m, ref, bmasks
     torch.cuda.empty_cache()
     return dict(mask_logit_max_abs_err=float(f"{err:.3e}"), tolerance=1e-3, attention_mask_bit_flips=flips,
-                sample=f"1x3x{size}^2 {model_name} Mask2Former, {queries} queries, fp32 kernel mode vs the oracle "
-                       f"CPU restatement, all {cfg.dec_layers} decoder steps")
+                bf16=dict(mask_logit_max_abs_err=float(f"{max(abs_err):.3e}"),
+                          max_rel_to_logit_scale=float(f"{max(rel_err):.3e}"),
+                          mean_abs_err=float(f"{mean_err:.3e}"), logit_scale=float(f"{scale:.3e}"),
+                          tolerance="max abs err <= 0.02 x max|logit| of the step (bf16 activations, "
+                                    "tests/test_gpu_model.py)", forced_attention_masks=True),
+                oracle_forward_s=round(t_ref, 2),
+                sample=f"1x3x{size}^2 {model_name} Mask2Former, {queries} queries, bf16-rounded weights and input, "
+                       f"vs the oracle CPU restatement (fp32), all {cfg.dec_layers} decoder steps")
+
+
+# Algorithmic training FLOPs per image (forward matmul/conv FLOPs x 3; forward counted
+# with torch.utils.flop_counter on the HF oracle) for the BASELINE configs
+TRAIN_FLOPS_PER_IMAGE = {("swin_t", 1024): 3 * 530.6e9, ("swin_b", 1024): 3 * 1022.2e9,
+                         ("swin_l", 1536): 3 * 3974.2e9}
 
 
 def _config_tag(model, size):
@@ -231,8 +314,8 @@ def main():
     dev = torch.device("cuda", local)
     cfg = M2FConfig.preset(a.model, num_queries=a.queries)
     model = Mask2Former(cfg).init_weights(seed=0)
-    trainer = Trainer(model, SetCriterion(cfg, matcher=a.matcher), SolverConfig(precision=a.precision), device=dev,
-                      graphs=bool(a.graphs))
+    trainer = Trainer(model, SetCriterion(cfg, matcher=a.matcher),
+                      SolverConfig(precision=a.precision, optimizer=a.optimizer), device=dev, graphs=bool(a.graphs))
     graphs = trainer.graphs
     images, ml, cl = synthetic_batch(a.batch, a.size, seed=42 + rank, device=dev)
     torch.cuda.synchronize()
@@ -259,7 +342,7 @@ def main():
         # of the same workload right after the timed region (outside it)
         timer.__enter__()
         for _ in range(max(1, a.timing_steps)):
-            trainer._eager_split_step(images, ml, cl) if trainer.split else trainer._eager_bf16_step(images, ml, cl)
+            trainer.eager_step(images, ml, cl)
         torch.cuda.synchronize()
     if timer:
         timer.__exit__(None, None, None)
@@ -270,30 +353,43 @@ def main():
     ms = elapsed / a.steps * 1e3
     value = a.batch * world * a.steps / elapsed
     if rank == 0:
-        roof, table = kernel_roofline(timer.summary()) if timer else (None, {})
+        roof, table = kernel_roofline(timer.summary(), pmc_file(a.model, a.size)) if timer else (None, {})
         cpu, parity = None, None
         if world == 1 and not a.no_cpu_baseline:
-            torch.set_num_threads(min(16, os.cpu_count() or 1))
             cpu = cpu_baseline(a.model, a.size, a.cpu_iters, a.queries)
+        if world == 1 and not a.no_parity:
             parity = parity_check(a.model, a.size, a.queries, dev)
+        fl = TRAIN_FLOPS_PER_IMAGE.get((a.model, a.size))
+        step_roof = None
+        if fl:
+            ach = fl * value / 1e12
+            step_roof = dict(bound="mfma", achieved=round(ach, 1), peak=MFMA_BF16_PEAK_TFS * world, unit="TFLOP/s",
+                             frac=round(ach / (MFMA_BF16_PEAK_TFS * world), 4),
+                             algorithmic_flops_per_image=fl,
+                             note="whole training step: 3 x forward matmul/conv FLOPs (BASELINE.md §2) x images/s "
+                                  "/ (dense bf16 MFMA peak x GPUs)")
+        prec = ("bf16 parameters and activations, f32 master weights, gradients reduced and applied in f32 "
+                "(pure bf16, not autocast)" if a.precision == "bf16" else "f32 parameters + bf16 autocast")
         line = {
             "metric": f"images/sec @{a.size}^2 {MODEL_NAMES.get(a.model, a.model)} Mask2Former training "
-                      "(fwd+loss+bwd+AdamW)",
+                      f"(fwd+loss+bwd+{a.optimizer.upper()})",
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic COCO-format defect batches (random-init weights)",
-            "config": {"workload": f"{_config_tag(a.model, a.size)}: {a.model} + Mask2Former, {a.batch}x3x{a.size}^2 per GPU, "
-                                   f"{cfg.num_queries} queries, bf16 autocast, 1 class",
+            "config": {"workload": f"{_config_tag(a.model, a.size)}: {a.model} + Mask2Former, {a.batch}x3x{a.size}^2 "
+                                   f"per GPU, {cfg.num_queries} queries, {prec}, 1 class",
                        "model": f"{a.model}_mask2former", "global_batch": a.batch * world, "image_size": a.size,
                        "parallelism": f"dp{world}"},
             "final_loss": round(float(loss.item()), 4),
             "gemm_tuning": a.gemm_tuning,
             "precision": a.precision,
+            "optimizer": a.optimizer,
             "matcher": a.matcher,
             "graphs": graphs,
             "kernel_timing": ("HIP events over %d eager steps after the timed region" % max(1, a.timing_steps))
             if graphs else "HIP events over the timed region",
             "roofline": roof,
+            "step_roofline": step_roof,
             "cpu_baseline": cpu,
             "parity": parity,
             "kernels": table,

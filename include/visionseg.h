@@ -261,15 +261,40 @@ VS_API long long vs_column_sum_workspace_bytes(int rows, int cols);
 VS_API int vs_column_sum(int dtype, const void* x, void* out, void* workspace, int rows, int cols,
                          void* stream);
 
-/* ---- Per-parameter gradient clipping (csrc/optim.hip) --------------------------------
- * detectron2 "norm" clipping (reference training/maskdino/train_full.py:266-271:
- * clip_grad_norm_(p, 0.01) for every parameter p) over a flat f32 gradient buffer whose
- * parameters start 16-B aligned.  table: device int32 [num_chunks][4] = {start, len,
- * first chunk of the parameter, chunks of the parameter}, chunks of one parameter
- * consecutive.  g *= min(1, max_norm / (||g_param||_2 + eps)), deterministic. */
-VS_API long long vs_segment_clip_workspace_bytes(int num_chunks);
-VS_API int vs_segment_clip(float* data, const int* table, int num_chunks, float max_norm, float eps,
-                           void* workspace, void* stream);
+/* ---- Fused optimiser step over flat buffers (csrc/optim.hip) --------------------------
+ * Replaces detectron2's clipped optimiser step as the reference runs it
+ * (training/maskdino/train_full.py:153-167 DefaultTrainer.build_optimizer -> torch SGD,
+ * momentum 0.9, weight decay 0.05 / 0 on norm parameters; CLIP_GRADIENTS "norm" 0.01 =
+ * clip_grad_norm_(p, 0.01) per parameter, :266-271), or upstream Mask2Former/MaskDINO's
+ * AdamW.  All buffers are flat device arrays over the same element index:
+ *   grad      [total] f32 or bf16 (grad_dtype), scaled by grad_scale (1/world: summed
+ *             gradients -> mean) before clipping;
+ *   master    [total] f32 weights, state1 [total] f32 (SGD momentum / Adam exp_avg),
+ *   state2    [total] f32 (Adam exp_avg_sq; unused, may be NULL, for SGD);
+ *   weights_bf16 [total] bf16 working weights written from the updated master (or NULL).
+ * table: int32 [num_chunks][4] = {start (multiple of 8), len, first chunk of the
+ * parameter, chunks of the parameter}; hyper: f32 [num_chunks][2] = {lr multiplier,
+ * weight decay}.  optimizer 0 = SGD (torch semantics: d = g + wd*p; buf = d on the first
+ * step, else momentum*buf + d; p -= lr*buf), 1 = AdamW (torch semantics).  clip 0 = none,
+ * 1 = per parameter, 2 = one global norm; scale = min(1, clip_value / (norm + clip_eps)).
+ * lr: device f32 scalar (base lr, scheduler-owned); step: device f32 counter, advanced by
+ * one at the start of the call (step == 1 is the first step).  Deterministic; 2 launches. */
+VS_API long long vs_flat_step_workspace_bytes(int num_chunks);
+VS_API int vs_flat_step(int grad_dtype, const void* grad, float grad_scale, float* master, float* state1,
+                        float* state2, void* weights_bf16, const int* table, const float* hyper, int num_chunks,
+                        int optimizer, int clip, float clip_value, float clip_eps, float momentum, float beta1,
+                        float beta2, float eps, const float* lr, float* step, void* workspace, void* stream);
+
+/* ---- In-graph external events (csrc/stream.hip) ----------------------------------------
+ * For the gradient all-reduce overlapped with a graph-replayed backward (no reference
+ * counterpart: the reference's DDP all-reduce is eager, detectron2 create_ddp_model).
+ * vs_event_record_external records `event` on `stream` with hipEventRecordExternal: under
+ * stream capture it becomes an event-record node of the graph, fired when the replay
+ * reaches it; vs_stream_wait_event makes `stream` wait on the event's last record. */
+VS_API int vs_event_create(void** event);
+VS_API int vs_event_destroy(void* event);
+VS_API int vs_event_record_external(void* event, void* stream);
+VS_API int vs_stream_wait_event(void* stream, void* event);
 
 /* ---- Hungarian matching on the device (csrc/match.hip) -------------------------------
  * Replaces scipy.optimize.linear_sum_assignment(cost.cpu()) of the set-criterion matcher

@@ -286,13 +286,13 @@ class RefPixelDecoder(nn.Module):
         embeds, pos = [], []
         for lvl, x in enumerate(feats[::-1][:3]):                     # HF:m2f:1328-1332
             embeds.append(self.input_proj[lvl](x))
-            pos.append(R.sine_pos_embed(x.shape[0], x.shape[2], x.shape[3], F_ // 2))
+            pos.append(R.sine_pos_embed(x.shape[0], x.shape[2], x.shape[3], F_ // 2).to(x.dtype))
         shapes = [(e.shape[2], e.shape[3]) for e in embeds]
         h = torch.cat([e.flatten(2).transpose(1, 2) for e in embeds], 1)
         p = torch.cat([q.flatten(2).transpose(1, 2) + self.level_embed[i].view(1, 1, -1)
                        for i, q in enumerate(pos)], 1)
         B = h.shape[0]
-        ref = R.reference_points(shapes, B)
+        ref = R.reference_points(shapes, B).to(h.dtype)
         for layer in self.encoder:
             h = layer(h, p, ref, shapes)
         outs, s = [], 0
@@ -400,16 +400,17 @@ class RefDecoder(nn.Module):
         for i in range(3):
             f = ms_feats[i]
             sizes.append(tuple(f.shape[-2:]))
-            mposs.append(R.sine_pos_embed(B, f.shape[2], f.shape[3], d // 2).flatten(2).transpose(1, 2))
+            mposs.append(R.sine_pos_embed(B, f.shape[2], f.shape[3], d // 2).to(f.dtype).flatten(2).transpose(1, 2))
             mems.append((f.flatten(2) + self.level_embed.weight[i][None, :, None]).transpose(1, 2))
         qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
         h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
         self.trace = []
         inter, logits, blocked = self.predict(h, mask_features, sizes[0])
         inters, masks = [inter], [logits]
+        override = getattr(self, "mask_override", None)      # test hook: forced mask decisions
         for idx, layer in enumerate(self.layers):
             lvl = idx % 3
-            blocked = R.unblock_full_rows(blocked)
+            blocked = R.unblock_full_rows(blocked) if override is None else override[idx]
             h = layer(h, qpos, mems[lvl], mposs[lvl], blocked)
             inter, logits, blocked = self.predict(h, mask_features, sizes[(idx + 1) % 3])
             inters.append(inter)
@@ -471,8 +472,14 @@ def _pair_dice(inputs, labels):
 class RefCriterion:
     """HF:m2f:378-794 with scipy's linear_sum_assignment (CPU)."""
 
-    def __init__(self, cfg: RefConfig):
+    def __init__(self, cfg: RefConfig, point_source=None):
+        """point_source: None (torch.rand in HF's draw order) or a test hook with
+        `match_points(B, P, device) -> [B,P,2]` and `loss_points(S, B, Kc, n, kind,
+        device) -> [S,B,Kc,n,2]` (kind "over" / "rand") in [0,1): draws keyed by (decoder
+        step, image, target) instead of by call order, so a criterion that batches its
+        draws differently (the product's) can be fed the very same points."""
         self.cfg = cfg
+        self.point_source = point_source
         self.empty_weight = torch.ones(cfg.num_labels + 1)
         self.empty_weight[-1] = cfg.no_object_weight
 
@@ -487,7 +494,10 @@ class RefCriterion:
             cost_class = -probs[:, class_labels[i]]
             tgt = mask_labels[i].to(masks)[:, None]
             pred = masks[i][:, None]
-            pts = torch.rand(1, c.train_num_points, 2, device=pred.device)
+            if self.point_source is not None:
+                pts = self.point_source.match_points(masks.shape[0], c.train_num_points, pred.device)[i][None]
+            else:
+                pts = torch.rand(1, c.train_num_points, 2, device=pred.device)
             tgt = _sample_point(tgt, pts.repeat(tgt.shape[0], 1, 1)).squeeze(1)
             pred = _sample_point(pred, pts.repeat(pred.shape[0], 1, 1)).squeeze(1)
             cost = c.mask_weight * _pair_bce(pred, tgt) + c.class_weight * cost_class + \
@@ -499,12 +509,18 @@ class RefCriterion:
             out.append((torch.as_tensor(a, dtype=torch.int64), torch.as_tensor(b, dtype=torch.int64)))
         return out
 
-    def _points(self, logits):
+    def _draw(self, kind, n, nb, keyed, device):
+        if keyed is None:
+            return torch.rand(nb, n, 2, device=device)
+        step, steps, bi, ti, kc, B = keyed
+        return self.point_source.loss_points(steps, B, kc, n, kind, device)[step, bi, ti]
+
+    def _points(self, logits, keyed=None):
         """HF:m2f:671-724."""
         c = self.cfg
         nb = logits.shape[0]
         ns = int(c.train_num_points * c.oversample_ratio)
-        coords = torch.rand(nb, ns, 2, device=logits.device)
+        coords = self._draw("over", ns, nb, keyed, logits.device)
         unc = -torch.abs(_sample_point(logits, coords))
         nu = int(c.importance_sample_ratio * c.train_num_points)
         nr = c.train_num_points - nu
@@ -512,10 +528,10 @@ class RefCriterion:
         idx = idx + (ns * torch.arange(nb, dtype=torch.long, device=logits.device))[:, None]
         coords = coords.view(-1, 2)[idx.view(-1), :].view(nb, nu, 2)
         if nr > 0:
-            coords = torch.cat([coords, torch.rand(nb, nr, 2, device=logits.device)], dim=1)
+            coords = torch.cat([coords, self._draw("rand", nr, nb, keyed, logits.device)], dim=1)
         return coords
 
-    def single(self, masks, classes, mask_labels, class_labels):
+    def single(self, masks, classes, mask_labels, class_labels, step=0, steps=1):
         c = self.cfg
         idx = self.match(masks, classes, mask_labels, class_labels)
         nm = torch.clamp(torch.as_tensor(float(sum(len(x) for x in class_labels))), min=1)
@@ -525,8 +541,12 @@ class RefCriterion:
         pred = masks[(bi, si)][:, None]
         # HF pads targets to the batch max (HF:m2f:529-542); equal sizes here
         tgt = torch.cat([mask_labels[i][t] for i, (_, t) in enumerate(idx)]).to(masks)[:, None]
+        keyed = None
+        if self.point_source is not None:
+            kc = max([len(t) for t in class_labels] + [1])
+            keyed = (step, steps, bi, ti, kc, masks.shape[0])
         with torch.no_grad():
-            pts = self._points(pred)
+            pts = self._points(pred, keyed)
             plab = _sample_point(tgt, pts).squeeze(1)
         plog = _sample_point(pred, pts).squeeze(1)
         loss_mask = F.binary_cross_entropy_with_logits(plog, plab, reduction="none").mean(1).sum() / nm
@@ -540,9 +560,10 @@ class RefCriterion:
     def __call__(self, masks, classes, mask_labels, class_labels):
         """HF:m2f:726-779 + weighting HF:m2f:2312-2321; final prediction first, then aux."""
         c = self.cfg
-        losses = dict(self.single(masks[-1], classes[-1], mask_labels, class_labels))
+        S = len(masks)
+        losses = dict(self.single(masks[-1], classes[-1], mask_labels, class_labels, S - 1, S))
         for i, (m, cl) in enumerate(zip(masks[:-1], classes[:-1])):
-            for k, v in self.single(m, cl, mask_labels, class_labels).items():
+            for k, v in self.single(m, cl, mask_labels, class_labels, i, S).items():
                 losses[f"{k}_{i}"] = v
         w = {"loss_cross_entropy": c.class_weight, "loss_mask": c.mask_weight, "loss_dice": c.dice_weight}
         for k in list(losses):

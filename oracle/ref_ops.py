@@ -107,7 +107,7 @@ def window_attention_ref(q, k, v, rel_table, ws: int, shift_mask=None, scale=Non
     if shift_mask is not None:
         nW = shift_mask.shape[0]
         s = s + shift_mask.unsqueeze(1).unsqueeze(0).expand(Bw // nW, -1, -1, -1, -1).reshape(Bw, 1, N, N)
-    p = torch.softmax(s, dim=-1, dtype=torch.float32)
+    p = torch.softmax(s, dim=-1, dtype=torch.float32).to(v.dtype)     # HF:swin:392
     o = torch.matmul(p, v)
     return o.transpose(1, 2).reshape(Bw, N, heads * d)
 

@@ -1,5 +1,9 @@
 """Data-parallel path on CPU: world_size-2 gloo processes vs one process on the global
-batch (gradient averaging equivalence, identical replicas, num_masks all-reduce)."""
+batch, through the product Trainer's flat gradient buffer and bucketed all-reduce
+(visionseg.optim.GradReducer, several buckets, an unused parameter), the f32 master
+update, identical replicas and the criterion's num_masks all-reduce.  The HIP optimiser
+kernel is replaced by its CPU emulation (tests/_flatref.py); everything else is the
+product host logic."""
 import os
 import socket
 
@@ -25,11 +29,13 @@ class TinyNet(torch.nn.Module):
         super().__init__()
         torch.manual_seed(0)
         self.conv = torch.nn.Conv2d(3, 8, 3, padding=1)
+        self.norm = torch.nn.GroupNorm(2, 8)
         self.q = torch.nn.Parameter(torch.randn(5, 8))
         self.cls = torch.nn.Linear(8, 2)
+        self.unused = torch.nn.Parameter(torch.randn(3))
 
     def forward(self, x):
-        f = self.conv(x)                                   # [B,8,H,W]
+        f = self.norm(self.conv(x))                        # [B,8,H,W]
         m = torch.einsum("qc,bchw->bqhw", self.q, f)
         c = self.cls(self.q).unsqueeze(0).expand(x.shape[0], -1, -1)
         return [m * 0.5, m], [c, c]
@@ -40,18 +46,29 @@ def _mse_criterion(masks, classes, ml, cl):
     return loss, {}
 
 
-def _worker(rank, world, port, data, out_q):
+def _solver(optimizer, clip):
+    from visionseg.train import SolverConfig
+    # tiny bucket cap: the 8 parameters land in several buckets
+    return SolverConfig(warmup_iters=0, amp=False, clip_type=clip, clip_value=0.05, optimizer=optimizer,
+                        lr=0.05, bucket_cap_mb=1e-4)
+
+
+def _worker(rank, world, port, data, optimizer, clip, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
-    from visionseg.train import Trainer, SolverConfig, init_distributed
+    import _flatref
+    from visionseg import optim
+    from visionseg.train import Trainer, init_distributed
     from visionseg.criterion import SetCriterion, PaddedTargets
     from visionseg.model import M2FConfig
+    optim.FlatOptimizer.step = _flatref.flat_step_reference
     init_distributed("gloo")
     x = data[rank:rank + 1]
-    tr = Trainer(TinyNet(), _mse_criterion, SolverConfig(warmup_iters=0, amp=False, clip_type="none"), device="cpu")
-    assert tr.distributed
-    tr.step(x, None, None)
-    flat = torch.cat([p.detach().flatten() for p in tr.model.parameters()])
+    tr = Trainer(TinyNet(), _mse_criterion, _solver(optimizer, clip), device="cpu")
+    assert tr.distributed and len(tr.opt.layout.buckets) > 2
+    for _ in range(3):
+        tr.step(x, None, None)
+    flat = tr.opt.master.detach().clone()
     # criterion num_masks is the global mean over ranks (upstream SetCriterion semantics)
     crit = SetCriterion(M2FConfig(num_queries=5))
     tg = PaddedTargets.from_lists([torch.zeros(rank + 1, 4, 4, dtype=torch.bool)],
@@ -62,15 +79,18 @@ def _worker(rank, world, port, data, out_q):
     dist.destroy_process_group()
 
 
-def test_ddp_matches_single_process():
-    from visionseg.train import Trainer, SolverConfig
+@pytest.mark.parametrize("optimizer,clip", [("sgd", "norm"), ("adamw", "full_model")])
+def test_ddp_matches_single_process(monkeypatch, optimizer, clip):
+    import _flatref
+    from visionseg import optim
+    from visionseg.train import Trainer
     torch.manual_seed(1)
     data = torch.randn(2, 3, 16, 16)
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, data, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, optimizer, clip, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
@@ -81,11 +101,55 @@ def test_ddp_matches_single_process():
     f0, f1 = torch.from_numpy(f0), torch.from_numpy(f1)
     assert torch.equal(f0, f1), "replicas diverged"
     assert n0 == n1 == pytest.approx(1.5)
-    # single process, global batch of 2: mean-reduced loss over per-image terms = DDP average
+    # single process, global batch of 2: mean-reduced loss over per-image terms = the
+    # average of the ranks' gradients
+    monkeypatch.setattr(optim.FlatOptimizer, "step", _flatref.flat_step_reference)
     tr = Trainer(TinyNet(), lambda m, c, a, b: (sum(_mse_criterion([mm[i:i + 1] for mm in m],
                                                                    [cc[i:i + 1] for cc in c], a, b)[0]
                                                     for i in range(2)) / 2, {}),
-                 SolverConfig(warmup_iters=0, amp=False, clip_type="none"), device="cpu", distributed=False)
-    tr.step(data, None, None)
-    ref = torch.cat([p.detach().flatten() for p in tr.model.parameters()])
+                 _solver(optimizer, clip), device="cpu", distributed=False)
+    for _ in range(3):
+        tr.step(data, None, None)
+    ref = tr.opt.master.detach()
     assert torch.allclose(f0, ref, atol=1e-6), float((f0 - ref).abs().max())
+    # the unused parameter received zero gradients: only weight decay moved it
+    assert not torch.equal(ref, torch.zeros_like(ref))
+
+
+def test_flat_layout_buckets_and_groups():
+    """Parameter groups (no decay on norm parameters; AdamW: none on embeddings and
+    relative-position tables, 0.1 lr on the backbone) and the flat layout: aligned,
+    non-overlapping, buckets contiguous and in backward order."""
+    from visionseg.optim import FlatLayout, param_hyper, ALIGN
+    from visionseg.train import SolverConfig
+    from oracle.ref_solver import ref_param_groups
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.backbone = torch.nn.Sequential(torch.nn.Linear(4, 5), torch.nn.LayerNorm(5))
+            self.emb = torch.nn.Embedding(7, 3)
+            self.head = torch.nn.Linear(5, 2)
+            self.gn = torch.nn.GroupNorm(1, 2)
+            self.backbone.rel_table = torch.nn.Parameter(torch.zeros(9, 2))
+
+    m = M()
+    for opt in ("sgd", "adamw"):
+        s = SolverConfig(optimizer=opt)
+        got = {n: (lrm * s.lr, wd) for n, _, lrm, wd in param_hyper(m, s)}
+        exp = {g["name"]: (g["lr"], g["weight_decay"]) for g in ref_param_groups(m, s.lr, s.weight_decay, opt)}
+        assert got.keys() == exp.keys()
+        for k in exp:
+            assert got[k] == pytest.approx(exp[k]), (opt, k)
+    lay = FlatLayout(param_hyper(m, SolverConfig()), bucket_cap_mb=40 * 4 / 2 ** 20)
+    end = 0
+    for (o, n) in lay.offsets:
+        assert o % ALIGN == 0 and o >= end
+        end = o + n
+    assert lay.entries[0][0] == "gn.bias"                   # reverse registration order
+    prev = 0
+    for lo, hi, ids in lay.buckets:
+        assert lo == prev and hi > lo
+        prev = hi
+        assert all(lay.bucket_of[i] == lay.buckets.index((lo, hi, ids)) for i in ids)
+    assert prev == lay.total and len(lay.buckets) > 1

@@ -45,7 +45,7 @@ def _compare(ta, tb, la, lb):
     for a, b in zip(la, lb):
         assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (la, lb)
     worst = 0.0
-    for pa, pb in zip(ta.params, tb.params):
+    for pa, pb in zip(ta.master_params(), tb.master_params()):
         d = float((pa.detach() - pb.detach()).abs().max())
         worst = max(worst, d / max(1e-3, float(pa.detach().abs().max())))
     assert worst < 5e-2, worst
@@ -58,16 +58,18 @@ def test_graph_step_matches_eager():
     cfg, model, crit, b1, b2 = _setup()
     ta = Trainer(copy.deepcopy(model), crit, device=DEV)
     tb = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV, graphs=True, graph_warmup=2)
-    before = [p.detach().clone() for p in tb.params]
+    before = [p.detach().clone() for p in tb.master_params()]
     batches = [b1, b1, b1, b2, b1, b2]
     la = _run(ta, batches)
     lb = _run(tb, batches)
     assert len(tb._graph_states) == 1
     _compare(ta, tb, la, lb)
-    moved = max(float((p.detach() - q).abs().max()) for p, q in zip(tb.params, before))
+    moved = max(float((p.detach() - q).abs().max()) for p, q in zip(tb.master_params(), before))
     assert moved > 0.0
-    # lr schedule reaches the optimiser through the tensor lr (warmup ramp)
-    assert abs(float(tb.opt.param_groups[0]["lr"]) - ta.opt.param_groups[0]["lr"]) < 1e-12
+    # lr schedule reaches the optimiser through the device lr tensor (warmup ramp), and the
+    # replays advanced the device step counter
+    assert abs(float(tb.opt.lr) - float(ta.opt.lr)) < 1e-12
+    assert float(tb.opt.step_count) == float(ta.opt.step_count) == len(batches)
 
 
 def test_graph_new_signature_recaptures():

@@ -101,6 +101,62 @@ def test_swin_t_mask_logits_vs_oracle(size):
         assert max(free) <= 1e-3
 
 
+def _rel_errors(got, exp):
+    """(max over decoder steps of max|err| / max|exp|, same with mean|err|)."""
+    wmax, wmean = 0.0, 0.0
+    for a, b in zip(got, exp):
+        d = (a.float().cpu() - b).abs()
+        sc = float(b.abs().max())
+        wmax = max(wmax, float(d.max()) / sc)
+        wmean = max(wmean, float(d.mean()) / sc)
+    return wmax, wmean
+
+
+@pytest.mark.parametrize("size", [256, 1024])
+def test_swin_t_bf16_production_path_vs_oracle(size):
+    """The PRODUCTION path (bf16 parameters and activations: MFMA window attention, MFMA
+    masked attention, bf16 mask head, bf16 GEMMs) vs the fp32 oracle on the same
+    bf16-rounded weights and input; 1024^2 is the benchmarked C2 shape.  The oracle's
+    attention-mask decisions are forced into both (a logit near 0 flips freely at bf16
+    resolution).
+
+    Tolerance: bf16 storage of every activation through ~70 layers has no analytic bound,
+    so the yardstick is the oracle ITSELF run in bf16 (same weights, torch CPU bf16
+    kernels): the production path must be as close to the fp32 oracle as that, within a
+    factor 1.25, in max and in mean error per decoder step (relative to the step's max
+    |logit|), and within the absolute caps max 0.03 / mean 0.004 (measured round 2:
+    ours 0.015 / 0.0024 at 256^2, 0.016 / 0.0022 at 1024^2; oracle-in-bf16 0.016 / 0.0025
+    and 0.027 / 0.0030 on the build container's CPU)."""
+    import copy
+    m, ref, cfg = _swin_t_pair(size)
+    with torch.no_grad():
+        for p in list(m.parameters()) + list(ref.parameters()):
+            p.copy_(p.to(torch.bfloat16).float())
+    g = torch.Generator().manual_seed(5)
+    px = torch.randn(1, 3, size, size, generator=g).to(torch.bfloat16).float()
+    with torch.no_grad():
+        ref.decoder.record = True
+        rmasks, rclasses = ref(px)
+        forced = [rb for rb, _ in ref.decoder.trace]
+        ref16 = copy.deepcopy(ref).to(torch.bfloat16)
+        ref16.decoder.record = False
+        ref16.decoder.mask_override = forced
+        t0 = time.time()
+        omasks, _ = ref16(px.to(torch.bfloat16))
+        t16 = time.time() - t0
+        m = m.to(torch.bfloat16)
+        m.decoder.mask_override = forced
+        masks, classes = m(px.to(DEV).to(torch.bfloat16))
+    ours = _rel_errors(masks, rmasks)
+    yard = _rel_errors(omasks, rmasks)
+    cerr = max(float((a.float().cpu() - b).abs().max()) for a, b in zip(classes, rclasses))
+    print(f"swin_t@{size} bf16 production path: max|err|/max|logit| {ours[0]:.2e}, mean {ours[1]:.2e}; "
+          f"oracle-in-bf16 {yard[0]:.2e} / {yard[1]:.2e} ({t16:.1f}s); class-logit max|err| {cerr:.2e}")
+    assert ours[0] <= 1.25 * yard[0] and ours[1] <= 1.25 * yard[1]
+    assert ours[0] <= 0.03 and ours[1] <= 0.004
+    assert cerr <= 0.05
+
+
 def test_bf16_training_step():
     from visionseg.model import M2FConfig, Mask2Former
     from visionseg.criterion import SetCriterion

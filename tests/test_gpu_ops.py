@@ -600,26 +600,6 @@ def test_column_sum_vs_torch(dtype, M, N):
     assert float((got - exp).abs().max()) <= tol * max(1.0, float(exp.abs().max())) + 1e-3 * (M ** 0.5) * (dtype != torch.float32)
 
 
-def test_segment_clip_vs_clip_grad_norm():
-    """Per-parameter clip over the flat buffer (csrc/optim.hip) vs torch's
-    clip_grad_norm_(p, 0.01) applied to every parameter (detectron2 "norm")."""
-    from visionseg.ops import FlatParams
-    g = torch.Generator().manual_seed(0)
-    shapes = [(96,), (3, 5), (7,), (1024, 256), (300000,), (1,), (2, 3, 4, 5), (65536,), (65537,)]
-    scales = [1e-4, 1.0, 0.0, 0.3, 5.0, 0.001, 1e-3, 2.0, 0.002]
-    grads = [torch.randn(s, generator=g) * k / max(1.0, float(np.prod(s)) ** 0.5) for s, k in zip(shapes, scales)]
-    fp = FlatParams(shapes, DEV)
-    flat = fp.buffer()
-    for v, gr in zip(fp.views(flat), grads):
-        v.copy_(gr)
-    fp.clip_(flat, 0.01)
-    for v, gr in zip(fp.views(flat), grads):
-        p = torch.nn.Parameter(torch.zeros_like(gr, dtype=torch.float64))
-        p.grad = gr.double().clone()
-        torch.nn.utils.clip_grad_norm_([p], 0.01)
-        np.testing.assert_allclose(v.cpu().double().numpy(), p.grad.numpy(), rtol=2e-6, atol=1e-12)
-
-
 @pytest.mark.parametrize("shift", [0, 3])
 @pytest.mark.parametrize("heads,nWh,nWw", [(3, 4, 4), (6, 3, 5), (12, 2, 2)])
 @pytest.mark.parametrize("kernel", ["mfma", "scalar"])

@@ -1,0 +1,112 @@
+"""One fp32 TRAINING step of the MI355X path vs the oracle (ROADMAP item 1 of round 2).
+
+Same weights, same batch, same point draws (tests/_draws.py, fed to both criteria), the
+oracle's attention-mask decisions forced into the GPU decoder (threshold flips at
+|logit| ~ 1e-6 are decisions, not arithmetic; tests/test_gpu_model.py measures them):
+
+* oracle: RefMask2Former + RefCriterion (pinned to HF transformers 5.15.0) on CPU, then
+  the reference's solver (oracle/ref_solver.py: detectron2 param groups, clip_grad_norm_
+  per parameter = train_full.py:266-271, torch SGD momentum 0.9);
+* product: visionseg.train.Trainer in fp32 mode on the GPU (HIP kernels, device
+  matcher, flat-buffer optimiser csrc/optim.hip).
+
+Checked: every weighted loss component of every decoder step (rel. 1e-4), every
+parameter gradient (max error <= 2e-3 x that parameter's max |grad|; fp32 arithmetic
+in different summation orders over a 10-step decoder), and the weight update of the
+step (max error <= 2e-3 x max |update| per parameter).
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from _draws import KeyedDraws
+from oracle.detinit import det_init
+from oracle.ref_model import RefConfig, RefCriterion, RefMask2Former
+from oracle.ref_solver import ref_clip_per_parameter, ref_optimizer, ref_param_groups
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+GRAD_TOL = 2e-3
+LOSS_TOL = 1e-4
+
+
+def _setup(kind, golden):
+    from visionseg.model import M2FConfig
+    if kind == "tiny":
+        d = golden("model_tiny.npz")
+        cfgd = json.loads(str(d["config"]))
+        cfg = M2FConfig.from_dict(cfgd)
+        ref = RefMask2Former(RefConfig.from_dict(cfgd))
+        sd = det_init({k: v.shape for k, v in ref.state_dict().items()}, int(d["weight_seed"]))
+        return cfg, sd, 128
+    cfg = M2FConfig.preset("swin_t")
+    ref = RefMask2Former(RefConfig.from_dict(cfg.to_dict()))
+    sd = det_init({k: v.shape for k, v in ref.state_dict().items()}, 77)
+    return cfg, sd, 256
+
+
+@pytest.mark.parametrize("kind", ["tiny", "swin_t"])
+def test_training_step_vs_oracle(golden, kind):
+    from visionseg.criterion import SetCriterion
+    from visionseg.data import synthetic_batch
+    from visionseg.model import Mask2Former
+    from visionseg.train import SolverConfig, Trainer, lr_at
+    cfg, sd, size = _setup(kind, golden)
+    rcfg = RefConfig.from_dict(cfg.to_dict())
+    ref = RefMask2Former(rcfg)
+    ref.load_state_dict(sd)
+    ref.train()
+    prod = Mask2Former(cfg)
+    prod.load_state_dict(sd)
+    imgs, ml, cl = synthetic_batch(2, size, seed=4)
+    draws = KeyedDraws(2, max(len(c) for c in cl) + 1, seed=5)
+    s = SolverConfig(amp=False, optimizer="sgd", warmup_iters=0, lr=0.05)
+
+    # ---- oracle: forward + loss + backward on CPU, then the reference's solver step
+    ref.decoder.record = True
+    rmasks, rclasses = ref(imgs)
+    rloss, rparts = RefCriterion(rcfg, point_source=draws)(rmasks, rclasses, [m.float() for m in ml], cl)
+    rloss.backward()
+    rparams = dict(ref.named_parameters())
+    rgrad = {n: p.grad.detach().clone() for n, p in rparams.items()}
+    before = {n: p.detach().clone() for n, p in rparams.items()}
+    ref_clip_per_parameter(list(rparams.values()), s.clip_value)
+    ref_optimizer(ref_param_groups(ref, lr_at(s, 0), s.weight_decay, "sgd"), "sgd", s.momentum).step()
+
+    # ---- product: the same step on the GPU
+    crit = SetCriterion(cfg, matcher="device", point_source=draws)
+    tr = Trainer(prod, crit, s, device=DEV)
+    assert tr.mode == "fp32"
+    prod.decoder.mask_override = [b for b, _ in ref.decoder.trace]
+    tr._set_lr()
+    loss, parts = tr.forward_backward(imgs.to(DEV), [m.to(DEV) for m in ml], [c.to(DEV) for c in cl])
+    ggrad = {n: g.detach().cpu().clone() for n, g in zip(tr.opt.names, tr.opt.grad_views)}
+    tr.apply_gradients()
+    torch.cuda.synchronize()
+    after = {n: m.detach().cpu() for n, m in zip(tr.opt.names, tr.master_params())}
+
+    # ---- loss components
+    assert set(parts) == set(rparts)
+    worst_l = max(abs(float(parts[k]) - float(rparts[k])) / max(1e-3, abs(float(rparts[k]))) for k in rparts)
+    # ---- gradients and weight updates, per parameter
+    worst_g, worst_u, wg, wu = 0.0, 0.0, "", ""
+    assert set(ggrad) == set(rgrad)
+    for n in rgrad:
+        den = float(rgrad[n].abs().max())
+        e = float((ggrad[n] - rgrad[n]).abs().max()) / max(den, 1e-12)
+        if den > 0 and e > worst_g:
+            worst_g, wg = e, n
+        ru = rparams[n].detach() - before[n]
+        gu = after[n] - before[n]
+        den = float(ru.abs().max())
+        e = float((gu - ru).abs().max()) / max(den, 1e-12)
+        if den > 0 and e > worst_u:
+            worst_u, wu = e, n
+    print(f"{kind}: loss {float(loss):.6f} vs oracle {float(rloss):.6f}; worst loss-part rel err {worst_l:.2e}; "
+          f"worst grad err {worst_g:.2e} ({wg}); worst update err {worst_u:.2e} ({wu})")
+    assert worst_l <= LOSS_TOL
+    assert abs(float(loss) - float(rloss)) <= LOSS_TOL * abs(float(rloss))
+    assert worst_g <= GRAD_TOL, wg
+    assert worst_u <= GRAD_TOL, wu

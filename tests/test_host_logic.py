@@ -12,7 +12,7 @@ from visionseg.data import write_coco_dataset, CocoInstanceDataset, collate_padd
 from visionseg.evaluate import MaskAPEvaluator
 from visionseg.convert import from_hf_state_dict, to_hf_state_dict
 from visionseg.model import M2FConfig, Mask2Former
-from visionseg.train import SolverConfig, _lr_lambda
+from visionseg.train import SolverConfig, lr_at
 from visionseg.inference import instance_inference
 
 
@@ -81,9 +81,11 @@ def test_state_dict_conversion_roundtrip():
 
 
 def test_lr_schedules():
-    f = _lr_lambda(SolverConfig(warmup_iters=200, steps=(3500, 4500)))
+    s = SolverConfig(warmup_iters=200, steps=(3500, 4500), lr=1.0)
+    f = lambda it: lr_at(s, it)  # noqa: E731
     assert f(0) == pytest.approx(0.001) and f(200) == 1.0 and f(3600) == pytest.approx(0.1) and f(4600) == pytest.approx(0.01)
-    c = _lr_lambda(SolverConfig(warmup_iters=0, schedule="cosine", max_iter=100))
+    sc = SolverConfig(warmup_iters=0, schedule="cosine", max_iter=100, lr=1.0)
+    c = lambda it: lr_at(sc, it)  # noqa: E731
     assert c(0) == 1.0 and c(50) == pytest.approx(0.5) and c(100) == pytest.approx(0.0, abs=1e-12)
 
 

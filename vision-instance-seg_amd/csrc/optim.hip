@@ -1,24 +1,44 @@
-// Per-parameter gradient-norm clipping over a flat f32 gradient buffer.
+// Fused optimiser step over flat parameter / gradient / state buffers.
 //
-// detectron2's "norm" clip (reference training/maskdino/train_full.py:266-271, clip
-// value 0.01) calls torch.nn.utils.clip_grad_norm_(p, 0.01) for EVERY parameter:
-// g *= min(1, max_norm / (||g||_2 + 1e-6)).  With ~500 parameters that is thousands of
-// tiny launches per step in eager PyTorch.  Here the f32 master gradients live in one
-// flat buffer (each parameter 16-B aligned) and a static chunk table splits every
-// parameter into chunks of <= kChunk elements:
-//   table[c] = {start, len, first chunk of the parameter, chunks of the parameter}.
-// Kernel 1 writes each chunk's sum of squares; kernel 2 recomputes its parameter's norm
-// from that parameter's chunk partials (same order in every block: deterministic, no
-// atomics) and scales the chunk.
+// The reference trains through detectron2's DefaultTrainer (training/maskdino/
+// train_full.py:153-167): SGD with momentum 0.9, weight decay 0.05 except on norm
+// parameters, and CLIP_GRADIENTS type "norm", value 0.01 (train_full.py:266-271), i.e.
+// torch.nn.utils.clip_grad_norm_(p, 0.01) for EVERY parameter before the update.  In
+// eager PyTorch that is thousands of tiny launches per step (a norm, a scale and a
+// multi-tensor update per parameter, then a bf16 cast-copy of every weight).
+//
+// Here every buffer of the optimiser is flat: gradients (the model's .grad tensors are
+// views of one buffer), f32 master weights, the f32 momentum / Adam moments, and the
+// bf16 working weights the model reads (views of one buffer too).  Each parameter starts
+// 8-element aligned; a static chunk table splits every parameter into chunks of
+// <= kChunk elements:
+//   table[c]  = {start, len, first chunk of the parameter, chunks of the parameter}
+//   hyper[c]  = {lr multiplier, weight decay} of the chunk's parameter group.
+// Two launches per step:
+//   flat_sumsq_kernel: each chunk's sum of squares of the (averaged) gradient; block 0
+//                      also advances the device step counter (Adam bias correction);
+//   flat_step_kernel:  recomputes its parameter's norm from that parameter's partials
+//                      (per-parameter clip; or from all partials: "full_model" clip),
+//                      then clip-scale + weight decay + SGD-momentum / AdamW update of
+//                      the master weights + bf16 round of the working weights, one pass.
+// Deterministic: no atomics, every block sums the partials in the same order.
+// HBM-bound: per element it reads the gradient (2 or 4 B) and master + state (8 or 12 B)
+// and writes master + state + working weight (10 or 14 B).
 #include "common.h"
 
 namespace vs {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kVec = 8;
+
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+  return v;
+}
 
 __device__ __forceinline__ float block_sum(float v, float* sh) {
-  for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+  v = wave_sum(v);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   if (l == 0) sh[w] = v;
   __syncthreads();
@@ -31,48 +51,137 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return sh[kThreads / 64];
 }
 
-__global__ void __launch_bounds__(kThreads) chunk_sumsq_kernel(const float* __restrict__ data,
-                                                               const int* __restrict__ table,
-                                                               float* __restrict__ partial) {
+template <typename G> __device__ __forceinline__ void load8(const G* p, float* out);
+template <> __device__ __forceinline__ void load8<bf16>(const bf16* p, float* out) { Vec16<bf16>::load(p, out); }
+template <> __device__ __forceinline__ void load8<float>(const float* p, float* out) {
+  Vec16<float>::load(p, out);
+  Vec16<float>::load(p + 4, out + 4);
+}
+__device__ __forceinline__ void store8(float* p, const float* in) {
+  Vec16<float>::store(p, in);
+  Vec16<float>::store(p + 4, in + 4);
+}
+
+template <typename G>
+__global__ void __launch_bounds__(kThreads) flat_sumsq_kernel(const G* __restrict__ grad, const int* __restrict__ table,
+                                                              float* __restrict__ partial, float* __restrict__ step) {
   __shared__ float sh[kThreads / 64 + 1];
   const int c = blockIdx.x;
+  if (c == 0 && threadIdx.x == 0 && step) step[0] += 1.f;
   const int start = table[c * 4 + 0], len = table[c * 4 + 1];
-  const float* p = data + start;               // start % 4 == 0 (16-B aligned parameters)
+  const G* p = grad + start;                  // start % 8 == 0
   float acc = 0.f;
-  const int n4 = len >> 2;
-  for (int i = threadIdx.x; i < n4; i += kThreads) {
-    const float4 v = reinterpret_cast<const float4*>(p)[i];
-    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  const int n8 = len / kVec;
+  for (int i = threadIdx.x; i < n8; i += kThreads) {
+    float v[kVec];
+    load8<G>(p + i * kVec, v);
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) acc += v[j] * v[j];
   }
-  for (int i = (n4 << 2) + threadIdx.x; i < len; i += kThreads) acc += p[i] * p[i];
+  for (int i = n8 * kVec + threadIdx.x; i < len; i += kThreads) {
+    const float v = to_f32(p[i]);
+    acc += v * v;
+  }
   const float t = block_sum(acc, sh);
   if (threadIdx.x == 0) partial[c] = t;
 }
 
-__global__ void __launch_bounds__(kThreads) chunk_scale_kernel(float* __restrict__ data,
-                                                               const int* __restrict__ table,
-                                                               const float* __restrict__ partial, float max_norm,
-                                                               float eps) {
-  __shared__ float scale;
+struct StepArgs {
+  float grad_scale;      // 1 / world size (gradients summed by the all-reduce)
+  int clip;              // 0 none, 1 per parameter (detectron2 "norm"), 2 full model
+  float clip_value;
+  float clip_eps;        // clip_grad_norm_: max_norm / (norm + 1e-6)
+  int optimizer;         // 0 SGD (momentum, dampening 0, no nesterov), 1 AdamW
+  float momentum, beta1, beta2, eps;
+};
+
+// Per-element update, torch.optim semantics (SGD: torch/optim/sgd.py; AdamW:
+// torch/optim/adamw.py, single-tensor path).
+__device__ __forceinline__ void update(float g, float& p, float& s1, float& s2, float lr, float wd, bool first,
+                                       const StepArgs& a, float bc1, float bc2_sqrt) {
+  if (a.optimizer == 0) {
+    const float d = g + wd * p;
+    s1 = first ? d : a.momentum * s1 + d;
+    p -= lr * s1;
+  } else {
+    p *= 1.f - lr * wd;
+    s1 += (1.f - a.beta1) * (g - s1);
+    s2 = a.beta2 * s2 + (1.f - a.beta2) * g * g;
+    const float denom = sqrtf(s2) / bc2_sqrt + a.eps;
+    p -= (lr / bc1) * s1 / denom;
+  }
+}
+
+template <typename G, typename W>
+__global__ void __launch_bounds__(kThreads) flat_step_kernel(const G* __restrict__ grad, float* __restrict__ master,
+                                                             float* __restrict__ s1buf, float* __restrict__ s2buf,
+                                                             W* __restrict__ wout, const int* __restrict__ table,
+                                                             const float* __restrict__ hyper,
+                                                             const float* __restrict__ partial, int num_chunks,
+                                                             const float* __restrict__ lr_ptr,
+                                                             const float* __restrict__ step_ptr, StepArgs a) {
+  __shared__ float s_scale;
   const int c = blockIdx.x;
   const int start = table[c * 4 + 0], len = table[c * 4 + 1];
-  if (threadIdx.x == 0) {
-    const int first = table[c * 4 + 2], count = table[c * 4 + 3];
-    float s = 0.f;
-    for (int i = 0; i < count; ++i) s += partial[first + i];
-    scale = fminf(1.f, max_norm / (sqrtf(s) + eps));
+  if (threadIdx.x < 64) {
+    float k = 1.f;
+    if (a.clip != 0) {
+      const int first = a.clip == 1 ? table[c * 4 + 2] : 0;
+      const int count = a.clip == 1 ? table[c * 4 + 3] : num_chunks;
+      float s = 0.f;
+      for (int i = threadIdx.x; i < count; i += 64) s += partial[first + i];
+      s = wave_sum(s);
+      const float norm = sqrtf(s) * a.grad_scale;
+      k = fminf(1.f, a.clip_value / (norm + a.clip_eps));
+    }
+    if (threadIdx.x == 0) s_scale = k * a.grad_scale;
   }
   __syncthreads();
-  const float k = scale;
-  if (k == 1.f) return;
-  float* p = data + start;
-  const int n4 = len >> 2;
-  for (int i = threadIdx.x; i < n4; i += kThreads) {
-    float4 v = reinterpret_cast<float4*>(p)[i];
-    v.x *= k; v.y *= k; v.z *= k; v.w *= k;
-    reinterpret_cast<float4*>(p)[i] = v;
+  const float gk = s_scale;
+  const float lr = lr_ptr[0] * hyper[c * 2 + 0];
+  const float wd = hyper[c * 2 + 1];
+  const float t = step_ptr[0];
+  const bool first = t <= 1.f;
+  float bc1 = 1.f, bc2s = 1.f;
+  if (a.optimizer == 1) {
+    bc1 = 1.f - powf(a.beta1, t);
+    bc2s = sqrtf(1.f - powf(a.beta2, t));
   }
-  for (int i = (n4 << 2) + threadIdx.x; i < len; i += kThreads) p[i] *= k;
+  const int n8 = len / kVec;
+  for (int i = threadIdx.x; i < n8; i += kThreads) {
+    const int o = start + i * kVec;
+    float g[kVec], p[kVec], m[kVec], v[kVec];
+    load8<G>(grad + o, g);
+    load8<float>(master + o, p);
+    load8<float>(s1buf + o, m);
+    if (a.optimizer == 1) load8<float>(s2buf + o, v);
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) update(g[j] * gk, p[j], m[j], v[j], lr, wd, first, a, bc1, bc2s);
+    store8(master + o, p);
+    store8(s1buf + o, m);
+    if (a.optimizer == 1) store8(s2buf + o, v);
+    if (wout) Vec16<W>::store(wout + o, p);
+  }
+  for (int i = n8 * kVec + threadIdx.x; i < len; i += kThreads) {
+    const int o = start + i;
+    float p = master[o], m = s1buf[o], v = a.optimizer == 1 ? s2buf[o] : 0.f;
+    update(to_f32(grad[o]) * gk, p, m, v, lr, wd, first, a, bc1, bc2s);
+    master[o] = p;
+    s1buf[o] = m;
+    if (a.optimizer == 1) s2buf[o] = v;
+    if (wout) wout[o] = from_f32<W>(p);
+  }
+}
+
+template <typename G>
+int launch_step(const G* grad, float* master, float* s1, float* s2, bf16* wout, const int* table, const float* hyper,
+                int num_chunks, const StepArgs& a, const float* lr, float* step, float* partial, hipStream_t st) {
+  // always launched: block 0 also advances the step counter
+  hipLaunchKernelGGL(flat_sumsq_kernel<G>, dim3(num_chunks), dim3(kThreads), 0, st, grad, table, partial, step);
+  hipLaunchKernelGGL((flat_step_kernel<G, bf16>), dim3(num_chunks), dim3(kThreads), 0, st, grad, master, s1, s2, wout,
+                     table, hyper, partial, num_chunks, lr, step, a);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
 }
 
 }  // namespace
@@ -80,21 +189,28 @@ __global__ void __launch_bounds__(kThreads) chunk_scale_kernel(float* __restrict
 
 using namespace vs;
 
-extern "C" long long vs_segment_clip_workspace_bytes(int num_chunks) {
-  return (long long)num_chunks * sizeof(float);
-}
+extern "C" long long vs_flat_step_workspace_bytes(int num_chunks) { return (long long)num_chunks * sizeof(float); }
 
-extern "C" int vs_segment_clip(float* data, const int* table, int num_chunks, float max_norm, float eps,
-                               void* workspace, void* stream) {
+extern "C" int vs_flat_step(int grad_dtype, const void* grad, float grad_scale, float* master, float* state1,
+                            float* state2, void* weights_bf16, const int* table, const float* hyper, int num_chunks,
+                            int optimizer, int clip, float clip_value, float clip_eps, float momentum, float beta1,
+                            float beta2, float eps, const float* lr, float* step, void* workspace, void* stream) {
   VS_CHECK(num_chunks >= 0, "bad chunk count");
   if (num_chunks == 0) return VS_OK;
-  VS_CHECK(data && table && workspace, "null pointer");
-  VS_CHECK(max_norm > 0.f, "max_norm must be positive");
+  VS_CHECK(grad && master && state1 && table && hyper && lr && step && workspace, "null pointer");
+  VS_CHECK(grad_dtype == VS_F32 || grad_dtype == VS_BF16, "gradient dtype must be f32 or bf16");
+  VS_CHECK(optimizer == 0 || optimizer == 1, "optimizer must be 0 (SGD) or 1 (AdamW)");
+  VS_CHECK(optimizer == 0 || state2, "AdamW needs the second-moment buffer");
+  VS_CHECK(clip >= 0 && clip <= 2, "clip must be 0 (none), 1 (per parameter) or 2 (full model)");
+  VS_CHECK(clip == 0 || clip_value > 0.f, "clip value must be positive");
+  VS_CHECK(grad_scale > 0.f, "grad_scale must be positive");
+  StepArgs a{grad_scale, clip, clip_value, clip_eps, optimizer, momentum, beta1, beta2, eps};
   hipStream_t st = (hipStream_t)stream;
   float* partial = (float*)workspace;
-  hipLaunchKernelGGL(chunk_sumsq_kernel, dim3(num_chunks), dim3(kThreads), 0, st, data, table, partial);
-  hipLaunchKernelGGL(chunk_scale_kernel, dim3(num_chunks), dim3(kThreads), 0, st, data, table, partial, max_norm,
-                     eps);
-  VS_LAUNCH_CHECK();
-  return VS_OK;
+  bf16* w = (bf16*)weights_bf16;
+  if (grad_dtype == VS_BF16)
+    return launch_step<bf16>((const bf16*)grad, master, state1, state2, w, table, hyper, num_chunks, a, lr, step,
+                             partial, st);
+  return launch_step<float>((const float*)grad, master, state1, state2, w, table, hyper, num_chunks, a, lr, step,
+                            partial, st);
 }

@@ -16,4 +16,13 @@ import os as _os
 # memory accesses on MI355X (tools/graph_diag.py --variant recapture).  Plain per-node
 # graph launches cost nothing measurable here (59.2 vs 59.0 ms/step).  The runtime reads
 # the flag once, at HIP initialisation: import visionseg before touching the device.
+import sys as _sys
+
+_flag_before = _os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE")
+_torch = _sys.modules.get("torch")
+_hip_up_before = bool(_torch is not None and hasattr(_torch, "cuda") and _torch.cuda.is_initialized())
 _os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+# False when HIP was already initialised (by the caller) before the flag was in place:
+# Trainer(graphs=True) refuses to capture then
+GRAPH_CAPTURE_SAFE = (_os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] == "0"
+                      and (not _hip_up_before or _flag_before == "0"))

@@ -55,8 +55,13 @@ SIGNATURES = {
     "vs_layer_norm_backward_add": [_c_int] + [_P] * 10 + [_c_int] * 2 + [_P],
     "vs_column_sum_workspace_bytes": [_c_int] * 2,
     "vs_column_sum": [_c_int] + [_P] * 3 + [_c_int] * 2 + [_P],
-    "vs_segment_clip_workspace_bytes": [_c_int],
-    "vs_segment_clip": [_P, _P, _c_int, _c_float, _c_float, _P, _P],
+    "vs_flat_step_workspace_bytes": [_c_int],
+    "vs_flat_step": [_c_int, _P, _c_float, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _c_int] + [_c_float] * 6
+                    + [_P, _P, _P, _P],
+    "vs_event_create": [ctypes.POINTER(_c_void_p)],
+    "vs_event_destroy": [_P],
+    "vs_event_record_external": [_P, _P],
+    "vs_stream_wait_event": [_P, _P],
     "vs_lsa_max_targets": [_c_int],
     "vs_lsa_batch": [_P, _P] + [_c_int] * 4 + [_P, _P],
     "vs_lsa_batch_device_counts": [_P, _P] + [_c_int] * 4 + [_P, _P],
@@ -76,7 +81,7 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_mask_head_backward_workspace_bytes": ctypes.c_longlong,
             "vs_layer_norm_backward_workspace_bytes": ctypes.c_longlong,
             "vs_column_sum_workspace_bytes": ctypes.c_longlong,
-            "vs_segment_clip_workspace_bytes": ctypes.c_longlong,
+            "vs_flat_step_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_nchw_workspace_bytes": ctypes.c_longlong,
             "vs_msda_backward_sorted_workspace_bytes": ctypes.c_longlong,

@@ -80,6 +80,7 @@ def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, ba
     if max_iters is not None:
         total = min(total, max_iters)
     solver = SolverConfig(lr=float(hp["learning_rate"]), weight_decay=float(hp["weight_decay"]),
+                          optimizer="adamw" if str(hp.get("optimizer", "")).lower() == "adamw" else "sgd",
                           schedule="cosine" if hp.get("lr_scheduler") == "cosine" else "multistep",
                           warmup_iters=int(hp.get("warmup_epochs", 0)) * iters_per_epoch, max_iter=total,
                           amp=device.type == "cuda")

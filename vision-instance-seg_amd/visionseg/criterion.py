@@ -21,8 +21,9 @@ restructured for the device:
 
 `matcher="host"` keeps scipy's `linear_sum_assignment` (the reference's choice); both
 return the same optimum (unique for generic costs).  The random points come from the
-device generator, so a GPU loss is not bit-comparable with the CPU oracle's (documented
-in DESIGN.md; the oracle's loss is pinned to HF).
+device generator; the `point_source` hook feeds both this criterion and the oracle's the
+same keyed draws, which is how tests/test_gpu_train_parity.py compares the GPU loss and
+gradients with the oracle's.
 """
 from __future__ import annotations
 
@@ -101,15 +102,25 @@ def as_padded(mask_labels, class_labels, device):
 
 
 class SetCriterion:
-    def __init__(self, cfg, matcher: str = "device"):
+    def __init__(self, cfg, matcher: str = "device", point_source=None):
         """matcher: "device" (csrc/match.hip, no host sync) or "host" (scipy, the
-        reference's linear_sum_assignment)."""
+        reference's linear_sum_assignment).  point_source: None (device RNG) or a parity
+        hook with `match_points(B, P, device) -> [B,P,2]` and `loss_points(S, B, Kc, n,
+        kind, device) -> [S,B,Kc,n,2]` in [0,1) (kind "over": the oversampled candidates,
+        "rand": the uniform remainder), draws keyed by (step, image, target) so the
+        oracle criterion (oracle/ref_model.RefCriterion) can be fed the same points."""
         if matcher not in ("device", "host"):
             raise ValueError(matcher)
         self.cfg = cfg
         self.num_labels = cfg.num_labels
         self.matcher = matcher
+        self.point_source = point_source
         self._ew = {}
+
+    def _loss_points(self, S, B, Kc, n, kind, dev):
+        if self.point_source is None:
+            return torch.rand(S * B * Kc, n, 2, device=dev)
+        return self.point_source.loss_points(S, B, Kc, n, kind, dev).reshape(S * B * Kc, n, 2).to(dev)
 
     # --------------------------------------------------------------- matching
     @torch.no_grad()
@@ -130,7 +141,9 @@ class SetCriterion:
         # one uniform point set per image, shared by its queries, targets and the S steps:
         # queries / targets are grid_sample CHANNELS (one call per step, one for all targets)
         P = c.train_num_points
-        grid = (2.0 * torch.rand(B, P, 2, device=dev) - 1.0).unsqueeze(2)              # [B,P,1,2]
+        u = (self.point_source.match_points(B, P, dev).to(dev) if self.point_source is not None
+             else torch.rand(B, P, 2, device=dev))
+        grid = (2.0 * u - 1.0).unsqueeze(2)                                              # [B,P,1,2]
         if (self.matcher == "device" and dev.type == "cuda" and 1 <= tg.kc <= 16 and S <= 16
                 and Kc <= ops.lsa_max_targets(Q) and _FUSED_COST):
             # one kernel: point-sampled logits, BCE / dice / class costs (csrc/match.hip).
@@ -234,12 +247,12 @@ class SetCriterion:
                 npts = c.train_num_points
                 ns = int(npts * c.oversample_ratio)
                 nu = int(c.importance_sample_ratio * npts)
-                coords = torch.rand(S * NP, ns, 2, device=dev)
+                coords = self._loss_points(S, B, Kc, ns, "over", dev)
                 unc = -torch.abs(_sample(pred.detach().float(), coords))
                 top = torch.topk(unc, k=nu, dim=1)[1]
                 coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
                 if npts - nu > 0:
-                    coords = torch.cat([coords, torch.rand(S * NP, npts - nu, 2, device=dev)], 1)
+                    coords = torch.cat([coords, self._loss_points(S, B, Kc, npts - nu, "rand", dev)], 1)
                 # sample each full-resolution target once, with the coordinates of the S
                 # predictions it is matched to
                 by_t = coords.view(S, NP, npts, 2).transpose(0, 1)                         # [NP,S,P,2]

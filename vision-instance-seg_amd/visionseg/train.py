@@ -3,17 +3,25 @@
 One process per GPU (torchrun-style env: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*),
 `torch.distributed` with backend "nccl" (= RCCL on ROCm, over xGMI inside a node) or
 "gloo" on CPU.  Image batches are sharded by rank (independent images, per-rank seed
-42 + rank); the only exchanges are the bucketed gradient all-reduce, which DDP
-launches from autograd hooks on its communication stream while the backward pass is
-still running (overlapped with the remaining backward kernels), and the scalar
-`num_masks` all-reduce of the criterion (upstream SetCriterion; HF:m2f:781-794).
+42 + rank); the only exchanges are the bucketed f32 gradient all-reduce, overlapped
+with the backward pass (optim.GradReducer: from autograd hooks in eager steps, behind
+in-graph events in graph-replayed steps), and the scalar `num_masks` all-reduce of the
+criterion (upstream SetCriterion; HF:m2f:781-794).
 
-Solver semantics follow the reference's detectron2 config
-(training/maskdino/train_full.py:246-271): AdamW lr 1e-4 (train_template.py:47-50),
-WarmupMultiStep (warmup 200 iters, steps 3500/4500, gamma 0.1), bf16 autocast when
-AMP is on (train_experiments.py:229-230), and CLIP_GRADIENTS type "norm", value 0.01,
-L2 — detectron2's "norm" clips EACH parameter's gradient to norm 0.01 (its
-"full_model" type would clip the global norm; both are provided).
+Solver semantics follow the reference (training/maskdino/train_full.py:246-271 on top of
+detectron2's DefaultTrainer, which it does not override, :153-167; restated in
+oracle/ref_solver.py): SGD momentum 0.9, BASE_LR 1e-4, WEIGHT_DECAY 0.05 (MaskDINO base
+config, upstream) with 0 on normalisation parameters (WEIGHT_DECAY_NORM), WarmupMultiStep
+(warmup 200 iters, steps 3500/4500, gamma 0.1), CLIP_GRADIENTS type "norm", value 0.01,
+L2: detectron2's "norm" clips EACH parameter's gradient to norm 0.01 ("full_model", one
+global norm, is provided too).  `optimizer="adamw"` gives upstream Mask2Former/MaskDINO
+train_net.py's AdamW (train_template.py:49's "AdamW" hyper-parameter).  The reference
+runs fp32 (SOLVER.AMP.ENABLED False, train_full.py:263); `precision` "bf16" keeps f32
+master weights and optimiser state and computes in bf16.
+
+The optimiser is csrc/optim.hip over flat buffers (optim.FlatOptimizer): the model's
+parameters and gradients are views of one buffer each, and clip + decay + update + bf16
+cast of the whole model is two kernels.
 """
 from __future__ import annotations
 
@@ -22,24 +30,31 @@ from dataclasses import dataclass
 
 import torch
 import torch.distributed as dist
-from torch.nn.parallel import DistributedDataParallel as DDP
+
+from .optim import FlatOptimizer, GradReducer
 
 
 @dataclass
 class SolverConfig:
     lr: float = 1e-4
+    optimizer: str = "sgd"           # "sgd" (the reference: detectron2 DefaultTrainer) | "adamw"
+    momentum: float = 0.9            # SOLVER.MOMENTUM
     weight_decay: float = 0.05
+    weight_decay_norm: float = 0.0   # SOLVER.WEIGHT_DECAY_NORM
+    weight_decay_embed: float = 0.0  # AdamW / upstream train_net only
+    backbone_multiplier: float = 0.1  # AdamW / upstream train_net only
     betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
     clip_type: str = "norm"          # "norm" (per parameter, detectron2) | "full_model" | "none"
     clip_value: float = 0.01
     warmup_iters: int = 200
     warmup_factor: float = 0.001     # detectron2 SOLVER.WARMUP_FACTOR, linear warmup
     steps: tuple = (3500, 4500)
     gamma: float = 0.1
-    amp: bool = True                 # bf16 compute on a cuda device (see `precision`)
-    precision: str = "bf16"          # "bf16": bf16 params/activations + f32 master weights in the
-                                     # optimizer; "amp": f32 params + bf16 autocast; "fp32"
-    bucket_cap_mb: int = 64
+    amp: bool = True                 # reduced-precision compute on a cuda device (see `precision`)
+    precision: str = "bf16"          # "bf16": bf16 params/activations + f32 master weights and state;
+                                     # "amp": f32 params + bf16 autocast; "fp32" (also amp=False)
+    bucket_cap_mb: float = 25.0      # f32 all-reduce bucket size
     schedule: str = "multistep"      # detectron2 WarmupMultiStep | "cosine" (train_template.py:51)
     max_iter: int = 5000
 
@@ -64,18 +79,25 @@ def init_distributed(backend: str | None = None):
     return rank, local, world
 
 
-def _lr_lambda(cfg: SolverConfig):
+def lr_at(cfg: SolverConfig, it: int) -> float:
+    """WarmupMultiStepLR / WarmupCosineLR (detectron2 solver/lr_scheduler.py semantics)."""
     import math
+    w = 1.0
+    if it < cfg.warmup_iters:
+        a = it / max(1, cfg.warmup_iters)
+        w = cfg.warmup_factor * (1 - a) + a
+    if cfg.schedule == "cosine":
+        return cfg.lr * w * 0.5 * (1.0 + math.cos(math.pi * min(it, cfg.max_iter) / max(1, cfg.max_iter)))
+    return cfg.lr * w * cfg.gamma ** sum(1 for s in cfg.steps if it >= s)
 
-    def f(it):
-        w = 1.0
-        if it < cfg.warmup_iters:
-            a = it / max(1, cfg.warmup_iters)
-            w = cfg.warmup_factor * (1 - a) + a
-        if cfg.schedule == "cosine":
-            return w * 0.5 * (1.0 + math.cos(math.pi * min(it, cfg.max_iter) / max(1, cfg.max_iter)))
-        return w * cfg.gamma ** sum(1 for s in cfg.steps if it >= s)
-    return f
+
+def graph_capture_safe() -> bool:
+    """HIP graphs of the training step need ROCm's graph packet capture off
+    (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0, read once when HIP initialises; see
+    visionseg/__init__.py and tools/graph_diag.py): False if the flag is not "0" now, or
+    if HIP was initialised before `import visionseg` put it in place."""
+    import visionseg
+    return os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") == "0" and visionseg.GRAPH_CAPTURE_SAFE
 
 
 class Trainer:
@@ -84,12 +106,11 @@ class Trainer:
 
     def __init__(self, model, criterion, solver: SolverConfig | None = None, device=None,
                  distributed: bool | None = None, graphs: bool = False, graph_warmup: int = 2):
-        self.solver = solver or SolverConfig()
+        self.solver = s = solver or SolverConfig()
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
         self.model = model.to(self.device)
         self.criterion = criterion
-        s = self.solver
         self.mode = "fp32"
         if s.amp and self.device.type == "cuda":
             self.mode = s.precision
@@ -97,128 +118,81 @@ class Trainer:
             self.model.to(torch.bfloat16)
         if distributed is None:
             distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-        self.distributed = distributed
-        # HIP-graph replay of the whole step (bf16 mode on a device; see step()): with
-        # several ranks the gradient all-reduce stays an eager RCCL call between two
-        # graphs (no collective inside a capture), so DDP's hooks are not used
+        self.distributed = bool(distributed)
+        self.world = dist.get_world_size() if self.distributed else 1
+        if self.distributed:
+            with torch.no_grad():                       # replicas start identical (rank 0's init)
+                for t in list(self.model.parameters()) + list(self.model.buffers()):
+                    dist.broadcast(t, 0)
+        self.opt = FlatOptimizer(self.model, s, self.device, self.world)
+        self.reducer = GradReducer(self.opt) if self.distributed else None
+        # HIP-graph replay of the whole step (on a device): with several ranks the step is
+        # two graphs (forward+backward, optimiser) with the bucket all-reduces issued
+        # between them behind in-graph events
         self.graphs = bool(graphs) and self.device.type == "cuda" and self.mode == "bf16"
-        self.split = self.graphs and distributed
+        if self.graphs and not graph_capture_safe():
+            raise RuntimeError(
+                "Trainer(graphs=True) needs DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 set before HIP initialises "
+                "(import visionseg before touching the GPU, or export it); graph replays faulted without it")
+        self.split = self.graphs and self.distributed
         # at least two eager steps of a signature before its capture (lazy library state
-        # and the optimiser's moments exist before the capture records anything)
+        # and the optimiser's state exist before the capture records anything)
         self.graph_warmup = max(2, int(graph_warmup))
         self._graph_states, self._eager_seen = {}, {}
         if self.split:
-            self.net = self.model
-            with torch.no_grad():                       # DDP's start-up broadcast from rank 0
-                for t in list(self.model.parameters()) + list(self.model.buffers()):
-                    dist.broadcast(t, 0)
-        elif distributed:
-            kw = dict(bucket_cap_mb=self.solver.bucket_cap_mb, gradient_as_bucket_view=True, broadcast_buffers=False)
-            if self.device.type == "cuda":
-                kw["device_ids"] = [self.device.index]
-            self.net = DDP(self.model, **kw)
-        else:
-            self.net = self.model
-        params = [p for p in self.model.parameters() if p.requires_grad]
-        self.model_params = params
-        self.flat = None
-        if self.mode == "bf16":
-            # f32 master copy owned by the optimiser, packed in one flat buffer (and the f32
-            # master grads in another) so the per-parameter clip is two kernels; the model
-            # keeps bf16 working weights
-            from .ops import FlatParams
-            self.flat = FlatParams([p.shape for p in params], self.device)
-            self.flat_master, self.flat_grad = self.flat.buffer(), self.flat.buffer()
-            self.params = []
-            with torch.no_grad():
-                for v, g, p in zip(self.flat.views(self.flat_master), self.flat.views(self.flat_grad), params):
-                    v.copy_(p.detach().float())
-                    m = torch.nn.Parameter(v)
-                    m.grad = g
-                    self.params.append(m)
-        else:
-            self.params = params
-        fused = self.device.type == "cuda"
-        okw = dict(fused=fused, foreach=None if fused else True)
-        lr = self.solver.lr
-        if self.graphs:
-            # device-side step count and a tensor lr: replays see the scheduler's updates
-            okw["capturable"] = True
-            lr = torch.tensor(lr, device=self.device, dtype=torch.float32)
-        self.opt = torch.optim.AdamW(self.params, lr=lr, betas=self.solver.betas,
-                                     weight_decay=self.solver.weight_decay, **okw)
-        if self.split:
-            self.flat_g16 = torch.zeros(self.flat.total, device=self.device, dtype=torch.bfloat16)
-            self.g16_views = self.flat.views(self.flat_g16)
             self.num_masks_total = torch.zeros((), device=self.device, dtype=torch.float32)
-        self.sched = torch.optim.lr_scheduler.LambdaLR(self.opt, _lr_lambda(self.solver))
-        if self.graphs:
-            # float bases: the scheduler then fills the lr tensor from a host float (a tensor
-            # base would make it read the value back, one host sync per step)
-            self.sched.base_lrs = [float(self.solver.lr) for _ in self.opt.param_groups]
         self.iter = 0
 
-    @torch.no_grad()
-    def clip_gradients(self):
-        s = self.solver
-        grads = [p.grad for p in self.params if p.grad is not None]
-        if not grads or s.clip_type == "none":
-            return
-        if s.clip_type == "full_model":
-            torch.nn.utils.clip_grad_norm_(self.params, s.clip_value)
-            return
-        if self.flat is not None and self.device.type == "cuda":
-            self.flat.clip_(self.flat_grad, s.clip_value)      # csrc/optim.hip, 2 launches
-            return
-        # detectron2 "norm": clip_grad_norm_(p, clip_value) for every parameter, fused
-        # (one stacked scale vector: a handful of launches instead of several per parameter)
-        norms = torch.stack(torch._foreach_norm(grads))
-        scales = (s.clip_value / (norms + 1e-6)).clamp_(max=1.0)
-        torch._foreach_mul_(grads, list(scales.unbind(0)))
+    @property
+    def params(self):
+        """The trainable parameters in the optimiser's (flat) order."""
+        return self.opt.params
+
+    def master_params(self):
+        """f32 master weights, per parameter (views of the flat master buffer)."""
+        return self.opt.layout.views(self.opt.master)
 
     def forward_loss(self, images, mask_labels, class_labels):
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.mode == "amp"):
-            masks, classes = self.net(images)
+            masks, classes = self.model(images)
         masks = [m.float() for m in masks]
         classes = [c.float() for c in classes]
         return self.criterion(masks, classes, mask_labels, class_labels)
 
-    # ----------------------------------------------------------- graph-replayed step
-    def _phase1(self, images, mask_labels, class_labels):
-        """Forward + loss + backward, then the gradients into the flat buffer of the next
-        phase (f32 master grads; bf16 all-reduce buffer when split)."""
-        for p in self.model_params:
-            p.grad = None
-        loss, _ = self.forward_loss(images, mask_labels, class_labels)
+    # ----------------------------------------------------------------- step phases
+    def forward_backward(self, images, mask_labels, class_labels, reduce_mode: str = "eager"):
+        """Zeroed flat gradients, forward + loss + backward (autograd accumulates into the
+        flat buffer); with several ranks the buckets are reduced as they complete.
+        Returns (loss, loss components)."""
+        self.opt.zero_grad()
+        if self.reducer is not None:
+            self.reducer.begin(reduce_mode)
+        loss, parts = self.forward_loss(images, mask_labels, class_labels)
         loss.backward()
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.model_params]
-        with torch.no_grad():
-            torch._foreach_copy_(self.g16_views if self.split else [m.grad for m in self.params], grads)
-        return loss.detach()
+        if self.reducer is not None:
+            self.reducer.finish_backward()
+        return loss.detach(), parts
 
-    @torch.no_grad()
-    def _phase2(self):
-        """(split: averaged bf16 grads -> f32 master grads) clip, AdamW, master -> bf16."""
-        if self.split:
-            torch._foreach_copy_([m.grad for m in self.params], self.g16_views)
-            self.flat_grad.mul_(1.0 / dist.get_world_size())
-        self.clip_gradients()
+    def apply_gradients(self):
+        """clip + weight decay + update + bf16 cast (csrc/optim.hip)."""
         self.opt.step()
-        torch._foreach_copy_(self.model_params, self.params)
 
+    def _set_lr(self):
+        self.opt.set_lr(lr_at(self.solver, self.iter))
+
+    def eager_step(self, images, mask_labels, class_labels):
+        self._set_lr()
+        loss, _ = self.forward_backward(images, mask_labels, class_labels)
+        self.apply_gradients()
+        return loss
+
+    # ----------------------------------------------------------- graph-replayed step
     def _set_num_masks(self, class_labels):
         """split mode: the criterion's global target count, all-reduced eagerly (it is a
         graph input, not a collective inside the capture)."""
         self.num_masks_total.fill_(float(sum(int(t.shape[0]) for t in class_labels)))
         dist.all_reduce(self.num_masks_total)
         self.criterion.num_masks_total = self.num_masks_total
-
-    def _eager_split_step(self, images, mask_labels, class_labels):
-        self._set_num_masks(class_labels)
-        loss = self._phase1(images, mask_labels, class_labels)
-        dist.all_reduce(self.flat_g16)
-        self._phase2()
-        return loss
 
     def _capture(self, images, mask_labels, class_labels, kc):
         # static inputs: the image batch and the targets padded to kc (criterion.PaddedTargets),
@@ -235,14 +209,14 @@ class Trainer:
         torch._C._cuda_clearCublasWorkspaces()
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=pool):
-            st["loss"] = self._phase1(st["images"], st["tg"], None)
+            st["loss"], _ = self.forward_backward(st["images"], st["tg"], None, reduce_mode="capture")
             if not self.split:
-                self._phase2()
+                self.apply_gradients()
         st["graphs"].append(g1)
         if self.split:
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2, pool=pool):
-                self._phase2()
+                self.apply_gradients()
             st["graphs"].append(g2)
         torch.cuda.synchronize(self.device)
         torch._C._cuda_clearCublasWorkspaces()
@@ -251,8 +225,6 @@ class Trainer:
     def _drop_graphs(self):
         if not self._graph_states:
             return
-        for p in self.model_params:          # gradients living in the old graph's pool
-            p.grad = None
         for st in self._graph_states.values():
             for g in st["graphs"]:
                 g.reset()
@@ -266,75 +238,51 @@ class Trainer:
         if st is None:
             # one live graph per trainer (bounded pool memory): another signature's graph
             # is destroyed before any eager work of this one, and a returning signature is
-            # captured again.  (Replays that faulted after a recapture were ROCm's graph
-            # packet capture, disabled in visionseg/__init__.py; tools/graph_diag.py.)
+            # captured again
             self._drop_graphs()
             seen = self._eager_seen.get(key, 0)
             if seen < self.graph_warmup:
-                # eager steps first: lazy library state and the optimiser's moments exist
+                # eager steps first: lazy library state and the optimiser's state exist
                 # before the capture (a capture records launches, it runs nothing)
                 self._eager_seen[key] = seen + 1
-                return self._eager_split_step(images, mask_labels, class_labels) if self.split else \
-                    self._eager_bf16_step(images, mask_labels, class_labels)
+                if self.split:
+                    self._set_num_masks(class_labels)
+                return self.eager_step(images, mask_labels, class_labels)
             st = self._graph_states[key] = self._capture(images, mask_labels, class_labels, kc)
+        self._set_lr()
         with torch.no_grad():
             st["images"].copy_(images)
             st["tg"].copy_from_lists(mask_labels, class_labels)
         if self.split:
             self._set_num_masks(class_labels)
             st["graphs"][0].replay()
-            dist.all_reduce(self.flat_g16)
+            self.reducer.replay_collectives()
             st["graphs"][1].replay()
         else:
             st["graphs"][0].replay()
         return st["loss"].clone()
 
-    def _eager_bf16_step(self, images, mask_labels, class_labels):
-        loss = self._phase1(images, mask_labels, class_labels)
-        self._phase2()
-        return loss
-
     def step(self, images, mask_labels, class_labels):
         """One optimisation step; returns the (device) loss tensor, no host sync.  With
         graphs=True the step is captured per signature (image shape, largest target count
         of the batch; after `graph_warmup` eager steps of it) and replayed with the batch's
-        targets padded into static buffers: one launch per graph instead of ~3200 per
+        targets padded into static buffers: one launch per graph instead of ~3000 per
         step.  One signature's graph lives at a time: another signature destroys it and is
         captured in its place."""
         if self.graphs:
             loss = self._graph_step(images, mask_labels, class_labels)
-            self.sched.step()
-            self.iter += 1
-            return loss
-        if self.mode != "bf16":
-            self.opt.zero_grad(set_to_none=True)
-        for p in self.model_params:
-            p.grad = None
-        loss, _ = self.forward_loss(images, mask_labels, class_labels)
-        loss.backward()
-        if self.mode == "bf16":
-            # (DDP has already averaged the bf16 grads) -> the flat f32 master grads, one
-            # multi-tensor cast-copy
-            grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.model_params]
-            torch._foreach_copy_([m.grad for m in self.params], grads)
-        self.clip_gradients()
-        self.opt.step()
-        if self.mode == "bf16":
-            with torch.no_grad():
-                torch._foreach_copy_(self.model_params, self.params)
-        self.sched.step()
-        self.iter += 1
-        return loss.detach()
-
-    def state_dict(self):
-        if self.mode == "bf16":   # checkpoint the f32 master weights under the model's names
-            names = [n for n, p in self.model.named_parameters() if p.requires_grad]
-            sd = {k: v.float() for k, v in self.model.state_dict().items()}
-            sd.update({n: m.detach().clone() for n, m in zip(names, self.params)})
         else:
-            sd = self.model.state_dict()
-        return {"model": sd, "optimizer": self.opt.state_dict(),
-                "scheduler": self.sched.state_dict(), "iter": self.iter}
+            loss = self.eager_step(images, mask_labels, class_labels)
+        self.iter += 1
+        return loss
+
+    # ------------------------------------------------------------------ checkpoints
+    def state_dict(self):
+        """The model's state dict with the f32 master weights under the model's names,
+        the flat optimiser state, and the iteration."""
+        sd = {k: v.float() if v.is_floating_point() else v for k, v in self.model.state_dict().items()}
+        sd.update({n: m.detach().cpu().clone() for n, m in zip(self.opt.names, self.master_params())})
+        return {"model": sd, "optimizer": self.opt.state_dict(), "iter": self.iter}
 
     def save(self, path):
         """Checkpoint (rank 0 writes; detectron2 PeriodicCheckpointer equivalent)."""
@@ -342,13 +290,14 @@ class Trainer:
             torch.save(self.state_dict(), path)
 
     def load(self, path):
-        sd = torch.load(path, map_location=self.device, weights_only=True)
-        self.model.load_state_dict(sd["model"])
-        if self.mode == "bf16":
-            names = [n for n, p in self.model.named_parameters() if p.requires_grad]
-            with torch.no_grad():
-                for n, m in zip(names, self.params):
-                    m.copy_(sd["model"][n])
+        """Resume: weights, optimiser state and iteration.  Captured graphs are dropped
+        first (they hold the previous run's static inputs) and recaptured on demand."""
+        self._drop_graphs()
+        self._eager_seen.clear()
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        with torch.no_grad():
+            self.model.load_state_dict({k: v for k, v in sd["model"].items() if k not in self.opt.names},
+                                       strict=False)
+            self.opt.load_master(sd["model"])
         self.opt.load_state_dict(sd["optimizer"])
-        self.sched.load_state_dict(sd["scheduler"])
         self.iter = int(sd["iter"])
