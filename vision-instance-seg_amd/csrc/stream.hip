@@ -1,8 +1,8 @@
 // In-graph event nodes for the overlapped gradient all-reduce (visionseg/optim.py
 // GradReducer): while the forward+backward step is captured into a HIP graph, each
 // all-reduce bucket's completion point is marked with an EXTERNAL event record
-// (hipEventRecordWithFlags(..., hipEventRecordExternal)), which the capture turns into an
-// event-record node of the graph instead of a capture-internal dependency.  After the
+// (an event-record node added to the graph being captured, after the stream's capture
+// frontier) instead of a capture-internal dependency.  After the
 // graph is launched, a side stream waits on those events (hipStreamWaitEvent) and issues
 // the RCCL all-reduce of each bucket there, overlapping the rest of the replay.
 // (torch.cuda.Event(external=True) is refused on ROCm builds of PyTorch, hence these
@@ -26,7 +26,25 @@ extern "C" int vs_event_destroy(void* event) {
 
 extern "C" int vs_event_record_external(void* event, void* stream) {
   VS_CHECK(event, "null event");
-  VS_HIP(hipEventRecordWithFlags((hipEvent_t)event, (hipStream_t)stream, hipEventRecordExternal));
+  hipStream_t s = (hipStream_t)stream;
+  hipEvent_t e = (hipEvent_t)event;
+  hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  VS_HIP(hipStreamGetCaptureInfo_v2(s, &status, &id, &graph, &deps, &ndeps));
+  if (status != hipStreamCaptureStatusActive) {
+    VS_HIP(hipEventRecord(e, s));
+    return VS_OK;
+  }
+  // Under capture: what hipEventRecordWithFlags(..., hipEventRecordExternal) documents
+  // (the ROCm 7.2 runtime rejects that flag during capture), done by hand: an
+  // event-record node after the stream's current capture frontier, which then becomes
+  // the frontier.
+  hipGraphNode_t node;
+  VS_HIP(hipGraphAddEventRecordNode(&node, graph, deps, ndeps, e));
+  VS_HIP(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
   return VS_OK;
 }
 

@@ -207,15 +207,18 @@ class Trainer:
         # clear_cublass_cache does the same)
         pool = torch.cuda.graph_pool_handle()
         torch._C._cuda_clearCublasWorkspaces()
+        # several ranks: "thread_local" capture, so RCCL's watchdog thread may keep querying
+        # the events of earlier eager collectives while this thread captures
+        mode = "thread_local" if self.split else "global"
         g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, pool=pool):
+        with torch.cuda.graph(g1, pool=pool, capture_error_mode=mode):
             st["loss"], _ = self.forward_backward(st["images"], st["tg"], None, reduce_mode="capture")
             if not self.split:
                 self.apply_gradients()
         st["graphs"].append(g1)
         if self.split:
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=pool):
+            with torch.cuda.graph(g2, pool=pool, capture_error_mode=mode):
                 self.apply_gradients()
             st["graphs"].append(g2)
         torch.cuda.synchronize(self.device)
