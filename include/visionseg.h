@@ -82,31 +82,6 @@ VS_API int vs_msda_backward(int dtype, const void* value, const int64_t* spatial
                      int num_heads, int channels, int num_levels, int num_query,
                      int num_point, void* stream);
 
-/* Encoder self-attention backward (the pixel decoder's case: the queries ARE the value
- * grid, Q == S, level-major).  Same tensors as vs_msda_backward with num_query = S;
- * grad_value is produced by destination bands in LDS (no global atomics except for
- * taps more than 4 rows from their query's mapped row).  Same results up to f32
- * summation order. */
-VS_API int vs_msda_backward_encoder(int dtype, const void* value, const int64_t* spatial_shapes_host,
-                                    const int64_t* level_start_host, const float* sampling_loc,
-                                    const float* attn_weight, const void* grad_out, float* grad_value,
-                                    float* grad_loc, float* grad_attn, int batch, int spatial_size,
-                                    int num_heads, int channels, int num_levels, int num_point,
-                                    void* stream);
-
-/* Backward with grad_value built by destination after a counting sort of the corner
- * contributions (any queries; no float atomics): grad_value [B, S, H, 32] is written in
- * the value dtype (every row once), grad_loc / grad_attn as in vs_msda_backward.  Same
- * results up to f32 summation order.  workspace >= vs_msda_backward_sorted_workspace_bytes. */
-VS_API long long vs_msda_backward_sorted_workspace_bytes(int batch, int spatial_size, int num_heads, int num_query,
-                                                         int num_levels, int num_point);
-VS_API int vs_msda_backward_sorted(int dtype, const void* value, const int64_t* spatial_shapes_host,
-                                   const int64_t* level_start_host, const float* sampling_loc,
-                                   const float* attn_weight, const void* grad_out, void* grad_value,
-                                   float* grad_loc, float* grad_attn, void* workspace, int batch, int spatial_size,
-                                   int num_heads, int channels, int num_levels, int num_query, int num_point,
-                                   void* stream);
-
 /* Opt-in backward (VS_MSDA_BWD=tiled; replaces ms_deform_attn_backward like the others):
  * grad_value by destination tiles
  * (image, head, level, te x te cells), each owned by one wave that accumulates its

@@ -373,14 +373,12 @@ def test_mask_head_backward_bf16_vs_oracle(shape):
     dict(B=2, shapes=[(48, 80), (24, 40), (12, 20), (6, 10)], H=4, spread=3.0),  # 4 levels, finest first
 ])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("near_r", ["5", "0", "9"])
-def test_msda_encoder_backward_vs_oracle(monkeypatch, cfg, dtype, near_r):
-    """Encoder mode (queries = value grid): LDS destination-tile kernel (near taps) +
-    far-tap atomics vs the oracle; R0 = 0 sends most taps through the far (atomic) path."""
-    monkeypatch.setenv("VS_MSDA_NEAR_R", near_r)
+def test_msda_encoder_shapes_backward_vs_oracle(cfg, dtype):
+    """The default backward (geom gather + query-tile LDS-window scatter) on pixel-decoder
+    encoder problems (queries = value grid) vs the oracle: the 1024^2 level shapes with
+    init-like offsets, many far taps (clipped windows: direct atomics), non-square
+    levels, and 4 levels stored finest first."""
     ops = _ops()
-    monkeypatch.setattr(ops, "_MSDA_SORTED", False)          # the atomic scatter paths
-    monkeypatch.setattr(ops, "_MSDA_BWD", "carry")
     shapes, B, H, L, P = cfg["shapes"], cfg["B"], cfg["H"], len(cfg["shapes"]), 4
     S = sum(h * w for h, w in shapes)
     g = torch.Generator().manual_seed(31)
@@ -396,7 +394,7 @@ def test_msda_encoder_backward_vs_oracle(monkeypatch, cfg, dtype, near_r):
     go_q = go.to(dtype).float()
     out_r.backward(go_q)
     vd, ld, wd = value.to(DEV).requires_grad_(True), loc.to(DEV).requires_grad_(True), w.to(DEV).requires_grad_(True)
-    out = ops.ms_deform_attn(vd, shapes, ld, wd, encoder=True)
+    out = ops.ms_deform_attn(vd, shapes, ld, wd)
     out.backward(go.to(dtype).to(DEV))
     if dtype == torch.float32:
         # f32: the coordinate x*W-0.5 carries ~|xW|*2^-24 rounding (fma vs mul+sub), scaled
@@ -408,12 +406,6 @@ def test_msda_encoder_backward_vs_oracle(monkeypatch, cfg, dtype, near_r):
         gvr = vr.grad
         err = (vd.grad.float().cpu() - gvr).abs()
         assert bool((err <= gvr.abs() * 2 ** -8 + 1e-4).all()), float(err.max())
-    # encoder mode and the general (all-atomic) path agree
-    vd2 = value.to(DEV).requires_grad_(True)
-    out2 = ops.ms_deform_attn(vd2, shapes, loc.to(DEV), w.to(DEV), encoder=False)
-    out2.backward(go.to(dtype).to(DEV))
-    d = (vd2.grad.float() - vd.grad.float()).abs().max().item()
-    assert d <= (1e-5 if dtype == torch.float32 else 2 ** -7 * float(vd.grad.float().abs().max())), d
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -455,20 +447,26 @@ def _encoder_like_inputs(B, shapes, H, P, seed, jitter):
     return value, loc, w
 
 
-@pytest.mark.parametrize("run,win", [("16", "1"), ("16", "0"), ("7", "0"), ("0", "0"), ("16", "sub")])
+@pytest.mark.parametrize("run,win", [("16", "tile"), ("16", "tile8"), ("16", "0"), ("7", "0"), ("0", "0"),
+                                     ("16", "sub"), ("16", "tile-1024"), ("16", "tile-odd"), ("16", "tile8-odd")])
 @pytest.mark.parametrize("jitter", [0.0, 0.3, 3.0])
 def test_msda_carry_backward_vs_oracle(monkeypatch, run, win, jitter):
-    """Atomic-scatter grad_value on encoder-shaped queries vs the oracle: the query-tile
-    LDS-window kernel (csrc/msda.hip msda_bwd_window_kernel; 4x4 grid tiles, or runs of
-    16 queries for a query subset "sub"), the register-carry kernel with runs of 16 / 7
-    (ragged) queries, and the plain kernel (run 0)."""
+    """Atomic-scatter grad_value on encoder-shaped queries vs the oracle: the binned
+    query-tile kernel (csrc/msda.hip msda_bwd_binned_kernel; 4x4 grid tiles "tile", 8x8
+    "tile8", also at the 1024^2 level shapes and on odd level sizes with partial tiles, or
+    runs of 16 queries for a query subset "sub"), the register-carry kernel with runs of
+    16 / 7 (ragged) queries, and the plain kernel (run 0)."""
     monkeypatch.setenv("VS_MSDA_RUN", run)
     monkeypatch.setenv("VS_MSDA_WIN", "0" if win == "0" else "1")
+    monkeypatch.setenv("VS_MSDA_TILE", "8" if win.startswith("tile8") else "4")
     ops = _ops()
-    monkeypatch.setattr(ops, "_MSDA_SORTED", False)
     monkeypatch.setattr(ops, "_MSDA_BWD", "carry")
-    shapes = [(8, 8), (16, 16), (32, 32)]
-    value, loc, w = _encoder_like_inputs(2, shapes, 4, 4, seed=11, jitter=jitter)
+    shapes, B, H = [(8, 8), (16, 16), (32, 32)], 2, 4
+    if win == "tile-1024":
+        shapes, B, H = [(32, 32), (64, 64), (128, 128)], 1, 8
+    elif win.endswith("-odd"):
+        shapes = [(9, 13), (18, 26), (35, 51)]
+    value, loc, w = _encoder_like_inputs(B, shapes, H, 4, seed=11, jitter=jitter)
     if win == "sub":                                   # Q != S: windows over runs of 16 queries
         idx = torch.randperm(loc.shape[1], generator=torch.Generator().manual_seed(5))[:700].sort().values
         loc, w = loc[:, idx].contiguous(), w[:, idx].contiguous()
@@ -480,7 +478,10 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, win, jitter):
     out = ops.ms_deform_attn(vd, shapes, ld, wd)
     out.backward(go.to(DEV))
     np.testing.assert_allclose(vd.grad.cpu().numpy(), vr.grad.numpy(), atol=2e-5, rtol=0)
-    np.testing.assert_allclose(wd.grad.cpu().numpy(), wr.grad.numpy(), atol=2e-5, rtol=0)
+    # grad_attn / grad_loc: fp32 dots of 32 channels whose interpolation weights differ by
+    # an ulp of the unnormalised coordinate (fma on the GPU) -- relative to their scale
+    gw = wr.grad.numpy()
+    np.testing.assert_allclose(wd.grad.cpu().numpy(), gw, atol=2e-5 * max(1.0, np.abs(gw).max()), rtol=0)
     gl = lr.grad.numpy()
     np.testing.assert_allclose(ld.grad.cpu().numpy(), gl, atol=2e-5 * max(1.0, np.abs(gl).max()), rtol=0)
 
@@ -494,13 +495,12 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, win, jitter):
     dict(B=1, shapes=[(5, 7)], H=2, jitter=1.0, Q=0),                                  # no queries
 ])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("mode", ["tiled", "sorted"])
+@pytest.mark.parametrize("mode", ["tiled"])
 def test_msda_destination_backward_vs_oracle(monkeypatch, case, dtype, mode):
-    """grad_value by destination -- tiles owned by one wave (vs_msda_backward_tiled, the
-    default) or after a per-cell counting sort (vs_msda_backward_sorted, opt-in) -- vs the
-    oracle; bf16: grad_value is produced in bf16 from f32 sums."""
+    """Deterministic backward: grad_value by destination tiles owned by one wave
+    (vs_msda_backward_tiled, VS_MSDA_BWD=tiled; no float atomics) vs the oracle; bf16:
+    grad_value is produced in bf16 from f32 sums."""
     ops = _ops()
-    monkeypatch.setattr(ops, "_MSDA_SORTED", mode == "sorted")
     monkeypatch.setattr(ops, "_MSDA_BWD", mode)
     shapes, B, H = case["shapes"], case["B"], case["H"]
     value, loc, w = _encoder_like_inputs(B, shapes, H, 4, seed=21, jitter=case["jitter"])

@@ -40,6 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="msda,mask,win,xattn")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--msda-modes", default="window,carry16,tiled")
     a = ap.parse_args()
     dev = "cuda"
     bf = torch.bfloat16
@@ -65,20 +66,17 @@ def main():
         for oname, off in offs.items():
             loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
             locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
-            for mode in ("window", "carry16", "tiled", "sorted"):
-                ops._MSDA_SORTED = mode == "sorted"
-                ops._MSDA_BWD = {"tiled": "tiled", "sorted": "sorted"}.get(mode, "carry")
+            for mode in a.msda_modes.split(","):
+                ops._MSDA_BWD = "tiled" if mode == "tiled" else "carry"
                 os.environ["VS_MSDA_RUN"] = {"carry16": "16", "window": "16"}.get(mode, "0")
                 os.environ["VS_MSDA_WIN"] = "1" if mode == "window" else "0"
-                os.environ["VS_MSDA_NEAR_R"] = mode[4:] if mode.startswith("pull") else "5"
 
-                def fb(enc=mode.startswith("pull")):
-                    o = ops.ms_deform_attn(v, shapes, locr, wr, encoder=enc)
+                def fb():
+                    o = ops.ms_deform_attn(v, shapes, locr, wr)
                     o.backward(go)
                 run(f"msda {oname} {mode}", fb, a.iters)
             os.environ.pop("VS_MSDA_RUN")
             os.environ.pop("VS_MSDA_WIN")
-            os.environ.pop("VS_MSDA_NEAR_R")
     if "mask" in a.only:
         Q, C, Hm = 100, 256, 256
         E = torch.randn(B, Q, C, device=dev, generator=g).to(bf).requires_grad_(True)

@@ -10,26 +10,17 @@
 // one 16-B load per lane, adjacent lanes read adjacent bytes; the group's loc/attn
 // rows (96 B / 48 B, 16-B aligned) are read as float4.  Accumulation in f32.
 //
-// Backward, general queries (decoder cross-attention, or whenever the encoder path
-// does not apply): grad_loc / grad_attn from a gather kernel (msda_bwd_geom_kernel) and
-// grad_value from a scatter kernel with a register carry (msda_bwd_scatter_kernel; see
-// there).  Small problems use the single fused kernel (msda_bwd_kernel, one f32 atomic
-// per corner).  grad_value is bound by the float-atomic rate (~1.3 TB/s of added bytes,
-// MI355X_MICROARCH §Global float atomics).
-//
-// Backward, encoder self-attention (queries ARE the value grid, Q == S, level-major),
-// opt-in (encoder=True): grad_value is first PULLED by destination
-// (msda_bwd_pull_kernel): a wave owns a 4x16 block of value cells of one (image, head,
-// level l), enumerates the queries of levels not finer than l whose reference point
-// maps within R0 cells of the block (an implicit inverse index: the queries are the
-// grid), stages their taps and grad_out rows in LDS and accumulates each cell's 32
-// channels in registers; every grad_value element is written once with a plain store.
-// The carry scatter kernel then adds every other tap (finer query levels, or farther
-// than R0 cells) with atomics; pull_tap() assigns each tap to exactly one of the two.
-// Measured at 4x1024^2 (tools/msda_probe.py, smooth offsets, R0 = 5): pull 0.9 ms +
-// scatter 2.1 ms + geom 0.36 ms, against geom + carry scatter ~2.0 ms for the default
-// path — the remaining atomics pile onto the small coarse levels and the per-query level
-// decode costs integer divisions — so the model uses the default path.
+// Backward: grad_loc / grad_attn from a gather kernel (msda_bwd_geom_kernel); grad_value
+// (f32, then cast) by a scatter with f32 global atomics (~1.3 TB/s of added bytes,
+// MI355X_MICROARCH §Global float atomics):
+//   * default (P == 4, enough queries): the binned query-tile kernel
+//     (msda_bwd_binned_kernel; grid tiles of 4 x 4 queries when the queries are the
+//     value grid -- the pixel-decoder encoder --, else runs of 16 queries): counting
+//     sort of the tile's corners by cell, register sums, one atomic row per cell;
+//   * VS_MSDA_WIN=0: the register-carry scatter (msda_bwd_scatter_kernel);
+//   * small problems / other P: one fused kernel (msda_bwd_kernel, an atomic per corner).
+// vs_msda_backward_tiled is the deterministic, atomic-free variant (grad_value by
+// destination tile, written once in the value dtype; ops VS_MSDA_BWD=tiled).
 #include "common.h"
 
 namespace vs {
@@ -45,9 +36,8 @@ struct Levels {
 };
 
 
-// ---- backward helpers shared by the tile and scatter kernels (must stay identical: a
-// tap is accumulated by exactly one of them, decided by `near_tap`).
-constexpr int kNearR = 5;           // default near margin R0 of the tile kernel (VS_MSDA_NEAR_R)
+// ---- tap geometry shared by every backward kernel (the same fp32 floor/frac math as the
+// forward: a tap's corners and weights are identical everywhere).
 
 struct Tap {
   int h0, w0;
@@ -68,30 +58,6 @@ __device__ __forceinline__ Tap tap_geom(float x, float y, int Hl, int Wl) {
   t.hh = 1.f - t.lh;
   t.hw = 1.f - t.lw;
   return t;
-}
-
-// Cell of level l (extent nl) onto which query coordinate xq of level lq (extent nq)
-// maps: floor((xq + 0.5) * nl / nq - 0.5), integer arithmetic (exact, no fp ambiguity).
-__host__ __device__ __forceinline__ int mapped_cell(int xq, int nq, int nl) {
-  const int num = (2 * xq + 1) * nl - nq;
-  const int den = 2 * nq;
-  return num >= 0 ? num / den : -((-num + den - 1) / den);
-}
-
-// a tap belongs to the tile kernel ("near") iff it is inside and its top-left cell is
-// within R0 cells (both axes) of the query's mapped cell on the tap's level; every other
-// tap is added by the scatter kernel
-__device__ __forceinline__ bool near_tap(const Tap& t, int mcy, int mcx, int R0) {
-  return t.inside && abs(t.h0 - mcy) <= R0 && abs(t.w0 - mcx) <= R0;
-}
-
-__device__ __forceinline__ int ceil_div(int a, int b) { return a >= 0 ? (a + b - 1) / b : -((-a) / b); }
-
-// exact range of query coordinates x (level extent nq) whose mapped cell on a level of
-// extent nl lies in [lo, hi]:  mapped_cell(x) >= lo  <=>  x >= ceil(((2lo+1)nq - nl) / 2nl)
-__device__ __forceinline__ void mapped_range(int lo, int hi, int nq, int nl, int* xa, int* xb) {
-  *xa = max(0, ceil_div((2 * lo + 1) * nq - nl, 2 * nl));
-  *xb = min(nq - 1, ceil_div((2 * hi + 3) * nq - nl, 2 * nl) - 1);
 }
 
 template <typename T>
@@ -346,12 +312,10 @@ __global__ void __launch_bounds__(256) msda_bwd_geom_kernel(
 
 constexpr int kScatterRun = 16;        // queries per half-wave run (LDS staging is sized for it)
 
-// ENC (encoder mode, Q == S level-major): near taps (near_tap) are skipped here; the
-// tile kernel has already written every grad_value element.
-template <typename T, int L, int P, bool ENC>
+template <typename T, int L, int P>
 __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
     const float* __restrict__ loc, const float* __restrict__ attw, const T* __restrict__ gout,
-    float* __restrict__ gvalue, Levels lv, int S, int Hh, int Q, int R, int nrun, long long halfwaves, int R0) {
+    float* __restrict__ gvalue, Levels lv, int S, int Hh, int Q, int R, int nrun, long long halfwaves) {
   constexpr int LP = L * P;
   // per half-wave staging: loc [R][LP][2], attn [R][LP], grad_out [R][32] (f32)
   constexpr int kStage = kScatterRun * (LP * 3 + kD);
@@ -397,13 +361,6 @@ __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
   };
   for (int i = 0; i < nq; ++i) {
     const float g = sg[i * kD + c];
-    int lq = 0, yq = 0, xq = 0;
-    if (ENC) {
-      const int q = q0 + i;
-      while (lq + 1 < L && q >= lv.start[lq + 1]) ++lq;
-      yq = (q - lv.start[lq]) / lv.w[lq];
-      xq = (q - lv.start[lq]) % lv.w[lq];
-    }
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       const int Hl = lv.h[l], Wl = lv.w[l];
@@ -413,7 +370,6 @@ __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
         const int t = l * P + p;
         const Tap tg = tap_geom(sl[(i * LP + t) * 2 + 0], sl[(i * LP + t) * 2 + 1], Hl, Wl);
         if (!tg.inside) continue;             // no contribution; the held block stays
-        if (ENC && near_tap(tg, mapped_cell(yq, lv.h[lq], Hl), mapped_cell(xq, lv.w[lq], Wl), R0)) continue;
         const float ga = g * sw[i * LP + t];
         const int dy = tg.h0 - ph[t], dx = tg.w0 - pw[t];
         // held corner k = (cy, cx) survives iff (cy - dy, cx - dx) lies in the new block
@@ -450,233 +406,11 @@ __global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
   }
 }
 
-// grad_value by destination tile (encoder mode; see the header).  Block = (16x16 cell
-// tile of level l, head, image); the tile's 256 cells x 32 channels are accumulated in
-// LDS (32 KB f32).  For every query level lq the block enumerates the rectangle of
-// queries whose mapped cell on level l lies within R0 cells of a corner block touching
-// the tile (mapped_range), 16 queries per wave at a time: lane = (query, point) computes
-// the tap on level l, keeps it if near_tap() and one of its four corners is in the tile,
-// and the kept taps are compacted (wave ballot) into a per-wave list with the query's
-// grad_out row staged in LDS.  Then the two half-waves walk the list with lane = channel
-// and add weight * grad_out into the tile with LDS float atomics (32 consecutive floats
-// per half-wave: conflict-free).  Far taps are left to the scatter kernel.  Finally every
-// cell of the tile is stored once (plain f32 stores; the scatter adds on top).
-//
-// Work per tile grows with the number of queries mapping into its window, so coarse
-// levels (whose window holds the finer levels' queries) cost more per tile: the block
-// order is tile-major with the coarsest level first (longest jobs start first), and the
-// heads of one (tile, image) are consecutive workgroups of one XCD (their loc / grad_out
-// rows share cache lines).
-constexpr int kTile = 16;
-
-struct TileOrder {
-  int level[kMaxLevels];      // levels by ascending cell count (coarsest first)
-  int prefix[kMaxLevels + 1]; // tile-slot prefix over that order (slots = tiles x images)
-  int slots;                  // total (tile, image) slots
-};
-
-template <typename T>
-__global__ void __launch_bounds__(256) msda_bwd_tile_kernel(const float* __restrict__ loc,
-                                                            const float* __restrict__ attw,
-                                                            const T* __restrict__ gout, float* __restrict__ gvalue,
-                                                            Levels lv, int S, int Hh, int B, int L, int R0,
-                                                            TileOrder to) {
-  constexpr int P = 4;
-  __shared__ __attribute__((aligned(16))) float sAcc[kTile * kTile * kD];
-  __shared__ int4 sCell[4][64];
-  __shared__ float4 sWgt[4][64];
-  __shared__ int sQ[4][64];
-  __shared__ __attribute__((aligned(16))) float sG[4][16][kD];
-  // physical id -> (slot, head): workgroup i runs on XCD i % 8; heads of one slot are
-  // consecutive workgroups of that XCD, slots advance in order (coarsest level first)
-  const int i = blockIdx.x;
-  const int xcd = i & 7, j = i >> 3;
-  const int h = j % Hh;
-  const int slot = (j / Hh) * 8 + xcd;
-  if (slot >= to.slots) return;                     // padding (uniform per block)
-  int oi = 0;
-  while (oi + 1 < L && slot >= to.prefix[oi + 1]) ++oi;
-  const int l = to.level[oi];
-  const int local = slot - to.prefix[oi];
-  const int b = local % B, t = local / B;
-  const int Hl = lv.h[l], Wl = lv.w[l];
-  const int txn = (Wl + kTile - 1) / kTile;
-  const int ty0 = (t / txn) * kTile, tx0 = (t % txn) * kTile;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int LP = L * P;
-
-  for (int k = tid; k < kTile * kTile * kD / 4; k += 256)
-    reinterpret_cast<float4*>(sAcc)[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
-
-  const int half = lane >> 5, c = lane & 31;
-  for (int lq = 0; lq < L; ++lq) {
-    const int Hq = lv.h[lq], Wq = lv.w[lq];
-    // a near tap's top-left cell is within R0 of the query's mapped cell; its corner
-    // block touches the tile iff the top-left cell is in [tile0 - 1, tile0 + 15]
-    int ya, yb, xa, xb;
-    mapped_range(ty0 - 1 - R0, ty0 + kTile - 1 + R0, Hq, Hl, &ya, &yb);
-    mapped_range(tx0 - 1 - R0, tx0 + kTile - 1 + R0, Wq, Wl, &xa, &xb);
-    if (ya > yb || xa > xb) continue;
-    const int nx = xb - xa + 1;
-    const int ncand = (yb - ya + 1) * nx;
-    for (int base = wave * 16; base < ncand; base += 64) {
-      // ---- geometry: lane = (query base + lane/4, point lane%4)
-      const int qi = base + (lane >> 2), p = lane & 3;
-      int4 cell = make_int4(-1, -1, -1, -1);
-      float4 wgt = make_float4(0.f, 0.f, 0.f, 0.f);
-      bool keep = false;
-      long long grp = 0;
-      if (qi < ncand) {
-        const int yq = ya + qi / nx, xq = xa + qi % nx;
-        grp = ((long long)b * S + lv.start[lq] + yq * Wq + xq) * Hh + h;
-        const int mcy = mapped_cell(yq, Hq, Hl), mcx = mapped_cell(xq, Wq, Wl);
-        const float2 xy = *reinterpret_cast<const float2*>(loc + (grp * LP + l * P + p) * 2);
-        const float a = attw[grp * LP + l * P + p];
-        const Tap tg = tap_geom(xy.x, xy.y, Hl, Wl);
-        if (near_tap(tg, mcy, mcx, R0)) {
-          const int ry0 = tg.h0 - ty0, rx0 = tg.w0 - tx0;
-          const bool y0in = (unsigned)ry0 < (unsigned)kTile && tg.h0 >= 0;
-          const bool y1in = (unsigned)(ry0 + 1) < (unsigned)kTile && tg.h0 + 1 < Hl;
-          const bool x0in = (unsigned)rx0 < (unsigned)kTile && tg.w0 >= 0;
-          const bool x1in = (unsigned)(rx0 + 1) < (unsigned)kTile && tg.w0 + 1 < Wl;
-          const int base_cell = (ry0 * kTile + rx0) * kD;
-          cell.x = y0in && x0in ? base_cell : -1;
-          cell.y = y0in && x1in ? base_cell + kD : -1;
-          cell.z = y1in && x0in ? base_cell + kTile * kD : -1;
-          cell.w = y1in && x1in ? base_cell + (kTile + 1) * kD : -1;
-          wgt = make_float4(tg.hh * tg.hw * a, tg.hh * tg.lw * a, tg.lh * tg.hw * a, tg.lh * tg.lw * a);
-          keep = cell.x >= 0 || cell.y >= 0 || cell.z >= 0 || cell.w >= 0;
-        }
-      }
-      // ---- grad_out rows of the wave's 16 queries -> LDS (lane = query lane/4, 8 channels)
-      {
-        const int qg = lane >> 2, c8 = (lane & 3) * 8;
-        const int qn = base + qg;
-        float gv[8];
-        if (qn < ncand) {
-          const int yq = ya + qn / nx, xq = xa + qn % nx;
-          const long long g2 = ((long long)b * S + lv.start[lq] + yq * Wq + xq) * Hh + h;
-          Vec16<T>::load(gout + g2 * kD + c8, gv);
-          if constexpr (Vec16<T>::N == 4) Vec16<T>::load(gout + g2 * kD + c8 + 4, gv + 4);
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) gv[k] = 0.f;
-        }
-        float4* dst = reinterpret_cast<float4*>(&sG[wave][qg][c8]);
-        dst[0] = make_float4(gv[0], gv[1], gv[2], gv[3]);
-        dst[1] = make_float4(gv[4], gv[5], gv[6], gv[7]);
-      }
-      // ---- compact the kept taps
-      const unsigned long long mask = __ballot(keep);
-      const int n = __popcll(mask);
-      if (keep) {
-        const int pos = __popcll(mask & ((1ull << lane) - 1ull));
-        sCell[wave][pos] = cell;
-        sWgt[wave][pos] = wgt;
-        sQ[wave][pos] = lane >> 2;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // ---- add: half-wave per list entry, lane = channel
-      for (int e = half; e < n; e += 2) {
-        const int4 ce = sCell[wave][e];
-        const float4 we = sWgt[wave][e];
-        const float g = sG[wave][sQ[wave][e]][c];
-        if (ce.x >= 0) atomicAdd(&sAcc[ce.x + c], we.x * g);
-        if (ce.y >= 0) atomicAdd(&sAcc[ce.y + c], we.y * g);
-        if (ce.z >= 0) atomicAdd(&sAcc[ce.z + c], we.z * g);
-        if (ce.w >= 0) atomicAdd(&sAcc[ce.w + c], we.w * g);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-  }
-  __syncthreads();
-  // ---- store the tile: 8 consecutive lanes per cell (128 B), every cell once
-  const size_t rowstride = (size_t)Hh * kD;
-  float* gl = gvalue + (((size_t)b * S + lv.start[l]) * Hh + h) * kD;
-  for (int k = tid; k < kTile * kTile * 8; k += 256) {
-    const int cl = k >> 3, part = k & 7;
-    const int cy = ty0 + cl / kTile, cx = tx0 + cl % kTile;
-    if (cy < Hl && cx < Wl)
-      *reinterpret_cast<float4*>(gl + (size_t)(cy * Wl + cx) * rowstride + part * 4) =
-          reinterpret_cast<const float4*>(sAcc)[k];
-  }
-}
-
 // ---------------------------------------------------------------------------------
-// grad_value by destination after a counting sort of the corner contributions (no float
-// atomics).  key(b, cell, h) = (b * S + cell) * Hh + h: the grad_value row of that
-// head, so keys in order are the output in order.
-//   count:  per valid corner of every tap, count[key] += 1 (int atomics)
-//   scan:   offset(key) = exclusive prefix of count (1024-key blocks + block prefix)
-//   fill:   slot = offset(key) + (atomicSub(count[key], 1) - 1): record {query, weight}
-//           (count returns to 0)
-//   pull:   a group of lanes per key sums weight * grad_out[b, query, h, :] over its
-//           records in f32 and writes the row once, in the value dtype
-// The contributions reaching one row come from the queries whose taps land next to it;
-// their grad_out rows are re-read from L2 / MALL, not HBM.
+// Exclusive prefix scan of per-tile counts (1024-entry blocks + a block prefix), used by
+// the destination-tile backward below.
 constexpr int kScanBlock = 1024;
 
-__device__ __forceinline__ void corner_keys(const Tap& tg, int Wl, int Hl, long long rowbase, int Hh, long long* key,
-                                            float* wk) {
-  const int h0 = tg.h0, w0 = tg.w0;
-  const bool ok[4] = {h0 >= 0 && w0 >= 0, h0 >= 0 && w0 + 1 <= Wl - 1, h0 + 1 <= Hl - 1 && w0 >= 0,
-                      h0 + 1 <= Hl - 1 && w0 + 1 <= Wl - 1};
-  const int off[4] = {h0 * Wl + w0, h0 * Wl + w0 + 1, (h0 + 1) * Wl + w0, (h0 + 1) * Wl + w0 + 1};
-  wk[0] = tg.hh * tg.hw;
-  wk[1] = tg.hh * tg.lw;
-  wk[2] = tg.lh * tg.hw;
-  wk[3] = tg.lh * tg.lw;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) key[k] = ok[k] ? (rowbase + off[k]) * Hh : -1;
-}
-
-// one thread per tap (b, q, h, l, p); FILL = false: count, true: write records
-template <bool FILL>
-__global__ void __launch_bounds__(256) msda_sort_kernel(const float* __restrict__ loc, const float* __restrict__ attw,
-                                                        int* __restrict__ count, const int* __restrict__ local,
-                                                        const int* __restrict__ bprefix, int2* __restrict__ rec,
-                                                        Levels lv, int S, int Hh, int Q, int L, int P, long long taps) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= taps) return;
-  const int LP = L * P;
-  const int t = (int)(i % LP);
-  const long long grp = i / LP;
-  const int h = (int)(grp % Hh);
-  const long long bq = grp / Hh;
-  const int q = (int)(bq % Q);
-  const long long b = bq / Q;
-  const int l = t / P;
-  const int Hl = lv.h[l], Wl = lv.w[l];
-  const float2 xy = reinterpret_cast<const float2*>(loc)[i];
-  const Tap tg = tap_geom(xy.x, xy.y, Hl, Wl);
-  if (!tg.inside) return;
-  long long key[4];
-  float wk[4];
-  corner_keys(tg, Wl, Hl, b * S + lv.start[l], Hh, key, wk);
-  if (!FILL) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (key[k] >= 0) atomicAdd(count + key[k] + h, 1);
-  } else {
-    const float a = attw[i];
-    int slot[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) slot[k] = key[k] >= 0 ? atomicSub(count + key[k] + h, 1) - 1 : 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (key[k] >= 0) {
-        const long long kk = key[k] + h;
-        rec[local[kk] + bprefix[kk / kScanBlock] + slot[k]] = make_int2(q, __float_as_int(a * wk[k]));
-      }
-  }
-}
-
-// block-local exclusive scan of count (kScanBlock keys per block) + block totals
 __global__ void __launch_bounds__(256) sort_scan_local_kernel(const int* __restrict__ count, int* __restrict__ local,
                                                               int* __restrict__ bsum, long long n) {
   __shared__ int sw[4];
@@ -736,53 +470,6 @@ __global__ void __launch_bounds__(1024) sort_scan_blocks_kernel(const int* __res
 }
 
 // one group of LPG lanes per key (grad_value row of one head), V channels per lane
-template <typename T>
-__global__ void __launch_bounds__(256) msda_pull_sorted_kernel(const int* __restrict__ local,
-                                                               const int* __restrict__ bprefix,
-                                                               const int2* __restrict__ rec, const T* __restrict__ gout,
-                                                               T* __restrict__ gvalue, int S, int Hh, int Q,
-                                                               long long nkeys) {
-  constexpr int V = Vec16<T>::N;
-  constexpr int LPG = kD / V;
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long key = gid / LPG;
-  const int sub = (int)(gid % LPG);
-  if (key >= nkeys) return;
-  const int r0 = local[key] + bprefix[key / kScanBlock];
-  const int r1 = key + 1 < nkeys ? local[key + 1] + bprefix[(key + 1) / kScanBlock] : bprefix[(nkeys - 1) / kScanBlock + 1];
-  const int h = (int)(key % Hh);
-  const long long b = key / Hh / S;
-  const T* gb = gout + ((size_t)b * Q * Hh + h) * kD + sub * V;
-  const size_t qstride = (size_t)Hh * kD;
-  float acc[V];
-#pragma unroll
-  for (int c = 0; c < V; ++c) acc[c] = 0.f;
-  int r = r0;
-  for (; r + 4 <= r1; r += 4) {            // 4 records' gathers in flight
-    int2 e[4];
-    float g[4][V];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) e[u] = rec[r + u];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) Vec16<T>::load(gb + (size_t)e[u].x * qstride, g[u]);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float w = __int_as_float(e[u].y);
-#pragma unroll
-      for (int c = 0; c < V; ++c) acc[c] = __fmaf_rn(w, g[u][c], acc[c]);
-    }
-  }
-  for (; r < r1; ++r) {
-    const int2 e = rec[r];
-    float g[V];
-    Vec16<T>::load(gb + (size_t)e.x * qstride, g);
-    const float w = __int_as_float(e.y);
-#pragma unroll
-    for (int c = 0; c < V; ++c) acc[c] = __fmaf_rn(w, g[c], acc[c]);
-  }
-  Vec16<T>::store(gvalue + key * kD + sub * V, acc);
-}
-
 // ---------------------------------------------------------------------------------
 // grad_value by destination TILES, without float atomics (default backward).
 //
@@ -975,69 +662,15 @@ __global__ void __launch_bounds__(256) msda_tile_accum_kernel(const float* __res
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// workspace: count [nkeys] | local [nkeys] | bsum [nb] | bprefix [nb + 1] | records
-void sorted_layout(long long nkeys, long long maxrec, size_t* off) {
-  const long long nb = (nkeys + kScanBlock - 1) / kScanBlock;
-  off[0] = 0;
-  off[1] = align256(off[0] + nkeys * 4);
-  off[2] = align256(off[1] + nkeys * 4);
-  off[3] = align256(off[2] + nb * 4);
-  off[4] = align256(off[3] + (nb + 1) * 4);
-  off[5] = align256(off[4] + (size_t)maxrec * 8);
-}
-
 
 // ---------------------------------------------------------------------------------
-// grad_value by QUERY tiles with a per-wave LDS window (Q == S and P == 4; default for
-// the pixel-decoder layers).
-//
-// A one-wave workgroup owns a tile of 16 queries of one (image, head, channel half): a
-// 4 x 4 block of one level when the queries are the value grid (level-major, mode 1),
-// else 16 consecutive queries (mode 0).  Per value level l the wave takes the bounding
-// box of the corners its 64 taps touch, clipped to kWinCells cells, as an f32 window in
-// LDS (cell x 16 channels, rows padded so the two corner rows use disjoint banks), and
-// walks the taps in order with lanes = 4 corner quadrants x 16 channels: every corner
-// is one plain LDS read-modify-write (a single wave: LDS ops retire in order, the four
-// quadrants of a tap are distinct cells, so no atomics and no races).  Then every
-// touched window cell is added to grad_value once (f32 atomics: neighbouring tiles'
-// windows overlap), and corners outside the clipped window are added directly.
-// Smoothly varying encoder offsets put a tile's taps of one level into a few dozen
-// cells, so the global atomics fall several-fold against one per corner per tap
-// (measured: pixel-decoder layer backward 1.74 -> 1.10 ms at C2).
-#ifndef VS_MSDA_WIN_CELLS
-#define VS_MSDA_WIN_CELLS 96
-#endif
-constexpr int kWinCells = VS_MSDA_WIN_CELLS;   // LDS window capacity (cells x 16 ch f32 = 6 KB)
-#ifndef VS_MSDA_TX
-#define VS_MSDA_TX 4
-#endif
-#ifndef VS_MSDA_TY
-#define VS_MSDA_TY 4
-#endif
-constexpr int kTX = VS_MSDA_TX, kTY = VS_MSDA_TY;   // query tile width / height (grid mode)
-constexpr int kTQ = kTX * kTY;                      // queries per tile (a power of two <= 64)
-static_assert((kTQ & (kTQ - 1)) == 0 && kTQ >= 4 && kTQ <= 64, "query tile must hold 4..64 queries, a power of 2");
-constexpr int kWinC = 16;                // channels per workgroup (a head's 32 split over two)
-
+// Query tiles of the grad_value kernel.
 struct QueryTiles {
-  int mode;                              // 1: 4x4 grid tiles per level, 0: runs of 16
+  int mode;                              // 1: grid tiles per level, 0: runs of consecutive queries
   int prefix[kMaxLevels + 1];            // grid mode: tile-index prefix per query level
   int ntx[kMaxLevels];
   int per_image;                         // tiles per image
 };
-
-__device__ __forceinline__ int tile_query(const QueryTiles& qt, const Levels& lv, int L, int tile, int idx, int Q) {
-  if (idx >= kTQ) return -1;
-  if (qt.mode == 0) {
-    const int q = tile * kTQ + idx;
-    return q < Q ? q : -1;
-  }
-  int lq = 0;
-  while (lq + 1 < L && tile >= qt.prefix[lq + 1]) ++lq;
-  const int t = tile - qt.prefix[lq];
-  const int y = (t / qt.ntx[lq]) * kTY + idx / kTX, x = (t % qt.ntx[lq]) * kTX + idx % kTX;
-  return (y < lv.h[lq] && x < lv.w[lq]) ? lv.start[lq] + y * lv.w[lq] + x : -1;
-}
 
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
@@ -1051,148 +684,240 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
-template <typename T>
-__global__ void __launch_bounds__(64)
-#ifdef VS_MSDA_WIN_WPE
-__attribute__((amdgpu_waves_per_eu(VS_MSDA_WIN_WPE)))
-#endif
-msda_bwd_window_kernel(const float* __restrict__ loc,
+// ---------------------------------------------------------------------------------
+// grad_value by QUERY tiles, binned per tile (default): one wave per (tile of 16
+// queries, image, head), all 32 channels, lane = (query, point) = one tap.
+//
+// Per value level l the tile's taps cover a small box of cells (smooth encoder
+// offsets: a few dozen cells).  Instead of adding every corner into an LDS window with
+// a chain of dependent read-modify-writes, the wave BINS the tile's 256 corner
+// contributions by cell: a counting sort inside the wave -- ranks from LDS INTEGER
+// atomics (ds_add_rtn_u32, ~12 lane-ops/clk/CU on gfx950, 35x the rate of ds_add_f32:
+// tools/micro/lds_atomic_bench.hip), one wave-wide scan, a scatter of {query, weight}
+// records -- and then sums each non-empty cell's records in REGISTERS (lane = cell
+// parity x 32 channels: independent LDS reads and FMAs, no dependent chain) and adds the
+// cell to grad_value with ONE f32 atomic per channel: two 128-B rows per atomic
+// wave-instruction (the full-rate shape, MI355X_MICROARCH §Global float atomics).
+// Boxes wider than kCellCap cells are clipped; the corners outside go straight to
+// grad_value (one 128-B atomic row each).
+constexpr int kCellCap = 512;
+
+template <int TX, int TY>
+__device__ __forceinline__ int btile_query(const QueryTiles& qt, const Levels& lv, int L, int tile, int idx, int Q) {
+  if (qt.mode == 0) {
+    const int q = tile * TX * TY + idx;
+    return q < Q ? q : -1;
+  }
+  int lq = 0;
+  while (lq + 1 < L && tile >= qt.prefix[lq + 1]) ++lq;
+  const int t = tile - qt.prefix[lq];
+  const int y = (t / qt.ntx[lq]) * TY + idx / TX, x = (t % qt.ntx[lq]) * TX + idx % TX;
+  return (y < lv.h[lq] && x < lv.w[lq]) ? lv.start[lq] + y * lv.w[lq] + x : -1;
+}
+
+// TX x TY queries per tile (<= 64: one query per lane); NT = taps per lane
+template <typename T, int TX, int TY>
+__global__ void __launch_bounds__(64) msda_bwd_binned_kernel(const float* __restrict__ loc,
                                                              const float* __restrict__ attw,
                                                              const T* __restrict__ gout, float* __restrict__ gvalue,
                                                              Levels lv, QueryTiles qt, int S, int Hh, int Q, int L,
                                                              int nblk, int dbg) {
   constexpr int P = 4;
-  constexpr int kWinFloats = kWinCells * kWinC + 32;   // + the row-pitch pad
-  __shared__ float win[kWinFloats + 64];               // + one trash slot per lane
-  __shared__ float sg[kTQ * kWinC];
-  __shared__ float rec[kTQ * 4 * 8];                     // [query][point][quadrant] {weight, target}
+  constexpr int NQ = TX * TY;                 // queries per tile
+  static_assert(NQ * P % 64 == 0 && NQ <= 64, "whole taps per lane");
+  constexpr int NT = NQ * P / 64;             // taps per lane
+  constexpr int NR = NQ * P * 4;              // corner records per level
+  __shared__ float sg[NQ * kD];
+  __shared__ int cnt[kCellCap];
+  __shared__ int offs[kCellCap];
+  __shared__ int cells[kCellCap];
+  __shared__ int2 srt[NR];
   const int blk = xcd_swizzle(blockIdx.x, nblk);
-  const int chalf = blk & 1;
-  const int h = (blk >> 1) % Hh;
-  const int tile = ((blk >> 1) / Hh) % qt.per_image;
-  const int b = (blk >> 1) / Hh / qt.per_image;
+  const int h = blk % Hh;
+  const int tile = (blk / Hh) % qt.per_image;
+  const int b = blk / Hh / qt.per_image;
   const int lane = threadIdx.x;
   const int LP = L * P;
-  const int myq = tile_query(qt, lv, L, tile, lane, Q);
-  const long long mygrp = ((long long)b * Q + (myq < 0 ? 0 : myq)) * Hh + h;
+  // tap i of the lane: (query (lane + 64 i) % NQ, point (lane + 64 i) / NQ)
+  int tq[NT], tpt[NT], qid[NT];
+  long long grp[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const int t = lane + 64 * i;
+    tq[i] = t % NQ;
+    tpt[i] = t / NQ;
+    qid[i] = btile_query<TX, TY>(qt, lv, L, tile, tq[i], Q);
+    grp[i] = ((long long)b * Q + (qid[i] < 0 ? 0 : qid[i])) * Hh + h;
+  }
+  // every tap of the lane on every level, loaded up front (one global round trip)
+  float2 pxy[kMaxLevels][NT];
+  float paw[kMaxLevels][NT];
+#pragma unroll
+  for (int l = 0; l < kMaxLevels; ++l)
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      pxy[l][i] = make_float2(0.f, 0.f);
+      paw[l][i] = 0.f;
+      if (l < L && qid[i] >= 0) {
+        pxy[l][i] = *reinterpret_cast<const float2*>(loc + (grp[i] * LP + l * P + tpt[i]) * 2);
+        paw[l][i] = attw[grp[i] * LP + l * P + tpt[i]];
+      }
+    }
   {
-    const int c = lane & 15, sub = lane >> 4;       // grad_out: 16 channels of 4 queries per pass
-    for (int r = 0; r < kTQ / 4; ++r) {
-      const int idx = 4 * r + sub;
-      const int q = __shfl(myq, idx, 64);
-      sg[idx * kWinC + c] = q >= 0 ? to_f32(gout[(((long long)b * Q + q) * Hh + h) * kD + chalf * kWinC + c]) : 0.f;
+    // grad_out rows of the tile's queries: lane = (query, 8-channel part)
+    constexpr int V = Vec16<T>::N;
+    constexpr int parts = kD / V;
+    for (int r = lane / parts; r < NQ; r += 64 / parts) {
+      const int q = btile_query<TX, TY>(qt, lv, L, tile, r, Q);
+      float v[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[j] = 0.f;
+      if (q >= 0) Vec16<T>::load(gout + (((long long)b * Q + q) * Hh + h) * kD + (lane % parts) * V, v);
+#pragma unroll
+      for (int j = 0; j < V; ++j) sg[r * kD + (lane % parts) * V + j] = v[j];
     }
   }
-  for (int i = lane; i < kWinFloats + 64; i += 64) win[i] = 0.f;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  // walk layout: lane = corner quadrant (qy, qx) x 16 channels
-  const int quad = lane >> 4, ch = lane & 15;
+  for (int i = lane; i < kCellCap; i += 64) cnt[i] = 0;
+  const int hp = lane >> 5, ch = lane & 31;
   const size_t rowstride = (size_t)Hh * kD;
-  const size_t vbase = ((size_t)b * S * Hh + h) * kD + chalf * kWinC + ch;
+  const size_t vbase = ((size_t)b * S * Hh + h) * kD;
   for (int l = 0; l < L; ++l) {
     const int Hl = lv.h[l], Wl = lv.w[l];
     const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
-    // lane = query: its 4 taps on level l, and the bounding box of their valid corners
-    int th[P], tw[P];
-    float tlh[P], tlw[P], ta[P];
-    bool tv[P];
+    int cy[NT][4], cx[NT][4];
+    float cw[NT][4];
+    bool ok[NT][4];
     int ylo = 1 << 30, xlo = 1 << 30, yhi = -1, xhi = -1;
-    {
-      float4 xy0 = make_float4(0.f, 0.f, 0.f, 0.f), xy1 = xy0, aw = xy0;
-      if (myq >= 0) {
-        const float4* lp = reinterpret_cast<const float4*>(loc + (mygrp * LP + l * P) * 2);
-        xy0 = lp[0];
-        xy1 = lp[1];
-        aw = *reinterpret_cast<const float4*>(attw + mygrp * LP + l * P);
-      }
-      const float xs[P] = {xy0.x, xy0.z, xy1.x, xy1.z}, ys[P] = {xy0.y, xy0.w, xy1.y, xy1.w};
-      const float as[P] = {aw.x, aw.y, aw.z, aw.w};
+    bool anyok = false;
 #pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const Tap t = tap_geom(xs[p], ys[p], Hl, Wl);
-        tv[p] = myq >= 0 && t.inside;
-        th[p] = t.h0;
-        tw[p] = t.w0;
-        tlh[p] = t.lh;
-        tlw[p] = t.lw;
-        ta[p] = as[p];
-        if (tv[p]) {
-          ylo = min(ylo, max(t.h0, 0));
-          yhi = max(yhi, min(t.h0 + 1, Hl - 1));
-          xlo = min(xlo, max(t.w0, 0));
-          xhi = max(xhi, min(t.w0 + 1, Wl - 1));
+    for (int i = 0; i < NT; ++i) {
+      float2 xy = pxy[0][i];
+      float aw = paw[0][i];
+#pragma unroll
+      for (int k = 1; k < kMaxLevels; ++k)
+        if (l == k) {
+          xy = pxy[k][i];
+          aw = paw[k][i];
+        }
+      const Tap t = tap_geom(xy.x, xy.y, Hl, Wl);
+      const bool tv = qid[i] >= 0 && t.inside;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        cy[i][k] = t.h0 + (k >> 1);
+        cx[i][k] = t.w0 + (k & 1);
+        ok[i][k] = tv && cy[i][k] >= 0 && cy[i][k] < Hl && cx[i][k] >= 0 && cx[i][k] < Wl;
+        cw[i][k] = ((k >> 1) ? t.lh : t.hh) * ((k & 1) ? t.lw : t.hw) * aw;
+        if (ok[i][k]) {
+          anyok = true;
+          ylo = min(ylo, cy[i][k]);
+          yhi = max(yhi, cy[i][k]);
+          xlo = min(xlo, cx[i][k]);
+          xhi = max(xhi, cx[i][k]);
         }
       }
     }
-    unsigned long long vm[P];
-#pragma unroll
-    for (int p = 0; p < P; ++p) vm[p] = __ballot(tv[p]);
-    if ((vm[0] | vm[1] | vm[2] | vm[3]) == 0ull) continue;
+    if (__ballot(anyok) == 0ull) continue;
     const int oy = wave_min(ylo), ox = wave_min(xlo);
-    int WX = min(wave_max(xhi) - ox + 1, kWinCells);
-    // row pitch = 32 (mod 64) floats: the two corner rows of a tap use disjoint LDS banks
-    const int RP = WX * kWinC + ((32 - (WX * kWinC) % 64) + 64) % 64;
-    const int WY = min(wave_max(yhi) - oy + 1, kWinFloats / RP);
-    // Tap records: lane = query writes, per tap p and corner quadrant k, {weight, target}
-    // where target >= 0 is the corner's window offset (the trash slot for an invalid
-    // tap or corner outside the level, weight 0) and target < 0 encodes -(level cell + 1)
-    // for a valid corner outside the clipped window (direct atomic).
+    const int BX = min(wave_max(xhi) - ox + 1, kCellCap);
+    const int BY = min(wave_max(yhi) - oy + 1, kCellCap / BX);
+    const int ncell = BX * BY;
+    // ranks within the corner's cell (LDS integer atomics)
+    int cell[NT][4], rk[NT][4];
+    bool out[NT][4];
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
-      float2 r[4];
+    for (int i = 0; i < NT; ++i)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int y = th[p] + (k >> 1), x = tw[p] + (k & 1);
-        const bool ok = tv[p] && y >= 0 && y < Hl && x >= 0 && x < Wl;
-        const bool in = ok && (unsigned)(y - oy) < (unsigned)WY && (unsigned)(x - ox) < (unsigned)WX;
-        const float wy = (k >> 1) ? tlh[p] : 1.f - tlh[p], wx = (k & 1) ? tlw[p] : 1.f - tlw[p];
-        const int tgt = in ? (y - oy) * RP + (x - ox) * kWinC : ok ? -(y * Wl + x + 1) : kWinFloats;
-        r[k] = make_float2(ok ? wy * wx * ta[p] : 0.f, __int_as_float(tgt));
+        const bool in = ok[i][k] && (unsigned)(cy[i][k] - oy) < (unsigned)BY && (unsigned)(cx[i][k] - ox) < (unsigned)BX;
+        out[i][k] = ok[i][k] && !in;
+        cell[i][k] = in ? (cy[i][k] - oy) * BX + (cx[i][k] - ox) : -1;
+        rk[i][k] = in ? atomicAdd(&cnt[cell[i][k]], 1) : 0;
       }
-      float4* dst = reinterpret_cast<float4*>(rec + ((lane & (kTQ - 1)) * P + p) * 8);
-      if (lane < kTQ) dst[0] = make_float4(r[0].x, r[0].y, r[1].x, r[1].y);
-      if (lane < kTQ) dst[1] = make_float4(r[2].x, r[2].y, r[3].x, r[3].y);
-    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    // walk: lane = corner quadrant x 16 channels; each tap is one record read (hoisted,
-    // independent of the window) and one LDS read-modify-write per lane
-    const int trash = kWinFloats + lane;
-    float2 rn[P];
-    float gn = sg[ch];
+    // exclusive scan of the counts + compaction of the non-empty cells: lane owns cells
+    // [CPL lane, CPL lane + CPL); one wave scan of (records << 12 | non-empty cells)
+    constexpr int CPL = kCellCap / 64;
+    int c4[CPL], pk = 0;
 #pragma unroll
-    for (int p = 0; p < P; ++p) rn[p] = *reinterpret_cast<const float2*>(rec + p * 8 + quad * 2);
-    for (int q = 0; q < ((dbg & 1) ? 0 : kTQ); ++q) {
-      float2 r[P];
+    for (int j = 0; j < CPL; ++j) {
+      const int e = CPL * lane + j;
+      c4[j] = e < ncell ? cnt[e] : 0;
+      pk += (c4[j] << 12) + (c4[j] > 0);
+    }
+    int inc = pk;
 #pragma unroll
-      for (int p = 0; p < P; ++p) r[p] = rn[p];
-      const float g = gn;
-      const int qn = (q + 1) & (kTQ - 1);        // prefetch the next query's records
-      gn = sg[qn * kWinC + ch];
+    for (int d = 1; d < 64; d <<= 1) {
+      const int u = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += u;
+    }
+    const int total = __shfl(inc, 63, 64);
+    int ex = inc - pk;
 #pragma unroll
-      for (int p = 0; p < P; ++p) rn[p] = *reinterpret_cast<const float2*>(rec + (qn * P + p) * 8 + quad * 2);
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const int tgt = __float_as_int(r[p].y);
-        const float d = r[p].x * g;
-        const int a = tgt >= 0 ? tgt + ch : trash;
-        win[a] += d;
-        if (tgt < 0 && !(dbg & 8)) atomicAdd(gvalue + lbase + (size_t)(-tgt - 1) * rowstride, d);
+    for (int j = 0; j < CPL; ++j) {
+      const int e = CPL * lane + j;
+      if (e < ncell) {
+        offs[e] = ex >> 12;
+        if (c4[j] > 0) cells[ex & 4095] = e;
+        ex += (c4[j] << 12) + (c4[j] > 0);
       }
     }
-    // add the window to grad_value once per touched cell, and clear it for the next level
-    const int ncell = WY * WX;
-    for (int i = quad; i < ncell; i += 4) {
-      const int cy = i / WX, cx = i - cy * WX;
-      float* pw = win + cy * RP + cx * kWinC + ch;
-      const float v = *pw;
-      *pw = 0.f;
-      if (v != 0.f && !(dbg & 2))
-        atomicAdd(gvalue + lbase + (size_t)((oy + cy) * Wl + ox + cx) * rowstride, v);
+    const int nlist = total & 4095;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (cell[i][k] >= 0) srt[offs[cell[i][k]] + rk[i][k]] = make_int2(tq[i] * kD, __float_as_int(cw[i][k]));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // per non-empty cell: sum its records in registers (4 records in flight), one atomic
+    // per channel
+    if (!(dbg & 1)) {
+      for (int i = hp; i < nlist; i += 2) {
+        const int e = cells[i];
+        const int o = offs[e], n = cnt[e];
+        float v0 = 0.f, v1 = 0.f;
+        int j = o;
+        for (; j + 4 <= o + n; j += 4) {
+          const int2 r0 = srt[j], r1 = srt[j + 1], r2 = srt[j + 2], r3 = srt[j + 3];
+          const float g0 = sg[r0.x + ch], g1 = sg[r1.x + ch], g2 = sg[r2.x + ch], g3 = sg[r3.x + ch];
+          v0 = __fmaf_rn(__int_as_float(r0.y), g0, v0);
+          v1 = __fmaf_rn(__int_as_float(r1.y), g1, v1);
+          v0 = __fmaf_rn(__int_as_float(r2.y), g2, v0);
+          v1 = __fmaf_rn(__int_as_float(r3.y), g3, v1);
+        }
+        for (; j < o + n; ++j) {
+          const int2 r = srt[j];
+          v0 = __fmaf_rn(__int_as_float(r.y), sg[r.x + ch], v0);
+        }
+        const int y = oy + e / BX, x = ox + e % BX;
+        if (!(dbg & 2)) atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + ch, v0 + v1);
+      }
     }
+    // clipped corners: one 128-B atomic row each
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        unsigned long long m = __ballot(out[i][k]);
+        while (m) {
+          const int src = __ffsll((long long)m) - 1;
+          m &= m - 1;
+          const int y = __shfl(cy[i][k], src, 64), x = __shfl(cx[i][k], src, 64), qq = __shfl(tq[i], src, 64);
+          const float w = __shfl(cw[i][k], src, 64);
+          if (lane < kD && !(dbg & 8))
+            atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + lane, w * sg[qq * kD + lane]);
+        }
+      }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int i = lane; i < ncell; i += 64) cnt[i] = 0;
   }
 }
 
@@ -1256,15 +981,14 @@ static void launch_geom(int dtype, const void* value, const float* loc, const fl
                        (const float*)gout, gloc, gattw, lv, S, Hh, Q, L, P, groups);
 }
 
-template <bool ENC>
 static void launch_scatter(int dtype, const float* loc, const float* attw, const void* gout, float* gvalue,
-                           const Levels& lv, int B, int S, int Hh, int Q, int L, int run, int R0, hipStream_t st) {
+                           const Levels& lv, int B, int S, int Hh, int Q, int L, int run, hipStream_t st) {
   const int nrun = (Q + run - 1) / run;
   const long long hws = (long long)B * nrun * Hh;
   const int sgrid = (int)((hws + 7) / 8);
 #define VS_SCATTER(TT, LL)                                                                                   \
-  hipLaunchKernelGGL((msda_bwd_scatter_kernel<TT, LL, 4, ENC>), dim3(sgrid), dim3(256), 0, st, loc, attw,     \
-                     (const TT*)gout, gvalue, lv, S, Hh, Q, run, nrun, hws, R0)
+  hipLaunchKernelGGL((msda_bwd_scatter_kernel<TT, LL, 4>), dim3(sgrid), dim3(256), 0, st, loc, attw,          \
+                     (const TT*)gout, gvalue, lv, S, Hh, Q, run, nrun, hws)
 #define VS_SCATTER_L(TT)                \
   switch (L) {                          \
     case 1: VS_SCATTER(TT, 1); break;   \
@@ -1283,8 +1007,7 @@ static void launch_scatter(int dtype, const float* loc, const float* attw, const
 
 static int msda_backward_impl(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
                               const float* loc, const float* attw, const void* gout, float* gvalue, float* gloc,
-                              float* gattw, int B, int S, int Hh, int D, int L, int Q, int P, void* stream,
-                              bool encoder) {
+                              float* gattw, int B, int S, int Hh, int D, int L, int Q, int P, void* stream) {
   VS_CHECK(D == kD, "channels per head must be 32");
   VS_CHECK(L >= 1 && L <= kMaxLevels, "1..4 levels supported");
   VS_CHECK(B > 0 && S > 0 && Hh > 0 && Q >= 0 && P > 0, "bad sizes");
@@ -1292,54 +1015,8 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   Levels lv;
   VS_CHECK(fill_levels(&lv, shapes, starts, L, S), "spatial shapes / level starts inconsistent with S");
-  VS_CHECK(!encoder || Q == S, "encoder mode needs the queries to be the value grid (Q == S)");
-  VS_CHECK(!encoder || P == 4, "encoder-mode backward is specialised for 4 sampling points");
   hipStream_t st = (hipStream_t)stream;
   const long long groups = (long long)B * Q * Hh;
-  if (encoder) {
-    // tile kernel (plain stores of every grad_value element: all near taps, LDS
-    // accumulation), then the carry scatter adds the far taps, and the geom kernel
-    // computes grad_loc / grad_attn
-    int R0 = kNearR;
-    if (const char* e = getenv("VS_MSDA_NEAR_R")) R0 = atoi(e);
-    VS_CHECK(R0 >= 0 && R0 <= 64, "VS_MSDA_NEAR_R out of range");
-    TileOrder to;
-    int ord[kMaxLevels];
-    for (int l = 0; l < L; ++l) ord[l] = l;
-    for (int a = 0; a < L; ++a)                 // ascending cell count (stable)
-      for (int c2 = a + 1; c2 < L; ++c2)
-        if ((long long)lv.h[ord[c2]] * lv.w[ord[c2]] < (long long)lv.h[ord[a]] * lv.w[ord[a]]) {
-          const int tmp = ord[a];
-          ord[a] = ord[c2];
-          ord[c2] = tmp;
-        }
-    to.prefix[0] = 0;
-    for (int k = 0; k < kMaxLevels; ++k) to.level[k] = k < L ? ord[k] : 0;
-    for (int k = 0; k < L; ++k) {
-      const int l = ord[k];
-      const int tiles = ((lv.h[l] + kTile - 1) / kTile) * ((lv.w[l] + kTile - 1) / kTile);
-      to.prefix[k + 1] = to.prefix[k] + tiles * B;
-    }
-    for (int k = L; k < kMaxLevels; ++k) to.prefix[k + 1] = to.prefix[L];
-    to.slots = to.prefix[L];
-    const long long nblk = (long long)((to.slots + 7) / 8) * 8 * Hh;
-    VS_CHECK(nblk < (1LL << 31), "too many tiles");
-    // VS_MSDA_SKIP (profiling only): bit 0 skips the tile kernel, bit 1 the scatter, bit 2 geom
-    int skip = 0;
-    if (const char* e = getenv("VS_MSDA_SKIP")) skip = atoi(e);
-    if (!(skip & 1)) {
-      if (dtype == VS_BF16)
-        hipLaunchKernelGGL(msda_bwd_tile_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0, st, loc, attw,
-                           (const bf16*)gout, gvalue, lv, S, Hh, B, L, R0, to);
-      else
-        hipLaunchKernelGGL(msda_bwd_tile_kernel<float>, dim3((unsigned)nblk), dim3(256), 0, st, loc, attw,
-                           (const float*)gout, gvalue, lv, S, Hh, B, L, R0, to);
-    }
-    if (!(skip & 2)) launch_scatter<true>(dtype, loc, attw, gout, gvalue, lv, B, S, Hh, Q, L, kScatterRun, R0, st);
-    if (!(skip & 4)) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
-    VS_LAUNCH_CHECK();
-    return VS_OK;
-  }
   VS_HIP(hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * Hh * kD, st));
   if (Q == 0) return VS_OK;
   // geom + register-carry scatter when there are enough queries for runs to fill the chip
@@ -1350,37 +1027,43 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     run = atoi(e);
     split = run >= 1;
   }
-  // query-tile LDS-window scatter (VS_MSDA_WIN=0 selects the register-carry scatter)
+  // binned query-tile kernel (VS_MSDA_WIN=0 selects the register-carry scatter)
   bool win = split && P == 4;
   if (const char* e = getenv("VS_MSDA_WIN")) win = win && atoi(e) != 0;
   if (win) {
-    QueryTiles qt;
-    qt.mode = Q == S ? 1 : 0;
-    qt.prefix[0] = 0;
-    for (int l = 0; l < kMaxLevels; ++l) {
-      const bool on = qt.mode == 1 && l < L;
-      qt.ntx[l] = on ? (lv.w[l] + kTX - 1) / kTX : 1;
-      qt.prefix[l + 1] = qt.prefix[l] + (on ? ((lv.h[l] + kTY - 1) / kTY) * qt.ntx[l] : 0);
-    }
-    qt.per_image = qt.mode == 1 ? qt.prefix[L] : (Q + kTQ - 1) / kTQ;
-    const long long nblk = 2LL * B * qt.per_image * Hh;
-    VS_CHECK(nblk < (1LL << 31), "too many query tiles");
-    int dbg = 0;                           // VS_MSDA_WIN_DBG (profiling only): 1 skips the walk, 2 the flush atomics
+    int dbg = 0;                           // VS_MSDA_WIN_DBG (profiling only; tools/msda_dbg.sh)
     if (const char* e = getenv("VS_MSDA_WIN_DBG")) dbg = atoi(e);
-    launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
-    if (dtype == VS_BF16)
-      hipLaunchKernelGGL(msda_bwd_window_kernel<bf16>, dim3((unsigned)nblk), dim3(64), 0, st, loc, attw,
-                         (const bf16*)gout, gvalue, lv, qt, S, Hh, Q, L, (int)nblk, dbg);
-    else
-      hipLaunchKernelGGL(msda_bwd_window_kernel<float>, dim3((unsigned)nblk), dim3(64), 0, st, loc, attw,
-                         (const float*)gout, gvalue, lv, qt, S, Hh, Q, L, (int)nblk, dbg);
+    if (!(dbg & 16)) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
+    if (dbg & 32) return VS_OK;
+    int te = 4;                            // VS_MSDA_TILE: query tile edge, 4 (default) or 8
+    if (const char* e = getenv("VS_MSDA_TILE")) te = atoi(e) == 8 ? 8 : 4;
+    QueryTiles bt;
+    bt.mode = Q == S ? 1 : 0;              // grid tiles when the queries are the value grid
+    bt.prefix[0] = 0;
+    for (int l = 0; l < kMaxLevels; ++l) {
+      const bool on = bt.mode == 1 && l < L;
+      bt.ntx[l] = on ? (lv.w[l] + te - 1) / te : 1;
+      bt.prefix[l + 1] = bt.prefix[l] + (on ? ((lv.h[l] + te - 1) / te) * bt.ntx[l] : 0);
+    }
+    bt.per_image = bt.mode == 1 ? bt.prefix[L] : (Q + te * te - 1) / (te * te);
+    const long long nb2 = (long long)B * bt.per_image * Hh;
+    VS_CHECK(nb2 < (1LL << 31), "too many query tiles");
+#define VS_BINNED(TT, E)                                                                                     \
+  hipLaunchKernelGGL((msda_bwd_binned_kernel<TT, E, E>), dim3((unsigned)nb2), dim3(64), 0, st, loc, attw,     \
+                     (const TT*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, dbg)
+    if (dtype == VS_BF16) {
+      if (te == 4) VS_BINNED(bf16, 4); else VS_BINNED(bf16, 8);
+    } else {
+      if (te == 4) VS_BINNED(float, 4); else VS_BINNED(float, 8);
+    }
+#undef VS_BINNED
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
   if (split && P == 4) {
     VS_CHECK(run <= kScatterRun, "VS_MSDA_RUN must not exceed the LDS-staged run (16)");
     launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
-    launch_scatter<false>(dtype, loc, attw, gout, gvalue, lv, B, S, Hh, Q, L, run, 0, st);
+    launch_scatter(dtype, loc, attw, gout, gvalue, lv, B, S, Hh, Q, L, run, st);
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
@@ -1399,74 +1082,8 @@ extern "C" int vs_msda_backward(int dtype, const void* value, const int64_t* sha
                                 const float* loc, const float* attw, const void* gout, float* gvalue, float* gloc,
                                 float* gattw, int B, int S, int Hh, int D, int L, int Q, int P, void* stream) {
   return msda_backward_impl(dtype, value, shapes, starts, loc, attw, gout, gvalue, gloc, gattw, B, S, Hh, D, L, Q,
-                            P, stream, false);
+                            P, stream);
 }
-
-extern "C" int vs_msda_backward_encoder(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
-                                        const float* loc, const float* attw, const void* gout, float* gvalue,
-                                        float* gloc, float* gattw, int B, int S, int Hh, int D, int L, int P,
-                                        void* stream) {
-  return msda_backward_impl(dtype, value, shapes, starts, loc, attw, gout, gvalue, gloc, gattw, B, S, Hh, D, L, S,
-                            P, stream, true);
-}
-
-extern "C" long long vs_msda_backward_sorted_workspace_bytes(int B, int S, int Hh, int Q, int L, int P) {
-  size_t off[6];
-  sorted_layout((long long)B * S * Hh, 4LL * B * Q * Hh * L * P, off);
-  return (long long)off[5];
-}
-
-extern "C" int vs_msda_backward_sorted(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
-                                       const float* loc, const float* attw, const void* gout, void* gvalue,
-                                       float* gloc, float* gattw, void* workspace, int B, int S, int Hh, int D, int L,
-                                       int Q, int P, void* stream) {
-  VS_CHECK(D == kD, "channels per head must be 32");
-  VS_CHECK(L >= 1 && L <= kMaxLevels, "1..4 levels supported");
-  VS_CHECK(B > 0 && S > 0 && Hh > 0 && Q >= 0 && P > 0, "bad sizes");
-  VS_CHECK(value && gvalue && shapes && starts && workspace, "null pointer");
-  VS_CHECK(Q == 0 || (loc && attw && gout && gloc && gattw), "null pointer");
-  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
-  Levels lv;
-  VS_CHECK(fill_levels(&lv, shapes, starts, L, S), "spatial shapes / level starts inconsistent with S");
-  const long long nkeys = (long long)B * S * Hh;
-  const long long taps = (long long)B * Q * Hh * L * P;
-  VS_CHECK(4 * taps < (1LL << 31), "too many corner contributions for 32-bit record offsets");
-  hipStream_t st = (hipStream_t)stream;
-  size_t off[6];
-  sorted_layout(nkeys, 4 * taps, off);
-  char* ws = (char*)workspace;
-  int* count = (int*)(ws + off[0]);
-  int* local = (int*)(ws + off[1]);
-  int* bsum = (int*)(ws + off[2]);
-  int* bprefix = (int*)(ws + off[3]);
-  int2* rec = (int2*)(ws + off[4]);
-  const int nb = (int)((nkeys + kScanBlock - 1) / kScanBlock);
-  VS_HIP(hipMemsetAsync(count, 0, (size_t)nkeys * 4, st));
-  if (Q > 0) {
-    const int tgrid = (int)((taps + 255) / 256);
-    hipLaunchKernelGGL(msda_sort_kernel<false>, dim3(tgrid), dim3(256), 0, st, loc, attw, count, local, bprefix, rec,
-                       lv, S, Hh, Q, L, P, taps);
-  }
-  hipLaunchKernelGGL(sort_scan_local_kernel, dim3(nb), dim3(256), 0, st, count, local, bsum, nkeys);
-  hipLaunchKernelGGL(sort_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, bsum, bprefix, nb);
-  if (Q > 0) {
-    const int tgrid = (int)((taps + 255) / 256);
-    hipLaunchKernelGGL(msda_sort_kernel<true>, dim3(tgrid), dim3(256), 0, st, loc, attw, count, local, bprefix, rec,
-                       lv, S, Hh, Q, L, P, taps);
-  }
-  const int lpg = dtype == VS_BF16 ? 4 : 8;
-  const int pgrid = (int)((nkeys * lpg + 255) / 256);
-  if (dtype == VS_BF16)
-    hipLaunchKernelGGL(msda_pull_sorted_kernel<bf16>, dim3(pgrid), dim3(256), 0, st, local, bprefix, rec,
-                       (const bf16*)gout, (bf16*)gvalue, S, Hh, Q, nkeys);
-  else
-    hipLaunchKernelGGL(msda_pull_sorted_kernel<float>, dim3(pgrid), dim3(256), 0, st, local, bprefix, rec,
-                       (const float*)gout, (float*)gvalue, S, Hh, Q, nkeys);
-  if (Q > 0) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, (long long)B * Q * Hh, st);
-  VS_LAUNCH_CHECK();
-  return VS_OK;
-}
-
 
 // ---- tiled grad_value (default backward; see msda_tile_accum_kernel) ----------------
 static void tile_geo(TileGeo* tg, const int* hs, const int* ws, int L, int Q, int P) {

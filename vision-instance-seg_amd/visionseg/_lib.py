@@ -27,9 +27,6 @@ SIGNATURES = {
     "vs_last_error": [],
     "vs_msda_forward": [_c_int, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_msda_backward": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
-    "vs_msda_backward_encoder": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 6 + [_P],
-    "vs_msda_backward_sorted_workspace_bytes": [_c_int] * 6,
-    "vs_msda_backward_sorted": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_msda_backward_tiled_workspace_bytes": [_c_int] * 5 + [_P],
     "vs_msda_backward_tiled": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_msda_prep_forward": [_c_int, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P, _P,
@@ -84,7 +81,6 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_flat_step_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_nchw_workspace_bytes": ctypes.c_longlong,
-            "vs_msda_backward_sorted_workspace_bytes": ctypes.c_longlong,
             "vs_msda_backward_tiled_workspace_bytes": ctypes.c_longlong}
 
 _lib = None

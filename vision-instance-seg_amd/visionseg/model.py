@@ -253,10 +253,6 @@ class MSDeformAttn(nn.Module):
     def __init__(self, d, heads, levels, points):
         super().__init__()
         self.d, self.heads, self.levels, self.points = d, heads, levels, points
-        # True: encoder-mode backward (destination pull + carry scatter, csrc/msda.hip);
-        # opt-in (VS_MSDA_ENCODER=1): faster on uncorrelated offsets, slower than the
-        # general register-carry path on the smooth offsets of the C2 bench
-        self.encoder_backward = os.environ.get("VS_MSDA_ENCODER", "0") == "1"
         self.sampling_offsets = TokenLinear(d, heads * levels * points * 2)
         self.attention_weights = TokenLinear(d, heads * levels * points)
         self.value_proj = TokenLinear(d, d)
@@ -278,7 +274,7 @@ class MSDeformAttn(nn.Module):
             aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
             aw = F.softmax(aw.float(), -1).view(B, S, self.heads, self.levels, self.points)
             loc = ref[:, :, None, :, None, :] + off.float() / norm           # HF:m2f:994-1002
-        out = ops.ms_deform_attn(value, shapes, loc, aw, encoder=self.encoder_backward)
+        out = ops.ms_deform_attn(value, shapes, loc, aw)
         return self.output_proj(out)
 
 

@@ -44,15 +44,13 @@ def _level_arrays(shapes):
     return sh, starts, s
 
 
-# MSDA backward variant (A/B switch, VS_MSDA_BWD): "carry" (default; register-carry scatter
-# with f32 global atomics, then a cast), "tiled" (grad_value by destination tiles with plain
-# LDS read-modify-write, no float atomics, written once in the value dtype), "sorted"
-# (per-cell counting sort).  Both destination variants pay for building the inverse index
-# with integer atomics (~30 G/s on gfx950): at 4x1024^2 (tools/kbench.py --only msda,
-# smooth offsets) carry 2.1 ms, tiled 4.4 ms (count 1.1 + fill 1.6 + accumulate 1.7),
-# sorted 3.1 ms.
+# MSDA backward variant (A/B switch, VS_MSDA_BWD): "carry" (default; f32 atomic scatter:
+# the binned query-tile kernel, or the register-carry kernel with VS_MSDA_WIN=0, then
+# a cast) or "tiled" (deterministic: grad_value by destination tiles with plain LDS
+# read-modify-write, no float atomics, written once in the value dtype; pays for its
+# inverse index with integer atomics, ~30 G/s on gfx950: at 4x1024^2, tools/kbench.py
+# --only msda, smooth offsets, 4.4 ms against the binned kernel's 0.96 ms).
 _MSDA_BWD = os.environ.get("VS_MSDA_BWD", "carry")
-_MSDA_SORTED = os.environ.get("VS_MSDA_SORTED", "0") == "1" or _MSDA_BWD == "sorted"
 
 
 class MSDeformAttnFunction(torch.autograd.Function):
@@ -61,7 +59,7 @@ class MSDeformAttnFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, value, spatial_shapes, level_start_index, sampling_locations, attention_weights,
-                im2col_step=64, encoder=False):
+                im2col_step=64):
         shapes = _shapes_list(spatial_shapes)
         L.require_hip(value, sampling_locations, attention_weights)
         value = value.contiguous()
@@ -78,7 +76,6 @@ class MSDeformAttnFunction(torch.autograd.Function):
             L.check(L.lib().vs_msda_forward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
                                             L.ptr(out), B, S, H, D, Lv, Q, P, L.stream(value)), "msda_forward")
         ctx.shapes = shapes
-        ctx.encoder = bool(encoder) and Q == S and P == 4
         ctx.save_for_backward(value, loc, aw)
         return out
 
@@ -91,7 +88,7 @@ class MSDeformAttnFunction(torch.autograd.Function):
         gl = torch.empty_like(loc)
         ga = torch.empty_like(aw)
         sh, st, _ = _level_arrays(ctx.shapes)
-        if _MSDA_BWD == "tiled" and not _MSDA_SORTED and not ctx.encoder:
+        if _MSDA_BWD == "tiled":
             # grad_value by destination tiles (csrc/msda.hip msda_tile_*): atomic-free,
             # written once in value's dtype
             gv = torch.empty_like(value)
@@ -105,40 +102,20 @@ class MSDeformAttnFunction(torch.autograd.Function):
                                                        L.ptr(aw), L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga),
                                                        L.ptr(ws), B, S, H, D, Lv, Q, P, L.stream(value)),
                         "msda_backward_tiled")
-            return gv, None, None, gl, ga, None, None
-        if _MSDA_SORTED:
-            # grad_value by destination after a counting sort (csrc/msda.hip): no float
-            # atomics, written once in value's dtype
-            gv = torch.empty_like(value)
-            ws = torch.empty(int(L.lib().vs_msda_backward_sorted_workspace_bytes(B, S, H, Q, Lv, P)),
-                             device=value.device, dtype=torch.uint8)
-            nb = (2 * value.numel() + g.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 8
-            with timed("msda_bwd", value, bytes_=nb, flops=2.0 * aw.numel() * 10 * D):
-                L.check(L.lib().vs_msda_backward_sorted(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc),
-                                                        L.ptr(aw), L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga),
-                                                        L.ptr(ws), B, S, H, D, Lv, Q, P, L.stream(value)),
-                        "msda_backward_sorted")
-            return gv, None, None, gl, ga, None, None
+            return gv, None, None, gl, ga, None
         gv = torch.empty(B, S, H, D, device=value.device, dtype=torch.float32)
         nb = (value.numel() + g.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 8 + gv.numel() * 4
         with timed("msda_bwd", value, bytes_=nb, flops=2.0 * aw.numel() * 10 * D):
-            if ctx.encoder:
-                L.check(L.lib().vs_msda_backward_encoder(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc),
-                                                         L.ptr(aw), L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga), B, S,
-                                                         H, D, Lv, P, L.stream(value)), "msda_backward_encoder")
-            else:
-                L.check(L.lib().vs_msda_backward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
-                                                 L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga), B, S, H, D, Lv, Q, P,
-                                                 L.stream(value)), "msda_backward")
-        return gv.to(value.dtype), None, None, gl, ga, None, None
+            L.check(L.lib().vs_msda_backward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
+                                             L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga), B, S, H, D, Lv, Q, P,
+                                             L.stream(value)), "msda_backward")
+        return gv.to(value.dtype), None, None, gl, ga, None
 
 
-def ms_deform_attn(value, spatial_shapes, sampling_locations, attention_weights, encoder: bool = False):
-    """Functional form with the oracle's argument order (HF:m2f:798).  `encoder=True`
-    declares that the queries are the value grid itself (pixel-decoder self-attention,
-    Q == S): the backward then builds grad_value by destination band, without atomics."""
+def ms_deform_attn(value, spatial_shapes, sampling_locations, attention_weights):
+    """Functional form with the oracle's argument order (HF:m2f:798)."""
     shapes = _shapes_list(spatial_shapes)
-    return MSDeformAttnFunction.apply(value, shapes, None, sampling_locations, attention_weights, 64, encoder)
+    return MSDeformAttnFunction.apply(value, shapes, None, sampling_locations, attention_weights, 64)
 
 
 class MSDAPrepFunction(torch.autograd.Function):
