@@ -173,14 +173,17 @@ def _cpu_model_name():
 
 def cpu_baseline(model_name, size, iters, queries):
     """the oracle CPU restatement (fp32) on this host's cores, median of
-    `iters` after one warm-up, images/s, for (a) C1 = 2x512^2 forward+loss and (b) one
+    `iters`, images/s, for (a) C1 = 2x512^2 forward+loss (after one warm-up) and (b) one
     `size`^2 image forward+loss+backward (the like-for-like training sample; its rate is
-    `value`).  Threads = the CPUs this process may run on (its affinity set: the box's CPU
-    share), reported with os.cpu_count() and the CPU model."""
+    `value`), about 30-40 s of CPU work in all.  Threads = the CPUs this process may run on
+    (the box's CPU share), reported with os.cpu_count() and the CPU model."""
     from oracle.ref_model import RefConfig, RefMask2Former, RefCriterion
     from visionseg.model import M2FConfig
     from visionseg.data import synthetic_batch
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    # the CPUs this process may use: the box's CPU share (OMP_NUM_THREADS, set there)
+    # when given, else the affinity set (os.cpu_count() reports the whole machine)
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = min(aff, int(os.environ.get("OMP_NUM_THREADS", aff)))
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     cfg = RefConfig.from_dict(M2FConfig.preset(model_name, num_queries=queries).to_dict())
@@ -188,11 +191,13 @@ def cpu_baseline(model_name, size, iters, queries):
     m = RefMask2Former(cfg)
     crit = RefCriterion(cfg)
 
-    def run(batch, sz, backward):
+    def run(batch, sz, backward, warm):
         imgs, ml, cl = synthetic_batch(batch, sz, seed=42)
         ml = [x.float() for x in ml]
         ts = []
-        for i in range(iters + 1):
+        for i in range(iters + warm):
+            print(f"cpu baseline: {batch}x{sz}^2 {'fwd+loss+bwd' if backward else 'fwd+loss'} iter {i + 1}/"
+                  f"{iters + warm}", file=sys.stderr, flush=True)
             t0 = time.perf_counter()
             if backward:
                 masks, classes = m(imgs)
@@ -203,18 +208,18 @@ def cpu_baseline(model_name, size, iters, queries):
                 with torch.no_grad():
                     masks, classes = m(imgs)
                     crit(masks, classes, ml, cl)
-            if i > 0:
+            if i >= warm:
                 ts.append(time.perf_counter() - t0)
         ts.sort()
         med = ts[len(ts) // 2]
         return batch / med, med
 
-    c1, c1_t = run(2, 512, False)
-    v, t = run(1, size, True)
+    c1, c1_t = run(2, 512, False, 1)
+    v, t = run(1, size, True, 0)            # warmed up by the C1 runs (same model)
     torch.set_num_threads(prev)
     return dict(value=round(v, 4), unit="images/s", cores=threads, kind="port",
                 sample=f"1x3x{size}^2 {model_name} Mask2Former fp32 forward+loss+backward (oracle CPU restatement), "
-                       f"median of {iters} iters after 1 warm-up, {t:.2f} s/iter",
+                       f"median of {iters} iters (after the C1 runs on the same model), {t:.2f} s/iter",
                 c1_forward_loss=dict(value=round(c1, 4), unit="images/s",
                                      sample=f"C1: 2x3x512^2 forward+loss, median of {iters} after 1 warm-up, "
                                             f"{c1_t:.2f} s/iter"),
@@ -358,6 +363,7 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(a.model, a.size, a.cpu_iters, a.queries)
         if world == 1 and not a.no_parity:
+            print("parity check vs the oracle ...", file=sys.stderr, flush=True)
             parity = parity_check(a.model, a.size, a.queries, dev)
         fl = TRAIN_FLOPS_PER_IMAGE.get((a.model, a.size))
         step_roof = None

@@ -18,7 +18,7 @@ from visionseg.criterion import SetCriterion
 from visionseg.train import Trainer, SolverConfig
 from visionseg.data import synthetic_batch
 
-WATCH = ("copy_", "_to_copy", "add.Tensor", "add_.Tensor", "sum", "cat", "clone", "mul.Tensor", "fill_", "zero_",
+WATCH = ("copy_", "_to_copy", "add.Tensor", "add_.Tensor", "sum", "cat", "clone", "mul.Tensor", "fill_", "zero_", "clamp", "gelu", "where",
          "native_group_norm", "grid_sampler_2d", "mm.default", "addmm", "bmm")
 
 

@@ -7,7 +7,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/round
 mkdir -p $O
-timeout -k 10 300 python3 bench.py > $O/bench.log 2>&1 || exit $?
+timeout -k 10 400 python3 bench.py > $O/bench.log 2> $O/bench.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- python3 bench.py --no-cpu-baseline > $O/trace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/eager -o bench -- python3 bench.py --no-cpu-baseline --graphs 0 > $O/eager.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o b -- python3 bench.py --no-cpu-baseline --graphs 0 --steps 3 --warmup 2 > $O/fetch.log 2>&1 || exit $?

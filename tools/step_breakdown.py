@@ -1,6 +1,6 @@
 """Per-step kernel breakdown from a rocprofv3 --kernel-trace CSV of bench.py.
 
-A step is delimited by the fused optimizer launches (multi_tensor_apply_kernel): the
+A step is delimited by the flat optimiser step launches (flat_step_kernel): the
 last complete step is the span after the second-to-last optimizer burst up to the end
 of the last one.  Prints busy time by category and the top kernels of that step.
 Usage: python tools/step_breakdown.py <kernel_trace.csv> [top]
@@ -35,7 +35,7 @@ def main():
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    opt = [i for i, r in enumerate(rows) if "multi_tensor_apply_kernel" in r[2]]
+    opt = [i for i, r in enumerate(rows) if "flat_step_kernel" in r[2]]
     # group optimizer launches into bursts
     # bursts separated by the forward/backward: split at gaps above half the largest gap
     thr = max(b - a for a, b in zip(opt, opt[1:])) // 2

@@ -8,8 +8,8 @@ multiplier), CLIP_GRADIENTS "norm" = clip_grad_norm_(p, 0.01) for every paramete
 
 MI355X layout: every per-parameter tensor of the optimiser lives in ONE flat buffer —
 the model's working weights (bf16, the nn.Parameters become views of it), their
-gradients (autograd accumulates into views of one buffer), the f32 master weights and
-the f32 optimiser state.  The whole optimiser step is then two kernels
+gradients (packed after the backward -- or per bucket, as buckets complete -- with
+multi-tensor copies), the f32 master weights and the f32 optimiser state.  The whole optimiser step is then two kernels
 (csrc/optim.hip: per-chunk sum of squares, then clip + decay + update + bf16 cast) and a
 gradient bucket is a contiguous slice that RCCL reduces in place.
 
@@ -150,18 +150,33 @@ class FlatOptimizer:
             for p, w in zip(self.params, wv):
                 p.data = w                          # the model now reads the flat buffer
         self.grad_views = lay.views(self.grads)
-        self.attach_grads()
-
-    def attach_grads(self):
-        """(Re-)point every parameter's .grad at its view of the flat gradient buffer;
-        autograd then accumulates into it in place."""
-        for p, g in zip(self.params, self.grad_views):
-            if p.grad is None or p.grad.data_ptr() != g.data_ptr():
-                p.grad = g
+        self.reduce_views = lay.views(self.reduced_grads())
 
     def zero_grad(self):
-        self.attach_grads()
-        self.grads.zero_()
+        """Before a backward: no .grad tensors, so autograd hands each parameter its
+        gradient without an accumulate kernel (gather_grads packs them afterwards)."""
+        for p in self.params:
+            p.grad = None
+
+    def gather_grads(self, ids=None):
+        """Pack the parameters' .grad tensors (all, or those listed) into the buffer the
+        update reads -- the f32 all-reduce buffer when there is one (the bf16 -> f32
+        widening happens in this copy) -- with multi-tensor copies; a parameter that got
+        no gradient this step gets zeros."""
+        idx = range(len(self.params)) if ids is None else ids
+        src, dst, missing = [], [], []
+        for i in idx:
+            g = self.params[i].grad
+            if g is None:
+                missing.append(self.reduce_views[i])
+            else:
+                src.append(g)
+                dst.append(self.reduce_views[i])
+        with torch.no_grad():
+            if src:
+                torch._foreach_copy_(dst, src)
+            if missing:
+                torch._foreach_zero_(missing)
 
     def set_lr(self, value: float):
         self.lr.fill_(float(value))
@@ -291,9 +306,8 @@ class GradReducer:
             self.next += 1
 
     def _launch(self, b):
-        lo, hi, _ = self.lay.buckets[b]
-        if self.opt.grads32 is not None:
-            self.opt.grads32[lo:hi].copy_(self.opt.grads[lo:hi])       # widen to f32 (compute stream)
+        lo, hi, ids = self.lay.buckets[b]
+        self.opt.gather_grads(ids)                 # pack (and widen to f32) on the compute stream
         if self.mode == "eager":
             self.works.append(dist.all_reduce(self.buf[lo:hi], group=self.group, async_op=True))
         elif self.mode == "capture":

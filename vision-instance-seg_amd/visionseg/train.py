@@ -161,8 +161,8 @@ class Trainer:
 
     # ----------------------------------------------------------------- step phases
     def forward_backward(self, images, mask_labels, class_labels, reduce_mode: str = "eager"):
-        """Zeroed flat gradients, forward + loss + backward (autograd accumulates into the
-        flat buffer); with several ranks the buckets are reduced as they complete.
+        """Forward + loss + backward, the gradients packed into the flat buffer; with
+        several ranks each bucket is packed and reduced as it completes.
         Returns (loss, loss components)."""
         self.opt.zero_grad()
         if self.reducer is not None:
@@ -171,6 +171,8 @@ class Trainer:
         loss.backward()
         if self.reducer is not None:
             self.reducer.finish_backward()
+        else:
+            self.opt.gather_grads()
         return loss.detach(), parts
 
     def apply_gradients(self):
