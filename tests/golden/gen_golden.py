@@ -267,9 +267,39 @@ def gen_misc(out):
     out.append("misc.npz")
 
 
+def gen_postproc(out):
+    """HF Mask2FormerImageProcessor.post_process_instance_segmentation (HF:m2f-proc:627-746)
+    on synthetic logits: mask logits at 96^2 (HF interpolates them to 384^2 itself), two
+    images, 12 queries, 2 classes + no-object; threshold 0.3, binary maps returned."""
+    from types import SimpleNamespace
+    from transformers import Mask2FormerImageProcessor
+    g = torch.Generator().manual_seed(77)
+    B, Q, K = 2, 12, 2
+    masks = 4.0 * torch.randn(B, Q, 96, 96, generator=g)
+    masks = torch.nn.functional.avg_pool2d(masks, 5, 1, 2) * 3.0            # blobby masks
+    classes = 3.0 * torch.randn(B, Q, K + 1, generator=g)
+    proc = Mask2FormerImageProcessor()
+    outs = proc.post_process_instance_segmentation(
+        SimpleNamespace(class_queries_logits=classes, masks_queries_logits=masks), threshold=0.3,
+        return_binary_maps=True)
+    res = {"masks_queries_logits": masks.numpy(), "class_queries_logits": classes.numpy(), "threshold": 0.3}
+    for i, o in enumerate(outs):
+        segs = o["segments_info"]
+        res[f"scores_{i}"] = np.array([d["score"] for d in segs], dtype=np.float64)
+        res[f"labels_{i}"] = np.array([d["label_id"] for d in segs], dtype=np.int64)
+        maps = o["segmentation"].numpy().astype(bool) if segs else np.zeros((0, 384, 384), bool)
+        res[f"binary_maps_{i}"] = np.packbits(maps, axis=-1)
+    np.savez_compressed(os.path.join(HERE, "postproc.npz"), **res)
+    out.append("postproc.npz")
+
+
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     done = []
-    for fn in (gen_window, gen_swin_attention, gen_msda, gen_mask_head, gen_masked_attn, gen_misc, gen_model):
+    only = sys.argv[1:]
+    for fn in (gen_window, gen_swin_attention, gen_msda, gen_mask_head, gen_masked_attn, gen_misc, gen_model,
+               gen_postproc):
+        if only and fn.__name__ not in only:
+            continue
         fn(done)
         print("wrote", done[-1])

@@ -40,7 +40,7 @@ def _run(trainer, batches, seed0=100):
     return losses
 
 
-def _compare(ta, tb, la, lb):
+def _compare(ta, tb, la, lb, iters=None):
     assert all(torch.isfinite(torch.tensor(la + lb)))
     for a, b in zip(la, lb):
         assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (la, lb)
@@ -50,7 +50,7 @@ def _compare(ta, tb, la, lb):
         worst = max(worst, d / max(1e-3, float(pa.detach().abs().max())))
     assert worst < 5e-2, worst
     # the replays must have moved the weights (the optimiser really ran)
-    assert tb.iter == len(lb)
+    assert tb.iter == (len(lb) if iters is None else iters)
 
 
 def test_graph_step_matches_eager():
@@ -141,3 +141,24 @@ def test_split_graph_step_one_rank():
         assert len(tb._graph_states[next(iter(tb._graph_states))]["graphs"]) == 2
     finally:
         dist.destroy_process_group()
+
+
+def test_load_after_capture_recaptures(tmp_path):
+    """Trainer.load() drops the captured graphs (they hold the previous state's static
+    inputs): a graph trainer resumed from an eager trainer's checkpoint continues exactly
+    like that eager trainer (stale moments / lr after a resume)."""
+    from visionseg.train import Trainer
+    cfg, model, crit, b1, b2 = _setup()
+    ta = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV)
+    tb = Trainer(copy.deepcopy(model), copy.deepcopy(crit), device=DEV, graphs=True, graph_warmup=2)
+    _run(ta, [b1, b1, b1, b2], seed0=10)
+    _run(tb, [b2, b2, b2, b2], seed0=50)                # tb captured on its own history
+    assert len(tb._graph_states) == 1
+    path = str(tmp_path / "ck.pth")
+    ta.save(path)
+    tb.load(path)
+    assert not tb._graph_states and tb.iter == ta.iter
+    la = _run(ta, [b1, b1, b1, b1], seed0=200)
+    lb = _run(tb, [b1, b1, b1, b1], seed0=200)
+    _compare(ta, tb, la, lb, iters=8)
+    assert float(tb.opt.step_count) == float(ta.opt.step_count)

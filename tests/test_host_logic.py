@@ -7,6 +7,7 @@ import os
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from visionseg.data import write_coco_dataset, CocoInstanceDataset, collate_padded, synthetic_batch, normalize
 from visionseg.evaluate import MaskAPEvaluator
@@ -153,3 +154,83 @@ def test_criterion_padding_invariance(monkeypatch, ks):
         for b, k in enumerate(ks):
             q = a[s, b, :k].tolist()
             assert len(set(q)) == k and all(0 <= x < Q for x in q)
+
+
+def test_instance_inference_vs_hf_postprocess(golden):
+    """visionseg.inference.instance_inference vs HF post_process_instance_segmentation
+    (HF:m2f-proc:627-746), fixture tests/golden/postproc.npz (gen_golden.py): HF resizes
+    the logits to 384^2 and keeps the instances scoring >= threshold; the same selection
+    from the product's output gives the same scores, labels and binary masks."""
+    d = golden("postproc.npz")
+    thr = float(d["threshold"])
+    for i in range(d["class_queries_logits"].shape[0]):
+        s, lab, m = instance_inference(torch.from_numpy(d["masks_queries_logits"][i]),
+                                       torch.from_numpy(d["class_queries_logits"][i]), (384, 384))
+        keep = (s >= thr) & m.flatten(1).any(1)
+        got = sorted(zip(np.round(s[keep].numpy().astype(np.float64), 6).tolist(), lab[keep].tolist(),
+                         [np.packbits(x, axis=-1).tobytes() for x in m[keep].numpy()]))
+        exp_maps = d[f"binary_maps_{i}"]
+        exp = sorted(zip(d[f"scores_{i}"].tolist(), d[f"labels_{i}"].tolist(), [x.tobytes() for x in exp_maps]))
+        assert len(got) == len(exp)
+        for (gs, gl, gm), (es, el, em) in zip(got, exp):
+            assert abs(gs - es) <= 2e-6 and gl == el and gm == em
+
+
+def test_predictor_crop_follows_sem_seg_postprocess():
+    """Stride-4 logits -> padded input size -> crop -> original size (upstream
+    sem_seg_postprocess), for sizes that are not multiples of 4."""
+    g = torch.Generator().manual_seed(0)
+    ml = torch.randn(3, 25, 40, generator=g)            # stride 4 of a 100 x 160 padded input
+    cl = torch.randn(3, 2, generator=g)
+    s, lab, m = instance_inference(ml, cl, (77, 130), valid_hw=(97, 158), pad_hw=(100, 160))
+    up = F.interpolate(ml[None], size=(100, 160), mode="bilinear", align_corners=False)[..., :97, :158]
+    exp = F.interpolate(up, size=(77, 130), mode="bilinear", align_corners=False)[0] > 0
+    order = torch.softmax(cl, -1)[:, 0].topk(3, sorted=False)[1]
+    assert torch.equal(m, exp[order])
+
+
+def _rle_encode(mask):
+    """Uncompressed COCO RLE of a bool mask (column-major runs, background first) and
+    its compressed string (pycocotools rleToString semantics), for the decoder test."""
+    flat = mask.T.reshape(-1).astype(np.uint8)
+    counts, cur, n = [], 0, 0
+    for v in flat:
+        if v != cur:
+            counts.append(n)
+            cur, n = v, 0
+        n += 1
+    counts.append(n)
+    s = []
+    for i, x in enumerate(counts):
+        x = x - counts[i - 2] if i > 2 else x
+        more = True
+        while more:
+            c = x & 0x1F
+            x >>= 5
+            more = (x != -1) if (c & 0x10) else (x != 0)
+            if more:
+                c |= 0x20
+            s.append(chr(c + 48))
+    return {"counts": counts, "size": list(mask.shape)}, {"counts": "".join(s), "size": list(mask.shape)}
+
+
+def test_rle_annotations(tmp_path):
+    """CocoInstanceDataset decodes RLE segmentations (uncompressed and compressed COCO
+    strings) as the reference mapper does (train_full.py:116-129)."""
+    from visionseg.data import decode_rle
+    rng = np.random.default_rng(3)
+    m = np.zeros((37, 53), dtype=bool)
+    m[5:20, 8:30] = True
+    m[25:33, 40:50] = rng.random((8, 10)) > 0.3
+    un, comp = _rle_encode(m)
+    assert np.array_equal(decode_rle(un), m) and np.array_equal(decode_rle(comp), m)
+    coco = write_coco_dataset(str(tmp_path), n_images=1, size=64, seed=2)
+    big = np.zeros((64, 64), dtype=bool)
+    big[10:30, 20:50] = True
+    coco["annotations"].append({"id": 999, "image_id": 0, "category_id": 0, "segmentation": _rle_encode(big)[1],
+                                "area": float(big.sum()), "bbox": [20, 10, 30, 20], "iscrowd": 0})
+    with open(os.path.join(str(tmp_path), "annotations.json"), "w") as f:
+        json.dump(coco, f)
+    ds = CocoInstanceDataset(str(tmp_path), train=False, keep_size=True)
+    _, masks, classes = ds[0]
+    assert any(np.array_equal(x.numpy(), big) for x in masks)

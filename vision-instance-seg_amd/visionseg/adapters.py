@@ -84,7 +84,9 @@ def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, ba
                           schedule="cosine" if hp.get("lr_scheduler") == "cosine" else "multistep",
                           warmup_iters=int(hp.get("warmup_epochs", 0)) * iters_per_epoch, max_iter=total,
                           amp=device.type == "cuda")
-    trainer = Trainer(model, SetCriterion(cfg), solver, device=device)
+    # HIP-graph replay of the step for every batch signature seen more than twice (image
+    # size after ResizeShortestEdge + padding, padded target capacity)
+    trainer = Trainer(model, SetCriterion(cfg), solver, device=device, graphs=device.type == "cuda")
     output_dir.mkdir(parents=True, exist_ok=True)
     rng = np.random.default_rng(seed)
     it = 0

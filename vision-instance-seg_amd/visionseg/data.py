@@ -49,6 +49,54 @@ def thunderbolt_polygon(rng: np.random.Generator, H: int, W: int) -> list:
     return pts.reshape(-1).tolist()
 
 
+def _rle_counts_from_string(s: str) -> list:
+    """COCO compressed RLE string -> run lengths (pycocotools rleFrString: 5-bit groups
+    with a continuation bit, sign-extended, each count after the second delta-coded
+    against the count two places back)."""
+    counts, p, m = [], 0, 0
+    while p < len(s):
+        x, k, more = 0, 0, True
+        while more:
+            c = ord(s[p]) - 48
+            x |= (c & 0x1F) << (5 * k)
+            more = bool(c & 0x20)
+            p += 1
+            k += 1
+            if not more and (c & 0x10):
+                x |= -1 << (5 * k)
+        if m > 2:
+            x += counts[m - 2]
+        counts.append(x)
+        m += 1
+    return counts
+
+
+def decode_rle(rle: dict) -> np.ndarray:
+    """COCO RLE segmentation ({"counts": list or compressed string, "size": [h, w]}) ->
+    bool mask [h, w].  Runs alternate background / foreground starting with background,
+    in column-major order."""
+    h, w = (int(v) for v in rle["size"])
+    counts = rle["counts"]
+    if isinstance(counts, (bytes, str)):
+        counts = _rle_counts_from_string(counts.decode() if isinstance(counts, bytes) else counts)
+    flat = np.zeros(h * w, dtype=bool)
+    pos = 0
+    for i, n in enumerate(counts):
+        n = int(n)
+        if i % 2 == 1:
+            flat[pos:pos + n] = True
+        pos += n
+    return flat.reshape(w, h).T
+
+
+def _resize_nearest(m: np.ndarray, H: int, W: int) -> np.ndarray:
+    if m.shape == (H, W):
+        return m
+    ys = np.minimum((np.arange(H) + 0.5) * m.shape[0] / H, m.shape[0] - 1).astype(np.int64)
+    xs = np.minimum((np.arange(W) + 0.5) * m.shape[1] / W, m.shape[1] - 1).astype(np.int64)
+    return m[ys][:, xs]
+
+
 def rasterize(poly_flat: list, H: int, W: int) -> np.ndarray:
     img = Image.new("1", (W, H), 0)
     ImageDraw.Draw(img).polygon([(poly_flat[i], poly_flat[i + 1]) for i in range(0, len(poly_flat), 2)], fill=1)
@@ -146,10 +194,14 @@ class CocoInstanceDataset:
         for a in self.by_img.get(info["id"], []):
             if a.get("iscrowd", 0):
                 continue
-            m = np.zeros((H, W), dtype=bool)
-            for poly in a["segmentation"]:
-                p = np.array(poly, dtype=np.float64).reshape(-1, 2) * [sx, sy]
-                m |= rasterize(p.reshape(-1).tolist(), H, W)
+            segm = a["segmentation"]
+            if isinstance(segm, dict):            # RLE (train_full.py:116-129 decodes both forms)
+                m = _resize_nearest(decode_rle(segm), H, W)
+            else:
+                m = np.zeros((H, W), dtype=bool)
+                for poly in segm:
+                    p = np.array(poly, dtype=np.float64).reshape(-1, 2) * [sx, sy]
+                    m |= rasterize(p.reshape(-1).tolist(), H, W)
             masks.append(m)
             classes.append(self.cat_to_label[a["category_id"]])
         arr = np.asarray(img, dtype=np.uint8).transpose(2, 0, 1)

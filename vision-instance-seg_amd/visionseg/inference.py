@@ -43,9 +43,15 @@ class DetResult:
 
 
 @torch.no_grad()
-def instance_inference(mask_logits, class_logits, out_hw, valid_hw=None, top_k: int | None = None):
+def instance_inference(mask_logits, class_logits, out_hw, valid_hw=None, pad_hw=None, top_k: int | None = None):
     """mask_logits [Q,h,w], class_logits [Q,K+1] -> (scores [k], labels [k], masks bool [k,H,W]).
-    `valid_hw` crops the padded area (detectron2 sem_seg_postprocess) before resizing."""
+
+    Scores and binary masks as HF:m2f-proc:695-709 (softmax over classes without the
+    no-object column, top-k over queries x classes, mask = logit > 0, score x mean
+    foreground probability inside the mask); pinned by tests/golden/postproc.npz.
+    Resizing as upstream sem_seg_postprocess (detectron2): with `pad_hw` / `valid_hw`
+    the logits are first upsampled to the padded input size, cropped to the valid
+    (un-padded) region, then resized to `out_hw` -- bilinear, align_corners=False."""
     Q, K1 = class_logits.shape
     K = K1 - 1
     scores = F.softmax(class_logits.float(), -1)[:, :-1]
@@ -54,10 +60,14 @@ def instance_inference(mask_logits, class_logits, out_hw, valid_hw=None, top_k: 
     sc, idx = scores.flatten(0, 1).topk(min(k, Q * K), sorted=False)
     lab = labels[idx]
     qi = torch.div(idx, K, rounding_mode="floor")
-    m = mask_logits[qi].float()
+    m = mask_logits[qi].float()[None]
+    if pad_hw is not None:
+        m = F.interpolate(m, size=tuple(pad_hw), mode="bilinear", align_corners=False)
     if valid_hw is not None:
-        m = m[:, : valid_hw[0], : valid_hw[1]]
-    m = F.interpolate(m[None], size=tuple(out_hw), mode="bilinear", align_corners=False)[0]
+        m = m[..., : valid_hw[0], : valid_hw[1]]
+    if tuple(m.shape[-2:]) != tuple(out_hw):
+        m = F.interpolate(m, size=tuple(out_hw), mode="bilinear", align_corners=False)
+    m = m[0]
     binm = m > 0
     prob = m.sigmoid()
     mscore = (prob * binm).flatten(1).sum(1) / (binm.flatten(1).sum(1) + 1e-6)
@@ -94,8 +104,9 @@ class Predictor:
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.amp and self.device.type == "cuda"):
             masks, classes = self.model(x)
         m, c = masks[-1][0], classes[-1][0]
-        vh, vw = (valid[0] + 3) // 4, (valid[1] + 3) // 4     # valid region at mask resolution (stride 4)
-        scores, labels, binm = instance_inference(m, c, orig, valid_hw=(vh, vw), top_k=self.top_k)
+        # stride-4 logits -> padded input size -> crop the valid region -> original size
+        scores, labels, binm = instance_inference(m, c, orig, valid_hw=valid, pad_hw=tuple(x.shape[-2:]),
+                                                  top_k=self.top_k)
         return DetResult(InstanceData(scores=scores, masks=binm, labels=labels))
 
 

@@ -236,8 +236,15 @@ class Trainer:
         self._graph_states.clear()
         torch.cuda.synchronize(self.device)
 
-    def _graph_step(self, images, mask_labels, class_labels):
+    @staticmethod
+    def target_capacity(class_labels) -> int:
+        """Padded target capacity of a batch: its largest target count rounded up to a
+        multiple of 4, so batches whose counts vary (real COCO data) share a graph."""
         kc = max([int(c.shape[0]) for c in class_labels] + [0])
+        return max(4, (kc + 3) // 4 * 4)
+
+    def _graph_step(self, images, mask_labels, class_labels):
+        kc = self.target_capacity(class_labels)
         key = (tuple(images.shape), images.dtype, kc, tuple(mask_labels[0].shape[-2:]) if mask_labels else ())
         st = self._graph_states.get(key)
         if st is None:
@@ -269,11 +276,11 @@ class Trainer:
 
     def step(self, images, mask_labels, class_labels):
         """One optimisation step; returns the (device) loss tensor, no host sync.  With
-        graphs=True the step is captured per signature (image shape, largest target count
-        of the batch; after `graph_warmup` eager steps of it) and replayed with the batch's
-        targets padded into static buffers: one launch per graph instead of ~3000 per
-        step.  One signature's graph lives at a time: another signature destroys it and is
-        captured in its place."""
+        graphs=True the step is captured per signature (image shape, padded target
+        capacity of the batch; after `graph_warmup` eager steps of it) and replayed with the batch's
+        targets padded into static buffers (capacity: the largest count rounded up to a
+        multiple of 4): one launch per graph instead of ~3000 per step.  One signature's
+        graph lives at a time: another signature destroys it and is captured in its place."""
         if self.graphs:
             loss = self._graph_step(images, mask_labels, class_labels)
         else:
