@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adamw"],
                     help="sgd: the reference's detectron2 DefaultTrainer solver; adamw: upstream train_net")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--arch", default="mask2former", choices=["mask2former", "maskdino"],
+                    help="mask2former (C1-C3, C5) or maskdino (C4: 300 queries, 4-level encoder, DN; parity unpinned)")
     ap.add_argument("--gemm-tuning", default="file", choices=["file", "tune", "off"],
                     help="vendor GEMM solution table: in-tree TunableOp file (default), re-tune, or heuristics")
     return ap.parse_args()
@@ -298,8 +300,10 @@ TRAIN_FLOPS_PER_IMAGE = {("swin_t", 1024): 3 * 530.6e9, ("swin_b", 1024): 3 * 10
                          ("swin_l", 1536): 3 * 3974.2e9}
 
 
-def _config_tag(model, size):
+def _config_tag(model, size, arch="mask2former"):
     """BASELINE.json config the run corresponds to (C2 is the headline workload)."""
+    if arch == "maskdino":
+        return "C4 (per-GPU share)" if (model, size) == ("swin_l", 1024) else "custom"
     return {("swin_t", 1024): "C2", ("swin_b", 1024): "C3 (per-GPU share)",
             ("swin_l", 1536): "C5 (per-GPU share, bf16)"}.get((model, size), "custom")
 
@@ -317,10 +321,19 @@ def main():
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    cfg = M2FConfig.preset(a.model, num_queries=a.queries)
-    model = Mask2Former(cfg).init_weights(seed=0)
-    trainer = Trainer(model, SetCriterion(cfg, matcher=a.matcher),
-                      SolverConfig(precision=a.precision, optimizer=a.optimizer), device=dev, graphs=bool(a.graphs))
+    if a.arch == "maskdino":
+        from visionseg.maskdino import MaskDINO, MaskDINOConfig, MaskDINOCriterion
+        if a.queries == 100:
+            a.queries = 300
+        cfg = MaskDINOConfig.preset(a.model, num_queries=a.queries)
+        model = MaskDINO(cfg).init_weights(seed=0)
+        crit = MaskDINOCriterion(cfg, matcher=a.matcher)
+    else:
+        cfg = M2FConfig.preset(a.model, num_queries=a.queries)
+        model = Mask2Former(cfg).init_weights(seed=0)
+        crit = SetCriterion(cfg, matcher=a.matcher)
+    trainer = Trainer(model, crit, SolverConfig(precision=a.precision, optimizer=a.optimizer), device=dev,
+                      graphs=bool(a.graphs))
     graphs = trainer.graphs
     images, ml, cl = synthetic_batch(a.batch, a.size, seed=42 + rank, device=dev)
     torch.cuda.synchronize()
@@ -360,12 +373,15 @@ def main():
     if rank == 0:
         roof, table = kernel_roofline(timer.summary(), pmc_file(a.model, a.size)) if timer else (None, {})
         cpu, parity = None, None
-        if world == 1 and not a.no_cpu_baseline:
+        if a.arch == "maskdino":
+            parity = {"unpinned": "no MaskDINO implementation exists in the container (SURVEY §8c); "
+                                  "structural GPU tests only (tests/test_gpu_maskdino.py)"}
+        if world == 1 and not a.no_cpu_baseline and a.arch == "mask2former":
             cpu = cpu_baseline(a.model, a.size, a.cpu_iters, a.queries)
-        if world == 1 and not a.no_parity:
+        if world == 1 and not a.no_parity and a.arch == "mask2former":
             print("parity check vs the oracle ...", file=sys.stderr, flush=True)
             parity = parity_check(a.model, a.size, a.queries, dev)
-        fl = TRAIN_FLOPS_PER_IMAGE.get((a.model, a.size))
+        fl = TRAIN_FLOPS_PER_IMAGE.get((a.model, a.size)) if a.arch == "mask2former" else None
         step_roof = None
         if fl:
             ach = fl * value / 1e12
@@ -377,14 +393,15 @@ def main():
         prec = ("bf16 parameters and activations, f32 master weights, gradients reduced and applied in f32 "
                 "(pure bf16, not autocast)" if a.precision == "bf16" else "f32 parameters + bf16 autocast")
         line = {
-            "metric": f"images/sec @{a.size}^2 {MODEL_NAMES.get(a.model, a.model)} Mask2Former training "
+            "metric": f"images/sec @{a.size}^2 {MODEL_NAMES.get(a.model, a.model)} "
+                      f"{'MaskDINO' if a.arch == 'maskdino' else 'Mask2Former'} training "
                       f"(fwd+loss+bwd+{a.optimizer.upper()})",
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic COCO-format defect batches (random-init weights)",
-            "config": {"workload": f"{_config_tag(a.model, a.size)}: {a.model} + Mask2Former, {a.batch}x3x{a.size}^2 "
-                                   f"per GPU, {cfg.num_queries} queries, {prec}, 1 class",
-                       "model": f"{a.model}_mask2former", "global_batch": a.batch * world, "image_size": a.size,
+            "config": {"workload": f"{_config_tag(a.model, a.size, a.arch)}: {a.model} + {a.arch}, "
+                                   f"{a.batch}x3x{a.size}^2 per GPU, {cfg.num_queries} queries, {prec}, 1 class",
+                       "model": f"{a.model}_{a.arch}", "global_batch": a.batch * world, "image_size": a.size,
                        "parallelism": f"dp{world}"},
             "final_loss": round(float(loss.item()), 4),
             "gemm_tuning": a.gemm_tuning,

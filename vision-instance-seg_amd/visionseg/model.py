@@ -305,9 +305,9 @@ class ConvGN(nn.Module):
     nchw=True: the 1/4-resolution blocks run NCHW end to end (MIOpen's NCHW 3x3 conv
     kernels are the fast ones there; the NCHW GroupNorm needs no layout copy)."""
 
-    def __init__(self, cin, cout, k, bias, relu=False, nchw=False):
+    def __init__(self, cin, cout, k, bias, relu=False, nchw=False, stride=1):
         super().__init__()
-        self.conv = nn.Conv2d(cin, cout, kernel_size=k, padding=k // 2, bias=bias)
+        self.conv = nn.Conv2d(cin, cout, kernel_size=k, padding=k // 2, bias=bias, stride=stride)
         self.gn = nn.GroupNorm(32, cout)
         self.relu = relu
         self.nchw = nchw
@@ -330,13 +330,22 @@ class ConvGN(nn.Module):
 
 
 class PixelDecoder(nn.Module):
+    """Multi-scale deformable-attention pixel decoder: Mask2Former's (3 levels: res5, res4,
+    res3; HF:m2f:1236-1419) or MaskDINO's "4s" encoder (n_levels = 4: an extra 1/64
+    level from a stride-2 3x3 conv + GroupNorm of res5 in front; upstream MaskDINOEncoder,
+    not in the container).  Levels run coarse to fine."""
+
     def __init__(self, cfg: M2FConfig, channels):
         super().__init__()
         Fd = cfg.feature_size
         self.cfg = cfg
+        self.n_levels = int(getattr(cfg, "n_levels", 3))
+        if self.n_levels not in (3, 4):
+            raise ValueError("the pixel decoder takes 3 or 4 levels")
         self.input_proj = nn.ModuleList([ConvGN(c, Fd, 1, True) for c in channels[::-1][:3]])
-        self.level_embed = nn.Parameter(torch.zeros(3, Fd))
-        self.encoder = nn.ModuleList([EncoderLayer(Fd, cfg.enc_ffn, cfg.dec_heads, 3, cfg.n_points)
+        self.extra = ConvGN(channels[-1], Fd, 3, True, stride=2) if self.n_levels == 4 else None
+        self.level_embed = nn.Parameter(torch.zeros(self.n_levels, Fd))
+        self.encoder = nn.ModuleList([EncoderLayer(Fd, cfg.enc_ffn, cfg.dec_heads, self.n_levels, cfg.n_points)
                                       for _ in range(cfg.enc_layers)])
         self.lateral = ConvGN(channels[0], Fd, 1, False, nchw=True)
         self.output = ConvGN(Fd, Fd, 3, False, relu=True, nchw=True)
@@ -346,11 +355,12 @@ class PixelDecoder(nn.Module):
     def forward(self, feats):
         Fd = self.cfg.feature_size
         dev = feats[0].device
-        embeds, pos = [], []
+        embeds = []
+        if self.extra is not None:
+            embeds.append(self.extra(feats[-1]))
         for lvl, x in enumerate(feats[::-1][:3]):
-            e = self.input_proj[lvl](x)
-            embeds.append(e)
-            pos.append(sine_pos_embed(x.shape[0], x.shape[2], x.shape[3], Fd // 2, dev).to(e.dtype))
+            embeds.append(self.input_proj[lvl](x))
+        pos = [sine_pos_embed(e.shape[0], e.shape[2], e.shape[3], Fd // 2, dev).to(e.dtype) for e in embeds]
         shapes = [(int(e.shape[2]), int(e.shape[3])) for e in embeds]
         B = embeds[0].shape[0]
         h = torch.cat([e.flatten(2).transpose(1, 2) for e in embeds], 1)

@@ -334,20 +334,32 @@ class MaskHeadFunction(torch.autograd.Function):
         B, Q, C = E.shape
         N = P.shape[1]
         sink = ctx.sink
-        if E.dtype == torch.bfloat16 and Q <= 128 and C in (128, 256):
+        if E.dtype == torch.bfloat16 and C in (128, 256):
+            # the fused kernel takes <= 128 queries: more (MaskDINO's 300 + denoising
+            # queries) run as chunks of 128 that accumulate dP in place
             g = g.float().contiguous()
             gE = torch.empty_like(E)
             acc = sink is not None and sink.buf is not None
             if sink is not None and not acc:
                 sink.buf = torch.empty_like(P)
             gP = sink.buf if sink is not None else torch.empty_like(P)
-            ws = torch.empty(int(L.lib().vs_mask_head_backward_workspace_bytes(B, Q, C)), device=E.device,
-                             dtype=torch.uint8)
-            nb = g.numel() * 4 + (E.numel() * 2 + P.numel() * 2) * 2 + (P.numel() * 2 if acc else 0)
-            with timed("mask_head_bwd", E, bytes_=nb, flops=4.0 * B * Q * C * N):
-                L.check(L.lib().vs_mask_head_backward_ex(L.dtype_code(E), L.ptr(g), L.ptr(E), L.ptr(P), L.ptr(gE),
-                                                         L.ptr(gP), L.ptr(ws), B, Q, C, N, 1, int(acc), L.stream(E)),
-                        "mask_head_backward")
+            for q0 in range(0, Q, 128):
+                q1 = min(Q, q0 + 128)
+                whole = q0 == 0 and q1 == Q
+                gc = g if whole else g[:, q0:q1].contiguous()
+                Ec = E if whole else E[:, q0:q1].contiguous()
+                gEc = gE if whole else torch.empty_like(Ec)
+                nq = q1 - q0
+                ws = torch.empty(int(L.lib().vs_mask_head_backward_workspace_bytes(B, nq, C)), device=E.device,
+                                 dtype=torch.uint8)
+                nb = gc.numel() * 4 + (Ec.numel() * 2 + P.numel() * 2) * 2 + (P.numel() * 2 if acc else 0)
+                with timed("mask_head_bwd", E, bytes_=nb, flops=4.0 * B * nq * C * N):
+                    L.check(L.lib().vs_mask_head_backward_ex(L.dtype_code(E), L.ptr(gc), L.ptr(Ec), L.ptr(P),
+                                                             L.ptr(gEc), L.ptr(gP), L.ptr(ws), B, nq, C, N, 1,
+                                                             int(acc), L.stream(E)), "mask_head_backward")
+                if not whole:
+                    gE[:, q0:q1] = gEc
+                acc = True
             if sink is not None:
                 return gE, None, None, None, None
             return gE, gP.to(ctx.pdtype), None, None, None

@@ -153,6 +153,16 @@ class Trainer:
         return self.opt.layout.views(self.opt.master)
 
     def forward_loss(self, images, mask_labels, class_labels):
+        if getattr(self.model, "takes_targets", False):
+            # MaskDINO: the targets (padded) and their boxes feed the denoising queries
+            # and the box losses
+            from .criterion import as_padded
+            from .maskdino import masks_to_boxes
+            tg = as_padded(mask_labels, class_labels, self.device)
+            boxes = masks_to_boxes(tg.masks)
+            with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.mode == "amp"):
+                out = self.model(images, tg, boxes)
+            return self.criterion(out, tg, boxes)
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.mode == "amp"):
             masks, classes = self.model(images)
         masks = [m.float() for m in masks]
