@@ -84,6 +84,8 @@ def parse():
                     help="bf16: bf16 params/activations + f32 master weights; amp: f32 params + bf16 autocast")
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adamw"],
                     help="sgd: the reference's detectron2 DefaultTrainer solver; adamw: upstream train_net")
+    ap.add_argument("--attn-fp8", action="store_true",
+                    help="C5: Swin window attention on fp8 (e4m3) MFMA (window^2 <= 160; bf16 elsewhere)")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--arch", default="mask2former", choices=["mask2former", "maskdino"],
                     help="mask2former (C1-C3, C5) or maskdino (C4: 300 queries, 4-level encoder, DN; parity unpinned)")
@@ -108,6 +110,8 @@ OP_KERNELS = {
     "msda_fwd": ["msda_fwd_kernel"],
     "window_attn_fwd": ["win_attn_fwd_mfma"],
     "window_attn_bwd": ["win_attn_bwd_mfma"],
+    "window_attn_fwd_fp8": ["win_attn_fwd_mfma_big"],
+    "window_attn_bwd_fp8": ["win_attn_bwd_mfma_big"],
     "mask_head_fwd": ["mask_head_fwd_kernel"],
     "mask_head_bwd": ["mask_head_bwd_kernel", "mask_head_bwd_reduce"],
     "masked_attn_fwd": ["xattn_fwd_mfma", "xattn_fwd_combine"],
@@ -300,12 +304,13 @@ TRAIN_FLOPS_PER_IMAGE = {("swin_t", 1024): 3 * 530.6e9, ("swin_b", 1024): 3 * 10
                          ("swin_l", 1536): 3 * 3974.2e9}
 
 
-def _config_tag(model, size, arch="mask2former"):
+def _config_tag(model, size, arch="mask2former", fp8=False):
     """BASELINE.json config the run corresponds to (C2 is the headline workload)."""
     if arch == "maskdino":
         return "C4 (per-GPU share)" if (model, size) == ("swin_l", 1024) else "custom"
-    return {("swin_t", 1024): "C2", ("swin_b", 1024): "C3 (per-GPU share)",
-            ("swin_l", 1536): "C5 (per-GPU share, bf16)"}.get((model, size), "custom")
+    if (model, size) == ("swin_l", 1536):
+        return "C5 (per-GPU share, fp8 window attention)" if fp8 else "C5 shape (per-GPU share, bf16 attention)"
+    return {("swin_t", 1024): "C2", ("swin_b", 1024): "C3 (per-GPU share)"}.get((model, size), "custom")
 
 
 def main():
@@ -329,7 +334,7 @@ def main():
         model = MaskDINO(cfg).init_weights(seed=0)
         crit = MaskDINOCriterion(cfg, matcher=a.matcher)
     else:
-        cfg = M2FConfig.preset(a.model, num_queries=a.queries)
+        cfg = M2FConfig.preset(a.model, num_queries=a.queries, attn_fp8=a.attn_fp8)
         model = Mask2Former(cfg).init_weights(seed=0)
         crit = SetCriterion(cfg, matcher=a.matcher)
     trainer = Trainer(model, crit, SolverConfig(precision=a.precision, optimizer=a.optimizer), device=dev,
@@ -399,8 +404,9 @@ def main():
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic COCO-format defect batches (random-init weights)",
-            "config": {"workload": f"{_config_tag(a.model, a.size, a.arch)}: {a.model} + {a.arch}, "
-                                   f"{a.batch}x3x{a.size}^2 per GPU, {cfg.num_queries} queries, {prec}, 1 class",
+            "config": {"workload": f"{_config_tag(a.model, a.size, a.arch, a.attn_fp8)}: {a.model} + {a.arch}, "
+                                   f"{a.batch}x3x{a.size}^2 per GPU, {cfg.num_queries} queries, {prec}"
+                                   f"{', fp8 (e4m3) window attention' if a.attn_fp8 else ''}, 1 class",
                        "model": f"{a.model}_{a.arch}", "global_batch": a.batch * world, "image_size": a.size,
                        "parallelism": f"dp{world}"},
             "final_loss": round(float(loss.item()), 4),

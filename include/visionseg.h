@@ -157,6 +157,26 @@ VS_API int vs_window_attn_backward(int dtype, const void* qkv, const float* rel_
                                    float scale, void* stream);
 
 
+/* ---- C5: fp8 (OCP e4m3) window attention ----------------------------------------
+ * Same layouts and semantics as vs_window_attn_forward/backward with bf16 storage, for
+ * window^2 <= 160.  The logits S = q.k^T and the product P.V run on
+ * v_mfma_f32_32x32x16_fp8_fp8: q, k and v of each (window, head) are quantised to e4m3
+ * in-kernel with power-of-two scales 2^floor(log2(448/amax)) (amax over the window's
+ * N x 32 values), P (unnormalised, in [0,1]) with scale 256; f32 softmax and accumulate.
+ * The backward recomputes S from the same fp8 operands (so exp(S - lse) is the
+ * forward's P) and forms dV, dP, dQ, dK in bf16 from the bf16 operands
+ * (straight-through quantisation).  Replaces the same upstream call sites as
+ * vs_window_attn_* (HF:swin:373-398) under BASELINE config C5. */
+VS_API int vs_window_attn_forward_fp8(const void* qkv, const float* rel_table, void* out, float* lse,
+                                      int num_windows, int heads, int window, int shift, int nwin_h,
+                                      int nwin_w, float scale, void* stream);
+VS_API int vs_window_attn_backward_fp8(const void* qkv, const float* rel_table, const void* out,
+                                       const float* lse, const void* grad_out, void* grad_qkv,
+                                       float* grad_table_partial, int num_windows, int heads,
+                                       int window, int shift, int nwin_h, int nwin_w, float scale,
+                                       void* stream);
+
+
 /* ---- a11: mask head -----------------------------------------------------------------
  * logits f32 [B, Q, H*W] = E [B, Q, C] x P[b]^T, with the pixel embedding P
  * channels-last [B, H*W, C] (HF:m2f:2051 einsum 'bqc,bchw->bqhw').  dtype of E and P:

@@ -678,6 +678,83 @@ __global__ void __launch_bounds__(64 * kBwdWaves) win_attn_bwd_mfma(
 // dS^T for dK of key tile w; dQ^T of the wave's queries comes from registers as above.
 constexpr int kMaxT2Big = 529;    // (2*12-1)^2
 
+// ---- fp8 (OCP e4m3, gfx950) window attention, config C5 ------------------------------
+// F8 = true selects v_mfma_f32_32x32x16_fp8_fp8 for S^T = K Q^T (forward and the
+// backward's recompute) and for O^T = V^T P^T (forward).  Operands stay bf16 in HBM and
+// LDS; each wave quantises its MFMA fragments on the fly with per-(window, head)
+// power-of-two scales s = 2^floor(log2(448 / amax)) of q, k and v (amax over the window's
+// N x 32 values; exact descale), and P (in [0, 1] before normalisation) with s = 256.
+// The backward recomputes S with the same fp8 operands and scales (identical logits, so
+// exp(S - lse) is the forward's P) and forms every gradient product in bf16 from the
+// bf16 operands (straight-through quantisation).  Non-scaled fp8 MFMA issues at the bf16
+// rate on gfx950 (MI355X_MICROARCH §Matrix cores): this is a numerics mode of the same
+// latency/LDS-bound kernel, not a throughput change.
+typedef long fp8x8_t;
+
+__device__ __forceinline__ fp8x8_t fp8_pack8(const float* f) {
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+  return (fp8x8_t)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// bf16 fragment x s -> e4m3 fragment (element j in byte j)
+__device__ __forceinline__ fp8x8_t fp8_frag(bf16x8_t v, float s) {
+  float f[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = bf16_bits_to_f32((unsigned short)v[j]) * s;
+  return fp8_pack8(f);
+}
+
+// 8 consecutive accumulator registers x s -> e4m3 fragment (permuted k, as pack8)
+__device__ __forceinline__ fp8x8_t fp8_acc8(const f32x16_t& a, int base, float s) {
+  float f[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = a[base + j] * s;
+  return fp8_pack8(f);
+}
+
+__device__ __forceinline__ f32x16_t mfma_fp8(fp8x8_t a, fp8x8_t b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float amax8(bf16x8_t v, float m) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf16_bits_to_f32((unsigned short)v[j])));
+  return m;
+}
+
+// e4m3 scale of a block: largest power of two with amax * s <= 448 (1 for an all-zero block)
+__device__ __forceinline__ float fp8_scale(float amax) {
+  return amax > 0.f ? exp2f(floorf(log2f(448.f / amax))) : 1.f;
+}
+
+constexpr float kP8Scale = 256.f;
+
+// block-wide max of NV per-thread values through `red` [waves][NV] (one __syncthreads
+// supplied by the caller between the write and the read)
+template <int NV>
+__device__ __forceinline__ void wave_amax_store(float* v, float* red) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float m = v[i];
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) m = fmaxf(m, __shfl_xor(m, s, 64));
+    if ((threadIdx.x & 63) == 0) red[(threadIdx.x >> 6) * NV + i] = m;
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void block_amax_load(float* v, const float* red, int waves) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float m = 0.f;
+    for (int w = 0; w < waves; ++w) m = fmaxf(m, red[w * NV + i]);
+    v[i] = m;
+  }
+}
+
 template <int NT>
 __device__ __forceinline__ void window_tokens_blk(const WinGeom& g, int bw, int* tok) {
   const int ws = g.ws;
@@ -695,7 +772,7 @@ __device__ __forceinline__ void window_tokens_blk(const WinGeom& g, int bw, int*
   }
 }
 
-template <int NT>
+template <int NT, bool F8>
 __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __restrict__ qkv,
                                                                  const float* __restrict__ table,
                                                                  bf16* __restrict__ out, float* __restrict__ lse,
@@ -705,23 +782,31 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   __shared__ __attribute__((aligned(16))) short sVt[32 * PT];  // V^T [d][key]
   __shared__ float sBias[kMaxT2Big];
   __shared__ int sTok[NP];
+  __shared__ float sRed[F8 ? NT * 3 : 1];
   const int bw = blockIdx.x, h = blockIdx.y;
   const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
   const bf16* win = qkv + (size_t)bw * N * C3;
   window_tokens_blk<NT>(g, bw, sTok);
   for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
+  float am[3] = {0.f, 0.f, 0.f};              // |q|, |k|, |v| maxima (F8)
   for (int p = threadIdx.x; p < NP * 4; p += blockDim.x) {
     const int t = p >> 2, c = p & 3;
     bf16x8_t k = zero8(), v = zero8();
     if (t < N) {
       k = ld8(win + (size_t)t * C3 + C + h * kD + 8 * c);
       v = ld8(win + (size_t)t * C3 + 2 * C + h * kD + 8 * c);
+      if (F8) {
+        am[0] = amax8(ld8(win + (size_t)t * C3 + h * kD + 8 * c), am[0]);
+        am[1] = amax8(k, am[1]);
+        am[2] = amax8(v, am[2]);
+      }
     }
     *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = k;
 #pragma unroll
     for (int j = 0; j < 8; ++j) sVt[(8 * c + j) * PT + t] = v[j];
   }
+  if (F8) wave_amax_store<3>(am, sRed);
   bf16x8_t qb[2];
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
@@ -729,6 +814,15 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
     qb[st] = row < N ? ld8(win + (size_t)row * C3 + h * kD + 16 * st + 8 * hh) : zero8();
   }
   __syncthreads();
+  float sq = 1.f, sk = 1.f, sv = 1.f;
+  WinGeom gl = g;
+  if (F8) {
+    block_amax_load<3>(am, sRed, NT);
+    sq = fp8_scale(am[0]);
+    sk = fp8_scale(am[1]);
+    sv = fp8_scale(am[2]);
+    gl.scale = g.scale / (sq * sk);           // exact: powers of two
+  }
   // S^T = K Q^T for every key tile of this wave's queries
   f32x16_t acc[NT];
 #pragma unroll
@@ -738,12 +832,15 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
       const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(sK + (32 * kt + r) * PK + 16 * st + 8 * hh);
-      acc[kt] = mfma16(ka, qb[st], acc[kt]);
+      if (F8)
+        acc[kt] = mfma_fp8(fp8_frag(ka, sk), fp8_frag(qb[st], sq), acc[kt]);
+      else
+        acc[kt] = mfma16(ka, qb[st], acc[kt]);
     }
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
-    logits_tile(acc[kt], g, sTok, sBias, kt, qt, r, hh);
+    logits_tile(acc[kt], gl, sTok, sBias, kt, qt, r, hh);
 #pragma unroll
     for (int i = 0; i < 16; ++i) m = fmaxf(m, acc[kt][i]);
   }
@@ -757,7 +854,8 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
       sum += acc[kt][i];
     }
   sum += __shfl_xor(sum, 32, 64);
-  const float inv = 1.f / sum, lq = m + __logf(sum);
+  const float lq = m + __logf(sum);
+  const float inv = F8 ? 1.f / (sum * kP8Scale * sv) : 1.f / sum;
   // O^T = V^T P^T
   f32x16_t o;
   zero16(o);
@@ -765,7 +863,10 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   for (int t = 0; t < 2 * NT; ++t) {
     const int kt = t >> 1, th = t & 1;
     const bf16x8_t a = ld_perm(sVt + r * PT, 32 * kt + 16 * th + 4 * hh);
-    o = mfma16(a, pack8(acc[kt], 8 * th), o);
+    if (F8)
+      o = mfma_fp8(fp8_frag(a, sv), fp8_acc8(acc[kt], 8 * th, kP8Scale), o);
+    else
+      o = mfma16(a, pack8(acc[kt], 8 * th), o);
   }
   const int q = 32 * qt + r;
   if (q < N) {
@@ -781,7 +882,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   }
 }
 
-template <int NT>
+template <int NT, bool F8>
 __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
     const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
     const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
@@ -795,6 +896,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
   __shared__ __attribute__((aligned(16))) short sDoT[32 * PT]; // dO^T [d][q]
   __shared__ float sBias[kMaxT2Big];
   __shared__ int sTok[NP];
+  __shared__ float sRed[F8 ? NT * 2 : 1];
   short* sK = sU;
   short* sV = sU + kNat;
   short* sT = sU;
@@ -805,6 +907,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
   const bf16* gwin_o = gout + (size_t)bw * N * C + h * kD;
   window_tokens_blk<NT>(g, bw, sTok);
   for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
+  float am[2] = {0.f, 0.f};                   // |q|, |k| maxima (F8)
   for (int p = threadIdx.x; p < NP * 4; p += blockDim.x) {
     const int t = p >> 2, c = p & 3;
     bf16x8_t q = zero8(), k = zero8(), v = zero8(), d = zero8();
@@ -813,6 +916,10 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
       k = ld8(win + (size_t)t * C3 + C + h * kD + 8 * c);
       v = ld8(win + (size_t)t * C3 + 2 * C + h * kD + 8 * c);
       d = ld8(gwin_o + (size_t)t * C + 8 * c);
+      if (F8) {
+        am[0] = amax8(q, am[0]);
+        am[1] = amax8(k, am[1]);
+      }
     }
     *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = k;
     *reinterpret_cast<bf16x8_t*>(sV + t * PK + 8 * c) = v;
@@ -845,7 +952,16 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
     Lq = lse[((size_t)bw * g.heads + h) * N + q];
   }
   Dq += __shfl_xor(Dq, 32, 64);
+  if (F8) wave_amax_store<2>(am, sRed);
   __syncthreads();
+  float sq = 1.f, sk = 1.f;
+  WinGeom gl = g;
+  if (F8) {                                   // the forward's scales: identical logits
+    block_amax_load<2>(am, sRed, NT);
+    sq = fp8_scale(am[0]);
+    sk = fp8_scale(am[1]);
+    gl.scale = g.scale / (sq * sk);
+  }
   // S^T = K Q^T and dP^T = V dO^T for every key tile of this wave's queries
   f32x16_t sacc[NT], dacc[NT];
 #pragma unroll
@@ -858,13 +974,16 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
       const int o = (32 * kt + r) * PK + 16 * st + 8 * hh;
-      sacc[kt] = mfma16(*reinterpret_cast<const bf16x8_t*>(sK + o), qb[st], sacc[kt]);
+      if (F8)
+        sacc[kt] = mfma_fp8(fp8_frag(*reinterpret_cast<const bf16x8_t*>(sK + o), sk), fp8_frag(qb[st], sq), sacc[kt]);
+      else
+        sacc[kt] = mfma16(*reinterpret_cast<const bf16x8_t*>(sK + o), qb[st], sacc[kt]);
       dacc[kt] = mfma16(*reinterpret_cast<const bf16x8_t*>(sV + o), db[st], dacc[kt]);
     }
   __syncthreads();                            // K / V staging is overwritten by P^T below
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
-    logits_tile(sacc[kt], g, sTok, sBias, kt, qt, r, hh);
+    logits_tile(sacc[kt], gl, sTok, sBias, kt, qt, r, hh);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int key = 32 * kt + crow(i, hh);
@@ -976,11 +1095,11 @@ extern "C" int vs_window_attn_forward(int dtype, const void* qkv, const float* t
   } else if (dtype == VS_BF16 && g.N <= 160 && use_mfma()) {
     const int nt = (g.N + 31) / 32;
     if (nt == 3)
-      hipLaunchKernelGGL(win_attn_fwd_mfma_big<3>, grid, dim3(192), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
+      hipLaunchKernelGGL((win_attn_fwd_mfma_big<3, false>), grid, dim3(192), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
     else if (nt == 4)
-      hipLaunchKernelGGL(win_attn_fwd_mfma_big<4>, grid, dim3(256), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
+      hipLaunchKernelGGL((win_attn_fwd_mfma_big<4, false>), grid, dim3(256), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
     else
-      hipLaunchKernelGGL(win_attn_fwd_mfma_big<5>, grid, dim3(320), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
+      hipLaunchKernelGGL((win_attn_fwd_mfma_big<5, false>), grid, dim3(320), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
   } else if (dtype == VS_BF16) {
     hipLaunchKernelGGL(win_attn_fwd_kernel<bf16>, grid, dim3(threads), lds, st, (const bf16*)qkv, table,
                        (bf16*)out, lse, g);
@@ -1015,7 +1134,7 @@ extern "C" int vs_window_attn_backward(int dtype, const void* qkv, const float* 
   } else if (dtype == VS_BF16 && g.N <= 160 && use_mfma()) {
     const int nt = (g.N + 31) / 32;
 #define VS_WIN_BWD_BIG(NT_)                                                                                       \
-  hipLaunchKernelGGL(win_attn_bwd_mfma_big<NT_>, grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,            \
+  hipLaunchKernelGGL((win_attn_bwd_mfma_big<NT_, false>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,            \
                      (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, grad_table_partial, g)
     if (nt == 3)
       VS_WIN_BWD_BIG(3);
@@ -1033,6 +1152,57 @@ extern "C" int vs_window_attn_backward(int dtype, const void* qkv, const float* 
   } else {
     VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
   }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+// fp8 (e4m3) window attention (config C5): bf16 storage, fp8 MFMA for the logits and
+// P.V (see "fp8 window attention" above); N <= 160 (ws <= 12).
+extern "C" int vs_window_attn_forward_fp8(const void* qkv, const float* table, void* out, float* lse, int Bw,
+                                          int heads, int ws, int shift, int nWh, int nWw, float scale,
+                                          void* stream) {
+  WinGeom g;
+  VS_CHECK(check_geom(g, Bw, heads, ws, shift, nWh, nWw, scale), "bad window geometry");
+  VS_CHECK(qkv && table && out && lse, "null pointer");
+  VS_CHECK(g.N <= 160, "fp8 window attention needs window^2 <= 160");
+  dim3 grid(Bw, heads);
+  hipStream_t st = (hipStream_t)stream;
+  const int nt = (g.N + 31) / 32;
+#define VS_WIN_FWD_F8(NT_)                                                                                        \
+  hipLaunchKernelGGL((win_attn_fwd_mfma_big<NT_, true>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,    \
+                     (bf16*)out, lse, g)
+  switch (nt) {
+    case 1: case 2: VS_WIN_FWD_F8(2); break;
+    case 3: VS_WIN_FWD_F8(3); break;
+    case 4: VS_WIN_FWD_F8(4); break;
+    default: VS_WIN_FWD_F8(5); break;
+  }
+#undef VS_WIN_FWD_F8
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_window_attn_backward_fp8(const void* qkv, const float* table, const void* out, const float* lse,
+                                           const void* grad_out, void* grad_qkv, float* grad_table_partial, int Bw,
+                                           int heads, int ws, int shift, int nWh, int nWw, float scale,
+                                           void* stream) {
+  WinGeom g;
+  VS_CHECK(check_geom(g, Bw, heads, ws, shift, nWh, nWw, scale), "bad window geometry");
+  VS_CHECK(qkv && table && out && lse && grad_out && grad_qkv && grad_table_partial, "null pointer");
+  VS_CHECK(g.N <= 160, "fp8 window attention needs window^2 <= 160");
+  dim3 grid(Bw, heads);
+  hipStream_t st = (hipStream_t)stream;
+  const int nt = (g.N + 31) / 32;
+#define VS_WIN_BWD_F8(NT_)                                                                                        \
+  hipLaunchKernelGGL((win_attn_bwd_mfma_big<NT_, true>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,    \
+                     (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, grad_table_partial, g)
+  switch (nt) {
+    case 1: case 2: VS_WIN_BWD_F8(2); break;
+    case 3: VS_WIN_BWD_F8(3); break;
+    case 4: VS_WIN_BWD_F8(4); break;
+    default: VS_WIN_BWD_F8(5); break;
+  }
+#undef VS_WIN_BWD_F8
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

@@ -57,6 +57,9 @@ class M2FConfig:
     train_num_points: int = 12544
     oversample_ratio: float = 3.0
     importance_sample_ratio: float = 0.75
+    # BASELINE config C5: the Swin window-attention core on fp8 (e4m3) MFMA
+    # (vs_window_attn_forward_fp8; bf16 activations, window^2 <= 160)
+    attn_fp8: bool = False
 
     @staticmethod
     def preset(name: str, **kw) -> "M2FConfig":
@@ -123,6 +126,7 @@ class SwinBlock(nn.Module):
     def __init__(self, dim, heads, ws, shift, mlp_ratio):
         super().__init__()
         self.ws, self.shift = ws, shift
+        self.attn_fp8 = False                  # set by SwinBackbone from M2FConfig.attn_fp8
         self.norm1 = TokenLayerNorm(dim)
         self.attn = WindowAttention(dim, heads, ws)
         self.norm2 = TokenLayerNorm(dim)
@@ -142,7 +146,8 @@ class SwinBlock(nn.Module):
         win = ops.window_partition(h.to(_compute_dtype(h)), ws, shift)   # cast first: half the bytes moved
         qkv = self.attn.qkv(win)
         o = ops.window_attention(qkv, self.attn.rel_table, self.attn.heads, ws, shift,
-                                 _padded(H, ws) // ws, _padded(W, ws) // ws)
+                                 _padded(H, ws) // ws, _padded(W, ws) // ws,
+                                 fp8=self.attn_fp8 and qkv.dtype == torch.bfloat16)
         o = ops.window_reverse(o, B, H, W, ws, shift)                 # per-token proj commutes with crop
         o = self.attn.proj(o.view(B, H * W, C))
         x, h2 = self.norm2.add_forward(x, o)
@@ -191,6 +196,9 @@ class SwinBackbone(nn.Module):
             Stage(C * 2 ** i, cfg.depths[i], cfg.num_heads[i], cfg.window_size, cfg.mlp_ratio, i < n - 1)
             for i in range(n)])
         self.out_norms = nn.ModuleList([TokenLayerNorm(C * 2 ** i) for i in range(n)])
+        for st in self.stages:
+            for blk in st.blocks:
+                blk.attn_fp8 = bool(cfg.attn_fp8)
 
     def forward(self, px):
         H, W = px.shape[-2:]

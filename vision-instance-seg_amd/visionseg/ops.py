@@ -255,11 +255,15 @@ class WindowAttentionFunction(torch.autograd.Function):
     mask fused (HF:swin:373-398, 418-468, 584-607).
 
     qkv [Bw, N, 3*C] (fused q;k;v Linear output of the partitioned windows, C =
-    heads*32), rel_table [(2ws-1)^2, heads] -> [Bw, N, C]."""
+    heads*32), rel_table [(2ws-1)^2, heads] -> [Bw, N, C].  fp8=True (bf16 qkv, window^2
+    <= 160): the e4m3 MFMA path of config C5 (vs_window_attn_forward_fp8)."""
 
     @staticmethod
-    def forward(ctx, qkv, rel_table, heads, window, shift, nwin_h, nwin_w, scale):
+    def forward(ctx, qkv, rel_table, heads, window, shift, nwin_h, nwin_w, scale, fp8=False):
         L.require_hip(qkv, rel_table)
+        if fp8 and (qkv.dtype != torch.bfloat16 or window * window > 160):
+            raise ValueError(f"fp8 window attention needs bf16 qkv and window^2 <= 160 (got {qkv.dtype}, "
+                             f"window {window})")
         qkv = qkv.contiguous()
         table = rel_table.float().contiguous()
         Bw, N, C3 = qkv.shape
@@ -268,40 +272,53 @@ class WindowAttentionFunction(torch.autograd.Function):
             raise ValueError(f"qkv {tuple(qkv.shape)} does not match heads={heads} (x32) window={window}")
         out = torch.empty(Bw, N, C, device=qkv.device, dtype=qkv.dtype)
         lse = torch.empty(Bw, heads, N, device=qkv.device, dtype=torch.float32)
-        with timed("window_attn_fwd", qkv, bytes_=(qkv.numel() + out.numel()) * qkv.element_size() + lse.numel() * 4,
+        with timed("window_attn_fwd_fp8" if fp8 else "window_attn_fwd", qkv,
+                   bytes_=(qkv.numel() + out.numel()) * qkv.element_size() + lse.numel() * 4,
                    flops=4.0 * Bw * heads * N * N * 32):
-            L.check(L.lib().vs_window_attn_forward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
-                                                   L.ptr(lse), Bw, heads, window, shift, nwin_h, nwin_w,
-                                                   float(scale), L.stream(qkv)), "window_attn_forward")
-        ctx.meta = (heads, window, shift, nwin_h, nwin_w, float(scale), rel_table.dtype)
+            if fp8:
+                L.check(L.lib().vs_window_attn_forward_fp8(L.ptr(qkv), L.ptr(table), L.ptr(out), L.ptr(lse), Bw,
+                                                           heads, window, shift, nwin_h, nwin_w, float(scale),
+                                                           L.stream(qkv)), "window_attn_forward_fp8")
+            else:
+                L.check(L.lib().vs_window_attn_forward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
+                                                       L.ptr(lse), Bw, heads, window, shift, nwin_h, nwin_w,
+                                                       float(scale), L.stream(qkv)), "window_attn_forward")
+        ctx.meta = (heads, window, shift, nwin_h, nwin_w, float(scale), rel_table.dtype, bool(fp8))
         ctx.save_for_backward(qkv, table, out, lse)
         return out
 
     @staticmethod
     def backward(ctx, grad_out):
         qkv, table, out, lse = ctx.saved_tensors
-        heads, window, shift, nwin_h, nwin_w, scale, tdtype = ctx.meta
+        heads, window, shift, nwin_h, nwin_w, scale, tdtype, fp8 = ctx.meta
         Bw, N, C3 = qkv.shape
         g = grad_out.to(qkv.dtype).contiguous()
         gqkv = torch.empty_like(qkv)
         T2 = (2 * window - 1) ** 2
         part = torch.empty(Bw, heads, T2, device=qkv.device, dtype=torch.float32)
-        with timed("window_attn_bwd", qkv, bytes_=(3 * qkv.numel() + 2 * out.numel()) * qkv.element_size(),
+        with timed("window_attn_bwd_fp8" if fp8 else "window_attn_bwd", qkv,
+                   bytes_=(3 * qkv.numel() + 2 * out.numel()) * qkv.element_size(),
                    flops=10.0 * Bw * heads * N * N * 32):
-            L.check(L.lib().vs_window_attn_backward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
-                                                    L.ptr(lse), L.ptr(g), L.ptr(gqkv), L.ptr(part), Bw, heads,
-                                                    window, shift, nwin_h, nwin_w, scale, L.stream(qkv)),
-                    "window_attn_backward")
+            if fp8:
+                L.check(L.lib().vs_window_attn_backward_fp8(L.ptr(qkv), L.ptr(table), L.ptr(out), L.ptr(lse),
+                                                            L.ptr(g), L.ptr(gqkv), L.ptr(part), Bw, heads, window,
+                                                            shift, nwin_h, nwin_w, scale, L.stream(qkv)),
+                        "window_attn_backward_fp8")
+            else:
+                L.check(L.lib().vs_window_attn_backward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
+                                                        L.ptr(lse), L.ptr(g), L.ptr(gqkv), L.ptr(part), Bw, heads,
+                                                        window, shift, nwin_h, nwin_w, scale, L.stream(qkv)),
+                        "window_attn_backward")
         gtable = part.sum(0).t().contiguous().to(tdtype)
-        return gqkv, gtable, None, None, None, None, None, None
+        return gqkv, gtable, None, None, None, None, None, None, None
 
 
 def window_attention(qkv, rel_table, heads: int, window: int, shift: int, nwin_h: int, nwin_w: int,
-                     scale: float | None = None):
+                     scale: float | None = None, fp8: bool = False):
     if scale is None:
         scale = 32 ** -0.5
     return WindowAttentionFunction.apply(qkv, rel_table, int(heads), int(window), int(shift), int(nwin_h),
-                                         int(nwin_w), float(scale))
+                                         int(nwin_w), float(scale), bool(fp8))
 
 
 class MaskHeadFunction(torch.autograd.Function):
