@@ -12,9 +12,7 @@ Two yardsticks per case:
 The backward is the gradient of the quantised logits with straight-through operands
 (dV, dP, dQ, dK formed in bf16 from the bf16 operands); its yardstick is that formula in
 f32 and, loosely, the exact fp32 autograd gradient."""
-import math
 
-import numpy as np
 import pytest
 import torch
 

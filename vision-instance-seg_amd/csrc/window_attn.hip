@@ -289,67 +289,85 @@ __global__ void __launch_bounds__(256) win_attn_bwd_kernel(
 // O^T = V^T P^T takes P^T straight from the accumulators: the MFMA's k index is mapped to
 // keys in the C layout's row order (k = 8hh + j  <->  key 16t + (j&3) + 8(j>>2) + 4hh) and
 // the A operand (V^T, staged in LDS) is read in that same order, so P never leaves
-// registers.  Backward: dP^T = V dO^T (same layout), dV = P^T dO and dK = dS^T Q through
-// one LDS copy of P^T / dS^T, dQ^T = K^T dS^T again straight from registers; the bias
-// gradient is binned per window in LDS (as the scalar path).
-// Relative-position bias gradient of one (window, head) from its dS^T tile in LDS
-// ([key][query] bf16, row pitch `pitch`): bin t = (dy, dx) gets the sum of dS over the
-// pairs with ty_q - ty_k = dy, tx_q - tx_k = dx (HF:swin:350-365 index), each bin
-// summed by one thread in a fixed order (deterministic).  Threads `tid` of `nthreads`.
-__device__ __forceinline__ void bias_grad_bins(const short* dst, int pitch, const WinGeom& g, int tid, int nthreads,
-                                               float* out) {
-  const int ws = g.ws, tw = 2 * ws - 1;
-  for (int t = tid; t < g.T2; t += nthreads) {
-    const int dy = t / tw - (ws - 1), dx = t % tw - (ws - 1);
-    const int qy0 = dy > 0 ? dy : 0, qy1 = dy < 0 ? ws + dy : ws;
-    const int qx0 = dx > 0 ? dx : 0, qx1 = dx < 0 ? ws + dx : ws;
-    float acc = 0.f;
-    for (int qy = qy0; qy < qy1; ++qy)
-      for (int qx = qx0; qx < qx1; ++qx) {
-        const int q = qy * ws + qx, k = (qy - dy) * ws + (qx - dx);
-        acc += bf16_bits_to_f32((unsigned short)dst[k * pitch + q]);
-      }
-    out[t] = acc;
-  }
-}
+// registers.  Backward: win_attn_bwd_fa below (two phases, any N <= 160).
 
 constexpr int kMaxT2 = 225;       // (2*8-1)^2
 constexpr int kPadK = 72;         // LDS row pitch (shorts) of the 64-token operands
 
-// token metadata of the window: ty | tx << 8 | region << 16
-__device__ __forceinline__ void window_tokens(const WinGeom& g, int bw, int lane, int* tok) {
+// Token metadata of the window: tok[t] = kk | region << 16 with kk = ty (2ws-1) + tx, so
+// the relative-position index of a (query, key) pair is kk_q - kk_k + (ws-1) 2ws
+// (HF:swin:350-365: (ty_q - ty_k + ws-1)(2ws-1) + tx_q - tx_k + ws-1) -- one subtract per
+// logit, no integer multiply.  Region ids as HF:swin:584-607 (padded-grid position).
+__device__ __forceinline__ int token_meta(const WinGeom& g, int bw, int t) {
+  if (t >= g.N) return 0;
   const int ws = g.ws;
   const int wl = bw % (g.nWh * g.nWw);
   const int wy = wl / g.nWw, wx = wl % g.nWw;
-  const int Hp = g.nWh * ws, Wp = g.nWw * ws;
-  const int t = lane;
-  if (t < g.N) {
-    const int ty = t / ws, tx = t % ws;
-    const int reg = g.shift > 0 ? region_of(wy * ws + ty, Hp, ws, g.shift) * 3 + region_of(wx * ws + tx, Wp, ws, g.shift) : 0;
-    tok[t] = ty | (tx << 8) | (reg << 16);
-  } else {
-    tok[t] = 0;
+  const int ty = t / ws, tx = t % ws;
+  const int reg = g.shift > 0 ? region_of(wy * ws + ty, g.nWh * ws, ws, g.shift) * 3 +
+                                    region_of(wx * ws + tx, g.nWw * ws, ws, g.shift)
+                              : 0;
+  return (ty * (2 * ws - 1) + tx) | (reg << 16);
+}
+
+__device__ __forceinline__ void window_tokens(const WinGeom& g, int bw, int lane, int* tok) {
+  tok[lane] = token_meta(g, bw, lane);
+}
+
+__device__ __forceinline__ int rel_c0(const WinGeom& g) { return (g.ws - 1) * 2 * g.ws; }
+
+// Scaled logits + bias + shift mask of an S^T tile (rows = keys 32 kt + crow(i, hh) in the
+// registers, column = query q on the lane); keys >= N -> -inf.  rel[i] receives each
+// logit's bias index (the backward bins dS with it).  tok must be 16-B aligned.
+__device__ __forceinline__ void logits_kq(f32x16_t& s, const WinGeom& g, const int* tok, const float* bias, int kt,
+                                          int q, int hh, int* rel) {
+  const int tq = tok[q];
+  const int qo = (tq & 0xffff) + rel_c0(g), rq = tq >> 16;
+  const bool sh = g.shift > 0, tail = 32 * kt + 32 > g.N;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int kb = 32 * kt + 8 * g4 + 4 * hh;
+    const int4 t4 = *reinterpret_cast<const int4*>(tok + kb);
+    const int tk[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * g4 + e;
+      const int rl = qo - (tk[e] & 0xffff);
+      rel[i] = rl;
+      float v = s[i] * g.scale + bias[rl];
+      if (sh && (tk[e] >> 16) != rq) v += -100.f;
+      if (tail && kb + e >= g.N) v = -INFINITY;
+      s[i] = v;
+    }
   }
 }
 
-// scaled logits + bias + shift mask for the S^T accumulators of one (kt, qt) tile
 __device__ __forceinline__ void logits_tile(f32x16_t& s, const WinGeom& g, const int* tok, const float* bias, int kt,
                                             int qt, int r, int hh) {
-  const int q = 32 * qt + r;
-  const int tq = tok[q];
-  const int tyq = tq & 255, txq = (tq >> 8) & 255, rq = tq >> 16;
-  const int tw = 2 * g.ws - 1;
+  int rel[16];
+  logits_kq(s, g, tok, bias, kt, 32 * qt + r, hh, rel);
+}
+
+// The same logits for an S tile (rows = queries 32 qt + crow(i, hh), column = key on the
+// lane): identical values to logits_kq for every (query, key) pair; key >= N or
+// query >= N -> -inf.
+__device__ __forceinline__ void logits_qk(f32x16_t& s, const WinGeom& g, const int* tok, const float* bias, int qt,
+                                          int key, int hh) {
+  const int tk = tok[key];
+  const int ko = (tk & 0xffff) - rel_c0(g), rk = tk >> 16;
+  const bool sh = g.shift > 0, tail = 32 * qt + 32 > g.N, kin = key < g.N;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int k = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh;
-    if (k < g.N) {
-      const int tk = tok[k];
-      const int rel = (tyq - (tk & 255) + g.ws - 1) * tw + (txq - ((tk >> 8) & 255) + g.ws - 1);
-      float v = s[i] * g.scale + bias[rel];
-      if ((tk >> 16) != rq) v += -100.f;
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int qb = 32 * qt + 8 * g4 + 4 * hh;
+    const int4 t4 = *reinterpret_cast<const int4*>(tok + qb);
+    const int tq[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * g4 + e;
+      float v = s[i] * g.scale + bias[(tq[e] & 0xffff) - ko];
+      if (sh && (tq[e] >> 16) != rk) v += -100.f;
+      if (!kin || (tail && qb + e >= g.N)) v = -INFINITY;
       s[i] = v;
-    } else {
-      s[i] = -INFINITY;
     }
   }
 }
@@ -362,7 +380,7 @@ __global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* 
                                                                     WinGeom g, int items) {
   __shared__ __attribute__((aligned(16))) short sVt[kFwdWaves][32 * kPadK];   // V^T [d][key]
   __shared__ float sBias[kFwdWaves][kMaxT2];
-  __shared__ int sTok[kFwdWaves][64];
+  __shared__ __attribute__((aligned(16))) int sTok[kFwdWaves][64];
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int item = blockIdx.x * kFwdWaves + wave;
   if (item >= items) return;                  // wave-uniform; only wave-level syncs below
@@ -460,212 +478,6 @@ __global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* 
   }
 }
 
-constexpr int kBwdWaves = 2;
-
-__global__ void __launch_bounds__(64 * kBwdWaves) win_attn_bwd_mfma(
-    const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
-    const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
-    float* __restrict__ gtable_part, WinGeom g, int items) {
-  __shared__ __attribute__((aligned(16))) short sT[kBwdWaves][64 * kPadK];    // P^T, then dS^T [key][q]
-  __shared__ __attribute__((aligned(16))) short sDoT[kBwdWaves][32 * kPadK];  // dO^T [d][q]
-  __shared__ __attribute__((aligned(16))) short sQT[kBwdWaves][32 * kPadK];   // Q^T [d][q]
-  __shared__ __attribute__((aligned(16))) short sKT[kBwdWaves][32 * kPadK];   // K^T [d][key]
-  __shared__ float sBias[kBwdWaves][kMaxT2];
-  __shared__ int sTok[kBwdWaves][64];
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
-  const int item = blockIdx.x * kBwdWaves + wave;
-  if (item >= items) return;
-  const int h = item % g.heads, bw = item / g.heads;
-  const int N = g.N, C = g.heads * kD, C3 = 3 * C;
-  const bf16* win = qkv + (size_t)bw * N * C3;
-  const bf16* gwin_o = gout + (size_t)bw * N * C + h * kD;
-  short* pt = sT[wave];
-  short* dot_ = sDoT[wave];
-  short* qt_ = sQT[wave];
-  short* kt_ = sKT[wave];
-  float* bias = sBias[wave];
-  int* tok = sTok[wave];
-  window_tokens(g, bw, l, tok);
-  for (int t = l; t < g.T2; t += 64) bias[t] = table[t * g.heads + h];
-  {  // transposed copies, lane = token
-    const int t = l;
-    const bf16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const bf16x8_t q = t < N ? ld8(win + (size_t)t * C3 + h * kD + 8 * c) : z;
-      const bf16x8_t k = t < N ? ld8(win + (size_t)t * C3 + C + h * kD + 8 * c) : z;
-      const bf16x8_t d = t < N ? ld8(gwin_o + (size_t)t * C + 8 * c) : z;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        qt_[(8 * c + j) * kPadK + t] = q[j];
-        kt_[(8 * c + j) * kPadK + t] = k[j];
-        dot_[(8 * c + j) * kPadK + t] = d[j];
-      }
-    }
-  }
-  // S^T = K Q^T and dP^T = V dO^T
-  f32x16_t sacc[2][2], dacc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[a][b][i] = dacc[a][b][i] = 0.f;
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    bf16x8_t ka[2], va[2], qb[2], db[2];
-    const bf16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int row = 32 * t + r;
-      const int off = 16 * st + 8 * hh;
-      ka[t] = row < N ? ld8(win + (size_t)row * C3 + C + h * kD + off) : z;
-      va[t] = row < N ? ld8(win + (size_t)row * C3 + 2 * C + h * kD + off) : z;
-      qb[t] = row < N ? ld8(win + (size_t)row * C3 + h * kD + off) : z;
-      db[t] = row < N ? ld8(gwin_o + (size_t)row * C + off) : z;
-    }
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        sacc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kt], qb[qt], sacc[kt][qt], 0, 0, 0);
-        dacc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[kt], db[qt], dacc[kt][qt], 0, 0, 0);
-      }
-  }
-  // D_q = dO_q . O_q  and the saved log-sum-exp, per query column
-  float Dq[2], Lq[2];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = 32 * qt + r;
-    float d = 0.f;
-    Lq[qt] = 0.f;
-    if (q < N) {
-      const bf16* orow = out + ((size_t)bw * N + q) * C + h * kD + 16 * hh;
-      const bf16* grow = gwin_o + (size_t)q * C + 16 * hh;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const bf16x8_t ov = ld8(orow + 8 * c), gv = ld8(grow + 8 * c);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d += bf16_bits_to_f32((unsigned short)ov[j]) * bf16_bits_to_f32((unsigned short)gv[j]);
-      }
-      Lq[qt] = lse[((size_t)bw * g.heads + h) * N + q];
-    }
-    Dq[qt] = d + __shfl_xor(d, 32, 64);
-  }
-  wave_sync();
-  // P^T = exp(logits - lse); P^T -> LDS [key][q] (bf16)
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      logits_tile(sacc[kt][qt], g, tok, bias, kt, qt, r, hh);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = (32 * qt + r) < N ? __expf(sacc[kt][qt][i] - Lq[qt]) : 0.f;
-        sacc[kt][qt][i] = p;
-        pt[(32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh) * kPadK + 32 * qt + r] = bf16_bits(p);
-      }
-    }
-  wave_sync();
-  // dV = P^T dO  (rows = keys, cols = d; k over queries)
-  f32x16_t dv[2];
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dv[kt][i] = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(dot_ + r * kPadK + 16 * t + 8 * hh);
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(pt + (32 * kt + r) * kPadK + 16 * t + 8 * hh);
-      dv[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, dv[kt], 0, 0, 0);
-    }
-  }
-  bf16* gw = gqkv + (size_t)bw * N * C3 + h * kD;
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh;
-      if (key < N) gw[(size_t)key * C3 + 2 * C + r] = __float2bfloat16(dv[kt][i]);
-    }
-  // dS^T = P^T (dP^T - D_q)
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float ds = sacc[kt][qt][i] * (dacc[kt][qt][i] - Dq[qt]);
-        dacc[kt][qt][i] = ds;
-      }
-  }
-  wave_sync();                                // every lane has read P^T for dV
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        pt[(32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh) * kPadK + 32 * qt + r] = bf16_bits(dacc[kt][qt][i]);
-  wave_sync();
-  // dK = scale * dS^T Q
-  f32x16_t dk[2];
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dk[kt][i] = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(qt_ + r * kPadK + 16 * t + 8 * hh);
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(pt + (32 * kt + r) * kPadK + 16 * t + 8 * hh);
-      dk[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, dk[kt], 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh;
-      if (key < N) gw[(size_t)key * C3 + C + r] = __float2bfloat16(dk[kt][i] * g.scale);
-    }
-  // dQ^T = scale * K^T dS^T  (dS^T straight from registers, K^T read in the permuted key order)
-  f32x16_t dq[2];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dq[qt][i] = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int kt = t >> 1, th = t & 1;
-    const bf16x8_t a = ld_perm(kt_ + r * kPadK, 32 * kt + 16 * th + 4 * hh);
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-      dq[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pack8(dacc[kt][qt], 8 * th), dq[qt], 0, 0, 0);
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = 32 * qt + r;
-    if (q < N) {
-      bf16* dst = gw + (size_t)q * C3;
-#pragma unroll
-      for (int grp = 0; grp < 4; ++grp) {
-        bf16x4_t v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = bf16_bits(dq[qt][4 * grp + e] * g.scale);
-        *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
-      }
-    }
-  }
-  wave_sync();
-  // bias gradient: bin (dy, dx) sums dS over the query/key pairs at that offset, read
-  // back from the dS^T tile (no LDS float atomics: ~0.33 lane-ops/clk/CU on gfx950)
-  bias_grad_bins(pt, kPadK, g, l, 64, gtable_part + ((size_t)bw * g.heads + h) * g.T2);
-}
-
 // ---------------------------------------------------------------------------------------
 // bf16 MFMA path for windows of 64 < N <= 32*NT tokens (Swin-B/L ws = 12: N = 144, NT = 5).
 // One workgroup per (window, head), one wave per 32-query tile; fragments as above.
@@ -757,19 +569,7 @@ __device__ __forceinline__ void block_amax_load(float* v, const float* red, int 
 
 template <int NT>
 __device__ __forceinline__ void window_tokens_blk(const WinGeom& g, int bw, int* tok) {
-  const int ws = g.ws;
-  const int wl = bw % (g.nWh * g.nWw);
-  const int wy = wl / g.nWw, wx = wl % g.nWw;
-  const int Hp = g.nWh * ws, Wp = g.nWw * ws;
-  for (int t = threadIdx.x; t < 32 * NT; t += blockDim.x) {
-    if (t < g.N) {
-      const int ty = t / ws, tx = t % ws;
-      const int reg = g.shift > 0 ? region_of(wy * ws + ty, Hp, ws, g.shift) * 3 + region_of(wx * ws + tx, Wp, ws, g.shift) : 0;
-      tok[t] = ty | (tx << 8) | (reg << 16);
-    } else {
-      tok[t] = 0;
-    }
-  }
+  for (int t = threadIdx.x; t < 32 * NT; t += blockDim.x) tok[t] = token_meta(g, bw, t);
 }
 
 template <int NT, bool F8>
@@ -781,38 +581,44 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   __shared__ __attribute__((aligned(16))) short sK[NP * PK];   // K [key][d]
   __shared__ __attribute__((aligned(16))) short sVt[32 * PT];  // V^T [d][key]
   __shared__ float sBias[kMaxT2Big];
-  __shared__ int sTok[NP];
+  __shared__ __attribute__((aligned(16))) int sTok[NP];
   __shared__ float sRed[F8 ? NT * 3 : 1];
   const int bw = blockIdx.x, h = blockIdx.y;
   const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
   const bf16* win = qkv + (size_t)bw * N * C3;
-  window_tokens_blk<NT>(g, bw, sTok);
-  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
-  float am[3] = {0.f, 0.f, 0.f};              // |q|, |k|, |v| maxima (F8)
-  for (int p = threadIdx.x; p < NP * 4; p += blockDim.x) {
-    const int t = p >> 2, c = p & 3;
-    bf16x8_t k = zero8(), v = zero8();
-    if (t < N) {
-      k = ld8(win + (size_t)t * C3 + C + h * kD + 8 * c);
-      v = ld8(win + (size_t)t * C3 + 2 * C + h * kD + 8 * c);
-      if (F8) {
-        am[0] = amax8(ld8(win + (size_t)t * C3 + h * kD + 8 * c), am[0]);
-        am[1] = amax8(k, am[1]);
-        am[2] = amax8(v, am[2]);
-      }
-    }
-    *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = k;
+  // all global operands requested up front: two 16-B K / V chunks per thread (NP x 4
+  // chunks, 64 NT threads) and this lane's query row slices
+  bf16x8_t ck[2], cv[2], cq[2], qb[2];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sVt[(8 * c + j) * PT + t] = v[j];
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    const bf16* row = win + (size_t)t * C3 + h * kD + 8 * c;
+    ck[it] = t < N ? ld8(row + C) : zero8();
+    cv[it] = t < N ? ld8(row + 2 * C) : zero8();
+    if (F8) cq[it] = t < N ? ld8(row) : zero8();
   }
-  if (F8) wave_amax_store<3>(am, sRed);
-  bf16x8_t qb[2];
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
     const int row = 32 * qt + r;
     qb[st] = row < N ? ld8(win + (size_t)row * C3 + h * kD + 16 * st + 8 * hh) : zero8();
   }
+  window_tokens_blk<NT>(g, bw, sTok);
+  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
+  float am[3] = {0.f, 0.f, 0.f};              // |q|, |k|, |v| maxima (F8)
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = ck[it];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sVt[(8 * c + j) * PT + t] = cv[it][j];
+    if (F8) {
+      am[0] = amax8(cq[it], am[0]);
+      am[1] = amax8(ck[it], am[1]);
+      am[2] = amax8(cv[it], am[2]);
+    }
+  }
+  if (F8) wave_amax_store<3>(am, sRed);
   __syncthreads();
   float sq = 1.f, sk = 1.f, sv = 1.f;
   WinGeom gl = g;
@@ -882,76 +688,124 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Backward, flash-attention-2 split in two phases of ONE workgroup per (window, head),
+// NT = ceil(N / 32) waves, any N <= 160 (Swin-T ws 7: NT = 2; Swin-B/L ws 12: NT = 5).
+// The earlier kernels kept a whole query tile's S^T / dP^T rows in registers and a
+// [key][query] P^T / dS^T tile in LDS: 203 VGPR + 128 AGPR (1 wave/SIMD) for N <= 64 and
+// 89 KB of LDS (1 workgroup/CU) for N = 144.  Here each wave streams over 32-token tiles
+// with only the current tile's S and dP (2 x 16 f32) and its output accumulators live:
+//   phase 1 (wave = query tile qt):  for each key tile kt: S^T = K Q^T, dP^T = V dO^T,
+//     P = exp(S - lse), dS = P (dP - D); dQ^T += K^T dS^T (dS^T straight from registers,
+//     K^T read in the permuted key order); the bias gradient binned in the wave's own LDS
+//     bins (for one register and one lane half the 32 queries of a key have 32 distinct
+//     offsets, so the halves take turns and every update is a plain read-modify-write);
+//   phase 2 (wave = key tile kw, after the staging is swapped): for each query tile qt:
+//     S = Q K^T, dP = dO V^T (query rows, key columns), P, dS as above;
+//     dV^T += dO^T P and dK^T += Q^T dS (P, dS straight from registers, dO^T / Q^T read
+//     in the permuted query order).
+// S and dP are formed twice (the MFMA units idle in this kernel); LDS peaks at ~47 KB for
+// N = 144 (3 workgroups/CU).  F8: the logits on the forward's fp8 operands and scales.
 template <int NT, bool F8>
-__global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
+__global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
     const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
     float* __restrict__ gtable_part, WinGeom g) {
   constexpr int NP = 32 * NT, PT = NP + 8, PK = 40;
-  constexpr int kNat = NP * PK, kTB = NP * PT;
-  constexpr int kU = 2 * kNat > kTB ? 2 * kNat : kTB;
-  __shared__ __attribute__((aligned(16))) short sU[kU];        // K, V [token][d]; then P^T / dS^T [key][q]
-  __shared__ __attribute__((aligned(16))) short sQT[32 * PT];  // Q^T [d][q]
-  __shared__ __attribute__((aligned(16))) short sKT[32 * PT];  // K^T [d][key]
-  __shared__ __attribute__((aligned(16))) short sDoT[32 * PT]; // dO^T [d][q]
+  constexpr int kNat = NP * PK, kTr = 32 * PT;
+  constexpr int kT2 = NT <= 2 ? 225 : NT == 3 ? 289 : NT == 4 ? 441 : 529;   // (2 ws_max - 1)^2
+  constexpr int kBinW = kT2;                                  // f32 bias-gradient bins per wave
+  constexpr int kP1 = 2 * kNat + kTr + NT * kBinW * 2;        // K, V, K^T, f32 bins (in shorts)
+  constexpr int kP2 = 2 * kNat + 2 * kTr;                     // Q, dO, Q^T, dO^T
+  __shared__ __attribute__((aligned(16))) short sU[kP1 > kP2 ? kP1 : kP2];
   __shared__ float sBias[kMaxT2Big];
-  __shared__ int sTok[NP];
+  __shared__ __attribute__((aligned(16))) int sTok[NP];
+  __shared__ float sL[NP], sD[NP];
   __shared__ float sRed[F8 ? NT * 2 : 1];
-  short* sK = sU;
-  short* sV = sU + kNat;
-  short* sT = sU;
   const int bw = blockIdx.x, h = blockIdx.y;
-  const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
-  const bf16* win = qkv + (size_t)bw * N * C3;
-  const bf16* gwin_o = gout + (size_t)bw * N * C + h * kD;
-  window_tokens_blk<NT>(g, bw, sTok);
-  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
-  float am[2] = {0.f, 0.f};                   // |q|, |k| maxima (F8)
-  for (int p = threadIdx.x; p < NP * 4; p += blockDim.x) {
-    const int t = p >> 2, c = p & 3;
-    bf16x8_t q = zero8(), k = zero8(), v = zero8(), d = zero8();
-    if (t < N) {
-      q = ld8(win + (size_t)t * C3 + h * kD + 8 * c);
-      k = ld8(win + (size_t)t * C3 + C + h * kD + 8 * c);
-      v = ld8(win + (size_t)t * C3 + 2 * C + h * kD + 8 * c);
-      d = ld8(gwin_o + (size_t)t * C + 8 * c);
-      if (F8) {
-        am[0] = amax8(q, am[0]);
-        am[1] = amax8(k, am[1]);
-      }
-    }
-    *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = k;
-    *reinterpret_cast<bf16x8_t*>(sV + t * PK + 8 * c) = v;
+  const bf16* win = qkv + (size_t)bw * N * C3 + h * kD;
+  const bf16* gwo = gout + (size_t)bw * N * C + h * kD;
+  const bf16* owin = out + (size_t)bw * N * C + h * kD;
+  bf16* gw = gqkv + (size_t)bw * N * C3 + h * kD;
+  const float* lrow = lse + ((size_t)bw * g.heads + h) * N;
+  // Every global operand of a phase is requested before any is used (one round trip per
+  // phase): the staging chunks -- exactly two 16-B chunks per thread and tensor (NP x 4
+  // chunks, 64 NT threads) --, this lane's query row slices (phase 1: Q, dO, O for
+  // D = rowsum(dO * O), lse) or key row slices (phase 2: K, V).  Loading phase 2's operands
+  // up front as well, or giving each lane half its own bias bins, measured 1.5x slower at
+  // N = 144 (registers / LDS cost occupancy; tools/winbench.py).
+  const int qt = wv, kw = wv;
+  const int q = 32 * qt + r, key = 32 * kw + r;
+  bf16x8_t ck[2], cv[2], cq[2], cd[2];
+  auto load_p2 = [&]() {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sQT[(8 * c + j) * PT + t] = q[j];
-      sKT[(8 * c + j) * PT + t] = k[j];
-      sDoT[(8 * c + j) * PT + t] = d[j];
+    for (int it = 0; it < 2; ++it) {
+      const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+      cq[it] = t < N ? ld8(win + (size_t)t * C3 + 8 * c) : zero8();
+      cd[it] = t < N ? ld8(gwo + (size_t)t * C + 8 * c) : zero8();
     }
+  };
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    const bool in = t < N;
+    const bf16* row = win + (size_t)t * C3 + 8 * c;
+    ck[it] = in ? ld8(row + C) : zero8();
+    cv[it] = in ? ld8(row + 2 * C) : zero8();
+    if (F8) cq[it] = in ? ld8(row) : zero8();
   }
-  const int q = 32 * qt + r;
-  bf16x8_t qb[2], db[2];
+  bf16x8_t qb[2], db[2], ob[2], kb[2], vb[2];
+  auto load_kv = [&]() {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int off = 16 * st + 8 * hh;
+      kb[st] = key < N ? ld8(win + (size_t)key * C3 + C + off) : zero8();
+      vb[st] = key < N ? ld8(win + (size_t)key * C3 + 2 * C + off) : zero8();
+    }
+  };
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
     const int off = 16 * st + 8 * hh;
-    qb[st] = q < N ? ld8(win + (size_t)q * C3 + h * kD + off) : zero8();
-    db[st] = q < N ? ld8(gwin_o + (size_t)q * C + off) : zero8();
+    qb[st] = q < N ? ld8(win + (size_t)q * C3 + off) : zero8();
+    db[st] = q < N ? ld8(gwo + (size_t)q * C + off) : zero8();
+    ob[st] = q < N ? ld8(owin + (size_t)q * C + off) : zero8();
   }
-  // D_q = dO_q . O_q and the saved log-sum-exp of this lane's query
-  float Dq = 0.f, Lq = 0.f;
-  if (q < N) {
-    const bf16* orow = out + ((size_t)bw * N + q) * C + h * kD + 16 * hh;
-    const bf16* grow = gwin_o + (size_t)q * C + 16 * hh;
+
+  const float Lq = q < N ? lrow[q] : 0.f;
+  window_tokens_blk<NT>(g, bw, sTok);
+  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
+  // ---- phase 1 staging: K, V natural, K^T; D, lse; bins zeroed
+  short* sKn = sU;
+  short* sVn = sU + kNat;
+  short* sKT = sU + 2 * kNat;
+  float* sBins = reinterpret_cast<float*>(sU + 2 * kNat + kTr);
+  float am[2] = {0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const bf16x8_t ov = ld8(orow + 8 * c), gv = ld8(grow + 8 * c);
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    *reinterpret_cast<bf16x8_t*>(sKn + t * PK + 8 * c) = ck[it];
+    *reinterpret_cast<bf16x8_t*>(sVn + t * PK + 8 * c) = cv[it];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Dq += bf16_bits_to_f32((unsigned short)ov[j]) * bf16_bits_to_f32((unsigned short)gv[j]);
+    for (int j = 0; j < 8; ++j) sKT[(8 * c + j) * PT + t] = ck[it][j];
+    if (F8) {
+      am[0] = amax8(cq[it], am[0]);
+      am[1] = amax8(ck[it], am[1]);
     }
-    Lq = lse[((size_t)bw * g.heads + h) * N + q];
   }
+  float Dq = 0.f;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      Dq += bf16_bits_to_f32((unsigned short)ob[st][j]) * bf16_bits_to_f32((unsigned short)db[st][j]);
   Dq += __shfl_xor(Dq, 32, 64);
+  if (hh == 0) {
+    sD[q] = Dq;
+    sL[q] = Lq;
+  }
+  for (int t = threadIdx.x; t < NT * kBinW; t += blockDim.x) sBins[t] = 0.f;
   if (F8) wave_amax_store<2>(am, sRed);
   __syncthreads();
   float sq = 1.f, sk = 1.f;
@@ -962,100 +816,145 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_mfma_big(
     sk = fp8_scale(am[1]);
     gl.scale = g.scale / (sq * sk);
   }
-  // S^T = K Q^T and dP^T = V dO^T for every key tile of this wave's queries
-  f32x16_t sacc[NT], dacc[NT];
-#pragma unroll
-  for (int kt = 0; kt < NT; ++kt) {
-    zero16(sacc[kt]);
-    zero16(dacc[kt]);
+  fp8x8_t qb8[2];
+  if (F8) {
+    qb8[0] = fp8_frag(qb[0], sq);
+    qb8[1] = fp8_frag(qb[1], sq);
   }
+  float* bins = sBins + qt * kBinW;
+  f32x16_t dq;
+  zero16(dq);
+  for (int kt = 0; kt < NT; ++kt) {
+    f32x16_t s, dp;
+    zero16(s);
+    zero16(dp);
 #pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
+    for (int st = 0; st < 2; ++st) {
       const int o = (32 * kt + r) * PK + 16 * st + 8 * hh;
+      const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(sKn + o);
       if (F8)
-        sacc[kt] = mfma_fp8(fp8_frag(*reinterpret_cast<const bf16x8_t*>(sK + o), sk), fp8_frag(qb[st], sq), sacc[kt]);
+        s = mfma_fp8(fp8_frag(ka, sk), qb8[st], s);
       else
-        sacc[kt] = mfma16(*reinterpret_cast<const bf16x8_t*>(sK + o), qb[st], sacc[kt]);
-      dacc[kt] = mfma16(*reinterpret_cast<const bf16x8_t*>(sV + o), db[st], dacc[kt]);
+        s = mfma16(ka, qb[st], s);
+      dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sVn + o), db[st], dp);
     }
-  __syncthreads();                            // K / V staging is overwritten by P^T below
-#pragma unroll
-  for (int kt = 0; kt < NT; ++kt) {
-    logits_tile(sacc[kt], gl, sTok, sBias, kt, qt, r, hh);
+    int rel[16];
+    logits_kq(s, gl, sTok, sBias, kt, q, hh, rel);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int key = 32 * kt + crow(i, hh);
-      const float p = q < N ? __expf(sacc[kt][i] - Lq) : 0.f;
-      sT[key * PT + q] = bf16_bits(p);
-      dacc[kt][i] = p * (dacc[kt][i] - Dq);
+      const float p = q < N ? __expf(s[i] - Lq) : 0.f;
+      dp[i] = p * (dp[i] - Dq);
     }
-  }
-  __syncthreads();
-  // dV = P^T dO for key tile kw = wave (k over all queries)
-  const int kw = qt;
-  bf16* gw = gqkv + (size_t)bw * N * C3 + h * kD;
-  {
-    f32x16_t dv;
-    zero16(dv);
+    // dQ^T += K^T dS^T
 #pragma unroll
-    for (int t = 0; t < 2 * NT; ++t) {
-      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(sDoT + r * PT + 16 * t + 8 * hh);
-      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sT + (32 * kw + r) * PT + 16 * t + 8 * hh);
-      dv = mfma16(a, b, dv);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = 32 * kw + crow(i, hh);
-      if (key < N) gw[(size_t)key * C3 + 2 * C + r] = __float2bfloat16(dv[i]);
-    }
-  }
-  __syncthreads();                            // every wave has read P^T
-#pragma unroll
-  for (int kt = 0; kt < NT; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sT[(32 * kt + crow(i, hh)) * PT + q] = bf16_bits(dacc[kt][i]);
-  __syncthreads();
-  // dK = scale * dS^T Q for key tile kw
-  {
-    f32x16_t dk;
-    zero16(dk);
-#pragma unroll
-    for (int t = 0; t < 2 * NT; ++t) {
-      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(sQT + r * PT + 16 * t + 8 * hh);
-      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sT + (32 * kw + r) * PT + 16 * t + 8 * hh);
-      dk = mfma16(a, b, dk);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = 32 * kw + crow(i, hh);
-      if (key < N) gw[(size_t)key * C3 + C + r] = __float2bfloat16(dk[i] * g.scale);
-    }
-  }
-  // dQ^T = scale * K^T dS^T for this wave's queries (dS^T from registers)
-  {
-    f32x16_t dq;
-    zero16(dq);
-#pragma unroll
-    for (int t = 0; t < 2 * NT; ++t) {
-      const int kt = t >> 1, th = t & 1;
+    for (int th = 0; th < 2; ++th) {
       const bf16x8_t a = ld_perm(sKT + r * PT, 32 * kt + 16 * th + 4 * hh);
-      dq = mfma16(a, pack8(dacc[kt], 8 * th), dq);
+      dq = mfma16(a, pack8(dp, 8 * th), dq);
     }
-    if (q < N) {
-      bf16* dst = gw + (size_t)q * C3;
+    // relative-position bias gradient: for one register the 32 lanes of a half hold one
+    // key and 32 queries, i.e. 32 distinct bins, so with the halves taking turns every
+    // update is a plain LDS read-modify-write (ds_add_f32 is slow on gfx950); padded
+    // queries / keys carry dS = 0 (their rel index stays inside the table)
 #pragma unroll
-      for (int grp = 0; grp < 4; ++grp) {
-        bf16x4_t v;
+    for (int half = 0; half < 2; ++half) {
+      if (hh == half) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = bf16_bits(dq[4 * grp + e] * g.scale);
-        *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+        for (int i = 0; i < 16; ++i) bins[rel[i]] += dp[i];
       }
+      wave_sync();
     }
   }
-  __syncthreads();                            // (sT still holds dS^T)
-  bias_grad_bins(sT, PT, g, threadIdx.x, blockDim.x, gtable_part + ((size_t)bw * g.heads + h) * g.T2);
+  if (q < N) {
+    bf16* dst = gw + (size_t)q * C3;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      bf16x4_t v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = bf16_bits(dq[4 * grp + e] * g.scale);
+      *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+    }
+  }
+  __syncthreads();                            // bins complete; phase-1 staging dead after this
+  {
+    float* gp = gtable_part + ((size_t)bw * g.heads + h) * g.T2;
+    for (int t = threadIdx.x; t < g.T2; t += blockDim.x) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT; ++w) a += sBins[w * kT2 + t];
+      gp[t] = a;
+    }
+  }
+  __syncthreads();
+  // ---- phase 2 staging: Q, dO natural; Q^T, dO^T
+  load_p2();
+  load_kv();
+  short* sQn = sU;
+  short* sDn = sU + kNat;
+  short* sQT = sU + 2 * kNat;
+  short* sDT = sU + 2 * kNat + kTr;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    *reinterpret_cast<bf16x8_t*>(sQn + t * PK + 8 * c) = cq[it];
+    *reinterpret_cast<bf16x8_t*>(sDn + t * PK + 8 * c) = cd[it];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sQT[(8 * c + j) * PT + t] = cq[it][j];
+      sDT[(8 * c + j) * PT + t] = cd[it][j];
+    }
+  }
+  fp8x8_t kb8[2];
+  if (F8) {
+    kb8[0] = fp8_frag(kb[0], sk);
+    kb8[1] = fp8_frag(kb[1], sk);
+  }
+  __syncthreads();
+  f32x16_t dv, dk;
+  zero16(dv);
+  zero16(dk);
+  for (int qq = 0; qq < NT; ++qq) {
+    f32x16_t s, dp;
+    zero16(s);
+    zero16(dp);
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int o = (32 * qq + r) * PK + 16 * st + 8 * hh;
+      const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(sQn + o);
+      if (F8)
+        s = mfma_fp8(fp8_frag(qa, sq), kb8[st], s);
+      else
+        s = mfma16(qa, kb[st], s);
+      dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sDn + o), vb[st], dp);
+    }
+    logits_qk(s, gl, sTok, sBias, qq, key, hh);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qi = 32 * qq + crow(i, hh);
+      const float p = __expf(s[i] - sL[qi]);
+      s[i] = p;
+      dp[i] = p * (dp[i] - sD[qi]);
+    }
+#pragma unroll
+    for (int th = 0; th < 2; ++th) {
+      const int base = 32 * qq + 16 * th + 4 * hh;
+      dv = mfma16(ld_perm(sDT + r * PT, base), pack8(s, 8 * th), dv);
+      dk = mfma16(ld_perm(sQT + r * PT, base), pack8(dp, 8 * th), dk);
+    }
+  }
+  if (key < N) {
+    bf16* dst = gw + (size_t)key * C3;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      bf16x4_t a, b;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = bf16_bits(dk[4 * grp + e] * g.scale);
+        b[e] = bf16_bits(dv[4 * grp + e]);
+      }
+      *reinterpret_cast<bf16x4_t*>(dst + C + 8 * grp + 4 * hh) = a;
+      *reinterpret_cast<bf16x4_t*>(dst + 2 * C + 8 * grp + 4 * hh) = b;
+    }
+  }
 }
 
 int check_geom(WinGeom& g, int Bw, int heads, int ws, int shift, int nWh, int nWw, float scale) {
@@ -1077,6 +976,40 @@ static bool use_mfma() {
   return !(e && atoi(e) != 0);
 }
 
+// VS_WIN_FWD_BLK=1: the one-workgroup-per-(window, head) forward also for N <= 64 (A/B)
+static bool fwd_blk_small() {
+  const char* e = getenv("VS_WIN_FWD_BLK");
+  return e && atoi(e) != 0;
+}
+
+#define VS_NT_SWITCH(nt, M)            \
+  switch (nt) {                        \
+    case 1: case 2: M(2); break;       \
+    case 3: M(3); break;               \
+    case 4: M(4); break;               \
+    default: M(5); break;              \
+  }
+
+template <bool F8>
+static void launch_fwd_blk(const WinGeom& g, dim3 grid, hipStream_t st, const void* qkv, const float* table,
+                           void* out, float* lse) {
+#define VS_FWD_BLK(NT_)                                                                                     \
+  hipLaunchKernelGGL((win_attn_fwd_mfma_big<NT_, F8>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table, \
+                     (bf16*)out, lse, g)
+  VS_NT_SWITCH((g.N + 31) / 32, VS_FWD_BLK)
+#undef VS_FWD_BLK
+}
+
+template <bool F8>
+static void launch_bwd_fa(const WinGeom& g, dim3 grid, hipStream_t st, const void* qkv, const float* table,
+                          const void* out, const float* lse, const void* grad_out, void* grad_qkv, float* gpart) {
+#define VS_BWD_FA(NT_)                                                                                      \
+  hipLaunchKernelGGL((win_attn_bwd_fa<NT_, F8>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,       \
+                     (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g)
+  VS_NT_SWITCH((g.N + 31) / 32, VS_BWD_FA)
+#undef VS_BWD_FA
+}
+
 extern "C" int vs_window_attn_forward(int dtype, const void* qkv, const float* table, void* out,
                                       float* lse, int Bw, int heads, int ws, int shift, int nWh,
                                       int nWw, float scale, void* stream) {
@@ -1088,18 +1021,12 @@ extern "C" int vs_window_attn_forward(int dtype, const void* qkv, const float* t
   const size_t lds = sizeof(float) * (2 * g.N * kD + g.T2);
   dim3 grid(Bw, heads);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VS_BF16 && g.N <= 64 && use_mfma()) {
+  if (dtype == VS_BF16 && g.N <= 64 && use_mfma() && !fwd_blk_small()) {
     const int items = Bw * heads;
     hipLaunchKernelGGL(win_attn_fwd_mfma, dim3((items + kFwdWaves - 1) / kFwdWaves), dim3(64 * kFwdWaves), 0, st,
                        (const bf16*)qkv, table, (bf16*)out, lse, g, items);
   } else if (dtype == VS_BF16 && g.N <= 160 && use_mfma()) {
-    const int nt = (g.N + 31) / 32;
-    if (nt == 3)
-      hipLaunchKernelGGL((win_attn_fwd_mfma_big<3, false>), grid, dim3(192), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
-    else if (nt == 4)
-      hipLaunchKernelGGL((win_attn_fwd_mfma_big<4, false>), grid, dim3(256), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
-    else
-      hipLaunchKernelGGL((win_attn_fwd_mfma_big<5, false>), grid, dim3(320), 0, st, (const bf16*)qkv, table, (bf16*)out, lse, g);
+    launch_fwd_blk<false>(g, grid, st, qkv, table, out, lse);
   } else if (dtype == VS_BF16) {
     hipLaunchKernelGGL(win_attn_fwd_kernel<bf16>, grid, dim3(threads), lds, st, (const bf16*)qkv, table,
                        (bf16*)out, lse, g);
@@ -1126,23 +1053,8 @@ extern "C" int vs_window_attn_backward(int dtype, const void* qkv, const float* 
   VS_CHECK(lds <= 160 * 1024, "window too large for LDS");
   dim3 grid(Bw, heads);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VS_BF16 && g.N <= 64 && use_mfma()) {
-    const int items = Bw * heads;
-    hipLaunchKernelGGL(win_attn_bwd_mfma, dim3((items + kBwdWaves - 1) / kBwdWaves), dim3(64 * kBwdWaves), 0, st,
-                       (const bf16*)qkv, table, (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv,
-                       grad_table_partial, g, items);
-  } else if (dtype == VS_BF16 && g.N <= 160 && use_mfma()) {
-    const int nt = (g.N + 31) / 32;
-#define VS_WIN_BWD_BIG(NT_)                                                                                       \
-  hipLaunchKernelGGL((win_attn_bwd_mfma_big<NT_, false>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,            \
-                     (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, grad_table_partial, g)
-    if (nt == 3)
-      VS_WIN_BWD_BIG(3);
-    else if (nt == 4)
-      VS_WIN_BWD_BIG(4);
-    else
-      VS_WIN_BWD_BIG(5);
-#undef VS_WIN_BWD_BIG
+  if (dtype == VS_BF16 && g.N <= 160 && use_mfma()) {
+    launch_bwd_fa<false>(g, grid, st, qkv, table, out, lse, grad_out, grad_qkv, grad_table_partial);
   } else if (dtype == VS_BF16) {
     hipLaunchKernelGGL(win_attn_bwd_kernel<bf16>, grid, dim3(threads), lds, st, (const bf16*)qkv, table,
                        (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, grad_table_partial, g);
@@ -1165,19 +1077,7 @@ extern "C" int vs_window_attn_forward_fp8(const void* qkv, const float* table, v
   VS_CHECK(check_geom(g, Bw, heads, ws, shift, nWh, nWw, scale), "bad window geometry");
   VS_CHECK(qkv && table && out && lse, "null pointer");
   VS_CHECK(g.N <= 160, "fp8 window attention needs window^2 <= 160");
-  dim3 grid(Bw, heads);
-  hipStream_t st = (hipStream_t)stream;
-  const int nt = (g.N + 31) / 32;
-#define VS_WIN_FWD_F8(NT_)                                                                                        \
-  hipLaunchKernelGGL((win_attn_fwd_mfma_big<NT_, true>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,    \
-                     (bf16*)out, lse, g)
-  switch (nt) {
-    case 1: case 2: VS_WIN_FWD_F8(2); break;
-    case 3: VS_WIN_FWD_F8(3); break;
-    case 4: VS_WIN_FWD_F8(4); break;
-    default: VS_WIN_FWD_F8(5); break;
-  }
-#undef VS_WIN_FWD_F8
+  launch_fwd_blk<true>(g, dim3(Bw, heads), (hipStream_t)stream, qkv, table, out, lse);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
@@ -1190,19 +1090,8 @@ extern "C" int vs_window_attn_backward_fp8(const void* qkv, const float* table, 
   VS_CHECK(check_geom(g, Bw, heads, ws, shift, nWh, nWw, scale), "bad window geometry");
   VS_CHECK(qkv && table && out && lse && grad_out && grad_qkv && grad_table_partial, "null pointer");
   VS_CHECK(g.N <= 160, "fp8 window attention needs window^2 <= 160");
-  dim3 grid(Bw, heads);
-  hipStream_t st = (hipStream_t)stream;
-  const int nt = (g.N + 31) / 32;
-#define VS_WIN_BWD_F8(NT_)                                                                                        \
-  hipLaunchKernelGGL((win_attn_bwd_mfma_big<NT_, true>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,    \
-                     (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, grad_table_partial, g)
-  switch (nt) {
-    case 1: case 2: VS_WIN_BWD_F8(2); break;
-    case 3: VS_WIN_BWD_F8(3); break;
-    case 4: VS_WIN_BWD_F8(4); break;
-    default: VS_WIN_BWD_F8(5); break;
-  }
-#undef VS_WIN_BWD_F8
+  launch_bwd_fa<true>(g, dim3(Bw, heads), (hipStream_t)stream, qkv, table, out, lse, grad_out, grad_qkv,
+                      grad_table_partial);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
