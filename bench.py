@@ -106,7 +106,7 @@ def pmc_file(model, size):
 
 
 OP_KERNELS = {
-    "msda_bwd": ["msda_bwd_geom_kernel", "msda_bwd_binned_kernel"],
+    "msda_bwd": ["msda_bwd_geom_kernel", "msda_bwd_mfma_wg_kernel"],
     "msda_fwd": ["msda_fwd_kernel"],
     "window_attn_fwd": ["win_attn_fwd_mfma"],
     "window_attn_bwd": ["win_attn_bwd_mfma"],

@@ -247,6 +247,13 @@ VS_API int vs_layer_norm_backward_add(int dtype, const void* dy, const void* x, 
                                       const float* rstd, const void* dres, void* dx, void* dw, void* db, void* ws,
                                       int M, int C, void* stream);
 VS_API long long vs_layer_norm_backward_workspace_bytes(int rows, int cols);
+/* vs_layer_norm_backward(_add) (dres may be NULL) that also writes dx_colsum [C] (dtype,
+ * may be NULL): the column sums of dx as stored -- the bias gradient of a Linear whose
+ * output is the LayerNorm's residual input, with no second read of dx. */
+VS_API int vs_layer_norm_backward_ex(int dtype, const void* grad_y, const void* x, const void* weight,
+                                     const float* mean, const float* rstd, const void* grad_res, void* grad_x,
+                                     void* grad_weight, void* grad_bias, void* dx_colsum, void* workspace,
+                                     int rows, int cols, void* stream);
 /* grad_y [M, C] -> grad_x [M, C], grad_weight / grad_bias [C] (dtype, overwritten). */
 VS_API int vs_layer_norm_backward(int dtype, const void* grad_y, const void* x, const void* weight,
                                   const float* mean, const float* rstd, void* grad_x, void* grad_weight,

@@ -409,6 +409,47 @@ def test_msda_encoder_shapes_backward_vs_oracle(cfg, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [96, 256, 768])
+def test_add_layer_norm_colsum_feeds_linear_bias(monkeypatch, dtype, C):
+    """The LayerNorm backward's fused column sums of dx (vs_layer_norm_backward_ex) become
+    the bias gradient of the TokenLinear whose output is the residual branch r (no
+    column_sum launch), and equal autograd's sum of dL/dr (f64 reference); an in-place
+    update of the gradient afterwards invalidates them (version check)."""
+    from visionseg.linear import TokenLinear
+    ops = _ops()
+    calls = []
+    real = ops.column_sum
+    monkeypatch.setattr(ops, "column_sum", lambda t: calls.append(t.shape) or real(t))
+    g = torch.Generator(device="cuda").manual_seed(C)
+    M, Ci = 20000, 64
+    lin = TokenLinear(Ci, C).to(DEV, dtype)
+    w = (1 + 0.1 * torch.randn(C, device=DEV, generator=g)).to(dtype).requires_grad_(True)
+    b = (0.1 * torch.randn(C, device=DEV, generator=g)).to(dtype).requires_grad_(True)
+    x = torch.randn(M, C, device=DEV, generator=g).to(dtype).requires_grad_(True)
+    h = torch.randn(M, Ci, device=DEV, generator=g).to(dtype)
+    gy = torch.randn(M, C, device=DEV, generator=g).to(dtype)
+    gs = torch.randn(M, C, device=DEV, generator=g).to(dtype)
+    r = lin(h)
+    s, y = ops.add_layer_norm(x, r, w, b)
+    torch.autograd.backward([y, s], [gy, gs])
+    assert not calls, calls                                   # bias gradient came from the LN pass
+    # reference: dL/dr = dL/d(x + r) from an f64 torch LayerNorm
+    xs = (x.detach().double() + r.detach().double()).requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xs, (C,), w.detach().double(), b.detach().double(), 1e-5)
+    torch.autograd.backward([yr, xs], [gy.double(), gs.double()])
+    exp = xs.grad.sum(0)
+    tol = 1e-4 if dtype == torch.float32 else 2 ** -6
+    rel = float((lin.bias.grad.double() - exp).abs().max() / exp.abs().max())
+    assert rel <= tol, rel
+    # a modified gradient must not reuse the recorded sums
+    gx = torch.randn(M, C, device=DEV, generator=g).to(dtype)
+    ops.attach_colsum(gx, torch.zeros(C, device=DEV, dtype=dtype))
+    assert ops.take_colsum(gx) is not None
+    gx.add_(1)
+    assert ops.take_colsum(gx) is None
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("K", [40000, 70756])
 def test_token_linear_split_k_grads(dtype, K):
     """Split-K weight gradient (visionseg.linear) vs an f64 reference of dY^T X; the
@@ -484,6 +525,54 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, win, jitter):
     np.testing.assert_allclose(wd.grad.cpu().numpy(), gw, atol=2e-5 * max(1.0, np.abs(gw).max()), rtol=0)
     gl = lr.grad.numpy()
     np.testing.assert_allclose(ld.grad.cpu().numpy(), gl, atol=2e-5 * max(1.0, np.abs(gl).max()), rtol=0)
+
+
+@pytest.mark.parametrize("win", ["tile", "tile-1024", "tile-odd", "sub", "4lvl"])
+@pytest.mark.parametrize("jitter", [0.0, 0.3, 3.0, 12.0])
+def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
+    """bf16 grad_value by the MFMA query-tile kernels (msda_bwd_mfma_wg_kernel: 8 x 8 tiles per
+    4-wave workgroup, the default, VS_MSDA_MFMA=2; msda_bwd_mfma_kernel: 4 x 4 tiles per
+    wave, =1; W[cell][q] x g[q][c] per box, W split into bf16 hi + lo) vs (a) the binned kernel on the same
+    inputs (VS_MSDA_MFMA=0; both sum in f32: <= 1e-5 of the gradient scale) and (b) the
+    oracle (bf16 output rounding: 2^-8 relative + 1e-4).  jitter 12 px drives boxes past
+    the 128-cell cap (clipped corners take the direct atomics); "sub" runs 16 consecutive
+    queries of a query subset (Q != S), "4lvl" four levels stored finest first."""
+    ops = _ops()
+    monkeypatch.setattr(ops, "_MSDA_BWD", "carry")
+    shapes, B, H = [(8, 8), (16, 16), (32, 32)], 2, 4
+    if win == "tile-1024":
+        shapes, B, H = [(32, 32), (64, 64), (128, 128)], 1, 8
+    elif win == "tile-odd":
+        shapes = [(9, 13), (18, 26), (35, 51)]
+    elif win == "4lvl":
+        shapes = [(48, 80), (24, 40), (12, 20), (6, 10)]
+    value, loc, w = _encoder_like_inputs(B, shapes, H, 4, seed=13, jitter=jitter)
+    if win == "sub":
+        idx = torch.randperm(loc.shape[1], generator=torch.Generator().manual_seed(5))[:700].sort().values
+        loc, w = loc[:, idx].contiguous(), w[:, idx].contiguous()
+    value = value.to(torch.bfloat16)
+    vr, lr, wr = value.float().clone().requires_grad_(True), loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    ref = R.msda_ref(vr, shapes, lr, wr)
+    go = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3)).to(torch.bfloat16)
+    ref.backward(go.float())
+    grads = {}
+    for mf in ("2", "1", "0"):
+        monkeypatch.setenv("VS_MSDA_MFMA", mf)
+        vd = value.to(DEV).requires_grad_(True)
+        out = ops.ms_deform_attn(vd, shapes, loc.to(DEV), w.to(DEV))
+        out.backward(go.to(DEV))
+        grads[mf] = vd.grad.float().cpu()
+    scale = float(vr.grad.abs().max())
+    for mf in ("0", "2", "1"):
+        err = (grads[mf] - vr.grad).abs()
+        bad = err > vr.grad.abs() * 2 ** -8 + 1e-4
+        assert not bool(bad.any()), (mf, float(err.max()), int(bad.sum()), float(vr.grad[bad][0]),
+                                     float(grads[mf][bad][0]))
+    for mf in ("2", "1"):
+        d = (grads[mf] - grads["0"]).abs()
+        # all f32 sums, rounded to bf16 once: within two bf16 ulps, plus f32 summation-order
+        # noise (~1e-7 of the summed magnitudes) where contributions cancel to ~0
+        assert bool((d <= grads["0"].abs() * 2 ** -6 + 3e-5 * scale).all()), (mf, float(d.max()))
 
 
 @pytest.mark.parametrize("case", [
@@ -782,7 +871,7 @@ def test_small_linear_weight_slice():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,C,Hs,Ws,H,W", [(2, 256, 16, 16, 32, 32), (1, 64, 128, 128, 256, 256),
+@pytest.mark.parametrize("B,C,Hs,Ws,H,W", [(2, 256, 16, 16, 32, 32), (1, 64, 128, 128, 256, 256), (1, 64, 21, 36, 42, 72),
                                            (2, 32, 13, 21, 25, 42), (1, 32, 7, 9, 7, 9), (1, 96, 40, 70, 64, 100)])
 def test_upsample_add_vs_torch(dtype, B, C, Hs, Ws, H, W):
     """FPN merge (csrc/upsample.hip): cur + bilinear upsample of a token-major level vs

@@ -68,8 +68,12 @@ def main():
             locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
             for mode in a.msda_modes.split(","):
                 ops._MSDA_BWD = "tiled" if mode == "tiled" else "carry"
-                os.environ["VS_MSDA_RUN"] = {"carry16": "16", "window": "16"}.get(mode, "0")
-                os.environ["VS_MSDA_WIN"] = "1" if mode == "window" else "0"
+                os.environ["VS_MSDA_RUN"] = {"carry16": "16", "window": "16", "window8": "16"}.get(mode, "0")
+                os.environ["VS_MSDA_WIN"] = "1" if mode.startswith("window") else "0"
+                os.environ["VS_MSDA_TILE"] = "8" if mode == "window8" else "4"
+                os.environ["VS_MSDA_MFMA"] = {"mfma8": "2", "mfma4": "1"}.get(mode, "0")
+                if mode.startswith("mfma"):
+                    os.environ["VS_MSDA_RUN"], os.environ["VS_MSDA_WIN"] = "16", "1"
 
                 def fb():
                     o = ops.ms_deform_attn(v, shapes, locr, wr)

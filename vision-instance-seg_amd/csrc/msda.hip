@@ -22,6 +22,7 @@
 // vs_msda_backward_tiled is the deterministic, atomic-free variant (grad_value by
 // destination tile, written once in the value dtype; ops VS_MSDA_BWD=tiled).
 #include "common.h"
+#include "mfma_util.h"
 
 namespace vs {
 namespace {
@@ -921,6 +922,349 @@ __global__ void __launch_bounds__(64) msda_bwd_binned_kernel(const float* __rest
   }
 }
 
+// ---------------------------------------------------------------------------------
+// grad_value by query tiles as a dense MFMA product (default for bf16, P == 4): one wave
+// per (tile of 16 queries, image, head); lane = tap (query lane % 16, point lane / 16).
+// Per value level the tile's taps span a small box of cells; grad_value over the box is
+//     Gv[cell][c] = sum_q W[cell][q] g[q][c],
+// W[cell][q] = sum over q's 4 points of the bilinear x attention weight of the corner at
+// the cell: a [box x 16] by [16 x 32] product, i.e. one v_mfma_f32_32x32x16_bf16 per 32
+// cells (x2: W in f32 is split into bf16 hi + lo parts, exact to ~2^-17; g is bf16
+// already), then one 128-B f32 atomic row per non-empty cell.  W is built in LDS by plain
+// read-modify-writes: the 4 points take turns, so the 16 lanes of a turn (16 distinct
+// queries = 16 distinct columns) never collide.  This replaces the counting sort and the
+// per-cell record walk of the binned kernel (msda_bwd_binned_kernel, still the f32 path):
+// no integer atomics, no scan, no record scatter.  Boxes over kWCap cells are clipped;
+// the corners outside go straight to grad_value (one 128-B atomic row each).
+constexpr int kWCap = 128;     // cells per box (4 MFMA row tiles)
+constexpr int kWP = 20;        // W row pitch (floats): 16 queries + 4 (2-way banks on the A reads)
+
+template <int TX, int TY>
+__global__ void __launch_bounds__(64) msda_bwd_mfma_kernel(const float* __restrict__ loc,
+                                                           const float* __restrict__ attw,
+                                                           const bf16* __restrict__ gout, float* __restrict__ gvalue,
+                                                           Levels lv, QueryTiles qt, int S, int Hh, int Q, int L,
+                                                           int nblk) {
+  constexpr int P = 4;
+  constexpr int NQ = TX * TY;
+  static_assert(NQ == 16, "16 queries x 4 points = one tap per lane");
+  __shared__ __attribute__((aligned(16))) short sg[NQ * kD];   // grad_out rows of the tile [q][c] (bf16)
+  __shared__ __attribute__((aligned(16))) float sW[kWCap * kWP];
+  __shared__ int sHit[kWCap];
+  const int blk = xcd_swizzle(blockIdx.x, nblk);
+  const int h = blk % Hh;
+  const int tile = (blk / Hh) % qt.per_image;
+  const int b = blk / Hh / qt.per_image;
+  const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
+  const int LP = L * P;
+  const int tq = lane % NQ, tpt = lane / NQ;
+  const int qid = btile_query<TX, TY>(qt, lv, L, tile, tq, Q);
+  const long long grp = ((long long)b * Q + (qid < 0 ? 0 : qid)) * Hh + h;
+  float2 pxy[kMaxLevels];
+  float paw[kMaxLevels];
+#pragma unroll
+  for (int l = 0; l < kMaxLevels; ++l) {
+    pxy[l] = make_float2(0.f, 0.f);
+    paw[l] = 0.f;
+    if (l < L && qid >= 0) {
+      pxy[l] = *reinterpret_cast<const float2*>(loc + (grp * LP + l * P + tpt) * 2);
+      paw[l] = attw[grp * LP + l * P + tpt];
+    }
+  }
+  {  // grad_out rows: lane = (query, 8-channel part); zero rows for queries outside the grid
+    const int rq = lane >> 2, part = lane & 3;
+    const int q = btile_query<TX, TY>(qt, lv, L, tile, rq, Q);
+    bf16x8_t v = zero8();
+    if (q >= 0) v = ld8(gout + (((long long)b * Q + q) * Hh + h) * kD + part * 8);
+    *reinterpret_cast<bf16x8_t*>(sg + rq * kD + part * 8) = v;
+  }
+  wave_sync();
+  // B operand (same for every level and row tile): k = query 8 hh + j, column = channel r
+  bf16x8_t bq;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bq[j] = sg[(8 * hh + j) * kD + r];
+  const size_t rowstride = (size_t)Hh * kD;
+  const size_t vbase = ((size_t)b * S * Hh + h) * kD;
+  for (int l = 0; l < L; ++l) {
+    const int Hl = lv.h[l], Wl = lv.w[l];
+    const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
+    float2 xy = pxy[0];
+    float aw = paw[0];
+#pragma unroll
+    for (int k = 1; k < kMaxLevels; ++k)
+      if (l == k) {
+        xy = pxy[k];
+        aw = paw[k];
+      }
+    const Tap t = tap_geom(xy.x, xy.y, Hl, Wl);
+    const bool tv = qid >= 0 && t.inside;
+    int cy[4], cx[4];
+    float cw[4];
+    bool ok[4];
+    int ylo = 1 << 30, xlo = 1 << 30, yhi = -1, xhi = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      cy[k] = t.h0 + (k >> 1);
+      cx[k] = t.w0 + (k & 1);
+      ok[k] = tv && cy[k] >= 0 && cy[k] < Hl && cx[k] >= 0 && cx[k] < Wl;
+      cw[k] = ((k >> 1) ? t.lh : t.hh) * ((k & 1) ? t.lw : t.hw) * aw;
+      if (ok[k]) {
+        ylo = min(ylo, cy[k]);
+        yhi = max(yhi, cy[k]);
+        xlo = min(xlo, cx[k]);
+        xhi = max(xhi, cx[k]);
+      }
+    }
+    if (__ballot(ok[0] || ok[1] || ok[2] || ok[3]) == 0ull) continue;
+    const int oy = wave_min(ylo), ox = wave_min(xlo);
+    const int BX = min(wave_max(xhi) - ox + 1, kWCap);
+    const int BY = min(wave_max(yhi) - oy + 1, kWCap / BX);
+    const int ncell = BX * BY;
+    const int nmt = (ncell + 31) >> 5;
+    // zero the box's W rows (the row tiles the MFMAs read) and hit flags
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = lane; i < nmt * 32 * (kWP / 4); i += 64) reinterpret_cast<float4*>(sW)[i] = z4;
+    for (int i = lane; i < nmt * 32; i += 64) sHit[i] = 0;
+    wave_sync();
+    int cell[4];
+    bool out[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool in = ok[k] && (unsigned)(cy[k] - oy) < (unsigned)BY && (unsigned)(cx[k] - ox) < (unsigned)BX;
+      out[k] = ok[k] && !in;
+      cell[k] = in ? (cy[k] - oy) * BX + (cx[k] - ox) : -1;
+    }
+    // W[cell][q] += weight; the points take turns (16 lanes, 16 distinct query columns)
+#pragma unroll
+    for (int pt = 0; pt < P; ++pt) {
+      if (tpt == pt) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (cell[k] >= 0) {
+            sW[cell[k] * kWP + tq] += cw[k];
+            sHit[cell[k]] = 1;
+          }
+      }
+      wave_sync();
+    }
+    // Gv = W x G per 32-cell row tile, one atomic row per non-empty cell
+    for (int m = 0; m < nmt; ++m) {
+      const float* wr = sW + (32 * m + r) * kWP + 8 * hh;
+      const float4 w0 = *reinterpret_cast<const float4*>(wr);
+      const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      bf16x8_t ahi, alo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const short hb = bf16_bits(wv[j]);
+        ahi[j] = hb;
+        alo[j] = bf16_bits(wv[j] - bf16_bits_to_f32((unsigned short)hb));
+      }
+      f32x16_t acc;
+      zero16(acc);
+      acc = mfma16(ahi, bq, acc);
+      acc = mfma16(alo, bq, acc);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = 32 * m + crow(i, hh);
+        if (c < ncell && sHit[c]) {
+          const int y = oy + c / BX, x = ox + c % BX;
+          atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + r, acc[i]);
+        }
+      }
+    }
+    // clipped corners: one 128-B atomic row each
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      unsigned long long msk = __ballot(out[k]);
+      while (msk) {
+        const int src = __ffsll((long long)msk) - 1;
+        msk &= msk - 1;
+        const int y = __shfl(cy[k], src, 64), x = __shfl(cx[k], src, 64), qq = __shfl(tq, src, 64);
+        const float w = __shfl(cw[k], src, 64);
+        if (lane < kD)
+          atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + lane,
+                    w * bf16_bits_to_f32((unsigned short)sg[qq * kD + lane]));
+      }
+    }
+    wave_sync();                              // W / hit flags are rewritten by the next level
+  }
+}
+
+// The same product per 8 x 8 query tile (default for bf16): a 4-wave workgroup, thread =
+// tap (query tid / 4, point tid % 4), ONE box per level for the 64 queries, so the cells
+// that neighbouring 4 x 4 tiles would each flush are added once (grad_value is bound by
+// the float-atomic rate: ~1.1 TB/s of added bytes on gfx950).  W[cell][64 queries] is
+// built band by band (kBandCap cells; bands with no corner are skipped), each wave writes
+// its 16 queries' columns with the points taking turns, and the row tiles of the band's
+// product ([32 cells] x K = 64 queries, 4 K-steps x hi/lo) are spread over the waves.
+constexpr int kBandCap = 128;
+constexpr int kWP8 = 68;       // W row pitch (floats): 64 queries + 4
+
+template <int TX, int TY>
+__global__ void __launch_bounds__(256) msda_bwd_mfma_wg_kernel(const float* __restrict__ loc,
+                                                               const float* __restrict__ attw,
+                                                               const bf16* __restrict__ gout,
+                                                               float* __restrict__ gvalue, Levels lv, QueryTiles qt,
+                                                               int S, int Hh, int Q, int L, int nblk) {
+  constexpr int P = 4;
+  constexpr int NQ = TX * TY;
+  static_assert(NQ == 64, "64 queries x 4 points = one tap per thread");
+  __shared__ __attribute__((aligned(16))) short sg[NQ * kD];
+  __shared__ __attribute__((aligned(16))) float sW[kBandCap * kWP8];
+  __shared__ int sHit[kBandCap];
+  __shared__ int sBox[4][4];
+  const int blk = xcd_swizzle(blockIdx.x, nblk);
+  const int h = blk % Hh;
+  const int tile = (blk / Hh) % qt.per_image;
+  const int b = blk / Hh / qt.per_image;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int LP = L * P;
+  const int tq = tid >> 2, tpt = tid & 3;
+  const int qid = btile_query<TX, TY>(qt, lv, L, tile, tq, Q);
+  const long long grp = ((long long)b * Q + (qid < 0 ? 0 : qid)) * Hh + h;
+  float2 pxy[kMaxLevels];
+  float paw[kMaxLevels];
+#pragma unroll
+  for (int l = 0; l < kMaxLevels; ++l) {
+    pxy[l] = make_float2(0.f, 0.f);
+    paw[l] = 0.f;
+    if (l < L && qid >= 0) {
+      pxy[l] = *reinterpret_cast<const float2*>(loc + (grp * LP + l * P + tpt) * 2);
+      paw[l] = attw[grp * LP + l * P + tpt];
+    }
+  }
+  {  // grad_out rows: thread = (query, 8-channel part)
+    const int part = tid & 3;
+    bf16x8_t v = zero8();
+    if (qid >= 0) v = ld8(gout + (((long long)b * Q + qid) * Hh + h) * kD + part * 8);
+    *reinterpret_cast<bf16x8_t*>(sg + tq * kD + part * 8) = v;
+  }
+  __syncthreads();
+  bf16x8_t bq[4];                             // B operand per K-step: k = query 16 ks + 8 hh + j
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bq[ks][j] = sg[(16 * ks + 8 * hh + j) * kD + r];
+  const size_t rowstride = (size_t)Hh * kD;
+  const size_t vbase = ((size_t)b * S * Hh + h) * kD;
+  for (int l = 0; l < L; ++l) {
+    const int Hl = lv.h[l], Wl = lv.w[l];
+    const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
+    float2 xy = pxy[0];
+    float aw = paw[0];
+#pragma unroll
+    for (int k = 1; k < kMaxLevels; ++k)
+      if (l == k) {
+        xy = pxy[k];
+        aw = paw[k];
+      }
+    const Tap t = tap_geom(xy.x, xy.y, Hl, Wl);
+    const bool tv = qid >= 0 && t.inside;
+    int cy[4], cx[4];
+    float cw[4];
+    bool ok[4];
+    int ylo = 1 << 30, xlo = 1 << 30, yhi = -1, xhi = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      cy[k] = t.h0 + (k >> 1);
+      cx[k] = t.w0 + (k & 1);
+      ok[k] = tv && cy[k] >= 0 && cy[k] < Hl && cx[k] >= 0 && cx[k] < Wl;
+      cw[k] = ((k >> 1) ? t.lh : t.hh) * ((k & 1) ? t.lw : t.hw) * aw;
+      if (ok[k]) {
+        ylo = min(ylo, cy[k]);
+        yhi = max(yhi, cy[k]);
+        xlo = min(xlo, cx[k]);
+        xhi = max(xhi, cx[k]);
+      }
+    }
+    {
+      const int a = wave_min(ylo), bb = wave_max(yhi), c = wave_min(xlo), d = wave_max(xhi);
+      if (lane == 0) {
+        sBox[wave][0] = a;
+        sBox[wave][1] = bb;
+        sBox[wave][2] = c;
+        sBox[wave][3] = d;
+      }
+    }
+    __syncthreads();
+    int oy = sBox[0][0], yh = sBox[0][1], ox = sBox[0][2], xh = sBox[0][3];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      oy = min(oy, sBox[w][0]);
+      yh = max(yh, sBox[w][1]);
+      ox = min(ox, sBox[w][2]);
+      xh = max(xh, sBox[w][3]);
+    }
+    __syncthreads();                          // sBox is rewritten by the next level
+    if (yh < 0) continue;                     // no corner of the tile on this level (uniform)
+    const int BY = yh - oy + 1, BX = xh - ox + 1;
+    const int SBX = min(BX, kBandCap), SBY = kBandCap / SBX;
+    for (int by0 = 0; by0 < BY; by0 += SBY) {
+      for (int bx0 = 0; bx0 < BX; bx0 += SBX) {
+        const int bw = min(SBX, BX - bx0), bh = min(SBY, BY - by0);
+        int cell[4];
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int yy = cy[k] - oy - by0, xx = cx[k] - ox - bx0;
+          const bool in = ok[k] && (unsigned)yy < (unsigned)bh && (unsigned)xx < (unsigned)bw;
+          cell[k] = in ? yy * bw + xx : -1;
+          any |= in;
+        }
+        if (!__syncthreads_or(any)) continue;   // empty band (also the barrier after the last one)
+        const int ncell = bw * bh, nmt = (ncell + 31) >> 5;
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = tid; i < nmt * 32 * (kWP8 / 4); i += 256) reinterpret_cast<float4*>(sW)[i] = z4;
+        for (int i = tid; i < nmt * 32; i += 256) sHit[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int pt = 0; pt < P; ++pt) {      // a query's 4 points are lanes of one wave: take turns
+          if (tpt == pt) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (cell[k] >= 0) {
+                sW[cell[k] * kWP8 + tq] += cw[k];
+                sHit[cell[k]] = 1;
+              }
+          }
+          wave_sync();
+        }
+        __syncthreads();
+        for (int m = wave; m < nmt; m += 4) {
+          f32x16_t acc;
+          zero16(acc);
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            const float* wr = sW + (32 * m + r) * kWP8 + 16 * ks + 8 * hh;
+            const float4 w0 = *reinterpret_cast<const float4*>(wr);
+            const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
+            const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+            bf16x8_t ahi, alo;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const short hb = bf16_bits(wv[j]);
+              ahi[j] = hb;
+              alo[j] = bf16_bits(wv[j] - bf16_bits_to_f32((unsigned short)hb));
+            }
+            acc = mfma16(ahi, bq[ks], acc);
+            acc = mfma16(alo, bq[ks], acc);
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int c = 32 * m + crow(i, hh);
+            if (c < ncell && sHit[c]) {
+              const int y = oy + by0 + c / bw, x = ox + bx0 + c % bw;
+              atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + r, acc[i]);
+            }
+          }
+        }
+        __syncthreads();                      // W / hit flags are rewritten by the next band
+      }
+    }
+  }
+}
+
 int fill_levels(Levels* lv, const int64_t* shapes, const int64_t* starts, int L, int S) {
   long long tot = 0;
   for (int l = 0; l < L; ++l) {
@@ -1035,8 +1379,12 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     if (const char* e = getenv("VS_MSDA_WIN_DBG")) dbg = atoi(e);
     if (!(dbg & 16)) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
     if (dbg & 32) return VS_OK;
-    int te = 4;                            // VS_MSDA_TILE: query tile edge, 4 (default) or 8
-    if (const char* e = getenv("VS_MSDA_TILE")) te = atoi(e) == 8 ? 8 : 4;
+    // bf16: the MFMA product kernel (VS_MSDA_MFMA: 2 = 8 x 8 query tiles per 4-wave
+    // workgroup (default), 1 = 4 x 4 tiles per wave, 0 = the binned kernel); f32: binned
+    int mfk = dtype == VS_BF16 ? 2 : 0;
+    if (const char* e = getenv("VS_MSDA_MFMA")) mfk = dtype == VS_BF16 ? atoi(e) : 0;
+    int te = mfk == 2 ? 8 : 4;             // VS_MSDA_TILE: binned kernel's query tile edge, 4 or 8
+    if (const char* e = getenv("VS_MSDA_TILE")) te = mfk == 2 ? 8 : (atoi(e) == 8 ? 8 : 4);
     QueryTiles bt;
     bt.mode = Q == S ? 1 : 0;              // grid tiles when the queries are the value grid
     bt.prefix[0] = 0;
@@ -1048,6 +1396,18 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     bt.per_image = bt.mode == 1 ? bt.prefix[L] : (Q + te * te - 1) / (te * te);
     const long long nb2 = (long long)B * bt.per_image * Hh;
     VS_CHECK(nb2 < (1LL << 31), "too many query tiles");
+    if (mfk == 2) {
+      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
+                         (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2);
+      VS_LAUNCH_CHECK();
+      return VS_OK;
+    }
+    if (mfk == 1 && te == 4) {
+      hipLaunchKernelGGL((msda_bwd_mfma_kernel<4, 4>), dim3((unsigned)nb2), dim3(64), 0, st, loc, attw,
+                         (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2);
+      VS_LAUNCH_CHECK();
+      return VS_OK;
+    }
 #define VS_BINNED(TT, E)                                                                                     \
   hipLaunchKernelGGL((msda_bwd_binned_kernel<TT, E, E>), dim3((unsigned)nb2), dim3(64), 0, st, loc, attw,     \
                      (const TT*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, dbg)

@@ -112,27 +112,36 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ 
   }
 }
 
-// dx, plus per-workgroup partial dw / db rows (f32) in part[blockIdx][2][C]
+// dx, plus per-workgroup partial dw / db rows (f32) in part[blockIdx][NR][C]
 // ADD: dx += dres (the gradient reaching the LayerNorm input through the residual path),
 // accumulated in f32 and rounded once.
-template <typename T, int K, bool ADD = false>
+// CS: a third partial row, the column sums of dx as stored (rounded to T): the bias
+// gradient of the Linear whose output fed the LayerNorm input (a Swin block's attention
+// projection / MLP fc2, an encoder layer's output projection / fc2), so that Linear's
+// backward reads no dY for it (visionseg.linear, ops.AddLayerNormFunction).
+template <typename T, int K, bool ADD = false, bool CS = false>
 __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const T* __restrict__ w, const float* __restrict__ mean,
                                                           const float* __restrict__ rstd, T* __restrict__ dx,
                                                           float* __restrict__ part, int M, int C, int G,
                                                           const T* __restrict__ dres = nullptr) {
-  extern __shared__ float red[];             // [4 waves][2][C]
+  extern __shared__ float red[];             // [4 waves][NR][C]
+  constexpr int NR = CS ? 3 : 2;
   const int nch = C >> 3;
   const int lane = threadIdx.x & (G - 1);
   const int grp = threadIdx.x / G;
   const int rows_per_block = kThreads / G;
   const float invC = 1.f / (float)C;
-  float dw[K][8], db[K][8], wv[K][8];
+  float dw[K][8], db[K][8], wv[K][8], ds[CS ? K : 1][8];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int j = lane + k * G;
 #pragma unroll
     for (int i = 0; i < 8; ++i) dw[k][i] = db[k][i] = wv[k][i] = 0.f;   // masked chunks must hold 0, not garbage
+    if constexpr (CS) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ds[k][i] = 0.f;
+    }
     if (j < nch) load_chunk(w + j * 8, wv[k]);
   }
   // U rows per iteration, all loads issued before the math (memory-level parallelism)
@@ -193,6 +202,10 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
               for (int i = 0; i < 8; ++i) o[i] += rv[i];
             }
             store_chunk(dx + row * C + j * 8, o);
+            if constexpr (CS) {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) ds[k][i] += to_f32(from_f32<T>(o[i]));
+            }
           }
         }
       }
@@ -207,11 +220,12 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
       for (int i = 0; i < 8; ++i) {
         dw[k][i] += __shfl_xor(dw[k][i], o, 64);
         db[k][i] += __shfl_xor(db[k][i], o, 64);
+        if constexpr (CS) ds[k][i] += __shfl_xor(ds[k][i], o, 64);
       }
   }
   const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) < G) {
-    float* mine = red + (size_t)wave * 2 * C;
+    float* mine = red + (size_t)wave * NR * C;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int j = lane + k * G;
@@ -220,14 +234,15 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
         for (int i = 0; i < 8; ++i) {
           mine[j * 8 + i] = dw[k][i];
           mine[C + j * 8 + i] = db[k][i];
+          if constexpr (CS) mine[2 * C + j * 8 + i] = ds[k][i];
         }
       }
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * C; c += kThreads) {
-    const float acc = (red[c] + red[2 * C + c]) + (red[4 * C + c] + red[6 * C + c]);
-    part[(size_t)blockIdx.x * 2 * C + c] = acc;
+  for (int c = threadIdx.x; c < NR * C; c += kThreads) {
+    const float acc = (red[c] + red[NR * C + c]) + (red[2 * NR * C + c] + red[3 * NR * C + c]);
+    part[(size_t)blockIdx.x * NR * C + c] = acc;
   }
 }
 
@@ -274,11 +289,12 @@ __global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ 
 }
 
 // out[c] = sum_b part[b][c] (b < nb) in a fixed order; columns [0, split) go to out0,
-// [split, N) to out1.  A block = 32 columns x 8 row slices, 4 independent accumulators
-// per thread (memory-level parallelism), slices combined in LDS.
+// [split, split2) to out1, [split2, N) to out2.  A block = 32 columns x 8 row slices, 4
+// independent accumulators per thread (memory-level parallelism), slices combined in LDS.
 template <typename T>
 __global__ void __launch_bounds__(kThreads) colsum_partials_kernel(const float* __restrict__ part, T* __restrict__ out0,
-                                                                   T* __restrict__ out1, int nb, int N, int split) {
+                                                                   T* __restrict__ out1, int nb, int N, int split,
+                                                                   T* __restrict__ out2 = nullptr, int split2 = 1 << 30) {
   __shared__ float red[8][33];
   const int lane = threadIdx.x & 31;
   const int sl = threadIdx.x >> 5;
@@ -301,7 +317,8 @@ __global__ void __launch_bounds__(kThreads) colsum_partials_kernel(const float* 
 #pragma unroll
     for (int i = 0; i < 8; ++i) t += red[i][lane];
     if (col < split) out0[col] = from_f32<T>(t);
-    else out1[col - split] = from_f32<T>(t);
+    else if (col < split2) out1[col - split] = from_f32<T>(t);
+    else out2[col - split2] = from_f32<T>(t);
   }
 }
 
@@ -426,29 +443,35 @@ extern "C" int vs_add_layer_norm_forward(int dtype, const void* x, const void* r
 }
 
 extern "C" long long vs_layer_norm_backward_workspace_bytes(int M, int C) {
-  return (long long)kMaxPartials * 2 * C * sizeof(float);
+  return (long long)kMaxPartials * 3 * C * sizeof(float);     // dw, db (+ dx column sums)
 }
 
 static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, const void* w, const float* mean,
-                                    const float* rstd, const void* dres, void* dx, void* dw, void* db, void* ws, int M,
-                                    int C, void* stream);
+                                    const float* rstd, const void* dres, void* dx, void* dw, void* db, void* dsum,
+                                    void* ws, int M, int C, void* stream);
 
 extern "C" int vs_layer_norm_backward(int dtype, const void* dy, const void* x, const void* w, const float* mean,
                                       const float* rstd, void* dx, void* dw, void* db, void* ws, int M, int C,
                                       void* stream) {
-  return layer_norm_backward_impl(dtype, dy, x, w, mean, rstd, nullptr, dx, dw, db, ws, M, C, stream);
+  return layer_norm_backward_impl(dtype, dy, x, w, mean, rstd, nullptr, dx, dw, db, nullptr, ws, M, C, stream);
 }
 
 extern "C" int vs_layer_norm_backward_add(int dtype, const void* dy, const void* x, const void* w, const float* mean,
                                           const float* rstd, const void* dres, void* dx, void* dw, void* db, void* ws,
                                           int M, int C, void* stream) {
   VS_CHECK(M == 0 || dres, "null pointer");
-  return layer_norm_backward_impl(dtype, dy, x, w, mean, rstd, dres, dx, dw, db, ws, M, C, stream);
+  return layer_norm_backward_impl(dtype, dy, x, w, mean, rstd, dres, dx, dw, db, nullptr, ws, M, C, stream);
+}
+
+extern "C" int vs_layer_norm_backward_ex(int dtype, const void* dy, const void* x, const void* w, const float* mean,
+                                         const float* rstd, const void* dres, void* dx, void* dw, void* db,
+                                         void* dx_colsum, void* ws, int M, int C, void* stream) {
+  return layer_norm_backward_impl(dtype, dy, x, w, mean, rstd, dres, dx, dw, db, dx_colsum, ws, M, C, stream);
 }
 
 static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, const void* w, const float* mean,
-                                    const float* rstd, const void* dres, void* dx, void* dw, void* db, void* ws, int M,
-                                    int C, void* stream) {
+                                    const float* rstd, const void* dres, void* dx, void* dw, void* db, void* dsum,
+                                    void* ws, int M, int C, void* stream) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && dw && db && ws && (M == 0 || (dy && x && mean && rstd && dx)), "null pointer");
@@ -457,32 +480,35 @@ static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, co
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   const int grid = blocks_for(M, kThreads / G, kMaxPartials);
-  const size_t lds = (size_t)(kThreads / 64) * 2 * C * sizeof(float);
+  const int NR = dsum ? 3 : 2;
+  const size_t lds = (size_t)(kThreads / 64) * NR * C * sizeof(float);
   VS_CHECK(lds <= 64 * 1024, "LayerNorm backward LDS budget exceeded");
-#define VS_LNB(KK)                                                                                            \
-  if (dtype == VS_BF16 && dres)                                                                               \
-    hipLaunchKernelGGL((ln_bwd_kernel<bf16, KK, true>), dim3(grid), dim3(kThreads), lds, st, (const bf16*)dy, \
-                       (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, C, G, (const bf16*)dres); \
-  else if (dtype == VS_BF16)                                                                                  \
-    hipLaunchKernelGGL((ln_bwd_kernel<bf16, KK>), dim3(grid), dim3(kThreads), lds, st, (const bf16*)dy,       \
-                       (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx, part, M, C, G, nullptr);        \
-  else if (dres)                                                                                              \
-    hipLaunchKernelGGL((ln_bwd_kernel<float, KK, true>), dim3(grid), dim3(kThreads), lds, st,                 \
-                       (const float*)dy, (const float*)x, (const float*)w, mean, rstd, (float*)dx, part, M, C, \
-                       G, (const float*)dres);                                                                \
-  else                                                                                                        \
-    hipLaunchKernelGGL((ln_bwd_kernel<float, KK>), dim3(grid), dim3(kThreads), lds, st, (const float*)dy,     \
-                       (const float*)x, (const float*)w, mean, rstd, (float*)dx, part, M, C, G, nullptr)
+#define VS_LNB_T(TT, KK, AD, CS_)                                                                            \
+  hipLaunchKernelGGL((ln_bwd_kernel<TT, KK, AD, CS_>), dim3(grid), dim3(kThreads), lds, st, (const TT*)dy,    \
+                     (const TT*)x, (const TT*)w, mean, rstd, (TT*)dx, part, M, C, G, (const TT*)dres)
+#define VS_LNB_D(TT, KK)                                        \
+  if (dres && dsum) VS_LNB_T(TT, KK, true, true);               \
+  else if (dres) VS_LNB_T(TT, KK, true, false);                 \
+  else if (dsum) VS_LNB_T(TT, KK, false, true);                 \
+  else VS_LNB_T(TT, KK, false, false)
+#define VS_LNB(KK)                   \
+  if (dtype == VS_BF16) {            \
+    VS_LNB_D(bf16, KK);              \
+  } else {                           \
+    VS_LNB_D(float, KK);             \
+  }
   VS_LN_K(K, VS_LNB)
 #undef VS_LNB
-  // dw = column sums of the partial rows' first halves, db of the second halves
-  const int rgrid = (2 * C + 31) / 32;
+#undef VS_LNB_D
+#undef VS_LNB_T
+  // dw / db (/ dx column sums) = column sums of the partial rows' thirds
+  const int rgrid = (NR * C + 31) / 32;
   if (dtype == VS_BF16)
     hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3(rgrid), dim3(kThreads), 0, st, part, (bf16*)dw, (bf16*)db,
-                       grid, 2 * C, C);
+                       grid, NR * C, C, (bf16*)dsum, 2 * C);
   else
     hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3(rgrid), dim3(kThreads), 0, st, part, (float*)dw,
-                       (float*)db, grid, 2 * C, C);
+                       (float*)db, grid, NR * C, C, (float*)dsum, 2 * C);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

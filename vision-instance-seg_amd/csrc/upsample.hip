@@ -150,6 +150,74 @@ __global__ void __launch_bounds__(256) upsample_bwd_kernel(const T* __restrict__
   }
 }
 
+// Backward for the exact 2x case (H = 2 Hs, W = 2 Ws: the 1024^2 pixel decoder), separable:
+// block = (32 channels, 4 source rows, 32 source columns, image).  Pass 1 (vertical): a
+// thread takes (channel, source row, 8 output columns) and reads the <= 4 output rows
+// whose taps reach the source row as 16-B vectors (NCHW rows are contiguous along x),
+// weighting them by the row adjoint; the 8 column sums go to LDS.  Pass 2 (horizontal):
+// (source column, channel) per thread, the <= 4 output columns' sums weighted by the
+// column adjoint, written token-major (channel runs contiguous).  Weights come from the
+// forward's source-index rule (up_index), boundaries included.  ~1.2x the bytes of dL/dout
+// read (halo columns), none re-read from HBM.
+constexpr int kR2 = 4, kC2 = 32, kX2 = 80;   // source rows / columns per block, staged output columns
+
+__device__ __forceinline__ float adj_w(int y, int s, int in, int out) {
+  int i0, i1;
+  float l0, l1;
+  up_index(y, in, out, i0, i1, l0, l1);
+  return (i0 == s ? l0 : 0.f) + (i1 == s ? l1 : 0.f);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) upsample_bwd2x_kernel(const T* __restrict__ dout, T* __restrict__ dsrc, int C,
+                                                             int H, int W, int Hs, int Ws) {
+  __shared__ float sV[kCB][kR2][kX2 + 1];
+  const int sx0 = blockIdx.x * kC2, sy0 = blockIdx.y * kR2;
+  const int cb = blockIdx.z % (C / kCB), b = blockIdx.z / (C / kCB);
+  const int c0 = cb * kCB;
+  const int xbase = 2 * sx0 - 8;             // first staged output column (16-B aligned: W % 8 == 0)
+  // pass 1: items (c, r, chunk of 8 columns) = 32 x 4 x 10
+  for (int it = threadIdx.x; it < kCB * kR2 * (kX2 / 8); it += 256) {
+    const int ch = it % (kX2 / 8), r = (it / (kX2 / 8)) % kR2, c = it / ((kX2 / 8) * kR2);
+    const int sy = sy0 + r, x = xbase + 8 * ch;
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    if (sy < Hs && x >= 0 && x < W) {
+      const T* plane = dout + ((size_t)b * C + c0 + c) * H * W;
+#pragma unroll
+      for (int dy = -1; dy <= 2; ++dy) {
+        const int y = 2 * sy + dy;
+        if (y < 0 || y >= H) continue;
+        const float w = adj_w(y, sy, Hs, H);
+        if (w == 0.f) continue;
+        float v[8];
+        Vec16<T>::load(plane + (size_t)y * W + x, v);
+        if (Vec16<T>::N == 4) Vec16<T>::load(plane + (size_t)y * W + x + 4, v + 4);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += w * v[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sV[c][r][8 * ch + k] = acc[k];
+  }
+  __syncthreads();
+  // pass 2: items (r, source column, channel) = 4 x 32 x 32, channel fastest
+  for (int it = threadIdx.x; it < kR2 * kC2 * kCB; it += 256) {
+    const int c = it % kCB, sxi = (it / kCB) % kC2, r = it / (kCB * kC2);
+    const int sy = sy0 + r, sx = sx0 + sxi;
+    if (sy >= Hs || sx >= Ws) continue;
+    float acc = 0.f;
+#pragma unroll
+    for (int dx = -1; dx <= 2; ++dx) {
+      const int x = 2 * sx + dx;
+      if (x < 0 || x >= W) continue;
+      acc += adj_w(x, sx, Ws, W) * sV[c][r][x - xbase];
+    }
+    dsrc[((size_t)b * Hs * Ws + (size_t)sy * Ws + sx) * C + c0 + c] = from_f32<T>(acc);
+  }
+}
+
 }  // namespace
 }  // namespace vs
 
@@ -179,8 +247,19 @@ extern "C" int vs_upsample_backward(int dtype, const void* grad_out, void* grad_
   VS_CHECK(B > 0 && C > 0 && C % kCB == 0 && H > 0 && W > 0 && Hs > 0 && Ws > 0, "bad sizes (C % 32 == 0)");
   VS_CHECK(Hs <= H && Ws <= W && 2 * Hs >= H && 2 * Ws >= W, "upsampling factor must lie in [1, 2]");
   VS_CHECK(grad_out && grad_src, "null pointer");
-  dim3 grid((Ws + 31) / 32, Hs, B * (C / kCB));
   hipStream_t st = (hipStream_t)stream;
+  if (H == 2 * Hs && W == 2 * Ws && W % 8 == 0) {
+    dim3 g2((Ws + kC2 - 1) / kC2, (Hs + kR2 - 1) / kR2, B * (C / kCB));
+    if (dtype == VS_BF16)
+      hipLaunchKernelGGL(upsample_bwd2x_kernel<bf16>, g2, dim3(256), 0, st, (const bf16*)grad_out, (bf16*)grad_src,
+                         C, H, W, Hs, Ws);
+    else
+      hipLaunchKernelGGL(upsample_bwd2x_kernel<float>, g2, dim3(256), 0, st, (const float*)grad_out,
+                         (float*)grad_src, C, H, W, Hs, Ws);
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
+  dim3 grid((Ws + 31) / 32, Hs, B * (C / kCB));
   if (dtype == VS_BF16)
     hipLaunchKernelGGL(upsample_bwd_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)grad_out, (bf16*)grad_src, C,
                        H, W, Hs, Ws);

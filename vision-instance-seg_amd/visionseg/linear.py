@@ -69,7 +69,10 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gw = weight_grad(gy2, x.reshape(-1, x.shape[-1]).to(gy2.dtype), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            if gy2.shape[1] % 8 == 0 and gy2.shape[1] <= 2048:
+            cs = ops.take_colsum(gy)
+            if cs is not None:                                     # from the LayerNorm backward's pass
+                gb = cs.to(weight.dtype)
+            elif gy2.shape[1] % 8 == 0 and gy2.shape[1] <= 2048:
                 gb = ops.column_sum(gy2).to(weight.dtype)          # HIP column sum, f32 accumulation
             else:
                 gb = gy2.sum(0, dtype=torch.float32).to(weight.dtype)

@@ -537,6 +537,22 @@ class LayerNormFunction(torch.autograd.Function):
         return gx, gw, gb, None
 
 
+def attach_colsum(g: torch.Tensor, colsum: torch.Tensor) -> None:
+    """Record the column sums over the leading dims of gradient `g` (computed by the kernel
+    that produced g) so a consumer needing them -- the bias gradient of the Linear whose
+    output received g -- skips a second read of g.  Keyed to g's version counter: an
+    in-place update of g afterwards (e.g. autograd accumulating into it) invalidates it."""
+    g._vs_colsum = (colsum, g._version)
+
+
+def take_colsum(g: torch.Tensor):
+    """The column sums recorded by attach_colsum if still valid for g, else None."""
+    rec = getattr(g, "_vs_colsum", None)
+    if rec is None or rec[1] != g._version or rec[0].shape[0] != g.shape[-1]:
+        return None
+    return rec[0]
+
+
 class AddLayerNormFunction(torch.autograd.Function):
     """(s, y) = (x + r, layer_norm(x + r)) in one pass (csrc/norm.hip, RES variant); the
     backward adds the gradient of s (residual path) inside the LayerNorm backward."""
@@ -571,17 +587,18 @@ class AddLayerNormFunction(torch.autograd.Function):
         gb = torch.empty_like(weight)
         ws = torch.empty(int(L.lib().vs_layer_norm_backward_workspace_bytes(M, C)), device=s.device,
                          dtype=torch.uint8)
+        # the column sums of gx come out of the same pass (C <= 1024: LDS budget); they are
+        # the bias gradient of the Linear that produced r (see attach_colsum)
+        cs = torch.empty(C, device=s.device, dtype=s.dtype) if C <= 1024 else None
         with timed("layer_norm_bwd", s, bytes_=(3 + (gs is not None)) * s.numel() * s.element_size()):
-            if gs is None:
-                L.check(L.lib().vs_layer_norm_backward(L.dtype_code(s), L.ptr(gy), L.ptr(s), L.ptr(weight),
-                                                       L.ptr(mean), L.ptr(rstd), L.ptr(gx), L.ptr(gw), L.ptr(gb),
-                                                       L.ptr(ws), M, C, L.stream(s)), "layer_norm_backward")
-            else:
-                gsc = gs.to(s.dtype).contiguous()
-                L.check(L.lib().vs_layer_norm_backward_add(L.dtype_code(s), L.ptr(gy), L.ptr(s), L.ptr(weight),
-                                                           L.ptr(mean), L.ptr(rstd), L.ptr(gsc), L.ptr(gx),
-                                                           L.ptr(gw), L.ptr(gb), L.ptr(ws), M, C, L.stream(s)),
-                        "layer_norm_backward_add")
+            gsc = gs.to(s.dtype).contiguous() if gs is not None else None
+            L.check(L.lib().vs_layer_norm_backward_ex(L.dtype_code(s), L.ptr(gy), L.ptr(s), L.ptr(weight),
+                                                      L.ptr(mean), L.ptr(rstd), L.ptr(gsc) if gsc is not None else None,
+                                                      L.ptr(gx), L.ptr(gw), L.ptr(gb),
+                                                      L.ptr(cs) if cs is not None else None, L.ptr(ws), M, C,
+                                                      L.stream(s)), "layer_norm_backward_ex")
+        if cs is not None:
+            attach_colsum(gx, cs)
         return gx, gx, gw, gb, None
 
 
