@@ -200,15 +200,19 @@ def test_bf16_training_step():
     print("bf16 losses", losses)
 
 
-def test_train_template_seam_and_inference_seam(tmp_path):
-    """train_template.train_maskdino(...) contract (metrics dict, results, checkpoint) and
-    the ai_segmentation init_detector / inference_detector contract on the trained model."""
-    from visionseg.adapters import train_maskdino
+@pytest.mark.parametrize("arch", ["maskdino", "mask2former"])
+def test_train_template_seam_and_inference_seam(tmp_path, arch):
+    """train_template.train_maskdino(...) contract (metrics dict, results, checkpoint; the
+    MaskDINO model) and the `--model mask2former` branch, through the prefetching loader
+    (2 worker processes), and the ai_segmentation init_detector / inference_detector
+    contract on the trained model (MaskDINO recognised from its checkpoint)."""
+    from visionseg import adapters
     from visionseg.data import write_coco_dataset
     from visionseg.inference import init_detector, inference_detector
+    train_maskdino = adapters.train_maskdino if arch == "maskdino" else adapters.train_mask2former
     write_coco_dataset(str(tmp_path / "train"), 4, 128, seed=1)
     write_coco_dataset(str(tmp_path / "val"), 2, 128, seed=2)
-    hp = dict(epochs=2, batch_size=2, img_size=128, save_period=1, warmup_epochs=0)
+    hp = dict(epochs=2, batch_size=2, img_size=128, save_period=1, warmup_epochs=0, workers=2)
     r = train_maskdino("exp_test", tmp_path / "train", tmp_path / "val", tmp_path / "out", hp)
     assert set(r) == {"mAP50", "mAP75", "mAP", "precision", "recall"}
     assert all(0.0 <= v <= 1.0 for v in r.values())

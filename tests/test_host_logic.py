@@ -234,3 +234,35 @@ def test_rle_annotations(tmp_path):
     ds = CocoInstanceDataset(str(tmp_path), train=False, keep_size=True)
     _, masks, classes = ds[0]
     assert any(np.array_equal(x.numpy(), big) for x in masks)
+
+
+def test_prefetch_loader_matches_serial_batches(tmp_path):
+    """visionseg.data.PrefetchLoader (2 worker processes, host collate + device-side
+    normalisation) yields the serial loop's batches: same per-epoch seeded permutation,
+    rank slots, padding and normalisation as collate_padded (no random augmentation here:
+    train=False), across an epoch boundary and for rank 1 of 2."""
+    from visionseg.data import PrefetchLoader
+    write_coco_dataset(str(tmp_path), 7, 96, seed=1)
+    ds = CocoInstanceDataset(str(tmp_path), train=False, fixed_size=96)
+    for rank, world in ((0, 1), (1, 2)):
+        per_rank, iters = 2, 5
+        ld = PrefetchLoader(ds, per_rank, iters, rank=rank, world=world, seed=5, num_workers=2, device="cpu")
+        rng = np.random.default_rng(5)
+        epoch_iters = -(-len(ds) // (per_rank * world))
+        got = list(ld)
+        assert len(got) == iters
+        k = 0
+        while k < iters:
+            order = rng.permutation(len(ds))
+            for j in range(epoch_iters):
+                if k >= iters:
+                    break
+                a = (j * world + rank) * per_rank
+                idx = order[a:a + per_rank]
+                if len(idx) == 0:
+                    idx = order[:per_rank]
+                ei, em, ec = collate_padded([ds[int(i)] for i in idx])
+                gi, gm, gc = got[k]
+                assert torch.allclose(gi, ei) and all(torch.equal(x, y) for x, y in zip(gm, em))
+                assert all(torch.equal(x, y) for x, y in zip(gc, ec))
+                k += 1

@@ -4,11 +4,14 @@ The reference dispatches `--model` to `train_<model>(exp_name, train_dir, test_d
 output_dir, hyperparams) -> dict` (training/train_template.py:104, 197-205) and writes
 the returned metrics (`mAP50, mAP75, mAP, precision, recall`, :139-145) plus
 exp_name / model_type / hyperparams to `output_dir/results.json` (:207-214).  Its
-MaskDINO slot is a stub returning zeros (:104-145).  `train_mask2former` is a working
-implementation of that contract on the MI355X path (Swin + Mask2Former, COCO json in
-`train_dir/annotations.json`, evaluation on `test_dir`); `train_maskdino` is the same
-function under the reference's name (the MaskDINO decoder itself is the next row of the
-plan).  Missing annotations -> None, as the caller expects (:188-194).
+MaskDINO slot is a stub returning zeros (:104-145).  `train_maskdino` implements that
+contract on the MI355X path with the MaskDINO decoder (visionseg.maskdino: Swin backbone,
+4-level deformable encoder, two-stage query selection, denoising queries, box
+refinement; parity unpinned), `train_mask2former` with Mask2Former (the
+`--model mask2former` branch); both read the COCO json in `train_dir/annotations.json`
+through the prefetching loader (visionseg.data.PrefetchLoader: worker processes, pinned
+host batches, H2D one batch ahead on a side stream) and evaluate mask AP on `test_dir`.
+Missing annotations -> None, as the caller expects (:188-194).
 
 Multi-GPU: run the caller under torchrun; images are sharded by rank, gradients are
 all-reduced by the Trainer (RCCL), rank 0 writes checkpoints and evaluates.
@@ -24,7 +27,7 @@ import torch
 import torch.distributed as dist
 
 from .criterion import SetCriterion
-from .data import CocoInstanceDataset, collate_padded
+from .data import CocoInstanceDataset, PrefetchLoader
 from .evaluate import MaskAPEvaluator
 from .inference import Predictor
 from .model import M2FConfig, Mask2Former
@@ -56,7 +59,7 @@ def evaluate_dir(model: Mask2Former, test_dir, img_size: int = 640, device="cuda
 
 
 def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, backbone: str = "swin_t",
-                      device=None, max_iters: int | None = None):
+                      device=None, max_iters: int | None = None, arch: str = "mask2former"):
     hp = dict(HYPERPARAMS)
     hp.update(hyperparams or {})
     train_dir, output_dir = Path(train_dir), Path(output_dir)
@@ -71,8 +74,16 @@ def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, ba
     img = int(hp["img_size"])
     ds = CocoInstanceDataset(str(train_dir), min_size=(img,), max_size=int(round(img * 1.25)), train=True,
                              seed=seed + rank)
-    cfg = M2FConfig.preset(backbone, num_labels=max(1, len(ds.cat_to_label)))
-    model = Mask2Former(cfg).init_weights(seed)
+    backbone = str(hp.get("backbone", backbone))
+    if arch == "maskdino":
+        from .maskdino import MaskDINO, MaskDINOConfig, MaskDINOCriterion
+        cfg = MaskDINOConfig.preset(backbone, num_labels=max(1, len(ds.cat_to_label)))
+        model = MaskDINO(cfg).init_weights(seed)
+        criterion = MaskDINOCriterion(cfg)
+    else:
+        cfg = M2FConfig.preset(backbone, num_labels=max(1, len(ds.cat_to_label)))
+        model = Mask2Former(cfg).init_weights(seed)
+        criterion = SetCriterion(cfg)
     bs = int(hp["batch_size"])
     per_rank = max(1, bs // world)
     iters_per_epoch = max(1, math.ceil(len(ds) / (per_rank * world)))
@@ -86,25 +97,17 @@ def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, ba
                           amp=device.type == "cuda")
     # HIP-graph replay of the step for every batch signature seen more than twice (image
     # size after ResizeShortestEdge + padding, padded target capacity)
-    trainer = Trainer(model, SetCriterion(cfg), solver, device=device, graphs=device.type == "cuda")
+    trainer = Trainer(model, criterion, solver, device=device, graphs=device.type == "cuda")
     output_dir.mkdir(parents=True, exist_ok=True)
-    rng = np.random.default_rng(seed)
-    it = 0
-    for epoch in range(int(hp["epochs"])):
-        order = rng.permutation(len(ds))
-        for k in range(iters_per_epoch):
-            if it >= total:
-                break
-            idx = order[(k * world + rank) * per_rank:(k * world + rank + 1) * per_rank]
-            if len(idx) == 0:
-                idx = order[:per_rank]
-            images, masks, classes = collate_padded([ds[int(i)] for i in idx], device=device)
-            trainer.step(images, masks, classes)
-            it += 1
-        if hp.get("save_period") and (epoch + 1) % int(hp["save_period"]) == 0:
-            trainer.save(str(output_dir / f"model_epoch{epoch + 1:04d}.pth"))
-        if it >= total:
-            break
+    # the serial loop's batches (per-epoch seeded permutation, rank r takes its slots of
+    # each global batch), mapped in worker processes and prefetched to the device
+    loader = PrefetchLoader(ds, per_rank, total, rank=rank, world=world, seed=seed,
+                            num_workers=int(hp.get("workers", 4)), device=device)
+    save_every = int(hp.get("save_period") or 0) * iters_per_epoch
+    for it, (images, masks, classes) in enumerate(loader, start=1):
+        trainer.step(images, masks, classes)
+        if save_every and it % save_every == 0:
+            trainer.save(str(output_dir / f"model_epoch{it // iters_per_epoch:04d}.pth"))
     trainer.save(str(output_dir / "model_final.pth"))
     metrics = {"mAP50": 0.0, "mAP75": 0.0, "mAP": 0.0, "precision": 0.0, "recall": 0.0}
     if rank == 0 and device.type == "cuda":
@@ -116,5 +119,8 @@ def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, ba
     return metrics
 
 
-# the reference's seam name (train_template.py:104)
-train_maskdino = train_mask2former
+def train_maskdino(exp_name, train_dir, test_dir, output_dir, hyperparams, backbone: str = "swin_t", device=None,
+                   max_iters: int | None = None):
+    """The reference's seam (train_template.py:104): MaskDINO on the MI355X path."""
+    return train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, backbone=backbone, device=device,
+                             max_iters=max_iters, arch="maskdino")

@@ -228,3 +228,132 @@ def collate_padded(samples, size_divisibility: int = 32, device="cpu"):
         masks.append(mm.to(device))
         classes.append(c.to(device))
     return imgs, masks, classes
+
+
+# ----------------------------------------------------------------------------------
+# Loader: worker processes + pinned host batches + H2D on a side stream, one batch ahead
+# ----------------------------------------------------------------------------------
+
+
+def collate_host(samples, size_divisibility: int = 32):
+    """CPU half of collate_padded, run inside the loader workers: uint8 images padded to a
+    common size divisible by 32 [B,3,H,W], the (unpadded) image sizes, masks padded to the
+    same size (bool [K,H,W] per image), classes.  Normalisation happens on the device."""
+    H = max(s[0].shape[1] for s in samples)
+    W = max(s[0].shape[2] for s in samples)
+    H = (H + size_divisibility - 1) // size_divisibility * size_divisibility
+    W = (W + size_divisibility - 1) // size_divisibility * size_divisibility
+    imgs = torch.zeros(len(samples), 3, H, W, dtype=torch.uint8)
+    sizes = torch.zeros(len(samples), 2, dtype=torch.int64)
+    masks, classes = [], []
+    for i, (im, m, c) in enumerate(samples):
+        imgs[i, :, :im.shape[1], :im.shape[2]] = im
+        sizes[i, 0], sizes[i, 1] = im.shape[1], im.shape[2]
+        mm = torch.zeros(m.shape[0], H, W, dtype=torch.bool)
+        mm[:, :m.shape[1], :m.shape[2]] = m
+        masks.append(mm)
+        classes.append(c)
+    return imgs, sizes, masks, classes
+
+
+def normalize_padded(imgs_u8: torch.Tensor, sizes: torch.Tensor) -> torch.Tensor:
+    """Device half of collate_padded: normalise, then zero the padding (detectron2 pads the
+    normalised image with 0; collate_padded does the same)."""
+    out = normalize(imgs_u8)
+    H, W = out.shape[-2:]
+    rows = torch.arange(H, device=out.device).view(1, H, 1)
+    cols = torch.arange(W, device=out.device).view(1, 1, W)
+    s = sizes.to(out.device)
+    keep = (rows < s[:, 0].view(-1, 1, 1)) & (cols < s[:, 1].view(-1, 1, 1))
+    return out * keep[:, None].to(out.dtype)
+
+
+class _EpochSampler(torch.utils.data.Sampler):
+    """Batches of this rank's share of a seeded permutation per epoch (the serial loop of
+    adapters.train_mask2former: rank r takes slots r, r + world, ... of each global batch)."""
+
+    def __init__(self, n, per_rank, rank, world, seed, iters):
+        self.n, self.per_rank, self.rank, self.world, self.seed, self.iters = n, per_rank, rank, world, seed, iters
+
+    def __iter__(self):
+        rng = np.random.default_rng(self.seed)
+        it, epoch_iters = 0, max(1, -(-self.n // (self.per_rank * self.world)))
+        while it < self.iters:
+            order = rng.permutation(self.n)
+            for k in range(epoch_iters):
+                if it >= self.iters:
+                    return
+                a = (k * self.world + self.rank) * self.per_rank
+                idx = order[a:a + self.per_rank]
+                if len(idx) == 0:
+                    idx = order[:self.per_rank]
+                yield [int(i) for i in idx]
+                it += 1
+
+    def __len__(self):
+        return self.iters
+
+
+def _seed_worker(worker_id):
+    info = torch.utils.data.get_worker_info()
+    ds = info.dataset
+    if hasattr(ds, "rng"):      # independent augmentation streams per worker
+        ds.rng = np.random.default_rng(int(info.seed % (2 ** 32)))
+
+
+class PrefetchLoader:
+    """The data path of the training seam at speed (the reference runs the
+    detectron2 mapper in loader workers, train_full.py:50-67, 116-143): `num_workers`
+    processes decode / resize / flip / rasterise (CocoInstanceDataset) and collate padded
+    uint8 batches into pinned host memory; the iterator copies batch i+1 to the device on a
+    side stream (non-blocking) while the caller trains on batch i, and normalises on the
+    device.  Yields (images f32 [B,3,H,W], masks [bool [K,H,W]], classes [int64 [K]]) on
+    `device`, like collate_padded."""
+
+    def __init__(self, dataset, per_rank: int, iters: int, rank: int = 0, world: int = 1, seed: int = 42,
+                 num_workers: int = 4, device="cuda", prefetch_factor: int = 2):
+        self.device = torch.device(device)
+        pin = self.device.type == "cuda"
+        sampler = _EpochSampler(len(dataset), per_rank, rank, world, seed, iters)
+        kw = dict(num_workers=num_workers, collate_fn=collate_host, pin_memory=pin, batch_sampler=sampler)
+        if num_workers > 0:
+            kw.update(worker_init_fn=_seed_worker, prefetch_factor=prefetch_factor, persistent_workers=False)
+        self.loader = torch.utils.data.DataLoader(dataset, **kw)
+        self.stream = torch.cuda.Stream(self.device) if pin else None
+
+    def __len__(self):
+        return len(self.loader)
+
+    def _to_device(self, batch):
+        imgs, sizes, masks, classes = batch
+        if self.stream is None:
+            return normalize_padded(imgs, sizes), masks, classes, None
+        with torch.cuda.stream(self.stream):
+            imgs = imgs.to(self.device, non_blocking=True)
+            sizes = sizes.to(self.device, non_blocking=True)
+            masks = [m.to(self.device, non_blocking=True) for m in masks]
+            classes = [c.to(self.device, non_blocking=True) for c in classes]
+            imgs = normalize_padded(imgs, sizes)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return imgs, masks, classes, ev
+
+    def __iter__(self):
+        it = iter(self.loader)
+        nxt = None
+        try:
+            nxt = self._to_device(next(it))
+        except StopIteration:
+            return
+        while nxt is not None:
+            cur = nxt
+            try:
+                nxt = self._to_device(next(it))       # H2D of the next batch overlaps this step
+            except StopIteration:
+                nxt = None
+            imgs, masks, classes, ev = cur
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                for t in [imgs, *masks, *classes]:
+                    t.record_stream(torch.cuda.current_stream(self.device))
+            yield imgs, masks, classes

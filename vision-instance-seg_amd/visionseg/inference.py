@@ -43,7 +43,8 @@ class DetResult:
 
 
 @torch.no_grad()
-def instance_inference(mask_logits, class_logits, out_hw, valid_hw=None, pad_hw=None, top_k: int | None = None):
+def instance_inference(mask_logits, class_logits, out_hw, valid_hw=None, pad_hw=None, top_k: int | None = None,
+                       sigmoid_classes: bool = False):
     """mask_logits [Q,h,w], class_logits [Q,K+1] -> (scores [k], labels [k], masks bool [k,H,W]).
 
     Scores and binary masks as HF:m2f-proc:695-709 (softmax over classes without the
@@ -51,10 +52,17 @@ def instance_inference(mask_logits, class_logits, out_hw, valid_hw=None, pad_hw=
     foreground probability inside the mask); pinned by tests/golden/postproc.npz.
     Resizing as upstream sem_seg_postprocess (detectron2): with `pad_hw` / `valid_hw`
     the logits are first upsampled to the padded input size, cropped to the valid
-    (un-padded) region, then resized to `out_hw` -- bilinear, align_corners=False."""
+    (un-padded) region, then resized to `out_hw` -- bilinear, align_corners=False.
+    sigmoid_classes: MaskDINO's scoring (focal-loss classes, no no-object column: class
+    scores = sigmoid(logits) over all K columns; upstream MaskDINO instance_inference, not
+    in the container -- parity unpinned), the rest as above."""
     Q, K1 = class_logits.shape
-    K = K1 - 1
-    scores = F.softmax(class_logits.float(), -1)[:, :-1]
+    if sigmoid_classes:
+        K = K1
+        scores = class_logits.float().sigmoid()
+    else:
+        K = K1 - 1
+        scores = F.softmax(class_logits.float(), -1)[:, :-1]
     labels = torch.arange(K, device=scores.device).unsqueeze(0).repeat(Q, 1).flatten(0, 1)
     k = top_k or Q
     sc, idx = scores.flatten(0, 1).topk(min(k, Q * K), sorted=False)
@@ -75,7 +83,8 @@ def instance_inference(mask_logits, class_logits, out_hw, valid_hw=None, pad_hw=
 
 
 class Predictor:
-    """Swin + Mask2Former predictor on the MI355X kernels (eval mode, bf16 autocast)."""
+    """Swin + Mask2Former (or MaskDINO) predictor on the MI355X kernels (eval mode, bf16
+    autocast)."""
 
     def __init__(self, model: Mask2Former, device="cuda:0", min_size: int = 640, max_size: int = 800,
                  amp: bool = True, top_k: int = 100):
@@ -102,11 +111,14 @@ class Predictor:
     def __call__(self, image_bgr: np.ndarray) -> DetResult:
         x, valid, orig = self._preprocess(image_bgr)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.amp and self.device.type == "cuda"):
-            masks, classes = self.model(x)
-        m, c = masks[-1][0], classes[-1][0]
+            out = self.model(x)
+        if isinstance(out, dict):            # MaskDINO: per-step lists in a dict, sigmoid class scores
+            m, c, sig = out["masks"][-1][0], out["classes"][-1][0], True
+        else:
+            m, c, sig = out[0][-1][0], out[1][-1][0], False
         # stride-4 logits -> padded input size -> crop the valid region -> original size
         scores, labels, binm = instance_inference(m, c, orig, valid_hw=valid, pad_hw=tuple(x.shape[-2:]),
-                                                  top_k=self.top_k)
+                                                  top_k=self.top_k, sigmoid_classes=sig)
         return DetResult(InstanceData(scores=scores, masks=binm, labels=labels))
 
 
@@ -124,18 +136,32 @@ def load_checkpoint(path: str, device="cpu") -> dict:
 
 def init_detector(config, checkpoint: str | None = None, device: str = "cuda:0") -> Predictor:
     """mmdet.apis.init_detector-compatible entry (ai_segmentation.py:41-50).
-    `config`: an M2FConfig, a preset name ("swin_t", "swin_b", ...), or a JSON file."""
-    if isinstance(config, M2FConfig):
-        cfg = config
-    elif isinstance(config, str) and os.path.exists(config):
-        with open(config) as f:
-            d = json.load(f)
-        cfg = M2FConfig.preset(d.pop("preset")) if "preset" in d and len(d) == 1 else M2FConfig.from_dict(d)
+    `config`: an M2FConfig, a preset name ("swin_t", "swin_b", ...; "maskdino_swin_t" ...
+    for MaskDINO), or a JSON file.  A MaskDINO checkpoint (train_maskdino's) is recognised
+    by its keys and served by the MaskDINO model with the preset's backbone."""
+    sd = load_checkpoint(checkpoint) if checkpoint else None
+    name = config if isinstance(config, str) and not os.path.exists(config) else None
+    maskdino = bool(name and name.startswith("maskdino")) or bool(
+        sd is not None and any(k.startswith("decoder.enc_output.") for k in sd))
+    if maskdino:
+        from .maskdino import MaskDINO, MaskDINOConfig
+        preset = (name or "swin_t").replace("maskdino_", "") or "swin_t"
+        kw = {}
+        if sd is not None and "decoder.class_embed.weight" in sd:
+            kw["num_labels"] = int(sd["decoder.class_embed.weight"].shape[0])
+        model = MaskDINO(MaskDINOConfig.preset(preset, **kw))
     else:
-        cfg = M2FConfig.preset(config or "swin_t")
-    model = Mask2Former(cfg)
-    if checkpoint:
-        model.load_state_dict(load_checkpoint(checkpoint))
+        if isinstance(config, M2FConfig):
+            cfg = config
+        elif isinstance(config, str) and os.path.exists(config):
+            with open(config) as f:
+                d = json.load(f)
+            cfg = M2FConfig.preset(d.pop("preset")) if "preset" in d and len(d) == 1 else M2FConfig.from_dict(d)
+        else:
+            cfg = M2FConfig.preset(config or "swin_t")
+        model = Mask2Former(cfg)
+    if sd is not None:
+        model.load_state_dict(sd)
     else:
         model.init_weights()
     return Predictor(model, device=device)
