@@ -40,7 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="msda,mask,win,xattn")
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--msda-modes", default="window,carry16,tiled")
+    ap.add_argument("--msda-modes", default="mfma,binned,tiled")
     a = ap.parse_args()
     dev = "cuda"
     bf = torch.bfloat16
@@ -68,19 +68,17 @@ def main():
             locr, wr = loc.clone().requires_grad_(True), w.clone().requires_grad_(True)
             for mode in a.msda_modes.split(","):
                 ops._MSDA_BWD = "tiled" if mode == "tiled" else "carry"
-                os.environ["VS_MSDA_RUN"] = {"carry16": "16", "window": "16", "window8": "16"}.get(mode, "0")
-                os.environ["VS_MSDA_WIN"] = "1" if mode.startswith("window") else "0"
-                os.environ["VS_MSDA_TILE"] = "8" if mode == "window8" else "4"
-                os.environ["VS_MSDA_MFMA"] = {"mfma8": "2", "mfma4": "1"}.get(mode, "0")
-                if mode.startswith("mfma"):
-                    os.environ["VS_MSDA_RUN"], os.environ["VS_MSDA_WIN"] = "16", "1"
+                # mfma: the default split backward; binned: its f32-path grad_value kernel on
+                # bf16 data; fused: the single kernel; tiled: the deterministic variant
+                os.environ["VS_MSDA_RUN"] = "0" if mode == "fused" else "16"
+                os.environ["VS_MSDA_MFMA"] = "0" if mode == "binned" else "1"
 
                 def fb():
                     o = ops.ms_deform_attn(v, shapes, locr, wr)
                     o.backward(go)
                 run(f"msda {oname} {mode}", fb, a.iters)
             os.environ.pop("VS_MSDA_RUN")
-            os.environ.pop("VS_MSDA_WIN")
+            os.environ.pop("VS_MSDA_MFMA")
     if "mask" in a.only:
         Q, C, Hm = 100, 256, 256
         E = torch.randn(B, Q, C, device=dev, generator=g).to(bf).requires_grad_(True)

@@ -11,14 +11,17 @@
 // rows (96 B / 48 B, 16-B aligned) are read as float4.  Accumulation in f32.
 //
 // Backward: grad_loc / grad_attn from a gather kernel (msda_bwd_geom_kernel); grad_value
-// (f32, then cast) by a scatter with f32 global atomics (~1.3 TB/s of added bytes,
-// MI355X_MICROARCH §Global float atomics):
-//   * default (P == 4, enough queries): the binned query-tile kernel
-//     (msda_bwd_binned_kernel; grid tiles of 4 x 4 queries when the queries are the
-//     value grid -- the pixel-decoder encoder --, else runs of 16 queries): counting
-//     sort of the tile's corners by cell, register sums, one atomic row per cell;
-//   * VS_MSDA_WIN=0: the register-carry scatter (msda_bwd_scatter_kernel);
-//   * small problems / other P: one fused kernel (msda_bwd_kernel, an atomic per corner).
+// (f32, then cast) by f32 global atomics, bound by their rate (~1.1 TB/s of added bytes
+// on gfx950, MI355X_MICROARCH §Global float atomics), so the kernels cut the added bytes:
+//   * bf16, P == 4, enough queries (default): msda_bwd_mfma_wg_kernel -- per 8 x 8 query
+//     tile (runs of 64 queries when the queries are not the value grid) and level,
+//     grad_value over the tile's box of cells as one MFMA product W[cell][query] x
+//     grad_out[query][c], one atomic row per touched cell;
+//   * f32 (parity mode): msda_bwd_binned_kernel -- 4 x 4 tiles, the tile's corners
+//     counting-sorted by cell, register sums in exact f32, one atomic row per cell
+//     (also bf16 with VS_MSDA_MFMA=0, for A/B and the cross-check test);
+//   * small problems / other P (VS_MSDA_RUN=0 forces it): one fused kernel
+//     (msda_bwd_kernel, an atomic per corner).
 // vs_msda_backward_tiled is the deterministic, atomic-free variant (grad_value by
 // destination tile, written once in the value dtype; ops VS_MSDA_BWD=tiled).
 #include "common.h"
@@ -201,31 +204,9 @@ __global__ void __launch_bounds__(256) msda_bwd_kernel(
   }
 }
 
-// Backward, default path: two kernels.
-//
-// (1) msda_bwd_geom_kernel — grad_attn / grad_loc.  Gather-only, laid out like the
-//     forward (a lane owns a 16-B channel slice, 4 (bf16) / 8 (f32) lanes per (b,q,head)),
-//     partial dot products reduced over the group's lanes with shuffles.
-//
-// (2) msda_bwd_scatter_kernel — grad_value, with a register carry.  A half-wave (32
-//     lanes = the 32 channels of one head) walks a run of R consecutive queries of one
-//     (image, head).  For every tap (level l, point p) it holds the 2x2 block of corners
-//     it touched last: 4 per-lane f32 sums and the block's top-left cell.  When the next
-//     query's tap lands on a block overlapping the held one (cell offset dx, dy in
-//     {-1,0,1}), the shared corners stay in registers and only the corners leaving the
-//     block are added to HBM (f32 atomics); a disjoint block flushes all four.  Same sum
-//     as one atomic per corner, in a different order.
-//
-// Why: grad_value is bound by the chip's float-atomic rate (~1.3 TB/s of added bytes,
-// MI355X_MICROARCH §Global float atomics): 4 corners x 32 ch x 4 B per tap, 4.2 GB per
-// pixel-decoder layer at 4x1024^2.  In the encoder, consecutive queries are horizontally
-// adjacent pixels whose (smoothly varying) sampling points move by 1 cell on their own
-// level and 1/2, 1/4 cell on coarser ones, so about half the corner adds are shared with
-// the previous query (tools/kbench.py "smooth").  Loads and no-return atomics retire in
-// order through one counter (vmcnt), so a load issued after an atomic waits for it: the
-// scatter kernel therefore stages its run's loc / attn / grad_out in LDS first and its
-// query loop issues nothing but LDS reads and atomics.  Unrelated queries (a decoder)
-// degrade to one add per corner.
+// msda_bwd_geom_kernel — grad_attn / grad_loc of the split backward.  Gather-only, laid
+// out like the forward (a lane owns a 16-B channel slice, 4 (bf16) / 8 (f32) lanes per
+// (b, q, head)), partial dot products reduced over the group's lanes with shuffles.
 template <typename T>
 __global__ void __launch_bounds__(256) msda_bwd_geom_kernel(
     const T* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attw,
@@ -311,101 +292,7 @@ __global__ void __launch_bounds__(256) msda_bwd_geom_kernel(
   }
 }
 
-constexpr int kScatterRun = 16;        // queries per half-wave run (LDS staging is sized for it)
-
-template <typename T, int L, int P>
-__global__ void __launch_bounds__(256) msda_bwd_scatter_kernel(
-    const float* __restrict__ loc, const float* __restrict__ attw, const T* __restrict__ gout,
-    float* __restrict__ gvalue, Levels lv, int S, int Hh, int Q, int R, int nrun, long long halfwaves) {
-  constexpr int LP = L * P;
-  // per half-wave staging: loc [R][LP][2], attn [R][LP], grad_out [R][32] (f32)
-  constexpr int kStage = kScatterRun * (LP * 3 + kD);
-  __shared__ float stage[8][kStage];
-  const int hwl = threadIdx.x >> 5;           // half-wave within the workgroup
-  const long long hw_id = (long long)blockIdx.x * 8 + hwl;
-  const int c = threadIdx.x & 31;
-  if (hw_id >= halfwaves) return;             // uniform per half-wave; no block-wide barrier below
-  const int h = (int)(hw_id % Hh);
-  const long long br = hw_id / Hh;
-  const int run = (int)(br % nrun);
-  const long long b = br / nrun;
-  const int q0 = run * R;
-  const int nq = min(Q, q0 + R) - q0;
-  float* sl = stage[hwl];
-  float* sw = sl + kScatterRun * LP * 2;
-  float* sg = sw + kScatterRun * LP;
-  for (int i = 0; i < nq; ++i) {
-    const long long grp = ((long long)b * Q + q0 + i) * Hh + h;
-    if (c < LP * 2) sl[i * LP * 2 + c] = loc[grp * LP * 2 + c];
-    if (c < LP) sw[i * LP + c] = attw[grp * LP + c];
-    sg[i * kD + c] = to_f32(gout[grp * kD + c]);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-  const size_t rowstride = (size_t)Hh * kD;
-  const size_t vbase = ((size_t)b * S * Hh + h) * kD + c;
-  int ph[LP], pw[LP];                         // held block's top-left cell per tap
-  float acc[LP][4];                           // held corner sums: (0,0) (0,1) (1,0) (1,1)
-#pragma unroll
-  for (int t = 0; t < LP; ++t) {
-    ph[t] = -(1 << 28);
-    pw[t] = -(1 << 28);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc[t][k] = 0.f;
-  }
-  auto flush = [&](int t, int k, int Hl, int Wl, size_t lbase) {
-    const int y = ph[t] + (k >> 1), x = pw[t] + (k & 1);
-    if (y >= 0 && y < Hl && x >= 0 && x < Wl)
-      atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride, acc[t][k]);
-  };
-  for (int i = 0; i < nq; ++i) {
-    const float g = sg[i * kD + c];
-#pragma unroll
-    for (int l = 0; l < L; ++l) {
-      const int Hl = lv.h[l], Wl = lv.w[l];
-      const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const int t = l * P + p;
-        const Tap tg = tap_geom(sl[(i * LP + t) * 2 + 0], sl[(i * LP + t) * 2 + 1], Hl, Wl);
-        if (!tg.inside) continue;             // no contribution; the held block stays
-        const float ga = g * sw[i * LP + t];
-        const int dy = tg.h0 - ph[t], dx = tg.w0 - pw[t];
-        // held corner k = (cy, cx) survives iff (cy - dy, cx - dx) lies in the new block
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int ny = (k >> 1) - dy, nx = (k & 1) - dx;
-          if (!((unsigned)ny <= 1u && (unsigned)nx <= 1u)) flush(t, k, Hl, Wl, lbase);
-        }
-        float carried[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int sy = (k >> 1) + dy, sx = (k & 1) + dx;
-          const int s = sy * 2 + sx;
-          const bool in = (unsigned)sy <= 1u && (unsigned)sx <= 1u;
-          carried[k] = !in ? 0.f : s == 0 ? acc[t][0] : s == 1 ? acc[t][1] : s == 2 ? acc[t][2] : acc[t][3];
-        }
-        // corners outside the level get sums too but are never flushed
-        acc[t][0] = carried[0] + tg.hh * tg.hw * ga;
-        acc[t][1] = carried[1] + tg.hh * tg.lw * ga;
-        acc[t][2] = carried[2] + tg.lh * tg.hw * ga;
-        acc[t][3] = carried[3] + tg.lh * tg.lw * ga;
-        ph[t] = tg.h0;
-        pw[t] = tg.w0;
-      }
-    }
-  }
-#pragma unroll
-  for (int l = 0; l < L; ++l) {
-    const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) flush(l * P + p, k, lv.h[l], lv.w[l], lbase);
-  }
-}
+constexpr int kSplitMin = 16 * 8192;    // (b, q, head) groups from which the split backward pays
 
 // ---------------------------------------------------------------------------------
 // Exclusive prefix scan of per-tile counts (1024-entry blocks + a block prefix), used by
@@ -722,7 +609,7 @@ __global__ void __launch_bounds__(64) msda_bwd_binned_kernel(const float* __rest
                                                              const float* __restrict__ attw,
                                                              const T* __restrict__ gout, float* __restrict__ gvalue,
                                                              Levels lv, QueryTiles qt, int S, int Hh, int Q, int L,
-                                                             int nblk, int dbg) {
+                                                             int nblk) {
   constexpr int P = 4;
   constexpr int NQ = TX * TY;                 // queries per tile
   static_assert(NQ * P % 64 == 0 && NQ <= 64, "whole taps per lane");
@@ -878,7 +765,7 @@ __global__ void __launch_bounds__(64) msda_bwd_binned_kernel(const float* __rest
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // per non-empty cell: sum its records in registers (4 records in flight), one atomic
     // per channel
-    if (!(dbg & 1)) {
+    {
       for (int i = hp; i < nlist; i += 2) {
         const int e = cells[i];
         const int o = offs[e], n = cnt[e];
@@ -897,7 +784,7 @@ __global__ void __launch_bounds__(64) msda_bwd_binned_kernel(const float* __rest
           v0 = __fmaf_rn(__int_as_float(r.y), sg[r.x + ch], v0);
         }
         const int y = oy + e / BX, x = ox + e % BX;
-        if (!(dbg & 2)) atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + ch, v0 + v1);
+        atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + ch, v0 + v1);
       }
     }
     // clipped corners: one 128-B atomic row each
@@ -911,7 +798,7 @@ __global__ void __launch_bounds__(64) msda_bwd_binned_kernel(const float* __rest
           m &= m - 1;
           const int y = __shfl(cy[i][k], src, 64), x = __shfl(cx[i][k], src, 64), qq = __shfl(tq[i], src, 64);
           const float w = __shfl(cw[i][k], src, 64);
-          if (lane < kD && !(dbg & 8))
+          if (lane < kD)
             atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + lane, w * sg[qq * kD + lane]);
         }
       }
@@ -923,176 +810,20 @@ __global__ void __launch_bounds__(64) msda_bwd_binned_kernel(const float* __rest
 }
 
 // ---------------------------------------------------------------------------------
-// grad_value by query tiles as a dense MFMA product (default for bf16, P == 4): one wave
-// per (tile of 16 queries, image, head); lane = tap (query lane % 16, point lane / 16).
-// Per value level the tile's taps span a small box of cells; grad_value over the box is
+// grad_value by query tiles as a dense MFMA product (default for bf16, P == 4).
+// Per value level the taps of a tile of queries span a small box of cells; grad_value
+// over the box is
 //     Gv[cell][c] = sum_q W[cell][q] g[q][c],
 // W[cell][q] = sum over q's 4 points of the bilinear x attention weight of the corner at
-// the cell: a [box x 16] by [16 x 32] product, i.e. one v_mfma_f32_32x32x16_bf16 per 32
-// cells (x2: W in f32 is split into bf16 hi + lo parts, exact to ~2^-17; g is bf16
-// already), then one 128-B f32 atomic row per non-empty cell.  W is built in LDS by plain
-// read-modify-writes: the 4 points take turns, so the 16 lanes of a turn (16 distinct
-// queries = 16 distinct columns) never collide.  This replaces the counting sort and the
-// per-cell record walk of the binned kernel (msda_bwd_binned_kernel, still the f32 path):
-// no integer atomics, no scan, no record scatter.  Boxes over kWCap cells are clipped;
-// the corners outside go straight to grad_value (one 128-B atomic row each).
-constexpr int kWCap = 128;     // cells per box (4 MFMA row tiles)
-constexpr int kWP = 20;        // W row pitch (floats): 16 queries + 4 (2-way banks on the A reads)
-
-template <int TX, int TY>
-__global__ void __launch_bounds__(64) msda_bwd_mfma_kernel(const float* __restrict__ loc,
-                                                           const float* __restrict__ attw,
-                                                           const bf16* __restrict__ gout, float* __restrict__ gvalue,
-                                                           Levels lv, QueryTiles qt, int S, int Hh, int Q, int L,
-                                                           int nblk) {
-  constexpr int P = 4;
-  constexpr int NQ = TX * TY;
-  static_assert(NQ == 16, "16 queries x 4 points = one tap per lane");
-  __shared__ __attribute__((aligned(16))) short sg[NQ * kD];   // grad_out rows of the tile [q][c] (bf16)
-  __shared__ __attribute__((aligned(16))) float sW[kWCap * kWP];
-  __shared__ int sHit[kWCap];
-  const int blk = xcd_swizzle(blockIdx.x, nblk);
-  const int h = blk % Hh;
-  const int tile = (blk / Hh) % qt.per_image;
-  const int b = blk / Hh / qt.per_image;
-  const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
-  const int LP = L * P;
-  const int tq = lane % NQ, tpt = lane / NQ;
-  const int qid = btile_query<TX, TY>(qt, lv, L, tile, tq, Q);
-  const long long grp = ((long long)b * Q + (qid < 0 ? 0 : qid)) * Hh + h;
-  float2 pxy[kMaxLevels];
-  float paw[kMaxLevels];
-#pragma unroll
-  for (int l = 0; l < kMaxLevels; ++l) {
-    pxy[l] = make_float2(0.f, 0.f);
-    paw[l] = 0.f;
-    if (l < L && qid >= 0) {
-      pxy[l] = *reinterpret_cast<const float2*>(loc + (grp * LP + l * P + tpt) * 2);
-      paw[l] = attw[grp * LP + l * P + tpt];
-    }
-  }
-  {  // grad_out rows: lane = (query, 8-channel part); zero rows for queries outside the grid
-    const int rq = lane >> 2, part = lane & 3;
-    const int q = btile_query<TX, TY>(qt, lv, L, tile, rq, Q);
-    bf16x8_t v = zero8();
-    if (q >= 0) v = ld8(gout + (((long long)b * Q + q) * Hh + h) * kD + part * 8);
-    *reinterpret_cast<bf16x8_t*>(sg + rq * kD + part * 8) = v;
-  }
-  wave_sync();
-  // B operand (same for every level and row tile): k = query 8 hh + j, column = channel r
-  bf16x8_t bq;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bq[j] = sg[(8 * hh + j) * kD + r];
-  const size_t rowstride = (size_t)Hh * kD;
-  const size_t vbase = ((size_t)b * S * Hh + h) * kD;
-  for (int l = 0; l < L; ++l) {
-    const int Hl = lv.h[l], Wl = lv.w[l];
-    const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
-    float2 xy = pxy[0];
-    float aw = paw[0];
-#pragma unroll
-    for (int k = 1; k < kMaxLevels; ++k)
-      if (l == k) {
-        xy = pxy[k];
-        aw = paw[k];
-      }
-    const Tap t = tap_geom(xy.x, xy.y, Hl, Wl);
-    const bool tv = qid >= 0 && t.inside;
-    int cy[4], cx[4];
-    float cw[4];
-    bool ok[4];
-    int ylo = 1 << 30, xlo = 1 << 30, yhi = -1, xhi = -1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      cy[k] = t.h0 + (k >> 1);
-      cx[k] = t.w0 + (k & 1);
-      ok[k] = tv && cy[k] >= 0 && cy[k] < Hl && cx[k] >= 0 && cx[k] < Wl;
-      cw[k] = ((k >> 1) ? t.lh : t.hh) * ((k & 1) ? t.lw : t.hw) * aw;
-      if (ok[k]) {
-        ylo = min(ylo, cy[k]);
-        yhi = max(yhi, cy[k]);
-        xlo = min(xlo, cx[k]);
-        xhi = max(xhi, cx[k]);
-      }
-    }
-    if (__ballot(ok[0] || ok[1] || ok[2] || ok[3]) == 0ull) continue;
-    const int oy = wave_min(ylo), ox = wave_min(xlo);
-    const int BX = min(wave_max(xhi) - ox + 1, kWCap);
-    const int BY = min(wave_max(yhi) - oy + 1, kWCap / BX);
-    const int ncell = BX * BY;
-    const int nmt = (ncell + 31) >> 5;
-    // zero the box's W rows (the row tiles the MFMAs read) and hit flags
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = lane; i < nmt * 32 * (kWP / 4); i += 64) reinterpret_cast<float4*>(sW)[i] = z4;
-    for (int i = lane; i < nmt * 32; i += 64) sHit[i] = 0;
-    wave_sync();
-    int cell[4];
-    bool out[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool in = ok[k] && (unsigned)(cy[k] - oy) < (unsigned)BY && (unsigned)(cx[k] - ox) < (unsigned)BX;
-      out[k] = ok[k] && !in;
-      cell[k] = in ? (cy[k] - oy) * BX + (cx[k] - ox) : -1;
-    }
-    // W[cell][q] += weight; the points take turns (16 lanes, 16 distinct query columns)
-#pragma unroll
-    for (int pt = 0; pt < P; ++pt) {
-      if (tpt == pt) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (cell[k] >= 0) {
-            sW[cell[k] * kWP + tq] += cw[k];
-            sHit[cell[k]] = 1;
-          }
-      }
-      wave_sync();
-    }
-    // Gv = W x G per 32-cell row tile, one atomic row per non-empty cell
-    for (int m = 0; m < nmt; ++m) {
-      const float* wr = sW + (32 * m + r) * kWP + 8 * hh;
-      const float4 w0 = *reinterpret_cast<const float4*>(wr);
-      const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
-      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      bf16x8_t ahi, alo;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const short hb = bf16_bits(wv[j]);
-        ahi[j] = hb;
-        alo[j] = bf16_bits(wv[j] - bf16_bits_to_f32((unsigned short)hb));
-      }
-      f32x16_t acc;
-      zero16(acc);
-      acc = mfma16(ahi, bq, acc);
-      acc = mfma16(alo, bq, acc);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int c = 32 * m + crow(i, hh);
-        if (c < ncell && sHit[c]) {
-          const int y = oy + c / BX, x = ox + c % BX;
-          atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + r, acc[i]);
-        }
-      }
-    }
-    // clipped corners: one 128-B atomic row each
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      unsigned long long msk = __ballot(out[k]);
-      while (msk) {
-        const int src = __ffsll((long long)msk) - 1;
-        msk &= msk - 1;
-        const int y = __shfl(cy[k], src, 64), x = __shfl(cx[k], src, 64), qq = __shfl(tq, src, 64);
-        const float w = __shfl(cw[k], src, 64);
-        if (lane < kD)
-          atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + lane,
-                    w * bf16_bits_to_f32((unsigned short)sg[qq * kD + lane]));
-      }
-    }
-    wave_sync();                              // W / hit flags are rewritten by the next level
-  }
-}
-
-// The same product per 8 x 8 query tile (default for bf16): a 4-wave workgroup, thread =
-// tap (query tid / 4, point tid % 4), ONE box per level for the 64 queries, so the cells
+// the cell: a [box x queries] by [queries x 32] product on v_mfma_f32_32x32x16_bf16 (W in
+// f32 split into bf16 hi + lo parts, exact to ~2^-17; g is bf16 already), then one 128-B
+// f32 atomic row per non-empty cell.  W is built in LDS by plain read-modify-writes: a
+// query's 4 points take turns, so the lanes of a turn (distinct queries = distinct
+// columns) never collide -- no integer atomics, no sort (the binned kernel's counting
+// sort and per-cell record walk measured no faster at 4 x 4 tiles; the win is the tile
+// size: tools/kbench.py --only msda, 0.95 -> 0.67 ms per backward at C2).
+// msda_bwd_mfma_wg_kernel: 8 x 8 query tiles, a 4-wave workgroup, thread = tap (query
+// tid / 4, point tid % 4), ONE box per level for the 64 queries, so the cells
 // that neighbouring 4 x 4 tiles would each flush are added once (grad_value is bound by
 // the float-atomic rate: ~1.1 TB/s of added bytes on gfx950).  W[cell][64 queries] is
 // built band by band (kBandCap cells; bands with no corner are skipped), each wave writes
@@ -1325,30 +1056,6 @@ static void launch_geom(int dtype, const void* value, const float* loc, const fl
                        (const float*)gout, gloc, gattw, lv, S, Hh, Q, L, P, groups);
 }
 
-static void launch_scatter(int dtype, const float* loc, const float* attw, const void* gout, float* gvalue,
-                           const Levels& lv, int B, int S, int Hh, int Q, int L, int run, hipStream_t st) {
-  const int nrun = (Q + run - 1) / run;
-  const long long hws = (long long)B * nrun * Hh;
-  const int sgrid = (int)((hws + 7) / 8);
-#define VS_SCATTER(TT, LL)                                                                                   \
-  hipLaunchKernelGGL((msda_bwd_scatter_kernel<TT, LL, 4>), dim3(sgrid), dim3(256), 0, st, loc, attw,          \
-                     (const TT*)gout, gvalue, lv, S, Hh, Q, run, nrun, hws)
-#define VS_SCATTER_L(TT)                \
-  switch (L) {                          \
-    case 1: VS_SCATTER(TT, 1); break;   \
-    case 2: VS_SCATTER(TT, 2); break;   \
-    case 3: VS_SCATTER(TT, 3); break;   \
-    default: VS_SCATTER(TT, 4); break;  \
-  }
-  if (dtype == VS_BF16) {
-    VS_SCATTER_L(bf16)
-  } else {
-    VS_SCATTER_L(float)
-  }
-#undef VS_SCATTER_L
-#undef VS_SCATTER
-}
-
 static int msda_backward_impl(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
                               const float* loc, const float* attw, const void* gout, float* gvalue, float* gloc,
                               float* gattw, int B, int S, int Hh, int D, int L, int Q, int P, void* stream) {
@@ -1363,30 +1070,18 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   const long long groups = (long long)B * Q * Hh;
   VS_HIP(hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * Hh * kD, st));
   if (Q == 0) return VS_OK;
-  // geom + register-carry scatter when there are enough queries for runs to fill the chip
-  // (VS_MSDA_RUN=n forces runs of n <= kScatterRun queries at any size, 0 the single kernel)
-  int run = kScatterRun;
-  bool split = (long long)B * Q * Hh >= (long long)kScatterRun * 8192;
-  if (const char* e = getenv("VS_MSDA_RUN")) {
-    run = atoi(e);
-    split = run >= 1;
-  }
-  // binned query-tile kernel (VS_MSDA_WIN=0 selects the register-carry scatter)
-  bool win = split && P == 4;
-  if (const char* e = getenv("VS_MSDA_WIN")) win = win && atoi(e) != 0;
-  if (win) {
-    int dbg = 0;                           // VS_MSDA_WIN_DBG (profiling only; tools/msda_dbg.sh)
-    if (const char* e = getenv("VS_MSDA_WIN_DBG")) dbg = atoi(e);
-    if (!(dbg & 16)) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
-    if (dbg & 32) return VS_OK;
-    // bf16: the MFMA product kernel (VS_MSDA_MFMA: 2 = 8 x 8 query tiles per 4-wave
-    // workgroup (default), 1 = 4 x 4 tiles per wave, 0 = the binned kernel); f32: binned
-    int mfk = dtype == VS_BF16 ? 2 : 0;
-    if (const char* e = getenv("VS_MSDA_MFMA")) mfk = dtype == VS_BF16 ? atoi(e) : 0;
-    int te = mfk == 2 ? 8 : 4;             // VS_MSDA_TILE: binned kernel's query tile edge, 4 or 8
-    if (const char* e = getenv("VS_MSDA_TILE")) te = mfk == 2 ? 8 : (atoi(e) == 8 ? 8 : 4);
+  // split backward (geom gather + grad_value product / binned kernel) when there are enough
+  // queries to fill the chip; VS_MSDA_RUN=0 forces the single fused kernel
+  bool split = groups >= kSplitMin;
+  if (const char* e = getenv("VS_MSDA_RUN")) split = atoi(e) >= 1;   // tests: force either path
+  split = split && P == 4;
+  if (split) {
+    launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
+    bool mfma = dtype == VS_BF16;            // VS_MSDA_MFMA=0: the binned kernel for bf16 too
+    if (const char* e = getenv("VS_MSDA_MFMA")) mfma = mfma && atoi(e) != 0;
+    const int te = mfma ? 8 : 4;             // query tile edge
     QueryTiles bt;
-    bt.mode = Q == S ? 1 : 0;              // grid tiles when the queries are the value grid
+    bt.mode = Q == S ? 1 : 0;                // grid tiles when the queries are the value grid
     bt.prefix[0] = 0;
     for (int l = 0; l < kMaxLevels; ++l) {
       const bool on = bt.mode == 1 && l < L;
@@ -1396,34 +1091,15 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     bt.per_image = bt.mode == 1 ? bt.prefix[L] : (Q + te * te - 1) / (te * te);
     const long long nb2 = (long long)B * bt.per_image * Hh;
     VS_CHECK(nb2 < (1LL << 31), "too many query tiles");
-    if (mfk == 2) {
+    if (mfma)
       hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
                          (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2);
-      VS_LAUNCH_CHECK();
-      return VS_OK;
-    }
-    if (mfk == 1 && te == 4) {
-      hipLaunchKernelGGL((msda_bwd_mfma_kernel<4, 4>), dim3((unsigned)nb2), dim3(64), 0, st, loc, attw,
+    else if (dtype == VS_BF16)
+      hipLaunchKernelGGL((msda_bwd_binned_kernel<bf16, 4, 4>), dim3((unsigned)nb2), dim3(64), 0, st, loc, attw,
                          (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2);
-      VS_LAUNCH_CHECK();
-      return VS_OK;
-    }
-#define VS_BINNED(TT, E)                                                                                     \
-  hipLaunchKernelGGL((msda_bwd_binned_kernel<TT, E, E>), dim3((unsigned)nb2), dim3(64), 0, st, loc, attw,     \
-                     (const TT*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, dbg)
-    if (dtype == VS_BF16) {
-      if (te == 4) VS_BINNED(bf16, 4); else VS_BINNED(bf16, 8);
-    } else {
-      if (te == 4) VS_BINNED(float, 4); else VS_BINNED(float, 8);
-    }
-#undef VS_BINNED
-    VS_LAUNCH_CHECK();
-    return VS_OK;
-  }
-  if (split && P == 4) {
-    VS_CHECK(run <= kScatterRun, "VS_MSDA_RUN must not exceed the LDS-staged run (16)");
-    launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
-    launch_scatter(dtype, loc, attw, gout, gvalue, lv, B, S, Hh, Q, L, run, st);
+    else
+      hipLaunchKernelGGL((msda_bwd_binned_kernel<float, 4, 4>), dim3((unsigned)nb2), dim3(64), 0, st, loc, attw,
+                         (const float*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2);
     VS_LAUNCH_CHECK();
     return VS_OK;
   }

@@ -44,9 +44,9 @@ def _level_arrays(shapes):
     return sh, starts, s
 
 
-# MSDA backward variant (A/B switch, VS_MSDA_BWD): "carry" (default; f32 atomic scatter:
-# the binned query-tile kernel, or the register-carry kernel with VS_MSDA_WIN=0, then
-# a cast) or "tiled" (deterministic: grad_value by destination tiles with plain LDS
+# MSDA backward variant (A/B switch, VS_MSDA_BWD): "carry" (default; f32 atomics into
+# grad_value: the MFMA query-tile product for bf16, the binned query-tile kernel for f32,
+# then a cast) or "tiled" (deterministic: grad_value by destination tiles with plain LDS
 # read-modify-write, no float atomics, written once in the value dtype; pays for its
 # inverse index with integer atomics, ~30 G/s on gfx950: at 4x1024^2, tools/kbench.py
 # --only msda, smooth offsets, 4.4 ms against the binned kernel's 0.96 ms).
