@@ -32,21 +32,25 @@ def split_count(K: int, M: int, N: int) -> int:
     return max(1, min(s, K // MIN_CHUNK))
 
 
-def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype, out: torch.Tensor | None = None):
     """dW = gy^T x for gy [K, M], x [K, N] -> [M, N] (out_dtype), f32 accumulation: a
     batched GEMM over S token chunks with f32 outputs, then one HIP epilogue that sums
-    the chunks (+ the remainder rows' product) and rounds once (csrc/norm.hip)."""
+    the chunks (+ the remainder rows' product) and rounds once (csrc/norm.hip).
+    `out`: a contiguous [M, N] tensor of out_dtype to write into (e.g. a row block of a
+    fused parameter's gradient)."""
     K, M = gy.shape
     N = x.shape[1]
     S = split_count(K, M, N)
     if S <= 1 or (M * N) % 4 or out_dtype not in (torch.float32, torch.bfloat16):
-        return (gy.t() @ x).to(out_dtype)
+        g = (gy.t() @ x).to(out_dtype)
+        return g if out is None else out.copy_(g)
     chunk = K // S
     main = chunk * S
     part = torch.bmm(gy[:main].view(S, chunk, M).transpose(1, 2), x[:main].view(S, chunk, N),
                      out_dtype=torch.float32)
     extra = torch.mm(gy[main:].t(), x[main:], out_dtype=torch.float32) if main < K else None
-    out = torch.empty(M, N, device=gy.device, dtype=out_dtype)
+    if out is None:
+        out = torch.empty(M, N, device=gy.device, dtype=out_dtype)
     L.check(L.lib().vs_splitk_sum(L.dtype_code(out), L.ptr(part), S, M * N, L.ptr(extra) if extra is not None else None,
                                   L.ptr(out), L.stream(out)), "splitk_sum")
     return out
@@ -186,6 +190,61 @@ class _SmallLinearFn(torch.autograd.Function):
             if not ctx.needs_input_grad[1]:
                 gw = None
         return gx, gw, gb
+
+
+class _InProjFn(torch.autograd.Function):
+    """The cross-attention input projections of one decoder layer, q = xq W_q^T + b_q,
+    k = xk W_k^T + b_k, v = xv W_v^T + b_v, with W = [W_q; W_k; W_v] and b one parameter
+    each (nn.MultiheadAttention's in_proj_weight / in_proj_bias; HF:m2f:1644-1650).  The
+    backward writes the three row blocks of dW and db straight into one [3D, D] / [3D]
+    gradient each -- slicing the parameters in the forward made autograd zero-fill a
+    full-size gradient per slice and add the three (2 fills + 2 adds per parameter and
+    layer).  q: a few hundred tokens (dW, db by the one-launch small wgrad kernel); k, v:
+    the level memory (split-K dW, HIP column sums)."""
+
+    @staticmethod
+    def forward(ctx, xq, xk, xv, weight, bias):
+        D = weight.shape[1]
+        W = (weight[:D], weight[D:2 * D], weight[2 * D:])
+        B = (bias[:D], bias[D:2 * D], bias[2 * D:])
+        ctx.save_for_backward(xq, xk, xv, weight)
+        return tuple(F.linear(x, w, b) for x, w, b in zip((xq, xk, xv), W, B))
+
+    @staticmethod
+    def backward(ctx, gq, gk, gv):
+        xq, xk, xv, weight = ctx.saved_tensors
+        D = weight.shape[1]
+        gw = torch.empty_like(weight)
+        gb = torch.empty(3 * D, device=weight.device, dtype=weight.dtype)
+        gx = []
+        for i, (g, x) in enumerate(((gq, xq), (gk, xk), (gv, xv))):
+            g2 = g.reshape(-1, D).contiguous()
+            x2 = x.reshape(-1, D).contiguous()
+            w_i = weight[i * D:(i + 1) * D]
+            gx.append((g2 @ w_i).view(x.shape) if ctx.needs_input_grad[i] else None)
+            rows = slice(i * D, (i + 1) * D)
+            if i == 0 and _SMALL and g2.dtype == torch.bfloat16 and g2.shape[0] <= SMALL_MAX_TOKENS and D % 64 == 0:
+                L.check(L.lib().vs_small_linear_wgrad(L.dtype_code(gw), L.ptr(g2), L.ptr(x2), L.ptr(gw[rows]),
+                                                      L.ptr(gb[rows]), g2.shape[0], D, D, L.stream(g2)),
+                        "small_linear_wgrad")
+                continue
+            weight_grad(g2, x2.to(g2.dtype), weight.dtype, out=gw[rows])
+            if D % 8 == 0 and D <= 2048 and g2.dtype == weight.dtype:
+                ops.column_sum(g2, out=gb[rows])
+            else:
+                gb[rows].copy_(g2.sum(0, dtype=torch.float32))
+        return gx[0], gx[1], gx[2], gw, gb
+
+
+def in_projection(xq, xk, xv, weight, bias):
+    """(q, k, v) of nn.MultiheadAttention's packed in-projection (see _InProjFn); plain
+    slicing off the device / under autocast / without grad."""
+    D = weight.shape[1]
+    if (xq.is_cuda and torch.is_grad_enabled() and weight.requires_grad and not torch.is_autocast_enabled()
+            and xq.dtype == weight.dtype == xk.dtype == xv.dtype == bias.dtype):
+        return _InProjFn.apply(xq, xk, xv, weight, bias)
+    return (F.linear(xq, weight[:D], bias[:D]), F.linear(xk, weight[D:2 * D], bias[D:2 * D]),
+            F.linear(xv, weight[2 * D:], bias[2 * D:]))
 
 
 def small_linear(x, w, b=None):

@@ -28,7 +28,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .linear import SmallLinear, TokenLayerNorm, TokenLinear, linear_tokens, plane_projection, small_linear
+from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_tokens, plane_projection,
+                     small_linear)
 
 
 @dataclass
@@ -439,15 +440,13 @@ class DecoderLayer(nn.Module):
         """mem: level memory [B, hw, D] (contiguous), mem_pos = mem + its position embedding."""
         B, Q, D = h.shape
         H, d = self.heads, D // self.heads
-        W, b = self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias
-        q = small_linear(h + qpos, W[:D], b[:D])
-        k = linear_tokens(mem_pos, W[D:2 * D], b[D:2 * D])
-        v = linear_tokens(mem, W[2 * D:], b[2 * D:])
+        q, k, v = in_projection(h + qpos, mem_pos, mem, self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias)
         o = ops.masked_attention(q, k, v, words, H, d ** -0.5)
         _, h = self.norm_cross.add_forward(h, self.cross_attn.out_proj(o))       # post-norm, fused add
         sa = self.self_attn
-        qs = sa.q_proj(h + qpos).view(B, Q, H, d).transpose(1, 2)
-        ks = sa.k_proj(h + qpos).view(B, Q, H, d).transpose(1, 2)
+        hq = h + qpos                                                            # shared by q and k
+        qs = sa.q_proj(hq).view(B, Q, H, d).transpose(1, 2)
+        ks = sa.k_proj(hq).view(B, Q, H, d).transpose(1, 2)
         vs = sa.v_proj(h).view(B, Q, H, d).transpose(1, 2)
         att = F.scaled_dot_product_attention(qs, ks, vs)
         _, h = self.norm_self.add_forward(h, sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)))

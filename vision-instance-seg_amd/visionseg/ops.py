@@ -617,13 +617,16 @@ def layer_norm_supported(x, weight) -> bool:
             and C % 8 == 0 and C <= 2048)
 
 
-def column_sum(x2d):
+def column_sum(x2d, out=None):
     """x [M, N] -> [N] (x's dtype, f32 accumulation): the bias gradient of a token-major
-    Linear (csrc/norm.hip)."""
+    Linear (csrc/norm.hip).  `out`: a contiguous [N] tensor of x's dtype to write into."""
     L.require_hip(x2d)
     x2d = x2d.contiguous()
     M, N = x2d.shape
-    out = torch.empty(N, device=x2d.device, dtype=x2d.dtype)
+    if out is None:
+        out = torch.empty(N, device=x2d.device, dtype=x2d.dtype)
+    elif out.shape != (N,) or out.dtype != x2d.dtype or not out.is_contiguous():
+        raise ValueError("column_sum: out must be a contiguous [N] tensor of the input dtype")
     ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=x2d.device, dtype=torch.uint8)
     with timed("column_sum", x2d, bytes_=x2d.numel() * x2d.element_size()):
         L.check(L.lib().vs_column_sum(L.dtype_code(x2d), L.ptr(x2d), L.ptr(out), L.ptr(ws), M, N, L.stream(x2d)),
