@@ -354,19 +354,28 @@ __global__ void __launch_bounds__(kThreads) splitk_sum_kernel(const float* __res
   }
 }
 
-// pick (G, K): smallest K whose power-of-two group fits in 16 lanes, else 64 lanes
+// pick (G, K): a power-of-two group of G <= 16 lanes (else <= 64) with K chunks per lane,
+// fewest idle chunk slots G*K - nch first, then the smaller K (registers).  C = 96
+// (nch 12): G = 4, K = 3 -- no idle lanes -- where the smallest-K rule gave G = 16, K = 1
+// with a quarter of the lanes idle (Swin-T stage 1, the largest LayerNorm of the step).
 bool pick_gk(int nch, int kmax, int* G, int* K) {
-  static const int ks[] = {1, 2, 3, 4};
   for (int lim : {16, 64}) {
-    for (int k : ks) {
-      if (k > kmax) break;
+    int best_g = 0, best_k = 0, best_w = 1 << 30;
+    for (int k = 1; k <= kmax && k <= 4; ++k) {
       int g = 4;
       while (g * k < nch) g <<= 1;
-      if (g <= lim) {
-        *G = g;
-        *K = k;
-        return true;
+      if (g > lim) continue;
+      const int w = g * k - nch;
+      if (w < best_w) {
+        best_w = w;
+        best_g = g;
+        best_k = k;
       }
+    }
+    if (best_g) {
+      *G = best_g;
+      *K = best_k;
+      return true;
     }
   }
   return false;

@@ -247,6 +247,51 @@ def in_projection(xq, xk, xv, weight, bias):
             F.linear(xv, weight[2 * D:], bias[2 * D:]))
 
 
+class _ValueQueryProjFn(torch.autograd.Function):
+    """An encoder MSDeformAttn layer's two input projections of the same tokens h
+    (HF:m2f:919-1002): value = h Wv^T + bv and proj = (h + pos) Wp^T + bp (the fused
+    sampling-offset / attention-weight projection).  The backward forms dq = dproj Wp
+    once (it is both d pos and proj's share of d h) and dh = dq + dvalue Wv as ONE GEMM
+    with dq as its C operand (beta = 1): autograd would add the two shares with a
+    separate full-size kernel.  Weight gradients: split-K; bias gradients: HIP column sums."""
+
+    @staticmethod
+    def forward(ctx, h, pos, wv, bv, wp, bp):
+        q = h + pos
+        ctx.save_for_backward(h, q, wv, wp)
+        return F.linear(h, wv, bv), F.linear(q, wp, bp)
+
+    @staticmethod
+    def backward(ctx, gv, gp):
+        h, q, wv, wp = ctx.saved_tensors
+        Dh = h.shape[-1]
+        gv2 = gv.reshape(-1, gv.shape[-1]).contiguous()
+        gp2 = gp.reshape(-1, gp.shape[-1]).contiguous()
+        dq = gp2 @ wp.to(gp2.dtype)                                   # d pos, and proj's share of d h
+        dh = torch.addmm(dq, gv2, wv.to(gv2.dtype))                   # + value's share, in the GEMM epilogue
+        h2, q2 = h.reshape(-1, Dh), q.reshape(-1, Dh)
+        gwv = weight_grad(gv2, h2.to(gv2.dtype), wv.dtype)
+        gwp = weight_grad(gp2, q2.to(gp2.dtype), wp.dtype)
+
+        def bias_grad(g2, dt):
+            if g2.shape[1] % 8 == 0 and g2.shape[1] <= 2048:
+                return ops.column_sum(g2).to(dt)
+            return g2.sum(0, dtype=torch.float32).to(dt)
+
+        return (dh.view(h.shape), dq.view(h.shape) if ctx.needs_input_grad[1] else None, gwv,
+                bias_grad(gv2, wv.dtype), gwp, bias_grad(gp2, wp.dtype))
+
+
+def value_query_projection(h, pos, wv, bv, wp, bp):
+    """(h Wv^T + bv, (h + pos) Wp^T + bp) with the fused backward of _ValueQueryProjFn on
+    token-heavy device tensors; the plain composition otherwise."""
+    tokens = h.numel() // max(1, h.shape[-1])
+    if (h.is_cuda and torch.is_grad_enabled() and wv.requires_grad and tokens >= MIN_TOKENS
+            and not torch.is_autocast_enabled() and h.dtype == pos.dtype == wv.dtype == wp.dtype):
+        return _ValueQueryProjFn.apply(h, pos, wv, bv, wp, bp)
+    return linear_tokens(h, wv, bv), linear_tokens(h + pos, wp, bp)
+
+
 def small_linear(x, w, b=None):
     """F.linear with the one-launch weight/bias gradient for small bf16 token counts."""
     tokens = x.numel() // max(1, x.shape[-1])

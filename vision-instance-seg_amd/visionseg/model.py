@@ -29,7 +29,7 @@ import torch.nn.functional as F
 
 from . import ops
 from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_tokens, plane_projection,
-                     small_linear)
+                     small_linear, value_query_projection)
 
 
 @dataclass
@@ -269,16 +269,19 @@ class MSDeformAttn(nn.Module):
 
     def forward(self, h, pos, ref, shapes, norm):
         B, S, _ = h.shape
-        q = h + pos
-        value = self.value_proj(h).view(B, S, self.heads, self.d // self.heads)
         if _MSDA_PREP:                       # one HIP kernel each way (csrc/msda_prep.hip)
-            # both projections of q as one GEMM (q read once, one dX GEMM, no add of
-            # their input gradients); the prologue reads the two column ranges as views
+            # both projections of q = h + pos as one GEMM (q read once, one dX GEMM, no add
+            # of their input gradients), the value projection of h beside it (its dX lands
+            # in the same GEMM epilogue); the prologue reads the two column ranges as views
             so, at = self.sampling_offsets, self.attention_weights
-            proj = linear_tokens(q, torch.cat((so.weight, at.weight)), torch.cat((so.bias, at.bias)))
+            value, proj = value_query_projection(h, pos, self.value_proj.weight, self.value_proj.bias,
+                                                 torch.cat((so.weight, at.weight)), torch.cat((so.bias, at.bias)))
+            value = value.view(B, S, self.heads, self.d // self.heads)
             n_off = so.out_features
             loc, aw = ops.msda_prep(proj[..., :n_off], proj[..., n_off:], ref, shapes, self.heads, self.points)
         else:
+            q = h + pos
+            value = self.value_proj(h).view(B, S, self.heads, self.d // self.heads)
             off = self.sampling_offsets(q).view(B, S, self.heads, self.levels, self.points, 2)
             aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
             aw = F.softmax(aw.float(), -1).view(B, S, self.heads, self.levels, self.points)
