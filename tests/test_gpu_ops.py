@@ -552,13 +552,25 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
     ref = R.msda_ref(vr, shapes, lr, wr)
     go = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3)).to(torch.bfloat16)
     ref.backward(go.float())
-    grads = {}
-    for mf in ("1", "0"):
+    grads, geo = {}, {}
+    for mf, gm in (("1", "1"), ("1", "0"), ("0", "0")):
         monkeypatch.setenv("VS_MSDA_MFMA", mf)
+        monkeypatch.setenv("VS_MSDA_GEOM", gm)
         vd = value.to(DEV).requires_grad_(True)
-        out = ops.ms_deform_attn(vd, shapes, loc.to(DEV), w.to(DEV))
+        ld, wd = loc.to(DEV).requires_grad_(True), w.to(DEV).requires_grad_(True)
+        out = ops.ms_deform_attn(vd, shapes, ld, wd)
         out.backward(go.to(DEV))
         grads[mf] = vd.grad.float().cpu()
+        geo[(mf, gm)] = (ld.grad.cpu(), wd.grad.cpu())
+    # grad_loc / grad_attn fused into the product kernel (GEOM, the default) vs the separate
+    # gather kernel: the same bf16 x bf16 products summed in f32 in another order
+    for a, b in zip(geo[("1", "1")], geo[("1", "0")]):
+        sc = float(b.abs().max())
+        assert float((a - b).abs().max()) <= 1e-4 * sc, float((a - b).abs().max()) / sc
+    # and vs the oracle (f32 value, bf16-rounded inputs): as test_msda_encoder_shapes_backward_vs_oracle
+    e = wr.grad.numpy()
+    np.testing.assert_allclose(geo[("1", "1")][1].numpy(), e, atol=2e-5 * max(1.0, np.abs(e).max()) * 400,
+                               rtol=2 ** -6)
     scale = float(vr.grad.abs().max())
     for mf in ("0", "1"):
         err = (grads[mf] - vr.grad).abs()

@@ -829,15 +829,24 @@ __global__ void __launch_bounds__(64) msda_bwd_binned_kernel(const float* __rest
 // built band by band (kBandCap cells; bands with no corner are skipped), each wave writes
 // its 16 queries' columns with the points taking turns, and the row tiles of the band's
 // product ([32 cells] x K = 64 queries, 4 K-steps x hi/lo) are spread over the waves.
+// GEOM: grad_loc / grad_attn in the same walk (replacing the geom gather kernel): a tap
+// needs d_k = grad_out[q] . value[corner k] for its 4 corners, and over a band those are
+// entries of the product Dm[q][cell] = grad_out[q][:] . value[cell][:] -- one MFMA GEMM
+// ([64 queries] x K = 32 channels x [band cells]) on the band's value rows, each loaded
+// once per tile (the gather kernel requested 4 corner rows per tap: ~6x the bytes).
+// Dm goes to LDS (over W, after the band's atomics), every tap reads its corners' entries.
 constexpr int kBandCap = 128;
 constexpr int kWP8 = 68;       // W row pitch (floats): 64 queries + 4
+constexpr int kDP = 132;       // Dm row pitch (floats): 128 band cells + 4
 
-template <int TX, int TY>
-__global__ void __launch_bounds__(256) msda_bwd_mfma_wg_kernel(const float* __restrict__ loc,
+template <int TX, int TY, bool GEOM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) msda_bwd_mfma_wg_kernel(const float* __restrict__ loc,
                                                                const float* __restrict__ attw,
                                                                const bf16* __restrict__ gout,
                                                                float* __restrict__ gvalue, Levels lv, QueryTiles qt,
-                                                               int S, int Hh, int Q, int L, int nblk) {
+                                                               int S, int Hh, int Q, int L, int nblk,
+                                                               const bf16* __restrict__ value, float* __restrict__ gloc,
+                                                               float* __restrict__ gattw) {
   constexpr int P = 4;
   constexpr int NQ = TX * TY;
   static_assert(NQ == 64, "64 queries x 4 points = one tap per thread");
@@ -877,6 +886,7 @@ __global__ void __launch_bounds__(256) msda_bwd_mfma_wg_kernel(const float* __re
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
     for (int j = 0; j < 8; ++j) bq[ks][j] = sg[(16 * ks + 8 * hh + j) * kD + r];
+
   const size_t rowstride = (size_t)Hh * kD;
   const size_t vbase = ((size_t)b * S * Hh + h) * kD;
   for (int l = 0; l < L; ++l) {
@@ -928,8 +938,8 @@ __global__ void __launch_bounds__(256) msda_bwd_mfma_wg_kernel(const float* __re
       xh = max(xh, sBox[w][3]);
     }
     __syncthreads();                          // sBox is rewritten by the next level
-    if (yh < 0) continue;                     // no corner of the tile on this level (uniform)
-    const int BY = yh - oy + 1, BX = xh - ox + 1;
+    float dk[4] = {0.f, 0.f, 0.f, 0.f};       // GEOM: grad_out . value at the tap's corners
+    const int BY = yh < 0 ? 0 : yh - oy + 1, BX = yh < 0 ? 1 : xh - ox + 1;   // yh < 0: no corner here
     const int SBX = min(BX, kBandCap), SBY = kBandCap / SBX;
     for (int by0 = 0; by0 < BY; by0 += SBY) {
       for (int bx0 = 0; bx0 < BX; bx0 += SBX) {
@@ -991,7 +1001,50 @@ __global__ void __launch_bounds__(256) msda_bwd_mfma_wg_kernel(const float* __re
           }
         }
         __syncthreads();                      // W / hit flags are rewritten by the next band
+        if (GEOM) {
+          // Dm[q][cell] over the band: wave w takes cell tile w (value rows loaded once)
+          float* sD = sW;
+          if (wave < nmt) {
+            bf16x8_t bv[2] = {zero8(), zero8()};
+            const int c = 32 * wave + r;
+            if (c < ncell) {
+              const int y = oy + by0 + c / bw, x = ox + bx0 + c % bw;
+              const bf16* vr = value + lbase + (size_t)(y * Wl + x) * rowstride + 8 * hh;
+              bv[0] = ld8(vr);
+              bv[1] = ld8(vr + 16);
+            }
+#pragma unroll
+            for (int mq = 0; mq < 2; ++mq) {
+              // A operand grad_out[q = 32 mq + r][c = 16 ks + 8 hh + j], read from LDS here
+              // (held in registers it cost occupancy: 4 -> 2 waves/SIMD)
+              const short* ga = sg + (32 * mq + r) * kD + 8 * hh;
+              f32x16_t acc;
+              zero16(acc);
+              acc = mfma16(*reinterpret_cast<const bf16x8_t*>(ga), bv[0], acc);
+              acc = mfma16(*reinterpret_cast<const bf16x8_t*>(ga + 16), bv[1], acc);
+#pragma unroll
+              for (int i = 0; i < 16; ++i) sD[(32 * mq + crow(i, hh)) * kDP + 32 * wave + r] = acc[i];
+            }
+          }
+          __syncthreads();
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (cell[k] >= 0) dk[k] += sD[tq * kDP + cell[k]];
+          __syncthreads();                    // Dm is overwritten by the next band's W
+        }
       }
+    }
+    if (GEOM && qid >= 0) {                   // same formulas as msda_bwd_geom_kernel
+      const float fW = (float)Wl, fH = (float)Hl;
+      float r_w = 0.f, r_x = 0.f, r_y = 0.f;
+      if (tv) {
+        r_w = t.hh * t.hw * dk[0] + t.hh * t.lw * dk[1] + t.lh * t.hw * dk[2] + t.lh * t.lw * dk[3];
+        r_x = fW * aw * (-t.hh * dk[0] + t.hh * dk[1] - t.lh * dk[2] + t.lh * dk[3]);
+        r_y = fH * aw * (-t.hw * dk[0] - t.lw * dk[1] + t.hw * dk[2] + t.lw * dk[3]);
+      }
+      const long long o = grp * LP + l * P + tpt;
+      gattw[o] = r_w;
+      *reinterpret_cast<float2*>(gloc + o * 2) = make_float2(r_x, r_y);
     }
   }
 }
@@ -1076,9 +1129,11 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   if (const char* e = getenv("VS_MSDA_RUN")) split = atoi(e) >= 1;   // tests: force either path
   split = split && P == 4;
   if (split) {
-    launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
     bool mfma = dtype == VS_BF16;            // VS_MSDA_MFMA=0: the binned kernel for bf16 too
     if (const char* e = getenv("VS_MSDA_MFMA")) mfma = mfma && atoi(e) != 0;
+    bool fused = mfma;                       // VS_MSDA_GEOM=0: the separate geom gather kernel
+    if (const char* e = getenv("VS_MSDA_GEOM")) fused = fused && atoi(e) != 0;
+    if (!fused) launch_geom(dtype, value, loc, attw, gout, gloc, gattw, lv, S, Hh, Q, L, P, groups, st);
     const int te = mfma ? 8 : 4;             // query tile edge
     QueryTiles bt;
     bt.mode = Q == S ? 1 : 0;                // grid tiles when the queries are the value grid
@@ -1091,9 +1146,13 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     bt.per_image = bt.mode == 1 ? bt.prefix[L] : (Q + te * te - 1) / (te * te);
     const long long nb2 = (long long)B * bt.per_image * Hh;
     VS_CHECK(nb2 < (1LL << 31), "too many query tiles");
-    if (mfma)
-      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
-                         (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2);
+    if (mfma && fused)
+      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
+                         (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc, gattw);
+    else if (mfma)
+      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, false>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
+                         (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)nullptr, nullptr,
+                         nullptr);
     else if (dtype == VS_BF16)
       hipLaunchKernelGGL((msda_bwd_binned_kernel<bf16, 4, 4>), dim3((unsigned)nb2), dim3(64), 0, st, loc, attw,
                          (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2);
