@@ -105,34 +105,33 @@ def pmc_file(model, size):
     return os.path.join(PMC_DIR, f"pmc_traffic_{model}_{size}.json")
 
 
-OP_KERNELS = {
-    "msda_bwd": ["msda_bwd_geom_kernel", "msda_bwd_mfma_wg_kernel"],
-    "msda_fwd": ["msda_fwd_kernel"],
-    "window_attn_fwd": ["win_attn_fwd_mfma"],
-    "window_attn_bwd": ["win_attn_bwd_mfma"],
-    "window_attn_fwd_fp8": ["win_attn_fwd_mfma_big"],
-    "window_attn_bwd_fp8": ["win_attn_bwd_mfma_big"],
-    "mask_head_fwd": ["mask_head_fwd_kernel"],
-    "mask_head_bwd": ["mask_head_bwd_kernel", "mask_head_bwd_reduce"],
-    "masked_attn_fwd": ["xattn_fwd_mfma", "xattn_fwd_combine"],
-    "masked_attn_bwd": ["xattn_bwd_prep", "xattn_bwd_mfma", "xattn_bwd_dq_combine"],
+OP_KERNELS = {   # op -> kernel-name substrings (template arguments included) whose dispatches make one launch
+    "msda_bwd": ["msda_bwd_mfma_wg_kernel<8, 8, true>"],
+    "msda_fwd": ["msda_fwd_kernel<"],
+    "window_attn_fwd": ["win_attn_fwd_mfma(", "win_attn_fwd_mfma_big<3, false>", "win_attn_fwd_mfma_big<4, false>",
+                        "win_attn_fwd_mfma_big<5, false>"],
+    "window_attn_bwd": ["win_attn_bwd_fa<2, false>", "win_attn_bwd_fa<3, false>", "win_attn_bwd_fa<4, false>",
+                        "win_attn_bwd_fa<5, false>"],
+    "window_attn_fwd_fp8": [f"win_attn_fwd_mfma_big<{n}, true>" for n in (2, 3, 4, 5)],
+    "window_attn_bwd_fp8": [f"win_attn_bwd_fa<{n}, true>" for n in (2, 3, 4, 5)],
+    "mask_head_fwd": ["mask_head_fwd_bf16_kernel<"],
+    "mask_head_bwd": ["mask_head_bwd_kernel<"],
 }
 
 
 def pmc_traffic(op, path):
-    """(bytes per launch, kernels counted) of `op` from the committed PMC profile, or None."""
+    """(bytes per launch, kernels counted) of `op` from the committed PMC profile, or None:
+    the mean per-dispatch bytes (FETCH + WRITE) of the kernels matching the op's patterns
+    (one launch of the op = one dispatch of one of them)."""
     if op not in OP_KERNELS or not os.path.exists(path):
         return None, None
     rows = json.load(open(path))
-    tot, used = 0.0, []
-    for pat in OP_KERNELS[op]:
-        hits = [(k, v) for k, v in rows.items() if pat + "<" in k or pat + "(" in k]
-        if not hits:
-            return None, None
-        for k, v in hits:
-            tot += v["fetch_bytes"] + v["write_bytes"]
-            used.append(pat)
-    return int(tot), used
+    hits = [(k, v) for k, v in rows.items() if any(p in k for p in OP_KERNELS[op])]
+    if not hits:
+        return None, None
+    n = sum(v["dispatches"] for _, v in hits)
+    tot = sum((v["fetch_bytes"] + v["write_bytes"]) * v["dispatches"] for _, v in hits) / max(1, n)
+    return int(tot), sorted({p for p in OP_KERNELS[op] for k, _ in hits if p in k})
 
 
 def kernel_roofline(summary, pmc_path):

@@ -369,6 +369,14 @@ VS_API int vs_group_norm_nchw_backward(int dtype, const void* grad_y, const void
 VS_API int vs_small_linear_wgrad(int dtype, const void* grad_y, const void* x, void* grad_w, void* grad_b,
                                  int tokens, int out_features, int in_features, void* stream);
 
+/* ---- activation backward + bias gradient (csrc/norm.hip) ------------------------------
+ * dx = dy * act'(x) for act 0 = ReLU, 1 = exact GELU (torch's F.gelu, approximate='none'),
+ * x the activation's input, all [M, N] dtype; dx_colsum [N] dtype = column sums of dx as
+ * stored (the bias gradient of the Linear that produced x: Swin MLP fc1, encoder FFN fc1).
+ * workspace: vs_column_sum_workspace_bytes(M, N) bytes. */
+VS_API int vs_act_backward_colsum(int dtype, int act, const void* grad_y, const void* x, void* grad_x,
+                                  void* dx_colsum, void* workspace, int rows, int cols, void* stream);
+
 /* ---- split-K epilogue (csrc/norm.hip) -------------------------------------------------
  * out[i] = sum_{s < num_parts} partials[s * n + i] (+ extra[i] when extra != NULL), f32
  * accumulation in a fixed order, out in dtype: the weight gradient of a token-major

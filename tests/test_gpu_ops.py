@@ -961,3 +961,32 @@ def test_msda_prep_vs_torch(case, dtype):
     assert offr.grad.dtype == dtype and lgr.grad.dtype == dtype
     torch.testing.assert_close(offr.grad.float().cpu(), o32.grad, **tol)
     torch.testing.assert_close(lgr.grad.float().cpu(), l32.grad, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("kind,N", [("gelu", 384), ("gelu", 96), ("relu", 1024), ("relu", 256)])
+def test_activation_backward_colsum(dtype, kind, N):
+    """ops.activation: torch's forward; the HIP backward (vs_act_backward_colsum) vs
+    autograd of F.gelu / F.relu (f64), and its recorded column sums as the bias gradient of
+    the TokenLinear feeding it (no column_sum launch for that bias)."""
+    from visionseg.linear import TokenLinear
+    ops = _ops()
+    g = torch.Generator(device="cuda").manual_seed(N)
+    M, Ci = 20000, 64
+    lin = TokenLinear(Ci, N).to(DEV, dtype)
+    h = torch.randn(M, Ci, device=DEV, generator=g).to(dtype)
+    gy = torch.randn(M, N, device=DEV, generator=g).to(dtype)
+    pre = lin(h)
+    y = ops.activation(pre, kind)
+    ref_f = torch.nn.functional.gelu if kind == "gelu" else torch.nn.functional.relu
+    assert torch.equal(y, ref_f(pre))
+    pre.retain_grad()
+    y.backward(gy)
+    xr = pre.detach().double().requires_grad_(True)
+    ref_f(xr).backward(gy.double())
+    tol = 1e-5 if dtype == torch.float32 else 2 ** -7
+    err = float((pre.grad.double() - xr.grad).abs().max() / xr.grad.abs().max())
+    assert err <= tol, err
+    exp_b = xr.grad.sum(0)
+    rel = float((lin.bias.grad.double() - exp_b).abs().max() / exp_b.abs().max())
+    assert rel <= (1e-4 if dtype == torch.float32 else 2 ** -6), rel

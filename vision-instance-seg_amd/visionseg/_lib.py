@@ -55,6 +55,7 @@ SIGNATURES = {
     "vs_layer_norm_backward_ex": [_c_int] + [_P] * 11 + [_c_int] * 2 + [_P],
     "vs_column_sum_workspace_bytes": [_c_int] * 2,
     "vs_column_sum": [_c_int] + [_P] * 3 + [_c_int] * 2 + [_P],
+    "vs_act_backward_colsum": [_c_int, _c_int] + [_P] * 5 + [_c_int] * 2 + [_P],
     "vs_flat_step_workspace_bytes": [_c_int],
     "vs_flat_step": [_c_int, _P, _c_float, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _c_int] + [_c_float] * 6
                     + [_P, _P, _P, _P],

@@ -120,7 +120,7 @@ class Mlp(nn.Module):
         self.fc2 = TokenLinear(hidden, dim)
 
     def forward(self, x):
-        return self.fc2(F.gelu(self.fc1(x)))
+        return self.fc2(ops.activation(self.fc1(x), "gelu"))
 
 
 class SwinBlock(nn.Module):
@@ -301,7 +301,7 @@ class EncoderLayer(nn.Module):
 
     def forward(self, h, pos, ref, shapes, norm):
         _, h = self.norm1.add_forward(h, self.attn(h, pos, ref, shapes, norm))     # post-norm, fused add
-        _, h = self.norm2.add_forward(h, self.fc2(F.relu(self.fc1(h))))
+        _, h = self.norm2.add_forward(h, self.fc2(ops.activation(self.fc1(h), "relu")))
         return h
 
 

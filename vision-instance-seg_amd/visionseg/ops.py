@@ -20,6 +20,7 @@ import ctypes
 import os
 
 import torch
+import torch.nn.functional as F
 
 from . import _lib as L
 from .profiling import timed
@@ -632,6 +633,44 @@ def column_sum(x2d, out=None):
         L.check(L.lib().vs_column_sum(L.dtype_code(x2d), L.ptr(x2d), L.ptr(out), L.ptr(ws), M, N, L.stream(x2d)),
                 "column_sum")
     return out
+
+
+class _ActColsumFunction(torch.autograd.Function):
+    """y = act(x) (torch's ReLU / exact GELU forward); the backward is one HIP pass
+    (vs_act_backward_colsum) that also records the column sums of dx (attach_colsum): the
+    bias gradient of the Linear that produced x, which then reads no dY for it."""
+
+    @staticmethod
+    def forward(ctx, x, act):
+        ctx.act = act
+        ctx.save_for_backward(x)
+        return F.gelu(x) if act == 1 else F.relu(x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        N = x.shape[-1]
+        M = x.numel() // N
+        gy = gy.to(x.dtype).contiguous()
+        gx = torch.empty_like(x)
+        cs = torch.empty(N, device=x.device, dtype=x.dtype)
+        ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=x.device, dtype=torch.uint8)
+        with timed("act_bwd_colsum", x, bytes_=3 * x.numel() * x.element_size()):
+            L.check(L.lib().vs_act_backward_colsum(L.dtype_code(x), int(ctx.act), L.ptr(gy), L.ptr(x), L.ptr(gx),
+                                                   L.ptr(cs), L.ptr(ws), M, N, L.stream(x)), "act_backward_colsum")
+        attach_colsum(gx, cs)
+        return gx, None
+
+
+def activation(x, kind: str):
+    """F.gelu / F.relu whose backward feeds the preceding Linear's bias gradient (see
+    _ActColsumFunction) on contiguous f32 / bf16 device tensors with N % 8 == 0."""
+    act = {"relu": 0, "gelu": 1}[kind]
+    N = x.shape[-1]
+    if (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and N % 8 == 0 and N <= 2048
+            and x.is_contiguous() and torch.is_grad_enabled() and x.requires_grad and not torch.is_autocast_enabled()):
+        return _ActColsumFunction.apply(x, act)
+    return F.gelu(x) if act == 1 else F.relu(x)
 
 
 # ------------------------------------------------------------------ per-parameter clip

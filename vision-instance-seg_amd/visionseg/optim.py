@@ -269,7 +269,10 @@ class GradReducer:
         self.buf = opt.reduced_grads()
         self.nb = len(self.lay.buckets)
         self.cuda = self.buf.is_cuda
-        self.side = torch.cuda.Stream(device=self.buf.device) if self.cuda else None
+        # high priority: its own hardware queue (a default-priority stream can share the
+        # compute stream's queue and then only runs after the replay), and the collectives
+        # are scheduled ahead of the backward's kernels
+        self.side = torch.cuda.Stream(device=self.buf.device, priority=-1) if self.cuda else None
         self.mode = "off"
         self.events = None
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook(i)) for i, p in enumerate(opt.params)]
