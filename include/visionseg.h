@@ -262,6 +262,13 @@ VS_API long long vs_column_sum_workspace_bytes(int rows, int cols);
 /* out[n] = sum_m x[m, n] (f32 accumulation, fixed order); N a multiple of 8, <= 2048. */
 VS_API int vs_column_sum(int dtype, const void* x, void* out, void* workspace, int rows, int cols,
                          void* stream);
+VS_API long long vs_column_sum_segments_workspace_bytes(int batch, int cols, int nseg);
+/* Per-segment column sums of x [B, S, N] (f32 out [nseg, N], fixed order): segment k =
+ * rows [seg_start[k], seg_start[k+1]) of every image (host array of nseg + 1 ints,
+ * nseg <= 8).  The level-embedding gradient of a multi-scale encoder: the encoder token
+ * sequence is the levels concatenated (HF:m2f:1236-1290 level_embed + position). */
+VS_API int vs_column_sum_segments(int dtype, const void* x, float* out, void* workspace, int batch, int rows,
+                                  int cols, const int* seg_start, int nseg, void* stream);
 
 /* ---- Fused optimiser step over flat buffers (csrc/optim.hip) --------------------------
  * Replaces detectron2's clipped optimiser step as the reference runs it

@@ -990,3 +990,102 @@ def test_activation_backward_colsum(dtype, kind, N):
     exp_b = xr.grad.sum(0)
     rel = float((lin.bias.grad.double() - exp_b).abs().max() / exp_b.abs().max())
     assert rel <= (1e-4 if dtype == torch.float32 else 2 ** -6), rel
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,sizes,N", [(4, [1024, 4096, 16384], 288), (2, [0, 37, 1000, 5], 256), (1, [7], 8),
+                                       (3, [16384, 4096, 1024, 256], 64)])
+def test_column_sum_segments(dtype, B, sizes, N):
+    """Per-segment column sums of [B, S, N] (the level-embedding gradient's reduction)
+    vs f64 torch sums over each level's rows of every image; empty segments give 0."""
+    ops = _ops()
+    g = torch.Generator(device="cuda").manual_seed(N + B)
+    x = torch.randn(B, sum(sizes), N, device=DEV, generator=g).to(dtype)
+    got = ops.column_sum_segments(x, sizes)
+    exp = torch.stack([c.double().sum((0, 1)) for c in torch.split(x, sizes, 1)])
+    assert got.shape == exp.shape and got.dtype == torch.float32
+    err = float((got.double() - exp).abs().max())
+    assert err <= 1e-5 * max(1.0, float(exp.abs().max())) + 1e-4, err
+    with pytest.raises(ValueError):
+        ops.column_sum_segments(x, sizes + [1])
+
+
+def _encoder_grads(monkeypatch, fused, dtype, seed=0):
+    """Parameter + input gradients of a 2-layer MSDeformAttn encoder stack (PixelDecoder's
+    encoder loop, 3 levels at 1024^2 strides, B = 1) with the fused paths
+    (value_query_projection with level-embedding routing and residual sinks, TokenLinear
+    fc1 with a sink) or, fused=False, every Linear as F.linear (MIN_TOKENS above S)."""
+    from visionseg import linear as LN
+    from visionseg.model import EncoderLayer, reference_points
+    if not fused:
+        monkeypatch.setattr(LN, "MIN_TOKENS", 1 << 30)
+    torch.manual_seed(seed)
+    d, shapes = 256, [(32, 32), (64, 64), (128, 128)]
+    layers = torch.nn.ModuleList([EncoderLayer(d, 1024, 8, 3, 4) for _ in range(2)]).to(DEV, dtype)
+    for m in layers.modules():
+        if isinstance(m, torch.nn.Linear):
+            torch.nn.init.normal_(m.weight, std=0.05)
+            torch.nn.init.normal_(m.bias, std=0.05)
+    lvl = torch.nn.Parameter(torch.randn(3, d, device=DEV).to(dtype))
+    S = sum(h * w for h, w in shapes)
+    g = torch.Generator(device="cuda").manual_seed(seed + 1)
+    h0 = torch.randn(1, S, d, device=DEV, generator=g).to(dtype).requires_grad_(True)
+    sine = torch.randn(1, S, d, device=DEV, generator=g).to(dtype)
+    sizes = [h * w for h, w in shapes]
+    p = sine + torch.cat([lvl.detach()[i].view(1, 1, -1).expand(1, n, -1) for i, n in enumerate(sizes)], 1)
+    ref = reference_points(shapes, 1, DEV)
+    norm = torch.tensor([[w, hh] for hh, w in shapes], device=DEV, dtype=torch.float32)[None, None, None, :, None, :]
+    h = h0
+    for layer in layers:
+        h = layer(h, p, ref, shapes, norm, (lvl, sizes))
+    gy = torch.randn(h.shape, device=DEV, generator=g).to(dtype)
+    h.backward(gy)
+    out = {n: q.grad.detach().float().clone() for n, q in layers.named_parameters()}
+    out["level_embed"] = lvl.grad.detach().float().clone()
+    out["h0"] = h0.grad.detach().float().clone()
+    return out
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_encoder_fused_gradients_match_plain_composition(monkeypatch, dtype):
+    """The encoder's fused backward -- residual gradients added by the dX GEMMs
+    (ops.ResidualSink), the level embedding's gradient from per-level column sums x Wp,
+    one packed offset/weight projection gradient -- equals the plain autograd composition
+    (every Linear as F.linear, pos carrying the level rows with their gradient).  f32:
+    2e-4 of each gradient's max (summation order, f32 MSDA atomics); bf16: 3e-2."""
+    a = _encoder_grads(monkeypatch, True, dtype)
+    monkeypatch.undo()
+    b = _encoder_grads(monkeypatch, False, dtype)
+    tol = 2e-4 if dtype == torch.float32 else 3e-2
+    for k in b:
+        scale = float(b[k].abs().max())
+        err = float((a[k] - b[k]).abs().max())
+        assert err <= tol * scale + 1e-6, (k, err, scale)
+
+
+def test_residual_sink_plain_paths_keep_gradients():
+    """A sink that no consumer armed leaves the LayerNorm's x gradient with autograd; an
+    armed sink hands it to the consumer's dX GEMM and x's gradient still equals the sum
+    of both paths."""
+    from visionseg.linear import TokenLinear
+    ops = _ops()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    M, C = 20000, 64
+    lin = TokenLinear(C, C).to(DEV)
+    w = torch.ones(C, device=DEV)
+    b = torch.zeros(C, device=DEV)
+    x = torch.randn(M, C, device=DEV, generator=g)
+    gy = torch.randn(M, C, device=DEV, generator=g)
+    res = []
+    for arm in (False, True):
+        xx = x.clone().requires_grad_(True)
+        sink = ops.ResidualSink()
+        r = lin(xx, sink) if arm else lin(xx)
+        _, y = ops.add_layer_norm(xx, r, w, b, 1e-5, sink)
+        assert sink.armed == arm
+        y.backward(gy)
+        assert sink.g is None
+        res.append(xx.grad.clone())
+        lin.zero_grad()
+    err = float((res[0] - res[1]).abs().max())
+    assert err <= 1e-4 * float(res[0].abs().max()), err

@@ -26,7 +26,8 @@ def site():
     for fr in reversed(traceback.extract_stack()[:-3]):
         if "visionseg" in fr.filename or "criterion" in fr.filename:
             return f"{os.path.basename(fr.filename)}:{fr.lineno}"
-    return "<autograd/other>"
+    node = torch._C._current_autograd_node()
+    return f"<{node.name()}>" if node is not None else "<other>"
 
 
 class Census(TorchDispatchMode):

@@ -248,10 +248,41 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
 
 // column sums of x [M, N] -> part[blockIdx][N] (f32); a thread owns one 8-column chunk
 // and a subset of rows
+// Row segments of a [B, S, N] tensor (the levels of a multi-scale token sequence):
+// segment k = rows [start[k], start[k + 1]) of every image.
+struct RowSegments {
+  int start[9];
+  int nseg;
+};
+
+template <typename T>
+__device__ __forceinline__ void colsum_rows(const T* __restrict__ x, float* __restrict__ part, long long M, int N,
+                                            int nblk, int blk, float* red);
+
 template <typename T>
 __global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ x, float* __restrict__ part, int M,
                                                           int N) {
-  extern __shared__ float red[];             // [rowsets][N]
+  extern __shared__ float red[];
+  colsum_rows(x, part + (size_t)blockIdx.x * N, M, N, gridDim.x, blockIdx.x, red);
+}
+
+// per-segment column sums of x [B, S, N]: grid (nblk, nseg * B); workgroup (x, k*B + b)
+// sums its share of image b's rows of segment k -> part[(k*B + b)*nblk + x][N]
+template <typename T>
+__global__ void __launch_bounds__(kThreads) colsum_seg_kernel(const T* __restrict__ x, float* __restrict__ part,
+                                                              int B, int S, int N, RowSegments seg) {
+  extern __shared__ float red[];
+  const int k = blockIdx.y / B, b = blockIdx.y % B;
+  const int r0 = seg.start[k];
+  colsum_rows(x + ((size_t)b * S + r0) * N, part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * N,
+              seg.start[k + 1] - r0, N, gridDim.x, blockIdx.x, red);
+}
+
+// column sums of rows [0, M) of x [M, N] -> part[N] (f32) for workgroup blk of nblk; a
+// thread owns one 8-column chunk and a subset of rows
+template <typename T>
+__device__ __forceinline__ void colsum_rows(const T* __restrict__ x, float* __restrict__ part, long long M, int N,
+                                            int nblk, int blk, float* red) {   // red: [rowsets][N]
   const int nch = N >> 3;
   const int rowsets = kThreads / nch;        // nch <= 256
   const int ch = threadIdx.x % nch;
@@ -260,8 +291,8 @@ __global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ 
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = 0.f;
   if (rs < rowsets) {
-    const long long stride = (long long)gridDim.x * rowsets;
-    for (long long row = (long long)blockIdx.x * rowsets + rs; row < M; row += 4 * stride) {
+    const long long stride = (long long)nblk * rowsets;
+    for (long long row = (long long)blk * rowsets + rs; row < M; row += 4 * stride) {
       float v[4][8];                            // 4 rows' loads in flight
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -284,7 +315,7 @@ __global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ 
   for (int c = threadIdx.x; c < N; c += kThreads) {
     float a = 0.f;
     for (int r = 0; r < rowsets; ++r) a += red[(size_t)r * N + c];
-    part[(size_t)blockIdx.x * N + c] = a;
+    part[c] = a;
   }
 }
 
@@ -362,6 +393,8 @@ __global__ void __launch_bounds__(kThreads) colsum_partials_kernel(const float* 
   const int lane = threadIdx.x & 31;
   const int sl = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + lane;
+  part += (size_t)blockIdx.y * nb * N;         // grid.y > 1: one output row per segment
+  out0 += (size_t)blockIdx.y * N;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (col < N) {
     int r = sl;
@@ -607,6 +640,43 @@ extern "C" int vs_column_sum(int dtype, const void* x, void* out, void* ws, int 
     hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part,
                        (float*)out, (float*)nullptr, grid, N, N);
   }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" long long vs_column_sum_segments_workspace_bytes(int B, int N, int nseg) {
+  return (long long)std::max(kMaxPartials, nseg * std::max(B, 1)) * N * sizeof(float);
+}
+
+extern "C" int vs_column_sum_segments(int dtype, const void* x, float* out, void* ws, int B, int S, int N,
+                                      const int* seg_start, int nseg, void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(B >= 0 && S >= 0 && N > 0 && N % 8 == 0 && N / 8 <= kThreads, "N must be a multiple of 8, <= 2048");
+  VS_CHECK(nseg >= 1 && nseg <= 8 && seg_start, "1..8 segments");
+  VS_CHECK(out && ws && (B * (long long)S == 0 || x), "null pointer");
+  RowSegments seg{};
+  seg.nseg = nseg;
+  for (int k = 0; k <= nseg; ++k) {
+    seg.start[k] = seg_start[k];
+    VS_CHECK(seg_start[k] >= 0 && seg_start[k] <= S && (k == 0 || seg_start[k] >= seg_start[k - 1]),
+             "segment starts must be non-decreasing within [0, S]");
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (B == 0) return hipMemsetAsync(out, 0, (size_t)nseg * N * sizeof(float), st) == hipSuccess ? VS_OK : VS_ERR_HIP;
+  float* part = (float*)ws;
+  const int rowsets = kThreads / (N / 8);
+  int maxrows = 0;
+  for (int k = 0; k < nseg; ++k) maxrows = std::max(maxrows, seg.start[k + 1] - seg.start[k]);
+  const int nblk = std::max(1, std::min(blocks_for(maxrows, rowsets * 16, kMaxPartials), kMaxPartials / (nseg * B)));
+  const size_t lds = (size_t)rowsets * N * sizeof(float);
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(colsum_seg_kernel<bf16>, dim3(nblk, nseg * B), dim3(kThreads), lds, st, (const bf16*)x, part,
+                       B, S, N, seg);
+  else
+    hipLaunchKernelGGL(colsum_seg_kernel<float>, dim3(nblk, nseg * B), dim3(kThreads), lds, st, (const float*)x,
+                       part, B, S, N, seg);
+  hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32, nseg), dim3(kThreads), 0, st, part, out,
+                     (float*)nullptr, nblk * B, N, N);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

@@ -55,6 +55,8 @@ SIGNATURES = {
     "vs_layer_norm_backward_ex": [_c_int] + [_P] * 11 + [_c_int] * 2 + [_P],
     "vs_column_sum_workspace_bytes": [_c_int] * 2,
     "vs_column_sum": [_c_int] + [_P] * 3 + [_c_int] * 2 + [_P],
+    "vs_column_sum_segments_workspace_bytes": [_c_int] * 3,
+    "vs_column_sum_segments": [_c_int] + [_P] * 3 + [_c_int] * 3 + [_P, _c_int, _P],
     "vs_act_backward_colsum": [_c_int, _c_int] + [_P] * 5 + [_c_int] * 2 + [_P],
     "vs_flat_step_workspace_bytes": [_c_int],
     "vs_flat_step": [_c_int, _P, _c_float, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _c_int] + [_c_float] * 6
@@ -82,6 +84,7 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_mask_head_backward_workspace_bytes": ctypes.c_longlong,
             "vs_layer_norm_backward_workspace_bytes": ctypes.c_longlong,
             "vs_column_sum_workspace_bytes": ctypes.c_longlong,
+            "vs_column_sum_segments_workspace_bytes": ctypes.c_longlong,
             "vs_flat_step_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_nchw_workspace_bytes": ctypes.c_longlong,

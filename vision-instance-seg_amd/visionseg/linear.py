@@ -58,9 +58,12 @@ def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype, out: 
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, sink=None):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.sink = sink
+        if sink is not None:
+            sink.arm()
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -69,7 +72,11 @@ class _LinearFn(torch.autograd.Function):
         gy2 = gy.reshape(-1, gy.shape[-1])
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = (gy2 @ weight.to(gy2.dtype)).view(x.shape)
+            gres = ctx.sink.take() if ctx.sink is not None else None
+            if gres is not None:       # the residual path's gradient of x, added by the GEMM (beta = 1)
+                gx = torch.addmm(gres.reshape(gy2.shape[0], -1).to(gy2.dtype), gy2, weight.to(gy2.dtype)).view(x.shape)
+            else:
+                gx = (gy2 @ weight.to(gy2.dtype)).view(x.shape)
         if ctx.needs_input_grad[1]:
             gw = weight_grad(gy2, x.reshape(-1, x.shape[-1]).to(gy2.dtype), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -80,7 +87,7 @@ class _LinearFn(torch.autograd.Function):
                 gb = ops.column_sum(gy2).to(weight.dtype)          # HIP column sum, f32 accumulation
             else:
                 gb = gy2.sum(0, dtype=torch.float32).to(weight.dtype)
-        return gx, gw, gb
+        return gx, gw, gb, None
 
 
 class _PlaneProjectionFn(torch.autograd.Function):
@@ -250,25 +257,44 @@ def in_projection(xq, xk, xv, weight, bias):
 class _ValueQueryProjFn(torch.autograd.Function):
     """An encoder MSDeformAttn layer's two input projections of the same tokens h
     (HF:m2f:919-1002): value = h Wv^T + bv and proj = (h + pos) Wp^T + bp (the fused
-    sampling-offset / attention-weight projection).  The backward forms dq = dproj Wp
-    once (it is both d pos and proj's share of d h) and dh = dq + dvalue Wv as ONE GEMM
-    with dq as its C operand (beta = 1): autograd would add the two shares with a
-    separate full-size kernel.  Weight gradients: split-K; bias gradients: HIP column sums."""
+    sampling-offset / attention-weight projection).
+
+    Backward: dh = [g_res] + dproj Wp + dvalue Wv as chained GEMMs with beta = 1 (g_res:
+    the post-norm residual gradient of h handed over by ResidualSink), so autograd adds
+    nothing at full size.  With `level_embed` (pos = a constant sine embedding + level
+    embedding rows, the level sizes in `level_sizes`), pos gets no gradient: the level
+    embedding's is (per-level column sums of dproj) Wp, exact by linearity, and the bias
+    gradient of proj is the sum of the same per-level sums.  Weight gradients: split-K."""
 
     @staticmethod
-    def forward(ctx, h, pos, wv, bv, wp, bp):
+    def forward(ctx, h, pos, wv, bv, wp, bp, level_embed=None, level_sizes=None, sink=None):
         q = h + pos
         ctx.save_for_backward(h, q, wv, wp)
+        ctx.level = (level_embed is not None, tuple(level_sizes or ()),
+                     level_embed.dtype if level_embed is not None else None)
+        ctx.sink = sink
+        if sink is not None:
+            sink.arm()
         return F.linear(h, wv, bv), F.linear(q, wp, bp)
 
     @staticmethod
     def backward(ctx, gv, gp):
         h, q, wv, wp = ctx.saved_tensors
         Dh = h.shape[-1]
+        has_level, sizes, ldt = ctx.level
         gv2 = gv.reshape(-1, gv.shape[-1]).contiguous()
         gp2 = gp.reshape(-1, gp.shape[-1]).contiguous()
-        dq = gp2 @ wp.to(gp2.dtype)                                   # d pos, and proj's share of d h
-        dh = torch.addmm(dq, gv2, wv.to(gv2.dtype))                   # + value's share, in the GEMM epilogue
+        gres = ctx.sink.take() if ctx.sink is not None else None
+        dq = None
+        wp_, wv_ = wp.to(gp2.dtype), wv.to(gv2.dtype)
+        if ctx.needs_input_grad[1]:                                   # d pos wanted on its own
+            dq = gp2 @ wp_
+            dh = torch.addmm(dq, gv2, wv_)
+            if gres is not None:
+                dh = dh + gres.reshape(dh.shape)
+        else:
+            dh = gp2 @ wp_ if gres is None else torch.addmm(gres.reshape(gp2.shape[0], Dh).to(gp2.dtype), gp2, wp_)
+            dh = torch.addmm(dh, gv2, wv_)                            # + value's share, in the GEMM epilogue
         h2, q2 = h.reshape(-1, Dh), q.reshape(-1, Dh)
         gwv = weight_grad(gv2, h2.to(gv2.dtype), wv.dtype)
         gwp = weight_grad(gp2, q2.to(gp2.dtype), wp.dtype)
@@ -278,18 +304,44 @@ class _ValueQueryProjFn(torch.autograd.Function):
                 return ops.column_sum(g2).to(dt)
             return g2.sum(0, dtype=torch.float32).to(dt)
 
-        return (dh.view(h.shape), dq.view(h.shape) if ctx.needs_input_grad[1] else None, gwv,
-                bias_grad(gv2, wv.dtype), gwp, bias_grad(gp2, wp.dtype))
+        glvl = None
+        if has_level and gp2.shape[1] % 8 == 0 and gp2.shape[1] <= 2048:
+            seg = ops.column_sum_segments(gp2.view(-1, sum(sizes), gp2.shape[1]), sizes)   # [levels, Np] f32
+            gbp = seg.sum(0).to(wp.dtype)
+            if ctx.needs_input_grad[6]:
+                glvl = (seg @ wp.float()).to(ldt)
+        else:
+            gbp = bias_grad(gp2, wp.dtype)
+            if has_level and ctx.needs_input_grad[6]:
+                g3 = gp2.view(-1, sum(sizes), gp2.shape[1]).float()
+                glvl = torch.stack([c.sum((0, 1)) for c in torch.split(g3, list(sizes), 1)]) @ wp.float()
+                glvl = glvl.to(ldt)
+        return (dh.view(h.shape), dq.view(h.shape) if dq is not None else None, gwv,
+                bias_grad(gv2, wv.dtype), gwp, gbp, glvl, None, None)
 
 
-def value_query_projection(h, pos, wv, bv, wp, bp):
+def value_query_projection(h, pos, wv, bv, wp, bp, level_embed=None, level_sizes=None, sink=None):
     """(h Wv^T + bv, (h + pos) Wp^T + bp) with the fused backward of _ValueQueryProjFn on
-    token-heavy device tensors; the plain composition otherwise."""
+    token-heavy device tensors; the plain composition otherwise.  `level_embed` /
+    `level_sizes`: pos already holds the level-embedding rows (detached) and the
+    gradient goes to `level_embed` directly; `sink`: see ops.ResidualSink."""
     tokens = h.numel() // max(1, h.shape[-1])
     if (h.is_cuda and torch.is_grad_enabled() and wv.requires_grad and tokens >= MIN_TOKENS
             and not torch.is_autocast_enabled() and h.dtype == pos.dtype == wv.dtype == wp.dtype):
-        return _ValueQueryProjFn.apply(h, pos, wv, bv, wp, bp)
+        return _ValueQueryProjFn.apply(h, pos, wv, bv, wp, bp, level_embed, level_sizes, sink)
+    pos = reattach_level_embed(pos, level_embed, level_sizes)
     return linear_tokens(h, wv, bv), linear_tokens(h + pos, wp, bp)
+
+
+def reattach_level_embed(pos, level_embed, sizes):
+    """pos (holding detached level-embedding rows) with the level embedding's gradient
+    path restored for the plain composition: pos + (rows - rows.detach()), exactly pos in
+    value."""
+    if level_embed is None or not (torch.is_grad_enabled() and level_embed.requires_grad):
+        return pos
+    rows = torch.cat([level_embed[i].view(1, 1, -1).expand(pos.shape[0], n, -1) for i, n in enumerate(sizes)], 1)
+    rows = rows.to(pos.dtype)
+    return pos + (rows - rows.detach())
 
 
 def small_linear(x, w, b=None):
@@ -321,18 +373,20 @@ class TokenLayerNorm(nn.LayerNorm):
             return ops.layer_norm(x, self.weight, self.bias, self.eps)
         return F.layer_norm(x, self.normalized_shape, self.weight, self.bias, self.eps)
 
-    def add_forward(self, x, r):
+    def add_forward(self, x, r, sink=None):
         """(x + r, LN(x + r)): the residual add fused into the norm on the HIP kernel
-        (ops.add_layer_norm) where the plain norm would run there too."""
+        (ops.add_layer_norm) where the plain norm would run there too.  `sink`: hand x's
+        gradient to the armed consumer of x (ops.ResidualSink)."""
         if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
                 and r.shape == x.shape and r.dtype == x.dtype and not torch.is_autocast_enabled():
-            return ops.add_layer_norm(x, r, self.weight, self.bias, self.eps)
+            return ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink)
         s = x + r
         return s, self(s)
 
 
-def linear_tokens(x, w, b=None):
-    """F.linear with the split-K weight gradient when x carries many tokens."""
+def linear_tokens(x, w, b=None, sink=None):
+    """F.linear with the split-K weight gradient when x carries many tokens (`sink`: see
+    ops.ResidualSink; armed only on that path)."""
     tokens = x.numel() // max(1, x.shape[-1])
     if not (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and tokens >= MIN_TOKENS):
         return F.linear(x, w, b)
@@ -340,11 +394,11 @@ def linear_tokens(x, w, b=None):
         dt = torch.get_autocast_dtype("cuda")
         with torch.autocast("cuda", enabled=False):
             return _LinearFn.apply(x.to(dt), w.to(dt), None if b is None else b.to(dt))
-    return _LinearFn.apply(x, w, b)
+    return _LinearFn.apply(x, w, b, sink)
 
 
 class TokenLinear(nn.Linear):
     """nn.Linear whose backward splits the token axis of dW (see module docstring)."""
 
-    def forward(self, x):
-        return linear_tokens(x, self.weight, self.bias)
+    def forward(self, x, sink=None):
+        return linear_tokens(x, self.weight, self.bias, sink)

@@ -29,7 +29,7 @@ import torch.nn.functional as F
 
 from . import ops
 from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_tokens, plane_projection,
-                     small_linear, value_query_projection)
+                     small_linear, value_query_projection, reattach_level_embed)
 
 
 @dataclass
@@ -267,20 +267,24 @@ class MSDeformAttn(nn.Module):
         self.value_proj = TokenLinear(d, d)
         self.output_proj = TokenLinear(d, d)
 
-    def forward(self, h, pos, ref, shapes, norm):
+    def forward(self, h, pos, ref, shapes, norm, level=None, sink=None):
+        """level: (level_embed, level sizes) when pos holds detached level-embedding rows
+        (PixelDecoder); sink: ops.ResidualSink of the post-norm residual around this op."""
         B, S, _ = h.shape
+        lvl_embed, lvl_sizes = level if level is not None else (None, None)
         if _MSDA_PREP:                       # one HIP kernel each way (csrc/msda_prep.hip)
             # both projections of q = h + pos as one GEMM (q read once, one dX GEMM, no add
             # of their input gradients), the value projection of h beside it (its dX lands
-            # in the same GEMM epilogue); the prologue reads the two column ranges as views
+            # in the same GEMM epilogue); the prologue reads the packed projection's two
+            # column ranges and its backward writes one packed gradient
             so, at = self.sampling_offsets, self.attention_weights
             value, proj = value_query_projection(h, pos, self.value_proj.weight, self.value_proj.bias,
-                                                 torch.cat((so.weight, at.weight)), torch.cat((so.bias, at.bias)))
+                                                 torch.cat((so.weight, at.weight)), torch.cat((so.bias, at.bias)),
+                                                 lvl_embed, lvl_sizes, sink)
             value = value.view(B, S, self.heads, self.d // self.heads)
-            n_off = so.out_features
-            loc, aw = ops.msda_prep(proj[..., :n_off], proj[..., n_off:], ref, shapes, self.heads, self.points)
+            loc, aw = ops.msda_prep(proj, None, ref, shapes, self.heads, self.points)
         else:
-            q = h + pos
+            q = h + reattach_level_embed(pos, lvl_embed, lvl_sizes)
             value = self.value_proj(h).view(B, S, self.heads, self.d // self.heads)
             off = self.sampling_offsets(q).view(B, S, self.heads, self.levels, self.points, 2)
             aw = self.attention_weights(q).view(B, S, self.heads, self.levels * self.points)
@@ -299,9 +303,12 @@ class EncoderLayer(nn.Module):
         self.fc2 = TokenLinear(ffn, d)
         self.norm2 = TokenLayerNorm(d)
 
-    def forward(self, h, pos, ref, shapes, norm):
-        _, h = self.norm1.add_forward(h, self.attn(h, pos, ref, shapes, norm))     # post-norm, fused add
-        _, h = self.norm2.add_forward(h, self.fc2(ops.activation(self.fc1(h), "relu")))
+    def forward(self, h, pos, ref, shapes, norm, level=None):
+        # post-norm, residual add fused into the norm; each residual gradient is added by
+        # the dX GEMM of the branch's first op (ops.ResidualSink), not by autograd
+        s1, s2 = ops.ResidualSink(), ops.ResidualSink()
+        _, h = self.norm1.add_forward(h, self.attn(h, pos, ref, shapes, norm, level, s1), s1)
+        _, h = self.norm2.add_forward(h, self.fc2(ops.activation(self.fc1(h, s2), "relu")), s2)
         return h
 
 
@@ -376,8 +383,12 @@ class PixelDecoder(nn.Module):
         shapes = [(int(e.shape[2]), int(e.shape[3])) for e in embeds]
         B = embeds[0].shape[0]
         h = torch.cat([e.flatten(2).transpose(1, 2) for e in embeds], 1)
-        p = torch.cat([q.flatten(2).transpose(1, 2) + self.level_embed[i].view(1, 1, -1).to(q.dtype)
+        # position term with detached level-embedding rows: the layers route the level
+        # embedding's gradient themselves (per-level column sums, linear.value_query_projection)
+        lvl = self.level_embed.detach()
+        p = torch.cat([q.flatten(2).transpose(1, 2) + lvl[i].view(1, 1, -1).to(q.dtype)
                        for i, q in enumerate(pos)], 1)
+        level = (self.level_embed, [Hl * Wl for (Hl, Wl) in shapes])
         ref = reference_points(shapes, B, dev)
         key = (tuple(shapes), dev)
         norm = self._norm_cache.get(key)
@@ -385,7 +396,7 @@ class PixelDecoder(nn.Module):
             norm = torch.tensor([[w, hh] for hh, w in shapes], device=dev, dtype=torch.float32)[None, None, None, :, None, :]
             self._norm_cache[key] = norm
         for layer in self.encoder:
-            h = layer(h, p, ref, shapes, norm)
+            h = layer(h, p, ref, shapes, norm, level)
         # encoder levels, token-major [B, H_l*W_l, C] (split: one concatenating backward
         # instead of a zero-filled full-size gradient per slice)
         toks = torch.split(h, [Hl * Wl for (Hl, Wl) in shapes], dim=1)

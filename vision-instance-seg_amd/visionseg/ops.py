@@ -123,14 +123,22 @@ class MSDAPrepFunction(torch.autograd.Function):
     """(offsets [B,Q,H*L*P*2], logits [B,Q,H*L*P], ref [B,Q,L,2] f32) -> (sampling
     locations [B,Q,H,L,P,2] f32, attention weights [B,Q,H,L,P] f32) as
     `ref + offsets.float() / (W_l, H_l)` and `softmax(logits.float())` over L*P
-    (HF:m2f:994-1002; csrc/msda_prep.hip).  ref gets no gradient (a buffer)."""
+    (HF:m2f:994-1002; csrc/msda_prep.hip).  ref gets no gradient (a buffer).
+    logits=None: `off` is the packed projection [B,Q,H*L*P*3] (offsets then logits, one
+    GEMM's output); its gradient is then written as one tensor (the kernel takes row
+    strides), not as two slice gradients that autograd zero-fills and adds."""
 
     @staticmethod
     def forward(ctx, off, logits, ref, shapes, heads, points):
-        L.require_hip(off, logits, ref)
-        B, Q = off.shape[0], off.shape[1]
         nl = len(shapes)
         lp = nl * points
+        ctx.packed = logits is None
+        if ctx.packed:
+            if off.shape[-1] != heads * lp * 3:
+                raise ValueError(f"packed projection width {off.shape[-1]} != {heads * lp * 3}")
+            off, logits = off[..., :heads * lp * 2], off[..., heads * lp * 2:]
+        L.require_hip(off, logits, ref)
+        B, Q = off.shape[0], off.shape[1]
         if off.dtype != logits.dtype:
             raise ValueError("offsets / logits dtypes differ")
         if off.shape[-1] != heads * lp * 2 or logits.shape[-1] != heads * lp:
@@ -166,20 +174,26 @@ class MSDAPrepFunction(torch.autograd.Function):
         lp = nl * points
         gloc = aw.new_zeros(*aw.shape, 2) if gloc is None else gloc.float().contiguous()
         gaw = torch.zeros_like(aw) if gaw is None else gaw.float().contiguous()
-        goff = torch.empty(B, Q, heads * lp * 2, device=aw.device, dtype=dt)
-        glg = torch.empty(B, Q, heads * lp, device=aw.device, dtype=dt)
+        if ctx.packed:
+            gproj = torch.empty(B, Q, heads * lp * 3, device=aw.device, dtype=dt)
+            goff, glg = gproj[..., :heads * lp * 2], gproj[..., heads * lp * 2:]
+        else:
+            goff = torch.empty(B, Q, heads * lp * 2, device=aw.device, dtype=dt)
+            glg = torch.empty(B, Q, heads * lp, device=aw.device, dtype=dt)
         sh, _, _ = _level_arrays(shapes)
         with timed("msda_prep_bwd", aw, bytes_=(gloc.numel() + gaw.numel() + aw.numel()) * 4
                    + (goff.numel() + glg.numel()) * goff.element_size()):
             L.check(L.lib().vs_msda_prep_backward(L.dtype_code(goff), L.ptr(gloc), L.ptr(gaw), L.ptr(aw), sh,
-                                                  L.ptr(goff), goff.shape[-1], L.ptr(glg), glg.shape[-1], B, Q, heads,
+                                                  L.ptr(goff), goff.stride(1), L.ptr(glg), glg.stride(1), B, Q, heads,
                                                   nl, points, L.stream(aw)), "msda_prep_backward")
+        if ctx.packed:
+            return gproj, None, None, None, None, None
         return goff, glg, None, None, None, None
 
 
 def msda_prep(offsets, logits, ref, spatial_shapes, heads: int, points: int):
     """Sampling locations and attention weights of MSDeformAttn from its two projections
-    (see MSDAPrepFunction)."""
+    (see MSDAPrepFunction; logits=None: `offsets` is the packed projection)."""
     return MSDAPrepFunction.apply(offsets, logits, ref, _shapes_list(spatial_shapes), int(heads), int(points))
 
 
@@ -559,8 +573,9 @@ class AddLayerNormFunction(torch.autograd.Function):
     backward adds the gradient of s (residual path) inside the LayerNorm backward."""
 
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps):
+    def forward(ctx, x, r, weight, bias, eps, sink=None):
         L.require_hip(x, r, weight, bias)
+        ctx.sink = sink if sink is not None and sink.armed else None
         C = x.shape[-1]
         xc, rc = x.contiguous(), r.to(x.dtype).contiguous()
         M = xc.numel() // C
@@ -600,12 +615,17 @@ class AddLayerNormFunction(torch.autograd.Function):
                                                       L.stream(s)), "layer_norm_backward_ex")
         if cs is not None:
             attach_colsum(gx, cs)
-        return gx, gx, gw, gb, None
+        gxx = gx
+        if ctx.sink is not None and ctx.needs_input_grad[0]:
+            ctx.sink.g = gx            # the armed consumer of x adds it in its dX GEMM
+            gxx = None
+        return gxx, gx, gw, gb, None, None
 
 
-def add_layer_norm(x, r, weight, bias, eps: float = 1e-5):
-    """(x + r, layer_norm(x + r)) for token-major [..., C] tensors (see AddLayerNormFunction)."""
-    return AddLayerNormFunction.apply(x, r, weight, bias, eps)
+def add_layer_norm(x, r, weight, bias, eps: float = 1e-5, sink: ResidualSink | None = None):
+    """(x + r, layer_norm(x + r)) for token-major [..., C] tensors (see AddLayerNormFunction;
+    `sink`: see ResidualSink)."""
+    return AddLayerNormFunction.apply(x, r, weight, bias, eps, sink)
 
 
 def layer_norm(x, weight, bias, eps: float = 1e-5):
@@ -633,6 +653,56 @@ def column_sum(x2d, out=None):
         L.check(L.lib().vs_column_sum(L.dtype_code(x2d), L.ptr(x2d), L.ptr(out), L.ptr(ws), M, N, L.stream(x2d)),
                 "column_sum")
     return out
+
+
+def column_sum_segments(x3d, sizes):
+    """x [B, S, N] -> f32 [len(sizes), N]: column sums over every image's rows of each
+    consecutive segment (sizes sum to S) -- the per-level sums of a multi-scale token
+    sequence (csrc/norm.hip colsum_seg_kernel)."""
+    L.require_hip(x3d)
+    x3d = x3d.contiguous()
+    B, S, N = x3d.shape
+    sizes = [int(v) for v in sizes]
+    if sum(sizes) != S or not 1 <= len(sizes) <= 8:
+        raise ValueError(f"column_sum_segments: segment sizes {sizes} do not cover S = {S} (1..8 segments)")
+    starts = [0]
+    for v in sizes:
+        starts.append(starts[-1] + v)
+    seg = (ctypes.c_int * len(starts))(*starts)
+    out = torch.empty(len(sizes), N, device=x3d.device, dtype=torch.float32)
+    ws = torch.empty(int(L.lib().vs_column_sum_segments_workspace_bytes(B, N, len(sizes))), device=x3d.device,
+                     dtype=torch.uint8)
+    with timed("column_sum", x3d, bytes_=x3d.numel() * x3d.element_size()):
+        L.check(L.lib().vs_column_sum_segments(L.dtype_code(x3d), L.ptr(x3d), L.ptr(out), L.ptr(ws), B, S, N, seg,
+                                               len(sizes), L.stream(x3d)), "column_sum_segments")
+    return out
+
+
+class ResidualSink:
+    """Hands a post-norm residual block's residual-path gradient to the GEMM that also
+    consumes the block input, so that GEMM adds it in its epilogue (beta = 1) instead of
+    autograd adding the two input gradients with a separate full-size kernel.
+
+    Protocol (one object per forward call): the consumer (first op of the branch, e.g.
+    the encoder FFN's fc1 or the MSDeformAttn input projections) `arm()`s the sink in its
+    forward when it takes its fused path; `add_layer_norm(x, branch, ..., sink)` then
+    returns no gradient for x and stores it here in its backward (which runs first: the
+    consumer's output feeds the branch); the consumer `take()`s it in its backward.  If
+    either side takes a plain path the sink is never armed or never filled, and autograd
+    adds the gradients as usual."""
+
+    __slots__ = ("armed", "g")
+
+    def __init__(self):
+        self.armed = False
+        self.g = None
+
+    def arm(self):
+        self.armed = True
+
+    def take(self):
+        g, self.g = self.g, None
+        return g
 
 
 class _ActColsumFunction(torch.autograd.Function):
