@@ -50,3 +50,34 @@ def test_ops_refuse_cpu_tensors():
     from visionseg import ops
     with pytest.raises(RuntimeError, match="HIP device"):
         ops.window_partition(torch.zeros(1, 4, 4, 8), 4, 0)
+
+
+# the operator surface of SURVEY §8(b): TORCH_LIBRARY(visionseg) in csrc/torch_ops.cpp
+TORCH_OPS = ["msda_fwd", "msda_bwd", "swin_window_fwd", "swin_window_bwd", "win_attn_fwd", "win_attn_bwd",
+             "mask_head_fwd", "mask_head_bwd", "attn_bitmask", "masked_xattn_fwd", "masked_xattn_bwd"]
+
+
+def test_torch_library_registers_every_op():
+    import torch
+    assert os.path.exists(L.TORCH_LIB_PATH), "torch ops library not built (run __graft_entry__.build())"
+    ns = L.tops()
+    for name in TORCH_OPS:
+        op = getattr(ns, name).default
+        assert op._schema.name == f"visionseg::{name}"
+    sch = str(ns.msda_fwd.default._schema)
+    assert "Tensor spatial_shapes" in sch and "int im2col_step" in sch
+    # grad_pixel of mask_head_bwd is declared as written in place
+    assert "Tensor(a!) grad_pixel" in str(ns.mask_head_bwd.default._schema)
+    del torch
+
+
+def test_torch_ops_refuse_cpu_tensors():
+    """No CPU kernel is registered: a CPU tensor never reaches a fallback."""
+    import torch
+    ns = L.tops()
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        ns.swin_window_fwd(torch.zeros(1, 4, 4, 8), 4, 0)
+    sh, st = L.level_tensors([(2, 2)])
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        ns.msda_fwd(torch.zeros(1, 4, 1, 32), sh, st, torch.zeros(1, 1, 1, 1, 1, 2), torch.zeros(1, 1, 1, 1, 1), 64)
+    assert sh.tolist() == [[2, 2]] and st.tolist() == [0]

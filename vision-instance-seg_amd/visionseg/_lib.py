@@ -14,6 +14,9 @@ import torch  # load torch (and its HIP runtime) before the kernels library
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvisionseg_hip.so")
+# torch.ops.visionseg.* (csrc/torch_ops.cpp, TORCH_LIBRARY over this C ABI): the §8(b)
+# operator surface; the remaining helper kernels are called through ctypes below
+TORCH_LIB_PATH = os.path.join(_HERE, "libvisionseg_torch.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "visionseg.h")
 
 VS_F32, VS_BF16 = 0, 1
@@ -91,6 +94,7 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_msda_backward_tiled_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
+_tops = None
 
 
 def lib():
@@ -107,6 +111,36 @@ def lib():
             fn.restype = RESTYPES.get(name, _c_int)
         _lib = L
     return _lib
+
+
+def tops():
+    """torch.ops.visionseg, loaded from the in-tree libvisionseg_torch.so (no fallback)."""
+    global _tops
+    if _tops is None:
+        lib()
+        if not os.path.exists(TORCH_LIB_PATH):
+            raise RuntimeError(f"{TORCH_LIB_PATH} is not built: run `make -C vision-instance-seg_amd`")
+        torch.ops.load_library(TORCH_LIB_PATH)
+        _tops = torch.ops.visionseg
+    return _tops
+
+
+_level_tensors = {}
+
+
+def level_tensors(shapes):
+    """CPU int64 (spatial_shapes [L,2], level_start_index [L]) for msda_fwd/bwd, cached per
+    shape list (host tensors: the op reads them without a device sync)."""
+    key = tuple(shapes)
+    t = _level_tensors.get(key)
+    if t is None:
+        starts, s = [], 0
+        for h, w in shapes:
+            starts.append(s)
+            s += h * w
+        t = (torch.tensor(shapes, dtype=torch.int64).reshape(-1, 2), torch.tensor(starts, dtype=torch.int64))
+        _level_tensors[key] = t
+    return t
 
 
 def check(rc: int, what: str):

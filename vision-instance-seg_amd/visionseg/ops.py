@@ -68,14 +68,13 @@ class MSDeformAttnFunction(torch.autograd.Function):
         aw = attention_weights.float().contiguous()
         B, S, H, D = value.shape
         _, Q, _, Lv, P, _ = loc.shape
-        out = torch.empty(B, Q, H * D, device=value.device, dtype=value.dtype)
-        sh, st, tot = _level_arrays(shapes)
+        tot = sum(h * w for h, w in shapes)
         if tot != S:
             raise ValueError(f"spatial shapes cover {tot} positions, value has {S}")
-        nb = (value.numel() + out.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 4
+        sh_t, st_t = L.level_tensors(shapes)
+        nb = (value.numel() + B * Q * H * D) * value.element_size() + (loc.numel() + aw.numel()) * 4
         with timed("msda_fwd", value, bytes_=nb, flops=2.0 * aw.numel() * (4 * D + D)):
-            L.check(L.lib().vs_msda_forward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
-                                            L.ptr(out), B, S, H, D, Lv, Q, P, L.stream(value)), "msda_forward")
+            out = L.tops().msda_fwd(value, sh_t, st_t, loc, aw, int(im2col_step or 64))
         ctx.shapes = shapes
         ctx.save_for_backward(value, loc, aw)
         return out
@@ -86,10 +85,10 @@ class MSDeformAttnFunction(torch.autograd.Function):
         B, S, H, D = value.shape
         _, Q, _, Lv, P, _ = loc.shape
         g = grad_out.to(value.dtype).contiguous()
-        gl = torch.empty_like(loc)
-        ga = torch.empty_like(aw)
-        sh, st, _ = _level_arrays(ctx.shapes)
         if _MSDA_BWD == "tiled":
+            gl = torch.empty_like(loc)
+            ga = torch.empty_like(aw)
+            sh, st, _ = _level_arrays(ctx.shapes)
             # grad_value by destination tiles (csrc/msda.hip msda_tile_*): atomic-free,
             # written once in value's dtype
             gv = torch.empty_like(value)
@@ -104,13 +103,11 @@ class MSDeformAttnFunction(torch.autograd.Function):
                                                        L.ptr(ws), B, S, H, D, Lv, Q, P, L.stream(value)),
                         "msda_backward_tiled")
             return gv, None, None, gl, ga, None
-        gv = torch.empty(B, S, H, D, device=value.device, dtype=torch.float32)
-        nb = (value.numel() + g.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 8 + gv.numel() * 4
+        sh_t, st_t = L.level_tensors(ctx.shapes)
+        nb = (value.numel() + g.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 8 + value.numel() * 4
         with timed("msda_bwd", value, bytes_=nb, flops=2.0 * aw.numel() * 10 * D):
-            L.check(L.lib().vs_msda_backward(L.dtype_code(value), L.ptr(value), sh, st, L.ptr(loc), L.ptr(aw),
-                                             L.ptr(g), L.ptr(gv), L.ptr(gl), L.ptr(ga), B, S, H, D, Lv, Q, P,
-                                             L.stream(value)), "msda_backward")
-        return gv.to(value.dtype), None, None, gl, ga, None
+            gv, gl, ga = L.tops().msda_bwd(value, sh_t, st_t, loc, aw, g, 64)
+        return gv, None, None, gl, ga, None
 
 
 def ms_deform_attn(value, spatial_shapes, sampling_locations, attention_weights):
@@ -207,11 +204,7 @@ class _WindowPartition(torch.autograd.Function):
         L.require_hip(x)
         x = x.contiguous()
         B, H, W, C = x.shape
-        Hp, Wp = _padded(H, ws), _padded(W, ws)
-        out = torch.empty(B * (Hp // ws) * (Wp // ws), ws * ws, C, device=x.device, dtype=x.dtype)
-        with timed("window_partition", x, bytes_=(x.numel() + out.numel()) * x.element_size()):
-            L.check(L.lib().vs_window_partition(L.ptr(x), L.ptr(out), x.element_size(), B, H, W, C, ws, shift,
-                                                L.stream(x)), "window_partition")
+        out = _window_partition_raw(x, ws, shift)
         ctx.meta = (B, H, W, C, ws, shift)
         return out
 
@@ -222,21 +215,15 @@ class _WindowPartition(torch.autograd.Function):
 
 
 def _window_reverse_raw(win, B, H, W, C, ws, shift):
-    out = torch.empty(B, H, W, C, device=win.device, dtype=win.dtype)
-    with timed("window_reverse", win, bytes_=(win.numel() + out.numel()) * win.element_size()):
-        L.check(L.lib().vs_window_reverse(L.ptr(win), L.ptr(out), win.element_size(), B, H, W, C, ws, shift,
-                                          L.stream(win)), "window_reverse")
-    return out
+    with timed("window_reverse", win, bytes_=(win.numel() + B * H * W * C) * win.element_size()):
+        return L.tops().swin_window_bwd(win, B, H, W, ws, shift)
 
 
 def _window_partition_raw(x, ws, shift):
     B, H, W, C = x.shape
-    Hp, Wp = _padded(H, ws), _padded(W, ws)
-    out = torch.empty(B * (Hp // ws) * (Wp // ws), ws * ws, C, device=x.device, dtype=x.dtype)
-    with timed("window_partition", x, bytes_=(x.numel() + out.numel()) * x.element_size()):
-        L.check(L.lib().vs_window_partition(L.ptr(x), L.ptr(out), x.element_size(), B, H, W, C, ws, shift,
-                                            L.stream(x)), "window_partition")
-    return out
+    n_out = B * _padded(H, ws) * _padded(W, ws) * C
+    with timed("window_partition", x, bytes_=(x.numel() + n_out) * x.element_size()):
+        return L.tops().swin_window_fwd(x, ws, shift)
 
 
 class _WindowReverse(torch.autograd.Function):
@@ -285,19 +272,11 @@ class WindowAttentionFunction(torch.autograd.Function):
         C = C3 // 3
         if C != heads * 32 or N != window * window:
             raise ValueError(f"qkv {tuple(qkv.shape)} does not match heads={heads} (x32) window={window}")
-        out = torch.empty(Bw, N, C, device=qkv.device, dtype=qkv.dtype)
-        lse = torch.empty(Bw, heads, N, device=qkv.device, dtype=torch.float32)
         with timed("window_attn_fwd_fp8" if fp8 else "window_attn_fwd", qkv,
-                   bytes_=(qkv.numel() + out.numel()) * qkv.element_size() + lse.numel() * 4,
+                   bytes_=(qkv.numel() + Bw * N * C) * qkv.element_size() + Bw * heads * N * 4,
                    flops=4.0 * Bw * heads * N * N * 32):
-            if fp8:
-                L.check(L.lib().vs_window_attn_forward_fp8(L.ptr(qkv), L.ptr(table), L.ptr(out), L.ptr(lse), Bw,
-                                                           heads, window, shift, nwin_h, nwin_w, float(scale),
-                                                           L.stream(qkv)), "window_attn_forward_fp8")
-            else:
-                L.check(L.lib().vs_window_attn_forward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
-                                                       L.ptr(lse), Bw, heads, window, shift, nwin_h, nwin_w,
-                                                       float(scale), L.stream(qkv)), "window_attn_forward")
+            out, lse = L.tops().win_attn_fwd(qkv, table, heads, window, shift, nwin_h, nwin_w, float(scale),
+                                             bool(fp8))
         ctx.meta = (heads, window, shift, nwin_h, nwin_w, float(scale), rel_table.dtype, bool(fp8))
         ctx.save_for_backward(qkv, table, out, lse)
         return out
@@ -308,23 +287,12 @@ class WindowAttentionFunction(torch.autograd.Function):
         heads, window, shift, nwin_h, nwin_w, scale, tdtype, fp8 = ctx.meta
         Bw, N, C3 = qkv.shape
         g = grad_out.to(qkv.dtype).contiguous()
-        gqkv = torch.empty_like(qkv)
-        T2 = (2 * window - 1) ** 2
-        part = torch.empty(Bw, heads, T2, device=qkv.device, dtype=torch.float32)
         with timed("window_attn_bwd_fp8" if fp8 else "window_attn_bwd", qkv,
                    bytes_=(3 * qkv.numel() + 2 * out.numel()) * qkv.element_size(),
                    flops=10.0 * Bw * heads * N * N * 32):
-            if fp8:
-                L.check(L.lib().vs_window_attn_backward_fp8(L.ptr(qkv), L.ptr(table), L.ptr(out), L.ptr(lse),
-                                                            L.ptr(g), L.ptr(gqkv), L.ptr(part), Bw, heads, window,
-                                                            shift, nwin_h, nwin_w, scale, L.stream(qkv)),
-                        "window_attn_backward_fp8")
-            else:
-                L.check(L.lib().vs_window_attn_backward(L.dtype_code(qkv), L.ptr(qkv), L.ptr(table), L.ptr(out),
-                                                        L.ptr(lse), L.ptr(g), L.ptr(gqkv), L.ptr(part), Bw, heads,
-                                                        window, shift, nwin_h, nwin_w, scale, L.stream(qkv)),
-                        "window_attn_backward")
-        gtable = part.sum(0).t().contiguous().to(tdtype)
+            gqkv, gtable = L.tops().win_attn_bwd(qkv, table, out, lse, g, heads, window, shift, nwin_h, nwin_w,
+                                                 scale, bool(fp8))
+        gtable = gtable.to(tdtype)
         return gqkv, gtable, None, None, None, None, None, None, None
 
 
@@ -351,11 +319,9 @@ class MaskHeadFunction(torch.autograd.Function):
         B, Q, C = E.shape
         if P.shape != (B, height * width, C):
             raise ValueError(f"pixel embedding {tuple(P.shape)} != {(B, height * width, C)}")
-        out = torch.empty(B, Q, height, width, device=E.device, dtype=torch.float32)
-        with timed("mask_head_fwd", E, bytes_=(E.numel() + P.numel()) * E.element_size() + out.numel() * 4,
+        with timed("mask_head_fwd", E, bytes_=(E.numel() + P.numel()) * E.element_size() + B * Q * height * width * 4,
                    flops=2.0 * B * Q * C * height * width):
-            L.check(L.lib().vs_mask_head_forward(L.dtype_code(E), L.ptr(E), L.ptr(P), L.ptr(out), B, Q, C, height,
-                                                 width, L.stream(E)), "mask_head_forward")
+            out = L.tops().mask_head_fwd(E, P, height, width)
         ctx.save_for_backward(E, P)
         ctx.pdtype = pixel_nhwc.dtype
         return out
@@ -369,29 +335,13 @@ class MaskHeadFunction(torch.autograd.Function):
         if E.dtype == torch.bfloat16 and C in (128, 256):
             # the fused kernel takes <= 128 queries: more (MaskDINO's 300 + denoising
             # queries) run as chunks of 128 that accumulate dP in place
-            g = g.float().contiguous()
-            gE = torch.empty_like(E)
             acc = sink is not None and sink.buf is not None
             if sink is not None and not acc:
                 sink.buf = torch.empty_like(P)
             gP = sink.buf if sink is not None else torch.empty_like(P)
-            for q0 in range(0, Q, 128):
-                q1 = min(Q, q0 + 128)
-                whole = q0 == 0 and q1 == Q
-                gc = g if whole else g[:, q0:q1].contiguous()
-                Ec = E if whole else E[:, q0:q1].contiguous()
-                gEc = gE if whole else torch.empty_like(Ec)
-                nq = q1 - q0
-                ws = torch.empty(int(L.lib().vs_mask_head_backward_workspace_bytes(B, nq, C)), device=E.device,
-                                 dtype=torch.uint8)
-                nb = gc.numel() * 4 + (Ec.numel() * 2 + P.numel() * 2) * 2 + (P.numel() * 2 if acc else 0)
-                with timed("mask_head_bwd", E, bytes_=nb, flops=4.0 * B * nq * C * N):
-                    L.check(L.lib().vs_mask_head_backward_ex(L.dtype_code(E), L.ptr(gc), L.ptr(Ec), L.ptr(P),
-                                                             L.ptr(gEc), L.ptr(gP), L.ptr(ws), B, nq, C, N, 1,
-                                                             int(acc), L.stream(E)), "mask_head_backward")
-                if not whole:
-                    gE[:, q0:q1] = gEc
-                acc = True
+            nb = g.numel() * 4 + (E.numel() * 2 + P.numel() * 2) * 2 + (P.numel() * 2 if acc else 0)
+            with timed("mask_head_bwd", E, bytes_=nb, flops=4.0 * B * Q * C * N):
+                gE = L.tops().mask_head_bwd(g, E, P, gP, bool(acc))
             if sink is not None:
                 return gE, None, None, None, None
             return gE, gP.to(ctx.pdtype), None, None, None
@@ -448,10 +398,8 @@ def attn_bitmask(logits, target_hw):
     lg = logits.detach().float().contiguous()
     B, Q, H, W = lg.shape
     th, tw = int(target_hw[0]), int(target_hw[1])
-    words = torch.empty(B, Q, (th * tw + 31) // 32, device=lg.device, dtype=torch.int32)
-    with timed("attn_bitmask", lg, bytes_=min(lg.numel(), B * Q * th * tw * 4) * 4 + words.numel() * 4):
-        L.check(L.lib().vs_attn_bitmask(L.ptr(lg), L.ptr(words), B * Q, H, W, th, tw, L.stream(lg)), "attn_bitmask")
-    return words
+    with timed("attn_bitmask", lg, bytes_=min(lg.numel(), B * Q * th * tw * 4) * 4 + B * Q * ((th * tw + 31) // 32) * 4):
+        return L.tops().attn_bitmask(lg, th, tw)
 
 
 def unpack_bitmask(words, n_keys: int):
@@ -475,15 +423,9 @@ class MaskedAttentionFunction(torch.autograd.Function):
             raise ValueError("masked attention shape mismatch")
         if words.shape != (B, Q, (S + 31) // 32):
             raise ValueError(f"bitmask {tuple(words.shape)} does not cover {S} keys")
-        out = torch.empty_like(q)
-        lse = torch.empty(B, heads, Q, device=q.device, dtype=torch.float32)
-        ws = torch.empty(int(L.lib().vs_masked_attn_workspace_bytes(B, Q, S, heads)), device=q.device,
-                         dtype=torch.uint8)
         nb = (q.numel() * 2 + k.numel() + v.numel()) * q.element_size() + words.numel() * 4
         with timed("masked_attn_fwd", q, bytes_=nb, flops=4.0 * B * heads * Q * S * 32):
-            L.check(L.lib().vs_masked_attn_forward(L.dtype_code(q), L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(words),
-                                                   L.ptr(out), L.ptr(lse), L.ptr(ws), B, Q, S, heads, float(scale),
-                                                   L.stream(q)), "masked_attn_forward")
+            out, lse = L.tops().masked_xattn_fwd(q, k, v, words, heads, float(scale))
         ctx.meta = (heads, float(scale))
         ctx.save_for_backward(q, k, v, words, out, lse)
         return out
@@ -494,16 +436,9 @@ class MaskedAttentionFunction(torch.autograd.Function):
         heads, scale = ctx.meta
         B, Q, C = q.shape
         S = k.shape[1]
-        g = g.to(q.dtype).contiguous()
-        gq, gk, gv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        ws = torch.empty(int(L.lib().vs_masked_attn_workspace_bytes(B, Q, S, heads)), device=q.device,
-                         dtype=torch.uint8)
         nb = (q.numel() * 4 + 2 * k.numel() + 2 * v.numel()) * q.element_size() + words.numel() * 4
         with timed("masked_attn_bwd", q, bytes_=nb, flops=10.0 * B * heads * Q * S * 32):
-            L.check(L.lib().vs_masked_attn_backward(L.dtype_code(q), L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(words),
-                                                    L.ptr(out), L.ptr(lse), L.ptr(g), L.ptr(gq), L.ptr(gk),
-                                                    L.ptr(gv), L.ptr(ws), B, Q, S, heads, scale, L.stream(q)),
-                    "masked_attn_backward")
+            gq, gk, gv = L.tops().masked_xattn_bwd(q, k, v, words, out, lse, g, heads, scale)
         return gq, gk, gv, None, None, None
 
 

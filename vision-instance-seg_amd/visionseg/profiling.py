@@ -5,6 +5,12 @@
 current stream — the same stream the ops pass to the C ABI) and records the launch's
 ALGORITHMIC work (compulsory HBM bytes and/or useful flops, computed from the shapes).
 Disabled (one global check) unless a `KernelTimer` is active.
+
+Eager steps are host-bound (the host enqueues slower than the GPU drains), so a start
+event recorded on an idle stream would also time the host's op preparation.  With
+`spin` (default) a short device spin (`torch.cuda._sleep`) is enqueued before the start
+event: the GPU is still busy with it while the host enqueues the event and the op, so the
+pair brackets only the op's kernels.
 """
 from __future__ import annotations
 
@@ -16,9 +22,13 @@ import torch
 _active = None
 
 
+_SPIN_CYCLES = 200_000   # ~0.1 ms of device clock: longer than one op's host-side enqueue
+
+
 class KernelTimer:
-    def __init__(self):
+    def __init__(self, spin: bool = True):
         self.events = defaultdict(list)
+        self.spin = spin
 
     def __enter__(self):
         global _active
@@ -56,6 +66,9 @@ def timed(name: str, like: torch.Tensor, bytes_: float = 0.0, flops: float = 0.0
     s = torch.cuda.current_stream(like.device)
     a = torch.cuda.Event(enable_timing=True)
     b = torch.cuda.Event(enable_timing=True)
+    if t.spin:
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(_SPIN_CYCLES)
     a.record(s)
     try:
         yield
