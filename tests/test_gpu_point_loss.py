@@ -1,0 +1,58 @@
+"""The set criterion's mask losses through the mask head's factors
+(ops.MatchedPointLogitsFunction) vs autograd through the full logits.
+
+The function replaces the full-size [B, Q, H, W] logits gradients of every decoder step
+(zero except the matched rows) with a scatter into the matched maps and one adjoint GEMM
+pair for all steps; mathematically the same gradient.  f32: <= 1e-5 of max|grad|; bf16
+factors: the adjoint GEMMs round G to bf16 (2^-8 relative) -> 1e-2 of max|grad|.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("S,B,Q,Kc,C,H,W,n", [(3, 2, 20, 3, 128, 32, 48, 300), (10, 4, 100, 3, 256, 64, 64, 1000)])
+def test_matched_point_logits_grad(dtype, tol, S, B, Q, Kc, C, H, W, n):
+    from visionseg import ops
+    g = torch.Generator(device=DEV).manual_seed(S * 100 + Q)
+    E = [torch.randn(B, Q, C, device=DEV, generator=g).to(dtype).requires_grad_() for _ in range(S)]
+    P0 = (torch.randn(B, H * W, C, device=DEV, generator=g) / C ** 0.5).to(dtype).requires_grad_()
+    # distinct matched queries per (step, image): a matching; last slot padded (-> Q-1, no loss)
+    qsel = torch.stack([torch.stack([torch.randperm(Q, device=DEV, generator=g)[:Kc] for _ in range(B)])
+                        for _ in range(S)])
+    coords = torch.rand(S * B * Kc, n, 2, device=DEV, generator=g)
+    wts = torch.randn(S * B * Kc, n, device=DEV, generator=g)
+    keep = torch.ones(S, B, Kc, dtype=torch.bool, device=DEV)
+    keep[:, :, -1] = False
+
+    def loss_of(plog):
+        return (torch.where(keep.reshape(-1, 1), plog * wts, torch.zeros((), device=DEV))).sum()
+
+    # product path: logits from the HIP mask head, loss through the factors
+    masks = [ops.mask_head(e, P0, H, W) for e in E]
+    maps, fac = ops.matched_maps(masks, qsel)
+    assert fac is not None and not maps.requires_grad
+    loss_of(ops.point_logits(maps, coords, qsel, fac)).backward()
+    gE = [e.grad.float().clone() for e in E]
+    gP = P0.grad.float().clone()
+    for t in E + [P0]:
+        t.grad = None
+    # reference: the same sampling, autograd through the full logits (f32 einsum)
+    Ef = [e.detach().float().requires_grad_() for e in E]
+    Pf = P0.detach().float().requires_grad_()
+    full = [torch.einsum("bqc,bnc->bqn", e, Pf).view(B, Q, H, W) for e in Ef]
+    bidx = torch.arange(B, device=DEV)[:, None].expand(B, Kc)
+    pred = torch.stack([full[s][bidx, qsel[s]] for s in range(S)]).reshape(S * B * Kc, 1, H, W)
+    ref = torch.nn.functional.grid_sample(pred, 2 * coords.unsqueeze(2) - 1, align_corners=False).squeeze(3).squeeze(1)
+    loss_of(ref).backward()
+    for a, b in zip(gE, Ef):
+        assert float((a - b.grad).abs().max()) <= tol * float(b.grad.abs().max()) + 1e-30
+    assert float((gP - Pf.grad).abs().max()) <= tol * float(Pf.grad.abs().max())
+    # unmatched query rows get exactly zero
+    hit = torch.zeros(S, B, Q, dtype=torch.bool, device=DEV)
+    hit.scatter_(2, qsel[..., :-1], True)
+    for s in range(S):
+        assert float(gE[s][~hit[s]].abs().max()) == 0.0

@@ -82,11 +82,13 @@ at::Tensor msda_fwd(const at::Tensor& value, const at::Tensor& spatial_shapes, c
   return out;
 }
 
-// -> (grad_value in value's dtype, grad_sampling_loc f32, grad_attn_weight f32)
+// -> (grad_value in value's dtype -- or the f32 accumulator itself with f32_grad_value --,
+//     grad_sampling_loc f32, grad_attn_weight f32)
 std::tuple<at::Tensor, at::Tensor, at::Tensor> msda_bwd(const at::Tensor& value, const at::Tensor& spatial_shapes,
                                                         const at::Tensor& level_start_index,
                                                         const at::Tensor& sampling_loc, const at::Tensor& attn_weight,
-                                                        const at::Tensor& grad_output, int64_t im2col_step) {
+                                                        const at::Tensor& grad_output, int64_t im2col_step,
+                                                        bool f32_grad_value) {
   (void)im2col_step;
   on_device({&value, &sampling_loc, &attn_weight, &grad_output});
   const auto sh = host_i64(spatial_shapes, "spatial_shapes");
@@ -106,7 +108,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> msda_bwd(const at::Tensor& value,
                          as_int(B, "batch"), as_int(S, "S"), as_int(H, "heads"), as_int(D, "channels"),
                          as_int(L, "levels"), as_int(Q, "queries"), as_int(P, "points"), cur_stream(v)),
         "msda_bwd");
-  return {v.scalar_type() == at::kFloat ? gv : gv.to(v.scalar_type()), gl, ga};
+  return {(v.scalar_type() == at::kFloat || f32_grad_value) ? gv : gv.to(v.scalar_type()), gl, ga};
 }
 
 // ---- a2: pad + roll + window partition (and its exact inverse)
@@ -179,7 +181,7 @@ std::tuple<at::Tensor, at::Tensor> win_attn_bwd(const at::Tensor& qkv, const at:
                                                 const at::Tensor& out, const at::Tensor& lse,
                                                 const at::Tensor& grad_out, int64_t heads, int64_t window,
                                                 int64_t shift, int64_t nwin_h, int64_t nwin_w, double scale,
-                                                bool fp8) {
+                                                bool fp8, bool table_partials) {
   on_device({&qkv, &rel_table, &out, &lse, &grad_out});
   check_qkv(qkv, heads, window);
   at::Tensor q = qkv.contiguous(), table = rel_table.to(at::kFloat).contiguous();
@@ -200,7 +202,9 @@ std::tuple<at::Tensor, at::Tensor> win_attn_bwd(const at::Tensor& qkv, const at:
                                   cur_stream(q)),
           "win_attn_bwd");
   }
-  // per-window partial bias gradients summed in a fixed order (deterministic)
+  // per-window partial bias gradients summed in a fixed order (deterministic); or the
+  // partials themselves [Bw, heads, (2ws-1)^2] (table_partials)
+  if (table_partials) return {gqkv, part};
   return {gqkv, part.sum(0).t().contiguous()};
 }
 
@@ -321,13 +325,13 @@ TORCH_LIBRARY(visionseg, m) {
   m.def("msda_fwd(Tensor value, Tensor spatial_shapes, Tensor level_start_index, Tensor sampling_loc, "
         "Tensor attn_weight, int im2col_step) -> Tensor");
   m.def("msda_bwd(Tensor value, Tensor spatial_shapes, Tensor level_start_index, Tensor sampling_loc, "
-        "Tensor attn_weight, Tensor grad_output, int im2col_step) -> (Tensor, Tensor, Tensor)");
+        "Tensor attn_weight, Tensor grad_output, int im2col_step, bool f32_grad_value=False) -> (Tensor, Tensor, Tensor)");
   m.def("swin_window_fwd(Tensor x, int window, int shift) -> Tensor");
   m.def("swin_window_bwd(Tensor windows, int batch, int height, int width, int window, int shift) -> Tensor");
   m.def("win_attn_fwd(Tensor qkv, Tensor rel_table, int heads, int window, int shift, int nwin_h, int nwin_w, "
         "float scale, bool fp8=False) -> (Tensor, Tensor)");
   m.def("win_attn_bwd(Tensor qkv, Tensor rel_table, Tensor out, Tensor lse, Tensor grad_out, int heads, int window, "
-        "int shift, int nwin_h, int nwin_w, float scale, bool fp8=False) -> (Tensor, Tensor)");
+        "int shift, int nwin_h, int nwin_w, float scale, bool fp8=False, bool table_partials=False) -> (Tensor, Tensor)");
   m.def("mask_head_fwd(Tensor mask_embed, Tensor pixel_nhwc, int height, int width) -> Tensor");
   m.def("mask_head_bwd(Tensor grad_logits, Tensor mask_embed, Tensor pixel_nhwc, Tensor(a!) grad_pixel, "
         "bool accumulate) -> Tensor");

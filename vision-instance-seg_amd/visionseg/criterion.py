@@ -238,11 +238,11 @@ class SetCriterion:
             # every (step, image, target slot) pair; padded slots point at query 0 and are
             # masked out of the sums
             qsel = qidx.clamp(max=Q - 1)                                                 # [S,B,Kc]
-            bidx = torch.arange(B, device=dev)[:, None].expand(B, Kc)
-            pred = torch.stack([masks_list[k][bidx, qsel[k]] for k in range(S)])          # [S,B,Kc,H,W]
-            H, W = pred.shape[-2:]
+            # the matched maps [S*B*Kc, 1, H, W]; when the logits came from the mask head the
+            # loss differentiates through its factors (ops.MatchedPointLogitsFunction: no
+            # full-size logits gradient, one adjoint GEMM pair for all steps)
+            pred, fac = ops.matched_maps(masks_list, qsel)
             NP = B * Kc
-            pred = pred.reshape(S * NP, 1, H, W)
             with torch.no_grad():
                 npts = c.train_num_points
                 ns = int(npts * c.oversample_ratio)
@@ -259,7 +259,7 @@ class SetCriterion:
                 tgt = tg.masks.reshape(NP, 1, *tg.masks.shape[-2:]).float()
                 lab_t = _sample(tgt, by_t.reshape(NP, S * npts, 2)).view(NP, S, npts)
                 plab = lab_t.transpose(0, 1).reshape(S * NP, npts)
-            plog = _sample(pred.float(), coords)
+            plog = ops.point_logits(pred, coords, qsel, fac)
             keep = valid.reshape(1, NP).expand(S, NP).reshape(S * NP)
             bce = F.binary_cross_entropy_with_logits(plog, plab, reduction="none").mean(1)  # [S*NP]
             zero = torch.zeros((), device=dev)

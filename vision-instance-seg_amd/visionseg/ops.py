@@ -16,6 +16,7 @@ kernels library is missing or an input is on the CPU.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -106,8 +107,8 @@ class MSDeformAttnFunction(torch.autograd.Function):
         sh_t, st_t = L.level_tensors(ctx.shapes)
         nb = (value.numel() + g.numel()) * value.element_size() + (loc.numel() + aw.numel()) * 8 + value.numel() * 4
         with timed("msda_bwd", value, bytes_=nb, flops=2.0 * aw.numel() * 10 * D):
-            gv, gl, ga = L.tops().msda_bwd(value, sh_t, st_t, loc, aw, g, 64)
-        return gv, None, None, gl, ga, None
+            gv, gl, ga = L.tops().msda_bwd(value, sh_t, st_t, loc, aw, g, 64, True)
+        return gv.to(value.dtype), None, None, gl, ga, None
 
 
 def ms_deform_attn(value, spatial_shapes, sampling_locations, attention_weights):
@@ -290,9 +291,9 @@ class WindowAttentionFunction(torch.autograd.Function):
         with timed("window_attn_bwd_fp8" if fp8 else "window_attn_bwd", qkv,
                    bytes_=(3 * qkv.numel() + 2 * out.numel()) * qkv.element_size(),
                    flops=10.0 * Bw * heads * N * N * 32):
-            gqkv, gtable = L.tops().win_attn_bwd(qkv, table, out, lse, g, heads, window, shift, nwin_h, nwin_w,
-                                                 scale, bool(fp8))
-        gtable = gtable.to(tdtype)
+            gqkv, part = L.tops().win_attn_bwd(qkv, table, out, lse, g, heads, window, shift, nwin_h, nwin_w,
+                                               scale, bool(fp8), True)
+        gtable = part.sum(0).t().contiguous().to(tdtype)
         return gqkv, gtable, None, None, None, None, None, None, None
 
 
@@ -359,7 +360,84 @@ def mask_head(mask_embed, pixel_nhwc, height: int, width: int, sink=None):
     """sink (GradSink): the pixel-embedding gradient of every call sharing the sink is
     summed in one buffer inside the backward kernel (pass `pixel_nhwc` through
     `sink.source(...)` once); without a sink each call returns its own gradient."""
-    return MaskHeadFunction.apply(mask_embed, pixel_nhwc, int(height), int(width), sink)
+    out = MaskHeadFunction.apply(mask_embed, pixel_nhwc, int(height), int(width), sink)
+    # the factors, for losses that only read a few rows of the logits (matched_point_logits)
+    out._vs_src = (mask_embed, pixel_nhwc)
+    return out
+
+
+def mask_head_factors(masks_list):
+    """(E [S,B,Q,C], P [B,HW,C]) if every logits tensor came from `mask_head` with one
+    shared pixel embedding, else None."""
+    srcs = [getattr(m, "_vs_src", None) for m in masks_list]
+    if not srcs or any(s is None for s in srcs) or any(s[1] is not srcs[0][1] for s in srcs):
+        return None
+    return torch.stack([s[0] for s in srcs]), srcs[0][1]
+
+
+class MatchedPointLogitsFunction(torch.autograd.Function):
+    """Point samples of the matched mask logits, differentiable w.r.t. the mask head's
+    factors instead of the logits.
+
+    The set criterion's mask losses (HF:m2f:671-724) read the logits of the MATCHED
+    (step, image, target) pairs at sampled points only, so the gradient of the full
+    [B, Q, H, W] logits of every decoder step is zero except on <= Kc of Q query rows.
+    Autograd through the logits would zero-fill and scatter those full-size gradients and
+    run the mask-head backward over all Q rows, once per step.  Here the backward scatters
+    the point gradients into the matched maps only (G [S, B, Kc, H, W]) and applies the
+    einsum's adjoint to them directly, all steps at once:
+        dE[s, b, q_sk] = G[s, b, k] . P[b]            (one [S*Kc, HW] x [HW, C] GEMM per image)
+        dP[b]          = sum_{s,k} G[s, b, k]^T E[s, b, q_sk]   ([HW, S*Kc] x [S*Kc, C])
+    pred: the matched maps [S*B*Kc, 1, H, W] (detached), coords [S*B*Kc, n, 2] in [0, 1),
+    qsel int64 [S, B, Kc], E [S, B, Q, C], P [B, H*W, C] -> logits at the points [S*B*Kc, n]."""
+
+    @staticmethod
+    def forward(ctx, pred, coords, qsel, E, P):
+        grid = 2.0 * coords.unsqueeze(2) - 1.0
+        out = F.grid_sample(pred, grid, align_corners=False).squeeze(3).squeeze(1)
+        ctx.save_for_backward(grid, qsel, E, P)
+        ctx.map_shape = tuple(pred.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        grid, qsel, E, P = ctx.saved_tensors
+        S, B, Kc = qsel.shape
+        N, _, H, W = ctx.map_shape
+        C = E.shape[-1]
+        like = torch.empty((), device=g.device, dtype=torch.float32).expand(ctx.map_shape)
+        G = torch.ops.aten.grid_sampler_2d_backward(g.float().reshape(N, 1, -1, 1).contiguous(), like, grid, 0, 0,
+                                                    False, [True, False])[0]             # [N,1,H,W] f32
+        Gb = G.view(S, B, Kc, H * W).transpose(0, 1).reshape(B, S * Kc, H * W).to(P.dtype)
+        dEs = torch.bmm(Gb, P)                                                          # [B, S*Kc, C]
+        bq = qsel.transpose(0, 1)                                                       # [B, S, Kc]
+        Esel = torch.gather(E.transpose(0, 1), 2, bq[..., None].expand(B, S, Kc, C))     # [B, S, Kc, C]
+        dP = torch.bmm(Gb.transpose(1, 2), Esel.reshape(B, S * Kc, C).to(P.dtype))        # [B, HW, C]
+        dE = torch.zeros(B, S, E.shape[2], C, device=E.device, dtype=dEs.dtype)
+        dE.scatter_add_(2, bq[..., None].expand(B, S, Kc, C), dEs.view(B, S, Kc, C))
+        return None, None, None, dE.transpose(0, 1).to(E.dtype), dP.to(P.dtype)
+
+
+def matched_maps(masks_list, qsel):
+    """(maps [S*B*Kc, 1, H, W] f32 of mask_list[s][b, qsel[s, b, k]], factors): detached
+    maps + the mask head's factors (E, P) when every step's logits came from `mask_head`
+    (the loss then differentiates through `point_logits` -> MatchedPointLogitsFunction),
+    else the maps with their autograd history and factors None."""
+    S, B, Kc = qsel.shape
+    bidx = torch.arange(B, device=qsel.device)[:, None].expand(B, Kc)
+    fac = mask_head_factors(masks_list)
+    with torch.no_grad() if fac is not None else contextlib.nullcontext():
+        pred = torch.stack([masks_list[s][bidx, qsel[s]] for s in range(S)])            # [S,B,Kc,H,W]
+    H, W = pred.shape[-2:]
+    return pred.reshape(S * B * Kc, 1, H, W).float(), fac
+
+
+def point_logits(maps, coords, qsel, fac):
+    """Logits of `matched_maps` at coords [S*B*Kc, n, 2] in [0,1) (bilinear, zero padding:
+    point_sample HF:m2f:245-275) -> [S*B*Kc, n] f32."""
+    if fac is None:
+        return F.grid_sample(maps, 2.0 * coords.unsqueeze(2) - 1.0, align_corners=False).squeeze(3).squeeze(1)
+    return MatchedPointLogitsFunction.apply(maps, coords, qsel, fac[0], fac[1])
 
 
 class _SinkSource(torch.autograd.Function):
