@@ -16,11 +16,14 @@ def first(key):
 
 
 last_x = max(i for i, r in enumerate(step) if "xattn_bwd" in r[2] or "mask_head_bwd" in r[2])
+bwd0 = first("grid_sampler_2d_backward")
 span = {"dec_fwd": (first("mask_head_fwd"), first("match_cost")),
-        "crit": (first("match_cost"), first("mask_head_bwd")),
-        "dec_bwd": (first("mask_head_bwd"), last_x + 1),
+        "crit": (first("match_cost"), bwd0),
+        "dec_bwd": (bwd0, last_x + 1),
         "pix_bwd": (last_x + 1, first("win_attn_bwd"))}[sys.argv[2]]
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+seg = step[span[0]:span[1]]
+print(f"# {sys.argv[2]}: {len(seg)} launches, {sum(e - s for s, e, _ in seg) / 1e6:.2f} ms busy")
 per = defaultdict(lambda: [0, 0.0])
 for s, e, n in step[span[0]:span[1]]:
     per[n[:110]][0] += 1

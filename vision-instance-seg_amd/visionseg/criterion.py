@@ -268,7 +268,9 @@ class SetCriterion:
             dice = 1 - (2 * (pr * plab).sum(-1) + 1) / (pr.sum(-1) + plab.sum(-1) + 1)
             loss_dice = torch.where(keep, dice, zero).view(S, NP).sum(-1) / nm
         else:
-            loss_mask = sum(m.sum() for m in masks_list) * 0.0 + torch.zeros(S, device=dev)
+            fac = ops.mask_head_factors(masks_list)
+            anchor = (fac[0].float().sum() + fac[1].float().sum()) if fac is not None else sum(m.sum() for m in masks_list)
+            loss_mask = anchor * 0.0 + torch.zeros(S, device=dev)
             loss_dice = torch.zeros(S, device=dev)
         losses = {}
         for s in range(S):

@@ -484,13 +484,17 @@ class Decoder(nn.Module):
         # separate threshold-decision flips (sigmoid(x) < 0.5 at |x| ~ rounding) from arithmetic.
         self.mask_override = None
         self.record = False
+        self.batched_heads = True
 
-    def predict(self, h, mf_nhwc, Hm, Wm, target_hw, sink=None):
+    def embed(self, h, dtype):
+        """(LN(h), mask embedding MLP_3(LN(h))) -- HF:m2f:2040-2048."""
         x = self.norm(h)
         e = F.relu(self.mask_embed[0](x))
         e = F.relu(self.mask_embed[1](e))
-        e = self.mask_embed[2](e)
-        e = e.to(mf_nhwc.dtype)
+        return x, self.mask_embed[2](e).to(dtype)
+
+    def predict(self, h, mf_nhwc, Hm, Wm, target_hw, sink=None):
+        x, e = self.embed(h, mf_nhwc.dtype)
         logits = ops.mask_head(e, mf_nhwc, Hm, Wm, sink=sink)
         words = ops.attn_bitmask(logits, target_hw) if target_hw is not None else None
         return x, logits, words
@@ -500,10 +504,20 @@ class Decoder(nn.Module):
         B, _, Hm, Wm = mask_features.shape
         dev = mask_features.device
         mf = mask_features.to(_compute_dtype(mask_features)).permute(0, 2, 3, 1).reshape(B, Hm * Wm, -1).contiguous()
-        # the mask-head calls sum their pixel-embedding gradient in one buffer (ops.GradSink)
-        sink = ops.GradSink() if (mf.requires_grad and torch.is_grad_enabled() and mf.is_cuda) else None
-        if sink is not None:
-            mf = sink.source(mf)
+        # Batched prediction heads (training on the device): every step's mask embedding and
+        # logits are computed WITHOUT autograd inside the loop (they only steer the next
+        # layer's attention mask and the matching), and the heads run once more, batched
+        # over the S steps, with autograd: norm + 3-layer MLP over [S, B, Q] rows, whose
+        # embeddings E [S, B, Q, C] and mf are the factors the set criterion differentiates
+        # through (logits._vs_src; ops.MatchedPointLogitsFunction).  The backward is one
+        # launch per head instead of S, and the shared weights' gradients need no adds.
+        batched = bool(mf.requires_grad and torch.is_grad_enabled() and mf.is_cuda and self.batched_heads)
+        sink = None
+        if not batched:
+            # the mask-head calls sum their pixel-embedding gradient in one buffer (ops.GradSink)
+            sink = ops.GradSink() if (mf.requires_grad and torch.is_grad_enabled() and mf.is_cuda) else None
+            if sink is not None:
+                mf = sink.source(mf)
         mems, mem_pos, sizes = [], [], []
         for i in range(3):
             # once per level (shared by the decoder rounds): token-major memory and memory + pos
@@ -516,7 +530,15 @@ class Decoder(nn.Module):
         qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
         h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
         n = len(self.layers)
-        inter, logits, words = self.predict(h, mf, Hm, Wm, sizes[0] if n else None, sink)
+
+        def step(hh, target_hw):
+            if not batched:
+                return self.predict(hh, mf, Hm, Wm, target_hw, sink)
+            with torch.no_grad():
+                return self.predict(hh, mf.detach(), Hm, Wm, target_hw)
+
+        hs = [h]
+        inter, logits, words = step(h, sizes[0] if n else None)
         inters, masks = [inter], [logits]
         self.trace = []
         for idx, layer in enumerate(self.layers):
@@ -526,10 +548,16 @@ class Decoder(nn.Module):
             if self.mask_override is not None:
                 words = pack_bitmask(self.mask_override[idx].to(dev))
             h = layer(h, qpos, mems[lvl], mem_pos[lvl], words)
+            hs.append(h)
             nxt = sizes[(idx + 1) % 3] if idx + 1 < n else None
-            inter, logits, words = self.predict(h, mf, Hm, Wm, nxt, sink)
+            inter, logits, words = step(h, nxt)
             inters.append(inter)
             masks.append(logits)
+        if batched:
+            X, E = self.embed(torch.stack(hs), mf.dtype)                                # [S,B,Q,D], [S,B,Q,C]
+            inters = list(X.unbind(0))
+            for s_, m in enumerate(masks):
+                m._vs_src = (E, mf, s_)
         return inters, masks
 
 
@@ -561,7 +589,8 @@ class Mask2Former(nn.Module):
         feats = self.backbone(pixel_values.to(self.backbone.patch_embed.proj.weight.dtype))
         mask_features, ms = self.pixel_decoder(feats)
         inters, masks = self.decoder(ms, mask_features)
-        classes = [self.class_head(x) for x in inters]
+        # one launch for all decoder steps (HF:m2f:2479-2481 per step)
+        classes = list(self.class_head(torch.stack(inters)).unbind(0))
         return masks, classes
 
     @torch.no_grad()

@@ -372,6 +372,9 @@ def mask_head_factors(masks_list):
     srcs = [getattr(m, "_vs_src", None) for m in masks_list]
     if not srcs or any(s is None for s in srcs) or any(s[1] is not srcs[0][1] for s in srcs):
         return None
+    if all(len(s) == 3 and s[0] is srcs[0][0] and s[2] == i for i, s in enumerate(srcs)) \
+            and srcs[0][0].shape[0] == len(srcs):
+        return srcs[0][0], srcs[0][1]        # (E [S,B,Q,C], P): the decoder's batched heads
     return torch.stack([s[0] for s in srcs]), srcs[0][1]
 
 
