@@ -201,6 +201,17 @@ VS_API int vs_mask_head_backward_ex(int dtype, const float* grad_logits, const v
                                     void* grad_P, void* workspace, int batch, int num_queries, int channels,
                                     int height, int width, int accumulate_grad_P, void* stream);
 
+/* Adjoint of the mask losses' point sampling (point_sample = grid_sample bilinear,
+ * align_corners=False, zero padding; HF:m2f:245-275) for the matched (step, image, target)
+ * pairs: grad_points f32 [S*B*K, n] (pair order (s, b, k)), grid f32 [S*B*K, n, 2] (the
+ * sampling grid in [-1, 1], x then y) -> maps f32 [B, S*K, H, W] (pair order (b, s, k)),
+ * every element written: maps[b, s*K + k] = sum over the pair's points of the point's
+ * gradient times its bilinear corner weights (the same float formulas as
+ * grid_sampler_2d_backward).  The maps feed vs_mask_head_backward as grad_logits with
+ * num_queries = S*K, the pairs' mask embeddings gathered as E. */
+VS_API int vs_point_scatter(const float* grad_points, const float* grid, float* maps, int S, int B, int K, int n,
+                            int height, int width, void* stream);
+
 /* Attention bitmask of the next decoder layer (HF:m2f:2049-2055 + row fix 1912-1914):
  * bilinear (align_corners=False) resize of each logits row [H, W] to [th, tw], key k
  * blocked iff sigmoid(v) < 0.5, stored as bit k%32 of words[row, k/32]

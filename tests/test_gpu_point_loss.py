@@ -56,3 +56,26 @@ def test_matched_point_logits_grad(dtype, tol, S, B, Q, Kc, C, H, W, n):
     hit.scatter_(2, qsel[..., :-1], True)
     for s in range(S):
         assert float(gE[s][~hit[s]].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("S,B,K,n,H,W", [(2, 3, 2, 500, 40, 56), (10, 4, 3, 12544, 256, 256), (1, 1, 1, 7, 300, 9)])
+def test_point_scatter_vs_grid_sampler_backward(S, B, K, n, H, W):
+    """vs_point_scatter == torch's grid_sampler_2d_backward (same float weights; only the
+    summation order differs), pairs reordered (s, b, k) -> (b, s, k); points include the
+    border and outside-the-map cases."""
+    from visionseg import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(n)
+    N = S * B * K
+    coords = torch.rand(N, n, 2, device=DEV, generator=g) * 1.2 - 0.1      # some taps outside
+    coords[:, :3] = torch.tensor([[0.0, 0.0], [1.0, 1.0], [0.5 / W, 0.5 / H]], device=DEV)
+    grid = (2.0 * coords.unsqueeze(2) - 1.0).contiguous()
+    gp = torch.randn(N, n, device=DEV, generator=g)
+    ref = torch.ops.aten.grid_sampler_2d_backward(gp.view(N, 1, n, 1), torch.empty(N, 1, H, W, device=DEV), grid,
+                                                  0, 0, False, [True, False])[0]
+    ref = ref.view(S, B, K, H, W).transpose(0, 1).reshape(B, S * K, H, W)
+    out = torch.full((B, S * K, H, W), float("nan"), device=DEV)
+    L.check(L.lib().vs_point_scatter(L.ptr(gp), L.ptr(grid), L.ptr(out), S, B, K, n, H, W, L.stream(gp)),
+            "point_scatter")
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert float((out - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))

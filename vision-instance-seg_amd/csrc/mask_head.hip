@@ -567,6 +567,60 @@ extern "C" int vs_attn_bitmask(const float* logits, uint32_t* words, int rows, i
 
 static int mask_head_bwd_parts(int B) { return B >= 64 ? 1 : (256 + B - 1) / B; }
 
+// ---------------------------------------------------------------------------------
+// Point scatter: the adjoint of the mask losses' bilinear point sampling into dense maps.
+// One workgroup per (pair, band of RB map rows): the band lives in LDS (<= 64 KB), every
+// point of the pair is visited and the corners inside the band are added there (LDS f32
+// atomics: a pair's 12544 points land on distinct cells mostly), then the band is written
+// out once with 16-B stores -- no zero-fill pass and no global atomics (torch's
+// grid_sampler_2d_backward: one global f32 atomic per corner, one lane per row).
+constexpr int kScatterLds = 16384;    // floats per band
+
+__global__ void __launch_bounds__(256) point_scatter_kernel(const float* __restrict__ gp,
+                                                            const float* __restrict__ grid, float* __restrict__ maps,
+                                                            int S, int B, int K, int n, int H, int W, int RB) {
+  __shared__ __attribute__((aligned(16))) float band[kScatterLds];
+  const int pair = blockIdx.x;                       // (s, b, k)
+  const int r0 = blockIdx.y * RB;
+  const int rows = min(RB, H - r0);
+  const int k = pair % K, b = (pair / K) % B, s = pair / (K * B);
+  for (int i = threadIdx.x; i < rows * W; i += 256) band[i] = 0.f;
+  __syncthreads();
+  const float* g = gp + (size_t)pair * n;
+  const float2* xy = reinterpret_cast<const float2*>(grid) + (size_t)pair * n;
+  const float fW = (float)W, fH = (float)H;
+  for (int p = threadIdx.x; p < n; p += 256) {
+    const float go = g[p];
+    const float2 c = xy[p];
+    // grid_sampler_compute_source_index, align_corners = false
+    const float ix = ((c.x + 1.f) * fW - 1.f) / 2.f;
+    const float iy = ((c.y + 1.f) * fH - 1.f) / 2.f;
+    const float ix_nw = floorf(ix), iy_nw = floorf(iy);
+    const float ix_se = ix_nw + 1.f, iy_se = iy_nw + 1.f;
+    const float w_nw = (ix_se - ix) * (iy_se - iy);
+    const float w_ne = (ix - ix_nw) * (iy_se - iy);
+    const float w_sw = (ix_se - ix) * (iy - iy_nw);
+    const float w_se = (ix - ix_nw) * (iy - iy_nw);
+    const int x0 = (int)ix_nw, y0 = (int)iy_nw;
+    const float wts[4] = {w_nw, w_ne, w_sw, w_se};
+#pragma unroll
+    for (int cnr = 0; cnr < 4; ++cnr) {
+      const int yy = y0 + (cnr >> 1), xx = x0 + (cnr & 1);
+      const int ry = yy - r0;
+      if (xx >= 0 && xx < W && yy >= 0 && yy < H && ry >= 0 && ry < rows) atomicAdd(&band[ry * W + xx], wts[cnr] * go);
+    }
+  }
+  __syncthreads();
+  float* out = maps + (((size_t)b * S + s) * K + k) * H * W + (size_t)r0 * W;
+  const int nv = rows * W;
+  if ((nv & 3) == 0) {
+    for (int i = threadIdx.x; i < nv / 4; i += 256)
+      reinterpret_cast<float4*>(out)[i] = reinterpret_cast<const float4*>(band)[i];
+  } else {
+    for (int i = threadIdx.x; i < nv; i += 256) out[i] = band[i];
+  }
+}
+
 extern "C" long long vs_mask_head_backward_workspace_bytes(int B, int Q, int C) {
   return (long long)mask_head_bwd_parts(B) * B * Q * C * 4;
 }
@@ -620,6 +674,21 @@ static int mask_head_backward_impl(int dtype, const float* grad_logits, const vo
   const long long per = (long long)B * Q * C;
   hipLaunchKernelGGL(mask_head_bwd_reduce, dim3((int)((per / 4 + 255) / 256)), dim3(256), 0, st, part, (bf16*)grad_E,
                      parts, per);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_point_scatter(const float* grad_points, const float* grid, float* maps, int S, int B, int K, int n,
+                                int H, int W, void* stream) {
+  VS_CHECK(S > 0 && B > 0 && K > 0 && n >= 0 && H > 0 && W > 0, "bad sizes");
+  VS_CHECK(W <= kScatterLds, "map rows wider than the LDS band");
+  VS_CHECK(maps && (n == 0 || (grad_points && grid)), "null pointer");
+  VS_CHECK(((uintptr_t)grid & 7) == 0 && ((uintptr_t)maps & 15) == 0, "grid must be 8-B and maps 16-B aligned");
+  const int RB = kScatterLds / W < H ? kScatterLds / W : H;
+  const long long pairs = (long long)S * B * K;
+  VS_CHECK(pairs <= 0x7fffffff, "too many pairs");
+  hipLaunchKernelGGL(point_scatter_kernel, dim3((unsigned)pairs, (H + RB - 1) / RB), dim3(256), 0,
+                     (hipStream_t)stream, grad_points, grid, maps, S, B, K, n, H, W, RB);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

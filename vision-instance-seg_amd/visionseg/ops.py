@@ -387,10 +387,13 @@ class MatchedPointLogitsFunction(torch.autograd.Function):
     [B, Q, H, W] logits of every decoder step is zero except on <= Kc of Q query rows.
     Autograd through the logits would zero-fill and scatter those full-size gradients and
     run the mask-head backward over all Q rows, once per step.  Here the backward scatters
-    the point gradients into the matched maps only (G [S, B, Kc, H, W]) and applies the
-    einsum's adjoint to them directly, all steps at once:
-        dE[s, b, q_sk] = G[s, b, k] . P[b]            (one [S*Kc, HW] x [HW, C] GEMM per image)
-        dP[b]          = sum_{s,k} G[s, b, k]^T E[s, b, q_sk]   ([HW, S*Kc] x [S*Kc, C])
+    the point gradients into the matched maps only (G [B, S*Kc, H, W]: vs_point_scatter,
+    LDS bands, no global atomics) and applies the einsum's adjoint to them directly, all
+    steps at once:
+        dE[s, b, q_sk] = G[b, (s, k)] . P[b]                     ([S*Kc, HW] x [HW, C])
+        dP[b]          = sum_{s,k} G[b, (s, k)]^T E[s, b, q_sk]  ([HW, S*Kc] x [S*Kc, C])
+    -- for bf16 the fused mask-head backward kernel with the S*Kc pairs as its queries
+    (one pass over G), else two batched GEMMs.
     pred: the matched maps [S*B*Kc, 1, H, W] (detached), coords [S*B*Kc, n, 2] in [0, 1),
     qsel int64 [S, B, Kc], E [S, B, Q, C], P [B, H*W, C] -> logits at the points [S*B*Kc, n]."""
 
@@ -407,18 +410,33 @@ class MatchedPointLogitsFunction(torch.autograd.Function):
         grid, qsel, E, P = ctx.saved_tensors
         S, B, Kc = qsel.shape
         N, _, H, W = ctx.map_shape
-        C = E.shape[-1]
-        like = torch.empty((), device=g.device, dtype=torch.float32).expand(ctx.map_shape)
-        G = torch.ops.aten.grid_sampler_2d_backward(g.float().reshape(N, 1, -1, 1).contiguous(), like, grid, 0, 0,
-                                                    False, [True, False])[0]             # [N,1,H,W] f32
-        Gb = G.view(S, B, Kc, H * W).transpose(0, 1).reshape(B, S * Kc, H * W).to(P.dtype)
-        dEs = torch.bmm(Gb, P)                                                          # [B, S*Kc, C]
+        Q, C = E.shape[2], E.shape[3]
+        n = g.shape[-1]
+        # point gradients -> dense maps of the matched pairs, [B, S*Kc, H, W] f32
+        # (csrc/mask_head.hip point_scatter_kernel: LDS bands, no global atomics)
+        G = torch.empty(B, S * Kc, H, W, device=g.device, dtype=torch.float32)
+        gc = g.float().contiguous()
+        gr = grid.contiguous()
+        with timed("point_scatter", gc, bytes_=gc.numel() * 12 + G.numel() * 4):
+            L.check(L.lib().vs_point_scatter(L.ptr(gc), L.ptr(gr), L.ptr(G), S, B, Kc, n, H, W, L.stream(gc)),
+                    "point_scatter")
         bq = qsel.transpose(0, 1)                                                       # [B, S, Kc]
-        Esel = torch.gather(E.transpose(0, 1), 2, bq[..., None].expand(B, S, Kc, C))     # [B, S, Kc, C]
-        dP = torch.bmm(Gb.transpose(1, 2), Esel.reshape(B, S * Kc, C).to(P.dtype))        # [B, HW, C]
-        dE = torch.zeros(B, S, E.shape[2], C, device=E.device, dtype=dEs.dtype)
-        dE.scatter_add_(2, bq[..., None].expand(B, S, Kc, C), dEs.view(B, S, Kc, C))
-        return None, None, None, dE.transpose(0, 1).to(E.dtype), dP.to(P.dtype)
+        Esel = torch.gather(E.transpose(0, 1), 2, bq[..., None].expand(B, S, Kc, C)).reshape(B, S * Kc, C)
+        if P.dtype == torch.bfloat16 and C in (128, 256) and S * Kc <= 128:
+            # the fused mask-head backward with the S*Kc matched pairs as its queries:
+            # dE_sel = G.P and dP = G^T.E_sel in one pass over G
+            dP = torch.empty_like(P)
+            Ec = Esel.contiguous()
+            with timed("mask_head_bwd", Ec, bytes_=G.numel() * 4 + (Ec.numel() * 2 + P.numel() * 2) * 2,
+                       flops=4.0 * B * S * Kc * C * H * W):
+                dEs = L.tops().mask_head_bwd(G, Ec, P, dP, False)
+        else:
+            Gb = G.view(B, S * Kc, H * W).to(P.dtype)
+            dEs = torch.bmm(Gb, P)                                                      # [B, S*Kc, C]
+            dP = torch.bmm(Gb.transpose(1, 2), Esel.to(P.dtype))                        # [B, HW, C]
+        dE = torch.zeros(S, B, Q, C, device=E.device, dtype=E.dtype)
+        dE.scatter_add_(2, qsel[..., None].expand(S, B, Kc, C), dEs.view(B, S, Kc, C).transpose(0, 1).to(E.dtype))
+        return None, None, None, dE, dP.to(P.dtype)
 
 
 def matched_maps(masks_list, qsel):
