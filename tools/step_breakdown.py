@@ -3,7 +3,10 @@
 A step is delimited by the flat optimiser step launches (flat_step_kernel): the
 last complete step is the span after the second-to-last optimizer burst up to the end
 of the last one.  Prints busy time by category and the top kernels of that step.
-Usage: python tools/step_breakdown.py <kernel_trace.csv> [top]
+Usage: python tools/step_breakdown.py <kernel_trace.csv> [top] [step]
+step counts back from the end (-1 = last, -3 = the last graph-replayed step of a bench
+run whose final 2 steps are the eager kernel-timing steps).  The timing steps' device
+spin kernels (bench.py keeps the host enqueue out of the measured window) are dropped.
 """
 import csv
 import sys
@@ -30,10 +33,12 @@ def category(name):
 def main():
     path = sys.argv[1]
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    which = int(sys.argv[3]) if len(sys.argv) > 3 else -1
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+            if "spin_kernel" not in r["Kernel_Name"]:
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     opt = [i for i, r in enumerate(rows) if "flat_step_kernel" in r[2]]
     # group optimizer launches into bursts
@@ -47,7 +52,7 @@ def main():
             bursts.append(cur)
             cur = [i]
     bursts.append(cur)
-    a, b = bursts[-2][-1] + 1, bursts[-1][-1]
+    a, b = bursts[which - 1][-1] + 1, bursts[which][-1]
     step = rows[a:b + 1]
     window = (step[-1][1] - step[0][0]) / 1e6
     busy = sum(e - s for s, e, _ in step) / 1e6
@@ -56,7 +61,7 @@ def main():
         cat[category(n)] += (e - s) / 1e6
         per[n][0] += (e - s) / 1e6
         per[n][1] += 1
-    print(f"# last step window {window:.1f} ms under the profiler; kernel busy {busy:.1f} ms, {len(step)} launches")
+    print(f"# step {which} window {window:.1f} ms under the profiler; kernel busy {busy:.1f} ms, {len(step)} launches")
     for k, v in sorted(cat.items(), key=lambda x: -x[1]):
         print(f"#   {k:12s} {v:7.2f} ms")
     for n, (t, c) in sorted(per.items(), key=lambda x: -x[1][0])[:top]:
