@@ -524,7 +524,7 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, win, jitter):
     np.testing.assert_allclose(ld.grad.cpu().numpy(), gl, atol=2e-5 * max(1.0, np.abs(gl).max()), rtol=0)
 
 
-@pytest.mark.parametrize("win", ["tile", "tile-1024", "tile-odd", "sub", "4lvl"])
+@pytest.mark.parametrize("win", ["tile", "tile-1024", "tile-odd", "sub", "4lvl", "ragged"])
 @pytest.mark.parametrize("jitter", [0.0, 0.3, 3.0, 12.0])
 def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
     """bf16 grad_value by the MFMA query-tile kernel (msda_bwd_mfma_wg_kernel: 8 x 8 tiles per
@@ -533,9 +533,11 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
     inputs (VS_MSDA_MFMA=0; both sum in f32: <= 1e-5 of the gradient scale) and (b) the
     oracle (bf16 output rounding: 2^-8 relative + 1e-4).  jitter 12 px drives boxes past
     the 128-cell cap (clipped corners take the direct atomics); "sub" runs 16 consecutive
-    queries of a query subset (Q != S), "4lvl" four levels stored finest first."""
+    queries of a query subset (Q != S), "4lvl" four levels stored finest first, "ragged" a 2x
+    pyramid whose finest level is not a multiple of the 8 x 8 tile."""
     ops = _ops()
     monkeypatch.setattr(ops, "_MSDA_BWD", "carry")
+    monkeypatch.setenv("VS_MSDA_RUN", "16")            # the split kernels at every size
     shapes, B, H = [(8, 8), (16, 16), (32, 32)], 2, 4
     if win == "tile-1024":
         shapes, B, H = [(32, 32), (64, 64), (128, 128)], 1, 8
@@ -543,6 +545,8 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
         shapes = [(9, 13), (18, 26), (35, 51)]
     elif win == "4lvl":
         shapes = [(48, 80), (24, 40), (12, 20), (6, 10)]
+    elif win == "ragged":                              # partial border tiles
+        shapes = [(5, 3), (10, 6), (20, 12)]
     value, loc, w = _encoder_like_inputs(B, shapes, H, 4, seed=13, jitter=jitter)
     if win == "sub":
         idx = torch.randperm(loc.shape[1], generator=torch.Generator().manual_seed(5))[:700].sort().values
@@ -553,7 +557,7 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
     go = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3)).to(torch.bfloat16)
     ref.backward(go.float())
     grads, geo = {}, {}
-    for mf, gm in (("1", "1"), ("1", "0"), ("0", "0")):
+    for mf, gm in (("1", "0"), ("0", "0"), ("1", "1")):
         monkeypatch.setenv("VS_MSDA_MFMA", mf)
         monkeypatch.setenv("VS_MSDA_GEOM", gm)
         vd = value.to(DEV).requires_grad_(True)

@@ -72,6 +72,8 @@ def main():
                 # bf16 data; fused: the single kernel; tiled: the deterministic variant
                 os.environ["VS_MSDA_RUN"] = "0" if mode == "fused" else "16"
                 os.environ["VS_MSDA_MFMA"] = "0" if mode == "binned" else "1"
+                # fwd1: the runtime-P forward kernel instead of the unrolled P = 4 one
+                os.environ["VS_MSDA_FWD4"] = "0" if mode == "fwd1" else "1"
 
                 def fb():
                     o = ops.ms_deform_attn(v, shapes, locr, wr)

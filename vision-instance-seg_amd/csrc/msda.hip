@@ -129,6 +129,90 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ val
   }
 }
 
+// bf16, P == 4, L levels known at compile time (the production shapes): a level's 4
+// sampling locations and weights arrive as three 16-B loads (the rows are 16-B aligned:
+// 32 L and 16 L bytes per group) and the corner rows of two taps at a time are loaded raw
+// (4 VGPRs each) before any is used, so 8 issue back to back instead of one tap's 4
+// (msda_fwd_kernel's runtime-P loop).  Same arithmetic, same order.
+template <int L>
+__global__ void __launch_bounds__(256) msda_fwd4_kernel(const bf16* __restrict__ value,
+                                                         const float* __restrict__ loc,
+                                                         const float* __restrict__ attw,
+                                                         bf16* __restrict__ out, Levels lv, int S,
+                                                         int Hh, int Q, long long groups) {
+  constexpr int P = 4, LP = L * P, V = 8, LPG = kD / V;
+  long long gid = (long long)xcd_swizzle(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (; gid < groups * LPG; gid += stride) {
+    const long long grp = gid / LPG;
+    const int sub = (int)(gid % LPG);
+    const int h = (int)(grp % Hh);
+    const long long b = grp / Hh / Q;
+    const float4* lp = reinterpret_cast<const float4*>(loc + grp * LP * 2);
+    const float4* wp = reinterpret_cast<const float4*>(attw + grp * LP);
+    const size_t rowstride = (size_t)Hh * kD;
+    const bf16* vb = value + ((size_t)b * S * Hh + h) * kD + sub * V;
+    float acc[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll 1
+    for (int l = 0; l < L; ++l) {
+      const int Hl = lv.h[l], Wl = lv.w[l];
+      const bf16* vl = vb + (size_t)lv.start[l] * rowstride;
+      const float fH = (float)Hl, fW = (float)Wl;
+      const float4 w4 = wp[l];
+#pragma unroll 1
+      for (int hf = 0; hf < 2; ++hf) {        // two taps (8 corner rows) in flight at a time
+        const float4 lq = lp[2 * l + hf];
+        const float xs[2] = {lq.x, lq.z}, ys[2] = {lq.y, lq.w};
+        const float as[2] = {hf ? w4.z : w4.x, hf ? w4.w : w4.y};
+        uint4 raw[2][4];
+        float cw[2][4];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const float him = ys[p] * fH - 0.5f;
+          const float wim = xs[p] * fW - 0.5f;
+          const bool in = him > -1.f && wim > -1.f && him < fH && wim < fW;
+          const float fh0 = floorf(him), fw0 = floorf(wim);
+          const int h0 = (int)fh0, w0 = (int)fw0;
+          const float lh = him - fh0, lw = wim - fw0;
+          const float hh = 1.f - lh, hw = 1.f - lw;
+          cw[p][0] = in ? hh * hw : 0.f;        // a tap outside adds nothing (NaN-safe)
+          cw[p][1] = in ? hh * lw : 0.f;
+          cw[p][2] = in ? lh * hw : 0.f;
+          cw[p][3] = in ? lh * lw : 0.f;
+          const bool ok[4] = {in && h0 >= 0 && w0 >= 0, in && h0 >= 0 && w0 + 1 <= Wl - 1,
+                              in && h0 + 1 <= Hl - 1 && w0 >= 0, in && h0 + 1 <= Hl - 1 && w0 + 1 <= Wl - 1};
+          const int off[4] = {h0 * Wl + w0, h0 * Wl + w0 + 1, (h0 + 1) * Wl + w0, (h0 + 1) * Wl + w0 + 1};
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            raw[p][c] = ok[c] ? *reinterpret_cast<const uint4*>(vl + (size_t)off[c] * rowstride)
+                              : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          float val[V];
+#pragma unroll
+          for (int i = 0; i < V; ++i) val[i] = 0.f;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const unsigned wd[4] = {raw[p][c].x, raw[p][c].y, raw[p][c].z, raw[p][c].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              val[2 * j] += cw[p][c] * __uint_as_float(wd[j] << 16);
+              val[2 * j + 1] += cw[p][c] * __uint_as_float(wd[j] & 0xffff0000u);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < V; ++i) acc[i] += as[p] * val[i];
+        }
+      }
+    }
+    Vec16<bf16>::store(out + grp * kD + sub * V, acc);
+  }
+}
+
+
 template <typename T>
 __global__ void __launch_bounds__(256) msda_bwd_kernel(
     const T* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attw,
@@ -1075,7 +1159,21 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
   hipStream_t st = (hipStream_t)stream;
   const long long groups = (long long)B * Q * Hh;
   const int block = 256;
-  if (dtype == VS_BF16) {
+  bool unrolled = P == 4;                    // VS_MSDA_FWD4=0: the runtime-P kernel
+  if (const char* e = getenv("VS_MSDA_FWD4")) unrolled = unrolled && atoi(e) != 0;
+  if (dtype == VS_BF16 && unrolled) {
+    int grid = grid_for(groups * 4, block, 256 * 64);
+#define VS_FWD4(LL)                                                                                          \
+  hipLaunchKernelGGL((msda_fwd4_kernel<LL>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, \
+                     attw, (bf16*)out, lv, S, Hh, Q, groups)
+    switch (L) {
+      case 1: VS_FWD4(1); break;
+      case 2: VS_FWD4(2); break;
+      case 3: VS_FWD4(3); break;
+      default: VS_FWD4(4); break;
+    }
+#undef VS_FWD4
+  } else if (dtype == VS_BF16) {
     int grid = grid_for(groups * 4, block, 256 * 64);
     hipLaunchKernelGGL(msda_fwd_kernel<bf16>, dim3(grid), dim3(block), 0, st, (const bf16*)value,
                        loc, attw, (bf16*)out, lv, S, Hh, Q, L, P, groups);

@@ -166,8 +166,13 @@ class PatchMerging(nn.Module):
         x = x.view(B, H, W, C)
         if H % 2 == 1 or W % 2 == 1:
             x = F.pad(x, (0, 0, 0, W % 2, 0, H % 2))
-        x = torch.cat([x[:, r::2, c::2, :] for c in range(2) for r in range(2)], dim=-1)
-        return self.reduction(self.norm(x.reshape(B, -1, 4 * C)))
+        # HF's cat of the 4 strided quarters (x0 = [0::2, 0::2], x1 = [1::2, 0::2],
+        # x2 = [0::2, 1::2], x3 = [1::2, 1::2]; HF:swin PatchMerging) as one space-to-depth
+        # permute: channel block j = 2 c + r.  Its backward is one copy, where the cat's was
+        # 4 zero-filled slice gradients and 3 full-size adds.
+        Hp, Wp = x.shape[1] // 2, x.shape[2] // 2
+        x = x.view(B, Hp, 2, Wp, 2, C).permute(0, 1, 3, 4, 2, 5).reshape(B, Hp * Wp, 4 * C)
+        return self.reduction(self.norm(x))
 
 
 class Stage(nn.Module):
