@@ -35,20 +35,16 @@ for _p in (ROOT, os.path.join(ROOT, "vision-instance-seg_amd")):
         sys.path.insert(0, _p)
 
 # Vendor-GEMM solution table (PyTorch TunableOp over hipBLASLt/rocBLAS, incl. split-K for
-# the tall-K weight-gradient GEMMs), tuned on MI355X for this workload and shipped
-# in-tree; read-only unless --gemm-tuning tune.  Must be set before torch loads.
-_TUNE_FILE = os.path.join(ROOT, "vision-instance-seg_amd", "visionseg", "tuning", "tunableop_mi355x.csv")
+# the tall-K weight-gradient GEMMs), tuned on MI355X for the bench configs and shipped
+# in-tree: loaded read-only in main() (visionseg.linear.load_gemm_table).  --gemm-tuning
+# tune re-tunes instead; that mode's environment must be set before torch loads.
 _gt = "file"
 for _i, _a in enumerate(sys.argv):
     if _a == "--gemm-tuning" and _i + 1 < len(sys.argv):
         _gt = sys.argv[_i + 1]
     elif _a.startswith("--gemm-tuning="):
         _gt = _a.split("=", 1)[1]
-if _gt == "file" and os.path.exists(_TUNE_FILE):
-    os.environ.setdefault("PYTORCH_TUNABLEOP_ENABLED", "1")
-    os.environ.setdefault("PYTORCH_TUNABLEOP_TUNING", "0")
-    os.environ.setdefault("PYTORCH_TUNABLEOP_FILENAME", _TUNE_FILE)
-elif _gt == "tune":
+if _gt == "tune":
     os.environ.setdefault("PYTORCH_TUNABLEOP_ENABLED", "1")
     os.environ.setdefault("PYTORCH_TUNABLEOP_TUNING", "1")
     os.environ.setdefault("PYTORCH_TUNABLEOP_FILENAME", os.path.join(ROOT, "gpurun_out", "tunableop_results%d.csv"))
@@ -325,6 +321,10 @@ def main():
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if a.gemm_tuning == "file":
+        from visionseg.linear import load_gemm_table
+        if not load_gemm_table():
+            a.gemm_tuning = "file (not loaded)"
     if a.arch == "maskdino":
         from visionseg.maskdino import MaskDINO, MaskDINOConfig, MaskDINOCriterion
         if a.queries == 100:

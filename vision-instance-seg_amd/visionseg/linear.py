@@ -22,6 +22,27 @@ import os
 
 # split when K is at least this many tokens; chunks never drop below MIN_CHUNK rows
 MIN_TOKENS = int(os.environ.get("VS_SPLITK_MIN_TOKENS", "16384"))
+
+GEMM_TABLE = os.environ.get("VS_GEMM_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                             "tuning", "tunableop_mi355x.csv")
+
+
+def load_gemm_table(path: str = GEMM_TABLE) -> bool:
+    """Use the shipped vendor-GEMM solution table (PyTorch TunableOp over hipBLASLt /
+    rocBLAS, tuned on MI355X for the bench configs by tools/retune.sh) for every later
+    GEMM of this process, without tuning: shapes it lacks run the default heuristic.
+
+    Loaded through the Python API on purpose: TunableOp inserts the device ordinal into a
+    PYTORCH_TUNABLEOP_FILENAME without "%d" ("x.csv" -> "x0.csv" on device 0), so the
+    environment variable alone never read this file, and a "%d" name would need one copy
+    per GPU.  Returns False (nothing enabled) when the file or a device is missing."""
+    if not (os.path.exists(path) and torch.cuda.is_available()):
+        return False
+    from torch.cuda import tunable
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.set_filename(path, False)
+    return bool(tunable.read_file(path))
 MIN_CHUNK = 1024
 TARGET_TILES = 768          # aim for this many 128x128 output tiles over all chunks
 
