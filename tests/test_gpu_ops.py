@@ -759,14 +759,18 @@ def test_window_attention_bf16_large_windows_vs_oracle(ws, shift, heads, nWh, nW
     assert e <= 2e-2 * float(tr.grad.abs().max()), e
 
 
-@pytest.mark.parametrize("kernel", ["mfma", "scalar"])
+@pytest.mark.parametrize("kernel", ["mfma", "mfma-4blk", "scalar"])
 @pytest.mark.parametrize("B,Q,S", [(2, 100, 4096), (1, 100, 1000), (2, 7, 300), (1, 128, 16384), (1, 130, 512)])
 def test_masked_attention_bf16_fwd_bwd_vs_oracle(monkeypatch, kernel, B, Q, S):
     """bf16 masked cross-attention forward + backward (MFMA kernels, and the scalar ones
     via VS_XATTN_SCALAR=1) vs the f32 oracle on the same bf16-rounded inputs: ragged key
-    counts, fully blocked rows (unblocked by the producer's rule), Q > 128 (scalar bwd)."""
+    counts, fully blocked rows (unblocked by the producer's rule), Q > 128 (scalar bwd);
+    "mfma-4blk": four 128-key blocks per backward workgroup (dQ partial accumulated over
+    the blocks, chunks that end past S), as the C2 decoder's 128^2 level runs."""
     if kernel == "scalar":
         monkeypatch.setenv("VS_XATTN_SCALAR", "1")
+    elif kernel == "mfma-4blk":
+        monkeypatch.setenv("VS_XATTN_BLOCKS", "4")
     ops = _ops()
     heads = 8
     q, k, v, blocked, words = _xattn_case(B, Q, S, heads, seed=Q + S, dtype=torch.bfloat16)

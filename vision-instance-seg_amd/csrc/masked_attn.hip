@@ -16,7 +16,7 @@
 // partials (m, l, o) into O and the log-sum-exp.  Backward: dQ per chunk (lane per
 // query, P recomputed from the saved lse, partials summed over chunks by a combine
 // kernel — deterministic) and dK/dV with one lane per key over all queries staged in
-// LDS.  Scalar f32 FMA datapath (first correct path; MFMA version is the next step).
+// LDS.  Those are the f32 (parity) kernels; bf16 runs the MFMA kernels further below.
 #include "mfma_util.h"
 
 #include <algorithm>
@@ -147,35 +147,50 @@ __global__ void __launch_bounds__(kQTile) xattn_fwd_partial(const T* __restrict_
   pml[prow * 2 + 1] = l;
 }
 
-// one lane per (b, h, q, channel-quad): merge chunk partials
+// merge chunk partials: 32 lanes per (b, h, q) = 8 channel quads x 4 chunk phases (lane
+// phase s takes chunks s, s + 4, ...), reduced across the phases by shuffles -- 4x the
+// lanes of one-lane-per-quad, whose serial walk over 64 chunks (C2's 128^2 level) left
+// the launch latency-bound on 100 workgroups
 template <typename T>
 __global__ void __launch_bounds__(256) xattn_fwd_combine(const float* __restrict__ po, const float* __restrict__ pml,
                                                          T* __restrict__ out, float* __restrict__ lse, XGeom g) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long rows = (long long)g.B * g.heads * g.Q;
-  if (gid >= rows * 8) return;
-  const int quad = (int)(gid & 7);
-  const long long row = gid >> 3;  // (b, h, q)
-  const int i = (int)(row % g.Q);
-  const long long bh = row / g.Q;
+  const int quad = (int)(gid & 7), ph = (int)((gid >> 3) & 3);
+  const long long row = gid >> 5;  // (b, h, q); the grid is whole waves, rows beyond are idle
+  const bool live = row < rows;
+  const long long rr = live ? row : 0;
+  const int i = (int)(rr % g.Q);
+  const long long bh = rr / g.Q;
   const int h = (int)(bh % g.heads);
   const long long b = bh / g.heads;
   float M = -INFINITY;
-  for (int c = 0; c < g.nchunk; ++c) M = fmaxf(M, pml[((bh * g.nchunk + c) * g.Q + i) * 2]);
+#pragma unroll 4
+  for (int c = ph; c < g.nchunk; c += 4) M = fmaxf(M, pml[((bh * g.nchunk + c) * g.Q + i) * 2]);
+  M = fmaxf(M, __shfl_xor(M, 8, 64));
+  M = fmaxf(M, __shfl_xor(M, 16, 64));
   float lsum = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int c = 0; c < g.nchunk; ++c) {
+#pragma unroll 4
+  for (int c = ph; c < g.nchunk; c += 4) {
     const size_t pr = (bh * g.nchunk + c) * g.Q + i;
-    const float mc = pml[pr * 2];
-    if (mc == -INFINITY) continue;
-    const float w = __expf(mc - M);
-    lsum += w * pml[pr * 2 + 1];
+    const float2 ml = *reinterpret_cast<const float2*>(pml + pr * 2);
     const float4 v = reinterpret_cast<const float4*>(po + pr * kD)[quad];
+    if (ml.x == -INFINITY) continue;         // a chunk whose keys are all blocked
+    const float w = __expf(ml.x - M);
+    lsum += w * ml.y;
     acc[0] += w * v.x; acc[1] += w * v.y; acc[2] += w * v.z; acc[3] += w * v.w;
   }
+#pragma unroll
+  for (int sh = 8; sh <= 16; sh <<= 1) {
+    lsum += __shfl_xor(lsum, sh, 64);
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) acc[e2] += __shfl_xor(acc[e2], sh, 64);
+  }
+  if (!live || ph != 0) return;
   const float inv = 1.f / lsum;
   T* dst = out + ((size_t)b * g.Q + i) * (g.heads * kD) + h * kD + quad * 4;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) dst[e] = from_f32<T>(acc[e] * inv);
+  for (int e2 = 0; e2 < 4; ++e2) dst[e2] = from_f32<T>(acc[e2] * inv);
   if (quad == 0) lse[row] = M + __logf(lsum);
 }
 
@@ -337,8 +352,10 @@ __global__ void __launch_bounds__(256) xattn_bwd_dkdv(const T* __restrict__ q, c
 // softmax in registers and accumulates O^T += V^T P^T with P^T taken straight from the
 // accumulators (permuted k).  Chunk partials (o, m, l) go to xattn_fwd_combine.
 //
-// Backward: workgroup = (128-key chunk, head, image), all queries (<= 128, padded) in
-// the workgroup, wave w owns keys 32w..32w+31.  S = Q K^T and dP = dO V^T with QUERIES on
+// Backward: workgroup = (chunk of 1-4 128-key blocks, head, image), all queries (<= 128,
+// padded) in the workgroup, wave w owns keys 32w..32w+31 of each block; the query tiles
+// are walked one at a time (one tile's S / dP accumulators live: 2 waves/SIMD instead
+// of 1) and the dQ partial accumulates over the chunk's blocks in registers.  S = Q K^T and dP = dO V^T with QUERIES on
 // rows, so dV^T = dO^T P and dK^T = scale Q^T dS take P / dS straight from registers
 // (dO^T, Q^T read from LDS in the permuted query order); dS goes to LDS once so that
 // wave w can form the chunk's dQ partial for query tile w (dQ = scale dS K), summed over
@@ -463,16 +480,11 @@ __global__ void __launch_bounds__(256) xattn_bwd_mfma(const bf16* __restrict__ q
   const int chunk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int C = g.heads * kD, Q = g.Q;
-  const int jbeg = chunk * kBChunk;
-  const int n = min(kBChunk, g.S - jbeg);
+  const int t = threadIdx.x & 127;
+  const bool second = threadIdx.x >= 128;
   const bf16* qb = q + (size_t)b * Q * C + h * kD;
   const bf16* ob = gout + (size_t)b * Q * C + h * kD;
-  const bf16* kb = k + ((size_t)b * g.S + jbeg) * C + h * kD;
-  const bf16* vb = v + ((size_t)b * g.S + jbeg) * C + h * kD;
-  {
-    const int t = threadIdx.x & 127;
-    const bool second = threadIdx.x >= 128;
-    // Q^T / dO^T (threads 0..127 / 128..255, one query each)
+  {  // Q^T / dO^T (threads 0..127 / 128..255, one query each), lse and D rows: once per chunk
     const bf16* src = second ? ob : qb;
     short* dstT = second ? sDoT : sQT;
 #pragma unroll
@@ -481,15 +493,30 @@ __global__ void __launch_bounds__(256) xattn_bwd_mfma(const bf16* __restrict__ q
 #pragma unroll
       for (int j = 0; j < 8; ++j) dstT[(8 * c + j) * kBPadQ + t] = x[j];
     }
+    if (!second) {
+      sL[t] = t < Q ? lse[((size_t)b * g.heads + h) * Q + t] : 0.f;
+      sD[t] = t < Q ? Dbuf[((size_t)b * g.heads + h) * Q + t] : 0.f;
+    }
+  }
+  // the chunk is g.chunk keys = g.chunk / kBChunk blocks of 128; the dQ partial of query
+  // tile `wave` accumulates over the blocks in registers and is written once per chunk
+  f32x16_t dq;
+  zero16(dq);
+  const int nblk = g.chunk / kBChunk;
+  for (int kb = 0; kb < nblk; ++kb) {
+    const int jbeg = chunk * g.chunk + kb * kBChunk;
+    if (jbeg >= g.S) break;                     // uniform over the workgroup
+    const int n = min(kBChunk, g.S - jbeg);
+    const bf16* kb_ = k + ((size_t)b * g.S + jbeg) * C + h * kD;
+    const bf16* vb = v + ((size_t)b * g.S + jbeg) * C + h * kD;
+    __syncthreads();                            // the previous block's K^T / dS / words are read
     if (!second) {   // K^T, one key each
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const bf16x8_t x = t < n ? ld8(kb + (size_t)t * C + 8 * c) : zero8();
+        const bf16x8_t x = t < n ? ld8(kb_ + (size_t)t * C + 8 * c) : zero8();
 #pragma unroll
         for (int j = 0; j < 8; ++j) sKT[(8 * c + j) * kBPadK + t] = x[j];
       }
-      sL[t] = t < Q ? lse[((size_t)b * g.heads + h) * Q + t] : 0.f;
-      sD[t] = t < Q ? Dbuf[((size_t)b * g.heads + h) * Q + t] : 0.f;
     } else {
 #pragma unroll
       for (int c = 0; c < kBChunk / 32; ++c) {
@@ -497,77 +524,73 @@ __global__ void __launch_bounds__(256) xattn_bwd_mfma(const bf16* __restrict__ q
         sW[t][c] = (t < Q && wi < g.nw) ? words[((size_t)b * Q + t) * g.nw + wi] : 0xffffffffu;
       }
     }
-  }
-  __syncthreads();
-  // S = Q K^T and dP = dO V^T for queries (rows, 4 tiles) x this wave's 32 keys (cols)
-  const int kl = wave * 32 + r;                 // key within the chunk (this lane's column)
-  const bool kok = kl < n;
-  f32x16_t sacc[4], dacc[4];
+    __syncthreads();
+    // per query tile qt (32 rows): S = Q K^T and dP = dO V^T against this wave's 32 keys
+    // (cols), P and dS, then dV^T += dO^T P and dK^T += Q^T dS over the tile's queries --
+    // one tile's S / dP accumulators live at a time (4 at once cost 1 wave per SIMD)
+    const int kl = wave * 32 + r;               // key within the block (this lane's column)
+    const bool kok = kl < n;
+    bf16x8_t kf[2], vf[2];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    zero16(sacc[t]);
-    zero16(dacc[t]);
-  }
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    const bf16x8_t kf = kok ? ld8(kb + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
-    const bf16x8_t vf = kok ? ld8(vb + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
-#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      kf[st] = kok ? ld8(kb_ + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
+      vf[st] = kok ? ld8(vb + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
+    }
+    f32x16_t dv, dk;
+    zero16(dv);
+    zero16(dk);
+#pragma unroll 1
     for (int qt = 0; qt < 4; ++qt) {
-      const int qr = 32 * qt + r;
-      const bf16x8_t qa = qr < Q ? ld8(qb + (size_t)qr * C + 16 * st + 8 * hh) : zero8();
-      const bf16x8_t da = qr < Q ? ld8(ob + (size_t)qr * C + 16 * st + 8 * hh) : zero8();
-      sacc[qt] = mfma16(qa, kf, sacc[qt]);
-      dacc[qt] = mfma16(da, vf, dacc[qt]);
-    }
-  }
-  // P and dS (queries on rows)
+      f32x16_t sacc, dacc;
+      zero16(sacc);
+      zero16(dacc);
+      const int qr0 = 32 * qt + r;
 #pragma unroll
-  for (int qt = 0; qt < 4; ++qt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qr = 32 * qt + crow(i, hh);
-      const bool ok = kok && qr < Q && !((sW[qr][wave] >> r) & 1u);
-      const float p = ok ? __expf(sacc[qt][i] * g.scale - sL[qr]) : 0.f;
-      sacc[qt][i] = p;
-      dacc[qt][i] = p * (dacc[qt][i] - sD[qr]);
-      sDS[qr * kBPadK + kl] = bf16_bits(dacc[qt][i]);
-    }
-  // dV^T = dO^T P, dK^T = Q^T dS (k over queries, permuted order)
-  f32x16_t dv, dk;
-  zero16(dv);
-  zero16(dk);
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int qt = t >> 1, th = t & 1;
-    const int base = 32 * qt + 16 * th + 4 * hh;
-    dv = mfma16(ld_perm(sDoT + r * kBPadQ, base), pack8(sacc[qt], 8 * th), dv);
-    dk = mfma16(ld_perm(sQT + r * kBPadQ, base), pack8(dacc[qt], 8 * th), dk);
-  }
-  if (kok) {
-    bf16* gvr = gv + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
-    bf16* gkr = gk + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
-#pragma unroll
-    for (int grp = 0; grp < 4; ++grp) {
-      bf16x4_t a, c;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a[e] = bf16_bits(dv[4 * grp + e]);
-        c[e] = bf16_bits(dk[4 * grp + e] * g.scale);
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8_t qa = qr0 < Q ? ld8(qb + (size_t)qr0 * C + 16 * st + 8 * hh) : zero8();
+        const bf16x8_t da = qr0 < Q ? ld8(ob + (size_t)qr0 * C + 16 * st + 8 * hh) : zero8();
+        sacc = mfma16(qa, kf[st], sacc);
+        dacc = mfma16(da, vf[st], dacc);
       }
-      *reinterpret_cast<bf16x4_t*>(gvr + 8 * grp + 4 * hh) = a;
-      *reinterpret_cast<bf16x4_t*>(gkr + 8 * grp + 4 * hh) = c;
-    }
-  }
-  __syncthreads();                               // every wave's dS is in LDS
-  // dQ partial of query tile `wave`: dQ = scale * dS K (k over the chunk's keys)
-  f32x16_t dq;
-  zero16(dq);
 #pragma unroll
-  for (int t = 0; t < kBChunk / 16; ++t) {
-    const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sDS + (wave * 32 + r) * kBPadK + 16 * t + 8 * hh);
-    const bf16x8_t bb = *reinterpret_cast<const bf16x8_t*>(sKT + r * kBPadK + 16 * t + 8 * hh);
-    dq = mfma16(a, bb, dq);
+      for (int i = 0; i < 16; ++i) {
+        const int qr = 32 * qt + crow(i, hh);
+        const bool ok = kok && qr < Q && !((sW[qr][wave] >> r) & 1u);
+        const float p = ok ? __expf(sacc[i] * g.scale - sL[qr]) : 0.f;
+        sacc[i] = p;
+        dacc[i] = p * (dacc[i] - sD[qr]);
+        sDS[qr * kBPadK + kl] = bf16_bits(dacc[i]);
+      }
+#pragma unroll
+      for (int th = 0; th < 2; ++th) {           // k over the tile's queries, permuted order
+        const int base = 32 * qt + 16 * th + 4 * hh;
+        dv = mfma16(ld_perm(sDoT + r * kBPadQ, base), pack8(sacc, 8 * th), dv);
+        dk = mfma16(ld_perm(sQT + r * kBPadQ, base), pack8(dacc, 8 * th), dk);
+      }
+    }
+    if (kok) {
+      bf16* gvr = gv + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
+      bf16* gkr = gk + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        bf16x4_t av, ck;
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          av[e2] = bf16_bits(dv[4 * grp + e2]);
+          ck[e2] = bf16_bits(dk[4 * grp + e2] * g.scale);
+        }
+        *reinterpret_cast<bf16x4_t*>(gvr + 8 * grp + 4 * hh) = av;
+        *reinterpret_cast<bf16x4_t*>(gkr + 8 * grp + 4 * hh) = ck;
+      }
+    }
+    __syncthreads();                            // every wave's dS is in LDS
+    // dQ of query tile `wave` += dS K over the block's keys
+#pragma unroll
+    for (int tt = 0; tt < kBChunk / 16; ++tt) {
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sDS + (wave * 32 + r) * kBPadK + 16 * tt + 8 * hh);
+      const bf16x8_t bb = *reinterpret_cast<const bf16x8_t*>(sKT + r * kBPadK + 16 * tt + 8 * hh);
+      dq = mfma16(a, bb, dq);
+    }
   }
   const size_t prow0 = (((size_t)b * g.heads + h) * g.nchunk + chunk) * Q;
 #pragma unroll
@@ -629,7 +652,7 @@ extern "C" int vs_masked_attn_forward(int dtype, const void* q, const void* k, c
     dim3 grid(g.nchunk, heads, B * ((Q + 127) / 128));
     hipLaunchKernelGGL(xattn_fwd_mfma, grid, dim3(256), 0, st, (const bf16*)q, (const bf16*)k, (const bf16*)v, words,
                        po, pml, g);
-    const long long crows = (long long)B * heads * Q * 8;
+    const long long crows = (long long)B * heads * Q * 32;
     hipLaunchKernelGGL(xattn_fwd_combine<bf16>, dim3((int)((crows + 255) / 256)), dim3(256), 0, st, po, pml,
                        (bf16*)out, lse, g);
     VS_LAUNCH_CHECK();
@@ -642,7 +665,7 @@ extern "C" int vs_masked_attn_forward(int dtype, const void* q, const void* k, c
   const int nqg = (Q + kQTile - 1) / kQTile;
   dim3 grid(g.nchunk, heads, B * nqg);
   const size_t lds = 2 * kStage * kD * sizeof(float);
-  const long long crows = (long long)B * heads * Q * 8;
+  const long long crows = (long long)B * heads * Q * 32;
   const int cgrid = (int)((crows + 255) / 256);
   if (dtype == VS_BF16) {
     hipLaunchKernelGGL(xattn_fwd_partial<bf16>, grid, dim3(kQTile), lds, st, (const bf16*)q, (const bf16*)k,
@@ -668,7 +691,13 @@ extern "C" int vs_masked_attn_backward(int dtype, const void* q, const void* k, 
            "null pointer");
   VS_CHECK(B > 0 && Q > 0 && S > 0 && heads > 0, "bad sizes");
   if (dtype == VS_BF16 && Q <= kBQ && xattn_use_mfma()) {
-    XGeom g = mfma_geom(B, Q, S, heads, scale, kBChunk);
+    // 128-key blocks, several per workgroup once there are >= 2048 blocks in the grid
+    // (the Q^T / dO^T staging and the dQ partial are per workgroup; VS_XATTN_BLOCKS=n
+    // forces n blocks per workgroup, for tests)
+    const long long nb128 = (long long)B * heads * ((S + kBChunk - 1) / kBChunk);
+    int per = nb128 >= 4096 ? 4 : nb128 >= 2048 ? 2 : 1;     // C2's 128^2 level: 4 (kbench 0.174 -> 0.135 ms)
+    if (const char* e = getenv("VS_XATTN_BLOCKS")) per = std::max(1, std::min(16, atoi(e)));
+    XGeom g = mfma_geom(B, Q, S, heads, scale, kBChunk * per);
     float* pdq = (float*)workspace;
     float* Dbuf = pdq + (size_t)B * heads * g.nchunk * Q * kD + (size_t)B * heads * g.nchunk * Q * 2;
     hipStream_t st = (hipStream_t)stream;

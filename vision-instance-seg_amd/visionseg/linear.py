@@ -43,6 +43,8 @@ def load_gemm_table(path: str = GEMM_TABLE) -> bool:
     tunable.tuning_enable(False)
     tunable.set_filename(path, False)
     return bool(tunable.read_file(path))
+
+
 MIN_CHUNK = 1024
 TARGET_TILES = 768          # aim for this many 128x128 output tiles over all chunks
 
