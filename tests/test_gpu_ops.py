@@ -1097,3 +1097,32 @@ def test_residual_sink_plain_paths_keep_gradients():
         lin.zero_grad()
     err = float((res[0] - res[1]).abs().max())
     assert err <= 1e-4 * float(res[0].abs().max()), err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_linear_relu_fused_vs_torch(dtype):
+    """Encoder-FFN fc1 + ReLU with bias and ReLU in the GEMM epilogue
+    (linear._LinearReluFn: torch._addmm_activation, backward masked by the OUTPUT and fused
+    with the bias column sums) vs F.relu(F.linear) in f64 on the same rounded inputs:
+    output, dX, dW, db.  Tolerances: f32 1e-4 of the scale; bf16 2^-7 relative + a
+    bf16-rounding term of the scale."""
+    from visionseg.linear import linear_relu_tokens
+    g = torch.Generator().manual_seed(7)
+    T, Ci, Co = 2 * 8192 + 24, 256, 1024
+    x = (torch.randn(1, T, Ci, generator=g)).to(dtype)
+    w = (torch.randn(Co, Ci, generator=g) / 16).to(dtype)
+    b = (torch.randn(Co, generator=g) / 4).to(dtype)
+    go = torch.randn(1, T, Co, generator=g).to(dtype)
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+    ref = F.relu(F.linear(xr, wr, br))
+    ref.backward(go.double())
+    xd, wd, bd = (t.to(DEV).requires_grad_(True) for t in (x, w, b))
+    out = linear_relu_tokens(xd, wd, bd)
+    assert out.grad_fn is not None and "LinearRelu" in type(out.grad_fn).__name__
+    out.backward(go.to(DEV))
+    tol = 1e-4 if dtype == torch.float32 else 2 ** -7
+    for got, exp in ((out, ref), (xd.grad, xr.grad), (wd.grad, wr.grad), (bd.grad, br.grad)):
+        e = (got.detach().double().cpu() - exp.detach()).abs()
+        scale = float(exp.detach().abs().max())
+        assert float(e.max()) <= tol * scale + (1e-6 if dtype == torch.float32 else 2 ** -8 * scale), \
+            (float(e.max()), scale)

@@ -420,6 +420,62 @@ def linear_tokens(x, w, b=None, sink=None):
     return _LinearFn.apply(x, w, b, sink)
 
 
+class _LinearReluFn(torch.autograd.Function):
+    """relu(x W^T + b) with the bias and the ReLU in the GEMM epilogue
+    (torch._addmm_activation: hipBLASLt RELU_BIAS), so the pre-activation is never
+    written and re-read by a separate ReLU pass (HF:m2f:1080-1082, the encoder FFN).
+    Backward: ReLU's derivative from the OUTPUT (y > 0 exactly where x W^T + b > 0), one
+    HIP pass for dY * [y > 0] and its column sums (= the bias gradient), then the dX GEMM
+    (with the residual sink's gradient, beta = 1) and the split-K weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, sink=None):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = torch._addmm_activation(bias, x2, weight.t(), use_gelu=False)
+        ctx.save_for_backward(x, weight, y)
+        ctx.sink = sink
+        if sink is not None:
+            sink.arm()
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y = ctx.saved_tensors
+        N = y.shape[-1]
+        M = y.shape[0]
+        gy2 = gy.reshape(M, N).to(y.dtype).contiguous()
+        gp = torch.empty_like(y)
+        cs = torch.empty(N, device=y.device, dtype=y.dtype)
+        ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=y.device, dtype=torch.uint8)
+        L.check(L.lib().vs_act_backward_colsum(L.dtype_code(y), 0, L.ptr(gy2), L.ptr(y), L.ptr(gp), L.ptr(cs),
+                                               L.ptr(ws), M, N, L.stream(y)), "act_backward_colsum")
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gres = ctx.sink.take() if ctx.sink is not None else None
+            if gres is not None:
+                gx = torch.addmm(gres.reshape(M, -1).to(gp.dtype), gp, weight.to(gp.dtype)).view(x.shape)
+            else:
+                gx = (gp @ weight.to(gp.dtype)).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            gw = weight_grad(gp, x.reshape(-1, x.shape[-1]).to(gp.dtype), weight.dtype)
+        if ctx.needs_input_grad[2]:
+            gb = cs.to(weight.dtype)
+        return gx, gw, gb, None
+
+
+def linear_relu_tokens(x, w, b, sink=None):
+    """relu(F.linear(x, w, b)) -- fused on token-heavy device tensors (see _LinearReluFn);
+    the unfused composition otherwise (`sink`: ops.ResidualSink, armed only when fused)."""
+    from . import ops
+    tokens = x.numel() // max(1, x.shape[-1])
+    N = w.shape[0]
+    if (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and b is not None and tokens >= MIN_TOKENS
+            and not torch.is_autocast_enabled() and x.dtype == w.dtype == b.dtype
+            and x.dtype in (torch.float32, torch.bfloat16) and N % 8 == 0 and N <= 2048 and x.is_contiguous()):
+        return _LinearReluFn.apply(x, w, b, sink)
+    return ops.activation(linear_tokens(x, w, b, sink), "relu")
+
+
 class TokenLinear(nn.Linear):
     """nn.Linear whose backward splits the token axis of dW (see module docstring)."""
 

@@ -28,8 +28,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_tokens, plane_projection,
-                     small_linear, value_query_projection, reattach_level_embed)
+from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_relu_tokens, linear_tokens,
+                     plane_projection, small_linear, value_query_projection, reattach_level_embed)
 
 
 @dataclass
@@ -313,7 +313,8 @@ class EncoderLayer(nn.Module):
         # the dX GEMM of the branch's first op (ops.ResidualSink), not by autograd
         s1, s2 = ops.ResidualSink(), ops.ResidualSink()
         _, h = self.norm1.add_forward(h, self.attn(h, pos, ref, shapes, norm, level, s1), s1)
-        _, h = self.norm2.add_forward(h, self.fc2(ops.activation(self.fc1(h, s2), "relu")), s2)
+        f = linear_relu_tokens(h, self.fc1.weight, self.fc1.bias, s2)                # bias + ReLU in the GEMM
+        _, h = self.norm2.add_forward(h, self.fc2(f), s2)
         return h
 
 
