@@ -249,6 +249,28 @@ def sine_pos_embed(B, H, W, num_feats, device, dtype=torch.float32, temperature=
     return torch.cat((py, px), dim=3).permute(0, 3, 1, 2)
 
 
+_SINE_CACHE: dict = {}
+
+
+def sine_pos_tokens(B, H, W, num_feats, device, dtype):
+    """sine_pos_embed in the token-major layout [B, H*W, 2*num_feats] and `dtype`, made
+    once per (shape, device, dtype): it depends on nothing else, so the training step does
+    not recompute it (~15 kernels and 67 MB f32 intermediates per 128x128 level).  Never
+    cached while a HIP graph is being captured (the entry would live in the graph's pool);
+    the trainer's eager warm-up steps fill the cache first."""
+    key = (B, H, W, num_feats, str(device), dtype)
+    t = _SINE_CACHE.get(key)
+    if t is None:
+        with torch.no_grad():
+            t = sine_pos_embed(B, H, W, num_feats, device).to(dtype).flatten(2).transpose(1, 2).contiguous()
+        capturing = t.is_cuda and torch.cuda.is_current_stream_capturing()
+        if not capturing:
+            if len(_SINE_CACHE) >= 32:
+                _SINE_CACHE.clear()
+            _SINE_CACHE[key] = t
+    return t
+
+
 def reference_points(shapes, B, device, dtype=torch.float32):
     """HF:m2f:1127-1156 with valid ratios 1 -> [B, S, L, 2]."""
     refs = []
@@ -376,6 +398,7 @@ class PixelDecoder(nn.Module):
         self.output = ConvGN(Fd, Fd, 3, False, relu=True, nchw=True)
         self.mask_proj = nn.Conv2d(Fd, cfg.mask_feature_size, kernel_size=1)
         self._norm_cache = {}
+        self._ref_cache = {}
 
     def forward(self, feats):
         Fd = self.cfg.feature_size
@@ -385,17 +408,20 @@ class PixelDecoder(nn.Module):
             embeds.append(self.extra(feats[-1]))
         for lvl, x in enumerate(feats[::-1][:3]):
             embeds.append(self.input_proj[lvl](x))
-        pos = [sine_pos_embed(e.shape[0], e.shape[2], e.shape[3], Fd // 2, dev).to(e.dtype) for e in embeds]
+        pos = [sine_pos_tokens(e.shape[0], e.shape[2], e.shape[3], Fd // 2, dev, e.dtype) for e in embeds]
         shapes = [(int(e.shape[2]), int(e.shape[3])) for e in embeds]
         B = embeds[0].shape[0]
         h = torch.cat([e.flatten(2).transpose(1, 2) for e in embeds], 1)
         # position term with detached level-embedding rows: the layers route the level
         # embedding's gradient themselves (per-level column sums, linear.value_query_projection)
         lvl = self.level_embed.detach()
-        p = torch.cat([q.flatten(2).transpose(1, 2) + lvl[i].view(1, 1, -1).to(q.dtype)
-                       for i, q in enumerate(pos)], 1)
+        p = torch.cat([q + lvl[i].view(1, 1, -1).to(q.dtype) for i, q in enumerate(pos)], 1)
         level = (self.level_embed, [Hl * Wl for (Hl, Wl) in shapes])
-        ref = reference_points(shapes, B, dev)
+        ref = self._ref_cache.get((tuple(shapes), B, str(dev)))
+        if ref is None:       # constant per shape set, like the sine embedding (sine_pos_tokens)
+            ref = reference_points(shapes, B, dev)
+            if not (ref.is_cuda and torch.cuda.is_current_stream_capturing()):
+                self._ref_cache[(tuple(shapes), B, str(dev))] = ref
         key = (tuple(shapes), dev)
         norm = self._norm_cache.get(key)
         if norm is None:      # made once per shape set: no host->device copy inside a graph capture
@@ -529,7 +555,7 @@ class Decoder(nn.Module):
             # once per level (shared by the decoder rounds): token-major memory and memory + pos
             f, (Hl, Wl) = ms_feats[i]                       # token-major [B, Hl*Wl, C]
             sizes.append((int(Hl), int(Wl)))
-            pos = sine_pos_embed(B, Hl, Wl, d // 2, dev).to(f.dtype).flatten(2).transpose(1, 2)
+            pos = sine_pos_tokens(B, Hl, Wl, d // 2, dev, f.dtype)
             m = f + self.level_embed.weight[i][None, None, :].to(f.dtype)
             mems.append(m)
             mem_pos.append(m + pos)
