@@ -1126,3 +1126,30 @@ def test_linear_relu_fused_vs_torch(dtype):
         scale = float(exp.detach().abs().max())
         assert float(e.max()) <= tol * scale + (1e-6 if dtype == torch.float32 else 2 ** -8 * scale), \
             (float(e.max()), scale)
+
+
+@pytest.mark.parametrize("S,n", [(3, 36864), (16, 65536), (33, 4100), (256, 36864)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_splitk_sum_vs_torch(monkeypatch, S, n, dtype):
+    """Split-K epilogue (csrc/norm.hip vs_splitk_sum): out = sum_s part[s] + extra, f32
+    sums rounded once -- the phased kernel (S >= 16: 8 partial phases per element quad,
+    combined in phase order) and the one-thread-per-quad kernel (VS_SPLITK_PHASED=0) vs
+    torch's f64 sum: f32 summation-order error only (<= 1e-6 of the summed magnitudes),
+    then one rounding to the output dtype."""
+    from visionseg import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(S)
+    part = torch.randn(S, n, device=DEV, generator=g)
+    extra = torch.randn(n, device=DEV, generator=g)
+    exp = part.double().sum(0) + extra.double()
+    mag = part.double().abs().sum(0) + extra.double().abs()
+    outs = []
+    for phased in ("1", "0"):
+        monkeypatch.setenv("VS_SPLITK_PHASED", phased)
+        out = torch.empty(n, device=DEV, dtype=dtype)
+        L.check(L.lib().vs_splitk_sum(L.dtype_code(out), L.ptr(part), S, n, L.ptr(extra), L.ptr(out), L.stream(out)),
+                "splitk_sum")
+        torch.cuda.synchronize()
+        outs.append(out)
+        ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 0.0
+        err = (out.double() - exp).abs()
+        assert bool((err <= 1e-6 * mag + ulp * exp.abs()).all()), (phased, float(err.max()))

@@ -450,6 +450,50 @@ __global__ void __launch_bounds__(kThreads) splitk_sum_kernel(const float* __res
   }
 }
 
+// Many partials (S >= 16, the split-K weight gradients of the token-heavy Linears: up to
+// 256 chunks): the S loop is the latency.  A workgroup takes 256 / PH element quads and
+// PH phases; phase p sums partials p, p + PH, ... (two rows in flight), and the phases
+// are combined in LDS in phase order (fixed order: deterministic).  PH = 8 gives 8x the
+// workgroups of splitk_sum_kernel for the same output.
+template <typename T, int PH>
+__global__ void __launch_bounds__(kThreads) splitk_sum_phased_kernel(const float* __restrict__ part,
+                                                                     const float* __restrict__ extra,
+                                                                     T* __restrict__ out, int S, long long n4) {
+  constexpr int QPB = kThreads / PH;         // element quads per workgroup
+  __shared__ float4 red[PH][QPB];
+  const int qi = threadIdx.x % QPB, ph = threadIdx.x / QPB;
+  const long long i = (long long)blockIdx.x * QPB + qi;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  if (i < n4) {
+    const float4* p = reinterpret_cast<const float4*>(part) + i;
+    int s = ph;
+    for (; s + PH < S; s += 2 * PH) {
+      const float4 v0 = p[(size_t)s * n4], v1 = p[(size_t)(s + PH) * n4];
+      a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+      b.x += v1.x; b.y += v1.y; b.z += v1.z; b.w += v1.w;
+    }
+    if (s < S) {
+      const float4 v = p[(size_t)s * n4];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[ph][qi] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  __syncthreads();
+  if (ph == 0 && i < n4) {
+    float4 r = extra ? reinterpret_cast<const float4*>(extra)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < PH; ++k) {
+      const float4 v = red[k][qi];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    T* o = out + i * 4;
+    o[0] = from_f32<T>(r.x);
+    o[1] = from_f32<T>(r.y);
+    o[2] = from_f32<T>(r.z);
+    o[3] = from_f32<T>(r.w);
+  }
+}
+
 // pick (G, K): a power-of-two group of G <= 16 lanes (else <= 64) with K chunks per lane,
 // fewest idle chunk slots G*K - nch first, then the smaller K (registers).  C = 96
 // (nch 12): G = 4, K = 3 -- no idle lanes -- where the smallest-K rule gave G = 16, K = 1
@@ -689,6 +733,21 @@ extern "C" int vs_splitk_sum(int dtype, const float* partials, int num_parts, lo
   if (n == 0) return VS_OK;
   hipStream_t st = (hipStream_t)stream;
   const long long n4 = n / 4;
+  bool phased = num_parts >= 16;             // VS_SPLITK_PHASED=0: one thread per quad
+  if (const char* e = getenv("VS_SPLITK_PHASED")) phased = phased && atoi(e) != 0;
+  if (phased) {
+    constexpr int PH = 8;
+    const long long blocks = (n4 + kThreads / PH - 1) / (kThreads / PH);
+    VS_CHECK(blocks < (1LL << 31), "split-K output too large");
+    if (dtype == VS_BF16)
+      hipLaunchKernelGGL((splitk_sum_phased_kernel<bf16, PH>), dim3((unsigned)blocks), dim3(kThreads), 0, st,
+                         partials, extra, (bf16*)out, num_parts, n4);
+    else
+      hipLaunchKernelGGL((splitk_sum_phased_kernel<float, PH>), dim3((unsigned)blocks), dim3(kThreads), 0, st,
+                         partials, extra, (float*)out, num_parts, n4);
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
   const int grid = (int)std::min<long long>((n4 + kThreads - 1) / kThreads, 256 * 16);
   if (dtype == VS_BF16)
     hipLaunchKernelGGL(splitk_sum_kernel<bf16>, dim3(grid), dim3(kThreads), 0, st, partials, extra, (bf16*)out,
