@@ -398,6 +398,9 @@ __global__ void __launch_bounds__(kThreads) colsum_partials_kernel(const float* 
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (col < N) {
     int r = sl;
+    // unrolled: up to 16 independent loads in flight per thread (512 partials = 16 trips
+    // of 4 at one load batch each were the launch's latency); same summation order
+#pragma unroll 4
     for (; r + 24 < nb; r += 32) {
       a0 += part[(size_t)r * N + col];
       a1 += part[(size_t)(r + 8) * N + col];
