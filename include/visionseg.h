@@ -292,18 +292,26 @@ VS_API int vs_column_sum_segments(int dtype, const void* x, float* out, void* wo
  *   master    [total] f32 weights, state1 [total] f32 (SGD momentum / Adam exp_avg),
  *   state2    [total] f32 (Adam exp_avg_sq; unused, may be NULL, for SGD);
  *   weights_bf16 [total] bf16 working weights written from the updated master (or NULL).
- * table: int32 [num_chunks][4] = {start (multiple of 8), len, first chunk of the
- * parameter, chunks of the parameter}; hyper: f32 [num_chunks][2] = {lr multiplier,
- * weight decay}.  optimizer 0 = SGD (torch semantics: d = g + wd*p; buf = d on the first
- * step, else momentum*buf + d; p -= lr*buf), 1 = AdamW (torch semantics).  clip 0 = none,
+ * grad_flags [num_params] (grad_dtype, or NULL = every parameter has a gradient): > 0.5
+ *             when the parameter got a gradient this step on some rank (the all-reduce sums
+ *             them); a parameter without one is skipped entirely, as torch.optim skips a
+ *             parameter whose .grad is None (no decay, no state update).
+ * table: int32 [num_chunks][5] = {start (multiple of 8), len, first chunk of the
+ * parameter, chunks of the parameter, parameter index}; hyper: f32 [num_chunks][2] = {lr
+ * multiplier, weight decay}.  optimizer 0 = SGD (torch semantics: d = g + wd*p; buf = d on
+ * the parameter's first step, else momentum*buf + d; p -= lr*buf), 1 = AdamW (torch
+ * semantics, bias correction by the parameter's own step count).  clip 0 = none,
  * 1 = per parameter, 2 = one global norm; scale = min(1, clip_value / (norm + clip_eps)).
  * lr: device f32 scalar (base lr, scheduler-owned); step: device f32 counter, advanced by
- * one at the start of the call (step == 1 is the first step).  Deterministic; 2 launches. */
+ * one at the start of the call; param_steps: f32 [num_params], each flagged parameter's
+ * count advanced by one (== 1 on its first step).  Deterministic; 2 launches (3 with the
+ * global clip).  workspace: vs_flat_step_workspace_bytes(num_chunks) bytes. */
 VS_API long long vs_flat_step_workspace_bytes(int num_chunks);
-VS_API int vs_flat_step(int grad_dtype, const void* grad, float grad_scale, float* master, float* state1,
-                        float* state2, void* weights_bf16, const int* table, const float* hyper, int num_chunks,
-                        int optimizer, int clip, float clip_value, float clip_eps, float momentum, float beta1,
-                        float beta2, float eps, const float* lr, float* step, void* workspace, void* stream);
+VS_API int vs_flat_step(int grad_dtype, const void* grad, const void* grad_flags, float grad_scale, float* master,
+                        float* state1, float* state2, void* weights_bf16, const int* table, const float* hyper,
+                        int num_chunks, int optimizer, int clip, float clip_value, float clip_eps, float momentum,
+                        float beta1, float beta2, float eps, const float* lr, float* step, float* param_steps,
+                        void* workspace, void* stream);
 
 /* ---- In-graph external events (csrc/stream.hip) ----------------------------------------
  * For the gradient all-reduce overlapped with a graph-replayed backward (no reference

@@ -524,8 +524,12 @@ class RefCriterion:
         unc = -torch.abs(_sample_point(logits, coords))
         nu = int(c.importance_sample_ratio * c.train_num_points)
         nr = c.train_num_points - nu
-        idx = torch.topk(unc[:, 0, :], k=nu, dim=1)[1]
-        idx = idx + (ns * torch.arange(nb, dtype=torch.long, device=logits.device))[:, None]
+        select = getattr(self.point_source, "select", None)
+        if select is not None and keyed is not None:   # test hook: decisions keyed (step, image, target)
+            idx = select(unc[:, 0, :], nu, torch.full_like(keyed[2], keyed[0]), keyed[2], keyed[3])
+        else:
+            idx = torch.topk(unc[:, 0, :], k=nu, dim=1)[1]
+        idx = idx +(ns * torch.arange(nb, dtype=torch.long, device=logits.device))[:, None]
         coords = coords.view(-1, 2)[idx.view(-1), :].view(nb, nu, 2)
         if nr > 0:
             coords = torch.cat([coords, self._draw("rand", nr, nb, keyed, logits.device)], dim=1)
@@ -534,7 +538,10 @@ class RefCriterion:
     def single(self, masks, classes, mask_labels, class_labels, step=0, steps=1):
         c = self.cfg
         idx = self.match(masks, classes, mask_labels, class_labels)
-        nm = torch.clamp(torch.as_tensor(float(sum(len(x) for x in class_labels))), min=1)
+        forced = getattr(self.point_source, "forced_match", None)
+        if forced is not None:       # test hook: record / replay the matching of each step
+            idx = forced(step, idx)
+        nm =torch.clamp(torch.as_tensor(float(sum(len(x) for x in class_labels))), min=1)
         bi = torch.cat([torch.full_like(s, i) for i, (s, _) in enumerate(idx)])
         si = torch.cat([s for s, _ in idx])
         ti = torch.cat([t for _, t in idx])

@@ -1,7 +1,9 @@
 """CPU emulation of csrc/optim.hip vs_flat_step over a visionseg.optim.FlatOptimizer's
 buffers (test infrastructure: the product step is HIP-only).  Per parameter:
 clip_grad_norm_ (detectron2 "norm") or one global norm, then torch.optim SGD / AdamW
-arithmetic — the same formulas as oracle/ref_solver.py's torch optimisers."""
+arithmetic — the same formulas as oracle/ref_solver.py's torch optimisers; parameters
+whose gradient flag is clear are skipped (torch.optim: .grad None), AdamW's bias
+correction counts each parameter's own steps."""
 from __future__ import annotations
 
 import math
@@ -14,16 +16,22 @@ def flat_step_reference(opt):
     s = opt.solver
     lay = opt.layout
     g = opt.reduced_grads().double() / opt.world
+    has = (opt.flags.float() > 0.5).tolist()          # torch.optim skips parameters without .grad
     opt.step_count += 1
-    t = float(opt.step_count)
+    for i, h in enumerate(has):
+        if h:
+            opt.param_steps[i] += 1
     views = [(o, n) for (o, n) in lay.offsets]
     scale = [1.0] * len(views)
     if s.clip_type == "norm":
         scale = [min(1.0, s.clip_value / (float(g[o:o + n].norm()) + 1e-6)) for o, n in views]
     elif s.clip_type == "full_model":
-        tot = math.sqrt(sum(float(g[o:o + n].pow(2).sum()) for o, n in views))
+        tot = math.sqrt(sum(float(g[o:o + n].pow(2).sum()) for (o, n), h in zip(views, has) if h))
         scale = [min(1.0, s.clip_value / (tot + 1e-6))] * len(views)
     for i, ((o, n), (_, _, lrm, wd)) in enumerate(zip(views, lay.entries)):
+        if not has[i]:
+            continue
+        t = float(opt.param_steps[i])
         gi = g[o:o + n] * scale[i]
         p = opt.master[o:o + n].double()
         lr = float(opt.lr) * lrm

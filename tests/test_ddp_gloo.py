@@ -108,11 +108,16 @@ def test_ddp_matches_single_process(monkeypatch, optimizer, clip):
                                                                    [cc[i:i + 1] for cc in c], a, b)[0]
                                                     for i in range(2)) / 2, {}),
                  _solver(optimizer, clip), device="cpu", distributed=False)
+    init = {n: p.detach().clone() for n, p in TinyNet().named_parameters()}
     for _ in range(3):
         tr.step(data, None, None)
     ref = tr.opt.master.detach()
     assert torch.allclose(f0, ref, atol=1e-6), float((f0 - ref).abs().max())
-    # the unused parameter received zero gradients: only weight decay moved it
+    # the unused parameter got no gradient on any rank: skipped (torch.optim semantics: no
+    # weight decay, no momentum), so it still holds its initial value on every replica
+    (o, n), = [off for off, nm in zip(tr.opt.layout.offsets, tr.opt.names) if nm == "unused"]
+    for flat in (f0, f1, ref):
+        assert torch.equal(flat[o:o + n], init["unused"])
     assert not torch.equal(ref, torch.zeros_like(ref))
 
 
@@ -152,4 +157,8 @@ def test_flat_layout_buckets_and_groups():
         assert lo == prev and hi > lo
         prev = hi
         assert all(lay.bucket_of[i] == lay.buckets.index((lo, hi, ids)) for i in ids)
-    assert prev == lay.total and len(lay.buckets) > 1
+    assert prev == lay.size and len(lay.buckets) > 1
+    # the gradient flags sit after the parameters, inside the last bucket
+    assert lay.flag_off == lay.total and lay.size >= lay.total + lay.num_params
+    assert lay.buckets[-1][0] <= lay.flag_off and lay.buckets[-1][1] == lay.size
+    assert lay.table[:, 4].tolist() == lay.chunk_param

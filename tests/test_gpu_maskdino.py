@@ -31,7 +31,7 @@ def test_forward_structure():
     boxes = masks_to_boxes(tg.masks)
     out = m(imgs, tg, boxes)
     pad = out["dn"]["pad"]
-    assert pad == (cfg.dn_num // 4) * 4
+    assert pad == cfg.dn_num
     S = cfg.dec_layers + 1
     assert len(out["classes"]) == len(out["masks"]) == len(out["boxes"]) == S
     for c, mk, b in zip(out["classes"], out["masks"], out["boxes"]):

@@ -406,6 +406,9 @@ def test_msda_encoder_shapes_backward_vs_oracle(cfg, dtype):
         gvr = vr.grad
         err = (vd.grad.float().cpu() - gvr).abs()
         assert bool((err <= gvr.abs() * 2 ** -8 + 1e-4).all()), float(err.max())
+        # grad_loc / grad_attn of the production bf16 kernel vs the oracle (bf16 value and
+        # grad_out are exact in f32; f32 sums in another order + fma'd coordinates)
+        _check_geo_vs_oracle(ld.grad.cpu(), lr.grad, wd.grad.cpu(), wr.grad)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -469,6 +472,33 @@ def test_token_linear_split_k_grads(dtype, K):
     for got, exp in ((lin.weight.grad, ew), (lin.bias.grad, eb), (x.grad.reshape(-1, 192), ex)):
         rel = float((got.double() - exp).abs().max() / exp.abs().max())
         assert rel <= tol, rel
+
+
+# grad_loc / grad_attn of the bf16 MSDA backward vs the oracle.  value and grad_out are
+# bf16 (exact in f32), so the products are the oracle's; what differs is the f32
+# summation order over 32 channels x 4 corners and the coordinate x*W-0.5 (one fma on the
+# GPU, mul + sub in grid_sample), which can put a tap that sits within an ulp of a cell
+# edge into the neighbouring cell: grad_loc jumps there (d bilinear / d loc is
+# discontinuous at cell edges).  Bound: every element within 1e-4 of the tensor's max
+# |value| + 2^-8 relative, except at most 1e-4 of the grad_loc entries (edge taps)
+# which must still be within 5e-2 of the max.
+GEO_ATOL, GEO_RTOL, EDGE_FRAC, EDGE_ATOL = 1e-4, 2 ** -8, 1e-4, 5e-2
+
+
+def _check_geo_vs_oracle(gl, gl_ref, gw, gw_ref):
+    out = []
+    for name, got, exp, edges in (("grad_loc", gl, gl_ref, True), ("grad_attn", gw, gw_ref, False)):
+        sc = max(float(exp.abs().max()), 1e-12)
+        err = (got.float() - exp).abs()
+        bad = err > GEO_ATOL * sc + GEO_RTOL * exp.abs()
+        nbad = int(bad.sum())
+        out.append(f"{name} max|err|/max {float(err.max()) / sc:.2e} ({nbad} of {err.numel()} beyond tol)")
+        if edges:
+            assert nbad <= EDGE_FRAC * err.numel(), out[-1]
+            assert float(err.max()) <= EDGE_ATOL * sc, out[-1]
+        else:
+            assert nbad == 0, out[-1]
+    print("; ".join(out))
 
 
 def _encoder_like_inputs(B, shapes, H, P, seed, jitter):
@@ -571,10 +601,9 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
     for a, b in zip(geo[("1", "1")], geo[("1", "0")]):
         sc = float(b.abs().max())
         assert float((a - b).abs().max()) <= 1e-4 * sc, float((a - b).abs().max()) / sc
-    # and vs the oracle (f32 value, bf16-rounded inputs): as test_msda_encoder_shapes_backward_vs_oracle
-    e = wr.grad.numpy()
-    np.testing.assert_allclose(geo[("1", "1")][1].numpy(), e, atol=2e-5 * max(1.0, np.abs(e).max()) * 400,
-                               rtol=2 ** -6)
+    # and vs the oracle (f32 value, bf16-rounded inputs): grad_loc and grad_attn of the
+    # production kernel (GEOM fused into the band walk)
+    _check_geo_vs_oracle(geo[("1", "1")][0], lr.grad, geo[("1", "1")][1], wr.grad)
     scale = float(vr.grad.abs().max())
     for mf in ("0", "1"):
         err = (grads[mf] - vr.grad).abs()
@@ -624,10 +653,13 @@ def test_msda_destination_backward_vs_oracle(monkeypatch, case, dtype, mode):
     else:
         err = (vd.grad.float().cpu() - vr.grad).abs()
         assert bool((err <= vr.grad.abs() * 2 ** -8 + 1e-4).all()), float(err.max())
-    if loc.shape[1]:
+    if loc.shape[1] and dtype == torch.float32:
         e = wr.grad.numpy()
-        np.testing.assert_allclose(wd.grad.cpu().numpy(), e, atol=2e-5 * max(1.0, np.abs(e).max()) * (
-            1 if dtype == torch.float32 else 400), rtol=0 if dtype == torch.float32 else 2 ** -6)
+        np.testing.assert_allclose(wd.grad.cpu().numpy(), e, atol=2e-5 * max(1.0, np.abs(e).max()), rtol=0)
+        gl = lr.grad.numpy()
+        np.testing.assert_allclose(ld.grad.cpu().numpy(), gl, atol=2e-5 * max(1.0, np.abs(gl).max()), rtol=0)
+    elif loc.shape[1]:
+        _check_geo_vs_oracle(ld.grad.cpu(), lr.grad, wd.grad.cpu(), wr.grad)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

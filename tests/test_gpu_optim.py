@@ -40,12 +40,21 @@ def test_flat_step_vs_oracle_solver(dtype, optimizer, clip):
     rparams = dict(ref.named_parameters())
     bases = [grp["lr"] for grp in ropt.param_groups]
     g = torch.Generator().manual_seed(11)
+    flag = dict(zip(opt.names, opt.flag_views))
     for it in range(4):
         with torch.no_grad():
-            for name, p in rparams.items():
+            opt.flags.fill_(1.0)
+            for k, (name, p) in enumerate(rparams.items()):
                 # gradient magnitudes on both sides of the clip threshold
                 gr = torch.randn(p.shape, generator=g) * (10 ** float(torch.empty(()).uniform_(-5, 0, generator=g)))
                 gr = gr.to(dtype).float()
+                if it < 2 and k % 4 == it:
+                    # no gradient this step (torch.optim skips .grad None: no decay, no
+                    # momentum; AdamW's bias correction counts the parameter's own steps)
+                    p.grad = None
+                    byname[name].zero_()
+                    flag[name].zero_()
+                    continue
                 p.grad = gr.clone()
                 byname[name].copy_(gr.to(dtype))
         if clip == "norm":
@@ -60,6 +69,8 @@ def test_flat_step_vs_oracle_solver(dtype, optimizer, clip):
         opt.step()
     torch.cuda.synchronize()
     assert float(opt.step_count) == 4
+    steps = opt.param_steps.cpu().tolist()
+    assert min(steps) == 3 and max(steps) == 4
     worst = 0.0
     for name, m in zip(opt.names, opt.layout.views(opt.master)):
         r = rparams[name].detach()

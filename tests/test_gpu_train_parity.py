@@ -125,3 +125,116 @@ def test_training_step_vs_oracle(golden, kind):
     assert abs(float(loss) - float(rloss)) <= LOSS_TOL * abs(float(rloss))
     assert worst_g <= GRAD_TOL, wg
     assert worst_u <= GRAD_TOL, wu
+
+
+def _rel_l2(a, b, floor):
+    """||a - b|| / max(||b||, floor), in f64."""
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a - b).norm()) / max(float(b.norm()), floor)
+
+
+def test_bf16_training_step_vs_oracle():
+    """The PRODUCTION training step (bf16 Trainer: MFMA window attention fwd/bwd, the
+    MFMA MSDA backward with grad_loc / grad_attn in its band walk, MFMA masked attention,
+    the fused mask-head backward through the point-scatter kernel, bf16 GEMMs, the
+    flat-buffer optimiser) vs the oracle (RefMask2Former + RefCriterion + the reference's
+    solver, fp32 on CPU), Swin-T at 256^2, on the same bf16-rounded weights and input
+    and the same point draws (HF:m2f:726-779 losses, train_full.py:266-271 clip).
+
+    Decisions are forced from the fp32 oracle into the other runs: the decoder's attention
+    masks (mask_override), the Hungarian matching of every decoder step and the
+    importance-sampling top-k choice (tests/_draws.ForcedDecisions).
+
+    Yardstick: the oracle ITSELF run in bf16 (torch CPU bf16 kernels, same weights,
+    forced decisions).  Per parameter, the error is the relative L2 distance to the fp32
+    oracle's gradient (norm floor 1e-3 of the median parameter gradient norm, for
+    gradients that are analytically ~0).  Bounds (stated here, measured values in the
+    print):
+      * loss: |ours - fp32| <= 1.25 x |oracle-bf16 - fp32| + 2e-3 x loss;
+      * gradients: the median and the 90th percentile over parameters of ours <=
+        1.25 x the yardstick's; every parameter <= max(1.25 x its yardstick error, 0.05);
+      * weight updates of the step (per-parameter clip to norm 0.01, SGD): the same two
+        percentile bounds against the yardstick's update."""
+    from _draws import ForcedDecisions
+    from visionseg.criterion import SetCriterion
+    from visionseg.data import synthetic_batch
+    from visionseg.model import M2FConfig, Mask2Former
+    from visionseg.train import SolverConfig, Trainer, lr_at
+    cfg = M2FConfig.preset("swin_t")
+    rcfg = RefConfig.from_dict(cfg.to_dict())
+    ref = RefMask2Former(rcfg)
+    sd = det_init({k: v.shape for k, v in ref.state_dict().items()}, 78)
+    sd = {k: (v.to(torch.bfloat16).float() if v.is_floating_point() else v) for k, v in sd.items()}
+    ref.load_state_dict(sd)
+    ref.train()
+    imgs, ml, cl = synthetic_batch(2, 256, seed=6)
+    imgs = imgs.to(torch.bfloat16).float()
+    draws = ForcedDecisions(2, max(len(c) for c in cl) + 1, seed=7)
+    s = SolverConfig(optimizer="sgd", warmup_iters=0, lr=0.05)
+    lr = lr_at(s, 0)
+
+    def oracle_step(model, x, dtype):
+        model.decoder.record = dtype == torch.float32
+        masks, classes = model(x.to(dtype))
+        masks, classes = [m.float() for m in masks], [c.float() for c in classes]
+        loss, _ = RefCriterion(rcfg, point_source=draws)(masks, classes, [m.float() for m in ml], cl)
+        loss.backward()
+        ps = dict(model.named_parameters())
+        grads = {n: p.grad.detach().float().clone() for n, p in ps.items()}
+        # the reference's solver on an f32 copy (the update of the same weights)
+        f32 = {n: torch.nn.Parameter(p.detach().float().clone()) for n, p in ps.items()}
+        for n, p in f32.items():
+            p.grad = grads[n].clone()
+        before = {n: p.detach().clone() for n, p in f32.items()}
+        ref_clip_per_parameter(list(f32.values()), s.clip_value)
+        groups = ref_param_groups(model, lr, s.weight_decay, "sgd")
+        for gr in groups:
+            gr["params"] = [f32[gr["name"]]]
+        ref_optimizer(groups, "sgd", s.momentum).step()
+        upd = {n: f32[n].detach() - before[n] for n in f32}
+        return float(loss), grads, upd
+
+    # ---- oracle fp32 (records the decisions), then oracle bf16 (replays them)
+    l32, g32, u32 = oracle_step(ref, imgs, torch.float32)
+    forced = [rb for rb, _ in ref.decoder.trace]
+    draws.replay = True
+    ref16 = RefMask2Former(rcfg)
+    ref16.load_state_dict(sd)
+    ref16 = ref16.to(torch.bfloat16).train()
+    ref16.decoder.mask_override = forced
+    l16, g16, u16 = oracle_step(ref16, imgs, torch.bfloat16)
+
+    # ---- product: one bf16 Trainer step on the GPU
+    prod = Mask2Former(cfg)
+    prod.load_state_dict(sd)
+    tr = Trainer(prod, SetCriterion(cfg, matcher="device", point_source=draws), s, device=DEV)
+    assert tr.mode == "bf16"
+    prod.decoder.mask_override = forced
+    tr._set_lr()
+    w0 = {n: m.detach().cpu().clone() for n, m in zip(tr.opt.names, tr.master_params())}
+    loss, _ = tr.forward_backward(imgs.to(DEV), [m.to(DEV) for m in ml], [c.to(DEV) for c in cl])
+    gp = {n: g.detach().float().cpu().clone() for n, g in zip(tr.opt.names, tr.opt.grad_views)}
+    tr.apply_gradients()
+    torch.cuda.synchronize()
+    up = {n: m.detach().cpu() - w0[n] for n, m in zip(tr.opt.names, tr.master_params())}
+    lp = float(loss)
+
+    assert set(gp) == set(g32)
+    names = sorted(g32)
+    gfloor = 1e-3 * float(np.median([float(g32[n].norm()) for n in names]))
+    ufloor = 1e-3 * float(np.median([float(u32[n].norm()) for n in names]))
+    eg = {n: _rel_l2(gp[n], g32[n], gfloor) for n in names}
+    yg = {n: _rel_l2(g16[n], g32[n], gfloor) for n in names}
+    eu = {n: _rel_l2(up[n], u32[n], ufloor) for n in names}
+    yu = {n: _rel_l2(u16[n], u32[n], ufloor) for n in names}
+    q = lambda d, p: float(np.percentile(list(d.values()), p))          # noqa: E731
+    ratio = sorted(((eg[n] / max(yg[n], 1e-12), n) for n in names), reverse=True)[:5]
+    print(f"bf16 step: loss ours {lp:.5f} / oracle-bf16 {l16:.5f} / fp32 {l32:.5f}; grad rel-L2 median "
+          f"{q(eg, 50):.2e} (yard {q(yg, 50):.2e}), p90 {q(eg, 90):.2e} (yard {q(yg, 90):.2e}), max {q(eg, 100):.2e} "
+          f"(yard {q(yg, 100):.2e}); update median {q(eu, 50):.2e} (yard {q(yu, 50):.2e}), p90 {q(eu, 90):.2e} "
+          f"(yard {q(yu, 90):.2e}); worst ratios {[(n, f'{r:.2f}', f'{eg[n]:.1e}') for r, n in ratio]}")
+    assert abs(lp - l32) <= 1.25 * abs(l16 - l32) + 2e-3 * abs(l32)
+    assert q(eg, 50) <= 1.25 * q(yg, 50) and q(eg, 90) <= 1.25 * q(yg, 90)
+    bad = [(n, eg[n], yg[n]) for n in names if eg[n] > max(1.25 * yg[n], 0.05)]
+    assert not bad, bad[:5]
+    assert q(eu, 50) <= 1.25 * q(yu, 50) and q(eu, 90) <= 1.25 * q(yu, 90)

@@ -72,31 +72,69 @@ def test_proposals_and_dn_queries():
     assert unsig.shape == (20, 4) and valid.shape == (20,)
     p = unsig[valid].sigmoid()
     assert torch.allclose(p[0], torch.tensor([0.25, 0.25, 0.05, 0.05]), atol=1e-6)
-    # dn: counts 2 and 1, capacity 4 (bucketed) -> 8 // 4 = 2 groups of 4 slots
+    # dn: counts 2 and 1, capacity 4 (bucketed) -> K = 2: 8 // 2 = 4 groups of 2 slots
     ml = [torch.zeros(2, 16, 16, dtype=torch.bool), torch.zeros(1, 16, 16, dtype=torch.bool)]
     ml[0][0, 2:8, 2:8] = True
     ml[0][1, 10:14, 3:9] = True
     ml[1][0, 5:9, 5:9] = True
-    tg = PaddedTargets.from_lists(ml, [torch.tensor([0, 1]), torch.tensor([1])], kc=4)
+    cl = [torch.tensor([0, 1]), torch.tensor([1])]
+    tg = PaddedTargets.from_lists(ml, cl, kc=4)
     boxes = masks_to_boxes(tg.masks)
     torch.manual_seed(0)
     emb, unsig_dn, blocked, meta = dec._dn(tg, boxes, 2, torch.device("cpu"), torch.float32)
-    assert meta["groups"] == 2 and meta["pad"] == 8
+    assert int(meta["groups"]) == 4 and meta["pad"] == 8 and bool(meta["active"].all())
+    assert meta["slot"].tolist() == [0, 1] * 4
     assert emb.shape == (2, 8, 64) and unsig_dn.shape == (2, 8, 4)
     valid_dn = meta["valid"]
-    assert valid_dn.tolist() == [[True, True, False, False] * 2, [True, False, False, False] * 2]
+    assert valid_dn.tolist() == [[True, True] * 4, [True, False] * 4]
     assert float(emb[~valid_dn].abs().sum()) == 0.0 and float(unsig_dn[~valid_dn].abs().sum()) == 0.0
     Qt = 8 + cfg.num_queries
     assert blocked.shape == (Qt, Qt)
     # matching queries see each other but no DN query; DN groups see only themselves
     assert not blocked[8:, 8:].any() and blocked[8:, :8].all()
-    assert not blocked[:4, :4].any() and blocked[:4, 4:8].all() and blocked[4:8, :4].all()
+    for gi in range(4):
+        lo, hi = 2 * gi, 2 * gi + 2
+        assert not blocked[lo:hi, lo:hi].any()
+        assert blocked[lo:hi, :lo].all() and blocked[lo:hi, hi:8].all()
     assert not blocked[:8, 8:].any()
     # noised boxes stay in the unit square, near their targets
     bx = unsig_dn.sigmoid()[valid_dn]
-    tb = boxes.repeat(1, 2, 1)[valid_dn]
+    tb = boxes[:, :2].repeat(1, 4, 1)[valid_dn]
     assert bool(((bx >= 0) & (bx <= 1)).all())
     assert float((bx - tb).abs().max()) <= cfg.noise_scale * float(tb[:, 2:].max()) + 1e-5
+
+
+def test_dn_layout_independent_of_target_capacity():
+    """Eager steps pad the targets to the batch's largest count, graph-replayed steps to
+    a multiple of 4 (train.Trainer.target_capacity): the denoising layout (groups, slots,
+    validity, attention mask, noised queries) must be the same for both (upstream
+    prepare_for_dn: dn_num // max count groups)."""
+    cfg = _tiny_cfg(dn_num=8)
+    dec = MaskDINODecoder(cfg)
+    ml, cl = _targets(B=3)                      # counts 2, 1, 3 -> K = 3: 2 groups, 2 inactive queries
+    res = []
+    for kc in (3, 4, 8):
+        tg = PaddedTargets.from_lists(ml, cl, kc=kc)
+        boxes = masks_to_boxes(tg.masks)
+        torch.manual_seed(7)
+        res.append(dec._dn(tg, boxes, 3, torch.device("cpu"), torch.float32))
+    for emb, unsig, blocked, meta in res[1:]:
+        assert torch.equal(emb, res[0][0]) and torch.equal(unsig, res[0][1]) and torch.equal(blocked, res[0][2])
+        for k in ("slot", "active", "valid"):
+            assert torch.equal(meta[k], res[0][3][k])
+    meta, blocked = res[0][3], res[0][2]
+    assert int(meta["groups"]) == 2 and meta["active"].tolist() == [True] * 6 + [False] * 2
+    assert meta["valid"][2].tolist() == [True] * 6 + [False] * 2
+    assert meta["valid"][1].tolist() == [True, False, False] * 2 + [False] * 2
+    # an inactive query is seen by nobody else and sees no other DN query
+    for q in (6, 7):
+        others = [j for j in range(8 + cfg.num_queries) if j != q]
+        assert blocked[others, q].all() and blocked[q, [j for j in range(8) if j != q]].all()
+    # no targets anywhere (a graph step's padded capacity): every DN query inactive
+    tg = PaddedTargets.from_lists([torch.zeros(0, 96, 96, dtype=torch.bool)] * 2,
+                                  [torch.zeros(0, dtype=torch.int64)] * 2, kc=4)
+    _, _, blocked, meta = dec._dn(tg, masks_to_boxes(tg.masks), 2, torch.device("cpu"), torch.float32)
+    assert not meta["valid"].any() and not meta["active"].any() and blocked[8:, :8].all()
 
 
 def test_focal_loss_formula():

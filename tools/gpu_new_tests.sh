@@ -1,0 +1,4 @@
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -s tests/test_gpu_train_parity.py tests/test_gpu_optim.py tests/test_gpu_maskdino.py "tests/test_gpu_ops.py::test_msda_mfma_backward_vs_binned_and_oracle" "tests/test_gpu_ops.py::test_msda_encoder_shapes_backward_vs_oracle" "tests/test_gpu_ops.py::test_msda_destination_backward_vs_oracle" > gpurun_out/r3_new_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r3_new_tests.log; exit $rc

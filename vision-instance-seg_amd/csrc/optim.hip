@@ -12,15 +12,22 @@
 // bf16 working weights the model reads (views of one buffer too).  Each parameter starts
 // 8-element aligned; a static chunk table splits every parameter into chunks of
 // <= kChunk elements:
-//   table[c]  = {start, len, first chunk of the parameter, chunks of the parameter}
+//   table[c]  = {start, len, first chunk of the parameter, chunks of the parameter, parameter}
 //   hyper[c]  = {lr multiplier, weight decay} of the chunk's parameter group.
-// Two launches per step:
-//   flat_sumsq_kernel: each chunk's sum of squares of the (averaged) gradient; block 0
-//                      also advances the device step counter (Adam bias correction);
+// Per parameter, a gradient FLAG (> 0.5: the parameter got a gradient this step on some
+// rank; it travels in the gradient buffer and is summed by the all-reduce) and a step
+// COUNT: torch.optim skips a parameter whose .grad is None -- no decay, no momentum /
+// moment update -- and AdamW's bias correction counts the steps that parameter took.
+// Two launches per step (three with the "full_model" clip):
+//   flat_sumsq_kernel: each chunk's sum of squares of the (averaged) gradient; the first
+//                      chunk of a flagged parameter advances its step count; block 0 the
+//                      global step counter;
+//   flat_total_kernel: ("full_model" only) the one global sum of squares, in chunk order;
 //   flat_step_kernel:  recomputes its parameter's norm from that parameter's partials
-//                      (per-parameter clip; or from all partials: "full_model" clip),
-//                      then clip-scale + weight decay + SGD-momentum / AdamW update of
-//                      the master weights + bf16 round of the working weights, one pass.
+//                      (per-parameter clip; or reads the global total), then clip-scale +
+//                      weight decay + SGD-momentum / AdamW update of the master weights +
+//                      bf16 round of the working weights, one pass; unflagged parameters
+//                      are left untouched.
 // Deterministic: no atomics, every block sums the partials in the same order.
 // HBM-bound: per element it reads the gradient (2 or 4 B) and master + state (8 or 12 B)
 // and writes master + state + working weight (10 or 14 B).
@@ -62,13 +69,26 @@ __device__ __forceinline__ void store8(float* p, const float* in) {
   Vec16<float>::store(p + 4, in + 4);
 }
 
+constexpr int kCols = 5;          // chunk table columns
+
 template <typename G>
-__global__ void __launch_bounds__(kThreads) flat_sumsq_kernel(const G* __restrict__ grad, const int* __restrict__ table,
-                                                              float* __restrict__ partial, float* __restrict__ step) {
+__device__ __forceinline__ bool has_grad(const G* flags, int prm) {
+  return flags == nullptr || to_f32(flags[prm]) > 0.5f;
+}
+
+template <typename G>
+__global__ void __launch_bounds__(kThreads) flat_sumsq_kernel(const G* __restrict__ grad, const G* __restrict__ flags,
+                                                              const int* __restrict__ table, float* __restrict__ partial,
+                                                              float* __restrict__ step, float* __restrict__ psteps) {
   __shared__ float sh[kThreads / 64 + 1];
   const int c = blockIdx.x;
   if (c == 0 && threadIdx.x == 0 && step) step[0] += 1.f;
-  const int start = table[c * 4 + 0], len = table[c * 4 + 1];
+  const int start = table[c * kCols + 0], len = table[c * kCols + 1], prm = table[c * kCols + 4];
+  if (!has_grad(flags, prm)) {           // uniform per block
+    if (threadIdx.x == 0) partial[c] = 0.f;
+    return;
+  }
+  if (threadIdx.x == 0 && table[c * kCols + 2] == c) psteps[prm] += 1.f;
   const G* p = grad + start;                  // start % 8 == 0
   float acc = 0.f;
   const int n8 = len / kVec;
@@ -84,6 +104,16 @@ __global__ void __launch_bounds__(kThreads) flat_sumsq_kernel(const G* __restric
   }
   const float t = block_sum(acc, sh);
   if (threadIdx.x == 0) partial[c] = t;
+}
+
+// "full_model" clip: partial[num_chunks] = the sum of every chunk's partial (one block,
+// fixed order), read by every block of the step kernel instead of num_chunks partials.
+__global__ void __launch_bounds__(kThreads) flat_total_kernel(float* __restrict__ partial, int num_chunks) {
+  __shared__ float sh[kThreads / 64 + 1];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < num_chunks; i += kThreads) acc += partial[i];
+  const float t = block_sum(acc, sh);
+  if (threadIdx.x == 0) partial[num_chunks] = t;
 }
 
 struct StepArgs {
@@ -113,26 +143,28 @@ __device__ __forceinline__ void update(float g, float& p, float& s1, float& s2, 
 }
 
 template <typename G, typename W>
-__global__ void __launch_bounds__(kThreads) flat_step_kernel(const G* __restrict__ grad, float* __restrict__ master,
+__global__ void __launch_bounds__(kThreads) flat_step_kernel(const G* __restrict__ grad, const G* __restrict__ flags,
+                                                             float* __restrict__ master,
                                                              float* __restrict__ s1buf, float* __restrict__ s2buf,
                                                              W* __restrict__ wout, const int* __restrict__ table,
                                                              const float* __restrict__ hyper,
                                                              const float* __restrict__ partial, int num_chunks,
                                                              const float* __restrict__ lr_ptr,
-                                                             const float* __restrict__ step_ptr, StepArgs a) {
+                                                             const float* __restrict__ psteps, StepArgs a) {
   __shared__ float s_scale;
   const int c = blockIdx.x;
-  const int start = table[c * 4 + 0], len = table[c * 4 + 1];
+  const int start = table[c * kCols + 0], len = table[c * kCols + 1], prm = table[c * kCols + 4];
+  if (!has_grad(flags, prm)) return;     // torch.optim: a parameter without a gradient is skipped
   if (threadIdx.x < 64) {
     float k = 1.f;
-    if (a.clip != 0) {
-      const int first = a.clip == 1 ? table[c * 4 + 2] : 0;
-      const int count = a.clip == 1 ? table[c * 4 + 3] : num_chunks;
+    if (a.clip == 1) {
+      const int first = table[c * kCols + 2], count = table[c * kCols + 3];
       float s = 0.f;
       for (int i = threadIdx.x; i < count; i += 64) s += partial[first + i];
       s = wave_sum(s);
-      const float norm = sqrtf(s) * a.grad_scale;
-      k = fminf(1.f, a.clip_value / (norm + a.clip_eps));
+      k = fminf(1.f, a.clip_value / (sqrtf(s) * a.grad_scale + a.clip_eps));
+    } else if (a.clip == 2) {
+      k = fminf(1.f, a.clip_value / (sqrtf(partial[num_chunks]) * a.grad_scale + a.clip_eps));
     }
     if (threadIdx.x == 0) s_scale = k * a.grad_scale;
   }
@@ -140,7 +172,7 @@ __global__ void __launch_bounds__(kThreads) flat_step_kernel(const G* __restrict
   const float gk = s_scale;
   const float lr = lr_ptr[0] * hyper[c * 2 + 0];
   const float wd = hyper[c * 2 + 1];
-  const float t = step_ptr[0];
+  const float t = psteps[prm];           // this parameter's steps, this one included
   const bool first = t <= 1.f;
   float bc1 = 1.f, bc2s = 1.f;
   if (a.optimizer == 1) {
@@ -174,12 +206,15 @@ __global__ void __launch_bounds__(kThreads) flat_step_kernel(const G* __restrict
 }
 
 template <typename G>
-int launch_step(const G* grad, float* master, float* s1, float* s2, bf16* wout, const int* table, const float* hyper,
-                int num_chunks, const StepArgs& a, const float* lr, float* step, float* partial, hipStream_t st) {
+int launch_step(const G* grad, const G* flags, float* master, float* s1, float* s2, bf16* wout, const int* table,
+                const float* hyper, int num_chunks, const StepArgs& a, const float* lr, float* step, float* psteps,
+                float* partial, hipStream_t st) {
   // always launched: block 0 also advances the step counter
-  hipLaunchKernelGGL(flat_sumsq_kernel<G>, dim3(num_chunks), dim3(kThreads), 0, st, grad, table, partial, step);
-  hipLaunchKernelGGL((flat_step_kernel<G, bf16>), dim3(num_chunks), dim3(kThreads), 0, st, grad, master, s1, s2, wout,
-                     table, hyper, partial, num_chunks, lr, step, a);
+  hipLaunchKernelGGL(flat_sumsq_kernel<G>, dim3(num_chunks), dim3(kThreads), 0, st, grad, flags, table, partial, step,
+                     psteps);
+  if (a.clip == 2) hipLaunchKernelGGL(flat_total_kernel, dim3(1), dim3(kThreads), 0, st, partial, num_chunks);
+  hipLaunchKernelGGL((flat_step_kernel<G, bf16>), dim3(num_chunks), dim3(kThreads), 0, st, grad, flags, master, s1,
+                     s2, wout, table, hyper, partial, num_chunks, lr, psteps, a);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
@@ -189,15 +224,18 @@ int launch_step(const G* grad, float* master, float* s1, float* s2, bf16* wout, 
 
 using namespace vs;
 
-extern "C" long long vs_flat_step_workspace_bytes(int num_chunks) { return (long long)num_chunks * sizeof(float); }
+extern "C" long long vs_flat_step_workspace_bytes(int num_chunks) {
+  return ((long long)num_chunks + 1) * sizeof(float);
+}
 
-extern "C" int vs_flat_step(int grad_dtype, const void* grad, float grad_scale, float* master, float* state1,
-                            float* state2, void* weights_bf16, const int* table, const float* hyper, int num_chunks,
-                            int optimizer, int clip, float clip_value, float clip_eps, float momentum, float beta1,
-                            float beta2, float eps, const float* lr, float* step, void* workspace, void* stream) {
+extern "C" int vs_flat_step(int grad_dtype, const void* grad, const void* grad_flags, float grad_scale, float* master,
+                            float* state1, float* state2, void* weights_bf16, const int* table, const float* hyper,
+                            int num_chunks, int optimizer, int clip, float clip_value, float clip_eps, float momentum,
+                            float beta1, float beta2, float eps, const float* lr, float* step, float* param_steps,
+                            void* workspace, void* stream) {
   VS_CHECK(num_chunks >= 0, "bad chunk count");
   if (num_chunks == 0) return VS_OK;
-  VS_CHECK(grad && master && state1 && table && hyper && lr && step && workspace, "null pointer");
+  VS_CHECK(grad && master && state1 && table && hyper && lr && step && param_steps && workspace, "null pointer");
   VS_CHECK(grad_dtype == VS_F32 || grad_dtype == VS_BF16, "gradient dtype must be f32 or bf16");
   VS_CHECK(optimizer == 0 || optimizer == 1, "optimizer must be 0 (SGD) or 1 (AdamW)");
   VS_CHECK(optimizer == 0 || state2, "AdamW needs the second-moment buffer");
@@ -209,8 +247,8 @@ extern "C" int vs_flat_step(int grad_dtype, const void* grad, float grad_scale, 
   float* partial = (float*)workspace;
   bf16* w = (bf16*)weights_bf16;
   if (grad_dtype == VS_BF16)
-    return launch_step<bf16>((const bf16*)grad, master, state1, state2, w, table, hyper, num_chunks, a, lr, step,
-                             partial, st);
-  return launch_step<float>((const float*)grad, master, state1, state2, w, table, hyper, num_chunks, a, lr, step,
-                            partial, st);
+    return launch_step<bf16>((const bf16*)grad, (const bf16*)grad_flags, master, state1, state2, w, table, hyper,
+                             num_chunks, a, lr, step, param_steps, partial, st);
+  return launch_step<float>((const float*)grad, (const float*)grad_flags, master, state1, state2, w, table, hyper,
+                            num_chunks, a, lr, step, param_steps, partial, st);
 }

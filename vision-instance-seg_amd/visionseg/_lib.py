@@ -63,8 +63,8 @@ SIGNATURES = {
     "vs_column_sum_segments": [_c_int] + [_P] * 3 + [_c_int] * 3 + [_P, _c_int, _P],
     "vs_act_backward_colsum": [_c_int, _c_int] + [_P] * 5 + [_c_int] * 2 + [_P],
     "vs_flat_step_workspace_bytes": [_c_int],
-    "vs_flat_step": [_c_int, _P, _c_float, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _c_int] + [_c_float] * 6
-                    + [_P, _P, _P, _P],
+    "vs_flat_step": [_c_int, _P, _P, _c_float, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _c_int] + [_c_float] * 6
+                    + [_P, _P, _P, _P, _P],
     "vs_event_create": [ctypes.POINTER(_c_void_p)],
     "vs_event_destroy": [_P],
     "vs_event_record_external": [_P, _P],

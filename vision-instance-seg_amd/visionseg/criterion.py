@@ -214,6 +214,9 @@ class SetCriterion:
         tg = as_padded(mask_labels, class_labels, dev)
         Kc = tg.kc
         assign = self.match([m.detach() for m in masks_list], classes.detach(), tg)
+        forced = getattr(self.point_source, "forced_assign", None)
+        if forced is not None:      # parity hook: another run's matching decisions (tests/_draws.py)
+            assign = forced(assign)
         nm = self._num_masks(tg, dev)
         ew = self._ew.get(dev)
         if ew is None:        # made once: a scalar store is a host->device copy (not capturable)
@@ -249,7 +252,13 @@ class SetCriterion:
                 nu = int(c.importance_sample_ratio * npts)
                 coords = self._loss_points(S, B, Kc, ns, "over", dev)
                 unc = -torch.abs(_sample(pred.detach().float(), coords))
-                top = torch.topk(unc, k=nu, dim=1)[1]
+                select = getattr(self.point_source, "select", None)
+                if select is None:
+                    top = torch.topk(unc, k=nu, dim=1)[1]
+                else:               # parity hook, rows keyed (step, image, target slot)
+                    keys = (torch.arange(S).repeat_interleave(B * Kc), torch.arange(B).repeat_interleave(Kc).repeat(S),
+                            torch.arange(Kc).repeat(S * B))
+                    top = select(unc, nu, *keys)
                 coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
                 if npts - nu > 0:
                     coords = torch.cat([coords, self._loss_points(S, B, Kc, npts - nu, "rand", dev)], 1)

@@ -16,9 +16,10 @@ pixel_decoder/maskdino_encoder.py, criterion.py, matcher.py) on the build's kern
   and their boxes its reference boxes (detached); those tokens' own predictions are the
   "interm" outputs;
 * denoising (DN, "seg"): noised ground-truth boxes and labels as extra queries (label
-  flips with probability noise_scale/2, box jitter of noise_scale), groups of the
-  padded target capacity, an attention mask keeping the matching queries from the DN
-  queries and the DN groups from each other;
+  flips with probability noise_scale/2, box jitter of noise_scale), dn_num // K groups
+  of K slots (K = the batch's largest target count, read on the device), an attention
+  mask keeping the matching queries from the DN queries and the DN groups from each
+  other;
 * 9 deformable decoder layers (self-attention with the DN mask -> MSDA cross-attention
   to the 4-level memory with box reference points: loc = c + off / P * wh / 2 ->
   ReLU FFN 2048, post-norm), query positions from the sine embedding of the box through
@@ -246,20 +247,35 @@ class MaskDINODecoder(nn.Module):
         return cls, ops.mask_head(e, mf, Hm, Wm, sink=sink)
 
     def _dn(self, tg, boxes, B, dev, dtype):
-        """Denoising queries from the padded targets: groups of kc slots (slot k = target
-        k of the image, padded slots zero), label flips with probability noise_scale/2,
-        box jitter noise_scale * (wh/2, wh), clamped to [0, 1].  Returns (label
-        embeddings [B, pad, d], unsigmoided boxes [B, pad, 4], attention mask [Qt, Qt]
-        (True = blocked), meta)."""
+        """Denoising queries (upstream prepare_for_dn).  With K = the batch's largest
+        target count, dn_num // K groups of K slots: slot k of every group is target k of
+        the image, slots past an image's count are padding queries (zero label embedding,
+        zero unsigmoided box, as upstream); label flips with probability noise_scale/2,
+        box jitter noise_scale * (wh/2, wh), clamped to [0, 1].
+
+        K is read ON THE DEVICE (no host sync), so the layout depends only on the true
+        counts, not on the capacity the targets are padded to: an eager step (capacity =
+        K) and a graph-replayed one (capacity rounded up to a multiple of 4) build the same
+        groups.  The query count is fixed at dn_num (>= groups x K for every K), so one
+        captured graph serves every batch; queries past groups x K are inactive: each is a
+        group of its own (no other query sees it) and every loss masks it out.
+
+        Returns (label embeddings [B, dn_num, d], unsigmoided boxes [B, dn_num, 4],
+        attention mask [Qt, Qt] (True = blocked), meta)."""
         c = self.cfg
-        kc = tg.kc
-        groups = c.dn_num // kc if kc > 0 else 0
-        if groups == 0:
+        if tg.kc == 0 or c.dn_num <= 0:
             return None
-        pad = groups * kc
-        valid = tg.valid().repeat(1, groups)                                         # [B, pad]
-        labels = tg.classes.repeat(1, groups)
-        bx = boxes.repeat(1, groups, 1)
+        pad = c.dn_num
+        counts = tg.counts.long()
+        kmax = counts.max().clamp(min=1)                                           # device scalar
+        groups = torch.div(pad, kmax, rounding_mode="floor")
+        i = torch.arange(pad, device=dev)
+        slot = i % kmax                                                            # < K <= capacity
+        grp = torch.div(i, kmax, rounding_mode="floor")
+        active = (grp < groups) & (counts.max() > 0)       # [pad]; no targets: no DN (upstream scalar 0)
+        valid = active[None] & (slot[None] < counts[:, None])                      # [B, pad]
+        labels = torch.gather(tg.classes, 1, slot[None].expand(B, pad))
+        bx = torch.gather(boxes, 1, slot[None, :, None].expand(B, pad, 4))
         if c.noise_scale > 0:
             flip = torch.rand(B, pad, device=dev) < c.noise_scale * 0.5
             labels = torch.where(flip, torch.randint_like(labels, 0, c.num_labels), labels)
@@ -269,10 +285,13 @@ class MaskDINODecoder(nn.Module):
         unsig = torch.where(valid[..., None], inverse_sigmoid(bx), torch.zeros_like(bx))
         Qt = pad + c.num_queries
         g = torch.arange(Qt, device=dev)
-        grp = torch.where(g < pad, torch.div(g, kc, rounding_mode="floor"), torch.full_like(g, -1))
-        blocked = (grp[:, None] >= 0) & (grp[None, :] >= 0) & (grp[:, None] != grp[None, :])
-        blocked |= (grp[:, None] < 0) & (grp[None, :] >= 0)            # matching queries cannot see DN
-        return emb, unsig.to(dtype), blocked, dict(pad=pad, groups=groups, kc=kc, valid=valid)
+        # group id: DN group, a private id for an inactive DN query, -1 for matching queries
+        gid = torch.full((Qt,), -1, dtype=torch.long, device=dev)
+        gid[:pad] = torch.where(active, grp, pad + i)
+        dn_q = g < pad
+        blocked = dn_q[:, None] & dn_q[None, :] & (gid[:, None] != gid[None, :])
+        blocked |= ~dn_q[:, None] & dn_q[None, :]                          # matching queries cannot see DN
+        return emb, unsig.to(dtype), blocked, dict(pad=pad, groups=groups, slot=slot, active=active, valid=valid)
 
     # ------------------------------------------------------------------ forward
     def forward(self, ms_feats, mask_features, targets=None, boxes=None):
@@ -468,14 +487,17 @@ class MaskDINOCriterion:
                     out[s, b, col] = r
         return torch.from_numpy(out).to(dev)
 
-    def _mask_losses(self, pred, tmask, keep, nb):
-        """pred [B, G, Kc, H, W]: the logits of the query paired with target slot k in
-        group g; tmask [B, Kc, Ht, Wt] the targets; keep [B, G, Kc] bool.  Importance-
-        sampled point BCE and dice (HF:m2f:671-724 semantics); each full-resolution
-        target is sampled once, at the points of all G predictions paired with it."""
+    def _mask_losses(self, pred, tmask, slot, keep, nb):
+        """pred [B, R, H, W]: the logits of R queries per image; tmask [B, Kc, Ht, Wt] f32
+        the targets; slot [B, R] the target slot each query is paired with; keep [B, R]
+        bool.  Importance-sampled point BCE and dice (HF:m2f:671-724 semantics).  The
+        labels: every target channel of the image sampled at all R x P points of its
+        queries (one grid_sample per batch, fixed shapes whatever the pairing), then each
+        query's own slot picked."""
         c = self.cfg
-        B, G, Kc = pred.shape[:3]
-        N = B * G * Kc
+        B, R = pred.shape[:2]
+        Kc = tmask.shape[1]
+        N = B * R
         pred = pred.reshape(N, 1, *pred.shape[-2:])
         P = c.train_num_points
         with torch.no_grad():
@@ -486,9 +508,9 @@ class MaskDINOCriterion:
             coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
             if P - nu > 0:
                 coords = torch.cat([coords, torch.rand(N, P - nu, 2, device=pred.device)], 1)
-            by_t = coords.view(B, G, Kc, P, 2).permute(0, 2, 1, 3, 4).reshape(B * Kc, G * P, 2)
-            lab = _point_sample(tmask.reshape(B * Kc, 1, *tmask.shape[-2:]).float(), by_t)
-            lab = lab.view(B, Kc, G, P).permute(0, 2, 1, 3).reshape(N, P)
+            grid = (2.0 * coords - 1.0).view(B, R * P, 1, 2)
+            lab = F.grid_sample(tmask, grid, align_corners=False).view(B, Kc, R, P)
+            lab = torch.gather(lab, 1, slot[:, None, :, None].expand(B, 1, R, P)).reshape(N, P)
         logit = _point_sample(pred.float(), coords)
         keep = keep.reshape(N)
         zero = torch.zeros((), device=pred.device)
@@ -497,9 +519,10 @@ class MaskDINOCriterion:
         dice = torch.where(keep, 1 - (2 * (pr * lab).sum(-1) + 1) / (pr.sum(-1) + lab.sum(-1) + 1), zero)
         return bce.sum() / nb, dice.sum() / nb
 
-    def _pair_losses(self, cls, box, mask, qsel, valid, tg, tboxes, nb):
+    def _pair_losses(self, cls, box, mask, qsel, valid, tg, tmf, tboxes, nb):
         """Losses of one prediction set: cls [B,Q,K], box [B,Q,4], mask [B,Q,H,W]; qsel
-        [B,Kc] the query paired with each target slot, valid [B,Kc]."""
+        [B,Kc] the query paired with each target slot, valid [B,Kc]; tmf the target masks
+        in f32."""
         c = self.cfg
         B, Q, K = cls.shape
         Kc = tg.kc
@@ -517,29 +540,32 @@ class MaskDINOCriterion:
         giou = torch.diagonal(generalized_box_iou(box_cxcywh_to_xyxy(pb), box_cxcywh_to_xyxy(tb)), dim1=-2, dim2=-1)
         l_giou = ((1 - giou) * v).sum() / nb
         pm = mask[bidx, qs]                                                           # [B,Kc,H,W]
-        l_bce, l_dice = self._mask_losses(pm[:, None], tg.masks, valid[:, None], nb)
+        slots = torch.arange(Kc, device=cls.device)[None].expand(B, Kc)
+        l_bce, l_dice = self._mask_losses(pm, tmf, slots, valid, nb)
         return dict(loss_ce=c.class_weight * l_cls, loss_bbox=c.box_weight * l_l1, loss_giou=c.giou_weight * l_giou,
                     loss_mask=c.mask_weight * l_bce, loss_dice=c.dice_weight * l_dice)
 
-    def _dn_losses(self, cls, box, mask, dn, tg, tboxes, nb):
-        """Denoising queries against the targets they were made from: DN query g * kc + k
-        <-> target slot k (valid where the image has that target); normalised by the
-        target count x the number of groups (upstream num_boxes * scalar)."""
+    def _dn_losses(self, cls, box, mask, dn, tg, tmf, tboxes, nb):
+        """Denoising queries against the targets they were made from: DN query i <->
+        target slot dn["slot"][i] (valid where its group is active and the image has that
+        target); normalised by the target count x the number of groups (upstream
+        num_boxes * scalar).  The class loss covers the active DN queries (upstream: the
+        first groups x K queries, padding slots as negatives)."""
         c = self.cfg
-        g, kc, pad = dn["groups"], dn["kc"], dn["pad"]
-        valid = dn["valid"]                                                          # [B, pad]
+        pad, slot, valid, active = dn["pad"], dn["slot"], dn["valid"], dn["active"]
         B, _, K = cls.shape
-        slot = torch.arange(pad, device=cls.device) % kc
-        nbg = nb * g
-        tcls = tg.classes[:, slot]
+        nbg = nb * dn["groups"].clamp(min=1).float()
+        sl = slot[None].expand(B, pad)
+        tcls = torch.gather(tg.classes, 1, sl)
         onehot = F.one_hot(tcls, K).to(cls.dtype) * valid[..., None].to(cls.dtype)
-        l_cls = sigmoid_focal_loss(cls[:, :pad], onehot, c.focal_alpha).sum() / nbg
-        pb, tb, v = box[:, :pad].float(), tboxes[:, slot].float(), valid.float()
+        focal = sigmoid_focal_loss(cls[:, :pad], onehot, c.focal_alpha)
+        l_cls = (focal * active[None, :, None].to(focal.dtype)).sum() / nbg
+        pb, v = box[:, :pad].float(), valid.float()
+        tb = torch.gather(tboxes.float(), 1, sl[..., None].expand(B, pad, 4))
         l_l1 = ((pb - tb).abs().sum(-1) * v).sum() / nbg
         giou = torch.diagonal(generalized_box_iou(box_cxcywh_to_xyxy(pb), box_cxcywh_to_xyxy(tb)), dim1=-2, dim2=-1)
         l_giou = ((1 - giou) * v).sum() / nbg
-        pm = mask[:, :pad].reshape(B, g, kc, *mask.shape[-2:])
-        l_bce, l_dice = self._mask_losses(pm, tg.masks, valid.view(B, g, kc), nbg)
+        l_bce, l_dice = self._mask_losses(mask[:, :pad], tmf, sl, valid, nbg)
         return dict(loss_ce=c.class_weight * l_cls, loss_bbox=c.box_weight * l_l1, loss_giou=c.giou_weight * l_giou,
                     loss_mask=c.mask_weight * l_bce, loss_dice=c.dice_weight * l_dice)
 
@@ -568,13 +594,14 @@ class MaskDINOCriterion:
             return total, losses
         assign = self.match(cls_m.detach(), box_m.detach(), [m.detach() for m in masks_m], tg, boxes)
         valid = tg.valid()
+        tmf = tg.masks.float()                         # the targets as f32 once per step
         for s, nm in enumerate(names):
             part = self._pair_losses(cls_m[s], box_m[s], masks_m[s], assign[s].long(), valid & (assign[s] >= 0),
-                                     tg, boxes, nb)
+                                     tg, tmf, boxes, nb)
             losses.update({k + nm: v for k, v in part.items()})
         if dn:
             for s in range(S):
-                part = self._dn_losses(out["classes"][s], out["boxes"][s], out["masks"][s], dn, tg, boxes, nb)
+                part = self._dn_losses(out["classes"][s], out["boxes"][s], out["masks"][s], dn, tg, tmf, boxes, nb)
                 nm = "_dn" if s == S - 1 else f"_dn_{s}"
                 losses.update({k + nm: v for k, v in part.items()})
         total = sum(losses.values())

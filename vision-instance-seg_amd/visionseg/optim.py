@@ -70,7 +70,13 @@ def param_hyper(model: nn.Module, solver):
 
 class FlatLayout:
     """Offsets of the parameters in the flat buffers (reverse registration order,
-    ALIGN-aligned), the optimiser chunk table and the all-reduce buckets."""
+    ALIGN-aligned), the optimiser chunk table and the all-reduce buckets.
+
+    The gradient buffers carry one FLAG per parameter after the parameters
+    ([flag_off, flag_off + num_params)): 1 when the parameter got a gradient this step.
+    The flags belong to the last bucket, so the all-reduce sums them across ranks (a
+    parameter with a gradient on any rank is updated, as DDP does) and the last bucket
+    launches after every other bucket has written its flags."""
 
     def __init__(self, entries, bucket_cap_mb: float = 25.0):
         self.entries = list(reversed(entries))          # backward order
@@ -79,12 +85,15 @@ class FlatLayout:
             n = p.numel()
             self.offsets.append((off, n))
             off += (n + ALIGN - 1) // ALIGN * ALIGN
-        self.total = off
+        self.total = off                                  # parameter elements (weights, state)
+        self.num_params = len(self.entries)
+        self.flag_off = off
+        self.size = off + (self.num_params + ALIGN - 1) // ALIGN * ALIGN      # gradient buffers
         rows, hyper, self.chunk_param = [], [], []
         for i, ((o, n), (_, _, lrm, wd)) in enumerate(zip(self.offsets, self.entries)):
             first, count = len(rows), max(1, (n + CHUNK - 1) // CHUNK)
             for c in range(count):
-                rows.append([o + c * CHUNK, max(0, min(CHUNK, n - c * CHUNK)), first, count])
+                rows.append([o + c * CHUNK, max(0, min(CHUNK, n - c * CHUNK)), first, count, i])
                 hyper.append([float(lrm), float(wd)])
                 self.chunk_param.append(i)
         self.table = torch.tensor(rows, dtype=torch.int32)
@@ -101,7 +110,7 @@ class FlatLayout:
             cur.append(i)
             self.bucket_of.append(len(self.buckets))
         if cur:
-            self.buckets.append((lo, self.total, cur))
+            self.buckets.append((lo, self.size, cur))
 
     def views(self, flat):
         return [flat[o:o + n].view(p.shape) for (o, n), (_, p, _, _) in zip(self.offsets, self.entries)]
@@ -129,18 +138,19 @@ class FlatOptimizer:
         self.params = [p for _, p, _, _ in lay.entries]
         kw = dict(device=self.device)
         self.weights = torch.zeros(lay.total, dtype=self.wdtype, **kw)
-        self.grads = torch.zeros(lay.total, dtype=self.wdtype, **kw)
+        self.grads = torch.zeros(lay.size, dtype=self.wdtype, **kw)
         self.master = self.weights if self.wdtype == torch.float32 else torch.zeros(lay.total, dtype=torch.float32, **kw)
         # f32 all-reduce buffer (bf16 models with more than one rank)
-        self.grads32 = (torch.zeros(lay.total, dtype=torch.float32, **kw)
+        self.grads32 = (torch.zeros(lay.size, dtype=torch.float32, **kw)
                         if self.world > 1 and self.wdtype != torch.float32 else None)
         self.state1 = torch.zeros(lay.total, dtype=torch.float32, **kw)
         self.state2 = torch.zeros(lay.total, dtype=torch.float32, **kw) if solver.optimizer == "adamw" else None
         self.lr = torch.full((), float(solver.lr), dtype=torch.float32, **kw)
         self.step_count = torch.zeros((), dtype=torch.float32, **kw)
+        self.param_steps = torch.zeros(lay.num_params, dtype=torch.float32, **kw)   # per parameter (AdamW)
         self.table = lay.table.to(self.device)
         self.hyper = lay.hyper.to(self.device)
-        self.workspace = torch.empty(lay.num_chunks, dtype=torch.float32, **kw)
+        self.workspace = torch.empty(lay.num_chunks + 1, dtype=torch.float32, **kw)
         with torch.no_grad():
             wv, mv = lay.views(self.weights), lay.views(self.master)
             for p, w, m in zip(self.params, wv, mv):
@@ -151,18 +161,24 @@ class FlatOptimizer:
                 p.data = w                          # the model now reads the flat buffer
         self.grad_views = lay.views(self.grads)
         self.reduce_views = lay.views(self.reduced_grads())
+        self.flags = self.reduced_grads()[lay.flag_off:lay.flag_off + lay.num_params]
+        self.flag_views = [self.flags[i:i + 1] for i in range(lay.num_params)]
 
     def zero_grad(self):
         """Before a backward: no .grad tensors, so autograd hands each parameter its
-        gradient without an accumulate kernel (gather_grads packs them afterwards)."""
+        gradient without an accumulate kernel (gather_grads packs them afterwards); every
+        parameter's gradient flag set (gather_grads clears those that get none)."""
         for p in self.params:
             p.grad = None
+        with torch.no_grad():
+            self.flags.fill_(1.0)
 
     def gather_grads(self, ids=None):
         """Pack the parameters' .grad tensors (all, or those listed) into the buffer the
         update reads -- the f32 all-reduce buffer when there is one (the bf16 -> f32
         widening happens in this copy) -- with multi-tensor copies; a parameter that got
-        no gradient this step gets zeros."""
+        no gradient this step gets zeros and its flag cleared: the step skips it (torch.optim
+        skips a parameter whose .grad is None), unless another rank's gradient arrives."""
         idx = range(len(self.params)) if ids is None else ids
         src, dst, missing = [], [], []
         for i in idx:
@@ -177,6 +193,7 @@ class FlatOptimizer:
                 torch._foreach_copy_(dst, src)
             if missing:
                 torch._foreach_zero_(missing)
+                torch._foreach_zero_([self.flag_views[i] for i in idx if self.params[i].grad is None])
 
     def set_lr(self, value: float):
         self.lr.fill_(float(value))
@@ -199,17 +216,18 @@ class FlatOptimizer:
                                       + (12 if opt else 8))
         with timed("flat_step", g, bytes_=nbytes):
             L.check(L.lib().vs_flat_step(
-                L.dtype_code(g), L.ptr(g), 1.0 / self.world, L.ptr(self.master), L.ptr(self.state1),
+                L.dtype_code(g), L.ptr(g), L.ptr(self.flags), 1.0 / self.world, L.ptr(self.master), L.ptr(self.state1),
                 L.ptr(self.state2) if self.state2 is not None else None, L.ptr(w16) if w16 is not None else None,
                 L.ptr(self.table), L.ptr(self.hyper), self.layout.num_chunks, opt, clip, float(s.clip_value), 1e-6,
                 float(s.momentum), float(s.betas[0]), float(s.betas[1]), float(s.eps), L.ptr(self.lr),
-                L.ptr(self.step_count), L.ptr(self.workspace), L.stream(g)), "flat_step")
+                L.ptr(self.step_count), L.ptr(self.param_steps), L.ptr(self.workspace), L.stream(g)), "flat_step")
 
     # ---------------------------------------------------------------- checkpoints
     def state_dict(self):
         return {"master": self.master.detach().cpu().clone(), "state1": self.state1.cpu().clone(),
                 "state2": None if self.state2 is None else self.state2.cpu().clone(),
-                "step": float(self.step_count), "names": list(self.names), "optimizer": self.solver.optimizer}
+                "step": float(self.step_count), "param_steps": self.param_steps.cpu().clone(),
+                "names": list(self.names), "optimizer": self.solver.optimizer}
 
     @torch.no_grad()
     def load_state_dict(self, sd):
@@ -222,6 +240,10 @@ class FlatOptimizer:
         if self.state2 is not None and sd["state2"] is not None:
             self.state2.copy_(sd["state2"])
         self.step_count.fill_(float(sd["step"]))
+        if sd.get("param_steps") is not None:
+            self.param_steps.copy_(sd["param_steps"])
+        else:                                   # older checkpoints: one global count
+            self.param_steps.fill_(float(sd["step"]))
         if self.master is not self.weights:
             self.weights.copy_(self.master)
 
