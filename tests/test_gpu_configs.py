@@ -1,0 +1,157 @@
+"""BASELINE configs C3, C4 and C5 exercised at their own workloads on one GPU (the
+per-GPU share of the 8-GPU runs): Swin-B at 1024^2 against the oracle, one Swin-L
+MaskDINO training step with 300 queries at 1024^2 (eager and graph-replayed), and one
+Swin-L 1536^2 training step with fp8 window attention plus its forward logits against the
+bf16-attention path.  The smaller-shape versions of these checks live in
+test_gpu_model.py, test_gpu_maskdino.py and test_gpu_fp8.py."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _perturbed(model, seed=1):
+    """init_weights + perturbed tables / offsets so every path carries signal, rounded to
+    bf16 (one oracle run serves the f32 and bf16 comparisons)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            if "rel_table" in n or "attention_weights" in n or "level_embed" in n:
+                p.add_(0.3 * torch.randn(p.shape, generator=g))
+        for p in model.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    return model
+
+
+def _rel(got, exp):
+    wmax = max(float((a.float().cpu() - b).abs().max()) / float(b.abs().max()) for a, b in zip(got, exp))
+    wmean = max(float((a.float().cpu() - b).abs().mean()) / float(b.abs().max()) for a, b in zip(got, exp))
+    return wmax, wmean
+
+
+def _train_steps(trainer, batch, n):
+    w0 = trainer.opt.master.clone()
+    losses = [float(trainer.step(*batch)) for _ in range(n)]
+    torch.cuda.synchronize()
+    assert all(np.isfinite(losses)), losses
+    assert bool(torch.isfinite(trainer.opt.master).all())
+    assert bool(torch.isfinite(trainer.opt.reduced_grads()).all())
+    assert float((trainer.opt.master - w0).abs().max()) > 0
+    return losses
+
+
+def test_c3_swin_b_1024_vs_oracle_and_training_step():
+    """C3 (Swin-B + Mask2Former, ws 12, 1024^2): the forward vs the oracle with the
+    oracle's attention masks forced in -- fp32 kernel mode within the BASELINE bound 1e-3,
+    the bf16 production path within max 0.05 / mean 0.006 of the step's max |logit| (the
+    bounds of test_gpu_model.test_swin_b_c3_model_vs_oracle at 512^2) -- then one bf16
+    training step at C3's per-GPU batch (4 x 1024^2): finite loss and gradients, weights
+    move."""
+    from oracle.ref_model import RefConfig, RefMask2Former
+    from visionseg.criterion import SetCriterion
+    from visionseg.data import synthetic_batch
+    from visionseg.model import M2FConfig, Mask2Former
+    from visionseg.train import SolverConfig, Trainer
+    cfg = M2FConfig.preset("swin_b")
+    m = _perturbed(Mask2Former(cfg).init_weights(0))
+    ref = RefMask2Former(RefConfig.from_dict(cfg.to_dict()))
+    ref.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
+    ref.eval()
+    m = m.to(DEV).eval()
+    px = torch.randn(1, 3, 1024, 1024, generator=torch.Generator().manual_seed(5)).to(torch.bfloat16).float()
+    with torch.no_grad():
+        ref.decoder.record = True
+        rmasks, rclasses = ref(px)
+        m.decoder.mask_override = [rb for rb, _ in ref.decoder.trace]
+        fmasks, fclasses = m(px.to(DEV))
+        f32err = max(float((a.cpu() - b).abs().max()) for a, b in zip(fmasks, rmasks))
+        cerr = max(float((a.cpu() - b).abs().max()) for a, b in zip(fclasses, rclasses))
+        del fmasks
+        m = m.to(torch.bfloat16)
+        bmasks, _ = m(px.to(DEV).to(torch.bfloat16))
+    ours = _rel(bmasks, rmasks)
+    print(f"C3 swin_b@1024: fp32-mode mask-logit max|err| {f32err:.2e} (class {cerr:.2e}); bf16 production "
+          f"max|err|/max|logit| {ours[0]:.2e}, mean {ours[1]:.2e}")
+    assert f32err <= 1e-3 and cerr <= 1e-3
+    assert ours[0] <= 0.05 and ours[1] <= 0.006
+    del m, bmasks
+    torch.cuda.empty_cache()
+    model = Mask2Former(cfg).init_weights(0)
+    tr = Trainer(model, SetCriterion(cfg), SolverConfig(warmup_iters=0), device=DEV)
+    batch = synthetic_batch(4, 1024, seed=42, device=DEV)
+    print("C3 losses", _train_steps(tr, batch, 2))
+
+
+def test_c4_swin_l_maskdino_300q_1024_step_and_graph_replay():
+    """C4 (Swin-L + MaskDINO, 300 queries, 4-level encoder, denoising, 1024^2; parity
+    unpinned: no MaskDINO oracle exists in the container): bf16 training steps through
+    the product Trainer, eager and HIP-graph-replayed (capture after 2 eager steps), on
+    the same batches and seeds -- finite losses and gradients, weights move, and the
+    replayed losses equal the eager ones within the tolerance of
+    test_gpu_maskdino.test_graph_replay_matches_eager (the denoising layout no longer
+    depends on the padded target capacity, tests/test_maskdino_host.py)."""
+    from visionseg.data import synthetic_batch
+    from visionseg.maskdino import MaskDINO, MaskDINOConfig, MaskDINOCriterion
+    from visionseg.train import SolverConfig, Trainer
+    cfg = MaskDINOConfig.preset("swin_l", num_queries=300)
+    m = MaskDINO(cfg).init_weights(0)
+    batch = synthetic_batch(2, 1024, seed=42, device=DEV)
+    ta = Trainer(copy.deepcopy(m), MaskDINOCriterion(cfg), SolverConfig(warmup_iters=0), device=DEV)
+    tb = Trainer(m, MaskDINOCriterion(cfg), SolverConfig(warmup_iters=0), device=DEV, graphs=True)
+    la, lb = [], []
+    wa0, wb0 = ta.opt.master.clone(), tb.opt.master.clone()
+    for i in range(4):
+        torch.manual_seed(100 + i)
+        la.append(float(ta.step(*batch)))
+        torch.manual_seed(100 + i)
+        lb.append(float(tb.step(*batch)))
+    torch.cuda.synchronize()
+    print("C4 eager", la, "graph", lb)
+    assert len(tb._graph_states) == 1                      # steps 3 and 4 were replays
+    for tr, w0 in ((ta, wa0), (tb, wb0)):
+        assert bool(torch.isfinite(tr.opt.master).all()) and float((tr.opt.master - w0).abs().max()) > 0
+    assert all(np.isfinite(la + lb))
+    for a, b in zip(la, lb):
+        assert abs(a - b) <= 3e-2 * max(1.0, abs(a)), (la, lb)
+
+
+def test_c5_swin_l_1536_fp8_step_and_logits():
+    """C5 (Swin-L + Mask2Former, fp8 (e4m3) window attention in every Swin block, bf16
+    elsewhere, 1536^2): the forward mask logits with fp8 attention vs the same model with
+    bf16 attention (relative to the step's max |logit|: max <= 0.08, mean <= 0.01, the
+    absolute caps of test_gpu_fp8.test_swin_l_fp8_model_vs_oracle), then one fp8 training
+    step at 1536^2: finite loss and gradients, weights move."""
+    from visionseg.criterion import SetCriterion
+    from visionseg.data import synthetic_batch
+    from visionseg.model import M2FConfig, Mask2Former
+    from visionseg.train import SolverConfig, Trainer
+    cfg = M2FConfig.preset("swin_l", attn_fp8=True)
+    m = _perturbed(Mask2Former(cfg).init_weights(0)).to(DEV).to(torch.bfloat16).eval()
+    px = torch.randn(1, 3, 1536, 1536, generator=torch.Generator().manual_seed(5)).to(DEV).to(torch.bfloat16)
+    from visionseg.model import unpack_bitmask_like
+    keys = [(1536 // st) ** 2 for st in (32, 16, 8)]          # decoder layer i attends level i % 3
+    with torch.no_grad():
+        res = {}
+        for fp8 in (False, True):
+            for st in m.backbone.stages:
+                for blk in st.blocks:
+                    blk.attn_fp8 = fp8
+            m.decoder.record = not fp8
+            masks, _ = m(px)
+            if not fp8:       # the bf16 run's attention masks forced into the fp8 run
+                m.decoder.mask_override = [unpack_bitmask_like(w, keys[i % 3]) for i, w in enumerate(m.decoder.trace)]
+            res[fp8] = [x.float().cpu() for x in masks]
+        m.decoder.mask_override = None
+    d = _rel(res[True], res[False])
+    print(f"C5 swin_l@1536 fp8 vs bf16 attention: max|diff|/max|logit| {d[0]:.2e}, mean {d[1]:.2e}")
+    assert d[0] <= 0.08 and d[1] <= 0.01
+    del m
+    torch.cuda.empty_cache()
+    model = Mask2Former(cfg).init_weights(0)
+    tr = Trainer(model, SetCriterion(cfg), SolverConfig(warmup_iters=0), device=DEV)
+    batch = synthetic_batch(1, 1536, seed=42, device=DEV)
+    print("C5 fp8 losses", _train_steps(tr, batch, 2))

@@ -223,3 +223,29 @@ def test_criterion_without_targets_and_without_dn():
     out = _fake_outputs(cfg, tg, boxes, dec, 2, dn=False)
     loss, parts = MaskDINOCriterion(cfg, matcher="host")(out, tg, boxes)
     assert torch.isfinite(loss) and not any("_dn" in k for k in parts)
+
+
+def test_init_detector_maskdino_backbone_from_config_or_checkpoint(tmp_path):
+    """A MaskDINO checkpoint served by init_detector takes its backbone from the config
+    argument (object or JSON file) when one is given and from its own backbone tensors
+    otherwise -- not silently from the swin_t preset (inference.py)."""
+    import json
+    from visionseg.inference import backbone_from_state_dict, init_detector
+    from visionseg.maskdino import MaskDINO
+    # non-backbone parts at the MaskDINO defaults: a checkpoint alone must then be enough
+    cfg = MaskDINOConfig(embed_dim=64, depths=(1, 1, 3, 1), num_heads=(2, 4, 8, 16), window_size=5, num_labels=3)
+    m = MaskDINO(cfg)
+    path = tmp_path / "md.pth"
+    torch.save({"model": m.state_dict()}, path)
+    got = backbone_from_state_dict(m.state_dict())
+    assert got == dict(embed_dim=64, depths=(1, 1, 3, 1), num_heads=(2, 4, 8, 16), window_size=5)
+    for config in (None, cfg, str(tmp_path / "c.json")):
+        if isinstance(config, str):
+            with open(config, "w") as f:
+                json.dump(cfg.to_dict(), f)
+        det = init_detector(config, str(path), device="cpu")
+        c = det.model.cfg
+        assert (c.embed_dim, tuple(c.depths), tuple(c.num_heads), c.window_size, c.num_labels) == \
+            (64, (1, 1, 3, 1), (2, 4, 8, 16), 5, 3)
+    with pytest.raises(ValueError):
+        backbone_from_state_dict({"backbone.patch_embed.proj.weight": torch.zeros(8, 3, 4, 4)})

@@ -74,6 +74,8 @@ def main():
                 os.environ["VS_MSDA_MFMA"] = "0" if mode == "binned" else "1"
                 # fwd1: the runtime-P forward kernel instead of the unrolled P = 4 one
                 os.environ["VS_MSDA_FWD4"] = "0" if mode == "fwd1" else "1"
+                # syncbar: __syncthreads instead of the LDS-only barriers in the band walk
+                os.environ["VS_MSDA_LDSBAR"] = "0" if mode == "syncbar" else "1"
 
                 def fb():
                     o = ops.ms_deform_attn(v, shapes, locr, wr)

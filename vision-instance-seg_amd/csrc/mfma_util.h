@@ -58,6 +58,13 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier for LDS ordering only: waits for this wave's LDS traffic
+// (lgkmcnt), NOT for its outstanding global loads / stores / atomics -- __syncthreads'
+// release fence drains vmcnt, so a kernel that issues fire-and-forget atomics before a
+// barrier whose only job is LDS reuse would stall on their round trip to L2.  Use only
+// where no other wave reads global memory this wave wrote before the barrier.
+__device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // C-tile row of register i for lane half hh
 __device__ __forceinline__ constexpr int crow(int i, int hh) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
 

@@ -923,7 +923,7 @@ constexpr int kBandCap = 128;
 constexpr int kWP8 = 68;       // W row pitch (floats): 64 queries + 4
 constexpr int kDP = 132;       // Dm row pitch (floats): 128 band cells + 4
 
-template <int TX, int TY, bool GEOM>
+template <int TX, int TY, bool GEOM, bool LB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) msda_bwd_mfma_wg_kernel(const float* __restrict__ loc,
                                                                const float* __restrict__ attw,
                                                                const bf16* __restrict__ gout,
@@ -943,6 +943,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
   const int tile = (blk / Hh) % qt.per_image;
   const int b = blk / Hh / qt.per_image;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  // LB: every barrier of the band walk orders LDS only (lds_barrier), so the band's
+  // fire-and-forget grad_value atomics stay in flight across the next band's barriers
+  auto bar = [&]() {
+    if (LB) lds_barrier();
+    else __syncthreads();
+  };
+  __shared__ int sAny[2][4];
+  int band_par = 0;
   const int LP = L * P;
   const int tq = tid >> 2, tpt = tid & 3;
   const int qid = btile_query<TX, TY>(qt, lv, L, tile, tq, Q);
@@ -1006,7 +1014,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
         sBox[wave][3] = d;
       }
     }
-    __syncthreads();
+    bar();
     int oy = sBox[0][0], yh = sBox[0][1], ox = sBox[0][2], xh = sBox[0][3];
 #pragma unroll
     for (int w = 1; w < 4; ++w) {
@@ -1015,7 +1023,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
       ox = min(ox, sBox[w][2]);
       xh = max(xh, sBox[w][3]);
     }
-    __syncthreads();                          // sBox is rewritten by the next level
+    bar();                                    // sBox is rewritten by the next level
     float dk[4] = {0.f, 0.f, 0.f, 0.f};       // GEOM: grad_out . value at the tap's corners
     const int BY = yh < 0 ? 0 : yh - oy + 1, BX = yh < 0 ? 1 : xh - ox + 1;   // yh < 0: no corner here
     const int SBX = min(BX, kBandCap), SBY = kBandCap / SBX;
@@ -1031,12 +1039,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
           cell[k] = in ? yy * bw + xx : -1;
           any |= in;
         }
-        if (!__syncthreads_or(any)) continue;   // empty band (also the barrier after the last one)
+        bool band_any;
+        if (LB) {                             // double-buffered per-wave flags: a wave cannot
+          if (lane == 0) sAny[band_par][wave] = __ballot(any) != 0;   // lap a slower one by 2
+          lds_barrier();
+          band_any = sAny[band_par][0] | sAny[band_par][1] | sAny[band_par][2] | sAny[band_par][3];
+          band_par ^= 1;
+        } else {
+          band_any = __syncthreads_or(any);
+        }
+        if (!band_any) continue;              // empty band (also the barrier after the last one)
         const int ncell = bw * bh, nmt = (ncell + 31) >> 5;
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int i = tid; i < nmt * 32 * (kWP8 / 4); i += 256) reinterpret_cast<float4*>(sW)[i] = z4;
         for (int i = tid; i < nmt * 32; i += 256) sHit[i] = 0;
-        __syncthreads();
+        bar();
 #pragma unroll
         for (int pt = 0; pt < P; ++pt) {      // a query's 4 points are lanes of one wave: take turns
           if (tpt == pt) {
@@ -1049,7 +1066,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
           }
           wave_sync();
         }
-        __syncthreads();
+        bar();
         for (int m = wave; m < nmt; m += 4) {
           f32x16_t acc;
           zero16(acc);
@@ -1078,7 +1095,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
             }
           }
         }
-        __syncthreads();                      // W / hit flags are rewritten by the next band
+        bar();                                // W / hit flags are rewritten by the next band
         if (GEOM) {
           // Dm[q][cell] over the band: wave w takes cell tile w (value rows loaded once)
           float* sD = sW;
@@ -1104,11 +1121,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
               for (int i = 0; i < 16; ++i) sD[(32 * mq + crow(i, hh)) * kDP + 32 * wave + r] = acc[i];
             }
           }
-          __syncthreads();
+          bar();
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (cell[k] >= 0) dk[k] += sD[tq * kDP + cell[k]];
-          __syncthreads();                    // Dm is overwritten by the next band's W
+          bar();                              // Dm is overwritten by the next band's W
         }
       }
     }
@@ -1238,11 +1255,18 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     bt.per_image = bt.mode == 1 ? bt.prefix[L] : (Q + te * te - 1) / (te * te);
     const long long nb2 = (long long)B * bt.per_image * Hh;
     VS_CHECK(nb2 < (1LL << 31), "too many query tiles");
-    if (mfma && fused)
-      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
-                         (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc, gattw);
+    bool ldsbar = true;                      // VS_MSDA_LDSBAR=0: __syncthreads in the band walk
+    if (const char* e = getenv("VS_MSDA_LDSBAR")) ldsbar = atoi(e) != 0;
+    if (mfma && fused && ldsbar)
+      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true, true>), dim3((unsigned)nb2), dim3(256), 0, st, loc,
+                         attw, (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc,
+                         gattw);
+    else if (mfma && fused)
+      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true, false>), dim3((unsigned)nb2), dim3(256), 0, st, loc,
+                         attw, (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc,
+                         gattw);
     else if (mfma)
-      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, false>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
+      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, false, false>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
                          (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)nullptr, nullptr,
                          nullptr);
     else if (dtype == VS_BF16)

@@ -57,27 +57,39 @@ std::vector<int64_t> host_i64(const at::Tensor& t, const char* what) {
 }
 
 // ---- a8: MSDeformAttn sampling (upstream MultiScaleDeformableAttention.ms_deform_attn_*)
+struct MsdaDims {
+  int64_t B, S, H, D, Q, L, P;
+};
+
+// one shape check for both directions: value [B, S, heads, 32], sampling_loc [B, Q, heads, L,
+// P, 2] f32, attn_weight [B, Q, heads, L, P] f32, L levels of shapes / starts
+MsdaDims check_msda(const at::Tensor& value, const std::vector<int64_t>& sh, const std::vector<int64_t>& st,
+                    const at::Tensor& loc, const at::Tensor& aw) {
+  TORCH_CHECK(value.dim() == 4, "value must be [B, S, heads, 32]");
+  TORCH_CHECK(loc.dim() == 6 && loc.size(5) == 2, "sampling_loc must be [B, Q, heads, L, P, 2]");
+  TORCH_CHECK(loc.scalar_type() == at::kFloat && aw.scalar_type() == at::kFloat,
+              "sampling_loc / attn_weight must be float32");
+  MsdaDims d{value.size(0), value.size(1), value.size(2), value.size(3), loc.size(1), loc.size(3), loc.size(4)};
+  TORCH_CHECK((int64_t)sh.size() == 2 * d.L && (int64_t)st.size() == d.L,
+              "spatial_shapes / level_start_index do not have ", d.L, " levels");
+  TORCH_CHECK(loc.size(0) == d.B && loc.size(2) == d.H, "sampling_loc batch/heads do not match value");
+  TORCH_CHECK(aw.sizes() == at::IntArrayRef({d.B, d.Q, d.H, d.L, d.P}), "attn_weight must be [B, Q, heads, L, P]");
+  return d;
+}
+
 at::Tensor msda_fwd(const at::Tensor& value, const at::Tensor& spatial_shapes, const at::Tensor& level_start_index,
                     const at::Tensor& sampling_loc, const at::Tensor& attn_weight, int64_t im2col_step) {
   (void)im2col_step;  // the kernel tiles by query groups, not im2col steps
   on_device({&value, &sampling_loc, &attn_weight});
-  TORCH_CHECK(value.dim() == 4, "value must be [B, S, heads, 32]");
-  TORCH_CHECK(sampling_loc.dim() == 6 && sampling_loc.size(5) == 2, "sampling_loc must be [B, Q, heads, L, P, 2]");
-  TORCH_CHECK(sampling_loc.scalar_type() == at::kFloat && attn_weight.scalar_type() == at::kFloat,
-              "sampling_loc / attn_weight must be float32");
   const auto sh = host_i64(spatial_shapes, "spatial_shapes");
   const auto st = host_i64(level_start_index, "level_start_index");
   at::Tensor v = value.contiguous(), loc = sampling_loc.contiguous(), aw = attn_weight.contiguous();
-  const int64_t B = v.size(0), S = v.size(1), H = v.size(2), D = v.size(3);
-  const int64_t Q = loc.size(1), L = loc.size(3), P = loc.size(4);
-  TORCH_CHECK((int64_t)sh.size() == 2 * L && (int64_t)st.size() == L, "spatial_shapes / level_start_index do not have ",
-              L, " levels");
-  TORCH_CHECK(loc.size(0) == B && loc.size(2) == H, "sampling_loc batch/heads do not match value");
-  TORCH_CHECK(aw.sizes() == at::IntArrayRef({B, Q, H, L, P}), "attn_weight must be [B, Q, heads, L, P]");
-  at::Tensor out = at::empty({B, Q, H * D}, v.options());
+  const MsdaDims d = check_msda(v, sh, st, loc, aw);
+  at::Tensor out = at::empty({d.B, d.Q, d.H * d.D}, v.options());
   vs_ok(vs_msda_forward(dcode(v), v.data_ptr(), sh.data(), st.data(), loc.data_ptr<float>(), aw.data_ptr<float>(),
-                        out.data_ptr(), as_int(B, "batch"), as_int(S, "S"), as_int(H, "heads"), as_int(D, "channels"),
-                        as_int(L, "levels"), as_int(Q, "queries"), as_int(P, "points"), cur_stream(v)),
+                        out.data_ptr(), as_int(d.B, "batch"), as_int(d.S, "S"), as_int(d.H, "heads"),
+                        as_int(d.D, "channels"), as_int(d.L, "levels"), as_int(d.Q, "queries"), as_int(d.P, "points"),
+                        cur_stream(v)),
         "msda_fwd");
   return out;
 }
@@ -94,19 +106,18 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> msda_bwd(const at::Tensor& value,
   const auto sh = host_i64(spatial_shapes, "spatial_shapes");
   const auto st = host_i64(level_start_index, "level_start_index");
   at::Tensor v = value.contiguous(), loc = sampling_loc.contiguous(), aw = attn_weight.contiguous();
+  const MsdaDims d = check_msda(v, sh, st, loc, aw);
+  TORCH_CHECK(grad_output.numel() == d.B * d.Q * d.H * d.D && grad_output.dim() >= 2 && grad_output.size(0) == d.B &&
+                  grad_output.size(1) == d.Q,
+              "grad_output must be [B, Q, heads*32]");
   at::Tensor g = grad_output.to(v.scalar_type()).contiguous();
-  const int64_t B = v.size(0), S = v.size(1), H = v.size(2), D = v.size(3);
-  const int64_t Q = loc.size(1), L = loc.size(3), P = loc.size(4);
-  TORCH_CHECK((int64_t)sh.size() == 2 * L && (int64_t)st.size() == L, "spatial_shapes / level_start_index do not have ",
-              L, " levels");
-  TORCH_CHECK(g.numel() == B * Q * H * D, "grad_output must be [B, Q, heads*32]");
   // grad_value accumulates in f32 (float atomics), then takes value's dtype
-  at::Tensor gv = at::empty({B, S, H, D}, v.options().dtype(at::kFloat));
+  at::Tensor gv = at::empty({d.B, d.S, d.H, d.D}, v.options().dtype(at::kFloat));
   at::Tensor gl = at::empty_like(loc), ga = at::empty_like(aw);
   vs_ok(vs_msda_backward(dcode(v), v.data_ptr(), sh.data(), st.data(), loc.data_ptr<float>(), aw.data_ptr<float>(),
                          g.data_ptr(), gv.data_ptr<float>(), gl.data_ptr<float>(), ga.data_ptr<float>(),
-                         as_int(B, "batch"), as_int(S, "S"), as_int(H, "heads"), as_int(D, "channels"),
-                         as_int(L, "levels"), as_int(Q, "queries"), as_int(P, "points"), cur_stream(v)),
+                         as_int(d.B, "batch"), as_int(d.S, "S"), as_int(d.H, "heads"), as_int(d.D, "channels"),
+                         as_int(d.L, "levels"), as_int(d.Q, "queries"), as_int(d.P, "points"), cur_stream(v)),
         "msda_bwd");
   return {(v.scalar_type() == at::kFloat || f32_grad_value) ? gv : gv.to(v.scalar_type()), gl, ga};
 }
@@ -186,7 +197,12 @@ std::tuple<at::Tensor, at::Tensor> win_attn_bwd(const at::Tensor& qkv, const at:
   check_qkv(qkv, heads, window);
   at::Tensor q = qkv.contiguous(), table = rel_table.to(at::kFloat).contiguous();
   at::Tensor o = out.contiguous(), l = lse.contiguous(), g = grad_out.to(q.scalar_type()).contiguous();
-  const int64_t Bw = q.size(0), T2 = (2 * window - 1) * (2 * window - 1);
+  const int64_t Bw = q.size(0), N = q.size(1), T2 = (2 * window - 1) * (2 * window - 1);
+  TORCH_CHECK(o.sizes() == at::IntArrayRef({Bw, N, heads * 32}) && g.sizes() == o.sizes(),
+              "out / grad_out must be [B*nW, window^2, heads*32]");
+  TORCH_CHECK(l.scalar_type() == at::kFloat && l.sizes() == at::IntArrayRef({Bw, heads, N}),
+              "lse must be float32 [B*nW, heads, window^2]");
+  TORCH_CHECK(table.numel() == T2 * heads, "rel_table must be [(2ws-1)^2, heads]");
   at::Tensor gqkv = at::empty_like(q);
   at::Tensor part = at::empty({Bw, heads, T2}, q.options().dtype(at::kFloat));
   if (fp8) {
@@ -310,6 +326,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> masked_xattn_bwd(const at::Tensor
   at::Tensor oc = out.contiguous(), lc = lse.contiguous(), g = grad_out.to(q.scalar_type()).contiguous();
   TORCH_CHECK(kc.scalar_type() == qc.scalar_type() && vc.scalar_type() == qc.scalar_type(), "q / k / v dtypes differ");
   const int B = as_int(q.size(0), "batch"), Q = as_int(q.size(1), "queries"), S = as_int(k.size(1), "keys");
+  TORCH_CHECK(oc.sizes() == qc.sizes() && g.sizes() == qc.sizes(), "out / grad_out must be shaped like q");
+  TORCH_CHECK(lc.scalar_type() == at::kFloat && lc.sizes() == at::IntArrayRef({(int64_t)B, heads, (int64_t)Q}),
+              "lse must be float32 [B, heads, Q]");
   at::Tensor gq = at::empty_like(qc), gk = at::empty_like(kc), gv = at::empty_like(vc);
   at::Tensor ws = at::empty({vs_masked_attn_workspace_bytes(B, Q, S, (int)heads)}, qc.options().dtype(at::kByte));
   vs_ok(vs_masked_attn_backward(dcode(qc), qc.data_ptr(), kc.data_ptr(), vc.data_ptr(), (const uint32_t*)wc.data_ptr(),

@@ -134,31 +134,65 @@ def load_checkpoint(path: str, device="cpu") -> dict:
     return sd
 
 
+def backbone_from_state_dict(sd: dict) -> dict:
+    """Swin backbone hyper-parameters (embed_dim, depths, num_heads, window_size) read off a
+    checkpoint's backbone tensors: patch-embedding width, blocks per stage, and the
+    relative-position tables [(2ws-1)^2, heads] of each stage."""
+    import math
+    import re
+    embed = int(sd["backbone.patch_embed.proj.weight"].shape[0])
+    blocks, heads, ws = {}, {}, None
+    for k, v in sd.items():
+        mt = re.match(r"backbone\.stages\.(\d+)\.blocks\.(\d+)\.attn\.rel_table$", k)
+        if mt:
+            i, j = int(mt.group(1)), int(mt.group(2))
+            blocks[i] = max(blocks.get(i, 0), j + 1)
+            heads[i] = int(v.shape[1])
+            ws = (int(round(math.sqrt(v.shape[0]))) + 1) // 2
+    n = len(blocks)
+    if not n or sorted(blocks) != list(range(n)):
+        raise ValueError("the checkpoint's backbone stages could not be read")
+    return dict(embed_dim=embed, depths=tuple(blocks[i] for i in range(n)),
+                num_heads=tuple(heads[i] for i in range(n)), window_size=ws)
+
+
 def init_detector(config, checkpoint: str | None = None, device: str = "cuda:0") -> Predictor:
     """mmdet.apis.init_detector-compatible entry (ai_segmentation.py:41-50).
-    `config`: an M2FConfig, a preset name ("swin_t", "swin_b", ...; "maskdino_swin_t" ...
-    for MaskDINO), or a JSON file.  A MaskDINO checkpoint (train_maskdino's) is recognised
-    by its keys and served by the MaskDINO model with the preset's backbone."""
+    `config`: an M2FConfig / MaskDINOConfig, a preset name ("swin_t", "swin_b", ...;
+    "maskdino_swin_t" ... for MaskDINO), or a JSON file (a config dict, or {"preset":
+    name}).  A MaskDINO checkpoint (train_maskdino's) is recognised by its keys; its
+    backbone comes from the config when one is given, else from the checkpoint's own
+    backbone tensors (an explicit error when neither can be read)."""
+    from .maskdino import MaskDINO, MaskDINOConfig
     sd = load_checkpoint(checkpoint) if checkpoint else None
     name = config if isinstance(config, str) and not os.path.exists(config) else None
-    maskdino = bool(name and name.startswith("maskdino")) or bool(
+    given = None                                    # a config dict from the argument / JSON file
+    if isinstance(config, M2FConfig):
+        given = config.to_dict()
+    elif isinstance(config, str) and os.path.exists(config):
+        with open(config) as f:
+            given = json.load(f)
+        if set(given) == {"preset"}:
+            name, given = given["preset"], None
+    maskdino = isinstance(config, MaskDINOConfig) or bool(name and name.startswith("maskdino")) or bool(
         sd is not None and any(k.startswith("decoder.enc_output.") for k in sd))
     if maskdino:
-        from .maskdino import MaskDINO, MaskDINOConfig
-        preset = (name or "swin_t").replace("maskdino_", "") or "swin_t"
-        kw = {}
-        if sd is not None and "decoder.class_embed.weight" in sd:
-            kw["num_labels"] = int(sd["decoder.class_embed.weight"].shape[0])
-        model = MaskDINO(MaskDINOConfig.preset(preset, **kw))
-    else:
-        if isinstance(config, M2FConfig):
-            cfg = config
-        elif isinstance(config, str) and os.path.exists(config):
-            with open(config) as f:
-                d = json.load(f)
-            cfg = M2FConfig.preset(d.pop("preset")) if "preset" in d and len(d) == 1 else M2FConfig.from_dict(d)
+        if given is not None:
+            cfg = MaskDINOConfig.from_dict(given)
+        elif name:
+            cfg = MaskDINOConfig.preset(name.replace("maskdino_", "") or "swin_t")
+        elif sd is not None:
+            cfg = MaskDINOConfig.from_dict(backbone_from_state_dict(sd))
         else:
-            cfg = M2FConfig.preset(config or "swin_t")
+            cfg = MaskDINOConfig.preset("swin_t")
+        if sd is not None and "decoder.class_embed.weight" in sd:
+            cfg.num_labels = int(sd["decoder.class_embed.weight"].shape[0])
+        model = MaskDINO(cfg)
+    else:
+        if given is not None:
+            cfg = M2FConfig.from_dict(given)
+        else:
+            cfg = M2FConfig.preset(name or "swin_t")
         model = Mask2Former(cfg)
     if sd is not None:
         model.load_state_dict(sd)
