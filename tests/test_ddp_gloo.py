@@ -162,3 +162,106 @@ def test_flat_layout_buckets_and_groups():
     assert lay.flag_off == lay.total and lay.size >= lay.total + lay.num_params
     assert lay.buckets[-1][0] <= lay.flag_off and lay.buckets[-1][1] == lay.size
     assert lay.table[:, 4].tolist() == lay.chunk_param
+
+
+class _StubEvent:
+    """Stands in for optim.ExternalEvent on CPU (no HIP): logs record / wait order."""
+    log = []
+
+    def __init__(self):
+        self.id = len([e for e in _StubEvent.log if e[0] == "new"])
+        _StubEvent.log.append(("new", self.id))
+
+    def record(self, stream=None):
+        _StubEvent.log.append(("record", self.id))
+
+    def wait(self, stream):
+        _StubEvent.log.append(("wait", self.id))
+
+
+class _StubStream:
+    def wait_stream(self, other):
+        pass
+
+
+def _capture_worker(rank, world, port, data, out_q):
+    """GradReducer in "capture" mode (what a captured HIP-graph step records) followed by
+    replay_collectives() (what the trainer issues after launching the graph), with the
+    HIP events and streams stubbed: bucket events recorded in bucket order during the
+    backward, one all-reduce per bucket in index order behind its event, the f32 sums of
+    the ranks' gradients in the buffer, and the same update as the eager path."""
+    import contextlib
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import _flatref
+    from visionseg import optim
+    from visionseg.train import Trainer, init_distributed
+    optim.FlatOptimizer.step = _flatref.flat_step_reference
+    optim.ExternalEvent = _StubEvent
+    torch.cuda.current_stream = lambda *a, **k: _StubStream()
+    torch.cuda.stream = lambda s: contextlib.nullcontext()
+    init_distributed("gloo")
+    x = data[rank:rank + 1]
+    res = {}
+    for mode in ("eager", "capture"):
+        tr = Trainer(TinyNet(), _mse_criterion, _solver("sgd", "norm"), device="cpu")
+        red = tr.reducer
+        nb = len(tr.opt.layout.buckets)
+        calls = []
+        real = dist.all_reduce
+
+        def counting(t, *a, **k):
+            calls.append((t.data_ptr() - red.buf.data_ptr()) // t.element_size())
+            return real(t, *a, **k)
+        dist.all_reduce = counting
+        _StubEvent.log = []
+        tr._set_lr()
+        tr.opt.zero_grad()
+        red.begin(mode)
+        loss, _ = tr.forward_loss(x, None, None)
+        loss.backward()
+        red.finish_backward()
+        if mode == "capture":
+            assert not calls, "a collective was issued during the capture"
+            recs = [e[1] for e in _StubEvent.log if e[0] == "record"]
+            assert recs == list(range(nb)), recs                       # launch order = bucket index
+            red.replay_collectives()
+            waits = [e[1] for e in _StubEvent.log if e[0] == "wait"]
+            assert waits == list(range(nb)), waits
+        dist.all_reduce = real
+        assert calls == [lo for lo, _, _ in tr.opt.layout.buckets], calls  # every bucket once, in order
+        res[mode] = (red.buf.detach().clone(), None)
+        tr.apply_gradients()
+        res[mode] = (res[mode][0], tr.opt.master.detach().clone())
+    out_q.put((rank, {m: (g.numpy().copy(), w.numpy().copy()) for m, (g, w) in res.items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_capture_mode_bucket_order():
+    torch.manual_seed(1)
+    data = torch.randn(2, 3, 16, 16)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_capture_worker, args=(r, world, port, data, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, r0), (_, r1) = res
+    for mode in ("eager", "capture"):
+        assert (r0[mode][0] == r1[mode][0]).all() and (r0[mode][1] == r1[mode][1]).all()
+    # capture + replay == eager: the same reduced f32 gradients (flags included) and update
+    assert (r0["capture"][0] == r0["eager"][0]).all()
+    assert (r0["capture"][1] == r0["eager"][1]).all()
+    # the reduced buffer holds the SUM over ranks: every flag of a used parameter is 2
+    from visionseg.optim import FlatLayout, param_hyper
+    from visionseg.train import SolverConfig
+    lay = FlatLayout(param_hyper(TinyNet(), SolverConfig()), 1e-4)
+    flags = r0["capture"][0][lay.flag_off:lay.flag_off + lay.num_params]
+    used = [n != "unused" for n, _, _, _ in lay.entries]
+    assert [float(f) for f in flags] == [2.0 if u else 0.0 for u in used]
