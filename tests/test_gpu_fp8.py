@@ -1,12 +1,15 @@
 """fp8 (OCP e4m3) window attention, BASELINE config C5 (Swin-L, 1536^2, "fp8 MFMA
-window-attention path"), through vs_window_attn_forward_fp8 / _backward_fp8.
+window-attention path"), through vs_window_attn_forward_fp8 / _backward_fp8: the
+block-scaled MX MFMA v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 operands, one e8m0 scale per
+32-element block: every q / k token, and per (query, 32-key block) of P and (channel,
+32-key block) of V).
 
 Two yardsticks per case:
   * the kernel's own quantisation model, emulated in torch on the CPU (f32 math on
-    torch.float8_e4m3fn-rounded operands, the same per-(window, head) power-of-two
-    scales): checks the MFMA fragment layout, the scales and the descale exactly up to
-    f32 summation order and the occasional one-ulp e4m3 flip of P (the kernel's exp
-    differs from torch's in the last f32 bit);
+    torch.float8_e4m3fn-rounded operands, the same power-of-two block scales and the same
+    grouping of keys into scale blocks): checks the MX fragment layout, the scales and the
+    fused dequantisation up to f32 summation order and the occasional one-ulp e4m3 flip
+    of P (the kernel's exp differs from torch's in the last f32 bit);
   * the exact fp32 oracle (oracle/ref_ops.window_attention_ref, pinned to HF): the fp8
     error budget, stated per test as a relative RMS / max bound.
 The backward is the gradient of the quantised logits with straight-through operands
@@ -34,6 +37,23 @@ def _q8(x, s):
     return (x * s).to(E4M3).float() / s
 
 
+def _key_groups(N):
+    """Scale block of every key in the kernel's P V product: 64 keys (key tiles 2b, 2b+1)
+    per instruction, lane half hh = bit 2 of the key's row in its 32-key tile
+    (accumulator rows crow(i, hh) = (i & 3) + 8 (i >> 2) + 4 hh)."""
+    t = torch.arange(N)
+    return 2 * (t // 64) + ((t % 32) >> 2 & 1)
+
+
+def _q8_groups(x, grp):
+    """e4m3 rounding of x [..., N] with one power-of-two scale per key group."""
+    G = int(grp.max()) + 1
+    idx = grp.expand_as(x)
+    am = torch.zeros(*x.shape[:-1], G).scatter_reduce(-1, idx, x.abs(), "amax", include_self=True)
+    s = torch.gather(_pow2_scale(am), -1, idx)
+    return _q8(x, s)
+
+
 def _split(qkv, heads):
     Bw, N, C3 = qkv.shape
     q, k, v = qkv.float().view(Bw, N, 3, heads, 32).permute(2, 0, 3, 1, 4)   # [Bw, heads, N, 32]
@@ -51,8 +71,8 @@ def _bias_mask(table, ws, shift, nWh, nWw, Bw):
 
 
 def _fp8_logits(q, k, bm, scale):
-    sq = _pow2_scale(q.abs().amax(dim=(2, 3), keepdim=True))
-    sk = _pow2_scale(k.abs().amax(dim=(2, 3), keepdim=True))
+    sq = _pow2_scale(q.abs().amax(dim=3, keepdim=True))          # one scale per token (32 channels)
+    sk = _pow2_scale(k.abs().amax(dim=3, keepdim=True))
     return (_q8(q, sq) @ _q8(k, sk).transpose(2, 3)) * scale + bm
 
 
@@ -63,8 +83,9 @@ def emulate_fwd(qkv, table, heads, ws, shift, nWh, nWw, scale=32 ** -0.5):
     m = s.amax(-1, keepdim=True)
     p = torch.exp(s - m)
     l = p.sum(-1, keepdim=True)
-    sv = _pow2_scale(v.abs().amax(dim=(2, 3), keepdim=True))
-    o = ((p * 256).to(E4M3).float() @ (_q8(v, sv) * sv)) / (256 * sv) / l
+    grp = _key_groups(p.shape[-1])
+    v8 = _q8_groups(v.transpose(2, 3), grp).transpose(2, 3)     # per (channel, key block)
+    o = (_q8_groups(p, grp) @ v8) / l
     return o.transpose(1, 2).reshape(Bw, -1, heads * 32), s
 
 
@@ -137,7 +158,7 @@ def test_fp8_window_attention_forward(cfg):
     assert float(err_emu.mean()) <= 2e-3 * vmax
     assert float(err_emu.max()) <= 0.08 * vmax
     # fp8 budget vs the exact fp32 attention (e4m3: 3 mantissa bits on q, k, v and P);
-    # measured round 2 on MI355X: rel-RMS 0.043-0.048 over these cases
+    # measured round 2 on MI355X (per-window scales): rel-RMS 0.043-0.048 over these cases
     assert rr <= 0.08, rr
 
 
@@ -177,7 +198,7 @@ def test_fp8_window_attention_backward(cfg):
 
 
 def test_fp8_scales_cover_large_and_small_magnitudes():
-    """Per-(window, head) scales: activations at 1e-3 and at 1e2 scale (where a fixed e4m3
+    """Per-block scales: activations at 1e-3 and at 1e2 scale (where a fixed e4m3
     scale would underflow / overflow) keep the same relative error."""
     from visionseg import ops
     cfg = CASES[0]

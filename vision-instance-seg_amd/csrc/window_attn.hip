@@ -491,80 +491,67 @@ __global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* 
 constexpr int kMaxT2Big = 529;    // (2*12-1)^2
 
 // ---- fp8 (OCP e4m3, gfx950) window attention, config C5 ------------------------------
-// F8 = true selects v_mfma_f32_32x32x16_fp8_fp8 for S^T = K Q^T (forward and the
-// backward's recompute) and for O^T = V^T P^T (forward).  Operands stay bf16 in HBM and
-// LDS; each wave quantises its MFMA fragments on the fly with per-(window, head)
-// power-of-two scales s = 2^floor(log2(448 / amax)) of q, k and v (amax over the window's
-// N x 32 values; exact descale), and P (in [0, 1] before normalisation) with s = 256.
-// The backward recomputes S with the same fp8 operands and scales (identical logits, so
-// exp(S - lse) is the forward's P) and forms every gradient product in bf16 from the
-// bf16 operands (straight-through quantisation).  Non-scaled fp8 MFMA issues at the bf16
-// rate on gfx950 (MI355X_MICROARCH §Matrix cores): this is a numerics mode of the same
-// latency/LDS-bound kernel, not a throughput change.
-typedef long fp8x8_t;
+// F8 = true runs the logits S^T = K Q^T (forward and the backward's recomputes) and
+// O^T = V^T P^T (forward) on the BLOCK-SCALED MX MFMA v_mfma_scale_f32_32x32x64_f8f6f4
+// with e4m3 operands: 2x the bf16 MFMA rate per clock on gfx950 (MI355X_MICROARCH.md
+// §Matrix cores), the dequantisation fused into the instruction.  Operand lane layout
+// (tools/micro/mfma_scale_probe.hip checks it on the box): lane l holds A[row l&31]
+// [k = 32 (l>>5) + j] in byte j of 8 dwords and B[k = 32 (l>>5) + j][col l&31]; its e8m0
+// scale byte (2^(e-127)) scales those 32 elements: one scale per 32-element block.
+//   * logits: the head dimension (32) is one block: every q and k TOKEN gets its own
+//     power-of-two scale (amax over its 32 values, in-lane -- no block reduction);
+//     lanes 32..63 carry the zero upper half of the 64-deep K;
+//   * P V: 64 keys per instruction (key tiles 2b and 2b+1); lane half hh takes the keys
+//     of its own accumulator rows (crow(., hh)) of both tiles -- the products' k order is
+//     free as long as A and B agree --, so P comes straight from the registers, and each
+//     (query, block) of P and (channel, block) of V has its own scale.
+// Operands stay bf16 in HBM and LDS; the backward recomputes S on the same fp8 operands
+// and scales (identical logits, so exp(S - lse) is the forward's P) and forms every
+// gradient product in bf16 from the bf16 operands (straight-through quantisation).
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ fp8x8_t fp8_pack8(const float* f) {
-  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
-  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
-  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
-  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
-  return (fp8x8_t)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
+__device__ __forceinline__ f32x16_t mfma_mx(i32x8_t a, int sa, i32x8_t b, int sb, f32x16_t c) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
 }
 
-// bf16 fragment x s -> e4m3 fragment (element j in byte j)
-__device__ __forceinline__ fp8x8_t fp8_frag(bf16x8_t v, float s) {
-  float f[8];
+// 32 values -> e4m3 (byte j = element j) and their e8m0 block scale: x ~ q 2^(e-127),
+// q = x 2^k with k = floor(log2(448 / amax)) (exact: a power of two), e = 127 - k.
+// `at(j)` yields element j (called twice per element: amax pass, then conversion), so
+// the values need not sit in 32 extra registers.
+template <typename F>
+__device__ __forceinline__ int mx_pack32(F at, i32x8_t& q) {
+  float am = 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = bf16_bits_to_f32((unsigned short)v[j]) * s;
-  return fp8_pack8(f);
-}
-
-// 8 consecutive accumulator registers x s -> e4m3 fragment (permuted k, as pack8)
-__device__ __forceinline__ fp8x8_t fp8_acc8(const f32x16_t& a, int base, float s) {
-  float f[8];
+  for (int j = 0; j < 32; ++j) am = fmaxf(am, fabsf(at(j)));
+  int k = am > 0.f ? (int)floorf(log2f(448.f / am)) : 0;
+  k = min(max(k, -126), 126);
+  const float s = __builtin_ldexpf(1.f, k);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = a[base + j] * s;
-  return fp8_pack8(f);
-}
-
-__device__ __forceinline__ f32x16_t mfma_fp8(fp8x8_t a, fp8x8_t b, f32x16_t c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ float amax8(bf16x8_t v, float m) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf16_bits_to_f32((unsigned short)v[j])));
-  return m;
-}
-
-// e4m3 scale of a block: largest power of two with amax * s <= 448 (1 for an all-zero block)
-__device__ __forceinline__ float fp8_scale(float amax) {
-  return amax > 0.f ? exp2f(floorf(log2f(448.f / amax))) : 1.f;
-}
-
-constexpr float kP8Scale = 256.f;
-
-// block-wide max of NV per-thread values through `red` [waves][NV] (one __syncthreads
-// supplied by the caller between the write and the read)
-template <int NV>
-__device__ __forceinline__ void wave_amax_store(float* v, float* red) {
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    float m = v[i];
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) m = fmaxf(m, __shfl_xor(m, s, 64));
-    if ((threadIdx.x & 63) == 0) red[(threadIdx.x >> 6) * NV + i] = m;
+  for (int w = 0; w < 8; ++w) {
+    const int v = __builtin_amdgcn_cvt_pk_fp8_f32(at(4 * w) * s, at(4 * w + 1) * s, 0, false);
+    q[w] = __builtin_amdgcn_cvt_pk_fp8_f32(at(4 * w + 2) * s, at(4 * w + 3) * s, v, true);
   }
+  return 127 - k;
 }
 
-template <int NV>
-__device__ __forceinline__ void block_amax_load(float* v, const float* red, int waves) {
+// a token's 32 head channels (4 x 16-B bf16 chunks) -> the MX operand of lanes 0..31;
+// lanes 32..63 (the zero upper half of K) pass valid = false
+__device__ __forceinline__ int mx_row(const bf16x8_t* c, i32x8_t& q) {
+  return mx_pack32([&](int j) { return bf16_bits_to_f32((unsigned short)c[j >> 3][j & 7]); }, q);
+}
+
+__device__ __forceinline__ int mx_row_lds(const short* row, bool valid, i32x8_t& q) {
+  bf16x8_t c[4];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    float m = 0.f;
-    for (int w = 0; w < waves; ++w) m = fmaxf(m, red[w * NV + i]);
-    v[i] = m;
-  }
+  for (int i = 0; i < 4; ++i) c[i] = valid ? *reinterpret_cast<const bf16x8_t*>(row + 8 * i) : zero8();
+  return mx_row(c, q);
+}
+
+__device__ __forceinline__ int mx_row_gmem(const bf16* row, bool valid, i32x8_t& q) {
+  bf16x8_t c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = valid ? ld8(row + 8 * i) : zero8();
+  return mx_row(c, q);
 }
 
 template <int NT>
@@ -582,67 +569,62 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   __shared__ __attribute__((aligned(16))) short sVt[32 * PT];  // V^T [d][key]
   __shared__ float sBias[kMaxT2Big];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
-  __shared__ float sRed[F8 ? NT * 3 : 1];
   const int bw = blockIdx.x, h = blockIdx.y;
   const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
   const bf16* win = qkv + (size_t)bw * N * C3;
   // all global operands requested up front: two 16-B K / V chunks per thread (NP x 4
   // chunks, 64 NT threads) and this lane's query row slices
-  bf16x8_t ck[2], cv[2], cq[2], qb[2];
+  bf16x8_t ck[2], cv[2], qb[2];
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
     const bf16* row = win + (size_t)t * C3 + h * kD + 8 * c;
     ck[it] = t < N ? ld8(row + C) : zero8();
     cv[it] = t < N ? ld8(row + 2 * C) : zero8();
-    if (F8) cq[it] = t < N ? ld8(row) : zero8();
   }
+  const int qrow = 32 * qt + r;
+  i32x8_t qm;                                 // F8: the query token as an MX operand (lanes 0..31)
+  int qs = 127;
+  if (F8) {
+    qs = mx_row_gmem(win + (size_t)qrow * C3 + h * kD, hh == 0 && qrow < N, qm);
+  } else {
 #pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    const int row = 32 * qt + r;
-    qb[st] = row < N ? ld8(win + (size_t)row * C3 + h * kD + 16 * st + 8 * hh) : zero8();
+    for (int st = 0; st < 2; ++st)
+      qb[st] = qrow < N ? ld8(win + (size_t)qrow * C3 + h * kD + 16 * st + 8 * hh) : zero8();
   }
   window_tokens_blk<NT>(g, bw, sTok);
   for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
-  float am[3] = {0.f, 0.f, 0.f};              // |q|, |k|, |v| maxima (F8)
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
     *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = ck[it];
 #pragma unroll
     for (int j = 0; j < 8; ++j) sVt[(8 * c + j) * PT + t] = cv[it][j];
-    if (F8) {
-      am[0] = amax8(cq[it], am[0]);
-      am[1] = amax8(ck[it], am[1]);
-      am[2] = amax8(cv[it], am[2]);
-    }
   }
-  if (F8) wave_amax_store<3>(am, sRed);
   __syncthreads();
-  float sq = 1.f, sk = 1.f, sv = 1.f;
-  WinGeom gl = g;
-  if (F8) {
-    block_amax_load<3>(am, sRed, NT);
-    sq = fp8_scale(am[0]);
-    sk = fp8_scale(am[1]);
-    sv = fp8_scale(am[2]);
-    gl.scale = g.scale / (sq * sk);           // exact: powers of two
-  }
+  const WinGeom& gl = g;
   // S^T = K Q^T for every key tile of this wave's queries
   f32x16_t acc[NT];
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) zero16(acc[kt]);
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
+  if (F8) {
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
-      const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(sK + (32 * kt + r) * PK + 16 * st + 8 * hh);
-      if (F8)
-        acc[kt] = mfma_fp8(fp8_frag(ka, sk), fp8_frag(qb[st], sq), acc[kt]);
-      else
-        acc[kt] = mfma16(ka, qb[st], acc[kt]);
+      i32x8_t km;
+      const int ks = mx_row_lds(sK + (32 * kt + r) * PK, hh == 0, km);
+      acc[kt] = mfma_mx(km, ks, qm, qs, acc[kt]);
+      __builtin_amdgcn_sched_barrier(0);      // one key tile's operand quantised at a time
     }
+  } else {
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+        const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(sK + (32 * kt + r) * PK + 16 * st + 8 * hh);
+        acc[kt] = mfma16(ka, qb[st], acc[kt]);
+      }
+  }
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
@@ -661,20 +643,42 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
     }
   sum += __shfl_xor(sum, 32, 64);
   const float lq = m + __logf(sum);
-  const float inv = F8 ? 1.f / (sum * kP8Scale * sv) : 1.f / sum;
+  const float inv = 1.f / sum;
   // O^T = V^T P^T
   f32x16_t o;
   zero16(o);
+  if (F8) {
 #pragma unroll
-  for (int t = 0; t < 2 * NT; ++t) {
-    const int kt = t >> 1, th = t & 1;
-    const bf16x8_t a = ld_perm(sVt + r * PT, 32 * kt + 16 * th + 4 * hh);
-    if (F8)
-      o = mfma_fp8(fp8_frag(a, sv), fp8_acc8(acc[kt], 8 * th, kP8Scale), o);
-    else
+    for (int b2 = 0; b2 < (NT + 1) / 2; ++b2) {
+      // block of key tiles 2 b2, 2 b2 + 1: this lane's k = its accumulator rows of both
+      constexpr int kLast = NT - 1;
+      const int k0 = 2 * b2, k1 = 2 * b2 + 1 < NT ? 2 * b2 + 1 : kLast;
+      const bool has1 = 2 * b2 + 1 < NT;
+      bf16x4_t v4[8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const bf16x4_t z = {0, 0, 0, 0};
+          v4[4 * u + g4] = (u == 0 || has1) ? *reinterpret_cast<const bf16x4_t*>(
+                                                   sVt + r * PT + 32 * (u ? k1 : k0) + 8 * g4 + 4 * hh)
+                                             : z;
+        }
+      i32x8_t vm, pm;
+      const int vs = mx_pack32([&](int j) { return bf16_bits_to_f32((unsigned short)v4[j >> 2][j & 3]); }, vm);
+      const int ps = mx_pack32([&](int j) { return j < 16 ? acc[k0][j] : (has1 ? acc[k1][j - 16] : 0.f); }, pm);
+      o = mfma_mx(vm, vs, pm, ps, o);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2 * NT; ++t) {
+      const int kt = t >> 1, th = t & 1;
+      const bf16x8_t a = ld_perm(sVt + r * PT, 32 * kt + 16 * th + 4 * hh);
       o = mfma16(a, pack8(acc[kt], 8 * th), o);
+    }
   }
-  const int q = 32 * qt + r;
+  const int q = qrow;
   if (q < N) {
     bf16* dst = out + ((size_t)bw * N + q) * C + h * kD;
 #pragma unroll
@@ -721,7 +725,6 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   __shared__ float sBias[kMaxT2Big];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
   __shared__ float sL[NP], sD[NP];
-  __shared__ float sRed[F8 ? NT * 2 : 1];
   const int bw = blockIdx.x, h = blockIdx.y;
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
@@ -754,7 +757,6 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     const bf16* row = win + (size_t)t * C3 + 8 * c;
     ck[it] = in ? ld8(row + C) : zero8();
     cv[it] = in ? ld8(row + 2 * C) : zero8();
-    if (F8) cq[it] = in ? ld8(row) : zero8();
   }
   bf16x8_t qb[2], db[2], ob[2], kb[2], vb[2];
   auto load_kv = [&]() {
@@ -781,7 +783,6 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   short* sVn = sU + kNat;
   short* sKT = sU + 2 * kNat;
   float* sBins = reinterpret_cast<float*>(sU + 2 * kNat + kTr);
-  float am[2] = {0.f, 0.f};
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
@@ -789,10 +790,6 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     *reinterpret_cast<bf16x8_t*>(sVn + t * PK + 8 * c) = cv[it];
 #pragma unroll
     for (int j = 0; j < 8; ++j) sKT[(8 * c + j) * PT + t] = ck[it][j];
-    if (F8) {
-      am[0] = amax8(cq[it], am[0]);
-      am[1] = amax8(ck[it], am[1]);
-    }
   }
   float Dq = 0.f;
 #pragma unroll
@@ -806,21 +803,11 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     sL[q] = Lq;
   }
   for (int t = threadIdx.x; t < NT * kBinW; t += blockDim.x) sBins[t] = 0.f;
-  if (F8) wave_amax_store<2>(am, sRed);
   __syncthreads();
-  float sq = 1.f, sk = 1.f;
-  WinGeom gl = g;
-  if (F8) {                                   // the forward's scales: identical logits
-    block_amax_load<2>(am, sRed, NT);
-    sq = fp8_scale(am[0]);
-    sk = fp8_scale(am[1]);
-    gl.scale = g.scale / (sq * sk);
-  }
-  fp8x8_t qb8[2];
-  if (F8) {
-    qb8[0] = fp8_frag(qb[0], sq);
-    qb8[1] = fp8_frag(qb[1], sq);
-  }
+  const WinGeom& gl = g;
+  i32x8_t qm;                                 // F8: this lane's query token, the forward's MX operand
+  int qs = 127;
+  if (F8) qs = mx_row_gmem(win + (size_t)q * C3, hh == 0 && q < N, qm);
   float* bins = sBins + qt * kBinW;
   f32x16_t dq;
   zero16(dq);
@@ -828,14 +815,15 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     f32x16_t s, dp;
     zero16(s);
     zero16(dp);
+    if (F8) {                                 // the forward's logits: same operands, order, scales
+      i32x8_t km;
+      const int ks = mx_row_lds(sKn + (32 * kt + r) * PK, hh == 0, km);
+      s = mfma_mx(km, ks, qm, qs, s);
+    }
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       const int o = (32 * kt + r) * PK + 16 * st + 8 * hh;
-      const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(sKn + o);
-      if (F8)
-        s = mfma_fp8(fp8_frag(ka, sk), qb8[st], s);
-      else
-        s = mfma16(ka, qb[st], s);
+      if (!F8) s = mfma16(*reinterpret_cast<const bf16x8_t*>(sKn + o), qb[st], s);
       dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sVn + o), db[st], dp);
     }
     int rel[16];
@@ -903,11 +891,9 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
       sDT[(8 * c + j) * PT + t] = cd[it][j];
     }
   }
-  fp8x8_t kb8[2];
-  if (F8) {
-    kb8[0] = fp8_frag(kb[0], sk);
-    kb8[1] = fp8_frag(kb[1], sk);
-  }
+  i32x8_t km;                                 // F8: this lane's key token as an MX operand
+  int ks = 127;
+  if (F8) ks = mx_row_gmem(win + (size_t)key * C3 + C, hh == 0 && key < N, km);
   __syncthreads();
   f32x16_t dv, dk;
   zero16(dv);
@@ -916,14 +902,15 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     f32x16_t s, dp;
     zero16(s);
     zero16(dp);
+    if (F8) {                                 // S = Q K^T on the same MX operands (A / B swapped)
+      i32x8_t qa8;
+      const int qa_s = mx_row_lds(sQn + (32 * qq + r) * PK, hh == 0, qa8);
+      s = mfma_mx(qa8, qa_s, km, ks, s);
+    }
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       const int o = (32 * qq + r) * PK + 16 * st + 8 * hh;
-      const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(sQn + o);
-      if (F8)
-        s = mfma_fp8(fp8_frag(qa, sq), kb8[st], s);
-      else
-        s = mfma16(qa, kb[st], s);
+      if (!F8) s = mfma16(*reinterpret_cast<const bf16x8_t*>(sQn + o), kb[st], s);
       dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sDn + o), vb[st], dp);
     }
     logits_qk(s, gl, sTok, sBias, qq, key, hh);
