@@ -77,7 +77,9 @@ def test_flat_step_vs_oracle_solver(dtype, optimizer, clip):
         err = float((m.cpu() - r).abs().max())
         worst = max(worst, err / (float(r.abs().max()) + s.lr))
     print(f"{optimizer}/{clip}/{dtype}: worst master-weight error {worst:.2e} (relative to max|p| + lr)")
-    assert worst <= 2e-6
+    # f32 arithmetic in another order (the global norm of "full_model" is one block's sum
+    # over the chunk partials): a few f32 ulps of the weight scale
+    assert worst <= 4e-6
     if dtype == torch.bfloat16:                 # working weights = bf16 rounding of the master
         assert torch.equal(opt.weights, opt.master.to(torch.bfloat16))
         for p, w in zip(opt.params, opt.layout.views(opt.weights)):

@@ -152,9 +152,10 @@ def test_bf16_training_step_vs_oracle():
     noise on every path).  Bounds (stated here, measured values in the print):
       * loss: |ours - fp32| <= 1.25 x |oracle-bf16 - fp32| + 2e-3 x loss;
       * gradients: the median and the 90th percentile over parameters of ours <=
-        1.25 x the yardstick's; every parameter <= max(2 x its yardstick error, 0.1)
-        (round 3, first box run: median 2.97e-2 vs 3.33e-2, p90 6.75e-2 vs 5.75e-2,
-        loss 86.801 / oracle-bf16 86.701 / fp32 86.771);
+        1.25 x the yardstick's; every parameter's absolute L2 error <= max(2 x the
+        yardstick's, 0.05 x the median parameter-gradient norm) (round 3 on the box:
+        median 2.76e-2 vs 3.29e-2, p90 5.80e-2 vs 5.47e-2; loss 86.694 / oracle-bf16
+        86.701 / fp32 86.771);
       * weight updates of the step (per-parameter clip to norm 0.01, SGD): the same two
         percentile bounds against the yardstick's update."""
     from _draws import ForcedDecisions
@@ -237,6 +238,12 @@ def test_bf16_training_step_vs_oracle():
           f"(yard {q(yu, 90):.2e}); worst ratios {[(n, f'{r:.2f}', f'{eg[n]:.1e}') for r, n in ratio]}")
     assert abs(lp - l32) <= 1.25 * abs(l16 - l32) + 2e-3 * abs(l32)
     assert q(eg, 50) <= 1.25 * q(yg, 50) and q(eg, 90) <= 1.25 * q(yg, 90)
-    bad = [(n, eg[n], yg[n], float(g32[n].norm()) / gfloor) for n in names if eg[n] > max(2.0 * yg[n], 0.1)]
+    # per parameter, in absolute L2 terms: within 2x the yardstick's error, or within 5 % of
+    # the median parameter-gradient norm (tiny gradients -- the decoder self-attention's
+    # q / k weights at init -- are rounding noise on every bf16 path)
+    med = gfloor / 1e-2
+    dist = {n: float((gp[n].double() - g32[n].double()).norm()) for n in names}
+    ydist = {n: float((g16[n].double() - g32[n].double()).norm()) for n in names}
+    bad = [(n, dist[n] / med, ydist[n] / med) for n in names if dist[n] > max(2.0 * ydist[n], 0.05 * med)]
     assert not bad, bad[:5]
     assert q(eu, 50) <= 1.25 * q(yu, 50) and q(eu, 90) <= 1.25 * q(yu, 90)

@@ -63,7 +63,11 @@ __device__ __forceinline__ void wave_sync() {
 // release fence drains vmcnt, so a kernel that issues fire-and-forget atomics before a
 // barrier whose only job is LDS reuse would stall on their round trip to L2.  Use only
 // where no other wave reads global memory this wave wrote before the barrier.
-__device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");   // LDS-only release: lgkmcnt, no vmcnt
+  __builtin_amdgcn_s_barrier();                                      // (a builtin: convergent, never duplicated)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 // C-tile row of register i for lane half hh
 __device__ __forceinline__ constexpr int crow(int i, int hh) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }

@@ -83,14 +83,53 @@ def instance_inference(mask_logits, class_logits, out_hw, valid_hw=None, pad_hw=
 
 
 class Predictor:
-    """Swin + Mask2Former (or MaskDINO) predictor on the MI355X kernels (eval mode, bf16
-    autocast)."""
+    """Swin + Mask2Former (or MaskDINO) predictor on the MI355X kernels, eval mode.
+
+    On a HIP device with `amp` the model runs the training step's production path: bf16
+    parameters and activations (the fused kernels need matching dtypes; autocast would
+    leave them), and each padded input shape is captured once as a HIP graph and
+    replayed (`graphs`; the eager forward is ~1 000 host launches).  A small LRU keeps
+    the graphs of the last `max_graphs` shapes (the preprocessing pads to multiples of
+    32, so a labelling session sees a handful of shapes).  Without a device, or with
+    graphs off, the forward runs eagerly (f32 autocast-free on CPU)."""
 
     def __init__(self, model: Mask2Former, device="cuda:0", min_size: int = 640, max_size: int = 800,
-                 amp: bool = True, top_k: int = 100):
+                 amp: bool = True, top_k: int = 100, graphs: bool = True, max_graphs: int = 4):
         self.device = torch.device(device)
+        self.bf16 = bool(amp) and self.device.type == "cuda"
+        if self.bf16 and next(model.parameters()).dtype != torch.bfloat16:
+            # a bf16 copy: the caller's model (e.g. an f32 Trainer's, whose parameters are
+            # views of its flat buffers) is left as it is
+            import copy
+            model = copy.deepcopy(model).to(torch.bfloat16)
         self.model = model.to(self.device).eval()
         self.min_size, self.max_size, self.amp, self.top_k = min_size, max_size, amp, top_k
+        from .train import graph_capture_safe
+        self.graphs = bool(graphs) and self.bf16 and graph_capture_safe()
+        self.max_graphs = int(max_graphs)
+        self._graphs = {}                     # padded input shape -> (graph, static input, static outputs)
+
+    def _forward(self, x):
+        if not self.graphs:
+            return self.model(x)
+        key = tuple(x.shape)
+        hit = self._graphs.pop(key, None)
+        if hit is None:
+            self.model(x)                     # lazy library state before the capture
+            torch.cuda.synchronize(self.device)
+            while len(self._graphs) >= self.max_graphs:      # oldest shape out
+                old = self._graphs.pop(next(iter(self._graphs)))
+                old[0].reset()
+            g = torch.cuda.CUDAGraph()
+            static = x.clone()
+            with torch.cuda.graph(g):
+                out = self.model(static)
+            hit = (g, static, out)
+        self._graphs[key] = hit               # most recently used last
+        g, static, out = hit
+        static.copy_(x)
+        g.replay()
+        return out
 
     def _preprocess(self, image_bgr: np.ndarray):
         h, w = image_bgr.shape[:2]
@@ -110,8 +149,7 @@ class Predictor:
     @torch.no_grad()
     def __call__(self, image_bgr: np.ndarray) -> DetResult:
         x, valid, orig = self._preprocess(image_bgr)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.amp and self.device.type == "cuda"):
-            out = self.model(x)
+        out = self._forward(x.to(torch.bfloat16) if self.bf16 else x)
         if isinstance(out, dict):            # MaskDINO: per-step lists in a dict, sigmoid class scores
             m, c, sig = out["masks"][-1][0], out["classes"][-1][0], True
         else:
