@@ -1,8 +1,8 @@
 """fp8 (OCP e4m3) window attention, BASELINE config C5 (Swin-L, 1536^2, "fp8 MFMA
 window-attention path"), through vs_window_attn_forward_fp8 / _backward_fp8: the
 block-scaled MX MFMA v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 operands, one e8m0 scale per
-32-element block: every q / k token, and per (query, 32-key block) of P and (channel,
-32-key block) of V).
+32-element block: every q / k token, and per (query, 32-key tile) of P and (channel,
+32-key tile) of V).
 
 Two yardsticks per case:
   * the kernel's own quantisation model, emulated in torch on the CPU (f32 math on
@@ -38,11 +38,10 @@ def _q8(x, s):
 
 
 def _key_groups(N):
-    """Scale block of every key in the kernel's P V product: 64 keys (key tiles 2b, 2b+1)
-    per instruction, lane half hh = bit 2 of the key's row in its 32-key tile
-    (accumulator rows crow(i, hh) = (i & 3) + 8 (i >> 2) + 4 hh)."""
-    t = torch.arange(N)
-    return 2 * (t // 64) + ((t % 32) >> 2 & 1)
+    """Scale block of every key in the kernel's P V product: K-block b of an instruction is
+    one 32-key tile (tools/micro/mfma_scale_probe.hip: the two lane halves of a row share
+    each 32-deep block and its scale)."""
+    return torch.arange(N) // 32
 
 
 def _q8_groups(x, grp):

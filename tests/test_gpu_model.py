@@ -226,3 +226,24 @@ def test_train_template_seam_and_inference_seam(tmp_path, arch):
     best = int(pi.scores.cpu().numpy().argmax())                  # the caller's selection (ai_segmentation.py:83-88)
     mask = pi.masks[best].cpu().numpy()
     assert mask.shape == img.shape[:2] and int(pi.labels[best]) == 0
+
+
+def test_predictor_graph_replay_matches_eager():
+    """The inference Predictor (labeling_server seam): the pure-bf16 forward replayed as a
+    HIP graph per padded input shape gives the same instances as the eager forward, for
+    several image shapes (more shapes than the LRU keeps: graphs are evicted and recaptured)."""
+    from visionseg.inference import Predictor
+    from visionseg.model import M2FConfig, Mask2Former
+    cfg = M2FConfig.preset("swin_t")
+    m = Mask2Former(cfg).init_weights(0)
+    pg = Predictor(m, device=DEV, min_size=256, max_size=320, graphs=True, max_graphs=2)
+    pe = Predictor(m, device=DEV, min_size=256, max_size=320, graphs=False)
+    assert pg.graphs and next(pg.model.parameters()).dtype == torch.bfloat16
+    assert next(m.parameters()).dtype == torch.float32           # the caller's model is left as it is
+    rng = np.random.default_rng(0)
+    for shape in ((200, 260), (256, 256), (300, 180), (200, 260)):
+        img = rng.integers(0, 256, (*shape, 3)).astype(np.uint8)
+        a, b = pg(img).pred_instances, pe(img).pred_instances
+        assert torch.equal(a.masks, b.masks) and torch.equal(a.labels, b.labels)
+        assert torch.equal(a.scores, b.scores)
+    assert len(pg._graphs) == 2

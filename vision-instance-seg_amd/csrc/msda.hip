@@ -923,14 +923,14 @@ constexpr int kBandCap = 128;
 constexpr int kWP8 = 68;       // W row pitch (floats): 64 queries + 4
 constexpr int kDP = 132;       // Dm row pitch (floats): 128 band cells + 4
 
-template <int TX, int TY, bool GEOM, bool LB>
+template <int TX, int TY, bool GEOM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) msda_bwd_mfma_wg_kernel(const float* __restrict__ loc,
                                                                const float* __restrict__ attw,
                                                                const bf16* __restrict__ gout,
                                                                float* __restrict__ gvalue, Levels lv, QueryTiles qt,
                                                                int S, int Hh, int Q, int L, int nblk,
                                                                const bf16* __restrict__ value, float* __restrict__ gloc,
-                                                               float* __restrict__ gattw) {
+                                                               float* __restrict__ gattw, int lbmask) {
   constexpr int P = 4;
   constexpr int NQ = TX * TY;
   static_assert(NQ == 64, "64 queries x 4 points = one tap per thread");
@@ -943,12 +943,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
   const int tile = (blk / Hh) % qt.per_image;
   const int b = blk / Hh / qt.per_image;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  // LB: every barrier of the band walk orders LDS only (lds_barrier), so the band's
-  // fire-and-forget grad_value atomics stay in flight across the next band's barriers
-  auto bar = [&]() {
-    if (LB) lds_barrier();
+  // lbmask bit i: barrier i of the band walk orders LDS only (lds_barrier), so the band's
+  // fire-and-forget grad_value atomics stay in flight across it (else __syncthreads)
+  auto bar = [&](int bit) {
+    if (lbmask & bit) lds_barrier();
     else __syncthreads();
   };
+  const bool LB = (lbmask & 2) != 0;
   __shared__ int sAny[2][4];
   int band_par = 0;
   const int LP = L * P;
@@ -1014,7 +1015,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
         sBox[wave][3] = d;
       }
     }
-    bar();
+    bar(1);
     int oy = sBox[0][0], yh = sBox[0][1], ox = sBox[0][2], xh = sBox[0][3];
 #pragma unroll
     for (int w = 1; w < 4; ++w) {
@@ -1023,7 +1024,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
       ox = min(ox, sBox[w][2]);
       xh = max(xh, sBox[w][3]);
     }
-    bar();                                    // sBox is rewritten by the next level
+    bar(1);                                   // sBox is rewritten by the next level
     float dk[4] = {0.f, 0.f, 0.f, 0.f};       // GEOM: grad_out . value at the tap's corners
     const int BY = yh < 0 ? 0 : yh - oy + 1, BX = yh < 0 ? 1 : xh - ox + 1;   // yh < 0: no corner here
     const int SBX = min(BX, kBandCap), SBY = kBandCap / SBX;
@@ -1053,7 +1054,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int i = tid; i < nmt * 32 * (kWP8 / 4); i += 256) reinterpret_cast<float4*>(sW)[i] = z4;
         for (int i = tid; i < nmt * 32; i += 256) sHit[i] = 0;
-        bar();
+        bar(4);
 #pragma unroll
         for (int pt = 0; pt < P; ++pt) {      // a query's 4 points are lanes of one wave: take turns
           if (tpt == pt) {
@@ -1066,7 +1067,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
           }
           wave_sync();
         }
-        bar();
+        bar(8);
         for (int m = wave; m < nmt; m += 4) {
           f32x16_t acc;
           zero16(acc);
@@ -1095,7 +1096,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
             }
           }
         }
-        bar();                                // W / hit flags are rewritten by the next band
+        bar(16);                              // W / hit flags are rewritten by the next band
         if (GEOM) {
           // Dm[q][cell] over the band: wave w takes cell tile w (value rows loaded once)
           float* sD = sW;
@@ -1121,11 +1122,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
               for (int i = 0; i < 16; ++i) sD[(32 * mq + crow(i, hh)) * kDP + 32 * wave + r] = acc[i];
             }
           }
-          bar();
+          bar(32);
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (cell[k] >= 0) dk[k] += sD[tq * kDP + cell[k]];
-          bar();                              // Dm is overwritten by the next band's W
+          bar(64);                            // Dm is overwritten by the next band's W
         }
       }
     }
@@ -1255,20 +1256,18 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     bt.per_image = bt.mode == 1 ? bt.prefix[L] : (Q + te * te - 1) / (te * te);
     const long long nb2 = (long long)B * bt.per_image * Hh;
     VS_CHECK(nb2 < (1LL << 31), "too many query tiles");
-    bool ldsbar = true;                      // VS_MSDA_LDSBAR=0: __syncthreads in the band walk
-    if (const char* e = getenv("VS_MSDA_LDSBAR")) ldsbar = atoi(e) != 0;
-    if (mfma && fused && ldsbar)
-      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true, true>), dim3((unsigned)nb2), dim3(256), 0, st, loc,
-                         attw, (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc,
-                         gattw);
-    else if (mfma && fused)
-      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true, false>), dim3((unsigned)nb2), dim3(256), 0, st, loc,
-                         attw, (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc,
-                         gattw);
+    // VS_MSDA_LDSBAR: mask of the band walk's barriers that order LDS only (bits of
+    // msda_bwd_mfma_wg_kernel's bar(); 0 = __syncthreads everywhere)
+    int lbmask = 0;
+    if (const char* e = getenv("VS_MSDA_LDSBAR")) lbmask = atoi(e);
+    if (mfma && fused)
+      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
+                         (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc, gattw,
+                         lbmask);
     else if (mfma)
-      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, false, false>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
+      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, false>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
                          (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)nullptr, nullptr,
-                         nullptr);
+                         nullptr, 0);
     else if (dtype == VS_BF16)
       hipLaunchKernelGGL((msda_bwd_binned_kernel<bf16, 4, 4>), dim3((unsigned)nb2), dim3(64), 0, st, loc, attw,
                          (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2);

@@ -494,17 +494,19 @@ constexpr int kMaxT2Big = 529;    // (2*12-1)^2
 // F8 = true runs the logits S^T = K Q^T (forward and the backward's recomputes) and
 // O^T = V^T P^T (forward) on the BLOCK-SCALED MX MFMA v_mfma_scale_f32_32x32x64_f8f6f4
 // with e4m3 operands: 2x the bf16 MFMA rate per clock on gfx950 (MI355X_MICROARCH.md
-// §Matrix cores), the dequantisation fused into the instruction.  Operand lane layout
-// (tools/micro/mfma_scale_probe.hip checks it on the box): lane l holds A[row l&31]
-// [k = 32 (l>>5) + j] in byte j of 8 dwords and B[k = 32 (l>>5) + j][col l&31]; its e8m0
-// scale byte (2^(e-127)) scales those 32 elements: one scale per 32-element block.
-//   * logits: the head dimension (32) is one block: every q and k TOKEN gets its own
-//     power-of-two scale (amax over its 32 values, in-lane -- no block reduction);
-//     lanes 32..63 carry the zero upper half of the 64-deep K;
-//   * P V: 64 keys per instruction (key tiles 2b and 2b+1); lane half hh takes the keys
-//     of its own accumulator rows (crow(., hh)) of both tiles -- the products' k order is
-//     free as long as A and B agree --, so P comes straight from the registers, and each
-//     (query, block) of P and (channel, block) of V has its own scale.
+// §Matrix cores), the dequantisation fused into the instruction.  Operand layout, as
+// measured on the box (tools/micro/mfma_scale_probe.hip, profiles/r3_mfma_scale_probe.txt):
+// K = 64 is two 32-deep scale blocks; lane l (row / column l&31, half hh = l>>5) holds 16
+// elements of block 0 in its dwords 0-3 and 16 of block 1 in dwords 4-7 (the two lanes of
+// a row hold all 32 of each block; any k order works as long as A and B agree), and its
+// e8m0 scale byte (2^(e-127)) is the scale of block hh of its row / column.
+//   * logits: the head dimension (32) is block 0 (block 1 is zero): lane half hh carries
+//     channels 16hh..16hh+15, so every q and k TOKEN gets its own power-of-two scale (amax
+//     over its 32 channels: the lane's 16 and one cross-half shuffle);
+//   * P V: 64 keys per instruction, block 0 = key tile 2b, block 1 = tile 2b+1; lane half
+//     hh takes its own accumulator rows (crow(., hh)) of both tiles, so P comes straight
+//     from the registers; each (query, key tile) of P and (channel, key tile) of V has its
+//     own scale.
 // Operands stay bf16 in HBM and LDS; the backward recomputes S on the same fp8 operands
 // and scales (identical logits, so exp(S - lse) is the forward's P) and forms every
 // gradient product in bf16 from the bf16 operands (straight-through quantisation).
@@ -514,44 +516,66 @@ __device__ __forceinline__ f32x16_t mfma_mx(i32x8_t a, int sa, i32x8_t b, int sb
   return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
 }
 
-// 32 values -> e4m3 (byte j = element j) and their e8m0 block scale: x ~ q 2^(e-127),
-// q = x 2^k with k = floor(log2(448 / amax)) (exact: a power of two), e = 127 - k.
-// `at(j)` yields element j (called twice per element: amax pass, then conversion), so
-// the values need not sit in 32 extra registers.
+// block scale exponent: the largest k with amax 2^k <= 448 (e4m3 max); 0 for an empty block
+__device__ __forceinline__ int mx_exp(float amax) {
+  const int k = amax > 0.f ? (int)floorf(log2f(448.f / amax)) : 0;
+  return min(max(k, -126), 126);
+}
+
+// 16 + 16 values (this lane's share of K-block 0, then of block 1) -> e4m3 dwords 0-3 /
+// 4-7, scaled by 2^k0 / 2^k1 (exact: powers of two); `at(j)` yields element j
 template <typename F>
-__device__ __forceinline__ int mx_pack32(F at, i32x8_t& q) {
-  float am = 0.f;
-#pragma unroll
-  for (int j = 0; j < 32; ++j) am = fmaxf(am, fabsf(at(j)));
-  int k = am > 0.f ? (int)floorf(log2f(448.f / am)) : 0;
-  k = min(max(k, -126), 126);
-  const float s = __builtin_ldexpf(1.f, k);
+__device__ __forceinline__ void mx_pack(F at, int k0, int k1, i32x8_t& q) {
+  const float s0 = __builtin_ldexpf(1.f, k0), s1 = __builtin_ldexpf(1.f, k1);
 #pragma unroll
   for (int w = 0; w < 8; ++w) {
-    const int v = __builtin_amdgcn_cvt_pk_fp8_f32(at(4 * w) * s, at(4 * w + 1) * s, 0, false);
-    q[w] = __builtin_amdgcn_cvt_pk_fp8_f32(at(4 * w + 2) * s, at(4 * w + 3) * s, v, true);
+    const float sc = w < 4 ? s0 : s1;
+    const int v = __builtin_amdgcn_cvt_pk_fp8_f32(at(4 * w) * sc, at(4 * w + 1) * sc, 0, false);
+    q[w] = __builtin_amdgcn_cvt_pk_fp8_f32(at(4 * w + 2) * sc, at(4 * w + 3) * sc, v, true);
   }
-  return 127 - k;
 }
 
-// a token's 32 head channels (4 x 16-B bf16 chunks) -> the MX operand of lanes 0..31;
-// lanes 32..63 (the zero upper half of K) pass valid = false
-__device__ __forceinline__ int mx_row(const bf16x8_t* c, i32x8_t& q) {
-  return mx_pack32([&](int j) { return bf16_bits_to_f32((unsigned short)c[j >> 3][j & 7]); }, q);
-}
+__device__ __forceinline__ float xhalf_max(float v) { return fmaxf(v, __shfl_xor(v, 32, 64)); }
 
-__device__ __forceinline__ int mx_row_lds(const short* row, bool valid, i32x8_t& q) {
-  bf16x8_t c[4];
+// a token's channels 16hh..16hh+15 (two 16-B bf16 chunks) -> its logit operand: block 0 =
+// the token (scale from all 32 channels), block 1 zero.  Returns the lane's scale byte.
+__device__ __forceinline__ int mx_token(bf16x8_t c0, bf16x8_t c1, int hh, i32x8_t& q) {
+  auto at = [&](int j) {
+    return j < 16 ? bf16_bits_to_f32((unsigned short)(j < 8 ? c0[j] : c1[j - 8])) : 0.f;
+  };
+  float am = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) c[i] = valid ? *reinterpret_cast<const bf16x8_t*>(row + 8 * i) : zero8();
-  return mx_row(c, q);
+  for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(at(j)));
+  const int k = mx_exp(xhalf_max(am));
+  mx_pack(at, k, 0, q);
+  return hh == 0 ? 127 - k : 127;
 }
 
-__device__ __forceinline__ int mx_row_gmem(const bf16* row, bool valid, i32x8_t& q) {
-  bf16x8_t c[4];
+__device__ __forceinline__ int mx_token_lds(const short* row, int hh, bool valid, i32x8_t& q) {
+  const bf16x8_t c0 = valid ? *reinterpret_cast<const bf16x8_t*>(row + 16 * hh) : zero8();
+  const bf16x8_t c1 = valid ? *reinterpret_cast<const bf16x8_t*>(row + 16 * hh + 8) : zero8();
+  return mx_token(c0, c1, hh, q);
+}
+
+__device__ __forceinline__ int mx_token_gmem(const bf16* row, int hh, bool valid, i32x8_t& q) {
+  const bf16x8_t c0 = valid ? ld8(row + 16 * hh) : zero8();
+  const bf16x8_t c1 = valid ? ld8(row + 16 * hh + 8) : zero8();
+  return mx_token(c0, c1, hh, q);
+}
+
+// 16 + 16 values of two 32-element blocks (this lane's halves): per-block scales from the
+// cross-half amax; returns the lane's scale byte (block hh)
+template <typename F>
+__device__ __forceinline__ int mx_blocks(F at, int hh, i32x8_t& q) {
+  float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) c[i] = valid ? ld8(row + 8 * i) : zero8();
-  return mx_row(c, q);
+  for (int j = 0; j < 16; ++j) {
+    a0 = fmaxf(a0, fabsf(at(j)));
+    a1 = fmaxf(a1, fabsf(at(16 + j)));
+  }
+  const int k0 = mx_exp(xhalf_max(a0)), k1 = mx_exp(xhalf_max(a1));
+  mx_pack(at, k0, k1, q);
+  return 127 - (hh ? k1 : k0);
 }
 
 template <int NT>
@@ -584,10 +608,10 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
     cv[it] = t < N ? ld8(row + 2 * C) : zero8();
   }
   const int qrow = 32 * qt + r;
-  i32x8_t qm;                                 // F8: the query token as an MX operand (lanes 0..31)
+  i32x8_t qm;                                 // F8: the query token as an MX operand
   int qs = 127;
   if (F8) {
-    qs = mx_row_gmem(win + (size_t)qrow * C3 + h * kD, hh == 0 && qrow < N, qm);
+    qs = mx_token_gmem(win + (size_t)qrow * C3 + h * kD, hh, qrow < N, qm);
   } else {
 #pragma unroll
     for (int st = 0; st < 2; ++st)
@@ -612,7 +636,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
       i32x8_t km;
-      const int ks = mx_row_lds(sK + (32 * kt + r) * PK, hh == 0, km);
+      const int ks = mx_token_lds(sK + (32 * kt + r) * PK, hh, true, km);
       acc[kt] = mfma_mx(km, ks, qm, qs, acc[kt]);
       __builtin_amdgcn_sched_barrier(0);      // one key tile's operand quantised at a time
     }
@@ -665,8 +689,9 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
                                              : z;
         }
       i32x8_t vm, pm;
-      const int vs = mx_pack32([&](int j) { return bf16_bits_to_f32((unsigned short)v4[j >> 2][j & 3]); }, vm);
-      const int ps = mx_pack32([&](int j) { return j < 16 ? acc[k0][j] : (has1 ? acc[k1][j - 16] : 0.f); }, pm);
+      const int vs = mx_blocks([&](int j) { return bf16_bits_to_f32((unsigned short)v4[j >> 2][j & 3]); }, hh, vm);
+      const int ps = mx_blocks([&](int j) { return j < 16 ? acc[k0][j] : (has1 ? acc[k1][j - 16] : 0.f); }, hh,
+                               pm);
       o = mfma_mx(vm, vs, pm, ps, o);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -807,7 +832,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   const WinGeom& gl = g;
   i32x8_t qm;                                 // F8: this lane's query token, the forward's MX operand
   int qs = 127;
-  if (F8) qs = mx_row_gmem(win + (size_t)q * C3, hh == 0 && q < N, qm);
+  if (F8) qs = mx_token_gmem(win + (size_t)q * C3, hh, q < N, qm);
   float* bins = sBins + qt * kBinW;
   f32x16_t dq;
   zero16(dq);
@@ -817,7 +842,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     zero16(dp);
     if (F8) {                                 // the forward's logits: same operands, order, scales
       i32x8_t km;
-      const int ks = mx_row_lds(sKn + (32 * kt + r) * PK, hh == 0, km);
+      const int ks = mx_token_lds(sKn + (32 * kt + r) * PK, hh, true, km);
       s = mfma_mx(km, ks, qm, qs, s);
     }
 #pragma unroll
@@ -893,7 +918,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   }
   i32x8_t km;                                 // F8: this lane's key token as an MX operand
   int ks = 127;
-  if (F8) ks = mx_row_gmem(win + (size_t)key * C3 + C, hh == 0 && key < N, km);
+  if (F8) ks = mx_token_gmem(win + (size_t)key * C3 + C, hh, key < N, km);
   __syncthreads();
   f32x16_t dv, dk;
   zero16(dv);
@@ -904,7 +929,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     zero16(dp);
     if (F8) {                                 // S = Q K^T on the same MX operands (A / B swapped)
       i32x8_t qa8;
-      const int qa_s = mx_row_lds(sQn + (32 * qq + r) * PK, hh == 0, qa8);
+      const int qa_s = mx_token_lds(sQn + (32 * qq + r) * PK, hh, true, qa8);
       s = mfma_mx(qa8, qa_s, km, ks, s);
     }
 #pragma unroll
