@@ -19,6 +19,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace vs {
 namespace {
@@ -594,8 +595,16 @@ extern "C" int vs_add_layer_norm_forward(int dtype, const void* x, const void* r
   return VS_OK;
 }
 
+// workgroups of the LayerNorm backward sweep: VS_LN_BWD_PARTS (A/B; <= kMaxPartialsLN)
+constexpr int kMaxPartialsLN = 2048;
+static int ln_bwd_parts() {
+  int p = 512;
+  if (const char* e = getenv("VS_LN_BWD_PARTS")) p = atoi(e);
+  return std::min(std::max(p, 1), kMaxPartialsLN);
+}
+
 extern "C" long long vs_layer_norm_backward_workspace_bytes(int M, int C) {
-  return (long long)kMaxPartials * 3 * C * sizeof(float);     // dw, db (+ dx column sums)
+  return (long long)kMaxPartialsLN * 3 * C * sizeof(float);   // dw, db (+ dx column sums)
 }
 
 static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, const void* w, const float* mean,
@@ -631,7 +640,7 @@ static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, co
   VS_CHECK(pick_gk(C / 8, ln_kmax(dtype), &G, &K), "row too long for the LayerNorm kernel (C <= 2048)");
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
-  const int grid = blocks_for(M, kThreads / G, kMaxPartials);
+  const int grid = blocks_for(M, kThreads / G, ln_bwd_parts());
   const int NR = dsum ? 3 : 2;
   const size_t lds = (size_t)(kThreads / 64) * NR * C * sizeof(float);
   VS_CHECK(lds <= 64 * 1024, "LayerNorm backward LDS budget exceeded");
