@@ -1042,7 +1042,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
         }
         bool band_any;
         if (LB) {                             // double-buffered per-wave flags: a wave cannot
-          if (lane == 0) sAny[band_par][wave] = __ballot(any) != 0;   // lap a slower one by 2
+          const bool wany = __ballot(any) != 0;   // lap a slower one by 2; the ballot runs in
+          if (lane == 0) sAny[band_par][wave] = wany;   // all lanes (inside `if (lane == 0)` it saw one)
           lds_barrier();
           band_any = sAny[band_par][0] | sAny[band_par][1] | sAny[band_par][2] | sAny[band_par][3];
           band_par ^= 1;
@@ -1257,8 +1258,8 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     const long long nb2 = (long long)B * bt.per_image * Hh;
     VS_CHECK(nb2 < (1LL << 31), "too many query tiles");
     // VS_MSDA_LDSBAR: mask of the band walk's barriers that order LDS only (bits of
-    // msda_bwd_mfma_wg_kernel's bar(); 0 = __syncthreads everywhere)
-    int lbmask = 0;
+    // msda_bwd_mfma_wg_kernel's bar(); default all; 0 = __syncthreads everywhere)
+    int lbmask = 127;
     if (const char* e = getenv("VS_MSDA_LDSBAR")) lbmask = atoi(e);
     if (mfma && fused)
       hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
