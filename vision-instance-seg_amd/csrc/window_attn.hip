@@ -31,6 +31,7 @@ constexpr int kD = 32;
 struct WinGeom {
   int heads, ws, shift, nWh, nWw, N, T2;  // T2 = (2ws-1)^2
   float scale;
+  int f8dbg;                              // debug (VS_FP8_DBG): bit 0/1/2 = unit scales for P / V / q,k
 };
 
 __device__ __forceinline__ int region_of(int p, int Pp, int ws, int shift) {
@@ -539,41 +540,41 @@ __device__ __forceinline__ float xhalf_max(float v) { return fmaxf(v, __shfl_xor
 
 // a token's channels 16hh..16hh+15 (two 16-B bf16 chunks) -> its logit operand: block 0 =
 // the token (scale from all 32 channels), block 1 zero.  Returns the lane's scale byte.
-__device__ __forceinline__ int mx_token(bf16x8_t c0, bf16x8_t c1, int hh, i32x8_t& q) {
+__device__ __forceinline__ int mx_token(bf16x8_t c0, bf16x8_t c1, int hh, i32x8_t& q, bool unit = false) {
   auto at = [&](int j) {
     return j < 16 ? bf16_bits_to_f32((unsigned short)(j < 8 ? c0[j] : c1[j - 8])) : 0.f;
   };
   float am = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(at(j)));
-  const int k = mx_exp(xhalf_max(am));
+  const int k = unit ? 0 : mx_exp(xhalf_max(am));
   mx_pack(at, k, 0, q);
   return hh == 0 ? 127 - k : 127;
 }
 
-__device__ __forceinline__ int mx_token_lds(const short* row, int hh, bool valid, i32x8_t& q) {
+__device__ __forceinline__ int mx_token_lds(const short* row, int hh, bool valid, i32x8_t& q, bool unit = false) {
   const bf16x8_t c0 = valid ? *reinterpret_cast<const bf16x8_t*>(row + 16 * hh) : zero8();
   const bf16x8_t c1 = valid ? *reinterpret_cast<const bf16x8_t*>(row + 16 * hh + 8) : zero8();
-  return mx_token(c0, c1, hh, q);
+  return mx_token(c0, c1, hh, q, unit);
 }
 
-__device__ __forceinline__ int mx_token_gmem(const bf16* row, int hh, bool valid, i32x8_t& q) {
+__device__ __forceinline__ int mx_token_gmem(const bf16* row, int hh, bool valid, i32x8_t& q, bool unit = false) {
   const bf16x8_t c0 = valid ? ld8(row + 16 * hh) : zero8();
   const bf16x8_t c1 = valid ? ld8(row + 16 * hh + 8) : zero8();
-  return mx_token(c0, c1, hh, q);
+  return mx_token(c0, c1, hh, q, unit);
 }
 
 // 16 + 16 values of two 32-element blocks (this lane's halves): per-block scales from the
 // cross-half amax; returns the lane's scale byte (block hh)
 template <typename F>
-__device__ __forceinline__ int mx_blocks(F at, int hh, i32x8_t& q) {
+__device__ __forceinline__ int mx_blocks(F at, int hh, i32x8_t& q, bool unit = false) {
   float a0 = 0.f, a1 = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     a0 = fmaxf(a0, fabsf(at(j)));
     a1 = fmaxf(a1, fabsf(at(16 + j)));
   }
-  const int k0 = mx_exp(xhalf_max(a0)), k1 = mx_exp(xhalf_max(a1));
+  const int k0 = unit ? 0 : mx_exp(xhalf_max(a0)), k1 = unit ? 0 : mx_exp(xhalf_max(a1));
   mx_pack(at, k0, k1, q);
   return 127 - (hh ? k1 : k0);
 }
@@ -611,7 +612,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   i32x8_t qm;                                 // F8: the query token as an MX operand
   int qs = 127;
   if (F8) {
-    qs = mx_token_gmem(win + (size_t)qrow * C3 + h * kD, hh, qrow < N, qm);
+    qs = mx_token_gmem(win + (size_t)qrow * C3 + h * kD, hh, qrow < N, qm, g.f8dbg & 4);
   } else {
 #pragma unroll
     for (int st = 0; st < 2; ++st)
@@ -636,7 +637,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
       i32x8_t km;
-      const int ks = mx_token_lds(sK + (32 * kt + r) * PK, hh, true, km);
+      const int ks = mx_token_lds(sK + (32 * kt + r) * PK, hh, true, km, g.f8dbg & 4);
       acc[kt] = mfma_mx(km, ks, qm, qs, acc[kt]);
       __builtin_amdgcn_sched_barrier(0);      // one key tile's operand quantised at a time
     }
@@ -689,9 +690,10 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
                                              : z;
         }
       i32x8_t vm, pm;
-      const int vs = mx_blocks([&](int j) { return bf16_bits_to_f32((unsigned short)v4[j >> 2][j & 3]); }, hh, vm);
+      const int vs = mx_blocks([&](int j) { return bf16_bits_to_f32((unsigned short)v4[j >> 2][j & 3]); }, hh, vm,
+                               g.f8dbg & 2);
       const int ps = mx_blocks([&](int j) { return j < 16 ? acc[k0][j] : (has1 ? acc[k1][j - 16] : 0.f); }, hh,
-                               pm);
+                               pm, g.f8dbg & 1);
       o = mfma_mx(vm, vs, pm, ps, o);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -971,6 +973,8 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
 
 int check_geom(WinGeom& g, int Bw, int heads, int ws, int shift, int nWh, int nWw, float scale) {
   g.heads = heads; g.ws = ws; g.shift = shift; g.nWh = nWh; g.nWw = nWw; g.scale = scale;
+  g.f8dbg = 0;
+  if (const char* e = getenv("VS_FP8_DBG")) g.f8dbg = atoi(e);
   g.N = ws * ws;
   g.T2 = (2 * ws - 1) * (2 * ws - 1);
   return Bw > 0 && heads > 0 && ws > 0 && ws <= 16 && shift >= 0 && shift < ws && nWh > 0 && nWw > 0 &&
