@@ -1,5 +1,6 @@
-"""fp8 (MX) window attention forward on one small case: NaN census per (window, head,
-query tile) and the error vs the CPU emulation (tests/test_gpu_fp8.py)."""
+"""fp8 (MX) window attention forward on one small case: where the output is wrong
+(NaN / far from the emulation) by window, head, query and channel, and whether it is
+reproducible across launches."""
 import os
 import sys
 
@@ -10,25 +11,23 @@ import torch  # noqa: E402
 import test_gpu_fp8 as T  # noqa: E402
 from visionseg import ops  # noqa: E402
 
-for dbg in ("0", "1", "2", "4", "7"):
-  os.environ["VS_FP8_DBG"] = dbg
-  print("VS_FP8_DBG", dbg)
-  for cfg in (T.CASES[4], T.CASES[0]):
-      qkv, table, _ = T._inputs(cfg, 11)
-      geo = (cfg["heads"], cfg["ws"], cfg["shift"], cfg["nWh"], cfg["nWw"])
-      with torch.no_grad():
-          out = ops.window_attention(qkv.cuda(), table.cuda(), *geo, fp8=True).float().cpu()
-          outb = ops.window_attention(qkv.cuda(), table.cuda(), *geo, fp8=False).float().cpu()
-      emu, _ = T.emulate_fwd(qkv, table, *geo)
-      N = cfg["ws"] ** 2
-      o = out.view(out.shape[0], N, cfg["heads"], 32)
-      nanmask = torch.isnan(o)
-      print(f"ws {cfg['ws']}: NaN fraction {float(nanmask.float().mean()):.3f}; NaN per query tile",
-            [float(nanmask[:, 32 * t:32 * t + 32].float().mean()) for t in range((N + 31) // 32)],
-            "per channel half", [float(nanmask[..., 16 * i:16 * i + 16].float().mean()) for i in range(2)])
-      ok = ~torch.isnan(out)
-      if ok.any():
-          print("  finite entries vs emulation max", float((out[ok] - emu[ok]).abs().max()), "vs bf16 path max",
-                float((out[ok] - outb[ok]).abs().max()), "scale", float(outb.abs().max()))
-      print("  sample fp8", out[0, :3, :6].tolist())
-      print("  sample emu", emu[0, :3, :6].tolist())
+for cfg in (T.CASES[4], T.CASES[0]):
+    qkv, table, _ = T._inputs(cfg, 11)
+    geo = (cfg["heads"], cfg["ws"], cfg["shift"], cfg["nWh"], cfg["nWw"])
+    N, H = cfg["ws"] ** 2, cfg["heads"]
+    emu, _ = T.emulate_fwd(qkv, table, *geo)
+    emu = emu.view(-1, N, H, 32)
+    outs = []
+    for rep in range(3):
+        with torch.no_grad():
+            o = ops.window_attention(qkv.cuda(), table.cuda(), *geo, fp8=True).float().cpu().view(-1, N, H, 32)
+        outs.append(o)
+    bad = ~((outs[0] - emu).abs() <= 0.1)                  # NaN counts as bad
+    print(f"ws {cfg['ws']} N {N}: bad fraction {float(bad.float().mean()):.4f}; runs identical "
+          f"{[bool(torch.equal(torch.nan_to_num(outs[0], 7.0), torch.nan_to_num(o, 7.0))) for o in outs[1:]]}")
+    print("  bad by query:", [int(x) for x in bad.sum(dim=(0, 2, 3)).tolist()])
+    print("  bad by channel:", [int(x) for x in bad.sum(dim=(0, 1, 2)).tolist()])
+    print("  bad by head:", [int(x) for x in bad.sum(dim=(0, 1, 3)).tolist()], "by window:",
+          [int(x) for x in bad.sum(dim=(1, 2, 3)).tolist()][:16])
+    good = ~bad
+    print(f"  good entries vs emulation max {float((outs[0][good] - emu[good]).abs().max()):.3e}")

@@ -513,8 +513,16 @@ constexpr int kMaxT2Big = 529;    // (2*12-1)^2
 // gradient product in bf16 from the bf16 operands (straight-through quantisation).
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
+// The MX MFMA builtin is not marked convergent by this compiler (ROCm 7.2): when its result
+// only feeds a divergent store (the forward's `if (q < N)` epilogue) LLVM sinks it, with the
+// VALU that builds its operands, into that branch, and the operand lanes of inactive
+// queries are then never written (tools/fp8_debug.py: channels of the last query tile came
+// out garbage).  The empty volatile asm consuming the result pins the instruction -- and so
+// its operands -- where it is written, with every lane active.
 __device__ __forceinline__ f32x16_t mfma_mx(i32x8_t a, int sa, i32x8_t b, int sb, f32x16_t c) {
-  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+  f32x16_t d = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+  __asm__ volatile("" : "+v"(d));
+  return d;
 }
 
 // block scale exponent: the largest k with amax 2^k <= 448 (e4m3 max); 0 for an empty block
