@@ -1,8 +1,8 @@
 """fp8 (OCP e4m3) window attention, BASELINE config C5 (Swin-L, 1536^2, "fp8 MFMA
 window-attention path"), through vs_window_attn_forward_fp8 / _backward_fp8: the
 block-scaled MX MFMA v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 operands, one e8m0 scale per
-32-element block: every q / k token, and per (query, 32-key tile) of P and (channel,
-32-key tile) of V).
+32-element block: every q / k token and every (query, 32-key tile) of P; V, quantised once
+per workgroup while staged, with one scale per (window, head)).
 
 Two yardsticks per case:
   * the kernel's own quantisation model, emulated in torch on the CPU (f32 math on
@@ -83,8 +83,8 @@ def emulate_fwd(qkv, table, heads, ws, shift, nWh, nWw, scale=32 ** -0.5):
     p = torch.exp(s - m)
     l = p.sum(-1, keepdim=True)
     grp = _key_groups(p.shape[-1])
-    v8 = _q8_groups(v.transpose(2, 3), grp).transpose(2, 3)     # per (channel, key block)
-    o = (_q8_groups(p, grp) @ v8) / l
+    sv = _pow2_scale(v.abs().amax(dim=(2, 3), keepdim=True))    # one scale per (window, head)
+    o = (_q8_groups(p, grp) @ _q8(v, sv)) / l
     return o.transpose(1, 2).reshape(Bw, -1, heads * 32), s
 
 

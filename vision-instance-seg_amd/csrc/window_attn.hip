@@ -31,7 +31,6 @@ constexpr int kD = 32;
 struct WinGeom {
   int heads, ws, shift, nWh, nWw, N, T2;  // T2 = (2ws-1)^2
   float scale;
-  int f8dbg;                              // debug (VS_FP8_DBG): bit 0/1/2 = unit scales for P / V / q,k
 };
 
 __device__ __forceinline__ int region_of(int p, int Pp, int ws, int shift) {
@@ -548,43 +547,70 @@ __device__ __forceinline__ float xhalf_max(float v) { return fmaxf(v, __shfl_xor
 
 // a token's channels 16hh..16hh+15 (two 16-B bf16 chunks) -> its logit operand: block 0 =
 // the token (scale from all 32 channels), block 1 zero.  Returns the lane's scale byte.
-__device__ __forceinline__ int mx_token(bf16x8_t c0, bf16x8_t c1, int hh, i32x8_t& q, bool unit = false) {
+__device__ __forceinline__ int mx_token(bf16x8_t c0, bf16x8_t c1, int hh, i32x8_t& q) {
   auto at = [&](int j) {
     return j < 16 ? bf16_bits_to_f32((unsigned short)(j < 8 ? c0[j] : c1[j - 8])) : 0.f;
   };
   float am = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(at(j)));
-  const int k = unit ? 0 : mx_exp(xhalf_max(am));
+  const int k = mx_exp(xhalf_max(am));
   mx_pack(at, k, 0, q);
   return hh == 0 ? 127 - k : 127;
 }
 
-__device__ __forceinline__ int mx_token_lds(const short* row, int hh, bool valid, i32x8_t& q, bool unit = false) {
-  const bf16x8_t c0 = valid ? *reinterpret_cast<const bf16x8_t*>(row + 16 * hh) : zero8();
-  const bf16x8_t c1 = valid ? *reinterpret_cast<const bf16x8_t*>(row + 16 * hh + 8) : zero8();
-  return mx_token(c0, c1, hh, q, unit);
-}
-
-__device__ __forceinline__ int mx_token_gmem(const bf16* row, int hh, bool valid, i32x8_t& q, bool unit = false) {
+__device__ __forceinline__ int mx_token_gmem(const bf16* row, int hh, bool valid, i32x8_t& q) {
   const bf16x8_t c0 = valid ? ld8(row + 16 * hh) : zero8();
   const bf16x8_t c1 = valid ? ld8(row + 16 * hh + 8) : zero8();
-  return mx_token(c0, c1, hh, q, unit);
+  return mx_token(c0, c1, hh, q);
 }
 
 // 16 + 16 values of two 32-element blocks (this lane's halves): per-block scales from the
 // cross-half amax; returns the lane's scale byte (block hh)
 template <typename F>
-__device__ __forceinline__ int mx_blocks(F at, int hh, i32x8_t& q, bool unit = false) {
+__device__ __forceinline__ int mx_blocks(F at, int hh, i32x8_t& q) {
   float a0 = 0.f, a1 = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     a0 = fmaxf(a0, fabsf(at(j)));
     a1 = fmaxf(a1, fabsf(at(16 + j)));
   }
-  const int k0 = unit ? 0 : mx_exp(xhalf_max(a0)), k1 = unit ? 0 : mx_exp(xhalf_max(a1));
+  const int k0 = mx_exp(xhalf_max(a0)), k1 = mx_exp(xhalf_max(a1));
   mx_pack(at, k0, k1, q);
   return 127 - (hh ? k1 : k0);
+}
+
+// Staging-time quantisation of a token held as 4 lanes x 8 channels (lane & 3 = chunk):
+// the token's amax over its 32 channels (two shuffles), its e4m3 bytes (x 2^k, the same
+// bytes mx_token makes from the same values) and its scale byte.
+__device__ __forceinline__ uint2 mx_chunk8(bf16x8_t c, int* scale_byte) {
+  float am = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(bf16_bits_to_f32((unsigned short)c[j])));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  const int k = mx_exp(am);
+  const float sc = __builtin_ldexpf(1.f, k);
+  uint2 out;
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[0]) * sc,
+                                          bf16_bits_to_f32((unsigned short)c[1]) * sc, 0, false);
+  out.x = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[2]) * sc,
+                                          bf16_bits_to_f32((unsigned short)c[3]) * sc, v, true);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[4]) * sc,
+                                      bf16_bits_to_f32((unsigned short)c[5]) * sc, 0, false);
+  out.y = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[6]) * sc,
+                                          bf16_bits_to_f32((unsigned short)c[7]) * sc, v, true);
+  *scale_byte = 127 - k;
+  return out;
+}
+
+// a token's logit operand from its staged e4m3 row (32 bytes at `row8`): lane half hh
+// takes bytes 16hh..16hh+15 as K-block 0, block 1 zero; scale byte of block hh
+__device__ __forceinline__ int mx_token_lds8(const unsigned char* row8, int scale_byte, int hh, i32x8_t& q) {
+  const uint4 v = *reinterpret_cast<const uint4*>(row8 + 16 * hh);
+  q[0] = (int)v.x; q[1] = (int)v.y; q[2] = (int)v.z; q[3] = (int)v.w;
+  q[4] = q[5] = q[6] = q[7] = 0;
+  return hh == 0 ? scale_byte : 127;
 }
 
 template <int NT>
@@ -616,16 +642,11 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
     ck[it] = t < N ? ld8(row + C) : zero8();
     cv[it] = t < N ? ld8(row + 2 * C) : zero8();
   }
+  static_assert(!F8, "fp8: win_attn_fwd_mx");
   const int qrow = 32 * qt + r;
-  i32x8_t qm;                                 // F8: the query token as an MX operand
-  int qs = 127;
-  if (F8) {
-    qs = mx_token_gmem(win + (size_t)qrow * C3 + h * kD, hh, qrow < N, qm, g.f8dbg & 4);
-  } else {
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
-      qb[st] = qrow < N ? ld8(win + (size_t)qrow * C3 + h * kD + 16 * st + 8 * hh) : zero8();
-  }
+  for (int st = 0; st < 2; ++st)
+    qb[st] = qrow < N ? ld8(win + (size_t)qrow * C3 + h * kD + 16 * st + 8 * hh) : zero8();
   window_tokens_blk<NT>(g, bw, sTok);
   for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
 #pragma unroll
@@ -641,23 +662,13 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   f32x16_t acc[NT];
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) zero16(acc[kt]);
-  if (F8) {
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
-      i32x8_t km;
-      const int ks = mx_token_lds(sK + (32 * kt + r) * PK, hh, true, km, g.f8dbg & 4);
-      acc[kt] = mfma_mx(km, ks, qm, qs, acc[kt]);
-      __builtin_amdgcn_sched_barrier(0);      // one key tile's operand quantised at a time
+      const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(sK + (32 * kt + r) * PK + 16 * st + 8 * hh);
+      acc[kt] = mfma16(ka, qb[st], acc[kt]);
     }
-  } else {
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-        const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(sK + (32 * kt + r) * PK + 16 * st + 8 * hh);
-        acc[kt] = mfma16(ka, qb[st], acc[kt]);
-      }
-  }
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
@@ -680,32 +691,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   // O^T = V^T P^T
   f32x16_t o;
   zero16(o);
-  if (F8) {
-#pragma unroll
-    for (int b2 = 0; b2 < (NT + 1) / 2; ++b2) {
-      // block of key tiles 2 b2, 2 b2 + 1: this lane's k = its accumulator rows of both
-      constexpr int kLast = NT - 1;
-      const int k0 = 2 * b2, k1 = 2 * b2 + 1 < NT ? 2 * b2 + 1 : kLast;
-      const bool has1 = 2 * b2 + 1 < NT;
-      bf16x4_t v4[8];
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const bf16x4_t z = {0, 0, 0, 0};
-          v4[4 * u + g4] = (u == 0 || has1) ? *reinterpret_cast<const bf16x4_t*>(
-                                                   sVt + r * PT + 32 * (u ? k1 : k0) + 8 * g4 + 4 * hh)
-                                             : z;
-        }
-      i32x8_t vm, pm;
-      const int vs = mx_blocks([&](int j) { return bf16_bits_to_f32((unsigned short)v4[j >> 2][j & 3]); }, hh, vm,
-                               g.f8dbg & 2);
-      const int ps = mx_blocks([&](int j) { return j < 16 ? acc[k0][j] : (has1 ? acc[k1][j - 16] : 0.f); }, hh,
-                               pm, g.f8dbg & 1);
-      o = mfma_mx(vm, vs, pm, ps, o);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
+  {
 #pragma unroll
     for (int t = 0; t < 2 * NT; ++t) {
       const int kt = t >> 1, th = t & 1;
@@ -724,6 +710,133 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
       *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
     }
     if (hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = lq;
+  }
+}
+
+// fp8 forward (C5): K and V are quantised ONCE per workgroup while staged -- K per token
+// (e4m3 rows + a scale byte each), V with one power-of-two scale for the (window, head),
+// stored transposed as bytes -- so every wave reads ready MX operands from LDS (half the
+// bytes of the bf16 staging) and only quantises its own query and its P tiles (per
+// (query, 32-key tile) scale, in registers).
+template <int NT>
+__global__ void __launch_bounds__(64 * NT) win_attn_fwd_mx(const bf16* __restrict__ qkv, const float* __restrict__ table,
+                                                           bf16* __restrict__ out, float* __restrict__ lse, WinGeom g) {
+  constexpr int NP = 32 * NT, PK8 = 48, PV8 = NP + 16;      // bytes per K row / V^T row
+  __shared__ __attribute__((aligned(16))) unsigned char sK8[NP * PK8];
+  __shared__ __attribute__((aligned(16))) unsigned char sV8[32 * PV8];
+  __shared__ int sKs[NP];
+  __shared__ float sVam[NT];
+  __shared__ float sBias[kMaxT2Big];
+  __shared__ __attribute__((aligned(16))) int sTok[NP];
+  const int bw = blockIdx.x, h = blockIdx.y;
+  const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int N = g.N, C = g.heads * kD, C3 = 3 * C;
+  const bf16* win = qkv + (size_t)bw * N * C3;
+  bf16x8_t ck[2], cv[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    const bf16* row = win + (size_t)t * C3 + h * kD + 8 * c;
+    ck[it] = t < N ? ld8(row + C) : zero8();
+    cv[it] = t < N ? ld8(row + 2 * C) : zero8();
+  }
+  const int qrow = 32 * qt + r;
+  i32x8_t qm;
+  const int qs = mx_token_gmem(win + (size_t)qrow * C3 + h * kD, hh, qrow < N, qm);
+  window_tokens_blk<NT>(g, bw, sTok);
+  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
+  float vam = 0.f;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    int sb;
+    *reinterpret_cast<uint2*>(sK8 + t * PK8 + 8 * c) = mx_chunk8(ck[it], &sb);
+    if (c == 0) sKs[t] = sb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vam = fmaxf(vam, fabsf(bf16_bits_to_f32((unsigned short)cv[it][j])));
+  }
+#pragma unroll
+  for (int sft = 32; sft >= 1; sft >>= 1) vam = fmaxf(vam, __shfl_xor(vam, sft, 64));
+  if (l == 0) sVam[qt] = vam;
+  __syncthreads();
+  float va = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT; ++w) va = fmaxf(va, sVam[w]);
+  const int kv = mx_exp(va);
+  const float svs = __builtin_ldexpf(1.f, kv);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)cv[it][j]) * svs,
+                                                     bf16_bits_to_f32((unsigned short)cv[it][j + 1]) * svs, 0,
+                                                     false);
+      sV8[(8 * c + j) * PV8 + t] = (unsigned char)(pk & 0xff);
+      sV8[(8 * c + j + 1) * PV8 + t] = (unsigned char)((pk >> 8) & 0xff);
+    }
+  }
+  __syncthreads();
+  // S^T = K Q^T: the staged key rows straight into the MX MFMA
+  f32x16_t acc[NT];
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) {
+    zero16(acc[kt]);
+    i32x8_t km;
+    const int key = 32 * kt + r;
+    const int ks = mx_token_lds8(sK8 + key * PK8, sKs[key], hh, km);
+    acc[kt] = mfma_mx(km, ks, qm, qs, acc[kt]);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) {
+    logits_tile(acc[kt], g, sTok, sBias, kt, qt, r, hh);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m = fmaxf(m, acc[kt][i]);
+  }
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      acc[kt][i] = __expf(acc[kt][i] - m);
+      sum += acc[kt][i];
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float lq = m + __logf(sum);
+  const float inv = 1.f / sum;
+  // O^T = V^T P^T, 64 keys (tiles 2 b2, 2 b2 + 1) per instruction; lane half hh takes the
+  // keys of its accumulator rows crow(., hh): 4 consecutive keys = one V^T dword
+  f32x16_t o;
+  zero16(o);
+  const int vsb = 127 - kv;
+#pragma unroll
+  for (int b2 = 0; b2 < (NT + 1) / 2; ++b2) {
+    constexpr int kLast = NT - 1;
+    const int k0 = 2 * b2, k1 = 2 * b2 + 1 < NT ? 2 * b2 + 1 : kLast;
+    const bool has1 = 2 * b2 + 1 < NT;
+    i32x8_t vm, pm;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        vm[4 * u + g4] = (u == 0 || has1)
+                             ? *reinterpret_cast<const int*>(sV8 + r * PV8 + 32 * (u ? k1 : k0) + 8 * g4 + 4 * hh)
+                             : 0;
+    const int ps = mx_blocks([&](int j) { return j < 16 ? acc[k0][j] : (has1 ? acc[k1][j - 16] : 0.f); }, hh, pm);
+    o = mfma_mx(vm, vsb, pm, ps, o);
+  }
+  if (qrow < N) {
+    bf16* dst = out + ((size_t)bw * N + qrow) * C + h * kD;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      bf16x4_t v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[4 * grp + e] * inv);
+      *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+    }
+    if (hh == 0) lse[((size_t)bw * g.heads + h) * N + qrow] = lq;
   }
 }
 
@@ -818,10 +931,21 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   short* sVn = sU + kNat;
   short* sKT = sU + 2 * kNat;
   float* sBins = reinterpret_cast<float*>(sU + 2 * kNat + kTr);
+  // F8: the key rows staged as the forward's e4m3 rows + scale bytes (in sKn's space:
+  // the logits are the only phase-1 reader of natural-order K)
+  constexpr int PK8 = 48;
+  unsigned char* sK8 = reinterpret_cast<unsigned char*>(sKn);
+  int* sKs = reinterpret_cast<int*>(sK8 + NP * PK8);
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
-    *reinterpret_cast<bf16x8_t*>(sKn + t * PK + 8 * c) = ck[it];
+    if (F8) {
+      int sb;
+      *reinterpret_cast<uint2*>(sK8 + t * PK8 + 8 * c) = mx_chunk8(ck[it], &sb);
+      if (c == 0) sKs[t] = sb;
+    } else {
+      *reinterpret_cast<bf16x8_t*>(sKn + t * PK + 8 * c) = ck[it];
+    }
     *reinterpret_cast<bf16x8_t*>(sVn + t * PK + 8 * c) = cv[it];
 #pragma unroll
     for (int j = 0; j < 8; ++j) sKT[(8 * c + j) * PT + t] = ck[it][j];
@@ -852,7 +976,8 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     zero16(dp);
     if (F8) {                                 // the forward's logits: same operands, order, scales
       i32x8_t km;
-      const int ks = mx_token_lds(sKn + (32 * kt + r) * PK, hh, true, km);
+      const int key = 32 * kt + r;
+      const int ks = mx_token_lds8(sK8 + key * PK8, sKs[key], hh, km);
       s = mfma_mx(km, ks, qm, qs, s);
     }
 #pragma unroll
@@ -915,10 +1040,18 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   short* sDn = sU + kNat;
   short* sQT = sU + 2 * kNat;
   short* sDT = sU + 2 * kNat + kTr;
+  unsigned char* sQ8 = reinterpret_cast<unsigned char*>(sQn);   // F8: the query rows as e4m3
+  int* sQs = reinterpret_cast<int*>(sQ8 + NP * PK8);
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
-    *reinterpret_cast<bf16x8_t*>(sQn + t * PK + 8 * c) = cq[it];
+    if (F8) {
+      int sb;
+      *reinterpret_cast<uint2*>(sQ8 + t * PK8 + 8 * c) = mx_chunk8(cq[it], &sb);
+      if (c == 0) sQs[t] = sb;
+    } else {
+      *reinterpret_cast<bf16x8_t*>(sQn + t * PK + 8 * c) = cq[it];
+    }
     *reinterpret_cast<bf16x8_t*>(sDn + t * PK + 8 * c) = cd[it];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -939,7 +1072,8 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     zero16(dp);
     if (F8) {                                 // S = Q K^T on the same MX operands (A / B swapped)
       i32x8_t qa8;
-      const int qa_s = mx_token_lds(sQn + (32 * qq + r) * PK, hh, true, qa8);
+      const int qrw = 32 * qq + r;
+      const int qa_s = mx_token_lds8(sQ8 + qrw * PK8, sQs[qrw], hh, qa8);
       s = mfma_mx(qa8, qa_s, km, ks, s);
     }
 #pragma unroll
@@ -981,8 +1115,6 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
 
 int check_geom(WinGeom& g, int Bw, int heads, int ws, int shift, int nWh, int nWw, float scale) {
   g.heads = heads; g.ws = ws; g.shift = shift; g.nWh = nWh; g.nWw = nWw; g.scale = scale;
-  g.f8dbg = 0;
-  if (const char* e = getenv("VS_FP8_DBG")) g.f8dbg = atoi(e);
   g.N = ws * ws;
   g.T2 = (2 * ws - 1) * (2 * ws - 1);
   return Bw > 0 && heads > 0 && ws > 0 && ws <= 16 && shift >= 0 && shift < ws && nWh > 0 && nWw > 0 &&
@@ -1018,8 +1150,12 @@ template <bool F8>
 static void launch_fwd_blk(const WinGeom& g, dim3 grid, hipStream_t st, const void* qkv, const float* table,
                            void* out, float* lse) {
 #define VS_FWD_BLK(NT_)                                                                                     \
-  hipLaunchKernelGGL((win_attn_fwd_mfma_big<NT_, F8>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table, \
-                     (bf16*)out, lse, g)
+  if (F8)                                                                                                   \
+    hipLaunchKernelGGL((win_attn_fwd_mx<NT_>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,         \
+                       (bf16*)out, lse, g);                                                                 \
+  else                                                                                                      \
+    hipLaunchKernelGGL((win_attn_fwd_mfma_big<NT_, false>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv,   \
+                       table, (bf16*)out, lse, g)
   VS_NT_SWITCH((g.N + 31) / 32, VS_FWD_BLK)
 #undef VS_FWD_BLK
 }
