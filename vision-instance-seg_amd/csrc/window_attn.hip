@@ -613,6 +613,36 @@ __device__ __forceinline__ int mx_token_lds8(const unsigned char* row8, int scal
   return hh == 0 ? scale_byte : 127;
 }
 
+// e4m3 round trip of 8 bf16 values at scale 2^k, back in bf16 (exact: e4m3 values carry 4
+// significant bits): the dequantised operand the fp8 logits were formed from.
+__device__ __forceinline__ bf16x8_t fp8_roundtrip8(bf16x8_t c, int k) {
+  const float sc = __builtin_ldexpf(1.f, k), inv = __builtin_ldexpf(1.f, -k);
+  bf16x8_t o;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[j]) * sc,
+                                                   bf16_bits_to_f32((unsigned short)c[j + 1]) * sc, 0, false);
+    o[j] = bf16_bits(__builtin_amdgcn_cvt_f32_fp8(pk, 0) * inv);
+    o[j + 1] = bf16_bits(__builtin_amdgcn_cvt_f32_fp8(pk, 1) * inv);
+  }
+  return o;
+}
+
+__device__ __forceinline__ float amax8(bf16x8_t c) {
+  float am = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(bf16_bits_to_f32((unsigned short)c[j])));
+  return am;
+}
+
+// a staged token chunk (4 lanes x 8 channels) rounded through e4m3 at its token scale
+__device__ __forceinline__ bf16x8_t fp8_token_chunk(bf16x8_t c) {
+  float am = amax8(c);
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  return fp8_roundtrip8(c, mx_exp(am));
+}
+
 template <int NT>
 __device__ __forceinline__ void window_tokens_blk(const WinGeom& g, int bw, int* tok) {
   for (int t = threadIdx.x; t < 32 * NT; t += blockDim.x) tok[t] = token_meta(g, bw, t);
@@ -931,21 +961,12 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   short* sVn = sU + kNat;
   short* sKT = sU + 2 * kNat;
   float* sBins = reinterpret_cast<float*>(sU + 2 * kNat + kTr);
-  // F8: the key rows staged as the forward's e4m3 rows + scale bytes (in sKn's space:
-  // the logits are the only phase-1 reader of natural-order K)
-  constexpr int PK8 = 48;
-  unsigned char* sK8 = reinterpret_cast<unsigned char*>(sKn);
-  int* sKs = reinterpret_cast<int*>(sK8 + NP * PK8);
+  // F8: natural-order K (read only by the logits) staged as the forward's e4m3 values
+  // (per-token scale), dequantised back to bf16 exactly; the gradients use raw K (sKT)
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
-    if (F8) {
-      int sb;
-      *reinterpret_cast<uint2*>(sK8 + t * PK8 + 8 * c) = mx_chunk8(ck[it], &sb);
-      if (c == 0) sKs[t] = sb;
-    } else {
-      *reinterpret_cast<bf16x8_t*>(sKn + t * PK + 8 * c) = ck[it];
-    }
+    *reinterpret_cast<bf16x8_t*>(sKn + t * PK + 8 * c) = F8 ? fp8_token_chunk(ck[it]) : ck[it];
     *reinterpret_cast<bf16x8_t*>(sVn + t * PK + 8 * c) = cv[it];
 #pragma unroll
     for (int j = 0; j < 8; ++j) sKT[(8 * c + j) * PT + t] = ck[it][j];
@@ -964,9 +985,12 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   for (int t = threadIdx.x; t < NT * kBinW; t += blockDim.x) sBins[t] = 0.f;
   __syncthreads();
   const WinGeom& gl = g;
-  i32x8_t qm;                                 // F8: this lane's query token, the forward's MX operand
-  int qs = 127;
-  if (F8) qs = mx_token_gmem(win + (size_t)q * C3, hh, q < N, qm);
+  bf16x8_t qs8[2] = {qb[0], qb[1]};          // F8: this lane's query as the forward's e4m3 values
+  if (F8) {
+    const int kq = mx_exp(xhalf_max(fmaxf(amax8(qb[0]), amax8(qb[1]))));
+    qs8[0] = fp8_roundtrip8(qb[0], kq);
+    qs8[1] = fp8_roundtrip8(qb[1], kq);
+  }
   float* bins = sBins + qt * kBinW;
   f32x16_t dq;
   zero16(dq);
@@ -974,16 +998,12 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     f32x16_t s, dp;
     zero16(s);
     zero16(dp);
-    if (F8) {                                 // the forward's logits: same operands, order, scales
-      i32x8_t km;
-      const int key = 32 * kt + r;
-      const int ks = mx_token_lds8(sK8 + key * PK8, sKs[key], hh, km);
-      s = mfma_mx(km, ks, qm, qs, s);
-    }
+    // F8: the forward's logits from the same e4m3 values (dequantised exactly), summed in
+    // another order: S agrees to f32 rounding, so exp(S - lse) is the forward's P
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       const int o = (32 * kt + r) * PK + 16 * st + 8 * hh;
-      if (!F8) s = mfma16(*reinterpret_cast<const bf16x8_t*>(sKn + o), qb[st], s);
+      s = mfma16(*reinterpret_cast<const bf16x8_t*>(sKn + o), qs8[st], s);
       dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sVn + o), db[st], dp);
     }
     int rel[16];
@@ -1040,18 +1060,11 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   short* sDn = sU + kNat;
   short* sQT = sU + 2 * kNat;
   short* sDT = sU + 2 * kNat + kTr;
-  unsigned char* sQ8 = reinterpret_cast<unsigned char*>(sQn);   // F8: the query rows as e4m3
-  int* sQs = reinterpret_cast<int*>(sQ8 + NP * PK8);
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
-    if (F8) {
-      int sb;
-      *reinterpret_cast<uint2*>(sQ8 + t * PK8 + 8 * c) = mx_chunk8(cq[it], &sb);
-      if (c == 0) sQs[t] = sb;
-    } else {
-      *reinterpret_cast<bf16x8_t*>(sQn + t * PK + 8 * c) = cq[it];
-    }
+    // F8: natural-order Q (read only by the logits) as its e4m3 values
+    *reinterpret_cast<bf16x8_t*>(sQn + t * PK + 8 * c) = F8 ? fp8_token_chunk(cq[it]) : cq[it];
     *reinterpret_cast<bf16x8_t*>(sDn + t * PK + 8 * c) = cd[it];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1059,9 +1072,12 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
       sDT[(8 * c + j) * PT + t] = cd[it][j];
     }
   }
-  i32x8_t km;                                 // F8: this lane's key token as an MX operand
-  int ks = 127;
-  if (F8) ks = mx_token_gmem(win + (size_t)key * C3 + C, hh, key < N, km);
+  bf16x8_t ks8[2] = {kb[0], kb[1]};          // F8: this lane's key as the forward's e4m3 values
+  if (F8) {
+    const int kk = mx_exp(xhalf_max(fmaxf(amax8(kb[0]), amax8(kb[1]))));
+    ks8[0] = fp8_roundtrip8(kb[0], kk);
+    ks8[1] = fp8_roundtrip8(kb[1], kk);
+  }
   __syncthreads();
   f32x16_t dv, dk;
   zero16(dv);
@@ -1070,16 +1086,10 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     f32x16_t s, dp;
     zero16(s);
     zero16(dp);
-    if (F8) {                                 // S = Q K^T on the same MX operands (A / B swapped)
-      i32x8_t qa8;
-      const int qrw = 32 * qq + r;
-      const int qa_s = mx_token_lds8(sQ8 + qrw * PK8, sQs[qrw], hh, qa8);
-      s = mfma_mx(qa8, qa_s, km, ks, s);
-    }
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       const int o = (32 * qq + r) * PK + 16 * st + 8 * hh;
-      if (!F8) s = mfma16(*reinterpret_cast<const bf16x8_t*>(sQn + o), kb[st], s);
+      s = mfma16(*reinterpret_cast<const bf16x8_t*>(sQn + o), ks8[st], s);
       dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sDn + o), vb[st], dp);
     }
     logits_qk(s, gl, sTok, sBias, qq, key, hh);
