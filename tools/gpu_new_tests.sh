@@ -6,3 +6,5 @@ timeout -k 10 300 python tools/winbench.py --configs C5 > gpurun_out/r3_winbench
 grep "sum over" gpurun_out/r3_winbench_c5.txt
 timeout -k 10 300 python bench.py --model swin_l --size 1536 --attn-fp8 --no-cpu-baseline --no-parity --steps 5 > gpurun_out/r3_bench_c5_fp8.log 2>&1 || exit $?
 tail -1 gpurun_out/r3_bench_c5_fp8.log | cut -c1-200
+timeout -k 10 300 python bench.py --model swin_l --size 1536 --no-cpu-baseline --no-parity --steps 5 > gpurun_out/r3_bench_c5_bf16.log 2>&1 || exit $?
+tail -1 gpurun_out/r3_bench_c5_bf16.log | cut -c1-200

@@ -491,25 +491,25 @@ __global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* 
 constexpr int kMaxT2Big = 529;    // (2*12-1)^2
 
 // ---- fp8 (OCP e4m3, gfx950) window attention, config C5 ------------------------------
-// F8 = true runs the logits S^T = K Q^T (forward and the backward's recomputes) and
-// O^T = V^T P^T (forward) on the BLOCK-SCALED MX MFMA v_mfma_scale_f32_32x32x64_f8f6f4
-// with e4m3 operands: 2x the bf16 MFMA rate per clock on gfx950 (MI355X_MICROARCH.md
-// §Matrix cores), the dequantisation fused into the instruction.  Operand layout, as
-// measured on the box (tools/micro/mfma_scale_probe.hip, profiles/r3_mfma_scale_probe.txt):
-// K = 64 is two 32-deep scale blocks; lane l (row / column l&31, half hh = l>>5) holds 16
-// elements of block 0 in its dwords 0-3 and 16 of block 1 in dwords 4-7 (the two lanes of
-// a row hold all 32 of each block; any k order works as long as A and B agree), and its
-// e8m0 scale byte (2^(e-127)) is the scale of block hh of its row / column.
+// F8 = true runs the forward's logits S^T = K Q^T and O^T = V^T P^T on the BLOCK-SCALED MX
+// MFMA v_mfma_scale_f32_32x32x64_f8f6f4 with e4m3 operands: 2x the bf16 MFMA rate per clock
+// on gfx950 (MI355X_MICROARCH.md §Matrix cores), the dequantisation fused into the
+// instruction.  Operand layout, as measured on the box (tools/micro/mfma_scale_probe.hip,
+// profiles/r3_mfma_scale_probe.txt): K = 64 is two 32-deep scale blocks; lane l (row /
+// column l&31, half hh = l>>5) holds 16 elements of block 0 in its dwords 0-3 and 16 of
+// block 1 in dwords 4-7 (the two lanes of a row hold all 32 of each block; any k order
+// works as long as A and B agree), and its e8m0 scale byte (2^(e-127)) is the scale of
+// block hh of its row / column.
 //   * logits: the head dimension (32) is block 0 (block 1 is zero): lane half hh carries
 //     channels 16hh..16hh+15, so every q and k TOKEN gets its own power-of-two scale (amax
-//     over its 32 channels: the lane's 16 and one cross-half shuffle);
+//     over its 32 channels);
 //   * P V: 64 keys per instruction, block 0 = key tile 2b, block 1 = tile 2b+1; lane half
 //     hh takes its own accumulator rows (crow(., hh)) of both tiles, so P comes straight
-//     from the registers; each (query, key tile) of P and (channel, key tile) of V has its
-//     own scale.
-// Operands stay bf16 in HBM and LDS; the backward recomputes S on the same fp8 operands
-// and scales (identical logits, so exp(S - lse) is the forward's P) and forms every
-// gradient product in bf16 from the bf16 operands (straight-through quantisation).
+//     from the registers, at one fixed scale (mx_pfixed); V has one scale per (window, head).
+// Operands stay bf16 in HBM; the backward recomputes S from the same e4m3 values,
+// dequantised exactly to bf16 (the logits agree to f32 rounding, so exp(S - lse) is the
+// forward's P), and forms every gradient product in bf16 from the bf16 operands
+// (straight-through quantisation).
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
 // The MX MFMA builtin is not marked convergent by this compiler (ROCm 7.2): when its result
@@ -524,38 +524,69 @@ __device__ __forceinline__ f32x16_t mfma_mx(i32x8_t a, int sa, i32x8_t b, int sb
   return d;
 }
 
+// Conversions use gfx950's scaled instructions straight from / to bf16 pairs (one
+// instruction per pair and direction): v_cvt_scalef32_pk_fp8_bf16 with scale 2^-k makes
+// e4m3(x 2^k), and v_cvt_scalef32_pk_bf16_fp8 with the same scale gives back e4m3 2^-k, both
+// bit-identical to the unscaled conversion of the rescaled value
+// (tools/micro/cvt_scale_probe.hip, profiles/r3_cvt_scale_probe.txt).
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint4 bits128(bf16x8_t c) { return __builtin_bit_cast(uint4, c); }
+
+// e4m3 bytes of two bf16 pairs, x 2^k (inv = 2^-k)
+__device__ __forceinline__ int e4m3x4(unsigned lo, unsigned hi, float inv) {
+  s16x2_t r = {0, 0};
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, __builtin_bit_cast(bf16x2v_t, lo), inv, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, __builtin_bit_cast(bf16x2v_t, hi), inv, true);
+  return __builtin_bit_cast(int, r);
+}
+
+// largest |x| of 8 bf16 values as bf16 bits (for non-negative bf16, integer order is value
+// order): packed 16-bit max over the sign-cleared dwords
+__device__ __forceinline__ unsigned amax8_bits(bf16x8_t c) {
+  const uint4 u = bits128(c);
+  u16x2_t m = __builtin_bit_cast(u16x2_t, u.x & 0x7fff7fffu);
+  m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2_t, u.y & 0x7fff7fffu));
+  m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2_t, u.z & 0x7fff7fffu));
+  m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2_t, u.w & 0x7fff7fffu));
+  return m[0] > m[1] ? m[0] : m[1];
+}
+
+__device__ __forceinline__ unsigned umax_xor(unsigned v, int sft) {
+  const unsigned o = (unsigned)__shfl_xor((int)v, sft, 64);
+  return o > v ? o : v;
+}
+
 // block scale exponent: the largest k with amax 2^k <= 448 (e4m3 max); 0 for an empty block
 __device__ __forceinline__ int mx_exp(float amax) {
   const int k = amax > 0.f ? (int)floorf(log2f(448.f / amax)) : 0;
   return min(max(k, -126), 126);
 }
 
-// 16 + 16 values (this lane's share of K-block 0, then of block 1) -> e4m3 dwords 0-3 /
-// 4-7, scaled by 2^k0 / 2^k1 (exact: powers of two); `at(j)` yields element j
-template <typename F>
-__device__ __forceinline__ void mx_pack(F at, int k0, int k1, i32x8_t& q) {
-  const float s0 = __builtin_ldexpf(1.f, k0), s1 = __builtin_ldexpf(1.f, k1);
-#pragma unroll
-  for (int w = 0; w < 8; ++w) {
-    const float sc = w < 4 ? s0 : s1;
-    const int v = __builtin_amdgcn_cvt_pk_fp8_f32(at(4 * w) * sc, at(4 * w + 1) * sc, 0, false);
-    q[w] = __builtin_amdgcn_cvt_pk_fp8_f32(at(4 * w + 2) * sc, at(4 * w + 3) * sc, v, true);
-  }
+// the same from the amax's bf16 bits: amax = 1.m 2^(e-127) and 448 = 1.75 2^8, so
+// k = 135 - e, one less when the mantissa exceeds 1.75 (0x60); subnormals take the float path
+__device__ __forceinline__ int mx_exp_bits(unsigned b) {
+  if (b < 0x80u) return mx_exp(__uint_as_float(b << 16));
+  const int k = 135 - (int)(b >> 7) - ((b & 0x7fu) > 0x60u ? 1 : 0);
+  return min(max(k, -126), 126);
 }
 
-__device__ __forceinline__ float xhalf_max(float v) { return fmaxf(v, __shfl_xor(v, 32, 64)); }
+__device__ __forceinline__ unsigned xhalf_max_bits(unsigned v) { return umax_xor(v, 32); }
 
 // a token's channels 16hh..16hh+15 (two 16-B bf16 chunks) -> its logit operand: block 0 =
 // the token (scale from all 32 channels), block 1 zero.  Returns the lane's scale byte.
 __device__ __forceinline__ int mx_token(bf16x8_t c0, bf16x8_t c1, int hh, i32x8_t& q) {
-  auto at = [&](int j) {
-    return j < 16 ? bf16_bits_to_f32((unsigned short)(j < 8 ? c0[j] : c1[j - 8])) : 0.f;
-  };
-  float am = 0.f;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(at(j)));
-  const int k = mx_exp(xhalf_max(am));
-  mx_pack(at, k, 0, q);
+  const unsigned am = xhalf_max_bits(max(amax8_bits(c0), amax8_bits(c1)));
+  const int k = mx_exp_bits(am);
+  const float inv = __builtin_ldexpf(1.f, -k);
+  const uint4 u0 = bits128(c0), u1 = bits128(c1);
+  q[0] = e4m3x4(u0.x, u0.y, inv);
+  q[1] = e4m3x4(u0.z, u0.w, inv);
+  q[2] = e4m3x4(u1.x, u1.y, inv);
+  q[3] = e4m3x4(u1.z, u1.w, inv);
+  q[4] = q[5] = q[6] = q[7] = 0;
   return hh == 0 ? 127 - k : 127;
 }
 
@@ -565,43 +596,33 @@ __device__ __forceinline__ int mx_token_gmem(const bf16* row, int hh, bool valid
   return mx_token(c0, c1, hh, q);
 }
 
-// 16 + 16 values of two 32-element blocks (this lane's halves): per-block scales from the
-// cross-half amax; returns the lane's scale byte (block hh)
+// P = exp(S - max) <= 1 as an MX operand with ONE fixed scale: e4m3(256 P), scale byte
+// 127 - 8.  A per-block scale would pick 2^8 too for every block holding its row's maximum
+// and differs only below 2^-14 (subnormal e4m3 here), so no amax is needed; `at(j)` yields
+// this lane's element j (16 of K-block 0, then 16 of block 1)
+constexpr int kPScaleByte = 127 - 8;
 template <typename F>
-__device__ __forceinline__ int mx_blocks(F at, int hh, i32x8_t& q) {
-  float a0 = 0.f, a1 = 0.f;
+__device__ __forceinline__ void mx_pfixed(F at, i32x8_t& q) {
+  constexpr float inv = 1.f / 256.f;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    a0 = fmaxf(a0, fabsf(at(j)));
-    a1 = fmaxf(a1, fabsf(at(16 + j)));
+  for (int w = 0; w < 8; ++w) {
+    s16x2_t r = {0, 0};
+    r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, at(4 * w), at(4 * w + 1), inv, false);
+    r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, at(4 * w + 2), at(4 * w + 3), inv, true);
+    q[w] = __builtin_bit_cast(int, r);
   }
-  const int k0 = mx_exp(xhalf_max(a0)), k1 = mx_exp(xhalf_max(a1));
-  mx_pack(at, k0, k1, q);
-  return 127 - (hh ? k1 : k0);
 }
 
 // Staging-time quantisation of a token held as 4 lanes x 8 channels (lane & 3 = chunk):
 // the token's amax over its 32 channels (two shuffles), its e4m3 bytes (x 2^k, the same
 // bytes mx_token makes from the same values) and its scale byte.
 __device__ __forceinline__ uint2 mx_chunk8(bf16x8_t c, int* scale_byte) {
-  float am = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(bf16_bits_to_f32((unsigned short)c[j])));
-  am = fmaxf(am, __shfl_xor(am, 1, 64));
-  am = fmaxf(am, __shfl_xor(am, 2, 64));
-  const int k = mx_exp(am);
-  const float sc = __builtin_ldexpf(1.f, k);
-  uint2 out;
-  int v = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[0]) * sc,
-                                          bf16_bits_to_f32((unsigned short)c[1]) * sc, 0, false);
-  out.x = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[2]) * sc,
-                                          bf16_bits_to_f32((unsigned short)c[3]) * sc, v, true);
-  v = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[4]) * sc,
-                                      bf16_bits_to_f32((unsigned short)c[5]) * sc, 0, false);
-  out.y = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[6]) * sc,
-                                          bf16_bits_to_f32((unsigned short)c[7]) * sc, v, true);
+  const unsigned am = umax_xor(umax_xor(amax8_bits(c), 1), 2);
+  const int k = mx_exp_bits(am);
+  const float inv = __builtin_ldexpf(1.f, -k);
+  const uint4 u = bits128(c);
   *scale_byte = 127 - k;
-  return out;
+  return make_uint2((unsigned)e4m3x4(u.x, u.y, inv), (unsigned)e4m3x4(u.z, u.w, inv));
 }
 
 // a token's logit operand from its staged e4m3 row (32 bytes at `row8`): lane half hh
@@ -614,33 +635,32 @@ __device__ __forceinline__ int mx_token_lds8(const unsigned char* row8, int scal
 }
 
 // e4m3 round trip of 8 bf16 values at scale 2^k, back in bf16 (exact: e4m3 values carry 4
-// significant bits): the dequantised operand the fp8 logits were formed from.
+// significant bits): the dequantised operand the fp8 logits were formed from
 __device__ __forceinline__ bf16x8_t fp8_roundtrip8(bf16x8_t c, int k) {
-  const float sc = __builtin_ldexpf(1.f, k), inv = __builtin_ldexpf(1.f, -k);
-  bf16x8_t o;
+  const float inv = __builtin_ldexpf(1.f, -k);
+  const uint4 u = bits128(c);
+  const unsigned in[4] = {u.x, u.y, u.z, u.w};
+  unsigned o[4];
 #pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)c[j]) * sc,
-                                                   bf16_bits_to_f32((unsigned short)c[j + 1]) * sc, 0, false);
-    o[j] = bf16_bits(__builtin_amdgcn_cvt_f32_fp8(pk, 0) * inv);
-    o[j + 1] = bf16_bits(__builtin_amdgcn_cvt_f32_fp8(pk, 1) * inv);
+  for (int j = 0; j < 4; ++j) {
+    const s16x2_t r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(s16x2_t{0, 0}, __builtin_bit_cast(bf16x2v_t, in[j]),
+                                                                inv, false);
+    o[j] = __builtin_bit_cast(unsigned,
+                              __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(__builtin_bit_cast(unsigned, r), inv, false));
   }
-  return o;
-}
-
-__device__ __forceinline__ float amax8(bf16x8_t c) {
-  float am = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(bf16_bits_to_f32((unsigned short)c[j])));
-  return am;
+  return __builtin_bit_cast(bf16x8_t, make_uint4(o[0], o[1], o[2], o[3]));
 }
 
 // a staged token chunk (4 lanes x 8 channels) rounded through e4m3 at its token scale
 __device__ __forceinline__ bf16x8_t fp8_token_chunk(bf16x8_t c) {
-  float am = amax8(c);
-  am = fmaxf(am, __shfl_xor(am, 1, 64));
-  am = fmaxf(am, __shfl_xor(am, 2, 64));
-  return fp8_roundtrip8(c, mx_exp(am));
+  return fp8_roundtrip8(c, mx_exp_bits(umax_xor(umax_xor(amax8_bits(c), 1), 2)));
+}
+
+// this lane's half-token (two chunks) rounded through e4m3 at the token's scale
+__device__ __forceinline__ void fp8_token_lane(bf16x8_t* c) {
+  const int k = mx_exp_bits(xhalf_max_bits(max(amax8_bits(c[0]), amax8_bits(c[1]))));
+  c[0] = fp8_roundtrip8(c[0], k);
+  c[1] = fp8_roundtrip8(c[1], k);
 }
 
 template <int NT>
@@ -755,7 +775,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mx(const bf16* __restric
   __shared__ __attribute__((aligned(16))) unsigned char sK8[NP * PK8];
   __shared__ __attribute__((aligned(16))) unsigned char sV8[32 * PV8];
   __shared__ int sKs[NP];
-  __shared__ float sVam[NT];
+  __shared__ unsigned sVam[NT];
   __shared__ float sBias[kMaxT2Big];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
   const int bw = blockIdx.x, h = blockIdx.y;
@@ -775,36 +795,31 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mx(const bf16* __restric
   const int qs = mx_token_gmem(win + (size_t)qrow * C3 + h * kD, hh, qrow < N, qm);
   window_tokens_blk<NT>(g, bw, sTok);
   for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
-  float vam = 0.f;
+  unsigned vam = 0;
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
     int sb;
     *reinterpret_cast<uint2*>(sK8 + t * PK8 + 8 * c) = mx_chunk8(ck[it], &sb);
     if (c == 0) sKs[t] = sb;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) vam = fmaxf(vam, fabsf(bf16_bits_to_f32((unsigned short)cv[it][j])));
+    vam = max(vam, amax8_bits(cv[it]));
   }
 #pragma unroll
-  for (int sft = 32; sft >= 1; sft >>= 1) vam = fmaxf(vam, __shfl_xor(vam, sft, 64));
+  for (int sft = 32; sft >= 1; sft >>= 1) vam = umax_xor(vam, sft);
   if (l == 0) sVam[qt] = vam;
   __syncthreads();
-  float va = 0.f;
+  unsigned va = 0;
 #pragma unroll
-  for (int w = 0; w < NT; ++w) va = fmaxf(va, sVam[w]);
-  const int kv = mx_exp(va);
-  const float svs = __builtin_ldexpf(1.f, kv);
+  for (int w = 0; w < NT; ++w) va = max(va, sVam[w]);
+  const int kv = mx_exp_bits(va);
+  const float vinv = __builtin_ldexpf(1.f, -kv);
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    const uint4 u = bits128(cv[it]);
+    const int w0 = e4m3x4(u.x, u.y, vinv), w1 = e4m3x4(u.z, u.w, vinv);
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_bits_to_f32((unsigned short)cv[it][j]) * svs,
-                                                     bf16_bits_to_f32((unsigned short)cv[it][j + 1]) * svs, 0,
-                                                     false);
-      sV8[(8 * c + j) * PV8 + t] = (unsigned char)(pk & 0xff);
-      sV8[(8 * c + j + 1) * PV8 + t] = (unsigned char)((pk >> 8) & 0xff);
-    }
+    for (int j = 0; j < 8; ++j) sV8[(8 * c + j) * PV8 + t] = (unsigned char)(((j < 4 ? w0 : w1) >> (8 * (j & 3))) & 0xff);
   }
   __syncthreads();
   // S^T = K Q^T: the staged key rows straight into the MX MFMA
@@ -854,8 +869,8 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mx(const bf16* __restric
         vm[4 * u + g4] = (u == 0 || has1)
                              ? *reinterpret_cast<const int*>(sV8 + r * PV8 + 32 * (u ? k1 : k0) + 8 * g4 + 4 * hh)
                              : 0;
-    const int ps = mx_blocks([&](int j) { return j < 16 ? acc[k0][j] : (has1 ? acc[k1][j - 16] : 0.f); }, hh, pm);
-    o = mfma_mx(vm, vsb, pm, ps, o);
+    mx_pfixed([&](int j) { return j < 16 ? acc[k0][j] : (has1 ? acc[k1][j - 16] : 0.f); }, pm);
+    o = mfma_mx(vm, vsb, pm, kPScaleByte, o);
   }
   if (qrow < N) {
     bf16* dst = out + ((size_t)bw * N + qrow) * C + h * kD;
@@ -986,11 +1001,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   __syncthreads();
   const WinGeom& gl = g;
   bf16x8_t qs8[2] = {qb[0], qb[1]};          // F8: this lane's query as the forward's e4m3 values
-  if (F8) {
-    const int kq = mx_exp(xhalf_max(fmaxf(amax8(qb[0]), amax8(qb[1]))));
-    qs8[0] = fp8_roundtrip8(qb[0], kq);
-    qs8[1] = fp8_roundtrip8(qb[1], kq);
-  }
+  if (F8) fp8_token_lane(qs8);
   float* bins = sBins + qt * kBinW;
   f32x16_t dq;
   zero16(dq);
@@ -1073,11 +1084,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     }
   }
   bf16x8_t ks8[2] = {kb[0], kb[1]};          // F8: this lane's key as the forward's e4m3 values
-  if (F8) {
-    const int kk = mx_exp(xhalf_max(fmaxf(amax8(kb[0]), amax8(kb[1]))));
-    ks8[0] = fp8_roundtrip8(kb[0], kk);
-    ks8[1] = fp8_roundtrip8(kb[1], kk);
-  }
+  if (F8) fp8_token_lane(ks8);
   __syncthreads();
   f32x16_t dv, dk;
   zero16(dv);
