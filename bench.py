@@ -293,10 +293,16 @@ def parity_check(model_name, size, queries, dev):
                        f"vs the oracle CPU restatement (fp32), all {cfg.dec_layers} decoder steps")
 
 
-# Algorithmic training FLOPs per image (forward matmul/conv FLOPs x 3; forward counted
-# with torch.utils.flop_counter on the HF oracle) for the BASELINE configs
-TRAIN_FLOPS_PER_IMAGE = {("swin_t", 1024): 3 * 530.6e9, ("swin_b", 1024): 3 * 1022.2e9,
-                         ("swin_l", 1536): 3 * 3974.2e9}
+# Algorithmic training FLOPs per image (forward matmul/conv FLOPs x 3) for the BASELINE
+# configs: Mask2Former forward counted with torch.utils.flop_counter on the HF oracle
+# (BASELINE.md §2); MaskDINO (C4, no HF model exists) counted by the same method on the
+# product's own training forward, denoising queries included, with the custom ops priced
+# as the matmuls they replace (tools/flops.py --arch maskdino --model swin_l, measured on
+# the box: 2198.3 GFLOP; profiles/r3_flops_c4.json)
+TRAIN_FLOPS_PER_IMAGE = {("mask2former", "swin_t", 1024): 3 * 530.6e9,
+                         ("mask2former", "swin_b", 1024): 3 * 1022.2e9,
+                         ("mask2former", "swin_l", 1536): 3 * 3974.2e9,
+                         ("maskdino", "swin_l", 1024): 3 * 2198.3e9}
 
 
 def _config_tag(model, size, arch="mask2former", fp8=False):
@@ -385,14 +391,14 @@ def main():
         if world == 1 and not a.no_parity and a.arch == "mask2former":
             print("parity check vs the oracle ...", file=sys.stderr, flush=True)
             parity = parity_check(a.model, a.size, a.queries, dev)
-        fl = TRAIN_FLOPS_PER_IMAGE.get((a.model, a.size)) if a.arch == "mask2former" else None
+        fl = TRAIN_FLOPS_PER_IMAGE.get((a.arch, a.model, a.size))
         step_roof = None
         if fl:
             ach = fl * value / 1e12
             step_roof = dict(bound="mfma", achieved=round(ach, 1), peak=MFMA_BF16_PEAK_TFS * world, unit="TFLOP/s",
                              frac=round(ach / (MFMA_BF16_PEAK_TFS * world), 4),
                              algorithmic_flops_per_image=fl,
-                             note="whole training step: 3 x forward matmul/conv FLOPs (BASELINE.md §2) x images/s "
+                             note="whole training step: 3 x forward matmul/conv FLOPs (BASELINE.md §2; C4: tools/flops.py) x images/s "
                                   "/ (dense bf16 MFMA peak x GPUs)")
         prec = ("bf16 parameters and activations, f32 master weights, gradients reduced and applied in f32 "
                 "(pure bf16, not autocast)" if a.precision == "bf16" else "f32 parameters + bf16 autocast")

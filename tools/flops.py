@@ -63,6 +63,8 @@ def count(arch, model, size, queries, batch=1):
         cfg = M2FConfig.preset(model, num_queries=queries)
         m = Mask2Former(cfg).init_weights(0).to(dev).to(torch.bfloat16).train()
         args = (imgs,)
+    for p in m.parameters():          # no autograd state: FlopCounterMode's module tracker
+        p.requires_grad_(False)       # hooks every grad-requiring input otherwise
     with torch.no_grad(), FlopCounterMode(display=False) as fc:
         m(*args)
     per_op = {str(k): v for k, v in fc.get_flop_counts().get("Global", {}).items()}

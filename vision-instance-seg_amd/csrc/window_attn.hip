@@ -292,14 +292,20 @@ __global__ void __launch_bounds__(256) win_attn_bwd_kernel(
 // registers.  Backward: win_attn_bwd_fa below (two phases, any N <= 160).
 
 constexpr int kMaxT2 = 225;       // (2*8-1)^2
+constexpr int kZoneSmall = 7 * 16 + 1;   // bias_zone for ws <= 8
 constexpr int kPadK = 72;         // LDS row pitch (shorts) of the 64-token operands
 
-// Token metadata of the window: tok[t] = kk | region << 16 with kk = ty (2ws-1) + tx, so
+// Token metadata of the window: tok[t] = kk << 16 | region with kk = ty (2ws-1) + tx, so
 // the relative-position index of a (query, key) pair is kk_q - kk_k + (ws-1) 2ws
 // (HF:swin:350-365: (ty_q - ty_k + ws-1)(2ws-1) + tx_q - tx_k + ws-1) -- one subtract per
 // logit, no integer multiply.  Region ids as HF:swin:584-607 (padded-grid position).
+// A padded token (t >= N) gets kk = rel_c0 - T2: every pair it forms with a real token
+// then indexes one of the two -inf zones staged around the bias table (stage_bias), so
+// padded keys drop out of the softmax with no per-logit test.
+__device__ __forceinline__ int rel_c0(const WinGeom& g) { return (g.ws - 1) * 2 * g.ws; }
+
 __device__ __forceinline__ int token_meta(const WinGeom& g, int bw, int t) {
-  if (t >= g.N) return 0;
+  if (t >= g.N) return (int)((unsigned)(rel_c0(g) - g.T2) << 16);
   const int ws = g.ws;
   const int wl = bw % (g.nWh * g.nWw);
   const int wy = wl / g.nWw, wx = wl % g.nWw;
@@ -307,23 +313,44 @@ __device__ __forceinline__ int token_meta(const WinGeom& g, int bw, int t) {
   const int reg = g.shift > 0 ? region_of(wy * ws + ty, g.nWh * ws, ws, g.shift) * 3 +
                                     region_of(wx * ws + tx, g.nWw * ws, ws, g.shift)
                               : 0;
-  return (ty * (2 * ws - 1) + tx) | (reg << 16);
+  return (int)((unsigned)(ty * (2 * ws - 1) + tx) << 16) | reg;
+}
+
+// Only windows of the last window row / column of a shifted block mix regions (the roll
+// wraps there); every other window skips the mask with a uniform branch.
+__device__ __forceinline__ bool window_mixed(const WinGeom& g, int bw) {
+  const int wl = bw % (g.nWh * g.nWw);
+  return g.shift > 0 && (wl / g.nWw == g.nWh - 1 || wl % g.nWw == g.nWw - 1);
 }
 
 __device__ __forceinline__ void window_tokens(const WinGeom& g, int bw, int lane, int* tok) {
   tok[lane] = token_meta(g, bw, lane);
 }
 
-__device__ __forceinline__ int rel_c0(const WinGeom& g) { return (g.ws - 1) * 2 * g.ws; }
+// Logits in log2 units (softmax through exp2): S2 = (q.k) scale log2e + table log2e
+// (+ mask -100 log2e).  The staged bias is [zone | table column | zone], zone = rel_c0 + 1
+// entries of -inf (the reach of a padded token's kk); `bias` points at the table.
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kMaskLog2 = -100.f * kLog2e;
 
-// Scaled logits + bias + shift mask of an S^T tile (rows = keys 32 kt + crow(i, hh) in the
-// registers, column = query q on the lane); keys >= N -> -inf.  rel[i] receives each
+__device__ __forceinline__ int bias_zone(const WinGeom& g) { return rel_c0(g) + 1; }
+
+__device__ __forceinline__ float* stage_bias(float* sb, const float* table, const WinGeom& g, int h, int tid,
+                                             int nthr) {
+  const int z = bias_zone(g), n = g.T2 + 2 * z;
+  for (int t = tid; t < n; t += nthr) {
+    const int k = t - z;
+    sb[t] = (k >= 0 && k < g.T2) ? table[k * g.heads + h] * kLog2e : -INFINITY;
+  }
+  return sb + z;
+}
+
+// Scaled logits + bias of an S^T tile (rows = keys 32 kt + crow(i, hh) in the registers,
+// column = query q on the lane), padded keys -inf through the zones.  rel[i] receives each
 // logit's bias index (the backward bins dS with it).  tok must be 16-B aligned.
-__device__ __forceinline__ void logits_kq(f32x16_t& s, const WinGeom& g, const int* tok, const float* bias, int kt,
-                                          int q, int hh, int* rel) {
-  const int tq = tok[q];
-  const int qo = (tq & 0xffff) + rel_c0(g), rq = tq >> 16;
-  const bool sh = g.shift > 0, tail = 32 * kt + 32 > g.N;
+__device__ __forceinline__ void logits_kq(f32x16_t& s, const WinGeom& g, float scale2, const int* tok,
+                                          const float* bias, int kt, int q, int hh, int* rel) {
+  const int qo = (tok[q] >> 16) + rel_c0(g);
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
     const int kb = 32 * kt + 8 * g4 + 4 * hh;
@@ -332,45 +359,60 @@ __device__ __forceinline__ void logits_kq(f32x16_t& s, const WinGeom& g, const i
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int i = 4 * g4 + e;
-      const int rl = qo - (tk[e] & 0xffff);
+      const int rl = qo - (tk[e] >> 16);
       rel[i] = rl;
-      float v = s[i] * g.scale + bias[rl];
-      if (sh && (tk[e] >> 16) != rq) v += -100.f;
-      if (tail && kb + e >= g.N) v = -INFINITY;
-      s[i] = v;
+      s[i] = fmaf(s[i], scale2, bias[rl]);
     }
   }
 }
 
-__device__ __forceinline__ void logits_tile(f32x16_t& s, const WinGeom& g, const int* tok, const float* bias, int kt,
-                                            int qt, int r, int hh) {
+// the shift mask of the same tile (mixed windows only)
+__device__ __forceinline__ void mask_kq(f32x16_t& s, const int* tok, int kt, int q, int hh) {
+  const int rq = tok[q] & 0xffff;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int4 t4 = *reinterpret_cast<const int4*>(tok + 32 * kt + 8 * g4 + 4 * hh);
+    const int tk[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if ((tk[e] & 0xffff) != rq) s[4 * g4 + e] += kMaskLog2;
+  }
+}
+
+__device__ __forceinline__ void logits_tile(f32x16_t& s, const WinGeom& g, float scale2, bool mixed, const int* tok,
+                                            const float* bias, int kt, int qt, int r, int hh) {
   int rel[16];
-  logits_kq(s, g, tok, bias, kt, 32 * qt + r, hh, rel);
+  logits_kq(s, g, scale2, tok, bias, kt, 32 * qt + r, hh, rel);
+  if (mixed) mask_kq(s, tok, kt, 32 * qt + r, hh);
 }
 
 // The same logits for an S tile (rows = queries 32 qt + crow(i, hh), column = key on the
-// lane): identical values to logits_kq for every (query, key) pair; key >= N or
-// query >= N -> -inf.
-__device__ __forceinline__ void logits_qk(f32x16_t& s, const WinGeom& g, const int* tok, const float* bias, int qt,
-                                          int key, int hh) {
+// lane): identical values to logits_kq for every (query, key) pair; a padded query row or
+// padded key column is -inf through the zones.
+__device__ __forceinline__ void logits_qk(f32x16_t& s, const WinGeom& g, float scale2, bool mixed, const int* tok,
+                                          const float* bias, int qt, int key, int hh) {
   const int tk = tok[key];
-  const int ko = (tk & 0xffff) - rel_c0(g), rk = tk >> 16;
-  const bool sh = g.shift > 0, tail = 32 * qt + 32 > g.N, kin = key < g.N;
+  const int ko = (tk >> 16) - rel_c0(g), rk = tk & 0xffff;
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
-    const int qb = 32 * qt + 8 * g4 + 4 * hh;
-    const int4 t4 = *reinterpret_cast<const int4*>(tok + qb);
+    const int4 t4 = *reinterpret_cast<const int4*>(tok + 32 * qt + 8 * g4 + 4 * hh);
     const int tq[4] = {t4.x, t4.y, t4.z, t4.w};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int i = 4 * g4 + e;
-      float v = s[i] * g.scale + bias[(tq[e] & 0xffff) - ko];
-      if (sh && (tq[e] >> 16) != rk) v += -100.f;
-      if (!kin || (tail && qb + e >= g.N)) v = -INFINITY;
-      s[i] = v;
+    for (int e = 0; e < 4; ++e) s[4 * g4 + e] = fmaf(s[4 * g4 + e], scale2, bias[(tq[e] >> 16) - ko]);
+  }
+  if (mixed) {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int4 t4 = *reinterpret_cast<const int4*>(tok + 32 * qt + 8 * g4 + 4 * hh);
+      const int tq[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if ((tq[e] & 0xffff) != rk) s[4 * g4 + e] += kMaskLog2;
     }
   }
 }
+
+__device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
 
 constexpr int kFwdWaves = 4;
 
@@ -379,7 +421,7 @@ __global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* 
                                                                     bf16* __restrict__ out, float* __restrict__ lse,
                                                                     WinGeom g, int items) {
   __shared__ __attribute__((aligned(16))) short sVt[kFwdWaves][32 * kPadK];   // V^T [d][key]
-  __shared__ float sBias[kFwdWaves][kMaxT2];
+  __shared__ float sBias[kFwdWaves][kMaxT2 + 2 * kZoneSmall];
   __shared__ __attribute__((aligned(16))) int sTok[kFwdWaves][64];
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int item = blockIdx.x * kFwdWaves + wave;
@@ -388,10 +430,11 @@ __global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* 
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
   const bf16* win = qkv + (size_t)bw * N * C3;
   short* vt = sVt[wave];
-  float* bias = sBias[wave];
   int* tok = sTok[wave];
   window_tokens(g, bw, l, tok);
-  for (int t = l; t < g.T2; t += 64) bias[t] = table[t * g.heads + h];
+  const float* bias = stage_bias(sBias[wave], table, g, h, l, 64);
+  const bool mixed = window_mixed(g, bw);
+  const float scale2 = g.scale * kLog2e;
   {  // V^T: lane = key
     const int key = l;
 #pragma unroll
@@ -430,8 +473,8 @@ __global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* 
   float inv[2], lq[2];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    logits_tile(acc[0][qt], g, tok, bias, 0, qt, r, hh);
-    logits_tile(acc[1][qt], g, tok, bias, 1, qt, r, hh);
+    logits_tile(acc[0][qt], g, scale2, mixed, tok, bias, 0, qt, r, hh);
+    logits_tile(acc[1][qt], g, scale2, mixed, tok, bias, 1, qt, r, hh);
     float m = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) m = fmaxf(m, fmaxf(acc[0][qt][i], acc[1][qt][i]));
@@ -439,13 +482,13 @@ __global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* 
     float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      acc[0][qt][i] = __expf(acc[0][qt][i] - m);
-      acc[1][qt][i] = __expf(acc[1][qt][i] - m);
+      acc[0][qt][i] = exp2_fast(acc[0][qt][i] - m);
+      acc[1][qt][i] = exp2_fast(acc[1][qt][i] - m);
       sum += acc[0][qt][i] + acc[1][qt][i];
     }
     sum += __shfl_xor(sum, 32, 64);
     inv[qt] = 1.f / sum;
-    lq[qt] = m + __logf(sum);
+    lq[qt] = (m + __log2f(sum)) * (1.f / kLog2e);
   }
   // O^T = V^T P^T
   f32x16_t o[2];
@@ -489,6 +532,7 @@ __global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* 
 // wave w computes dV of key tile w over all queries; the tile is then overwritten with
 // dS^T for dK of key tile w; dQ^T of the wave's queries comes from registers as above.
 constexpr int kMaxT2Big = 529;    // (2*12-1)^2
+constexpr int kZoneBig = 11 * 24 + 1;    // bias_zone for ws <= 12
 
 // ---- fp8 (OCP e4m3, gfx950) window attention, config C5 ------------------------------
 // F8 = true runs the forward's logits S^T = K Q^T and O^T = V^T P^T on the BLOCK-SCALED MX
@@ -676,7 +720,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   constexpr int NP = 32 * NT, PT = NP + 8, PK = 40;
   __shared__ __attribute__((aligned(16))) short sK[NP * PK];   // K [key][d]
   __shared__ __attribute__((aligned(16))) short sVt[32 * PT];  // V^T [d][key]
-  __shared__ float sBias[kMaxT2Big];
+  __shared__ float sBias[kMaxT2Big + 2 * kZoneBig];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
   const int bw = blockIdx.x, h = blockIdx.y;
   const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
@@ -698,7 +742,9 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   for (int st = 0; st < 2; ++st)
     qb[st] = qrow < N ? ld8(win + (size_t)qrow * C3 + h * kD + 16 * st + 8 * hh) : zero8();
   window_tokens_blk<NT>(g, bw, sTok);
-  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
+  const float* bias = stage_bias(sBias, table, g, h, threadIdx.x, blockDim.x);
+  const bool mixed = window_mixed(g, bw);
+  const float scale2 = g.scale * kLog2e;
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
@@ -722,7 +768,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
-    logits_tile(acc[kt], gl, sTok, sBias, kt, qt, r, hh);
+    logits_tile(acc[kt], gl, scale2, mixed, sTok, bias, kt, qt, r, hh);
 #pragma unroll
     for (int i = 0; i < 16; ++i) m = fmaxf(m, acc[kt][i]);
   }
@@ -732,11 +778,11 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      acc[kt][i] = __expf(acc[kt][i] - m);
+      acc[kt][i] = exp2_fast(acc[kt][i] - m);
       sum += acc[kt][i];
     }
   sum += __shfl_xor(sum, 32, 64);
-  const float lq = m + __logf(sum);
+  const float lq = (m + __log2f(sum)) * (1.f / kLog2e);
   const float inv = 1.f / sum;
   // O^T = V^T P^T
   f32x16_t o;
@@ -769,14 +815,14 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
 // bytes of the bf16 staging) and only quantises its own query and its P tiles (per
 // (query, 32-key tile) scale, in registers).
 template <int NT>
-__global__ void __launch_bounds__(64 * NT) win_attn_fwd_mx(const bf16* __restrict__ qkv, const float* __restrict__ table,
+__global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : 1) win_attn_fwd_mx(const bf16* __restrict__ qkv, const float* __restrict__ table,
                                                            bf16* __restrict__ out, float* __restrict__ lse, WinGeom g) {
   constexpr int NP = 32 * NT, PK8 = 48, PV8 = NP + 16;      // bytes per K row / V^T row
   __shared__ __attribute__((aligned(16))) unsigned char sK8[NP * PK8];
   __shared__ __attribute__((aligned(16))) unsigned char sV8[32 * PV8];
   __shared__ int sKs[NP];
   __shared__ unsigned sVam[NT];
-  __shared__ float sBias[kMaxT2Big];
+  __shared__ float sBias[kMaxT2Big + 2 * kZoneBig];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
   const int bw = blockIdx.x, h = blockIdx.y;
   const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
@@ -794,7 +840,9 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mx(const bf16* __restric
   i32x8_t qm;
   const int qs = mx_token_gmem(win + (size_t)qrow * C3 + h * kD, hh, qrow < N, qm);
   window_tokens_blk<NT>(g, bw, sTok);
-  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
+  const float* bias = stage_bias(sBias, table, g, h, threadIdx.x, blockDim.x);
+  const bool mixed = window_mixed(g, bw);
+  const float scale2 = g.scale * kLog2e;
   unsigned vam = 0;
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
@@ -835,7 +883,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mx(const bf16* __restric
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
-    logits_tile(acc[kt], g, sTok, sBias, kt, qt, r, hh);
+    logits_tile(acc[kt], g, scale2, mixed, sTok, bias, kt, qt, r, hh);
 #pragma unroll
     for (int i = 0; i < 16; ++i) m = fmaxf(m, acc[kt][i]);
   }
@@ -845,11 +893,11 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mx(const bf16* __restric
   for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      acc[kt][i] = __expf(acc[kt][i] - m);
+      acc[kt][i] = exp2_fast(acc[kt][i] - m);
       sum += acc[kt][i];
     }
   sum += __shfl_xor(sum, 32, 64);
-  const float lq = m + __logf(sum);
+  const float lq = (m + __log2f(sum)) * (1.f / kLog2e);
   const float inv = 1.f / sum;
   // O^T = V^T P^T, 64 keys (tiles 2 b2, 2 b2 + 1) per instruction; lane half hh takes the
   // keys of its accumulator rows crow(., hh): 4 consecutive keys = one V^T dword
@@ -904,7 +952,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mx(const bf16* __restric
 // S and dP are formed twice (the MFMA units idle in this kernel); LDS peaks at ~47 KB for
 // N = 144 (3 workgroups/CU).  F8: the logits on the forward's fp8 operands and scales.
 template <int NT, bool F8>
-__global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
+__global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : 1) win_attn_bwd_fa(
     const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
     const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
     float* __restrict__ gtable_part, WinGeom g) {
@@ -915,7 +963,7 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
   constexpr int kP1 = 2 * kNat + kTr + NT * kBinW * 2;        // K, V, K^T, f32 bins (in shorts)
   constexpr int kP2 = 2 * kNat + 2 * kTr;                     // Q, dO, Q^T, dO^T
   __shared__ __attribute__((aligned(16))) short sU[kP1 > kP2 ? kP1 : kP2];
-  __shared__ float sBias[kMaxT2Big];
+  __shared__ float sBias[kMaxT2Big + 2 * kZoneBig];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
   __shared__ float sL[NP], sD[NP];
   const int bw = blockIdx.x, h = blockIdx.y;
@@ -968,9 +1016,11 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     ob[st] = q < N ? ld8(owin + (size_t)q * C + off) : zero8();
   }
 
-  const float Lq = q < N ? lrow[q] : 0.f;
+  const float Lq = q < N ? lrow[q] * kLog2e : 0.f;      // log2 units
   window_tokens_blk<NT>(g, bw, sTok);
-  for (int t = threadIdx.x; t < g.T2; t += blockDim.x) sBias[t] = table[t * g.heads + h];
+  const float* bias = stage_bias(sBias, table, g, h, threadIdx.x, blockDim.x);
+  const bool mixed = window_mixed(g, bw);
+  const float scale2 = g.scale * kLog2e;
   // ---- phase 1 staging: K, V natural, K^T; D, lse; bins zeroed
   short* sKn = sU;
   short* sVn = sU + kNat;
@@ -1018,10 +1068,11 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
       dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sVn + o), db[st], dp);
     }
     int rel[16];
-    logits_kq(s, gl, sTok, sBias, kt, q, hh, rel);
+    logits_kq(s, gl, scale2, sTok, bias, kt, q, hh, rel);
+    if (mixed) mask_kq(s, sTok, kt, q, hh);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float p = q < N ? __expf(s[i] - Lq) : 0.f;
+      const float p = q < N ? exp2_fast(s[i] - Lq) : 0.f;
       dp[i] = p * (dp[i] - Dq);
     }
     // dQ^T += K^T dS^T
@@ -1032,13 +1083,15 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
     }
     // relative-position bias gradient: for one register the 32 lanes of a half hold one
     // key and 32 queries, i.e. 32 distinct bins, so with the halves taking turns every
-    // update is a plain LDS read-modify-write (ds_add_f32 is slow on gfx950); padded
-    // queries / keys carry dS = 0 (their rel index stays inside the table)
+    // update is a plain LDS read-modify-write (ds_add_f32 is slow on gfx950).  Padded
+    // query lanes index the zone below the table and are masked off; a padded key row
+    // (dS = 0 on every lane: P = exp2(-inf)) indexes the zone above it and is clamped onto
+    // the last bin, where its whole instruction adds zero
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      if (hh == half) {
+      if (hh == half && q < N) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) bins[rel[i]] += dp[i];
+        for (int i = 0; i < 16; ++i) bins[min(rel[i], g.T2 - 1)] += dp[i];
       }
       wave_sync();
     }
@@ -1099,11 +1152,11 @@ __global__ void __launch_bounds__(64 * NT) win_attn_bwd_fa(
       s = mfma16(*reinterpret_cast<const bf16x8_t*>(sQn + o), ks8[st], s);
       dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sDn + o), vb[st], dp);
     }
-    logits_qk(s, gl, sTok, sBias, qq, key, hh);
+    logits_qk(s, gl, scale2, mixed, sTok, bias, qq, key, hh);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qi = 32 * qq + crow(i, hh);
-      const float p = __expf(s[i] - sL[qi]);
+      const float p = exp2_fast(s[i] - sL[qi]);
       s[i] = p;
       dp[i] = p * (dp[i] - sD[qi]);
     }
