@@ -28,5 +28,9 @@ timeout -k 10 300 python3 bench.py --model swin_b --no-cpu-baseline --no-parity 
 timeout -k 10 300 python3 bench.py --arch maskdino --model swin_l --no-cpu-baseline --steps 5 > $O/c4.log 2>&1 || exit $?
 timeout -k 10 300 python3 bench.py --model swin_l --size 1536 --no-cpu-baseline --no-parity --steps 5 > $O/c5_bf16.log 2>&1 || exit $?
 timeout -k 10 300 python3 bench.py --model swin_l --size 1536 --attn-fp8 --no-cpu-baseline --no-parity --steps 5 > $O/c5_fp8.log 2>&1 || exit $?
+# C5 step breakdown (graph-replayed steps under the kernel trace)
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace5 -o b -- python3 bench.py --model swin_l --size 1536 --no-cpu-baseline --no-parity --steps 3 > $O/trace5.log 2>&1 || exit $?
+python tools/step_breakdown.py $O/trace5/b_kernel_trace.csv 60 -3 > $O/step_c5.txt || exit 1
+rm -rf $O/trace5
 du -sh gpurun_out
 echo done
