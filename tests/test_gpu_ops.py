@@ -724,7 +724,8 @@ def test_add_layer_norm_vs_torch(dtype, M, C, use_s):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,N", [(262144, 96), (86016, 256), (5, 384), (0, 64), (1023, 2048)])
+@pytest.mark.parametrize("M,N", [(262144, 96), (86016, 256), (5, 384), (0, 64), (1023, 2048), (4099, 3072),
+                                 (1500, 6144), (77, 2056)])
 def test_column_sum_vs_torch(dtype, M, N):
     ops = _ops()
     x = torch.randn(M, N, generator=torch.Generator().manual_seed(N)).to(dtype)
@@ -1004,7 +1005,8 @@ def test_msda_prep_vs_torch(case, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("kind,N", [("gelu", 384), ("gelu", 96), ("relu", 1024), ("relu", 256)])
+@pytest.mark.parametrize("kind,N", [("gelu", 384), ("gelu", 96), ("relu", 1024), ("relu", 256), ("gelu", 3072),
+                                    ("gelu", 6144), ("relu", 2056)])
 def test_activation_backward_colsum(dtype, kind, N):
     """ops.activation: torch's forward; the HIP backward (vs_act_backward_colsum) vs
     autograd of F.gelu / F.relu (f64), and its recorded column sums as the bias gradient of

@@ -258,13 +258,18 @@ struct RowSegments {
 
 template <typename T>
 __device__ __forceinline__ void colsum_rows(const T* __restrict__ x, float* __restrict__ part, long long M, int N,
-                                            int nblk, int blk, float* red);
+                                            int nblk, int blk, float* red, int c0, int Nb);
+
+// Column blocks: a workgroup covers at most kColBlock columns (one 8-column chunk per
+// thread); wider rows (Swin-L MLP hidden: 3072, 6144) take grid.y = ceil(N / kColBlock).
+constexpr int kColBlock = 8 * kThreads;
 
 template <typename T>
 __global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ x, float* __restrict__ part, int M,
                                                           int N) {
   extern __shared__ float red[];
-  colsum_rows(x, part + (size_t)blockIdx.x * N, M, N, gridDim.x, blockIdx.x, red);
+  const int c0 = blockIdx.y * kColBlock;
+  colsum_rows(x, part + (size_t)blockIdx.x * N, M, N, gridDim.x, blockIdx.x, red, c0, min(kColBlock, N - c0));
 }
 
 // per-segment column sums of x [B, S, N]: grid (nblk, nseg * B); workgroup (x, k*B + b)
@@ -276,15 +281,17 @@ __global__ void __launch_bounds__(kThreads) colsum_seg_kernel(const T* __restric
   const int k = blockIdx.y / B, b = blockIdx.y % B;
   const int r0 = seg.start[k];
   colsum_rows(x + ((size_t)b * S + r0) * N, part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * N,
-              seg.start[k + 1] - r0, N, gridDim.x, blockIdx.x, red);
+              seg.start[k + 1] - r0, N, gridDim.x, blockIdx.x, red, 0, N);
 }
 
-// column sums of rows [0, M) of x [M, N] -> part[N] (f32) for workgroup blk of nblk; a
-// thread owns one 8-column chunk and a subset of rows
+// column sums of rows [0, M) of x [M, N], columns [c0, c0 + Nb) -> part[c0 ..] (f32) for
+// workgroup blk of nblk; a thread owns one 8-column chunk and a subset of rows
 template <typename T>
 __device__ __forceinline__ void colsum_rows(const T* __restrict__ x, float* __restrict__ part, long long M, int N,
-                                            int nblk, int blk, float* red) {   // red: [rowsets][N]
-  const int nch = N >> 3;
+                                            int nblk, int blk, float* red, int c0, int Nb) {   // red: [rowsets][Nb]
+  x += c0;
+  part += c0;
+  const int nch = Nb >> 3;
   const int rowsets = kThreads / nch;        // nch <= 256
   const int ch = threadIdx.x % nch;
   const int rs = threadIdx.x / nch;
@@ -310,12 +317,12 @@ __device__ __forceinline__ void colsum_rows(const T* __restrict__ x, float* __re
         for (int i = 0; i < 8; ++i) acc[i] += v[u][i];
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) red[(size_t)rs * N + ch * 8 + i] = acc[i];
+    for (int i = 0; i < 8; ++i) red[(size_t)rs * Nb + ch * 8 + i] = acc[i];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < N; c += kThreads) {
+  for (int c = threadIdx.x; c < Nb; c += kThreads) {
     float a = 0.f;
-    for (int r = 0; r < rowsets; ++r) a += red[(size_t)r * N + c];
+    for (int r = 0; r < rowsets; ++r) a += red[(size_t)r * Nb + c];
     part[c] = a;
   }
 }
@@ -330,8 +337,13 @@ template <typename T, int ACT>   // ACT 0: ReLU, 1: GELU (erf)
 __global__ void __launch_bounds__(kThreads) act_bwd_colsum_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                   T* __restrict__ dx, float* __restrict__ part, int M,
                                                                   int N) {
-  extern __shared__ float red[];             // [rowsets][N]
-  const int nch = N >> 3;
+  extern __shared__ float red[];             // [rowsets][Nb]
+  const int c0 = blockIdx.y * kColBlock, Nb = min(kColBlock, N - c0);   // this workgroup's columns
+  dy += c0;
+  x += c0;
+  dx += c0;
+  part += c0;
+  const int nch = Nb >> 3;
   const int rowsets = kThreads / nch;
   const int ch = threadIdx.x % nch;
   const int rs = threadIdx.x / nch;
@@ -373,12 +385,12 @@ __global__ void __launch_bounds__(kThreads) act_bwd_colsum_kernel(const T* __res
       }
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) red[(size_t)rs * N + ch * 8 + i] = acc[i];
+    for (int i = 0; i < 8; ++i) red[(size_t)rs * Nb + ch * 8 + i] = acc[i];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < N; c += kThreads) {
+  for (int c = threadIdx.x; c < Nb; c += kThreads) {
     float a = 0.f;
-    for (int r = 0; r < rowsets; ++r) a += red[(size_t)r * N + c];
+    for (int r = 0; r < rowsets; ++r) a += red[(size_t)r * Nb + c];
     part[(size_t)blockIdx.x * N + c] = a;
   }
 }
@@ -680,19 +692,20 @@ extern "C" long long vs_column_sum_workspace_bytes(int M, int N) {
 
 extern "C" int vs_column_sum(int dtype, const void* x, void* out, void* ws, int M, int N, void* stream) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
-  VS_CHECK(M >= 0 && N > 0 && N % 8 == 0 && N / 8 <= kThreads, "N must be a multiple of 8, <= 2048");
+  VS_CHECK(M >= 0 && N > 0 && N % 8 == 0 && N <= 8 * kColBlock, "N must be a multiple of 8, <= 16384");
   VS_CHECK(out && ws && (M == 0 || x), "null pointer");
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
-  const int rowsets = kThreads / (N / 8);
+  const int Nb = std::min(N, kColBlock), rowsets = kThreads / (Nb / 8);
   const int grid = blocks_for(M, rowsets * 16, kMaxPartials);
-  const size_t lds = (size_t)rowsets * N * sizeof(float);
+  const dim3 g2(grid, (N + kColBlock - 1) / kColBlock);
+  const size_t lds = (size_t)rowsets * Nb * sizeof(float);   // >= every column block's rowsets x Nb
   if (dtype == VS_BF16) {
-    hipLaunchKernelGGL(colsum_kernel<bf16>, dim3(grid), dim3(kThreads), lds, st, (const bf16*)x, part, M, N);
+    hipLaunchKernelGGL(colsum_kernel<bf16>, g2, dim3(kThreads), lds, st, (const bf16*)x, part, M, N);
     hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part, (bf16*)out,
                        (bf16*)nullptr, grid, N, N);
   } else {
-    hipLaunchKernelGGL(colsum_kernel<float>, dim3(grid), dim3(kThreads), lds, st, (const float*)x, part, M, N);
+    hipLaunchKernelGGL(colsum_kernel<float>, g2, dim3(kThreads), lds, st, (const float*)x, part, M, N);
     hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part,
                        (float*)out, (float*)nullptr, grid, N, N);
   }
@@ -777,15 +790,16 @@ extern "C" int vs_act_backward_colsum(int dtype, int act, const void* dy, const 
                                       void* ws, int M, int N, void* stream) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(act == 0 || act == 1, "act must be 0 (ReLU) or 1 (GELU)");
-  VS_CHECK(M >= 0 && N > 0 && N % 8 == 0 && N / 8 <= kThreads, "N must be a multiple of 8, <= 2048");
+  VS_CHECK(M >= 0 && N > 0 && N % 8 == 0 && N <= 8 * kColBlock, "N must be a multiple of 8, <= 16384");
   VS_CHECK(dx_colsum && ws && (M == 0 || (dy && x && dx)), "null pointer");
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
-  const int rowsets = kThreads / (N / 8);
+  const int Nb = std::min(N, kColBlock), rowsets = kThreads / (Nb / 8);
   const int grid = blocks_for(M, rowsets * 16, kMaxPartials);
-  const size_t lds = (size_t)rowsets * N * sizeof(float);
+  const dim3 g2(grid, (N + kColBlock - 1) / kColBlock);
+  const size_t lds = (size_t)rowsets * Nb * sizeof(float);
 #define VS_ACTB(TT, A)                                                                                          \
-  hipLaunchKernelGGL((act_bwd_colsum_kernel<TT, A>), dim3(grid), dim3(kThreads), lds, st, (const TT*)dy,        \
+  hipLaunchKernelGGL((act_bwd_colsum_kernel<TT, A>), g2, dim3(kThreads), lds, st, (const TT*)dy,                \
                      (const TT*)x, (TT*)dx, part, M, N)
   if (dtype == VS_BF16) {
     if (act) VS_ACTB(bf16, 1); else VS_ACTB(bf16, 0);

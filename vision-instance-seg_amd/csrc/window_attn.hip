@@ -416,7 +416,7 @@ __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_ex
 
 constexpr int kFwdWaves = 4;
 
-__global__ void __launch_bounds__(64 * kFwdWaves) win_attn_fwd_mfma(const bf16* __restrict__ qkv,
+__global__ void __launch_bounds__(64 * kFwdWaves, 3) win_attn_fwd_mfma(const bf16* __restrict__ qkv,
                                                                     const float* __restrict__ table,
                                                                     bf16* __restrict__ out, float* __restrict__ lse,
                                                                     WinGeom g, int items) {
@@ -809,13 +809,109 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   }
 }
 
+// The same forward with an ONLINE softmax: a wave walks its key tiles keeping one S^T tile,
+// the running max / sum and the O^T accumulator live (rescaled by exp2(m_old - m_new) per
+// tile): 80 VGPRs instead of 120 (NT x 16 accumulators).  The kernel is latency-bound (SQ
+// counters at C5, profiles/r3_win_pmc.txt: waves parked at waitcnt / barrier ~45-50 % of
+// their cycles with 3 workgroups per CU), so the registers buy resident workgroups: 4 per
+// CU at NT = 5 (6 waves / SIMD) instead of 3.  The tile loop stays rolled: unrolled, the
+// scheduler hoists every tile's QK^T MFMAs and all S^T tiles are live again.
+template <int NT>
+__global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(6))) win_attn_fwd_online(const bf16* __restrict__ qkv,
+                                                                   const float* __restrict__ table,
+                                                                   bf16* __restrict__ out, float* __restrict__ lse,
+                                                                   WinGeom g) {
+  constexpr int NP = 32 * NT, PT = NP + 8, PK = 40;
+  __shared__ __attribute__((aligned(16))) short sK[NP * PK];   // K [key][d]
+  __shared__ __attribute__((aligned(16))) short sVt[32 * PT];  // V^T [d][key]
+  __shared__ float sBias[kMaxT2Big + 2 * kZoneBig];
+  __shared__ __attribute__((aligned(16))) int sTok[NP];
+  const int bw = blockIdx.x, h = blockIdx.y;
+  const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int N = g.N, C = g.heads * kD, C3 = 3 * C;
+  const bf16* win = qkv + (size_t)bw * N * C3;
+  bf16x8_t qb[2];
+  {
+    bf16x8_t ck[2], cv[2];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+      const bf16* row = win + (size_t)t * C3 + h * kD + 8 * c;
+      ck[it] = t < N ? ld8(row + C) : zero8();
+      cv[it] = t < N ? ld8(row + 2 * C) : zero8();
+    }
+    const int qrow = 32 * qt + r;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+      qb[st] = qrow < N ? ld8(win + (size_t)qrow * C3 + h * kD + 16 * st + 8 * hh) : zero8();
+    window_tokens_blk<NT>(g, bw, sTok);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+      *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = ck[it];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sVt[(8 * c + j) * PT + t] = cv[it][j];
+    }
+  }
+  const float* bias = stage_bias(sBias, table, g, h, threadIdx.x, blockDim.x);
+  const bool mixed = window_mixed(g, bw);
+  const float scale2 = g.scale * kLog2e;
+  __syncthreads();
+  float m = -INFINITY, sum = 0.f;
+  f32x16_t o;
+  zero16(o);
+#pragma unroll 1
+  for (int kt = 0; kt < NT; ++kt) {            // not unrolled: the scheduler would hoist every
+    f32x16_t s;                                // tile's QK^T MFMAs and keep all S^T tiles live
+    zero16(s);
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+      s = mfma16(*reinterpret_cast<const bf16x8_t*>(sK + (32 * kt + r) * PK + 16 * st + 8 * hh), qb[st], s);
+    logits_tile(s, g, scale2, mixed, sTok, bias, kt, qt, r, hh);
+    float tm = s[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) tm = fmaxf(tm, s[i]);
+    tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+    const float mn = fmaxf(m, tm);            // finite: every tile of a real query holds a real key
+    if (kt > 0) {                             // (tile 0 always does; padded query lanes are never stored)
+      const float alpha = exp2_fast(m - mn);
+      sum *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[i] *= alpha;
+    }
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s[i] = exp2_fast(s[i] - mn);
+      sum += s[i];
+    }
+#pragma unroll
+    for (int th = 0; th < 2; ++th)
+      o = mfma16(ld_perm(sVt + r * PT, 32 * kt + 16 * th + 4 * hh), pack8(s, 8 * th), o);
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  const int q = 32 * qt + r;
+  if (q < N) {
+    const float inv = 1.f / sum;
+    bf16* dst = out + ((size_t)bw * N + q) * C + h * kD;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      bf16x4_t v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[4 * grp + e] * inv);
+      *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+    }
+    if (hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = (m + __log2f(sum)) * (1.f / kLog2e);
+  }
+}
+
 // fp8 forward (C5): K and V are quantised ONCE per workgroup while staged -- K per token
 // (e4m3 rows + a scale byte each), V with one power-of-two scale for the (window, head),
 // stored transposed as bytes -- so every wave reads ready MX operands from LDS (half the
 // bytes of the bf16 staging) and only quantises its own query and its P tiles (per
 // (query, 32-key tile) scale, in registers).
-template <int NT>
-__global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : 1) win_attn_fwd_mx(const bf16* __restrict__ qkv, const float* __restrict__ table,
+template <int NT, bool ONLINE>
+__global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(ONLINE ? 5 : NT == 5 ? 4 : 1))) win_attn_fwd_mx(const bf16* __restrict__ qkv, const float* __restrict__ table,
                                                            bf16* __restrict__ out, float* __restrict__ lse, WinGeom g) {
   constexpr int NP = 32 * NT, PK8 = 48, PV8 = NP + 16;      // bytes per K row / V^T row
   __shared__ __attribute__((aligned(16))) unsigned char sK8[NP * PK8];
@@ -870,6 +966,81 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : 1) win_attn_fwd_mx(cons
     for (int j = 0; j < 8; ++j) sV8[(8 * c + j) * PV8 + t] = (unsigned char)(((j < 4 ? w0 : w1) >> (8 * (j & 3))) & 0xff);
   }
   __syncthreads();
+  if constexpr (ONLINE) {
+    // online softmax over key-tile PAIRS (one MX P V instruction each): two S^T tiles, the
+    // running max / sum and O^T live (see win_attn_fwd_online)
+    float m = -INFINITY, sum = 0.f;
+    f32x16_t o;
+    zero16(o);
+    const int vsb = 127 - kv;
+#pragma unroll 1
+    for (int b2 = 0; b2 < (NT + 1) / 2; ++b2) {
+      const int k0 = 2 * b2, k1 = 2 * b2 + 1;
+      const bool has1 = k1 < NT;
+      f32x16_t s0, s1;
+      zero16(s0);
+      zero16(s1);
+      {
+        i32x8_t km;
+        const int key = 32 * k0 + r;
+        const int ks = mx_token_lds8(sK8 + key * PK8, sKs[key], hh, km);
+        s0 = mfma_mx(km, ks, qm, qs, s0);
+      }
+      logits_tile(s0, g, scale2, mixed, sTok, bias, k0, qt, r, hh);
+      if (has1) {
+        i32x8_t km;
+        const int key = 32 * k1 + r;
+        const int ks = mx_token_lds8(sK8 + key * PK8, sKs[key], hh, km);
+        s1 = mfma_mx(km, ks, qm, qs, s1);
+        logits_tile(s1, g, scale2, mixed, sTok, bias, k1, qt, r, hh);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s1[i] = -INFINITY;
+      }
+      float tm = fmaxf(s0[0], s1[0]);
+#pragma unroll
+      for (int i = 1; i < 16; ++i) tm = fmaxf(tm, fmaxf(s0[i], s1[i]));
+      tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+      const float mn = fmaxf(m, tm);
+      if (b2 > 0) {
+        const float alpha = exp2_fast(m - mn);
+        sum *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[i] *= alpha;
+      }
+      m = mn;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s0[i] = exp2_fast(s0[i] - mn);
+        s1[i] = exp2_fast(s1[i] - mn);
+        sum += s0[i] + s1[i];
+      }
+      i32x8_t vm, pm;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          vm[4 * u + g4] = (u == 0 || has1)
+                               ? *reinterpret_cast<const int*>(sV8 + r * PV8 + 32 * (u ? k1 : k0) + 8 * g4 + 4 * hh)
+                               : 0;
+      mx_pfixed([&](int j) { return j < 16 ? s0[j] : s1[j - 16]; }, pm);
+      o = mfma_mx(vm, vsb, pm, kPScaleByte, o);
+    }
+    sum += __shfl_xor(sum, 32, 64);
+    if (qrow < N) {
+      const float inv = 1.f / sum;
+      bf16* dst = out + ((size_t)bw * N + qrow) * C + h * kD;
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        bf16x4_t v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[4 * grp + e] * inv);
+        *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+      }
+      if (hh == 0) lse[((size_t)bw * g.heads + h) * N + qrow] = (m + __log2f(sum)) * (1.f / kLog2e);
+    }
+    return;
+  }
   // S^T = K Q^T: the staged key rows straight into the MX MFMA
   f32x16_t acc[NT];
 #pragma unroll
@@ -952,7 +1123,7 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : 1) win_attn_fwd_mx(cons
 // S and dP are formed twice (the MFMA units idle in this kernel); LDS peaks at ~47 KB for
 // N = 144 (3 workgroups/CU).  F8: the logits on the forward's fp8 operands and scales.
 template <int NT, bool F8>
-__global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : 1) win_attn_bwd_fa(
+__global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_attn_bwd_fa(
     const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
     const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
     float* __restrict__ gtable_part, WinGeom g) {
@@ -1208,6 +1379,15 @@ static bool fwd_blk_small() {
   return e && atoi(e) != 0;
 }
 
+// VS_WIN_FWD_ONLINE=0: the two-pass forward (all NT S^T tiles live) instead of the online one (A/B)
+static bool fwd_online() {
+  static const int v = [] {
+    const char* e = getenv("VS_WIN_FWD_ONLINE");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
 #define VS_NT_SWITCH(nt, M)            \
   switch (nt) {                        \
     case 1: case 2: M(2); break;       \
@@ -1220,8 +1400,14 @@ template <bool F8>
 static void launch_fwd_blk(const WinGeom& g, dim3 grid, hipStream_t st, const void* qkv, const float* table,
                            void* out, float* lse) {
 #define VS_FWD_BLK(NT_)                                                                                     \
-  if (F8)                                                                                                   \
-    hipLaunchKernelGGL((win_attn_fwd_mx<NT_>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,         \
+  if (F8 && fwd_online())                                                                                   \
+    hipLaunchKernelGGL((win_attn_fwd_mx<NT_, true>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,   \
+                       (bf16*)out, lse, g);                                                                 \
+  else if (F8)                                                                                              \
+    hipLaunchKernelGGL((win_attn_fwd_mx<NT_, false>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,  \
+                       (bf16*)out, lse, g);                                                                 \
+  else if (fwd_online())                                                                                    \
+    hipLaunchKernelGGL((win_attn_fwd_online<NT_>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,     \
                        (bf16*)out, lse, g);                                                                 \
   else                                                                                                      \
     hipLaunchKernelGGL((win_attn_fwd_mfma_big<NT_, false>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv,   \

@@ -106,7 +106,7 @@ class _LinearFn(torch.autograd.Function):
             cs = ops.take_colsum(gy)
             if cs is not None:                                     # from the LayerNorm backward's pass
                 gb = cs.to(weight.dtype)
-            elif gy2.shape[1] % 8 == 0 and gy2.shape[1] <= 2048:
+            elif gy2.shape[1] % 8 == 0 and gy2.shape[1] <= ops.COLSUM_MAX_N:
                 gb = ops.column_sum(gy2).to(weight.dtype)          # HIP column sum, f32 accumulation
             else:
                 gb = gy2.sum(0, dtype=torch.float32).to(weight.dtype)
@@ -149,7 +149,7 @@ class _PlaneProjectionFn(torch.autograd.Function):
             gw = _plane_weight_grad(gp, y3.to(gp.dtype), weight.dtype).view_as(weight)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             g2 = gp.view(-1, Co)
-            gb = (ops.column_sum(g2) if Co % 8 == 0 and Co <= 2048 else g2.sum(0, dtype=torch.float32))
+            gb = (ops.column_sum(g2) if Co % 8 == 0 and Co <= ops.COLSUM_MAX_N else g2.sum(0, dtype=torch.float32))
             gb = gb.to(weight.dtype)
         return gy, gw, gb
 
@@ -323,7 +323,7 @@ class _ValueQueryProjFn(torch.autograd.Function):
         gwp = weight_grad(gp2, q2.to(gp2.dtype), wp.dtype)
 
         def bias_grad(g2, dt):
-            if g2.shape[1] % 8 == 0 and g2.shape[1] <= 2048:
+            if g2.shape[1] % 8 == 0 and g2.shape[1] <= ops.COLSUM_MAX_N:
                 return ops.column_sum(g2).to(dt)
             return g2.sum(0, dtype=torch.float32).to(dt)
 
@@ -471,7 +471,7 @@ def linear_relu_tokens(x, w, b, sink=None):
     N = w.shape[0]
     if (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and b is not None and tokens >= MIN_TOKENS
             and not torch.is_autocast_enabled() and x.dtype == w.dtype == b.dtype
-            and x.dtype in (torch.float32, torch.bfloat16) and N % 8 == 0 and N <= 2048 and x.is_contiguous()):
+            and x.dtype in (torch.float32, torch.bfloat16) and N % 8 == 0 and N <= ops.COLSUM_MAX_N and x.is_contiguous()):
         return _LinearReluFn.apply(x, w, b, sink)
     return ops.activation(linear_tokens(x, w, b, sink), "relu")
 

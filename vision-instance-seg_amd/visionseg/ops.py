@@ -672,6 +672,11 @@ def layer_norm_supported(x, weight) -> bool:
             and C % 8 == 0 and C <= 2048)
 
 
+# widest row of the column-sum / activation-backward kernels (column blocks of 2048 on
+# grid.y, csrc/norm.hip kColBlock): covers the Swin-L MLP hidden widths 3072 / 6144
+COLSUM_MAX_N = 16384
+
+
 def column_sum(x2d, out=None):
     """x [M, N] -> [N] (x's dtype, f32 accumulation): the bias gradient of a token-major
     Linear (csrc/norm.hip).  `out`: a contiguous [N] tensor of x's dtype to write into."""
@@ -771,7 +776,7 @@ def activation(x, kind: str):
     _ActColsumFunction) on contiguous f32 / bf16 device tensors with N % 8 == 0."""
     act = {"relu": 0, "gelu": 1}[kind]
     N = x.shape[-1]
-    if (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and N % 8 == 0 and N <= 2048
+    if (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and N % 8 == 0 and N <= COLSUM_MAX_N
             and x.is_contiguous() and torch.is_grad_enabled() and x.requires_grad and not torch.is_autocast_enabled()):
         return _ActColsumFunction.apply(x, act)
     return F.gelu(x) if act == 1 else F.relu(x)
