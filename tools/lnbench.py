@@ -23,7 +23,7 @@ def main():
         gy = torch.randn(M, C, device=DEV, generator=g).to(bf)
         gs = torch.randn(M, C, device=DEV, generator=g).to(bf)
         s, y = ops.add_layer_norm(x, r, w, b)
-        for parts in (256, 512, 1024, 2048):
+        for parts in [int(v) for v in os.environ.get("LNB_PARTS", "256,512,1024,2048").split(",")]:
             os.environ["VS_LN_BWD_PARTS"] = str(parts)
             for _ in range(3):
                 torch.autograd.backward([y, s], [gy, gs], retain_graph=True)

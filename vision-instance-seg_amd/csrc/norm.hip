@@ -45,6 +45,35 @@ __device__ __forceinline__ void store_chunk(T* p, const float* v) {
   if constexpr (Vec16<T>::N == 4) Vec16<T>::store(p + 4, v + 4);
 }
 
+// A chunk as loaded (16 B of bf16 / 32 B of f32), unpacked to f32 only where it is used:
+// a row's operands stay in flight in half the registers for bf16.
+template <typename T> struct RawChunk;
+template <> struct RawChunk<bf16> {
+  uint4 a;
+  __device__ __forceinline__ void load(const bf16* p) { a = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void zero() { a = make_uint4(0u, 0u, 0u, 0u); }
+  __device__ __forceinline__ void unpack(float* out) const {
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      out[2 * i] = __uint_as_float(w[i] << 16);
+      out[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+};
+template <> struct RawChunk<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const float4*>(p);
+    b = *reinterpret_cast<const float4*>(p + 4);
+  }
+  __device__ __forceinline__ void zero() { a = b = make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ __forceinline__ void unpack(float* out) const {
+    out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+    out[4] = b.x; out[5] = b.y; out[6] = b.z; out[7] = b.w;
+  }
+};
+
 // chunk = 8 elements (one 16-B load for bf16, two for f32); C % 8 == 0
 // RES: y = LN(s) with s = x + r rounded to T (the residual add of a pre-/post-norm block,
 // written to s_out): one pass instead of an add kernel plus a LayerNorm.
@@ -145,11 +174,14 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
     }
     if (j < nch) load_chunk(w + j * 8, wv[k]);
   }
-  // U rows per iteration, all loads issued before the math (memory-level parallelism)
+  // U rows per iteration, every load of them (x, dy and the residual gradient) issued before
+  // the math and held packed (memory-level parallelism: the residual gradient used to be a
+  // second round trip, loaded only when its row was stored)
   constexpr int U = K <= 2 ? 2 : 1;
   const long long stride = (long long)gridDim.x * rows_per_block;
   for (long long row0 = (long long)blockIdx.x * rows_per_block + grp; row0 < M; row0 += U * stride) {
-    float xv[U][K][8], dv[U][K][8], mu[U], rs[U];
+    RawChunk<T> xr[U][K], dr[U][K], rr[ADD ? U : 1][ADD ? K : 1];
+    float mu[U], rs[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long row = row0 + u * stride;
@@ -160,30 +192,35 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
       for (int k = 0; k < K; ++k) {
         const int j = lane + k * G;
         if (ok && j < nch) {
-          load_chunk(x + row * C + j * 8, xv[u][k]);
-          load_chunk(dy + row * C + j * 8, dv[u][k]);
+          xr[u][k].load(x + row * C + j * 8);
+          dr[u][k].load(dy + row * C + j * 8);
+          if constexpr (ADD) rr[u][k].load(dres + row * C + j * 8);
         } else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) xv[u][k][i] = dv[u][k][i] = 0.f;
+          xr[u][k].zero();
+          dr[u][k].zero();
+          if constexpr (ADD) rr[u][k].zero();
         }
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long row = row0 + u * stride;
+      float xv[K][8], dv[K][8];
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
+        xr[u][k].unpack(xv[k]);
+        dr[u][k].unpack(dv[k]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const float xh = (xv[u][k][i] - mu[u]) * rs[u];   // masked chunks / rows have dv = 0: no effect
-          const float g = dv[u][k][i] * wv[k][i];
+          const float xh = (xv[k][i] - mu[u]) * rs[u];   // masked chunks / rows have dv = 0: no effect
+          const float g = dv[k][i] * wv[k][i];
           s1 += g;
           s2 += g * xh;
-          dw[k][i] += dv[u][k][i] * xh;
-          db[k][i] += dv[u][k][i];
-          xv[u][k][i] = xh;                                  // keep xhat, reuse dv for g
-          dv[u][k][i] = g;
+          dw[k][i] += dv[k][i] * xh;
+          db[k][i] += dv[k][i];
+          xv[k][i] = xh;                                  // keep xhat, reuse dv for g
+          dv[k][i] = g;
         }
       }
       s1 = group_sum(s1, G) * invC;
@@ -195,10 +232,10 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
           if (j < nch) {
             float o[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) o[i] = rs[u] * (dv[u][k][i] - s1 - xv[u][k][i] * s2);
+            for (int i = 0; i < 8; ++i) o[i] = rs[u] * (dv[k][i] - s1 - xv[k][i] * s2);
             if constexpr (ADD) {
               float rv[8];
-              load_chunk(dres + row * C + j * 8, rv);
+              rr[u][k].unpack(rv);
 #pragma unroll
               for (int i = 0; i < 8; ++i) o[i] += rv[i];
             }
