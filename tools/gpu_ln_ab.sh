@@ -13,11 +13,12 @@ for v in new old; do
   python3 - $v <<'PY'
 import csv, sys
 rows = sorted(csv.DictReader(open(f"gpurun_out/lnprof_{sys.argv[1]}/ln_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
-t = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if "ln_bwd" in r["Kernel_Name"]]
 shapes = ["M 262144 C 96", "M 65536 C 192", "M 589824 C 192", "M 147456 C 384"]
-for i, sh in enumerate(shapes):
-    g = t[23 * i + 3: 23 * i + 23]
-    print(f"{sys.argv[1]} {sh}: ln_bwd_kernel mean {sum(g) / max(1, len(g)):.1f} us over {len(g)}")
+for kname, per in (("ln_bwd", 23), ("ln_fwd", 24)):
+    t = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if kname in r["Kernel_Name"]]
+    for i, sh in enumerate(shapes):
+        g = t[per * i + per - 20: per * i + per]
+        print(f"{sys.argv[1]} {sh}: {kname}_kernel mean {sum(g) / max(1, len(g)):.1f} us over {len(g)}")
 PY
   rm -rf gpurun_out/lnprof_$v
 done

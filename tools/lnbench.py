@@ -39,6 +39,10 @@ def main():
             byt = M * C * 2 * 4          # dy, gs, x read + dx written (bf16)
             print(f"M {M} C {C} parts {parts}: add_layer_norm backward {ms:.4f} ms ({byt / ms / 1e6:.0f} GB/s incl. "
                   f"the colsum pass)", flush=True)
+        with torch.no_grad():                # forward launches for the kernel trace (23 per shape)
+            for _ in range(23):
+                ops.add_layer_norm(x, r, w, b)
+        torch.cuda.synchronize()
 
 
 if __name__ == "__main__":

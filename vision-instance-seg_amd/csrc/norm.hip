@@ -88,56 +88,87 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ 
   const int lane = threadIdx.x & (G - 1);
   const int rows_per_block = kThreads / G;
   const float invC = 1.f / (float)C;
-  for (long long row = (long long)blockIdx.x * rows_per_block + threadIdx.x / G; row < M;
-       row += (long long)gridDim.x * rows_per_block) {
-    const T* xr = x + row * C;
-    float v[K][8];
-    float s = 0.f;
+  // weight / bias loaded once (they were a dependent round trip at every row's store), U
+  // rows per iteration with every load (x, and r for the residual form) issued up front
+  float wv[K][8], bv[K][8];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int j = lane + k * G;
-      if (j < nch) {
-        load_chunk(xr + j * 8, v[k]);
+  for (int k = 0; k < K; ++k) {
+    const int j = lane + k * G;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wv[k][i] = bv[k][i] = 0.f;
+    if (j < nch) {
+      load_chunk(w + j * 8, wv[k]);
+      load_chunk(b + j * 8, bv[k]);
+    }
+  }
+  constexpr int U = K <= 2 ? 2 : 1;
+  const long long stride = (long long)gridDim.x * rows_per_block;
+  for (long long row0 = (long long)blockIdx.x * rows_per_block + threadIdx.x / G; row0 < M; row0 += U * stride) {
+    RawChunk<T> xr[U][K], rr[RES ? U : 1][RES ? K : 1];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = row0 + u * stride;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int j = lane + k * G;
+        if (row < M && j < nch) {
+          xr[u][k].load(x + row * C + j * 8);
+          if constexpr (RES) rr[u][k].load(r + row * C + j * 8);
+        } else {
+          xr[u][k].zero();
+          if constexpr (RES) rr[u][k].zero();
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = row0 + u * stride;
+      float v[K][8];
+      float sm = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int j = lane + k * G;
+        xr[u][k].unpack(v[k]);
         if constexpr (RES) {
           float rv[8];
-          load_chunk(r + row * C + j * 8, rv);
+          rr[u][k].unpack(rv);
 #pragma unroll
           for (int i = 0; i < 8; ++i) v[k][i] = to_f32(from_f32<T>(v[k][i] + rv[i]));
-          store_chunk(s_out + row * C + j * 8, v[k]);
+          if (row < M && j < nch) store_chunk(s_out + row * C + j * 8, v[k]);
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) s += v[k][i];
+        for (int i = 0; i < 8; ++i) sm += v[k][i];          // masked chunks are zero
       }
-    }
-    const float mu = group_sum(s, G) * invC;
-    float q = 0.f;
+      const float mu = group_sum(sm, G) * invC;
+      float q = 0.f;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int j = lane + k * G;
-      if (j < nch) {
+      for (int k = 0; k < K; ++k) {
+        const int j = lane + k * G;
+        if (j < nch) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float d = v[k][i] - mu;
-          q += d * d;
+          for (int i = 0; i < 8; ++i) {
+            const float d = v[k][i] - mu;
+            q += d * d;
+          }
         }
       }
-    }
-    const float rs = rsqrtf(group_sum(q, G) * invC + eps);
+      const float rs = rsqrtf(group_sum(q, G) * invC + eps);
+      if (row < M) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int j = lane + k * G;
-      if (j < nch) {
-        float wv[8], bv[8], o[8];
-        load_chunk(w + j * 8, wv);
-        load_chunk(b + j * 8, bv);
+        for (int k = 0; k < K; ++k) {
+          const int j = lane + k * G;
+          if (j < nch) {
+            float o[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mu) * rs * wv[i] + bv[i];
-        store_chunk(y + row * C + j * 8, o);
+            for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mu) * rs * wv[k][i] + bv[k][i];
+            store_chunk(y + row * C + j * 8, o);
+          }
+        }
+        if (lane == 0) {
+          mean[row] = mu;
+          rstd[row] = rs;
+        }
       }
-    }
-    if (lane == 0) {
-      mean[row] = mu;
-      rstd[row] = rs;
     }
   }
 }
