@@ -4,7 +4,7 @@ FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads on gfx950 (x2 here);
 WRITE_SIZE is exact for 16-B stores and float atomics.
 
 Usage: python tools/pmc_traffic.py <fetch counter_collection.csv> <write ...csv> [out.json]
-Prints per-kernel mean bytes per dispatch (last half of the dispatches = steady state)
+Prints per-kernel mean bytes per dispatch (steady-state steps: see load())
 and writes the json that bench.py reads for roofline.traffic."""
 import csv
 import json
@@ -13,9 +13,18 @@ from collections import defaultdict
 
 
 def load(path, counter):
+    """Per-kernel values of one counter over the steady-state steps only: dispatches after
+    the second optimiser step (flat_step_kernel) -- the first steps carry MIOpen's
+    convolution Find (reference / candidate kernels that the training step never runs) --
+    and of those the last half per kernel."""
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+    did = lambda r: int(r.get("Dispatch_Id") or 0)
+    rows.sort(key=did)
+    steps = sorted({did(r) for r in rows if "flat_step_kernel" in r["Kernel_Name"]})
+    start = steps[1] if len(steps) > 2 else -1
     per = defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter:
+    for r in rows:
+        if did(r) > start:
             per[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)
     return {k: v[len(v) // 2:] for k, v in per.items()}   # steady-state half
 
