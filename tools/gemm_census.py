@@ -1,6 +1,7 @@
 """Achieved TF/s of every matrix op of one training step, grouped by op and input shapes:
 torch.profiler with FLOP annotation (mm / addmm / bmm / baddbmm / convolution), device
-time per group, sorted by device time.  Run on the GPU box from the repo root."""
+time per group, sorted by device time.  Run on the GPU box from the repo root:
+    python tools/gemm_census.py [model] [size] [batch]"""
 import os
 import sys
 
@@ -22,9 +23,12 @@ OPS = ("aten::mm", "aten::addmm", "aten::bmm", "aten::baddbmm", "aten::convoluti
 
 def main():
     dev = torch.device("cuda", 0)
-    cfg = M2FConfig.preset("swin_t")
+    model = sys.argv[1] if len(sys.argv) > 1 else "swin_t"
+    size = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    batch = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    cfg = M2FConfig.preset(model)
     tr = Trainer(Mask2Former(cfg).init_weights(0), SetCriterion(cfg), SolverConfig(), device=dev)
-    images, ml, cl = synthetic_batch(4, 1024, seed=42, device=dev)
+    images, ml, cl = synthetic_batch(batch, size, seed=42, device=dev)
     for _ in range(3):
         tr.step(images, ml, cl)
     torch.cuda.synchronize()

@@ -97,6 +97,12 @@ class Predictor:
                  amp: bool = True, top_k: int = 100, graphs: bool = True, max_graphs: int = 4):
         self.device = torch.device(device)
         self.bf16 = bool(amp) and self.device.type == "cuda"
+        if self.device.type == "cuda":
+            # MIOpen Find (as the Trainer): without it MIOpen's immediate mode ran a fallback
+            # solver on the FIRST call of a convolution shape and another afterwards, so the
+            # first forward of a shape differed from every later one -- and from its graph
+            # capture (tools/det_debug.py: pixel_decoder.input_proj.0.conv)
+            torch.backends.cudnn.benchmark = True
         if self.bf16 and next(model.parameters()).dtype != torch.bfloat16:
             # a bf16 copy: the caller's model (e.g. an f32 Trainer's, whose parameters are
             # views of its flat buffers) is left as it is

@@ -184,10 +184,32 @@ class Stage(nn.Module):
 
 
 class PatchEmbed(nn.Module):
+    """Swin patch embedding (HF:swin:231-260): Conv2d(3, dim, 4, stride 4), then LayerNorm.
+    The stride equals the kernel, so the conv is one GEMM over non-overlapping 4x4 patches:
+    the image is cut into [B * H/4 * W/4, 3 * 4 * 4] patch rows (one permute copy of the
+    input, which needs no gradient) and projected by the conv weight viewed [dim, 48] in its
+    own (c, kh, kw) order -- token-major output for the LayerNorm, the split-K weight
+    gradient of TokenLinear.  MIOpen ran this conv's forward at ~26 TF/s and its weight
+    gradient at ~12 TF/s (C5: 0.42 + 0.90 ms per step, tools/gemm_census.py).  Training
+    path only: under no_grad the library GEMM's choice differed between eager and
+    graph-captured runs (tests/test_gpu_model.py::test_predictor_graph_replay_matches_eager)."""
+
     def __init__(self, dim):
         super().__init__()
         self.proj = nn.Conv2d(3, dim, kernel_size=4, stride=4)
         self.norm = TokenLayerNorm(dim)
+
+    def tokens(self, px):
+        """px [B, 3, H, W] (H, W multiples of 4) -> ([B, H/4 * W/4, dim], H/4, W/4)."""
+        B, Ci, H, W = px.shape
+        h, w = H // 4, W // 4
+        if not (px.is_cuda and torch.is_grad_enabled()):   # inference keeps the conv: its graph
+            x = self.proj(px)                              # replay is bit-identical to eager
+            return x.flatten(2).transpose(1, 2), h, w
+        patches = px.view(B, Ci, h, 4, w, 4).permute(0, 2, 4, 1, 3, 5).reshape(B * h * w, Ci * 16)
+        wt = self.proj.weight
+        y = linear_tokens(patches, wt.view(wt.shape[0], -1), self.proj.bias)
+        return y.view(B, h * w, -1), h, w
 
 
 class SwinBackbone(nn.Module):
@@ -212,9 +234,9 @@ class SwinBackbone(nn.Module):
             px = F.pad(px, (0, 4 - W % 4))
         if H % 4:
             px = F.pad(px, (0, 0, 0, 4 - H % 4))
-        x = self.patch_embed.proj(px)
-        B, C, H, W = x.shape
-        x = self.patch_embed.norm(x.flatten(2).transpose(1, 2))
+        x, H, W = self.patch_embed.tokens(px)
+        B = x.shape[0]
+        x = self.patch_embed.norm(x)
         feats = []
         for i, st in enumerate(self.stages):
             res = None
