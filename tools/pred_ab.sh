@@ -1,6 +1,7 @@
+# one test, repeated in separate processes (run-to-run stability; debug aid)
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-M=vision-instance-seg_amd/visionseg/model.py
-for i in 1 2; do timeout -k 10 200 python -u -m pytest -q --timeout 150 --timeout-method thread -k predictor tests/test_gpu_model.py > gpurun_out/pred_new_$i.log 2>&1; echo "new $i rc=$?"; done
-cp gpurun_model_old.py $M || exit 1
-for i in 1 2; do timeout -k 10 200 python -u -m pytest -q --timeout 150 --timeout-method thread -k predictor tests/test_gpu_model.py > gpurun_out/pred_old_$i.log 2>&1; echo "old $i rc=$?"; done
+T=${AB_TEST:-tests/test_gpu_train_parity.py::test_bf16_training_step_vs_oracle}
+for i in 1; do
+  timeout -k 10 300 python -u -m pytest -q -s --timeout 250 --timeout-method thread $T > gpurun_out/ab_$i.log 2>&1; echo "run $i rc=$?"; grep "bf16 step" gpurun_out/ab_$i.log | cut -c1-330
+done
