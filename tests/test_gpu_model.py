@@ -234,7 +234,14 @@ def test_train_template_seam_and_inference_seam(tmp_path, arch):
 def test_predictor_graph_replay_matches_eager():
     """The inference Predictor (labeling_server seam): the pure-bf16 forward replayed as a
     HIP graph per padded input shape gives the same instances as the eager forward, for
-    several image shapes (more shapes than the LRU keeps: graphs are evicted and recaptured)."""
+    several image shapes (more shapes than the LRU keeps: graphs are evicted and recaptured).
+
+    Same labels; scores within 5e-3 and at most 1 % of mask pixels flipped.  Not bit-exact:
+    inside a long test process the vendor libraries (MIOpen Find, hipBLASLt) occasionally
+    ran another solver for a captured launch than for the eager one, and with bf16
+    activations that moves scores by ~1e-3 and flips pixels at the 0.5 threshold (seen
+    in 2 of 5 full-file runs; the same comparison in a fresh process, 16 shape passes:
+    bit-identical, tools/pred_debug.py)."""
     from visionseg.inference import Predictor
     from visionseg.model import M2FConfig, Mask2Former
     cfg = M2FConfig.preset("swin_t")
@@ -247,6 +254,7 @@ def test_predictor_graph_replay_matches_eager():
     for shape in ((200, 260), (256, 256), (300, 180), (200, 260)):
         img = rng.integers(0, 256, (*shape, 3)).astype(np.uint8)
         a, b = pg(img).pred_instances, pe(img).pred_instances
-        assert torch.equal(a.masks, b.masks) and torch.equal(a.labels, b.labels)
-        assert torch.equal(a.scores, b.scores)
+        assert torch.equal(a.labels, b.labels)
+        assert float((a.scores - b.scores).abs().max()) <= 5e-3
+        assert float((a.masks != b.masks).float().mean()) <= 1e-2
     assert len(pg._graphs) == 2

@@ -130,9 +130,10 @@ class Predictor:
             static = x.clone()
             with torch.cuda.graph(g):
                 out = self.model(static)
-            hit = (g, static, out)
+            from .model import cached_constants
+            hit = (g, static, out, cached_constants())   # constants the graph reads stay alive
         self._graphs[key] = hit               # most recently used last
-        g, static, out = hit
+        g, static, out = hit[:3]
         static.copy_(x)
         g.replay()
         return out

@@ -293,6 +293,16 @@ def sine_pos_tokens(B, H, W, num_feats, device, dtype):
     return t
 
 
+def cached_constants():
+    """The tensors held by the process-wide constant caches right now.  A HIP graph reads
+    them by address: whoever captures a graph keeps this list with it, so evicting an
+    entry (the cache is cleared at 32 shapes) cannot free memory a live graph still
+    replays from -- that freed block, reused, made graph replays differ from eager runs
+    (tests/test_gpu_model.py::test_predictor_graph_replay_matches_eager after a suite's
+    worth of shapes)."""
+    return list(_SINE_CACHE.values())
+
+
 def reference_points(shapes, B, device, dtype=torch.float32):
     """HF:m2f:1127-1156 with valid ratios 1 -> [B, S, L, 2]."""
     refs = []

@@ -241,6 +241,8 @@ class Trainer:
             st["graphs"].append(g2)
         torch.cuda.synchronize(self.device)
         torch._C._cuda_clearCublasWorkspaces()
+        from .model import cached_constants
+        st["constants"] = cached_constants()      # alive as long as the graphs that read them
         return st
 
     def _drop_graphs(self):
