@@ -85,12 +85,16 @@ def test_swin_t_mask_logits_vs_oracle(size):
             got = unpack_bitmask_like(words, rb.shape[-1]).cpu()
             diff = got != rb
             flips += int(diff.sum())
-            if diff.any():
-                worst = max(worst, float(ram[diff].abs().max()))
+            if diff.any() and worst == 0.0:
+                worst = float(ram[diff].abs().max())
         # a flip is a threshold decision on a logit within rounding of 0 (the oracle's own
         # rounding varies with the CPU thread count of the box): |logit| < 5e-4 against
-        # logits of magnitude ~10 (measured flips: 1e-6 .. 1.1e-4)
-        assert worst < 5e-4, f"mask bit differs where the oracle logit is {worst:.2e} from the threshold"
+        # logits of magnitude ~10 (measured flips: 1e-6 .. 1.1e-4).  Checked in the FIRST
+        # decoder step that has any: once a bit differs, the self-attention carries the
+        # difference into every later step's logits, whose flips then sit further from 0
+        # (a 3.7e-3 flip seen downstream of a 1e-5 one; the GPU side's last bits vary from
+        # run to run -- 0 or 5 flips over three runs of this test)
+        assert worst < 5e-4, f"first mask-bit flip where the oracle logit is {worst:.2e} from the threshold"
         m.decoder.mask_override = [rb for rb, _ in ref.decoder.trace]
         fmasks, fclasses = m(px.to(DEV))
         m.decoder.mask_override = None
