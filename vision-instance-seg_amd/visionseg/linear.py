@@ -46,7 +46,7 @@ def load_gemm_table(path: str = GEMM_TABLE) -> bool:
 
 
 MIN_CHUNK = 1024
-TARGET_TILES = 768          # aim for this many 128x128 output tiles over all chunks
+TARGET_TILES = int(os.environ.get("VS_SPLITK_TILES", "768"))   # aim for this many 128x128 output tiles over all chunks
 
 
 def split_count(K: int, M: int, N: int) -> int:
