@@ -159,14 +159,15 @@ VS_API int vs_window_attn_backward(int dtype, const void* qkv, const float* rel_
 
 /* ---- C5: fp8 (OCP e4m3) window attention ----------------------------------------
  * Same layouts and semantics as vs_window_attn_forward/backward with bf16 storage, for
- * window^2 <= 160.  The logits S = q.k^T and the product P.V run on
- * v_mfma_f32_32x32x16_fp8_fp8: q, k and v of each (window, head) are quantised to e4m3
- * in-kernel with power-of-two scales 2^floor(log2(448/amax)) (amax over the window's
- * N x 32 values), P (unnormalised, in [0,1]) with scale 256; f32 softmax and accumulate.
- * The backward recomputes S from the same fp8 operands (so exp(S - lse) is the
- * forward's P) and forms dV, dP, dQ, dK in bf16 from the bf16 operands
- * (straight-through quantisation).  Replaces the same upstream call sites as
- * vs_window_attn_* (HF:swin:373-398) under BASELINE config C5. */
+ * window^2 <= 160.  The forward's logits S = q.k^T and product P.V run on the
+ * block-scaled MX MFMA v_mfma_scale_f32_32x32x64_f8f6f4 with e4m3 operands and e8m0
+ * power-of-two scales 2^floor(log2(448/amax)): one per q / k token (amax over its 32
+ * channels), one per (window, head) for V, and a fixed 2^8 for P = exp(S - max) <= 1;
+ * f32 softmax and accumulation.  The backward recomputes S from the same e4m3 values
+ * (dequantised exactly to bf16, so exp(S - lse) is the forward's P) and forms dV, dP,
+ * dQ, dK in bf16 from the bf16 operands (straight-through quantisation).  Replaces the
+ * same upstream call sites as vs_window_attn_* (HF:swin:373-398) under BASELINE config
+ * C5. */
 VS_API int vs_window_attn_forward_fp8(const void* qkv, const float* rel_table, void* out, float* lse,
                                       int num_windows, int heads, int window, int shift, int nwin_h,
                                       int nwin_w, float scale, void* stream);
@@ -175,6 +176,23 @@ VS_API int vs_window_attn_backward_fp8(const void* qkv, const float* rel_table, 
                                        float* grad_table_partial, int num_windows, int heads,
                                        int window, int shift, int nwin_h, int nwin_w, float scale,
                                        void* stream);
+
+/* Image-layout variants: the window reverse (vs_window_reverse) folded into the attention
+ * kernels.  out / grad_out are [batch, height, width, heads*32] in the un-shifted,
+ * un-padded image layout (nwin_h * window >= height > (nwin_h - 1) * window, likewise the
+ * width); qkv, grad_qkv, lse and the table partials keep the window layout.  bf16 only
+ * (fp8 != 0: the C5 e4m3 kernels), window^2 <= 160.  The partition of grad_out that the
+ * reverse's backward would run is folded into the backward's loads the same way (padded
+ * tokens: zero output gradient).  Replace HF:swin:558-566 + the attention core. */
+VS_API int vs_window_attn_forward_image(int dtype, int fp8, const void* qkv, const float* rel_table,
+                                        void* out, float* lse, int num_windows, int heads, int window,
+                                        int shift, int nwin_h, int nwin_w, int height, int width,
+                                        float scale, void* stream);
+VS_API int vs_window_attn_backward_image(int dtype, int fp8, const void* qkv, const float* rel_table,
+                                         const void* out, const float* lse, const void* grad_out,
+                                         void* grad_qkv, float* grad_table_partial, int num_windows,
+                                         int heads, int window, int shift, int nwin_h, int nwin_w,
+                                         int height, int width, float scale, void* stream);
 
 
 /* ---- a11: mask head -----------------------------------------------------------------

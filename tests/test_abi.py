@@ -54,6 +54,7 @@ def test_ops_refuse_cpu_tensors():
 
 # the operator surface of SURVEY §8(b): TORCH_LIBRARY(visionseg) in csrc/torch_ops.cpp
 TORCH_OPS = ["msda_fwd", "msda_bwd", "swin_window_fwd", "swin_window_bwd", "win_attn_fwd", "win_attn_bwd",
+             "win_attn_fwd_img", "win_attn_bwd_img",
              "mask_head_fwd", "mask_head_bwd", "attn_bitmask", "masked_xattn_fwd", "masked_xattn_bwd"]
 
 

@@ -1187,3 +1187,39 @@ def test_splitk_sum_vs_torch(monkeypatch, S, n, dtype):
         ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 0.0
         err = (out.double() - exp).abs()
         assert bool((err <= 1e-6 * mag + ulp * exp.abs()).all()), (phased, float(err.max()))
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("ws,shift,heads,B,H,W", [(7, 3, 3, 2, 20, 26), (7, 0, 6, 1, 14, 14), (12, 6, 4, 2, 26, 30),
+                                                  (12, 0, 8, 1, 24, 36), (7, 3, 2, 1, 8, 6)])
+def test_window_attention_image_layout_equals_reverse(fp8, ws, shift, heads, B, H, W):
+    """ops.window_attention_image (the window reverse folded into the bf16 / fp8 kernels:
+    output and output gradient in the image layout, padding cropped) == window_attention +
+    window_reverse, bit for bit: same kernels, only the rows they read / write move.  The
+    backward gets the same image-layout gradient both ways; grad_qkv and the table gradient
+    are identical too (padded tokens carry a zero output gradient either way)."""
+    ops = _ops()
+    if fp8 and ws * ws > 160:
+        pytest.skip("fp8 needs window^2 <= 160")
+    g = torch.Generator(device="cuda").manual_seed(ws * 100 + H + W + shift)
+    nwh, nww = -(-H // ws), -(-W // ws)
+    C = heads * 32
+    qkv = torch.randn(B * nwh * nww, ws * ws, 3 * C, device=DEV, generator=g).to(torch.bfloat16)
+    table = 0.3 * torch.randn((2 * ws - 1) ** 2, heads, device=DEV, generator=g)
+    gy = torch.randn(B, H, W, C, device=DEV, generator=g).to(torch.bfloat16)
+    res = []
+    for image in (True, False):
+        q = qkv.clone().requires_grad_(True)
+        t = table.clone().requires_grad_(True)
+        if image:
+            o = ops.window_attention_image(q, t, heads, ws, shift, B, H, W, fp8=fp8)
+        else:
+            o = ops.window_reverse(ops.window_attention(q, t, heads, ws, shift, nwh, nww, fp8=fp8), B, H, W, ws, shift)
+        o.backward(gy)
+        res.append((o.detach(), q.grad, t.grad))
+    torch.cuda.synchronize()
+    (oi, gqi, gti), (ow, gqw, gtw) = res
+    assert oi.shape == (B, H, W, C)
+    assert torch.equal(oi, ow)
+    assert torch.equal(gqi, gqw)
+    assert torch.equal(gti, gtw)

@@ -224,6 +224,55 @@ std::tuple<at::Tensor, at::Tensor> win_attn_bwd(const at::Tensor& qkv, const at:
   return {gqkv, part.sum(0).t().contiguous()};
 }
 
+// image-layout window attention (the window reverse folded in): out / grad_out
+// [B, height, width, heads*32]; qkv, lse, grad_qkv in the window layout
+std::tuple<at::Tensor, at::Tensor> win_attn_fwd_img(const at::Tensor& qkv, const at::Tensor& rel_table, int64_t heads,
+                                                    int64_t window, int64_t shift, int64_t nwin_h, int64_t nwin_w,
+                                                    int64_t height, int64_t width, double scale, bool fp8) {
+  on_device({&qkv, &rel_table});
+  check_qkv(qkv, heads, window);
+  at::Tensor q = qkv.contiguous(), table = rel_table.to(at::kFloat).contiguous();
+  TORCH_CHECK(table.numel() == (2 * window - 1) * (2 * window - 1) * heads, "rel_table must be [(2ws-1)^2, heads]");
+  const int64_t Bw = q.size(0), N = q.size(1), nw = nwin_h * nwin_w;
+  TORCH_CHECK(nw > 0 && Bw % nw == 0, "num_windows must be a multiple of nwin_h * nwin_w");
+  at::Tensor out = at::empty({Bw / nw, height, width, heads * 32}, q.options());
+  at::Tensor lse = at::empty({Bw, heads, N}, q.options().dtype(at::kFloat));
+  vs_ok(vs_window_attn_forward_image(dcode(q), fp8 ? 1 : 0, q.data_ptr(), table.data_ptr<float>(), out.data_ptr(),
+                                     lse.data_ptr<float>(), as_int(Bw, "windows"), (int)heads, (int)window,
+                                     (int)shift, (int)nwin_h, (int)nwin_w, as_int(height, "height"),
+                                     as_int(width, "width"), (float)scale, cur_stream(q)),
+        "win_attn_fwd_img");
+  return {out, lse};
+}
+
+// -> (grad_qkv [window layout], grad_rel_table partials [Bw, heads, (2ws-1)^2] f32)
+std::tuple<at::Tensor, at::Tensor> win_attn_bwd_img(const at::Tensor& qkv, const at::Tensor& rel_table,
+                                                    const at::Tensor& out, const at::Tensor& lse,
+                                                    const at::Tensor& grad_out, int64_t heads, int64_t window,
+                                                    int64_t shift, int64_t nwin_h, int64_t nwin_w, int64_t height,
+                                                    int64_t width, double scale, bool fp8) {
+  on_device({&qkv, &rel_table, &out, &lse, &grad_out});
+  check_qkv(qkv, heads, window);
+  at::Tensor q = qkv.contiguous(), table = rel_table.to(at::kFloat).contiguous();
+  at::Tensor o = out.contiguous(), l = lse.contiguous(), g = grad_out.to(q.scalar_type()).contiguous();
+  const int64_t Bw = q.size(0), N = q.size(1), T2 = (2 * window - 1) * (2 * window - 1), nw = nwin_h * nwin_w;
+  TORCH_CHECK(nw > 0 && Bw % nw == 0, "num_windows must be a multiple of nwin_h * nwin_w");
+  TORCH_CHECK(o.sizes() == at::IntArrayRef({Bw / nw, height, width, heads * 32}) && g.sizes() == o.sizes(),
+              "out / grad_out must be [B, height, width, heads*32]");
+  TORCH_CHECK(l.scalar_type() == at::kFloat && l.sizes() == at::IntArrayRef({Bw, heads, N}),
+              "lse must be float32 [B*nW, heads, window^2]");
+  TORCH_CHECK(table.numel() == T2 * heads, "rel_table must be [(2ws-1)^2, heads]");
+  at::Tensor gqkv = at::empty_like(q);
+  at::Tensor part = at::empty({Bw, heads, T2}, q.options().dtype(at::kFloat));
+  vs_ok(vs_window_attn_backward_image(dcode(q), fp8 ? 1 : 0, q.data_ptr(), table.data_ptr<float>(), o.data_ptr(),
+                                      l.data_ptr<float>(), g.data_ptr(), gqkv.data_ptr(), part.data_ptr<float>(),
+                                      as_int(Bw, "windows"), (int)heads, (int)window, (int)shift, (int)nwin_h,
+                                      (int)nwin_w, as_int(height, "height"), as_int(width, "width"), (float)scale,
+                                      cur_stream(q)),
+        "win_attn_bwd_img");
+  return {gqkv, part};
+}
+
 // ---- a11: mask head einsum('bqc,bchw->bqhw') with channels-last pixel embedding
 at::Tensor mask_head_fwd(const at::Tensor& mask_embed, const at::Tensor& pixel_nhwc, int64_t height, int64_t width) {
   on_device({&mask_embed, &pixel_nhwc});
@@ -351,6 +400,11 @@ TORCH_LIBRARY(visionseg, m) {
         "float scale, bool fp8=False) -> (Tensor, Tensor)");
   m.def("win_attn_bwd(Tensor qkv, Tensor rel_table, Tensor out, Tensor lse, Tensor grad_out, int heads, int window, "
         "int shift, int nwin_h, int nwin_w, float scale, bool fp8=False, bool table_partials=False) -> (Tensor, Tensor)");
+  m.def("win_attn_fwd_img(Tensor qkv, Tensor rel_table, int heads, int window, int shift, int nwin_h, int nwin_w, "
+        "int height, int width, float scale, bool fp8) -> (Tensor, Tensor)");
+  m.def("win_attn_bwd_img(Tensor qkv, Tensor rel_table, Tensor out, Tensor lse, Tensor grad_out, int heads, "
+        "int window, int shift, int nwin_h, int nwin_w, int height, int width, float scale, bool fp8) "
+        "-> (Tensor, Tensor)");
   m.def("mask_head_fwd(Tensor mask_embed, Tensor pixel_nhwc, int height, int width) -> Tensor");
   m.def("mask_head_bwd(Tensor grad_logits, Tensor mask_embed, Tensor pixel_nhwc, Tensor(a!) grad_pixel, "
         "bool accumulate) -> Tensor");
@@ -367,6 +421,8 @@ TORCH_LIBRARY_IMPL(visionseg, CUDA, m) {
   m.impl("swin_window_bwd", swin_window_bwd);
   m.impl("win_attn_fwd", win_attn_fwd);
   m.impl("win_attn_bwd", win_attn_bwd);
+  m.impl("win_attn_fwd_img", win_attn_fwd_img);
+  m.impl("win_attn_bwd_img", win_attn_bwd_img);
   m.impl("mask_head_fwd", mask_head_fwd);
   m.impl("mask_head_bwd", mask_head_bwd);
   m.impl("attn_bitmask", attn_bitmask);

@@ -31,7 +31,24 @@ constexpr int kD = 32;
 struct WinGeom {
   int heads, ws, shift, nWh, nWw, N, T2;  // T2 = (2ws-1)^2
   float scale;
+  int H, W, nat;                           // nat: out / grad_out in the image layout [B, H, W, C]
 };
+
+// Row of window token t of window bw in the output / output-gradient layout: the window
+// layout (bw N + t), or -- nat, the window reverse folded into the kernel -- the token's
+// pixel in [B, H, W] (the partition's roll undone; -1 for a token of the zero padding,
+// which the reverse crops: its output is not stored and its output gradient is zero)
+__device__ __forceinline__ long long out_row(const WinGeom& g, int bw, int t) {
+  if (!g.nat) return (long long)bw * g.N + t;
+  const int nw = g.nWh * g.nWw, b = bw / nw, wl = bw - b * nw;
+  const int wy = wl / g.nWw, wx = wl - wy * g.nWw;
+  const int ty = t / g.ws, tx = t - ty * g.ws;
+  int y = wy * g.ws + ty + g.shift, x = wx * g.ws + tx + g.shift;
+  if (y >= g.nWh * g.ws) y -= g.nWh * g.ws;
+  if (x >= g.nWw * g.ws) x -= g.nWw * g.ws;
+  if (y >= g.H || x >= g.W) return -1;
+  return ((long long)b * g.H + y) * g.W + x;
+}
 
 __device__ __forceinline__ int region_of(int p, int Pp, int ws, int shift) {
   return (p >= Pp - ws) + (p >= Pp - shift);
@@ -507,8 +524,10 @@ __global__ void __launch_bounds__(64 * kFwdWaves, 3) win_attn_fwd_mfma(const bf1
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = 32 * qt + r;
-    if (q < N) {
-      bf16* dst = out + ((size_t)bw * N + q) * C + h * kD;
+    const long long orow = q < N ? out_row(g, bw, q) : -1;
+    if (q < N && hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = lq[qt];
+    if (orow >= 0) {
+      bf16* dst = out + orow * C + h * kD;
 #pragma unroll
       for (int grp = 0; grp < 4; ++grp) {
         bf16x4_t v;
@@ -516,7 +535,6 @@ __global__ void __launch_bounds__(64 * kFwdWaves, 3) win_attn_fwd_mfma(const bf1
         for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[qt][4 * grp + e] * inv[qt]);
         *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
       }
-      if (hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = lq[qt];
     }
   }
 }
@@ -796,8 +814,10 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
     }
   }
   const int q = qrow;
-  if (q < N) {
-    bf16* dst = out + ((size_t)bw * N + q) * C + h * kD;
+  const long long orow = q < N ? out_row(g, bw, q) : -1;
+  if (q < N && hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = lq;   // every token: the backward reads it
+  if (orow >= 0) {
+    bf16* dst = out + orow * C + h * kD;
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
       bf16x4_t v;
@@ -805,7 +825,6 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
       for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[4 * grp + e] * inv);
       *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
     }
-    if (hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = lq;
   }
 }
 
@@ -891,9 +910,11 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(6)
   }
   sum += __shfl_xor(sum, 32, 64);
   const int q = 32 * qt + r;
-  if (q < N) {
+  const long long orow = q < N ? out_row(g, bw, q) : -1;
+  if (q < N && hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = (m + __log2f(sum)) * (1.f / kLog2e);
+  if (orow >= 0) {
     const float inv = 1.f / sum;
-    bf16* dst = out + ((size_t)bw * N + q) * C + h * kD;
+    bf16* dst = out + orow * C + h * kD;
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
       bf16x4_t v;
@@ -901,7 +922,6 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(6)
       for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[4 * grp + e] * inv);
       *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
     }
-    if (hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = (m + __log2f(sum)) * (1.f / kLog2e);
   }
 }
 
@@ -1027,9 +1047,11 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(ON
       o = mfma_mx(vm, vsb, pm, kPScaleByte, o);
     }
     sum += __shfl_xor(sum, 32, 64);
-    if (qrow < N) {
+    const long long orow = qrow < N ? out_row(g, bw, qrow) : -1;
+    if (qrow < N && hh == 0) lse[((size_t)bw * g.heads + h) * N + qrow] = (m + __log2f(sum)) * (1.f / kLog2e);
+    if (orow >= 0) {
       const float inv = 1.f / sum;
-      bf16* dst = out + ((size_t)bw * N + qrow) * C + h * kD;
+      bf16* dst = out + orow * C + h * kD;
 #pragma unroll
       for (int grp = 0; grp < 4; ++grp) {
         bf16x4_t v;
@@ -1037,7 +1059,6 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(ON
         for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[4 * grp + e] * inv);
         *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
       }
-      if (hh == 0) lse[((size_t)bw * g.heads + h) * N + qrow] = (m + __log2f(sum)) * (1.f / kLog2e);
     }
     return;
   }
@@ -1091,8 +1112,10 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(ON
     mx_pfixed([&](int j) { return j < 16 ? acc[k0][j] : (has1 ? acc[k1][j - 16] : 0.f); }, pm);
     o = mfma_mx(vm, vsb, pm, kPScaleByte, o);
   }
-  if (qrow < N) {
-    bf16* dst = out + ((size_t)bw * N + qrow) * C + h * kD;
+  const long long orow = qrow < N ? out_row(g, bw, qrow) : -1;
+  if (qrow < N && hh == 0) lse[((size_t)bw * g.heads + h) * N + qrow] = lq;
+  if (orow >= 0) {
+    bf16* dst = out + orow * C + h * kD;
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
       bf16x4_t v;
@@ -1100,7 +1123,6 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(ON
       for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[4 * grp + e] * inv);
       *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
     }
-    if (hh == 0) lse[((size_t)bw * g.heads + h) * N + qrow] = lq;
   }
 }
 
@@ -1141,8 +1163,8 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
   const bf16* win = qkv + (size_t)bw * N * C3 + h * kD;
-  const bf16* gwo = gout + (size_t)bw * N * C + h * kD;
-  const bf16* owin = out + (size_t)bw * N * C + h * kD;
+  const bf16* gwo = gout + h * kD;            // rows through out_row (window or image layout)
+  const bf16* owin = out + h * kD;
   bf16* gw = gqkv + (size_t)bw * N * C3 + h * kD;
   const float* lrow = lse + ((size_t)bw * g.heads + h) * N;
   // Every global operand of a phase is requested before any is used (one round trip per
@@ -1159,7 +1181,8 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
     for (int it = 0; it < 2; ++it) {
       const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
       cq[it] = t < N ? ld8(win + (size_t)t * C3 + 8 * c) : zero8();
-      cd[it] = t < N ? ld8(gwo + (size_t)t * C + 8 * c) : zero8();
+      const long long orow = t < N ? out_row(g, bw, t) : -1;
+      cd[it] = orow >= 0 ? ld8(gwo + orow * C + 8 * c) : zero8();
     }
   };
 #pragma unroll
@@ -1179,12 +1202,13 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
       vb[st] = key < N ? ld8(win + (size_t)key * C3 + 2 * C + off) : zero8();
     }
   };
+  const long long qorow = q < N ? out_row(g, bw, q) : -1;
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
     const int off = 16 * st + 8 * hh;
     qb[st] = q < N ? ld8(win + (size_t)q * C3 + off) : zero8();
-    db[st] = q < N ? ld8(gwo + (size_t)q * C + off) : zero8();
-    ob[st] = q < N ? ld8(owin + (size_t)q * C + off) : zero8();
+    db[st] = qorow >= 0 ? ld8(gwo + qorow * C + off) : zero8();
+    ob[st] = qorow >= 0 ? ld8(owin + qorow * C + off) : zero8();
   }
 
   const float Lq = q < N ? lrow[q] * kLog2e : 0.f;      // log2 units
@@ -1358,6 +1382,7 @@ int check_geom(WinGeom& g, int Bw, int heads, int ws, int shift, int nWh, int nW
   g.heads = heads; g.ws = ws; g.shift = shift; g.nWh = nWh; g.nWw = nWw; g.scale = scale;
   g.N = ws * ws;
   g.T2 = (2 * ws - 1) * (2 * ws - 1);
+  g.H = nWh * ws; g.W = nWw * ws; g.nat = 0;
   return Bw > 0 && heads > 0 && ws > 0 && ws <= 16 && shift >= 0 && shift < ws && nWh > 0 && nWw > 0 &&
          Bw % (nWh * nWw) == 0;
 }
@@ -1508,6 +1533,59 @@ extern "C" int vs_window_attn_backward_fp8(const void* qkv, const float* table, 
   VS_CHECK(g.N <= 160, "fp8 window attention needs window^2 <= 160");
   launch_bwd_fa<true>(g, dim3(Bw, heads), (hipStream_t)stream, qkv, table, out, lse, grad_out, grad_qkv,
                       grad_table_partial);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+// Image-layout variants (the window reverse folded into the attention kernels): out /
+// grad_out are [B, height, width, heads*32] in the un-shifted, un-padded image layout
+// (what vs_window_reverse would make of the window-layout output), qkv / grad_qkv / lse /
+// the table partials keep the window layout.  bf16 MFMA / fp8 MX kernels only.
+static int image_geom(WinGeom& g, int dtype, int Bw, int heads, int ws, int shift, int nWh, int nWw, int height,
+                      int width, float scale) {
+  if (!check_geom(g, Bw, heads, ws, shift, nWh, nWw, scale)) return 0;
+  g.H = height;
+  g.W = width;
+  g.nat = 1;
+  return dtype == VS_BF16 && use_mfma() && g.N <= 160 && height > (nWh - 1) * ws && height <= nWh * ws &&
+         width > (nWw - 1) * ws && width <= nWw * ws;
+}
+
+extern "C" int vs_window_attn_forward_image(int dtype, int fp8, const void* qkv, const float* table, void* out,
+                                            float* lse, int Bw, int heads, int ws, int shift, int nWh, int nWw,
+                                            int height, int width, float scale, void* stream) {
+  WinGeom g;
+  VS_CHECK(image_geom(g, dtype, Bw, heads, ws, shift, nWh, nWw, height, width, scale),
+           "bad window / image geometry (image layout: bf16, window^2 <= 160, nwin x window covering the image)");
+  VS_CHECK(qkv && table && out && lse, "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  if (fp8) {
+    launch_fwd_blk<true>(g, dim3(Bw, heads), st, qkv, table, out, lse);
+  } else if (g.N <= 64 && !fwd_blk_small()) {
+    const int items = Bw * heads;
+    hipLaunchKernelGGL(win_attn_fwd_mfma, dim3((items + kFwdWaves - 1) / kFwdWaves), dim3(64 * kFwdWaves), 0, st,
+                       (const bf16*)qkv, table, (bf16*)out, lse, g, items);
+  } else {
+    launch_fwd_blk<false>(g, dim3(Bw, heads), st, qkv, table, out, lse);
+  }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_window_attn_backward_image(int dtype, int fp8, const void* qkv, const float* table,
+                                             const void* out, const float* lse, const void* grad_out, void* grad_qkv,
+                                             float* grad_table_partial, int Bw, int heads, int ws, int shift,
+                                             int nWh, int nWw, int height, int width, float scale, void* stream) {
+  WinGeom g;
+  VS_CHECK(image_geom(g, dtype, Bw, heads, ws, shift, nWh, nWw, height, width, scale),
+           "bad window / image geometry (image layout: bf16, window^2 <= 160, nwin x window covering the image)");
+  VS_CHECK(qkv && table && out && lse && grad_out && grad_qkv && grad_table_partial, "null pointer");
+  if (fp8)
+    launch_bwd_fa<true>(g, dim3(Bw, heads), (hipStream_t)stream, qkv, table, out, lse, grad_out, grad_qkv,
+                        grad_table_partial);
+  else
+    launch_bwd_fa<false>(g, dim3(Bw, heads), (hipStream_t)stream, qkv, table, out, lse, grad_out, grad_qkv,
+                         grad_table_partial);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

@@ -146,10 +146,10 @@ class SwinBlock(nn.Module):
         h = h.view(B, H, W, C)
         win = ops.window_partition(h.to(_compute_dtype(h)), ws, shift)   # cast first: half the bytes moved
         qkv = self.attn.qkv(win)
-        o = ops.window_attention(qkv, self.attn.rel_table, self.attn.heads, ws, shift,
-                                 _padded(H, ws) // ws, _padded(W, ws) // ws,
-                                 fp8=self.attn_fp8 and qkv.dtype == torch.bfloat16)
-        o = ops.window_reverse(o, B, H, W, ws, shift)                 # per-token proj commutes with crop
+        # output in the image layout (window reverse folded into the kernel); the per-token
+        # proj commutes with the crop
+        o = ops.window_attention_image(qkv, self.attn.rel_table, self.attn.heads, ws, shift, B, H, W,
+                                       fp8=self.attn_fp8 and qkv.dtype == torch.bfloat16)
         o = self.attn.proj(o.view(B, H * W, C))
         x, h2 = self.norm2.add_forward(x, o)
         return x, self.mlp(h2)

@@ -297,6 +297,62 @@ class WindowAttentionFunction(torch.autograd.Function):
         return gqkv, gtable, None, None, None, None, None, None, None
 
 
+class WindowAttentionImageFunction(torch.autograd.Function):
+    """WindowAttentionFunction with the window reverse folded into the kernels
+    (vs_window_attn_forward_image / _backward_image): the output (and its gradient) in the
+    image layout [B, H, W, C] -- un-rolled, padding cropped -- so neither the reverse nor
+    the partition of the output gradient runs as its own pass over HBM.  bf16 MFMA / fp8
+    kernels; qkv and lse stay in the window layout."""
+
+    @staticmethod
+    def forward(ctx, qkv, rel_table, heads, window, shift, nwin_h, nwin_w, height, width, scale, fp8=False):
+        L.require_hip(qkv, rel_table)
+        qkv = qkv.contiguous()
+        table = rel_table.float().contiguous()
+        Bw, N, C3 = qkv.shape
+        if C3 != 3 * heads * 32 or N != window * window:
+            raise ValueError(f"qkv {tuple(qkv.shape)} does not match heads={heads} (x32) window={window}")
+        with timed("window_attn_fwd_fp8" if fp8 else "window_attn_fwd", qkv,
+                   bytes_=(qkv.numel() + Bw * N * C3 // 3) * qkv.element_size() + Bw * heads * N * 4,
+                   flops=4.0 * Bw * heads * N * N * 32):
+            out, lse = L.tops().win_attn_fwd_img(qkv, table, heads, window, shift, nwin_h, nwin_w, height, width,
+                                                 float(scale), bool(fp8))
+        ctx.meta = (heads, window, shift, nwin_h, nwin_w, height, width, float(scale), rel_table.dtype, bool(fp8))
+        ctx.save_for_backward(qkv, table, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        qkv, table, out, lse = ctx.saved_tensors
+        heads, window, shift, nwin_h, nwin_w, height, width, scale, tdtype, fp8 = ctx.meta
+        Bw, N, C3 = qkv.shape
+        g = grad_out.to(qkv.dtype).contiguous()
+        with timed("window_attn_bwd_fp8" if fp8 else "window_attn_bwd", qkv,
+                   bytes_=(3 * qkv.numel() + 2 * Bw * N * C3 // 3) * qkv.element_size(),
+                   flops=10.0 * Bw * heads * N * N * 32):
+            gqkv, part = L.tops().win_attn_bwd_img(qkv, table, out, lse, g, heads, window, shift, nwin_h, nwin_w,
+                                                   height, width, scale, bool(fp8))
+        gtable = part.sum(0).t().contiguous().to(tdtype)
+        return gqkv, gtable, None, None, None, None, None, None, None, None, None
+
+
+def window_attention_image(qkv, rel_table, heads: int, window: int, shift: int, batch: int, height: int,
+                           width: int, scale: float | None = None, fp8: bool = False):
+    """Window attention of the partitioned qkv [B*nW, ws^2, 3C] with the output in the image
+    layout [B, H, W, C] (= window_reverse(window_attention(...))): the reverse folded into
+    the bf16 kernels; the f32 parity mode (and VS_WIN_ATTN_SCALAR) keeps the separate
+    reverse."""
+    if scale is None:
+        scale = 32 ** -0.5
+    nwin_h, nwin_w = -(-height // window), -(-width // window)
+    if (qkv.is_cuda and qkv.dtype == torch.bfloat16 and window * window <= 160
+            and os.environ.get("VS_WIN_ATTN_SCALAR", "0") == "0" and os.environ.get("VS_WIN_IMAGE", "1") != "0"):
+        return WindowAttentionImageFunction.apply(qkv, rel_table, int(heads), int(window), int(shift), nwin_h, nwin_w,
+                                                  int(height), int(width), float(scale), bool(fp8))
+    o = window_attention(qkv, rel_table, heads, window, shift, nwin_h, nwin_w, scale, fp8)
+    return window_reverse(o, batch, height, width, window, shift)
+
+
 def window_attention(qkv, rel_table, heads: int, window: int, shift: int, nwin_h: int, nwin_w: int,
                      scale: float | None = None, fp8: bool = False):
     if scale is None:
