@@ -287,6 +287,22 @@ VS_API int vs_layer_norm_backward_ex(int dtype, const void* grad_y, const void* 
 VS_API int vs_layer_norm_backward(int dtype, const void* grad_y, const void* x, const void* weight,
                                   const float* mean, const float* rstd, void* grad_x, void* grad_weight,
                                   void* grad_bias, void* workspace, int rows, int cols, void* stream);
+/* Row-mapped variants: the Swin window partition (HF:swin:546-551: pad, roll, partition)
+ * folded into the LayerNorm that precedes it.  y row m is written at row y_rows[m] of y
+ * (the window-layout row of image token m; y has as many rows as the windows hold, the
+ * padding rows are the caller's), and the backward reads grad_y row m from row
+ * dy_rows[m].  Otherwise as vs_layer_norm_forward / vs_add_layer_norm_forward /
+ * vs_layer_norm_backward_ex. */
+VS_API int vs_layer_norm_forward_rows(int dtype, const void* x, const void* weight, const void* bias, void* y,
+                                      float* mean, float* rstd, int rows, int cols, float eps, const int* y_rows,
+                                      void* stream);
+VS_API int vs_add_layer_norm_forward_rows(int dtype, const void* x, const void* r, const void* w, const void* b,
+                                          void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
+                                          const int* y_rows, void* stream);
+VS_API int vs_layer_norm_backward_rows(int dtype, const void* grad_y, const void* x, const void* weight,
+                                       const float* mean, const float* rstd, const void* grad_res, void* grad_x,
+                                       void* grad_weight, void* grad_bias, void* dx_colsum, void* workspace,
+                                       int rows, int cols, const int* dy_rows, void* stream);
 VS_API long long vs_column_sum_workspace_bytes(int rows, int cols);
 /* out[n] = sum_m x[m, n] (f32 accumulation, fixed order); N a multiple of 8, <= 2048. */
 VS_API int vs_column_sum(int dtype, const void* x, void* out, void* workspace, int rows, int cols,

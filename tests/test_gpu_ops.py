@@ -1223,3 +1223,40 @@ def test_window_attention_image_layout_equals_reverse(fp8, ws, shift, heads, B, 
     assert torch.equal(oi, ow)
     assert torch.equal(gqi, gqw)
     assert torch.equal(gti, gtw)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,H,W,C,ws,shift", [(2, 20, 26, 96, 7, 3), (1, 14, 14, 192, 7, 0), (2, 26, 30, 128, 12, 6),
+                                              (1, 24, 36, 384, 12, 0), (1, 8, 6, 64, 7, 3)])
+def test_layer_norm_window_rows_equals_partition(dtype, B, H, W, C, ws, shift):
+    """The Swin window partition folded into the LayerNorm before it (ops.WindowRows,
+    vs_*layer_norm*_rows): LN(x) / add-LN(x, r) written straight into the window layout ==
+    window_partition of the image-layout result, bit for bit (the same row kernel, only the
+    row it stores moves; padding rows zero); the backward reading grad_y through the same
+    row map gives the same input / weight / bias gradients."""
+    ops = _ops()
+    g = torch.Generator(device="cuda").manual_seed(H * 100 + W + C + shift)
+    x = torch.randn(B, H * W, C, device=DEV, generator=g).to(dtype)
+    r = torch.randn(B, H * W, C, device=DEV, generator=g).to(dtype)
+    w = (1 + 0.1 * torch.randn(C, device=DEV, generator=g)).to(dtype)
+    b = (0.1 * torch.randn(C, device=DEV, generator=g)).to(dtype)
+    wr = ops.window_rows(B, H, W, ws, shift, torch.device(DEV))
+    nw = -(-H // ws) * -(-W // ws)
+    gy = torch.randn(B * nw * ws * ws, C, device=DEV, generator=g).to(dtype)
+    gs = torch.randn(B, H * W, C, device=DEV, generator=g).to(dtype)
+    for add in (False, True):
+        res = []
+        for rows in (True, False):
+            xx, rr, ww, bb = (t.clone().requires_grad_(True) for t in (x, r, w, b))
+            if add:
+                s, y = ops.add_layer_norm(xx, rr, ww, bb, wrows=wr if rows else None)
+            else:
+                s, y = None, ops.layer_norm(xx, ww, bb, wrows=wr if rows else None)
+            if not rows:
+                y = ops.window_partition(y.view(B, H, W, C), ws, shift).view(-1, C)
+            outs = [y] + ([s] if add else [])
+            torch.autograd.backward(outs, [gy] + ([gs] if add else []))
+            res.append([y.detach(), xx.grad, ww.grad, bb.grad] + ([rr.grad, s.detach()] if add else []))
+        torch.cuda.synchronize()
+        for a, c in zip(*res):
+            assert a.shape == c.shape and torch.equal(a, c)

@@ -83,7 +83,8 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ 
                                                           float* __restrict__ mean, float* __restrict__ rstd,
                                                           int M, int C, float eps, int G,
                                                           const T* __restrict__ r = nullptr,
-                                                          T* __restrict__ s_out = nullptr) {
+                                                          T* __restrict__ s_out = nullptr,
+                                                          const int* __restrict__ yrows = nullptr) {
   const int nch = C >> 3;
   const int lane = threadIdx.x & (G - 1);
   const int rows_per_block = kThreads / G;
@@ -161,7 +162,7 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ 
             float o[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mu) * rs * wv[k][i] + bv[k][i];
-            store_chunk(y + row * C + j * 8, o);
+            store_chunk(y + (yrows ? (long long)yrows[row] : row) * C + j * 8, o);
           }
         }
         if (lane == 0) {
@@ -185,7 +186,8 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
                                                           const T* __restrict__ w, const float* __restrict__ mean,
                                                           const float* __restrict__ rstd, T* __restrict__ dx,
                                                           float* __restrict__ part, int M, int C, int G,
-                                                          const T* __restrict__ dres = nullptr) {
+                                                          const T* __restrict__ dres = nullptr,
+                                                          const int* __restrict__ dyrows = nullptr) {
   extern __shared__ float red[];             // [4 waves][NR][C]
   constexpr int NR = CS ? 3 : 2;
   const int nch = C >> 3;
@@ -224,7 +226,7 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
         const int j = lane + k * G;
         if (ok && j < nch) {
           xr[u][k].load(x + row * C + j * 8);
-          dr[u][k].load(dy + row * C + j * 8);
+          dr[u][k].load(dy + (dyrows ? (long long)dyrows[row] : row) * C + j * 8);
           if constexpr (ADD) rr[u][k].load(dres + row * C + j * 8);
         } else {
           xr[u][k].zero();
@@ -626,8 +628,23 @@ using namespace vs;
 // at most 4 chunks of 8 per lane (register budget of the backward): C <= 64 * 32 = 2048
 static int ln_kmax(int) { return 4; }
 
+static int layer_norm_forward_impl(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
+                                   float* rstd, int M, int C, float eps, const int* yrows, void* stream);
+
 extern "C" int vs_layer_norm_forward(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
                                      float* rstd, int M, int C, float eps, void* stream) {
+  return layer_norm_forward_impl(dtype, x, w, b, y, mean, rstd, M, C, eps, nullptr, stream);
+}
+
+extern "C" int vs_layer_norm_forward_rows(int dtype, const void* x, const void* w, const void* b, void* y,
+                                          float* mean, float* rstd, int M, int C, float eps, const int* y_rows,
+                                          void* stream) {
+  VS_CHECK(M == 0 || y_rows, "null pointer");
+  return layer_norm_forward_impl(dtype, x, w, b, y, mean, rstd, M, C, eps, y_rows, stream);
+}
+
+static int layer_norm_forward_impl(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
+                                   float* rstd, int M, int C, float eps, const int* yrows, void* stream) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && b && (M == 0 || (x && y && mean && rstd)), "null pointer");
@@ -639,19 +656,38 @@ extern "C" int vs_layer_norm_forward(int dtype, const void* x, const void* w, co
 #define VS_LNF(KK)                                                                                          \
   if (dtype == VS_BF16)                                                                                     \
     hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK>), dim3(grid), dim3(kThreads), 0, st, (const bf16*)x,        \
-                       (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G);                 \
+                       (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G, nullptr, nullptr, \
+                       yrows);                                                                              \
   else                                                                                                      \
     hipLaunchKernelGGL((ln_fwd_kernel<float, KK>), dim3(grid), dim3(kThreads), 0, st, (const float*)x,      \
-                       (const float*)w, (const float*)b, (float*)y, mean, rstd, M, C, eps, G)
+                       (const float*)w, (const float*)b, (float*)y, mean, rstd, M, C, eps, G, nullptr,      \
+                       nullptr, yrows)
   VS_LN_K(K, VS_LNF)
 #undef VS_LNF
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
 
+static int add_layer_norm_forward_impl(int dtype, const void* x, const void* r, const void* w, const void* b,
+                                       void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
+                                       const int* yrows, void* stream);
+
 extern "C" int vs_add_layer_norm_forward(int dtype, const void* x, const void* r, const void* w, const void* b,
                                          void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
                                          void* stream) {
+  return add_layer_norm_forward_impl(dtype, x, r, w, b, s, y, mean, rstd, M, C, eps, nullptr, stream);
+}
+
+extern "C" int vs_add_layer_norm_forward_rows(int dtype, const void* x, const void* r, const void* w, const void* b,
+                                              void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
+                                              const int* y_rows, void* stream) {
+  VS_CHECK(M == 0 || y_rows, "null pointer");
+  return add_layer_norm_forward_impl(dtype, x, r, w, b, s, y, mean, rstd, M, C, eps, y_rows, stream);
+}
+
+static int add_layer_norm_forward_impl(int dtype, const void* x, const void* r, const void* w, const void* b,
+                                       void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
+                                       const int* yrows, void* stream) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && b && (M == 0 || (x && r && s && y && mean && rstd)), "null pointer");
@@ -664,11 +700,11 @@ extern "C" int vs_add_layer_norm_forward(int dtype, const void* x, const void* r
   if (dtype == VS_BF16)                                                                                       \
     hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, true>), dim3(grid), dim3(kThreads), 0, st, (const bf16*)x,    \
                        (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G, (const bf16*)r,    \
-                       (bf16*)s);                                                                             \
+                       (bf16*)s, yrows);                                                                      \
   else                                                                                                        \
     hipLaunchKernelGGL((ln_fwd_kernel<float, KK, true>), dim3(grid), dim3(kThreads), 0, st, (const float*)x,  \
                        (const float*)w, (const float*)b, (float*)y, mean, rstd, M, C, eps, G, (const float*)r, \
-                       (float*)s)
+                       (float*)s, yrows)
   VS_LN_K(K, VS_ALNF)
 #undef VS_ALNF
   VS_LAUNCH_CHECK();
@@ -689,7 +725,7 @@ extern "C" long long vs_layer_norm_backward_workspace_bytes(int M, int C) {
 
 static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, const void* w, const float* mean,
                                     const float* rstd, const void* dres, void* dx, void* dw, void* db, void* dsum,
-                                    void* ws, int M, int C, void* stream);
+                                    void* ws, int M, int C, void* stream, const int* dyrows = nullptr);
 
 extern "C" int vs_layer_norm_backward(int dtype, const void* dy, const void* x, const void* w, const float* mean,
                                       const float* rstd, void* dx, void* dw, void* db, void* ws, int M, int C,
@@ -710,9 +746,18 @@ extern "C" int vs_layer_norm_backward_ex(int dtype, const void* dy, const void* 
   return layer_norm_backward_impl(dtype, dy, x, w, mean, rstd, dres, dx, dw, db, dx_colsum, ws, M, C, stream);
 }
 
+extern "C" int vs_layer_norm_backward_rows(int dtype, const void* dy, const void* x, const void* w, const float* mean,
+                                           const float* rstd, const void* dres, void* dx, void* dw, void* db,
+                                           void* dx_colsum, void* ws, int M, int C, const int* dy_rows,
+                                           void* stream) {
+  VS_CHECK(M == 0 || dy_rows, "null pointer");
+  return layer_norm_backward_impl(dtype, dy, x, w, mean, rstd, dres, dx, dw, db, dx_colsum, ws, M, C, stream,
+                                  dy_rows);
+}
+
 static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, const void* w, const float* mean,
                                     const float* rstd, const void* dres, void* dx, void* dw, void* db, void* dsum,
-                                    void* ws, int M, int C, void* stream) {
+                                    void* ws, int M, int C, void* stream, const int* dyrows) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && dw && db && ws && (M == 0 || (dy && x && mean && rstd && dx)), "null pointer");
@@ -726,7 +771,7 @@ static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, co
   VS_CHECK(lds <= 64 * 1024, "LayerNorm backward LDS budget exceeded");
 #define VS_LNB_T(TT, KK, AD, CS_)                                                                            \
   hipLaunchKernelGGL((ln_bwd_kernel<TT, KK, AD, CS_>), dim3(grid), dim3(kThreads), lds, st, (const TT*)dy,    \
-                     (const TT*)x, (const TT*)w, mean, rstd, (TT*)dx, part, M, C, G, (const TT*)dres)
+                     (const TT*)x, (const TT*)w, mean, rstd, (TT*)dx, part, M, C, G, (const TT*)dres, dyrows)
 #define VS_LNB_D(TT, KK)                                        \
   if (dres && dsum) VS_LNB_T(TT, KK, true, true);               \
   else if (dres) VS_LNB_T(TT, KK, true, false);                 \

@@ -59,6 +59,9 @@ SIGNATURES = {
     "vs_add_layer_norm_forward": [_c_int] + [_P] * 8 + [_c_int] * 2 + [_c_float, _P],
     "vs_layer_norm_backward_add": [_c_int] + [_P] * 10 + [_c_int] * 2 + [_P],
     "vs_layer_norm_backward_ex": [_c_int] + [_P] * 11 + [_c_int] * 2 + [_P],
+    "vs_layer_norm_forward_rows": [_c_int] + [_P] * 6 + [_c_int] * 2 + [_c_float, _P, _P],
+    "vs_add_layer_norm_forward_rows": [_c_int] + [_P] * 8 + [_c_int] * 2 + [_c_float, _P, _P],
+    "vs_layer_norm_backward_rows": [_c_int] + [_P] * 11 + [_c_int] * 2 + [_P, _P],
     "vs_column_sum_workspace_bytes": [_c_int] * 2,
     "vs_column_sum": [_c_int] + [_P] * 3 + [_c_int] * 2 + [_P],
     "vs_column_sum_segments_workspace_bytes": [_c_int] * 3,

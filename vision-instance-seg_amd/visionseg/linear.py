@@ -385,6 +385,10 @@ class SmallLinear(nn.Linear):
         return small_linear(x, self.weight, self.bias)
 
 
+def _autocast_dtype(t):
+    return torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled() else t.dtype
+
+
 class TokenLayerNorm(nn.LayerNorm):
     """nn.LayerNorm on the HIP row kernel (csrc/norm.hip) for f32 / bf16 device tensors
     whose weight shares their dtype; anything else (autocast's f32 LayerNorm, CPU
@@ -395,6 +399,23 @@ class TokenLayerNorm(nn.LayerNorm):
                 and not torch.is_autocast_enabled():
             return ops.layer_norm(x, self.weight, self.bias, self.eps)
         return F.layer_norm(x, self.normalized_shape, self.weight, self.bias, self.eps)
+
+    def forward_windows(self, x, wrows):
+        """LN(x) in the window layout of wrows (ops.WindowRows: the Swin partition folded
+        into the kernel's stores) -> [wrows.total, C]."""
+        if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
+                and not torch.is_autocast_enabled():
+            return ops.layer_norm(x, self.weight, self.bias, self.eps, wrows=wrows)
+        y = self(x)
+        return ops._to_windows(y.to(_autocast_dtype(y)), wrows)
+
+    def add_forward_windows(self, x, r, wrows, sink=None):
+        """(x + r, LN(x + r) in the window layout of wrows)."""
+        if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
+                and r.shape == x.shape and r.dtype == x.dtype and not torch.is_autocast_enabled():
+            return ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, wrows=wrows)
+        s, y = self.add_forward(x, r, sink)
+        return s, ops._to_windows(y.to(_autocast_dtype(y)), wrows)
 
     def add_forward(self, x, r, sink=None):
         """(x + r, LN(x + r)): the residual add fused into the norm on the HIP kernel

@@ -139,13 +139,14 @@ class SwinBlock(nn.Module):
         caller adds the branch in the next norm (ops.add_layer_norm)."""
         B, L, C = x.shape
         ws, shift = self.ws, self.shift
+        # the window partition folded into the norm's stores (ops.WindowRows): h comes out
+        # in the window layout [B*nW*ws^2, C], padding rows zero
+        wr = ops.window_rows(B, H, W, ws, shift, x.device)
         if res is None:
-            h = self.norm1(x)
+            h = self.norm1.forward_windows(x, wr)
         else:
-            x, h = self.norm1.add_forward(x, res)
-        h = h.view(B, H, W, C)
-        win = ops.window_partition(h.to(_compute_dtype(h)), ws, shift)   # cast first: half the bytes moved
-        qkv = self.attn.qkv(win)
+            x, h = self.norm1.add_forward_windows(x, res, wr)
+        qkv = self.attn.qkv(h.view(-1, ws * ws, C))
         # output in the image layout (window reverse folded into the kernel); the per-token
         # proj commutes with the crop
         o = ops.window_attention_image(qkv, self.attn.rel_table, self.attn.heads, ws, shift, B, H, W,
@@ -279,7 +280,8 @@ def sine_pos_tokens(B, H, W, num_feats, device, dtype):
     once per (shape, device, dtype): it depends on nothing else, so the training step does
     not recompute it (~15 kernels and 67 MB f32 intermediates per 128x128 level).  Never
     cached while a HIP graph is being captured (the entry would live in the graph's pool);
-    the trainer's eager warm-up steps fill the cache first."""
+    the trainer's eager warm-up steps fill the cache first.  An LRU of 32 entries (a full
+    clear could drop an entry between a warm-up and the capture that reads it)."""
     key = (B, H, W, num_feats, str(device), dtype)
     t = _SINE_CACHE.get(key)
     if t is None:
@@ -287,9 +289,11 @@ def sine_pos_tokens(B, H, W, num_feats, device, dtype):
             t = sine_pos_embed(B, H, W, num_feats, device).to(dtype).flatten(2).transpose(1, 2).contiguous()
         capturing = t.is_cuda and torch.cuda.is_current_stream_capturing()
         if not capturing:
-            if len(_SINE_CACHE) >= 32:
-                _SINE_CACHE.clear()
             _SINE_CACHE[key] = t
+            while len(_SINE_CACHE) > 32:               # LRU: the warm-up's entries stay
+                _SINE_CACHE.pop(next(iter(_SINE_CACHE)))
+    else:
+        _SINE_CACHE[key] = _SINE_CACHE.pop(key)        # most recently used last
     return t
 
 
@@ -300,7 +304,7 @@ def cached_constants():
     replays from -- that freed block, reused, made graph replays differ from eager runs
     (tests/test_gpu_model.py::test_predictor_graph_replay_matches_eager after a suite's
     worth of shapes)."""
-    return list(_SINE_CACHE.values())
+    return list(_SINE_CACHE.values()) + ops.window_rows_constants()
 
 
 def reference_points(shapes, B, device, dtype=torch.float32):

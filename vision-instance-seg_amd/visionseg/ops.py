@@ -16,6 +16,7 @@ kernels library is missing or an input is on the CPU.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import ctypes
 import os
@@ -604,23 +605,90 @@ def masked_attention(q, k, v, words, heads: int, scale: float | None = None):
 
 
 # ------------------------------------------------------------------ LayerNorm / bias grad
+class WindowRows:
+    """Window-layout rows of the image tokens of a [B, H, W] grid, for the Swin window
+    partition folded into the LayerNorm before it (HF:swin:546-551: zero pad to multiples
+    of ws, roll by -shift, partition): rows int32 [B*H*W] = the window row of image token
+    m, pad int64 = the window rows of the zero padding, total = B * nWh * nWw * ws^2."""
+
+    def __init__(self, B, H, W, ws, shift, device):
+        self.B, self.H, self.W, self.ws, self.shift = B, H, W, ws, shift
+        nwh, nww = -(-H // ws), -(-W // ws)
+        Hp, Wp = nwh * ws, nww * ws
+        self.total = B * Hp * Wp
+        with torch.no_grad():
+            y = torch.arange(H, device=device).view(1, H, 1)
+            x = torch.arange(W, device=device).view(1, 1, W)
+            b = torch.arange(B, device=device).view(B, 1, 1)
+            py, px = (y - shift) % Hp, (x - shift) % Wp            # padded-grid position of each pixel
+            row = ((b * nwh + py // ws) * nww + px // ws) * (ws * ws) + (py % ws) * ws + px % ws
+            self.rows = row.reshape(-1).to(torch.int32).contiguous()
+            hit = torch.zeros(self.total, dtype=torch.bool, device=device)
+            hit[self.rows.long()] = True
+            self.pad = torch.nonzero(~hit).view(-1)
+
+    def tensors(self):
+        return [self.rows, self.pad]
+
+
+_WROWS: "collections.OrderedDict" = collections.OrderedDict()
+
+
+def window_rows(B, H, W, ws, shift, device):
+    """WindowRows for the shape, made once per (shape, device) and kept in an LRU of 64:
+    the eager warm-up before a HIP graph capture (trainer, predictor) makes every entry
+    the capture reads, the most recently used, so none is evicted before the capture
+    (making one needs a host sync, which a capture refuses; see model.cached_constants
+    for the lifetime of the tensors a graph reads)."""
+    key = (B, H, W, ws, shift, str(device))
+    wr = _WROWS.get(key)
+    if wr is None:
+        wr = WindowRows(B, H, W, ws, shift, device)
+        _WROWS[key] = wr
+        while len(_WROWS) > 64:
+            _WROWS.popitem(last=False)
+    else:
+        _WROWS.move_to_end(key)
+    return wr
+
+
+def window_rows_constants():
+    return [t for wr in _WROWS.values() for t in wr.tensors()]
+
+
+def _to_windows(y, wr):
+    """The window partition of a [B*H*W, C] tensor as the row-mapped kernels lay it out."""
+    return window_partition(y.view(wr.B, wr.H, wr.W, -1), wr.ws, wr.shift).view(wr.total, -1)
+
+
 class LayerNormFunction(torch.autograd.Function):
     """F.layer_norm over the last dim of a token-major [..., C] tensor (csrc/norm.hip);
     x, weight, bias share one dtype (f32 or bf16)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
+    def forward(ctx, x, weight, bias, eps, wrows=None):
+        """wrows (WindowRows): y in the window layout [wrows.total, C] (the partition folded
+        into the kernel's stores; padding rows zero)."""
         L.require_hip(x, weight, bias)
         C = x.shape[-1]
         xc = x.contiguous()
         M = xc.numel() // C
-        y = torch.empty_like(xc)
         mean = torch.empty(M, device=x.device, dtype=torch.float32)
         rstd = torch.empty(M, device=x.device, dtype=torch.float32)
         with timed("layer_norm_fwd", xc, bytes_=2 * xc.numel() * xc.element_size()):
-            L.check(L.lib().vs_layer_norm_forward(L.dtype_code(xc), L.ptr(xc), L.ptr(weight), L.ptr(bias), L.ptr(y),
-                                                  L.ptr(mean), L.ptr(rstd), M, C, float(eps), L.stream(xc)),
-                    "layer_norm_forward")
+            if wrows is None:
+                y = torch.empty_like(xc)
+                L.check(L.lib().vs_layer_norm_forward(L.dtype_code(xc), L.ptr(xc), L.ptr(weight), L.ptr(bias),
+                                                      L.ptr(y), L.ptr(mean), L.ptr(rstd), M, C, float(eps),
+                                                      L.stream(xc)), "layer_norm_forward")
+            else:
+                y = torch.empty(wrows.total, C, device=x.device, dtype=xc.dtype)
+                L.check(L.lib().vs_layer_norm_forward_rows(L.dtype_code(xc), L.ptr(xc), L.ptr(weight), L.ptr(bias),
+                                                           L.ptr(y), L.ptr(mean), L.ptr(rstd), M, C, float(eps),
+                                                           L.ptr(wrows.rows), L.stream(xc)), "layer_norm_forward_rows")
+                if wrows.pad.numel():
+                    y.index_fill_(0, wrows.pad, 0)
+        ctx.wrows = wrows
         ctx.save_for_backward(xc, weight, mean, rstd)
         return y
 
@@ -636,10 +704,16 @@ class LayerNormFunction(torch.autograd.Function):
         ws = torch.empty(int(L.lib().vs_layer_norm_backward_workspace_bytes(M, C)), device=xc.device,
                          dtype=torch.uint8)
         with timed("layer_norm_bwd", xc, bytes_=3 * xc.numel() * xc.element_size()):
-            L.check(L.lib().vs_layer_norm_backward(L.dtype_code(xc), L.ptr(gy), L.ptr(xc), L.ptr(weight), L.ptr(mean),
-                                                   L.ptr(rstd), L.ptr(gx), L.ptr(gw), L.ptr(gb), L.ptr(ws), M, C,
-                                                   L.stream(xc)), "layer_norm_backward")
-        return gx, gw, gb, None
+            if ctx.wrows is None:
+                L.check(L.lib().vs_layer_norm_backward(L.dtype_code(xc), L.ptr(gy), L.ptr(xc), L.ptr(weight),
+                                                       L.ptr(mean), L.ptr(rstd), L.ptr(gx), L.ptr(gw), L.ptr(gb),
+                                                       L.ptr(ws), M, C, L.stream(xc)), "layer_norm_backward")
+            else:
+                L.check(L.lib().vs_layer_norm_backward_rows(L.dtype_code(xc), L.ptr(gy), L.ptr(xc), L.ptr(weight),
+                                                            L.ptr(mean), L.ptr(rstd), None, L.ptr(gx), L.ptr(gw),
+                                                            L.ptr(gb), None, L.ptr(ws), M, C, L.ptr(ctx.wrows.rows),
+                                                            L.stream(xc)), "layer_norm_backward_rows")
+        return gx, gw, gb, None, None
 
 
 def attach_colsum(g: torch.Tensor, colsum: torch.Tensor) -> None:
@@ -663,20 +737,31 @@ class AddLayerNormFunction(torch.autograd.Function):
     backward adds the gradient of s (residual path) inside the LayerNorm backward."""
 
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps, sink=None):
+    def forward(ctx, x, r, weight, bias, eps, sink=None, wrows=None):
+        """wrows (WindowRows): y in the window layout (see LayerNormFunction); s stays in x's."""
         L.require_hip(x, r, weight, bias)
         ctx.sink = sink if sink is not None and sink.armed else None
         C = x.shape[-1]
         xc, rc = x.contiguous(), r.to(x.dtype).contiguous()
         M = xc.numel() // C
         s = torch.empty_like(xc)
-        y = torch.empty_like(xc)
         mean = torch.empty(M, device=x.device, dtype=torch.float32)
         rstd = torch.empty(M, device=x.device, dtype=torch.float32)
         with timed("add_layer_norm_fwd", xc, bytes_=4 * xc.numel() * xc.element_size()):
-            L.check(L.lib().vs_add_layer_norm_forward(L.dtype_code(xc), L.ptr(xc), L.ptr(rc), L.ptr(weight),
-                                                      L.ptr(bias), L.ptr(s), L.ptr(y), L.ptr(mean), L.ptr(rstd), M,
-                                                      C, float(eps), L.stream(xc)), "add_layer_norm_forward")
+            if wrows is None:
+                y = torch.empty_like(xc)
+                L.check(L.lib().vs_add_layer_norm_forward(L.dtype_code(xc), L.ptr(xc), L.ptr(rc), L.ptr(weight),
+                                                          L.ptr(bias), L.ptr(s), L.ptr(y), L.ptr(mean), L.ptr(rstd),
+                                                          M, C, float(eps), L.stream(xc)), "add_layer_norm_forward")
+            else:
+                y = torch.empty(wrows.total, C, device=x.device, dtype=xc.dtype)
+                L.check(L.lib().vs_add_layer_norm_forward_rows(L.dtype_code(xc), L.ptr(xc), L.ptr(rc), L.ptr(weight),
+                                                               L.ptr(bias), L.ptr(s), L.ptr(y), L.ptr(mean),
+                                                               L.ptr(rstd), M, C, float(eps), L.ptr(wrows.rows),
+                                                               L.stream(xc)), "add_layer_norm_forward_rows")
+                if wrows.pad.numel():
+                    y.index_fill_(0, wrows.pad, 0)
+        ctx.wrows = wrows
         ctx.save_for_backward(s, weight, mean, rstd)
         return s, y
 
@@ -698,28 +783,36 @@ class AddLayerNormFunction(torch.autograd.Function):
         cs = torch.empty(C, device=s.device, dtype=s.dtype) if C <= 1024 else None
         with timed("layer_norm_bwd", s, bytes_=(3 + (gs is not None)) * s.numel() * s.element_size()):
             gsc = gs.to(s.dtype).contiguous() if gs is not None else None
-            L.check(L.lib().vs_layer_norm_backward_ex(L.dtype_code(s), L.ptr(gy), L.ptr(s), L.ptr(weight),
-                                                      L.ptr(mean), L.ptr(rstd), L.ptr(gsc) if gsc is not None else None,
-                                                      L.ptr(gx), L.ptr(gw), L.ptr(gb),
-                                                      L.ptr(cs) if cs is not None else None, L.ptr(ws), M, C,
-                                                      L.stream(s)), "layer_norm_backward_ex")
+            if ctx.wrows is None:
+                L.check(L.lib().vs_layer_norm_backward_ex(L.dtype_code(s), L.ptr(gy), L.ptr(s), L.ptr(weight),
+                                                          L.ptr(mean), L.ptr(rstd),
+                                                          L.ptr(gsc) if gsc is not None else None, L.ptr(gx), L.ptr(gw),
+                                                          L.ptr(gb), L.ptr(cs) if cs is not None else None, L.ptr(ws),
+                                                          M, C, L.stream(s)), "layer_norm_backward_ex")
+            else:
+                L.check(L.lib().vs_layer_norm_backward_rows(L.dtype_code(s), L.ptr(gy), L.ptr(s), L.ptr(weight),
+                                                            L.ptr(mean), L.ptr(rstd),
+                                                            L.ptr(gsc) if gsc is not None else None, L.ptr(gx),
+                                                            L.ptr(gw), L.ptr(gb), L.ptr(cs) if cs is not None else None,
+                                                            L.ptr(ws), M, C, L.ptr(ctx.wrows.rows), L.stream(s)),
+                        "layer_norm_backward_rows")
         if cs is not None:
             attach_colsum(gx, cs)
         gxx = gx
         if ctx.sink is not None and ctx.needs_input_grad[0]:
             ctx.sink.g = gx            # the armed consumer of x adds it in its dX GEMM
             gxx = None
-        return gxx, gx, gw, gb, None, None
+        return gxx, gx, gw, gb, None, None, None
 
 
-def add_layer_norm(x, r, weight, bias, eps: float = 1e-5, sink: ResidualSink | None = None):
+def add_layer_norm(x, r, weight, bias, eps: float = 1e-5, sink: ResidualSink | None = None, wrows=None):
     """(x + r, layer_norm(x + r)) for token-major [..., C] tensors (see AddLayerNormFunction;
-    `sink`: see ResidualSink)."""
-    return AddLayerNormFunction.apply(x, r, weight, bias, eps, sink)
+    `sink`: see ResidualSink; `wrows`: y in the window layout)."""
+    return AddLayerNormFunction.apply(x, r, weight, bias, eps, sink, wrows)
 
 
-def layer_norm(x, weight, bias, eps: float = 1e-5):
-    return LayerNormFunction.apply(x, weight, bias, eps)
+def layer_norm(x, weight, bias, eps: float = 1e-5, wrows=None):
+    return LayerNormFunction.apply(x, weight, bias, eps, wrows)
 
 
 def layer_norm_supported(x, weight) -> bool:
