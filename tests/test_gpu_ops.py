@@ -881,9 +881,11 @@ def _check_group_norm(fn, dtype, relu, shape, groups, cl):
 # ------------------------------------------------------------------ small-token Linear
 @pytest.mark.parametrize("T,I,O,bias", [(400, 256, 256, True), (400, 256, 2048, True), (400, 2048, 256, True),
                                         (1, 64, 128, True), (1000, 128, 64, False), (64, 256, 256, True),
-                                        (0, 64, 64, True)])
+                                        (0, 64, 64, True), (130, 64, 64, True), (257, 128, 192, True),
+                                        (2000, 64, 128, True)])
 def test_small_linear_grads_vs_torch(T, I, O, bias):
-    """csrc/small_linear.hip dW / db (+ library dX) vs torch f64 on the same bf16 operands."""
+    """csrc/small_linear.hip dW / db (+ library dX) vs torch f64 on the same bf16 operands
+    (T > 64: the token-split kernel, chunks spread over the four waves, ragged last chunk)."""
     from visionseg.linear import small_linear
     g = torch.Generator().manual_seed(T + I + O)
     x = torch.randn(T, I, generator=g).to(torch.bfloat16)

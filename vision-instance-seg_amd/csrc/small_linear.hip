@@ -113,6 +113,100 @@ __global__ void __launch_bounds__(256) small_wgrad_kernel(const bf16* __restrict
   }
 }
 
+// The same product with the TOKENS split over the four waves: wave w takes the 64-token
+// chunks w, w + 4, ... and accumulates the whole 64 x 64 dW^T block (four 32 x 32 MFMA
+// tiles) from its own LDS staging, so the chunks' loads are in flight at once instead of
+// one after another (400 tokens: two rounds instead of seven); the four partial blocks are
+// then summed in LDS in wave order (fixed order: deterministic).  Same operand layout and
+// output mapping as small_wgrad_kernel.
+__global__ void __launch_bounds__(256) small_wgrad_split_kernel(const bf16* __restrict__ gy,
+                                                                const bf16* __restrict__ x, bf16* __restrict__ dw,
+                                                                bf16* __restrict__ db, int T, int O, int I) {
+  constexpr int kStage = kTC * kPitch;                 // one operand chunk (elements)
+  __shared__ __attribute__((aligned(16))) bf16 sbuf[4 * 2 * kStage];   // per wave: gY, X chunks (96 KB)
+  __shared__ float sB[4][kBlk];
+  const int i0 = blockIdx.x * kBlk, o0 = blockIdx.y * kBlk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  bf16* sG = sbuf + wave * 2 * kStage;
+  bf16* sX = sG + kStage;
+  const bool do_bias = db != nullptr && blockIdx.x == 0;
+  uint4 rg[8], rx[8];
+  auto load = [&](int t0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int p = lane + 64 * k;
+      const int row = p >> 3, c = (p & 7) * 8;
+      const int t = t0 + row;
+      rg[k] = t < T ? *reinterpret_cast<const uint4*>(gy + (size_t)t * O + o0 + c) : make_uint4(0, 0, 0, 0);
+      rx[k] = t < T ? *reinterpret_cast<const uint4*>(x + (size_t)t * I + i0 + c) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) zero16(acc[a][b]);
+  float bsum = 0.f;
+  const int nchunk = (T + kTC - 1) / kTC;
+  if (wave < nchunk) load(wave * kTC);
+  for (int ch = wave; ch < nchunk; ch += 4) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int p = lane + 64 * k;
+      const int row = p >> 3, c = (p & 7) * 8;
+      *reinterpret_cast<uint4*>(sG + row * kPitch + c) = rg[k];
+      *reinterpret_cast<uint4*>(sX + row * kPitch + c) = rx[k];
+    }
+    wave_sync();
+    if (ch + 4 < nchunk) load((ch + 4) * kTC);
+    if (do_bias) {      // column o = lane, this chunk's 64 rows
+#pragma unroll 8
+      for (int j = 0; j < kTC; ++j) bsum += __bfloat162float(sG[j * kPitch + lane]);
+    }
+#pragma unroll
+    for (int st = 0; st < kTC / 16; ++st)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const bf16x8_t fa = tr_frag(sX, 16 * st, 32 * a, lane);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, tr_frag(sG, 16 * st, 32 * b, lane), acc[a][b], 0, 0, 0);
+      }
+    wave_sync();                              // this wave's staging is rewritten next round
+  }
+  __syncthreads();
+  // partial dW^T blocks [wave][i][o] (f32, over the staging) summed in wave order
+  float* red = reinterpret_cast<float*>(sbuf);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        red[(wave * kBlk + 32 * a + crow(k, hh)) * kBlk + 32 * b + r] = acc[a][b][k];
+  if (do_bias) sB[wave][lane] = bsum;
+  __syncthreads();
+  // thread -> o = tid & 63, i quad 4 (tid >> 6) + 16 q: 8-B stores of 4 consecutive i
+#pragma unroll
+  for (int qd = 0; qd < 4; ++qd) {
+    const int o = tid & 63, i = 4 * ((tid >> 6) + 4 * qd);
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) t += red[(w * kBlk + i + e) * kBlk + o];
+      v[e] = t;
+    }
+    uint2 wv;
+    wv.x = pack2(v[0], v[1]);
+    wv.y = pack2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(dw + (size_t)(o0 + o) * I + i0 + i) = wv;
+  }
+  if (do_bias && tid < kBlk) db[o0 + tid] = __float2bfloat16((sB[0][tid] + sB[1][tid]) + (sB[2][tid] + sB[3][tid]));
+}
+
 }  // namespace
 }  // namespace vs
 
@@ -130,9 +224,19 @@ extern "C" int vs_small_linear_wgrad(int dtype, const void* grad_y, const void* 
     return VS_OK;
   }
   VS_CHECK(grad_y && x, "null pointer");
-  hipLaunchKernelGGL(small_wgrad_kernel, dim3(in_features / kBlk, out_features / kBlk), dim3(256), 0,
-                     (hipStream_t)stream, (const bf16*)grad_y, (const bf16*)x, (bf16*)grad_w, (bf16*)grad_b, tokens,
-                     out_features, in_features);
+  // token split over the waves from 2 chunks up (VS_SMALL_WGRAD_SPLIT=0: the chunk-serial kernel, A/B)
+  static const int split = [] {
+    const char* e = getenv("VS_SMALL_WGRAD_SPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  if (split && tokens > kTC)
+    hipLaunchKernelGGL(small_wgrad_split_kernel, dim3(in_features / kBlk, out_features / kBlk), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16*)grad_y, (const bf16*)x, (bf16*)grad_w, (bf16*)grad_b, tokens,
+                       out_features, in_features);
+  else
+    hipLaunchKernelGGL(small_wgrad_kernel, dim3(in_features / kBlk, out_features / kBlk), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16*)grad_y, (const bf16*)x, (bf16*)grad_w, (bf16*)grad_b, tokens,
+                       out_features, in_features);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
