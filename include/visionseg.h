@@ -429,6 +429,20 @@ VS_API int vs_group_norm_nchw_backward(int dtype, const void* grad_y, const void
 VS_API int vs_small_linear_wgrad(int dtype, const void* grad_y, const void* x, void* grad_w, void* grad_b,
                                  int tokens, int out_features, int in_features, void* stream);
 
+/* The same Linear's forward and whole backward, each one launch (bf16, f32 accumulation,
+ * the reduction split over four waves and summed in a fixed order):
+ *   forward:  y [tokens, out] = x [tokens, in] weight[out, in]^T (+ bias[out] when non-NULL)
+ *   backward: grad_x [tokens, in] = grad_y weight (skipped when grad_x is NULL) and
+ *             grad_w / grad_b as vs_small_linear_wgrad (skipped when grad_w is NULL),
+ *             the two products in one grid.
+ * Replaces autograd's addmm forward and its mm input gradient for the decoder Linears
+ * above (torch.nn.functional.linear / LinearBackward). */
+VS_API int vs_small_linear_forward(int dtype, const void* x, const void* weight, const void* bias, void* y,
+                                   int tokens, int out_features, int in_features, void* stream);
+VS_API int vs_small_linear_backward(int dtype, const void* grad_y, const void* x, const void* weight,
+                                    void* grad_x, void* grad_w, void* grad_b, int tokens, int out_features,
+                                    int in_features, void* stream);
+
 /* ---- activation backward + bias gradient (csrc/norm.hip) ------------------------------
  * dx = dy * act'(x) for act 0 = ReLU, 1 = exact GELU (torch's F.gelu, approximate='none'),
  * x the activation's input, all [M, N] dtype; dx_colsum [N] dtype = column sums of dx as

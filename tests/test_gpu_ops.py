@@ -884,8 +884,9 @@ def _check_group_norm(fn, dtype, relu, shape, groups, cl):
                                         (0, 64, 64, True), (130, 64, 64, True), (257, 128, 192, True),
                                         (2000, 64, 128, True)])
 def test_small_linear_grads_vs_torch(T, I, O, bias):
-    """csrc/small_linear.hip dW / db (+ library dX) vs torch f64 on the same bf16 operands
-    (T > 64: the token-split kernel, chunks spread over the four waves, ragged last chunk)."""
+    """csrc/small_linear.hip forward Y, dX and dW / db (one backward launch) vs torch f64 on
+    the same bf16 operands (T > 64: the token-split dW, chunks spread over the four waves,
+    ragged last chunk; T % 32 != 0: ragged token tiles of the forward / dX)."""
     from visionseg.linear import small_linear
     g = torch.Generator().manual_seed(T + I + O)
     x = torch.randn(T, I, generator=g).to(torch.bfloat16)
@@ -899,12 +900,37 @@ def test_small_linear_grads_vs_torch(T, I, O, bias):
     y.backward(gy.to(DEV))
     xr, wr = x.double().requires_grad_(True), w.double().requires_grad_(True)
     br = b.double().requires_grad_(True) if bias else None
-    torch.nn.functional.linear(xr, wr, br).backward(gy.double())
-    pairs = [("dx", xd.grad, xr.grad), ("dw", wd.grad, wr.grad)] + ([("db", bd.grad, br.grad)] if bias else [])
+    yr = torch.nn.functional.linear(xr, wr, br)
+    yr.backward(gy.double())
+    pairs = [("y", y.detach(), yr.detach()), ("dx", xd.grad, xr.grad), ("dw", wd.grad, wr.grad)] + \
+        ([("db", bd.grad, br.grad)] if bias else [])
     for name, got, exp in pairs:
         e = float((got.double().cpu() - exp).abs().max()) if exp.numel() else 0.0
         scale = float(exp.abs().max()) if exp.numel() else 0.0
         assert e <= 2 ** -7 * max(1.0, scale) + 1e-3, (name, e, scale)
+
+
+@pytest.mark.parametrize("need", ["x", "w"])
+def test_small_linear_partial_backward(need):
+    """Only dX (frozen weight) or only dW / db (input without grad) requested: the fused
+    backward launches just that half; the result equals the full backward's."""
+    from visionseg.linear import _SmallLinearFn
+    small_linear = _SmallLinearFn.apply
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(4, 100, 256, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(512, 256, generator=g) / 16).to(torch.bfloat16).to(DEV)
+    b = torch.randn(512, generator=g).to(torch.bfloat16).to(DEV)
+    gy = torch.randn(4, 100, 512, generator=g).to(torch.bfloat16).to(DEV)
+    xf, wf, bf = (t.clone().requires_grad_(True) for t in (x, w, b))
+    small_linear(xf, wf, bf).backward(gy)
+    xp = x.clone().requires_grad_(need == "x")
+    wp = w.clone().requires_grad_(need == "w")
+    bp = b.clone().requires_grad_(need == "w")
+    small_linear(xp, wp, bp).backward(gy)
+    if need == "x":
+        assert wp.grad is None and bp.grad is None and torch.equal(xp.grad, xf.grad)
+    else:
+        assert xp.grad is None and torch.equal(wp.grad, wf.grad) and torch.equal(bp.grad, bf.grad)
 
 
 def test_small_linear_weight_slice():

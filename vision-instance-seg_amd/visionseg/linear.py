@@ -192,15 +192,29 @@ SMALL_MAX_TOKENS = 4096
 _SMALL = os.environ.get("VS_SMALL_LINEAR", "1") == "1"      # A/B switch
 
 
+_SMALL_FUSED = os.environ.get("VS_SMALL_LINEAR_FUSED", "1") == "1"   # A/B: library forward / dX GEMMs
+
+
 class _SmallLinearFn(torch.autograd.Function):
-    """Linear over a few hundred tokens: forward / dX are library GEMMs, dW and db one HIP
-    launch (csrc/small_linear.hip) instead of a single-tile GEMM plus a reduction."""
+    """Linear over a few hundred tokens on csrc/small_linear.hip: the forward one launch
+    (Y = X W^T + b, vs_small_linear_forward) and the whole backward one launch (dX = dY W
+    and the token-split dW / db in one grid, vs_small_linear_backward) -- autograd ran an
+    addmm forward and an mm + a single-tile dW GEMM + a bias reduction backward.
+    VS_SMALL_LINEAR_FUSED=0: library forward / dX GEMMs, dW and db by vs_small_linear_wgrad."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        return F.linear(x, weight, bias)
+        if not _SMALL_FUSED:
+            return F.linear(x, weight, bias)
+        O, I = weight.shape
+        x2 = x.reshape(-1, I).contiguous()
+        y = torch.empty(x2.shape[0], O, device=x.device, dtype=torch.bfloat16)
+        L.check(L.lib().vs_small_linear_forward(L.dtype_code(y), L.ptr(x2), L.ptr(weight.contiguous()),
+                                                L.ptr(bias) if bias is not None else None, L.ptr(y),
+                                                x2.shape[0], O, I, L.stream(x2)), "small_linear_forward")
+        return y.view(*x.shape[:-1], O)
 
     @staticmethod
     def backward(ctx, gy):
@@ -208,17 +222,32 @@ class _SmallLinearFn(torch.autograd.Function):
         O, I = weight.shape
         gy2 = gy.reshape(-1, O).contiguous()
         gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = (gy2 @ weight).view(x.shape)
-        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            x2 = x.reshape(-1, I).contiguous()
+        want_w = ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2])
+        x2 = x.reshape(-1, I).contiguous()
+        if want_w:
             gw = torch.empty(O, I, device=gy2.device, dtype=torch.bfloat16)
             gb = torch.empty(O, device=gy2.device, dtype=torch.bfloat16) if ctx.has_bias else None
-            L.check(L.lib().vs_small_linear_wgrad(L.dtype_code(gw), L.ptr(gy2), L.ptr(x2), L.ptr(gw),
-                                                  L.ptr(gb) if gb is not None else None, gy2.shape[0], O, I,
-                                                  L.stream(gy2)), "small_linear_wgrad")
-            if not ctx.needs_input_grad[1]:
-                gw = None
+        if _SMALL_FUSED:
+            if ctx.needs_input_grad[0]:
+                gx = torch.empty(gy2.shape[0], I, device=gy2.device, dtype=torch.bfloat16)
+            if gx is not None or gw is not None:
+                L.check(L.lib().vs_small_linear_backward(
+                    L.dtype_code(gy2), L.ptr(gy2), L.ptr(x2), L.ptr(weight.contiguous()),
+                    L.ptr(gx) if gx is not None else None, L.ptr(gw) if gw is not None else None,
+                    L.ptr(gb) if gb is not None else None, gy2.shape[0], O, I, L.stream(gy2)), "small_linear_backward")
+            if gx is not None:
+                gx = gx.view(x.shape)
+        else:
+            if ctx.needs_input_grad[0]:
+                gx = (gy2 @ weight).view(x.shape)
+            if want_w:
+                L.check(L.lib().vs_small_linear_wgrad(L.dtype_code(gw), L.ptr(gy2), L.ptr(x2), L.ptr(gw),
+                                                      L.ptr(gb) if gb is not None else None, gy2.shape[0], O, I,
+                                                      L.stream(gy2)), "small_linear_wgrad")
+        if not ctx.needs_input_grad[1]:
+            gw = None
+        if not (ctx.has_bias and ctx.needs_input_grad[2]):
+            gb = None
         return gx, gw, gb
 
 
