@@ -443,6 +443,26 @@ VS_API int vs_small_linear_backward(int dtype, const void* grad_y, const void* x
                                     void* grad_x, void* grad_w, void* grad_b, int tokens, int out_features,
                                     int in_features, void* stream);
 
+/* The self-attention input projections of a masked-attention decoder layer (HF:m2f
+ * Mask2FormerMaskedAttentionDecoderLayer.forward_post: q = k = hidden + query_pos,
+ * v = hidden; Mask2FormerAttention q_proj / k_proj / v_proj), bf16, [tokens, dim] rows,
+ * dim x dim weights, arrays of 3 pointers in q, k, v order:
+ *   forward:  outs[0] = (h + pos) Wq^T + bq, outs[1] = (h + pos) Wk^T + bk,
+ *             outs[2] = h Wv^T + bv                     -- one launch
+ *   backward: grad_pos = dq Wq + dk Wk (may be NULL), grad_h = grad_pos + dv Wv, and the
+ *             three weight / bias gradients              -- one launch
+ * pos row of token t is t % pos_rows (pos_rows = queries: the query-position table
+ * broadcast over the batch; = tokens: a full tensor); grad_pos is per token [tokens, dim].
+ * h + pos is rounded to bf16 before the products (torch's bf16 add).  Replaces the add,
+ * three Linear forwards and their backwards plus autograd's gradient adds. */
+VS_API int vs_self_attn_in_proj_forward(int dtype, const void* h, const void* pos, int pos_rows,
+                                        const void* const* weights, const void* const* biases, void* const* outs,
+                                        int tokens, int dim, void* stream);
+VS_API int vs_self_attn_in_proj_backward(int dtype, const void* h, const void* pos, int pos_rows,
+                                         const void* const* weights, const void* const* grad_outs, void* grad_h,
+                                         void* grad_pos, void* const* grad_weights, void* const* grad_biases,
+                                         int tokens, int dim, void* stream);
+
 /* ---- activation backward + bias gradient (csrc/norm.hip) ------------------------------
  * dx = dy * act'(x) for act 0 = ReLU, 1 = exact GELU (torch's F.gelu, approximate='none'),
  * x the activation's input, all [M, N] dtype; dx_colsum [N] dtype = column sums of dx as

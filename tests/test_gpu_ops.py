@@ -933,6 +933,52 @@ def test_small_linear_partial_backward(need):
         assert xp.grad is None and torch.equal(wp.grad, wf.grad) and torch.equal(bp.grad, bf.grad)
 
 
+@pytest.mark.parametrize("B,Q,D,expand", [(4, 100, 256, True), (4, 100, 256, False), (2, 37, 128, True),
+                                         (1, 300, 64, False)])
+def test_self_attn_in_proj_vs_torch(B, Q, D, expand):
+    """linear.self_attn_in_proj (one forward, one backward launch: q, k from h + pos, v from
+    h, every gradient use summed in-kernel) vs torch f64 on the same bf16 operands: q / k /
+    v, dh, dpos (through the batch expand of the query-position table when expand=True),
+    dW / db of the three projections.  h + pos is rounded to bf16 first, as torch's add."""
+    from visionseg.linear import SmallLinear, self_attn_in_proj
+    g = torch.Generator().manual_seed(B * Q + D)
+    h = torch.randn(B, Q, D, generator=g).to(torch.bfloat16)
+    table = torch.randn(Q, D, generator=g).to(torch.bfloat16)
+    full = torch.randn(B, Q, D, generator=g).to(torch.bfloat16)
+    lins = [SmallLinear(D, D).to(torch.bfloat16) for _ in range(3)]
+    for m in lins:
+        with torch.no_grad():
+            m.weight.copy_((torch.randn(D, D, generator=g) / D ** 0.5).to(torch.bfloat16))
+            m.bias.copy_(torch.randn(D, generator=g).to(torch.bfloat16))
+    gys = [torch.randn(B, Q, D, generator=g).to(torch.bfloat16) for _ in range(3)]
+    dl = [SmallLinear(D, D).to(torch.bfloat16).to(DEV) for _ in range(3)]
+    for a, m in zip(dl, lins):
+        a.load_state_dict(m.state_dict())
+    hd = h.to(DEV).requires_grad_(True)
+    src = (table if expand else full).to(DEV).requires_grad_(True)
+    pd = src.unsqueeze(0).expand(B, -1, -1) if expand else src
+    outs = self_attn_in_proj(hd, pd, *dl)
+    torch.autograd.backward(outs, [t.to(DEV) for t in gys])
+    hr = h.double().requires_grad_(True)
+    sr = (table if expand else full).double().requires_grad_(True)
+    pr = sr.unsqueeze(0).expand(B, -1, -1) if expand else sr
+    wr = [(m.weight.detach().double().requires_grad_(True), m.bias.detach().double().requires_grad_(True))
+          for m in lins]
+    hq = (h.float() + (table.float() if expand else full.float())).to(torch.bfloat16).double()  # bf16 add
+    hq = hq + (hr + pr - (hr + pr).detach())                       # value of the rounded add, grads of h + pos
+    F_ = torch.nn.functional
+    ref = [F_.linear(hq, *wr[0]), F_.linear(hq, *wr[1]), F_.linear(hr, *wr[2])]
+    torch.autograd.backward(ref, [t.double() for t in gys])
+    pairs = [("q", outs[0], ref[0]), ("k", outs[1], ref[1]), ("v", outs[2], ref[2]), ("dh", hd.grad, hr.grad),
+             ("dpos", src.grad, sr.grad)]
+    for i, (a, (w_, b_)) in enumerate(zip(dl, wr)):
+        pairs += [(f"dw{i}", a.weight.grad, w_.grad), (f"db{i}", a.bias.grad, b_.grad)]
+    for name, got, exp in pairs:
+        e = float((got.detach().double().cpu() - exp.detach()).abs().max())
+        scale = float(exp.detach().abs().max())
+        assert e <= 2 ** -7 * max(1.0, scale) + 1e-3, (name, e, scale)
+
+
 def test_small_linear_weight_slice():
     """A weight slice (the decoder's cross-attention q rows of in_proj_weight) gets its
     gradient rows back through autograd's slice."""

@@ -122,9 +122,30 @@ __global__ void __launch_bounds__(256) small_wgrad_kernel(const bf16* __restrict
 constexpr int kStage = kTC * kPitch;                   // one operand chunk (elements)
 constexpr int kSplitLds = 4 * 2 * kStage;               // per wave: gY, X chunks (96 KB)
 
+// x + pos rounded to bf16 (torch's bf16 add: f32 sum, one rounding), 8 elements
+__device__ __forceinline__ uint4 add_bf16x8(uint4 a, uint4 b) {
+  const uint32_t* pa = reinterpret_cast<const uint32_t*>(&a);
+  const uint32_t* pb = reinterpret_cast<const uint32_t*>(&b);
+  uint4 o;
+  uint32_t* po = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    po[j] = pack2(bf16_bits_to_f32(pa[j] & 0xffffu) + bf16_bits_to_f32(pb[j] & 0xffffu),
+                  bf16_bits_to_f32(pa[j] >> 16) + bf16_bits_to_f32(pb[j] >> 16));
+  return o;
+}
+
+__device__ __forceinline__ bf16x8_t add8(bf16x8_t a, bf16x8_t b) {
+  const uint4 o = add_bf16x8(*reinterpret_cast<const uint4*>(&a), *reinterpret_cast<const uint4*>(&b));
+  return *reinterpret_cast<const bf16x8_t*>(&o);
+}
+
+// pos (may be NULL): the x operand is x + pos (the decoder's query + query-position input),
+// pos row t % prows (prows = Q: one query-position table broadcast over the batch)
 __device__ __forceinline__ void wgrad_split_block(bf16* sbuf, float (*sB)[kBlk], int bx, int by,
                                                   const bf16* __restrict__ gy, const bf16* __restrict__ x,
-                                                  bf16* __restrict__ dw, bf16* __restrict__ db, int T, int O, int I) {
+                                                  bf16* __restrict__ dw, bf16* __restrict__ db, int T, int O, int I,
+                                                  const bf16* __restrict__ pos = nullptr, int prows = 1) {
   const int i0 = bx * kBlk, o0 = by * kBlk;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -140,6 +161,8 @@ __device__ __forceinline__ void wgrad_split_block(bf16* sbuf, float (*sB)[kBlk],
       const int t = t0 + row;
       rg[k] = t < T ? *reinterpret_cast<const uint4*>(gy + (size_t)t * O + o0 + c) : make_uint4(0, 0, 0, 0);
       rx[k] = t < T ? *reinterpret_cast<const uint4*>(x + (size_t)t * I + i0 + c) : make_uint4(0, 0, 0, 0);
+      if (pos && t < T)
+        rx[k] = add_bf16x8(rx[k], *reinterpret_cast<const uint4*>(pos + (size_t)(t % prows) * I + i0 + c));
     }
   };
   f32x16_t acc[2][2];
@@ -228,38 +251,45 @@ __global__ void __launch_bounds__(256) small_wgrad_split_kernel(const bf16* __re
 constexpr int kRT = 32;          // output tile edge
 constexpr int kWC = 64;          // W rows per LDS chunk (input-gradient path)
 
+// One wave's partial product over k in [kb, kb + klen) (klen a multiple of 16) for the
+// tile (features f0.., tokens t0..): !TRANS_A: A = W rows [f][k]; TRANS_A: A = W^T, W rows
+// k, columns f (staged through this wave's LDS chunk sW).  B = token rows of bmat (ldb
+// elements per row) + pos row t % prows (pos may be NULL).
 template <bool TRANS_A>
-__device__ __forceinline__ void reduce_tile(bf16* sbuf, int tt, int ft, const bf16* __restrict__ w,
-                                            const bf16* __restrict__ bmat, const bf16* __restrict__ bias,
-                                            bf16* __restrict__ out, int T, int K, int ldw, int F) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, hh = lane >> 5;
-  const int t0 = tt * kRT, f0 = ft * kRT;
-  const int kq = K / 4, kb = wave * kq;                       // this wave's K quarter (multiple of 16)
+__device__ __forceinline__ f32x16_t tile_partial(bf16* sW, const bf16* __restrict__ w, int ldw,
+                                                 const bf16* __restrict__ bmat, const bf16* __restrict__ pos, int ldb,
+                                                 int kb, int klen, int T, int t0, int f0, int prows = 1) {
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int t = t0 + r;
-  const bf16* brow = bmat + (size_t)min(t, T - 1) * K + kb + 8 * hh;   // B: token row t, k contiguous
   const bool tv = t < T;
+  const int tc = min(t, T - 1);
+  const size_t boff = (size_t)tc * ldb + kb + 8 * hh;             // B: token row t, k contiguous
+  const size_t poff = (size_t)(tc % prows) * ldb + kb + 8 * hh;
+  auto ldb8 = [&](int k) {
+    if (!tv) return zero8();
+    const bf16x8_t v = ld8(bmat + boff + k);
+    return pos ? add8(v, ld8(pos + poff + k)) : v;
+  };
   f32x16_t acc;
   zero16(acc);
   if (!TRANS_A) {
-    const bf16* arow = w + (size_t)(f0 + r) * ldw + kb + 8 * hh;       // A: W row o = f0 + r
-    for (int k = 0; k < kq; k += 64) {
+    const bf16* arow = w + (size_t)(f0 + r) * ldw + kb + 8 * hh;     // A: W row f0 + r
+    for (int k = 0; k < klen; k += 64) {
       bf16x8_t a[4], b[4];
-      const int ns = min(4, (kq - k) >> 4);
+      const int ns = min(4, (klen - k) >> 4);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
         if (s < ns) {
           a[s] = ld8(arow + k + 16 * s);
-          b[s] = tv ? ld8(brow + k + 16 * s) : zero8();
+          b[s] = ldb8(k + 16 * s);
         }
 #pragma unroll
       for (int s = 0; s < 4; ++s)
         if (s < ns) acc = mfma16(a[s], b[s], acc);
     }
   } else {
-    bf16* sW = sbuf + wave * kWC * kPitch;                    // this wave's W chunk [o][32 i]
-    for (int k = 0; k < kq; k += kWC) {
-      const int rows = min(kWC, kq - k);
+    for (int k = 0; k < klen; k += kWC) {
+      const int rows = min(kWC, klen - k);
       uint4 wv[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {                           // 64 rows x 64 B: lane -> (row, 16-B piece)
@@ -269,7 +299,7 @@ __device__ __forceinline__ void reduce_tile(bf16* sbuf, int tt, int ft, const bf
       }
       bf16x8_t b[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) b[s] = (tv && 16 * s < rows) ? ld8(brow + k + 16 * s) : zero8();
+      for (int s = 0; s < 4; ++s) b[s] = 16 * s < rows ? ldb8(k + 16 * s) : zero8();
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int p = lane + 64 * q, row = p >> 2, c = (p & 3) * 8;
@@ -282,28 +312,51 @@ __device__ __forceinline__ void reduce_tile(bf16* sbuf, int tt, int ft, const bf
       wave_sync();                                            // the chunk is rewritten next round
     }
   }
+  return acc;
+}
+
+// The four waves' partials -> LDS [wave][feature 32][token 32] (f32), after a barrier
+__device__ __forceinline__ float* stash_partials(bf16* sbuf, const f32x16_t& acc) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, hh = lane >> 5;
   __syncthreads();
-  float* red = reinterpret_cast<float*>(sbuf);                // [wave][feature 32][token 32]
+  float* red = reinterpret_cast<float*>(sbuf);
 #pragma unroll
   for (int i = 0; i < 16; ++i) red[(wave * kRT + crow(i, hh)) * kRT + r] = acc[i];
   __syncthreads();
-  {  // thread -> token tid & 31, features 4 (tid >> 5) .. + 3
-    const int tk = tid & 31, fq = 4 * (tid >> 5), tg = t0 + tk;
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float s_ = red[(0 * kRT + fq + e) * kRT + tk];
-#pragma unroll
-      for (int wv_ = 1; wv_ < 4; ++wv_) s_ += red[(wv_ * kRT + fq + e) * kRT + tk];
-      v[e] = bias ? s_ + __bfloat162float(bias[f0 + fq + e]) : s_;
-    }
-    if (tg < T) {
-      uint2 o;
-      o.x = pack2(v[0], v[1]);
-      o.y = pack2(v[2], v[3]);
-      *reinterpret_cast<uint2*>(out + (size_t)tg * F + f0 + fq) = o;
-    }
+  return red;
+}
+
+// thread -> token tid & 31, features 4 (tid >> 5) .. + 3: 8-B store of 4 values
+__device__ __forceinline__ void store_quad(bf16* __restrict__ out, int ld, int T, int t0, int f0, const float* v) {
+  const int tid = threadIdx.x, tg = t0 + (tid & 31), fq = 4 * (tid >> 5);
+  if (tg < T) {
+    uint2 o;
+    o.x = pack2(v[0], v[1]);
+    o.y = pack2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(out + (size_t)tg * ld + f0 + fq) = o;
   }
+}
+
+template <bool TRANS_A>
+__device__ __forceinline__ void reduce_tile(bf16* sbuf, int tt, int ft, const bf16* __restrict__ w,
+                                            const bf16* __restrict__ bmat, const bf16* __restrict__ pos,
+                                            const bf16* __restrict__ bias, bf16* __restrict__ out, int T, int K,
+                                            int ldw, int F, int prows = 1) {
+  const int wave = threadIdx.x >> 6;
+  const int t0 = tt * kRT, f0 = ft * kRT, kq = K / 4;        // this wave's K quarter (multiple of 16)
+  const f32x16_t acc = tile_partial<TRANS_A>(sbuf + wave * kWC * kPitch, w, ldw, bmat, pos, K, wave * kq, kq, T,
+                                             t0, f0, prows);
+  const float* red = stash_partials(sbuf, acc);
+  const int tk = threadIdx.x & 31, fq = 4 * (threadIdx.x >> 5);
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float s_ = red[(0 * kRT + fq + e) * kRT + tk];
+#pragma unroll
+    for (int w_ = 1; w_ < 4; ++w_) s_ += red[(w_ * kRT + fq + e) * kRT + tk];
+    v[e] = bias ? s_ + __bfloat162float(bias[f0 + fq + e]) : s_;
+  }
+  store_quad(out, F, T, t0, f0, v);
 }
 
 // grid (ceil(T / 32), O / 32): y [T, O] = x [T, I] w[O, I]^T + b
@@ -311,7 +364,7 @@ __global__ void __launch_bounds__(256) small_fwd_kernel(const bf16* __restrict__
                                                         const bf16* __restrict__ b, bf16* __restrict__ y, int T,
                                                         int O, int I) {
   __shared__ __attribute__((aligned(16))) bf16 sbuf[4 * kRT * kRT * 2];   // the f32 reduction (16 KB)
-  reduce_tile<false>(sbuf, blockIdx.x, blockIdx.y, w, x, b, y, T, I, I, O);
+  reduce_tile<false>(sbuf, blockIdx.x, blockIdx.y, w, x, nullptr, b, y, T, I, I, O);
 }
 
 // One launch for the whole backward: blocks [0, nx) are dX tiles (ceil(T / 32) x I / 32,
@@ -325,10 +378,69 @@ __global__ void __launch_bounds__(256) small_bwd_kernel(const bf16* __restrict__
   const int blk = blockIdx.x;
   const int ntt = (T + kRT - 1) / kRT;
   if (blk < nx) {
-    reduce_tile<true>(sbuf, blk % ntt, blk / ntt, w, gy, nullptr, dx, T, O, I, I);
+    reduce_tile<true>(sbuf, blk % ntt, blk / ntt, w, gy, nullptr, nullptr, dx, T, O, I, I);
   } else {
     const int wb = blk - nx, nbx = I / kBlk;
     wgrad_split_block(sbuf, sB, wb % nbx, wb / nbx, gy, x, dw, db, T, O, I);
+  }
+}
+
+// ---- the self-attention input projections of a decoder layer ------------------------------
+// q = (h + pos) Wq^T + bq, k = (h + pos) Wk^T + bk, v = h Wv^T + bv (HF:m2f
+// Mask2FormerAttention: queries and keys carry the query position embedding, values do
+// not), all [T, D] with D x D weights.  Forward: one launch, the tile's group picked by its
+// feature block, h + pos formed in the operand loads (bf16-rounded like torch's add).
+// Backward: one launch --
+//   dpos = dq Wq + dk Wk             (the position embedding's gradient)
+//   dh   = dpos + dv Wv              (h's, every use summed in-kernel: no autograd adds)
+// per dX tile wave 0 takes the q term, wave 1 the k term, waves 2 / 3 the two halves of the
+// v term, summed in that order; plus the three groups' token-split dW / db blocks.
+struct QkvPtrs {
+  const bf16* w[3];
+  const bf16* b[3];
+  bf16* y[3];
+  const bf16* dy[3];
+  bf16* dw[3];
+  bf16* db[3];
+};
+
+__global__ void __launch_bounds__(256) qkv_fwd_kernel(const bf16* __restrict__ h, const bf16* __restrict__ pos,
+                                                      QkvPtrs p, int T, int D, int prows) {
+  __shared__ __attribute__((aligned(16))) bf16 sbuf[4 * kRT * kRT * 2];
+  const int fpg = D / kRT, g = blockIdx.y / fpg, ft = blockIdx.y % fpg;
+  reduce_tile<false>(sbuf, blockIdx.x, ft, p.w[g], h, g < 2 ? pos : nullptr, p.b[g], p.y[g], T, D, D, D, prows);
+}
+
+__global__ void __launch_bounds__(256) qkv_bwd_kernel(const bf16* __restrict__ h, const bf16* __restrict__ pos,
+                                                      QkvPtrs p, bf16* __restrict__ dh, bf16* __restrict__ dpos,
+                                                      int T, int D, int nx, int prows) {
+  __shared__ __attribute__((aligned(16))) bf16 sbuf[kSplitLds];
+  __shared__ float sB[4][kBlk];
+  const int blk = blockIdx.x;
+  const int ntt = (T + kRT - 1) / kRT;
+  if (blk < nx) {
+    const int wave = threadIdx.x >> 6;
+    const int t0 = (blk % ntt) * kRT, f0 = (blk / ntt) * kRT;
+    const int g = wave < 2 ? wave : 2;
+    const int kb = wave < 2 ? 0 : (wave - 2) * (D / 2), klen = wave < 2 ? D : D / 2;
+    const f32x16_t acc = tile_partial<true>(sbuf + wave * kWC * kPitch, p.w[g], D, p.dy[g], nullptr, D, kb, klen,
+                                            T, t0, f0);
+    const float* red = stash_partials(sbuf, acc);
+    const int tk = threadIdx.x & 31, fq = 4 * (threadIdx.x >> 5);
+    float vp[4], vh[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int o = (fq + e) * kRT + tk;
+      vp[e] = red[0 * kRT * kRT + o] + red[1 * kRT * kRT + o];
+      vh[e] = vp[e] + (red[2 * kRT * kRT + o] + red[3 * kRT * kRT + o]);
+    }
+    if (dpos) store_quad(dpos, D, T, t0, f0, vp);
+    store_quad(dh, D, T, t0, f0, vh);
+  } else {
+    const int nb = (D / kBlk) * (D / kBlk);
+    const int wb = blk - nx, g = wb / nb, r_ = wb % nb;
+    wgrad_split_block(sbuf, sB, r_ % (D / kBlk), r_ / (D / kBlk), p.dy[g], h, p.dw[g], p.db[g], T, D, D,
+                      g < 2 ? pos : nullptr, prows);
   }
 }
 
@@ -400,6 +512,61 @@ extern "C" int vs_small_linear_backward(int dtype, const void* grad_y, const voi
   hipLaunchKernelGGL(small_bwd_kernel, dim3(nx + nw), dim3(256), 0, st, (const bf16*)grad_y, (const bf16*)x,
                      (const bf16*)weight, (bf16*)grad_x, (bf16*)grad_w, (bf16*)grad_b, tokens, out_features,
                      in_features, nx);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_self_attn_in_proj_forward(int dtype, const void* h, const void* pos, int pos_rows,
+                                            const void* const* weights, const void* const* biases, void* const* outs,
+                                            int tokens, int dim, void* stream) {
+  VS_CHECK(dtype == VS_BF16, "the small-token Linear is the bf16 path");
+  VS_CHECK(tokens >= 0 && dim > 0 && dim % kBlk == 0, "dim must be a positive multiple of 64");
+  VS_CHECK(pos_rows > 0 && tokens % pos_rows == 0, "pos_rows must divide tokens");
+  if (tokens == 0) return VS_OK;
+  VS_CHECK(h && pos && weights && biases && outs, "null pointer");
+  QkvPtrs p{};
+  for (int g = 0; g < 3; ++g) {
+    VS_CHECK(weights[g] && biases[g] && outs[g], "null pointer");
+    p.w[g] = (const bf16*)weights[g];
+    p.b[g] = (const bf16*)biases[g];
+    p.y[g] = (bf16*)outs[g];
+  }
+  hipLaunchKernelGGL(qkv_fwd_kernel, dim3((tokens + kRT - 1) / kRT, 3 * dim / kRT), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)h, (const bf16*)pos, p, tokens, dim, pos_rows);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_self_attn_in_proj_backward(int dtype, const void* h, const void* pos, int pos_rows,
+                                             const void* const* weights, const void* const* grad_outs, void* grad_h,
+                                             void* grad_pos, void* const* grad_weights, void* const* grad_biases,
+                                             int tokens, int dim, void* stream) {
+  VS_CHECK(dtype == VS_BF16, "the small-token Linear is the bf16 path");
+  VS_CHECK(tokens >= 0 && dim > 0 && dim % kBlk == 0, "dim must be a positive multiple of 64");
+  VS_CHECK(pos_rows > 0 && tokens % pos_rows == 0, "pos_rows must divide tokens");
+  VS_CHECK(grad_h && grad_weights && grad_biases, "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  if (tokens == 0) {
+    for (int g = 0; g < 3; ++g) {
+      VS_CHECK(grad_weights[g] && grad_biases[g], "null pointer");
+      VS_HIP(hipMemsetAsync(grad_weights[g], 0, (size_t)dim * dim * 2, st));
+      VS_HIP(hipMemsetAsync(grad_biases[g], 0, (size_t)dim * 2, st));
+    }
+    return VS_OK;
+  }
+  VS_CHECK(h && pos && weights && grad_outs, "null pointer");
+  QkvPtrs p{};
+  for (int g = 0; g < 3; ++g) {
+    VS_CHECK(weights[g] && grad_outs[g] && grad_weights[g] && grad_biases[g], "null pointer");
+    p.w[g] = (const bf16*)weights[g];
+    p.dy[g] = (const bf16*)grad_outs[g];
+    p.dw[g] = (bf16*)grad_weights[g];
+    p.db[g] = (bf16*)grad_biases[g];
+  }
+  const int nx = ((tokens + kRT - 1) / kRT) * (dim / kRT);
+  const int nw = 3 * (dim / kBlk) * (dim / kBlk);
+  hipLaunchKernelGGL(qkv_bwd_kernel, dim3(nx + nw), dim3(256), 0, st, (const bf16*)h, (const bf16*)pos, p,
+                     (bf16*)grad_h, (bf16*)grad_pos, tokens, dim, nx, pos_rows);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

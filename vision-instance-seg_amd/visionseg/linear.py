@@ -18,6 +18,7 @@ import torch.nn.functional as F
 from . import _lib as L
 from . import ops
 
+import ctypes
 import os
 
 # split when K is at least this many tokens; chunks never drop below MIN_CHUNK rows
@@ -193,6 +194,7 @@ _SMALL = os.environ.get("VS_SMALL_LINEAR", "1") == "1"      # A/B switch
 
 
 _SMALL_FUSED = os.environ.get("VS_SMALL_LINEAR_FUSED", "1") == "1"   # A/B: library forward / dX GEMMs
+_QKV_FUSED = os.environ.get("VS_SELF_ATTN_FUSED", "1") == "1"      # A/B: add + three small Linears
 
 
 class _SmallLinearFn(torch.autograd.Function):
@@ -405,6 +407,70 @@ def small_linear(x, w, b=None):
             and tokens <= SMALL_MAX_TOKENS and O % 64 == 0 and I % 64 == 0 and not torch.is_autocast_enabled()):
         return _SmallLinearFn.apply(x, w, b)
     return F.linear(x, w, b)
+
+
+def _ptrs3(ts):
+    return (ctypes.c_void_p * 3)(*[L.ptr(t) for t in ts])
+
+
+class _SelfAttnInProjFn(torch.autograd.Function):
+    """q = (h + pos) Wq^T + bq, k = (h + pos) Wk^T + bk, v = h Wv^T + bv over the decoder's
+    B x Q tokens (HF:m2f:1730-1745 with_pos_embed, Mask2FormerAttention q/k/v_proj) as one
+    forward and one backward launch (csrc/small_linear.hip vs_self_attn_in_proj_*): the
+    backward sums every use of h and of pos in-kernel (dpos = dq Wq + dk Wk, dh = dpos +
+    dv Wv), where autograd ran an add, three Linear backwards and three gradient adds."""
+
+    @staticmethod
+    def forward(ctx, h, pos, wq, bq, wk, bk, wv, bv):
+        B, Q, D = h.shape
+        h2 = h.reshape(-1, D).contiguous()
+        if pos.stride(0) == 0 and pos[0].is_contiguous():     # query_embed expanded over the batch
+            p2, prows = pos[0], Q
+        else:
+            p2, prows = pos.reshape(-1, D).contiguous(), B * Q
+        ws = [w.contiguous() for w in (wq, wk, wv)]
+        outs = [torch.empty(h2.shape[0], D, device=h.device, dtype=torch.bfloat16) for _ in range(3)]
+        L.check(L.lib().vs_self_attn_in_proj_forward(L.dtype_code(h2), L.ptr(h2), L.ptr(p2), prows, _ptrs3(ws),
+                                                     _ptrs3([bq, bk, bv]), _ptrs3(outs), h2.shape[0], D,
+                                                     L.stream(h2)), "self_attn_in_proj_forward")
+        ctx.save_for_backward(h2, p2, *ws)
+        ctx.shape, ctx.prows = h.shape, prows
+        return tuple(o.view(B, Q, D) for o in outs)
+
+    @staticmethod
+    def backward(ctx, gq, gk, gv):
+        h2, p2, wq, wk, wv = ctx.saved_tensors
+        D = h2.shape[1]
+        gs = [(g if g is not None else torch.zeros(ctx.shape, device=h2.device, dtype=torch.bfloat16))
+              .reshape(-1, D).contiguous() for g in (gq, gk, gv)]
+        gh = torch.empty_like(h2)
+        gp = torch.empty_like(h2) if ctx.needs_input_grad[1] else None
+        gw = [torch.empty(D, D, device=h2.device, dtype=torch.bfloat16) for _ in range(3)]
+        gb = [torch.empty(D, device=h2.device, dtype=torch.bfloat16) for _ in range(3)]
+        L.check(L.lib().vs_self_attn_in_proj_backward(
+            L.dtype_code(h2), L.ptr(h2), L.ptr(p2), ctx.prows, _ptrs3([wq, wk, wv]), _ptrs3(gs), L.ptr(gh),
+            L.ptr(gp) if gp is not None else None, _ptrs3(gw), _ptrs3(gb), h2.shape[0], D, L.stream(h2)),
+            "self_attn_in_proj_backward")
+        return (gh.view(ctx.shape), gp.view(ctx.shape) if gp is not None else None,
+                gw[0], gb[0], gw[1], gb[1], gw[2], gb[2])
+
+
+def self_attn_in_proj(h, pos, q_proj, k_proj, v_proj):
+    """(q, k, v) of the decoder self-attention: q = q_proj(h + pos), k = k_proj(h + pos),
+    v = v_proj(h), each [B, Q, D] -- one launch each way on the bf16 device path (see
+    _SelfAttnInProjFn), the plain composition otherwise."""
+    D = h.shape[-1]
+    lins = (q_proj, k_proj, v_proj)
+    tokens = h.numel() // max(1, D)
+    if (_SMALL and _SMALL_FUSED and _QKV_FUSED and h.is_cuda and torch.is_grad_enabled() and h.dim() == 3
+            and pos.shape == h.shape and not torch.is_autocast_enabled() and D % 64 == 0
+            and tokens <= SMALL_MAX_TOKENS and h.dtype == pos.dtype == torch.bfloat16
+            and all(m.weight.shape == (D, D) and m.bias is not None and m.weight.requires_grad
+                    and m.weight.dtype == m.bias.dtype == torch.bfloat16 for m in lins)):
+        return _SelfAttnInProjFn.apply(h, pos, q_proj.weight, q_proj.bias, k_proj.weight, k_proj.bias,
+                                       v_proj.weight, v_proj.bias)
+    hq = h + pos
+    return q_proj(hq), k_proj(hq), v_proj(h)
 
 
 class SmallLinear(nn.Linear):

@@ -29,7 +29,8 @@ import torch.nn.functional as F
 
 from . import ops
 from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_relu_tokens, linear_tokens,
-                     plane_projection, small_linear, value_query_projection, reattach_level_embed)
+                     plane_projection, self_attn_in_proj, small_linear, value_query_projection,
+                     reattach_level_embed)
 
 
 @dataclass
@@ -526,10 +527,10 @@ class DecoderLayer(nn.Module):
         o = ops.masked_attention(q, k, v, words, H, d ** -0.5)
         _, h = self.norm_cross.add_forward(h, self.cross_attn.out_proj(o))       # post-norm, fused add
         sa = self.self_attn
-        hq = h + qpos                                                            # shared by q and k
-        qs = sa.q_proj(hq).view(B, Q, H, d).transpose(1, 2)
-        ks = sa.k_proj(hq).view(B, Q, H, d).transpose(1, 2)
-        vs = sa.v_proj(h).view(B, Q, H, d).transpose(1, 2)
+        q_, k_, v_ = self_attn_in_proj(h, qpos, sa.q_proj, sa.k_proj, sa.v_proj)   # q, k see h + qpos
+        qs = q_.view(B, Q, H, d).transpose(1, 2)
+        ks = k_.view(B, Q, H, d).transpose(1, 2)
+        vs = v_.view(B, Q, H, d).transpose(1, 2)
         att = F.scaled_dot_product_attention(qs, ks, vs)
         _, h = self.norm_self.add_forward(h, sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)))
         _, h = self.norm_ffn.add_forward(h, self.fc2(F.relu(self.fc1(h))))
