@@ -431,17 +431,24 @@ VS_API int vs_small_linear_wgrad(int dtype, const void* grad_y, const void* x, v
 
 /* The same Linear's forward and whole backward, each one launch (bf16, f32 accumulation,
  * the reduction split over four waves and summed in a fixed order):
- *   forward:  y [tokens, out] = x [tokens, in] weight[out, in]^T (+ bias[out] when non-NULL)
- *   backward: grad_x [tokens, in] = grad_y weight (skipped when grad_x is NULL) and
- *             grad_w / grad_b as vs_small_linear_wgrad (skipped when grad_w is NULL),
- *             the two products in one grid.
- * Replaces autograd's addmm forward and its mm input gradient for the decoder Linears
- * above (torch.nn.functional.linear / LinearBackward). */
-VS_API int vs_small_linear_forward(int dtype, const void* x, const void* weight, const void* bias, void* y,
-                                   int tokens, int out_features, int in_features, void* stream);
-VS_API int vs_small_linear_backward(int dtype, const void* grad_y, const void* x, const void* weight,
-                                    void* grad_x, void* grad_w, void* grad_b, int tokens, int out_features,
-                                    int in_features, void* stream);
+ *   forward:  y [tokens, out] = act(x' weight[out, in]^T (+ bias[out] when non-NULL)),
+ *             x' = x [tokens, in] (+ pos when non-NULL: pos row t % pos_rows, the sum
+ *             rounded to bf16 like torch's add), act = ReLU when relu != 0
+ *   backward: g = grad_y, masked where relu_out (the forward's ReLU output; NULL: no
+ *             ReLU) is not positive; grad_x [tokens, in] = g weight (skipped when grad_x is
+ *             NULL; grad_pos, when non-NULL, receives the same per-token rows: the gradient
+ *             of pos) and grad_w = g^T x', grad_b = colsum g
+ *             (as vs_small_linear_wgrad; skipped when grad_w is NULL), both in one grid.
+ * Replaces autograd's addmm forward, F.relu and its threshold_backward, and the mm input
+ * gradient for the decoder Linears above (torch.nn.functional.linear / LinearBackward;
+ * HF:m2f:1730-1745 with_pos_embed for the cross-attention query). */
+VS_API int vs_small_linear_forward(int dtype, const void* x, const void* pos, int pos_rows, const void* weight,
+                                   const void* bias, int relu, void* y, int tokens, int out_features,
+                                   int in_features, void* stream);
+VS_API int vs_small_linear_backward(int dtype, const void* grad_y, const void* x, const void* pos, int pos_rows,
+                                    const void* weight, const void* relu_out, void* grad_x, void* grad_pos,
+                                    void* grad_w, void* grad_b, int tokens, int out_features, int in_features,
+                                    void* stream);
 
 /* The self-attention input projections of a masked-attention decoder layer (HF:m2f
  * Mask2FormerMaskedAttentionDecoderLayer.forward_post: q = k = hidden + query_pos,

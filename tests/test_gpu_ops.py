@@ -979,6 +979,44 @@ def test_self_attn_in_proj_vs_torch(B, Q, D, expand):
         assert e <= 2 ** -7 * max(1.0, scale) + 1e-3, (name, e, scale)
 
 
+@pytest.mark.parametrize("relu,pos", [(True, None), (False, "expand"), (True, "full"), (False, "full")])
+def test_small_linear_relu_pos_vs_torch(relu, pos):
+    """_SmallLinearFn with the fused ReLU (forward epilogue; backward: gY masked by the
+    ReLU output in both the dX and the dW / db loads) and the position rows added to X in
+    the operand loads (pos expanded over the batch or per token; pos gets X's gradient)
+    vs torch f64 on the same bf16 operands, x + pos rounded to bf16 first."""
+    from visionseg.linear import _SmallLinearFn
+    B, Q, I, O = 4, 100, 256, 512
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(B, Q, I, generator=g).to(torch.bfloat16)
+    w = (torch.randn(O, I, generator=g) / I ** 0.5).to(torch.bfloat16)
+    b = torch.randn(O, generator=g).to(torch.bfloat16)
+    src = None if pos is None else torch.randn(*((Q, I) if pos == "expand" else (B, Q, I)), generator=g).to(torch.bfloat16)
+    gy = torch.randn(B, Q, O, generator=g).to(torch.bfloat16)
+    xd, wd, bd = (t.to(DEV).requires_grad_(True) for t in (x, w, b))
+    sd = src.to(DEV).requires_grad_(True) if src is not None else None
+    pd = None if sd is None else (sd.unsqueeze(0).expand(B, -1, -1) if pos == "expand" else sd)
+    y = _SmallLinearFn.apply(xd, wd, bd, relu, pd)
+    y.backward(gy.to(DEV))
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+    sr = src.double().requires_grad_(True) if src is not None else None
+    xin = xr
+    if sr is not None:
+        pr = sr.unsqueeze(0).expand(B, -1, -1) if pos == "expand" else sr
+        rounded = (x.float() + (src.float() if pos == "full" else src.float()[None])).to(torch.bfloat16).double()
+        xin = rounded + (xr + pr - (xr + pr).detach())
+    yr = torch.nn.functional.linear(xin, wr, br)
+    yr = torch.relu(yr) if relu else yr
+    yr.backward(gy.double())
+    pairs = [("y", y.detach(), yr.detach()), ("dx", xd.grad, xr.grad), ("dw", wd.grad, wr.grad), ("db", bd.grad, br.grad)]
+    if sr is not None:
+        pairs.append(("dpos", sd.grad, sr.grad))
+    for name, got, exp in pairs:
+        e = float((got.double().cpu() - exp).abs().max())
+        scale = float(exp.abs().max())
+        assert e <= 2 ** -7 * max(1.0, scale) + 1e-3, (name, e, scale)
+
+
 def test_small_linear_weight_slice():
     """A weight slice (the decoder's cross-attention q rows of in_proj_weight) gets its
     gradient rows back through autograd's slice."""

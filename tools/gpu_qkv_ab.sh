@@ -9,8 +9,6 @@ tail -1 $O/tests.log
 timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_model.py tests/test_gpu_train_parity.py > $O/model.log 2>&1 || exit $?
 tail -1 $O/model.log
 for s in 1 0 1 0; do
-  VS_SELF_ATTN_FUSED=$s timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-parity --steps 20 > $O/bench_$s.log 2>&1 || exit $?
-  echo "qkv_fused=$s $(grep -o '"ms_per_step": [0-9.]*' $O/bench_$s.log)"
+  VS_SMALL_LINEAR_FUSED=$s timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-parity --steps 20 > $O/bench_$s.log 2>&1 || exit $?
+  echo "small_fused=$s $(grep -o '"ms_per_step": [0-9.]*' $O/bench_$s.log)"
 done
-timeout -k 10 300 python3 tools/loader_bench.py --images 64 --workers 4,8,16 > $O/loader.log 2>&1 || exit $?
-cat $O/loader.log

@@ -135,17 +135,41 @@ __device__ __forceinline__ uint4 add_bf16x8(uint4 a, uint4 b) {
   return o;
 }
 
+// g where the ReLU output y > 0, else 0 (relu'(x) as torch's threshold_backward on the
+// result), 8 bf16 elements
+__device__ __forceinline__ uint4 mask_bf16x8(uint4 g, uint4 y) {
+  const uint32_t* pg = reinterpret_cast<const uint32_t*>(&g);
+  const uint32_t* py = reinterpret_cast<const uint32_t*>(&y);
+  uint4 o;
+  uint32_t* po = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t lo = py[j] & 0xffffu, hi = py[j] >> 16;
+    const uint32_t keep = ((lo != 0u && !(lo & 0x8000u)) ? 0x0000ffffu : 0u) |
+                          ((hi != 0u && !(hi & 0x8000u)) ? 0xffff0000u : 0u);
+    po[j] = pg[j] & keep;
+  }
+  return o;
+}
+
+__device__ __forceinline__ bf16x8_t mask8(bf16x8_t g, bf16x8_t y) {
+  const uint4 o = mask_bf16x8(*reinterpret_cast<const uint4*>(&g), *reinterpret_cast<const uint4*>(&y));
+  return *reinterpret_cast<const bf16x8_t*>(&o);
+}
+
 __device__ __forceinline__ bf16x8_t add8(bf16x8_t a, bf16x8_t b) {
   const uint4 o = add_bf16x8(*reinterpret_cast<const uint4*>(&a), *reinterpret_cast<const uint4*>(&b));
   return *reinterpret_cast<const bf16x8_t*>(&o);
 }
 
 // pos (may be NULL): the x operand is x + pos (the decoder's query + query-position input),
-// pos row t % prows (prows = Q: one query-position table broadcast over the batch)
+// pos row t % prows (prows = Q: one query-position table broadcast over the batch);
+// gmask (may be NULL): gY is masked by a ReLU output of gY's shape (fused ReLU backward)
 __device__ __forceinline__ void wgrad_split_block(bf16* sbuf, float (*sB)[kBlk], int bx, int by,
                                                   const bf16* __restrict__ gy, const bf16* __restrict__ x,
                                                   bf16* __restrict__ dw, bf16* __restrict__ db, int T, int O, int I,
-                                                  const bf16* __restrict__ pos = nullptr, int prows = 1) {
+                                                  const bf16* __restrict__ pos = nullptr, int prows = 1,
+                                                  const bf16* __restrict__ gmask = nullptr) {
   const int i0 = bx * kBlk, o0 = by * kBlk;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -160,6 +184,8 @@ __device__ __forceinline__ void wgrad_split_block(bf16* sbuf, float (*sB)[kBlk],
       const int row = p >> 3, c = (p & 7) * 8;
       const int t = t0 + row;
       rg[k] = t < T ? *reinterpret_cast<const uint4*>(gy + (size_t)t * O + o0 + c) : make_uint4(0, 0, 0, 0);
+      if (gmask && t < T)
+        rg[k] = mask_bf16x8(rg[k], *reinterpret_cast<const uint4*>(gmask + (size_t)t * O + o0 + c));
       rx[k] = t < T ? *reinterpret_cast<const uint4*>(x + (size_t)t * I + i0 + c) : make_uint4(0, 0, 0, 0);
       if (pos && t < T)
         rx[k] = add_bf16x8(rx[k], *reinterpret_cast<const uint4*>(pos + (size_t)(t % prows) * I + i0 + c));
@@ -254,11 +280,13 @@ constexpr int kWC = 64;          // W rows per LDS chunk (input-gradient path)
 // One wave's partial product over k in [kb, kb + klen) (klen a multiple of 16) for the
 // tile (features f0.., tokens t0..): !TRANS_A: A = W rows [f][k]; TRANS_A: A = W^T, W rows
 // k, columns f (staged through this wave's LDS chunk sW).  B = token rows of bmat (ldb
-// elements per row) + pos row t % prows (pos may be NULL).
+// elements per row) + pos row t % prows (pos may be NULL), masked where bmask (a ReLU
+// output of bmat's shape, may be NULL) is not positive.
 template <bool TRANS_A>
 __device__ __forceinline__ f32x16_t tile_partial(bf16* sW, const bf16* __restrict__ w, int ldw,
                                                  const bf16* __restrict__ bmat, const bf16* __restrict__ pos, int ldb,
-                                                 int kb, int klen, int T, int t0, int f0, int prows = 1) {
+                                                 int kb, int klen, int T, int t0, int f0, int prows = 1,
+                                                 const bf16* __restrict__ bmask = nullptr) {
   const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int t = t0 + r;
   const bool tv = t < T;
@@ -267,7 +295,8 @@ __device__ __forceinline__ f32x16_t tile_partial(bf16* sW, const bf16* __restric
   const size_t poff = (size_t)(tc % prows) * ldb + kb + 8 * hh;
   auto ldb8 = [&](int k) {
     if (!tv) return zero8();
-    const bf16x8_t v = ld8(bmat + boff + k);
+    bf16x8_t v = ld8(bmat + boff + k);
+    if (bmask) v = mask8(v, ld8(bmask + boff + k));
     return pos ? add8(v, ld8(pos + poff + k)) : v;
   };
   f32x16_t acc;
@@ -341,11 +370,12 @@ template <bool TRANS_A>
 __device__ __forceinline__ void reduce_tile(bf16* sbuf, int tt, int ft, const bf16* __restrict__ w,
                                             const bf16* __restrict__ bmat, const bf16* __restrict__ pos,
                                             const bf16* __restrict__ bias, bf16* __restrict__ out, int T, int K,
-                                            int ldw, int F, int prows = 1) {
+                                            int ldw, int F, int prows = 1, const bf16* __restrict__ bmask = nullptr,
+                                            bool relu = false, bf16* __restrict__ out2 = nullptr) {
   const int wave = threadIdx.x >> 6;
   const int t0 = tt * kRT, f0 = ft * kRT, kq = K / 4;        // this wave's K quarter (multiple of 16)
   const f32x16_t acc = tile_partial<TRANS_A>(sbuf + wave * kWC * kPitch, w, ldw, bmat, pos, K, wave * kq, kq, T,
-                                             t0, f0, prows);
+                                             t0, f0, prows, bmask);
   const float* red = stash_partials(sbuf, acc);
   const int tk = threadIdx.x & 31, fq = 4 * (threadIdx.x >> 5);
   float v[4];
@@ -355,22 +385,28 @@ __device__ __forceinline__ void reduce_tile(bf16* sbuf, int tt, int ft, const bf
 #pragma unroll
     for (int w_ = 1; w_ < 4; ++w_) s_ += red[(w_ * kRT + fq + e) * kRT + tk];
     v[e] = bias ? s_ + __bfloat162float(bias[f0 + fq + e]) : s_;
+    if (relu) v[e] = fmaxf(v[e], 0.f);
   }
   store_quad(out, F, T, t0, f0, v);
+  if (out2) store_quad(out2, F, T, t0, f0, v);
 }
 
-// grid (ceil(T / 32), O / 32): y [T, O] = x [T, I] w[O, I]^T + b
-__global__ void __launch_bounds__(256) small_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
-                                                        const bf16* __restrict__ b, bf16* __restrict__ y, int T,
-                                                        int O, int I) {
+// grid (ceil(T / 32), O / 32): y [T, O] = [relu](x (+ pos) [T, I] w[O, I]^T + b)
+__global__ void __launch_bounds__(256) small_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ pos,
+                                                        int prows, const bf16* __restrict__ w,
+                                                        const bf16* __restrict__ b, int relu, bf16* __restrict__ y,
+                                                        int T, int O, int I) {
   __shared__ __attribute__((aligned(16))) bf16 sbuf[4 * kRT * kRT * 2];   // the f32 reduction (16 KB)
-  reduce_tile<false>(sbuf, blockIdx.x, blockIdx.y, w, x, nullptr, b, y, T, I, I, O);
+  reduce_tile<false>(sbuf, blockIdx.x, blockIdx.y, w, x, pos, b, y, T, I, I, O, prows, nullptr, relu != 0);
 }
 
 // One launch for the whole backward: blocks [0, nx) are dX tiles (ceil(T / 32) x I / 32,
-// when dx is requested), the rest the token-split dW / db blocks (I / 64 x O / 64).
+// when dx is requested), the rest the token-split dW / db blocks (I / 64 x O / 64).  pos:
+// the forward's x + pos operand (dW); ymask: the forward's ReLU output (gY masked by it).
 __global__ void __launch_bounds__(256) small_bwd_kernel(const bf16* __restrict__ gy, const bf16* __restrict__ x,
-                                                        const bf16* __restrict__ w, bf16* __restrict__ dx,
+                                                        const bf16* __restrict__ pos, int prows,
+                                                        const bf16* __restrict__ w, const bf16* __restrict__ ymask,
+                                                        bf16* __restrict__ dx, bf16* __restrict__ dpos,
                                                         bf16* __restrict__ dw, bf16* __restrict__ db, int T, int O,
                                                         int I, int nx) {
   __shared__ __attribute__((aligned(16))) bf16 sbuf[kSplitLds];
@@ -378,10 +414,10 @@ __global__ void __launch_bounds__(256) small_bwd_kernel(const bf16* __restrict__
   const int blk = blockIdx.x;
   const int ntt = (T + kRT - 1) / kRT;
   if (blk < nx) {
-    reduce_tile<true>(sbuf, blk % ntt, blk / ntt, w, gy, nullptr, nullptr, dx, T, O, I, I);
+    reduce_tile<true>(sbuf, blk % ntt, blk / ntt, w, gy, nullptr, nullptr, dx, T, O, I, I, 1, ymask, false, dpos);
   } else {
     const int wb = blk - nx, nbx = I / kBlk;
-    wgrad_split_block(sbuf, sB, wb % nbx, wb / nbx, gy, x, dw, db, T, O, I);
+    wgrad_split_block(sbuf, sB, wb % nbx, wb / nbx, gy, x, dw, db, T, O, I, pos, prows, ymask);
   }
 }
 
@@ -478,25 +514,29 @@ extern "C" int vs_small_linear_wgrad(int dtype, const void* grad_y, const void* 
   return VS_OK;
 }
 
-extern "C" int vs_small_linear_forward(int dtype, const void* x, const void* weight, const void* bias, void* y,
-                                       int tokens, int out_features, int in_features, void* stream) {
+extern "C" int vs_small_linear_forward(int dtype, const void* x, const void* pos, int pos_rows, const void* weight,
+                                       const void* bias, int relu, void* y, int tokens, int out_features,
+                                       int in_features, void* stream) {
   VS_CHECK(dtype == VS_BF16, "the small-token Linear is the bf16 path");
   VS_CHECK(tokens >= 0 && out_features > 0 && in_features > 0, "bad sizes");
+  VS_CHECK(!pos || (pos_rows > 0 && tokens % pos_rows == 0), "pos_rows must divide tokens");
   VS_CHECK(out_features % kBlk == 0 && in_features % kBlk == 0, "features must be multiples of 64");
   if (tokens == 0) return VS_OK;
   VS_CHECK(x && weight && y, "null pointer");
   hipLaunchKernelGGL(small_fwd_kernel, dim3((tokens + kRT - 1) / kRT, out_features / kRT), dim3(256), 0,
-                     (hipStream_t)stream, (const bf16*)x, (const bf16*)weight, (const bf16*)bias, (bf16*)y, tokens,
-                     out_features, in_features);
+                     (hipStream_t)stream, (const bf16*)x, (const bf16*)pos, pos ? pos_rows : 1, (const bf16*)weight,
+                     (const bf16*)bias, relu, (bf16*)y, tokens, out_features, in_features);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
 
-extern "C" int vs_small_linear_backward(int dtype, const void* grad_y, const void* x, const void* weight,
-                                        void* grad_x, void* grad_w, void* grad_b, int tokens, int out_features,
-                                        int in_features, void* stream) {
+extern "C" int vs_small_linear_backward(int dtype, const void* grad_y, const void* x, const void* pos, int pos_rows,
+                                        const void* weight, const void* relu_out, void* grad_x, void* grad_pos,
+                                        void* grad_w, void* grad_b, int tokens, int out_features, int in_features,
+                                        void* stream) {
   VS_CHECK(dtype == VS_BF16, "the small-token Linear is the bf16 path");
   VS_CHECK(tokens >= 0 && out_features > 0 && in_features > 0, "bad sizes");
+  VS_CHECK(!pos || (pos_rows > 0 && tokens % pos_rows == 0), "pos_rows must divide tokens");
   VS_CHECK(out_features % kBlk == 0 && in_features % kBlk == 0, "features must be multiples of 64");
   VS_CHECK(grad_w || grad_x, "nothing to compute");
   hipStream_t st = (hipStream_t)stream;
@@ -507,10 +547,12 @@ extern "C" int vs_small_linear_backward(int dtype, const void* grad_y, const voi
   }
   VS_CHECK(grad_y && (!grad_x || weight) && (!grad_w || x), "null pointer");
   if (!grad_w) VS_CHECK(!grad_b, "grad_b needs grad_w");
+  VS_CHECK(!grad_pos || grad_x, "grad_pos needs grad_x");
   const int nx = grad_x ? ((tokens + kRT - 1) / kRT) * (in_features / kRT) : 0;
   const int nw = grad_w ? (in_features / kBlk) * (out_features / kBlk) : 0;
   hipLaunchKernelGGL(small_bwd_kernel, dim3(nx + nw), dim3(256), 0, st, (const bf16*)grad_y, (const bf16*)x,
-                     (const bf16*)weight, (bf16*)grad_x, (bf16*)grad_w, (bf16*)grad_b, tokens, out_features,
+                     (const bf16*)pos, pos ? pos_rows : 1, (const bf16*)weight, (const bf16*)relu_out,
+                     (bf16*)grad_x, (bf16*)grad_pos, (bf16*)grad_w, (bf16*)grad_b, tokens, out_features,
                      in_features, nx);
   VS_LAUNCH_CHECK();
   return VS_OK;

@@ -197,51 +197,84 @@ _SMALL_FUSED = os.environ.get("VS_SMALL_LINEAR_FUSED", "1") == "1"   # A/B: libr
 _QKV_FUSED = os.environ.get("VS_SELF_ATTN_FUSED", "1") == "1"      # A/B: add + three small Linears
 
 
+def _pos_rows(pos, T):
+    """(contiguous pos rows, rows): the query-position table itself when pos is its batch
+    expand (stride 0 over the batch), else the per-token rows."""
+    if pos.dim() == 3 and pos.stride(0) == 0 and pos[0].is_contiguous():
+        return pos[0], pos.shape[1]
+    return pos.reshape(T, -1).contiguous(), T
+
+
 class _SmallLinearFn(torch.autograd.Function):
     """Linear over a few hundred tokens on csrc/small_linear.hip: the forward one launch
-    (Y = X W^T + b, vs_small_linear_forward) and the whole backward one launch (dX = dY W
-    and the token-split dW / db in one grid, vs_small_linear_backward) -- autograd ran an
-    addmm forward and an mm + a single-tile dW GEMM + a bias reduction backward.
-    VS_SMALL_LINEAR_FUSED=0: library forward / dX GEMMs, dW and db by vs_small_linear_wgrad."""
+    (Y = act((X [+ pos]) W^T + b), vs_small_linear_forward) and the whole backward one
+    launch (dX = dY' W and the token-split dW / db in one grid, dY' = dY masked by the
+    ReLU output when relu, vs_small_linear_backward) -- autograd ran an add, an addmm, a
+    relu forward, and threshold_backward + mm + a single-tile dW GEMM + a bias reduction
+    backward.  pos (optional, e.g. the query-position table expanded over the batch) gets
+    the same gradient as X.  VS_SMALL_LINEAR_FUSED=0: library forward / dX GEMMs, dW and db
+    by vs_small_linear_wgrad."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
+    def forward(ctx, x, weight, bias, relu=False, pos=None):
         ctx.has_bias = bias is not None
+        ctx.relu = bool(relu)
         if not _SMALL_FUSED:
-            return F.linear(x, weight, bias)
+            ctx.prows = 0
+            xin = x if pos is None else x + pos
+            y = F.linear(xin, weight, bias)
+            y = F.relu(y) if relu else y
+            ctx.save_for_backward(xin, weight, y if relu else None, None)
+            return y
         O, I = weight.shape
         x2 = x.reshape(-1, I).contiguous()
-        y = torch.empty(x2.shape[0], O, device=x.device, dtype=torch.bfloat16)
-        L.check(L.lib().vs_small_linear_forward(L.dtype_code(y), L.ptr(x2), L.ptr(weight.contiguous()),
-                                                L.ptr(bias) if bias is not None else None, L.ptr(y),
-                                                x2.shape[0], O, I, L.stream(x2)), "small_linear_forward")
+        T = x2.shape[0]
+        p2, prows = _pos_rows(pos, T) if pos is not None else (None, 0)
+        ctx.prows, ctx.pos_shape = prows, (pos.shape if pos is not None else None)
+        y = torch.empty(T, O, device=x.device, dtype=torch.bfloat16)
+        L.check(L.lib().vs_small_linear_forward(L.dtype_code(y), L.ptr(x2), L.ptr(p2) if p2 is not None else None,
+                                                prows, L.ptr(weight.contiguous()),
+                                                L.ptr(bias) if bias is not None else None, int(relu), L.ptr(y),
+                                                T, O, I, L.stream(x2)), "small_linear_forward")
+        ctx.save_for_backward(x2, weight, y if relu else None, p2)
         return y.view(*x.shape[:-1], O)
 
     @staticmethod
     def backward(ctx, gy):
-        x, weight = ctx.saved_tensors
+        x, weight, y, p2 = ctx.saved_tensors
         O, I = weight.shape
         gy2 = gy.reshape(-1, O).contiguous()
-        gx = gw = gb = None
+        gx = gw = gb = gpos = None
         want_w = ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2])
+        want_pos = len(ctx.needs_input_grad) > 4 and ctx.needs_input_grad[4]
         x2 = x.reshape(-1, I).contiguous()
         if want_w:
             gw = torch.empty(O, I, device=gy2.device, dtype=torch.bfloat16)
             gb = torch.empty(O, device=gy2.device, dtype=torch.bfloat16) if ctx.has_bias else None
         if _SMALL_FUSED:
-            if ctx.needs_input_grad[0]:
-                gx = torch.empty(gy2.shape[0], I, device=gy2.device, dtype=torch.bfloat16)
+            T = gy2.shape[0]
+            if ctx.needs_input_grad[0] or want_pos:
+                gx = torch.empty(T, I, device=gy2.device, dtype=torch.bfloat16)
+            if want_pos:
+                gpos = torch.empty(T, I, device=gy2.device, dtype=torch.bfloat16)
             if gx is not None or gw is not None:
                 L.check(L.lib().vs_small_linear_backward(
-                    L.dtype_code(gy2), L.ptr(gy2), L.ptr(x2), L.ptr(weight.contiguous()),
-                    L.ptr(gx) if gx is not None else None, L.ptr(gw) if gw is not None else None,
-                    L.ptr(gb) if gb is not None else None, gy2.shape[0], O, I, L.stream(gy2)), "small_linear_backward")
+                    L.dtype_code(gy2), L.ptr(gy2), L.ptr(x2), L.ptr(p2) if p2 is not None else None, ctx.prows,
+                    L.ptr(weight.contiguous()), L.ptr(y) if y is not None else None,
+                    L.ptr(gx) if gx is not None else None, L.ptr(gpos) if gpos is not None else None,
+                    L.ptr(gw) if gw is not None else None, L.ptr(gb) if gb is not None else None,
+                    T, O, I, L.stream(gy2)), "small_linear_backward")
             if gx is not None:
-                gx = gx.view(x.shape)
+                gx = gx.view(*gy.shape[:-1], I) if ctx.needs_input_grad[0] else None
+            if gpos is not None:
+                gpos = gpos.view(*gy.shape[:-1], I)
         else:
-            if ctx.needs_input_grad[0]:
-                gx = (gy2 @ weight).view(x.shape)
+            if y is not None:
+                gy2 = gy2 * (y.reshape(-1, O) > 0).to(gy2.dtype)
+            if ctx.needs_input_grad[0] or want_pos:
+                gx = (gy2 @ weight).view(*gy.shape[:-1], I)
+                gpos = gx if want_pos else None
+                gx = gx if ctx.needs_input_grad[0] else None
             if want_w:
                 L.check(L.lib().vs_small_linear_wgrad(L.dtype_code(gw), L.ptr(gy2), L.ptr(x2), L.ptr(gw),
                                                       L.ptr(gb) if gb is not None else None, gy2.shape[0], O, I,
@@ -250,7 +283,7 @@ class _SmallLinearFn(torch.autograd.Function):
             gw = None
         if not (ctx.has_bias and ctx.needs_input_grad[2]):
             gb = None
-        return gx, gw, gb
+        return gx, gw, gb, None, gpos
 
 
 class _InProjFn(torch.autograd.Function):
@@ -264,46 +297,82 @@ class _InProjFn(torch.autograd.Function):
     the level memory (split-K dW, HIP column sums)."""
 
     @staticmethod
-    def forward(ctx, xq, xk, xv, weight, bias):
+    def forward(ctx, xq, xk, xv, weight, bias, q_pos=None):
         D = weight.shape[1]
         W = (weight[:D], weight[D:2 * D], weight[2 * D:])
         B = (bias[:D], bias[D:2 * D], bias[2 * D:])
-        ctx.save_for_backward(xq, xk, xv, weight)
-        return tuple(F.linear(x, w, b) for x, w, b in zip((xq, xk, xv), W, B))
+        T = xq.numel() // D
+        # the query rows on the small-token kernels (one launch each way, q_pos in the
+        # operand loads): bf16, a few hundred tokens
+        ctx.small = bool(_SMALL and _SMALL_FUSED and xq.dtype == weight.dtype == torch.bfloat16
+                         and T <= SMALL_MAX_TOKENS and D % 64 == 0)
+        ctx.prows = 0
+        if ctx.small:
+            x2 = xq.reshape(-1, D).contiguous()
+            p2, ctx.prows = _pos_rows(q_pos, T) if q_pos is not None else (None, 0)
+            q = torch.empty(T, D, device=xq.device, dtype=torch.bfloat16)
+            L.check(L.lib().vs_small_linear_forward(L.dtype_code(q), L.ptr(x2),
+                                                    L.ptr(p2) if p2 is not None else None, ctx.prows,
+                                                    L.ptr(W[0]), L.ptr(B[0]), 0, L.ptr(q), T, D, D,
+                                                    L.stream(x2)), "small_linear_forward")
+            q = q.view(xq.shape)
+            ctx.save_for_backward(x2, xk, xv, weight, p2)
+        else:
+            xq_ = xq if q_pos is None else xq + q_pos
+            q = F.linear(xq_, W[0], B[0])
+            ctx.save_for_backward(xq_, xk, xv, weight, None)
+        return (q,) + tuple(F.linear(x, w, b) for x, w, b in zip((xk, xv), W[1:], B[1:]))
 
     @staticmethod
     def backward(ctx, gq, gk, gv):
-        xq, xk, xv, weight = ctx.saved_tensors
+        xq, xk, xv, weight, p2 = ctx.saved_tensors
         D = weight.shape[1]
         gw = torch.empty_like(weight)
         gb = torch.empty(3 * D, device=weight.device, dtype=weight.dtype)
         gx = []
+        gpos = None
+        want_pos = len(ctx.needs_input_grad) > 5 and ctx.needs_input_grad[5]
         for i, (g, x) in enumerate(((gq, xq), (gk, xk), (gv, xv))):
             g2 = g.reshape(-1, D).contiguous()
             x2 = x.reshape(-1, D).contiguous()
             w_i = weight[i * D:(i + 1) * D]
-            gx.append((g2 @ w_i).view(x.shape) if ctx.needs_input_grad[i] else None)
             rows = slice(i * D, (i + 1) * D)
-            if i == 0 and _SMALL and g2.dtype == torch.bfloat16 and g2.shape[0] <= SMALL_MAX_TOKENS and D % 64 == 0:
-                L.check(L.lib().vs_small_linear_wgrad(L.dtype_code(gw), L.ptr(g2), L.ptr(x2), L.ptr(gw[rows]),
-                                                      L.ptr(gb[rows]), g2.shape[0], D, D, L.stream(g2)),
-                        "small_linear_wgrad")
+            if i == 0 and ctx.small:
+                T = g2.shape[0]
+                need_x = ctx.needs_input_grad[0] or want_pos
+                gxq = torch.empty(T, D, device=g2.device, dtype=torch.bfloat16) if need_x else None
+                gpos = torch.empty(T, D, device=g2.device, dtype=torch.bfloat16) if want_pos else None
+                L.check(L.lib().vs_small_linear_backward(
+                    L.dtype_code(g2), L.ptr(g2), L.ptr(x2), L.ptr(p2) if p2 is not None else None, ctx.prows,
+                    L.ptr(w_i), None, L.ptr(gxq) if gxq is not None else None,
+                    L.ptr(gpos) if gpos is not None else None, L.ptr(gw[rows]), L.ptr(gb[rows]), T, D, D,
+                    L.stream(g2)), "small_linear_backward")
+                gx.append(gxq.view(gq.shape) if ctx.needs_input_grad[0] else None)
+                gpos = gpos.view(gq.shape) if gpos is not None else None
                 continue
+            gxi = (g2 @ w_i).view(x.shape) if (ctx.needs_input_grad[i] or (i == 0 and want_pos)) else None
+            if i == 0 and want_pos:
+                gpos = gxi
+            gx.append(gxi if ctx.needs_input_grad[i] else None)
             weight_grad(g2, x2.to(g2.dtype), weight.dtype, out=gw[rows])
             if D % 8 == 0 and D <= 2048 and g2.dtype == weight.dtype:
                 ops.column_sum(g2, out=gb[rows])
             else:
                 gb[rows].copy_(g2.sum(0, dtype=torch.float32))
-        return gx[0], gx[1], gx[2], gw, gb
+        return gx[0], gx[1], gx[2], gw, gb, gpos
 
 
-def in_projection(xq, xk, xv, weight, bias):
-    """(q, k, v) of nn.MultiheadAttention's packed in-projection (see _InProjFn); plain
-    slicing off the device / under autocast / without grad."""
+def in_projection(xq, xk, xv, weight, bias, q_pos=None):
+    """(q, k, v) of nn.MultiheadAttention's packed in-projection (see _InProjFn), the query
+    input being xq + q_pos when q_pos is given (HF:m2f with_pos_embed); plain slicing off
+    the device / under autocast / without grad."""
     D = weight.shape[1]
     if (xq.is_cuda and torch.is_grad_enabled() and weight.requires_grad and not torch.is_autocast_enabled()
-            and xq.dtype == weight.dtype == xk.dtype == xv.dtype == bias.dtype):
-        return _InProjFn.apply(xq, xk, xv, weight, bias)
+            and xq.dtype == weight.dtype == xk.dtype == xv.dtype == bias.dtype
+            and (q_pos is None or (q_pos.shape == xq.shape and q_pos.dtype == xq.dtype))):
+        return _InProjFn.apply(xq, xk, xv, weight, bias, q_pos)
+    if q_pos is not None:
+        xq = xq + q_pos
     return (F.linear(xq, weight[:D], bias[:D]), F.linear(xk, weight[D:2 * D], bias[D:2 * D]),
             F.linear(xv, weight[2 * D:], bias[2 * D:]))
 
@@ -398,15 +467,17 @@ def reattach_level_embed(pos, level_embed, sizes):
     return pos + (rows - rows.detach())
 
 
-def small_linear(x, w, b=None):
-    """F.linear with the one-launch weight/bias gradient for small bf16 token counts."""
+def small_linear(x, w, b=None, relu=False):
+    """F.linear (+ ReLU when relu) on the small-token HIP kernels for bf16 device tokens
+    (see _SmallLinearFn); the plain composition otherwise."""
     tokens = x.numel() // max(1, x.shape[-1])
     O, I = w.shape
     if (_SMALL and x.is_cuda and torch.is_grad_enabled() and w.requires_grad and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and (b is None or b.dtype == torch.bfloat16)
             and tokens <= SMALL_MAX_TOKENS and O % 64 == 0 and I % 64 == 0 and not torch.is_autocast_enabled()):
-        return _SmallLinearFn.apply(x, w, b)
-    return F.linear(x, w, b)
+        return _SmallLinearFn.apply(x, w, b, relu)
+    y = F.linear(x, w, b)
+    return F.relu(y) if relu else y
 
 
 def _ptrs3(ts):

@@ -523,7 +523,8 @@ class DecoderLayer(nn.Module):
         """mem: level memory [B, hw, D] (contiguous), mem_pos = mem + its position embedding."""
         B, Q, D = h.shape
         H, d = self.heads, D // self.heads
-        q, k, v = in_projection(h + qpos, mem_pos, mem, self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias)
+        q, k, v = in_projection(h, mem_pos, mem, self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias,
+                                q_pos=qpos)                                      # query = h + qpos
         o = ops.masked_attention(q, k, v, words, H, d ** -0.5)
         _, h = self.norm_cross.add_forward(h, self.cross_attn.out_proj(o))       # post-norm, fused add
         sa = self.self_attn
@@ -533,7 +534,7 @@ class DecoderLayer(nn.Module):
         vs = v_.view(B, Q, H, d).transpose(1, 2)
         att = F.scaled_dot_product_attention(qs, ks, vs)
         _, h = self.norm_self.add_forward(h, sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)))
-        _, h = self.norm_ffn.add_forward(h, self.fc2(F.relu(self.fc1(h))))
+        _, h = self.norm_ffn.add_forward(h, self.fc2(small_linear(h, self.fc1.weight, self.fc1.bias, relu=True)))
         return h
 
 
