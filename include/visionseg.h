@@ -437,7 +437,10 @@ VS_API int vs_small_linear_wgrad(int dtype, const void* grad_y, const void* x, v
  *   backward: g = grad_y, masked where relu_out (the forward's ReLU output; NULL: no
  *             ReLU) is not positive; grad_x [tokens, in] = g weight (skipped when grad_x is
  *             NULL; grad_pos, when non-NULL, receives the same per-token rows: the gradient
- *             of pos) and grad_w = g^T x', grad_b = colsum g
+ *             of pos; added to what grad_pos holds when accumulate_pos != 0: several
+ *             consumers of one position table sum into one buffer) and grad_w = g^T x',
+ *             grad_b = colsum g; grad_res (may be NULL) is added to grad_x only: the
+ *             residual-path gradient of x (one rounding instead of a separate add)
  *             (as vs_small_linear_wgrad; skipped when grad_w is NULL), both in one grid.
  * Replaces autograd's addmm forward, F.relu and its threshold_backward, and the mm input
  * gradient for the decoder Linears above (torch.nn.functional.linear / LinearBackward;
@@ -446,9 +449,9 @@ VS_API int vs_small_linear_forward(int dtype, const void* x, const void* pos, in
                                    const void* bias, int relu, void* y, int tokens, int out_features,
                                    int in_features, void* stream);
 VS_API int vs_small_linear_backward(int dtype, const void* grad_y, const void* x, const void* pos, int pos_rows,
-                                    const void* weight, const void* relu_out, void* grad_x, void* grad_pos,
-                                    void* grad_w, void* grad_b, int tokens, int out_features, int in_features,
-                                    void* stream);
+                                    const void* weight, const void* relu_out, const void* grad_res, void* grad_x,
+                                    void* grad_pos, int accumulate_pos, void* grad_w, void* grad_b, int tokens,
+                                    int out_features, int in_features, void* stream);
 
 /* The self-attention input projections of a masked-attention decoder layer (HF:m2f
  * Mask2FormerMaskedAttentionDecoderLayer.forward_post: q = k = hidden + query_pos,
@@ -456,8 +459,10 @@ VS_API int vs_small_linear_backward(int dtype, const void* grad_y, const void* x
  * dim x dim weights, arrays of 3 pointers in q, k, v order:
  *   forward:  outs[0] = (h + pos) Wq^T + bq, outs[1] = (h + pos) Wk^T + bk,
  *             outs[2] = h Wv^T + bv                     -- one launch
- *   backward: grad_pos = dq Wq + dk Wk (may be NULL), grad_h = grad_pos + dv Wv, and the
- *             three weight / bias gradients              -- one launch
+ *   backward: grad_pos (+)= dq Wq + dk Wk (may be NULL; accumulated into when
+ *             accumulate_pos != 0), grad_h = dq Wq + dk Wk + dv Wv (+ grad_res, the
+ *             residual-path gradient of h, when non-NULL), and the three weight / bias
+ *             gradients                                   -- one launch
  * pos row of token t is t % pos_rows (pos_rows = queries: the query-position table
  * broadcast over the batch; = tokens: a full tensor); grad_pos is per token [tokens, dim].
  * h + pos is rounded to bf16 before the products (torch's bf16 add).  Replaces the add,
@@ -466,9 +471,10 @@ VS_API int vs_self_attn_in_proj_forward(int dtype, const void* h, const void* po
                                         const void* const* weights, const void* const* biases, void* const* outs,
                                         int tokens, int dim, void* stream);
 VS_API int vs_self_attn_in_proj_backward(int dtype, const void* h, const void* pos, int pos_rows,
-                                         const void* const* weights, const void* const* grad_outs, void* grad_h,
-                                         void* grad_pos, void* const* grad_weights, void* const* grad_biases,
-                                         int tokens, int dim, void* stream);
+                                         const void* const* weights, const void* const* grad_outs,
+                                         const void* grad_res, void* grad_h, void* grad_pos, int accumulate_pos,
+                                         void* const* grad_weights, void* const* grad_biases, int tokens, int dim,
+                                         void* stream);
 
 /* ---- activation backward + bias gradient (csrc/norm.hip) ------------------------------
  * dx = dy * act'(x) for act 0 = ReLU, 1 = exact GELU (torch's F.gelu, approximate='none'),

@@ -4,6 +4,8 @@ Index ops: bit-exact.  f32 kernels vs the fp32 oracle: <= 1e-5 abs (op level).  
 kernels: compared with the oracle evaluated on the same bf16-rounded inputs in f32;
 tolerance stated per test (bf16 output rounding, 2^-8 relative).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -14,6 +16,7 @@ from oracle import ref_ops as R
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _ops():
@@ -1015,6 +1018,28 @@ def test_small_linear_relu_pos_vs_torch(relu, pos):
         e = float((got.double().cpu() - exp).abs().max())
         scale = float(exp.abs().max())
         assert e <= 2 ** -7 * max(1.0, scale) + 1e-3, (name, e, scale)
+
+
+def test_decoder_layer_small_kernels_vs_library():
+    """One masked-attention decoder layer (B = 2, Q = 100, a 32 x 32 memory level) in bf16
+    on the small-token kernels (fused Linears, q / k / v in one launch, residual gradients
+    handed to the projections through ops.ResidualSink, the query-position gradient summed
+    in one ops.GradSink buffer) and on the library path: each against the same layer in
+    fp32; every output / gradient error of the fused path <= 1.25 x the library path's
+    (+ 1e-3): the fusions add no error beyond bf16 rounding (tools/decoder_layer_ab.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("dl_ab", os.path.join(ROOT, "tools", "decoder_layer_ab.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    from visionseg import linear
+    saved = (linear._SMALL_FUSED, linear._QKV_FUSED)
+    try:
+        errs = mod.compare()
+    finally:
+        linear._SMALL_FUSED, linear._QKV_FUSED = saved
+    bad = {k: v for k, v in errs.items() if k != "self_attn.k_proj.bias" and v[0] > 1.25 * v[1] + 1e-3}
+    assert not bad, bad
+    assert errs["out"][0] < 1e-2 and errs["dh"][0] < 5e-2 and errs["dpos"][0] < 5e-2
 
 
 def test_small_linear_weight_slice():

@@ -35,7 +35,8 @@ def run(layer, dtype, h, table, mem, gy, fused):
     return res
 
 
-def main():
+def compare():
+    """{tensor name: (fused rel-L2 error, library rel-L2 error)} against the fp32 layer."""
     torch.manual_seed(0)
     D = 256
     base = DecoderLayer(D, 2048, 8).to(DEV)
@@ -57,16 +58,18 @@ def main():
         lay.load_state_dict(sd)
         results[name] = run(lay, dtype, h, table, mem, gy, fused)
     ref = results["fp32"]
+    return {k: tuple(float((results[name][k] - ref[k]).norm() / ref[k].norm().clamp_min(1e-12))
+                     for name in ("bf16 fused", "bf16 unfused")) for k in ref}
+
+
+def main():
+    errs = compare()
     print(f"{'tensor':45s} {'fused':>10s} {'unfused':>10s}")
-    worst = 0.0
-    for k in ref:
-        e = []
-        for name in ("bf16 fused", "bf16 unfused"):
-            d = (results[name][k] - ref[k]).norm() / ref[k].norm().clamp_min(1e-12)
-            e.append(float(d))
-        worst = max(worst, e[0] / max(e[1], 1e-12))
-        print(f"{k:45s} {e[0]:10.3e} {e[1]:10.3e}")
-    print(f"worst fused / unfused error ratio {worst:.2f}")
+    for k, (a, b) in errs.items():
+        print(f"{k:45s} {a:10.3e} {b:10.3e}")
+    print("worst fused / unfused error ratio "
+          f"{max(a / max(b, 1e-12) for k, (a, b) in errs.items() if k != 'self_attn.k_proj.bias'):.2f} "
+          "(self_attn.k_proj.bias: analytically zero gradient, rounding noise on both paths)")
 
 
 if __name__ == "__main__":

@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/qkv
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -k "small_linear or self_attn_in_proj" tests/test_gpu_ops.py > $O/tests.log 2>&1 || exit $?
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -k "small_linear or self_attn_in_proj or decoder_layer" tests/test_gpu_ops.py > $O/tests.log 2>&1 || exit $?
 tail -1 $O/tests.log
 timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_model.py tests/test_gpu_train_parity.py > $O/model.log 2>&1 || exit $?
 tail -1 $O/model.log

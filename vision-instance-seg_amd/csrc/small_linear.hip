@@ -366,12 +366,23 @@ __device__ __forceinline__ void store_quad(bf16* __restrict__ out, int ld, int T
   }
 }
 
+// v[0..3] += src[token tg][features f .. f + 3] (bf16), when src is non-NULL and tg < T
+__device__ __forceinline__ void add_quad(const bf16* __restrict__ src, int ld, int T, int tg, int f, float* v) {
+  if (!src || tg >= T) return;
+  const uint2 q = *reinterpret_cast<const uint2*>(src + (size_t)tg * ld + f);
+  v[0] += bf16_bits_to_f32(q.x & 0xffffu);
+  v[1] += bf16_bits_to_f32(q.x >> 16);
+  v[2] += bf16_bits_to_f32(q.y & 0xffffu);
+  v[3] += bf16_bits_to_f32(q.y >> 16);
+}
+
 template <bool TRANS_A>
 __device__ __forceinline__ void reduce_tile(bf16* sbuf, int tt, int ft, const bf16* __restrict__ w,
                                             const bf16* __restrict__ bmat, const bf16* __restrict__ pos,
                                             const bf16* __restrict__ bias, bf16* __restrict__ out, int T, int K,
                                             int ldw, int F, int prows = 1, const bf16* __restrict__ bmask = nullptr,
-                                            bool relu = false, bf16* __restrict__ out2 = nullptr) {
+                                            bool relu = false, bf16* __restrict__ out2 = nullptr,
+                                            bool acc2 = false, const bf16* __restrict__ add_in = nullptr) {
   const int wave = threadIdx.x >> 6;
   const int t0 = tt * kRT, f0 = ft * kRT, kq = K / 4;        // this wave's K quarter (multiple of 16)
   const f32x16_t acc = tile_partial<TRANS_A>(sbuf + wave * kWC * kPitch, w, ldw, bmat, pos, K, wave * kq, kq, T,
@@ -387,8 +398,14 @@ __device__ __forceinline__ void reduce_tile(bf16* sbuf, int tt, int ft, const bf
     v[e] = bias ? s_ + __bfloat162float(bias[f0 + fq + e]) : s_;
     if (relu) v[e] = fmaxf(v[e], 0.f);
   }
+  const int tg = t0 + tk;
+  if (out2) {                                 // the position rows' gradient (+= when accumulating)
+    float v2[4] = {v[0], v[1], v[2], v[3]};
+    if (acc2) add_quad(out2, F, T, tg, f0 + fq, v2);
+    store_quad(out2, F, T, t0, f0, v2);
+  }
+  add_quad(add_in, F, T, tg, f0 + fq, v);     // the residual gradient (ops.ResidualSink)
   store_quad(out, F, T, t0, f0, v);
-  if (out2) store_quad(out2, F, T, t0, f0, v);
 }
 
 // grid (ceil(T / 32), O / 32): y [T, O] = [relu](x (+ pos) [T, I] w[O, I]^T + b)
@@ -408,13 +425,14 @@ __global__ void __launch_bounds__(256) small_bwd_kernel(const bf16* __restrict__
                                                         const bf16* __restrict__ w, const bf16* __restrict__ ymask,
                                                         bf16* __restrict__ dx, bf16* __restrict__ dpos,
                                                         bf16* __restrict__ dw, bf16* __restrict__ db, int T, int O,
-                                                        int I, int nx) {
+                                                        int I, int nx, const bf16* __restrict__ gres, int acc_pos) {
   __shared__ __attribute__((aligned(16))) bf16 sbuf[kSplitLds];
   __shared__ float sB[4][kBlk];
   const int blk = blockIdx.x;
   const int ntt = (T + kRT - 1) / kRT;
   if (blk < nx) {
-    reduce_tile<true>(sbuf, blk % ntt, blk / ntt, w, gy, nullptr, nullptr, dx, T, O, I, I, 1, ymask, false, dpos);
+    reduce_tile<true>(sbuf, blk % ntt, blk / ntt, w, gy, nullptr, nullptr, dx, T, O, I, I, 1, ymask, false, dpos,
+                      acc_pos != 0, gres);
   } else {
     const int wb = blk - nx, nbx = I / kBlk;
     wgrad_split_block(sbuf, sB, wb % nbx, wb / nbx, gy, x, dw, db, T, O, I, pos, prows, ymask);
@@ -449,7 +467,8 @@ __global__ void __launch_bounds__(256) qkv_fwd_kernel(const bf16* __restrict__ h
 
 __global__ void __launch_bounds__(256) qkv_bwd_kernel(const bf16* __restrict__ h, const bf16* __restrict__ pos,
                                                       QkvPtrs p, bf16* __restrict__ dh, bf16* __restrict__ dpos,
-                                                      int T, int D, int nx, int prows) {
+                                                      int T, int D, int nx, int prows, const bf16* __restrict__ gres,
+                                                      int acc_pos) {
   __shared__ __attribute__((aligned(16))) bf16 sbuf[kSplitLds];
   __shared__ float sB[4][kBlk];
   const int blk = blockIdx.x;
@@ -470,7 +489,11 @@ __global__ void __launch_bounds__(256) qkv_bwd_kernel(const bf16* __restrict__ h
       vp[e] = red[0 * kRT * kRT + o] + red[1 * kRT * kRT + o];
       vh[e] = vp[e] + (red[2 * kRT * kRT + o] + red[3 * kRT * kRT + o]);
     }
-    if (dpos) store_quad(dpos, D, T, t0, f0, vp);
+    if (dpos) {
+      if (acc_pos) add_quad(dpos, D, T, t0 + tk, f0 + fq, vp);
+      store_quad(dpos, D, T, t0, f0, vp);
+    }
+    add_quad(gres, D, T, t0 + tk, f0 + fq, vh);
     store_quad(dh, D, T, t0, f0, vh);
   } else {
     const int nb = (D / kBlk) * (D / kBlk);
@@ -531,9 +554,9 @@ extern "C" int vs_small_linear_forward(int dtype, const void* x, const void* pos
 }
 
 extern "C" int vs_small_linear_backward(int dtype, const void* grad_y, const void* x, const void* pos, int pos_rows,
-                                        const void* weight, const void* relu_out, void* grad_x, void* grad_pos,
-                                        void* grad_w, void* grad_b, int tokens, int out_features, int in_features,
-                                        void* stream) {
+                                        const void* weight, const void* relu_out, const void* grad_res,
+                                        void* grad_x, void* grad_pos, int accumulate_pos, void* grad_w,
+                                        void* grad_b, int tokens, int out_features, int in_features, void* stream) {
   VS_CHECK(dtype == VS_BF16, "the small-token Linear is the bf16 path");
   VS_CHECK(tokens >= 0 && out_features > 0 && in_features > 0, "bad sizes");
   VS_CHECK(!pos || (pos_rows > 0 && tokens % pos_rows == 0), "pos_rows must divide tokens");
@@ -553,7 +576,7 @@ extern "C" int vs_small_linear_backward(int dtype, const void* grad_y, const voi
   hipLaunchKernelGGL(small_bwd_kernel, dim3(nx + nw), dim3(256), 0, st, (const bf16*)grad_y, (const bf16*)x,
                      (const bf16*)pos, pos ? pos_rows : 1, (const bf16*)weight, (const bf16*)relu_out,
                      (bf16*)grad_x, (bf16*)grad_pos, (bf16*)grad_w, (bf16*)grad_b, tokens, out_features,
-                     in_features, nx);
+                     in_features, nx, (const bf16*)grad_res, accumulate_pos);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
@@ -580,9 +603,10 @@ extern "C" int vs_self_attn_in_proj_forward(int dtype, const void* h, const void
 }
 
 extern "C" int vs_self_attn_in_proj_backward(int dtype, const void* h, const void* pos, int pos_rows,
-                                             const void* const* weights, const void* const* grad_outs, void* grad_h,
-                                             void* grad_pos, void* const* grad_weights, void* const* grad_biases,
-                                             int tokens, int dim, void* stream) {
+                                             const void* const* weights, const void* const* grad_outs,
+                                             const void* grad_res, void* grad_h, void* grad_pos, int accumulate_pos,
+                                             void* const* grad_weights, void* const* grad_biases, int tokens,
+                                             int dim, void* stream) {
   VS_CHECK(dtype == VS_BF16, "the small-token Linear is the bf16 path");
   VS_CHECK(tokens >= 0 && dim > 0 && dim % kBlk == 0, "dim must be a positive multiple of 64");
   VS_CHECK(pos_rows > 0 && tokens % pos_rows == 0, "pos_rows must divide tokens");
@@ -608,7 +632,8 @@ extern "C" int vs_self_attn_in_proj_backward(int dtype, const void* h, const voi
   const int nx = ((tokens + kRT - 1) / kRT) * (dim / kRT);
   const int nw = 3 * (dim / kBlk) * (dim / kBlk);
   hipLaunchKernelGGL(qkv_bwd_kernel, dim3(nx + nw), dim3(256), 0, st, (const bf16*)h, (const bf16*)pos, p,
-                     (bf16*)grad_h, (bf16*)grad_pos, tokens, dim, nx, pos_rows);
+                     (bf16*)grad_h, (bf16*)grad_pos, tokens, dim, nx, pos_rows, (const bf16*)grad_res,
+                     accumulate_pos);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

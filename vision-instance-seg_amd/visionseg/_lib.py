@@ -85,9 +85,11 @@ SIGNATURES = {
     "vs_group_norm_nchw_workspace_bytes": [_c_int] * 3,
     "vs_small_linear_wgrad": [_c_int, _P, _P, _P, _P, _c_int, _c_int, _c_int, _P],
     "vs_small_linear_forward": [_c_int, _P, _P, _c_int, _P, _P, _c_int, _P, _c_int, _c_int, _c_int, _P],
-    "vs_small_linear_backward": [_c_int, _P, _P, _P, _c_int, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _c_int, _P],
+    "vs_small_linear_backward": [_c_int, _P, _P, _P, _c_int, _P, _P, _P, _P, _P, _c_int, _P, _P, _c_int, _c_int,
+                                 _c_int, _P],
     "vs_self_attn_in_proj_forward": [_c_int, _P, _P, _c_int, _P, _P, _P, _c_int, _c_int, _P],
-    "vs_self_attn_in_proj_backward": [_c_int, _P, _P, _c_int, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _P],
+    "vs_self_attn_in_proj_backward": [_c_int, _P, _P, _c_int, _P, _P, _P, _P, _P, _c_int, _P, _P, _c_int, _c_int,
+                                      _P],
     "vs_group_norm_nchw_forward": [_c_int] + [_P] * 7 + [_c_int] * 4 + [_c_float, _c_int, _P],
     "vs_group_norm_nchw_backward": [_c_int] + [_P] * 10 + [_c_int] * 5 + [_P],
     "vs_upsample_add_forward": [_c_int, _P, _P, _P] + [_c_int] * 6 + [ctypes.c_longlong, _P],

@@ -205,6 +205,19 @@ def _pos_rows(pos, T):
     return pos.reshape(T, -1).contiguous(), T
 
 
+def _pos_grad_buffer(psink, T, D, like):
+    """(buffer, accumulate) for a consumer's position-row gradient: a fresh [T, D] buffer,
+    or -- with a GradSink (ops.GradSink: every consumer of one position table sums into
+    one buffer, the source node hands the sum to autograd once) -- the sink's buffer,
+    created by the first consumer and accumulated into by the rest."""
+    if psink is None:
+        return torch.empty(T, D, device=like.device, dtype=torch.bfloat16), False
+    if psink.buf is None:
+        psink.buf = torch.empty(T, D, device=like.device, dtype=torch.bfloat16)
+        return psink.buf, False
+    return psink.buf, True
+
+
 class _SmallLinearFn(torch.autograd.Function):
     """Linear over a few hundred tokens on csrc/small_linear.hip: the forward one launch
     (Y = act((X [+ pos]) W^T + b), vs_small_linear_forward) and the whole backward one
@@ -216,9 +229,10 @@ class _SmallLinearFn(torch.autograd.Function):
     by vs_small_linear_wgrad."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, relu=False, pos=None):
+    def forward(ctx, x, weight, bias, relu=False, pos=None, sink=None, psink=None):
         ctx.has_bias = bias is not None
         ctx.relu = bool(relu)
+        ctx.sink = ctx.psink = None
         if not _SMALL_FUSED:
             ctx.prows = 0
             xin = x if pos is None else x + pos
@@ -237,6 +251,9 @@ class _SmallLinearFn(torch.autograd.Function):
                                                 L.ptr(bias) if bias is not None else None, int(relu), L.ptr(y),
                                                 T, O, I, L.stream(x2)), "small_linear_forward")
         ctx.save_for_backward(x2, weight, y if relu else None, p2)
+        ctx.sink, ctx.psink = sink, (psink if pos is not None else None)
+        if sink is not None:
+            sink.arm()
         return y.view(*x.shape[:-1], O)
 
     @staticmethod
@@ -253,21 +270,26 @@ class _SmallLinearFn(torch.autograd.Function):
             gb = torch.empty(O, device=gy2.device, dtype=torch.bfloat16) if ctx.has_bias else None
         if _SMALL_FUSED:
             T = gy2.shape[0]
+            gres = ctx.sink.take() if ctx.sink is not None else None
+            if gres is not None:
+                gres = gres.reshape(T, I).contiguous()
             if ctx.needs_input_grad[0] or want_pos:
                 gx = torch.empty(T, I, device=gy2.device, dtype=torch.bfloat16)
+            acc = False
             if want_pos:
-                gpos = torch.empty(T, I, device=gy2.device, dtype=torch.bfloat16)
+                gpos, acc = _pos_grad_buffer(ctx.psink, T, I, gy2)
             if gx is not None or gw is not None:
                 L.check(L.lib().vs_small_linear_backward(
                     L.dtype_code(gy2), L.ptr(gy2), L.ptr(x2), L.ptr(p2) if p2 is not None else None, ctx.prows,
                     L.ptr(weight.contiguous()), L.ptr(y) if y is not None else None,
-                    L.ptr(gx) if gx is not None else None, L.ptr(gpos) if gpos is not None else None,
+                    L.ptr(gres) if gres is not None else None, L.ptr(gx) if gx is not None else None,
+                    L.ptr(gpos) if gpos is not None else None, int(acc),
                     L.ptr(gw) if gw is not None else None, L.ptr(gb) if gb is not None else None,
                     T, O, I, L.stream(gy2)), "small_linear_backward")
             if gx is not None:
                 gx = gx.view(*gy.shape[:-1], I) if ctx.needs_input_grad[0] else None
             if gpos is not None:
-                gpos = gpos.view(*gy.shape[:-1], I)
+                gpos = None if ctx.psink is not None else gpos.view(*gy.shape[:-1], I)
         else:
             if y is not None:
                 gy2 = gy2 * (y.reshape(-1, O) > 0).to(gy2.dtype)
@@ -283,7 +305,7 @@ class _SmallLinearFn(torch.autograd.Function):
             gw = None
         if not (ctx.has_bias and ctx.needs_input_grad[2]):
             gb = None
-        return gx, gw, gb, None, gpos
+        return gx, gw, gb, None, gpos, None, None
 
 
 class _InProjFn(torch.autograd.Function):
@@ -297,7 +319,7 @@ class _InProjFn(torch.autograd.Function):
     the level memory (split-K dW, HIP column sums)."""
 
     @staticmethod
-    def forward(ctx, xq, xk, xv, weight, bias, q_pos=None):
+    def forward(ctx, xq, xk, xv, weight, bias, q_pos=None, sink=None, psink=None):
         D = weight.shape[1]
         W = (weight[:D], weight[D:2 * D], weight[2 * D:])
         B = (bias[:D], bias[D:2 * D], bias[2 * D:])
@@ -307,7 +329,11 @@ class _InProjFn(torch.autograd.Function):
         ctx.small = bool(_SMALL and _SMALL_FUSED and xq.dtype == weight.dtype == torch.bfloat16
                          and T <= SMALL_MAX_TOKENS and D % 64 == 0)
         ctx.prows = 0
+        ctx.sink = ctx.psink = None
         if ctx.small:
+            ctx.sink, ctx.psink = sink, (psink if q_pos is not None else None)
+            if sink is not None:
+                sink.arm()
             x2 = xq.reshape(-1, D).contiguous()
             p2, ctx.prows = _pos_rows(q_pos, T) if q_pos is not None else (None, 0)
             q = torch.empty(T, D, device=xq.device, dtype=torch.bfloat16)
@@ -341,14 +367,17 @@ class _InProjFn(torch.autograd.Function):
                 T = g2.shape[0]
                 need_x = ctx.needs_input_grad[0] or want_pos
                 gxq = torch.empty(T, D, device=g2.device, dtype=torch.bfloat16) if need_x else None
-                gpos = torch.empty(T, D, device=g2.device, dtype=torch.bfloat16) if want_pos else None
+                gpos, acc = _pos_grad_buffer(ctx.psink, T, D, g2) if want_pos else (None, False)
+                gres = ctx.sink.take() if ctx.sink is not None else None
+                if gres is not None:
+                    gres = gres.reshape(T, D).contiguous()
                 L.check(L.lib().vs_small_linear_backward(
                     L.dtype_code(g2), L.ptr(g2), L.ptr(x2), L.ptr(p2) if p2 is not None else None, ctx.prows,
-                    L.ptr(w_i), None, L.ptr(gxq) if gxq is not None else None,
-                    L.ptr(gpos) if gpos is not None else None, L.ptr(gw[rows]), L.ptr(gb[rows]), T, D, D,
-                    L.stream(g2)), "small_linear_backward")
+                    L.ptr(w_i), None, L.ptr(gres) if gres is not None else None,
+                    L.ptr(gxq) if gxq is not None else None, L.ptr(gpos) if gpos is not None else None, int(acc),
+                    L.ptr(gw[rows]), L.ptr(gb[rows]), T, D, D, L.stream(g2)), "small_linear_backward")
                 gx.append(gxq.view(gq.shape) if ctx.needs_input_grad[0] else None)
-                gpos = gpos.view(gq.shape) if gpos is not None else None
+                gpos = gpos.view(gq.shape) if (gpos is not None and ctx.psink is None) else None
                 continue
             gxi = (g2 @ w_i).view(x.shape) if (ctx.needs_input_grad[i] or (i == 0 and want_pos)) else None
             if i == 0 and want_pos:
@@ -359,10 +388,10 @@ class _InProjFn(torch.autograd.Function):
                 ops.column_sum(g2, out=gb[rows])
             else:
                 gb[rows].copy_(g2.sum(0, dtype=torch.float32))
-        return gx[0], gx[1], gx[2], gw, gb, gpos
+        return gx[0], gx[1], gx[2], gw, gb, gpos, None, None
 
 
-def in_projection(xq, xk, xv, weight, bias, q_pos=None):
+def in_projection(xq, xk, xv, weight, bias, q_pos=None, sink=None, psink=None):
     """(q, k, v) of nn.MultiheadAttention's packed in-projection (see _InProjFn), the query
     input being xq + q_pos when q_pos is given (HF:m2f with_pos_embed); plain slicing off
     the device / under autocast / without grad."""
@@ -370,7 +399,7 @@ def in_projection(xq, xk, xv, weight, bias, q_pos=None):
     if (xq.is_cuda and torch.is_grad_enabled() and weight.requires_grad and not torch.is_autocast_enabled()
             and xq.dtype == weight.dtype == xk.dtype == xv.dtype == bias.dtype
             and (q_pos is None or (q_pos.shape == xq.shape and q_pos.dtype == xq.dtype))):
-        return _InProjFn.apply(xq, xk, xv, weight, bias, q_pos)
+        return _InProjFn.apply(xq, xk, xv, weight, bias, q_pos, sink, psink)
     if q_pos is not None:
         xq = xq + q_pos
     return (F.linear(xq, weight[:D], bias[:D]), F.linear(xk, weight[D:2 * D], bias[D:2 * D]),
@@ -467,15 +496,16 @@ def reattach_level_embed(pos, level_embed, sizes):
     return pos + (rows - rows.detach())
 
 
-def small_linear(x, w, b=None, relu=False):
+def small_linear(x, w, b=None, relu=False, sink=None):
     """F.linear (+ ReLU when relu) on the small-token HIP kernels for bf16 device tokens
-    (see _SmallLinearFn); the plain composition otherwise."""
+    (see _SmallLinearFn; sink: ops.ResidualSink, x's residual-path gradient added
+    in-kernel); the plain composition otherwise."""
     tokens = x.numel() // max(1, x.shape[-1])
     O, I = w.shape
     if (_SMALL and x.is_cuda and torch.is_grad_enabled() and w.requires_grad and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and (b is None or b.dtype == torch.bfloat16)
             and tokens <= SMALL_MAX_TOKENS and O % 64 == 0 and I % 64 == 0 and not torch.is_autocast_enabled()):
-        return _SmallLinearFn.apply(x, w, b, relu)
+        return _SmallLinearFn.apply(x, w, b, relu, None, sink)
     y = F.linear(x, w, b)
     return F.relu(y) if relu else y
 
@@ -492,7 +522,7 @@ class _SelfAttnInProjFn(torch.autograd.Function):
     dv Wv), where autograd ran an add, three Linear backwards and three gradient adds."""
 
     @staticmethod
-    def forward(ctx, h, pos, wq, bq, wk, bk, wv, bv):
+    def forward(ctx, h, pos, wq, bq, wk, bk, wv, bv, sink=None, psink=None):
         B, Q, D = h.shape
         h2 = h.reshape(-1, D).contiguous()
         if pos.stride(0) == 0 and pos[0].is_contiguous():     # query_embed expanded over the batch
@@ -506,6 +536,9 @@ class _SelfAttnInProjFn(torch.autograd.Function):
                                                      L.stream(h2)), "self_attn_in_proj_forward")
         ctx.save_for_backward(h2, p2, *ws)
         ctx.shape, ctx.prows = h.shape, prows
+        ctx.sink, ctx.psink = sink, psink
+        if sink is not None:
+            sink.arm()
         return tuple(o.view(B, Q, D) for o in outs)
 
     @staticmethod
@@ -514,22 +547,30 @@ class _SelfAttnInProjFn(torch.autograd.Function):
         D = h2.shape[1]
         gs = [(g if g is not None else torch.zeros(ctx.shape, device=h2.device, dtype=torch.bfloat16))
               .reshape(-1, D).contiguous() for g in (gq, gk, gv)]
+        T = h2.shape[0]
         gh = torch.empty_like(h2)
-        gp = torch.empty_like(h2) if ctx.needs_input_grad[1] else None
+        gres = ctx.sink.take() if ctx.sink is not None else None
+        if gres is not None:
+            gres = gres.reshape(T, D).contiguous()
+        gp, acc = _pos_grad_buffer(ctx.psink, T, D, h2) if ctx.needs_input_grad[1] else (None, False)
         gw = [torch.empty(D, D, device=h2.device, dtype=torch.bfloat16) for _ in range(3)]
         gb = [torch.empty(D, device=h2.device, dtype=torch.bfloat16) for _ in range(3)]
         L.check(L.lib().vs_self_attn_in_proj_backward(
-            L.dtype_code(h2), L.ptr(h2), L.ptr(p2), ctx.prows, _ptrs3([wq, wk, wv]), _ptrs3(gs), L.ptr(gh),
-            L.ptr(gp) if gp is not None else None, _ptrs3(gw), _ptrs3(gb), h2.shape[0], D, L.stream(h2)),
-            "self_attn_in_proj_backward")
+            L.dtype_code(h2), L.ptr(h2), L.ptr(p2), ctx.prows, _ptrs3([wq, wk, wv]), _ptrs3(gs),
+            L.ptr(gres) if gres is not None else None, L.ptr(gh), L.ptr(gp) if gp is not None else None, int(acc),
+            _ptrs3(gw), _ptrs3(gb), T, D, L.stream(h2)), "self_attn_in_proj_backward")
+        if ctx.psink is not None:
+            gp = None
         return (gh.view(ctx.shape), gp.view(ctx.shape) if gp is not None else None,
-                gw[0], gb[0], gw[1], gb[1], gw[2], gb[2])
+                gw[0], gb[0], gw[1], gb[1], gw[2], gb[2], None, None)
 
 
-def self_attn_in_proj(h, pos, q_proj, k_proj, v_proj):
+def self_attn_in_proj(h, pos, q_proj, k_proj, v_proj, sink=None, psink=None):
     """(q, k, v) of the decoder self-attention: q = q_proj(h + pos), k = k_proj(h + pos),
     v = v_proj(h), each [B, Q, D] -- one launch each way on the bf16 device path (see
-    _SelfAttnInProjFn), the plain composition otherwise."""
+    _SelfAttnInProjFn), the plain composition otherwise.  sink: ops.ResidualSink (h's
+    residual-path gradient added in-kernel); psink: ops.GradSink of pos (see
+    _pos_grad_buffer)."""
     D = h.shape[-1]
     lins = (q_proj, k_proj, v_proj)
     tokens = h.numel() // max(1, D)
@@ -539,7 +580,7 @@ def self_attn_in_proj(h, pos, q_proj, k_proj, v_proj):
             and all(m.weight.shape == (D, D) and m.bias is not None and m.weight.requires_grad
                     and m.weight.dtype == m.bias.dtype == torch.bfloat16 for m in lins)):
         return _SelfAttnInProjFn.apply(h, pos, q_proj.weight, q_proj.bias, k_proj.weight, k_proj.bias,
-                                       v_proj.weight, v_proj.bias)
+                                       v_proj.weight, v_proj.bias, sink, psink)
     hq = h + pos
     return q_proj(hq), k_proj(hq), v_proj(h)
 

@@ -519,22 +519,28 @@ class DecoderLayer(nn.Module):
         self.fc2 = SmallLinear(ffn, d)
         self.norm_ffn = TokenLayerNorm(d)
 
-    def forward(self, h, qpos, mem, mem_pos, words):
-        """mem: level memory [B, hw, D] (contiguous), mem_pos = mem + its position embedding."""
+    def forward(self, h, qpos, mem, mem_pos, words, psink=None):
+        """mem: level memory [B, hw, D] (contiguous), mem_pos = mem + its position embedding.
+        psink: ops.GradSink of qpos (the layers' query-position gradients summed in one
+        buffer by the projection kernels).  Each post-norm block hands its residual-path
+        gradient to the projection that consumes its input (ops.ResidualSink): no
+        gradient adds between the blocks."""
         B, Q, D = h.shape
         H, d = self.heads, D // self.heads
+        s1, s2, s3 = ops.ResidualSink(), ops.ResidualSink(), ops.ResidualSink()
         q, k, v = in_projection(h, mem_pos, mem, self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias,
-                                q_pos=qpos)                                      # query = h + qpos
+                                q_pos=qpos, sink=s1, psink=psink)               # query = h + qpos
         o = ops.masked_attention(q, k, v, words, H, d ** -0.5)
-        _, h = self.norm_cross.add_forward(h, self.cross_attn.out_proj(o))       # post-norm, fused add
+        _, h = self.norm_cross.add_forward(h, self.cross_attn.out_proj(o), sink=s1)   # post-norm, fused add
         sa = self.self_attn
-        q_, k_, v_ = self_attn_in_proj(h, qpos, sa.q_proj, sa.k_proj, sa.v_proj)   # q, k see h + qpos
+        q_, k_, v_ = self_attn_in_proj(h, qpos, sa.q_proj, sa.k_proj, sa.v_proj, sink=s2, psink=psink)
         qs = q_.view(B, Q, H, d).transpose(1, 2)
         ks = k_.view(B, Q, H, d).transpose(1, 2)
         vs = v_.view(B, Q, H, d).transpose(1, 2)
         att = F.scaled_dot_product_attention(qs, ks, vs)
-        _, h = self.norm_self.add_forward(h, sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)))
-        _, h = self.norm_ffn.add_forward(h, self.fc2(small_linear(h, self.fc1.weight, self.fc1.bias, relu=True)))
+        _, h = self.norm_self.add_forward(h, sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)), sink=s2)
+        f = small_linear(h, self.fc1.weight, self.fc1.bias, relu=True, sink=s3)
+        _, h = self.norm_ffn.add_forward(h, self.fc2(f), sink=s3)
         return h
 
 
@@ -598,6 +604,10 @@ class Decoder(nn.Module):
             mems.append(m)
             mem_pos.append(m + pos)
         qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
+        psink = None
+        if qpos.is_cuda and torch.is_grad_enabled() and qpos.requires_grad:
+            psink = ops.GradSink()                   # every layer's qpos gradient in one buffer
+            qpos = psink.source(qpos)
         h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
         n = len(self.layers)
 
@@ -617,7 +627,7 @@ class Decoder(nn.Module):
                 self.trace.append(words)
             if self.mask_override is not None:
                 words = pack_bitmask(self.mask_override[idx].to(dev))
-            h = layer(h, qpos, mems[lvl], mem_pos[lvl], words)
+            h = layer(h, qpos, mems[lvl], mem_pos[lvl], words, psink)
             hs.append(h)
             nxt = sizes[(idx + 1) % 3] if idx + 1 < n else None
             inter, logits, words = step(h, nxt)

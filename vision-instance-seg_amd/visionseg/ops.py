@@ -522,13 +522,17 @@ class _SinkSource(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, sink):
         ctx.sink = sink
+        ctx.shape = x.shape
         ctx.set_materialize_grads(False)
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
-        # runs after every consumer of the output: their in-place sum is in sink.buf
+        # runs after every consumer of the output: their in-place sum is in sink.buf (kept
+        # in the consumers' row layout: viewed back to the source's shape here)
         buf, ctx.sink.buf = ctx.sink.buf, None
+        if buf is not None:
+            buf = buf.view(ctx.shape)
         if g is not None:
             buf = g if buf is None else buf + g
         return buf, None
