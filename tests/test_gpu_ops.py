@@ -590,9 +590,12 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
     go = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3)).to(torch.bfloat16)
     ref.backward(go.float())
     grads, geo = {}, {}
-    for mf, gm in (("1", "0"), ("0", "0"), ("1", "1")):
-        monkeypatch.setenv("VS_MSDA_MFMA", mf)
+    # (mfma, geom, band skeleton): "s" = the product kernel on its default clear-after band
+    # skeleton (VS_MSDA_SKEL=2), "1" = the zero-fill-per-band skeleton (VS_MSDA_SKEL=0)
+    for mf, gm, sk in (("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"), ("s", "1", "2")):
+        monkeypatch.setenv("VS_MSDA_MFMA", "1" if mf == "s" else mf)
         monkeypatch.setenv("VS_MSDA_GEOM", gm)
+        monkeypatch.setenv("VS_MSDA_SKEL", sk)
         vd = value.to(DEV).requires_grad_(True)
         ld, wd = loc.to(DEV).requires_grad_(True), w.to(DEV).requires_grad_(True)
         out = ops.ms_deform_attn(vd, shapes, ld, wd)
@@ -607,13 +610,17 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
     # and vs the oracle (f32 value, bf16-rounded inputs): grad_loc and grad_attn of the
     # production kernel (GEOM fused into the band walk)
     _check_geo_vs_oracle(geo[("1", "1")][0], lr.grad, geo[("1", "1")][1], wr.grad)
+    # the two band skeletons walk the same bands in the same order: grad_loc / grad_attn
+    # bit-identical; grad_value differs only by the order of its f32 atomics
+    for a, b in zip(geo[("s", "1")], geo[("1", "1")]):
+        assert torch.equal(a, b), float((a - b).abs().max())
     scale = float(vr.grad.abs().max())
-    for mf in ("0", "1"):
+    for mf in ("0", "1", "s"):
         err = (grads[mf] - vr.grad).abs()
         bad = err > vr.grad.abs() * 2 ** -8 + 1e-4
         assert not bool(bad.any()), (mf, float(err.max()), int(bad.sum()), float(vr.grad[bad][0]),
                                      float(grads[mf][bad][0]))
-    for mf in ("1",):
+    for mf in ("1", "s"):
         d = (grads[mf] - grads["0"]).abs()
         # all f32 sums, rounded to bf16 once: within two bf16 ulps, plus f32 summation-order
         # noise (~1e-7 of the summed magnitudes) where contributions cancel to ~0

@@ -76,11 +76,11 @@ def main():
                 os.environ["VS_MSDA_FWD4"] = "0" if mode == "fwd1" else "1"
                 # syncbar: __syncthreads instead of the LDS-only barriers in the band walk
                 os.environ["VS_MSDA_LDSBAR"] = "0" if mode == "syncbar" else "1"
-                # prod: the product defaults (all band barriers LDS-only); skel3: + the band
-                # bitmask / clear-after skeleton (VS_MSDA_SKEL=3)
-                if mode in ("prod", "skel3"):
+                # prod: the product defaults (all band barriers LDS-only, the clear-after band
+                # skeleton); skel<k>: the product with VS_MSDA_SKEL=k (0: zero-fill per band)
+                if mode == "prod" or mode.startswith("skel"):
                     os.environ["VS_MSDA_LDSBAR"] = "127"
-                os.environ["VS_MSDA_SKEL"] = "3" if mode == "skel3" else "0"
+                os.environ["VS_MSDA_SKEL"] = mode[4:] if mode.startswith("skel") else "2"
 
                 def fb():
                     o = ops.ms_deform_attn(v, shapes, locr, wr)

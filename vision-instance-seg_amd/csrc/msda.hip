@@ -919,11 +919,23 @@ __global__ void __launch_bounds__(64) msda_bwd_binned_kernel(const float* __rest
 // ([64 queries] x K = 32 channels x [band cells]) on the band's value rows, each loaded
 // once per tile (the gather kernel requested 4 corner rows per tap: ~6x the bytes).
 // Dm goes to LDS (over W, after the band's atomics), every tap reads its corners' entries.
+// Band skeleton (template SKEL; VS_MSDA_SKEL selects the variant at run time):
+//  * SKEL 2 (ZAFTER, default): W is cleared AFTER a band's last barrier, each wave clearing
+//    only the W columns it writes (its 16 queries), so the next band starts on zeroed LDS
+//    with no zero-fill pass + barrier of its own (5 barriers a non-empty band instead of
+//    6), and the hit flags are replaced by "product != 0": C2 encoder shape 0.539 ->
+//    0.517 ms ("smooth" offsets), 0.674 -> 0.643 ms (iid +-4 px), tools/kbench.py;
+//  * SKEL 0: zero-fill + barrier at the start of every band, per-cell hit flags.
+//  Measured and dropped: a per-level bitmask of the non-empty bands in place of the
+//  per-band vote (its barrier gone too) cost more than the barrier it removed (LDS atomics:
+//  0.62 ms; a wave-shuffle OR with integer band divisions: 0.535 ms vs 0.517).
 constexpr int kBandCap = 128;
 constexpr int kWP8 = 68;       // W row pitch (floats): 64 queries + 4
-constexpr int kDP = 132;       // Dm row pitch (floats): 128 band cells + 4
+constexpr int kWFloats = kBandCap * kWP8;
+constexpr int kMsdaSkelDefault = 2;
+constexpr int kDP = 132;       // Dm row pitch (floats) of the SKEL 0 walk: 128 band cells + 4
 
-template <int TX, int TY, bool GEOM>
+template <int TX, int TY, bool GEOM, int SKEL = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) msda_bwd_mfma_wg_kernel(const float* __restrict__ loc,
                                                                const float* __restrict__ attw,
                                                                const bf16* __restrict__ gout,
@@ -950,8 +962,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
     else __syncthreads();
   };
   const bool LB = (lbmask & 2) != 0;
+  constexpr bool ZAFTER = (SKEL & 2) != 0;   // band skeleton variant (see kMsdaSkelDefault)
   __shared__ int sAny[2][4];
   int band_par = 0;
+  if (ZAFTER) {                               // every band starts on a zeroed W
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = tid; i < kWFloats / 4; i += 256) reinterpret_cast<float4*>(sW)[i] = z4;
+  }
   const int LP = L * P;
   const int tq = tid >> 2, tpt = tid & 3;
   const int qid = btile_query<TX, TY>(qt, lv, L, tile, tq, Q);
@@ -1024,10 +1041,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
       ox = min(ox, sBox[w][2]);
       xh = max(xh, sBox[w][3]);
     }
-    bar(1);                                   // sBox is rewritten by the next level
     float dk[4] = {0.f, 0.f, 0.f, 0.f};       // GEOM: grad_out . value at the tap's corners
     const int BY = yh < 0 ? 0 : yh - oy + 1, BX = yh < 0 ? 1 : xh - ox + 1;   // yh < 0: no corner here
     const int SBX = min(BX, kBandCap), SBY = kBandCap / SBX;
+    bar(1);                                   // sBox is rewritten by the next level
     for (int by0 = 0; by0 < BY; by0 += SBY) {
       for (int bx0 = 0; bx0 < BX; bx0 += SBX) {
         const int bw = min(SBX, BX - bx0), bh = min(SBY, BY - by0);
@@ -1053,9 +1070,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
         if (!band_any) continue;              // empty band (also the barrier after the last one)
         const int ncell = bw * bh, nmt = (ncell + 31) >> 5;
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int i = tid; i < nmt * 32 * (kWP8 / 4); i += 256) reinterpret_cast<float4*>(sW)[i] = z4;
-        for (int i = tid; i < nmt * 32; i += 256) sHit[i] = 0;
-        bar(4);
+        // Dm pitch: the band's cell tiles + 4 (keeps the Dm overlay inside the rows W used)
+        const int dp = ZAFTER ? nmt * 32 + 4 : kDP;
+        if (!ZAFTER) {
+          for (int i = tid; i < nmt * 32 * (kWP8 / 4); i += 256) reinterpret_cast<float4*>(sW)[i] = z4;
+          for (int i = tid; i < nmt * 32; i += 256) sHit[i] = 0;
+          bar(4);
+        }
 #pragma unroll
         for (int pt = 0; pt < P; ++pt) {      // a query's 4 points are lanes of one wave: take turns
           if (tpt == pt) {
@@ -1063,7 +1084,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
             for (int k = 0; k < 4; ++k)
               if (cell[k] >= 0) {
                 sW[cell[k] * kWP8 + tq] += cw[k];
-                sHit[cell[k]] = 1;
+                if (!ZAFTER) sHit[cell[k]] = 1;
               }
           }
           wave_sync();
@@ -1091,7 +1112,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int c = 32 * m + crow(i, hh);
-            if (c < ncell && sHit[c]) {
+            // ZAFTER: a cell no tap touched has an all-zero W row, so its product is +0
+            // exactly and is skipped like an unhit cell (adding 0 would not change
+            // grad_value either: it starts at +0 and never becomes -0; grad_out finite)
+            if (c < ncell && (ZAFTER ? acc[i] != 0.f : sHit[c] != 0)) {
               const int y = oy + by0 + c / bw, x = ox + bx0 + c % bw;
               atomicAdd(gvalue + lbase + (size_t)(y * Wl + x) * rowstride + r, acc[i]);
             }
@@ -1120,14 +1144,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
               acc = mfma16(*reinterpret_cast<const bf16x8_t*>(ga), bv[0], acc);
               acc = mfma16(*reinterpret_cast<const bf16x8_t*>(ga + 16), bv[1], acc);
 #pragma unroll
-              for (int i = 0; i < 16; ++i) sD[(32 * mq + crow(i, hh)) * kDP + 32 * wave + r] = acc[i];
+              for (int i = 0; i < 16; ++i) sD[(32 * mq + crow(i, hh)) * dp + 32 * wave + r] = acc[i];
             }
           }
           bar(32);
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            if (cell[k] >= 0) dk[k] += sD[tq * kDP + cell[k]];
+            if (cell[k] >= 0) dk[k] += sD[tq * dp + cell[k]];
           bar(64);                            // Dm is overwritten by the next band's W
+        }
+        if (ZAFTER) {
+          // clear W for the next band: wave w clears only the columns it writes (its 16
+          // queries), over every row this band's W or Dm touched, so no other wave's next
+          // build can race with the clear and no barrier is needed; Dm leftovers in the
+          // pad columns are never read as W, and Dm itself is always written before read
+          // Rows in blocks of 16; within a 16-lane group the rows are 4 apart, so the group's
+          // 16-B stores cover all 64 banks once (pitch 68: bank = 4 row + column).
+          const int zr = GEOM ? min(kBandCap, max(nmt * 32, (64 * dp + kWP8 - 1) / kWP8)) : nmt * 32;
+          const int zrow = 4 * ((lane >> 2) & 3) + (lane >> 4);
+          for (int rb = 0; rb < zr; rb += 16)
+            *reinterpret_cast<float4*>(sW + (rb + zrow) * kWP8 + 16 * wave + 4 * (lane & 3)) = z4;
         }
       }
     }
@@ -1261,7 +1297,15 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     // msda_bwd_mfma_wg_kernel's bar(); default all; 0 = __syncthreads everywhere)
     int lbmask = 127;
     if (const char* e = getenv("VS_MSDA_LDSBAR")) lbmask = atoi(e);
-    if (mfma && fused)
+    // VS_MSDA_SKEL: band skeleton variant (2, default: clear-after; 0: zero-fill + barrier
+    // at every band start)
+    int skel = kMsdaSkelDefault;
+    if (const char* e = getenv("VS_MSDA_SKEL")) skel = atoi(e);
+    if (mfma && fused && skel == 2)
+      hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true, 2>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
+                         (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc, gattw,
+                         lbmask);
+    else if (mfma && fused)
       hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
                          (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc, gattw,
                          lbmask);
