@@ -266,3 +266,41 @@ def test_prefetch_loader_matches_serial_batches(tmp_path):
                 assert torch.allclose(gi, ei) and all(torch.equal(x, y) for x, y in zip(gm, em))
                 assert all(torch.equal(x, y) for x, y in zip(gc, ec))
                 k += 1
+
+
+def test_pad_buckets_and_mixed_aspect_loader(tmp_path):
+    """The seam's padding canvases: (512, 640, 800) for the reference's MIN_SIZE_TRAIN
+    480..640 / MAX_SIZE_TRAIN 800 (train_full.py:244-245); a bucketed batch equals the
+    detectron2-padded batch zero-extended to the canvas (image and masks), so only the
+    amount of zero padding changes; multi-scale mixed-aspect data gives at most 9 shapes."""
+    from visionseg.adapters import MAX_SIZE_TRAIN, MIN_SIZE_TRAIN
+    from visionseg.data import PrefetchLoader, bucket_size, default_pad_buckets
+    bk = default_pad_buckets(MIN_SIZE_TRAIN, MAX_SIZE_TRAIN)
+    assert bk == (512, 640, 800)
+    assert [bucket_size(n, 32, bk) for n in (480, 481, 512, 513, 640, 641, 800, 801)] == \
+        [512, 512, 512, 640, 640, 800, 800, 832]
+    assert bucket_size(481) == 512 and bucket_size(480) == 480
+    write_coco_dataset(str(tmp_path), 12, [(120, 160), (160, 120), (100, 100)], seed=2)
+    ds = CocoInstanceDataset(str(tmp_path), min_size=(60, 64, 68, 72, 76, 80), max_size=100, train=True, seed=4)
+    small = default_pad_buckets(ds.min_size, ds.max_size)
+    assert small == (64, 96, 128)     # 64, 80 -> 96, 100 -> 128 (rounded to 32)
+    shapes = set()
+    for buckets in (None, small):
+        ds.rng = np.random.default_rng(4)
+        ld = PrefetchLoader(ds, 3, 8, seed=5, num_workers=0, device="cpu", pad_buckets=buckets)
+        for imgs, masks, classes in ld:
+            H, W = imgs.shape[-2:]
+            if buckets:
+                assert H in small and W in small
+                shapes.add((H, W))
+            assert all(m.shape[-2:] == (H, W) for m in masks)
+    assert len(shapes) <= 9
+    # bucketed == exact padding, zero-extended
+    ds.rng = np.random.default_rng(9)
+    samples = [ds[i] for i in range(3)]
+    from visionseg.data import collate_host
+    ei, es, em, ec = collate_host(samples)
+    bi, bs, bm, bc = collate_host(samples, buckets=small)
+    h, w = ei.shape[-2:]
+    assert torch.equal(bi[..., :h, :w], ei) and int(bi[..., h:, :].sum()) == 0 and int(bi[..., :, w:].sum()) == 0
+    assert torch.equal(es, bs) and all(torch.equal(x[:, :h, :w], y) and not x[:, h:].any() for x, y in zip(bm, em))

@@ -249,3 +249,17 @@ def test_init_detector_maskdino_backbone_from_config_or_checkpoint(tmp_path):
             (64, (1, 1, 3, 1), (2, 4, 8, 16), 5, 3)
     with pytest.raises(ValueError):
         backbone_from_state_dict({"backbone.patch_embed.proj.weight": torch.zeros(8, 3, 4, 4)})
+
+
+def test_point_sample_rows_matches_grid_sample():
+    """The criterion's per-query label sampler (each query reads only its own target map)
+    == grid_sample on the gathered maps, incl. points outside [0, 1] and the border."""
+    from visionseg.maskdino import _point_sample, _point_sample_rows
+    g = torch.Generator().manual_seed(3)
+    maps = (torch.rand(6, 17, 23, generator=g) > 0.5).float()
+    rows = torch.tensor([0, 5, 2, 2, 3, 1, 4, 0], dtype=torch.int64)
+    coords = torch.rand(8, 50, 2, generator=g) * 1.2 - 0.1
+    coords[0, :4] = torch.tensor([[0.0, 0.0], [1.0, 1.0], [0.0, 1.0], [1.0, 0.0]])
+    exp = _point_sample(maps[rows][:, None], coords)
+    got = _point_sample_rows(maps, rows, coords)
+    assert float((got - exp).abs().max()) <= 1e-6

@@ -27,7 +27,7 @@ import torch
 import torch.distributed as dist
 
 from .criterion import SetCriterion
-from .data import CocoInstanceDataset, PrefetchLoader
+from .data import CocoInstanceDataset, PrefetchLoader, default_pad_buckets
 from .evaluate import MaskAPEvaluator
 from .inference import Predictor
 from .model import M2FConfig, Mask2Former
@@ -38,6 +38,10 @@ HYPERPARAMS = {   # defaults of training/train_template.py:45-57
     "lr_scheduler": "cosine", "warmup_epochs": 5, "img_size": 640, "random_seed": 42,
     "early_stopping_patience": 15, "save_period": 10,
 }
+# INPUT.MIN_SIZE_TRAIN / MAX_SIZE_TRAIN of training/maskdino/train_full.py:244-245 (at
+# img_size 640; scaled with img_size otherwise)
+MIN_SIZE_TRAIN = (480, 512, 544, 576, 608, 640)
+MAX_SIZE_TRAIN = 800
 
 
 def evaluate_dir(model: Mask2Former, test_dir, img_size: int = 640, device="cuda", max_images: int | None = None):
@@ -59,7 +63,14 @@ def evaluate_dir(model: Mask2Former, test_dir, img_size: int = 640, device="cuda
 
 
 def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, backbone: str = "swin_t",
-                      device=None, max_iters: int | None = None, arch: str = "mask2former"):
+                      device=None, max_iters: int | None = None, arch: str = "mask2former", step_callback=None):
+    """Multi-scale training as the reference's mapper does it (ResizeShortestEdge over
+    MIN_SIZE_TRAIN / MAX_SIZE_TRAIN, random flip; hyperparams "min_size_train",
+    "max_size_train" override).  Batches are padded to a few canvases
+    (`data.default_pad_buckets`, hyperparams "pad_buckets": a list, or [] for detectron2's
+    pad-to-the-batch-max); the trainer keeps one HIP graph per padded shape (LRU, one
+    memory pool).  `step_callback(it, trainer, images)` runs after every step (timing
+    tools)."""
     hp = dict(HYPERPARAMS)
     hp.update(hyperparams or {})
     train_dir, output_dir = Path(train_dir), Path(output_dir)
@@ -72,8 +83,13 @@ def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, ba
     seed = int(hp["random_seed"])
     torch.manual_seed(seed + rank)
     img = int(hp["img_size"])
-    ds = CocoInstanceDataset(str(train_dir), min_size=(img,), max_size=int(round(img * 1.25)), train=True,
-                             seed=seed + rank)
+    min_sizes = tuple(int(v) for v in hp.get("min_size_train") or
+                      [int(round(m * img / 640)) for m in MIN_SIZE_TRAIN])
+    max_size = int(hp.get("max_size_train") or int(round(MAX_SIZE_TRAIN * img / 640)))
+    pad_buckets = hp.get("pad_buckets", "auto")
+    if pad_buckets == "auto":
+        pad_buckets = default_pad_buckets(min_sizes, max_size)
+    ds = CocoInstanceDataset(str(train_dir), min_size=min_sizes, max_size=max_size, train=True, seed=seed + rank)
     backbone = str(hp.get("backbone", backbone))
     if arch == "maskdino":
         from .maskdino import MaskDINO, MaskDINOConfig, MaskDINOCriterion
@@ -97,15 +113,18 @@ def train_mask2former(exp_name, train_dir, test_dir, output_dir, hyperparams, ba
                           amp=device.type == "cuda")
     # HIP-graph replay of the step for every batch signature seen more than twice (image
     # size after ResizeShortestEdge + padding, padded target capacity)
-    trainer = Trainer(model, criterion, solver, device=device, graphs=device.type == "cuda")
+    trainer = Trainer(model, criterion, solver, device=device, graphs=device.type == "cuda",
+                      max_graphs=int(hp.get("max_graphs", 16)))
     output_dir.mkdir(parents=True, exist_ok=True)
     # the serial loop's batches (per-epoch seeded permutation, rank r takes its slots of
     # each global batch), mapped in worker processes and prefetched to the device
     loader = PrefetchLoader(ds, per_rank, total, rank=rank, world=world, seed=seed,
-                            num_workers=int(hp.get("workers", 4)), device=device)
+                            num_workers=int(hp.get("workers", 4)), device=device, pad_buckets=pad_buckets)
     save_every = int(hp.get("save_period") or 0) * iters_per_epoch
     for it, (images, masks, classes) in enumerate(loader, start=1):
         trainer.step(images, masks, classes)
+        if step_callback is not None:
+            step_callback(it, trainer, images)
         if save_every and it % save_every == 0:
             trainer.save(str(output_dir / f"model_epoch{it // iters_per_epoch:04d}.pth"))
     trainer.save(str(output_dir / "model_final.pth"))

@@ -124,17 +124,21 @@ def synthetic_batch(batch: int, size: int, seed: int = 42, device="cpu"):
     return images, masks, classes
 
 
-def write_coco_dataset(root: str, n_images: int, size: int, seed: int = 42, category: str = "thunderbolt"):
-    """Write `root/annotations.json` + `root/images/*.png` in the reference's COCO layout."""
+def write_coco_dataset(root: str, n_images: int, size, seed: int = 42, category: str = "thunderbolt"):
+    """Write `root/annotations.json` + `root/images/*.png` in the reference's COCO layout.
+    `size`: a side length (square images) or a list of (height, width) cycled over the
+    images (mixed aspect ratios)."""
     os.makedirs(os.path.join(root, "images"), exist_ok=True)
     rng = np.random.default_rng(seed)
+    shapes = [(int(size), int(size))] if isinstance(size, int) else [(int(h), int(w)) for h, w in size]
     images, anns = [], []
     aid = 1
     for i in range(n_images):
-        im, masks, _, polys = synthetic_sample(rng, size, size)
+        H, W = shapes[i % len(shapes)]
+        im, masks, _, polys = synthetic_sample(rng, H, W)
         fn = f"{i:06d}.png"
         Image.fromarray(np.transpose(im, (1, 2, 0))).save(os.path.join(root, "images", fn))
-        images.append({"id": i, "file_name": fn, "height": size, "width": size})
+        images.append({"id": i, "file_name": fn, "height": H, "width": W})
         for m, p in zip(masks, polys):
             ys, xs = np.nonzero(m)
             bbox = [float(xs.min()), float(ys.min()), float(xs.max() - xs.min() + 1), float(ys.max() - ys.min() + 1)] \
@@ -235,14 +239,36 @@ def collate_padded(samples, size_divisibility: int = 32, device="cpu"):
 # ----------------------------------------------------------------------------------
 
 
-def collate_host(samples, size_divisibility: int = 32):
+def bucket_size(n: int, size_divisibility: int = 32, buckets=None) -> int:
+    """A padded side: n rounded up to `size_divisibility` (detectron2 ImageList), then --
+    with `buckets` (ascending side lengths) -- up to the smallest bucket that holds it (a
+    side above the largest bucket keeps its 32-rounded size)."""
+    n = (n + size_divisibility - 1) // size_divisibility * size_divisibility
+    for b in buckets or ():
+        if n <= b:
+            return int(b)
+    return n
+
+
+def default_pad_buckets(min_sizes, max_size, size_divisibility: int = 32):
+    """The seam's padding canvases for ResizeShortestEdge(min_sizes, max_size): per side
+    the second-smallest and the largest short-edge choice and the long-edge limit, each
+    rounded up to `size_divisibility` -- (512, 640, 800) for the reference's
+    MIN_SIZE_TRAIN 480..640 / MAX_SIZE_TRAIN 800 (train_full.py:244-245): at most 9
+    padded shapes per run, so the trainer's graphs and MIOpen's per-shape solver search
+    are paid a bounded number of times."""
+    r = lambda n: (int(n) + size_divisibility - 1) // size_divisibility * size_divisibility   # noqa: E731
+    ms = sorted(int(m) for m in min_sizes)
+    return tuple(sorted({r(ms[min(1, len(ms) - 1)]), r(ms[-1]), r(max_size)}))
+
+
+def collate_host(samples, size_divisibility: int = 32, buckets=None):
     """CPU half of collate_padded, run inside the loader workers: uint8 images padded to a
-    common size divisible by 32 [B,3,H,W], the (unpadded) image sizes, masks padded to the
-    same size (bool [K,H,W] per image), classes.  Normalisation happens on the device."""
-    H = max(s[0].shape[1] for s in samples)
-    W = max(s[0].shape[2] for s in samples)
-    H = (H + size_divisibility - 1) // size_divisibility * size_divisibility
-    W = (W + size_divisibility - 1) // size_divisibility * size_divisibility
+    common size divisible by 32 [B,3,H,W] (or to a bucket canvas, `bucket_size`), the
+    (unpadded) image sizes, masks padded to the same size (bool [K,H,W] per image),
+    classes.  Normalisation happens on the device."""
+    H = bucket_size(max(s[0].shape[1] for s in samples), size_divisibility, buckets)
+    W = bucket_size(max(s[0].shape[2] for s in samples), size_divisibility, buckets)
     imgs = torch.zeros(len(samples), 3, H, W, dtype=torch.uint8)
     sizes = torch.zeros(len(samples), 2, dtype=torch.int64)
     masks, classes = [], []
@@ -308,14 +334,19 @@ class PrefetchLoader:
     uint8 batches into pinned host memory; the iterator copies batch i+1 to the device on a
     side stream (non-blocking) while the caller trains on batch i, and normalises on the
     device.  Yields (images f32 [B,3,H,W], masks [bool [K,H,W]], classes [int64 [K]]) on
-    `device`, like collate_padded."""
+    `device`, like collate_padded.  `pad_buckets`: pad each batch to a canvas side from
+    this list (`bucket_size`) instead of its largest image rounded to 32: more zero
+    padding -- what detectron2 does to a batch whose largest image has that size -- in
+    exchange for a handful of distinct batch shapes."""
 
     def __init__(self, dataset, per_rank: int, iters: int, rank: int = 0, world: int = 1, seed: int = 42,
-                 num_workers: int = 4, device="cuda", prefetch_factor: int = 2):
+                 num_workers: int = 4, device="cuda", prefetch_factor: int = 2, pad_buckets=None):
+        import functools
         self.device = torch.device(device)
         pin = self.device.type == "cuda"
         sampler = _EpochSampler(len(dataset), per_rank, rank, world, seed, iters)
-        kw = dict(num_workers=num_workers, collate_fn=collate_host, pin_memory=pin, batch_sampler=sampler)
+        collate = functools.partial(collate_host, buckets=tuple(pad_buckets) if pad_buckets else None)
+        kw = dict(num_workers=num_workers, collate_fn=collate, pin_memory=pin, batch_sampler=sampler)
         if num_workers > 0:
             kw.update(worker_init_fn=_seed_worker, prefetch_factor=prefetch_factor, persistent_workers=False)
         self.loader = torch.utils.data.DataLoader(dataset, **kw)

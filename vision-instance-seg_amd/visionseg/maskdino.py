@@ -420,6 +420,29 @@ def _point_sample(feat, coords):
     return F.grid_sample(feat, 2.0 * coords.unsqueeze(2) - 1.0, align_corners=False).squeeze(3).squeeze(1)
 
 
+def _point_sample_rows(maps, rows, coords):
+    """maps [M, H, W] f32, rows [N] int64 (which map each of N point sets reads), coords
+    [N, P, 2] in [0, 1] -> [N, P]: `_point_sample(maps[rows][:, None], coords)` without
+    materialising maps[rows] (grid_sample's bilinear rule, align_corners=False, zeros
+    outside: the corner weights and the unnormalisation ((g + 1) * size - 1) / 2 of
+    ATen's grid sampler), four gathers of the flattened maps."""
+    M, H, W = maps.shape
+    flat = maps.reshape(-1)
+    g = 2.0 * coords - 1.0
+    ix = ((g[..., 0] + 1) * W - 1) / 2
+    iy = ((g[..., 1] + 1) * H - 1) / 2
+    x0, y0 = torch.floor(ix), torch.floor(iy)
+    x1, y1 = x0 + 1, y0 + 1
+    base = (rows * (H * W))[:, None]
+    out = torch.zeros_like(ix)
+    for xx, yy, wgt in ((x0, y0, (x1 - ix) * (y1 - iy)), (x1, y0, (ix - x0) * (y1 - iy)),
+                        (x0, y1, (x1 - ix) * (iy - y0)), (x1, y1, (ix - x0) * (iy - y0))):
+        inside = (xx >= 0) & (xx <= W - 1) & (yy >= 0) & (yy <= H - 1)
+        idx = base + (yy.clamp(0, H - 1).long() * W + xx.clamp(0, W - 1).long())
+        out = out + torch.where(inside, flat[idx], 0.0) * wgt
+    return out
+
+
 class MaskDINOCriterion:
     """Hungarian matching (focal class 4 + L1 box 5 + GIoU 2 + point-sampled mask BCE 5
     + dice 5) of every decoder step and of the two-stage selection, solved on the device
@@ -491,9 +514,9 @@ class MaskDINOCriterion:
         """pred [B, R, H, W]: the logits of R queries per image; tmask [B, Kc, Ht, Wt] f32
         the targets; slot [B, R] the target slot each query is paired with; keep [B, R]
         bool.  Importance-sampled point BCE and dice (HF:m2f:671-724 semantics).  The
-        labels: every target channel of the image sampled at all R x P points of its
-        queries (one grid_sample per batch, fixed shapes whatever the pairing), then each
-        query's own slot picked."""
+        labels: each query's own target (row b * Kc + slot of the flattened targets)
+        sampled at that query's P points (`_point_sample_rows`: fixed shapes whatever the
+        pairing, work and memory independent of Kc)."""
         c = self.cfg
         B, R = pred.shape[:2]
         Kc = tmask.shape[1]
@@ -508,9 +531,8 @@ class MaskDINOCriterion:
             coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
             if P - nu > 0:
                 coords = torch.cat([coords, torch.rand(N, P - nu, 2, device=pred.device)], 1)
-            grid = (2.0 * coords - 1.0).view(B, R * P, 1, 2)
-            lab = F.grid_sample(tmask, grid, align_corners=False).view(B, Kc, R, P)
-            lab = torch.gather(lab, 1, slot[:, None, :, None].expand(B, 1, R, P)).reshape(N, P)
+            rows = (torch.arange(B, device=pred.device)[:, None] * Kc + slot.clamp(0, Kc - 1)).reshape(N)
+            lab = _point_sample_rows(tmask.reshape(B * Kc, *tmask.shape[-2:]), rows, coords)
         logit = _point_sample(pred.float(), coords)
         keep = keep.reshape(N)
         zero = torch.zeros((), device=pred.device)

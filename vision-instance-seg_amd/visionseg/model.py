@@ -208,7 +208,8 @@ class PatchEmbed(nn.Module):
         if not (px.is_cuda and torch.is_grad_enabled()):   # inference keeps the conv: its graph
             x = self.proj(px)                              # replay is bit-identical to eager
             return x.flatten(2).transpose(1, 2), h, w
-        patches = px.view(B, Ci, h, 4, w, 4).permute(0, 2, 4, 1, 3, 5).reshape(B * h * w, Ci * 16)
+        # reshape, not view: a channels_last (or otherwise strided) batch is copied here
+        patches = px.reshape(B, Ci, h, 4, w, 4).permute(0, 2, 4, 1, 3, 5).reshape(B * h * w, Ci * 16)
         wt = self.proj.weight
         y = linear_tokens(patches, wt.view(wt.shape[0], -1), self.proj.bias)
         return y.view(B, h * w, -1), h, w

@@ -26,6 +26,7 @@ cast of the whole model is two kernels.
 from __future__ import annotations
 
 import os
+from collections import OrderedDict
 from dataclasses import dataclass
 
 import torch
@@ -107,7 +108,8 @@ class Trainer:
     criterion: callable(masks, classes, mask_labels, class_labels) -> (loss, parts)."""
 
     def __init__(self, model, criterion, solver: SolverConfig | None = None, device=None,
-                 distributed: bool | None = None, graphs: bool = False, graph_warmup: int = 2):
+                 distributed: bool | None = None, graphs: bool = False, graph_warmup: int = 2,
+                 max_graphs: int = 8):
         self.solver = s = solver or SolverConfig()
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
@@ -144,7 +146,13 @@ class Trainer:
         # at least two eager steps of a signature before its capture (lazy library state
         # and the optimiser's state exist before the capture records anything)
         self.graph_warmup = max(2, int(graph_warmup))
-        self._graph_states, self._eager_seen = {}, {}
+        # live graphs per signature, least recently replayed first; all of them capture into
+        # ONE memory pool (see _capture), so keeping several costs the largest graph's
+        # activations, not the sum
+        self.max_graphs = max(1, int(max_graphs))
+        self._graph_states, self._eager_seen = OrderedDict(), {}
+        self._pool = None
+        self.captures = 0
         if self.split:
             self.num_masks_total = torch.zeros((), device=self.device, dtype=torch.float32)
         self.iter = 0
@@ -219,11 +227,17 @@ class Trainer:
         st = {"images": images.clone(), "tg": PaddedTargets.from_lists(mask_labels, class_labels, kc=kc,
                                                                        device=self.device), "graphs": []}
         torch.cuda.synchronize(self.device)
-        # one live graph per trainer (see _graph_step).  The BLAS workspace cached per
-        # (handle, capture stream) is dropped before and after every capture, so each
-        # graph allocates its own inside its pool (torch/_inductor/cudagraph_trees.py
-        # clear_cublass_cache does the same)
-        pool = torch.cuda.graph_pool_handle()
+        # every signature's graph captures into the trainer's one private pool: a block that
+        # is a temporary of one graph may be a temporary of another, which is safe because
+        # the graphs replay one after another on one stream and nothing a graph leaves
+        # behind is read after another replay (the loss is cloned right after its replay;
+        # gradients, weights and optimiser state live outside the pool).  The BLAS
+        # workspace cached per (handle, capture stream) is dropped before and after every
+        # capture, so each graph allocates its own inside the pool
+        # (torch/_inductor/cudagraph_trees.py clear_cublass_cache does the same)
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        pool = self._pool
         torch._C._cuda_clearCublasWorkspaces()
         # several ranks: "thread_local" capture, so RCCL's watchdog thread may keep querying
         # the events of earlier eager collectives while this thread captures
@@ -243,33 +257,37 @@ class Trainer:
         torch._C._cuda_clearCublasWorkspaces()
         from .model import cached_constants
         st["constants"] = cached_constants()      # alive as long as the graphs that read them
+        self.captures += 1
         return st
 
-    def _drop_graphs(self):
-        if not self._graph_states:
+    def _drop_graphs(self, keep: int = 0):
+        """Destroy graphs, least recently replayed first, until at most `keep` remain."""
+        if len(self._graph_states) <= keep:
             return
-        for st in self._graph_states.values():
+        while len(self._graph_states) > keep:
+            _, st = self._graph_states.popitem(last=False)
             for g in st["graphs"]:
                 g.reset()
-        self._graph_states.clear()
         torch.cuda.synchronize(self.device)
 
     @staticmethod
     def target_capacity(class_labels) -> int:
         """Padded target capacity of a batch: its largest target count rounded up to a
-        multiple of 4, so batches whose counts vary (real COCO data) share a graph."""
+        multiple of 4 up to 16, to the next power of two above, so batches whose counts
+        vary (real COCO data) share a few graphs.  The padding slots carry no loss and
+        no matching cost (criterion.PaddedTargets), so the capacity changes no result."""
         kc = max([int(c.shape[0]) for c in class_labels] + [0])
-        return max(4, (kc + 3) // 4 * 4)
+        if kc <= 16:
+            return max(4, (kc + 3) // 4 * 4)
+        return 1 << (kc - 1).bit_length()
 
     def _graph_step(self, images, mask_labels, class_labels):
         kc = self.target_capacity(class_labels)
         key = (tuple(images.shape), images.dtype, kc, tuple(mask_labels[0].shape[-2:]) if mask_labels else ())
         st = self._graph_states.get(key)
-        if st is None:
-            # one live graph per trainer (bounded pool memory): another signature's graph
-            # is destroyed before any eager work of this one, and a returning signature is
-            # captured again
-            self._drop_graphs()
+        if st is not None:
+            self._graph_states.move_to_end(key)
+        else:
             seen = self._eager_seen.get(key, 0)
             if seen < self.graph_warmup:
                 # eager steps first: lazy library state and the optimiser's state exist
@@ -278,6 +296,7 @@ class Trainer:
                 if self.split:
                     self._set_num_masks(class_labels)
                 return self.eager_step(images, mask_labels, class_labels)
+            self._drop_graphs(keep=self.max_graphs - 1)      # the least recently replayed goes
             st = self._graph_states[key] = self._capture(images, mask_labels, class_labels, kc)
         self._set_lr()
         with torch.no_grad():
@@ -297,8 +316,10 @@ class Trainer:
         graphs=True the step is captured per signature (image shape, padded target
         capacity of the batch; after `graph_warmup` eager steps of it) and replayed with the batch's
         targets padded into static buffers (capacity: the largest count rounded up to a
-        multiple of 4): one launch per graph instead of ~3000 per step.  One signature's
-        graph lives at a time: another signature destroys it and is captured in its place."""
+        multiple of 4): one launch per graph instead of ~3000 per step.  Up to `max_graphs`
+        signatures keep their graphs (least recently replayed dropped first), all in one
+        memory pool, so a stream of mixed shapes (multi-scale COCO batches) replays instead
+        of recapturing."""
         if self.graphs:
             loss = self._graph_step(images, mask_labels, class_labels)
         else:
