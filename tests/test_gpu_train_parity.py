@@ -134,33 +134,13 @@ def _rel_l2(a, b, floor):
     return float((a - b).norm()) / max(float(b.norm()), floor)
 
 
-def test_bf16_training_step_vs_oracle():
-    """The PRODUCTION training step (bf16 Trainer: MFMA window attention fwd/bwd, the
-    MFMA MSDA backward with grad_loc / grad_attn in its band walk, MFMA masked attention,
-    the fused mask-head backward through the point-scatter kernel, bf16 GEMMs, the
-    flat-buffer optimiser) vs the oracle (RefMask2Former + RefCriterion + the reference's
-    solver, fp32 on CPU), Swin-T at 256^2, on the same bf16-rounded weights and input
-    and the same point draws (HF:m2f:726-779 losses, train_full.py:266-271 clip).
+SEEDS_BF16 = ((78, 6, 7), (178, 16, 17), (278, 26, 27))     # (weights, batch, point draws)
 
-    Decisions are forced from the fp32 oracle into the other runs: the decoder's attention
-    masks (mask_override), the Hungarian matching of every decoder step and the
-    importance-sampling top-k choice (tests/_draws.ForcedDecisions).
 
-    Yardstick: the oracle ITSELF run in bf16 (torch CPU bf16 kernels, same weights,
-    forced decisions).  Per parameter, the error is the relative L2 distance to the fp32
-    oracle's gradient (norm floor 1e-2 of the median parameter gradient norm: gradients
-    that are analytically ~0, e.g. the key bias of a softmax attention, are rounding
-    noise on every path).  Bounds (stated here, measured values in the print):
-      * loss: |ours - fp32| <= 1.25 x |oracle-bf16 - fp32| + 2e-3 x loss;
-      * gradients: the median over parameters of ours <= 1.25 x the yardstick's, the 90th
-        percentile <= 1.5 x; every parameter's absolute L2 error <= max(2 x the
-        yardstick's, 0.05 x the median parameter-gradient norm), or its relative error
-        inside 2.5 x the yardstick's p90 (round 3 on the box, MIOpen solvers fixed:
-        library decoder Linears median 2.8e-2 vs 3.29e-2, p90 5.5e-2 vs 5.47e-2, loss
-        86.613; decoder Linears on csrc/small_linear.hip median 3.2e-2, p90 7.9e-2, loss
-        86.680; oracle-bf16 86.701 / fp32 86.771);
-      * weight updates of the step (per-parameter clip to norm 0.01, SGD): the same two
-        percentile bounds against the yardstick's update."""
+def _bf16_step_errors(wseed, bseed, dseed):
+    """One seed of test_bf16_training_step_vs_oracle: the per-parameter relative L2 errors
+    of the bf16 Trainer step (ours) and of the oracle run in bf16 (yardstick) against the
+    fp32 oracle, for the gradients and the weight updates, plus the three losses."""
     from _draws import ForcedDecisions
     from visionseg.criterion import SetCriterion
     from visionseg.data import synthetic_batch
@@ -169,13 +149,13 @@ def test_bf16_training_step_vs_oracle():
     cfg = M2FConfig.preset("swin_t")
     rcfg = RefConfig.from_dict(cfg.to_dict())
     ref = RefMask2Former(rcfg)
-    sd = det_init({k: v.shape for k, v in ref.state_dict().items()}, 78)
+    sd = det_init({k: v.shape for k, v in ref.state_dict().items()}, wseed)
     sd = {k: (v.to(torch.bfloat16).float() if v.is_floating_point() else v) for k, v in sd.items()}
     ref.load_state_dict(sd)
     ref.train()
-    imgs, ml, cl = synthetic_batch(2, 256, seed=6)
+    imgs, ml, cl = synthetic_batch(2, 256, seed=bseed)
     imgs = imgs.to(torch.bfloat16).float()
-    draws = ForcedDecisions(2, max(len(c) for c in cl) + 1, seed=7)
+    draws = ForcedDecisions(2, max(len(c) for c in cl) + 1, seed=dseed)
     s = SolverConfig(optimizer="sgd", warmup_iters=0, lr=0.05)
     lr = lr_at(s, 0)
 
@@ -212,8 +192,7 @@ def test_bf16_training_step_vs_oracle():
 
     # ---- product: one bf16 Trainer step on the GPU.  MIOpen's convolution solvers fixed
     # (deterministic choice, no Find): with Find the solver of a conv shape is picked by
-    # timing, a different one in another process, and the step's bf16 rounding -- loss
-    # 86.63 .. 86.90 over runs -- with it; the bounds below are for one fixed kernel set
+    # timing, a different one in another process, and the step's bf16 rounding with it
     import dataclasses
     bench_state = (torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic)
     torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = False, True
@@ -233,46 +212,82 @@ def test_bf16_training_step_vs_oracle():
     finally:
         torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = bench_state
     up = {n: m.detach().cpu() - w0[n] for n, m in zip(tr.opt.names, tr.master_params())}
-    lp = float(loss)
-
     assert set(gp) == set(g32)
     names = sorted(g32)
     gfloor = 1e-2 * float(np.median([float(g32[n].norm()) for n in names]))
     ufloor = 1e-3 * float(np.median([float(u32[n].norm()) for n in names]))
-    eg = {n: _rel_l2(gp[n], g32[n], gfloor) for n in names}
-    yg = {n: _rel_l2(g16[n], g32[n], gfloor) for n in names}
-    eu = {n: _rel_l2(up[n], u32[n], ufloor) for n in names}
-    yu = {n: _rel_l2(u16[n], u32[n], ufloor) for n in names}
+    return dict(
+        loss=(float(loss), l16, l32),
+        eg={n: _rel_l2(gp[n], g32[n], gfloor) for n in names}, yg={n: _rel_l2(g16[n], g32[n], gfloor) for n in names},
+        eu={n: _rel_l2(up[n], u32[n], ufloor) for n in names}, yu={n: _rel_l2(u16[n], u32[n], ufloor) for n in names},
+        dist={n: float((gp[n].double() - g32[n].double()).norm()) / (gfloor / 1e-2) for n in names},
+        ydist={n: float((g16[n].double() - g32[n].double()).norm()) / (gfloor / 1e-2) for n in names})
+
+
+def _family(name):
+    """decoder.layers.6.fc2.weight -> decoder.layers.*.fc2.weight"""
+    return ".".join("*" if p.isdigit() else p for p in name.split("."))
+
+
+def test_bf16_training_step_vs_oracle():
+    """The PRODUCTION training step (bf16 Trainer: MFMA window attention fwd/bwd, the
+    MFMA MSDA backward with grad_loc / grad_attn in its band walk, MFMA masked attention,
+    the fused mask-head backward through the point-scatter kernel, the decoder Linears on
+    csrc/small_linear.hip, bf16 GEMMs, the flat-buffer optimiser) vs the oracle
+    (RefMask2Former + RefCriterion + the reference's solver, fp32 on CPU), Swin-T at
+    256^2, on the same bf16-rounded weights and input and the same point draws
+    (HF:m2f:726-779 losses, train_full.py:266-271 clip), for THREE weight / batch / draw
+    seeds (SEEDS_BF16): one draw is one rounding realisation, so the gates are on the mean
+    over seeds of the per-seed ratio to the yardstick.
+
+    Decisions are forced from the fp32 oracle into the other runs: the decoder's attention
+    masks (mask_override), the Hungarian matching of every decoder step and the
+    importance-sampling top-k choice (tests/_draws.ForcedDecisions).
+
+    Yardstick: the oracle ITSELF run in bf16 (torch CPU bf16 kernels, same weights,
+    forced decisions).  Per parameter, the error is the relative L2 distance to the fp32
+    oracle's gradient (norm floor 1e-2 of the median parameter gradient norm: gradients
+    that are analytically ~0, e.g. the key bias of a softmax attention, are rounding
+    noise on every path).  Bounds:
+      * loss, per seed: |ours - fp32| <= 1.25 x |oracle-bf16 - fp32| + 2e-3 x loss;
+      * gradients: mean over seeds of (median over parameters of ours / the yardstick's)
+        <= 1.25, and the same for the 90th percentile;
+      * weight updates of the step (per-parameter clip to norm 0.01, SGD): the same two
+        bounds against the yardstick's update;
+      * defects: no parameter whose error is above both 3 x its yardstick's and 2.5 x the
+        yardstick's p90 (relative) and 5 % of the median gradient norm (absolute) on
+        EVERY seed (a wrong kernel gives O(1) errors on every draw).
+    The per-family mean ratios are printed (largest first) for a diagnosis."""
+    runs = [_bf16_step_errors(*sd) for sd in SEEDS_BF16]
     q = lambda d, p: float(np.percentile(list(d.values()), p))          # noqa: E731
-    ratio = sorted(((eg[n] / max(yg[n], 1e-12), n) for n in names), reverse=True)[:5]
-    print(f"bf16 step: loss ours {lp:.5f} / oracle-bf16 {l16:.5f} / fp32 {l32:.5f}; grad rel-L2 median "
-          f"{q(eg, 50):.2e} (yard {q(yg, 50):.2e}), p90 {q(eg, 90):.2e} (yard {q(yg, 90):.2e}), max {q(eg, 100):.2e} "
-          f"(yard {q(yg, 100):.2e}); update median {q(eu, 50):.2e} (yard {q(yu, 50):.2e}), p90 {q(eu, 90):.2e} "
-          f"(yard {q(yu, 90):.2e}); worst ratios {[(n, f'{r:.2f}', f'{eg[n]:.1e}') for r, n in ratio]}")
+    rg50 = [q(r["eg"], 50) / q(r["yg"], 50) for r in runs]
+    rg90 = [q(r["eg"], 90) / q(r["yg"], 90) for r in runs]
+    ru50 = [q(r["eu"], 50) / q(r["yu"], 50) for r in runs]
+    ru90 = [q(r["eu"], 90) / q(r["yu"], 90) for r in runs]
+    names = sorted(runs[0]["eg"])
+    fam = {}
+    for n in names:
+        fam.setdefault(_family(n), []).append(n)
+    fam_ratio = {f: float(np.mean([np.mean([r["eg"][n] for n in ns]) / max(np.mean([r["yg"][n] for n in ns]), 1e-12)
+                                   for r in runs])) for f, ns in fam.items()}
+    top = sorted(fam_ratio.items(), key=lambda kv: -kv[1])[:8]
+    for i, r in enumerate(runs):
+        lp, l16, l32 = r["loss"]
+        print(f"bf16 step seed {SEEDS_BF16[i]}: loss ours {lp:.5f} / oracle-bf16 {l16:.5f} / fp32 {l32:.5f}; grad "
+              f"rel-L2 median {q(r['eg'], 50):.2e} (yard {q(r['yg'], 50):.2e}), p90 {q(r['eg'], 90):.2e} (yard "
+              f"{q(r['yg'], 90):.2e}); update median {q(r['eu'], 50):.2e} (yard {q(r['yu'], 50):.2e}), p90 "
+              f"{q(r['eu'], 90):.2e} (yard {q(r['yu'], 90):.2e})")
+    print(f"bf16 step mean ratios over seeds: grad p50 {np.mean(rg50):.3f} p90 {np.mean(rg90):.3f}, update p50 "
+          f"{np.mean(ru50):.3f} p90 {np.mean(ru90):.3f}; per-seed grad p90 {[round(v, 3) for v in rg90]}; "
+          f"families (mean ratio to yardstick): {[(f, round(v, 2)) for f, v in top]}")
     if os.environ.get("VS_PARITY_DUMP"):                 # per-parameter errors for a diagnosis
         with open(os.environ["VS_PARITY_DUMP"], "w") as f:
-            json.dump({"eg": eg, "yg": yg, "eu": eu, "yu": yu}, f)
-    assert abs(lp - l32) <= 1.25 * abs(l16 - l32) + 2e-3 * abs(l32)
-    # p90 at 1.5x: the p90 is a property of one rounding realisation, not of the kernels'
-    # accuracy -- two kernel sets of equal per-layer accuracy (tools/decoder_layer_ab.py:
-    # every output / gradient of one decoder layer vs fp32 within 2 % of each other,
-    # profiles/r3_decoder_layer_ab.txt) gave p90 5.5e-2 and 7.9e-2 here, the difference
-    # being one decoder layer (6) whose every gradient doubled while layer 8's halved:
-    # bf16 noise amplified through nine attention layers
-    assert q(eg, 50) <= 1.25 * q(yg, 50) and q(eg, 90) <= 1.5 * q(yg, 90)
-    # per parameter, in absolute L2 terms: within 2x the yardstick's error, or within 5 % of
-    # the median parameter-gradient norm (tiny gradients -- the decoder self-attention's
-    # q / k weights at init -- are rounding noise on every bf16 path), or -- relative to the
-    # parameter's own gradient -- inside 2.5x the yardstick's p90 relative error (a
-    # parameter whose yardstick error happens to be small is held to the bf16 noise band,
-    # not to 2x a lucky draw: decoder.layers.8.fc2.weight 4.0e-2 vs its yardstick's 1.7e-2,
-    # the yardstick's p90 5.5e-2; the amplified layer above reaches 1.07e-1).  A defective
-    # kernel shows as O(1) relative errors, far outside this band
-    med = gfloor / 1e-2
-    dist = {n: float((gp[n].double() - g32[n].double()).norm()) for n in names}
-    ydist = {n: float((g16[n].double() - g32[n].double()).norm()) for n in names}
-    yband = 2.5 * q(yg, 90)
-    bad = [(n, dist[n] / med, ydist[n] / med, eg[n], yg[n]) for n in names
-           if dist[n] > max(2.0 * ydist[n], 0.05 * med) and eg[n] > yband]
-    assert not bad, bad[:5]
-    assert q(eu, 50) <= 1.25 * q(yu, 50) and q(eu, 90) <= 1.5 * q(yu, 90)
+            json.dump([{k: r[k] for k in ("eg", "yg", "eu", "yu", "loss")} for r in runs], f)
+    for r in runs:
+        lp, l16, l32 = r["loss"]
+        assert abs(lp - l32) <= 1.25 * abs(l16 - l32) + 2e-3 * abs(l32), r["loss"]
+    assert np.mean(rg50) <= 1.25 and np.mean(rg90) <= 1.25, (rg50, rg90)
+    assert np.mean(ru50) <= 1.25 and np.mean(ru90) <= 1.25, (ru50, ru90)
+    bad = [n for n in names if all(
+        r["eg"][n] > max(3.0 * r["yg"][n], 2.5 * q(r["yg"], 90)) and r["dist"][n] > 0.05 for r in runs)]
+    assert not bad, [(n, [round(r["eg"][n], 3) for r in runs], [round(r["yg"][n], 3) for r in runs]) for n in bad[:5]]

@@ -235,7 +235,9 @@ class Trainer:
         # workspace cached per (handle, capture stream) is dropped before and after every
         # capture, so each graph allocates its own inside the pool
         # (torch/_inductor/cudagraph_trees.py clear_cublass_cache does the same)
-        if self._pool is None:
+        # a pool lives while a graph holds it: once the last graph is reset, the allocator
+        # releases it and its handle cannot be captured into again
+        if self._pool is None or not self._graph_states:
             self._pool = torch.cuda.graph_pool_handle()
         pool = self._pool
         torch._C._cuda_clearCublasWorkspaces()
