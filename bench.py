@@ -82,6 +82,8 @@ def parse():
                     help="sgd: the reference's detectron2 DefaultTrainer solver; adamw: upstream train_net")
     ap.add_argument("--attn-fp8", action="store_true",
                     help="C5: Swin window attention on fp8 (e4m3) MFMA (window^2 <= 160; bf16 elsewhere)")
+    ap.add_argument("--linear-fp8", action="store_true",
+                    help="C5: the Swin blocks' K-deep Linears on the block-scaled MX fp8 MFMA (csrc/token_gemm.hip)")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--arch", default="mask2former", choices=["mask2former", "maskdino"],
                     help="mask2former (C1-C3, C5) or maskdino (C4: 300 queries, 4-level encoder, DN; parity unpinned)")
@@ -310,7 +312,7 @@ def _config_tag(model, size, arch="mask2former", fp8=False):
     if arch == "maskdino":
         return "C4 (per-GPU share)" if (model, size) == ("swin_l", 1024) else "custom"
     if (model, size) == ("swin_l", 1536):
-        return "C5 (per-GPU share, fp8 window attention)" if fp8 else "C5 shape (per-GPU share, bf16 attention)"
+        return "C5 (per-GPU share, fp8)" if fp8 else "C5 shape (per-GPU share, bf16)"
     return {("swin_t", 1024): "C2", ("swin_b", 1024): "C3 (per-GPU share)"}.get((model, size), "custom")
 
 
@@ -339,7 +341,7 @@ def main():
         model = MaskDINO(cfg).init_weights(seed=0)
         crit = MaskDINOCriterion(cfg, matcher=a.matcher)
     else:
-        cfg = M2FConfig.preset(a.model, num_queries=a.queries, attn_fp8=a.attn_fp8)
+        cfg = M2FConfig.preset(a.model, num_queries=a.queries, attn_fp8=a.attn_fp8, linear_fp8=a.linear_fp8)
         model = Mask2Former(cfg).init_weights(seed=0)
         crit = SetCriterion(cfg, matcher=a.matcher)
     trainer = Trainer(model, crit, SolverConfig(precision=a.precision, optimizer=a.optimizer), device=dev,
@@ -409,9 +411,10 @@ def main():
             "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic COCO-format defect batches (random-init weights)",
-            "config": {"workload": f"{_config_tag(a.model, a.size, a.arch, a.attn_fp8)}: {a.model} + {a.arch}, "
+            "config": {"workload": f"{_config_tag(a.model, a.size, a.arch, a.attn_fp8 or a.linear_fp8)}: {a.model} + {a.arch}, "
                                    f"{a.batch}x3x{a.size}^2 per GPU, {cfg.num_queries} queries, {prec}"
-                                   f"{', fp8 (e4m3) window attention' if a.attn_fp8 else ''}, 1 class",
+                                   f"{', fp8 (e4m3) window attention' if a.attn_fp8 else ''}"
+                                   f"{', MX-fp8 (e4m3 + e8m0 per 32) Swin Linears with K >= 384' if a.linear_fp8 else ''}, 1 class",
                        "model": f"{a.model}_{a.arch}", "global_batch": a.batch * world, "image_size": a.size,
                        "parallelism": f"dp{world}"},
             "final_loss": round(float(loss.item()), 4),

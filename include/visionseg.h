@@ -195,6 +195,28 @@ VS_API int vs_window_attn_backward_image(int dtype, int fp8, const void* qkv, co
                                          int height, int width, float scale, void* stream);
 
 
+/* ---- a5 / a6: token GEMM (the Swin block's Linears) ----------------------------------
+ * y[M, N] = x[M, K] w[N, K]^T + bias[N] (bf16 out, f32 accumulation), both operands
+ * K-contiguous rows: the F.linear of HF:swin:418-468 (qkv, proj) and HF:swin:511-536
+ * (fc1, fc2) over B * H * W tokens.  mode bits:
+ *   VS_TGEMM_FP8  : x, w are e4m3 bytes with one e8m0 scale byte per 32 elements along K
+ *                   (x_scales [M, K/32], w_scales [N, K/32], from vs_mx_quantize); the
+ *                   block-scaled MX MFMA (config C5's fp8 path); K % 128 == 0.
+ *                   Without it x, w are bf16 (K % 8 == 0).
+ *   VS_TGEMM_GELU : y = gelu(x w^T + b) with the exact erf GELU of HF `gelu`, and y_pre =
+ *                   the bf16 pre-activation (the input of the GELU's backward); the GELU is
+ *                   taken of the rounded pre-activation.
+ * bias may be NULL.  N % 4 == 0. */
+#define VS_TGEMM_FP8 1
+#define VS_TGEMM_GELU 2
+VS_API int vs_token_gemm(int mode, const void* x, const void* x_scales, const void* w, const void* w_scales,
+                         const void* bias, void* y, void* y_pre, int M, int N, int K, void* stream);
+
+/* bf16 rows x [rows, K] -> e4m3 bytes q [rows, K] and e8m0 scales [rows, K/32]: per block of
+ * 32 elements the largest power of two 2^k with amax * 2^k <= 448 (scale byte 127 - k), the
+ * elements rounded to nearest even at that scale.  K % 32 == 0. */
+VS_API int vs_mx_quantize(const void* x, void* q, void* scales, int rows, int K, void* stream);
+
 /* ---- a11: mask head -----------------------------------------------------------------
  * logits f32 [B, Q, H*W] = E [B, Q, C] x P[b]^T, with the pixel embedding P
  * channels-last [B, H*W, C] (HF:m2f:2051 einsum 'bqc,bchw->bqhw').  dtype of E and P:

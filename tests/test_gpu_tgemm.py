@@ -1,0 +1,145 @@
+"""Token GEMM (csrc/token_gemm.hip, vs_token_gemm) and the MX quantiser (vs_mx_quantize)
+against torch references of the same arithmetic:
+
+* bf16: y = x w^T + b vs the f64 product of the same bf16 operands (f32 accumulation in
+  another order, one bf16 rounding of the output: bound 2^-7 relative + a small absolute
+  term); ragged M / N tiles, K tails (K = 96: a partial 128-byte K-step), no bias;
+* GELU epilogue: the pre-activation as above, the activation vs HF `gelu` (exact erf) of
+  the kernel's own rounded pre-activation in f64 (one bf16 rounding);
+* MX quantiser: bit-exact vs the rule in torch -- per 32 elements k = floor(log2(448 /
+  amax)) (0 for an all-zero block), e4m3 = float8_e4m3fn(x 2^k), scale byte 127 - k;
+* fp8 GEMM: vs the f64 product of the DEQUANTISED operands (e4m3 value x 2^-k): the
+  fused dequantisation and the MX fragment layout up to f32 summation order (1e-5 of the
+  largest |y| + the bf16 output rounding), and vs the bf16 product as the fp8 error budget
+  (relative RMS <= 0.06: e4m3 has 3 mantissa bits, errors of the two operands add).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ops():
+    from visionseg import ops
+    return ops
+
+
+def _rand(shape, g, scale=1.0):
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16)
+
+
+def _ref(x, w, b):
+    y = x.double() @ w.double().t()
+    return y + b.double() if b is not None else y
+
+
+SHAPES = [(300, 96, 96), (1000, 384, 96), (513, 200, 192), (4096, 576, 192), (777, 3072, 768), (256, 768, 3072),
+          (130, 132, 136)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_token_gemm_bf16_vs_f64(M, N, K, with_bias):
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + N + K)
+    x, w = _rand((M, K), g), _rand((N, K), g, 1 / math.sqrt(K))
+    b = _rand((N,), g) if with_bias else None
+    y = ops.token_gemm(x.to(DEV), w.to(DEV), b.to(DEV) if b is not None else None).cpu().double()
+    ref = _ref(x, w, b)
+    err = (y - ref).abs()
+    assert bool((err <= ref.abs() * 2 ** -7 + 1e-3 * float(ref.abs().max())).all()), float(err.max())
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 384, 96), (777, 3072, 768), (4096, 1536, 384)])
+def test_token_gemm_gelu_epilogue(M, N, K):
+    ops = _ops()
+    g = torch.Generator().manual_seed(7 * M + K)
+    x, w, b = _rand((M, K), g), _rand((N, K), g, 1 / math.sqrt(K)), _rand((N,), g)
+    y, pre = ops.token_gemm(x.to(DEV), w.to(DEV), b.to(DEV), gelu=True)
+    y, pre = y.cpu().double(), pre.cpu().double()
+    ref = _ref(x, w, b)
+    err = (pre - ref).abs()
+    assert bool((err <= ref.abs() * 2 ** -7 + 1e-3 * float(ref.abs().max())).all()), float(err.max())
+    gel = 0.5 * pre * (1 + torch.erf(pre / math.sqrt(2)))          # HF gelu of the kernel's pre-activation
+    e2 = (y - gel).abs()
+    assert bool((e2 <= gel.abs() * 2 ** -8 + 1e-6).all()), float(e2.max())
+
+
+def _mx_emulate(x):
+    """The quantiser's rule in torch: (e4m3 bytes, scale bytes, dequantised f64)."""
+    rows, K = x.shape
+    xb = x.float().view(rows, K // 32, 32)
+    amax = xb.abs().amax(-1, keepdim=True)
+    k = torch.where(amax > 0, torch.floor(torch.log2(448.0 / amax.clamp_min(1e-38))), torch.zeros_like(amax))
+    k = k.clamp(-126, 126)
+    q = (xb * torch.exp2(k)).to(torch.float8_e4m3fn)
+    deq = q.double() * torch.exp2(-k.double())
+    return q.view(torch.uint8).view(rows, K), (127 - k).to(torch.uint8).view(rows, K // 32), deq.view(rows, K)
+
+
+@pytest.mark.parametrize("rows,K,scale", [(64, 128, 1.0), (333, 768, 1e-3), (100, 3072, 30.0)])
+def test_mx_quantize_bit_exact(rows, K, scale):
+    ops = _ops()
+    g = torch.Generator().manual_seed(rows + K)
+    x = _rand((rows, K), g, scale)
+    x[0, :32] = 0                                   # an all-zero block
+    x[1, 5] = 0.0
+    q, s = ops.mx_quantize(x.to(DEV))
+    eq, es, _ = _mx_emulate(x)
+    assert torch.equal(s.cpu(), es)
+    assert torch.equal(q.cpu(), eq)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 384, 384), (777, 3072, 768), (256, 768, 3072), (4096, 576, 256)])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_token_gemm_fp8_vs_dequantised(M, N, K, gelu):
+    ops = _ops()
+    g = torch.Generator().manual_seed(3 * M + N)
+    x, w, b = _rand((M, K), g), _rand((N, K), g, 1 / math.sqrt(K)), _rand((N,), g)
+    xq, xs = ops.mx_quantize(x.to(DEV))
+    wq, ws = ops.mx_quantize(w.to(DEV))
+    out = ops.token_gemm(xq, wq, b.to(DEV), gelu=gelu, x_scales=xs, w_scales=ws)
+    y = (out[1] if gelu else out).cpu().double()
+    _, _, xd = _mx_emulate(x)
+    _, _, wd = _mx_emulate(w)
+    ref = xd @ wd.t() + b.double()
+    err = (y - ref).abs()
+    assert bool((err <= ref.abs() * 2 ** -7 + 1e-5 * float(ref.abs().max())).all()), float(err.max())
+    exact = _ref(x, w, b)
+    rel_rms = float((y - exact).norm() / exact.norm())
+    print(f"fp8 token GEMM {M}x{N}x{K}: vs dequantised max {float(err.max()):.2e}, vs bf16 operands rel-RMS {rel_rms:.3e}")
+    assert rel_rms <= 0.06
+    if gelu:
+        pre = y
+        gel = 0.5 * pre * (1 + torch.erf(pre / math.sqrt(2)))
+        e2 = (out[0].cpu().double() - gel).abs()
+        assert bool((e2 <= gel.abs() * 2 ** -8 + 1e-6).all()), float(e2.max())
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_linear_gelu_autograd_vs_f64(fp8):
+    """linear.linear_gelu_tokens (fc1 + GELU on the token GEMM, the backward through the
+    fused GELU-derivative + column-sum pass, the vendor dX GEMM and the split-K dW) vs torch
+    autograd in f64 on the same bf16 operands (fp8: the forward on the MX MFMA, the backward
+    straight-through, so the gradients match the bf16 formula up to the fp8 forward's
+    pre-activation error)."""
+    from visionseg.linear import linear_gelu_tokens
+    g = torch.Generator().manual_seed(11)
+    M, K, N = 20000, 384, 1536
+    x = _rand((M, K), g)
+    w = _rand((N, K), g, 1 / math.sqrt(K))
+    b = _rand((N,), g, 0.1)
+    gy = _rand((M, N), g, 0.01)
+    xd, wd, bd = (t.to(DEV).requires_grad_(True) for t in (x, w, b))
+    y = linear_gelu_tokens(xd, wd, bd, fp8=fp8)
+    y.backward(gy.to(DEV))
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.gelu(xr @ wr.t() + br)
+    yr.backward(gy.double())
+    tol = 0.05 if fp8 else 0.01
+    for got, exp in ((y, yr), (xd.grad, xr.grad), (wd.grad, wr.grad), (bd.grad, br.grad)):
+        rel = float((got.detach().cpu().double() - exp.detach()).norm() / exp.detach().norm())
+        assert rel <= tol, rel

@@ -709,3 +709,106 @@ class TokenLinear(nn.Linear):
 
     def forward(self, x, sink=None):
         return linear_tokens(x, self.weight, self.bias, sink)
+
+
+# ---------------------------------------------------------------------------------------
+# Swin block Linears on the hand-written token GEMM (csrc/token_gemm.hip)
+# ---------------------------------------------------------------------------------------
+# VS_TGEMM_GELU=0: fc1 + GELU as the vendor GEMM + a separate GELU pass (A/B)
+_TGEMM_GELU = os.environ.get("VS_TGEMM_GELU", "1") == "1"
+# fp8 Linears only where the product is MFMA-bound: the K-deep ones (C5: stages 2-4 and
+# every fc2); the stage-1 qkv / proj / fc1 of Swin-L (K = 192) are HBM-bound
+FP8_MIN_K = int(os.environ.get("VS_FP8_MIN_K", "384"))
+
+
+def _tgemm_ok(x, w, b, tokens_min=MIN_TOKENS):
+    tokens = x.numel() // max(1, x.shape[-1])
+    K, N = w.shape[1], w.shape[0]
+    return (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and tokens >= tokens_min
+            and not torch.is_autocast_enabled() and x.dtype == w.dtype == torch.bfloat16
+            and (b is None or b.dtype == torch.bfloat16) and K % 8 == 0 and N % 8 == 0
+            and N <= ops.COLSUM_MAX_N and x.is_contiguous())
+
+
+def _mx_pair(x2, weight):
+    xq, xs = ops.mx_quantize(x2)
+    wq, ws = ops.mx_quantize(weight)
+    return xq, xs, wq, ws
+
+
+class _LinearGeluFn(torch.autograd.Function):
+    """gelu(x W^T + b), exact erf GELU (HF `gelu`, the Swin MLP HF:swin:511-536) in the
+    token GEMM's epilogue: one kernel stores the pre-activation and the activation (the
+    vendor GEMM + ATen GELU wrote the pre-activation, read it back and wrote the
+    activation).  fp8: the GEMM on the block-scaled MX MFMA with the operands quantised
+    per 32 elements along K (straight-through: the backward sees the bf16 operands).
+    Backward: the GELU derivative at the saved pre-activation with the column sums (= the
+    bias gradient) in one HIP pass, then the vendor dX GEMM and the split-K dW."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, fp8=False):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if fp8:
+            xq, xs, wq, ws = _mx_pair(x2, weight)
+            y, pre = ops.token_gemm(xq, wq, bias, gelu=True, x_scales=xs, w_scales=ws)
+        else:
+            y, pre = ops.token_gemm(x2, weight, bias, gelu=True)
+        ctx.save_for_backward(x, weight, pre)
+        ctx.has_bias = bias is not None
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, pre = ctx.saved_tensors
+        M, N = pre.shape
+        gy2 = gy.reshape(M, N).to(pre.dtype).contiguous()
+        gp = torch.empty_like(pre)
+        cs = torch.empty(N, device=pre.device, dtype=pre.dtype)
+        ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=pre.device, dtype=torch.uint8)
+        with ops.timed("act_bwd_colsum", pre, bytes_=3 * pre.numel() * pre.element_size()):
+            L.check(L.lib().vs_act_backward_colsum(L.dtype_code(pre), 1, L.ptr(gy2), L.ptr(pre), L.ptr(gp), L.ptr(cs),
+                                                   L.ptr(ws), M, N, L.stream(pre)), "act_backward_colsum")
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = (gp @ weight.to(gp.dtype)).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            gw = weight_grad(gp, x.reshape(-1, x.shape[-1]), weight.dtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = cs.to(weight.dtype)
+        return gx, gw, gb, None
+
+
+class _LinearFp8Fn(torch.autograd.Function):
+    """x W^T + b with the product on the block-scaled MX MFMA (config C5's fp8 path): x and
+    W quantised per 32 elements along K (vs_mx_quantize: e4m3 + e8m0), f32 accumulation,
+    bf16 out.  Straight-through: the backward is _LinearFn's, on the bf16 operands."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        xq, xs, wq, ws = _mx_pair(x2, weight)
+        y = ops.token_gemm(xq, wq, bias, x_scales=xs, w_scales=ws)
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        ctx.sink = None
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    backward = _LinearFn.backward
+
+
+def linear_gelu_tokens(x, w, b, fp8: bool = False):
+    """gelu(F.linear(x, w, b)) with the exact erf GELU: fused into the token GEMM on
+    token-heavy bf16 device tensors (_LinearGeluFn), the composition otherwise."""
+    if _TGEMM_GELU and _tgemm_ok(x, w, b):
+        return _LinearGeluFn.apply(x, w, b, bool(fp8 and w.shape[1] % 128 == 0 and w.shape[1] >= FP8_MIN_K))
+    return ops.activation(linear_tokens(x, w, b), "gelu")
+
+
+def linear_fp8_tokens(x, w, b):
+    """F.linear with the product in MX fp8 (_LinearFp8Fn) where it pays (K % 128 == 0 and K
+    >= FP8_MIN_K on token-heavy bf16 tensors), linear_tokens otherwise."""
+    if _tgemm_ok(x, w, b) and w.shape[1] % 128 == 0 and w.shape[1] >= FP8_MIN_K:
+        return _LinearFp8Fn.apply(x, w, b)
+    return linear_tokens(x, w, b)

@@ -28,8 +28,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_relu_tokens, linear_tokens,
-                     plane_projection, self_attn_in_proj, small_linear, value_query_projection,
+from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_fp8_tokens, linear_gelu_tokens,
+                     linear_relu_tokens, linear_tokens, plane_projection, self_attn_in_proj, small_linear, value_query_projection,
                      reattach_level_embed)
 
 
@@ -62,6 +62,10 @@ class M2FConfig:
     # BASELINE config C5: the Swin window-attention core on fp8 (e4m3) MFMA
     # (vs_window_attn_forward_fp8; bf16 activations, window^2 <= 160)
     attn_fp8: bool = False
+    # BASELINE config C5: the Swin block's K-deep Linears (qkv, proj, fc1, fc2 with K % 128 == 0
+    # and K >= linear.FP8_MIN_K) on the block-scaled MX fp8 MFMA (vs_token_gemm; straight-through
+    # backward in bf16)
+    linear_fp8: bool = False
 
     @staticmethod
     def preset(name: str, **kw) -> "M2FConfig":
@@ -115,13 +119,21 @@ class WindowAttention(nn.Module):
 
 
 class Mlp(nn.Module):
+    """fc1 -> GELU (exact erf) -> fc2 (HF:swin:511-536): fc1's GELU in the token GEMM's
+    epilogue (linear.linear_gelu_tokens); fp8 (config C5): the K-deep products on the MX
+    MFMA (linear.linear_fp8_tokens)."""
+
     def __init__(self, dim, hidden):
         super().__init__()
         self.fc1 = TokenLinear(dim, hidden)
         self.fc2 = TokenLinear(hidden, dim)
+        self.fp8 = False
 
     def forward(self, x):
-        return self.fc2(ops.activation(self.fc1(x), "gelu"))
+        h = linear_gelu_tokens(x, self.fc1.weight, self.fc1.bias, fp8=self.fp8)
+        if self.fp8:
+            return linear_fp8_tokens(h, self.fc2.weight, self.fc2.bias)
+        return self.fc2(h)
 
 
 class SwinBlock(nn.Module):
@@ -129,6 +141,7 @@ class SwinBlock(nn.Module):
         super().__init__()
         self.ws, self.shift = ws, shift
         self.attn_fp8 = False                  # set by SwinBackbone from M2FConfig.attn_fp8
+        self.linear_fp8 = False                # set by SwinBackbone from M2FConfig.linear_fp8
         self.norm1 = TokenLayerNorm(dim)
         self.attn = WindowAttention(dim, heads, ws)
         self.norm2 = TokenLayerNorm(dim)
@@ -147,12 +160,18 @@ class SwinBlock(nn.Module):
             h = self.norm1.forward_windows(x, wr)
         else:
             x, h = self.norm1.add_forward_windows(x, res, wr)
-        qkv = self.attn.qkv(h.view(-1, ws * ws, C))
+        if self.linear_fp8:
+            qkv = linear_fp8_tokens(h.view(-1, ws * ws, C), self.attn.qkv.weight, self.attn.qkv.bias)
+        else:
+            qkv = self.attn.qkv(h.view(-1, ws * ws, C))
         # output in the image layout (window reverse folded into the kernel); the per-token
         # proj commutes with the crop
         o = ops.window_attention_image(qkv, self.attn.rel_table, self.attn.heads, ws, shift, B, H, W,
                                        fp8=self.attn_fp8 and qkv.dtype == torch.bfloat16)
-        o = self.attn.proj(o.view(B, H * W, C))
+        if self.linear_fp8:
+            o = linear_fp8_tokens(o.view(B, H * W, C), self.attn.proj.weight, self.attn.proj.bias)
+        else:
+            o = self.attn.proj(o.view(B, H * W, C))
         x, h2 = self.norm2.add_forward(x, o)
         return x, self.mlp(h2)
 
@@ -230,6 +249,7 @@ class SwinBackbone(nn.Module):
         for st in self.stages:
             for blk in st.blocks:
                 blk.attn_fp8 = bool(cfg.attn_fp8)
+                blk.linear_fp8 = blk.mlp.fp8 = bool(cfg.linear_fp8)
 
     def forward(self, px):
         H, W = px.shape[-2:]

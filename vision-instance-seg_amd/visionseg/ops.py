@@ -1171,3 +1171,53 @@ class UpsampleAddFunction(torch.autograd.Function):
 
 def upsample_add(cur, src_tokens, Hs: int, Ws: int):
     return UpsampleAddFunction.apply(cur, src_tokens, int(Hs), int(Ws))
+
+
+# ---------------------------------------------------------------------------------------
+# token GEMM (csrc/token_gemm.hip): the Swin blocks' Linears, bf16 or block-scaled MX fp8
+# ---------------------------------------------------------------------------------------
+TGEMM_FP8, TGEMM_GELU = 1, 2
+
+
+def mx_quantize(x: torch.Tensor):
+    """bf16 [..., K] (K % 32 == 0) -> (e4m3 bytes uint8 [..., K], e8m0 scale bytes uint8
+    [..., K / 32]): one power-of-two scale per 32 elements along K (vs_mx_quantize)."""
+    L.require_hip(x)
+    if x.dtype != torch.bfloat16 or x.shape[-1] % 32:
+        raise ValueError("mx_quantize: bf16 rows with K % 32 == 0")
+    x = x.contiguous()
+    K = x.shape[-1]
+    rows = x.numel() // K
+    q = torch.empty(x.shape, device=x.device, dtype=torch.uint8)
+    s = torch.empty(*x.shape[:-1], K // 32, device=x.device, dtype=torch.uint8)
+    with timed("mx_quantize", x, bytes_=x.numel() * 3 + s.numel()):
+        L.check(L.lib().vs_mx_quantize(L.ptr(x), L.ptr(q), L.ptr(s), rows, K, L.stream(x)), "mx_quantize")
+    return q, s
+
+
+def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None):
+    """y = x w^T + bias over token rows (x [..., K], w [N, K]; bf16, or -- with scales --
+    e4m3 bytes from mx_quantize) -> bf16 [..., N]; gelu=True -> (gelu(y) , y) with the
+    exact erf GELU in the epilogue (y = the bf16 pre-activation)."""
+    fp8 = x_scales is not None
+    L.require_hip(x, w)
+    K = x.shape[-1]
+    N = w.shape[0]
+    if w.shape[1] != K or N % 4 or (fp8 and (w_scales is None or K % 128)) or (not fp8 and K % 8):
+        raise ValueError(f"token_gemm: bad shapes x {tuple(x.shape)} w {tuple(w.shape)} fp8={fp8}")
+    x2 = x.reshape(-1, K).contiguous()
+    M = x2.shape[0]
+    y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
+    pre = torch.empty_like(y) if gelu else None
+    mode = (TGEMM_FP8 if fp8 else 0) | (TGEMM_GELU if gelu else 0)
+    esz = 1 if fp8 else 2
+    nb = (M * K + N * K) * esz + M * N * 2 * (2 if gelu else 1)
+    with timed("token_gemm_fp8" if fp8 else "token_gemm", x2, bytes_=nb, flops=2.0 * M * N * K):
+        L.check(L.lib().vs_token_gemm(mode, L.ptr(x2), L.ptr(x_scales.contiguous()) if fp8 else None,
+                                      L.ptr(w.contiguous()), L.ptr(w_scales.contiguous()) if fp8 else None,
+                                      L.ptr(bias.contiguous()) if bias is not None else None, L.ptr(y),
+                                      L.ptr(pre) if gelu else None, M, N, K, L.stream(x2)), "token_gemm")
+    shape = (*x.shape[:-1], N)
+    if gelu:
+        return y.view(shape), pre.view(shape)
+    return y.view(shape)

@@ -241,9 +241,11 @@ class Trainer:
             self._pool = torch.cuda.graph_pool_handle()
         pool = self._pool
         torch._C._cuda_clearCublasWorkspaces()
-        # several ranks: "thread_local" capture, so RCCL's watchdog thread may keep querying
-        # the events of earlier eager collectives while this thread captures
-        mode = "thread_local" if self.split else "global"
+        # "thread_local" capture: other threads keep using the device while this one
+        # captures -- RCCL's watchdog querying the events of earlier collectives (several
+        # ranks), and the data loader's pin-memory thread pinning the next batches (the
+        # seam: a "global" capture was invalidated by the pinning, tools/seam_bench.py)
+        mode = "thread_local"
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=pool, capture_error_mode=mode):
             st["loss"], _ = self.forward_backward(st["images"], st["tg"], None, reduce_mode="capture")
