@@ -715,7 +715,7 @@ class TokenLinear(nn.Linear):
 # Swin block Linears on the hand-written token GEMM (csrc/token_gemm.hip)
 # ---------------------------------------------------------------------------------------
 # VS_TGEMM_GELU=0: fc1 + GELU as the vendor GEMM + a separate GELU pass (A/B)
-_TGEMM_GELU = os.environ.get("VS_TGEMM_GELU", "1") == "1"
+_TGEMM_GELU = os.environ.get("VS_TGEMM_GELU", "0") == "1"
 # fp8 Linears only where the product is MFMA-bound: the K-deep ones (C5: stages 2-4 and
 # every fc2); the stage-1 qkv / proj / fc1 of Swin-L (K = 192) are HBM-bound
 FP8_MIN_K = int(os.environ.get("VS_FP8_MIN_K", "384"))
