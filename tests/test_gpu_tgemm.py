@@ -36,8 +36,9 @@ def _ref(x, w, b):
     return y + b.double() if b is not None else y
 
 
+# the last two take the 256 x 256 tile (>= 256 tiles, N >= 512, K >= 256), one with ragged edges
 SHAPES = [(300, 96, 96), (1000, 384, 96), (513, 200, 192), (4096, 576, 192), (777, 3072, 768), (256, 768, 3072),
-          (130, 132, 136)]
+          (130, 132, 136), (4096, 4096, 512), (4000, 4100, 264)]
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
@@ -53,7 +54,7 @@ def test_token_gemm_bf16_vs_f64(M, N, K, with_bias):
     assert bool((err <= ref.abs() * 2 ** -7 + 1e-3 * float(ref.abs().max())).all()), float(err.max())
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 384, 96), (777, 3072, 768), (4096, 1536, 384)])
+@pytest.mark.parametrize("M,N,K", [(1000, 384, 96), (777, 3072, 768), (4096, 1536, 384), (4000, 4100, 384)])
 def test_token_gemm_gelu_epilogue(M, N, K):
     ops = _ops()
     g = torch.Generator().manual_seed(7 * M + K)
@@ -93,7 +94,8 @@ def test_mx_quantize_bit_exact(rows, K, scale):
     assert torch.equal(q.cpu(), eq)
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 384, 384), (777, 3072, 768), (256, 768, 3072), (4096, 576, 256)])
+@pytest.mark.parametrize("M,N,K", [(300, 384, 384), (777, 3072, 768), (256, 768, 3072), (4096, 576, 256),
+                                   (4000, 4100, 512)])
 @pytest.mark.parametrize("gelu", [False, True])
 def test_token_gemm_fp8_vs_dequantised(M, N, K, gelu):
     ops = _ops()
@@ -120,13 +122,15 @@ def test_token_gemm_fp8_vs_dequantised(M, N, K, gelu):
 
 
 @pytest.mark.parametrize("fp8", [False, True])
-def test_linear_gelu_autograd_vs_f64(fp8):
+def test_linear_gelu_autograd_vs_f64(monkeypatch, fp8):
     """linear.linear_gelu_tokens (fc1 + GELU on the token GEMM, the backward through the
     fused GELU-derivative + column-sum pass, the vendor dX GEMM and the split-K dW) vs torch
     autograd in f64 on the same bf16 operands (fp8: the forward on the MX MFMA, the backward
     straight-through, so the gradients match the bf16 formula up to the fp8 forward's
     pre-activation error)."""
+    from visionseg import linear
     from visionseg.linear import linear_gelu_tokens
+    monkeypatch.setattr(linear, "_TGEMM_GELU", True)
     g = torch.Generator().manual_seed(11)
     M, K, N = 20000, 384, 1536
     x = _rand((M, K), g)

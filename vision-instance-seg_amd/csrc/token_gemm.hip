@@ -22,14 +22,16 @@
 // (row >> 1) & 7, so the fragment reads (ds_read_b128, 16-lane groups) are conflict-free;
 // the DMA writes lane-linear and the swizzle is applied to the global source address.
 // fp8: the per-row block scales of the K-step (4 bytes a row) are staged by 4-byte DMA.
+#include <stdlib.h>
+
+#include "gelu_table.h"
 #include "mfma_util.h"
 #include "mx_util.h"
 
 namespace vs {
 namespace {
 
-constexpr int kBM = 128, kBN = 128, kRowB = 128;      // tile tokens, tile features, bytes per K-step row
-constexpr int kTileB = 128 * kRowB;                   // one staged operand tile (16 KB)
+constexpr int kRowB = 128;                            // bytes of a row per K-step
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -54,136 +56,168 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-__device__ __forceinline__ float gelu_erf(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+// bf16 GELU (exact erf) of a bf16 value, branch-free: the generated table (gelu_table.h:
+// f64 gelu rounded to bf16) for 2^-10 <= |x| < 16, x (0.5 + x / sqrt(2 pi)) below (the next
+// term is 2^-30 relative), x resp. -0 above (Phi(-16) ~ 6e-58 underflows bf16); NaN stays NaN
+__device__ __forceinline__ unsigned short gelu_bits(unsigned short pb, const unsigned short* tab) {
+  const unsigned e = (pb >> 7) & 0xffu, sgn = pb >> 15;
+  const int ti = min(max((int)(pb & 0x7fffu) - kGeluE0 * 128, 0), kGeluNE * 128 - 1) + (int)sgn * (kGeluNE * 128);
+  const unsigned short tv = tab[ti];
+  const float z = bf16_bits_to_f32(pb);
+  const unsigned short small = (unsigned short)bf16_bits(z * (0.5f + 0.3989422804014327f * z));
+  const unsigned short big = (sgn && (pb & 0x7fffu) <= 0x7f80u) ? (unsigned short)0x8000 : pb;
+  return e < (unsigned)kGeluE0 ? small : (e >= (unsigned)(kGeluE0 + kGeluNE) ? big : tv);
+}
 
+// Tile shapes: GM x GN waves, each TM x TN MFMA tiles of 32 x 32 (tokens x features):
+//   <2, 2, 2, 2>: 128 x 128, 256 threads, 2 workgroups / CU (64 KB of staging);
+//   <2, 4, 4, 2>: 256 x 256, 512 threads, 1 workgroup / CU (128 KB): half the L2 -> LDS
+//   bytes per flop, for the MFMA-bound shapes.
 // EPI: 0 = bias, 1 = bias + GELU (y2 = pre-activation, y = gelu)
-template <bool F8, int EPI>
-__global__ void __launch_bounds__(256, 2) token_gemm_kernel(const unsigned char* __restrict__ X,
-                                                            const unsigned char* __restrict__ Xs,
-                                                            const unsigned char* __restrict__ Wt,
-                                                            const unsigned char* __restrict__ Ws,
-                                                            const bf16* __restrict__ bias, bf16* __restrict__ Y,
-                                                            bf16* __restrict__ Y2, int M, int N, int K) {
-  // [stage][X tile | W tile] then (fp8) [stage][X scales | W scales] (128 rows x 4 B each)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * 2 * kTileB + (F8 ? 2 * 2 * 512 : 0)];
+template <bool F8, int EPI, int GM, int GN, int TM, int TN>
+__global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned char* __restrict__ X,
+                                                                  const unsigned char* __restrict__ Xs,
+                                                                  const unsigned char* __restrict__ Wt,
+                                                                  const unsigned char* __restrict__ Ws,
+                                                                  const bf16* __restrict__ bias, bf16* __restrict__ Y,
+                                                                  bf16* __restrict__ Y2, int M, int N, int K) {
+  constexpr int BM = GM * TM * 32, BN = GN * TN * 32, NW = GM * GN, NT = 64 * NW;
+  constexpr int XB = BM * kRowB, WB = BN * kRowB, STB = XB + WB;      // staged bytes per K-step
+  constexpr int SCB = F8 ? (BM + BN) * 4 : 0;                         // staged scale bytes per K-step
+  // [stage][X tile | W tile] then (fp8) [stage][X scales | W scales] then the GELU table
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STB + 2 * SCB + (EPI == 1 ? kGeluEntries * 2 : 0)];
+  unsigned short* sgelu = reinterpret_cast<unsigned short*>(smem + 2 * STB + 2 * SCB);
   constexpr int ESZ = F8 ? 1 : 2;                      // bytes per element
   const int rowB = K * ESZ;                            // bytes per operand row
   const int nks = (rowB + kRowB - 1) / kRowB;          // K-steps (a partial last step is zero-filled)
-  const int tilesM = (M + kBM - 1) / kBM, tilesN = (N + kBN - 1) / kBN;
+  const int tilesM = (M + BM - 1) / BM, tilesN = (N + BN - 1) / BN;
   const int wg = xcd_swizzle(blockIdx.x, tilesM * tilesN);
   // N-tiles of one token tile are neighbours: the X tile is re-read from L2
   const int tm = wg / tilesN, tn = wg - tm * tilesN;
-  const int m0 = tm * kBM, n0 = tn * kBN;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
-  const int wm = w & 1, wn = w >> 1;                   // this wave: tokens wm*64.., features wn*64..
+  const int wm = w % GM, wn = w / GM;                  // this wave: tokens wm*TM*32.., features wn*TN*32..
 
-  // ---- DMA issue of K-step ks into stage st: every wave moves 4 x 1 KB of X and of W
-  // (8 rows per instruction, lane L -> row 8j + L/8, physical chunk L%8)
+  // ---- DMA issue of K-step ks into stage st: 1 KB (8 rows) per wave instruction, lane L ->
+  // row 8j + L/8, physical chunk L%8; X rows first, then W rows, spread over the waves
   auto issue = [&](int ks, int st) {
-    unsigned char* sx = smem + st * 2 * kTileB;
-    unsigned char* sw = sx + kTileB;
+    unsigned char* base = smem + st * STB;
+    constexpr int NI = (BM + BN) / 8 / NW;            // instructions per wave
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = (w * 4 + j) * 8 + (l >> 3);
-      const int chunk = (l & 7) ^ ((row >> 1) & 7);
+    for (int j = 0; j < NI; ++j) {
+      const int blk = w * NI + j;                     // 8-row block of the [X | W] image
+      const int row = blk * 8 + (l >> 3);             // < BM: X row, else W row BM..
+      const bool isx = row < BM;
+      const int rr = isx ? row : row - BM;
+      const int chunk = (l & 7) ^ ((rr >> 1) & 7);
       const int kb = min(ks * kRowB + chunk * 16, rowB - 16);   // past K: any valid bytes, zeroed later
-      const int mr = min(m0 + row, M - 1), nr = min(n0 + row, N - 1);
-      glds16(X + (size_t)mr * rowB + kb, sx + (w * 4 + j) * 1024);
-      glds16(Wt + (size_t)nr * rowB + kb, sw + (w * 4 + j) * 1024);
+      const unsigned char* src = isx ? X + (size_t)min(m0 + rr, M - 1) * rowB + kb
+                                     : Wt + (size_t)min(n0 + rr, N - 1) * rowB + kb;
+      glds16(src, base + blk * 1024);
     }
-    if (F8) {                                         // scales: waves 0-1 X rows, waves 2-3 W rows
-      unsigned char* ss = smem + 2 * 2 * kTileB + st * 1024;
+    if (F8) {                                         // scales: 4 bytes a row, 64 rows per instruction
+      unsigned char* ss = smem + 2 * STB + st * SCB;
       const int sb = K / 32;                          // scale bytes per row
-      const int row = (w & 1) * 64 + l;
-      if (w < 2) glds4(Xs + (size_t)min(m0 + row, M - 1) * sb + ks * 4, ss + (w & 1) * 256);
-      else glds4(Ws + (size_t)min(n0 + row, N - 1) * sb + ks * 4, ss + 512 + (w & 1) * 256);
+      for (int blk = w; blk < (BM + BN) / 64; blk += NW) {
+        const int row = blk * 64 + l;
+        const unsigned char* src = row < BM ? Xs + (size_t)min(m0 + row, M - 1) * sb + ks * 4
+                                            : Ws + (size_t)min(n0 + row - BM, N - 1) * sb + ks * 4;
+        glds4(src, ss + blk * 256);
+      }
     }
   };
-  constexpr int kIssued = F8 ? 9 : 8;                 // DMA instructions per wave per K-step
 
-  f32x16_t acc[2][2];                                 // [feature tile][token tile]
+  f32x16_t acc[TN][TM];                               // [feature tile][token tile]
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TN; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) zero16(acc[a][b]);
+    for (int b = 0; b < TM; ++b) zero16(acc[a][b]);
 
+  auto xrow = [&](int t) { return wm * TM * 32 + t * 32 + r; };
+  auto wrow = [&](int t) { return wn * TN * 32 + t * 32 + r; };
   issue(0, 0);
+  if (EPI == 1) {                                     // GELU table: read at the epilogue, after the loop's barriers
+    for (int i = threadIdx.x; i < kGeluEntries / 8; i += NT)
+      reinterpret_cast<uint4*>(sgelu)[i] = reinterpret_cast<const uint4*>(kGeluTable)[i];
+  }
   for (int ks = 0; ks < nks; ++ks) {
     const int st = ks & 1;
-    if (ks + 1 < nks) {
-      issue(ks + 1, st ^ 1);
-      wait_vm<kIssued>();                             // this wave's DMA of step ks landed
-    } else {
-      wait_vm<0>();
-    }
-    raw_barrier();                                    // every wave's DMA of step ks landed
-    const unsigned char* sx = smem + st * 2 * kTileB;
-    const unsigned char* sw = sx + kTileB;
+    wait_vm<0>();                                     // this wave's DMA of step ks landed
+    raw_barrier();                                    // every wave's did; every wave is done with step ks - 1
+    const unsigned char* sx = smem + st * STB;
+    const unsigned char* sw = sx + XB;
     if (ks * kRowB + kRowB > rowB) {                  // partial last step: zero the bytes past K
-      unsigned char* sxz = const_cast<unsigned char*>(sx);
-      for (int idx = threadIdx.x; idx < 2 * 128 * 8; idx += 256) {
-        const int op = idx >> 10, row = (idx >> 3) & 127, chunk = idx & 7;
+      unsigned char* sz = const_cast<unsigned char*>(sx);
+      for (int idx = threadIdx.x; idx < (BM + BN) * 8; idx += NT) {
+        const int row = idx >> 3, chunk = idx & 7, rr = row < BM ? row : row - BM;
         if (ks * kRowB + chunk * 16 >= rowB)
-          *reinterpret_cast<uint4*>(sxz + op * kTileB + tile_off(row, chunk)) = make_uint4(0, 0, 0, 0);
+          *reinterpret_cast<uint4*>(sz + (row < BM ? 0 : XB) + tile_off(rr, chunk)) = make_uint4(0, 0, 0, 0);
       }
       raw_barrier();
     }
+    if (ks + 1 < nks) issue(ks + 1, st ^ 1);          // the other buffer: last read in step ks - 1
     if (F8) {
-      const unsigned* ss = reinterpret_cast<const unsigned*>(smem + 2 * 2 * kTileB + st * 1024);
-      unsigned xsc[2], wsc[2];
+      const unsigned* ss = reinterpret_cast<const unsigned*>(smem + 2 * STB + st * SCB);
+      unsigned xsc[TM], wsc[TN];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        xsc[t] = ss[wm * 64 + t * 32 + r];
-        wsc[t] = ss[128 + wn * 64 + t * 32 + r];
-      }
+      for (int t = 0; t < TM; ++t) xsc[t] = ss[xrow(t)];
+#pragma unroll
+      for (int t = 0; t < TN; ++t) wsc[t] = ss[BM + wrow(t)];
+      i32x8_t xa[2][TM], wa[2][TN];                  // [buffer][tile]
+      auto ld2 = [&](const unsigned char* img, int row, int kk) {
+        const uint4 v0 = *reinterpret_cast<const uint4*>(img + tile_off(row, 4 * kk + hh));
+        const uint4 v1 = *reinterpret_cast<const uint4*>(img + tile_off(row, 4 * kk + 2 + hh));
+        return i32x8_t{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+      };
+      auto load = [&](int kk, int bsel) {
+#pragma unroll
+        for (int t = 0; t < TM; ++t) xa[bsel][t] = ld2(sx, xrow(t), kk);
+#pragma unroll
+        for (int t = 0; t < TN; ++t) wa[bsel][t] = ld2(sw, wrow(t), kk);
+      };
+      load(0, 0);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {                // two 64-element MX steps per K-step
-        i32x8_t xa[2], wa[2];
+        if (kk + 1 < 2) load(kk + 1, (kk + 1) & 1);
+        const int bs = kk & 1;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int xr = wm * 64 + t * 32 + r, wr = wn * 64 + t * 32 + r;
-          const uint4 x0 = *reinterpret_cast<const uint4*>(sx + tile_off(xr, 4 * kk + hh));
-          const uint4 x1 = *reinterpret_cast<const uint4*>(sx + tile_off(xr, 4 * kk + 2 + hh));
-          const uint4 w0 = *reinterpret_cast<const uint4*>(sw + tile_off(wr, 4 * kk + hh));
-          const uint4 w1 = *reinterpret_cast<const uint4*>(sw + tile_off(wr, 4 * kk + 2 + hh));
-          xa[t] = i32x8_t{(int)x0.x, (int)x0.y, (int)x0.z, (int)x0.w, (int)x1.x, (int)x1.y, (int)x1.z, (int)x1.w};
-          wa[t] = i32x8_t{(int)w0.x, (int)w0.y, (int)w0.z, (int)w0.w, (int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
-        }
+        for (int a = 0; a < TN; ++a)
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int b = 0; b < 2; ++b)
-            acc[a][b] = mfma_mx(wa[a], (int)((wsc[a] >> (8 * (2 * kk + hh))) & 0xffu), xa[b],
+          for (int b = 0; b < TM; ++b)
+            acc[a][b] = mfma_mx(wa[bs][a], (int)((wsc[a] >> (8 * (2 * kk + hh))) & 0xffu), xa[bs][b],
                                 (int)((xsc[b] >> (8 * (2 * kk + hh))) & 0xffu), acc[a][b]);
       }
     } else {
+      bf16x8_t xa[2][TM], wa[2][TN];                 // [buffer][tile]
+      auto load = [&](int kk, int bsel) {
+#pragma unroll
+        for (int t = 0; t < TM; ++t) xa[bsel][t] = *reinterpret_cast<const bf16x8_t*>(sx + tile_off(xrow(t), 2 * kk + hh));
+#pragma unroll
+        for (int t = 0; t < TN; ++t) wa[bsel][t] = *reinterpret_cast<const bf16x8_t*>(sw + tile_off(wrow(t), 2 * kk + hh));
+      };
+      load(0, 0);
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {                // four 16-element bf16 steps per K-step
-        bf16x8_t xa[2], wa[2];
+        if (kk + 1 < 4) load(kk + 1, (kk + 1) & 1);
+        const int bs = kk & 1;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          xa[t] = *reinterpret_cast<const bf16x8_t*>(sx + tile_off(wm * 64 + t * 32 + r, 2 * kk + hh));
-          wa[t] = *reinterpret_cast<const bf16x8_t*>(sw + tile_off(wn * 64 + t * 32 + r, 2 * kk + hh));
-        }
+        for (int a = 0; a < TN; ++a)
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int b = 0; b < 2; ++b) acc[a][b] = mfma16(wa[a], xa[b], acc[a][b]);
+          for (int b = 0; b < TM; ++b) acc[a][b] = mfma16(wa[bs][a], xa[bs][b], acc[a][b]);
       }
     }
-    raw_barrier();                                    // stage st free for the DMA of step ks + 2
   }
 
   // ---- epilogue: lane = token, registers = 4 groups of 4 consecutive features
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int m = m0 + wm * 64 + b * 32 + r;
+  for (int b = 0; b < TM; ++b) {
+    const int m = m0 + xrow(b);
     if (m >= M) continue;
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
+    for (int a = 0; a < TN; ++a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int n = n0 + wn * 64 + a * 32 + 8 * g + 4 * hh;
+        const int n = n0 + wn * TN * 32 + a * 32 + 8 * g + 4 * hh;
         if (n >= N) continue;                         // N % 4 == 0: a group is all in or all out
         float z[4];
         const bf16x4_t bv = bias ? *reinterpret_cast<const bf16x4_t*>(bias + n) : bf16x4_t{0, 0, 0, 0};
@@ -197,7 +231,7 @@ __global__ void __launch_bounds__(256, 2) token_gemm_kernel(const unsigned char*
             pre[e] = bf16_bits(z[e]);
             // GELU of the ROUNDED pre-activation: the value the backward (and an unfused
             // bf16 F.gelu) sees
-            o[e] = bf16_bits(gelu_erf(bf16_bits_to_f32((unsigned short)pre[e])));
+            o[e] = (short)gelu_bits((unsigned short)pre[e], sgelu);
           }
           *reinterpret_cast<bf16x4_t*>(Y2 + (size_t)m * N + n) = pre;
         } else {
@@ -253,14 +287,29 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
   VS_CHECK(N % 4 == 0, "N must be a multiple of 4");
   VS_CHECK(f8 ? (K % 128 == 0 && x_scales && w_scales) : (K % 8 == 0), "fp8: K % 128 == 0 and scales; bf16: K % 8 == 0");
   VS_CHECK(!gelu || y_pre, "gelu needs the pre-activation output");
-  const long long tiles = (long long)((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
+  // the 256 x 256 tile where the product is MFMA-bound and fills the chip (VS_TGEMM_TILE=128
+  // / 256 forces one, for A/B)
+  static const int force = [] {
+    const char* e = getenv("VS_TGEMM_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  const bool big = force ? force == 256 : (N >= 512 && K >= 256 && (long long)((M + 255) / 256) * ((N + 255) / 256) >= 256);
+  const int bm = big ? 256 : 128, bn = big ? 256 : 128;
+  const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   VS_CHECK(tiles < (1ll << 31), "too many tiles");
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((unsigned)tiles), block(256);
-#define VS_TG(F8_, E_)                                                                                           \
-  hipLaunchKernelGGL((token_gemm_kernel<F8_, E_>), grid, block, 0, st, (const unsigned char*)x,                 \
-                     (const unsigned char*)x_scales, (const unsigned char*)w, (const unsigned char*)w_scales,     \
-                     (const bf16*)bias, (bf16*)y, (bf16*)y_pre, M, N, K)
+  const dim3 grid((unsigned)tiles);
+#define VS_TG(F8_, E_)                                                                                               \
+  do {                                                                                                               \
+    if (big)                                                                                                         \
+      hipLaunchKernelGGL((token_gemm_kernel<F8_, E_, 2, 4, 4, 2>), grid, dim3(512), 0, st, (const unsigned char*)x,  \
+                         (const unsigned char*)x_scales, (const unsigned char*)w, (const unsigned char*)w_scales,     \
+                         (const bf16*)bias, (bf16*)y, (bf16*)y_pre, M, N, K);                                         \
+    else                                                                                                             \
+      hipLaunchKernelGGL((token_gemm_kernel<F8_, E_, 2, 2, 2, 2>), grid, dim3(256), 0, st, (const unsigned char*)x,  \
+                         (const unsigned char*)x_scales, (const unsigned char*)w, (const unsigned char*)w_scales,     \
+                         (const bf16*)bias, (bf16*)y, (bf16*)y_pre, M, N, K);                                         \
+  } while (0)
   if (f8 && gelu) VS_TG(true, 1);
   else if (f8) VS_TG(true, 0);
   else if (gelu) VS_TG(false, 1);
