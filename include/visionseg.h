@@ -206,11 +206,16 @@ VS_API int vs_window_attn_backward_image(int dtype, int fp8, const void* qkv, co
  *   VS_TGEMM_GELU : y = gelu(x w^T + b) with the exact erf GELU of HF `gelu`, and y_pre =
  *                   the bf16 pre-activation (the input of the GELU's backward); the GELU is
  *                   taken of the rounded pre-activation.
+ *   VS_TGEMM_QOUT : (with GELU) y also as MX fp8: y_q e4m3 [M, N] + y_qscales e8m0
+ *                   [M, N/32], the same bytes as vs_mx_quantize(y) (the next GEMM's operand
+ *                   without a quantisation pass); N % 32 == 0.
  * bias may be NULL.  N % 4 == 0. */
 #define VS_TGEMM_FP8 1
 #define VS_TGEMM_GELU 2
+#define VS_TGEMM_QOUT 4
 VS_API int vs_token_gemm(int mode, const void* x, const void* x_scales, const void* w, const void* w_scales,
-                         const void* bias, void* y, void* y_pre, int M, int N, int K, void* stream);
+                         const void* bias, void* y, void* y_pre, void* y_q, void* y_qscales, int M, int N, int K,
+                         void* stream);
 
 /* bf16 rows x [rows, K] -> e4m3 bytes q [rows, K] and e8m0 scales [rows, K/32]: per block of
  * 32 elements the largest power of two 2^k with amax * 2^k <= 448 (scale byte 127 - k), the

@@ -147,3 +147,52 @@ def test_linear_gelu_autograd_vs_f64(monkeypatch, fp8):
     for got, exp in ((y, yr), (xd.grad, xr.grad), (wd.grad, wr.grad), (bd.grad, br.grad)):
         rel = float((got.detach().cpu().double() - exp.detach()).norm() / exp.detach().norm())
         assert rel <= tol, rel
+
+
+@pytest.mark.parametrize("M,N,K,fp8", [(1000, 384, 96, False), (777, 3072, 768, True), (4000, 4096, 384, False),
+                                       (4000, 4096, 512, True)])
+def test_gelu_quantised_output_equals_mx_quantize(M, N, K, fp8):
+    """VS_TGEMM_QOUT: the GELU epilogue's MX fp8 copy of its output is bit-identical to
+    vs_mx_quantize of the bf16 output (the fc2 operand without a quantisation pass)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + 5 * N)
+    x, w, b = _rand((M, K), g).to(DEV), _rand((N, K), g, 1 / math.sqrt(K)).to(DEV), _rand((N,), g).to(DEV)
+    if fp8:
+        xq, xs = ops.mx_quantize(x)
+        wq, ws = ops.mx_quantize(w)
+        y, pre, (yq, ys) = ops.token_gemm(xq, wq, b, gelu=True, x_scales=xs, w_scales=ws, quant_out=True)
+        y2, pre2 = ops.token_gemm(xq, wq, b, gelu=True, x_scales=xs, w_scales=ws)
+    else:
+        y, pre, (yq, ys) = ops.token_gemm(x, w, b, gelu=True, quant_out=True)
+        y2, pre2 = ops.token_gemm(x, w, b, gelu=True)
+    assert torch.equal(y, y2) and torch.equal(pre, pre2)
+    eq, es = ops.mx_quantize(y)
+    assert torch.equal(ys, es)
+    assert torch.equal(yq, eq)
+
+
+def test_mlp_fp8_vs_bf16_mlp():
+    """linear.mlp_fp8 (config C5's Swin MLP: fc1 + GELU on the MX fp8 token GEMM writing fc2's
+    fp8 operand in its epilogue, fc2 on the MX fp8 GEMM, straight-through backward) vs the
+    same MLP in f64 on the bf16 operands: output rel-RMS <= 0.06 (the fp8 budget of two
+    chained products), input / weight / bias gradients rel-L2 <= 0.06."""
+    from visionseg.linear import mlp_fp8
+    g = torch.Generator().manual_seed(21)
+    M, C = 9216, 384
+    x = _rand((M, C), g)
+    w1, b1 = _rand((4 * C, C), g, 1 / math.sqrt(C)), _rand((4 * C,), g, 0.1)
+    w2, b2 = _rand((C, 4 * C), g, 1 / math.sqrt(4 * C)), _rand((C,), g, 0.1)
+    gy = _rand((M, C), g, 0.01)
+    dev = [t.to(DEV).requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    y = mlp_fp8(*dev)
+    y.backward(gy.to(DEV))
+    ref = [t.double().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    yr = torch.nn.functional.linear(torch.nn.functional.gelu(torch.nn.functional.linear(ref[0], ref[1], ref[2])),
+                                    ref[3], ref[4])
+    yr.backward(gy.double())
+    rel = float((y.detach().cpu().double() - yr.detach()).norm() / yr.detach().norm())
+    print(f"mlp fp8 vs f64: output rel-RMS {rel:.3e}")
+    assert rel <= 0.06
+    for d, r in zip(dev, ref):
+        e = float((d.grad.cpu().double() - r.grad).norm() / r.grad.norm())
+        assert e <= 0.06, e

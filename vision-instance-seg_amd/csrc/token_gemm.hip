@@ -73,19 +73,22 @@ __device__ __forceinline__ unsigned short gelu_bits(unsigned short pb, const uns
 //   <2, 2, 2, 2>: 128 x 128, 256 threads, 2 workgroups / CU (64 KB of staging);
 //   <2, 4, 4, 2>: 256 x 256, 512 threads, 1 workgroup / CU (128 KB): half the L2 -> LDS
 //   bytes per flop, for the MFMA-bound shapes.
-// EPI: 0 = bias, 1 = bias + GELU (y2 = pre-activation, y = gelu)
+// EPI: 0 = bias, 1 = bias + GELU (y2 = pre-activation, y = gelu), 2 = as 1 and the GELU
+// output also as MX fp8 (yq e4m3 [M, N] + yqs e8m0 [M, N/32]: the next GEMM's operand,
+// bit-identical to vs_mx_quantize of y)
 template <bool F8, int EPI, int GM, int GN, int TM, int TN>
 __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned char* __restrict__ X,
                                                                   const unsigned char* __restrict__ Xs,
                                                                   const unsigned char* __restrict__ Wt,
                                                                   const unsigned char* __restrict__ Ws,
                                                                   const bf16* __restrict__ bias, bf16* __restrict__ Y,
-                                                                  bf16* __restrict__ Y2, int M, int N, int K) {
+                                                                  bf16* __restrict__ Y2, unsigned char* __restrict__ YQ,
+                                                                  unsigned char* __restrict__ YQS, int M, int N, int K) {
   constexpr int BM = GM * TM * 32, BN = GN * TN * 32, NW = GM * GN, NT = 64 * NW;
   constexpr int XB = BM * kRowB, WB = BN * kRowB, STB = XB + WB;      // staged bytes per K-step
   constexpr int SCB = F8 ? (BM + BN) * 4 : 0;                         // staged scale bytes per K-step
   // [stage][X tile | W tile] then (fp8) [stage][X scales | W scales] then the GELU table
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STB + 2 * SCB + (EPI == 1 ? kGeluEntries * 2 : 0)];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STB + 2 * SCB + (EPI >= 1 ? kGeluEntries * 2 : 0)];
   unsigned short* sgelu = reinterpret_cast<unsigned short*>(smem + 2 * STB + 2 * SCB);
   constexpr int ESZ = F8 ? 1 : 2;                      // bytes per element
   const int rowB = K * ESZ;                            // bytes per operand row
@@ -136,7 +139,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
   auto xrow = [&](int t) { return wm * TM * 32 + t * 32 + r; };
   auto wrow = [&](int t) { return wn * TN * 32 + t * 32 + r; };
   issue(0, 0);
-  if (EPI == 1) {                                     // GELU table: read at the epilogue, after the loop's barriers
+  if (EPI >= 1) {                                     // GELU table: read at the epilogue, after the loop's barriers
     for (int i = threadIdx.x; i < kGeluEntries / 8; i += NT)
       reinterpret_cast<uint4*>(sgelu)[i] = reinterpret_cast<const uint4*>(kGeluTable)[i];
   }
@@ -212,6 +215,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
 #pragma unroll
   for (int b = 0; b < TM; ++b) {
     const int m = m0 + xrow(b);
+    bf16x4_t ov[TN][4];                                // EPI 2: this token's GELU outputs of the tile
     if (m >= M) continue;
 #pragma unroll
     for (int a = 0; a < TN; ++a) {
@@ -224,7 +228,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = acc[a][b][4 * g + e] + bf16_bits_to_f32((unsigned short)bv[e]);
         bf16x4_t o;
-        if (EPI == 1) {
+        if (EPI >= 1) {
           bf16x4_t pre;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -238,7 +242,34 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = bf16_bits(z[e]);
         }
+        if (EPI == 2) ov[a][g] = o;
         *reinterpret_cast<bf16x4_t*>(Y + (size_t)m * N + n) = o;
+      }
+      if (EPI == 2) {
+        // the 32-feature block of tile a is split between this lane (features 8g + 4hh +
+        // 0..3) and its partner lane ^ 32: block amax with one exchange, then e4m3 at the
+        // block's power-of-two scale (vs_mx_quantize's rule, the same bytes)
+        const int nb = n0 + wn * TN * 32 + a * 32;
+        unsigned am = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint2 u = __builtin_bit_cast(uint2, ov[a][g]);
+          am = max(am, max(max(u.x & 0x7fffu, (u.x >> 16) & 0x7fffu), max(u.y & 0x7fffu, (u.y >> 16) & 0x7fffu)));
+        }
+        am = max(am, (unsigned)__shfl_xor((int)am, 32, 64));
+        const int k = mx_exp_bits(am);
+        const float inv = __builtin_ldexpf(1.f, -k);
+        if (nb < N) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const uint2 u = __builtin_bit_cast(uint2, ov[a][g]);
+            s16x2_t q = {0, 0};
+            q = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(q, __builtin_bit_cast(bf16x2v_t, u.x), inv, false);
+            q = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(q, __builtin_bit_cast(bf16x2v_t, u.y), inv, true);
+            *reinterpret_cast<int*>(YQ + (size_t)m * N + nb + 8 * g + 4 * hh) = __builtin_bit_cast(int, q);
+          }
+          if (hh == 0) YQS[(size_t)m * (N / 32) + nb / 32] = (unsigned char)(127 - k);
+        }
       }
     }
   }
@@ -280,13 +311,16 @@ extern "C" int vs_mx_quantize(const void* x, void* q, void* scales, int rows, in
 }
 
 extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, const void* w, const void* w_scales,
-                             const void* bias, void* y, void* y_pre, int M, int N, int K, void* stream) {
+                             const void* bias, void* y, void* y_pre, void* y_q, void* y_qscales, int M, int N, int K,
+                             void* stream) {
   const bool f8 = (mode & VS_TGEMM_FP8) != 0, gelu = (mode & VS_TGEMM_GELU) != 0;
   VS_CHECK(x && w && y, "null pointer");
   VS_CHECK(M > 0 && N > 0 && K > 0, "empty GEMM");
   VS_CHECK(N % 4 == 0, "N must be a multiple of 4");
   VS_CHECK(f8 ? (K % 128 == 0 && x_scales && w_scales) : (K % 8 == 0), "fp8: K % 128 == 0 and scales; bf16: K % 8 == 0");
   VS_CHECK(!gelu || y_pre, "gelu needs the pre-activation output");
+  const bool qout = (mode & VS_TGEMM_QOUT) != 0;
+  VS_CHECK(!qout || (gelu && y_q && y_qscales && N % 32 == 0), "quantised output: with gelu, N % 32 == 0, both buffers");
   // the 256 x 256 tile where the product is MFMA-bound and fills the chip (VS_TGEMM_TILE=128
   // / 256 forces one, for A/B)
   static const int force = [] {
@@ -304,14 +338,16 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
     if (big)                                                                                                         \
       hipLaunchKernelGGL((token_gemm_kernel<F8_, E_, 2, 4, 4, 2>), grid, dim3(512), 0, st, (const unsigned char*)x,  \
                          (const unsigned char*)x_scales, (const unsigned char*)w, (const unsigned char*)w_scales,     \
-                         (const bf16*)bias, (bf16*)y, (bf16*)y_pre, M, N, K);                                         \
+                         (const bf16*)bias, (bf16*)y, (bf16*)y_pre, (unsigned char*)y_q, (unsigned char*)y_qscales, M, N, K);                                         \
     else                                                                                                             \
       hipLaunchKernelGGL((token_gemm_kernel<F8_, E_, 2, 2, 2, 2>), grid, dim3(256), 0, st, (const unsigned char*)x,  \
                          (const unsigned char*)x_scales, (const unsigned char*)w, (const unsigned char*)w_scales,     \
-                         (const bf16*)bias, (bf16*)y, (bf16*)y_pre, M, N, K);                                         \
+                         (const bf16*)bias, (bf16*)y, (bf16*)y_pre, (unsigned char*)y_q, (unsigned char*)y_qscales, M, N, K);                                         \
   } while (0)
-  if (f8 && gelu) VS_TG(true, 1);
+  if (f8 && qout) VS_TG(true, 2);
+  else if (f8 && gelu) VS_TG(true, 1);
   else if (f8) VS_TG(true, 0);
+  else if (qout) VS_TG(false, 2);
   else if (gelu) VS_TG(false, 1);
   else VS_TG(false, 0);
 #undef VS_TG

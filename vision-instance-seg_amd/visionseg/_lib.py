@@ -44,7 +44,7 @@ SIGNATURES = {
     "vs_window_attn_backward_fp8": [_P, _P, _P, _P, _P, _P, _P] + [_c_int] * 6 + [_c_float, _P],
     "vs_window_attn_forward_image": [_c_int, _c_int, _P, _P, _P, _P] + [_c_int] * 8 + [_c_float, _P],
     "vs_window_attn_backward_image": [_c_int, _c_int, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 8 + [_c_float, _P],
-    "vs_token_gemm": [_c_int, _P, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _c_int, _P],
+    "vs_token_gemm": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _c_int, _P],
     "vs_mx_quantize": [_P, _P, _P, _c_int, _c_int, _P],
     "vs_mask_head_forward": [_c_int, _P, _P, _P] + [_c_int] * 5 + [_P],
     "vs_mask_head_backward_workspace_bytes": [_c_int] * 3,

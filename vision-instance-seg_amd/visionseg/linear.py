@@ -746,20 +746,30 @@ class _LinearGeluFn(torch.autograd.Function):
     bias gradient) in one HIP pass, then the vendor dX GEMM and the split-K dW."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, fp8=False):
+    def forward(ctx, x, weight, bias, fp8=False, quant_out=False):
         K = x.shape[-1]
+        N = weight.shape[0]
         x2 = x.reshape(-1, K)
+        q = None
         if fp8:
             xq, xs, wq, ws = _mx_pair(x2, weight)
-            y, pre = ops.token_gemm(xq, wq, bias, gelu=True, x_scales=xs, w_scales=ws)
+            out = ops.token_gemm(xq, wq, bias, gelu=True, x_scales=xs, w_scales=ws, quant_out=quant_out)
         else:
-            y, pre = ops.token_gemm(x2, weight, bias, gelu=True)
+            out = ops.token_gemm(x2, weight, bias, gelu=True, quant_out=quant_out)
+        if quant_out:
+            y, pre, q = out
+        else:
+            y, pre = out
         ctx.save_for_backward(x, weight, pre)
         ctx.has_bias = bias is not None
-        return y.view(*x.shape[:-1], weight.shape[0])
+        y = y.view(*x.shape[:-1], N)
+        if quant_out:        # the MX fp8 copy of y for the next GEMM: not differentiable
+            ctx.mark_non_differentiable(q[0], q[1])
+            return y, q[0], q[1]
+        return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, *_):
         x, weight, pre = ctx.saved_tensors
         M, N = pre.shape
         gy2 = gy.reshape(M, N).to(pre.dtype).contiguous()
@@ -776,7 +786,7 @@ class _LinearGeluFn(torch.autograd.Function):
             gw = weight_grad(gp, x.reshape(-1, x.shape[-1]), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = cs.to(weight.dtype)
-        return gx, gw, gb, None
+        return gx, gw, gb, None, None
 
 
 class _LinearFp8Fn(torch.autograd.Function):
@@ -785,30 +795,47 @@ class _LinearFp8Fn(torch.autograd.Function):
     bf16 out.  Straight-through: the backward is _LinearFn's, on the bf16 operands."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, xq=None, xs=None):
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
-        xq, xs, wq, ws = _mx_pair(x2, weight)
-        y = ops.token_gemm(xq, wq, bias, x_scales=xs, w_scales=ws)
+        if xq is None:
+            xq, xs = ops.mx_quantize(x2)
+        wq, ws = ops.mx_quantize(weight)
+        y = ops.token_gemm(xq.reshape(-1, K), wq, bias, x_scales=xs.reshape(-1, K // 32), w_scales=ws)
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.sink = None
         return y.view(*x.shape[:-1], weight.shape[0])
 
-    backward = _LinearFn.backward
+    @staticmethod
+    def backward(ctx, gy):
+        return _LinearFn.backward(ctx, gy) + (None, None)
 
 
 def linear_gelu_tokens(x, w, b, fp8: bool = False):
     """gelu(F.linear(x, w, b)) with the exact erf GELU: fused into the token GEMM on
     token-heavy bf16 device tensors (_LinearGeluFn), the composition otherwise."""
-    if _TGEMM_GELU and _tgemm_ok(x, w, b):
+    if (_TGEMM_GELU or fp8) and _tgemm_ok(x, w, b):
         return _LinearGeluFn.apply(x, w, b, bool(fp8 and w.shape[1] % 128 == 0 and w.shape[1] >= FP8_MIN_K))
     return ops.activation(linear_tokens(x, w, b), "gelu")
 
 
-def linear_fp8_tokens(x, w, b):
+def linear_fp8_tokens(x, w, b, xq=None):
     """F.linear with the product in MX fp8 (_LinearFp8Fn) where it pays (K % 128 == 0 and K
-    >= FP8_MIN_K on token-heavy bf16 tensors), linear_tokens otherwise."""
+    >= FP8_MIN_K on token-heavy bf16 tensors), linear_tokens otherwise.  xq: x's MX fp8 copy
+    (e4m3, scales) when its producer made one (the fused GELU epilogue)."""
     if _tgemm_ok(x, w, b) and w.shape[1] % 128 == 0 and w.shape[1] >= FP8_MIN_K:
-        return _LinearFp8Fn.apply(x, w, b)
+        return _LinearFp8Fn.apply(x, w, b, *(xq if xq is not None else (None, None)))
     return linear_tokens(x, w, b)
+
+
+def mlp_fp8(x, w1, b1, w2, b2):
+    """fc2(gelu(fc1(x))) on the MX fp8 token GEMM: fc1's epilogue writes the GELU output in
+    bf16 (fc2's weight gradient) and as fc2's MX fp8 operand, so no quantisation pass runs
+    between the two GEMMs (config C5)."""
+    K1, N1 = w1.shape[1], w1.shape[0]
+    if _tgemm_ok(x, w1, b1) and N1 % 128 == 0 and N1 >= FP8_MIN_K:
+        fc1_fp8 = K1 % 128 == 0 and K1 >= FP8_MIN_K
+        h, hq, hs = _LinearGeluFn.apply(x, w1, b1, fc1_fp8, True)
+        return linear_fp8_tokens(h, w2, b2, (hq, hs))
+    return linear_fp8_tokens(linear_gelu_tokens(x, w1, b1, fp8=True), w2, b2)

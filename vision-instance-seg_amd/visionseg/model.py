@@ -29,7 +29,7 @@ import torch.nn.functional as F
 
 from . import ops
 from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_fp8_tokens, linear_gelu_tokens,
-                     linear_relu_tokens, linear_tokens, plane_projection, self_attn_in_proj, small_linear, value_query_projection,
+                     linear_relu_tokens, mlp_fp8, linear_tokens, plane_projection, self_attn_in_proj, small_linear, value_query_projection,
                      reattach_level_embed)
 
 
@@ -130,10 +130,9 @@ class Mlp(nn.Module):
         self.fp8 = False
 
     def forward(self, x):
-        h = linear_gelu_tokens(x, self.fc1.weight, self.fc1.bias, fp8=self.fp8)
         if self.fp8:
-            return linear_fp8_tokens(h, self.fc2.weight, self.fc2.bias)
-        return self.fc2(h)
+            return mlp_fp8(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias)
+        return self.fc2(linear_gelu_tokens(x, self.fc1.weight, self.fc1.bias))
 
 
 class SwinBlock(nn.Module):

@@ -1176,7 +1176,7 @@ def upsample_add(cur, src_tokens, Hs: int, Ws: int):
 # ---------------------------------------------------------------------------------------
 # token GEMM (csrc/token_gemm.hip): the Swin blocks' Linears, bf16 or block-scaled MX fp8
 # ---------------------------------------------------------------------------------------
-TGEMM_FP8, TGEMM_GELU = 1, 2
+TGEMM_FP8, TGEMM_GELU, TGEMM_QOUT = 1, 2, 4
 
 
 def mx_quantize(x: torch.Tensor):
@@ -1195,29 +1195,36 @@ def mx_quantize(x: torch.Tensor):
     return q, s
 
 
-def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None):
+def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None, quant_out: bool = False):
     """y = x w^T + bias over token rows (x [..., K], w [N, K]; bf16, or -- with scales --
-    e4m3 bytes from mx_quantize) -> bf16 [..., N]; gelu=True -> (gelu(y) , y) with the
-    exact erf GELU in the epilogue (y = the bf16 pre-activation)."""
+    e4m3 bytes from mx_quantize) -> bf16 [..., N]; gelu=True -> (gelu(y), y) with the exact
+    erf GELU in the epilogue (y = the bf16 pre-activation); quant_out=True (with gelu) ->
+    (gelu(y), y, (e4m3 bytes, e8m0 scales) of gelu(y), as mx_quantize would make them)."""
     fp8 = x_scales is not None
     L.require_hip(x, w)
     K = x.shape[-1]
     N = w.shape[0]
-    if w.shape[1] != K or N % 4 or (fp8 and (w_scales is None or K % 128)) or (not fp8 and K % 8):
+    if w.shape[1] != K or N % 4 or (fp8 and (w_scales is None or K % 128)) or (not fp8 and K % 8) \
+            or (quant_out and (not gelu or N % 32)):
         raise ValueError(f"token_gemm: bad shapes x {tuple(x.shape)} w {tuple(w.shape)} fp8={fp8}")
     x2 = x.reshape(-1, K).contiguous()
     M = x2.shape[0]
     y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
     pre = torch.empty_like(y) if gelu else None
-    mode = (TGEMM_FP8 if fp8 else 0) | (TGEMM_GELU if gelu else 0)
+    yq = torch.empty(M, N, device=x.device, dtype=torch.uint8) if quant_out else None
+    yqs = torch.empty(M, N // 32, device=x.device, dtype=torch.uint8) if quant_out else None
+    mode = (TGEMM_FP8 if fp8 else 0) | (TGEMM_GELU if gelu else 0) | (TGEMM_QOUT if quant_out else 0)
     esz = 1 if fp8 else 2
-    nb = (M * K + N * K) * esz + M * N * 2 * (2 if gelu else 1)
+    nb = (M * K + N * K) * esz + M * N * 2 * (2 if gelu else 1) + (M * N * 33 // 32 if quant_out else 0)
     with timed("token_gemm_fp8" if fp8 else "token_gemm", x2, bytes_=nb, flops=2.0 * M * N * K):
         L.check(L.lib().vs_token_gemm(mode, L.ptr(x2), L.ptr(x_scales.contiguous()) if fp8 else None,
                                       L.ptr(w.contiguous()), L.ptr(w_scales.contiguous()) if fp8 else None,
                                       L.ptr(bias.contiguous()) if bias is not None else None, L.ptr(y),
-                                      L.ptr(pre) if gelu else None, M, N, K, L.stream(x2)), "token_gemm")
+                                      L.ptr(pre) if gelu else None, L.ptr(yq) if quant_out else None,
+                                      L.ptr(yqs) if quant_out else None, M, N, K, L.stream(x2)), "token_gemm")
     shape = (*x.shape[:-1], N)
+    if quant_out:
+        return y.view(shape), pre.view(shape), (yq.view(shape), yqs.view(*x.shape[:-1], N // 32))
     if gelu:
         return y.view(shape), pre.view(shape)
     return y.view(shape)
