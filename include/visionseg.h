@@ -195,6 +195,18 @@ VS_API int vs_window_attn_backward_image(int dtype, int fp8, const void* qkv, co
                                          int height, int width, float scale, void* stream);
 
 
+/* LayerNorm forwards that also write their bf16 output as MX fp8 (e4m3 y_q [rows, C] + e8m0
+ * y_qscales [rows, C/32], the bytes vs_mx_quantize would make of y) at the same rows: the
+ * operand of the fp8 token GEMM that consumes y (config C5), without a quantisation pass.
+ * bf16, C % 32 == 0; otherwise as vs_layer_norm_forward_rows / vs_add_layer_norm_forward(_rows)
+ * (y_rows may be NULL for the add form: row-major output). */
+VS_API int vs_layer_norm_forward_rows_q(const void* x, const void* w, const void* b, void* y, void* y_q,
+                                        void* y_qscales, float* mean, float* rstd, int M, int C, float eps,
+                                        const int* y_rows, void* stream);
+VS_API int vs_add_layer_norm_forward_q(const void* x, const void* r, const void* w, const void* b, void* s,
+                                       void* y, void* y_q, void* y_qscales, float* mean, float* rstd, int M,
+                                       int C, float eps, const int* y_rows, void* stream);
+
 /* ---- a5 / a6: token GEMM (the Swin block's Linears) ----------------------------------
  * y[M, N] = x[M, K] w[N, K]^T + bias[N] (bf16 out, f32 accumulation), both operands
  * K-contiguous rows: the F.linear of HF:swin:418-468 (qkv, proj) and HF:swin:511-536

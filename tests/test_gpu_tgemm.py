@@ -196,3 +196,34 @@ def test_mlp_fp8_vs_bf16_mlp():
     for d, r in zip(dev, ref):
         e = float((d.grad.cpu().double() - r.grad).norm() / r.grad.norm())
         assert e <= 0.06, e
+
+
+@pytest.mark.parametrize("C,shift", [(384, 0), (768, 6)])
+def test_layer_norm_fp8_copy_equals_mx_quantize(C, shift):
+    """The LayerNorms' MX fp8 copy of their output (vs_layer_norm_forward_rows_q,
+    vs_add_layer_norm_forward_q; the qkv / fc1 operand of config C5's fp8 Swin block) is
+    bit-identical to vs_mx_quantize of the bf16 output they store, padding rows zero, and
+    the bf16 output itself equals the plain kernels'."""
+    from visionseg.linear import TokenLayerNorm
+    ops = _ops()
+    g = torch.Generator().manual_seed(C + shift)
+    B, H, W, ws = 2, 30, 26, 12
+    x = _rand((B, H * W, C), g).to(DEV)
+    r = _rand((B, H * W, C), g).to(DEV)
+    ln = TokenLayerNorm(C).to(DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        ln.weight.copy_(_rand((C,), g).to(DEV))
+        ln.bias.copy_(_rand((C,), g).to(DEV))
+    wr = ops.window_rows(B, H, W, ws, shift, x.device)
+    y, (yq, ys) = ln.forward_windows(x, wr, quant=True)
+    assert torch.equal(y, ln.forward_windows(x, wr))
+    eq, es = ops.mx_quantize(y)
+    assert torch.equal(yq, eq) and torch.equal(ys, es)
+    s, y2, (q2, s2) = ln.add_forward_windows(x, r, wr, quant=True)
+    s_ref, y2_ref = ln.add_forward_windows(x, r, wr)
+    assert torch.equal(s, s_ref) and torch.equal(y2, y2_ref)
+    eq, es = ops.mx_quantize(y2)
+    assert torch.equal(q2, eq) and torch.equal(s2, es)
+    s3, y3, (q3, s3q) = ln.add_forward(x, r, quant=True)
+    eq, es = ops.mx_quantize(y3)
+    assert torch.equal(q3, eq) and torch.equal(s3q, es)

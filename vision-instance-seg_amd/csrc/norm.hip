@@ -17,6 +17,7 @@
 // Column sum (bias gradient of a token-major Linear, sum over M of dY [M, N]): same
 // partial-row scheme.
 #include "common.h"
+#include "mx_util.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -77,14 +78,20 @@ template <> struct RawChunk<float> {
 // chunk = 8 elements (one 16-B load for bf16, two for f32); C % 8 == 0
 // RES: y = LN(s) with s = x + r rounded to T (the residual add of a pre-/post-norm block,
 // written to s_out): one pass instead of an add kernel plus a LayerNorm.
-template <typename T, int K, bool RES = false>
+// Q (bf16, C % 32 == 0): y also as MX fp8 -- e4m3 yq [rows, C] + e8m0 yqs [rows, C/32] at
+// the same (window-layout) rows, the bytes vs_mx_quantize would make of y: the operand of
+// the fp8 token GEMM that consumes y (config C5) without a quantisation pass.  A 32-element
+// block is the 4 chunks of lanes 4t..4t+3 (G is a multiple of 4): amax by two exchanges.
+template <typename T, int K, bool RES = false, bool Q = false>
 __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                           const T* __restrict__ b, T* __restrict__ y,
                                                           float* __restrict__ mean, float* __restrict__ rstd,
                                                           int M, int C, float eps, int G,
                                                           const T* __restrict__ r = nullptr,
                                                           T* __restrict__ s_out = nullptr,
-                                                          const int* __restrict__ yrows = nullptr) {
+                                                          const int* __restrict__ yrows = nullptr,
+                                                          unsigned char* __restrict__ yq = nullptr,
+                                                          unsigned char* __restrict__ yqs = nullptr) {
   const int nch = C >> 3;
   const int lane = threadIdx.x & (G - 1);
   const int rows_per_block = kThreads / G;
@@ -162,7 +169,20 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ 
             float o[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mu) * rs * wv[k][i] + bv[k][i];
-            store_chunk(y + (yrows ? (long long)yrows[row] : row) * C + j * 8, o);
+            const long long yr = yrows ? (long long)yrows[row] : row;
+            store_chunk(y + yr * C + j * 8, o);
+            if constexpr (Q) {
+              bf16x8_t c;
+#pragma unroll
+              for (int i = 0; i < 8; ++i) c[i] = bf16_bits(o[i]);      // the stored bf16 values
+              const unsigned am = umax_xor(umax_xor(amax8_bits(c), 1), 2);
+              const int kq = mx_exp_bits(am);
+              const float inv = __builtin_ldexpf(1.f, -kq);
+              const uint4 u = bits128(c);
+              *reinterpret_cast<uint2*>(yq + yr * C + j * 8) =
+                  make_uint2((unsigned)e4m3x4(u.x, u.y, inv), (unsigned)e4m3x4(u.z, u.w, inv));
+              if ((j & 3) == 0) yqs[yr * (C / 32) + (j >> 2)] = (unsigned char)(127 - kq);
+            }
           }
         }
         if (lane == 0) {
@@ -629,7 +649,8 @@ using namespace vs;
 static int ln_kmax(int) { return 4; }
 
 static int layer_norm_forward_impl(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
-                                   float* rstd, int M, int C, float eps, const int* yrows, void* stream);
+                                   float* rstd, int M, int C, float eps, const int* yrows, void* stream,
+                                   void* q = nullptr, void* qs = nullptr);
 
 extern "C" int vs_layer_norm_forward(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
                                      float* rstd, int M, int C, float eps, void* stream) {
@@ -643,8 +664,17 @@ extern "C" int vs_layer_norm_forward_rows(int dtype, const void* x, const void* 
   return layer_norm_forward_impl(dtype, x, w, b, y, mean, rstd, M, C, eps, y_rows, stream);
 }
 
+extern "C" int vs_layer_norm_forward_rows_q(const void* x, const void* w, const void* b, void* y, void* y_q,
+                                            void* y_qscales, float* mean, float* rstd, int M, int C, float eps,
+                                            const int* y_rows, void* stream) {
+  VS_CHECK(M == 0 || (y_rows && y_q && y_qscales), "null pointer");
+  VS_CHECK(C % 32 == 0, "C must be a multiple of 32 for the MX fp8 copy");
+  return layer_norm_forward_impl(VS_BF16, x, w, b, y, mean, rstd, M, C, eps, y_rows, stream, y_q, y_qscales);
+}
+
 static int layer_norm_forward_impl(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
-                                   float* rstd, int M, int C, float eps, const int* yrows, void* stream) {
+                                   float* rstd, int M, int C, float eps, const int* yrows, void* stream, void* q,
+                                   void* qs) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && b && (M == 0 || (x && y && mean && rstd)), "null pointer");
@@ -654,7 +684,11 @@ static int layer_norm_forward_impl(int dtype, const void* x, const void* w, cons
   hipStream_t st = (hipStream_t)stream;
   const int grid = blocks_for(M, kThreads / G, 256 * 32);
 #define VS_LNF(KK)                                                                                          \
-  if (dtype == VS_BF16)                                                                                     \
+  if (q)                                                                                                    \
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, false, true>), dim3(grid), dim3(kThreads), 0, st,           \
+                       (const bf16*)x, (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G,  \
+                       nullptr, nullptr, yrows, (unsigned char*)q, (unsigned char*)qs);                     \
+  else if (dtype == VS_BF16)                                                                                \
     hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK>), dim3(grid), dim3(kThreads), 0, st, (const bf16*)x,        \
                        (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G, nullptr, nullptr, \
                        yrows);                                                                              \
@@ -670,7 +704,7 @@ static int layer_norm_forward_impl(int dtype, const void* x, const void* w, cons
 
 static int add_layer_norm_forward_impl(int dtype, const void* x, const void* r, const void* w, const void* b,
                                        void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
-                                       const int* yrows, void* stream);
+                                       const int* yrows, void* stream, void* q = nullptr, void* qs = nullptr);
 
 extern "C" int vs_add_layer_norm_forward(int dtype, const void* x, const void* r, const void* w, const void* b,
                                          void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
@@ -685,9 +719,18 @@ extern "C" int vs_add_layer_norm_forward_rows(int dtype, const void* x, const vo
   return add_layer_norm_forward_impl(dtype, x, r, w, b, s, y, mean, rstd, M, C, eps, y_rows, stream);
 }
 
+extern "C" int vs_add_layer_norm_forward_q(const void* x, const void* r, const void* w, const void* b, void* s,
+                                           void* y, void* y_q, void* y_qscales, float* mean, float* rstd, int M,
+                                           int C, float eps, const int* y_rows, void* stream) {
+  VS_CHECK(M == 0 || (y_q && y_qscales), "null pointer");
+  VS_CHECK(C % 32 == 0, "C must be a multiple of 32 for the MX fp8 copy");
+  return add_layer_norm_forward_impl(VS_BF16, x, r, w, b, s, y, mean, rstd, M, C, eps, y_rows, stream, y_q,
+                                     y_qscales);
+}
+
 static int add_layer_norm_forward_impl(int dtype, const void* x, const void* r, const void* w, const void* b,
                                        void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
-                                       const int* yrows, void* stream) {
+                                       const int* yrows, void* stream, void* q, void* qs) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && b && (M == 0 || (x && r && s && y && mean && rstd)), "null pointer");
@@ -697,7 +740,11 @@ static int add_layer_norm_forward_impl(int dtype, const void* x, const void* r, 
   hipStream_t st = (hipStream_t)stream;
   const int grid = blocks_for(M, kThreads / G, 256 * 32);
 #define VS_ALNF(KK)                                                                                           \
-  if (dtype == VS_BF16)                                                                                       \
+  if (q)                                                                                                      \
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, true, true>), dim3(grid), dim3(kThreads), 0, st,              \
+                       (const bf16*)x, (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G,    \
+                       (const bf16*)r, (bf16*)s, yrows, (unsigned char*)q, (unsigned char*)qs);               \
+  else if (dtype == VS_BF16)                                                                                  \
     hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, true>), dim3(grid), dim3(kThreads), 0, st, (const bf16*)x,    \
                        (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G, (const bf16*)r,    \
                        (bf16*)s, yrows);                                                                      \

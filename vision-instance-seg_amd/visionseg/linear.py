@@ -607,32 +607,49 @@ class TokenLayerNorm(nn.LayerNorm):
             return ops.layer_norm(x, self.weight, self.bias, self.eps)
         return F.layer_norm(x, self.normalized_shape, self.weight, self.bias, self.eps)
 
-    def forward_windows(self, x, wrows):
+    def forward_windows(self, x, wrows, quant: bool = False):
         """LN(x) in the window layout of wrows (ops.WindowRows: the Swin partition folded
-        into the kernel's stores) -> [wrows.total, C]."""
+        into the kernel's stores) -> [wrows.total, C]; quant (bf16, C % 32 == 0): -> (y,
+        (e4m3, e8m0 scales) of y) for an fp8 consumer, (y, None) where the copy cannot be made."""
         if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
                 and not torch.is_autocast_enabled():
-            return ops.layer_norm(x, self.weight, self.bias, self.eps, wrows=wrows)
+            if quant and x.dtype == torch.bfloat16 and x.shape[-1] % 32 == 0:
+                y, yq, ys = ops.layer_norm(x, self.weight, self.bias, self.eps, wrows=wrows, quant=True)
+                return y, (yq, ys)
+            y = ops.layer_norm(x, self.weight, self.bias, self.eps, wrows=wrows)
+            return (y, None) if quant else y
         y = self(x)
-        return ops._to_windows(y.to(_autocast_dtype(y)), wrows)
+        y = ops._to_windows(y.to(_autocast_dtype(y)), wrows)
+        return (y, None) if quant else y
 
-    def add_forward_windows(self, x, r, wrows, sink=None):
-        """(x + r, LN(x + r) in the window layout of wrows)."""
+    def add_forward_windows(self, x, r, wrows, sink=None, quant: bool = False):
+        """(x + r, LN(x + r) in the window layout of wrows) (+ the MX fp8 copy, see
+        forward_windows)."""
         if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
                 and r.shape == x.shape and r.dtype == x.dtype and not torch.is_autocast_enabled():
-            return ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, wrows=wrows)
+            if quant and x.dtype == torch.bfloat16 and x.shape[-1] % 32 == 0:
+                s, y, yq, ys = ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, wrows=wrows, quant=True)
+                return s, y, (yq, ys)
+            s, y = ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, wrows=wrows)
+            return (s, y, None) if quant else (s, y)
         s, y = self.add_forward(x, r, sink)
-        return s, ops._to_windows(y.to(_autocast_dtype(y)), wrows)
+        y = ops._to_windows(y.to(_autocast_dtype(y)), wrows)
+        return (s, y, None) if quant else (s, y)
 
-    def add_forward(self, x, r, sink=None):
+    def add_forward(self, x, r, sink=None, quant: bool = False):
         """(x + r, LN(x + r)): the residual add fused into the norm on the HIP kernel
         (ops.add_layer_norm) where the plain norm would run there too.  `sink`: hand x's
-        gradient to the armed consumer of x (ops.ResidualSink)."""
+        gradient to the armed consumer of x (ops.ResidualSink); `quant`: + the MX fp8 copy of
+        LN(x + r) (see forward_windows)."""
         if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
                 and r.shape == x.shape and r.dtype == x.dtype and not torch.is_autocast_enabled():
-            return ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink)
+            if quant and x.dtype == torch.bfloat16 and x.shape[-1] % 32 == 0:
+                s, y, yq, ys = ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, quant=True)
+                return s, y, (yq.view(y.shape), ys.view(*y.shape[:-1], -1))
+            s, y = ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink)
+            return (s, y, None) if quant else (s, y)
         s = x + r
-        return s, self(s)
+        return (s, self(s), None) if quant else (s, self(s))
 
 
 def linear_tokens(x, w, b=None, sink=None):
@@ -721,6 +738,12 @@ _TGEMM_GELU = os.environ.get("VS_TGEMM_GELU", "0") == "1"
 FP8_MIN_K = int(os.environ.get("VS_FP8_MIN_K", "384"))
 
 
+def fp8_operand_ok(K: int) -> bool:
+    """Whether a Linear with K input features takes the MX fp8 path (linear_fp8_tokens):
+    the producer of its input then makes the fp8 copy too."""
+    return K % 128 == 0 and K >= FP8_MIN_K
+
+
 def _tgemm_ok(x, w, b, tokens_min=MIN_TOKENS):
     tokens = x.numel() // max(1, x.shape[-1])
     K, N = w.shape[1], w.shape[0]
@@ -746,13 +769,17 @@ class _LinearGeluFn(torch.autograd.Function):
     bias gradient) in one HIP pass, then the vendor dX GEMM and the split-K dW."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, fp8=False, quant_out=False):
+    def forward(ctx, x, weight, bias, fp8=False, quant_out=False, xq=None, xs=None):
         K = x.shape[-1]
         N = weight.shape[0]
         x2 = x.reshape(-1, K)
         q = None
         if fp8:
-            xq, xs, wq, ws = _mx_pair(x2, weight)
+            if xq is None:
+                xq, xs = ops.mx_quantize(x2)
+            else:
+                xq, xs = xq.reshape(-1, K), xs.reshape(-1, K // 32)
+            wq, ws = ops.mx_quantize(weight)
             out = ops.token_gemm(xq, wq, bias, gelu=True, x_scales=xs, w_scales=ws, quant_out=quant_out)
         else:
             out = ops.token_gemm(x2, weight, bias, gelu=True, quant_out=quant_out)
@@ -786,7 +813,7 @@ class _LinearGeluFn(torch.autograd.Function):
             gw = weight_grad(gp, x.reshape(-1, x.shape[-1]), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = cs.to(weight.dtype)
-        return gx, gw, gb, None, None
+        return gx, gw, gb, None, None, None, None
 
 
 class _LinearFp8Fn(torch.autograd.Function):
@@ -829,13 +856,14 @@ def linear_fp8_tokens(x, w, b, xq=None):
     return linear_tokens(x, w, b)
 
 
-def mlp_fp8(x, w1, b1, w2, b2):
+def mlp_fp8(x, w1, b1, w2, b2, xq=None):
     """fc2(gelu(fc1(x))) on the MX fp8 token GEMM: fc1's epilogue writes the GELU output in
     bf16 (fc2's weight gradient) and as fc2's MX fp8 operand, so no quantisation pass runs
-    between the two GEMMs (config C5)."""
+    between the two GEMMs (config C5).  xq: x's MX fp8 copy from its producer (the
+    LayerNorm), if it made one."""
     K1, N1 = w1.shape[1], w1.shape[0]
     if _tgemm_ok(x, w1, b1) and N1 % 128 == 0 and N1 >= FP8_MIN_K:
         fc1_fp8 = K1 % 128 == 0 and K1 >= FP8_MIN_K
-        h, hq, hs = _LinearGeluFn.apply(x, w1, b1, fc1_fp8, True)
+        h, hq, hs = _LinearGeluFn.apply(x, w1, b1, fc1_fp8, True, *(xq if (xq is not None and fc1_fp8) else (None, None)))
         return linear_fp8_tokens(h, w2, b2, (hq, hs))
     return linear_fp8_tokens(linear_gelu_tokens(x, w1, b1, fp8=True), w2, b2)

@@ -28,7 +28,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, in_projection, linear_fp8_tokens, linear_gelu_tokens,
+from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, fp8_operand_ok, in_projection, linear_fp8_tokens,
+                     linear_gelu_tokens,
                      linear_relu_tokens, mlp_fp8, linear_tokens, plane_projection, self_attn_in_proj, small_linear, value_query_projection,
                      reattach_level_embed)
 
@@ -129,9 +130,9 @@ class Mlp(nn.Module):
         self.fc2 = TokenLinear(hidden, dim)
         self.fp8 = False
 
-    def forward(self, x):
+    def forward(self, x, xq=None):
         if self.fp8:
-            return mlp_fp8(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias)
+            return mlp_fp8(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, xq)
         return self.fc2(linear_gelu_tokens(x, self.fc1.weight, self.fc1.bias))
 
 
@@ -155,13 +156,18 @@ class SwinBlock(nn.Module):
         # the window partition folded into the norm's stores (ops.WindowRows): h comes out
         # in the window layout [B*nW*ws^2, C], padding rows zero
         wr = ops.window_rows(B, H, W, ws, shift, x.device)
-        if res is None:
+        if self.linear_fp8:
+            # the norms also write their output as the fp8 GEMM operand (no quantisation pass)
+            if res is None:
+                h, hq = self.norm1.forward_windows(x, wr, quant=fp8_operand_ok(C))
+            else:
+                x, h, hq = self.norm1.add_forward_windows(x, res, wr, quant=fp8_operand_ok(C))
+            qkv = linear_fp8_tokens(h.view(-1, ws * ws, C), self.attn.qkv.weight, self.attn.qkv.bias, hq)
+        elif res is None:
             h = self.norm1.forward_windows(x, wr)
         else:
             x, h = self.norm1.add_forward_windows(x, res, wr)
-        if self.linear_fp8:
-            qkv = linear_fp8_tokens(h.view(-1, ws * ws, C), self.attn.qkv.weight, self.attn.qkv.bias)
-        else:
+        if not self.linear_fp8:
             qkv = self.attn.qkv(h.view(-1, ws * ws, C))
         # output in the image layout (window reverse folded into the kernel); the per-token
         # proj commutes with the crop
@@ -171,6 +177,9 @@ class SwinBlock(nn.Module):
             o = linear_fp8_tokens(o.view(B, H * W, C), self.attn.proj.weight, self.attn.proj.bias)
         else:
             o = self.attn.proj(o.view(B, H * W, C))
+        if self.linear_fp8:
+            x, h2, h2q = self.norm2.add_forward(x, o, quant=fp8_operand_ok(C))
+            return x, self.mlp(h2, h2q)
         x, h2 = self.norm2.add_forward(x, o)
         return x, self.mlp(h2)
 

@@ -670,9 +670,10 @@ class LayerNormFunction(torch.autograd.Function):
     x, weight, bias share one dtype (f32 or bf16)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, wrows=None):
+    def forward(ctx, x, weight, bias, eps, wrows=None, quant=False):
         """wrows (WindowRows): y in the window layout [wrows.total, C] (the partition folded
-        into the kernel's stores; padding rows zero)."""
+        into the kernel's stores; padding rows zero).  quant (bf16, with wrows): also y's MX
+        fp8 copy (e4m3, e8m0 scales) -> (y, y_q, y_qscales), the copy not differentiable."""
         L.require_hip(x, weight, bias)
         C = x.shape[-1]
         xc = x.contiguous()
@@ -680,7 +681,19 @@ class LayerNormFunction(torch.autograd.Function):
         mean = torch.empty(M, device=x.device, dtype=torch.float32)
         rstd = torch.empty(M, device=x.device, dtype=torch.float32)
         with timed("layer_norm_fwd", xc, bytes_=2 * xc.numel() * xc.element_size()):
-            if wrows is None:
+            if quant:
+                y = torch.empty(wrows.total, C, device=x.device, dtype=xc.dtype)
+                yq = torch.empty(wrows.total, C, device=x.device, dtype=torch.uint8)
+                ys = torch.empty(wrows.total, C // 32, device=x.device, dtype=torch.uint8)
+                L.check(L.lib().vs_layer_norm_forward_rows_q(L.ptr(xc), L.ptr(weight), L.ptr(bias), L.ptr(y),
+                                                             L.ptr(yq), L.ptr(ys), L.ptr(mean), L.ptr(rstd), M, C,
+                                                             float(eps), L.ptr(wrows.rows), L.stream(xc)),
+                        "layer_norm_forward_rows_q")
+                if wrows.pad.numel():
+                    y.index_fill_(0, wrows.pad, 0)
+                    yq.index_fill_(0, wrows.pad, 0)
+                    ys.index_fill_(0, wrows.pad, 127)          # scale 1 (0xff would be NaN)
+            elif wrows is None:
                 y = torch.empty_like(xc)
                 L.check(L.lib().vs_layer_norm_forward(L.dtype_code(xc), L.ptr(xc), L.ptr(weight), L.ptr(bias),
                                                       L.ptr(y), L.ptr(mean), L.ptr(rstd), M, C, float(eps),
@@ -694,10 +707,13 @@ class LayerNormFunction(torch.autograd.Function):
                     y.index_fill_(0, wrows.pad, 0)
         ctx.wrows = wrows
         ctx.save_for_backward(xc, weight, mean, rstd)
+        if quant:
+            ctx.mark_non_differentiable(yq, ys)
+            return y, yq, ys
         return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, *_):
         xc, weight, mean, rstd = ctx.saved_tensors
         C = xc.shape[-1]
         M = xc.numel() // C
@@ -717,7 +733,7 @@ class LayerNormFunction(torch.autograd.Function):
                                                             L.ptr(mean), L.ptr(rstd), None, L.ptr(gx), L.ptr(gw),
                                                             L.ptr(gb), None, L.ptr(ws), M, C, L.ptr(ctx.wrows.rows),
                                                             L.stream(xc)), "layer_norm_backward_rows")
-        return gx, gw, gb, None, None
+        return gx, gw, gb, None, None, None
 
 
 def attach_colsum(g: torch.Tensor, colsum: torch.Tensor) -> None:
@@ -741,8 +757,9 @@ class AddLayerNormFunction(torch.autograd.Function):
     backward adds the gradient of s (residual path) inside the LayerNorm backward."""
 
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps, sink=None, wrows=None):
-        """wrows (WindowRows): y in the window layout (see LayerNormFunction); s stays in x's."""
+    def forward(ctx, x, r, weight, bias, eps, sink=None, wrows=None, quant=False):
+        """wrows (WindowRows): y in the window layout (see LayerNormFunction); s stays in x's.
+        quant (bf16): also y's MX fp8 copy -> (s, y, y_q, y_qscales)."""
         L.require_hip(x, r, weight, bias)
         ctx.sink = sink if sink is not None and sink.armed else None
         C = x.shape[-1]
@@ -752,7 +769,23 @@ class AddLayerNormFunction(torch.autograd.Function):
         mean = torch.empty(M, device=x.device, dtype=torch.float32)
         rstd = torch.empty(M, device=x.device, dtype=torch.float32)
         with timed("add_layer_norm_fwd", xc, bytes_=4 * xc.numel() * xc.element_size()):
-            if wrows is None:
+            if quant:
+                rows = wrows.total if wrows is not None else M
+                y = torch.empty(rows, C, device=x.device, dtype=xc.dtype)
+                yq = torch.empty(rows, C, device=x.device, dtype=torch.uint8)
+                ys = torch.empty(rows, C // 32, device=x.device, dtype=torch.uint8)
+                L.check(L.lib().vs_add_layer_norm_forward_q(L.ptr(xc), L.ptr(rc), L.ptr(weight), L.ptr(bias),
+                                                            L.ptr(s), L.ptr(y), L.ptr(yq), L.ptr(ys), L.ptr(mean),
+                                                            L.ptr(rstd), M, C, float(eps),
+                                                            L.ptr(wrows.rows) if wrows is not None else None,
+                                                            L.stream(xc)), "add_layer_norm_forward_q")
+                if wrows is None:
+                    y = y.view(xc.shape)
+                elif wrows.pad.numel():
+                    y.index_fill_(0, wrows.pad, 0)
+                    yq.index_fill_(0, wrows.pad, 0)
+                    ys.index_fill_(0, wrows.pad, 127)
+            elif wrows is None:
                 y = torch.empty_like(xc)
                 L.check(L.lib().vs_add_layer_norm_forward(L.dtype_code(xc), L.ptr(xc), L.ptr(rc), L.ptr(weight),
                                                           L.ptr(bias), L.ptr(s), L.ptr(y), L.ptr(mean), L.ptr(rstd),
@@ -767,10 +800,13 @@ class AddLayerNormFunction(torch.autograd.Function):
                     y.index_fill_(0, wrows.pad, 0)
         ctx.wrows = wrows
         ctx.save_for_backward(s, weight, mean, rstd)
+        if quant:
+            ctx.mark_non_differentiable(yq, ys)
+            return s, y, yq, ys
         return s, y
 
     @staticmethod
-    def backward(ctx, gs, gy):
+    def backward(ctx, gs, gy, *_):
         s, weight, mean, rstd = ctx.saved_tensors
         C = s.shape[-1]
         M = s.numel() // C
@@ -806,17 +842,18 @@ class AddLayerNormFunction(torch.autograd.Function):
         if ctx.sink is not None and ctx.needs_input_grad[0]:
             ctx.sink.g = gx            # the armed consumer of x adds it in its dX GEMM
             gxx = None
-        return gxx, gx, gw, gb, None, None, None
+        return gxx, gx, gw, gb, None, None, None, None
 
 
-def add_layer_norm(x, r, weight, bias, eps: float = 1e-5, sink: ResidualSink | None = None, wrows=None):
+def add_layer_norm(x, r, weight, bias, eps: float = 1e-5, sink: ResidualSink | None = None, wrows=None,
+                   quant: bool = False):
     """(x + r, layer_norm(x + r)) for token-major [..., C] tensors (see AddLayerNormFunction;
-    `sink`: see ResidualSink; `wrows`: y in the window layout)."""
-    return AddLayerNormFunction.apply(x, r, weight, bias, eps, sink, wrows)
+    `sink`: see ResidualSink; `wrows`: y in the window layout; `quant`: + y's MX fp8 copy)."""
+    return AddLayerNormFunction.apply(x, r, weight, bias, eps, sink, wrows, quant)
 
 
-def layer_norm(x, weight, bias, eps: float = 1e-5, wrows=None):
-    return LayerNormFunction.apply(x, weight, bias, eps, wrows)
+def layer_norm(x, weight, bias, eps: float = 1e-5, wrows=None, quant: bool = False):
+    return LayerNormFunction.apply(x, weight, bias, eps, wrows, quant)
 
 
 def layer_norm_supported(x, weight) -> bool:
