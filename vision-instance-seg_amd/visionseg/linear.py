@@ -753,6 +753,21 @@ def _tgemm_ok(x, w, b, tokens_min=MIN_TOKENS):
             and N <= ops.COLSUM_MAX_N and x.is_contiguous())
 
 
+# config C5 fp8 Linears: the input gradient dX = dY W on the MX fp8 token GEMM too (dY and W^T
+# quantised per 32 along the output features); VS_FP8_DGRAD=0 keeps it on the bf16 vendor GEMM
+FP8_DGRAD = os.environ.get("VS_FP8_DGRAD", "1") == "1"
+
+
+def _dgrad(gy2, weight):
+    """dX = dY W for dY [M, N], W [N, K]: MX fp8 (FP8_DGRAD, N % 128 == 0) or the vendor GEMM."""
+    N, K = weight.shape
+    if FP8_DGRAD and N % 128 == 0 and K % 8 == 0 and gy2.dtype == torch.bfloat16:
+        gq, gs = ops.mx_quantize(gy2.contiguous())
+        wtq, wts = ops.mx_quantize(weight.t().contiguous())
+        return ops.token_gemm(gq, wtq, None, x_scales=gs, w_scales=wts)
+    return gy2 @ weight.to(gy2.dtype)
+
+
 def _mx_pair(x2, weight):
     xq, xs = ops.mx_quantize(x2)
     wq, ws = ops.mx_quantize(weight)
@@ -789,6 +804,7 @@ class _LinearGeluFn(torch.autograd.Function):
             y, pre = out
         ctx.save_for_backward(x, weight, pre)
         ctx.has_bias = bias is not None
+        ctx.fp8 = bool(fp8)
         y = y.view(*x.shape[:-1], N)
         if quant_out:        # the MX fp8 copy of y for the next GEMM: not differentiable
             ctx.mark_non_differentiable(q[0], q[1])
@@ -808,7 +824,7 @@ class _LinearGeluFn(torch.autograd.Function):
                                                    L.ptr(ws), M, N, L.stream(pre)), "act_backward_colsum")
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = (gp @ weight.to(gp.dtype)).view(x.shape)
+            gx = (_dgrad(gp, weight) if ctx.fp8 else gp @ weight.to(gp.dtype)).view(x.shape)
         if ctx.needs_input_grad[1]:
             gw = weight_grad(gp, x.reshape(-1, x.shape[-1]), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -836,7 +852,23 @@ class _LinearFp8Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        return _LinearFn.backward(ctx, gy) + (None, None)
+        """_LinearFn's backward with dX on the MX fp8 GEMM (FP8_DGRAD)."""
+        x, weight = ctx.saved_tensors
+        gy2 = gy.reshape(-1, gy.shape[-1])
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = _dgrad(gy2, weight).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            gw = weight_grad(gy2, x.reshape(-1, x.shape[-1]).to(gy2.dtype), weight.dtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            cs = ops.take_colsum(gy)
+            if cs is not None:
+                gb = cs.to(weight.dtype)
+            elif gy2.shape[1] % 8 == 0 and gy2.shape[1] <= ops.COLSUM_MAX_N:
+                gb = ops.column_sum(gy2).to(weight.dtype)
+            else:
+                gb = gy2.sum(0, dtype=torch.float32).to(weight.dtype)
+        return gx, gw, gb, None, None
 
 
 def linear_gelu_tokens(x, w, b, fp8: bool = False):
