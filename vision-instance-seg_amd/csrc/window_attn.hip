@@ -663,6 +663,23 @@ __device__ __forceinline__ void fp8_token_lane(bf16x8_t* c) {
   c[1] = fp8_roundtrip8(c[1], k);
 }
 
+// (window, head) of a one-workgroup-per-(window, head) kernel.  1-D launches (the default):
+// the heads of a window are consecutive logical workgroups on ONE XCD (xcd_swizzle): a
+// head's slice of a qkv / out / grad row is 64 B, half a 128-B line, so a window's heads
+// share every line they read or write and meet in that XCD's L2 instead of each pulling
+// (and, for the gradients, partially writing back) whole lines on different XCDs at
+// different times.  2-D launches (gridDim.y = heads): blockIdx as is.
+__device__ __forceinline__ void win_block(const WinGeom& g, int& bw, int& h) {
+  if (gridDim.y > 1) {
+    bw = blockIdx.x;
+    h = blockIdx.y;
+    return;
+  }
+  const int lg = xcd_swizzle(blockIdx.x, gridDim.x);
+  bw = lg / g.heads;
+  h = lg - bw * g.heads;
+}
+
 template <int NT>
 __device__ __forceinline__ void window_tokens_blk(const WinGeom& g, int bw, int* tok) {
   for (int t = threadIdx.x; t < 32 * NT; t += blockDim.x) tok[t] = token_meta(g, bw, t);
@@ -678,7 +695,8 @@ __global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __r
   __shared__ __attribute__((aligned(16))) short sVt[32 * PT];  // V^T [d][key]
   __shared__ float sBias[kMaxT2Big + 2 * kZoneBig];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
-  const int bw = blockIdx.x, h = blockIdx.y;
+  int bw, h;
+  win_block(g, bw, h);
   const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
   const bf16* win = qkv + (size_t)bw * N * C3;
@@ -783,7 +801,8 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(6)
   __shared__ __attribute__((aligned(16))) short sVt[32 * PT];  // V^T [d][key]
   __shared__ float sBias[kMaxT2Big + 2 * kZoneBig];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
-  const int bw = blockIdx.x, h = blockIdx.y;
+  int bw, h;
+  win_block(g, bw, h);
   const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
   const bf16* win = qkv + (size_t)bw * N * C3;
@@ -878,7 +897,8 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(ON
   __shared__ unsigned sVam[NT];
   __shared__ float sBias[kMaxT2Big + 2 * kZoneBig];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
-  const int bw = blockIdx.x, h = blockIdx.y;
+  int bw, h;
+  win_block(g, bw, h);
   const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
   const bf16* win = qkv + (size_t)bw * N * C3;
@@ -1097,7 +1117,8 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
   __shared__ float sBias[kMaxT2Big + 2 * kZoneBig];
   __shared__ __attribute__((aligned(16))) int sTok[NP];
   __shared__ float sL[NP], sD[NP];
-  const int bw = blockIdx.x, h = blockIdx.y;
+  int bw, h;
+  win_block(g, bw, h);
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int N = g.N, C = g.heads * kD, C3 = 3 * C;
   const bf16* win = qkv + (size_t)bw * N * C3 + h * kD;
@@ -1351,6 +1372,15 @@ static bool fwd_online() {
   return v != 0;
 }
 
+// VS_WIN_XCD=0: the 2-D (window, head) grid instead of the XCD-grouped 1-D one (A/B)
+static dim3 blk_grid(dim3 g2) {
+  static const int v = [] {
+    const char* e = getenv("VS_WIN_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  return v ? dim3(g2.x * g2.y) : g2;
+}
+
 #define VS_NT_SWITCH(nt, M)            \
   switch (nt) {                        \
     case 1: case 2: M(2); break;       \
@@ -1362,6 +1392,7 @@ static bool fwd_online() {
 template <bool F8>
 static void launch_fwd_blk(const WinGeom& g, dim3 grid, hipStream_t st, const void* qkv, const float* table,
                            void* out, float* lse) {
+  grid = blk_grid(grid);
 #define VS_FWD_BLK(NT_)                                                                                     \
   if (F8 && fwd_online())                                                                                   \
     hipLaunchKernelGGL((win_attn_fwd_mx<NT_, true>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,   \
@@ -1382,6 +1413,7 @@ static void launch_fwd_blk(const WinGeom& g, dim3 grid, hipStream_t st, const vo
 template <bool F8>
 static void launch_bwd_fa(const WinGeom& g, dim3 grid, hipStream_t st, const void* qkv, const float* table,
                           const void* out, const float* lse, const void* grad_out, void* grad_qkv, float* gpart) {
+  grid = blk_grid(grid);
 #define VS_BWD_FA(NT_)                                                                                      \
   hipLaunchKernelGGL((win_attn_bwd_fa<NT_, F8>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,       \
                      (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g)
