@@ -104,7 +104,8 @@ def pmc_file(model, size):
 
 
 OP_KERNELS = {   # op -> kernel-name substrings (template arguments included) whose dispatches make one launch
-    "msda_bwd": ["msda_bwd_mfma_wg_kernel<8, 8, true"],   # <8, 8, true, SKEL>
+    # the pyramid-column kernel (default for encoder problems) or the 8 x 8 tile kernel
+    "msda_bwd": ["msda_bwd_col_kernel<", "msda_bwd_mfma_wg_kernel<8, 8, true"],
     "msda_fwd": ["msda_fwd_kernel<"],
     "window_attn_fwd": ["win_attn_fwd_mfma(", "win_attn_fwd_mfma_big<3, false>", "win_attn_fwd_mfma_big<4, false>",
                         "win_attn_fwd_mfma_big<5, false>"],

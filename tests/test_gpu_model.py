@@ -269,3 +269,42 @@ def test_predictor_graph_replay_matches_eager():
         assert float((a.masks != b.masks).float().mean()) <= 3e-2
     assert torch.equal(a.masks, first.masks) and torch.equal(a.scores, first.scores)   # recaptured == first capture
     assert len(pg._graphs) == 2
+
+
+@pytest.mark.gpu
+def test_predictor_bf16_vs_f32_model():
+    """The default Predictor (amp: a pure-bf16 copy of the model, bf16 activations, the
+    production MFMA kernels) against the same model run in f32 (amp=False: f32 parameters
+    and the f32 kernel mode), on the same preprocessed images.  Bounds: class
+    probabilities within 2e-2, mask logits within 3e-2 of their max |logit| with at least
+    97 % of the binary-mask pixels equal, and the post-processed top-20 scores (sorted, so
+    near-tie reorderings between equal scores do not count) within 2e-2."""
+    from visionseg.inference import Predictor, instance_inference
+    from visionseg.model import M2FConfig, Mask2Former
+    m = Mask2Former(M2FConfig.preset("swin_t")).init_weights(0)
+    pb = Predictor(m, device=DEV, min_size=256, max_size=320, graphs=False)
+    pf = Predictor(m, device=DEV, min_size=256, max_size=320, amp=False, graphs=False)
+    assert next(pb.model.parameters()).dtype == torch.bfloat16
+    assert next(pf.model.parameters()).dtype == torch.float32
+    rng = np.random.default_rng(1)
+    for shape in ((200, 260), (300, 180)):
+        img = rng.integers(0, 256, (*shape, 3)).astype(np.uint8)
+        x, valid, orig = pf._preprocess(img)
+        with torch.no_grad():
+            ob, of = pb._forward(x.to(torch.bfloat16)), pf._forward(x)
+        mb, cb = ob[0][-1][0].float(), ob[1][-1][0].float()
+        mf, cf = of[0][-1][0].float(), of[1][-1][0].float()
+        dprob = float((cb.softmax(-1) - cf.softmax(-1)).abs().max())
+        assert dprob <= 2e-2, dprob
+        scale = float(mf.abs().max())
+        dm = float((mb - mf).abs().max())
+        assert dm <= 3e-2 * scale, (dm, scale)
+        agree = float(((mb > 0) == (mf > 0)).float().mean())
+        assert agree >= 0.97, agree
+        sb = instance_inference(mb, cb, orig, valid_hw=valid, pad_hw=tuple(x.shape[-2:]), top_k=20)[0]
+        sf = instance_inference(mf, cf, orig, valid_hw=valid, pad_hw=tuple(x.shape[-2:]), top_k=20)[0]
+        ds = float((sb.sort().values - sf.sort().values).abs().max())
+        assert ds <= 2e-2, ds
+        # the full seam agrees too (bf16 path end to end, post-processing included)
+        res = pb(img).pred_instances
+        assert res.masks.shape[1:] == shape and len(res) == 100

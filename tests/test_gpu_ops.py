@@ -557,17 +557,36 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, win, jitter):
     np.testing.assert_allclose(ld.grad.cpu().numpy(), gl, atol=2e-5 * max(1.0, np.abs(gl).max()), rtol=0)
 
 
-@pytest.mark.parametrize("win", ["tile", "tile-1024", "tile-odd", "sub", "4lvl", "ragged"])
+@pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(9, 13), (18, 26), (35, 51), (5, 7)]])
+def test_msda_forward_taps_in_flight_bit_identical(monkeypatch, shapes):
+    """The P = 4 forward with 4 taps' corner rows in flight (VS_MSDA_FWD_TAPS=4) does the same
+    arithmetic in the same order as the default 2: bit-identical outputs, incl. taps outside."""
+    ops = _ops()
+    value, loc, w = _encoder_like_inputs(1, shapes, 8, 4, seed=21, jitter=3.0)
+    vd, ld, wd = value.to(torch.bfloat16).to(DEV), loc.to(DEV), w.to(DEV)
+    outs = []
+    for taps in ("2", "4"):
+        monkeypatch.setenv("VS_MSDA_FWD_TAPS", taps)
+        outs.append(ops.ms_deform_attn(vd, shapes, ld, wd))
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("win", ["tile", "tile-1024", "tile-odd", "sub", "4lvl", "ragged", "wide"])
 @pytest.mark.parametrize("jitter", [0.0, 0.3, 3.0, 12.0])
 def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
-    """bf16 grad_value by the MFMA query-tile kernel (msda_bwd_mfma_wg_kernel: 8 x 8 tiles per
-    4-wave workgroup, W[cell][q] x g[q][c] per box, W split into bf16 hi + lo) vs (a) the
-    binned kernel on the same
-    inputs (VS_MSDA_MFMA=0; both sum in f32: <= 1e-5 of the gradient scale) and (b) the
-    oracle (bf16 output rounding: 2^-8 relative + 1e-4).  jitter 12 px drives boxes past
-    the 128-cell cap (clipped corners take the direct atomics); "sub" runs 16 consecutive
-    queries of a query subset (Q != S), "4lvl" four levels stored finest first, "ragged" a 2x
-    pyramid whose finest level is not a multiple of the 8 x 8 tile."""
+    """bf16 grad_value + grad_loc / grad_attn of the MFMA backward kernels vs (a) the binned
+    kernel on the same inputs (VS_MSDA_MFMA=0; all sum in f32: within two bf16 ulps) and (b)
+    the oracle (bf16 output rounding: 2^-8 relative + 1e-4):
+      * "col": msda_bwd_col_kernel, pyramid columns of 8 x 16 finest-level queries
+        (3 chunks of 64), one flush per (band, cell) per column; "col16": 16 x 16 (6 chunks);
+      * "tile" / "tile_s": msda_bwd_mfma_wg_kernel (VS_MSDA_COL=0), 8 x 8 query tiles, on its
+        two band skeletons (VS_MSDA_SKEL 0 / 2), and "tile_sep" with the separate grad_loc
+        gather kernel (VS_MSDA_GEOM=0).
+    jitter 12 px drives boxes past the 128-cell band cap; "sub" runs 16 consecutive queries
+    of a query subset (Q != S: the column kernel does not apply), "4lvl" four levels stored
+    finest first, "ragged" a 2x pyramid whose finest level is not a multiple of the blocks,
+    "wide" a finest level 150 cells wide with far taps (boxes wider than the band cap: bands
+    split along x too)."""
     ops = _ops()
     monkeypatch.setattr(ops, "_MSDA_BWD", "carry")
     monkeypatch.setenv("VS_MSDA_RUN", "16")            # the split kernels at every size
@@ -580,6 +599,8 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
         shapes = [(48, 80), (24, 40), (12, 20), (6, 10)]
     elif win == "ragged":                              # partial border tiles
         shapes = [(5, 3), (10, 6), (20, 12)]
+    elif win == "wide":
+        shapes, jitter = [(10, 38), (20, 75), (40, 150)], jitter * 4 + 20
     value, loc, w = _encoder_like_inputs(B, shapes, H, 4, seed=13, jitter=jitter)
     if win == "sub":
         idx = torch.randperm(loc.shape[1], generator=torch.Generator().manual_seed(5))[:700].sort().values
@@ -590,41 +611,49 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
     go = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3)).to(torch.bfloat16)
     ref.backward(go.float())
     grads, geo = {}, {}
-    # (mfma, geom, band skeleton): "s" = the product kernel on its default clear-after band
-    # skeleton (VS_MSDA_SKEL=2), "1" = the zero-fill-per-band skeleton (VS_MSDA_SKEL=0)
-    for mf, gm, sk in (("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"), ("s", "1", "2")):
-        monkeypatch.setenv("VS_MSDA_MFMA", "1" if mf == "s" else mf)
-        monkeypatch.setenv("VS_MSDA_GEOM", gm)
-        monkeypatch.setenv("VS_MSDA_SKEL", sk)
+    variants = {
+        "tile_sep": dict(VS_MSDA_MFMA="1", VS_MSDA_GEOM="0", VS_MSDA_SKEL="0", VS_MSDA_COL="0"),
+        "binned": dict(VS_MSDA_MFMA="0", VS_MSDA_GEOM="0", VS_MSDA_SKEL="0", VS_MSDA_COL="0"),
+        "tile": dict(VS_MSDA_MFMA="1", VS_MSDA_GEOM="1", VS_MSDA_SKEL="0", VS_MSDA_COL="0"),
+        "tile_s": dict(VS_MSDA_MFMA="1", VS_MSDA_GEOM="1", VS_MSDA_SKEL="2", VS_MSDA_COL="0"),
+        "col": dict(VS_MSDA_MFMA="1", VS_MSDA_GEOM="1", VS_MSDA_SKEL="2", VS_MSDA_COL="8x16"),
+        "col16": dict(VS_MSDA_MFMA="1", VS_MSDA_GEOM="1", VS_MSDA_SKEL="2", VS_MSDA_COL="16x16"),
+    }
+    for name, env in variants.items():
+        for k, v in env.items():
+            if v is None:
+                monkeypatch.delenv(k, raising=False)
+            else:
+                monkeypatch.setenv(k, v)
         vd = value.to(DEV).requires_grad_(True)
         ld, wd = loc.to(DEV).requires_grad_(True), w.to(DEV).requires_grad_(True)
         out = ops.ms_deform_attn(vd, shapes, ld, wd)
         out.backward(go.to(DEV))
-        grads[mf] = vd.grad.float().cpu()
-        geo[(mf, gm)] = (ld.grad.cpu(), wd.grad.cpu())
-    # grad_loc / grad_attn fused into the product kernel (GEOM, the default) vs the separate
-    # gather kernel: the same bf16 x bf16 products summed in f32 in another order
-    for a, b in zip(geo[("1", "1")], geo[("1", "0")]):
-        sc = float(b.abs().max())
-        assert float((a - b).abs().max()) <= 1e-4 * sc, float((a - b).abs().max()) / sc
-    # and vs the oracle (f32 value, bf16-rounded inputs): grad_loc and grad_attn of the
-    # production kernel (GEOM fused into the band walk)
-    _check_geo_vs_oracle(geo[("1", "1")][0], lr.grad, geo[("1", "1")][1], wr.grad)
-    # the two band skeletons walk the same bands in the same order: grad_loc / grad_attn
-    # bit-identical; grad_value differs only by the order of its f32 atomics
-    for a, b in zip(geo[("s", "1")], geo[("1", "1")]):
+        grads[name] = vd.grad.float().cpu()
+        geo[name] = (ld.grad.cpu(), wd.grad.cpu())
+    # grad_loc / grad_attn fused into the band walk vs the separate gather kernel: the same
+    # bf16 x bf16 products summed in f32 in another order
+    for name in ("tile", "col", "col16"):
+        for a, b in zip(geo[name], geo["tile_sep"]):
+            sc = float(b.abs().max())
+            assert float((a - b).abs().max()) <= 1e-4 * sc, (name, float((a - b).abs().max()) / sc)
+        # and vs the oracle (f32 value, bf16-rounded inputs)
+        _check_geo_vs_oracle(geo[name][0], lr.grad, geo[name][1], wr.grad)
+    # the two band skeletons of the tile kernel walk the same bands in the same order:
+    # grad_loc / grad_attn bit-identical; grad_value differs only by the order of its atomics
+    for a, b in zip(geo["tile_s"], geo["tile"]):
         assert torch.equal(a, b), float((a - b).abs().max())
     scale = float(vr.grad.abs().max())
-    for mf in ("0", "1", "s"):
-        err = (grads[mf] - vr.grad).abs()
+    for name, gv in grads.items():
+        err = (gv - vr.grad).abs()
         bad = err > vr.grad.abs() * 2 ** -8 + 1e-4
-        assert not bool(bad.any()), (mf, float(err.max()), int(bad.sum()), float(vr.grad[bad][0]),
-                                     float(grads[mf][bad][0]))
-    for mf in ("1", "s"):
-        d = (grads[mf] - grads["0"]).abs()
+        assert not bool(bad.any()), (name, float(err.max()), int(bad.sum()), float(vr.grad[bad][0]),
+                                     float(gv[bad][0]))
+    for name in ("tile", "tile_s", "col", "col16"):
+        d = (grads[name] - grads["binned"]).abs()
         # all f32 sums, rounded to bf16 once: within two bf16 ulps, plus f32 summation-order
         # noise (~1e-7 of the summed magnitudes) where contributions cancel to ~0
-        assert bool((d <= grads["0"].abs() * 2 ** -6 + 3e-5 * scale).all()), (mf, float(d.max()))
+        assert bool((d <= grads["binned"].abs() * 2 ** -6 + 3e-5 * scale).all()), (name, float(d.max()))
 
 
 @pytest.mark.parametrize("case", [

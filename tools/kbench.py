@@ -40,7 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="msda,mask,win,xattn")
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--msda-modes", default="mfma,binned,tiled")
+    ap.add_argument("--msda-modes", default="col,prod,binned,tiled")
     a = ap.parse_args()
     dev = "cuda"
     bf = torch.bfloat16
@@ -81,13 +81,18 @@ def main():
                 if mode == "prod" or mode.startswith("skel"):
                     os.environ["VS_MSDA_LDSBAR"] = "127"
                 os.environ["VS_MSDA_SKEL"] = mode[4:] if mode.startswith("skel") else "2"
+                # col: the pyramid-column kernel (default, 8x16 blocks), col16: 16x16 blocks;
+                # every other mode runs the 8 x 8 tile kernel (VS_MSDA_COL=0)
+                os.environ["VS_MSDA_COL"] = {"col": "8x16", "col16": "16x16", "col8": "8x8", "taps4": "8x16"}.get(mode, "0")
+                # taps4: the forward with 4 taps' corner rows in flight (default 2)
+                os.environ["VS_MSDA_FWD_TAPS"] = "4" if mode == "taps4" else "2"
 
                 def fb():
                     o = ops.ms_deform_attn(v, shapes, locr, wr)
                     o.backward(go)
                 run(f"msda {oname} {mode}", fb, a.iters)
-            os.environ.pop("VS_MSDA_RUN")
-            os.environ.pop("VS_MSDA_MFMA")
+            for k in ("VS_MSDA_RUN", "VS_MSDA_MFMA", "VS_MSDA_COL", "VS_MSDA_FWD_TAPS"):
+                os.environ.pop(k)
     if "mask" in a.only:
         Q, C, Hm = 100, 256, 256
         E = torch.randn(B, Q, C, device=dev, generator=g).to(bf).requires_grad_(True)

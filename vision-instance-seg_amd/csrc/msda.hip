@@ -24,6 +24,10 @@
 //     (msda_bwd_kernel, an atomic per corner).
 // vs_msda_backward_tiled is the deterministic, atomic-free variant (grad_value by
 // destination tile, written once in the value dtype; ops VS_MSDA_BWD=tiled).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+
 #include "common.h"
 #include "mfma_util.h"
 
@@ -134,7 +138,7 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ val
 // 32 L and 16 L bytes per group) and the corner rows of two taps at a time are loaded raw
 // (4 VGPRs each) before any is used, so 8 issue back to back instead of one tap's 4
 // (msda_fwd_kernel's runtime-P loop).  Same arithmetic, same order.
-template <int L>
+template <int L, int T>
 __global__ void __launch_bounds__(256) msda_fwd4_kernel(const bf16* __restrict__ value,
                                                          const float* __restrict__ loc,
                                                          const float* __restrict__ attw,
@@ -161,15 +165,22 @@ __global__ void __launch_bounds__(256) msda_fwd4_kernel(const bf16* __restrict__
       const bf16* vl = vb + (size_t)lv.start[l] * rowstride;
       const float fH = (float)Hl, fW = (float)Wl;
       const float4 w4 = wp[l];
+      const float4 lq0 = lp[2 * l], lq1 = lp[2 * l + 1];
+      const float xa[4] = {lq0.x, lq0.z, lq1.x, lq1.z}, ya[4] = {lq0.y, lq0.w, lq1.y, lq1.w};
+      const float aa[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll 1
-      for (int hf = 0; hf < 2; ++hf) {        // two taps (8 corner rows) in flight at a time
-        const float4 lq = lp[2 * l + hf];
-        const float xs[2] = {lq.x, lq.z}, ys[2] = {lq.y, lq.w};
-        const float as[2] = {hf ? w4.z : w4.x, hf ? w4.w : w4.y};
-        uint4 raw[2][4];
-        float cw[2][4];
+      for (int hf = 0; hf < P / T; ++hf) {    // T taps (4T corner rows) in flight at a time
+        float xs[T], ys[T], as[T];
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
+        for (int p = 0; p < T; ++p) {
+          xs[p] = T == P ? xa[p] : (hf ? xa[T + p] : xa[p]);
+          ys[p] = T == P ? ya[p] : (hf ? ya[T + p] : ya[p]);
+          as[p] = T == P ? aa[p] : (hf ? aa[T + p] : aa[p]);
+        }
+        uint4 raw[T][4];
+        float cw[T][4];
+#pragma unroll
+        for (int p = 0; p < T; ++p) {
           const float him = ys[p] * fH - 0.5f;
           const float wim = xs[p] * fW - 0.5f;
           const bool in = him > -1.f && wim > -1.f && him < fH && wim < fW;
@@ -190,7 +201,7 @@ __global__ void __launch_bounds__(256) msda_fwd4_kernel(const bf16* __restrict__
                               : make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
+        for (int p = 0; p < T; ++p) {
           float val[V];
 #pragma unroll
           for (int i = 0; i < V; ++i) val[i] = 0.f;
@@ -1182,6 +1193,289 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
   }
 }
 
+// ---------------------------------------------------------------------------------
+// grad_value + grad_loc / grad_attn by PYRAMID COLUMNS (default for bf16 encoder problems:
+// queries = the value grid, P == 4).  The tile kernel above flushes one f32 atomic row per
+// (8 x 8 query tile, sampled level, touched cell), and a cell is touched by the tiles of
+// every query level whose taps reach it: at the C2 shapes ~4.3 flushes per cell (a cell of
+// the 32 x 32 level is reached by the 16 tiles of the 128 x 128 level above it), 553 MB
+// written per launch for 187 MB of outputs (profiles/r3_pmc_traffic_top.txt).  Float
+// atomics execute memory-side at ~1.3 TB/s of added bytes (MI355X_MICROARCH §Global float
+// atomics), so those flushes bound the kernel.
+// Here a workgroup owns one COLUMN of the pyramid: a CY x CX block of the finest level and
+// the blocks over the same image area at every other level (ColGeo; 8 x 16, 4 x 8, 2 x 4
+// at a 2x pyramid = 168 queries), enumerated largest level first, row-major, in chunks of
+// 64 queries (thread = tap: query tid / 4, point tid % 4, as in the tile kernel).  Per
+// sampled level the union box of the column's corners is walked in bands of <= kBandCap
+// cells; a band's grad_value accumulates over ALL the chunks that reach it in the MFMA
+// accumulators (W[cell][q] x g[q][c], K = one chunk's 64 queries, W in bf16 hi + lo) and
+// is flushed ONCE: 128-B f32 atomic rows per non-zero cell.  grad_loc / grad_attn as in
+// the tile kernel (Dm[q][cell] = g[q] . value[cell] per (band, chunk), the band's value
+// rows loaded once and reused by every chunk, stored transposed over W: 16-B stores); a
+// tap's corner dots stay in registers across bands (dk[chunk][corner]).  Band / chunk pairs are skipped from per-chunk boxes
+// (no vote barrier).  4 LDS-only barriers per pair (W built -> product -> Dm -> dots).
+constexpr int kMsdaColDefault[2] = {0, 0};   // VS_MSDA_COL default (CY, CX); {0, 0}: tile kernel
+
+struct ColGeo {
+  int ty[kMaxLevels], tx[kMaxLevels];    // a column's query block per level (rows, cols)
+  int ord[kMaxLevels];                   // levels in enumeration order (largest first)
+  int ncx, per_image;                    // columns per block row / per image
+};
+
+// MFMA operand (8 k-values of one column, k = rows k0 + 8hh + j, column lane & 31) from a
+// row-major bf16 LDS image, by the gfx950 transposed read (cdna_hip_programming.md T10;
+// EXEC all ones).  64-B row pitch keeps the 16-lane groups in distinct banks.
+__device__ __forceinline__ bf16x8_t tr8(const short* img, int pitch, int k0, int lane) {
+  const int hh = lane >> 5;
+  const int row = k0 + 8 * hh + ((lane & 15) >> 2);
+  const int col = (lane & 16) + 4 * (lane & 3);
+  typedef __attribute__((address_space(3))) bf16x4_t lds_v4;
+  const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + row * pitch + col));
+  const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + (row + 4) * pitch + col));
+  bf16x8_t v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+__device__ __forceinline__ int sgpr(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <int NCH>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 3 ? 3 : 2)))
+msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ attw, const bf16* __restrict__ gout,
+                    const bf16* __restrict__ value, float* __restrict__ gvalue, float* __restrict__ gloc,
+                    float* __restrict__ gattw, Levels lv, ColGeo cg, int S, int Hh, int Q, int L, int nblk) {
+  constexpr int P = 4;
+  __shared__ __attribute__((aligned(16))) short sg[NCH * 64 * kD];   // grad_out rows, column order
+  __shared__ __attribute__((aligned(16))) float sW[kWFloats];        // W of a (band, chunk) / Dm overlay
+  __shared__ int sBox[2][4][NCH][4];                                 // [level parity][wave][chunk] box
+  const int blk = xcd_swizzle(blockIdx.x, nblk);                     // the 8 heads of a column: one XCD
+  const int h = blk % Hh;
+  const int col = (blk / Hh) % cg.per_image;
+  const int b = blk / Hh / cg.per_image;
+  const int cyy = col / cg.ncx, cxx = col - (col / cg.ncx) * cg.ncx;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int tq = tid >> 2, tpt = tid & 3;
+  // this thread's query in every chunk (-1: none)
+  int qid[NCH];
+#pragma unroll
+  for (int s = 0; s < NCH; ++s) qid[s] = -1;
+  int nq = 0;
+  for (int i = 0; i < L; ++i) {
+    const int l = cg.ord[i];
+    const int y0 = cyy * cg.ty[l], x0 = cxx * cg.tx[l];
+    const int ny = min(cg.ty[l], lv.h[l] - y0), nx = min(cg.tx[l], lv.w[l] - x0);
+    if (ny <= 0 || nx <= 0) continue;
+#pragma unroll
+    for (int s = 0; s < NCH; ++s) {
+      const int k = 64 * s + tq - nq;
+      if (k >= 0 && k < ny * nx) qid[s] = lv.start[l] + (y0 + k / nx) * lv.w[l] + x0 + k % nx;
+    }
+    nq += ny * nx;
+  }
+  const int nch = (nq + 63) >> 6;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int s = 0; s < NCH; ++s) {            // grad_out rows: thread = (query, 8-channel part)
+    bf16x8_t v = zero8();
+    if (qid[s] >= 0) v = ld8(gout + (((long long)b * Q + qid[s]) * Hh + h) * kD + tpt * 8);
+    *reinterpret_cast<bf16x8_t*>(sg + (64 * s + tq) * kD + tpt * 8) = v;
+  }
+  for (int i = tid; i < kWFloats / 4; i += 256) reinterpret_cast<float4*>(sW)[i] = z4;
+  __syncthreads();
+
+  const int LP = L * P;
+  const size_t rowstride = (size_t)Hh * kD;
+  const size_t vbase = ((size_t)b * S * Hh + h) * kD;
+  const int zrow = 4 * ((lane >> 2) & 3) + (lane >> 4);   // W clear: 16 rows x 4 quads per wave
+  for (int l = 0; l < L; ++l) {
+    const int Hl = lv.h[l], Wl = lv.w[l];
+    const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
+    float2 xy[NCH];
+    float aw[NCH], dk[NCH][4];
+#pragma unroll
+    for (int s = 0; s < NCH; ++s) {
+      xy[s] = make_float2(0.f, 0.f);
+      aw[s] = 0.f;
+      dk[s][0] = dk[s][1] = dk[s][2] = dk[s][3] = 0.f;
+      if (qid[s] >= 0) {
+        const long long o = (((long long)b * Q + qid[s]) * Hh + h) * LP + l * P + tpt;
+        xy[s] = *reinterpret_cast<const float2*>(loc + o * 2);
+        aw[s] = attw[o];
+      }
+    }
+    // per-chunk boxes of the in-level corners
+    const int par = l & 1;
+#pragma unroll
+    for (int s = 0; s < NCH; ++s) {
+      int ylo = 1 << 30, xlo = 1 << 30, yhi = -1, xhi = -1;
+      if (qid[s] >= 0) {
+        const Tap t = tap_geom(xy[s].x, xy[s].y, Hl, Wl);
+        if (t.inside) {
+          ylo = max(t.h0, 0);
+          yhi = min(t.h0 + 1, Hl - 1);
+          xlo = max(t.w0, 0);
+          xhi = min(t.w0 + 1, Wl - 1);
+        }
+      }
+      const int a = wave_min(ylo), c = wave_max(yhi), d = wave_min(xlo), e = wave_max(xhi);
+      if (lane == 0) {
+        sBox[par][wave][s][0] = a;
+        sBox[par][wave][s][1] = c;
+        sBox[par][wave][s][2] = d;
+        sBox[par][wave][s][3] = e;
+      }
+    }
+    lds_barrier();                            // (sBox is double-buffered by level parity)
+    int cb[NCH][4];
+    int oy = 1 << 30, yh = -1, ox = 1 << 30, xh = -1;
+#pragma unroll
+    for (int s = 0; s < NCH; ++s) {
+      int a = sBox[par][0][s][0], c = sBox[par][0][s][1], d = sBox[par][0][s][2], e = sBox[par][0][s][3];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        a = min(a, sBox[par][w][s][0]);
+        c = max(c, sBox[par][w][s][1]);
+        d = min(d, sBox[par][w][s][2]);
+        e = max(e, sBox[par][w][s][3]);
+      }
+      cb[s][0] = sgpr(a);
+      cb[s][1] = sgpr(c);
+      cb[s][2] = sgpr(d);
+      cb[s][3] = sgpr(e);
+      if (cb[s][1] >= 0) {
+        oy = min(oy, cb[s][0]);
+        yh = max(yh, cb[s][1]);
+        ox = min(ox, cb[s][2]);
+        xh = max(xh, cb[s][3]);
+      }
+    }
+    const int BY = yh < 0 ? 0 : yh - oy + 1, BX = yh < 0 ? 1 : xh - ox + 1;
+    const int SBX = min(BX, kBandCap), SBY = kBandCap / SBX;
+    for (int by0 = 0; by0 < BY; by0 += SBY) {
+      for (int bx0 = 0; bx0 < BX; bx0 += SBX) {
+        const int bw = min(SBX, BX - bx0), bh = min(SBY, BY - by0);
+        const int y0 = oy + by0, x0 = ox + bx0;     // band origin (cells of level l)
+        const int ncell = bw * bh, nmt = (ncell + 31) >> 5;
+        const int zr = nmt * 32;                    // rows W / Dm^T touch
+        bf16x8_t bv0 = zero8(), bv1 = zero8();      // value rows of this wave's cell tile
+        if (wave < nmt) {
+          const int c = 32 * wave + r;
+          if (c < ncell) {
+            const bf16* vr = value + lbase + (size_t)((y0 + c / bw) * Wl + x0 + c % bw) * rowstride + 8 * hh;
+            bv0 = ld8(vr);
+            bv1 = ld8(vr + 16);
+          }
+        }
+        f32x16_t acc;
+        zero16(acc);
+        bool any = false;
+#pragma unroll
+        for (int s = 0; s < NCH; ++s) {
+          if (s >= nch) break;
+          if (cb[s][1] < y0 || cb[s][0] >= y0 + bh || cb[s][3] < x0 || cb[s][2] >= x0 + bw) continue;
+          any = true;
+          int cell[4] = {-1, -1, -1, -1};
+          float cw[4] = {0.f, 0.f, 0.f, 0.f};
+          if (qid[s] >= 0) {
+            const Tap t = tap_geom(xy[s].x, xy[s].y, Hl, Wl);
+            if (t.inside) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int yy = t.h0 + (k >> 1) - y0, xx = t.w0 + (k & 1) - x0;
+                // band cells are inside the level (the box holds in-level corners only)
+                if ((unsigned)yy < (unsigned)bh && (unsigned)xx < (unsigned)bw) cell[k] = yy * bw + xx;
+                cw[k] = ((k >> 1) ? t.lh : t.hh) * ((k & 1) ? t.lw : t.hw) * aw[s];
+              }
+            }
+          }
+#pragma unroll
+          for (int pt = 0; pt < P; ++pt) {    // a query's 4 points are lanes of one wave: take turns
+            if (tpt == pt) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k)
+                if (cell[k] >= 0) sW[cell[k] * kWP8 + tq] += cw[k];
+            }
+            wave_sync();
+          }
+          lds_barrier();
+          if (wave < nmt) {                   // acc[cell][c] += W[cell][q] g[q][c]
+            const short* gs = sg + 64 * s * kD;
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+              const float* wr = sW + (32 * wave + r) * kWP8 + 16 * ks + 8 * hh;
+              const float4 w0 = *reinterpret_cast<const float4*>(wr);
+              const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
+              const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+              bf16x8_t ahi, alo;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const short hb = bf16_bits(wv[j]);
+                ahi[j] = hb;
+                alo[j] = bf16_bits(wv[j] - bf16_bits_to_f32((unsigned short)hb));
+              }
+              const bf16x8_t bq = tr8(gs, kD, 16 * ks, lane);
+              acc = mfma16(ahi, bq, acc);
+              acc = mfma16(alo, bq, acc);
+            }
+          }
+          lds_barrier();                      // W consumed: Dm^T overwrites it
+          float* sD = sW;                     // Dm^T[cell][q], W's layout (pitch kWP8)
+          if (wave < nmt) {                   // Dm[q][cell] = g[q] . value[cell], cell tile = wave
+#pragma unroll
+            for (int mq = 0; mq < 2; ++mq) {
+              const short* ga = sg + (64 * s + 32 * mq + r) * kD + 8 * hh;
+              f32x16_t dm;
+              zero16(dm);
+              dm = mfma16(*reinterpret_cast<const bf16x8_t*>(ga), bv0, dm);
+              dm = mfma16(*reinterpret_cast<const bf16x8_t*>(ga + 16), bv1, dm);
+              // lane = cell 32 wave + r, registers 4i4..4i4+3 = queries 32mq + 8i4 + 4hh + 0..3:
+              // one 16-B store each (pitch 68: a 16-lane group covers all 64 banks once)
+              float* row = sD + (32 * wave + r) * kWP8 + 32 * mq + 4 * hh;
+#pragma unroll
+              for (int i4 = 0; i4 < 4; ++i4)
+                *reinterpret_cast<float4*>(row + 8 * i4) =
+                    make_float4(dm[4 * i4], dm[4 * i4 + 1], dm[4 * i4 + 2], dm[4 * i4 + 3]);
+            }
+          }
+          lds_barrier();
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (cell[k] >= 0) dk[s][k] += sD[cell[k] * kWP8 + tq];
+          lds_barrier();                      // Dm read: clear W for the next pair
+          // each wave clears only the W columns it writes (its 16 queries) over every row W
+          // or Dm^T touched; no other wave's next build touches them (no barrier needed)
+          for (int rb = 0; rb < zr; rb += 16)
+            *reinterpret_cast<float4*>(sW + (rb + zrow) * kWP8 + 16 * wave + 4 * (lane & 3)) = z4;
+        }
+        if (any && wave < nmt) {              // one flush per (band, cell) for the whole column
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int c = 32 * wave + crow(i, hh);
+            if (c < ncell && acc[i] != 0.f)
+              atomicAdd(gvalue + lbase + (size_t)((y0 + c / bw) * Wl + x0 + c % bw) * rowstride + r, acc[i]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NCH; ++s) {           // same formulas as msda_bwd_geom_kernel
+      if (qid[s] < 0) continue;
+      const Tap t = tap_geom(xy[s].x, xy[s].y, Hl, Wl);
+      float r_w = 0.f, r_x = 0.f, r_y = 0.f;
+      if (t.inside) {
+        const float* d = dk[s];
+        r_w = t.hh * t.hw * d[0] + t.hh * t.lw * d[1] + t.lh * t.hw * d[2] + t.lh * t.lw * d[3];
+        r_x = (float)Wl * aw[s] * (-t.hh * d[0] + t.hh * d[1] - t.lh * d[2] + t.lh * d[3]);
+        r_y = (float)Hl * aw[s] * (-t.hw * d[0] - t.lw * d[1] + t.hw * d[2] + t.lw * d[3]);
+      }
+      const long long o = (((long long)b * Q + qid[s]) * Hh + h) * LP + l * P + tpt;
+      gattw[o] = r_w;
+      *reinterpret_cast<float2*>(gloc + o * 2) = make_float2(r_x, r_y);
+    }
+  }
+}
+
 int fill_levels(Levels* lv, const int64_t* shapes, const int64_t* starts, int L, int S) {
   long long tot = 0;
   for (int l = 0; l < L; ++l) {
@@ -1216,11 +1510,18 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
   const int block = 256;
   bool unrolled = P == 4;                    // VS_MSDA_FWD4=0: the runtime-P kernel
   if (const char* e = getenv("VS_MSDA_FWD4")) unrolled = unrolled && atoi(e) != 0;
+  // VS_MSDA_FWD_TAPS: taps whose corner rows are in flight together (2 default, or 4)
+  int taps = 2;
+  if (const char* e = getenv("VS_MSDA_FWD_TAPS")) taps = atoi(e) == 4 ? 4 : 2;
   if (dtype == VS_BF16 && unrolled) {
     int grid = grid_for(groups * 4, block, 256 * 64);
 #define VS_FWD4(LL)                                                                                          \
-  hipLaunchKernelGGL((msda_fwd4_kernel<LL>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, \
-                     attw, (bf16*)out, lv, S, Hh, Q, groups)
+  if (taps == 4)                                                                                           \
+    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 4>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, \
+                       attw, (bf16*)out, lv, S, Hh, Q, groups);                                            \
+  else                                                                                                     \
+    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, \
+                       attw, (bf16*)out, lv, S, Hh, Q, groups)
     switch (L) {
       case 1: VS_FWD4(1); break;
       case 2: VS_FWD4(2); break;
@@ -1254,6 +1555,40 @@ static void launch_geom(int dtype, const void* value, const float* loc, const fl
   else
     hipLaunchKernelGGL(msda_bwd_geom_kernel<float>, dim3(ggrid), dim3(256), 0, st, (const float*)value, loc, attw,
                        (const float*)gout, gloc, gattw, lv, S, Hh, Q, L, P, groups);
+}
+
+// Pyramid columns (msda_bwd_col_kernel): the finest level's CY x CX block and, at a level
+// 2^k times coarser, CY >> k x CX >> k (>= 1).  Every level's blocks tile it (ncy / ncx =
+// the most blocks any level needs), so each query is in exactly one column.  Returns the
+// chunks of 64 queries a column needs (0: more than 6, use the tile kernel).
+static int col_geo(const Levels& lv, int L, int CY, int CX, ColGeo* cg) {
+  int f = 0;
+  for (int l = 1; l < L; ++l)
+    if ((long long)lv.h[l] * lv.w[l] > (long long)lv.h[f] * lv.w[f]) f = l;
+  int ncy = 1, ncx = 1, nq = 0;
+  for (int l = 0; l < kMaxLevels; ++l) {
+    cg->ty[l] = cg->tx[l] = 1;
+    cg->ord[l] = l;
+  }
+  for (int l = 0; l < L; ++l) {
+    const int sy = std::min(30, std::max(0, (int)std::lround(std::log2((double)lv.h[f] / lv.h[l]))));
+    const int sx = std::min(30, std::max(0, (int)std::lround(std::log2((double)lv.w[f] / lv.w[l]))));
+    cg->ty[l] = std::max(1, CY >> sy);
+    cg->tx[l] = std::max(1, CX >> sx);
+    ncy = std::max(ncy, (lv.h[l] + cg->ty[l] - 1) / cg->ty[l]);
+    ncx = std::max(ncx, (lv.w[l] + cg->tx[l] - 1) / cg->tx[l]);
+    nq += cg->ty[l] * cg->tx[l];
+  }
+  for (int i = 1; i < L; ++i)                 // largest level first (stable)
+    for (int j = i; j > 0; --j) {
+      const int a = cg->ord[j - 1], c = cg->ord[j];
+      if ((long long)lv.h[c] * lv.w[c] > (long long)lv.h[a] * lv.w[a]) std::swap(cg->ord[j - 1], cg->ord[j]);
+      else break;
+    }
+  cg->ncx = ncx;
+  cg->per_image = ncy * ncx;
+  const int nch = (nq + 63) / 64;
+  return nch <= 6 ? nch : 0;
 }
 
 static int msda_backward_impl(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
@@ -1301,7 +1636,24 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     // at every band start)
     int skel = kMsdaSkelDefault;
     if (const char* e = getenv("VS_MSDA_SKEL")) skel = atoi(e);
-    if (mfma && fused && skel == 2)
+    // VS_MSDA_COL: the pyramid-column kernel's block at the finest level, "CYxCX" (8x16: 3
+    // chunks; 16x16 takes the 6-chunk build); 0 (default until measured on the box): the
+    // 8 x 8 tile kernel
+    int ccy = kMsdaColDefault[0], ccx = kMsdaColDefault[1];
+    if (const char* e = getenv("VS_MSDA_COL")) {
+      if (sscanf(e, "%dx%d", &ccy, &ccx) != 2) ccy = ccx = atoi(e);
+    }
+    ColGeo cg;
+    const int nch = ccy > 0 && ccx > 0 ? col_geo(lv, L, ccy, ccx, &cg) : 0;
+    const long long nbc = nch > 0 ? (long long)B * cg.per_image * Hh : 0;
+    if (mfma && fused && bt.mode == 1 && nch > 0 && nbc < (1LL << 31)) {
+      if (nch <= 3)
+        hipLaunchKernelGGL((msda_bwd_col_kernel<3>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,
+                           (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc);
+      else
+        hipLaunchKernelGGL((msda_bwd_col_kernel<6>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,
+                           (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc);
+    } else if (mfma && fused && skel == 2)
       hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true, 2>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
                          (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc, gattw,
                          lbmask);
