@@ -557,20 +557,6 @@ def test_msda_carry_backward_vs_oracle(monkeypatch, run, win, jitter):
     np.testing.assert_allclose(ld.grad.cpu().numpy(), gl, atol=2e-5 * max(1.0, np.abs(gl).max()), rtol=0)
 
 
-@pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(9, 13), (18, 26), (35, 51), (5, 7)]])
-def test_msda_forward_taps_in_flight_bit_identical(monkeypatch, shapes):
-    """The P = 4 forward with 4 taps' corner rows in flight (VS_MSDA_FWD_TAPS=4) does the same
-    arithmetic in the same order as the default 2: bit-identical outputs, incl. taps outside."""
-    ops = _ops()
-    value, loc, w = _encoder_like_inputs(1, shapes, 8, 4, seed=21, jitter=3.0)
-    vd, ld, wd = value.to(torch.bfloat16).to(DEV), loc.to(DEV), w.to(DEV)
-    outs = []
-    for taps in ("2", "4"):
-        monkeypatch.setenv("VS_MSDA_FWD_TAPS", taps)
-        outs.append(ops.ms_deform_attn(vd, shapes, ld, wd))
-    assert torch.equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("win", ["tile", "tile-1024", "tile-odd", "sub", "4lvl", "ragged", "wide"])
 @pytest.mark.parametrize("jitter", [0.0, 0.3, 3.0, 12.0])
 def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):

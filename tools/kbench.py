@@ -83,15 +83,13 @@ def main():
                 os.environ["VS_MSDA_SKEL"] = mode[4:] if mode.startswith("skel") else "2"
                 # col: the pyramid-column kernel (default, 8x16 blocks), col16: 16x16 blocks;
                 # every other mode runs the 8 x 8 tile kernel (VS_MSDA_COL=0)
-                os.environ["VS_MSDA_COL"] = {"col": "8x16", "col16": "16x16", "col8": "8x8", "taps4": "8x16"}.get(mode, "0")
-                # taps4: the forward with 4 taps' corner rows in flight (default 2)
-                os.environ["VS_MSDA_FWD_TAPS"] = "4" if mode == "taps4" else "2"
+                os.environ["VS_MSDA_COL"] = {"col": "8x16", "col16": "16x16", "col8": "8x8"}.get(mode, "0")
 
                 def fb():
                     o = ops.ms_deform_attn(v, shapes, locr, wr)
                     o.backward(go)
                 run(f"msda {oname} {mode}", fb, a.iters)
-            for k in ("VS_MSDA_RUN", "VS_MSDA_MFMA", "VS_MSDA_COL", "VS_MSDA_FWD_TAPS"):
+            for k in ("VS_MSDA_RUN", "VS_MSDA_MFMA", "VS_MSDA_COL"):
                 os.environ.pop(k)
     if "mask" in a.only:
         Q, C, Hm = 100, 256, 256

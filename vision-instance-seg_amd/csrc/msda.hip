@@ -137,7 +137,8 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ val
 // sampling locations and weights arrive as three 16-B loads (the rows are 16-B aligned:
 // 32 L and 16 L bytes per group) and the corner rows of two taps at a time are loaded raw
 // (4 VGPRs each) before any is used, so 8 issue back to back instead of one tap's 4
-// (msda_fwd_kernel's runtime-P loop).  Same arithmetic, same order.
+// (msda_fwd_kernel's runtime-P loop).  Same arithmetic, same order.  T = 4 (a level's 16
+// corner rows in flight) measured slower: 0.167 vs 0.156 ms at the C2 encoder shape.
 template <int L, int T>
 __global__ void __launch_bounds__(256) msda_fwd4_kernel(const bf16* __restrict__ value,
                                                          const float* __restrict__ loc,
@@ -1214,7 +1215,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
 // rows loaded once and reused by every chunk, stored transposed over W: 16-B stores); a
 // tap's corner dots stay in registers across bands (dk[chunk][corner]).  Band / chunk pairs are skipped from per-chunk boxes
 // (no vote barrier).  4 LDS-only barriers per pair (W built -> product -> Dm -> dots).
-constexpr int kMsdaColDefault[2] = {0, 0};   // VS_MSDA_COL default (CY, CX); {0, 0}: tile kernel
+constexpr int kMsdaColDefault[2] = {8, 16};  // VS_MSDA_COL default (CY, CX); {0, 0}: tile kernel
 
 struct ColGeo {
   int ty[kMaxLevels], tx[kMaxLevels];    // a column's query block per level (rows, cols)
@@ -1510,18 +1511,11 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
   const int block = 256;
   bool unrolled = P == 4;                    // VS_MSDA_FWD4=0: the runtime-P kernel
   if (const char* e = getenv("VS_MSDA_FWD4")) unrolled = unrolled && atoi(e) != 0;
-  // VS_MSDA_FWD_TAPS: taps whose corner rows are in flight together (2 default, or 4)
-  int taps = 2;
-  if (const char* e = getenv("VS_MSDA_FWD_TAPS")) taps = atoi(e) == 4 ? 4 : 2;
   if (dtype == VS_BF16 && unrolled) {
     int grid = grid_for(groups * 4, block, 256 * 64);
 #define VS_FWD4(LL)                                                                                          \
-  if (taps == 4)                                                                                           \
-    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 4>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, \
-                       attw, (bf16*)out, lv, S, Hh, Q, groups);                                            \
-  else                                                                                                     \
-    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, \
-                       attw, (bf16*)out, lv, S, Hh, Q, groups)
+  hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, \
+                     attw, (bf16*)out, lv, S, Hh, Q, groups)
     switch (L) {
       case 1: VS_FWD4(1); break;
       case 2: VS_FWD4(2); break;
@@ -1636,9 +1630,8 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     // at every band start)
     int skel = kMsdaSkelDefault;
     if (const char* e = getenv("VS_MSDA_SKEL")) skel = atoi(e);
-    // VS_MSDA_COL: the pyramid-column kernel's block at the finest level, "CYxCX" (8x16: 3
-    // chunks; 16x16 takes the 6-chunk build); 0 (default until measured on the box): the
-    // 8 x 8 tile kernel
+    // VS_MSDA_COL: the pyramid-column kernel's block at the finest level, "CYxCX" (default
+    // 8x16: 3 chunks; 16x16 takes the 6-chunk build); 0: the 8 x 8 tile kernel
     int ccy = kMsdaColDefault[0], ccx = kMsdaColDefault[1];
     if (const char* e = getenv("VS_MSDA_COL")) {
       if (sscanf(e, "%dx%d", &ccy, &ccx) != 2) ccy = ccx = atoi(e);

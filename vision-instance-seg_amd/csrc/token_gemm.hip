@@ -211,7 +211,52 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
     }
   }
 
-  // ---- epilogue: lane = token, registers = 4 groups of 4 consecutive features
+  if (EPI < 2 && N % 8 == 0) {
+    // ---- epilogue through LDS: the accumulators are 8-byte pieces of 32 token rows per
+    // store instruction (32 lines touched for 512 B); staged in LDS as the [BM][BN] bf16
+    // output tile (16-B chunks XOR-swizzled by row & 15: the 8-B writes of 16 rows and the
+    // row-contiguous 16-B reads are conflict-free) and stored 16 B a lane, 256 B per row
+    // segment (whole 128-B lines).  bias, then GELU: pass 0 writes y, pass 1 (GELU) y_pre.
+    constexpr int NCK = BN / 8;                        // 16-B chunks per tile row
+    auto so_off = [](int row, int chunk) { return row * (BN * 2) + ((chunk ^ (row & 15)) << 4); };
+    raw_barrier();                                     // every wave is done with the staging buffers
+#pragma unroll 1
+    for (int pass = 0; pass < (EPI >= 1 ? 2 : 1); ++pass) {
+#pragma unroll
+      for (int b = 0; b < TM; ++b) {
+        const int row = xrow(b);
+#pragma unroll
+        for (int a = 0; a < TN; ++a) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int f = wn * TN * 32 + a * 32 + 8 * g + 4 * hh, n = n0 + f;
+            const bf16x4_t bv = (bias && n < N) ? *reinterpret_cast<const bf16x4_t*>(bias + n) : bf16x4_t{0, 0, 0, 0};
+            bf16x4_t o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const short pre = bf16_bits(acc[a][b][4 * g + e] + bf16_bits_to_f32((unsigned short)bv[e]));
+              // GELU of the ROUNDED pre-activation: the value the backward (and an unfused
+              // bf16 F.gelu) sees
+              o[e] = (EPI >= 1 && pass == 0) ? (short)gelu_bits((unsigned short)pre, sgelu) : pre;
+            }
+            *reinterpret_cast<bf16x4_t*>(smem + so_off(row, f >> 3) + (f & 7) * 2) = o;
+          }
+        }
+      }
+      raw_barrier();
+      bf16* out = pass == 0 ? Y : Y2;
+      for (int idx = threadIdx.x; idx < BM * NCK; idx += NT) {
+        const int row = idx / NCK, chunk = idx - (idx / NCK) * NCK;
+        const int m = m0 + row, n = n0 + chunk * 8;
+        if (m < M && n < N)
+          *reinterpret_cast<uint4*>(out + (size_t)m * N + n) = *reinterpret_cast<const uint4*>(smem + so_off(row, chunk));
+      }
+      if (EPI >= 1 && pass == 0) raw_barrier();      // the tile is rewritten by pass 1
+    }
+    return;
+  }
+  // ---- direct epilogue (N % 8 != 0, or the MX fp8 output): lane = token, registers = 4
+  // groups of 4 consecutive features
 #pragma unroll
   for (int b = 0; b < TM; ++b) {
     const int m = m0 + xrow(b);
