@@ -15,6 +15,8 @@ The backward is the gradient of the quantised logits with straight-through opera
 (dV, dP, dQ, dK formed in bf16 from the bf16 operands); its yardstick is that formula in
 f32 and, loosely, the exact fp32 autograd gradient."""
 
+import math
+
 import pytest
 import torch
 
@@ -254,3 +256,65 @@ def test_swin_l_fp8_model_vs_oracle():
           f"fp8 attention max {res[True][0]:.2e} mean {res[True][1]:.2e}")
     assert res[True][0] <= max(2.5 * res[False][0], 0.02) and res[True][1] <= max(2.5 * res[False][1], 3e-3)
     assert res[True][0] <= 0.08 and res[True][1] <= 0.01
+
+
+def test_swin_l_fp8_linears_model_vs_oracle_and_step():
+    """Config C5's fp8 Linears (M2FConfig.linear_fp8: qkv / proj / fc1 / fc2 on the MX fp8
+    token GEMM where K >= 384, the norms and fc1's GELU epilogue handing over e4m3 + scales,
+    straight-through bf16 weight gradients), alone and with fp8 window attention, vs the
+    fp32 oracle at 384^2 with the oracle's attention masks forced in (Swin-L's stage 1 is
+    192 wide: its block stays bf16 except the 768-deep fc2).  Yardstick: the all-bf16 model.
+    Caps: max 0.15 / mean 0.02 of the step's max |logit| (twice the fp8-attention caps:
+    e4m3 operands in every K-deep product of the backbone; the per-GEMM error budget is
+    tests/test_gpu_tgemm.py's).  Then one training step with fp8 Linears through the
+    Trainer: finite loss and gradients, weights move."""
+    from visionseg.criterion import SetCriterion
+    from visionseg.data import synthetic_batch
+    from visionseg.model import M2FConfig, Mask2Former
+    from visionseg.train import SolverConfig, Trainer
+    from oracle.ref_model import RefConfig, RefMask2Former
+    cfg = M2FConfig.preset("swin_l", num_queries=100)
+    m = Mask2Former(cfg).init_weights(0)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "rel_table" in n or "attention_weights" in n or "level_embed" in n:
+                p.add_(0.3 * torch.randn(p.shape, generator=g))
+        for p in m.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    ref = RefMask2Former(RefConfig.from_dict(cfg.to_dict()))
+    ref.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
+    ref.eval()
+    px = torch.randn(1, 3, 384, 384, generator=torch.Generator().manual_seed(5)).to(torch.bfloat16).float()
+    with torch.no_grad():
+        ref.decoder.record = True
+        rmasks, _ = ref(px)
+        forced = [rb for rb, _ in ref.decoder.trace]
+        m = m.to(DEV).to(torch.bfloat16).eval()
+        m.decoder.mask_override = forced
+        res = {}
+        for mode in ("bf16", "linear_fp8", "all_fp8"):
+            for st in m.backbone.stages:
+                for blk in st.blocks:
+                    blk.linear_fp8 = blk.mlp.fp8 = mode != "bf16"
+                    blk.attn_fp8 = mode == "all_fp8"
+            masks, _ = m(px.to(DEV).to(torch.bfloat16))
+            wmax = max(float((a.float().cpu() - b).abs().max()) / float(b.abs().max()) for a, b in zip(masks, rmasks))
+            wmean = max(float((a.float().cpu() - b).abs().mean()) / float(b.abs().max()) for a, b in zip(masks, rmasks))
+            res[mode] = (wmax, wmean)
+    print("swin_l@384 mask logits vs fp32 oracle (max, mean of max|logit|): "
+          + ", ".join(f"{k} {v[0]:.2e} / {v[1]:.2e}" for k, v in res.items()))
+    for mode in ("linear_fp8", "all_fp8"):
+        assert res[mode][0] <= 0.15 and res[mode][1] <= 0.02, (mode, res)
+    del m
+    torch.cuda.empty_cache()
+    cfg8 = M2FConfig.preset("swin_l", linear_fp8=True)
+    tr = Trainer(Mask2Former(cfg8).init_weights(0), SetCriterion(cfg8), SolverConfig(warmup_iters=0), device=DEV)
+    assert any(b.linear_fp8 and b.mlp.fp8 for st in tr.model.backbone.stages for b in st.blocks)
+    batch = synthetic_batch(2, 384, seed=42, device=DEV)
+    w0 = tr.opt.master.clone()
+    losses = [float(tr.step(*batch)) for _ in range(2)]
+    torch.cuda.synchronize()
+    print("swin_l@384 fp8-Linear training losses", losses)
+    assert all(math.isfinite(v) for v in losses)
+    assert bool(torch.isfinite(tr.opt.master).all()) and float((tr.opt.master - w0).abs().max()) > 0

@@ -156,18 +156,19 @@ class SwinBlock(nn.Module):
         # the window partition folded into the norm's stores (ops.WindowRows): h comes out
         # in the window layout [B*nW*ws^2, C], padding rows zero
         wr = ops.window_rows(B, H, W, ws, shift, x.device)
-        if self.linear_fp8:
+        q8 = self.linear_fp8 and fp8_operand_ok(C)   # the Linears over C features take the MX fp8 path
+        if q8:
             # the norms also write their output as the fp8 GEMM operand (no quantisation pass)
             if res is None:
-                h, hq = self.norm1.forward_windows(x, wr, quant=fp8_operand_ok(C))
+                h, hq = self.norm1.forward_windows(x, wr, quant=True)
             else:
-                x, h, hq = self.norm1.add_forward_windows(x, res, wr, quant=fp8_operand_ok(C))
+                x, h, hq = self.norm1.add_forward_windows(x, res, wr, quant=True)
             qkv = linear_fp8_tokens(h.view(-1, ws * ws, C), self.attn.qkv.weight, self.attn.qkv.bias, hq)
         elif res is None:
             h = self.norm1.forward_windows(x, wr)
         else:
             x, h = self.norm1.add_forward_windows(x, res, wr)
-        if not self.linear_fp8:
+        if not q8:
             qkv = self.attn.qkv(h.view(-1, ws * ws, C))
         # output in the image layout (window reverse folded into the kernel); the per-token
         # proj commutes with the crop
@@ -177,8 +178,8 @@ class SwinBlock(nn.Module):
             o = linear_fp8_tokens(o.view(B, H * W, C), self.attn.proj.weight, self.attn.proj.bias)
         else:
             o = self.attn.proj(o.view(B, H * W, C))
-        if self.linear_fp8:
-            x, h2, h2q = self.norm2.add_forward(x, o, quant=fp8_operand_ok(C))
+        if q8:
+            x, h2, h2q = self.norm2.add_forward(x, o, quant=True)
             return x, self.mlp(h2, h2q)
         x, h2 = self.norm2.add_forward(x, o)
         return x, self.mlp(h2)
