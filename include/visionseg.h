@@ -258,6 +258,15 @@ VS_API int vs_mask_head_backward_ex(int dtype, const float* grad_logits, const v
                                     void* grad_P, void* workspace, int batch, int num_queries, int channels,
                                     int height, int width, int accumulate_grad_P, void* stream);
 
+/* vs_mask_head_forward (bf16, C in {128, 256}) with the logits rows stored in groups of
+ * `group` rows: row (b, q) of the product goes to row ((q / group) * B + b) * group +
+ * q % group of logits [Q / group, B, group, H*W] (Q % group == 0, Q * group < 2^20).
+ * With E = the matched (step, target) embeddings of S steps x group targets per image
+ * this writes the matched maps in (step, image, target) order from one launch. */
+VS_API int vs_mask_head_forward_grouped(const void* mask_embed, const void* pixel_embed_nhwc, float* logits,
+                                        int batch, int num_query, int channels, int height, int width, int group,
+                                        void* stream);
+
 /* Adjoint of the mask losses' point sampling (point_sample = grid_sample bilinear,
  * align_corners=False, zero padding; HF:m2f:245-275) for the matched (step, image, target)
  * pairs: grad_points f32 [S*B*K, n] (pair order (s, b, k)), grid f32 [S*B*K, n, 2] (the
@@ -425,6 +434,40 @@ VS_API int vs_match_cost(const float* const* mask_logits, int num_steps, const f
                          const float* target_point_labels, float* cost, int batch, int num_queries, int height,
                          int width, int num_points, int max_targets, float mask_weight, float class_weight,
                          float dice_weight, void* stream);
+
+/* ---- Matcher from the mask head's factors (csrc/match_factors.hip) -------------------
+ * The logits L_s[b, q, n] = E_s[b, q, :] . F[b, n, :] are never materialised at full
+ * resolution for matching: bilinear resampling commutes with the product.
+ * vs_feature_resize_hilo: F bf16 [B, H*W, C] -> out bf16 [B, th*tw, 2C], the bilinear
+ *   (align_corners=False, PyTorch upsample_bilinear2d index rule) resize of F in f32 stored
+ *   as hi = bf16(v) in channels [0, C) and lo = bf16(v - hi) in [C, 2C) (E . (hi + lo) =
+ *   the resized logits to ~2^-17 relative; HF:m2f:2049-2055 resizes the logits).
+ * vs_feature_sample_hilo: F at grid points f32 [B, P, 2] in [-1, 1] (grid_sample bilinear,
+ *   zeros padding, align_corners=False; HF:m2f:245-275) -> out bf16 [B, P, 2C] (hi | lo).
+ * vs_match_cost_factors: E bf16 [S, B, Q, C] (C in {64, 128, 256}), point_features from
+ *   vs_feature_sample_hilo at the matcher's points, class_probs f32 [S, B, Q, C+1],
+ *   target_classes int64 [B, Kc], target_point_labels f32 [B, Kc, P] -> cost f32
+ *   [S, B, Q, Kc], the same cost as vs_match_cost over the logits E_s . F (HF:m2f:434-481).
+ *   workspace: vs_match_cost_factors_workspace_bytes(S, B, Q, P, Kc) bytes of device
+ *   scratch (per-point-range partial sums, reduced in a fixed order: deterministic). */
+/* vs_level_bitmask_hilo: the attention bitmask (vs_attn_bitmask's format and rule,
+ *   sigmoid(x) < 0.5 with the all-blocked row fix) of the logits E . (hi + lo) at a level of
+ *   height x width keys, from E bf16 [B, Q, C] and level_features = vs_feature_resize_hilo's
+ *   output [B, height*width, 2C]: words u32 [B, Q, ceil(height*width/32)]; the logits are
+ *   never stored. */
+VS_API int vs_level_bitmask_hilo(const void* mask_embed, const void* level_features, uint32_t* words, int batch,
+                                 int num_queries, int channels, int height, int width, void* stream);
+VS_API int vs_feature_resize_hilo(const void* features, void* out, int batch, int height, int width, int channels,
+                                  int target_h, int target_w, void* stream);
+VS_API int vs_feature_sample_hilo(const void* features, const float* grid, void* out, int batch, int height,
+                                  int width, int channels, int num_points, void* stream);
+VS_API long long vs_match_cost_factors_workspace_bytes(int num_steps, int batch, int num_queries, int num_points,
+                                                       int max_targets);
+VS_API int vs_match_cost_factors(const void* mask_embed, const void* point_features, int num_steps,
+                                 const float* class_probs, int num_classes_plus1, const long long* target_classes,
+                                 const float* target_point_labels, float* cost, void* workspace, int batch,
+                                 int num_queries, int channels, int num_points, int max_targets, float mask_weight,
+                                 float class_weight, float dice_weight, void* stream);
 
 VS_API int vs_lsa_batch_device_counts(const float* cost, const int* targets_per_image_dev, int num_steps,
                                       int batch, int num_queries, int max_targets, int* assign, void* stream);

@@ -1,0 +1,214 @@
+"""Matcher cost and attention masks from the mask head's factors (csrc/match_factors.hip,
+ops.FactoredLogits) vs the full-resolution path they replace: the torch formulation of
+HF:m2f:413-481 / 2049-2055 on the materialised logits E . F, and the set criterion run on
+materialised logits (same matching, losses and factor gradients)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ops():
+    from visionseg import ops
+    return ops
+
+
+def _logits(E, Fm, H, W):
+    """f32 logits [.., Q, H, W] of bf16 factors E [..., B, Q, C], F [B, H*W, C] (exact products)."""
+    L = torch.einsum("...bqc,bnc->...bqn", E.double(), Fm.double())
+    return L.reshape(*L.shape[:-1], H, W)
+
+
+@pytest.mark.parametrize("B,H,W,C,th,tw", [(2, 64, 64, 256, 8, 8), (1, 64, 48, 64, 32, 24), (2, 40, 56, 128, 16, 28),
+                                           (1, 30, 50, 64, 11, 7)])
+def test_feature_resize_hilo_vs_interpolate(B, H, W, C, th, tw):
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(H + th)
+    Fm = (torch.randn(B, H * W, C, device=DEV, generator=g) * 2).to(torch.bfloat16)
+    out = ops.feature_resize_hilo(Fm, H, W, th, tw)
+    hi, lo = out[..., :C].float(), out[..., C:].float()
+    ref = F.interpolate(Fm.float().view(B, H, W, C).permute(0, 3, 1, 2), size=(th, tw), mode="bilinear",
+                        align_corners=False).permute(0, 2, 3, 1).reshape(B, th * tw, C)
+    assert torch.equal(hi, hi.to(torch.bfloat16).float())
+    assert float((hi + lo - ref).abs().max()) <= 2.0 ** -16 * float(ref.abs().max())
+    assert float((hi - ref).abs().max()) <= 2.0 ** -8 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("B,H,W,C,P", [(2, 64, 64, 256, 3000), (1, 33, 47, 64, 777)])
+def test_feature_sample_hilo_vs_grid_sample(B, H, W, C, P):
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(P)
+    Fm = torch.randn(B, H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    grid = torch.rand(B, P, 2, device=DEV, generator=g) * 2.2 - 1.1        # some outside: zero padding
+    out = ops.feature_sample_hilo(Fm, H, W, grid)
+    ref = F.grid_sample(Fm.float().view(B, H, W, C).permute(0, 3, 1, 2), grid.unsqueeze(2),
+                        align_corners=False).squeeze(3).transpose(1, 2)
+    v = out[..., :C].float() + out[..., C:].float()
+    assert float((v - ref).abs().max()) <= 2.0 ** -16 * float(ref.abs().max())
+
+
+def _torch_cost(Lmaps, probs, tcls, pts, tp, wm, wc, wd):
+    """HF:m2f:413-481 on materialised logits [S, B, Q, H, W] (float64)."""
+    S, B, Q = Lmaps.shape[:3]
+    Kc, P = tp.shape[1], tp.shape[2]
+    pp = torch.stack([F.grid_sample(Lmaps[s], pts.double().unsqueeze(2), align_corners=False).squeeze(3)
+                      for s in range(S)])
+    tpt = tp.double().transpose(1, 2)[None]
+    cm = torch.matmul(F.softplus(-pp) / P, tpt) + torch.matmul(F.softplus(pp) / P, 1 - tpt)
+    sg = pp.sigmoid()
+    cd = 1 - (2 * torch.matmul(sg, tpt) + 1) / (sg.sum(-1)[..., None] + tp.double().sum(-1)[None, :, None, :] + 1)
+    cc = -torch.gather(probs.double(), 3, tcls[None, :, None, :].expand(S, B, Q, Kc))
+    return wm * cm + wc * cc + wd * cd
+
+
+@pytest.mark.parametrize("S,B,Q,C,Kc,H,W,P", [(10, 2, 100, 256, 16, 64, 64, 12544), (3, 2, 37, 64, 3, 32, 48, 1000),
+                                               (1, 1, 20, 128, 1, 40, 40, 777), (4, 3, 100, 256, 8, 48, 64, 4097),
+                                               (2, 1, 300, 256, 5, 32, 32, 33)])
+def test_match_cost_factors_vs_torch(S, B, Q, C, Kc, H, W, P):
+    """Cost from the factors vs the torch formulation over the materialised logits (f64), and
+    vs the full-resolution kernel (csrc/match.hip) over the f32 logits: the same numbers up to
+    the f32 summation order."""
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(S * 100 + Q + Kc)
+    E = (torch.randn(S, B, Q, C, device=DEV, generator=g) * (2.0 / C ** 0.5)).to(torch.bfloat16)
+    Fm = torch.randn(B, H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    probs = torch.softmax(torch.randn(S, B, Q, 4, device=DEV, generator=g), -1)
+    tcls = torch.randint(0, 4, (B, Kc), device=DEV, generator=g)
+    pts = torch.rand(B, P, 2, device=DEV, generator=g) * 2.1 - 1.05
+    tmask = (torch.rand(B, Kc, 2 * H, 2 * W, device=DEV, generator=g) > 0.6).float()
+    tp = F.grid_sample(tmask, pts.unsqueeze(2), align_corners=False).squeeze(3)
+    fp = ops.feature_sample_hilo(Fm, H, W, pts)
+    got = ops.match_cost_factors(E, fp, probs, tcls, tp, 5.0, 2.0, 5.0)
+    Lm = _logits(E, Fm, H, W)
+    exp = _torch_cost(Lm, probs, tcls, pts, tp, 5.0, 2.0, 5.0)
+    err = float((got.double() - exp).abs().max())
+    print(f"match_cost_factors S{S} B{B} Q{Q} C{C} Kc{Kc} P{P}: max|err| vs f64 {err:.2e}")
+    assert err <= 2e-5
+    full = ops.match_cost([Lm[s].float() for s in range(S)], probs, tcls, pts, tp, 5.0, 2.0, 5.0)
+    assert float((got - full).abs().max()) <= 3e-5
+
+
+def test_match_cost_factors_assignment_equals_full_resolution():
+    """The device Hungarian matching on the factor cost equals the matching on the
+    full-resolution kernel's cost (a C2-shaped problem, random factors)."""
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    S, B, Q, C, Kc, H, W, P = 10, 4, 100, 256, 12, 64, 64, 12544
+    E = (torch.randn(S, B, Q, C, device=DEV, generator=g) * 0.15).to(torch.bfloat16)
+    Fm = torch.randn(B, H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    probs = torch.softmax(torch.randn(S, B, Q, 3, device=DEV, generator=g), -1)
+    tcls = torch.randint(0, 3, (B, Kc), device=DEV, generator=g)
+    pts = torch.rand(B, P, 2, device=DEV, generator=g) * 2 - 1
+    tmask = (torch.rand(B, Kc, 16, 16, device=DEV, generator=g) > 0.5).float()
+    tmask = F.interpolate(tmask, size=(4 * H, 4 * W), mode="nearest")
+    tp = F.grid_sample(tmask, pts.unsqueeze(2), align_corners=False).squeeze(3)
+    counts = torch.tensor([12, 5, 0, 9], dtype=torch.int32, device=DEV)
+    a = ops.linear_sum_assignment_padded(
+        ops.match_cost_factors(E, ops.feature_sample_hilo(Fm, H, W, pts), probs, tcls, tp, 5.0, 2.0, 5.0), counts)
+    Lm = _logits(E, Fm, H, W).float()
+    b = ops.linear_sum_assignment_padded(ops.match_cost([Lm[s] for s in range(S)], probs, tcls, pts, tp, 5.0, 2.0,
+                                                        5.0), counts)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("S,B,Kc,C", [(10, 2, 16, 256), (3, 3, 5, 128), (1, 1, 1, 256)])
+def test_mask_head_grouped_rows(S, B, Kc, C):
+    """Grouped stores: row (b, s*Kc + k) of E . F lands at [s, b, k], bit-identical to the
+    plain kernel's logits."""
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(S + Kc)
+    H, W = 48, 40
+    E = torch.randn(B, S * Kc, C, device=DEV, generator=g).to(torch.bfloat16)
+    Fm = torch.randn(B, H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    got = ops.mask_head_grouped(E, Fm, H, W, Kc)                         # [S, B, Kc, H, W]
+    with torch.no_grad():
+        ref = ops.mask_head(E, Fm, H, W).view(B, S, Kc, H, W).transpose(0, 1)
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("H,W,th,tw", [(256, 256, 32, 32), (256, 256, 128, 128), (96, 160, 24, 40), (60, 84, 15, 21)])
+def test_level_mask_from_factors(H, W, th, tw):
+    """Attention bitmask from E . resize(F) (hi | lo pair) vs the bitmask of the resized
+    full-resolution logits (HF:m2f:2049-2055): identical except keys whose logit is within
+    f32 rounding of the threshold."""
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(th)
+    B, Q, C = 2, 100, 256
+    E = (torch.randn(B, Q, C, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    Fm = torch.randn(B, H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    lv = ops.feature_resize_hilo(Fm, H, W, th, tw)
+    with torch.no_grad():
+        got = ops.level_bitmask_hilo(E, lv, th, tw)
+        via = ops.attn_bitmask(ops.mask_head(torch.cat([E, E], -1), lv, th, tw), (th, tw))
+        full = ops.mask_head(E, Fm, H, W)
+        exp = ops.attn_bitmask(full, (th, tw))
+    rz = F.interpolate(full, size=(th, tw), mode="bilinear", align_corners=False).reshape(B, Q, -1)
+    diff = ops.unpack_bitmask(got ^ exp, th * tw)
+    flips = int(diff.sum())
+    near = float(rz[diff].abs().max()) if flips else 0.0
+    print(f"level mask {H}x{W}->{th}x{tw}: {flips} flips of {B * Q * th * tw}, max |logit| at a flip {near:.1e}")
+    assert flips <= 1e-5 * B * Q * th * tw + 2
+    assert near <= 1e-4 * float(rz.abs().max())
+    # the fused kernel vs thresholding the stored level logits (same products, another order)
+    assert int(ops.unpack_bitmask(got ^ via, th * tw).sum()) <= 1e-5 * B * Q * th * tw + 2
+
+
+def test_level_bitmask_row_fix():
+    """A query whose logits are negative at every key of the level is written un-blocked
+    (HF:m2f:1912-1914); ragged key counts (th * tw not a multiple of 32)."""
+    ops = _ops()
+    B, Q, C, th, tw = 1, 40, 64, 7, 9
+    Fm = torch.ones(B, th * tw, C, device=DEV, dtype=torch.bfloat16)
+    lv = torch.cat([Fm, torch.zeros_like(Fm)], -1)
+    E = torch.full((B, Q, C), 0.25, device=DEV, dtype=torch.bfloat16)
+    E[0, ::2] = -0.25                                         # even queries: every key blocked
+    E[0, 1::4, :8] = -1.0                                     # some odd queries: x = 16 - 8 - ... > or < 0
+    words = ops.level_bitmask_hilo(E, lv, th, tw)
+    with torch.no_grad():
+        exp = ops.attn_bitmask(ops.mask_head(E, Fm, th, tw), (th, tw))
+    assert torch.equal(words, exp)
+    assert int(words[0, ::2].abs().sum()) == 0
+
+
+def test_factored_criterion_equals_materialised():
+    """SetCriterion on FactoredLogits (matcher + matched maps from the factors) vs the same
+    criterion on the materialised full-resolution logits: the same matching, the same losses
+    and the same gradients of E and F."""
+    from visionseg.criterion import SetCriterion
+    from visionseg.data import synthetic_batch
+    from visionseg.model import M2FConfig
+    ops = _ops()
+    cfg = M2FConfig.preset("swin_t", num_queries=100, train_num_points=2048)
+    _, ml, cl = synthetic_batch(2, 256, seed=5, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(2)
+    S, B, Q, C, H, W = 4, len(ml), 100, 256, 64, 64
+    E0 = (torch.randn(S, B, Q, C, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    F0 = torch.randn(B, H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    classes = [torch.randn(B, Q, 2, device=DEV, generator=g) for _ in range(S)]
+    out = []
+    for fact in (True, False):
+        E = E0.clone().requires_grad_(True)
+        Fm = F0.clone().requires_grad_(True)
+        if fact:
+            masks = [ops.FactoredLogits(E, Fm, s, H, W) for s in range(S)]
+        else:
+            masks = []
+            for s in range(S):
+                with torch.no_grad():
+                    m = ops.mask_head(E[s], Fm, H, W)
+                m._vs_src = (E, Fm, s)
+                masks.append(m)
+        crit = SetCriterion(cfg)
+        torch.cuda.manual_seed(9)
+        assign = crit.match([m.detach() for m in masks], torch.stack(classes), ml, cl)
+        torch.cuda.manual_seed(9)
+        loss, parts = crit(masks, classes, ml, cl)
+        loss.backward()
+        out.append((assign, float(loss), E.grad.float(), Fm.grad.float()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert abs(out[0][1] - out[1][1]) <= 1e-5 * abs(out[1][1])
+    for i in (2, 3):
+        a, b = out[0][i], out[1][i]
+        assert float((a - b).abs().max()) <= 1e-2 * float(b.abs().max())

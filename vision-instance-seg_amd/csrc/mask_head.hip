@@ -112,9 +112,13 @@ __global__ void __launch_bounds__(256) mask_head_fwd_kernel(const T* __restrict_
 // bf16 forward with a compile-time channel count: each wave streams its pixel tiles with
 // the NEXT tile's P fragments (KC/16 x 16 B per lane) in flight while the current tile's
 // MFMAs run, so at one wave per SIMD the HBM latency stays hidden.
-template <int KC>
+// GROUPED: logits row (b, q) is stored at row ((q / G) B + b) G + q % G of out (q / G by the
+// multiply-shift gm = ceil(2^20 / G), exact for Q G < 2^20): the matched maps of S decoder
+// steps x G targets land in (step, image, target) order straight from one launch.
+template <int KC, bool GROUPED = false>
 __global__ void __launch_bounds__(256) mask_head_fwd_bf16_kernel(const bf16* __restrict__ E, const bf16* __restrict__ P,
-                                                                 float* __restrict__ out, int Q, int N) {
+                                                                 float* __restrict__ out, int Q, int N, int G = 0,
+                                                                 unsigned gm = 0) {
   constexpr int S = KC / 16;
   constexpr int ldE = KC + 8;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -180,7 +184,14 @@ __global__ void __launch_bounds__(256) mask_head_fwd_bf16_kernel(const bf16* __r
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int row = q0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (row < Q) Ob[(size_t)row * N + n] = acc[t][i];
+          if (row < Q) {
+            if constexpr (GROUPED) {
+              const unsigned d = (unsigned)(((unsigned long long)row * gm) >> 20);
+              out[((size_t)(d * gridDim.y + b) * G + (row - d * G)) * N + n] = acc[t][i];
+            } else {
+              Ob[(size_t)row * N + n] = acc[t][i];
+            }
+          }
         }
     }
 #pragma unroll
@@ -549,6 +560,31 @@ extern "C" int vs_mask_head_forward(int dtype, const void* E, const void* P, flo
   } else {
     VS_CHECK(false, "dtype must be VS_F32 or VS_BF16");
   }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_mask_head_forward_grouped(const void* E, const void* P, float* logits, int B, int Q, int C, int H,
+                                            int W, int group, void* stream) {
+  VS_CHECK(E && P && logits, "null pointer");
+  VS_CHECK(B > 0 && Q > 0 && H > 0 && W > 0, "bad sizes");
+  VS_CHECK(C == 128 || C == 256, "grouped mask head: bf16, C in {128, 256}");
+  VS_CHECK(group > 0 && Q % group == 0 && (long long)Q * group < (1LL << 20), "group must divide Q, Q * group < 2^20");
+  const int N = H * W;
+  const int qz = (Q + 32 * kQT - 1) / (32 * kQT);
+  const int tiles = (N + 31) / 32;
+  int gx = (tiles + kWaves - 1) / kWaves;
+  const int pcap = (256 + B * qz - 1) / (B * qz);
+  if (gx > pcap) gx = pcap;
+  const unsigned gm = (unsigned)(((1u << 20) + group - 1) / group);
+  const size_t lds = (size_t)32 * kQT * (C + 8) * 2;
+  hipStream_t st = (hipStream_t)stream;
+  if (C == 256)
+    hipLaunchKernelGGL((mask_head_fwd_bf16_kernel<256, true>), dim3(gx, B, qz), dim3(256), lds, st, (const bf16*)E,
+                       (const bf16*)P, logits, Q, N, group, gm);
+  else
+    hipLaunchKernelGGL((mask_head_fwd_bf16_kernel<128, true>), dim3(gx, B, qz), dim3(256), lds, st, (const bf16*)E,
+                       (const bf16*)P, logits, Q, N, group, gm);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

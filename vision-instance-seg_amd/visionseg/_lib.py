@@ -53,6 +53,7 @@ SIGNATURES = {
     "vs_mask_head_backward": [_c_int] + [_P] * 6 + [_c_int] * 5 + [_P],
     "vs_mask_head_backward_ex": [_c_int] + [_P] * 6 + [_c_int] * 6 + [_P],
     "vs_attn_bitmask": [_P, _P] + [_c_int] * 5 + [_P],
+    "vs_mask_head_forward_grouped": [_P, _P, _P] + [_c_int] * 6 + [_P],
     "vs_point_scatter": [_P, _P, _P] + [_c_int] * 6 + [_P],
     "vs_masked_attn_workspace_bytes": [_c_int] * 4,
     "vs_masked_attn_forward": [_c_int, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 4 + [_c_float, _P],
@@ -82,6 +83,11 @@ SIGNATURES = {
     "vs_lsa_batch": [_P, _P] + [_c_int] * 4 + [_P, _P],
     "vs_lsa_batch_device_counts": [_P, _P] + [_c_int] * 4 + [_P, _P],
     "vs_match_cost": [_P, _c_int, _P, _c_int, _P, _P, _P, _P] + [_c_int] * 6 + [_c_float] * 3 + [_P],
+    "vs_feature_resize_hilo": [_P, _P] + [_c_int] * 6 + [_P],
+    "vs_level_bitmask_hilo": [_P, _P, _P] + [_c_int] * 5 + [_P],
+    "vs_feature_sample_hilo": [_P, _P, _P] + [_c_int] * 5 + [_P],
+    "vs_match_cost_factors_workspace_bytes": [_c_int] * 5,
+    "vs_match_cost_factors": [_P, _P, _c_int, _P, _c_int, _P, _P, _P, _P] + [_c_int] * 5 + [_c_float] * 3 + [_P],
     "vs_group_norm_workspace_bytes": [_c_int] * 4,
     "vs_group_norm_forward": [_c_int] + [_P] * 7 + [_c_int] * 4 + [_c_float, _c_int, _P],
     "vs_group_norm_backward": [_c_int] + [_P] * 10 + [_c_int] * 5 + [_P],
@@ -107,7 +113,8 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_flat_step_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_nchw_workspace_bytes": ctypes.c_longlong,
-            "vs_msda_backward_tiled_workspace_bytes": ctypes.c_longlong}
+            "vs_msda_backward_tiled_workspace_bytes": ctypes.c_longlong,
+            "vs_match_cost_factors_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
 _tops = None

@@ -144,6 +144,19 @@ class SetCriterion:
         u = (self.point_source.match_points(B, P, dev).to(dev) if self.point_source is not None
              else torch.rand(B, P, 2, device=dev))
         grid = (2.0 * u - 1.0).unsqueeze(2)                                              # [B,P,1,2]
+        if ops.factored(masks_list):
+            m0 = masks_list[0]
+            if (self.matcher == "device" and 1 <= tg.kc <= 16 and Kc <= ops.lsa_max_targets(Q)
+                    and m0.E.dtype == torch.bfloat16 and m0.E.shape[-1] in (64, 128, 256)):
+                # the point logits are E_s . F(p): F sampled once at the points (hi | lo
+                # bf16 pair), the costs from the factors (csrc/match_factors.hip) -- no
+                # full-resolution logits of the S steps are made or read
+                fp = ops.feature_sample_hilo(m0.F, m0.H, m0.W, grid.squeeze(2))
+                tp = F.grid_sample(tg.masks.float(), grid, align_corners=False).squeeze(3)  # [B,Kc,P]
+                cost = ops.match_cost_factors(m0.E, fp, probs, tg.classes, tp, c.mask_weight, c.class_weight,
+                                              c.dice_weight)
+                return ops.linear_sum_assignment_padded(cost, tg.counts)
+            masks_list = ops.materialize_masks(masks_list)
         if (self.matcher == "device" and dev.type == "cuda" and 1 <= tg.kc <= 16 and S <= 16
                 and Kc <= ops.lsa_max_targets(Q) and _FUSED_COST):
             # one kernel: point-sampled logits, BCE / dice / class costs (csrc/match.hip).

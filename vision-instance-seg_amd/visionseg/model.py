@@ -591,6 +591,11 @@ class Decoder(nn.Module):
         self.mask_override = None
         self.record = False
         self.batched_heads = True
+        # training (batched heads, bf16): the steps' mask logits stay factored
+        # (ops.FactoredLogits); the attention masks come from E . resize(F) at the level's
+        # size and the matcher from E . F(points) (csrc/match_factors.hip).  VS_FACTORED_MASKS=0
+        # keeps the full-resolution logits (A/B)
+        self.factored_masks = os.environ.get("VS_FACTORED_MASKS", "1") != "0"
 
     def embed(self, h, dtype):
         """(LN(h), mask embedding MLP_3(LN(h))) -- HF:m2f:2040-2048."""
@@ -604,6 +609,15 @@ class Decoder(nn.Module):
         logits = ops.mask_head(e, mf_nhwc, Hm, Wm, sink=sink)
         words = ops.attn_bitmask(logits, target_hw) if target_hw is not None else None
         return x, logits, words
+
+    def level_mask(self, h, mf_level, target_hw):
+        """Attention bitmask of the next layer from the factors: the logits at the level's
+        size are E . resize(F) (bilinear resizing commutes with the mask head's product,
+        HF:m2f:2049-2055), resize(F) given as the hi | lo bf16 pair of
+        ops.feature_resize_hilo (csrc/match_factors.hip level_bitmask_kernel: the logits are
+        thresholded in registers, never stored)."""
+        _, e = self.embed(h, mf_level.dtype)
+        return ops.level_bitmask_hilo(e, mf_level, *target_hw)
 
     def forward(self, ms_feats, mask_features):
         d = self.cfg.hidden_dim
@@ -641,11 +655,21 @@ class Decoder(nn.Module):
         h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
         n = len(self.layers)
 
+        fact = batched and self.factored_masks and mf.dtype == torch.bfloat16 and mf.shape[-1] in (64, 128, 256)
+        mf_levels = {}
+
         def step(hh, target_hw):
             if not batched:
                 return self.predict(hh, mf, Hm, Wm, target_hw, sink)
             with torch.no_grad():
-                return self.predict(hh, mf.detach(), Hm, Wm, target_hw)
+                if not fact:
+                    return self.predict(hh, mf.detach(), Hm, Wm, target_hw)
+                if target_hw is None:
+                    return None, None, None
+                lv = mf_levels.get(target_hw)
+                if lv is None:
+                    lv = mf_levels[target_hw] = ops.feature_resize_hilo(mf.detach(), Hm, Wm, *target_hw)
+                return None, None, self.level_mask(hh, lv, target_hw)
 
         hs = [h]
         inter, logits, words = step(h, sizes[0] if n else None)
@@ -666,8 +690,11 @@ class Decoder(nn.Module):
         if batched:
             X, E = self.embed(torch.stack(hs), mf.dtype)                                # [S,B,Q,D], [S,B,Q,C]
             inters = list(X.unbind(0))
-            for s_, m in enumerate(masks):
-                m._vs_src = (E, mf, s_)
+            if fact:
+                masks = [ops.FactoredLogits(E, mf, s_, Hm, Wm) for s_ in range(len(hs))]
+            else:
+                for s_, m in enumerate(masks):
+                    m._vs_src = (E, mf, s_)
         return inters, masks
 
 

@@ -496,12 +496,158 @@ class MatchedPointLogitsFunction(torch.autograd.Function):
         return None, None, None, dE, dP.to(P.dtype)
 
 
+class FactoredLogits:
+    """Mask logits of decoder step `s` kept as the mask head's factors, never materialised
+    at full resolution: L[b, q, n] = E[s, b, q, :] . F[b, n, :] (E [S, B, Q, C] the batched
+    heads' mask embeddings with their autograd history, F [B, H*W, C] the channels-last
+    pixel embedding).  The training step reads the logits only through linear resamplings
+    (the matcher's points, the attention masks' resize) and the matched rows, each computed
+    from the factors (csrc/match_factors.hip, `matched_maps`); `materialize()` gives the
+    full tensor for any other consumer."""
+
+    def __init__(self, E, F, s: int, height: int, width: int):
+        self.E, self.F, self.s, self.H, self.W = E, F, int(s), int(height), int(width)
+        self._vs_src = (E, F, self.s)
+
+    @property
+    def shape(self):
+        return torch.Size((self.E.shape[1], self.E.shape[2], self.H, self.W))
+
+    @property
+    def device(self):
+        return self.E.device
+
+    dtype = torch.float32
+
+    def detach(self):
+        return FactoredLogits(self.E.detach(), self.F.detach(), self.s, self.H, self.W)
+
+    def materialize(self):
+        return mask_head(self.E[self.s], self.F, self.H, self.W)
+
+    def float(self):
+        return self               # the logits are f32 already (the mask head's output dtype)
+
+
+def factored(masks_list) -> bool:
+    return bool(masks_list) and all(isinstance(m, FactoredLogits) for m in masks_list)
+
+
+def materialize_masks(masks_list):
+    return [m.materialize() if isinstance(m, FactoredLogits) else m for m in masks_list]
+
+
+def feature_resize_hilo(F_nhwc, height: int, width: int, th: int, tw: int):
+    """Bilinear (align_corners=False) resize of the channels-last pixel embedding bf16
+    [B, H*W, C] to [B, th*tw, 2C] as hi | lo bf16 pairs (csrc/match_factors.hip): E . (hi + lo)
+    = the resized logits of HF:m2f:2049-2055 to ~2^-17 relative."""
+    L.require_hip(F_nhwc)
+    Fc = F_nhwc.contiguous()
+    if Fc.dtype != torch.bfloat16:
+        raise TypeError("feature_resize_hilo takes the bf16 pixel embedding")
+    B, N, C = Fc.shape
+    if N != height * width:
+        raise ValueError("feature_resize_hilo: pixel embedding is not [B, H*W, C]")
+    out = torch.empty(B, th * tw, 2 * C, device=Fc.device, dtype=torch.bfloat16)
+    with timed("feature_resize_hilo", Fc, bytes_=out.numel() * 2 + min(Fc.numel(), out.numel() * 2) * 2):
+        L.check(L.lib().vs_feature_resize_hilo(L.ptr(Fc), L.ptr(out), B, int(height), int(width), C, int(th), int(tw),
+                                               L.stream(Fc)), "feature_resize_hilo")
+    return out
+
+
+def level_bitmask_hilo(E, level_features, height: int, width: int):
+    """Attention bitmask (attn_bitmask's format and rule) of E bf16 [B, Q, C] . resize(F) at a
+    level of height x width keys, resize(F) = feature_resize_hilo's [B, h*w, 2C] pair; the
+    level logits are never stored (csrc/match_factors.hip level_bitmask_kernel)."""
+    Ec, Fl = E.contiguous(), level_features.contiguous()
+    L.require_hip(Ec, Fl)
+    B, Q, C = Ec.shape
+    if Ec.dtype != torch.bfloat16 or tuple(Fl.shape) != (B, height * width, 2 * C):
+        raise ValueError("level_bitmask_hilo: bf16 E [B, Q, C] and features [B, h*w, 2C] expected")
+    words = torch.empty(B, Q, (height * width + 31) // 32, device=Ec.device, dtype=torch.int32)
+    with timed("level_bitmask", Ec, bytes_=Fl.numel() * 2 + words.numel() * 4, flops=4.0 * B * Q * C * height * width):
+        L.check(L.lib().vs_level_bitmask_hilo(L.ptr(Ec), L.ptr(Fl), L.ptr(words), B, Q, C, int(height), int(width),
+                                              L.stream(Ec)), "level_bitmask_hilo")
+    return words
+
+
+def feature_sample_hilo(F_nhwc, height: int, width: int, grid):
+    """The pixel embedding bf16 [B, H*W, C] at grid points f32 [B, P, 2] in [-1, 1]
+    (grid_sample bilinear, zeros padding, align_corners=False) -> [B, P, 2C] hi | lo bf16."""
+    L.require_hip(F_nhwc, grid)
+    Fc = F_nhwc.contiguous()
+    g = grid.float().contiguous()
+    B, N, C = Fc.shape
+    P = int(g.shape[1])
+    if Fc.dtype != torch.bfloat16 or N != height * width or tuple(g.shape) != (B, P, 2):
+        raise ValueError("feature_sample_hilo: bf16 [B, H*W, C] features and [B, P, 2] grid expected")
+    out = torch.empty(B, P, 2 * C, device=Fc.device, dtype=torch.bfloat16)
+    with timed("feature_sample_hilo", Fc, bytes_=out.numel() * 2 * 3):
+        L.check(L.lib().vs_feature_sample_hilo(L.ptr(Fc), L.ptr(g), L.ptr(out), B, int(height), int(width), C, P,
+                                               L.stream(Fc)), "feature_sample_hilo")
+    return out
+
+
+def match_cost_factors(E, point_features, probs, target_classes, target_labels, mask_weight, class_weight,
+                       dice_weight):
+    """Hungarian-matcher cost for all decoder steps from the mask head's factors
+    (csrc/match_factors.hip): E bf16 [S, B, Q, C], point_features = feature_sample_hilo at
+    the matcher's points [B, P, 2C], probs f32 [S, B, Q, C+1], target_classes int64
+    [B, Kc], target_labels f32 [B, Kc, P] -> cost f32 [S, B, Q, Kc] (= match_cost over the
+    logits E_s . F, HF:m2f:434-481)."""
+    Ec = E.contiguous()
+    Fp = point_features.contiguous()
+    L.require_hip(Ec, Fp, probs, target_classes, target_labels)
+    S, B, Q, C = Ec.shape
+    pr = probs.float().contiguous()
+    tc = target_classes.to(torch.int64).contiguous()
+    tl = target_labels.float().contiguous()
+    Kc, P = int(tl.shape[1]), int(tl.shape[2])
+    if (Ec.dtype != torch.bfloat16 or tuple(Fp.shape) != (B, P, 2 * C) or tuple(tc.shape) != (B, Kc)
+            or tuple(pr.shape[:3]) != (S, B, Q)):
+        raise ValueError("match_cost_factors: inconsistent shapes")
+    ws = torch.empty(int(L.lib().vs_match_cost_factors_workspace_bytes(S, B, Q, P, Kc)), device=Ec.device,
+                     dtype=torch.uint8)
+    cost = torch.empty(S, B, Q, Kc, device=Ec.device, dtype=torch.float32)
+    with timed("match_cost_factors", Ec, bytes_=Fp.numel() * 2 + tl.numel() * 4 + Ec.numel() * 2,
+               flops=4.0 * S * B * Q * P * C):
+        L.check(L.lib().vs_match_cost_factors(L.ptr(Ec), L.ptr(Fp), S, L.ptr(pr), int(pr.shape[3]), L.ptr(tc),
+                                              L.ptr(tl), L.ptr(cost), L.ptr(ws), B, Q, C, P, Kc,
+                                              float(mask_weight), float(class_weight), float(dice_weight),
+                                              L.stream(Ec)), "match_cost_factors")
+    return cost
+
+
+def mask_head_grouped(E, F_nhwc, height: int, width: int, group: int):
+    """mask_head of E bf16 [B, Q, C] (Q = R * group) over F [B, H*W, C] with the output rows
+    in (r, image, g) order: f32 [R, B, group, H, W] (csrc/mask_head.hip, grouped stores)."""
+    Ec, Fc = E.contiguous(), F_nhwc.contiguous()
+    L.require_hip(Ec, Fc)
+    B, Q, C = Ec.shape
+    if Ec.dtype != torch.bfloat16 or Fc.dtype != torch.bfloat16 or tuple(Fc.shape) != (B, height * width, C):
+        raise ValueError("mask_head_grouped: bf16 E [B, Q, C] and F [B, H*W, C] expected")
+    out = torch.empty(Q // group, B, group, height, width, device=Ec.device, dtype=torch.float32)
+    with timed("mask_head_fwd", Ec, bytes_=Fc.numel() * 2 + out.numel() * 4, flops=2.0 * B * Q * C * height * width):
+        L.check(L.lib().vs_mask_head_forward_grouped(L.ptr(Ec), L.ptr(Fc), L.ptr(out), B, Q, C, int(height),
+                                                     int(width), int(group), L.stream(Ec)), "mask_head_grouped")
+    return out
+
+
 def matched_maps(masks_list, qsel):
     """(maps [S*B*Kc, 1, H, W] f32 of mask_list[s][b, qsel[s, b, k]], factors): detached
     maps + the mask head's factors (E, P) when every step's logits came from `mask_head`
     (the loss then differentiates through `point_logits` -> MatchedPointLogitsFunction),
-    else the maps with their autograd history and factors None."""
+    else the maps with their autograd history and factors None.  FactoredLogits: the
+    matched rows only, E_sel . F in one grouped mask-head launch."""
     S, B, Kc = qsel.shape
+    if factored(masks_list):
+        m0 = masks_list[0]
+        E, Fm = m0.E, m0.F
+        C = E.shape[-1]
+        with torch.no_grad():
+            Esel = torch.gather(E.detach().transpose(0, 1), 2, qsel.transpose(0, 1)[..., None].expand(B, S, Kc, C))
+            maps = mask_head_grouped(Esel.reshape(B, S * Kc, C), Fm.detach(), m0.H, m0.W, Kc)
+        return maps.view(S * B * Kc, 1, m0.H, m0.W), (E, Fm)
     bidx = torch.arange(B, device=qsel.device)[:, None].expand(B, Kc)
     fac = mask_head_factors(masks_list)
     with torch.no_grad() if fac is not None else contextlib.nullcontext():
