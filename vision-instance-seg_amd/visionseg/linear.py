@@ -80,6 +80,50 @@ def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype, out: 
     return out
 
 
+# Forward of the token Linears: the hand-written token GEMM (csrc/token_gemm.hip) where it
+# beats the vendor GEMM on this shape -- measured once per (M, N, K, bias) on the first eager
+# call (HIP events, median of 5 alternating runs each; taken only when >= 3 % faster), never
+# inside a graph capture (an unmeasured shape runs the vendor GEMM there).  At C2 the token
+# GEMM wins the small-N Swin shapes (qkv, proj, fc2 of stages 1-3: tools/tgemm_bench.py,
+# profiles/r4_tgemm_bench3.txt).  VS_TGEMM_FWD=0: always the vendor GEMM.
+_TGEMM_FWD = os.environ.get("VS_TGEMM_FWD", "1") == "1"
+_fwd_choice: dict = {}
+
+
+def _pick_token_gemm(x2, weight, bias) -> bool:
+    fns = (lambda: F.linear(x2, weight, bias), lambda: ops.token_gemm(x2, weight, bias))
+    for f in fns:
+        f()
+    ev = [[], []]
+    for _ in range(5):
+        for i, f in enumerate(fns):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            f()
+            b.record()
+            ev[i].append((a, b))
+    torch.cuda.synchronize()
+    med = [sorted(a.elapsed_time(b) for a, b in e)[2] for e in ev]
+    return med[1] < 0.97 * med[0]
+
+
+def _forward_gemm(x, weight, bias):
+    """x W^T + b inside _LinearFn.forward (grad mode is off there, so no _tgemm_ok)."""
+    N, K = weight.shape
+    if not (_TGEMM_FWD and x.is_cuda and x.dtype == weight.dtype == torch.bfloat16 and x.is_contiguous()
+            and (bias is None or bias.dtype == torch.bfloat16) and K % 8 == 0 and N % 8 == 0
+            and x.numel() // K >= MIN_TOKENS):
+        return F.linear(x, weight, bias)
+    x2 = x.reshape(-1, K)
+    key = (x2.shape[0], N, K, bias is not None, x.device.index)
+    use = _fwd_choice.get(key)
+    if use is None:
+        if torch.cuda.is_current_stream_capturing():
+            return F.linear(x, weight, bias)
+        use = _fwd_choice[key] = _pick_token_gemm(x2, weight, bias)
+    return ops.token_gemm(x2, weight, bias).view(*x.shape[:-1], N) if use else F.linear(x, weight, bias)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, sink=None):
@@ -88,7 +132,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.sink = sink
         if sink is not None:
             sink.arm()
-        return F.linear(x, weight, bias)
+        return _forward_gemm(x, weight, bias)
 
     @staticmethod
     def backward(ctx, gy):
