@@ -327,17 +327,28 @@ __global__ void __launch_bounds__(256) level_bitmask_kernel(const bf16* __restri
   const int q0 = (qg * 4 + wave) * 32;
   if (q0 >= Q) return;                                   // whole wave: no barrier below
   const int q = q0 + r, n = kt * 32 + r;
+  // rows past Q / N are clamped onto row 0: their results are never stored (q >= Q) or
+  // masked out of the bits (keys >= N), so no selects; every load of a batch is issued
+  // before its products (the k-step loop is latency-bound otherwise)
   const bf16* er = E + ((size_t)b * Q + (q < Q ? q : 0)) * KC + 8 * hh;
   const bf16* fr = Fhl + ((size_t)b * N + (n < N ? n : 0)) * 2 * KC + 8 * hh;
   f32x16_t acc;
   zero16(acc);
+  constexpr int KB = KC / 16 < 8 ? KC / 16 : 8;
 #pragma unroll
-  for (int k = 0; k < KC / 16; ++k) {
-    const bf16x8_t a = q < Q ? *reinterpret_cast<const bf16x8_t*>(er + 16 * k) : zero8();
-    const bf16x8_t fh = n < N ? *reinterpret_cast<const bf16x8_t*>(fr + 16 * k) : zero8();
-    const bf16x8_t fl = n < N ? *reinterpret_cast<const bf16x8_t*>(fr + KC + 16 * k) : zero8();
-    acc = mfma16(fh, a, acc);                // rows = keys, column = query (S^T layout)
-    acc = mfma16(fl, a, acc);
+  for (int k0 = 0; k0 < KC / 16; k0 += KB) {
+    bf16x8_t a[KB], fh[KB], fl[KB];
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      a[j] = *reinterpret_cast<const bf16x8_t*>(er + 16 * (k0 + j));
+      fh[j] = *reinterpret_cast<const bf16x8_t*>(fr + 16 * (k0 + j));
+      fl[j] = *reinterpret_cast<const bf16x8_t*>(fr + KC + 16 * (k0 + j));
+    }
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      acc = mfma16(fh[j], a[j], acc);        // rows = keys, column = query (S^T layout)
+      acc = mfma16(fl[j], a[j], acc);
+    }
   }
   // acc[i] = the logit of query q (this lane's column) at key kt*32 + crow(i, hh): each
   // lane packs its 16 keys' bits, the other lane half holds the other 16 keys
