@@ -263,8 +263,10 @@ __global__ void __launch_bounds__(64 * kCostWaves, 1) match_cost_fac_kernel(
   }
 }
 
+// 4 lanes per column, each summing every 4th point range; the four partial sums are then
+// combined in lane order (fixed: deterministic) -- a quarter of the serial load rounds
 template <int KT>
-__global__ void __launch_bounds__(64) match_cost_fac_fin_kernel(const float* __restrict__ part,
+__global__ void __launch_bounds__(256) match_cost_fac_fin_kernel(const float* __restrict__ part,
                                                                  const float* __restrict__ tpart,
                                                                  const float* __restrict__ probs, int C1,
                                                                  const long long* __restrict__ tcls,
@@ -273,16 +275,17 @@ __global__ void __launch_bounds__(64) match_cost_fac_fin_kernel(const float* __r
                                                                  float wd) {
   constexpr int NF = 2 + 2 * KT;
   const int b = blockIdx.y;
-  const int col = blockIdx.x * 64 + threadIdx.x;
+  const int j = threadIdx.x & 3;
+  const int col = blockIdx.x * 64 + (threadIdx.x >> 2);
   const int SQ = S * Q, SQp = NCG * kCols;
-  if (col >= SQ) return;
-  const int s = col / Q, q = col % Q;
+  const bool ok = col < SQ;                  // no early return: the shuffles need all lanes
+  const int cc = ok ? col : 0;
   float SP = 0.f, SG = 0.f, N[KT], X[KT], T[KT];
 #pragma unroll
   for (int k = 0; k < KT; ++k) N[k] = X[k] = T[k] = 0.f;
-#pragma unroll 4
-  for (int ps = 0; ps < PS; ++ps) {
-    const float* pb = part + ((size_t)b * PS + ps) * NF * SQp + col;
+#pragma unroll 2
+  for (int ps = j; ps < PS; ps += 4) {
+    const float* pb = part + ((size_t)b * PS + ps) * NF * SQp + cc;
     SP += pb[0];
     SG += pb[(size_t)SQp];
 #pragma unroll
@@ -294,6 +297,21 @@ __global__ void __launch_bounds__(64) match_cost_fac_fin_kernel(const float* __r
       }
     }
   }
+  // lane order 0 + 1 + 2 + 3 (the 4 lanes of a column are consecutive)
+  auto comb = [&](float v) {
+    const float v1 = __shfl_down(v, 1, 64), v2 = __shfl_down(v, 2, 64), v3 = __shfl_down(v, 3, 64);
+    return ((v + v1) + v2) + v3;
+  };
+  SP = comb(SP);
+  SG = comb(SG);
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    N[k] = comb(N[k]);
+    X[k] = comb(X[k]);
+    T[k] = comb(T[k]);
+  }
+  if (!ok || j != 0) return;
+  const int s = col / Q, q = col % Q;
   const float* pr = probs + (((size_t)s * B + b) * Q + q) * C1;
   float* out = cost + (((size_t)s * B + b) * Q + q) * Kc;
 #pragma unroll
@@ -476,7 +494,7 @@ extern "C" int vs_match_cost_factors(const void* mask_embed, const void* point_f
   VS_LAUNCH_CHECK();
   const dim3 fg((num_steps * num_queries + 63) / 64, batch);
 #define VS_FIN(KT_)                                                                                               \
-  hipLaunchKernelGGL((match_cost_fac_fin_kernel<KT_>), fg, dim3(64), 0, st, part, tpart, class_probs,             \
+  hipLaunchKernelGGL((match_cost_fac_fin_kernel<KT_>), fg, dim3(256), 0, st, part, tpart, class_probs,            \
                      num_classes_plus1, target_classes, cost, num_steps, batch, num_queries, num_points, max_targets, \
                      pl.NCG, pl.PS, mask_weight, class_weight, dice_weight)
   if (pl.KT == 4)
