@@ -171,14 +171,16 @@ def test_gelu_quantised_output_equals_mx_quantize(M, N, K, fp8):
     assert torch.equal(yq, eq)
 
 
-def test_mlp_fp8_vs_bf16_mlp():
+@pytest.mark.parametrize("C", [384, 192])
+def test_mlp_fp8_vs_bf16_mlp(C):
     """linear.mlp_fp8 (config C5's Swin MLP: fc1 + GELU on the MX fp8 token GEMM writing fc2's
-    fp8 operand in its epilogue, fc2 on the MX fp8 GEMM, straight-through backward) vs the
-    same MLP in f64 on the bf16 operands: output rel-RMS <= 0.06 (the fp8 budget of two
-    chained products), input / weight / bias gradients rel-L2 <= 0.06."""
+    fp8 operand in its epilogue, fc2 on the MX fp8 GEMM, straight-through backward; C = 192:
+    fc1 too shallow for fp8, the vendor GEMM + GELU, fc2 on fp8) vs the same MLP in f64 on
+    the bf16 operands: output rel-RMS <= 0.06 (the fp8 budget of two chained products),
+    input / weight / bias gradients rel-L2 <= 0.06.  M above the token-GEMM threshold."""
     from visionseg.linear import mlp_fp8
     g = torch.Generator().manual_seed(21)
-    M, C = 9216, 384
+    M = 20000
     x = _rand((M, C), g)
     w1, b1 = _rand((4 * C, C), g, 1 / math.sqrt(C)), _rand((4 * C,), g, 0.1)
     w2, b2 = _rand((C, 4 * C), g, 1 / math.sqrt(4 * C)), _rand((C,), g, 0.1)
@@ -253,3 +255,26 @@ def test_linear_tokens_forward_dispatch(monkeypatch, choice):
     for got, exp in ((y, yr), (xd.grad, xr.grad), (wd.grad, wr.grad), (bd.grad, br.grad)):
         rel = float((got.detach().cpu().double() - exp.detach()).norm() / exp.detach().norm())
         assert rel <= 0.01, rel
+
+
+@pytest.mark.parametrize("fp8_dgrad", [False, True])
+def test_fp8_linear_dgrad_modes(monkeypatch, fp8_dgrad):
+    """linear_fp8_tokens' backward with dX on the bf16 vendor GEMM (default) or on the MX fp8
+    token GEMM (VS_FP8_DGRAD=1): dX, dW, db vs f64 autograd on the bf16 operands (fp8
+    forward: output rel-RMS <= 0.05; gradients rel-L2 <= 0.05, dX on bf16 <= 0.01)."""
+    from visionseg import linear
+    monkeypatch.setattr(linear, "FP8_DGRAD", fp8_dgrad)
+    g = torch.Generator().manual_seed(5)
+    M, K, N = 20000, 768, 384
+    x, w, b = _rand((M, K), g), _rand((N, K), g, 1 / math.sqrt(K)), _rand((N,), g, 0.1)
+    gy = _rand((M, N), g, 0.01)
+    xd, wd, bd = (t.to(DEV).requires_grad_(True) for t in (x, w, b))
+    y = linear.linear_fp8_tokens(xd, wd, bd)
+    y.backward(gy.to(DEV))
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+    yr = xr @ wr.t() + br
+    yr.backward(gy.double())
+    for got, exp, tol in ((y, yr, 0.05), (xd.grad, xr.grad, 0.05 if fp8_dgrad else 0.01), (wd.grad, wr.grad, 0.05),
+                          (bd.grad, br.grad, 0.05)):
+        rel = float((got.detach().cpu().double() - exp.detach()).norm() / exp.detach().norm())
+        assert rel <= tol, rel

@@ -798,8 +798,11 @@ def _tgemm_ok(x, w, b, tokens_min=MIN_TOKENS):
 
 
 # config C5 fp8 Linears: the input gradient dX = dY W on the MX fp8 token GEMM too (dY and W^T
-# quantised per 32 along the output features); VS_FP8_DGRAD=0 keeps it on the bf16 vendor GEMM
-FP8_DGRAD = os.environ.get("VS_FP8_DGRAD", "1") == "1"
+# quantised per 32 along the output features) with VS_FP8_DGRAD=1.  Off by default: the C5
+# step measured the same with it (131.05 vs 131.01 ms, profiles/r4_bench_c5_fp8_dgrad_ab.jsonl)
+# -- the dY quantisation passes cost what the fp8 product saves -- and the bf16 dX carries
+# no quantisation error
+FP8_DGRAD = os.environ.get("VS_FP8_DGRAD", "0") == "1"
 
 
 def _dgrad(gy2, weight):
@@ -938,8 +941,11 @@ def mlp_fp8(x, w1, b1, w2, b2, xq=None):
     between the two GEMMs (config C5).  xq: x's MX fp8 copy from its producer (the
     LayerNorm), if it made one."""
     K1, N1 = w1.shape[1], w1.shape[0]
-    if _tgemm_ok(x, w1, b1) and N1 % 128 == 0 and N1 >= FP8_MIN_K:
-        fc1_fp8 = K1 % 128 == 0 and K1 >= FP8_MIN_K
-        h, hq, hs = _LinearGeluFn.apply(x, w1, b1, fc1_fp8, True, *(xq if (xq is not None and fc1_fp8) else (None, None)))
+    fc1_fp8 = K1 % 128 == 0 and K1 >= FP8_MIN_K
+    if _tgemm_ok(x, w1, b1) and N1 % 128 == 0 and N1 >= FP8_MIN_K and fc1_fp8:
+        h, hq, hs = _LinearGeluFn.apply(x, w1, b1, True, True, *(xq if xq is not None else (None, None)))
         return linear_fp8_tokens(h, w2, b2, (hq, hs))
-    return linear_fp8_tokens(linear_gelu_tokens(x, w1, b1, fp8=True), w2, b2)
+    # fc1 too shallow for fp8 (Swin-L stage 1, K = 192): the vendor GEMM + the GELU pass and
+    # one quantisation of h for fc2 run faster than the bf16 token GEMM's GELU + MX-output
+    # epilogue (C5: 0.95 vs 1.37 ms a launch, profiles/r4_c5_fp8_vs_bf16_kernel_diff.txt)
+    return linear_fp8_tokens(ops.activation(linear_tokens(x, w1, b1), "gelu"), w2, b2)
