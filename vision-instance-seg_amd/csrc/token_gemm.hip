@@ -166,10 +166,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
       for (int t = 0; t < TM; ++t) xsc[t] = ss[xrow(t)];
 #pragma unroll
       for (int t = 0; t < TN; ++t) wsc[t] = ss[BM + wrow(t)];
-      // fragments double-buffered across the two MX steps, except for the 16-tile wave
-      // layout (its 256 accumulator registers leave no room for a second buffer)
-      constexpr int NBUF = TM * TN >= 16 ? 1 : 2;
-      i32x8_t xa[NBUF][TM], wa[NBUF][TN];            // [buffer][tile]
+      i32x8_t xa[2][TM], wa[2][TN];                  // [buffer][tile]
       auto ld2 = [&](const unsigned char* img, int row, int kk) {
         const uint4 v0 = *reinterpret_cast<const uint4*>(img + tile_off(row, 4 * kk + hh));
         const uint4 v1 = *reinterpret_cast<const uint4*>(img + tile_off(row, 4 * kk + 2 + hh));
@@ -184,9 +181,8 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
       load(0, 0);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {                // two 64-element MX steps per K-step
-        if (NBUF == 2 && kk + 1 < 2) load(kk + 1, (kk + 1) & 1);
-        if (NBUF == 1 && kk > 0) load(kk, 0);
-        const int bs = NBUF == 2 ? (kk & 1) : 0;
+        if (kk + 1 < 2) load(kk + 1, (kk + 1) & 1);
+        const int bs = kk & 1;
 #pragma unroll
         for (int a = 0; a < TN; ++a)
 #pragma unroll
@@ -377,12 +373,6 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
     return e ? atoi(e) : 0;
   }();
   const bool big = force ? force == 256 : (N >= 512 && K >= 256 && (long long)((M + 255) / 256) * ((N + 255) / 256) >= 256);
-  // VS_TGEMM_WIDE=1: the 256 x 256 tile on 4 waves of 128 x 128 (16 accumulator tiles a
-  // wave, one wave per SIMD): 2/3 of the LDS fragment reads per MFMA of the 8-wave layout
-  static const bool wide = [] {
-    const char* e = getenv("VS_TGEMM_WIDE");
-    return e && atoi(e) != 0;
-  }();
   const int bm = big ? 256 : 128, bn = big ? 256 : 128;
   const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   VS_CHECK(tiles < (1ll << 31), "too many tiles");
@@ -390,11 +380,7 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
   const dim3 grid((unsigned)tiles);
 #define VS_TG(F8_, E_)                                                                                               \
   do {                                                                                                               \
-    if (big && wide)                                                                                                 \
-      hipLaunchKernelGGL((token_gemm_kernel<F8_, E_, 2, 2, 4, 4>), grid, dim3(256), 0, st, (const unsigned char*)x,  \
-                         (const unsigned char*)x_scales, (const unsigned char*)w, (const unsigned char*)w_scales,     \
-                         (const bf16*)bias, (bf16*)y, (bf16*)y_pre, (unsigned char*)y_q, (unsigned char*)y_qscales, M, N, K); \
-    else if (big)                                                                                                    \
+    if (big)                                                                                                         \
       hipLaunchKernelGGL((token_gemm_kernel<F8_, E_, 2, 4, 4, 2>), grid, dim3(512), 0, st, (const unsigned char*)x,  \
                          (const unsigned char*)x_scales, (const unsigned char*)w, (const unsigned char*)w_scales,     \
                          (const bf16*)bias, (bf16*)y, (bf16*)y_pre, (unsigned char*)y_q, (unsigned char*)y_qscales, M, N, K);                                         \
