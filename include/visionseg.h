@@ -278,6 +278,12 @@ VS_API int vs_mask_head_forward_grouped(const void* mask_embed, const void* pixe
 VS_API int vs_point_scatter(const float* grad_points, const float* grid, float* maps, int S, int B, int K, int n,
                             int height, int width, void* stream);
 
+/* Point gather for the mask losses' labels: out f32 [N, P] = bilinear sample (point_sample
+ * = grid_sample, align_corners=False, zero padding; HF:m2f:245-275) of maps f32 [M, H, W]
+ * row rows[n] (int64 [N], each in [0, M)) at coords f32 [N, P, 2] in [0, 1] (x, y). */
+VS_API int vs_point_sample_rows(const float* maps, const long long* rows, const float* coords, float* out,
+                                int num_maps, int height, int width, int num_sets, int num_points, void* stream);
+
 /* Attention bitmask of the next decoder layer (HF:m2f:2049-2055 + row fix 1912-1914):
  * bilinear (align_corners=False) resize of each logits row [H, W] to [th, tw], key k
  * blocked iff sigmoid(v) < 0.5, stored as bit k%32 of words[row, k/32]

@@ -94,3 +94,21 @@ def test_swin_t_300_queries_256():
     imgs, ml, cl = synthetic_batch(2, 256, seed=5, device=DEV)
     losses = [float(tr.step(imgs, ml, cl)) for _ in range(2)]
     assert all(torch.isfinite(torch.tensor(losses))), losses
+
+
+def test_point_sample_rows_kernel_vs_grid_sample():
+    """csrc/mask_head.hip point_sample_rows_kernel (the MaskDINO mask losses' per-query label
+    sampler) == grid_sample on the gathered maps, incl. points outside [0, 1] and the border;
+    a C4-sized call (4 images x 400 queries x 12544 points) against the same reference."""
+    import torch.nn.functional as F
+    from visionseg.maskdino import _point_sample_rows
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for M, H, W, N, P in ((6, 17, 23, 8, 50), (40, 256, 256, 1600, 12544)):
+        maps = (torch.rand(M, H, W, device="cuda", generator=g) > 0.5).float()
+        rows = torch.randint(0, M, (N,), device="cuda", generator=g)
+        coords = torch.rand(N, P, 2, device="cuda", generator=g) * 1.2 - 0.1
+        coords[0, :4] = torch.tensor([[0.0, 0.0], [1.0, 1.0], [0.0, 1.0], [1.0, 0.0]], device="cuda")
+        exp = F.grid_sample(maps[rows][:, None], 2.0 * coords.unsqueeze(2) - 1.0,
+                            align_corners=False).squeeze(3).squeeze(1)
+        got = _point_sample_rows(maps, rows, coords)
+        assert float((got - exp).abs().max()) <= 1e-6

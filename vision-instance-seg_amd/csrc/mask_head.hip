@@ -657,6 +657,52 @@ __global__ void __launch_bounds__(256) point_scatter_kernel(const float* __restr
   }
 }
 
+// Point gather: out[n, p] = bilinear sample of maps[rows[n]] at coords[n, p] in [0, 1]
+// (point_sample = grid_sample with align_corners=False, zero padding: ATen's unnormalisation
+// ((2c - 1 + 1) W - 1) / 2 and corner weights), one thread per point -- the MaskDINO mask
+// losses' labels, each query's OWN target map sampled at its points, without materialising
+// the per-query maps or sampling every target channel.
+__global__ void __launch_bounds__(256) point_sample_rows_kernel(const float* __restrict__ maps,
+                                                                const long long* __restrict__ rows,
+                                                                const float* __restrict__ coords,
+                                                                float* __restrict__ out, int H, int W, long long total,
+                                                                int P) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const long long n = i / P;
+  const float* m = maps + rows[n] * (long long)H * W;
+  const float2 c = reinterpret_cast<const float2*>(coords)[i];
+  const float gx = 2.f * c.x - 1.f, gy = 2.f * c.y - 1.f;
+  const float ix = ((gx + 1.f) * (float)W - 1.f) / 2.f;
+  const float iy = ((gy + 1.f) * (float)H - 1.f) / 2.f;
+  const float fx = floorf(ix), fy = floorf(iy);
+  const int x0 = (int)fx, y0 = (int)fy;
+  const float w_nw = (fx + 1.f - ix) * (fy + 1.f - iy), w_ne = (ix - fx) * (fy + 1.f - iy);
+  const float w_sw = (fx + 1.f - ix) * (iy - fy), w_se = (ix - fx) * (iy - fy);
+  float v = 0.f;
+  const bool xi0 = x0 >= 0 && x0 < W, xi1 = x0 + 1 >= 0 && x0 + 1 < W;
+  const bool yi0 = y0 >= 0 && y0 < H, yi1 = y0 + 1 >= 0 && y0 + 1 < H;
+  if (yi0 && xi0) v += m[(size_t)y0 * W + x0] * w_nw;
+  if (yi0 && xi1) v += m[(size_t)y0 * W + x0 + 1] * w_ne;
+  if (yi1 && xi0) v += m[(size_t)(y0 + 1) * W + x0] * w_sw;
+  if (yi1 && xi1) v += m[(size_t)(y0 + 1) * W + x0 + 1] * w_se;
+  out[i] = v;
+}
+
+extern "C" int vs_point_sample_rows(const float* maps, const long long* rows, const float* coords, float* out,
+                                    int num_maps, int height, int width, int num_sets, int num_points,
+                                    void* stream) {
+  VS_CHECK(num_maps > 0 && height > 0 && width > 0 && num_sets >= 0 && num_points > 0, "bad sizes");
+  const long long total = (long long)num_sets * num_points;
+  if (total == 0) return VS_OK;
+  VS_CHECK(maps && rows && coords && out, "null pointer");
+  VS_CHECK(((uintptr_t)coords & 7) == 0, "coords must be 8-B aligned");
+  hipLaunchKernelGGL(point_sample_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, maps, rows, coords, out, height, width, total, num_points);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
 extern "C" long long vs_mask_head_backward_workspace_bytes(int B, int Q, int C) {
   return (long long)mask_head_bwd_parts(B) * B * Q * C * 4;
 }

@@ -424,22 +424,32 @@ def _point_sample_rows(maps, rows, coords):
     """maps [M, H, W] f32, rows [N] int64 (which map each of N point sets reads), coords
     [N, P, 2] in [0, 1] -> [N, P]: `_point_sample(maps[rows][:, None], coords)` without
     materialising maps[rows] (grid_sample's bilinear rule, align_corners=False, zeros
-    outside: the corner weights and the unnormalisation ((g + 1) * size - 1) / 2 of
-    ATen's grid sampler), four gathers of the flattened maps."""
+    outside), one HIP thread per point (csrc/mask_head.hip point_sample_rows_kernel); host
+    tensors (the CPU criterion tests) take the same rule as four gathers."""
+    from . import _lib as L
     M, H, W = maps.shape
-    flat = maps.reshape(-1)
-    g = 2.0 * coords - 1.0
-    ix = ((g[..., 0] + 1) * W - 1) / 2
-    iy = ((g[..., 1] + 1) * H - 1) / 2
-    x0, y0 = torch.floor(ix), torch.floor(iy)
-    x1, y1 = x0 + 1, y0 + 1
-    base = (rows * (H * W))[:, None]
-    out = torch.zeros_like(ix)
-    for xx, yy, wgt in ((x0, y0, (x1 - ix) * (y1 - iy)), (x1, y0, (ix - x0) * (y1 - iy)),
-                        (x0, y1, (x1 - ix) * (iy - y0)), (x1, y1, (ix - x0) * (iy - y0))):
-        inside = (xx >= 0) & (xx <= W - 1) & (yy >= 0) & (yy <= H - 1)
-        idx = base + (yy.clamp(0, H - 1).long() * W + xx.clamp(0, W - 1).long())
-        out = out + torch.where(inside, flat[idx], 0.0) * wgt
+    if not maps.is_cuda:
+        flat = maps.reshape(-1)
+        g = 2.0 * coords - 1.0
+        ix = ((g[..., 0] + 1) * W - 1) / 2
+        iy = ((g[..., 1] + 1) * H - 1) / 2
+        x0, y0 = torch.floor(ix), torch.floor(iy)
+        x1, y1 = x0 + 1, y0 + 1
+        base = (rows * (H * W))[:, None]
+        out = torch.zeros_like(ix)
+        for xx, yy, wgt in ((x0, y0, (x1 - ix) * (y1 - iy)), (x1, y0, (ix - x0) * (y1 - iy)),
+                            (x0, y1, (x1 - ix) * (iy - y0)), (x1, y1, (ix - x0) * (iy - y0))):
+            inside = (xx >= 0) & (xx <= W - 1) & (yy >= 0) & (yy <= H - 1)
+            idx = base + (yy.clamp(0, H - 1).long() * W + xx.clamp(0, W - 1).long())
+            out = out + torch.where(inside, flat[idx], 0.0) * wgt
+        return out
+    N, P = coords.shape[:2]
+    mc = maps.float().contiguous()
+    rc = rows.to(torch.int64).contiguous()
+    cc = coords.float().contiguous()
+    out = torch.empty(N, P, device=maps.device, dtype=torch.float32)
+    L.check(L.lib().vs_point_sample_rows(L.ptr(mc), L.ptr(rc), L.ptr(cc), L.ptr(out), M, H, W, N, P,
+                                         L.stream(mc)), "point_sample_rows")
     return out
 
 
