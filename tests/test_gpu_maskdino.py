@@ -112,3 +112,73 @@ def test_point_sample_rows_kernel_vs_grid_sample():
                             align_corners=False).squeeze(3).squeeze(1)
         got = _point_sample_rows(maps, rows, coords)
         assert float((got - exp).abs().max()) <= 1e-6
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_factor_mask_losses_equal_full_logit_autograd(precision):
+    """MaskDINOCriterion's mask losses through the mask head's factors on the selected rows
+    (ops.RowPointLogitsFunction: point scatter + the head's adjoint on R rows, dP summed in
+    one GradSink) vs autograd through the full logits (grid_sample backward, index
+    backward, mask-head backward over all queries): the same loss and the same gradient
+    of every parameter (bf16: mask features of 128 channels, the fused MFMA backward)."""
+    from visionseg.criterion import PaddedTargets
+    from visionseg.data import synthetic_batch
+    from visionseg.maskdino import MaskDINO, MaskDINOCriterion, masks_to_boxes
+    cfg = (_tiny(mask_feature_size=128, feature_size=128, hidden_dim=128, dec_heads=4) if precision == "bf16"
+           else _tiny())
+    m = MaskDINO(cfg).init_weights(0).to(DEV).train()
+    if precision == "bf16":
+        m = m.to(torch.bfloat16)
+    imgs, ml, cl = synthetic_batch(2, 128, seed=4, device=DEV)
+    tg = PaddedTargets.from_lists(ml, cl, kc=4, device=DEV)
+    boxes = masks_to_boxes(tg.masks)
+    res = []
+    for fl in (True, False):
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(0)
+        torch.cuda.manual_seed(0)
+        out = m(imgs.to(next(m.parameters()).dtype), tg, boxes)
+        loss, _ = MaskDINOCriterion(cfg, factor_losses=fl)(out, tg, boxes)
+        loss.backward()
+        res.append((float(loss), {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}))
+    (l1, g1), (l2, g2) = res
+    assert abs(l1 - l2) <= 1e-5 * abs(l2), (l1, l2)
+    assert set(g1) == set(g2)
+    tol = 2e-2 if precision == "bf16" else 1e-4
+    # the attention key biases' gradients are exactly zero in exact arithmetic (softmax is
+    # invariant to a per-row constant: ~1e-11 of rounding here): compared in absolute terms
+    errs = sorted(((float((g1[n] - g2[n]).norm() / g2[n].norm().clamp(min=1e-6)), n) for n in g2), reverse=True)
+    worst = errs[0][0]
+    print(f"maskdino {precision}: factor vs full-logit mask losses, loss {l1:.6f} / {l2:.6f}, worst grad rel-L2 "
+          f"{worst:.2e}; {[(f'{e:.1e}', n, float(g2[n].norm())) for e, n in errs[:6]]}")
+    assert worst <= tol
+
+
+def test_factor_matcher_equals_full_logit_matcher():
+    """MaskDINOCriterion.match with the mask costs from the mask head's factors
+    (csrc/match_factors.hip over E_s . F(p)) vs point-sampling the full logits: the same
+    assignment on a bf16 forward (mask features of 128 channels)."""
+    from visionseg.criterion import PaddedTargets
+    from visionseg.data import synthetic_batch
+    from visionseg.maskdino import MaskDINO, MaskDINOCriterion, masks_to_boxes
+    cfg = _tiny(mask_feature_size=128, feature_size=128, hidden_dim=128, dec_heads=4)
+    m = MaskDINO(cfg).init_weights(0).to(DEV).to(torch.bfloat16).train()
+    imgs, ml, cl = synthetic_batch(2, 128, seed=6, device=DEV)
+    tg = PaddedTargets.from_lists(ml, cl, kc=4, device=DEV)
+    boxes = masks_to_boxes(tg.masks)
+    with torch.no_grad():
+        out = m(imgs.to(torch.bfloat16), tg, boxes)
+    pad = out["dn"]["pad"]
+    S = len(out["classes"])
+    cls_m = torch.stack([x[:, pad:] for x in out["classes"]] + [out["interm"]["classes"]])
+    box_m = torch.stack([x[:, pad:] for x in out["boxes"]] + [out["interm"]["boxes"]])
+    masks_m = [x[:, pad:] for x in out["masks"]] + [out["interm"]["masks"]]
+    srcs = [mk._vs_src for mk in out["masks"]] + [out["interm"]["masks"]._vs_src]
+    fulls = out["masks"] + [out["interm"]["masks"]]
+    facs = [(sr[0], sr[1], pad if i < S else 0, None, fulls[i]) for i, sr in enumerate(srcs)]
+    crit = MaskDINOCriterion(cfg)
+    got = []
+    for f in (facs, None):
+        torch.cuda.manual_seed(11)
+        got.append(crit.match(cls_m, box_m, masks_m, tg, boxes, f))
+    assert torch.equal(got[0], got[1])

@@ -426,7 +426,6 @@ def _point_sample_rows(maps, rows, coords):
     materialising maps[rows] (grid_sample's bilinear rule, align_corners=False, zeros
     outside), one HIP thread per point (csrc/mask_head.hip point_sample_rows_kernel); host
     tensors (the CPU criterion tests) take the same rule as four gathers."""
-    from . import _lib as L
     M, H, W = maps.shape
     if not maps.is_cuda:
         flat = maps.reshape(-1)
@@ -443,14 +442,7 @@ def _point_sample_rows(maps, rows, coords):
             idx = base + (yy.clamp(0, H - 1).long() * W + xx.clamp(0, W - 1).long())
             out = out + torch.where(inside, flat[idx], 0.0) * wgt
         return out
-    N, P = coords.shape[:2]
-    mc = maps.float().contiguous()
-    rc = rows.to(torch.int64).contiguous()
-    cc = coords.float().contiguous()
-    out = torch.empty(N, P, device=maps.device, dtype=torch.float32)
-    L.check(L.lib().vs_point_sample_rows(L.ptr(mc), L.ptr(rc), L.ptr(cc), L.ptr(out), M, H, W, N, P,
-                                         L.stream(mc)), "point_sample_rows")
-    return out
+    return ops.point_sample_rows(maps, rows, coords)
 
 
 class MaskDINOCriterion:
@@ -462,10 +454,13 @@ class MaskDINOCriterion:
     criterion.PaddedTargets (+ boxes from masks_to_boxes).  Normalised by the global
     (all-reduced) mean target count, as upstream."""
 
-    def __init__(self, cfg: MaskDINOConfig, matcher: str = "device"):
+    def __init__(self, cfg: MaskDINOConfig, matcher: str = "device", factor_losses: bool = True):
         self.cfg = cfg
         self.matcher = matcher
         self.num_masks_total = None
+        # mask losses through the mask head's factors (ops.RowPointLogitsFunction) when the
+        # logits carry them; False: autograd through the full logits (A/B, tests)
+        self.factor_losses = factor_losses
 
     def _num_boxes(self, tg):
         import torch.distributed as dist
@@ -480,9 +475,12 @@ class MaskDINOCriterion:
         return torch.clamp(n / ws, min=1)
 
     @torch.no_grad()
-    def match(self, cls, box, masks, tg, tboxes):
+    def match(self, cls, box, masks, tg, tboxes, facs=None):
         """cls [S,B,Q,K], box [S,B,Q,4], masks S x [B,Q,H,W], targets (kc >= 1) ->
-        int32 [S,B,Kc]: the query matched to each target (-1 past the image's count)."""
+        int32 [S,B,Kc]: the query matched to each target (-1 past the image's count).
+        facs: per step (E [B, Qt, C], P [B, HW, C], row offset of masks[s] in E, _) when
+        the masks came from the mask head: the point-sampled mask costs are then computed
+        from the factors (csrc/match_factors.hip, as the Mask2Former criterion does)."""
         c = self.cfg
         S, B, Q, _ = cls.shape
         Kc = tg.kc
@@ -498,14 +496,24 @@ class MaskDINOCriterion:
         cost_giou = -generalized_box_iou(box_cxcywh_to_xyxy(box.float()), box_cxcywh_to_xyxy(tb))
         P = c.train_num_points
         grid = (2.0 * torch.rand(B, P, 2, device=dev) - 1.0).unsqueeze(2)
-        pp = torch.stack([F.grid_sample(m.float(), grid, align_corners=False).squeeze(3) for m in masks])
         tp = F.grid_sample(tg.masks.float(), grid, align_corners=False).squeeze(3)          # [B,Kc,P]
-        tpt = tp.transpose(1, 2)[None]
-        cm = torch.matmul(F.softplus(-pp) / P, tpt) + torch.matmul(F.softplus(pp) / P, 1 - tpt)
-        sg = pp.sigmoid()
-        cd = 1 - (2 * torch.matmul(sg, tpt) + 1) / (sg.sum(-1)[..., None] + tp.sum(-1)[None, :, None, :] + 1)
-        cost = (c.class_weight * cost_class + c.box_weight * cost_box + c.giou_weight * cost_giou
-                + c.mask_weight * cm + c.dice_weight * cd)
+        H, W = masks[0].shape[-2:]
+        if (facs is not None and all(f is not None for f in facs) and facs[0][1].dtype == torch.bfloat16
+                and facs[0][0].shape[-1] in (64, 128, 256) and 1 <= Kc <= 16 and facs[0][1].shape[1] == H * W):
+            # mask costs from E_s . F(p): F sampled once at the points, no logit map read
+            E = torch.stack([f[0].detach()[:, f[2]:f[2] + Q] for f in facs]).contiguous()     # [S,B,Q,C]
+            fp = ops.feature_sample_hilo(facs[0][1].detach(), H, W, grid.squeeze(2))
+            zp = torch.zeros(S, B, Q, 1, device=dev)
+            zc = torch.zeros(B, Kc, dtype=torch.int64, device=dev)
+            cmask = ops.match_cost_factors(E, fp, zp, zc, tp, c.mask_weight, 0.0, c.dice_weight)
+        else:
+            pp = torch.stack([F.grid_sample(m.float(), grid, align_corners=False).squeeze(3) for m in masks])
+            tpt = tp.transpose(1, 2)[None]
+            cm = torch.matmul(F.softplus(-pp) / P, tpt) + torch.matmul(F.softplus(pp) / P, 1 - tpt)
+            sg = pp.sigmoid()
+            cd = 1 - (2 * torch.matmul(sg, tpt) + 1) / (sg.sum(-1)[..., None] + tp.sum(-1)[None, :, None, :] + 1)
+            cmask = c.mask_weight * cm + c.dice_weight * cd
+        cost = c.class_weight * cost_class + c.box_weight * cost_box + c.giou_weight * cost_giou + cmask
         cost = torch.nan_to_num(cost.clamp(-1e10, 1e10), 0.0)
         if self.matcher == "device" and cost.is_cuda and Kc <= ops.lsa_max_targets(Q):
             return ops.linear_sum_assignment_padded(cost, tg.counts)
@@ -520,41 +528,59 @@ class MaskDINOCriterion:
                     out[s, b, col] = r
         return torch.from_numpy(out).to(dev)
 
-    def _mask_losses(self, pred, tmask, slot, keep, nb):
+    def _mask_losses(self, pred, tmask, slot, keep, nb, fac=None):
         """pred [B, R, H, W]: the logits of R queries per image; tmask [B, Kc, Ht, Wt] f32
         the targets; slot [B, R] the target slot each query is paired with; keep [B, R]
         bool.  Importance-sampled point BCE and dice (HF:m2f:671-724 semantics).  The
         labels: each query's own target (row b * Kc + slot of the flattened targets)
         sampled at that query's P points (`_point_sample_rows`: fixed shapes whatever the
-        pairing, work and memory independent of Kc)."""
+        pairing, work and memory independent of Kc).  fac = (E [B, Q, C], P [B, HW, C],
+        rows [B, R], sink): the logits came from the mask head and the loss differentiates
+        through its factors on the R selected rows (ops.RowPointLogitsFunction)."""
         c = self.cfg
-        B, R = pred.shape[:2]
+        B, R = slot.shape
         Kc = tmask.shape[1]
         N = B * R
-        pred = pred.reshape(N, 1, *pred.shape[-2:])
+        if fac is not None:
+            # pred is None: the selected rows qrows of the head's full logits `full`
+            E, Pf, qrows, sink, full = fac
+            Esel = torch.gather(E, 1, qrows[..., None].expand(B, R, E.shape[-1]))
+            Qt, H, W = full.shape[1:]
+            flat = full.detach().reshape(-1, H, W)
+            frows = (torch.arange(B, device=qrows.device)[:, None] * Qt + qrows).reshape(N)
+        else:
+            pred = pred.reshape(N, 1, *pred.shape[-2:])
         P = c.train_num_points
+        dev = Esel.device if fac is not None else pred.device
         with torch.no_grad():
             ns, nu = int(P * c.oversample_ratio), int(c.importance_sample_ratio * P)
-            coords = torch.rand(N, ns, 2, device=pred.device)
-            unc = -torch.abs(_point_sample(pred.detach().float(), coords))
+            coords = torch.rand(N, ns, 2, device=dev)
+            if fac is not None:
+                unc = -torch.abs(ops.point_sample_rows(flat, frows, coords))
+            else:
+                unc = -torch.abs(_point_sample(pred.detach().float(), coords))
             top = torch.topk(unc, k=nu, dim=1)[1]
             coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
             if P - nu > 0:
-                coords = torch.cat([coords, torch.rand(N, P - nu, 2, device=pred.device)], 1)
-            rows = (torch.arange(B, device=pred.device)[:, None] * Kc + slot.clamp(0, Kc - 1)).reshape(N)
+                coords = torch.cat([coords, torch.rand(N, P - nu, 2, device=dev)], 1)
+            rows = (torch.arange(B, device=dev)[:, None] * Kc + slot.clamp(0, Kc - 1)).reshape(N)
             lab = _point_sample_rows(tmask.reshape(B * Kc, *tmask.shape[-2:]), rows, coords)
-        logit = _point_sample(pred.float(), coords)
+        if fac is not None:
+            logit = ops.row_point_logits(flat, frows, coords, Esel, Pf, sink)
+        else:
+            logit = _point_sample(pred.float(), coords)
         keep = keep.reshape(N)
-        zero = torch.zeros((), device=pred.device)
+        zero = torch.zeros((), device=dev)
         bce = torch.where(keep, F.binary_cross_entropy_with_logits(logit, lab, reduction="none").mean(1), zero)
         pr = logit.sigmoid()
         dice = torch.where(keep, 1 - (2 * (pr * lab).sum(-1) + 1) / (pr.sum(-1) + lab.sum(-1) + 1), zero)
         return bce.sum() / nb, dice.sum() / nb
 
-    def _pair_losses(self, cls, box, mask, qsel, valid, tg, tmf, tboxes, nb):
+    def _pair_losses(self, cls, box, mask, qsel, valid, tg, tmf, tboxes, nb, fac=None):
         """Losses of one prediction set: cls [B,Q,K], box [B,Q,4], mask [B,Q,H,W]; qsel
         [B,Kc] the query paired with each target slot, valid [B,Kc]; tmf the target masks
-        in f32."""
+        in f32; fac: (E, P, query offset of mask's rows in E, sink) when mask came from the
+        mask head (see _mask_losses)."""
         c = self.cfg
         B, Q, K = cls.shape
         Kc = tg.kc
@@ -571,13 +597,16 @@ class MaskDINOCriterion:
         l_l1 = ((pb - tb).abs().sum(-1) * v).sum() / nb
         giou = torch.diagonal(generalized_box_iou(box_cxcywh_to_xyxy(pb), box_cxcywh_to_xyxy(tb)), dim1=-2, dim2=-1)
         l_giou = ((1 - giou) * v).sum() / nb
-        pm = mask[bidx, qs]                                                           # [B,Kc,H,W]
         slots = torch.arange(Kc, device=cls.device)[None].expand(B, Kc)
-        l_bce, l_dice = self._mask_losses(pm, tmf, slots, valid, nb)
+        if fac is not None:     # the selected rows are read from the full logits
+            pm, mfac = None, (fac[0], fac[1], qs + fac[2], fac[3], fac[4])
+        else:
+            pm, mfac = mask[bidx, qs], None                                           # [B,Kc,H,W]
+        l_bce, l_dice = self._mask_losses(pm, tmf, slots, valid, nb, mfac)
         return dict(loss_ce=c.class_weight * l_cls, loss_bbox=c.box_weight * l_l1, loss_giou=c.giou_weight * l_giou,
                     loss_mask=c.mask_weight * l_bce, loss_dice=c.dice_weight * l_dice)
 
-    def _dn_losses(self, cls, box, mask, dn, tg, tmf, tboxes, nb):
+    def _dn_losses(self, cls, box, mask, dn, tg, tmf, tboxes, nb, fac=None):
         """Denoising queries against the targets they were made from: DN query i <->
         target slot dn["slot"][i] (valid where its group is active and the image has that
         target); normalised by the target count x the number of groups (upstream
@@ -597,7 +626,11 @@ class MaskDINOCriterion:
         l_l1 = ((pb - tb).abs().sum(-1) * v).sum() / nbg
         giou = torch.diagonal(generalized_box_iou(box_cxcywh_to_xyxy(pb), box_cxcywh_to_xyxy(tb)), dim1=-2, dim2=-1)
         l_giou = ((1 - giou) * v).sum() / nbg
-        l_bce, l_dice = self._mask_losses(mask[:, :pad], tmf, sl, valid, nbg)
+        if fac is not None:
+            rows = torch.arange(pad, device=cls.device)[None].expand(B, pad)
+            l_bce, l_dice = self._mask_losses(None, tmf, sl, valid, nbg, (fac[0], fac[1], rows, fac[3], fac[4]))
+        else:
+            l_bce, l_dice = self._mask_losses(mask[:, :pad], tmf, sl, valid, nbg)
         return dict(loss_ce=c.class_weight * l_cls, loss_bbox=c.box_weight * l_l1, loss_giou=c.giou_weight * l_giou,
                     loss_mask=c.mask_weight * l_bce, loss_dice=c.dice_weight * l_dice)
 
@@ -624,16 +657,30 @@ class MaskDINOCriterion:
                 losses[f"loss_ce{nm}"] = l
                 total = total + l
             return total, losses
-        assign = self.match(cls_m.detach(), box_m.detach(), [m.detach() for m in masks_m], tg, boxes)
+        # the mask head's factors of every step (E, P), when the logits came from it with one
+        # shared pixel embedding: the matcher's mask costs and the mask losses then use the
+        # factors (the losses differentiate through the selected rows only; P goes through
+        # one GradSink so the calls sum dP in place)
+        srcs = [getattr(m, "_vs_src", None) for m in out["masks"]] + [getattr(out["interm"]["masks"], "_vs_src", None)]
+        facs = [None] * len(srcs)
+        if (self.factor_losses and all(sr is not None for sr in srcs) and all(sr[1] is srcs[0][1] for sr in srcs)
+                and srcs[0][1].is_cuda):
+            sink = ops.GradSink() if torch.is_grad_enabled() else None
+            P = sink.source(srcs[0][1]) if sink is not None else srcs[0][1]
+            fulls = out["masks"] + [out["interm"]["masks"]]
+            facs = [(sr[0], P, pad if i < S else 0, sink, fulls[i]) for i, sr in enumerate(srcs)]
+        assign = self.match(cls_m.detach(), box_m.detach(), [m.detach() for m in masks_m], tg, boxes,
+                            facs if facs[0] is not None else None)
         valid = tg.valid()
         tmf = tg.masks.float()                         # the targets as f32 once per step
         for s, nm in enumerate(names):
             part = self._pair_losses(cls_m[s], box_m[s], masks_m[s], assign[s].long(), valid & (assign[s] >= 0),
-                                     tg, tmf, boxes, nb)
+                                     tg, tmf, boxes, nb, facs[s])
             losses.update({k + nm: v for k, v in part.items()})
         if dn:
             for s in range(S):
-                part = self._dn_losses(out["classes"][s], out["boxes"][s], out["masks"][s], dn, tg, tmf, boxes, nb)
+                part = self._dn_losses(out["classes"][s], out["boxes"][s], out["masks"][s], dn, tg, tmf, boxes, nb,
+                                       facs[s])
                 nm = "_dn" if s == S - 1 else f"_dn_{s}"
                 losses.update({k + nm: v for k, v in part.items()})
         total = sum(losses.values())

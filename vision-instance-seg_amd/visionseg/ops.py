@@ -633,6 +633,86 @@ def mask_head_grouped(E, F_nhwc, height: int, width: int, group: int):
     return out
 
 
+class RowPointLogitsFunction(torch.autograd.Function):
+    """Point samples of SELECTED rows of one mask-head output, differentiable w.r.t. the
+    head's factors: the single-step form of MatchedPointLogitsFunction for a criterion
+    that pairs R queries per image with targets (MaskDINO: the matched queries of a step,
+    or its denoising queries).  logits [M, H, W] detached f32 (the head's output, all rows),
+    rows int64 [B*R] (the selected row of each point set), coords [B*R, n, 2] in [0, 1),
+    Esel [B, R, C] the selected rows' mask embeddings, P [B, HW, C] -> [B*R, n]; the forward
+    gathers the points straight from the selected rows (csrc/mask_head.hip
+    point_sample_rows_kernel: no copy of the selected maps).  Backward: point gradients
+    scattered into [B, R, H, W] (point_scatter, no
+    atomics), the mask head's adjoint on those R rows only (the fused bf16 backward, dP
+    accumulated in `sink`'s buffer when one is given) -- instead of grid_sample's atomic
+    backward over the maps and the mask-head backward over all Q rows of a zero-filled
+    full-size gradient."""
+
+    @staticmethod
+    def forward(ctx, logits, rows, coords, Esel, P, sink=None):
+        M, H, W = logits.shape
+        B, R = Esel.shape[:2]
+        out = point_sample_rows(logits, rows, coords)
+        grid = 2.0 * coords.unsqueeze(2) - 1.0
+        ctx.save_for_backward(grid, Esel, P)
+        ctx.geom = (B, R, H, W)
+        ctx.sink = sink
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        grid, Esel, P = ctx.saved_tensors
+        B, R, H, W = ctx.geom
+        n = g.shape[-1]
+        G = torch.empty(B, R, H, W, device=g.device, dtype=torch.float32)
+        gc = g.float().contiguous()
+        gr = grid.contiguous()
+        with timed("point_scatter", gc, bytes_=gc.numel() * 12 + G.numel() * 4):
+            L.check(L.lib().vs_point_scatter(L.ptr(gc), L.ptr(gr), L.ptr(G), 1, B, R, n, H, W, L.stream(gc)),
+                    "point_scatter")
+        C = Esel.shape[-1]
+        sink = ctx.sink
+        if P.dtype == torch.bfloat16 and C in (128, 256):
+            acc = sink is not None and sink.buf is not None
+            if sink is not None and not acc:
+                sink.buf = torch.empty_like(P)
+            dP = sink.buf if sink is not None else torch.empty_like(P)
+            Ec = Esel.contiguous()
+            with timed("mask_head_bwd", Ec, bytes_=G.numel() * 4 + (Ec.numel() * 2 + P.numel() * 2) * 2,
+                       flops=4.0 * B * R * C * H * W):
+                dE = L.tops().mask_head_bwd(G, Ec, P, dP, bool(acc))
+            return None, None, None, dE, (None if sink is not None else dP), None
+        Gb = G.view(B, R, H * W).to(P.dtype)
+        dE = torch.bmm(Gb, P)
+        dP = torch.bmm(Gb.transpose(1, 2), Esel.to(P.dtype))
+        if sink is not None:
+            sink.buf = dP if sink.buf is None else sink.buf + dP
+            dP = None
+        return None, None, None, dE.to(Esel.dtype), dP, None
+
+
+def row_point_logits(logits, rows, coords, Esel, P, sink=None):
+    """RowPointLogitsFunction (device tensors; sink: a GradSink whose source P is)."""
+    return RowPointLogitsFunction.apply(logits, rows, coords, Esel, P, sink)
+
+
+def point_sample_rows(maps, rows, coords):
+    """maps f32 [M, H, W], rows int64 [N], coords f32 [N, P, 2] in [0, 1] -> [N, P]: the
+    bilinear sample (grid_sample, align_corners=False, zeros) of map rows[n] at each of its
+    points (csrc/mask_head.hip point_sample_rows_kernel)."""
+    L.require_hip(maps, rows, coords)
+    M, H, W = maps.shape
+    N, P = coords.shape[:2]
+    mc = maps.float().contiguous()
+    rc = rows.to(torch.int64).contiguous()
+    cc = coords.float().contiguous()
+    out = torch.empty(N, P, device=maps.device, dtype=torch.float32)
+    with timed("point_sample_rows", mc, bytes_=cc.numel() * 4 + out.numel() * 4 * 5):
+        L.check(L.lib().vs_point_sample_rows(L.ptr(mc), L.ptr(rc), L.ptr(cc), L.ptr(out), M, H, W, N, P,
+                                             L.stream(mc)), "point_sample_rows")
+    return out
+
+
 def matched_maps(masks_list, qsel):
     """(maps [S*B*Kc, 1, H, W] f32 of mask_list[s][b, qsel[s, b, k]], factors): detached
     maps + the mask head's factors (E, P) when every step's logits came from `mask_head`
