@@ -263,3 +263,41 @@ def test_point_sample_rows_matches_grid_sample():
     exp = _point_sample(maps[rows][:, None], coords)
     got = _point_sample_rows(maps, rows, coords)
     assert float((got - exp).abs().max()) <= 1e-6
+
+
+def test_criterion_vectorised_equals_per_step():
+    """The criterion's class / box losses computed for all decoder steps at once (and the
+    DN set's) equal the per-step formulation (`_pair_losses` / `_dn_losses`, one call per
+    step) component by component, on the same matching and point draws."""
+    cfg = _tiny_cfg()
+    dec = MaskDINODecoder(cfg)
+    ml, cl = _targets()
+    tg = PaddedTargets.from_lists(ml, cl, kc=4)
+    boxes = masks_to_boxes(tg.masks)
+    out = _fake_outputs(cfg, tg, boxes, dec, 2)
+    crit = MaskDINOCriterion(cfg, matcher="host")
+    torch.manual_seed(5)
+    _, parts = crit(out, tg, boxes)
+    # the per-step reference, same RNG order: matcher, then the pair sets, then the DN sets
+    torch.manual_seed(5)
+    pad = out["dn"]["pad"]
+    S = len(out["classes"])
+    cls_m = torch.stack([x[:, pad:] for x in out["classes"]] + [out["interm"]["classes"]])
+    box_m = torch.stack([x[:, pad:] for x in out["boxes"]] + [out["interm"]["boxes"]])
+    masks_m = [x[:, pad:] for x in out["masks"]] + [out["interm"]["masks"]]
+    nb = crit._num_boxes(tg)
+    assign = crit.match(cls_m.detach(), box_m.detach(), [m.detach() for m in masks_m], tg, boxes)
+    valid, tmf = tg.valid(), tg.masks.float()
+    ref = {}
+    names = [("" if s == S - 1 else f"_{s}") for s in range(S)] + ["_interm"]
+    for s, nm in enumerate(names):
+        part = crit._pair_losses(cls_m[s], box_m[s], masks_m[s], assign[s].long(), valid & (assign[s] >= 0), tg, tmf,
+                                 boxes, nb)
+        ref.update({k + nm: v for k, v in part.items()})
+    for s in range(S):
+        part = crit._dn_losses(out["classes"][s], out["boxes"][s], out["masks"][s], out["dn"], tg, tmf, boxes, nb)
+        ref.update({k + ("_dn" if s == S - 1 else f"_dn_{s}"): v for k, v in part.items()})
+    assert set(parts) == set(ref)
+    for k in ref:
+        a, b = float(parts[k]), float(ref[k])
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), (k, a, b)

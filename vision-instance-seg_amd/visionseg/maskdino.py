@@ -104,6 +104,20 @@ def generalized_box_iou(a, b):
     return iou - (area - union) / area.clamp(min=1e-7)
 
 
+def paired_giou(a, b):
+    """GIoU of xyxy boxes a and b paired elementwise ([..., 4] each, broadcastable) -> [...]:
+    the diagonal of generalized_box_iou without the pairwise matrix."""
+    area_a = (a[..., 2] - a[..., 0]) * (a[..., 3] - a[..., 1])
+    area_b = (b[..., 2] - b[..., 0]) * (b[..., 3] - b[..., 1])
+    wh = (torch.minimum(a[..., 2:], b[..., 2:]) - torch.maximum(a[..., :2], b[..., :2])).clamp(min=0)
+    inter = wh[..., 0] * wh[..., 1]
+    union = area_a + area_b - inter
+    iou = inter / union.clamp(min=1e-7)
+    wh2 = (torch.maximum(a[..., 2:], b[..., 2:]) - torch.minimum(a[..., :2], b[..., :2])).clamp(min=0)
+    area = wh2[..., 0] * wh2[..., 1]
+    return iou - (area - union) / area.clamp(min=1e-7)
+
+
 def masks_to_boxes(masks):
     """bool [..., H, W] -> normalised (cx, cy, w, h) [..., 4] of each mask's pixel bounds
     (the detectron2 gt_boxes of a polygon instance); empty masks give zeros.  On the
@@ -606,6 +620,28 @@ class MaskDINOCriterion:
         return dict(loss_ce=c.class_weight * l_cls, loss_bbox=c.box_weight * l_l1, loss_giou=c.giou_weight * l_giou,
                     loss_mask=c.mask_weight * l_bce, loss_dice=c.dice_weight * l_dice)
 
+    def _cls_box_losses(self, cls, box, qsel, valid, tcls, tboxes, norm):
+        """Focal class, L1 and GIoU losses of S prediction sets at once (one launch per op
+        for all decoder steps instead of one per step): cls [S,B,Q,K], box [S,B,Q,4]; qsel
+        [S,B,R] the query paired with each of R targets (tcls [B,R] classes, tboxes [B,R,4]),
+        valid [S,B,R]; norm: scalar or [S].  -> (l_cls, l_l1, l_giou) each [S] (unweighted)."""
+        c = self.cfg
+        S, B, Q, K = cls.shape
+        R = qsel.shape[-1]
+        onehot = torch.zeros(S, B, Q + 1, K, device=cls.device, dtype=cls.dtype)
+        qi = torch.where(valid, qsel, torch.full_like(qsel, Q))
+        onehot.scatter_(2, qi[..., None].expand(S, B, R, K),
+                        F.one_hot(tcls, K).to(cls.dtype)[None].expand(S, B, R, K) * valid[..., None].to(cls.dtype))
+        l_cls = sigmoid_focal_loss(cls, onehot[:, :, :Q], c.focal_alpha).sum((1, 2, 3)) / norm
+        qs = qsel.clamp(0, Q - 1)
+        pb = torch.gather(box, 2, qs[..., None].expand(S, B, R, 4)).float()
+        tb = tboxes.float()[None]
+        v = valid.float()
+        l_l1 = ((pb - tb).abs().sum(-1) * v).sum((1, 2)) / norm
+        giou = paired_giou(box_cxcywh_to_xyxy(pb), box_cxcywh_to_xyxy(tb))
+        l_giou = ((1 - giou) * v).sum((1, 2)) / norm
+        return l_cls, l_l1, l_giou
+
     def _dn_losses(self, cls, box, mask, dn, tg, tmf, tboxes, nb, fac=None):
         """Denoising queries against the targets they were made from: DN query i <->
         target slot dn["slot"][i] (valid where its group is active and the image has that
@@ -673,15 +709,52 @@ class MaskDINOCriterion:
                             facs if facs[0] is not None else None)
         valid = tg.valid()
         tmf = tg.masks.float()                         # the targets as f32 once per step
+        c = self.cfg
+        Kc = tg.kc
+        qsel = assign.long()
+        vs = valid[None] & (assign >= 0)                                               # [S+1,B,Kc]
+        l_cls, l_l1, l_giou = self._cls_box_losses(cls_m, box_m, qsel, vs, tg.classes, boxes, nb)
+        B = cls_m.shape[1]
+        slots = torch.arange(Kc, device=cls_m.device)[None].expand(B, Kc)
         for s, nm in enumerate(names):
-            part = self._pair_losses(cls_m[s], box_m[s], masks_m[s], assign[s].long(), valid & (assign[s] >= 0),
-                                     tg, tmf, boxes, nb, facs[s])
-            losses.update({k + nm: v for k, v in part.items()})
+            if facs[s] is not None:     # the selected rows are read from the full logits
+                qs = qsel[s].clamp(0, masks_m[s].shape[1] - 1)
+                mfac = (facs[s][0], facs[s][1], qs + facs[s][2], facs[s][3], facs[s][4])
+                l_bce, l_dice = self._mask_losses(None, tmf, slots, vs[s], nb, mfac)
+            else:
+                bidx = torch.arange(B, device=cls_m.device)[:, None].expand(B, Kc)
+                pm = masks_m[s][bidx, qsel[s].clamp(0, masks_m[s].shape[1] - 1)]
+                l_bce, l_dice = self._mask_losses(pm, tmf, slots, vs[s], nb)
+            losses.update({"loss_ce" + nm: c.class_weight * l_cls[s], "loss_bbox" + nm: c.box_weight * l_l1[s],
+                           "loss_giou" + nm: c.giou_weight * l_giou[s], "loss_mask" + nm: c.mask_weight * l_bce,
+                           "loss_dice" + nm: c.dice_weight * l_dice})
         if dn:
+            pad, slot, dvalid, active = dn["pad"], dn["slot"], dn["valid"], dn["active"]
+            nbg = nb * dn["groups"].clamp(min=1).float()
+            sl = slot[None].expand(B, pad)
+            tcls = torch.gather(tg.classes, 1, sl)
+            K = cls_m.shape[-1]
+            cls_d = torch.stack([x[:, :pad] for x in out["classes"]])                   # [S,B,pad,K]
+            box_d = torch.stack([x[:, :pad] for x in out["boxes"]]).float()
+            # class loss over the active DN queries (padding slots as negatives), L1 / GIoU
+            # on the valid ones: DN query i <-> target slot slot[i]
+            onehot = F.one_hot(tcls, K).to(cls_d.dtype) * dvalid[..., None].to(cls_d.dtype)
+            focal = sigmoid_focal_loss(cls_d, onehot[None].expand_as(cls_d), c.focal_alpha)
+            d_cls = (focal * active[None, None, :, None].to(focal.dtype)).sum((1, 2, 3)) / nbg
+            tb = torch.gather(boxes.float(), 1, sl[..., None].expand(B, pad, 4))[None]
+            v = dvalid.float()[None]
+            d_l1 = ((box_d - tb).abs().sum(-1) * v).sum((1, 2)) / nbg
+            d_giou = ((1 - paired_giou(box_cxcywh_to_xyxy(box_d), box_cxcywh_to_xyxy(tb))) * v).sum((1, 2)) / nbg
+            rows = torch.arange(pad, device=cls_m.device)[None].expand(B, pad)
             for s in range(S):
-                part = self._dn_losses(out["classes"][s], out["boxes"][s], out["masks"][s], dn, tg, tmf, boxes, nb,
-                                       facs[s])
+                if facs[s] is not None:
+                    l_bce, l_dice = self._mask_losses(None, tmf, sl, dvalid, nbg,
+                                                      (facs[s][0], facs[s][1], rows, facs[s][3], facs[s][4]))
+                else:
+                    l_bce, l_dice = self._mask_losses(out["masks"][s][:, :pad], tmf, sl, dvalid, nbg)
                 nm = "_dn" if s == S - 1 else f"_dn_{s}"
-                losses.update({k + nm: v for k, v in part.items()})
+                losses.update({"loss_ce" + nm: c.class_weight * d_cls[s], "loss_bbox" + nm: c.box_weight * d_l1[s],
+                               "loss_giou" + nm: c.giou_weight * d_giou[s], "loss_mask" + nm: c.mask_weight * l_bce,
+                               "loss_dice" + nm: c.dice_weight * l_dice})
         total = sum(losses.values())
         return total, losses
