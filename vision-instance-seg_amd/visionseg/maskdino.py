@@ -590,6 +590,51 @@ class MaskDINOCriterion:
         dice = torch.where(keep, 1 - (2 * (pr * lab).sum(-1) + 1) / (pr.sum(-1) + lab.sum(-1) + 1), zero)
         return bce.sum() / nb, dice.sum() / nb
 
+    def _mask_losses_steps(self, steps, tmask, slot, keep, norm):
+        """_mask_losses of S prediction sets from the mask head's factors in one pass:
+        steps = [(E [B, Qt, C], P, qrows [B, R], sink, full logits [B, Qt, H, W])] (one P and
+        sink for all), slot [B, R] the target slot of each selected query (the same for
+        every step), keep [S, B, R] bool, norm scalar or [S] -> (bce [S], dice [S]).  The
+        points are drawn per step in the per-step order (oversampled, then the uniform
+        remainder), so a step sees the draws _mask_losses would give it."""
+        c = self.cfg
+        S = len(steps)
+        B, R = slot.shape
+        Kc = tmask.shape[1]
+        N = B * R
+        P_f, sink = steps[0][1], steps[0][3]
+        dev = slot.device
+        flats, frows, esel = [], [], []
+        for E, _, qrows, _, full in steps:
+            Qt, H, W = full.shape[1:]
+            flats.append(full.detach().reshape(-1, H, W))
+            frows.append((torch.arange(B, device=dev)[:, None] * Qt + qrows).reshape(N))
+            esel.append(torch.gather(E, 1, qrows[..., None].expand(B, R, E.shape[-1])))
+        Esel = torch.stack(esel, 1).reshape(B, S * R, -1)                      # image-major, step-major rows
+        Pn = c.train_num_points
+        ns, nu = int(Pn * c.oversample_ratio), int(c.importance_sample_ratio * Pn)
+        with torch.no_grad():
+            over, rest = [], []
+            for _ in range(S):
+                over.append(torch.rand(N, ns, 2, device=dev))
+                if Pn - nu > 0:
+                    rest.append(torch.rand(N, Pn - nu, 2, device=dev))
+            coords = torch.cat(over, 0)                                        # [S*N, ns, 2]
+            unc = torch.cat([-torch.abs(ops.point_sample_rows(fl, fr, co)) for fl, fr, co in zip(flats, frows, over)])
+            top = torch.topk(unc, k=nu, dim=1)[1]
+            coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
+            if rest:
+                coords = torch.cat([coords, torch.cat(rest, 0)], 1)
+            rows = (torch.arange(B, device=dev)[:, None] * Kc + slot.clamp(0, Kc - 1)).reshape(1, N).expand(S, N)
+            lab = _point_sample_rows(tmask.reshape(B * Kc, *tmask.shape[-2:]), rows.reshape(S * N), coords)
+        logit = ops.step_row_point_logits(flats, torch.stack(frows), coords, Esel, P_f, sink)
+        keep = keep.reshape(S * N)
+        zero = torch.zeros((), device=dev)
+        bce = torch.where(keep, F.binary_cross_entropy_with_logits(logit, lab, reduction="none").mean(1), zero)
+        pr = logit.sigmoid()
+        dice = torch.where(keep, 1 - (2 * (pr * lab).sum(-1) + 1) / (pr.sum(-1) + lab.sum(-1) + 1), zero)
+        return bce.view(S, N).sum(1) / norm, dice.view(S, N).sum(1) / norm
+
     def _pair_losses(self, cls, box, mask, qsel, valid, tg, tmf, tboxes, nb, fac=None):
         """Losses of one prediction set: cls [B,Q,K], box [B,Q,4], mask [B,Q,H,W]; qsel
         [B,Kc] the query paired with each target slot, valid [B,Kc]; tmf the target masks
@@ -716,11 +761,13 @@ class MaskDINOCriterion:
         l_cls, l_l1, l_giou = self._cls_box_losses(cls_m, box_m, qsel, vs, tg.classes, boxes, nb)
         B = cls_m.shape[1]
         slots = torch.arange(Kc, device=cls_m.device)[None].expand(B, Kc)
+        if facs[0] is not None:         # the selected rows of every step, read from the full logits
+            steps = [(f[0], f[1], qsel[s].clamp(0, masks_m[s].shape[1] - 1) + f[2], f[3], f[4])
+                     for s, f in enumerate(facs)]
+            m_bce, m_dice = self._mask_losses_steps(steps, tmf, slots, vs, nb)
         for s, nm in enumerate(names):
-            if facs[s] is not None:     # the selected rows are read from the full logits
-                qs = qsel[s].clamp(0, masks_m[s].shape[1] - 1)
-                mfac = (facs[s][0], facs[s][1], qs + facs[s][2], facs[s][3], facs[s][4])
-                l_bce, l_dice = self._mask_losses(None, tmf, slots, vs[s], nb, mfac)
+            if facs[0] is not None:
+                l_bce, l_dice = m_bce[s], m_dice[s]
             else:
                 bidx = torch.arange(B, device=cls_m.device)[:, None].expand(B, Kc)
                 pm = masks_m[s][bidx, qsel[s].clamp(0, masks_m[s].shape[1] - 1)]
@@ -746,10 +793,12 @@ class MaskDINOCriterion:
             d_l1 = ((box_d - tb).abs().sum(-1) * v).sum((1, 2)) / nbg
             d_giou = ((1 - paired_giou(box_cxcywh_to_xyxy(box_d), box_cxcywh_to_xyxy(tb))) * v).sum((1, 2)) / nbg
             rows = torch.arange(pad, device=cls_m.device)[None].expand(B, pad)
+            if facs[0] is not None:
+                steps = [(facs[s][0], facs[s][1], rows, facs[s][3], facs[s][4]) for s in range(S)]
+                d_bce, d_dice = self._mask_losses_steps(steps, tmf, sl, dvalid[None].expand(S, B, pad), nbg)
             for s in range(S):
-                if facs[s] is not None:
-                    l_bce, l_dice = self._mask_losses(None, tmf, sl, dvalid, nbg,
-                                                      (facs[s][0], facs[s][1], rows, facs[s][3], facs[s][4]))
+                if facs[0] is not None:
+                    l_bce, l_dice = d_bce[s], d_dice[s]
                 else:
                     l_bce, l_dice = self._mask_losses(out["masks"][s][:, :pad], tmf, sl, dvalid, nbg)
                 nm = "_dn" if s == S - 1 else f"_dn_{s}"

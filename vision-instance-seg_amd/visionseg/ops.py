@@ -691,6 +691,69 @@ class RowPointLogitsFunction(torch.autograd.Function):
         return None, None, None, dE.to(Esel.dtype), dP, None
 
 
+class StepRowPointLogitsFunction(torch.autograd.Function):
+    """RowPointLogitsFunction for S prediction sets at once (MaskDINO: the matched queries
+    of every decoder step, or the denoising queries of every step): logits = S detached
+    f32 [M_s, H, W] maps, rows int64 [S, B*R] (each set's selected row in its step's maps),
+    coords [S*B*R, n, 2], Esel [B, S*R, C] (image b's selected rows, step-major), P
+    [B, HW, C] -> [S*B*R, n] (set order (s, b, r)).  Backward: ONE point scatter into
+    [B, S*R, H, W] and ONE mask-head adjoint over the S*R rows (instead of S of each: the
+    fused kernel reads P once, not S times)."""
+
+    @staticmethod
+    def forward(ctx, rows, coords, Esel, P, sink, *logits):
+        S = len(logits)
+        H, W = logits[0].shape[-2:]
+        B, SR = Esel.shape[:2]
+        R = SR // S
+        n = coords.shape[1]
+        out = torch.empty(S * B * R, n, device=coords.device, dtype=torch.float32)
+        for s_, lg in enumerate(logits):
+            out[s_ * B * R:(s_ + 1) * B * R] = point_sample_rows(lg, rows[s_], coords[s_ * B * R:(s_ + 1) * B * R])
+        grid = 2.0 * coords.unsqueeze(2) - 1.0
+        ctx.save_for_backward(grid, Esel, P)
+        ctx.geom = (S, B, R, H, W)
+        ctx.sink = sink
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        grid, Esel, P = ctx.saved_tensors
+        S, B, R, H, W = ctx.geom
+        n = g.shape[-1]
+        G = torch.empty(B, S * R, H, W, device=g.device, dtype=torch.float32)
+        gc = g.float().contiguous()
+        gr = grid.contiguous()
+        with timed("point_scatter", gc, bytes_=gc.numel() * 12 + G.numel() * 4):
+            L.check(L.lib().vs_point_scatter(L.ptr(gc), L.ptr(gr), L.ptr(G), S, B, R, n, H, W, L.stream(gc)),
+                    "point_scatter")
+        C = Esel.shape[-1]
+        sink = ctx.sink
+        nones = (None,) * S
+        if P.dtype == torch.bfloat16 and C in (128, 256):
+            acc = sink is not None and sink.buf is not None
+            if sink is not None and not acc:
+                sink.buf = torch.empty_like(P)
+            dP = sink.buf if sink is not None else torch.empty_like(P)
+            Ec = Esel.contiguous()
+            with timed("mask_head_bwd", Ec, bytes_=G.numel() * 4 + (Ec.numel() * 2 + P.numel() * 2) * 2,
+                       flops=4.0 * B * S * R * C * H * W):
+                dE = L.tops().mask_head_bwd(G, Ec, P, dP, bool(acc))
+            return (None, None, dE, (None if sink is not None else dP), None) + nones
+        Gb = G.view(B, S * R, H * W).to(P.dtype)
+        dE = torch.bmm(Gb, P)
+        dP = torch.bmm(Gb.transpose(1, 2), Esel.to(P.dtype))
+        if sink is not None:
+            sink.buf = dP if sink.buf is None else sink.buf + dP
+            dP = None
+        return (None, None, dE.to(Esel.dtype), dP, None) + nones
+
+
+def step_row_point_logits(logits, rows, coords, Esel, P, sink=None):
+    """StepRowPointLogitsFunction (logits: a list of S detached [M_s, H, W] maps)."""
+    return StepRowPointLogitsFunction.apply(rows, coords, Esel, P, sink, *logits)
+
+
 def row_point_logits(logits, rows, coords, Esel, P, sink=None):
     """RowPointLogitsFunction (device tensors; sink: a GradSink whose source P is)."""
     return RowPointLogitsFunction.apply(logits, rows, coords, Esel, P, sink)
