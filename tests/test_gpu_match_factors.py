@@ -212,3 +212,28 @@ def test_factored_criterion_equals_materialised():
     for i in (2, 3):
         a, b = out[0][i], out[1][i]
         assert float((a - b).abs().max()) <= 1e-2 * float(b.abs().max())
+
+
+@pytest.mark.parametrize("C", [64, 128])
+def test_tiny_bf16_train_step_factored_or_not(C):
+    """A bf16 Trainer step of a tiny Swin + Mask2Former (the smoke() model): mask features of
+    64 channels keep the full-resolution logits (the grouped matched-maps kernel takes 128 /
+    256), 128 channels take the factored path; both give finite losses and move the weights."""
+    from visionseg import ops
+    from visionseg.criterion import SetCriterion
+    from visionseg.data import synthetic_batch
+    from visionseg.model import M2FConfig, Mask2Former
+    from visionseg.train import SolverConfig, Trainer
+    cfg = M2FConfig(embed_dim=32, depths=(2, 2, 2, 2), num_heads=(1, 2, 4, 8), feature_size=C, mask_feature_size=C,
+                    hidden_dim=C, enc_ffn=128, dec_ffn=128, dec_heads=C // 32, enc_layers=2, dec_layers=4,
+                    num_queries=10, train_num_points=256)
+    m = Mask2Former(cfg).init_weights(0)
+    tr = Trainer(m, SetCriterion(cfg), SolverConfig(warmup_iters=0), device=DEV)
+    imgs, ml, cl = synthetic_batch(2, 128, seed=0)
+    w0 = tr.opt.master.clone()
+    loss = tr.step(imgs.to(DEV), [x.to(DEV) for x in ml], [x.to(DEV) for x in cl])
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss) and bool(torch.isfinite(tr.opt.master).all())
+    assert float((tr.opt.master - w0).abs().max()) > 0
+    with torch.no_grad():
+        _ = ops  # the path taken is internal; the step must work either way

@@ -621,7 +621,9 @@ class MaskDINOCriterion:
                     rest.append(torch.rand(N, Pn - nu, 2, device=dev))
             coords = torch.cat(over, 0)                                        # [S*N, ns, 2]
             unc = torch.cat([-torch.abs(ops.point_sample_rows(fl, fr, co)) for fl, fr, co in zip(flats, frows, over)])
-            top = torch.topk(unc, k=nu, dim=1)[1]
+            # top-k per step: one call over all S * N rows takes a path that cannot be captured
+            # in a HIP graph (hipErrorStreamCaptureUnsupported at C4's DN set, 4000 rows)
+            top = torch.cat([torch.topk(unc[i * N:(i + 1) * N], k=nu, dim=1)[1] for i in range(S)])
             coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
             if rest:
                 coords = torch.cat([coords, torch.cat(rest, 0)], 1)

@@ -655,7 +655,8 @@ class Decoder(nn.Module):
         h = self.query_feat.weight.unsqueeze(0).expand(B, -1, -1)
         n = len(self.layers)
 
-        fact = batched and self.factored_masks and mf.dtype == torch.bfloat16 and mf.shape[-1] in (64, 128, 256)
+        # (C in {128, 256}: the grouped mask-head kernel of the matched maps)
+        fact = batched and self.factored_masks and mf.dtype == torch.bfloat16 and mf.shape[-1] in (128, 256)
         mf_levels = {}
 
         def step(hh, target_hw):
