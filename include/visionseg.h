@@ -284,6 +284,13 @@ VS_API int vs_point_scatter(const float* grad_points, const float* grid, float* 
 VS_API int vs_point_sample_rows(const float* maps, const long long* rows, const float* coords, float* out,
                                 int num_maps, int height, int width, int num_sets, int num_points, void* stream);
 
+/* Row-wise top-k indices for the importance sampling of the mask losses (the `topk` of
+ * HF:m2f:689-724 sample_points_using_uncertainty, MaskDINO's copy of it): indices int64
+ * [rows, k] = the positions of the k largest of values f32 [rows, n], per row, in ascending
+ * index order (radix select, csrc/topk.hip).  The same set as torch.topk when the k-th
+ * largest value is unique in its row; among ties at the threshold the lowest indices. */
+VS_API int vs_topk_rows(const float* values, long long* indices, int rows, int n, int k, void* stream);
+
 /* Attention bitmask of the next decoder layer (HF:m2f:2049-2055 + row fix 1912-1914):
  * bilinear (align_corners=False) resize of each logits row [H, W] to [th, tw], key k
  * blocked iff sigmoid(v) < 0.5, stored as bit k%32 of words[row, k/32]

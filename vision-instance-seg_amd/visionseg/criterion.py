@@ -267,8 +267,8 @@ class SetCriterion:
                 unc = -torch.abs(_sample(pred.detach().float(), coords))
                 select = getattr(self.point_source, "select", None)
                 if select is None:
-                    top = torch.topk(unc, k=nu, dim=1)[1]
-                else:               # parity hook, rows keyed (step, image, target slot)
+                    top = ops.topk_rows(unc, nu) if unc.is_cuda else torch.topk(unc, k=nu, dim=1)[1]
+                else:              # parity hook, rows keyed (step, image, target slot)
                     keys = (torch.arange(S).repeat_interleave(B * Kc), torch.arange(B).repeat_interleave(Kc).repeat(S),
                             torch.arange(Kc).repeat(S * B))
                     top = select(unc, nu, *keys)

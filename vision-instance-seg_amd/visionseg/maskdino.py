@@ -573,7 +573,7 @@ class MaskDINOCriterion:
                 unc = -torch.abs(ops.point_sample_rows(flat, frows, coords))
             else:
                 unc = -torch.abs(_point_sample(pred.detach().float(), coords))
-            top = torch.topk(unc, k=nu, dim=1)[1]
+            top = ops.topk_rows(unc, nu) if unc.is_cuda else torch.topk(unc, k=nu, dim=1)[1]
             coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
             if P - nu > 0:
                 coords = torch.cat([coords, torch.rand(N, P - nu, 2, device=dev)], 1)
@@ -621,9 +621,9 @@ class MaskDINOCriterion:
                     rest.append(torch.rand(N, Pn - nu, 2, device=dev))
             coords = torch.cat(over, 0)                                        # [S*N, ns, 2]
             unc = torch.cat([-torch.abs(ops.point_sample_rows(fl, fr, co)) for fl, fr, co in zip(flats, frows, over)])
-            # top-k per step: one call over all S * N rows takes a path that cannot be captured
-            # in a HIP graph (hipErrorStreamCaptureUnsupported at C4's DN set, 4000 rows)
-            top = torch.cat([torch.topk(unc[i * N:(i + 1) * N], k=nu, dim=1)[1] for i in range(S)])
+            # one radix select over all S * N rows (torch.topk here sorts per step -- one call
+            # over all rows is not capturable in a HIP graph -- ~6 ms of the C4 step)
+            top = ops.topk_rows(unc, nu)
             coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
             if rest:
                 coords = torch.cat([coords, torch.cat(rest, 0)], 1)

@@ -776,6 +776,20 @@ def point_sample_rows(maps, rows, coords):
     return out
 
 
+def topk_rows(values, k):
+    """values f32 [N, n] -> int64 [N, k]: per row the indices of the k largest values, in
+    ascending index order (csrc/topk.hip radix select; replaces `torch.topk(values, k)[1]`
+    of the importance sampling, HF:m2f:689-724 -- the points are used as a set)."""
+    L.require_hip(values)
+    vc = values.float().contiguous()
+    N, n = vc.shape
+    assert 0 < k <= n
+    out = torch.empty(N, k, device=vc.device, dtype=torch.int64)
+    with timed("topk_rows", vc, bytes_=vc.numel() * 4 * 5 + out.numel() * 8):
+        L.check(L.lib().vs_topk_rows(L.ptr(vc), L.ptr(out), N, n, k, L.stream(vc)), "topk_rows")
+    return out
+
+
 def matched_maps(masks_list, qsel):
     """(maps [S*B*Kc, 1, H, W] f32 of mask_list[s][b, qsel[s, b, k]], factors): detached
     maps + the mask head's factors (E, P) when every step's logits came from `mask_head`
