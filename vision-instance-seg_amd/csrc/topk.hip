@@ -115,22 +115,30 @@ constexpr int kTkLdsKeys = 39424;              // 154 KiB of keys + the histogra
 
 __global__ void __launch_bounds__(kTkLdsThreads) topk_rows_lds_kernel(const float* __restrict__ x,
                                                                       long long* __restrict__ idx, int n, int k) {
-  __shared__ unsigned keys[kTkLdsKeys];
+  __shared__ __attribute__((aligned(16))) unsigned keys[kTkLdsKeys];
   __shared__ unsigned hist[256];
-  __shared__ unsigned s_prefix, s_need, s_base;
-  __shared__ unsigned wcnt[kTkLdsThreads / 64][2];
-  constexpr int NW = kTkLdsThreads / 64;
+  __shared__ unsigned s_prefix, s_need;
+  __shared__ unsigned wcnt[kTkLdsThreads / 64];
   const float* row = x + (size_t)blockIdx.x * n;
   long long* out = idx + (size_t)blockIdx.x * k;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {   // rows 16-byte aligned: float4 loads
+    // every load of the row issued before the first LDS store (one HBM round trip, not 10)
+    constexpr int kIt = (kTkLdsKeys / 4 + kTkLdsThreads - 1) / kTkLdsThreads;
     const float4* r4 = reinterpret_cast<const float4*>(row);
-    for (int i = tid; i < (n >> 2); i += kTkLdsThreads) {
-      const float4 v = r4[i];
-      keys[4 * i] = order_key(v.x);
-      keys[4 * i + 1] = order_key(v.y);
-      keys[4 * i + 2] = order_key(v.z);
-      keys[4 * i + 3] = order_key(v.w);
+    const int n4 = n >> 2;
+    float4 buf[kIt];
+#pragma unroll
+    for (int u = 0; u < kIt; ++u) {
+      const int i = tid + u * kTkLdsThreads;
+      buf[u] = i < n4 ? r4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kIt; ++u) {
+      const int i = tid + u * kTkLdsThreads;
+      if (i < n4)
+        *reinterpret_cast<uint4*>(keys + 4 * i) =
+            make_uint4(order_key(buf[u].x), order_key(buf[u].y), order_key(buf[u].z), order_key(buf[u].w));
     }
   } else {
     for (int i = tid; i < n; i += kTkLdsThreads) keys[i] = order_key(row[i]);
@@ -195,42 +203,38 @@ __global__ void __launch_bounds__(kTkLdsThreads) topk_rows_lds_kernel(const floa
     need = s_need;
     pmask |= 0xffu << shift;
   }
+  // compaction: thread t owns the keys [t E, (t + 1) E), E = ceil(n / 1024) (37 at
+  // n = 37 632: an odd stride between lanes, no bank conflicts); its counts of keys > T and
+  // == T, one block scan, then each thread writes its selections in index order -- one
+  // barrier, where a 1024-key round per barrier pair took 37 rounds
   const unsigned T = prefix;
-  if (tid == 0) s_base = 0u;
-  unsigned eq_seen = 0;
-  __syncthreads();
-  for (int c0 = 0; c0 < n; c0 += kTkLdsThreads) {
-    const int i = c0 + tid;
-    const unsigned key = i < n ? keys[i] : 0u;
-    const bool gt = i < n && key > T, eq = i < n && key == T;
-    const unsigned long long bg = __ballot(gt), be = __ballot(eq);
-    if (lane == 0) {
-      wcnt[wave][0] = (unsigned)__popcll(bg);
-      wcnt[wave][1] = (unsigned)__popcll(be);
-    }
-    __syncthreads();
-    unsigned gt_before = 0, eq_before = 0, eq_tot = 0, gt_tot = 0;
+  const int E = (n + kTkLdsThreads - 1) / kTkLdsThreads;
+  const int b0 = min(tid * E, n), b1 = min(b0 + E, n);
+  unsigned cnt = 0;                            // (keys > T) | (keys == T) << 16; each < 2^16
+  for (int i = b0; i < b1; ++i) {
+    const unsigned key = keys[i];
+    cnt += (key > T ? 1u : 0u) + (key == T ? 0x10000u : 0u);
+  }
+  unsigned incl = cnt;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const unsigned a = wcnt[w][0], b = wcnt[w][1];
-      if (w < wave) {
-        gt_before += a;
-        eq_before += b;
-      }
-      gt_tot += a;
-      eq_tot += b;
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) wcnt[wave] = incl;
+  __syncthreads();
+  unsigned before = incl - cnt;
+  for (int w = 0; w < wave; ++w) before += wcnt[w];
+  unsigned gb = before & 0xffffu, eb = before >> 16;
+  for (int i = b0; i < b1; ++i) {
+    const unsigned key = keys[i];
+    if (key > T) {
+      out[gb + min(eb, need)] = i;
+      ++gb;
+    } else if (key == T) {
+      if (eb < need) out[gb + eb] = i;
+      ++eb;
     }
-    const unsigned long long lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const unsigned my_gt = gt_before + (unsigned)__popcll(bg & lt_mask);
-    const unsigned my_eq = eq_before + (unsigned)__popcll(be & lt_mask);
-    const unsigned eq_taken_before = min(eq_seen + my_eq, need) - min(eq_seen, need);
-    const unsigned base = s_base;
-    if (gt || (eq && eq_seen + my_eq < need)) out[base + my_gt + eq_taken_before] = i;
-    const unsigned eq_taken_chunk = min(eq_seen + eq_tot, need) - min(eq_seen, need);
-    eq_seen += eq_tot;
-    __syncthreads();
-    if (tid == 0) s_base = base + gt_tot + eq_taken_chunk;
-    __syncthreads();
   }
 }
 
