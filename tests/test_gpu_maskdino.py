@@ -4,6 +4,7 @@ bf16 (finite losses and gradients, weights move), graph replay vs eager, and the
 Swin-T / 300-query model at 256^2."""
 import copy
 
+import numpy as np
 import pytest
 import torch
 
@@ -145,13 +146,23 @@ def test_factor_mask_losses_equal_full_logit_autograd(precision):
     assert abs(l1 - l2) <= 1e-5 * abs(l2), (l1, l2)
     assert set(g1) == set(g2)
     tol = 2e-2 if precision == "bf16" else 1e-4
-    # the attention key biases' gradients are exactly zero in exact arithmetic (softmax is
-    # invariant to a per-row constant: ~1e-11 of rounding here): compared in absolute terms
-    errs = sorted(((float((g1[n] - g2[n]).norm() / g2[n].norm().clamp(min=1e-6)), n) for n in g2), reverse=True)
+    # Structural zeros: an attention key bias adds the same constant to every score of a
+    # query's row, which softmax cancels, so its exact gradient is 0 and both paths give
+    # pure rounding noise (bf16: ~1e-6-1e-5 norms).  Those are checked in ABSOLUTE terms
+    # against the model's gradient scale; every other parameter relatively, with a norm
+    # floor of 1e-2 x the median parameter-gradient norm (no gate divides by ~0).
+    zero = {n for n in g2 if n.endswith("k_proj.bias")}
+    gnorm = float(torch.sqrt(sum((g.double() ** 2).sum() for g in g2.values())))
+    floor = 1e-2 * float(np.median([float(g2[n].norm()) for n in g2]))
+    zmax = max([max(float(g1[n].norm()), float(g2[n].norm())) for n in zero] + [0.0])
+    errs = sorted(((float((g1[n] - g2[n]).norm()) / max(float(g2[n].norm()), floor), n) for n in g2 if n not in zero),
+                  reverse=True)
     worst = errs[0][0]
     print(f"maskdino {precision}: factor vs full-logit mask losses, loss {l1:.6f} / {l2:.6f}, worst grad rel-L2 "
-          f"{worst:.2e}; {[(f'{e:.1e}', n, float(g2[n].norm())) for e, n in errs[:6]]}")
+          f"{worst:.2e}; {[(f'{e:.1e}', n, float(g2[n].norm())) for e, n in errs[:6]]}; structural zeros "
+          f"{len(zero)}: max norm {zmax:.2e} of global {gnorm:.2e}")
     assert worst <= tol
+    assert zmax <= 1e-3 * gnorm
 
 
 def test_factor_matcher_equals_full_logit_matcher():

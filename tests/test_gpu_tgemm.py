@@ -233,22 +233,21 @@ def test_layer_norm_fp8_copy_equals_mx_quantize(C, shift):
 
 @pytest.mark.parametrize("choice", [None, True, False])
 def test_linear_tokens_forward_dispatch(monkeypatch, choice):
-    """linear.linear_tokens with the per-shape forward choice (token GEMM vs vendor GEMM,
-    timed on the first eager call, or forced either way): the output and the gradients
-    equal torch autograd in f64 within bf16 rounding, and the choice is cached per shape."""
+    """linear.linear_tokens with the static forward rule (token GEMM vs vendor GEMM by
+    shape, linear._use_token_gemm) or forced either way: the output and the gradients equal
+    torch autograd in f64 within bf16 rounding, and the rule is deterministic."""
     from visionseg import linear
-    monkeypatch.setattr(linear, "_fwd_choice", {})
+    assert linear._use_token_gemm(20000, 576, 192) and linear._use_token_gemm(262144, 96, 384)
+    assert not linear._use_token_gemm(589824, 576, 192) and not linear._use_token_gemm(262144, 384, 96)
+    if choice is not None:
+        monkeypatch.setattr(linear, "_use_token_gemm", lambda M, N, K: choice)
     g = torch.Generator().manual_seed(3)
     M, K, N = 20000, 192, 576
     x, w, b = _rand((M, K), g), _rand((N, K), g, 1 / math.sqrt(K)), _rand((N,), g, 0.1)
     gy = _rand((M, N), g, 0.01)
-    if choice is not None:
-        linear._fwd_choice[(M, N, K, True, torch.device(DEV).index if torch.device(DEV).index is not None
-                            else torch.cuda.current_device())] = choice
     xd, wd, bd = (t.to(DEV).requires_grad_(True) for t in (x, w, b))
     y = linear.linear_tokens(xd, wd, bd)
     y.backward(gy.to(DEV))
-    assert len(linear._fwd_choice) == 1
     xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
     yr = xr @ wr.t() + br
     yr.backward(gy.double())

@@ -256,7 +256,7 @@ def test_bf16_training_step_vs_oracle():
         bounds against the yardstick's update;
       * defects: no parameter whose error is above both 3 x its yardstick's and 2.5 x the
         yardstick's p90 (relative) and 5 % of the median gradient norm (absolute) on
-        EVERY seed (a wrong kernel gives O(1) errors on every draw).
+        2 of the 3 seeds, and none above 10 x / 5 x p90 / 20 % on any one seed.
     The per-family mean ratios are printed (largest first) for a diagnosis."""
     runs = [_bf16_step_errors(*sd) for sd in SEEDS_BF16]
     q = lambda d, p: float(np.percentile(list(d.values()), p))          # noqa: E731
@@ -288,6 +288,10 @@ def test_bf16_training_step_vs_oracle():
         assert abs(lp - l32) <= 1.25 * abs(l16 - l32) + 2e-3 * abs(l32), r["loss"]
     assert np.mean(rg50) <= 1.25 and np.mean(rg90) <= 1.25, (rg50, rg90)
     assert np.mean(ru50) <= 1.25 and np.mean(ru90) <= 1.25, (ru50, ru90)
-    bad = [n for n in names if all(
-        r["eg"][n] > max(3.0 * r["yg"][n], 2.5 * q(r["yg"], 90)) and r["dist"][n] > 0.05 for r in runs)]
+    # a defect on 2 of the 3 seeds (a data-dependent kernel bug -- a tie, an edge shape --
+    # need not show on every draw), or a gross one (10x the yardstick, 20 % of the median
+    # gradient norm) on any single seed
+    bad = [n for n in names if sum(
+        r["eg"][n] > max(3.0 * r["yg"][n], 2.5 * q(r["yg"], 90)) and r["dist"][n] > 0.05 for r in runs) >= 2
+        or any(r["eg"][n] > max(10.0 * r["yg"][n], 5.0 * q(r["yg"], 90)) and r["dist"][n] > 0.2 for r in runs)]
     assert not bad, [(n, [round(r["eg"][n], 3) for r in runs], [round(r["yg"][n], 3) for r in runs]) for n in bad[:5]]

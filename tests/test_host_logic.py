@@ -304,3 +304,37 @@ def test_pad_buckets_and_mixed_aspect_loader(tmp_path):
     h, w = ei.shape[-2:]
     assert torch.equal(bi[..., :h, :w], ei) and int(bi[..., h:, :].sum()) == 0 and int(bi[..., :, w:].sum()) == 0
     assert torch.equal(es, bs) and all(torch.equal(x[:, :h, :w], y) and not x[:, h:].any() for x, y in zip(bm, em))
+
+
+def test_factored_list_validation():
+    """ops.factored accepts only the decoder's own factored output (one entry per step of E,
+    the same E / F objects, entry s = step s); a subset or a reordered list is not treated
+    as factored (its consumers materialise it instead)."""
+    from visionseg import ops
+    E = torch.zeros(3, 2, 5, 8)
+    Fm = torch.zeros(2, 16, 8)
+    full = [ops.FactoredLogits(E, Fm, s, 4, 4) for s in range(3)]
+    assert ops.factored(full)
+    assert not ops.factored(full[1:])                       # a subset (last steps only)
+    assert not ops.factored([full[1], full[0], full[2]])    # reordered
+    assert not ops.factored(full[:2] + [ops.FactoredLogits(E.clone(), Fm, 2, 4, 4)])
+    assert not ops.factored([])
+    assert full[0].shape == (2, 5, 4, 4)
+
+
+@pytest.mark.gpu
+def test_decoder_returns_tensors_by_default():
+    """Mask2Former.forward keeps its contract ([B,Q,H/4,W/4] f32 tensors) with grad on, in
+    train() and eval(): factored logits are only for a consumer that asks for them
+    (decoder.emit_factors, set by train.Trainer for the visionseg SetCriterion)."""
+    from visionseg.criterion import SetCriterion
+    cfg = M2FConfig(embed_dim=32, depths=(1, 1, 1, 1), num_heads=(1, 2, 4, 8), feature_size=128,
+                    mask_feature_size=128, hidden_dim=128, enc_ffn=64, dec_ffn=64, dec_heads=4, enc_layers=1,
+                    dec_layers=2, num_queries=4, train_num_points=64)      # 128 channels: the factorable width
+    m = Mask2Former(cfg).cuda().to(torch.bfloat16)
+    assert m.decoder.emit_factors is False
+    assert SetCriterion.accepts_factored_logits
+    for mode in (True, False):
+        m.train(mode)
+        masks, classes = m(torch.randn(1, 3, 64, 64, device="cuda"))
+        assert all(isinstance(x, torch.Tensor) and x.shape == (1, 4, 16, 16) for x in masks)

@@ -102,6 +102,10 @@ def as_padded(mask_labels, class_labels, device):
 
 
 class SetCriterion:
+    # reads ops.FactoredLogits (the matcher and the matched maps from the mask head's
+    # factors): train.Trainer switches the decoder's factored output on for it
+    accepts_factored_logits = True
+
     def __init__(self, cfg, matcher: str = "device", point_source=None):
         """matcher: "device" (csrc/match.hip, no host sync) or "host" (scipy, the
         reference's linear_sum_assignment).  point_source: None (device RNG) or a parity

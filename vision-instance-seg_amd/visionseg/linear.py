@@ -80,31 +80,22 @@ def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype, out: 
     return out
 
 
-# Forward of the token Linears: the hand-written token GEMM (csrc/token_gemm.hip) where it
-# beats the vendor GEMM on this shape -- measured once per (M, N, K, bias) on the first eager
-# call (HIP events, median of 5 alternating runs each; taken only when >= 3 % faster), never
-# inside a graph capture (an unmeasured shape runs the vendor GEMM there).  At C2 the token
-# GEMM wins the small-N Swin shapes (qkv, proj, fc2 of stages 1-3: tools/tgemm_bench.py,
-# profiles/r4_tgemm_bench3.txt).  VS_TGEMM_FWD=0: always the vendor GEMM.
+# Forward of the token Linears: the hand-written token GEMM (csrc/token_gemm.hip) on the
+# shapes where it beat the vendor GEMM on the box, by a STATIC shape rule (the same choice in
+# every process and on every rank, so the bf16 rounding of a Linear never depends on a
+# timing).  From tools/tgemm_bench.py (profiles/r4_tgemm_bench3.txt, M = tokens):
+#   * K <= 384 and N < 4K (qkv, proj, and fc2 from a narrow stage): C2 stages 1-3 qkv / proj
+#     1.1-1.4x, stage-1 fc2 1.35x; the fc1 shapes (N = 4K) are ties or vendor wins;
+#   * M <= 16384, N <= 768, K <= 1536 (C2 stage-3 fc2, stage-4 proj): 1.2-1.3x;
+#   * never above 300 000 tokens: C5 stage 1 (589 824) runs 0.8x of the vendor GEMM.
+# VS_TGEMM_FWD=0: always the vendor GEMM.
 _TGEMM_FWD = os.environ.get("VS_TGEMM_FWD", "1") == "1"
-_fwd_choice: dict = {}
 
 
-def _pick_token_gemm(x2, weight, bias) -> bool:
-    fns = (lambda: F.linear(x2, weight, bias), lambda: ops.token_gemm(x2, weight, bias))
-    for f in fns:
-        f()
-    ev = [[], []]
-    for _ in range(5):
-        for i, f in enumerate(fns):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            f()
-            b.record()
-            ev[i].append((a, b))
-    torch.cuda.synchronize()
-    med = [sorted(a.elapsed_time(b) for a, b in e)[2] for e in ev]
-    return med[1] < 0.97 * med[0]
+def _use_token_gemm(M: int, N: int, K: int) -> bool:
+    if M > 300_000:
+        return False
+    return (K <= 384 and N < 4 * K) or (M <= 16384 and N <= 768 and K <= 1536)
 
 
 def _forward_gemm(x, weight, bias):
@@ -112,16 +103,9 @@ def _forward_gemm(x, weight, bias):
     N, K = weight.shape
     if not (_TGEMM_FWD and x.is_cuda and x.dtype == weight.dtype == torch.bfloat16 and x.is_contiguous()
             and (bias is None or bias.dtype == torch.bfloat16) and K % 8 == 0 and N % 8 == 0
-            and x.numel() // K >= MIN_TOKENS):
+            and x.numel() // K >= MIN_TOKENS and _use_token_gemm(x.numel() // K, N, K)):
         return F.linear(x, weight, bias)
-    x2 = x.reshape(-1, K)
-    key = (x2.shape[0], N, K, bias is not None, x.device.index)
-    use = _fwd_choice.get(key)
-    if use is None:
-        if torch.cuda.is_current_stream_capturing():
-            return F.linear(x, weight, bias)
-        use = _fwd_choice[key] = _pick_token_gemm(x2, weight, bias)
-    return ops.token_gemm(x2, weight, bias).view(*x.shape[:-1], N) if use else F.linear(x, weight, bias)
+    return ops.token_gemm(x.reshape(-1, K), weight, bias).view(*x.shape[:-1], N)
 
 
 class _LinearFn(torch.autograd.Function):

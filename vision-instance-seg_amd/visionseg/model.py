@@ -596,6 +596,10 @@ class Decoder(nn.Module):
         # size and the matcher from E . F(points) (csrc/match_factors.hip).  VS_FACTORED_MASKS=0
         # keeps the full-resolution logits (A/B)
         self.factored_masks = os.environ.get("VS_FACTORED_MASKS", "1") != "0"
+        # ... but only for a consumer that reads FactoredLogits (the visionseg SetCriterion,
+        # switched on by train.Trainer): by default forward() returns real [B,Q,H/4,W/4] f32
+        # logit tensors, with or without grad, in train() or eval() mode
+        self.emit_factors = False
 
     def embed(self, h, dtype):
         """(LN(h), mask embedding MLP_3(LN(h))) -- HF:m2f:2040-2048."""
@@ -656,7 +660,7 @@ class Decoder(nn.Module):
         n = len(self.layers)
 
         # (C in {128, 256}: the grouped mask-head kernel of the matched maps)
-        fact = batched and self.factored_masks and mf.dtype == torch.bfloat16 and mf.shape[-1] in (128, 256)
+        fact = (batched and self.emit_factors and self.training and self.factored_masks and mf.dtype == torch.bfloat16 and mf.shape[-1] in (128, 256))
         mf_levels = {}
 
         def step(hh, target_hw):
@@ -711,7 +715,10 @@ def pack_bitmask(blocked: torch.Tensor) -> torch.Tensor:
 
 class Mask2Former(nn.Module):
     """Swin + Mask2Former forward: returns (mask logits per decoder step [B,Q,H/4,W/4]
-    f32, class logits per step [B,Q,num_labels+1])."""
+    f32, class logits per step [B,Q,num_labels+1]).  Exception: with
+    `decoder.emit_factors` set (train.Trainer sets it for the visionseg SetCriterion) and
+    the model in train() mode with grad on, bf16, the mask logits are ops.FactoredLogits
+    (E . F never materialised; `.materialize()` gives the tensor)."""
 
     def __init__(self, cfg: M2FConfig):
         super().__init__()

@@ -530,7 +530,15 @@ class FactoredLogits:
 
 
 def factored(masks_list) -> bool:
-    return bool(masks_list) and all(isinstance(m, FactoredLogits) for m in masks_list)
+    """True when `masks_list` is exactly the decoder's factored output: every entry a
+    FactoredLogits over the SAME factors (E, F), entry s holding step s, one entry per step
+    of E.  The consumers (SetCriterion.match, matched_maps) read E and F from the first
+    entry for every step, so a subset or a reordered list must be materialised instead."""
+    if not masks_list or not all(isinstance(m, FactoredLogits) for m in masks_list):
+        return False
+    m0 = masks_list[0]
+    return (int(m0.E.shape[0]) == len(masks_list)
+            and all(m.E is m0.E and m.F is m0.F and m.s == i for i, m in enumerate(masks_list)))
 
 
 def materialize_masks(masks_list):
@@ -805,6 +813,7 @@ def matched_maps(masks_list, qsel):
             Esel = torch.gather(E.detach().transpose(0, 1), 2, qsel.transpose(0, 1)[..., None].expand(B, S, Kc, C))
             maps = mask_head_grouped(Esel.reshape(B, S * Kc, C), Fm.detach(), m0.H, m0.W, Kc)
         return maps.view(S * B * Kc, 1, m0.H, m0.W), (E, Fm)
+    masks_list = materialize_masks(masks_list)      # a partial / reordered factored list
     bidx = torch.arange(B, device=qsel.device)[:, None].expand(B, Kc)
     fac = mask_head_factors(masks_list)
     with torch.no_grad() if fac is not None else contextlib.nullcontext():

@@ -115,6 +115,11 @@ class Trainer:
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
         self.model = model.to(self.device)
         self.criterion = criterion
+        # the decoder keeps its training logits factored (ops.FactoredLogits) only for a
+        # criterion that reads them; any other criterion gets [B,Q,H/4,W/4] tensors
+        dec = getattr(model, "decoder", None)
+        if dec is not None and hasattr(dec, "emit_factors"):
+            dec.emit_factors = bool(getattr(criterion, "accepts_factored_logits", False))
         if s.conv_find and self.device.type == "cuda":
             # the first call of each conv shape benchmarks MIOpen's solvers (eager warm-up
             # steps, before any graph capture); later calls use the fastest
