@@ -284,6 +284,16 @@ VS_API int vs_point_scatter(const float* grad_points, const float* grid, float* 
 VS_API int vs_point_sample_rows(const float* maps, const long long* rows, const float* coords, float* out,
                                 int num_maps, int height, int width, int num_sets, int num_points, void* stream);
 
+/* The same bilinear point gather from bool target masks stored as u8 [M, H, W] (the
+ * criterion's target labels: matcher HF:m2f:453-459, loss labels HF:m2f:700-724) without an
+ * f32 copy of the masks.  rows: int64 [N] or NULL (set n reads mask n).  grid_space 0:
+ * coords f32 [N, P, 2] in [0, 1]; grid_space 1: coords already in grid_sample's [-1, 1]
+ * space, one [P, 2] point set per `sets_per_coord` consecutive sets (the matcher's points,
+ * shared by an image's Kc targets). */
+VS_API int vs_point_sample_masks(const unsigned char* masks, const long long* rows, const float* coords, float* out,
+                                 int num_maps, int height, int width, int num_sets, int num_points, int grid_space,
+                                 int sets_per_coord, void* stream);
+
 /* Row-wise top-k indices for the importance sampling of the mask losses (the `topk` of
  * HF:m2f:689-724 sample_points_using_uncertainty, MaskDINO's copy of it): indices int64
  * [rows, k] = the positions of the k largest of values f32 [rows, n], per row, in ascending

@@ -79,3 +79,31 @@ def test_point_scatter_vs_grid_sampler_backward(S, B, K, n, H, W):
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
     assert float((out - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
+
+
+def test_point_sample_masks_equals_grid_sample():
+    """ops.point_sample_masks (csrc/mask_head.hip, the criterion's target labels straight from
+    the bool masks) == grid_sample on the f32 copy (HF:m2f:245-275 point_sample), in both
+    coordinate modes: [0, 1] coords with a row map (the loss labels, pair (s, i) -> target i)
+    and grid-space coords shared by an image's targets (the matcher), incl. points on the
+    border and outside [0, 1]."""
+    import torch.nn.functional as F
+    from visionseg import ops
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for B, Kc, H, W, P, S in ((2, 3, 37, 53, 100, 2), (4, 2, 1024, 1024, 12544, 10)):
+        masks = torch.rand(B, Kc, H, W, device="cuda", generator=g) > 0.7
+        # matcher: one point set per image in [-1, 1]
+        grid = torch.rand(B, P, 1, 2, device="cuda", generator=g) * 2.2 - 1.1
+        grid[0, :3, 0] = torch.tensor([[-1.0, -1.0], [1.0, 1.0], [0.0, 0.0]], device="cuda")
+        exp = F.grid_sample(masks.float(), grid, align_corners=False).squeeze(3)
+        got = ops.point_sample_masks(masks.view(B * Kc, H, W), grid.squeeze(2), grid_space=True,
+                                     sets_per_coord=Kc).view(B, Kc, P)
+        assert float((got - exp).abs().max()) <= 1e-6
+        # loss labels: S x B*Kc point sets in [0, 1], set n reads mask n % (B*Kc)
+        NP = B * Kc
+        coords = torch.rand(S * NP, P, 2, device="cuda", generator=g) * 1.2 - 0.1
+        rows = torch.arange(S * NP, device="cuda") % NP
+        exp = F.grid_sample(masks.view(NP, 1, H, W).float()[rows], 2.0 * coords.unsqueeze(2) - 1.0,
+                            align_corners=False).view(S * NP, P)
+        got = ops.point_sample_masks(masks.view(NP, H, W), coords, rows=rows)
+        assert float((got - exp).abs().max()) <= 1e-6

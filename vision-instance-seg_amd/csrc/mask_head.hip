@@ -662,17 +662,20 @@ __global__ void __launch_bounds__(256) point_scatter_kernel(const float* __restr
 // ((2c - 1 + 1) W - 1) / 2 and corner weights), one thread per point -- the MaskDINO mask
 // losses' labels, each query's OWN target map sampled at its points, without materialising
 // the per-query maps or sampling every target channel.
-__global__ void __launch_bounds__(256) point_sample_rows_kernel(const float* __restrict__ maps,
+template <typename T, bool GRID>
+__global__ void __launch_bounds__(256) point_sample_rows_kernel(const T* __restrict__ maps,
                                                                 const long long* __restrict__ rows,
                                                                 const float* __restrict__ coords,
                                                                 float* __restrict__ out, int H, int W, long long total,
-                                                                int P) {
+                                                                int P, int sets_per_coord) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const long long n = i / P;
-  const float* m = maps + rows[n] * (long long)H * W;
-  const float2 c = reinterpret_cast<const float2*>(coords)[i];
-  const float gx = 2.f * c.x - 1.f, gy = 2.f * c.y - 1.f;
+  const T* m = maps + (rows ? rows[n] : n) * (long long)H * W;
+  // GRID: coords already in grid_sample's [-1, 1] space, one point set per sets_per_coord rows
+  const long long ci = GRID ? (n / sets_per_coord) * P + (i - n * P) : i;
+  const float2 c = reinterpret_cast<const float2*>(coords)[ci];
+  const float gx = GRID ? c.x : 2.f * c.x - 1.f, gy = GRID ? c.y : 2.f * c.y - 1.f;
   const float ix = ((gx + 1.f) * (float)W - 1.f) / 2.f;
   const float iy = ((gy + 1.f) * (float)H - 1.f) / 2.f;
   const float fx = floorf(ix), fy = floorf(iy);
@@ -682,10 +685,10 @@ __global__ void __launch_bounds__(256) point_sample_rows_kernel(const float* __r
   float v = 0.f;
   const bool xi0 = x0 >= 0 && x0 < W, xi1 = x0 + 1 >= 0 && x0 + 1 < W;
   const bool yi0 = y0 >= 0 && y0 < H, yi1 = y0 + 1 >= 0 && y0 + 1 < H;
-  if (yi0 && xi0) v += m[(size_t)y0 * W + x0] * w_nw;
-  if (yi0 && xi1) v += m[(size_t)y0 * W + x0 + 1] * w_ne;
-  if (yi1 && xi0) v += m[(size_t)(y0 + 1) * W + x0] * w_sw;
-  if (yi1 && xi1) v += m[(size_t)(y0 + 1) * W + x0 + 1] * w_se;
+  if (yi0 && xi0) v += (float)m[(size_t)y0 * W + x0] * w_nw;
+  if (yi0 && xi1) v += (float)m[(size_t)y0 * W + x0 + 1] * w_ne;
+  if (yi1 && xi0) v += (float)m[(size_t)(y0 + 1) * W + x0] * w_sw;
+  if (yi1 && xi1) v += (float)m[(size_t)(y0 + 1) * W + x0 + 1] * w_se;
   out[i] = v;
 }
 
@@ -697,8 +700,32 @@ extern "C" int vs_point_sample_rows(const float* maps, const long long* rows, co
   if (total == 0) return VS_OK;
   VS_CHECK(maps && rows && coords && out, "null pointer");
   VS_CHECK(((uintptr_t)coords & 7) == 0, "coords must be 8-B aligned");
-  hipLaunchKernelGGL(point_sample_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, maps, rows, coords, out, height, width, total, num_points);
+  hipLaunchKernelGGL((point_sample_rows_kernel<float, false>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, maps, rows, coords, out, height, width, total, num_points, 1);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+// The set criterion's target labels at points straight from the bool (u8) target masks:
+// no f32 copy of the full-resolution masks, one launch per point set (replaces
+// grid_sample(masks.float(), ...) at HF:m2f:453-459 (matcher) and 700-724 (loss labels)).
+extern "C" int vs_point_sample_masks(const unsigned char* masks, const long long* rows, const float* coords,
+                                     float* out, int num_maps, int height, int width, int num_sets, int num_points,
+                                     int grid_space, int sets_per_coord, void* stream) {
+  VS_CHECK(num_maps > 0 && height > 0 && width > 0 && num_sets >= 0 && num_points > 0, "bad sizes");
+  VS_CHECK(grid_space == 0 || sets_per_coord > 0, "sets_per_coord must be positive");
+  const long long total = (long long)num_sets * num_points;
+  if (total == 0) return VS_OK;
+  VS_CHECK(masks && coords && out, "null pointer");
+  VS_CHECK(rows || num_sets <= num_maps, "without rows, set n reads mask n");
+  VS_CHECK(((uintptr_t)coords & 7) == 0, "coords must be 8-B aligned");
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (grid_space)
+    hipLaunchKernelGGL((point_sample_rows_kernel<unsigned char, true>), grid, dim3(256), 0, (hipStream_t)stream,
+                       masks, rows, coords, out, height, width, total, num_points, sets_per_coord);
+  else
+    hipLaunchKernelGGL((point_sample_rows_kernel<unsigned char, false>), grid, dim3(256), 0, (hipStream_t)stream,
+                       masks, rows, coords, out, height, width, total, num_points, 1);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

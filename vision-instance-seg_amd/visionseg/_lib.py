@@ -56,6 +56,7 @@ SIGNATURES = {
     "vs_mask_head_forward_grouped": [_P, _P, _P] + [_c_int] * 6 + [_P],
     "vs_point_scatter": [_P, _P, _P] + [_c_int] * 6 + [_P],
     "vs_point_sample_rows": [_P, _P, _P, _P] + [_c_int] * 5 + [_P],
+    "vs_point_sample_masks": [_P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_topk_rows": [_P, _P] + [_c_int] * 3 + [_P],
     "vs_masked_attn_workspace_bytes": [_c_int] * 4,
     "vs_masked_attn_forward": [_c_int, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 4 + [_c_float, _P],

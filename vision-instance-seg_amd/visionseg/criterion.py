@@ -46,6 +46,18 @@ def _sample(feat, coords):
     return F.grid_sample(feat, 2.0 * coords.unsqueeze(2) - 1.0, align_corners=False).squeeze(3).squeeze(1)
 
 
+def _target_points(tg, grid):
+    """The padded target masks sampled at the matcher's points (HF:m2f:453-459):
+    grid [B,P,1,2] in [-1,1] (one point set per image) -> [B,Kc,P] f32.  On the device the
+    bool masks are read as they are (ops.point_sample_masks), not copied to f32 first."""
+    B, Kc = tg.masks.shape[:2]
+    if tg.masks.is_cuda:
+        H, W = tg.masks.shape[-2:]
+        return ops.point_sample_masks(tg.masks.view(B * Kc, H, W), grid.squeeze(2), grid_space=True,
+                                      sets_per_coord=Kc).view(B, Kc, -1)
+    return F.grid_sample(tg.masks.float(), grid, align_corners=False).squeeze(3)
+
+
 class PaddedTargets:
     """Per-image instance targets padded to the batch's largest count Kc.
 
@@ -120,6 +132,7 @@ class SetCriterion:
         self.matcher = matcher
         self.point_source = point_source
         self._ew = {}
+        self._rows = {}
 
     def _loss_points(self, S, B, Kc, n, kind, dev):
         if self.point_source is None:
@@ -156,7 +169,7 @@ class SetCriterion:
                 # bf16 pair), the costs from the factors (csrc/match_factors.hip) -- no
                 # full-resolution logits of the S steps are made or read
                 fp = ops.feature_sample_hilo(m0.F, m0.H, m0.W, grid.squeeze(2))
-                tp = F.grid_sample(tg.masks.float(), grid, align_corners=False).squeeze(3)  # [B,Kc,P]
+                tp = _target_points(tg, grid)                                              # [B,Kc,P]
                 cost = ops.match_cost_factors(m0.E, fp, probs, tg.classes, tp, c.mask_weight, c.class_weight,
                                               c.dice_weight)
                 return ops.linear_sum_assignment_padded(cost, tg.counts)
@@ -169,14 +182,14 @@ class SetCriterion:
             H, W = masks_list[0].shape[-2:]
             key = (((grid[..., 0, 1] + 1) * (H / 2)).floor() * W + ((grid[..., 0, 0] + 1) * (W / 2)).floor())
             grid = torch.gather(grid, 1, key.argsort(dim=1)[:, :, None, None].expand(B, P, 1, 2))
-            tp = F.grid_sample(tg.masks.float(), grid, align_corners=False).squeeze(3)  # [B,Kc,P]
+            tp = _target_points(tg, grid)                                                  # [B,Kc,P]
             cost = ops.match_cost(masks_list, probs, tg.classes, grid.squeeze(2), tp, c.mask_weight,
                                   c.class_weight, c.dice_weight)
             return ops.linear_sum_assignment_padded(cost, tg.counts)
         pp = torch.stack([F.grid_sample(m.float(), grid, align_corners=False).squeeze(3)
                           for m in masks_list])                                          # [S,B,Q,P]
         if tg.kc:
-            tp = F.grid_sample(tg.masks.float(), grid, align_corners=False).squeeze(3)  # [B,Kc,P]
+            tp = _target_points(tg, grid)                                                  # [B,Kc,P]
         else:
             tp = torch.zeros(B, 1, P, device=dev)
         tpt = tp.transpose(1, 2)[None]                                                   # [1,B,P,Kc]
@@ -279,12 +292,17 @@ class SetCriterion:
                 coords = torch.gather(coords, 1, top[..., None].expand(-1, -1, 2))
                 if npts - nu > 0:
                     coords = torch.cat([coords, self._loss_points(S, B, Kc, npts - nu, "rand", dev)], 1)
-                # sample each full-resolution target once, with the coordinates of the S
-                # predictions it is matched to
-                by_t = coords.view(S, NP, npts, 2).transpose(0, 1)                         # [NP,S,P,2]
-                tgt = tg.masks.reshape(NP, 1, *tg.masks.shape[-2:]).float()
-                lab_t = _sample(tgt, by_t.reshape(NP, S * npts, 2)).view(NP, S, npts)
-                plab = lab_t.transpose(0, 1).reshape(S * NP, npts)
+                # the target labels at the points: pair (s, i) reads target mask i
+                if dev.type == "cuda":             # straight from the bool masks, no f32 copy
+                    rows = self._rows.get((S, NP, dev))
+                    if rows is None:
+                        rows = self._rows[(S, NP, dev)] = torch.arange(S * NP, device=dev) % NP
+                    plab = ops.point_sample_masks(tg.masks.reshape(NP, *tg.masks.shape[-2:]), coords, rows=rows)
+                else:
+                    by_t = coords.view(S, NP, npts, 2).transpose(0, 1)                     # [NP,S,P,2]
+                    tgt = tg.masks.reshape(NP, 1, *tg.masks.shape[-2:]).float()
+                    lab_t = _sample(tgt, by_t.reshape(NP, S * npts, 2)).view(NP, S, npts)
+                    plab = lab_t.transpose(0, 1).reshape(S * NP, npts)
             plog = ops.point_logits(pred, coords, qsel, fac)
             keep = valid.reshape(1, NP).expand(S, NP).reshape(S * NP)
             bce = F.binary_cross_entropy_with_logits(plog, plab, reduction="none").mean(1)  # [S*NP]

@@ -784,6 +784,31 @@ def point_sample_rows(maps, rows, coords):
     return out
 
 
+def point_sample_masks(masks, coords, grid_space=False, sets_per_coord=1, rows=None):
+    """Bilinear point samples (grid_sample, align_corners=False, zeros) of bool / u8 target
+    masks [M, H, W] without an f32 copy of them (csrc/mask_head.hip, vs_point_sample_masks).
+    grid_space=False: coords f32 [N, P, 2] in [0, 1], set n reads masks[rows[n]] (rows None:
+    masks[n]) -> [N, P].  grid_space=True: coords f32 [G, P, 2] in [-1, 1], set n reads
+    masks[n] at point set n // sets_per_coord -> [G * sets_per_coord, P]."""
+    L.require_hip(masks, coords)
+    M, H, W = masks.shape
+    mc = masks.contiguous()
+    mc = mc.view(torch.uint8) if mc.dtype == torch.bool else mc.to(torch.uint8)
+    cc = coords.float().contiguous()
+    P = cc.shape[1]
+    N = cc.shape[0] * sets_per_coord if grid_space else cc.shape[0]
+    if rows is not None:
+        rows = rows.to(torch.int64).contiguous()
+    elif N > M:
+        raise ValueError(f"{N} point sets but {M} masks and no rows")
+    out = torch.empty(N, P, device=masks.device, dtype=torch.float32)
+    with timed("point_sample_masks", mc, bytes_=cc.numel() * 4 + out.numel() * 4 * 2):
+        L.check(L.lib().vs_point_sample_masks(L.ptr(mc), L.ptr(rows) if rows is not None else None, L.ptr(cc),
+                                              L.ptr(out), M, H, W, N, P, int(bool(grid_space)), int(sets_per_coord),
+                                              L.stream(mc)), "point_sample_masks")
+    return out
+
+
 def topk_rows(values, k):
     """values f32 [N, n] -> int64 [N, k]: per row the indices of the k largest values, in
     ascending index order (csrc/topk.hip radix select; replaces `torch.topk(values, k)[1]`
