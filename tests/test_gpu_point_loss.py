@@ -92,6 +92,8 @@ def test_point_sample_masks_equals_grid_sample():
     g = torch.Generator(device="cuda").manual_seed(11)
     for B, Kc, H, W, P, S in ((2, 3, 37, 53, 100, 2), (4, 2, 1024, 1024, 12544, 10)):
         masks = torch.rand(B, Kc, H, W, device="cuda", generator=g) > 0.7
+        # a bool tensor may hold any non-zero byte as True (views / casts of byte data)
+        masks.view(torch.uint8)[masks.view(torch.uint8) > 0] = 255 if H < 100 else 1
         # matcher: one point set per image in [-1, 1]
         grid = torch.rand(B, P, 1, 2, device="cuda", generator=g) * 2.2 - 1.1
         grid[0, :3, 0] = torch.tensor([[-1.0, -1.0], [1.0, 1.0], [0.0, 0.0]], device="cuda")

@@ -315,6 +315,7 @@ def test_factored_list_validation():
     Fm = torch.zeros(2, 16, 8)
     full = [ops.FactoredLogits(E, Fm, s, 4, 4) for s in range(3)]
     assert ops.factored(full)
+    assert ops.factored([m.detach() for m in full])        # detached views of the same factors
     assert not ops.factored(full[1:])                       # a subset (last steps only)
     assert not ops.factored([full[1], full[0], full[2]])    # reordered
     assert not ops.factored(full[:2] + [ops.FactoredLogits(E.clone(), Fm, 2, 4, 4)])

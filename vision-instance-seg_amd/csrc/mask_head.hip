@@ -662,6 +662,11 @@ __global__ void __launch_bounds__(256) point_scatter_kernel(const float* __restr
 // ((2c - 1 + 1) W - 1) / 2 and corner weights), one thread per point -- the MaskDINO mask
 // losses' labels, each query's OWN target map sampled at its points, without materialising
 // the per-query maps or sampling every target channel.
+// a map element as a sample value: f32 as is; u8 is a bool mask (any non-zero byte is True:
+// torch's bool tensors made by views / casts of byte data may hold 0xFF, not 0x01)
+__device__ __forceinline__ float map_value(float v) { return v; }
+__device__ __forceinline__ float map_value(unsigned char v) { return v != 0 ? 1.f : 0.f; }
+
 template <typename T, bool GRID>
 __global__ void __launch_bounds__(256) point_sample_rows_kernel(const T* __restrict__ maps,
                                                                 const long long* __restrict__ rows,
@@ -685,10 +690,10 @@ __global__ void __launch_bounds__(256) point_sample_rows_kernel(const T* __restr
   float v = 0.f;
   const bool xi0 = x0 >= 0 && x0 < W, xi1 = x0 + 1 >= 0 && x0 + 1 < W;
   const bool yi0 = y0 >= 0 && y0 < H, yi1 = y0 + 1 >= 0 && y0 + 1 < H;
-  if (yi0 && xi0) v += (float)m[(size_t)y0 * W + x0] * w_nw;
-  if (yi0 && xi1) v += (float)m[(size_t)y0 * W + x0 + 1] * w_ne;
-  if (yi1 && xi0) v += (float)m[(size_t)(y0 + 1) * W + x0] * w_sw;
-  if (yi1 && xi1) v += (float)m[(size_t)(y0 + 1) * W + x0 + 1] * w_se;
+  if (yi0 && xi0) v += map_value(m[(size_t)y0 * W + x0]) * w_nw;
+  if (yi0 && xi1) v += map_value(m[(size_t)y0 * W + x0 + 1]) * w_ne;
+  if (yi1 && xi0) v += map_value(m[(size_t)(y0 + 1) * W + x0]) * w_sw;
+  if (yi1 && xi1) v += map_value(m[(size_t)(y0 + 1) * W + x0 + 1]) * w_se;
   out[i] = v;
 }
 

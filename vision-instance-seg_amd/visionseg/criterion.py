@@ -39,6 +39,9 @@ from . import ops
 
 # A/B switch: the fused matcher-cost kernel (default) or the torch formulation below it
 _FUSED_COST = os.environ.get("VS_MATCH_FUSED", "1") == "1"
+# A/B switch: target labels at points from the bool masks on the HIP kernel (default) or
+# grid_sample on an f32 copy
+_MASK_SAMPLE_KERNEL = os.environ.get("VS_MASK_SAMPLE", "1") == "1"
 
 
 def _sample(feat, coords):
@@ -51,7 +54,7 @@ def _target_points(tg, grid):
     grid [B,P,1,2] in [-1,1] (one point set per image) -> [B,Kc,P] f32.  On the device the
     bool masks are read as they are (ops.point_sample_masks), not copied to f32 first."""
     B, Kc = tg.masks.shape[:2]
-    if tg.masks.is_cuda:
+    if tg.masks.is_cuda and _MASK_SAMPLE_KERNEL:
         H, W = tg.masks.shape[-2:]
         return ops.point_sample_masks(tg.masks.view(B * Kc, H, W), grid.squeeze(2), grid_space=True,
                                       sets_per_coord=Kc).view(B, Kc, -1)
@@ -293,7 +296,7 @@ class SetCriterion:
                 if npts - nu > 0:
                     coords = torch.cat([coords, self._loss_points(S, B, Kc, npts - nu, "rand", dev)], 1)
                 # the target labels at the points: pair (s, i) reads target mask i
-                if dev.type == "cuda":             # straight from the bool masks, no f32 copy
+                if dev.type == "cuda" and _MASK_SAMPLE_KERNEL:     # straight from the bool masks
                     rows = self._rows.get((S, NP, dev))
                     if rows is None:
                         rows = self._rows[(S, NP, dev)] = torch.arange(S * NP, device=dev) % NP

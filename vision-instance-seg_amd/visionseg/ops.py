@@ -537,8 +537,12 @@ def factored(masks_list) -> bool:
     if not masks_list or not all(isinstance(m, FactoredLogits) for m in masks_list):
         return False
     m0 = masks_list[0]
+
+    def same(a, b):          # the same tensor, or a detached view of it (FactoredLogits.detach)
+        return a.data_ptr() == b.data_ptr() and a.shape == b.shape and a.stride() == b.stride()
+
     return (int(m0.E.shape[0]) == len(masks_list)
-            and all(m.E is m0.E and m.F is m0.F and m.s == i for i, m in enumerate(masks_list)))
+            and all(same(m.E, m0.E) and same(m.F, m0.F) and m.s == i for i, m in enumerate(masks_list)))
 
 
 def materialize_masks(masks_list):
