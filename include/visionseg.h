@@ -234,6 +234,15 @@ VS_API int vs_token_gemm(int mode, const void* x, const void* x_scales, const vo
  * elements rounded to nearest even at that scale.  K % 32 == 0. */
 VS_API int vs_mx_quantize(const void* x, void* q, void* scales, int rows, int K, void* stream);
 
+/* Row-wise e4m3 quantisation for the vendor (hipBLASLt) fp8 GEMM with one f32 scale per
+ * operand row (torch._scaled_mm rowwise; config C5's fp8 Linears, csrc/fp8_rows.hip):
+ * x bf16 [rows, K] -> q e4m3 bytes [rows, K] and scale f32 [rows], x ~= q * scale with
+ * scale = 2^-k, k the largest exponent with amax(row) 2^k <= 448.  K % 8 == 0, K <= 8192;
+ * x / y 16-B aligned, q 8-B aligned.  The gelu variant quantises y = gelu(h) (exact erf,
+ * stored in bf16 to y) in the same pass: the Swin MLP's fc1 -> fc2 hand-off. */
+VS_API int vs_row_quantize_fp8(const void* x, void* q, float* scale, int rows, int K, void* stream);
+VS_API int vs_gelu_row_quantize_fp8(const void* h, void* y, void* q, float* scale, int rows, int K, void* stream);
+
 /* ---- a11: mask head -----------------------------------------------------------------
  * logits f32 [B, Q, H*W] = E [B, Q, C] x P[b]^T, with the pixel embedding P
  * channels-last [B, H*W, C] (HF:m2f:2051 einsum 'bqc,bchw->bqhw').  dtype of E and P:

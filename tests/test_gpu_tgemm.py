@@ -171,14 +171,17 @@ def test_gelu_quantised_output_equals_mx_quantize(M, N, K, fp8):
     assert torch.equal(yq, eq)
 
 
+@pytest.mark.parametrize("backend", ["rows", "mx"])
 @pytest.mark.parametrize("C", [384, 192])
-def test_mlp_fp8_vs_bf16_mlp(C):
+def test_mlp_fp8_vs_bf16_mlp(monkeypatch, C, backend):
     """linear.mlp_fp8 (config C5's Swin MLP: fc1 + GELU on the MX fp8 token GEMM writing fc2's
     fp8 operand in its epilogue, fc2 on the MX fp8 GEMM, straight-through backward; C = 192:
     fc1 too shallow for fp8, the vendor GEMM + GELU, fc2 on fp8) vs the same MLP in f64 on
     the bf16 operands: output rel-RMS <= 0.06 (the fp8 budget of two chained products),
     input / weight / bias gradients rel-L2 <= 0.06.  M above the token-GEMM threshold."""
+    from visionseg import linear
     from visionseg.linear import mlp_fp8
+    monkeypatch.setattr(linear, "FP8_GEMM", backend)
     g = torch.Generator().manual_seed(21)
     M = 20000
     x = _rand((M, C), g)
@@ -256,13 +259,14 @@ def test_linear_tokens_forward_dispatch(monkeypatch, choice):
         assert rel <= 0.01, rel
 
 
-@pytest.mark.parametrize("fp8_dgrad", [False, True])
-def test_fp8_linear_dgrad_modes(monkeypatch, fp8_dgrad):
+@pytest.mark.parametrize("fp8_dgrad,backend", [(False, "mx"), (True, "mx"), (False, "rows")])
+def test_fp8_linear_dgrad_modes(monkeypatch, fp8_dgrad, backend):
     """linear_fp8_tokens' backward with dX on the bf16 vendor GEMM (default) or on the MX fp8
     token GEMM (VS_FP8_DGRAD=1): dX, dW, db vs f64 autograd on the bf16 operands (fp8
     forward: output rel-RMS <= 0.05; gradients rel-L2 <= 0.05, dX on bf16 <= 0.01)."""
     from visionseg import linear
     monkeypatch.setattr(linear, "FP8_DGRAD", fp8_dgrad)
+    monkeypatch.setattr(linear, "FP8_GEMM", backend)
     g = torch.Generator().manual_seed(5)
     M, K, N = 20000, 768, 384
     x, w, b = _rand((M, K), g), _rand((N, K), g, 1 / math.sqrt(K)), _rand((N,), g, 0.1)
@@ -277,3 +281,55 @@ def test_fp8_linear_dgrad_modes(monkeypatch, fp8_dgrad):
                           (bd.grad, br.grad, 0.05)):
         rel = float((got.detach().cpu().double() - exp.detach()).norm() / exp.detach().norm())
         assert rel <= tol, rel
+
+
+def _row_emulate(x):
+    """The row quantiser's rule in torch: (e4m3 bytes [rows, K], scale f32 [rows, 1], dequantised f64)."""
+    xf = x.float()
+    amax = xf.abs().amax(-1, keepdim=True)
+    k = torch.where(amax > 0, torch.floor(torch.log2(448.0 / amax.clamp_min(1e-38))), torch.zeros_like(amax))
+    k = k.clamp(-126, 126)
+    q = (xf * torch.exp2(k)).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), torch.exp2(-k), q.double() * torch.exp2(-k.double())
+
+
+@pytest.mark.parametrize("rows,K,scale", [(64, 192, 1.0), (333, 768, 1e-3), (100, 6144, 30.0), (7, 40, 2.0)])
+def test_row_quantize_fp8_bit_exact(rows, K, scale):
+    """ops.row_quantize_fp8 (csrc/fp8_rows.hip: per-row power-of-two scale, e4m3 RNE) ==
+    the rule emulated in torch, bit for bit, incl. an all-zero row; the GELU variant ==
+    F.gelu (exact erf) in bf16 and its quantisation."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(rows + K)
+    x = _rand((rows, K), g, scale)
+    x[0] = 0                                        # an all-zero row
+    x[1, 5] = 0.0
+    q, s = ops.row_quantize_fp8(x.to(DEV))
+    eq, es, _ = _row_emulate(x)
+    assert torch.equal(q.view(torch.uint8).cpu(), eq)
+    assert torch.equal(s.cpu(), es)
+    y, qg, sg = ops.row_quantize_fp8(x.to(DEV), gelu=True)
+    ey = torch.nn.functional.gelu(x.float()).to(torch.bfloat16)
+    assert float((y.cpu().float() - ey.float()).abs().max()) <= 2.0 ** -7 * float(ey.float().abs().max())
+    eq2, es2, _ = _row_emulate(y.cpu())
+    assert torch.equal(qg.view(torch.uint8).cpu(), eq2) and torch.equal(sg.cpu(), es2)
+
+
+@pytest.mark.parametrize("M,N,K", [(20000, 384, 768), (16384, 1536, 384), (20000, 768, 3072)])
+def test_fp8_rows_linear_vs_dequantised(M, N, K):
+    """The rowwise vendor fp8 GEMM path (linear._LinearFp8RowFn: ops.row_quantize_fp8 +
+    torch._scaled_mm with the bias) vs the product of the dequantised operands in f64
+    (rel-RMS <= 1e-2: bf16 output rounding and f32 accumulation), and vs the exact bf16
+    product (rel-RMS <= 0.06, the e4m3 budget)."""
+    from visionseg import linear
+    g = torch.Generator().manual_seed(M + N + K)
+    x, w, b = _rand((M, K), g), _rand((N, K), g, 1 / math.sqrt(K)), _rand((N,), g, 0.1)
+    assert linear.fp8_rows_ok(M, N, K)
+    y = linear._LinearFp8RowFn.apply(x.to(DEV), w.to(DEV), b.to(DEV)).cpu().double()
+    _, _, xd = _row_emulate(x)
+    _, _, wd = _row_emulate(w)
+    ref = xd @ wd.t() + b.double()
+    rel = float((y - ref).norm() / ref.norm())
+    exact = x.double() @ w.double().t() + b.double()
+    rel2 = float((y - exact).norm() / exact.norm())
+    print(f"fp8 rows {M}x{N}x{K}: vs dequantised {rel:.2e}, vs exact {rel2:.2e}")
+    assert rel <= 1e-2 and rel2 <= 0.06

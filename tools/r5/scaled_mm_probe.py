@@ -17,6 +17,8 @@ SHAPES = [  # (name, M tokens, N out, K in) -- C5 Swin-L @1536^2, batch 4
     ("s2 qkv", 147456, 1152, 384), ("s2 fc1", 147456, 1536, 384), ("s2 fc2", 147456, 384, 1536),
     ("s3 qkv", 36864, 2304, 768), ("s3 fc1", 36864, 3072, 768), ("s3 fc2", 36864, 768, 3072),
     ("s4 fc1", 9216, 6144, 1536), ("s4 fc2", 9216, 1536, 6144),
+    ("s2 proj", 147456, 384, 384), ("s3 proj", 36864, 768, 768), ("s4 qkv", 9216, 4608, 1536),
+    ("s4 proj", 9216, 1536, 1536),
 ]
 E4 = torch.float8_e4m3fn
 
@@ -83,8 +85,17 @@ def main():
             err = float((out.float() - ref).norm() / ref.norm())
             t = timeit(lambda: torch._scaled_mm(xq, wq.t(), scale_a=sxr, scale_b=swr.t(), out_dtype=torch.bfloat16))
             line += f" | row {t:.4f} ({fl / t / 1e9:6.1f}) err {err:.1e}"
+            bias = torch.randn(N, device=DEV).bfloat16()
+            outb = torch._scaled_mm(xq, wq.t(), scale_a=sxr, scale_b=swr.t(), bias=bias, out_dtype=torch.bfloat16)
+            errb = float((outb.float() - out.float() - bias.float()).abs().max())
+            tb = timeit(lambda: torch._scaled_mm(xq, wq.t(), scale_a=sxr, scale_b=swr.t(), bias=bias,
+                                                 out_dtype=torch.bfloat16))
+            line += f" +bias {tb:.4f} (d {errb:.1e})"
         except Exception as e:  # noqa: BLE001
             line += f" | row FAIL {type(e).__name__}: {str(e)[:80]}"
+        if "--mx" not in sys.argv:
+            print(line, flush=True)
+            continue
         # MX 1x32 e8m0
         try:
             xq, xs, xsf = mx_quant(x)

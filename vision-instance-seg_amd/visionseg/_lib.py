@@ -46,6 +46,8 @@ SIGNATURES = {
     "vs_window_attn_backward_image": [_c_int, _c_int, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 8 + [_c_float, _P],
     "vs_token_gemm": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _c_int, _P],
     "vs_mx_quantize": [_P, _P, _P, _c_int, _c_int, _P],
+    "vs_row_quantize_fp8": [_P, _P, _P, _c_int, _c_int, _P],
+    "vs_gelu_row_quantize_fp8": [_P, _P, _P, _P, _c_int, _c_int, _P],
     "vs_layer_norm_forward_rows_q": [_P] * 8 + [_c_int, _c_int, _c_float, _P, _P],
     "vs_add_layer_norm_forward_q": [_P] * 10 + [_c_int, _c_int, _c_float, _P, _P],
     "vs_mask_head_forward": [_c_int, _P, _P, _P] + [_c_int] * 5 + [_P],

@@ -789,6 +789,53 @@ def _tgemm_ok(x, w, b, tokens_min=MIN_TOKENS):
 FP8_DGRAD = os.environ.get("VS_FP8_DGRAD", "0") == "1"
 
 
+# config C5 fp8 GEMM backend.  "rows" (default): hipBLASLt's fp8 GEMM with one f32 scale per
+# row of each operand (torch._scaled_mm rowwise: x per token, W per output feature; e4m3
+# rows from ops.row_quantize_fp8).  "mx": the hand-written block-scaled MX token GEMM
+# (csrc/token_gemm.hip), which reached 1.0-1.4 PF/s against the vendor kernel's 1.5-2.6
+# (tools/r5/scaled_mm_probe.py, profiles/r5_scaled_mm_probe.txt).
+FP8_GEMM = os.environ.get("VS_FP8_GEMM", "rows")
+
+
+def _fp8_rows_ready(x, w, b) -> bool:
+    """Operands the rowwise fp8 path takes: contiguous bf16 device tensors outside autocast
+    (with or without grad: inference runs the same numerics as training)."""
+    return (x.is_cuda and not torch.is_autocast_enabled() and x.dtype == w.dtype == torch.bfloat16
+            and (b is None or b.dtype == torch.bfloat16) and x.is_contiguous())
+
+
+def fp8_rows_ok(M: int, N: int, K: int) -> bool:
+    """Static shape rule for the rowwise vendor fp8 GEMM (from the probe at the C5 Swin-L
+    shapes, fp8 vs bf16 F.linear): K >= 768 ran 1.5-1.9x faster (qkv / fc1 / fc2 of stages
+    3-4, stage-1 fc2); K = 384 pays only for fc1 (N = 4K: 1.3x; qkv 0.9x); K = 192 never
+    (0.5x: the product is HBM-bound there)."""
+    return M >= MIN_TOKENS and K % 16 == 0 and N % 16 == 0 and (K >= 768 or (K >= 384 and N >= 4 * K))
+
+
+class _LinearFp8RowFn(torch.autograd.Function):
+    """x W^T + b on hipBLASLt's rowwise-scaled fp8 GEMM (config C5): x and W quantised per
+    row to e4m3 with power-of-two scales (ops.row_quantize_fp8; x's copy may come from its
+    producer, e.g. the fused GELU of the MLP), f32 accumulation, bf16 out, the bias in the
+    GEMM epilogue.  Straight-through: the backward is _LinearFn's on the bf16 operands."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, xq=None, xs=None):
+        K = x.shape[-1]
+        N = weight.shape[0]
+        if xq is None:
+            xq, xs = ops.row_quantize_fp8(x.reshape(-1, K))
+        wq, ws = ops.row_quantize_fp8(weight)
+        with ops.timed("fp8_rows_gemm", x, flops=2.0 * xq.shape[0] * N * K):
+            y = torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=ws.view(1, N), bias=bias,
+                                 out_dtype=torch.bfloat16)
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        ctx.sink = None
+        return y.view(*x.shape[:-1], N)
+
+    backward = _LinearFp8Fn_backward = None        # set below (shares _LinearFp8Fn's)
+
+
 def _dgrad(gy2, weight):
     """dX = dY W for dY [M, N], W [N, K]: MX fp8 (FP8_DGRAD, N % 128 == 0) or the vendor GEMM."""
     N, K = weight.shape
@@ -902,6 +949,9 @@ class _LinearFp8Fn(torch.autograd.Function):
         return gx, gw, gb, None, None
 
 
+_LinearFp8RowFn.backward = _LinearFp8Fn.backward
+
+
 def linear_gelu_tokens(x, w, b, fp8: bool = False):
     """gelu(F.linear(x, w, b)) with the exact erf GELU: fused into the token GEMM on
     token-heavy bf16 device tensors (_LinearGeluFn), the composition otherwise."""
@@ -911,9 +961,15 @@ def linear_gelu_tokens(x, w, b, fp8: bool = False):
 
 
 def linear_fp8_tokens(x, w, b, xq=None):
-    """F.linear with the product in MX fp8 (_LinearFp8Fn) where it pays (K % 128 == 0 and K
-    >= FP8_MIN_K on token-heavy bf16 tensors), linear_tokens otherwise.  xq: x's MX fp8 copy
-    (e4m3, scales) when its producer made one (the fused GELU epilogue)."""
+    """F.linear with the product in fp8 where it pays: FP8_GEMM "rows" -> the vendor rowwise
+    fp8 GEMM (_LinearFp8RowFn) on the shapes of fp8_rows_ok; "mx" -> the MX token GEMM
+    (_LinearFp8Fn: K % 128 == 0 and K >= FP8_MIN_K); linear_tokens otherwise.  xq: x's fp8
+    copy (e4m3, scales) in the backend's format when its producer made one."""
+    if FP8_GEMM == "rows":
+        K, N = w.shape[1], w.shape[0]
+        if _fp8_rows_ready(x, w, b) and fp8_rows_ok(x.numel() // K, N, K):
+            return _LinearFp8RowFn.apply(x, w, b, *(xq if xq is not None else (None, None)))
+        return linear_tokens(x, w, b)
     if _tgemm_ok(x, w, b) and w.shape[1] % 128 == 0 and w.shape[1] >= FP8_MIN_K:
         return _LinearFp8Fn.apply(x, w, b, *(xq if xq is not None else (None, None)))
     return linear_tokens(x, w, b)
@@ -925,6 +981,17 @@ def mlp_fp8(x, w1, b1, w2, b2, xq=None):
     between the two GEMMs (config C5).  xq: x's MX fp8 copy from its producer (the
     LayerNorm), if it made one."""
     K1, N1 = w1.shape[1], w1.shape[0]
+    if FP8_GEMM == "rows":
+        # fc1 on the rowwise fp8 GEMM where it pays, then ONE pass for GELU + fc2's fp8 rows
+        M = x.numel() // K1
+        h = linear_fp8_tokens(x, w1, b1)
+        if _fp8_rows_ready(h, w2, b2) and fp8_rows_ok(M, w2.shape[0], N1) and h.is_contiguous():
+            if torch.is_grad_enabled() and h.requires_grad:
+                y, yq, ys = ops.gelu_row_quant(h)
+            else:
+                y, yq, ys = ops.row_quantize_fp8(h, gelu=True)
+            return _LinearFp8RowFn.apply(y, w2, b2, yq, ys)
+        return linear_tokens(ops.activation(h, "gelu"), w2, b2)
     fc1_fp8 = K1 % 128 == 0 and K1 >= FP8_MIN_K
     if _tgemm_ok(x, w1, b1) and N1 % 128 == 0 and N1 >= FP8_MIN_K and fc1_fp8:
         h, hq, hs = _LinearGeluFn.apply(x, w1, b1, True, True, *(xq if xq is not None else (None, None)))

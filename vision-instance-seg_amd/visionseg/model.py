@@ -28,6 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from . import linear as linear_mod
 from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, fp8_operand_ok, in_projection, linear_fp8_tokens,
                      linear_gelu_tokens,
                      linear_relu_tokens, mlp_fp8, linear_tokens, plane_projection, self_attn_in_proj, small_linear, value_query_projection,
@@ -156,7 +157,10 @@ class SwinBlock(nn.Module):
         # the window partition folded into the norm's stores (ops.WindowRows): h comes out
         # in the window layout [B*nW*ws^2, C], padding rows zero
         wr = ops.window_rows(B, H, W, ws, shift, x.device)
-        q8 = self.linear_fp8 and fp8_operand_ok(C)   # the Linears over C features take the MX fp8 path
+        # MX backend: the Linears over C features take the MX fp8 path and the norms write
+        # their MX operand copies; the rowwise backend (linear.FP8_GEMM "rows") quantises in
+        # linear_fp8_tokens / the MLP's fused GELU pass instead
+        q8 = self.linear_fp8 and fp8_operand_ok(C) and linear_mod.FP8_GEMM == "mx"
         if q8:
             # the norms also write their output as the fp8 GEMM operand (no quantisation pass)
             if res is None:
@@ -169,7 +173,8 @@ class SwinBlock(nn.Module):
         else:
             x, h = self.norm1.add_forward_windows(x, res, wr)
         if not q8:
-            qkv = self.attn.qkv(h.view(-1, ws * ws, C))
+            qkv = (linear_fp8_tokens(h.view(-1, ws * ws, C), self.attn.qkv.weight, self.attn.qkv.bias)
+                   if self.linear_fp8 else self.attn.qkv(h.view(-1, ws * ws, C)))
         # output in the image layout (window reverse folded into the kernel); the per-token
         # proj commutes with the crop
         o = ops.window_attention_image(qkv, self.attn.rel_table, self.attn.heads, ws, shift, B, H, W,

@@ -1302,6 +1302,31 @@ class _ActColsumFunction(torch.autograd.Function):
         return gx, None
 
 
+class _GeluRowQuantFunction(torch.autograd.Function):
+    """y = gelu(x) (exact erf) plus y's row-wise e4m3 copy (q, scale) for the next vendor
+    fp8 GEMM, from one HIP pass over x (vs_gelu_row_quantize_fp8); q / scale are not
+    differentiable (straight-through: the next Linear's backward uses y).  Backward: that of
+    _ActColsumFunction (dx and the preceding Linear's bias gradient in one pass)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.act = 1
+        ctx.save_for_backward(x)
+        y, q, sc = row_quantize_fp8(x, gelu=True)
+        ctx.mark_non_differentiable(q, sc)
+        return y.view(x.shape), q, sc
+
+    @staticmethod
+    def backward(ctx, gy, gq=None, gs=None):
+        return _ActColsumFunction.backward(ctx, gy)[0]
+
+
+def gelu_row_quant(x):
+    """(gelu(x), e4m3 rows of it, f32 row scales) -- see _GeluRowQuantFunction; x a
+    contiguous bf16 device tensor with a gradient path."""
+    return _GeluRowQuantFunction.apply(x)
+
+
 def activation(x, kind: str):
     """F.gelu / F.relu whose backward feeds the preceding Linear's bias gradient (see
     _ActColsumFunction) on contiguous f32 / bf16 device tensors with N % 8 == 0."""
@@ -1571,6 +1596,30 @@ def mx_quantize(x: torch.Tensor):
     with timed("mx_quantize", x, bytes_=x.numel() * 3 + s.numel()):
         L.check(L.lib().vs_mx_quantize(L.ptr(x), L.ptr(q), L.ptr(s), rows, K, L.stream(x)), "mx_quantize")
     return q, s
+
+
+def row_quantize_fp8(x: torch.Tensor, gelu: bool = False):
+    """bf16 [..., K] -> (q float8_e4m3fn [rows, K], scale f32 [rows, 1]) with x ~= q * scale
+    per row (power-of-two scales; csrc/fp8_rows.hip), the operand form of the vendor
+    rowwise fp8 GEMM (torch._scaled_mm).  gelu=True: quantises gelu(x) (exact erf) and also
+    returns it in bf16: (y, q, scale)."""
+    L.require_hip(x)
+    if x.dtype != torch.bfloat16 or x.shape[-1] % 8:
+        raise ValueError("row_quantize_fp8: bf16 rows with K % 8 == 0")
+    x = x.contiguous()
+    K = x.shape[-1]
+    rows = x.numel() // K
+    q = torch.empty(rows, K, device=x.device, dtype=torch.float8_e4m3fn)
+    sc = torch.empty(rows, 1, device=x.device, dtype=torch.float32)
+    if gelu:
+        y = torch.empty_like(x)
+        with timed("gelu_row_quantize", x, bytes_=x.numel() * 5 + rows * 4):
+            L.check(L.lib().vs_gelu_row_quantize_fp8(L.ptr(x), L.ptr(y), L.ptr(q), L.ptr(sc), rows, K, L.stream(x)),
+                    "gelu_row_quantize_fp8")
+        return y, q, sc
+    with timed("row_quantize", x, bytes_=x.numel() * 3 + rows * 4):
+        L.check(L.lib().vs_row_quantize_fp8(L.ptr(x), L.ptr(q), L.ptr(sc), rows, K, L.stream(x)), "row_quantize_fp8")
+    return q, sc
 
 
 def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None, quant_out: bool = False):
