@@ -809,6 +809,8 @@ def fp8_rows_ok(M: int, N: int, K: int) -> bool:
     shapes, fp8 vs bf16 F.linear): K >= 768 ran 1.5-1.9x faster (qkv / fc1 / fc2 of stages
     3-4, stage-1 fc2); K = 384 pays only for fc1 (N = 4K: 1.3x; qkv 0.9x); K = 192 never
     (0.5x: the product is HBM-bound there)."""
+    if (N, K) == (384, 1536):         # Swin-L stage-2 fc2: 0.218 vs 0.193 ms bf16 (measured exception)
+        return False
     return M >= MIN_TOKENS and K % 16 == 0 and N % 16 == 0 and (K >= 768 or (K >= 384 and N >= 4 * K))
 
 
