@@ -207,6 +207,17 @@ VS_API int vs_add_layer_norm_forward_q(const void* x, const void* r, const void*
                                        void* y, void* y_q, void* y_qscales, float* mean, float* rstd, int M,
                                        int C, float eps, const int* y_rows, void* stream);
 
+/* The same LayerNorm forwards writing their bf16 output also as ROW-scaled e4m3 (y_q [rows, C]
+ * + f32 y_scale [rows], y ~= q * scale with a power-of-two scale per row, the rule of
+ * vs_row_quantize_fp8) at the same (window-layout) rows: the operand of the vendor rowwise
+ * fp8 GEMM (config C5's fp8 Linears) without a quantisation pass.  bf16 only. */
+VS_API int vs_layer_norm_forward_qr(const void* x, const void* w, const void* b, void* y, void* y_q, float* y_scale,
+                                    float* mean, float* rstd, int M, int C, float eps, const int* y_rows,
+                                    void* stream);
+VS_API int vs_add_layer_norm_forward_qr(const void* x, const void* r, const void* w, const void* b, void* s,
+                                        void* y, void* y_q, float* y_scale, float* mean, float* rstd, int M, int C,
+                                        float eps, const int* y_rows, void* stream);
+
 /* ---- a5 / a6: token GEMM (the Swin block's Linears) ----------------------------------
  * y[M, N] = x[M, K] w[N, K]^T + bias[N] (bf16 out, f32 accumulation), both operands
  * K-contiguous rows: the F.linear of HF:swin:418-468 (qkv, proj) and HF:swin:511-536

@@ -333,3 +333,31 @@ def test_fp8_rows_linear_vs_dequantised(M, N, K):
     rel2 = float((y - exact).norm() / exact.norm())
     print(f"fp8 rows {M}x{N}x{K}: vs dequantised {rel:.2e}, vs exact {rel2:.2e}")
     assert rel <= 1e-2 and rel2 <= 0.06
+
+
+@pytest.mark.parametrize("C,shift,res", [(768, 0, False), (384, 6, True), (1536, 0, True), (192, 0, False)])
+def test_layer_norm_row_quant_equals_row_quantize(C, shift, res):
+    """The LayerNorm forwards' row-scaled e4m3 copy (quant="rows", csrc/norm.hip Q == 2, the
+    rowwise fp8 GEMM's operand) == ops.row_quantize_fp8 of the bf16 output they store, bit for
+    bit, in the window layout (with shift) and token-major with the residual add."""
+    from visionseg import ops
+    from visionseg.linear import TokenLayerNorm
+    g = torch.Generator().manual_seed(C + shift)
+    B, H, W, ws = 1, 24, 24, 12
+    ln = TokenLayerNorm(C).to(DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        ln.weight.copy_(torch.randn(C, generator=g) * 0.5 + 1)
+        ln.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    x = _rand((B, H * W, C), g, 2.0).to(DEV)
+    r = _rand((B, H * W, C), g).to(DEV)
+    if res:
+        s, y, (yq, ys) = ln.add_forward(x, r, quant="rows")
+        s_ref, y_ref = ln.add_forward(x, r)
+        assert torch.equal(s, s_ref)
+    else:
+        wr = ops.window_rows(B, H, W, ws, shift, x.device)
+        y, (yq, ys) = ln.forward_windows(x, wr, quant="rows")
+        y_ref = ln.forward_windows(x, wr)
+    assert torch.equal(y.view(-1, C), y_ref.view(-1, C))
+    eq, es = ops.row_quantize_fp8(y.view(-1, C))
+    assert torch.equal(yq.view(torch.uint8), eq.view(torch.uint8)) and torch.equal(ys.view(-1, 1), es)

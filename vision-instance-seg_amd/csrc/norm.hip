@@ -82,7 +82,10 @@ template <> struct RawChunk<float> {
 // the same (window-layout) rows, the bytes vs_mx_quantize would make of y: the operand of
 // the fp8 token GEMM that consumes y (config C5) without a quantisation pass.  A 32-element
 // block is the 4 chunks of lanes 4t..4t+3 (G is a multiple of 4): amax by two exchanges.
-template <typename T, int K, bool RES = false, bool Q = false>
+// Q == 2 (bf16): y also as ROW-scaled e4m3 (yq [rows, C] + f32 scale [rows] in yqs, x ~= q
+// * scale, the power-of-two rule of csrc/fp8_rows.hip): the operand of the vendor rowwise fp8
+// GEMM (config C5's fp8 Linears); the row amax is a group max over the G lanes of the row.
+template <typename T, int K, bool RES = false, int Q = 0>
 __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                           const T* __restrict__ b, T* __restrict__ y,
                                                           float* __restrict__ mean, float* __restrict__ rstd,
@@ -161,7 +164,43 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ 
         }
       }
       const float rs = rsqrtf(group_sum(q, G) * invC + eps);
-      if (row < M) {
+      if (Q == 2 && row < M) {                // row-scaled fp8 copy: all chunks, then one scale
+        const long long yr = yrows ? (long long)yrows[row] : row;
+        bf16x8_t c[K];
+        unsigned am = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int j = lane + k * G;
+          c[k] = zero8();
+          if (j < nch) {
+            float o[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mu) * rs * wv[k][i] + bv[k][i];
+            store_chunk(y + yr * C + j * 8, o);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) c[k][i] = bf16_bits(o[i]);      // the stored bf16 values
+            const unsigned m = amax8_bits(c[k]);
+            am = m > am ? m : am;
+          }
+        }
+        for (int sft = 1; sft < G; sft <<= 1) am = umax_xor(am, sft);
+        const int kq = mx_exp_bits(am);
+        const float inv = __uint_as_float((unsigned)(127 - kq) << 23);   // 2^-kq
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int j = lane + k * G;
+          if (j < nch) {
+            const uint4 u = bits128(c[k]);
+            *reinterpret_cast<uint2*>(yq + yr * C + j * 8) =
+                make_uint2((unsigned)e4m3x4(u.x, u.y, inv), (unsigned)e4m3x4(u.z, u.w, inv));
+          }
+        }
+        if (lane == 0) {
+          reinterpret_cast<float*>(yqs)[yr] = inv;
+          mean[row] = mu;
+          rstd[row] = rs;
+        }
+      } else if (row < M) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const int j = lane + k * G;
@@ -171,7 +210,7 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(const T* __restrict__ 
             for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mu) * rs * wv[k][i] + bv[k][i];
             const long long yr = yrows ? (long long)yrows[row] : row;
             store_chunk(y + yr * C + j * 8, o);
-            if constexpr (Q) {
+            if constexpr (Q == 1) {
               bf16x8_t c;
 #pragma unroll
               for (int i = 0; i < 8; ++i) c[i] = bf16_bits(o[i]);      // the stored bf16 values
@@ -662,7 +701,7 @@ static int ln_kmax(int) { return 4; }
 
 static int layer_norm_forward_impl(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
                                    float* rstd, int M, int C, float eps, const int* yrows, void* stream,
-                                   void* q = nullptr, void* qs = nullptr);
+                                   void* q = nullptr, void* qs = nullptr, int qmode = 0);
 
 extern "C" int vs_layer_norm_forward(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
                                      float* rstd, int M, int C, float eps, void* stream) {
@@ -681,12 +720,19 @@ extern "C" int vs_layer_norm_forward_rows_q(const void* x, const void* w, const 
                                             const int* y_rows, void* stream) {
   VS_CHECK(M == 0 || (y_rows && y_q && y_qscales), "null pointer");
   VS_CHECK(C % 32 == 0, "C must be a multiple of 32 for the MX fp8 copy");
-  return layer_norm_forward_impl(VS_BF16, x, w, b, y, mean, rstd, M, C, eps, y_rows, stream, y_q, y_qscales);
+  return layer_norm_forward_impl(VS_BF16, x, w, b, y, mean, rstd, M, C, eps, y_rows, stream, y_q, y_qscales, 1);
+}
+
+extern "C" int vs_layer_norm_forward_qr(const void* x, const void* w, const void* b, void* y, void* y_q,
+                                        float* y_scale, float* mean, float* rstd, int M, int C, float eps,
+                                        const int* y_rows, void* stream) {
+  VS_CHECK(M == 0 || (y_q && y_scale), "null pointer");
+  return layer_norm_forward_impl(VS_BF16, x, w, b, y, mean, rstd, M, C, eps, y_rows, stream, y_q, y_scale, 2);
 }
 
 static int layer_norm_forward_impl(int dtype, const void* x, const void* w, const void* b, void* y, float* mean,
                                    float* rstd, int M, int C, float eps, const int* yrows, void* stream, void* q,
-                                   void* qs) {
+                                   void* qs, int qmode) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && b && (M == 0 || (x && y && mean && rstd)), "null pointer");
@@ -696,8 +742,12 @@ static int layer_norm_forward_impl(int dtype, const void* x, const void* w, cons
   hipStream_t st = (hipStream_t)stream;
   const int grid = blocks_for(M, kThreads / G, 256 * 32);
 #define VS_LNF(KK)                                                                                          \
-  if (q)                                                                                                    \
-    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, false, true>), dim3(grid), dim3(kThreads), 0, st,           \
+  if (q && qmode == 2)                                                                                      \
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, false, 2>), dim3(grid), dim3(kThreads), 0, st,              \
+                       (const bf16*)x, (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G,  \
+                       nullptr, nullptr, yrows, (unsigned char*)q, (unsigned char*)qs);                     \
+  else if (q)                                                                                               \
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, false, 1>), dim3(grid), dim3(kThreads), 0, st,              \
                        (const bf16*)x, (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G,  \
                        nullptr, nullptr, yrows, (unsigned char*)q, (unsigned char*)qs);                     \
   else if (dtype == VS_BF16)                                                                                \
@@ -716,7 +766,8 @@ static int layer_norm_forward_impl(int dtype, const void* x, const void* w, cons
 
 static int add_layer_norm_forward_impl(int dtype, const void* x, const void* r, const void* w, const void* b,
                                        void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
-                                       const int* yrows, void* stream, void* q = nullptr, void* qs = nullptr);
+                                       const int* yrows, void* stream, void* q = nullptr, void* qs = nullptr,
+                                       int qmode = 0);
 
 extern "C" int vs_add_layer_norm_forward(int dtype, const void* x, const void* r, const void* w, const void* b,
                                          void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
@@ -737,12 +788,20 @@ extern "C" int vs_add_layer_norm_forward_q(const void* x, const void* r, const v
   VS_CHECK(M == 0 || (y_q && y_qscales), "null pointer");
   VS_CHECK(C % 32 == 0, "C must be a multiple of 32 for the MX fp8 copy");
   return add_layer_norm_forward_impl(VS_BF16, x, r, w, b, s, y, mean, rstd, M, C, eps, y_rows, stream, y_q,
-                                     y_qscales);
+                                     y_qscales, 1);
+}
+
+extern "C" int vs_add_layer_norm_forward_qr(const void* x, const void* r, const void* w, const void* b, void* s,
+                                            void* y, void* y_q, float* y_scale, float* mean, float* rstd, int M,
+                                            int C, float eps, const int* y_rows, void* stream) {
+  VS_CHECK(M == 0 || (y_q && y_scale), "null pointer");
+  return add_layer_norm_forward_impl(VS_BF16, x, r, w, b, s, y, mean, rstd, M, C, eps, y_rows, stream, y_q,
+                                     y_scale, 2);
 }
 
 static int add_layer_norm_forward_impl(int dtype, const void* x, const void* r, const void* w, const void* b,
                                        void* s, void* y, float* mean, float* rstd, int M, int C, float eps,
-                                       const int* yrows, void* stream, void* q, void* qs) {
+                                       const int* yrows, void* stream, void* q, void* qs, int qmode) {
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && b && (M == 0 || (x && r && s && y && mean && rstd)), "null pointer");
@@ -752,8 +811,12 @@ static int add_layer_norm_forward_impl(int dtype, const void* x, const void* r, 
   hipStream_t st = (hipStream_t)stream;
   const int grid = blocks_for(M, kThreads / G, 256 * 32);
 #define VS_ALNF(KK)                                                                                           \
-  if (q)                                                                                                      \
-    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, true, true>), dim3(grid), dim3(kThreads), 0, st,              \
+  if (q && qmode == 2)                                                                                        \
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, true, 2>), dim3(grid), dim3(kThreads), 0, st,                 \
+                       (const bf16*)x, (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G,    \
+                       (const bf16*)r, (bf16*)s, yrows, (unsigned char*)q, (unsigned char*)qs);               \
+  else if (q)                                                                                                 \
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16, KK, true, 1>), dim3(grid), dim3(kThreads), 0, st,                 \
                        (const bf16*)x, (const bf16*)w, (const bf16*)b, (bf16*)y, mean, rstd, M, C, eps, G,    \
                        (const bf16*)r, (bf16*)s, yrows, (unsigned char*)q, (unsigned char*)qs);               \
   else if (dtype == VS_BF16)                                                                                  \

@@ -50,6 +50,8 @@ SIGNATURES = {
     "vs_gelu_row_quantize_fp8": [_P, _P, _P, _P, _c_int, _c_int, _P],
     "vs_layer_norm_forward_rows_q": [_P] * 8 + [_c_int, _c_int, _c_float, _P, _P],
     "vs_add_layer_norm_forward_q": [_P] * 10 + [_c_int, _c_int, _c_float, _P, _P],
+    "vs_layer_norm_forward_qr": [_P] * 8 + [_c_int, _c_int, _c_float, _P, _P],
+    "vs_add_layer_norm_forward_qr": [_P] * 10 + [_c_int, _c_int, _c_float, _P, _P],
     "vs_mask_head_forward": [_c_int, _P, _P, _P] + [_c_int] * 5 + [_P],
     "vs_mask_head_backward_workspace_bytes": [_c_int] * 3,
     "vs_mask_head_backward": [_c_int] + [_P] * 6 + [_c_int] * 5 + [_P],

@@ -641,8 +641,9 @@ class TokenLayerNorm(nn.LayerNorm):
         (e4m3, e8m0 scales) of y) for an fp8 consumer, (y, None) where the copy cannot be made."""
         if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
                 and not torch.is_autocast_enabled():
-            if quant and x.dtype == torch.bfloat16 and x.shape[-1] % 32 == 0:
-                y, yq, ys = ops.layer_norm(x, self.weight, self.bias, self.eps, wrows=wrows, quant=True)
+            if quant and x.dtype == torch.bfloat16 and x.shape[-1] % (8 if quant == "rows" else 32) == 0:
+                y, yq, ys = ops.layer_norm(x, self.weight, self.bias, self.eps, wrows=wrows,
+                                           quant="rows" if quant == "rows" else True)
                 return y, (yq, ys)
             y = ops.layer_norm(x, self.weight, self.bias, self.eps, wrows=wrows)
             return (y, None) if quant else y
@@ -655,8 +656,9 @@ class TokenLayerNorm(nn.LayerNorm):
         forward_windows)."""
         if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
                 and r.shape == x.shape and r.dtype == x.dtype and not torch.is_autocast_enabled():
-            if quant and x.dtype == torch.bfloat16 and x.shape[-1] % 32 == 0:
-                s, y, yq, ys = ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, wrows=wrows, quant=True)
+            if quant and x.dtype == torch.bfloat16 and x.shape[-1] % (8 if quant == "rows" else 32) == 0:
+                s, y, yq, ys = ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, wrows=wrows,
+                                                  quant="rows" if quant == "rows" else True)
                 return s, y, (yq, ys)
             s, y = ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, wrows=wrows)
             return (s, y, None) if quant else (s, y)
@@ -671,6 +673,9 @@ class TokenLayerNorm(nn.LayerNorm):
         LN(x + r) (see forward_windows)."""
         if self.elementwise_affine and self.bias is not None and ops.layer_norm_supported(x, self.weight) \
                 and r.shape == x.shape and r.dtype == x.dtype and not torch.is_autocast_enabled():
+            if quant == "rows" and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+                s, y, yq, ys = ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, quant="rows")
+                return s, y, (yq, ys)                  # [rows, C] e4m3, [rows, 1] f32
             if quant and x.dtype == torch.bfloat16 and x.shape[-1] % 32 == 0:
                 s, y, yq, ys = ops.add_layer_norm(x, r, self.weight, self.bias, self.eps, sink, quant=True)
                 return s, y, (yq.view(y.shape), ys.view(*y.shape[:-1], -1))
@@ -984,9 +989,10 @@ def mlp_fp8(x, w1, b1, w2, b2, xq=None):
     LayerNorm), if it made one."""
     K1, N1 = w1.shape[1], w1.shape[0]
     if FP8_GEMM == "rows":
-        # fc1 on the rowwise fp8 GEMM where it pays, then ONE pass for GELU + fc2's fp8 rows
+        # fc1 on the rowwise fp8 GEMM where it pays (x's row-scaled copy from the LayerNorm
+        # when it made one), then ONE pass for GELU + fc2's fp8 rows
         M = x.numel() // K1
-        h = linear_fp8_tokens(x, w1, b1)
+        h = linear_fp8_tokens(x, w1, b1, xq)
         if _fp8_rows_ready(h, w2, b2) and fp8_rows_ok(M, w2.shape[0], N1) and h.is_contiguous():
             if torch.is_grad_enabled() and h.requires_grad:
                 y, yq, ys = ops.gelu_row_quant(h)

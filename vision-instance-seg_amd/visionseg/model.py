@@ -161,7 +161,19 @@ class SwinBlock(nn.Module):
         # their MX operand copies; the rowwise backend (linear.FP8_GEMM "rows") quantises in
         # linear_fp8_tokens / the MLP's fused GELU pass instead
         q8 = self.linear_fp8 and fp8_operand_ok(C) and linear_mod.FP8_GEMM == "mx"
-        if q8:
+        # rowwise backend: the norms write the row-scaled e4m3 copy of their output where the
+        # consuming Linear (qkv: C -> 3C, fc1: C -> 4C) takes the fp8 GEMM
+        Mw = wr.total if wr is not None else B * L
+        r_qkv = self.linear_fp8 and linear_mod.FP8_GEMM == "rows" and linear_mod.fp8_rows_ok(Mw, 3 * C, C)
+        r_fc1 = (self.linear_fp8 and linear_mod.FP8_GEMM == "rows"
+                 and linear_mod.fp8_rows_ok(B * L, self.mlp.fc1.weight.shape[0], C))
+        if r_qkv:
+            if res is None:
+                h, hq = self.norm1.forward_windows(x, wr, quant="rows")
+            else:
+                x, h, hq = self.norm1.add_forward_windows(x, res, wr, quant="rows")
+            qkv = linear_fp8_tokens(h.view(-1, ws * ws, C), self.attn.qkv.weight, self.attn.qkv.bias, hq)
+        elif q8:
             # the norms also write their output as the fp8 GEMM operand (no quantisation pass)
             if res is None:
                 h, hq = self.norm1.forward_windows(x, wr, quant=True)
@@ -172,19 +184,22 @@ class SwinBlock(nn.Module):
             h = self.norm1.forward_windows(x, wr)
         else:
             x, h = self.norm1.add_forward_windows(x, res, wr)
-        if not q8:
+        if not (q8 or r_qkv):
             qkv = (linear_fp8_tokens(h.view(-1, ws * ws, C), self.attn.qkv.weight, self.attn.qkv.bias)
                    if self.linear_fp8 else self.attn.qkv(h.view(-1, ws * ws, C)))
         # output in the image layout (window reverse folded into the kernel); the per-token
         # proj commutes with the crop
         o = ops.window_attention_image(qkv, self.attn.rel_table, self.attn.heads, ws, shift, B, H, W,
                                        fp8=self.attn_fp8 and qkv.dtype == torch.bfloat16)
-        if self.linear_fp8:
+        # proj (C -> C): the MX backend only; on the rowwise backend its input would need a
+        # quantisation pass of its own, which costs what the fp8 GEMM saves (Swin-L stage 3:
+        # 0.0355 vs 0.0432 ms, tools/r5/scaled_mm_probe.py)
+        if self.linear_fp8 and linear_mod.FP8_GEMM == "mx":
             o = linear_fp8_tokens(o.view(B, H * W, C), self.attn.proj.weight, self.attn.proj.bias)
         else:
             o = self.attn.proj(o.view(B, H * W, C))
-        if q8:
-            x, h2, h2q = self.norm2.add_forward(x, o, quant=True)
+        if q8 or r_fc1:
+            x, h2, h2q = self.norm2.add_forward(x, o, quant="rows" if r_fc1 else True)
             return x, self.mlp(h2, h2q)
         x, h2 = self.norm2.add_forward(x, o)
         return x, self.mlp(h2)

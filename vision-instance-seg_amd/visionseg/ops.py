@@ -1022,7 +1022,23 @@ class LayerNormFunction(torch.autograd.Function):
         mean = torch.empty(M, device=x.device, dtype=torch.float32)
         rstd = torch.empty(M, device=x.device, dtype=torch.float32)
         with timed("layer_norm_fwd", xc, bytes_=2 * xc.numel() * xc.element_size()):
-            if quant:
+            if quant == "rows":              # row-scaled e4m3 copy for the vendor rowwise fp8 GEMM
+                rows = wrows.total if wrows is not None else M
+                y = torch.empty(rows, C, device=x.device, dtype=xc.dtype)
+                yq = torch.empty(rows, C, device=x.device, dtype=torch.uint8)
+                ys = torch.empty(rows, 1, device=x.device, dtype=torch.float32)
+                L.check(L.lib().vs_layer_norm_forward_qr(L.ptr(xc), L.ptr(weight), L.ptr(bias), L.ptr(y), L.ptr(yq),
+                                                         L.ptr(ys), L.ptr(mean), L.ptr(rstd), M, C, float(eps),
+                                                         L.ptr(wrows.rows) if wrows is not None else None,
+                                                         L.stream(xc)), "layer_norm_forward_qr")
+                if wrows is None:
+                    y = y.view(xc.shape)
+                elif wrows.pad.numel():
+                    y.index_fill_(0, wrows.pad, 0)
+                    yq.index_fill_(0, wrows.pad, 0)
+                    ys.index_fill_(0, wrows.pad, 1.0)
+                yq = yq.view(torch.float8_e4m3fn)
+            elif quant:
                 y = torch.empty(wrows.total, C, device=x.device, dtype=xc.dtype)
                 yq = torch.empty(wrows.total, C, device=x.device, dtype=torch.uint8)
                 ys = torch.empty(wrows.total, C // 32, device=x.device, dtype=torch.uint8)
@@ -1110,7 +1126,24 @@ class AddLayerNormFunction(torch.autograd.Function):
         mean = torch.empty(M, device=x.device, dtype=torch.float32)
         rstd = torch.empty(M, device=x.device, dtype=torch.float32)
         with timed("add_layer_norm_fwd", xc, bytes_=4 * xc.numel() * xc.element_size()):
-            if quant:
+            if quant == "rows":              # row-scaled e4m3 copy for the vendor rowwise fp8 GEMM
+                rows = wrows.total if wrows is not None else M
+                y = torch.empty(rows, C, device=x.device, dtype=xc.dtype)
+                yq = torch.empty(rows, C, device=x.device, dtype=torch.uint8)
+                ys = torch.empty(rows, 1, device=x.device, dtype=torch.float32)
+                L.check(L.lib().vs_add_layer_norm_forward_qr(L.ptr(xc), L.ptr(rc), L.ptr(weight), L.ptr(bias),
+                                                             L.ptr(s), L.ptr(y), L.ptr(yq), L.ptr(ys), L.ptr(mean),
+                                                             L.ptr(rstd), M, C, float(eps),
+                                                             L.ptr(wrows.rows) if wrows is not None else None,
+                                                             L.stream(xc)), "add_layer_norm_forward_qr")
+                if wrows is None:
+                    y = y.view(xc.shape)
+                elif wrows.pad.numel():
+                    y.index_fill_(0, wrows.pad, 0)
+                    yq.index_fill_(0, wrows.pad, 0)
+                    ys.index_fill_(0, wrows.pad, 1.0)
+                yq = yq.view(torch.float8_e4m3fn)
+            elif quant:
                 rows = wrows.total if wrows is not None else M
                 y = torch.empty(rows, C, device=x.device, dtype=xc.dtype)
                 yq = torch.empty(rows, C, device=x.device, dtype=torch.uint8)
