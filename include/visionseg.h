@@ -82,6 +82,18 @@ VS_API int vs_msda_backward(int dtype, const void* value, const int64_t* spatial
                      int num_heads, int channels, int num_levels, int num_query,
                      int num_point, void* stream);
 
+/* vs_msda_backward with a workspace (vs_msda_backward_workspace_bytes bytes, any content):
+ * bf16 encoder problems (queries = the value grid, P = 4) then take the destination-tile
+ * kernel -- every grad_value cell written once with plain stores, no memset, deterministic;
+ * taps further than 4 cells from their query's reference point go through a far-tap list
+ * and f32 atomics afterwards.  Other problems: as vs_msda_backward. */
+VS_API long long vs_msda_backward_workspace_bytes(int B, int Q, int heads, int L, int P);
+VS_API int vs_msda_backward_ex(int dtype, const void* value, const int64_t* spatial_shapes,
+                               const int64_t* level_start, const float* loc, const float* attn,
+                               const void* grad_out, float* grad_value, float* grad_loc, float* grad_attn,
+                               void* workspace, int B, int S, int heads, int D, int L, int Q, int P,
+                               void* stream);
+
 /* Opt-in backward (VS_MSDA_BWD=tiled; replaces ms_deform_attn_backward like the others):
  * grad_value by destination tiles
  * (image, head, level, te x te cells), each owned by one wave that accumulates its

@@ -40,7 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="msda,mask,win,xattn")
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--msda-modes", default="col,prod,binned,tiled")
+    ap.add_argument("--msda-modes", default="dst,col,prod,binned,tiled")
     a = ap.parse_args()
     dev = "cuda"
     bf = torch.bfloat16
@@ -60,7 +60,12 @@ def main():
         # offsets (pixels of the sampled level): iid uniform +-4 px per query (worst case for
         # the register carry) and a smooth field (per-head pattern + 0.3 px jitter), which is
         # what the encoder's Linear(query) offsets look like between neighbouring pixels
-        offs = {"iid4px": (torch.rand(B, S, H, L, P, 2, device=dev, generator=g) * 2 - 1) * 4,
+        th = torch.arange(H, device=dev, dtype=torch.float32) * (2.0 * 3.141592653589793 / H)
+        grid0 = torch.stack([th.cos(), th.sin()], -1)
+        grid0 = grid0 / grid0.abs().max(-1, keepdim=True)[0]
+        init = grid0.view(H, 1, 1, 2) * torch.arange(1, P + 1, device=dev, dtype=torch.float32).view(1, 1, P, 1)
+        offs = {"init": init.view(1, 1, H, 1, P, 2).expand(B, S, H, L, P, 2).contiguous(),   # the bench's (model init)
+                "iid4px": (torch.rand(B, S, H, L, P, 2, device=dev, generator=g) * 2 - 1) * 4,
                 "smooth": (torch.randn(1, 1, H, L, P, 2, device=dev, generator=g) * 2
                            + 0.3 * torch.randn(B, S, H, L, P, 2, device=dev, generator=g))}
         for oname, off in offs.items():
@@ -83,7 +88,8 @@ def main():
                 os.environ["VS_MSDA_SKEL"] = mode[4:] if mode.startswith("skel") else "2"
                 # col: the pyramid-column kernel (default, 8x16 blocks), col16: 16x16 blocks;
                 # every other mode runs the 8 x 8 tile kernel (VS_MSDA_COL=0)
-                os.environ["VS_MSDA_COL"] = {"col": "8x16", "col16": "16x16", "col8": "8x8"}.get(mode, "0")
+                # dst: the destination-tile kernel (the default of the torch op)
+                os.environ["VS_MSDA_COL"] = {"col": "8x16", "col16": "16x16", "col8": "8x8", "dst": "dst"}.get(mode, "0")
 
                 def fb():
                     o = ops.ms_deform_attn(v, shapes, locr, wr)

@@ -114,10 +114,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> msda_bwd(const at::Tensor& value,
   // grad_value accumulates in f32 (float atomics), then takes value's dtype
   at::Tensor gv = at::empty({d.B, d.S, d.H, d.D}, v.options().dtype(at::kFloat));
   at::Tensor gl = at::empty_like(loc), ga = at::empty_like(aw);
-  vs_ok(vs_msda_backward(dcode(v), v.data_ptr(), sh.data(), st.data(), loc.data_ptr<float>(), aw.data_ptr<float>(),
-                         g.data_ptr(), gv.data_ptr<float>(), gl.data_ptr<float>(), ga.data_ptr<float>(),
-                         as_int(d.B, "batch"), as_int(d.S, "S"), as_int(d.H, "heads"), as_int(d.D, "channels"),
-                         as_int(d.L, "levels"), as_int(d.Q, "queries"), as_int(d.P, "points"), cur_stream(v)),
+  // workspace of the destination-tile backward (its far-tap list; csrc/msda.hip)
+  const long long wsb = vs_msda_backward_workspace_bytes(as_int(d.B, "batch"), as_int(d.Q, "queries"),
+                                                         as_int(d.H, "heads"), as_int(d.L, "levels"),
+                                                         as_int(d.P, "points"));
+  TORCH_CHECK(wsb >= 0, "msda_bwd: bad sizes");
+  at::Tensor ws = at::empty({wsb}, v.options().dtype(at::kByte));
+  vs_ok(vs_msda_backward_ex(dcode(v), v.data_ptr(), sh.data(), st.data(), loc.data_ptr<float>(),
+                            aw.data_ptr<float>(), g.data_ptr(), gv.data_ptr<float>(), gl.data_ptr<float>(),
+                            ga.data_ptr<float>(), ws.data_ptr(), as_int(d.B, "batch"), as_int(d.S, "S"),
+                            as_int(d.H, "heads"), as_int(d.D, "channels"), as_int(d.L, "levels"),
+                            as_int(d.Q, "queries"), as_int(d.P, "points"), cur_stream(v)),
         "msda_bwd");
   return {(v.scalar_type() == at::kFloat || f32_grad_value) ? gv : gv.to(v.scalar_type()), gl, ga};
 }

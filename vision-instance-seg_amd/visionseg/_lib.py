@@ -30,6 +30,8 @@ SIGNATURES = {
     "vs_last_error": [],
     "vs_msda_forward": [_c_int, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_msda_backward": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
+    "vs_msda_backward_workspace_bytes": [_c_int] * 5,
+    "vs_msda_backward_ex": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_msda_backward_tiled_workspace_bytes": [_c_int] * 5 + [_P],
     "vs_msda_backward_tiled": [_c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 7 + [_P],
     "vs_msda_prep_forward": [_c_int, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P, _P,
@@ -121,6 +123,7 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_group_norm_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_nchw_workspace_bytes": ctypes.c_longlong,
             "vs_msda_backward_tiled_workspace_bytes": ctypes.c_longlong,
+            "vs_msda_backward_workspace_bytes": ctypes.c_longlong,
             "vs_match_cost_factors_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
