@@ -1364,7 +1364,9 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
         if (wave < nmt) {
           const int c = 32 * wave + r;
           if (c < ncell) {
-            const bf16* vr = value + lbase + (size_t)((y0 + c / bw) * Wl + x0 + c % bw) * rowstride + 8 * hh;
+            const unsigned inv = (65536u + (unsigned)bw - 1u) / (unsigned)bw;   // c / bw by multiply-shift
+            const unsigned cy = __umul24((unsigned)c, inv) >> 16, cx = (unsigned)c - __umul24(cy, (unsigned)bw);
+            const bf16* vr = value + lbase + (size_t)((y0 + (int)cy) * Wl + x0 + (int)cx) * rowstride + 8 * hh;
             bv0 = ld8(vr);
             bv1 = ld8(vr + 16);
           }
@@ -1451,11 +1453,21 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
             *reinterpret_cast<float4*>(sW + (rb + zrow) * kWP8 + 16 * wave + 4 * (lane & 3)) = z4;
         }
         if (any && wave < nmt) {              // one flush per (band, cell) for the whole column
+          // cell -> (row, column) of the band by a multiply-shift (c < 128, bw <= 128: exact
+          // with ceil(2^16 / bw)), 32-bit offsets from the (uniform) level base: the integer
+          // division and 64-bit address of every flushed row were ~40 VALU per atomic
+          const unsigned inv = (65536u + (unsigned)bw - 1u) / (unsigned)bw;
+          float* gvb = gvalue + lbase;
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int c = 32 * wave + crow(i, hh);
-            if (c < ncell && acc[i] != 0.f)
-              atomicAdd(gvalue + lbase + (size_t)((y0 + c / bw) * Wl + x0 + c % bw) * rowstride + r, acc[i]);
+            if (c < ncell && acc[i] != 0.f) {
+              // 24-bit multiplies: c * inv < 2^24, cells x rowstride < 2^24 at the encoder sizes
+              // (checked on the host: S * heads * 32 < 2^24)
+              const unsigned cy = __umul24((unsigned)c, inv) >> 16, cx = (unsigned)c - __umul24(cy, (unsigned)bw);
+              const unsigned cell = __umul24((unsigned)(y0 + (int)cy), (unsigned)Wl) + (unsigned)(x0 + (int)cx);
+              atomicAdd(gvb + (__umul24(cell, (unsigned)rowstride) + (unsigned)r), acc[i]);
+            }
           }
         }
       }
@@ -1964,12 +1976,16 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   split = split && P == 4;
   // destination tiles (default for bf16 encoder problems with a workspace; VS_MSDA_DST=0:
   // the pyramid-column kernel): every grad_value cell written once, no memset
+  // Opt-in (VS_MSDA_COL=dst or VS_MSDA_DST=1): measured SLOWER than the column kernel at
+  // the C2 encoder shapes (tools/kbench.py: 0.69 vs 0.39 ms, init offsets) -- a query's 4
+  // points land in 2-4 tiles per level, so each query is built into W about twice as often
+  // as in the column walk -- but every cell is written once, deterministic for near taps.
   bool dst = ws != nullptr && split && dtype == VS_BF16 && Q == S && Q > 0 &&
              (long long)B * Q * Hh * L * P < (1LL << 31);
-  if (const char* e = getenv("VS_MSDA_DST")) dst = dst && atoi(e) != 0;
-  if (const char* e = getenv("VS_MSDA_MFMA")) dst = dst && atoi(e) != 0;
-  if (const char* e = getenv("VS_MSDA_GEOM")) dst = dst && atoi(e) != 0;
-  if (const char* e = getenv("VS_MSDA_COL")) dst = dst && strcmp(e, "dst") == 0;
+  bool want = false;
+  if (const char* e = getenv("VS_MSDA_DST")) want = atoi(e) != 0;
+  if (const char* e = getenv("VS_MSDA_COL")) want = want || strcmp(e, "dst") == 0;
+  dst = dst && want;
   if (dst) {
     DstGeo dg;
     dst_geo(lv, L, &dg);
@@ -2023,7 +2039,7 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     ColGeo cg;
     const int nch = ccy > 0 && ccx > 0 ? col_geo(lv, L, ccy, ccx, &cg) : 0;
     const long long nbc = nch > 0 ? (long long)B * cg.per_image * Hh : 0;
-    if (mfma && fused && bt.mode == 1 && nch > 0 && nbc < (1LL << 31)) {
+    if (mfma && fused && bt.mode == 1 && nch > 0 && nbc < (1LL << 31) && (long long)S * Hh * kD < (1LL << 24)) {
       if (nch <= 3)
         hipLaunchKernelGGL((msda_bwd_col_kernel<3>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,
                            (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc);
