@@ -640,6 +640,34 @@ VS_API int vs_upsample_add_forward(int dtype, const void* cur, const void* src, 
  * grad_out [B, C, H, W]; fixed-order gather, no atomics. */
 VS_API int vs_upsample_backward(int dtype, const void* grad_out, void* grad_src, int batch, int channels, int height,
                                 int width, int src_height, int src_width, void* stream);
+/* Channels-last forms (the bf16 NHWC 1/4-resolution tail): cur / out / grad_out
+ * [B, H, W, C] contiguous, src / grad_src token-major [B, Hs*Ws, C]; C % 8 == 0, operands
+ * 16-B aligned.  Same arithmetic as the NCHW forms. */
+VS_API int vs_upsample_add_forward_nhwc(int dtype, const void* cur, const void* src, void* out, int batch,
+                                        int channels, int height, int width, int src_height, int src_width,
+                                        long long src_batch_stride, void* stream);
+VS_API int vs_upsample_backward_nhwc(int dtype, const void* grad_out, void* grad_src, int batch, int channels,
+                                     int height, int width, int src_height, int src_width, void* stream);
+
+/* ---- a9: the FPN's 3 x 3 output conv on NHWC planes (replaces MIOpen's conv + layout
+ * transposes under nn.Conv2d(256, 256, 3, padding=1, bias=False), HF:m2f:1394-1419).
+ * Stride 1, padding 1, bf16, channels-last x [B, H, W, Ci], y [B, H, W, Co].
+ * vs_conv3x3_forward: y = conv(x) (+ bias[Co] when non-NULL) with the weights in the layout
+ * w_fwd [Co, 3, 3, Ci]; Ci % 64 == 0, Co % 8 == 0.  The input gradient is the same call on
+ * grad_y with w_bwd [Ci, 3, 3, Co] (the flipped transpose: Ci and Co swap roles).
+ * vs_conv3x3_weight_layouts: w [Co, Ci, 3, 3] (torch) -> w_fwd and/or w_bwd (either NULL).
+ * vs_conv3x3_wgrad: dw [Co, Ci, 3, 3] (dtype VS_BF16 / VS_F32, overwritten) = sum over pixels
+ * of grad_y (x) x-neighbourhood; f32 partial sums in workspace (size from
+ * vs_conv3x3_wgrad_workspace_bytes, 0 = unsupported shape), reduced in a fixed order.
+ * Ci % 128 == 0 and Co % 128 == 0. */
+VS_API int vs_conv3x3_forward(const void* x, const void* w_fwd, const void* bias, void* y, int batch, int height,
+                              int width, int in_channels, int out_channels, void* stream);
+VS_API int vs_conv3x3_weight_layouts(const void* w, void* w_fwd, void* w_bwd, int out_channels, int in_channels,
+                                     void* stream);
+VS_API long long vs_conv3x3_wgrad_workspace_bytes(int batch, int height, int width, int in_channels,
+                                                  int out_channels);
+VS_API int vs_conv3x3_wgrad(int dtype, const void* grad_y, const void* x, void* dw, void* workspace, int batch,
+                            int height, int width, int in_channels, int out_channels, void* stream);
 
 #ifdef __cplusplus
 }

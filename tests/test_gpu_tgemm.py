@@ -361,3 +361,45 @@ def test_layer_norm_row_quant_equals_row_quantize(C, shift, res):
     assert torch.equal(y.view(-1, C), y_ref.view(-1, C))
     eq, es = ops.row_quantize_fp8(y.view(-1, C))
     assert torch.equal(yq.view(torch.uint8), eq.view(torch.uint8)) and torch.equal(ys.view(-1, 1), es)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_plane_projections_vs_conv1x1(dtype):
+    """linear.token_plane_projection (token-major -> NCHW planes, the pixel decoder's lateral
+    conv) and linear.plane_projection (NCHW planes -> channels-last planes, the mask projection) vs
+    F.conv2d with a 1x1 kernel: outputs and all three gradients (f32: 1e-4 relative; bf16:
+    one output rounding + f32-accumulated products, 2e-2 relative)."""
+    import torch.nn.functional as F
+    from visionseg.linear import plane_projection, token_plane_projection
+    g = torch.Generator().manual_seed(5)
+    B, Ci, Co, H, W = 2, 96, 256, 24, 20
+    x = torch.randn(B, H * W, Ci, generator=g).to(DEV, dtype)
+    w = (torch.randn(Co, Ci, 1, 1, generator=g) / Ci ** 0.5).to(DEV, dtype)
+    b = torch.randn(Co, generator=g).to(DEV, dtype)
+    gy = torch.randn(B, Co, H, W, generator=g).to(DEV, dtype)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+
+    def rel(a, r):
+        return float((a.float() - r.float()).norm() / r.float().norm())
+
+    xs, ws, bs = (t.clone().requires_grad_() for t in (x, w, b))
+    y = token_plane_projection(xs, ws, bs, H, W)
+    y.backward(gy)
+    xr, wr, br = (t.float().clone().requires_grad_() for t in (x, w, b))
+    yr = F.conv2d(xr.view(B, H, W, Ci).permute(0, 3, 1, 2), wr, br)
+    yr.backward(gy.float())
+    assert y.shape == (B, Co, H, W) and y.is_contiguous()
+    for a, r in ((y, yr), (xs.grad, xr.grad), (ws.grad, wr.grad), (bs.grad, br.grad)):
+        assert rel(a, r) <= tol
+    # the reverse direction: planes [B, Co, H, W] -> channels-last planes [B, Ci, H, W]
+    w2 = (torch.randn(Ci, Co, 1, 1, generator=g) / Co ** 0.5).to(DEV, dtype)
+    p = gy.clone().requires_grad_()
+    w2s = w2.clone().requires_grad_()
+    t = plane_projection(p, w2s, None)
+    gt = torch.randn(t.shape, generator=g).to(DEV, dtype)
+    t.backward(gt)
+    pr, w2r = gy.float().clone().requires_grad_(), w2.float().clone().requires_grad_()
+    tr = F.conv2d(pr, w2r)
+    tr.backward(gt.float())
+    assert t.shape == tr.shape and rel(t, tr) <= tol
+    assert rel(p.grad, pr.grad) <= tol and rel(w2s.grad, w2r.grad) <= tol

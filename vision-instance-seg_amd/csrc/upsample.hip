@@ -218,6 +218,88 @@ __global__ void __launch_bounds__(256) upsample_bwd2x_kernel(const T* __restrict
   }
 }
 
+// Channels-last variants (the pixel decoder's NHWC 1/4-resolution tail: cur / out / dout
+// are [B, H, W, C], src / dsrc token-major [B, Hs*Ws, C]).  A thread owns 16 bytes of
+// channels of one pixel: the forward reads the four source tokens' runs (L2-resident:
+// neighbouring outputs share them) and writes out coalesced; the backward gathers, for one
+// source token, the <= 4 x 4 output pixels whose taps reach it (adjoint weights from the
+// forward's index rule, boundaries included), fixed order, written once.
+template <typename T>
+__global__ void __launch_bounds__(256) upsample_add_nhwc_kernel(const T* __restrict__ cur, const T* __restrict__ src,
+                                                                T* __restrict__ out, int C, int H, int W, int Hs,
+                                                                int Ws, long long src_bstride, long long nvec) {
+  constexpr int V = Vec16<T>::N;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nvec) return;
+  const int cv = C / V;
+  const int c = (int)(idx % cv) * V;
+  const long long pix = idx / cv;
+  const int x = (int)(pix % W);
+  const long long by = pix / W;
+  const int y = (int)(by % H), b = (int)(by / H);
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  up_index(y, Hs, H, y0, y1, ly0, ly1);
+  up_index(x, Ws, W, x0, x1, lx0, lx1);
+  const T* sb = src + (size_t)b * src_bstride + c;
+  float s00[V], s01[V], s10[V], s11[V], cv_[V], o[V];
+  Vec16<T>::load(sb + ((size_t)y0 * Ws + x0) * C, s00);
+  Vec16<T>::load(sb + ((size_t)y0 * Ws + x1) * C, s01);
+  Vec16<T>::load(sb + ((size_t)y1 * Ws + x0) * C, s10);
+  Vec16<T>::load(sb + ((size_t)y1 * Ws + x1) * C, s11);
+  Vec16<T>::load(cur + pix * C + c, cv_);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const float up = ly0 * (lx0 * s00[k] + lx1 * s01[k]) + ly1 * (lx0 * s10[k] + lx1 * s11[k]);
+    o[k] = cv_[k] + to_f32(from_f32<T>(up));
+  }
+  Vec16<T>::store(out + pix * C + c, o);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) upsample_bwd_nhwc_kernel(const T* __restrict__ dout, T* __restrict__ dsrc, int C,
+                                                                int H, int W, int Hs, int Ws, long long nvec) {
+  constexpr int V = Vec16<T>::N, kMax = 8;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nvec) return;
+  const int cv = C / V;
+  const int c = (int)(idx % cv) * V;
+  const long long sp = idx / cv;
+  const int sx = (int)(sp % Ws);
+  const long long bsy = sp / Ws;
+  const int sy = (int)(bsy % Hs), b = (int)(bsy / Hs);
+  const float scy = (float)H / (float)Hs, scx = (float)W / (float)Ws;
+  const int ylo = max(0, (int)floorf(scy * (sy - 0.5f) - 0.5f) - 1);
+  const int yhi = min(H - 1, min(ylo + kMax - 1, (int)ceilf(scy * (sy + 1.5f) - 0.5f) + 1));
+  const int xlo = max(0, (int)floorf(scx * (sx - 0.5f) - 0.5f) - 1);
+  const int xhi = min(W - 1, min(xlo + kMax - 1, (int)ceilf(scx * (sx + 1.5f) - 0.5f) + 1));
+  float wx[kMax];
+#pragma unroll
+  for (int k = 0; k < kMax; ++k) wx[k] = (xlo + k <= xhi) ? adj_w(xlo + k, sx, Ws, W) : 0.f;
+  float acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = 0.f;
+  const T* base = dout + (size_t)b * H * W * C + c;
+  for (int y = ylo; y <= yhi; ++y) {
+    const float wy = adj_w(y, sy, Hs, H);
+    if (wy == 0.f) continue;
+    float row[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) row[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < kMax; ++j) {
+      if (wx[j] == 0.f) continue;
+      float v[V];
+      Vec16<T>::load(base + ((size_t)y * W + xlo + j) * C, v);
+#pragma unroll
+      for (int k = 0; k < V; ++k) row[k] += wx[j] * v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] += wy * row[k];
+  }
+  Vec16<T>::store(dsrc + sp * C + c, acc);
+}
+
 }  // namespace
 }  // namespace vs
 
@@ -266,6 +348,50 @@ extern "C" int vs_upsample_backward(int dtype, const void* grad_out, void* grad_
   else
     hipLaunchKernelGGL(upsample_bwd_kernel<float>, grid, dim3(256), 0, st, (const float*)grad_out, (float*)grad_src,
                        C, H, W, Hs, Ws);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_upsample_add_forward_nhwc(int dtype, const void* cur, const void* src, void* out, int B, int C,
+                                            int H, int W, int Hs, int Ws, long long src_batch_stride, void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && Hs > 0 && Ws > 0, "bad sizes (C % 8 == 0)");
+  VS_CHECK(Hs <= H && Ws <= W && 2 * Hs >= H && 2 * Ws >= W, "upsampling factor must lie in [1, 2]");
+  VS_CHECK(cur && src && out, "null pointer");
+  VS_CHECK(((uintptr_t)cur & 15) == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+               src_batch_stride % 8 == 0,
+           "16-B aligned operands");
+  const int V = dtype == VS_BF16 ? 8 : 4;
+  const long long nvec = (long long)B * H * W * (C / V);
+  const dim3 g((unsigned)((nvec + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(upsample_add_nhwc_kernel<bf16>, g, dim3(256), 0, st, (const bf16*)cur, (const bf16*)src,
+                       (bf16*)out, C, H, W, Hs, Ws, src_batch_stride, nvec);
+  else
+    hipLaunchKernelGGL(upsample_add_nhwc_kernel<float>, g, dim3(256), 0, st, (const float*)cur, (const float*)src,
+                       (float*)out, C, H, W, Hs, Ws, src_batch_stride, nvec);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_upsample_backward_nhwc(int dtype, const void* grad_out, void* grad_src, int B, int C, int H, int W,
+                                         int Hs, int Ws, void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && Hs > 0 && Ws > 0, "bad sizes (C % 8 == 0)");
+  VS_CHECK(Hs <= H && Ws <= W && 2 * Hs >= H && 2 * Ws >= W, "upsampling factor must lie in [1, 2]");
+  VS_CHECK(grad_out && grad_src, "null pointer");
+  VS_CHECK(((uintptr_t)grad_out & 15) == 0 && ((uintptr_t)grad_src & 15) == 0, "16-B aligned operands");
+  const int V = dtype == VS_BF16 ? 8 : 4;
+  const long long nvec = (long long)B * Hs * Ws * (C / V);
+  const dim3 g((unsigned)((nvec + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(upsample_bwd_nhwc_kernel<bf16>, g, dim3(256), 0, st, (const bf16*)grad_out, (bf16*)grad_src,
+                       C, H, W, Hs, Ws, nvec);
+  else
+    hipLaunchKernelGGL(upsample_bwd_nhwc_kernel<float>, g, dim3(256), 0, st, (const float*)grad_out,
+                       (float*)grad_src, C, H, W, Hs, Ws, nvec);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

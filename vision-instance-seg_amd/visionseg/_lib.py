@@ -113,6 +113,12 @@ SIGNATURES = {
     "vs_group_norm_nchw_backward": [_c_int] + [_P] * 10 + [_c_int] * 5 + [_P],
     "vs_upsample_add_forward": [_c_int, _P, _P, _P] + [_c_int] * 6 + [ctypes.c_longlong, _P],
     "vs_upsample_backward": [_c_int, _P, _P] + [_c_int] * 6 + [_P],
+    "vs_upsample_add_forward_nhwc": [_c_int, _P, _P, _P] + [_c_int] * 6 + [ctypes.c_longlong, _P],
+    "vs_upsample_backward_nhwc": [_c_int, _P, _P] + [_c_int] * 6 + [_P],
+    "vs_conv3x3_forward": [_P, _P, _P, _P] + [_c_int] * 5 + [_P],
+    "vs_conv3x3_weight_layouts": [_P, _P, _P, _c_int, _c_int, _P],
+    "vs_conv3x3_wgrad_workspace_bytes": [_c_int] * 5,
+    "vs_conv3x3_wgrad": [_c_int, _P, _P, _P, _P] + [_c_int] * 5 + [_P],
 }
 RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": ctypes.c_longlong,
             "vs_mask_head_backward_workspace_bytes": ctypes.c_longlong,
@@ -124,7 +130,8 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_group_norm_nchw_workspace_bytes": ctypes.c_longlong,
             "vs_msda_backward_tiled_workspace_bytes": ctypes.c_longlong,
             "vs_msda_backward_workspace_bytes": ctypes.c_longlong,
-            "vs_match_cost_factors_workspace_bytes": ctypes.c_longlong}
+            "vs_match_cost_factors_workspace_bytes": ctypes.c_longlong,
+            "vs_conv3x3_wgrad_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
 _tops = None

@@ -204,6 +204,49 @@ def _plane_weight_grad(gp, y3, out_dtype):
     return out
 
 
+class _TokenPlaneFn(torch.autograd.Function):
+    """1x1 convolution from token-major input to NCHW planes: out[b, o, p] = sum_i W[o, i]
+    x[b, p, i] + bias[o] (the pixel decoder's lateral conv on the stage-1 Swin feature,
+    HF:m2f:1394-1405).  x^T is read in place as a column-major operand, so the NCHW copy of
+    the [B, 96, 256, 256] feature that nn.Conv2d needed (~0.1 ms at C2) is gone; backward:
+    dX = dY^T W (dY's planes column-major in place), dW = sum_b dY_b X_b, db = sum dY."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, H, W):
+        B, HW, Ci = x.shape
+        Co = weight.shape[0]
+        w2 = weight.view(Co, Ci).unsqueeze(0).expand(B, Co, Ci)
+        xt = x.transpose(1, 2)                                           # [B, Ci, HW] column-major view
+        if bias is not None:
+            out = torch.baddbmm(bias.view(1, Co, 1).expand(B, Co, HW), w2, xt)
+        else:
+            out = torch.bmm(w2, xt)
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return out.view(B, Co, H, W)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        B, HW, Ci = x.shape
+        Co = weight.shape[0]
+        g3 = gy.contiguous().view(B, Co, HW).to(x.dtype)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.bmm(g3.transpose(1, 2), weight.view(Co, Ci).to(x.dtype).unsqueeze(0).expand(B, Co, Ci))
+        if ctx.needs_input_grad[1]:
+            gw = torch.bmm(g3, x).float().sum(0).to(weight.dtype).view_as(weight)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = g3.sum((0, 2), dtype=torch.float32).to(weight.dtype)
+        return gx, gw, gb, None, None
+
+
+def token_plane_projection(x, weight, bias, H, W):
+    """nn.Conv2d(k=1) of a token-major [B, H*W, Ci] tensor -> NCHW [B, Co, H, W] (see
+    _TokenPlaneFn)."""
+    return _TokenPlaneFn.apply(x, weight, bias, H, W)
+
+
 def plane_projection(y, weight, bias=None):
     """nn.Conv2d(k=1) of an NCHW tensor returned as a channels-last NCHW view (memory
     [B, H, W, Co]): the mask projection whose output the mask head reads token-major."""
@@ -347,8 +390,12 @@ class _InProjFn(torch.autograd.Function):
     the level memory (split-K dW, HIP column sums)."""
 
     @staticmethod
-    def forward(ctx, xq, xk, xv, weight, bias, q_pos=None, sink=None, psink=None):
+    def forward(ctx, xq, xk, xv, weight, bias, q_pos=None, sink=None, psink=None, kv_sink=None):
         D = weight.shape[1]
+        # kv_sink (ops.GradSink of the level memory m, with xk = m + pos and xv = m): dxk and
+        # dxv are summed into the sink's buffer by the dX GEMMs themselves (beta = 1), over
+        # every layer that reads this level -- no add of the two, no add across layers
+        ctx.kv_sink = kv_sink
         W = (weight[:D], weight[D:2 * D], weight[2 * D:])
         B = (bias[:D], bias[D:2 * D], bias[2 * D:])
         T = xq.numel() // D
@@ -407,19 +454,27 @@ class _InProjFn(torch.autograd.Function):
                 gx.append(gxq.view(gq.shape) if ctx.needs_input_grad[0] else None)
                 gpos = gpos.view(gq.shape) if (gpos is not None and ctx.psink is None) else None
                 continue
-            gxi = (g2 @ w_i).view(x.shape) if (ctx.needs_input_grad[i] or (i == 0 and want_pos)) else None
-            if i == 0 and want_pos:
-                gpos = gxi
-            gx.append(gxi if ctx.needs_input_grad[i] else None)
+            if i > 0 and ctx.kv_sink is not None:
+                ks = ctx.kv_sink
+                if ks.buf is None:
+                    ks.buf = g2 @ w_i
+                else:
+                    ks.buf.addmm_(g2, w_i)
+                gx.append(None)
+            else:
+                gxi = (g2 @ w_i).view(x.shape) if (ctx.needs_input_grad[i] or (i == 0 and want_pos)) else None
+                if i == 0 and want_pos:
+                    gpos = gxi
+                gx.append(gxi if ctx.needs_input_grad[i] else None)
             weight_grad(g2, x2.to(g2.dtype), weight.dtype, out=gw[rows])
             if D % 8 == 0 and D <= 2048 and g2.dtype == weight.dtype:
                 ops.column_sum(g2, out=gb[rows])
             else:
                 gb[rows].copy_(g2.sum(0, dtype=torch.float32))
-        return gx[0], gx[1], gx[2], gw, gb, gpos, None, None
+        return gx[0], gx[1], gx[2], gw, gb, gpos, None, None, None
 
 
-def in_projection(xq, xk, xv, weight, bias, q_pos=None, sink=None, psink=None):
+def in_projection(xq, xk, xv, weight, bias, q_pos=None, sink=None, psink=None, kv_sink=None):
     """(q, k, v) of nn.MultiheadAttention's packed in-projection (see _InProjFn), the query
     input being xq + q_pos when q_pos is given (HF:m2f with_pos_embed); plain slicing off
     the device / under autocast / without grad."""
@@ -427,7 +482,7 @@ def in_projection(xq, xk, xv, weight, bias, q_pos=None, sink=None, psink=None):
     if (xq.is_cuda and torch.is_grad_enabled() and weight.requires_grad and not torch.is_autocast_enabled()
             and xq.dtype == weight.dtype == xk.dtype == xv.dtype == bias.dtype
             and (q_pos is None or (q_pos.shape == xq.shape and q_pos.dtype == xq.dtype))):
-        return _InProjFn.apply(xq, xk, xv, weight, bias, q_pos, sink, psink)
+        return _InProjFn.apply(xq, xk, xv, weight, bias, q_pos, sink, psink, kv_sink)
     if q_pos is not None:
         xq = xq + q_pos
     return (F.linear(xq, weight[:D], bias[:D]), F.linear(xk, weight[D:2 * D], bias[D:2 * D]),

@@ -31,7 +31,7 @@ from . import ops
 from . import linear as linear_mod
 from .linear import (SmallLinear, TokenLayerNorm, TokenLinear, fp8_operand_ok, in_projection, linear_fp8_tokens,
                      linear_gelu_tokens,
-                     linear_relu_tokens, mlp_fp8, linear_tokens, plane_projection, self_attn_in_proj, small_linear, value_query_projection,
+                     linear_relu_tokens, mlp_fp8, linear_tokens, plane_projection, token_plane_projection, self_attn_in_proj, small_linear, value_query_projection,
                      reattach_level_embed)
 
 
@@ -429,6 +429,8 @@ class EncoderLayer(nn.Module):
 
 _TORCH_GN = os.environ.get("VS_TORCH_GROUPNORM", "0") == "1"     # A/B switch
 _PIXDEC_NCHW = os.environ.get("VS_PIXDEC_NCHW", "1") == "1"    # A/B switch: NCHW 1/4-res blocks
+# the bf16 1/4-res tail channels-last with the hand-written 3x3 conv (PixelDecoder._tail_nhwc)
+_PIXDEC_NHWC = os.environ.get("VS_PIXDEC_NHWC", "1") == "1"
 
 
 class ConvGN(nn.Module):
@@ -520,8 +522,22 @@ class PixelDecoder(nn.Module):
         # instead of a zero-filled full-size gradient per slice)
         toks = torch.split(h, [Hl * Wl for (Hl, Wl) in shapes], dim=1)
         outs = [(t, hw) for t, hw in zip(toks, shapes)]
-        cur = self.lateral(feats[0])
+        f0 = feats[0]
+        lat = self.lateral
         Hs, Ws = shapes[-1]
+        if self._nhwc_tail(f0):
+            return self._tail_nhwc(f0, toks[-1], Hs, Ws), outs
+        if (f0.is_cuda and _PIXDEC_NCHW and not torch.is_autocast_enabled() and lat.conv.kernel_size == (1, 1)
+                and f0.is_contiguous(memory_format=torch.channels_last) and f0.dtype == lat.conv.weight.dtype
+                and f0.dtype in (torch.float32, torch.bfloat16) and lat.gn.weight.dtype == f0.dtype and not _TORCH_GN):
+            # the 1x1 lateral conv straight from the channels-last (token-major) feature to
+            # NCHW planes: no NCHW copy of the feature (linear.token_plane_projection)
+            B0, C0, H0, W0 = f0.shape
+            cur = token_plane_projection(f0.permute(0, 2, 3, 1).reshape(B0, H0 * W0, C0), lat.conv.weight,
+                                         lat.conv.bias, H0, W0)
+            cur = ops.group_norm_nchw(cur, lat.gn.weight, lat.gn.bias, lat.gn.num_groups, lat.gn.eps, lat.relu)
+        else:
+            cur = self.lateral(f0)
         if (cur.is_cuda and _PIXDEC_NCHW and cur.shape[1] % 32 == 0 and cur.shape[2] <= 2 * Hs
                 and cur.shape[3] <= 2 * Ws and not torch.is_autocast_enabled()):
             y = ops.upsample_add(cur, toks[-1], Hs, Ws)                  # csrc/upsample.hip
@@ -533,6 +549,39 @@ class PixelDecoder(nn.Module):
             # token-major mask features straight from the NCHW planes (channels-last view)
             return plane_projection(y, self.mask_proj.weight, self.mask_proj.bias), outs
         return self.mask_proj(y), outs
+
+    def _nhwc_tail(self, f0) -> bool:
+        lat, out = self.lateral, self.output
+        return (f0.is_cuda and _PIXDEC_NHWC and not torch.is_autocast_enabled() and not _TORCH_GN
+                and f0.dtype == torch.bfloat16 and f0.is_contiguous(memory_format=torch.channels_last)
+                and lat.conv.kernel_size == (1, 1) and lat.conv.weight.dtype == f0.dtype
+                and out.conv.kernel_size == (3, 3) and out.conv.stride == (1, 1) and out.conv.padding == (1, 1)
+                and lat.gn.weight.dtype == f0.dtype and out.gn.weight.dtype == f0.dtype
+                and self.mask_proj.weight.dtype == f0.dtype
+                and out.conv.out_channels == 8 * out.gn.num_groups == 8 * lat.gn.num_groups
+                and out.conv.in_channels % 128 == 0 and out.conv.out_channels % 128 == 0
+                and out.conv.dilation == (1, 1) and out.conv.groups == 1)
+
+    def _tail_nhwc(self, f0, top, Hs, Ws):
+        """The 1/4-resolution FPN tail (HF:m2f:1394-1419) channels-last end to end: the 1x1
+        lateral conv as a token GEMM on the channels-last Swin feature, GroupNorm NHWC, the
+        upsample + add of the finest encoder level (upsample.hip NHWC), the 3x3 output conv
+        (conv3x3.hip) + GroupNorm + ReLU, and the 1x1 mask projection as a token GEMM whose
+        output is the token-major mask-feature map the mask head reads.  No NCHW <-> NHWC
+        transposes anywhere (MIOpen's conv needed 8-9 per step)."""
+        lat, out, mp = self.lateral, self.output, self.mask_proj
+        B0, C0, H0, W0 = f0.shape
+        Fd = lat.conv.out_channels
+        t0 = f0.permute(0, 2, 3, 1).reshape(B0, H0 * W0, C0)
+        cur = linear_tokens(t0, lat.conv.weight.view(Fd, C0), lat.conv.bias)
+        cur = ops.group_norm_nhwc(cur.view(B0, H0, W0, Fd).permute(0, 3, 1, 2), lat.gn.weight, lat.gn.bias,
+                                  lat.gn.num_groups, lat.gn.eps, lat.relu)
+        y = ops.upsample_add_nhwc(cur, top, Hs, Ws)
+        y = ops.conv3x3_nhwc(y, out.conv.weight, out.conv.bias)
+        y = ops.group_norm_nhwc(y, out.gn.weight, out.gn.bias, out.gn.num_groups, out.gn.eps, out.relu)
+        Cm = mp.out_channels
+        m = linear_tokens(y.permute(0, 2, 3, 1).reshape(B0, H0 * W0, Fd), mp.weight.view(Cm, Fd), mp.bias)
+        return m.view(B0, H0, W0, Cm).permute(0, 3, 1, 2)
 
 
 # ----------------------------------------------------------------------------------
@@ -569,7 +618,7 @@ class DecoderLayer(nn.Module):
         self.fc2 = SmallLinear(ffn, d)
         self.norm_ffn = TokenLayerNorm(d)
 
-    def forward(self, h, qpos, mem, mem_pos, words, psink=None):
+    def forward(self, h, qpos, mem, mem_pos, words, psink=None, msink=None):
         """mem: level memory [B, hw, D] (contiguous), mem_pos = mem + its position embedding.
         psink: ops.GradSink of qpos (the layers' query-position gradients summed in one
         buffer by the projection kernels).  Each post-norm block hands its residual-path
@@ -579,7 +628,7 @@ class DecoderLayer(nn.Module):
         H, d = self.heads, D // self.heads
         s1, s2, s3 = ops.ResidualSink(), ops.ResidualSink(), ops.ResidualSink()
         q, k, v = in_projection(h, mem_pos, mem, self.cross_attn.in_proj_weight, self.cross_attn.in_proj_bias,
-                                q_pos=qpos, sink=s1, psink=psink)               # query = h + qpos
+                                q_pos=qpos, sink=s1, psink=psink, kv_sink=msink)  # query = h + qpos
         o = ops.masked_attention(q, k, v, words, H, d ** -0.5)
         _, h = self.norm_cross.add_forward(h, self.cross_attn.out_proj(o), sink=s1)   # post-norm, fused add
         sa = self.self_attn
@@ -662,13 +711,20 @@ class Decoder(nn.Module):
             sink = ops.GradSink() if (mf.requires_grad and torch.is_grad_enabled() and mf.is_cuda) else None
             if sink is not None:
                 mf = sink.source(mf)
-        mems, mem_pos, sizes = [], [], []
+        mems, mem_pos, sizes, msinks = [], [], [], []
         for i in range(3):
             # once per level (shared by the decoder rounds): token-major memory and memory + pos
             f, (Hl, Wl) = ms_feats[i]                       # token-major [B, Hl*Wl, C]
             sizes.append((int(Hl), int(Wl)))
             pos = sine_pos_tokens(B, Hl, Wl, d // 2, dev, f.dtype)
             m = f + self.level_embed.weight[i][None, None, :].to(f.dtype)
+            ms = None
+            if m.is_cuda and torch.is_grad_enabled() and m.requires_grad:
+                # the layers reading this level sum their K / V input gradients in one
+                # buffer (ops.GradSink, linear._InProjFn)
+                ms = ops.GradSink()
+                m = ms.source(m)
+            msinks.append(ms)
             mems.append(m)
             mem_pos.append(m + pos)
         qpos = self.query_embed.weight.unsqueeze(0).expand(B, -1, -1)
@@ -706,7 +762,7 @@ class Decoder(nn.Module):
                 self.trace.append(words)
             if self.mask_override is not None:
                 words = pack_bitmask(self.mask_override[idx].to(dev))
-            h = layer(h, qpos, mems[lvl], mem_pos[lvl], words, psink)
+            h = layer(h, qpos, mems[lvl], mem_pos[lvl], words, psink, msinks[lvl])
             hs.append(h)
             nxt = sizes[(idx + 1) % 3] if idx + 1 < n else None
             inter, logits, words = step(h, nxt)
@@ -754,8 +810,9 @@ class Mask2Former(nn.Module):
         feats = self.backbone(pixel_values.to(self.backbone.patch_embed.proj.weight.dtype))
         mask_features, ms = self.pixel_decoder(feats)
         inters, masks = self.decoder(ms, mask_features)
-        # one launch for all decoder steps (HF:m2f:2479-2481 per step)
-        classes = list(self.class_head(torch.stack(inters)).unbind(0))
+        # one launch for all decoder steps (HF:m2f:2479-2481 per step), widened to f32 once
+        # (the criterion's softmax / CE run in f32; a per-step .float() was 10 + 10 launches)
+        classes = list(self.class_head(torch.stack(inters)).float().unbind(0))
         return masks, classes
 
     @torch.no_grad()

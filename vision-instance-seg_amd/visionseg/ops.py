@@ -1119,6 +1119,9 @@ class AddLayerNormFunction(torch.autograd.Function):
         quant (bf16): also y's MX fp8 copy -> (s, y, y_q, y_qscales)."""
         L.require_hip(x, r, weight, bias)
         ctx.sink = sink if sink is not None and sink.armed else None
+        # an unused output (the post-norm decoder drops s) gets no gradient instead of a
+        # zero-filled one (a fill kernel + the residual-add read of zeros, per block)
+        ctx.set_materialize_grads(False)
         C = x.shape[-1]
         xc, rc = x.contiguous(), r.to(x.dtype).contiguous()
         M = xc.numel() // C
@@ -1607,6 +1610,141 @@ class UpsampleAddFunction(torch.autograd.Function):
 
 def upsample_add(cur, src_tokens, Hs: int, Ws: int):
     return UpsampleAddFunction.apply(cur, src_tokens, int(Hs), int(Ws))
+
+
+class UpsampleAddNHWCFunction(torch.autograd.Function):
+    """UpsampleAddFunction on channels-last planes (csrc/upsample.hip NHWC forms): cur an
+    NCHW-shaped tensor stored channels-last, src token-major [B, Hs*Ws, C]; returns a
+    channels-last NCHW view."""
+
+    @staticmethod
+    def forward(ctx, cur, src, Hs, Ws):
+        L.require_hip(cur, src)
+        B, C, H, W = cur.shape
+        ct = cur.permute(0, 2, 3, 1)
+        if not ct.is_contiguous():
+            ct = ct.contiguous()
+        src = src.to(cur.dtype)
+        if src.stride(2) != 1 or src.stride(1) != C or src.stride(0) % 8 or src.data_ptr() % 16:
+            src = src.contiguous()
+        if tuple(src.shape) != (B, Hs * Ws, C):
+            raise ValueError(f"src {tuple(src.shape)} != {(B, Hs * Ws, C)}")
+        out = torch.empty_like(ct)
+        with timed("upsample_add_nhwc", ct, bytes_=(2 * ct.numel() + src.numel()) * ct.element_size()):
+            L.check(L.lib().vs_upsample_add_forward_nhwc(L.dtype_code(ct), L.ptr(ct), L.ptr(src), L.ptr(out), B, C,
+                                                         H, W, int(Hs), int(Ws), src.stride(0), L.stream(ct)),
+                    "upsample_add_forward_nhwc")
+        ctx.geom = (B, C, H, W, int(Hs), int(Ws))
+        ctx.src_dtype = src.dtype
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, C, H, W, Hs, Ws = ctx.geom
+        gt = g.permute(0, 2, 3, 1)
+        if not gt.is_contiguous():
+            gt = gt.contiguous()
+        gs = torch.empty(B, Hs * Ws, C, device=g.device, dtype=g.dtype)
+        with timed("upsample_bwd_nhwc", gt, bytes_=(gt.numel() + gs.numel()) * gt.element_size()):
+            L.check(L.lib().vs_upsample_backward_nhwc(L.dtype_code(gt), L.ptr(gt), L.ptr(gs), B, C, H, W, Hs, Ws,
+                                                      L.stream(gt)), "upsample_backward_nhwc")
+        return g, gs.to(ctx.src_dtype), None, None
+
+
+def upsample_add_nhwc(cur, src_tokens, Hs: int, Ws: int):
+    return UpsampleAddNHWCFunction.apply(cur, src_tokens, int(Hs), int(Ws))
+
+
+# ------------------------------------------------------------------ 3 x 3 conv (channels-last)
+def conv3x3_nhwc_ok(x, weight) -> bool:
+    """Shapes / dtypes csrc/conv3x3.hip covers: bf16 device tensors, a [Co, Ci, 3, 3] weight
+    with Ci and Co multiples of 128 (forward, input and weight gradients)."""
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and tuple(weight.shape[2:]) == (3, 3) and weight.shape[1] == x.shape[1]
+            and x.shape[1] % 128 == 0 and weight.shape[0] % 128 == 0)
+
+
+def conv3x3_layouts(weight, fwd=True, bwd=False):
+    """weight [Co, Ci, 3, 3] -> (w_fwd [Co, 3, 3, Ci] or None, w_bwd [Ci, 3, 3, Co] flipped or None)."""
+    L.require_hip(weight)
+    Co, Ci = weight.shape[:2]
+    w = weight.contiguous()
+    wf = torch.empty(Co, 3, 3, Ci, device=w.device, dtype=w.dtype) if fwd else None
+    wb = torch.empty(Ci, 3, 3, Co, device=w.device, dtype=w.dtype) if bwd else None
+    L.check(L.lib().vs_conv3x3_weight_layouts(L.ptr(w), L.ptr(wf) if wf is not None else None,
+                                              L.ptr(wb) if wb is not None else None, Co, Ci, L.stream(w)),
+            "conv3x3_weight_layouts")
+    return wf, wb
+
+
+def conv3x3_raw(xt, w_layout, bias=None):
+    """y [B, H, W, Co] = conv3x3(xt [B, H, W, Ci]) with the weights in the vs_conv3x3_forward
+    layout [Co, 3, 3, Ci] (the input gradient: grad_y and the w_bwd layout)."""
+    L.require_hip(xt, w_layout)
+    B, H, W, Ci = xt.shape
+    Co = w_layout.shape[0]
+    y = torch.empty(B, H, W, Co, device=xt.device, dtype=xt.dtype)
+    with timed("conv3x3_igemm", xt, flops=2.0 * B * H * W * Co * 9 * Ci):
+        L.check(L.lib().vs_conv3x3_forward(L.ptr(xt), L.ptr(w_layout), L.ptr(bias) if bias is not None else None,
+                                           L.ptr(y), B, H, W, Ci, Co, L.stream(xt)), "conv3x3_forward")
+    return y
+
+
+def conv3x3_wgrad(gyt, xt, dtype):
+    """dW [Co, Ci, 3, 3] (dtype) = sum over pixels of gyt [B, H, W, Co] x the 3 x 3
+    neighbourhoods of xt [B, H, W, Ci] (vs_conv3x3_wgrad)."""
+    B, H, W, Ci = xt.shape
+    Co = gyt.shape[3]
+    nb = int(L.lib().vs_conv3x3_wgrad_workspace_bytes(B, H, W, Ci, Co))
+    if nb <= 0:
+        raise ValueError(f"conv3x3_wgrad: unsupported shape {tuple(xt.shape)} -> {Co}")
+    ws = torch.empty(nb, device=xt.device, dtype=torch.uint8)
+    gw = torch.empty(Co, Ci, 3, 3, device=xt.device, dtype=dtype)
+    with timed("conv3x3_wgrad", xt, flops=2.0 * B * H * W * Co * 9 * Ci):
+        L.check(L.lib().vs_conv3x3_wgrad(L.dtype_code(gw), L.ptr(gyt), L.ptr(xt), L.ptr(gw), L.ptr(ws), B, H, W, Ci,
+                                         Co, L.stream(xt)), "conv3x3_wgrad")
+    return gw
+
+
+class Conv3x3NHWCFunction(torch.autograd.Function):
+    """nn.functional.conv2d(x, weight, bias, stride=1, padding=1) for a 3 x 3 kernel on a
+    channels-last bf16 NCHW tensor (csrc/conv3x3.hip): the pixel decoder's output conv
+    (HF:m2f:1394-1419).  Returns a channels-last NCHW view."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        L.require_hip(x, weight)
+        if not conv3x3_nhwc_ok(x, weight):
+            raise ValueError(f"conv3x3_nhwc: unsupported x {tuple(x.shape)} {x.dtype}, weight {tuple(weight.shape)}")
+        xt = x.permute(0, 2, 3, 1)
+        if not xt.is_contiguous():
+            xt = xt.contiguous()
+        wf, _ = conv3x3_layouts(weight)
+        b = bias.to(x.dtype).contiguous() if bias is not None else None
+        y = conv3x3_raw(xt, wf, b)
+        ctx.save_for_backward(xt, weight)
+        ctx.has_bias = bias is not None
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xt, weight = ctx.saved_tensors
+        gyt = gy.permute(0, 2, 3, 1).to(xt.dtype)
+        if not gyt.is_contiguous():
+            gyt = gyt.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            _, wb = conv3x3_layouts(weight, fwd=False, bwd=True)
+            gx = conv3x3_raw(gyt, wb).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            gw = conv3x3_wgrad(gyt, xt, weight.dtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gyt.sum((0, 1, 2), dtype=torch.float32).to(weight.dtype)
+        return gx, gw, gb
+
+
+def conv3x3_nhwc(x, weight, bias=None):
+    return Conv3x3NHWCFunction.apply(x, weight, bias)
 
 
 # ---------------------------------------------------------------------------------------
