@@ -649,6 +649,18 @@ VS_API int vs_upsample_add_forward_nhwc(int dtype, const void* cur, const void* 
 VS_API int vs_upsample_backward_nhwc(int dtype, const void* grad_out, void* grad_src, int batch, int channels,
                                      int height, int width, int src_height, int src_width, void* stream);
 
+/* ---- a5-a7: weight (+ bias) gradient of a token-major Linear ---------------------------
+ * dw [N, K] (dtype VS_BF16 / VS_F32, overwritten) = sum_t grad_y[t, n] x[t, k] and, when db
+ * is non-NULL, db [N] = sum_t grad_y[t, n]; bf16 operands with row strides ld_grad_y /
+ * ld_x (elements, % 8 == 0), unit column stride, 16-B aligned; N % 8 == 0, K % 8 == 0,
+ * 0 < tokens < 2^31.  f32 accumulation: per-split partials in workspace (size from
+ * vs_token_wgrad_workspace_bytes), summed in a fixed order (deterministic, no atomics).
+ * Replaces autograd's gy^T x of F.linear's backward (the reference's Linears, HF:swin /
+ * HF:m2f) for the token-heavy Linears. */
+VS_API long long vs_token_wgrad_workspace_bytes(long long tokens, int N, int K);
+VS_API int vs_token_wgrad(int dtype, const void* grad_y, long long ld_grad_y, const void* x, long long ld_x, void* dw,
+                          void* db, void* workspace, long long tokens, int N, int K, void* stream);
+
 /* ---- a9: the FPN's 3 x 3 output conv on NHWC planes (replaces MIOpen's conv + layout
  * transposes under nn.Conv2d(256, 256, 3, padding=1, bias=False), HF:m2f:1394-1419).
  * Stride 1, padding 1, bf16, channels-last x [B, H, W, Ci], y [B, H, W, Co].

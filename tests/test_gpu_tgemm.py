@@ -403,3 +403,49 @@ def test_plane_projections_vs_conv1x1(dtype):
     tr.backward(gt.float())
     assert t.shape == tr.shape and rel(t, tr) <= tol
     assert rel(p.grad, pr.grad) <= tol and rel(w2s.grad, w2r.grad) <= tol
+
+
+@pytest.mark.parametrize("T,N,K,ld_pad", [(5000, 96, 288, 0), (4096, 288, 96, 0), (20000, 1536, 384, 0),
+                                          (4200, 256, 1024, 0), (6001, 136, 200, 24)])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_token_wgrad_vs_f64(T, N, K, ld_pad, out_dtype):
+    """csrc/token_wgrad.hip: dW = gY^T X and db = column sums of gY vs f64 on the same bf16
+    operands: ragged token chunks (T % 64), ragged output / input tiles (N, K not multiples of
+    128 / 256), strided rows (ld_pad > 0: views of wider tensors).  f32 accumulation over T
+    products, one rounding to out_dtype: |err| <= 2^-8 |ref| (bf16 out; 1e-6 f32) + 1e-5
+    max|ref| (summation order over up to 20000 tokens)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(T + N + K)
+    gyw = _rand((T, N + ld_pad), g).to(DEV)
+    xw = _rand((T, K + ld_pad), g).to(DEV)
+    gy, x = gyw[:, :N], xw[:, :K]
+    dw, db = ops.token_wgrad(gy, x, out_dtype, bias=True)
+    ref = gy.double().t() @ x.double()
+    rb = gy.double().sum(0)
+    rel = 2.0 ** -8 if out_dtype == torch.bfloat16 else 1e-6
+    for a, r in ((dw, ref), (db, rb)):
+        assert a.dtype == out_dtype
+        err = (a.double() - r).abs()
+        assert bool((err <= rel * r.abs() + 1e-5 * r.abs().max()).all()), float(err.max())
+
+
+def test_linear_backward_token_wgrad_matches_vendor(monkeypatch):
+    """linear_tokens' backward with the token weight-gradient kernel (bias fused) vs the vendor
+    batched-GEMM path: the same gradients up to f32 summation order (bf16 outputs: 1e-2
+    relative RMS, both one rounding of the f32 sum)."""
+    from visionseg import linear as lin
+    g = torch.Generator().manual_seed(11)
+    x = _rand((4, 2048, 192), g).to(DEV)
+    w = _rand((576, 192), g, 0.05).to(DEV)
+    b = _rand((576,), g).to(DEV)
+    gy = _rand((4, 2048, 576), g).to(DEV)
+
+    def run(flag):
+        monkeypatch.setattr(lin, "_TOKEN_WGRAD", flag)
+        xs, ws, bs = (t.clone().requires_grad_() for t in (x, w, b))
+        lin.linear_tokens(xs, ws, bs).backward(gy)
+        return xs.grad.float(), ws.grad.float(), bs.grad.float()
+
+    a, v = run(True), run(False)
+    for p, q in zip(a, v):
+        assert float((p - q).norm() / q.norm()) < 1e-2

@@ -24,33 +24,12 @@
 //   summed in a fixed order by a second kernel that writes the torch [Co, Ci, 3, 3] layout.
 #include <stdlib.h>
 
-#include "mfma_util.h"
+#include "lds_dma.h"
 
 namespace vs {
 namespace {
 
 constexpr int kRowB = 128;   // bytes of a row per K-step (implicit GEMM)
-
-typedef __attribute__((address_space(3))) void lds_void;
-typedef short bf16x4v_t __attribute__((ext_vector_type(4)));
-
-// the DMA source of padding taps and of rows past the image: never written
-__device__ __attribute__((aligned(256))) unsigned char g_conv_zero_row[256];
-
-__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 // physical byte offset of (row, 16-B chunk) in an implicit-GEMM staged tile (128-B rows)
 __device__ __forceinline__ int tile_off(int row, int chunk) { return row * kRowB + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -108,7 +87,7 @@ __global__ void __launch_bounds__(64 * GM * GN) conv3x3_igemm_kernel(const bf16*
       if (isx) {
         const bool ok = xm[j] >= 0 && (unsigned)(xh[j] + dy) < (unsigned)H && (unsigned)(xw[j] + dx) < (unsigned)Wd;
         src = ok ? reinterpret_cast<const unsigned char*>(X + ((size_t)(xm[j] + shift) * Ci + cc * 64)) + chunk * 16
-                 : g_conv_zero_row + chunk * 16;
+                 : g_dma_zero_row + chunk * 16;
       } else {
         src = reinterpret_cast<const unsigned char*>(Wt) + (size_t)min(n0 + rr, N - 1) * rowB + ks * kRowB + chunk * 16;
       }
@@ -188,25 +167,6 @@ constexpr int kXRows = 68;                     // staged input pixels: the segme
 constexpr int kDyBytes = kSeg * 256, kXBytes = kXRows * 256, kStage = kDyBytes + kXBytes;
 constexpr int kDyBlk = kDyBytes / 1024, kXBlk = kXBytes / 1024;   // 16 + 17 DMA blocks
 
-// [row][128 x bf16] image, 256-B rows, the XOR that serves transposed reads conflict-free
-// (cdna_hip_programming.md T10, image (b))
-__device__ __forceinline__ int woff(int row, int ch) { return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))); }
-
-// MFMA operand (k = image rows row0 + 8hh + 0..7, m/n = image columns col0 + (lane & 31))
-__device__ __forceinline__ bf16x8_t tr_frag(const unsigned char* img, int row0, int col0, int lane) {
-  const int hh = lane >> 5;
-  const int row = row0 + 8 * hh + ((lane & 15) >> 2);
-  const int col = col0 + (lane & 16) + 4 * (lane & 3);
-  typedef __attribute__((address_space(3))) bf16x4v_t lds_v4;
-  const int within = (col & 7) * 2;
-  const bf16x4v_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + woff(row, col >> 3) + within));
-  const bf16x4v_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + woff(row + 4, col >> 3) + within));
-  bf16x8_t v;
-  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-  return v;
-}
-
 // grid: S x tiles workgroups (tiles = Co/128 x Ci/128 x 3 kernel rows), 512 threads;
 // part [S][Co][9][Ci] f32
 __global__ void __launch_bounds__(512) conv3x3_wgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
@@ -234,16 +194,16 @@ __global__ void __launch_bounds__(512) conv3x3_wgrad_kernel(const bf16* __restri
     for (int blk = w; blk < kDyBlk + kXBlk; blk += 8) {
       const unsigned char* src;
       if (blk < kDyBlk) {
-        const int row = blk * 4 + (l >> 4), ch = (l & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        const int row = blk * 4 + (l >> 4), ch = (l & 15) ^ img_swz(row);
         const int x = w0 + row;
         src = x < Wd ? reinterpret_cast<const unsigned char*>(dY + ((size_t)(rowid * Wd + x) * Co + cob * kWBlk)) + ch * 16
-                     : g_conv_zero_row + ch * 16;
+                     : g_dma_zero_row + ch * 16;
       } else {
-        const int row = (blk - kDyBlk) * 4 + (l >> 4), ch = (l & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        const int row = (blk - kDyBlk) * 4 + (l >> 4), ch = (l & 15) ^ img_swz(row);
         const int x = w0 - 1 + row;
         const bool ok = xrow_ok && row < kSeg + 2 && (unsigned)x < (unsigned)Wd;
         src = ok ? reinterpret_cast<const unsigned char*>(X + ((size_t)(xpix0 + x) * Ci + cib * kWBlk)) + ch * 16
-                 : g_conv_zero_row + ch * 16;
+                 : g_dma_zero_row + ch * 16;
       }
       glds16(src, base + blk * 1024);
     }

@@ -1,0 +1,58 @@
+// LDS-DMA staging and transposed-read helpers shared by the pixel-major weight-gradient
+// kernels (conv3x3.hip, token_wgrad.hip) and the implicit-GEMM conv.
+//
+// Images are [row][128 x bf16] with 256-B rows and the 16-B chunks XOR-swizzled so that both
+// the DMA's lane-linear 1-KB writes and the 32x32x16 transposed operand reads
+// (ds_read_b64_tr_b16) are conflict-free (cdna_hip_programming.md T10, image (b)).  The DMA
+// writes lane-linear, so the swizzle is applied to the GLOBAL source address of each lane.
+#pragma once
+#include "mfma_util.h"
+
+namespace vs {
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef short bf16x4v_t __attribute__((ext_vector_type(4)));
+
+// the DMA source of padding taps, rows past the end and columns past the width: never written
+__device__ __attribute__((aligned(256))) unsigned char g_dma_zero_row[256];
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// barrier that keeps outstanding DMA in flight (no vmcnt drain): the caller waits for its
+// own DMA with wait_vm first
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int img_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+// byte offset of (row, 16-B chunk) in a [row][128 x bf16] image
+__device__ __forceinline__ int woff(int row, int ch) { return 256 * row + 16 * (ch ^ img_swz(row)); }
+
+// MFMA operand from an image: k = rows row0 + 8hh + 0..7, m/n = columns col0 + (lane & 31)
+__device__ __forceinline__ bf16x8_t tr_frag(const unsigned char* img, int row0, int col0, int lane) {
+  const int hh = lane >> 5;
+  const int row = row0 + 8 * hh + ((lane & 15) >> 2);
+  const int col = col0 + (lane & 16) + 4 * (lane & 3);
+  typedef __attribute__((address_space(3))) bf16x4v_t lds_v4;
+  const int within = (col & 7) * 2;
+  const bf16x4v_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + woff(row, col >> 3) + within));
+  const bf16x4v_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + woff(row + 4, col >> 3) + within));
+  bf16x8_t v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+}  // namespace
+}  // namespace vs

@@ -364,6 +364,12 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
   VS_CHECK(N % 4 == 0, "N must be a multiple of 4");
   VS_CHECK(f8 ? (K % 128 == 0 && x_scales && w_scales) : (K % 8 == 0), "fp8: K % 128 == 0 and scales; bf16: K % 8 == 0");
   VS_CHECK(!gelu || y_pre, "gelu needs the pre-activation output");
+  // 16-B LDS-DMA row loads and epilogue stores, 8-B bias loads, 4-B scale loads
+  VS_CHECK(((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+               (!y_pre || ((uintptr_t)y_pre & 15) == 0) && (!bias || ((uintptr_t)bias & 7) == 0) &&
+               (!x_scales || ((uintptr_t)x_scales & 3) == 0) && (!w_scales || ((uintptr_t)w_scales & 3) == 0) &&
+               (!y_q || ((uintptr_t)y_q & 3) == 0),
+           "alignment: x / w / y / y_pre 16 B, bias 8 B, scales / y_q 4 B");
   const bool qout = (mode & VS_TGEMM_QOUT) != 0;
   VS_CHECK(!qout || (gelu && y_q && y_qscales && N % 32 == 0), "quantised output: with gelu, N % 32 == 0, both buffers");
   // the 256 x 256 tile where the product is MFMA-bound and fills the chip (VS_TGEMM_TILE=128

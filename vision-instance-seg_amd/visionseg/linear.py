@@ -56,12 +56,42 @@ def split_count(K: int, M: int, N: int) -> int:
     return max(1, min(s, K // MIN_CHUNK))
 
 
-def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype, out: torch.Tensor | None = None):
-    """dW = gy^T x for gy [K, M], x [K, N] -> [M, N] (out_dtype), f32 accumulation: a
-    batched GEMM over S token chunks with f32 outputs, then one HIP epilogue that sums
-    the chunks (+ the remainder rows' product) and rounds once (csrc/norm.hip).
+# The token-Linear weight gradient on the hand-written kernel (csrc/token_wgrad.hip) for
+# bf16 operands with >= WGRAD_MIN_TOKENS tokens; VS_TOKEN_WGRAD=0: the vendor batched GEMM.
+_TOKEN_WGRAD = os.environ.get("VS_TOKEN_WGRAD", "1") == "1"
+WGRAD_MIN_TOKENS = int(os.environ.get("VS_WGRAD_MIN_TOKENS", "4096"))
+
+
+def _token_wgrad_ok(gy, x, out_dtype) -> bool:
+    return (_TOKEN_WGRAD and gy.is_cuda and gy.dtype == x.dtype == torch.bfloat16
+            and out_dtype in (torch.float32, torch.bfloat16) and gy.shape[0] >= WGRAD_MIN_TOKENS
+            and gy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0 and gy.stride(1) == 1 and x.stride(1) == 1
+            and gy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0 and gy.data_ptr() % 16 == 0
+            and x.data_ptr() % 16 == 0)
+
+
+def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype, out: torch.Tensor | None = None,
+                bias: bool = False):
+    """dW = gy^T x for gy [K, M], x [K, N] -> [M, N] (out_dtype), f32 accumulation.  bf16
+    token-heavy operands: the hand-written token weight-gradient kernel (ops.token_wgrad);
+    otherwise a batched GEMM over S token chunks with f32 outputs, then one HIP epilogue
+    that sums the chunks (+ the remainder rows' product) and rounds once (csrc/norm.hip).
     `out`: a contiguous [M, N] tensor of out_dtype to write into (e.g. a row block of a
-    fused parameter's gradient)."""
+    fused parameter's gradient).  bias=True: returns (dW, db) with db = gy's column sums
+    (f32 accumulation, out_dtype) -- from the same kernel on the token path."""
+    if _token_wgrad_ok(gy, x, out_dtype) and (out is None or (out.is_contiguous() and out.dtype == out_dtype
+                                                               and out.data_ptr() % 4 == 0)):
+        return ops.token_wgrad(gy, x, out_dtype, bias=bias, out=out)
+    gw = _vendor_weight_grad(gy, x, out_dtype, out)
+    if bias:
+        gy = gy.contiguous()
+        if gy.shape[1] % 8 == 0 and gy.shape[1] <= ops.COLSUM_MAX_N and gy.is_cuda:
+            return gw, ops.column_sum(gy).to(out_dtype)
+        return gw, gy.sum(0, dtype=torch.float32).to(out_dtype)
+    return gw
+
+
+def _vendor_weight_grad(gy, x, out_dtype, out=None):
     K, M = gy.shape
     N = x.shape[1]
     S = split_count(K, M, N)
@@ -129,13 +159,18 @@ class _LinearFn(torch.autograd.Function):
                 gx = torch.addmm(gres.reshape(gy2.shape[0], -1).to(gy2.dtype), gy2, weight.to(gy2.dtype)).view(x.shape)
             else:
                 gx = (gy2 @ weight.to(gy2.dtype)).view(x.shape)
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        cs = ops.take_colsum(gy) if want_b else None               # from the LayerNorm backward's pass
+        if cs is not None:
+            gb = cs.to(weight.dtype)
         if ctx.needs_input_grad[1]:
-            gw = weight_grad(gy2, x.reshape(-1, x.shape[-1]).to(gy2.dtype), weight.dtype)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            cs = ops.take_colsum(gy)
-            if cs is not None:                                     # from the LayerNorm backward's pass
-                gb = cs.to(weight.dtype)
-            elif gy2.shape[1] % 8 == 0 and gy2.shape[1] <= ops.COLSUM_MAX_N:
+            x2 = x.reshape(-1, x.shape[-1]).to(gy2.dtype)
+            if want_b and gb is None and _token_wgrad_ok(gy2, x2, weight.dtype):
+                gw, gb = weight_grad(gy2, x2, weight.dtype, bias=True)     # db from the same kernel
+            else:
+                gw = weight_grad(gy2, x2, weight.dtype)
+        if want_b and gb is None:
+            if gy2.shape[1] % 8 == 0 and gy2.shape[1] <= ops.COLSUM_MAX_N:
                 gb = ops.column_sum(gy2).to(weight.dtype)          # HIP column sum, f32 accumulation
             else:
                 gb = gy2.sum(0, dtype=torch.float32).to(weight.dtype)

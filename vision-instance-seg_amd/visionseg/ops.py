@@ -1655,6 +1655,26 @@ def upsample_add_nhwc(cur, src_tokens, Hs: int, Ws: int):
     return UpsampleAddNHWCFunction.apply(cur, src_tokens, int(Hs), int(Ws))
 
 
+# ------------------------------------------------------------------ token-Linear weight gradient
+def token_wgrad(gy, x, out_dtype, bias: bool = False, out=None):
+    """dW [N, K] = gy^T x for token-major gy [T, N], x [T, K] (bf16, rows strided, unit
+    column stride), f32 accumulation, out_dtype; bias=True also returns db [N] = column sums
+    of gy (csrc/token_wgrad.hip).  `out`: a contiguous [N, K] tensor of out_dtype to write."""
+    L.require_hip(gy, x)
+    T, N = gy.shape
+    K = x.shape[1]
+    dev = gy.device
+    nb = int(L.lib().vs_token_wgrad_workspace_bytes(T, N, K))
+    ws = torch.empty(nb, device=dev, dtype=torch.uint8)
+    if out is None:
+        out = torch.empty(N, K, device=dev, dtype=out_dtype)
+    db = torch.empty(N, device=dev, dtype=out_dtype) if bias else None
+    with timed("token_wgrad", gy, flops=2.0 * T * N * K, bytes_=T * (N + K) * 2):
+        L.check(L.lib().vs_token_wgrad(L.dtype_code(out), L.ptr(gy), gy.stride(0), L.ptr(x), x.stride(0), L.ptr(out),
+                                       L.ptr(db) if bias else None, L.ptr(ws), T, N, K, L.stream(gy)), "token_wgrad")
+    return (out, db) if bias else out
+
+
 # ------------------------------------------------------------------ 3 x 3 conv (channels-last)
 def conv3x3_nhwc_ok(x, weight) -> bool:
     """Shapes / dtypes csrc/conv3x3.hip covers: bf16 device tensors, a [Co, Ci, 3, 3] weight
@@ -1806,6 +1826,17 @@ def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None
             or (quant_out and (not gelu or N % 32)):
         raise ValueError(f"token_gemm: bad shapes x {tuple(x.shape)} w {tuple(w.shape)} fp8={fp8}")
     x2 = x.reshape(-1, K).contiguous()
+    w = w.contiguous()
+    # the kernel's 16-B LDS-DMA rows, 8-B bias and 4-B scale loads: a view with a storage
+    # offset that breaks them is copied to a fresh (aligned) buffer
+    if x2.data_ptr() % 16:
+        x2 = x2.clone()
+    if w.data_ptr() % 16:
+        w = w.clone()
+    if bias is not None:
+        bias = bias.contiguous()
+        if bias.data_ptr() % 8:
+            bias = bias.clone()
     M = x2.shape[0]
     y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
     pre = torch.empty_like(y) if gelu else None
@@ -1816,8 +1847,8 @@ def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None
     nb = (M * K + N * K) * esz + M * N * 2 * (2 if gelu else 1) + (M * N * 33 // 32 if quant_out else 0)
     with timed("token_gemm_fp8" if fp8 else "token_gemm", x2, bytes_=nb, flops=2.0 * M * N * K):
         L.check(L.lib().vs_token_gemm(mode, L.ptr(x2), L.ptr(x_scales.contiguous()) if fp8 else None,
-                                      L.ptr(w.contiguous()), L.ptr(w_scales.contiguous()) if fp8 else None,
-                                      L.ptr(bias.contiguous()) if bias is not None else None, L.ptr(y),
+                                      L.ptr(w), L.ptr(w_scales.contiguous()) if fp8 else None,
+                                      L.ptr(bias) if bias is not None else None, L.ptr(y),
                                       L.ptr(pre) if gelu else None, L.ptr(yq) if quant_out else None,
                                       L.ptr(yqs) if quant_out else None, M, N, K, L.stream(x2)), "token_gemm")
     shape = (*x.shape[:-1], N)
