@@ -1,7 +1,6 @@
 """Token-Linear weight gradient at the C2 shapes (Swin-T stages 1-4, the pixel-decoder
 encoder): csrc/token_wgrad.hip (bias fused) vs the vendor batched GEMM + splitk_sum +
 column_sum.  HIP events, median of 20; TF/s of the 2 T N K flops and GB/s of the operands."""
-import os
 import sys
 
 import torch
@@ -54,9 +53,21 @@ def main():
               f"{by / ta / 1e6:6.0f} GB/s)  vendor+colsum {tb * 1e3:7.1f} us ({fl / tb / 1e9:6.1f} TF/s)  rel {err:.1e}",
               flush=True)
         del gy, x
-    print(f"total: token_wgrad {tot_a:.3f} ms, vendor {tot_b:.3f} ms")
-    for v in (128, 384, 512):
-        os.environ["VS_WGRAD_WGS"] = str(v)   # read once per process: informational only
+    print(f"total: token_wgrad {tot_a:.3f} ms, vendor {tot_b:.3f} ms", flush=True)
+    # input gradient dX = dY W ([T, N] x [N, K]): the token GEMM on W^T vs the vendor GEMM
+    tot_a = tot_b = 0.0
+    for name, T, N, K in SHAPES:
+        gy = torch.randn(T, N, device=DEV).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+        ta = timeit(lambda: ops.token_gemm(gy, w.t().contiguous()))
+        tb = timeit(lambda: gy @ w)
+        fl = 2.0 * T * N * K
+        tot_a += ta
+        tot_b += tb
+        print(f"dgrad {name:8s}: token_gemm(+W^T) {ta * 1e3:7.1f} us ({fl / ta / 1e9:6.1f} TF/s)  vendor {tb * 1e3:7.1f} us "
+              f"({fl / tb / 1e9:6.1f} TF/s)  rule {lin._use_token_gemm(T, K, N)}", flush=True)
+        del gy, w
+    print(f"dgrad total: token_gemm {tot_a:.3f} ms, vendor {tot_b:.3f} ms", flush=True)
     return 0
 
 

@@ -138,6 +138,21 @@ def _forward_gemm(x, weight, bias):
     return ops.token_gemm(x.reshape(-1, K), weight, bias).view(*x.shape[:-1], N)
 
 
+# The input gradient dX = dY W of the token Linears on the token GEMM (with W^T, a [K, N]
+# copy of the small weight) where the shape rule picks it: VS_TGEMM_DGRAD=1 (A/B switch).
+_TGEMM_DGRAD = os.environ.get("VS_TGEMM_DGRAD", "0") == "1"
+
+
+def _dgrad_gemm(gy2, weight):
+    """dX = dY W for dY [T, N] and W [N, K] (no residual term)."""
+    N, K = weight.shape
+    T = gy2.shape[0]
+    if (_TGEMM_DGRAD and gy2.is_cuda and gy2.dtype == weight.dtype == torch.bfloat16 and K % 8 == 0 and N % 8 == 0
+            and T >= MIN_TOKENS and _use_token_gemm(T, K, N)):
+        return ops.token_gemm(gy2.contiguous(), weight.t().contiguous())
+    return gy2 @ weight.to(gy2.dtype)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, sink=None):
@@ -158,7 +173,7 @@ class _LinearFn(torch.autograd.Function):
             if gres is not None:       # the residual path's gradient of x, added by the GEMM (beta = 1)
                 gx = torch.addmm(gres.reshape(gy2.shape[0], -1).to(gy2.dtype), gy2, weight.to(gy2.dtype)).view(x.shape)
             else:
-                gx = (gy2 @ weight.to(gy2.dtype)).view(x.shape)
+                gx = _dgrad_gemm(gy2, weight).view(x.shape)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         cs = ops.take_colsum(gy) if want_b else None               # from the LayerNorm backward's pass
         if cs is not None:
@@ -501,7 +516,12 @@ class _InProjFn(torch.autograd.Function):
                 if i == 0 and want_pos:
                     gpos = gxi
                 gx.append(gxi if ctx.needs_input_grad[i] else None)
-            weight_grad(g2, x2.to(g2.dtype), weight.dtype, out=gw[rows])
+            x2 = x2.to(g2.dtype)
+            if _token_wgrad_ok(g2, x2, weight.dtype) and weight.dtype == g2.dtype:
+                _, gbi = weight_grad(g2, x2, weight.dtype, out=gw[rows], bias=True)
+                gb[rows].copy_(gbi)
+                continue
+            weight_grad(g2, x2, weight.dtype, out=gw[rows])
             if D % 8 == 0 and D <= 2048 and g2.dtype == weight.dtype:
                 ops.column_sum(g2, out=gb[rows])
             else:
@@ -566,7 +586,7 @@ class _ValueQueryProjFn(torch.autograd.Function):
             dh = gp2 @ wp_ if gres is None else torch.addmm(gres.reshape(gp2.shape[0], Dh).to(gp2.dtype), gp2, wp_)
             dh = torch.addmm(dh, gv2, wv_)                            # + value's share, in the GEMM epilogue
         h2, q2 = h.reshape(-1, Dh), q.reshape(-1, Dh)
-        gwv = weight_grad(gv2, h2.to(gv2.dtype), wv.dtype)
+        gwv, gbv = weight_grad(gv2, h2.to(gv2.dtype), wv.dtype, bias=True)
         gwp = weight_grad(gp2, q2.to(gp2.dtype), wp.dtype)
 
         def bias_grad(g2, dt):
@@ -587,7 +607,7 @@ class _ValueQueryProjFn(torch.autograd.Function):
                 glvl = torch.stack([c.sum((0, 1)) for c in torch.split(g3, list(sizes), 1)]) @ wp.float()
                 glvl = glvl.to(ldt)
         return (dh.view(h.shape), dq.view(h.shape) if dq is not None else None, gwv,
-                bias_grad(gv2, wv.dtype), gwp, gbp, glvl, None, None)
+                gbv, gwp, gbp, glvl, None, None)
 
 
 def value_query_projection(h, pos, wv, bv, wp, bp, level_embed=None, level_sizes=None, sink=None):
@@ -823,7 +843,7 @@ class _LinearReluFn(torch.autograd.Function):
             if gres is not None:
                 gx = torch.addmm(gres.reshape(M, -1).to(gp.dtype), gp, weight.to(gp.dtype)).view(x.shape)
             else:
-                gx = (gp @ weight.to(gp.dtype)).view(x.shape)
+                gx = _dgrad_gemm(gp, weight).view(x.shape)
         if ctx.needs_input_grad[1]:
             gw = weight_grad(gp, x.reshape(-1, x.shape[-1]).to(gp.dtype), weight.dtype)
         if ctx.needs_input_grad[2]:
@@ -999,7 +1019,7 @@ class _LinearGeluFn(torch.autograd.Function):
                                                    L.ptr(ws), M, N, L.stream(pre)), "act_backward_colsum")
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = (_dgrad(gp, weight) if ctx.fp8 else gp @ weight.to(gp.dtype)).view(x.shape)
+            gx = (_dgrad(gp, weight) if ctx.fp8 else _dgrad_gemm(gp, weight)).view(x.shape)
         if ctx.needs_input_grad[1]:
             gw = weight_grad(gp, x.reshape(-1, x.shape[-1]), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
