@@ -11,7 +11,8 @@ fp32 references of the same arithmetic, and the whole NHWC tail against the NCHW
   the forward entry point alone (the input gradient needs Co % 64, the weight gradient
   Ci, Co % 128), the C2 shape (4 x 256 x 256 x 256) against MIOpen's bf16 conv (relative
   RMS 1e-2: both round to bf16, in different orders);
-* upsample NHWC forward bit-exact vs the NCHW kernel (same formula, same order), backward
+* upsample NHWC forward bit-exact vs the NCHW kernel at exact 2x / 1x (same formula, same order;
+  one bf16 rounding apart at other factors, where the compiler contracts differently), backward
   vs torch's F.interpolate adjoint in f32 (1e-5 relative)."""
 import pytest
 import torch
@@ -106,7 +107,13 @@ def test_upsample_nhwc_vs_nchw_and_torch(H, W, Hs, Ws):
     out_nchw = ops.upsample_add(cur, src, Hs, Ws)
     out_nhwc = ops.upsample_add_nhwc(cur.contiguous(memory_format=torch.channels_last), src, Hs, Ws)
     assert out_nhwc.is_contiguous(memory_format=torch.channels_last)
-    assert torch.equal(out_nhwc, out_nchw)
+    if 2 * Hs == H and 2 * Ws == W or (Hs, Ws) == (H, W):
+        assert torch.equal(out_nhwc, out_nchw)
+    else:   # the compiler may contract the bilinear sums differently: the rounded upsample and
+        # the rounded sum can each land one bf16 step apart (2^-8 relative at most, each)
+        d = (out_nhwc.float() - out_nchw.float()).abs()
+        bound = 2.0 ** -7 * (out_nchw.float().abs() + cur.float().abs()) + 1e-6
+        assert bool((d <= bound).all()), float(d.max())
     # backward in f32 vs torch's adjoint
     cur32 = cur.float().contiguous(memory_format=torch.channels_last).requires_grad_()
     src32 = src.float().requires_grad_()

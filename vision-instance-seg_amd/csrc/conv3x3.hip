@@ -166,13 +166,14 @@ constexpr int kWBlk = 128;                     // output / input channels per wo
 constexpr int kXRows = 68;                     // staged input pixels: the segment +- 1 (66), whole 1-KB DMA blocks
 constexpr int kDyBytes = kSeg * 256, kXBytes = kXRows * 256, kStage = kDyBytes + kXBytes;
 constexpr int kDyBlk = kDyBytes / 1024, kXBlk = kXBytes / 1024;   // 16 + 17 DMA blocks
+constexpr int kWStages = 4;                   // ring of segment buffers: 3 segments in flight (132 KB)
 
 // grid: S x tiles workgroups (tiles = Co/128 x Ci/128 x 3 kernel rows), 512 threads;
 // part [S][Co][9][Ci] f32
 __global__ void __launch_bounds__(512) conv3x3_wgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
                                                             float* __restrict__ part, int B, int H, int Wd, int Ci,
                                                             int Co, int S) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * kStage];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[kWStages * kStage];
   const int cib_n = Ci / kWBlk;
   const int tiles = (Co / kWBlk) * cib_n * 3;
   const int wg = xcd_swizzle(blockIdx.x, S * tiles);
@@ -214,25 +215,53 @@ __global__ void __launch_bounds__(512) conv3x3_wgrad_kernel(const bf16* __restri
   for (int a = 0; a < 3; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) zero16(acc[a][b]);
-  if (sb < se) issue(sb, 0);
+  // wave 0 issues 5 DMA blocks per segment (33 = 4 x 8 + 1), the others 4: the counted waits
+  // retire exactly the oldest segment
+#pragma unroll
+  for (int j = 0; j < kWStages - 1; ++j)
+    if (sb + j < se) issue(sb + j, j);
+  int st = 0;
   for (long long sg = sb; sg < se; ++sg) {
-    const int st = (int)((sg - sb) & 1);
-    wait_vm<0>();
-    raw_barrier();
-    if (sg + 1 < se) issue(sg + 1, st ^ 1);
+    if (sg + kWStages - 2 < se) {
+      if (w == 0)
+        wait_vm<5 * (kWStages - 2)>();
+      else
+        wait_vm<4 * (kWStages - 2)>();
+    } else {
+      wait_vm<0>();
+    }
+    raw_barrier();                                    // segment sg landed everywhere; sg - 1 consumed
+    if (sg + kWStages - 1 < se) issue(sg + kWStages - 1, st == 0 ? kWStages - 1 : st - 1);
     const unsigned char* sd = smem + st * kStage;
     const unsigned char* sx = sd + kDyBytes;
+    st = st == kWStages - 1 ? 0 : st + 1;
+    // operands of 16-pixel step k from asm transposed reads (lds_dma.h), one step ahead
+    bf16x8_t a[2][3], b[2][2];
+    auto load = [&](int k, int p) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) a[p][kx] = tr_frag_asm(sx, 16 * k + kx, ci_w, l);   // X^T: rows i, k = pixel
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) b[p][ct] = tr_frag_asm(sd, 16 * k, co_w + 32 * ct, l);   // dY: cols o
+    };
+    constexpr int RD = 10;                            // ds_read_tr per step
+    load(0, 0);
 #pragma unroll
     for (int k = 0; k < kSeg / 16; ++k) {
-      bf16x8_t a[3], b[2];
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) a[kx] = tr_frag(sx, 16 * k + kx, ci_w, l);   // X^T: rows i, k = pixel
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) b[ct] = tr_frag(sd, 16 * k, co_w + 32 * ct, l);   // dY: k = pixel, cols o
+      const int p = k & 1;
+      if (k + 1 < kSeg / 16) {
+        load(k + 1, p ^ 1);
+        lgkm_wait<RD>(a[p][0]);
+      } else {
+        lgkm_wait<0>(a[p][0]);
+      }
+      lgkm_wait<RD>(a[p][1]);
+      lgkm_wait<RD>(a[p][2]);
+      lgkm_wait<RD>(b[p][0]);
+      lgkm_wait<RD>(b[p][1]);
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct) acc[kx][ct] = mfma16(a[kx], b[ct], acc[kx][ct]);
+        for (int ct = 0; ct < 2; ++ct) acc[kx][ct] = mfma16(a[p][kx], b[p][ct], acc[kx][ct]);
     }
   }
   // lane column = o, registers = 4 groups of 4 consecutive i
@@ -251,28 +280,47 @@ __global__ void __launch_bounds__(512) conv3x3_wgrad_kernel(const bf16* __restri
   }
 }
 
-// dW[o, i, tap] (torch [Co, Ci, 3, 3]) = sum_s part[s][o][tap][i], fixed order; a thread owns 4 i
+// dW[o, i, tap] (torch [Co, Ci, 3, 3]) = sum_s part[s][o][tap][i], fixed order: a 256-thread
+// block owns 64 items of 4 i; thread (item, g) sums the splits g, g + 4, ..., the four group
+// sums are added in LDS in group order
 template <typename T>
 __global__ void __launch_bounds__(256) conv3x3_wgrad_reduce_kernel(const float* __restrict__ part, T* __restrict__ dw,
                                                                    int Ci, int Co, int S) {
-  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;   // (o, tap, i / 4)
+  __shared__ float4 sp[4][64];
+  const int it = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const long long q = (long long)blockIdx.x * 64 + it;  // (o, tap, i / 4)
   const long long nq = (long long)Co * 9 * (Ci / 4);
-  if (q >= nq) return;
-  const int i4 = (int)(q % (Ci / 4));
-  const long long ot = q / (Ci / 4);
-  const int tap = (int)(ot % 9), o = (int)(ot / 9);
+  const bool live = q < nq;
+  const long long qq = live ? q : 0;
+  const int i4 = (int)(qq % (Ci / 4));
+  const long long ot = qq / (Ci / 4);
   const size_t stride = (size_t)Co * 9 * Ci;
   const float* p = part + ot * Ci + 4 * i4;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = 0; s < S; ++s) {
-    const float4 v = *reinterpret_cast<const float4*>(p + s * stride);
-    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  if (live) {
+    int s = grp;
+    for (; s + 4 < S; s += 8) {
+      const float4 v0 = *reinterpret_cast<const float4*>(p + s * stride);
+      const float4 v1 = *reinterpret_cast<const float4*>(p + (s + 4) * stride);
+      a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+      a.x += v1.x; a.y += v1.y; a.z += v1.z; a.w += v1.w;
+    }
+    for (; s < S; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(p + s * stride);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
   }
-  T* d = dw + ((size_t)o * Ci + 4 * i4) * 9 + tap;
-  d[0] = from_f32<T>(a.x);
-  d[9] = from_f32<T>(a.y);
-  d[18] = from_f32<T>(a.z);
-  d[27] = from_f32<T>(a.w);
+  sp[grp][it] = a;
+  __syncthreads();
+  if (grp == 0 && live) {
+    const float4 b = sp[1][it], c = sp[2][it], d = sp[3][it];
+    const int tap = (int)(ot % 9), o = (int)(ot / 9);
+    T* dd = dw + ((size_t)o * Ci + 4 * i4) * 9 + tap;
+    dd[0] = from_f32<T>(((a.x + b.x) + c.x) + d.x);
+    dd[9] = from_f32<T>(((a.y + b.y) + c.y) + d.y);
+    dd[18] = from_f32<T>(((a.z + b.z) + c.z) + d.z);
+    dd[27] = from_f32<T>(((a.w + b.w) + c.w) + d.w);
+  }
 }
 
 // w [Co, Ci, 3, 3] -> wf [Co, 3, 3, Ci] (forward) and wb [Ci, 3, 3, Co] flipped (input gradient)
@@ -359,7 +407,7 @@ extern "C" int vs_conv3x3_wgrad(int dtype, const void* dy, const void* x, void* 
                      (const bf16*)x, (float*)workspace, B, H, W, Ci, Co, S);
   VS_LAUNCH_CHECK();
   const long long nq = (long long)Co * 9 * (Ci / 4);
-  const dim3 g((unsigned)((nq + 255) / 256));
+  const dim3 g((unsigned)((nq + 63) / 64));
   if (dtype == VS_BF16)
     hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel<bf16>, g, dim3(256), 0, st, (const float*)workspace, (bf16*)dw, Ci,
                        Co, S);

@@ -54,5 +54,43 @@ __device__ __forceinline__ bf16x8_t tr_frag(const unsigned char* img, int row0, 
   return v;
 }
 
+// The same operand read from inline asm.  The compiler's waitcnt pass models the
+// ds_read_tr intrinsic as possibly reading LDS that an in-flight LDS-DMA writes, so it drains
+// vmcnt(0) in front of it -- the next chunk's prefetch is then waited for before the current
+// chunk is multiplied (every chunk serialised behind its own DMA).  Hidden in asm, the read is
+// ordered only by what the kernel states: the buffer it reads was retired by a counted
+// wait_vm + barrier.  The pass does not track the asm's result either: lgkm_wait below must
+// sit between the reads and the first use, carrying the fragments as operands so that no use
+// (and no copy) is scheduled above it.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+__device__ __forceinline__ bf16x4v_t ds_tr16_asm(unsigned addr) {
+  bf16x4v_t v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+__device__ __forceinline__ bf16x8_t tr_frag_asm(const unsigned char* img, int row0, int col0, int lane) {
+  const int hh = lane >> 5;
+  const int row = row0 + 8 * hh + ((lane & 15) >> 2);
+  const int col = col0 + (lane & 16) + 4 * (lane & 3);
+  const int within = (col & 7) * 2;
+  const unsigned a = lds_addr(img);
+  const bf16x4v_t lo = ds_tr16_asm(a + woff(row, col >> 3) + within);
+  const bf16x4v_t hi = ds_tr16_asm(a + woff(row + 4, col >> 3) + within);
+  bf16x8_t v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+// wait until at most N LDS operations of this wave are outstanding; v is carried through
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8_t& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N) : "memory");
+}
+
 }  // namespace
 }  // namespace vs

@@ -139,8 +139,15 @@ def _forward_gemm(x, weight, bias):
 
 
 # The input gradient dX = dY W of the token Linears on the token GEMM (with W^T, a [K, N]
-# copy of the small weight) where the shape rule picks it: VS_TGEMM_DGRAD=1 (A/B switch).
-_TGEMM_DGRAD = os.environ.get("VS_TGEMM_DGRAD", "0") == "1"
+# copy of the small weight), by a static shape rule from tools/r5/wgrad_ab.py
+# (profiles/r5_wgrad_dgrad_ab.txt): the token GEMM won 1.0-1.5x at every C2 shape except the
+# reductions >= 4x the output width below 100k tokens (encoder fc1, stage-4 fc1: ties or
+# vendor wins).  VS_TGEMM_DGRAD=0: always the vendor GEMM.
+_TGEMM_DGRAD = os.environ.get("VS_TGEMM_DGRAD", "1") == "1"
+
+
+def _use_token_gemm_dgrad(T: int, K_out: int, N_red: int) -> bool:
+    return T <= 300_000 and not (N_red >= 4 * K_out and T <= 100_000)
 
 
 def _dgrad_gemm(gy2, weight):
@@ -148,7 +155,7 @@ def _dgrad_gemm(gy2, weight):
     N, K = weight.shape
     T = gy2.shape[0]
     if (_TGEMM_DGRAD and gy2.is_cuda and gy2.dtype == weight.dtype == torch.bfloat16 and K % 8 == 0 and N % 8 == 0
-            and T >= MIN_TOKENS and _use_token_gemm(T, K, N)):
+            and T >= MIN_TOKENS and _use_token_gemm_dgrad(T, K, N)):
         return ops.token_gemm(gy2.contiguous(), weight.t().contiguous())
     return gy2 @ weight.to(gy2.dtype)
 
