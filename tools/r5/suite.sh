@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 GPU call: the full -m gpu suite (no -x: every failure listed), smoke, default bench line.
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/r5
+O=gpurun_out/r5s
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread \
     --durations=30 > $O/gpu_tests_full.log 2>&1

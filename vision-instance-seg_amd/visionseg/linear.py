@@ -138,6 +138,16 @@ def _forward_gemm(x, weight, bias):
     return ops.token_gemm(x.reshape(-1, K), weight, bias).view(*x.shape[:-1], N)
 
 
+def _addmm_into(c, a, b):
+    """c + a @ b with the sum formed IN c (beta = 1 in the GEMM epilogue) when c is a
+    contiguous tensor of the product's dtype: torch.addmm into a new output first copies c
+    there (a full-size copyBuffer per call: ~15 us at the encoder's 87k x 256 tokens).  c is
+    a gradient handed over by ops.ResidualSink -- owned by the caller, dead afterwards."""
+    if c.dtype == a.dtype and c.is_contiguous():
+        return c.addmm_(a, b)
+    return torch.addmm(c.to(a.dtype), a, b)
+
+
 # The input gradient dX = dY W of the token Linears on the token GEMM (with W^T, a [K, N]
 # copy of the small weight), by a static shape rule from tools/r5/wgrad_ab.py
 # (profiles/r5_wgrad_dgrad_ab.txt): the token GEMM won 1.0-1.5x at every C2 shape except the
@@ -178,7 +188,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gres = ctx.sink.take() if ctx.sink is not None else None
             if gres is not None:       # the residual path's gradient of x, added by the GEMM (beta = 1)
-                gx = torch.addmm(gres.reshape(gy2.shape[0], -1).to(gy2.dtype), gy2, weight.to(gy2.dtype)).view(x.shape)
+                gx = _addmm_into(gres.reshape(gy2.shape[0], -1), gy2, weight.to(gy2.dtype)).view(x.shape)
             else:
                 gx = _dgrad_gemm(gy2, weight).view(x.shape)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
@@ -525,8 +535,7 @@ class _InProjFn(torch.autograd.Function):
                 gx.append(gxi if ctx.needs_input_grad[i] else None)
             x2 = x2.to(g2.dtype)
             if _token_wgrad_ok(g2, x2, weight.dtype) and weight.dtype == g2.dtype:
-                _, gbi = weight_grad(g2, x2, weight.dtype, out=gw[rows], bias=True)
-                gb[rows].copy_(gbi)
+                ops.token_wgrad(g2, x2, weight.dtype, bias=True, out=gw[rows], bias_out=gb[rows])
                 continue
             weight_grad(g2, x2, weight.dtype, out=gw[rows])
             if D % 8 == 0 and D <= 2048 and g2.dtype == weight.dtype:
@@ -590,8 +599,8 @@ class _ValueQueryProjFn(torch.autograd.Function):
             if gres is not None:
                 dh = dh + gres.reshape(dh.shape)
         else:
-            dh = gp2 @ wp_ if gres is None else torch.addmm(gres.reshape(gp2.shape[0], Dh).to(gp2.dtype), gp2, wp_)
-            dh = torch.addmm(dh, gv2, wv_)                            # + value's share, in the GEMM epilogue
+            dh = gp2 @ wp_ if gres is None else _addmm_into(gres.reshape(gp2.shape[0], Dh), gp2, wp_)
+            dh.addmm_(gv2, wv_)                                       # + value's share, in the GEMM epilogue
         h2, q2 = h.reshape(-1, Dh), q.reshape(-1, Dh)
         gwv, gbv = weight_grad(gv2, h2.to(gv2.dtype), wv.dtype, bias=True)
         gwp = weight_grad(gp2, q2.to(gp2.dtype), wp.dtype)
@@ -848,7 +857,7 @@ class _LinearReluFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gres = ctx.sink.take() if ctx.sink is not None else None
             if gres is not None:
-                gx = torch.addmm(gres.reshape(M, -1).to(gp.dtype), gp, weight.to(gp.dtype)).view(x.shape)
+                gx = _addmm_into(gres.reshape(M, -1), gp, weight.to(gp.dtype)).view(x.shape)
             else:
                 gx = _dgrad_gemm(gp, weight).view(x.shape)
         if ctx.needs_input_grad[1]:

@@ -1656,10 +1656,11 @@ def upsample_add_nhwc(cur, src_tokens, Hs: int, Ws: int):
 
 
 # ------------------------------------------------------------------ token-Linear weight gradient
-def token_wgrad(gy, x, out_dtype, bias: bool = False, out=None):
+def token_wgrad(gy, x, out_dtype, bias: bool = False, out=None, bias_out=None):
     """dW [N, K] = gy^T x for token-major gy [T, N], x [T, K] (bf16, rows strided, unit
     column stride), f32 accumulation, out_dtype; bias=True also returns db [N] = column sums
-    of gy (csrc/token_wgrad.hip).  `out`: a contiguous [N, K] tensor of out_dtype to write."""
+    of gy (csrc/token_wgrad.hip).  `out` / `bias_out`: contiguous [N, K] / [N] tensors of
+    out_dtype to write into (e.g. row blocks of a fused parameter's gradients)."""
     L.require_hip(gy, x)
     T, N = gy.shape
     K = x.shape[1]
@@ -1668,7 +1669,7 @@ def token_wgrad(gy, x, out_dtype, bias: bool = False, out=None):
     ws = torch.empty(nb, device=dev, dtype=torch.uint8)
     if out is None:
         out = torch.empty(N, K, device=dev, dtype=out_dtype)
-    db = torch.empty(N, device=dev, dtype=out_dtype) if bias else None
+    db = (bias_out if bias_out is not None else torch.empty(N, device=dev, dtype=out_dtype)) if bias else None
     with timed("token_wgrad", gy, flops=2.0 * T * N * K, bytes_=T * (N + K) * 2):
         L.check(L.lib().vs_token_wgrad(L.dtype_code(out), L.ptr(gy), gy.stride(0), L.ptr(x), x.stride(0), L.ptr(out),
                                        L.ptr(db) if bias else None, L.ptr(ws), T, N, K, L.stream(gy)), "token_wgrad")
