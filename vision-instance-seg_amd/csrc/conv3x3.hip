@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(512) conv3x3_wgrad_kernel(const bf16* __restri
   const int wg = xcd_swizzle(blockIdx.x, S * tiles);
   const int s = wg / tiles, tile = wg - s * tiles;    // a split's tiles are neighbours (same XCD, same pixels)
   const int ky = tile % 3, cib = (tile / 3) % cib_n, cob = tile / (3 * cib_n);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int co_w = (w & 1) * 64, ci_w = (w >> 1) * 32;  // this wave: 64 o x 32 i, three taps
   const int cpr = (Wd + kSeg - 1) / kSeg;               // segments per image row
   const long long nseg = (long long)B * H * cpr;
@@ -264,38 +264,44 @@ __global__ void __launch_bounds__(512) conv3x3_wgrad_kernel(const bf16* __restri
         for (int ct = 0; ct < 2; ++ct) acc[kx][ct] = mfma16(a[p][kx], b[p][ct], acc[kx][ct]);
     }
   }
-  // lane column = o, registers = 4 groups of 4 consecutive i
+  // partials in FRAGMENT order, whole 1-KB stores (token_wgrad.hip's layout): the
+  // workgroup's 128 o x 128 i x 3 taps block is [wave][kx][ct][g][lane][4 registers]
+  float* pw = part + ((size_t)s * tiles + tile) * (3 * kWBlk * kWBlk) + (size_t)w * 6144 + l * 4;
 #pragma unroll
-  for (int kx = 0; kx < 3; ++kx) {
-    const int tap = 3 * ky + kx;
+  for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      const int o = cob * kWBlk + co_w + 32 * ct + r;
-      float* dst = part + (((size_t)s * Co + o) * 9 + tap) * Ci + cib * kWBlk + ci_w + 4 * hh;
+    for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(dst + 8 * g) =
+        *reinterpret_cast<float4*>(pw + ((kx * 2 + ct) * 4 + g) * 256) =
             make_float4(acc[kx][ct][4 * g], acc[kx][ct][4 * g + 1], acc[kx][ct][4 * g + 2], acc[kx][ct][4 * g + 3]);
-    }
-  }
 }
 
-// dW[o, i, tap] (torch [Co, Ci, 3, 3]) = sum_s part[s][o][tap][i], fixed order: a 256-thread
-// block owns 64 items of 4 i; thread (item, g) sums the splits g, g + 4, ..., the four group
-// sums are added in LDS in group order
+// dW[o, i, tap] (torch [Co, Ci, 3, 3]) = sum over splits of the fragment-order partials,
+// fixed order.  A thread owns (o, tap, 4 consecutive i) -- one float4 of one lane per split;
+// consecutive threads take consecutive o (consecutive lanes).  A 256-thread block = 64 items x
+// 4 split groups (g, g + 4, ...), the group sums added in LDS in group order.
 template <typename T>
 __global__ void __launch_bounds__(256) conv3x3_wgrad_reduce_kernel(const float* __restrict__ part, T* __restrict__ dw,
                                                                    int Ci, int Co, int S) {
   __shared__ float4 sp[4][64];
   const int it = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const long long q = (long long)blockIdx.x * 64 + it;  // (o, tap, i / 4)
+  const long long q = (long long)blockIdx.x * 64 + it;    // (tap, i / 4, o), o fastest
   const long long nq = (long long)Co * 9 * (Ci / 4);
   const bool live = q < nq;
   const long long qq = live ? q : 0;
-  const int i4 = (int)(qq % (Ci / 4));
-  const long long ot = qq / (Ci / 4);
-  const size_t stride = (size_t)Co * 9 * Ci;
-  const float* p = part + ot * Ci + 4 * i4;
+  const int o = (int)(qq % Co);
+  const long long rest = qq / Co;
+  const int i = (int)(rest % (Ci / 4)) * 4, tap = (int)(rest / (Ci / 4));
+  const int cib_n = Ci / kWBlk, tiles = (Co / kWBlk) * cib_n * 3;
+  const int ky = tap / 3, kx = tap - 3 * ky;
+  const int cob = o / kWBlk, cib = i / kWBlk, oo = o % kWBlk, ii = i % kWBlk;
+  const int tile = (cob * cib_n + cib) * 3 + ky;
+  const int w = (ii >> 5) * 2 + (oo >> 6), ct = (oo & 63) >> 5, r = oo & 31;
+  const int row = ii & 31, g = row >> 3, hh = (row >> 2) & 1;
+  const size_t stride = (size_t)tiles * 3 * kWBlk * kWBlk;
+  const float* p = part + (size_t)tile * (3 * kWBlk * kWBlk) + (size_t)w * 6144 + ((kx * 2 + ct) * 4 + g) * 256 +
+                   (hh * 32 + r) * 4;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (live) {
     int s = grp;
@@ -314,8 +320,7 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_reduce_kernel(const float* 
   __syncthreads();
   if (grp == 0 && live) {
     const float4 b = sp[1][it], c = sp[2][it], d = sp[3][it];
-    const int tap = (int)(ot % 9), o = (int)(ot / 9);
-    T* dd = dw + ((size_t)o * Ci + 4 * i4) * 9 + tap;
+    T* dd = dw + ((size_t)o * Ci + i) * 9 + tap;
     dd[0] = from_f32<T>(((a.x + b.x) + c.x) + d.x);
     dd[9] = from_f32<T>(((a.y + b.y) + c.y) + d.y);
     dd[18] = from_f32<T>(((a.z + b.z) + c.z) + d.z);

@@ -32,7 +32,8 @@ namespace {
 // NS-stage ring of TK-token chunk buffers: NS - 1 chunks in flight while one is multiplied
 // (every wave issues the same PW DMA instructions per chunk, so a counted vmcnt wait retires
 // exactly the oldest chunk).
-template <int BO, int BI, int NS, int TK>
+// DBG (timing experiments only): 1 no MFMA, 2 no DMA, 3 neither and no LDS reads, 4 no chunk loop
+template <int BO, int BI, int NS, int TK, int DBG = 0>
 __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict__ gy, const bf16* __restrict__ x,
                                                           float* __restrict__ part, float* __restrict__ pbias, int T,
                                                           int N, int K, long long ldg, long long ldx, int S) {
@@ -93,7 +94,7 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
       const bool ok = ((dok >> j) & 1u) && drow[j] < left;
       const unsigned char* src = ok ? reinterpret_cast<const unsigned char*>(((dgy >> j) & 1u ? cg : cx) + doff[j])
                                     : g_dma_zero_row + ch * 16;
-      glds16(src, base + blk * 1024);
+      if (DBG != 2 && DBG != 3) glds16(src, base + blk * 1024);
     }
   };
 
@@ -127,6 +128,7 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
       // operands of 16-token step k (asm reads: see lds_dma.h), one step ahead of the MFMAs
       bf16x8_t a[2][2], b[2][TO];
       auto load = [&](int k, int p) {
+        if (DBG == 3) return;
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti) {
           const int ic = wi + 32 * ti;                                                         // X^T: rows i
@@ -161,54 +163,72 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
 #pragma unroll
         for (int to = 0; to < TO; ++to) {
 #pragma unroll
-          for (int ti = 0; ti < 2; ++ti) acc[to][ti] = mfma16(a[p][ti], b[p][to], acc[to][ti]);
+          for (int ti = 0; ti < 2; ++ti)
+            if (DBG != 1 && DBG != 3) acc[to][ti] = mfma16(a[p][ti], b[p][to], acc[to][ti]);
           if (BIAS && to == bt) accb = mfma16(ones, b[p][to], accb);   // bt: scalar, a branch
         }
       }
     }
   };
-  if (do_bias)
+  if (DBG == 4) {
+  } else if (do_bias) {
     run(std::true_type{});
-  else
+  } else {
     run(std::false_type{});
-  // C[i][o]: lane column = o, registers = 4 groups of 4 consecutive i
-#pragma unroll
-  for (int to = 0; to < TO; ++to) {
-    const int o = ob * BO + wo + 32 * to + r;
-    if (o >= N) continue;
-    float* prow = part + ((size_t)s * N + o) * K;
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti) {
-      const int i0 = ib * BI + wi + 32 * ti + 4 * hh;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int i = i0 + 8 * g;
-        if (i < K)
-          *reinterpret_cast<float4*>(prow + i) =
-              make_float4(acc[to][ti][4 * g], acc[to][ti][4 * g + 1], acc[to][ti][4 * g + 2], acc[to][ti][4 * g + 3]);
-      }
-    }
   }
+  // partials in FRAGMENT order (whole 1-KB stores: the [o][i] row layout wrote 16 B every
+  // 32 B across 32 rows per instruction, ~2 TB/s): the workgroup's block of BO x BI floats is
+  // [wave][to][ti][g][lane][4 registers]; token_wgrad_reduce_kernel maps (o, i) back
+  float* pw = part + ((size_t)s * tiles + tile) * (BO * BI) + (size_t)w * (TO * 2 * 1024) + l * 4;
+#pragma unroll
+  for (int to = 0; to < TO; ++to)
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(pw + ((to * 2 + ti) * 4 + g) * 256) =
+            make_float4(acc[to][ti][4 * g], acc[to][ti][4 * g + 1], acc[to][ti][4 * g + 2], acc[to][ti][4 * g + 3]);
   if (do_bias && hh == 0) {
     const int o = ob * BO + wo + 32 * bt + r;
     if (o < N) pbias[(size_t)s * N + o] = accb[0];
   }
 }
 
-// dW[n] = sum_s part[s][n] and db[o] = sum_s pbias[s][o] in a fixed order: a 256-thread block
-// owns 64 float4 items; thread (item, g) sums the splits g, g + 4, ... (four loads in flight
-// per pass), the four group sums are added in LDS in group order
+// dW[o][i] = sum_s (fragment-order partial of (o, i) in split s), db[o] = sum_s pbias[s][o],
+// fixed order.  A thread owns (o, 4 consecutive i): one float4 per split (the 4 registers of
+// a lane's group), consecutive threads take consecutive o (= consecutive lanes: 16-B reads of
+// one 1-KB block).  A 256-thread block = 64 items x 4 split groups (g, g + 4, ...), the group
+// sums added in LDS in group order.
 template <typename T>
 __global__ void __launch_bounds__(256) token_wgrad_reduce_kernel(const float* __restrict__ part,
                                                                  const float* __restrict__ pbias, T* __restrict__ dw,
-                                                                 T* __restrict__ db, long long nw, int N, int S) {
+                                                                 T* __restrict__ db, int N, int K, int BO, int BI,
+                                                                 int S) {
   __shared__ float4 sp[4][64];
   const int it = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const long long q = (long long)blockIdx.x * 64 + it;  // float4 item: dW, then db (N / 4 items)
-  const long long nq = nw / 4, nqb = db ? N / 4 : 0;
+  const long long q = (long long)blockIdx.x * 64 + it;
+  const long long nq = (long long)N * (K / 4), nqb = db ? N / 4 : 0;
   const bool isw = q < nq, isb = !isw && q - nq < nqb;
-  const float* src = isw ? part + 4 * q : (isb ? pbias + 4 * (q - nq) : part);
-  const long long stride = isw ? nw : (long long)N;
+  const int WO = BI == 128 ? 4 : 2, TO = BO / WO / 32;
+  const int tiles_i = (K + BI - 1) / BI, tiles = ((N + BO - 1) / BO) * tiles_i;
+  const long long tstride = (long long)tiles * BO * BI;          // floats per split
+  const float* src = part;
+  long long stride = tstride;
+  int o = 0, i = 0;
+  if (isw) {
+    o = (int)(q % N);
+    i = (int)(q / N) * 4;
+    const int ob = o / BO, ib = i / BI, oo = o - ob * BO, ii = i - ib * BI;
+    const int qo = oo / (BO / WO), qi = ii >> 6, to = (oo % (BO / WO)) >> 5, r = oo & 31;
+    const int ti = (ii & 63) >> 5, row = ii & 31;                // row % 4 == 0: registers 4g..4g+3
+    const int g = row >> 3, hh = (row >> 2) & 1;
+    const int w = qi * WO + qo;
+    src = part + (long long)(ob * tiles_i + ib) * BO * BI + (long long)w * (TO * 2 * 1024) +
+          ((to * 2 + ti) * 4 + g) * 256 + (hh * 32 + r) * 4;
+  } else if (isb) {
+    src = pbias + 4 * (q - nq);
+    stride = N;
+  }
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (isw || isb) {
     int s = grp;
@@ -233,11 +253,11 @@ __global__ void __launch_bounds__(256) token_wgrad_reduce_kernel(const float* __
     const float4 b = sp[1][it], c = sp[2][it], d = sp[3][it];
     const float r0 = ((a.x + b.x) + c.x) + d.x, r1 = ((a.y + b.y) + c.y) + d.y;
     const float r2 = ((a.z + b.z) + c.z) + d.z, r3 = ((a.w + b.w) + c.w) + d.w;
-    T* o = isw ? dw + 4 * q : db + 4 * (q - nq);
-    o[0] = from_f32<T>(r0);
-    o[1] = from_f32<T>(r1);
-    o[2] = from_f32<T>(r2);
-    o[3] = from_f32<T>(r3);
+    T* out = isw ? dw + (size_t)o * K + i : db + 4 * (q - nq);
+    out[0] = from_f32<T>(r0);
+    out[1] = from_f32<T>(r1);
+    out[2] = from_f32<T>(r2);
+    out[3] = from_f32<T>(r3);
   }
 }
 
@@ -294,7 +314,9 @@ using namespace vs;
 extern "C" long long vs_token_wgrad_workspace_bytes(long long tokens, int N, int K) {
   if (tokens <= 0 || N <= 0 || K <= 0) return 0;
   const long long S = wgrad_splits(tokens, N, K);
-  return S * ((long long)N * K + N) * 4;
+  const int BO = wgrad_bo(N), BI = wgrad_bi(N, K);
+  const long long padded = (long long)((N + BO - 1) / BO) * BO * (((K + BI - 1) / BI) * BI);
+  return S * (padded + N) * 4;
 }
 
 extern "C" int vs_token_wgrad(int dtype, const void* grad_y, long long ld_grad_y, const void* x, long long ld_x,
@@ -312,7 +334,7 @@ extern "C" int vs_token_wgrad(int dtype, const void* grad_y, long long ld_grad_y
   const long long tiles = (long long)((N + BO - 1) / BO) * ((K + BI - 1) / BI);
   VS_CHECK(S * tiles < (1ll << 31), "too many workgroups");
   float* part = (float*)workspace;
-  float* pb = db ? part + (size_t)S * N * K : nullptr;
+  float* pb = db ? part + (size_t)S * tiles * BO * BI : nullptr;
   hipStream_t st = (hipStream_t)stream;
   const dim3 g((unsigned)(S * tiles));
 #define VS_TW(BO_, BI_, NS_, TK_)                                                                                  \
@@ -327,21 +349,42 @@ extern "C" int vs_token_wgrad(int dtype, const void* grad_y, long long ld_grad_y
     }
   } else {
     if (BO == 256) {
-      if (t64) VS_TW(256, 128, 3, 64); else VS_TW(256, 128, 6, 32);
+      if (t64) {
+        static const int dbg = [] {
+          const char* e = getenv("VS_WGRAD_DEBUG");
+          return e ? atoi(e) : 0;
+        }();
+        if (dbg == 1)
+          hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 3, 64, 1>), g, dim3(512), 0, st, (const bf16*)grad_y,
+                             (const bf16*)x, part, pb, (int)tokens, N, K, ld_grad_y, ld_x, S);
+        else if (dbg == 2)
+          hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 3, 64, 2>), g, dim3(512), 0, st, (const bf16*)grad_y,
+                             (const bf16*)x, part, pb, (int)tokens, N, K, ld_grad_y, ld_x, S);
+        else if (dbg == 3)
+          hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 3, 64, 3>), g, dim3(512), 0, st, (const bf16*)grad_y,
+                             (const bf16*)x, part, pb, (int)tokens, N, K, ld_grad_y, ld_x, S);
+        else if (dbg == 4)
+          hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 3, 64, 4>), g, dim3(512), 0, st, (const bf16*)grad_y,
+                             (const bf16*)x, part, pb, (int)tokens, N, K, ld_grad_y, ld_x, S);
+        else
+          VS_TW(256, 128, 3, 64);
+      } else {
+        VS_TW(256, 128, 6, 32);
+      }
     } else {
       if (t64) VS_TW(128, 128, 4, 64); else VS_TW(128, 128, 8, 32);
     }
   }
 #undef VS_TW
   VS_LAUNCH_CHECK();
-  const long long nw = (long long)N * K;
-  const long long items = nw / 4 + (db ? N / 4 : 0);
+  const long long items = (long long)N * (K / 4) + (db ? N / 4 : 0);
   const dim3 gr((unsigned)((items + 63) / 64));
   if (dtype == VS_BF16)
-    hipLaunchKernelGGL(token_wgrad_reduce_kernel<bf16>, gr, dim3(256), 0, st, part, pb, (bf16*)dw, (bf16*)db, nw, N, S);
+    hipLaunchKernelGGL(token_wgrad_reduce_kernel<bf16>, gr, dim3(256), 0, st, part, pb, (bf16*)dw, (bf16*)db, N, K,
+                       BO, BI, S);
   else
-    hipLaunchKernelGGL(token_wgrad_reduce_kernel<float>, gr, dim3(256), 0, st, part, pb, (float*)dw, (float*)db, nw,
-                       N, S);
+    hipLaunchKernelGGL(token_wgrad_reduce_kernel<float>, gr, dim3(256), 0, st, part, pb, (float*)dw, (float*)db, N, K,
+                       BO, BI, S);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
