@@ -658,6 +658,21 @@ VS_API int vs_upsample_backward_nhwc(int dtype, const void* grad_out, void* grad
  * Replaces autograd's gy^T x of F.linear's backward (the reference's Linears, HF:swin /
  * HF:m2f) for the token-heavy Linears. */
 VS_API long long vs_token_wgrad_workspace_bytes(long long tokens, int N, int K);
+/* A GROUP of independent token-Linear weight gradients in one launch (plus one reduction
+ * launch when some are split): the plan spreads the Linears' tiles over the CUs, so most run
+ * unsplit and write dw / db directly.  Every problem as for vs_token_wgrad (db may be NULL;
+ * dw / db 16-B aligned); dtype applies to all dw / db.  Workspace from
+ * vs_token_wgrad_grouped_workspace_bytes(probs, n) (the same list). */
+typedef struct {
+  const void* grad_y;
+  const void* x;
+  void* dw;
+  void* db;
+  long long ld_grad_y, ld_x, tokens;
+  int N, K;
+} vs_wgrad_problem;
+VS_API long long vs_token_wgrad_grouped_workspace_bytes(const vs_wgrad_problem* probs, int n);
+VS_API int vs_token_wgrad_grouped(int dtype, const vs_wgrad_problem* probs, int n, void* workspace, void* stream);
 VS_API int vs_token_wgrad(int dtype, const void* grad_y, long long ld_grad_y, const void* x, long long ld_x, void* dw,
                           void* db, void* workspace, long long tokens, int N, int K, void* stream);
 

@@ -449,3 +449,55 @@ def test_linear_backward_token_wgrad_matches_vendor(monkeypatch):
     a, v = run(True), run(False)
     for p, q in zip(a, v):
         assert float((p - q).norm() / q.norm()) < 1e-2
+
+
+def test_token_wgrad_grouped_vs_f64():
+    """ops.token_wgrad_grouped: one launch for Linears of different shapes (both tile widths,
+    with and without bias, a strided operand, a ragged token count); every dW / db vs f64 with
+    the single-Linear bound (one f32 sum, one rounding)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(21)
+    shapes = [(4096, 288, 96, True), (6001, 96, 384, False), (20000, 1536, 384, True), (4200, 256, 1024, True),
+              (65536, 576, 192, False), (3000, 136, 200, True)]
+    items, refs = [], []
+    for T, N, K, bias in shapes:
+        gyw = _rand((T, N + 8), g).to(DEV)
+        gy, x = gyw[:, :N], _rand((T, K), g).to(DEV)
+        dw = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+        db = torch.empty(N, device=DEV, dtype=torch.bfloat16) if bias else None
+        items.append((gy, x, dw, db))
+        refs.append((gy.double().t() @ x.double(), gy.double().sum(0) if bias else None))
+    ops.token_wgrad_grouped(items, torch.bfloat16)
+    for (gy, x, dw, db), (rw, rb) in zip(items, refs):
+        for a, r in ((dw, rw), (db, rb)):
+            if r is None:
+                continue
+            err = (a.double() - r).abs()
+            assert bool((err <= 2.0 ** -8 * r.abs() + 1e-5 * r.abs().max()).all()), (tuple(gy.shape), float(err.max()))
+
+
+def test_deferred_weight_grads_equal_immediate(monkeypatch):
+    """linear.deferred_weight_grads: a token-Linear stack's parameter gradients computed in
+    one grouped launch at the end of the backward equal the per-Linear ones (f32 summation
+    order only: bf16 1e-2 relative), the .grad tensors are the ones the flush wrote, and a
+    weight used twice in one backward is computed immediately (the sum stays exact)."""
+    from visionseg import linear as lin
+    g = torch.Generator().manual_seed(3)
+    x = _rand((4, 2048, 192), g).to(DEV)
+    w1, b1 = _rand((576, 192), g, 0.05).to(DEV), _rand((576,), g).to(DEV)
+    w2, b2 = _rand((192, 576), g, 0.05).to(DEV), _rand((192,), g).to(DEV)
+    gy = _rand((4, 2048, 192), g).to(DEV)
+
+    def run(defer):
+        ps = [t.clone().requires_grad_() for t in (x, w1, b1, w2, b2)]
+        xs, a1, c1, a2, c2 = ps
+        h = lin.linear_tokens(xs, a1, c1)
+        y = lin.linear_tokens(h, a2, c2) + lin.linear_tokens(xs, a1[:192], c1[:192])   # a1 used twice
+        with lin.deferred_weight_grads(enabled=defer):
+            y.backward(gy)
+        return [p.grad.float() for p in ps]
+
+    monkeypatch.setattr(lin, "_DEFER_WGRAD", True)
+    a, b = run(True), run(False)
+    for p, q in zip(a, b):
+        assert float((p - q).norm() / q.norm()) < 1e-2

@@ -1,7 +1,7 @@
-// Weight (and bias) gradient of a token-major Linear: dW[o, i] = sum_t gY[t, o] X[t, i],
+// Weight (and bias) gradient of token-major Linears: dW[o, i] = sum_t gY[t, o] X[t, i],
 // db[o] = sum_t gY[t, o], for the token-heavy Linears of the Swin blocks and the pixel
 // decoder (qkv, proj, fc1, fc2; the encoder's value / output / offset
-// projections and FFN).
+// projections and FFN) -- one Linear per call, or a GROUP of independent Linears in one launch.
 //
 // The reduction runs over tokens -- the strided dimension of both operands.  The vendor path
 // was a batched GEMM over token chunks with f32 outputs (hipBLASLt, ~0.3 PF/s at these
@@ -12,8 +12,16 @@
 // (k = token runs down the rows).  A workgroup owns BO output rows x 128 input columns of dW
 // for one split of the tokens; the bias gradient rides along as one more MFMA per o-tile with
 // an all-ones A operand (its every row = the column sums of gY) in the workgroups of the first
-// input block.  Per-split f32 partials are summed in a fixed order by a second kernel that
-// writes dW / db in the parameter dtype (deterministic, no atomics).
+// input block.
+//
+// Splits: a Linear's output has few 256 x 128 tiles (18 at the C2 stage-3 fc1), so the
+// tokens are split to fill the chip, and every split's f32 tile goes to memory and back
+// through a reduction (~14 of a 33 us launch at that shape: one f32 block per CU).  A GROUP
+// launch plans all its Linears together: with the tiles of many Linears filling the CUs,
+// most of them run unsplit and write dW / db straight from the accumulators; a split is
+// only used to balance the chunks per workgroup (the plan sizes every workgroup to about the
+// same number of chunks).  Split partials are summed in a fixed order by a second kernel
+// (deterministic, no atomics).
 #include <stdlib.h>
 
 #include <type_traits>
@@ -23,43 +31,80 @@
 namespace vs {
 namespace {
 
+constexpr int kTK = 64;                      // tokens per chunk
+constexpr int kMaxProbs = 20;                // Linears per group launch (kernel-argument space)
 
-// A workgroup: BO output rows x BI input columns of dW (BO, BI in {128, 256}), 8 waves in a
-// WO x WI grid (WO = 4 for BI = 128, else 2): a wave owns BO / WO rows (TO MFMA tiles of 32) x
-// 64 columns (2 tiles).  The bias column sums: wave (qo, qi) adds the ones-row MFMA for its
-// o-tile qi (if it has one), so the extra MFMA is spread over the waves of the first input
-// block.  part [S][N][K], pbias [S][N].
-// NS-stage ring of TK-token chunk buffers: NS - 1 chunks in flight while one is multiplied
+// one Linear of a launch, planned on the host
+struct WgProb {
+  const bf16* gy;
+  const bf16* x;
+  void* dw;
+  void* db;
+  long long ldg, ldx;
+  long long part0;                           // first float of its split partial blocks (S > 1)
+  long long pb0;                             // first float of its bias partials (S > 1)
+  int T, N, K;
+  int S;                                     // token splits
+  int tiles_i, tiles;                        // tiles per split
+  int wg0;                                   // first workgroup
+  int item0;                                 // first reduction item (S > 1)
+};
+
+struct WgGroup {
+  WgProb p[kMaxProbs];
+  int n;
+  int f32;                                   // dW / db dtype: 1 f32, 0 bf16
+};
+
+__device__ __forceinline__ void store4(void* base, size_t idx, bool f32, float a, float b, float c, float d) {
+  if (f32) {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(base) + idx) = make_float4(a, b, c, d);
+  } else {
+    bf16x4_t v = {bf16_bits(a), bf16_bits(b), bf16_bits(c), bf16_bits(d)};
+    *reinterpret_cast<bf16x4_t*>(reinterpret_cast<bf16*>(base) + idx) = v;
+  }
+}
+
+// A workgroup: BO output rows x 128 input columns of one Linear's dW, 8 waves in a 4 x 2 grid:
+// a wave owns BO / 4 rows (TO MFMA tiles of 32) x 64 columns (2 tiles).  The bias column
+// sums: wave (qo, qi) adds the ones-row MFMA for its o-tile qi (if it has one).
+// NS-stage ring of 64-token chunk buffers: NS - 1 chunks in flight while one is multiplied
 // (every wave issues the same PW DMA instructions per chunk, so a counted vmcnt wait retires
 // exactly the oldest chunk).
 // DBG (timing experiments only): 1 no MFMA, 2 no DMA, 3 neither and no LDS reads, 4 no chunk loop
-template <int BO, int BI, int NS, int TK, int DBG = 0>
-__global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict__ gy, const bf16* __restrict__ x,
-                                                          float* __restrict__ part, float* __restrict__ pbias, int T,
-                                                          int N, int K, long long ldg, long long ldx, int S) {
+template <int BO, int BI, int WO, int WI, int NS, int DBG = 0>
+__global__ void __launch_bounds__(64 * WO * WI) token_wgrad_kernel(const WgGroup grp, float* __restrict__ part,
+                                                                   float* __restrict__ pbias, int spread) {
+  constexpr int TK = kTK, NW = WO * WI;
   constexpr int NH = BO / 128, NXH = BI / 128;          // gY / X half-images of 128 columns
   constexpr int IMG = TK * 256;                         // bytes of one half-image
   constexpr int GYB = NH * IMG, STG = (NH + NXH) * IMG;
   constexpr int RB = TK / 4;                            // 1-KB DMA blocks (4 rows) per image
   constexpr int NBLK = STG / 1024;                      // 1-KB DMA blocks per stage
-  constexpr int PW = NBLK / 8;                          // DMA instructions per wave per chunk
-  static_assert(NBLK % 8 == 0, "uniform DMA count per wave");
-  constexpr int WO = BI == 128 ? 4 : 2, WI = 8 / WO;
-  static_assert(WI * 64 == BI, "64 input columns per wave");
-  constexpr int TO = BO / WO / 32;                      // o-tiles per wave
-  static_assert(TO <= WI, "one bias o-tile per wave");
+  constexpr int PW = NBLK / NW;                         // DMA instructions per wave per chunk
+  static_assert(NBLK % NW == 0, "uniform DMA count per wave");
+  constexpr int TO = BO / WO / 32, TI = BI / WI / 32;   // o- / i-tiles per wave
+  constexpr int NB = TO / WI > 0 ? TO / WI : 1;         // bias o-tiles per wave (waves of one qo share)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * STG];
-  const int tiles_o = (N + BO - 1) / BO, tiles_i = (K + BI - 1) / BI, tiles = tiles_o * tiles_i;
-  const int wg = xcd_swizzle(blockIdx.x, S * tiles);
-  const int s = wg / tiles, tile = wg - s * tiles;      // a split's tiles are neighbours (one XCD)
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  int pi = 0;                                           // this workgroup's Linear (scalar scan)
+  for (int k = 1; k < grp.n; ++k)
+    if (wg >= grp.p[k].wg0) pi = k;
+  const WgProb& P = grp.p[pi];
+  const bf16* __restrict__ gy = P.gy;
+  const bf16* __restrict__ x = P.x;
+  const int T = P.T, N = P.N, K = P.K, S = P.S, tiles_i = P.tiles_i, tiles = P.tiles;
+  const long long ldg = P.ldg, ldx = P.ldx;
+  const int local = wg - P.wg0;
+  const int s = local / tiles, tile = local - s * tiles;   // a split's tiles are neighbours (one XCD)
   const int ob = tile / tiles_i, ib = tile - ob * tiles_i;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   const int qo = w % WO, qi = w / WO;
-  const int wo = qo * (BO / WO), wi = qi * 64;
+  const int wo = qo * (BO / WO), wi = qi * (BI / WI);
   const long long nchunk = ((long long)T + TK - 1) / TK;
   const long long cb = nchunk * s / S, ce = nchunk * (s + 1) / S;
-  const int bt = __builtin_amdgcn_readfirstlane(qi);    // this wave's bias o-tile (if < TO)
-  const bool do_bias = pbias != nullptr && ib == 0 && bt < TO;
+  const int bt = __builtin_amdgcn_readfirstlane(qi * NB);   // this wave's first bias o-tile (if < TO)
+  const bool do_bias = P.db != nullptr && ib == 0 && bt < TO;
 
   // per-lane DMA constants, hoisted out of the chunk loop: for the j-th piece, the element
   // offset of this lane's 16 B inside a chunk (row * ld + col), its row, and whether it reads
@@ -68,7 +113,7 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
   unsigned dgy = 0, dok = 0;
 #pragma unroll
   for (int j = 0; j < PW; ++j) {
-    const int blk = w + 8 * j;
+    const int blk = w + NW * j;
     const int img = blk / RB, row = (blk % RB) * 4 + (l >> 4), ch = (l & 15) ^ img_swz(row);
     drow[j] = row;
     if (img < NH) {
@@ -82,14 +127,16 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
       if (col < K) dok |= 1u << j;
     }
   }
-  auto issue = [&](long long c, int st) {
+  // pieces [J0, J1) of chunk c into stage st
+  auto issue_part = [&](long long c, int st, auto j0_tag, auto j1_tag) {
+    constexpr int J0 = decltype(j0_tag)::value, J1 = decltype(j1_tag)::value;
     unsigned char* base = smem + st * STG;
     const bf16* cg = gy + c * TK * ldg;                 // the chunk's first rows (wave-uniform)
     const bf16* cx = x + c * TK * ldx;
     const long long left = (long long)T - c * TK;       // rows of the chunk inside the matrix
 #pragma unroll
-    for (int j = 0; j < PW; ++j) {
-      const int blk = w + 8 * j;
+    for (int j = J0; j < J1; ++j) {
+      const int blk = w + NW * j;
       const int ch = (l & 15) ^ img_swz(drow[j]);
       const bool ok = ((dok >> j) & 1u) && drow[j] < left;
       const unsigned char* src = ok ? reinterpret_cast<const unsigned char*>(((dgy >> j) & 1u ? cg : cx) + doff[j])
@@ -97,14 +144,17 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
       if (DBG != 2 && DBG != 3) glds16(src, base + blk * 1024);
     }
   };
+  auto issue = [&](long long c, int st) {
+    issue_part(c, st, std::integral_constant<int, 0>{}, std::integral_constant<int, PW>{});
+  };
 
-  f32x16_t acc[TO][2], accb;
+  f32x16_t acc[TO][TI], accb[NB];
 #pragma unroll
-  for (int a = 0; a < TO; ++a) {
-    zero16(acc[a][0]);
-    zero16(acc[a][1]);
-  }
-  zero16(accb);
+  for (int a = 0; a < TO; ++a)
+#pragma unroll
+    for (int b = 0; b < TI; ++b) zero16(acc[a][b]);
+#pragma unroll
+  for (int a = 0; a < NB; ++a) zero16(accb[a]);
   const short one = (short)0x3f80;                      // bf16 1.0
   const bf16x8_t ones = {one, one, one, one, one, one, one, one};
 #pragma unroll
@@ -121,16 +171,21 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
       else
         wait_vm<0>();
       raw_barrier();                                    // every wave's did; chunk c - 1 is consumed
-      if (c + NS - 1 < ce) issue(c + NS - 1, st == 0 ? NS - 1 : st - 1);   // into chunk c - 1's stage
+      // chunk c + NS - 1 goes into chunk c - 1's stage, its DMA pieces issued between the
+      // MFMAs of chunk c's four steps (an LDS-DMA piece costs ~60-185 issue cycles: issued all
+      // at once after the barrier, by every wave at the same time, they idled the MFMA pipe)
+      const bool pre = spread && c + NS - 1 < ce;
+      const int pst = st == 0 ? NS - 1 : st - 1;
+      if (!spread && c + NS - 1 < ce) issue(c + NS - 1, pst);
       const unsigned char* sg = smem + st * STG;
       st = st == NS - 1 ? 0 : st + 1;
       const unsigned char* sx = sg + GYB;
       // operands of 16-token step k (asm reads: see lds_dma.h), one step ahead of the MFMAs
-      bf16x8_t a[2][2], b[2][TO];
+      bf16x8_t a[TO + TI <= 4 ? 2 : 1][TI], b[TO + TI <= 4 ? 2 : 1][TO];
       auto load = [&](int k, int p) {
         if (DBG == 3) return;
 #pragma unroll
-        for (int ti = 0; ti < 2; ++ti) {
+        for (int ti = 0; ti < TI; ++ti) {
           const int ic = wi + 32 * ti;                                                         // X^T: rows i
           a[p][ti] = tr_frag_asm(sx + (ic >> 7) * IMG, 16 * k, ic & 127, l);
         }
@@ -140,10 +195,13 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
           b[p][to] = tr_frag_asm(sg + (oc >> 7) * IMG, 16 * k, oc & 127, l);
         }
       };
-      constexpr int RD = 2 * (2 + TO);                   // ds_read_tr per step
-      // DB: step k + 1's operands in flight during step k's MFMAs (the 256 x 256 tile has no
-      // registers for a second set: its co-resident wave hides the reads instead)
-      constexpr bool DB = TO <= 2;
+      // ds_read_tr per step (the lgkmcnt field holds 15: a wait for "<= 15 outstanding" of 16
+      // newer reads also retires one of them -- correct, marginally early)
+      constexpr int RD = 2 * (TI + TO) > 15 ? 15 : 2 * (TI + TO);
+      // DB: step k + 1's operands read during step k's MFMAs (the 256 x 256 tile's 256
+      // accumulators leave no registers for a second set: one wave per SIMD, the next step's
+      // reads are issued right after the MFMAs that free them)
+      constexpr bool DB = TO + TI <= 4;
       if (DB) load(0, 0);
 #pragma unroll
       for (int k = 0; k < TK / 16; ++k) {
@@ -157,15 +215,33 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
         } else {
           lgkm_wait<0>(a[p][0]);
         }
-        lgkm_wait<RD>(a[p][1]);
+#pragma unroll
+        for (int ti = 1; ti < TI; ++ti) lgkm_wait<RD>(a[p][ti]);
 #pragma unroll
         for (int to = 0; to < TO; ++to) lgkm_wait<RD>(b[p][to]);
 #pragma unroll
         for (int to = 0; to < TO; ++to) {
 #pragma unroll
-          for (int ti = 0; ti < 2; ++ti)
+          for (int ti = 0; ti < TI; ++ti)
             if (DBG != 1 && DBG != 3) acc[to][ti] = mfma16(a[p][ti], b[p][to], acc[to][ti]);
-          if (BIAS && to == bt) accb = mfma16(ones, b[p][to], accb);   // bt: scalar, a branch
+          // bias: this wave's NB o-tiles from bt (a scalar: a uniform branch, compile-time slot)
+          if (BIAS && to >= bt && to < bt + NB) accb[to % NB] = mfma16(ones, b[p][to], accb[to % NB]);
+        }
+        // this step's share of the next chunk's DMA pieces, behind the MFMAs just issued
+        if (pre) {
+          constexpr int NSTEP = TK / 16;
+          if (k == 0)
+            issue_part(c + NS - 1, pst, std::integral_constant<int, 0>{},
+                       std::integral_constant<int, PW * 1 / NSTEP>{});
+          else if (k == 1)
+            issue_part(c + NS - 1, pst, std::integral_constant<int, PW * 1 / NSTEP>{},
+                       std::integral_constant<int, PW * 2 / NSTEP>{});
+          else if (k == 2)
+            issue_part(c + NS - 1, pst, std::integral_constant<int, PW * 2 / NSTEP>{},
+                       std::integral_constant<int, PW * 3 / NSTEP>{});
+          else if (k == 3)
+            issue_part(c + NS - 1, pst, std::integral_constant<int, PW * 3 / NSTEP>{},
+                       std::integral_constant<int, PW>{});
         }
       }
     }
@@ -176,62 +252,102 @@ __global__ void __launch_bounds__(512) token_wgrad_kernel(const bf16* __restrict
   } else {
     run(std::false_type{});
   }
-  // partials in FRAGMENT order (whole 1-KB stores: the [o][i] row layout wrote 16 B every
-  // 32 B across 32 rows per instruction, ~2 TB/s): the workgroup's block of BO x BI floats is
-  // [wave][to][ti][g][lane][4 registers]; token_wgrad_reduce_kernel maps (o, i) back
-  float* pw = part + ((size_t)s * tiles + tile) * (BO * BI) + (size_t)w * (TO * 2 * 1024) + l * 4;
+  if (S > 1) {
+    // split partials in FRAGMENT order (whole 1-KB stores): the workgroup's block of BO x BI
+    // floats is [wave][to][ti][g][lane][4 registers]; token_wgrad_reduce_kernel maps (o, i) back
+    float* pw = part + P.part0 + ((size_t)s * tiles + tile) * (BO * BI) + (size_t)w * (TO * TI * 1024) + l * 4;
 #pragma unroll
-  for (int to = 0; to < TO; ++to)
+    for (int to = 0; to < TO; ++to)
 #pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
+      for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(pw + ((to * 2 + ti) * 4 + g) * 256) =
-            make_float4(acc[to][ti][4 * g], acc[to][ti][4 * g + 1], acc[to][ti][4 * g + 2], acc[to][ti][4 * g + 3]);
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(pw + ((to * TI + ti) * 4 + g) * 256) =
+              make_float4(acc[to][ti][4 * g], acc[to][ti][4 * g + 1], acc[to][ti][4 * g + 2], acc[to][ti][4 * g + 3]);
+    if (do_bias && hh == 0) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int o = ob * BO + wo + 32 * (bt + j) + r;
+        if (bt + j < TO && o < N) pbias[P.pb0 + (size_t)s * N + o] = accb[j][0];
+      }
+    }
+    return;
+  }
+  // unsplit: dW / db straight from the accumulators (lane column = o, registers = 4 groups of
+  // 4 consecutive i), rounded once to the parameter dtype
+  const bool f32 = grp.f32 != 0;
+#pragma unroll
+  for (int to = 0; to < TO; ++to) {
+    const int o = ob * BO + wo + 32 * to + r;
+    if (o >= N) continue;
+#pragma unroll
+    for (int ti = 0; ti < TI; ++ti) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = ib * BI + wi + 32 * ti + 8 * g + 4 * hh;
+        if (i < K)
+          store4(P.dw, (size_t)o * K + i, f32, acc[to][ti][4 * g], acc[to][ti][4 * g + 1], acc[to][ti][4 * g + 2],
+                 acc[to][ti][4 * g + 3]);
+      }
+    }
+  }
   if (do_bias && hh == 0) {
-    const int o = ob * BO + wo + 32 * bt + r;
-    if (o < N) pbias[(size_t)s * N + o] = accb[0];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int o = ob * BO + wo + 32 * (bt + j) + r;
+      if (bt + j < TO && o < N) {
+        if (f32)
+          reinterpret_cast<float*>(P.db)[o] = accb[j][0];
+        else
+          reinterpret_cast<bf16*>(P.db)[o] = __float2bfloat16(accb[j][0]);
+      }
+    }
   }
 }
 
 // dW[o][i] = sum_s (fragment-order partial of (o, i) in split s), db[o] = sum_s pbias[s][o],
-// fixed order.  A thread owns (o, 4 consecutive i): one float4 per split (the 4 registers of
-// a lane's group), consecutive threads take consecutive o (= consecutive lanes: 16-B reads of
-// one 1-KB block).  A 256-thread block = 64 items x 4 split groups (g, g + 4, ...), the group
-// sums added in LDS in group order.
-template <typename T>
-__global__ void __launch_bounds__(256) token_wgrad_reduce_kernel(const float* __restrict__ part,
-                                                                 const float* __restrict__ pbias, T* __restrict__ dw,
-                                                                 T* __restrict__ db, int N, int K, int BO, int BI,
-                                                                 int S) {
+// fixed order, for the split Linears of a group.  A thread owns (o, 4 consecutive i): one
+// float4 per split (the 4 registers of a lane's group), consecutive threads take consecutive
+// o (= consecutive lanes: 16-B reads of one 1-KB block).  A 256-thread block = 64 items x 4
+// split groups (g, g + 4, ...), the group sums added in LDS in group order; a block's 64
+// items belong to one Linear (item0 is a multiple of 64).
+template <int BO, int BI, int WO, int WI>
+__global__ void __launch_bounds__(256) token_wgrad_reduce_kernel(const WgGroup grp, const float* __restrict__ part,
+                                                                 const float* __restrict__ pbias) {
+  constexpr int TO = BO / WO / 32, TI = BI / WI / 32;
   __shared__ float4 sp[4][64];
-  const int it = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const long long q = (long long)blockIdx.x * 64 + it;
-  const long long nq = (long long)N * (K / 4), nqb = db ? N / 4 : 0;
+  const int it = threadIdx.x & 63, gq = threadIdx.x >> 6;
+  const int item_blk = blockIdx.x * 64;
+  int pi = -1;
+  for (int k = 0; k < grp.n; ++k)
+    if (grp.p[k].S > 1 && item_blk >= grp.p[k].item0) pi = k;
+  if (pi < 0) return;
+  const WgProb& P = grp.p[pi];
+  const int N = P.N, K = P.K, S = P.S, tiles_i = P.tiles_i, tiles = P.tiles;
+  const long long q = (long long)item_blk - P.item0 + it;
+  const long long nq = (long long)N * (K / 4), nqb = P.db ? N / 4 : 0;
   const bool isw = q < nq, isb = !isw && q - nq < nqb;
-  const int WO = BI == 128 ? 4 : 2, TO = BO / WO / 32;
-  const int tiles_i = (K + BI - 1) / BI, tiles = ((N + BO - 1) / BO) * tiles_i;
   const long long tstride = (long long)tiles * BO * BI;          // floats per split
-  const float* src = part;
+  const float* src = part + P.part0;
   long long stride = tstride;
   int o = 0, i = 0;
   if (isw) {
     o = (int)(q % N);
     i = (int)(q / N) * 4;
     const int ob = o / BO, ib = i / BI, oo = o - ob * BO, ii = i - ib * BI;
-    const int qo = oo / (BO / WO), qi = ii >> 6, to = (oo % (BO / WO)) >> 5, r = oo & 31;
-    const int ti = (ii & 63) >> 5, row = ii & 31;                // row % 4 == 0: registers 4g..4g+3
+    const int qo = oo / (BO / WO), qi = ii / (BI / WI), to = (oo % (BO / WO)) >> 5, r = oo & 31;
+    const int ti = (ii % (BI / WI)) >> 5, row = ii & 31;        // row % 4 == 0: registers 4g..4g+3
     const int g = row >> 3, hh = (row >> 2) & 1;
     const int w = qi * WO + qo;
-    src = part + (long long)(ob * tiles_i + ib) * BO * BI + (long long)w * (TO * 2 * 1024) +
-          ((to * 2 + ti) * 4 + g) * 256 + (hh * 32 + r) * 4;
+    src += (long long)(ob * tiles_i + ib) * BO * BI + (long long)w * (TO * TI * 1024) + ((to * TI + ti) * 4 + g) * 256 +
+           (hh * 32 + r) * 4;
   } else if (isb) {
-    src = pbias + 4 * (q - nq);
+    src = pbias + P.pb0 + 4 * (q - nq);
     stride = N;
   }
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (isw || isb) {
-    int s = grp;
+    int s = gq;
     for (; s + 12 < S; s += 16) {
       const float4 v0 = *reinterpret_cast<const float4*>(src + s * stride);
       const float4 v1 = *reinterpret_cast<const float4*>(src + (s + 4) * stride);
@@ -247,63 +363,143 @@ __global__ void __launch_bounds__(256) token_wgrad_reduce_kernel(const float* __
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
   }
-  sp[grp][it] = a;
+  sp[gq][it] = a;
   __syncthreads();
-  if (grp == 0 && (isw || isb)) {
+  if (gq == 0 && (isw || isb)) {
     const float4 b = sp[1][it], c = sp[2][it], d = sp[3][it];
     const float r0 = ((a.x + b.x) + c.x) + d.x, r1 = ((a.y + b.y) + c.y) + d.y;
     const float r2 = ((a.z + b.z) + c.z) + d.z, r3 = ((a.w + b.w) + c.w) + d.w;
-    T* out = isw ? dw + (size_t)o * K + i : db + 4 * (q - nq);
-    out[0] = from_f32<T>(r0);
-    out[1] = from_f32<T>(r1);
-    out[2] = from_f32<T>(r2);
-    out[3] = from_f32<T>(r3);
+    if (isw)
+      store4(P.dw, (size_t)o * K + i, grp.f32 != 0, r0, r1, r2, r3);
+    else
+      store4(P.db, (size_t)(4 * (q - nq)), grp.f32 != 0, r0, r1, r2, r3);
   }
 }
 
-int wgrad_bo(int N) { return N > 128 ? 256 : 128; }
-
-// VS_WGRAD_CFG: 0 (default) -> 64-token chunks; 1 -> 32-token chunks, twice the ring depth
-// (same LDS): 0.737 vs 0.786 ms over the C2 shapes (profiles/r5_token_wgrad_ab.txt)
-int wgrad_cfg() {
-  static const int c = [] {
-    const char* e = getenv("VS_WGRAD_CFG");
-    return e ? atoi(e) : 0;
-  }();
-  return c;
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
 
-// 256 input columns per workgroup (half the L2 -> LDS bytes per flop of 256 x 128) where the
-// input is wide enough; VS_WGRAD_BI=128 forces the narrow tile
-int wgrad_bi(int N, int K) {
-  static const int force = [] {
-    const char* e = getenv("VS_WGRAD_BI");
-    return e ? atoi(e) : 0;
-  }();
-  if (force) return force;
-  // measured: no gain from the 256-wide tile at the C2 shapes (the LDS-DMA issue rate, not
-  // the L2 -> LDS bytes per flop, bounds the chunk loop: profiles/r5_token_wgrad_pmc.txt)
-  (void)N;
+// Plan one launch: the Linears share BO.  Every workgroup gets about the same number of
+// chunks C: C = max(8, total chunk-tiles / 256) (one workgroup per CU with 144 KB of LDS);
+// a Linear is split into ceil(nchunk / C) token ranges.  Returns the workgroup count and the
+// partial floats / reduction items it needs.
+struct Plan {
+  WgGroup g;
+  long long wgs, tile_floats, part_floats, items;   // part_floats = tile partials + bias partials
+};
+
+void plan_group(const vs_wgrad_problem* probs, const int* idx, int n, int BO, int BI, int f32, Plan& pl) {
+  static const int target = env_int("VS_WGRAD_WGS", 256);
+  static const int minc = env_int("VS_WGRAD_MIN_CHUNKS", 8);
+  long long total = 0;
+  for (int k = 0; k < n; ++k) {
+    const vs_wgrad_problem& q = probs[idx[k]];
+    const long long tiles = (long long)((q.N + BO - 1) / BO) * ((q.K + BI - 1) / BI);
+    total += tiles * ((q.tokens + kTK - 1) / kTK);
+  }
+  // the smallest C whose workgroups fit one round (ceil per Linear can push past the target:
+  // a second, mostly idle round of workgroups)
+  auto wgs_for = [&](long long c) {
+    long long w = 0;
+    for (int k = 0; k < n; ++k) {
+      const vs_wgrad_problem& q = probs[idx[k]];
+      const long long tiles = (long long)((q.N + BO - 1) / BO) * ((q.K + BI - 1) / BI);
+      w += tiles * (((q.tokens + kTK - 1) / kTK + c - 1) / c);
+    }
+    return w;
+  };
+  long long C = (total + target - 1) / target;
+  if (C < minc) C = minc;
+  long long cmax = 1;
+  for (int k = 0; k < n; ++k) {
+    const long long nc = (probs[idx[k]].tokens + kTK - 1) / kTK;
+    if (nc > cmax) cmax = nc;
+  }
+  while (wgs_for(C) > target && C < cmax) ++C;
+  pl.g.n = n;
+  pl.g.f32 = f32;
+  pl.wgs = pl.tile_floats = pl.part_floats = pl.items = 0;
+  long long pbf = 0;
+  for (int k = 0; k < n; ++k) {
+    const vs_wgrad_problem& q = probs[idx[k]];
+    WgProb& P = pl.g.p[k];
+    P.gy = (const bf16*)q.grad_y;
+    P.x = (const bf16*)q.x;
+    P.dw = q.dw;
+    P.db = q.db;
+    P.ldg = q.ld_grad_y;
+    P.ldx = q.ld_x;
+    P.T = (int)q.tokens;
+    P.N = q.N;
+    P.K = q.K;
+    P.tiles_i = (q.K + BI - 1) / BI;
+    P.tiles = ((q.N + BO - 1) / BO) * P.tiles_i;
+    const long long nchunk = (q.tokens + kTK - 1) / kTK;
+    long long S = (nchunk + C - 1) / C;
+    if (S < 1) S = 1;
+    P.S = (int)S;
+    P.wg0 = (int)pl.wgs;
+    pl.wgs += S * P.tiles;
+    P.part0 = P.pb0 = 0;
+    P.item0 = 0;
+    if (S > 1) {
+      P.part0 = pl.part_floats;
+      pl.part_floats += S * P.tiles * BO * BI;
+      P.item0 = (int)pl.items;
+      const long long items = (long long)q.N * (q.K / 4) + (q.db ? q.N / 4 : 0);
+      pl.items += (items + 63) / 64 * 64;
+      if (q.db) pbf += S * q.N;
+    }
+  }
+  // bias partials after all tile partials (pb0 relative to the bias region)
+  pl.tile_floats = pl.part_floats;
+  long long off = 0;
+  for (int k = 0; k < n; ++k) {
+    WgProb& P = pl.g.p[k];
+    if (P.S > 1 && P.db) {
+      P.pb0 = off;
+      off += (long long)P.S * P.N;
+    }
+  }
+  pl.part_floats += pbf;
+}
+
+// tile configurations: 0 = 256 x 128 (8 waves), 1 = 128 x 128 (8 waves, N <= 128).  (A
+// 256 x 256 tile of 4 waves -- 128 x 128 per wave, half the operand reads per MFMA -- needs
+// 256 accumulators per lane and spilled: not built.)
+int wgrad_cfg_of(int N, int K) {
   (void)K;
-  return 128;
+  return N <= 128 ? 1 : 0;
 }
 
-int wgrad_tok() { return wgrad_cfg() == 0 ? 64 : 32; }
-
-int wgrad_splits(long long T, int N, int K) {
-  const int BO = wgrad_bo(N), BI = wgrad_bi(N, K);
-  const long long tiles = (long long)((N + BO - 1) / BO) * ((K + BI - 1) / BI);
-  const long long nchunk = (T + wgrad_tok() - 1) / wgrad_tok();
-  static const int target = [] {
-    const char* e = getenv("VS_WGRAD_WGS");
-    return e ? atoi(e) : 256;
-  }();
-  long long S = target / tiles;                        // ~one workgroup per CU (>= 128 KB of LDS)
-  // at least 8 chunks a split: the per-split f32 partial block costs about as much traffic
-  // as a few chunks of the operands
-  if (S > nchunk / 8) S = nchunk / 8;
-  if (S < 1) S = 1;
-  return (int)S;
+// the launches of a call: problems grouped by tile configuration, in chunks of kMaxProbs
+template <typename F>
+int for_each_launch(const vs_wgrad_problem* probs, int n, int f32, F&& fn) {
+  for (int cfg : {0, 1}) {
+    const int BO = cfg == 1 ? 128 : 256, BI = 128;
+    int idx[kMaxProbs];
+    int m = 0;
+    for (int k = 0; k < n; ++k) {
+      if (wgrad_cfg_of(probs[k].N, probs[k].K) != cfg) continue;
+      idx[m++] = k;
+      if (m == kMaxProbs) {
+        Plan pl;
+        plan_group(probs, idx, m, BO, BI, f32, pl);
+        const int rc = fn(cfg, pl);
+        if (rc != VS_OK) return rc;
+        m = 0;
+      }
+    }
+    if (m) {
+      Plan pl;
+      plan_group(probs, idx, m, BO, BI, f32, pl);
+      const int rc = fn(cfg, pl);
+      if (rc != VS_OK) return rc;
+    }
+  }
+  return VS_OK;
 }
 
 }  // namespace
@@ -311,80 +507,86 @@ int wgrad_splits(long long T, int N, int K) {
 
 using namespace vs;
 
+static int check_problems(const vs_wgrad_problem* probs, int n) {
+  VS_CHECK(probs && n >= 0, "null problem list");
+  for (int k = 0; k < n; ++k) {
+    const vs_wgrad_problem& q = probs[k];
+    VS_CHECK(q.grad_y && q.x && q.dw, "null pointer");
+    VS_CHECK(q.tokens > 0 && q.tokens < (1ll << 31) && q.N > 0 && q.K > 0 && q.N % 8 == 0 && q.K % 8 == 0,
+             "0 < tokens < 2^31, N % 8 == 0, K % 8 == 0");
+    VS_CHECK(q.ld_grad_y >= q.N && q.ld_x >= q.K && q.ld_grad_y % 8 == 0 && q.ld_x % 8 == 0,
+             "row strides: >= width, % 8 == 0");
+    VS_CHECK(64 * (q.ld_grad_y > q.ld_x ? q.ld_grad_y : q.ld_x) < (1ll << 31), "row strides too large");
+    VS_CHECK(((uintptr_t)q.grad_y & 15) == 0 && ((uintptr_t)q.x & 15) == 0, "grad_y / x must be 16-B aligned");
+    VS_CHECK(((uintptr_t)q.dw & 15) == 0 && (!q.db || ((uintptr_t)q.db & 15) == 0), "dw / db must be 16-B aligned");
+  }
+  return VS_OK;
+}
+
+extern "C" long long vs_token_wgrad_grouped_workspace_bytes(const vs_wgrad_problem* probs, int n) {
+  if (!probs || n <= 0) return 0;
+  long long mx = 0;
+  for_each_launch(probs, n, 1, [&](int, const Plan& pl) {
+    if (pl.part_floats > mx) mx = pl.part_floats;
+    return VS_OK;
+  });
+  return mx * 4 + 256;
+}
+
+extern "C" int vs_token_wgrad_grouped(int dtype, const vs_wgrad_problem* probs, int n, void* workspace,
+                                      void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype (of dw / db) must be VS_F32 or VS_BF16");
+  const int rc = check_problems(probs, n);
+  if (rc != VS_OK) return rc;
+  if (n == 0) return VS_OK;
+  const long long need = vs_token_wgrad_grouped_workspace_bytes(probs, n);
+  VS_CHECK(need <= 256 || (workspace && ((uintptr_t)workspace & 15) == 0), "workspace: 16-B aligned, sized by "
+           "vs_token_wgrad_grouped_workspace_bytes");
+  hipStream_t st = (hipStream_t)stream;
+  static const int dbg = env_int("VS_WGRAD_DEBUG", 0);
+  // VS_WGRAD_SPREAD=1: the next chunk's DMA pieces issued between the MFMA steps instead of
+  // all after the barrier
+  static const int spread = env_int("VS_WGRAD_SPREAD", 1);
+  return for_each_launch(probs, n, dtype == VS_F32, [&](int cfg, const Plan& pl) -> int {
+    VS_CHECK(pl.wgs > 0 && pl.wgs < (1ll << 31), "bad workgroup count");
+    float* part = (float*)workspace;
+    float* pb = part ? part + pl.tile_floats : nullptr;
+    const dim3 g((unsigned)pl.wgs);
+    if (cfg == 0) {
+      if (dbg == 1)
+        hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 4, 2, 3, 1>), g, dim3(512), 0, st, pl.g, part, pb, spread);
+      else if (dbg == 2)
+        hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 4, 2, 3, 2>), g, dim3(512), 0, st, pl.g, part, pb, spread);
+      else if (dbg == 4)
+        hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 4, 2, 3, 4>), g, dim3(512), 0, st, pl.g, part, pb, spread);
+      else
+        hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 4, 2, 3>), g, dim3(512), 0, st, pl.g, part, pb, spread);
+    } else {
+      hipLaunchKernelGGL((token_wgrad_kernel<128, 128, 4, 2, 4>), g, dim3(512), 0, st, pl.g, part, pb, spread);
+    }
+    VS_LAUNCH_CHECK();
+    if (pl.items > 0) {
+      const dim3 gr((unsigned)(pl.items / 64));
+      if (cfg == 0)
+        hipLaunchKernelGGL((token_wgrad_reduce_kernel<256, 128, 4, 2>), gr, dim3(256), 0, st, pl.g,
+                           (const float*)part, (const float*)pb);
+      else
+        hipLaunchKernelGGL((token_wgrad_reduce_kernel<128, 128, 4, 2>), gr, dim3(256), 0, st, pl.g,
+                           (const float*)part, (const float*)pb);
+      VS_LAUNCH_CHECK();
+    }
+    return VS_OK;
+  });
+}
+
 extern "C" long long vs_token_wgrad_workspace_bytes(long long tokens, int N, int K) {
   if (tokens <= 0 || N <= 0 || K <= 0) return 0;
-  const long long S = wgrad_splits(tokens, N, K);
-  const int BO = wgrad_bo(N), BI = wgrad_bi(N, K);
-  const long long padded = (long long)((N + BO - 1) / BO) * BO * (((K + BI - 1) / BI) * BI);
-  return S * (padded + N) * 4;
+  vs_wgrad_problem q = {nullptr, nullptr, nullptr, (void*)1, N, K, tokens, N, K};
+  return vs_token_wgrad_grouped_workspace_bytes(&q, 1);
 }
 
 extern "C" int vs_token_wgrad(int dtype, const void* grad_y, long long ld_grad_y, const void* x, long long ld_x,
                               void* dw, void* db, void* workspace, long long tokens, int N, int K, void* stream) {
-  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype (of dw / db) must be VS_F32 or VS_BF16");
-  VS_CHECK(grad_y && x && dw && workspace, "null pointer");
-  VS_CHECK(tokens > 0 && tokens < (1ll << 31) && N > 0 && K > 0 && N % 8 == 0 && K % 8 == 0,
-           "0 < tokens < 2^31, N % 8 == 0, K % 8 == 0");
-  VS_CHECK(ld_grad_y >= N && ld_x >= K && ld_grad_y % 8 == 0 && ld_x % 8 == 0, "row strides: >= width, % 8 == 0");
-  VS_CHECK(64 * (ld_grad_y > ld_x ? ld_grad_y : ld_x) < (1ll << 31), "row strides too large");
-  VS_CHECK(((uintptr_t)grad_y & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)workspace & 15) == 0,
-           "grad_y / x / workspace must be 16-B aligned");
-  const int S = wgrad_splits(tokens, N, K);
-  const int BO = wgrad_bo(N), BI = wgrad_bi(N, K);
-  const long long tiles = (long long)((N + BO - 1) / BO) * ((K + BI - 1) / BI);
-  VS_CHECK(S * tiles < (1ll << 31), "too many workgroups");
-  float* part = (float*)workspace;
-  float* pb = db ? part + (size_t)S * tiles * BO * BI : nullptr;
-  hipStream_t st = (hipStream_t)stream;
-  const dim3 g((unsigned)(S * tiles));
-#define VS_TW(BO_, BI_, NS_, TK_)                                                                                  \
-  hipLaunchKernelGGL((token_wgrad_kernel<BO_, BI_, NS_, TK_>), g, dim3(512), 0, st, (const bf16*)grad_y,           \
-                     (const bf16*)x, part, pb, (int)tokens, N, K, ld_grad_y, ld_x, S)
-  const bool t64 = wgrad_cfg() == 0;
-  if (BI == 256) {
-    if (BO == 256) {
-      if (t64) VS_TW(256, 256, 2, 64); else VS_TW(256, 256, 4, 32);
-    } else {
-      if (t64) VS_TW(128, 256, 3, 64); else VS_TW(128, 256, 6, 32);
-    }
-  } else {
-    if (BO == 256) {
-      if (t64) {
-        static const int dbg = [] {
-          const char* e = getenv("VS_WGRAD_DEBUG");
-          return e ? atoi(e) : 0;
-        }();
-        if (dbg == 1)
-          hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 3, 64, 1>), g, dim3(512), 0, st, (const bf16*)grad_y,
-                             (const bf16*)x, part, pb, (int)tokens, N, K, ld_grad_y, ld_x, S);
-        else if (dbg == 2)
-          hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 3, 64, 2>), g, dim3(512), 0, st, (const bf16*)grad_y,
-                             (const bf16*)x, part, pb, (int)tokens, N, K, ld_grad_y, ld_x, S);
-        else if (dbg == 3)
-          hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 3, 64, 3>), g, dim3(512), 0, st, (const bf16*)grad_y,
-                             (const bf16*)x, part, pb, (int)tokens, N, K, ld_grad_y, ld_x, S);
-        else if (dbg == 4)
-          hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 3, 64, 4>), g, dim3(512), 0, st, (const bf16*)grad_y,
-                             (const bf16*)x, part, pb, (int)tokens, N, K, ld_grad_y, ld_x, S);
-        else
-          VS_TW(256, 128, 3, 64);
-      } else {
-        VS_TW(256, 128, 6, 32);
-      }
-    } else {
-      if (t64) VS_TW(128, 128, 4, 64); else VS_TW(128, 128, 8, 32);
-    }
-  }
-#undef VS_TW
-  VS_LAUNCH_CHECK();
-  const long long items = (long long)N * (K / 4) + (db ? N / 4 : 0);
-  const dim3 gr((unsigned)((items + 63) / 64));
-  if (dtype == VS_BF16)
-    hipLaunchKernelGGL(token_wgrad_reduce_kernel<bf16>, gr, dim3(256), 0, st, part, pb, (bf16*)dw, (bf16*)db, N, K,
-                       BO, BI, S);
-  else
-    hipLaunchKernelGGL(token_wgrad_reduce_kernel<float>, gr, dim3(256), 0, st, part, pb, (float*)dw, (float*)db, N, K,
-                       BO, BI, S);
-  VS_LAUNCH_CHECK();
-  return VS_OK;
+  vs_wgrad_problem q = {grad_y, x, dw, db, ld_grad_y, ld_x, tokens, N, K};
+  return vs_token_wgrad_grouped(dtype, &q, 1, workspace, stream);
 }

@@ -116,6 +116,8 @@ SIGNATURES = {
     "vs_upsample_add_forward_nhwc": [_c_int, _P, _P, _P] + [_c_int] * 6 + [ctypes.c_longlong, _P],
     "vs_upsample_backward_nhwc": [_c_int, _P, _P] + [_c_int] * 6 + [_P],
     "vs_token_wgrad_workspace_bytes": [ctypes.c_longlong, _c_int, _c_int],
+    "vs_token_wgrad_grouped_workspace_bytes": [_P, _c_int],
+    "vs_token_wgrad_grouped": [_c_int, _P, _c_int, _P, _P],
     "vs_token_wgrad": [_c_int, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P, _P, _P, ctypes.c_longlong, _c_int,
                        _c_int, _P],
     "vs_conv3x3_forward": [_P, _P, _P, _P] + [_c_int] * 5 + [_P],
@@ -135,7 +137,8 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_msda_backward_workspace_bytes": ctypes.c_longlong,
             "vs_match_cost_factors_workspace_bytes": ctypes.c_longlong,
             "vs_conv3x3_wgrad_workspace_bytes": ctypes.c_longlong,
-            "vs_token_wgrad_workspace_bytes": ctypes.c_longlong}
+            "vs_token_wgrad_workspace_bytes": ctypes.c_longlong,
+            "vs_token_wgrad_grouped_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
 _tops = None

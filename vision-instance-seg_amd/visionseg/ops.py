@@ -1676,6 +1676,41 @@ def token_wgrad(gy, x, out_dtype, bias: bool = False, out=None, bias_out=None):
     return (out, db) if bias else out
 
 
+class WgradProblem(ctypes.Structure):
+    """vs_wgrad_problem (include/visionseg.h)."""
+    _fields_ = [("grad_y", ctypes.c_void_p), ("x", ctypes.c_void_p), ("dw", ctypes.c_void_p),
+                ("db", ctypes.c_void_p), ("ld_grad_y", ctypes.c_longlong), ("ld_x", ctypes.c_longlong),
+                ("tokens", ctypes.c_longlong), ("N", ctypes.c_int), ("K", ctypes.c_int)]
+
+
+def token_wgrad_grouped(items, out_dtype):
+    """Several independent token-Linear weight gradients in one launch (+ one reduction launch
+    when some are split): items = [(gy [T, N], x [T, K], dw [N, K], db [N] or None)], gy / x bf16
+    with unit column stride, dw / db contiguous of out_dtype, all written
+    (vs_token_wgrad_grouped)."""
+    if not items:
+        return
+    L.require_hip(items[0][0])
+    n = len(items)
+    arr = (WgradProblem * n)()
+    flops = 0.0
+    for k, (gy, x, dw, db) in enumerate(items):
+        # dw / db: tensors, or raw device addresses (linear._DeferredWgrads holds no tensor
+        # reference to them, so that autograd adopts them as .grad without a copy)
+        pw = dw.data_ptr() if torch.is_tensor(dw) else int(dw)
+        pb = (db.data_ptr() if torch.is_tensor(db) else int(db)) if db is not None else None
+        arr[k] = WgradProblem(gy.data_ptr(), x.data_ptr(), pw, pb, gy.stride(0), x.stride(0), gy.shape[0],
+                              gy.shape[1], x.shape[1])
+        flops += 2.0 * gy.shape[0] * gy.shape[1] * x.shape[1]
+    gy0 = items[0][0]
+    nb = int(L.lib().vs_token_wgrad_grouped_workspace_bytes(arr, n))
+    ws = torch.empty(max(nb, 16), device=gy0.device, dtype=torch.uint8)
+    code = L.dtype_code(torch.empty(0, dtype=out_dtype))
+    with timed("token_wgrad", gy0, flops=flops, bytes_=sum(it[0].shape[0] * (it[0].shape[1] + it[1].shape[1]) * 2
+                                                           for it in items)):
+        L.check(L.lib().vs_token_wgrad_grouped(code, arr, n, L.ptr(ws), L.stream(gy0)), "token_wgrad_grouped")
+
+
 # ------------------------------------------------------------------ 3 x 3 conv (channels-last)
 def conv3x3_nhwc_ok(x, weight) -> bool:
     """Shapes / dtypes csrc/conv3x3.hip covers: bf16 device tensors, a [Co, Ci, 3, 3] weight
