@@ -115,7 +115,12 @@ OP_KERNELS = {   # op -> kernel-name substrings (template arguments included) wh
     "window_attn_bwd_fp8": [f"win_attn_bwd_fa<{n}, true>" for n in (2, 3, 4, 5)],
     "mask_head_fwd": ["mask_head_fwd_bf16_kernel<"],
     "mask_head_bwd": ["mask_head_bwd_kernel<"],
+    # one token_wgrad call = the weight-gradient kernel + (when split) its reduction
+    "token_wgrad": ["token_wgrad_kernel<", "token_wgrad_reduce_kernel<"],
 }
+# ops whose one launch dispatches one kernel of EACH pattern (traffic summed over the
+# patterns, per dispatch of the first) instead of one kernel of any of them
+OP_MULTI = {"token_wgrad"}
 
 
 def pmc_traffic(op, path):
@@ -128,7 +133,11 @@ def pmc_traffic(op, path):
     hits = [(k, v) for k, v in rows.items() if any(p in k for p in OP_KERNELS[op])]
     if not hits:
         return None, None
-    n = sum(v["dispatches"] for _, v in hits)
+    if op in OP_MULTI:
+        first = [v for k, v in hits if OP_KERNELS[op][0] in k]
+        n = sum(v["dispatches"] for v in first)
+    else:
+        n = sum(v["dispatches"] for _, v in hits)
     tot = sum((v["fetch_bytes"] + v["write_bytes"]) * v["dispatches"] for _, v in hits) / max(1, n)
     return int(tot), sorted({p for p in OP_KERNELS[op] for k, _ in hits if p in k})
 
@@ -156,6 +165,8 @@ def kernel_roofline(summary, pmc_path):
         traffic, kernels = pmc_traffic(name, pmc_path)
         roof = dict(bound="mfma", achieved=round(ach, 2), peak=MFMA_BF16_PEAK_TFS, unit="TFLOP/s",
                     frac=round(ach / MFMA_BF16_PEAK_TFS, 5), traffic=traffic, kernel=name,
+                    traffic_source=(f"profiles/{os.path.basename(pmc_path)}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) "
+                                    f"+ WRITE_SIZE per launch of {kernels}") if traffic else None,
                     algorithmic_flops_per_launch=int(s["flops"]), mean_launch_ms=round(s["mean_ms"], 4),
                     launches=s["launches"])
     table = {k: dict(launches=v["launches"], total_ms=round(v["total_ms"], 3), mean_ms=round(v["mean_ms"], 4),
