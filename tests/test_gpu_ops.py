@@ -821,6 +821,45 @@ def test_window_attention_bf16_large_windows_vs_oracle(ws, shift, heads, nWh, nW
     assert e <= 2e-2 * float(tr.grad.abs().max()), e
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("ws,shift,heads,nWh,nWw,amp", [(12, 6, 4, 3, 3, 1.0), (7, 3, 3, 4, 4, 1.0), (12, 0, 2, 2, 2, 12.0),
+                                                        (10, 5, 3, 3, 2, 1.0), (12, 6, 6, 4, 4, 0.0)])
+def test_window_attention_bwd_fixed_point_bins_equal_f32_bins(monkeypatch, fp8, ws, shift, heads, nWh, nWw, amp):
+    """The round-5 backward (win_attn_bwd_fb: natural-layout staging + transposed LDS reads,
+    the bias gradient in fixed-point integer bins) against the round-4 one (f32 bins): the
+    q / k / v gradients are the same products in the same order (bit-equal), the table
+    gradient agrees to the fixed-point quantum.  amp scales q / k (peaked softmax, large dS)
+    and 0 makes V and the gradient all-zero rows (the bound is 0)."""
+    ops = _ops()
+    if fp8 and ws * ws > 160:
+        pytest.skip("fp8 path: N <= 160")
+    B = 2
+    Bw, N, C = B * nWh * nWw, ws * ws, heads * 32
+    g = torch.Generator().manual_seed(ws * 7 + heads)
+    qkv = torch.randn(Bw, N, 3, C, generator=g)
+    qkv[:, :, :2] *= max(amp, 1.0)
+    if amp == 0.0:
+        qkv[:, :, 2] = 0
+    qkv = qkv.view(Bw, N, 3 * C).to(torch.bfloat16)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g)
+    go = torch.randn(Bw, N, C, generator=g).to(torch.bfloat16)
+    if amp == 0.0:
+        go.zero_()
+    res = []
+    for fb in ("0", "2"):                     # 2: the round-5 kernel for every N and fp8 too
+        monkeypatch.setenv("VS_WIN_BWD_FB", fb)
+        qd, td = qkv.to(DEV).requires_grad_(True), table.to(DEV).requires_grad_(True)
+        out = ops.window_attention(qd, td, heads, ws, shift, nWh, nWw, fp8=fp8)
+        out.backward(go.to(DEV))
+        torch.cuda.synchronize()
+        res.append((qd.grad.float().cpu(), td.grad.double().cpu()))
+    (gq0, gt0), (gq1, gt1) = res
+    assert torch.equal(gq0, gq1), float((gq0 - gq1).abs().max())
+    assert bool(torch.isfinite(gt1).all())
+    e = float((gt0 - gt1).abs().max())
+    assert e <= 1e-5 * max(float(gt0.abs().max()), 1e-30), (e, float(gt0.abs().max()))
+
+
 @pytest.mark.parametrize("kernel", ["mfma", "mfma-4blk", "scalar"])
 @pytest.mark.parametrize("B,Q,S", [(2, 100, 4096), (1, 100, 1000), (2, 7, 300), (1, 128, 16384), (1, 130, 512)])
 def test_masked_attention_bf16_fwd_bwd_vs_oracle(monkeypatch, kernel, B, Q, S):

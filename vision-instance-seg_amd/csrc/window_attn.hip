@@ -1102,7 +1102,9 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(ON
 //     in the permuted query order).
 // S and dP are formed twice (the MFMA units idle in this kernel); LDS peaks at ~47 KB for
 // N = 144 (3 workgroups/CU).  F8: the logits on the forward's fp8 operands and scales.
-template <int NT, bool F8>
+// DBG (timing-split instances, VS_WIN_BWD_VAR): 1 no bias binning, 2 no phase 2, 4 no phase-1
+// tile loop, 8 no bias gather in the logits
+template <int NT, bool F8, int DBG = 0>
 __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_attn_bwd_fa(
     const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
     const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
@@ -1213,7 +1215,7 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
   float* bins = sBins + qt * kBinW + (kHalfBins ? hh * kT2 : 0);
   f32x16_t dq;
   zero16(dq);
-  for (int kt = 0; kt < NT; ++kt) {
+  for (int kt = 0; kt < ((DBG & 4) ? 0 : NT); ++kt) {
     f32x16_t s, dp;
     zero16(s);
     zero16(dp);
@@ -1226,7 +1228,11 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
       dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sVn + o), db[st], dp);
     }
     int rel[16];
-    logits_kq(s, gl, scale2, sTok, bias, kt, q, hh, rel);
+    if (DBG & 8) {
+      for (int i = 0; i < 16; ++i) { s[i] *= scale2; rel[i] = 16 * kt + i; }
+    } else {
+      logits_kq(s, gl, scale2, sTok, bias, kt, q, hh, rel);
+    }
     if (mixed) mask_kq(s, sTok, kt, q, hh);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -1245,7 +1251,8 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
     // query lanes index the zone below the table and are masked off; a padded key row
     // (dS = 0 on every lane: P = exp2(-inf)) indexes the zone above it and is clamped onto
     // the last bin, where its whole instruction adds zero
-    if (kHalfBins) {
+    if (DBG & 1) {
+    } else if (kHalfBins) {
       // one lane half, one register: 32 queries x one key = 32 distinct bins; LDS accesses
       // of a wave stay in program order, so the registers' read-modify-writes chain safely
       if (q < N) {
@@ -1286,6 +1293,7 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
       gp[t] = a;
     }
   }
+  if (DBG & 2) return;
   __syncthreads();
   // ---- phase 2 staging: Q, dO natural; Q^T, dO^T
   load_p2();
@@ -1322,7 +1330,11 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
       s = mfma16(*reinterpret_cast<const bf16x8_t*>(sQn + o), ks8[st], s);
       dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sDn + o), vb[st], dp);
     }
-    logits_qk(s, gl, scale2, mixed, sTok, bias, qq, key, hh);
+    if (DBG & 8) {
+      for (int i = 0; i < 16; ++i) s[i] *= scale2;
+    } else {
+      logits_qk(s, gl, scale2, mixed, sTok, bias, qq, key, hh);
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qi = 32 * qq + crow(i, hh);
@@ -1346,6 +1358,359 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
       for (int e = 0; e < 4; ++e) {
         a[e] = bf16_bits(dk[4 * grp + e] * g.scale);
         b[e] = bf16_bits(dv[4 * grp + e]);
+      }
+      *reinterpret_cast<bf16x4_t*>(dst + C + 8 * grp + 4 * hh) = a;
+      *reinterpret_cast<bf16x4_t*>(dst + 2 * C + 8 * grp + 4 * hh) = b;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Backward, round 5 (win_attn_bwd_fb): the same two phases as win_attn_bwd_fa with
+//  * every operand staged ONCE in its natural [token][32] layout with 64-B rows, the 16-B
+//    chunks XOR-swizzled by (token >> 2) & 3 (a row-major 16-lane read of one chunk column
+//    and a 4-row ds_read_b64_tr_b16 read both cover all 64 banks): the transposed operands
+//    (K^T for dQ, dO^T for dV, Q^T for dK) come from the transposed LDS read in the permuted
+//    key / query order, so no [channel][token] copy is written (the fa kernel wrote it with
+//    16 two-byte stores per chunk, a third of its LDS cycles were bank conflicts);
+//  * the relative-position bias gradient accumulated as FIXED-POINT integers with no-return
+//    ds_add_u32 into the wave's bins (integer LDS atomics run at ~12 lane-ops/clk/CU on
+//    gfx950, f32 ones at 0.33; tools/micro/lds_atomic_bench.hip).  No lane halves taking
+//    turns, no read-modify-write chains.  The wave's quantum is a power of two set from a
+//    bound on what any of its bins can reach:
+//      |dS_qk| = P_qk |dP_qk - D_q| <= P_qk (|dO_q| |V_k| + |dO_q| |O_q|) <= 2 P_qk |dO_q| Vmax
+//    (|O_q| <= Vmax: O_q is a convex combination of V rows); a bin takes one key per query,
+//    so |bin| <= 2 Vmax sum_{q of the wave} |dO_q| =: B, and the quantum 2^(e - 31) with
+//    B < 2^e / 1.02 keeps every partial sum inside int32 (the 2 % covers the rounding of the
+//    <= 160 terms).  Each term is rounded once, to 2^-32 B: the bins agree with f32 sums to
+//    a few 1e-6 of the gradient's range (tests/test_gpu_ops.py).
+__device__ __forceinline__ int swz64(int t, int c) { return 32 * t + 8 * (c ^ ((t >> 2) & 3)); }
+
+// MFMA operand in the permuted token order (k = 8hh + j <-> token base + (j&3) + 8(j>>2) + 4hh,
+// m = channel lane & 31) from a swizzled [token][32] image: two transposed reads
+typedef short bf16x4tr_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8_t tr_perm64(const short* img, int base, int lane) {
+  typedef __attribute__((address_space(3))) bf16x4tr_t lds_v4;
+  const int hh = lane >> 5, e = (lane & 15) >> 2;
+  const int col = (lane & 16) + 4 * (lane & 3);
+  const int t0 = base + 4 * hh + e, t1 = t0 + 8;
+  const bf16x4tr_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + 32 * t0 + 8 * ((col >> 3) ^ ((t0 >> 2) & 3)) + (col & 7)));
+  const bf16x4tr_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + 32 * t1 + 8 * ((col >> 3) ^ ((t1 >> 2) & 3)) + (col & 7)));
+  bf16x8_t v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+__device__ __forceinline__ float sumsq8(bf16x8_t c) {
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = bf16_bits_to_f32((unsigned short)c[j]);
+    a = fmaf(x, x, a);
+  }
+  return a;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// round half up to an integer (one instruction; __float2int_rn is two)
+__device__ __forceinline__ int cvt_rpi(float x) {
+  int r;
+  asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// Per-logit work of the fb kernel, in VALU terms (the fa kernel spent ~290 VALU per 32x32
+// tile of phase 1, the tile's 6 MFMAs ~190 cycles):
+//  * the token metadata hold 4 kk (a byte offset) in the high half, so one subtract gives
+//    the bias AND the bin byte offset; the bias table sits at a compile-time LDS address
+//    (zone size fixed per NT), folded into the ds_read offset;
+//  * dS is formed already scaled by the bins' inverse quantum 2^(31-e): the same products
+//    (p (dp - D) scaled by a power of two is exact), so it feeds both the dQ MFMA (dQ is
+//    scaled back at the store, exactly) and v_cvt_rpi_i32_f32 for the bin;
+//  * a padded query has lse = +inf (P = 0 with no select).
+//  * bias and bins are PITCHED: relative offset (dy, dx) at (dy + ws-1) P + dx + ws-1 with
+//    P = ws + 32 (P = ws mod 32, so a token's pitched position y P + x is its raster index t
+//    mod 32): the 32 lanes of a half-wave (32 consecutive query or key tokens) hit 32 distinct
+//    banks in every bias read and every bin atomic (with rows of 2 ws - 1 they collided up to
+//    3-way, ~40 % of the LDS-busy cycles were conflicts, profiles/r5_win_bwd_sq_c5.txt).
+//    Columns 2 ws - 1 .. P-1 of a row are -inf in the bias: a padded KEY sits at x = -ws, so
+//    every (real query, padded key) pair lands there (P = 0 with no zone rows);
+// Padded queries / keys (dS = 0) index bins outside the wave's [0, T2): the bins of the
+// neighbouring waves or the margins around them, where adding 0 changes nothing.
+// DBG (timing-split instances, VS_WIN_BWD_VAR with VS_WIN_BWD_FB=1): 1 no bins, 2 no phase 2,
+// 4 no phase-1 tile loop
+template <int NT, bool F8, int WPE = 4, int DBG = 0>
+__global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(WPE))) win_attn_bwd_fb(
+    const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
+    const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
+    float* __restrict__ gtable_part, WinGeom g) {
+  constexpr int NP = 32 * NT, kImg = NP * 32;
+  constexpr int kWs = NT <= 2 ? 8 : NT == 3 ? 9 : NT == 4 ? 11 : 12;           // ws_max
+  constexpr int kBinW = (2 * kWs - 1) * (kWs + 32);                           // pitched bins
+  constexpr int kZ = 16;                                                      // >= ws margin
+  // phase 1: K (raw, for K^T), V [, K through e4m3 for the logits]; phase 2: Q, dO [, Q e4m3]
+  __shared__ __attribute__((aligned(16))) short sU[(F8 ? 3 : 2) * kImg];
+  __shared__ float sBias[kBinW + kZ];
+  __shared__ int sBins[NT * kBinW + kZ];
+  __shared__ __attribute__((aligned(16))) int sTok[NP];
+  __shared__ float sL[NP], sD[NP];
+  __shared__ float sVmax[NT], sQuant[NT];
+  int bw, h;
+  win_block(g, bw, h);
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int N = g.N, C = g.heads * kD, C3 = 3 * C;
+  const bf16* win = qkv + (size_t)bw * N * C3 + h * kD;
+  const bf16* gwo = gout + h * kD;
+  const bf16* owin = out + h * kD;
+  bf16* gw = gqkv + (size_t)bw * N * C3 + h * kD;
+  const float* lrow = lse + ((size_t)bw * g.heads + h) * N;
+  const int qt = wv, kw = wv;
+  const int q = 32 * qt + r, key = 32 * kw + r;
+  bf16x8_t ck[2], cv[2], cq[2], cd[2];
+  auto load_p2 = [&]() {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+      cq[it] = t < N ? ld8(win + (size_t)t * C3 + 8 * c) : zero8();
+      const long long orow = t < N ? out_row(g, bw, t) : -1;
+      cd[it] = orow >= 0 ? ld8(gwo + orow * C + 8 * c) : zero8();
+    }
+  };
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    const bool in = t < N;
+    const bf16* row = win + (size_t)t * C3 + 8 * c;
+    ck[it] = in ? ld8(row + C) : zero8();
+    cv[it] = in ? ld8(row + 2 * C) : zero8();
+  }
+  bf16x8_t qb[2], db[2], ob[2], kb[2], vb[2];
+  auto load_kv = [&]() {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int off = 16 * st + 8 * hh;
+      kb[st] = key < N ? ld8(win + (size_t)key * C3 + C + off) : zero8();
+      vb[st] = key < N ? ld8(win + (size_t)key * C3 + 2 * C + off) : zero8();
+    }
+  };
+  const long long qorow = q < N ? out_row(g, bw, q) : -1;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const int off = 16 * st + 8 * hh;
+    qb[st] = q < N ? ld8(win + (size_t)q * C3 + off) : zero8();
+    db[st] = qorow >= 0 ? ld8(gwo + qorow * C + off) : zero8();
+    ob[st] = qorow >= 0 ? ld8(owin + qorow * C + off) : zero8();
+  }
+
+  const float Lq = q < N ? lrow[q] * kLog2e : INFINITY;      // log2 units; padded: P = 0
+  // token metadata: 4 (y P + x) << 16 | region; a padded token at (0, -ws)
+  const int ws = g.ws, P = ws + 32, R = 2 * ws - 1;
+  for (int t = threadIdx.x; t < NP; t += blockDim.x) {
+    const int m = token_meta(g, bw, t);
+    const int ty = t / ws, kk = t < N ? ty * P + (t - ty * ws) : -ws;
+    sTok[t] = (int)((unsigned)(4 * kk) << 16) | (m & 0xffff);
+  }
+  // [margin | (2ws-1) rows of P: table row (log2 units), -inf gap], margin -inf
+  for (int t = threadIdx.x; t < kBinW + kZ; t += blockDim.x) {
+    const int k = t - kZ, a = k / P, b = k - a * P;
+    sBias[t] = (k >= 0 && a < R && b < R) ? table[(a * R + b) * g.heads + h] * kLog2e : -INFINITY;
+  }
+  const char* biasb = reinterpret_cast<const char*>(sBias + kZ);   // + 4 rel
+  const bool mixed = window_mixed(g, bw);
+  const float scale2 = g.scale * kLog2e;
+  const int c04 = 4 * (ws - 1) * (P + 1);
+  // ---- phase 1 staging: K, V natural (swizzled); D, lse; bins zeroed; the bound's maxima
+  short* sK = sU;
+  short* sV = sU + kImg;
+  short* sKq = sU + 2 * kImg;
+  float vmax2 = 0.f;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    *reinterpret_cast<bf16x8_t*>(sK + swz64(t, c)) = ck[it];
+    *reinterpret_cast<bf16x8_t*>(sV + swz64(t, c)) = cv[it];
+    if (F8) *reinterpret_cast<bf16x8_t*>(sKq + swz64(t, c)) = fp8_token_chunk(ck[it]);
+    float v2 = sumsq8(cv[it]);                 // the token's 4 chunks sit on 4 adjacent lanes
+    v2 += __shfl_xor(v2, 1, 64);
+    v2 += __shfl_xor(v2, 2, 64);
+    vmax2 = fmaxf(vmax2, v2);
+  }
+  float Dq = 0.f;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      Dq += bf16_bits_to_f32((unsigned short)ob[st][j]) * bf16_bits_to_f32((unsigned short)db[st][j]);
+  Dq += __shfl_xor(Dq, 32, 64);
+  float dn = sumsq8(db[0]) + sumsq8(db[1]);
+  dn = sqrtf(dn + __shfl_xor(dn, 32, 64));   // |dO_q| (0 for a padded query)
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) dn += __shfl_xor(dn, o, 64);   // sum over the wave's queries
+  vmax2 = wave_max(vmax2);
+  if (l == 0) sVmax[wv] = vmax2;
+  if (hh == 0) {
+    sD[q] = Dq;
+    sL[q] = Lq;
+  }
+  for (int t = threadIdx.x; t < NT * kBinW + kZ; t += blockDim.x) sBins[t] = 0;
+  __syncthreads();
+  float vm = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT; ++w) vm = fmaxf(vm, sVmax[w]);
+  const float bound = 2.04f * sqrtf(vm) * dn;
+  int e = -96;                                // keeps 2^(31 - e) a normal f32
+  if (bound > 0.f && bound < INFINITY) {
+    (void)frexpf(bound, &e);                  // bound < 2^e
+    e = max(e, -96);
+  }
+  const float inv_q = __builtin_ldexpf(1.f, 31 - e), quantum = __builtin_ldexpf(1.f, e - 31);
+  if (l == 0) sQuant[wv] = quantum;
+  const float nDq = -Dq * inv_q;
+  char* binsb = reinterpret_cast<char*>(sBins + kZ + wv * kBinW);   // + 4 rel
+  bf16x8_t qs8[2] = {qb[0], qb[1]};
+  if (F8) fp8_token_lane(qs8);
+  const short* sKl = F8 ? sKq : sK;           // the logits' K
+  const int qo4 = (sTok[q] >> 16) + c04;
+  f32x16_t dq;
+  zero16(dq);
+  for (int kt = 0; kt < ((DBG & 4) ? 0 : NT); ++kt) {
+    f32x16_t s, dp;
+    zero16(s);
+    zero16(dp);
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int t = 32 * kt + r, c = 2 * st + hh;
+      s = mfma16(*reinterpret_cast<const bf16x8_t*>(sKl + swz64(t, c)), qs8[st], s);
+      dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sV + swz64(t, c)), db[st], dp);
+    }
+    int rel4[16];
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int4 t4 = *reinterpret_cast<const int4*>(sTok + 32 * kt + 8 * g4 + 4 * hh);
+      const int tk[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int i = 4 * g4 + e4;
+        rel4[i] = qo4 - (tk[e4] >> 16);
+        s[i] = fmaf(s[i], scale2, *reinterpret_cast<const float*>(biasb + rel4[i]));
+      }
+    }
+    if (mixed) mask_kq(s, sTok, kt, q, hh);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dp[i] = exp2_fast(s[i] - Lq) * fmaf(dp[i], inv_q, nDq);   // dS / quantum
+#pragma unroll
+    for (int th = 0; th < 2; ++th) dq = mfma16(tr_perm64(sK, 32 * kt + 16 * th, l), pack8(dp, 8 * th), dq);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (!(DBG & 1))
+        __hip_atomic_fetch_add(reinterpret_cast<int*>(binsb + rel4[i]), cvt_rpi(dp[i]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  if (q < N) {
+    bf16* dst = gw + (size_t)q * C3;
+    const float sc = quantum * g.scale;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      bf16x4_t v;
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) v[e4] = bf16_bits(dq[4 * grp + e4] * sc);
+      *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
+    }
+  }
+  load_p2();
+  load_kv();
+  __syncthreads();                            // bins complete; phase-1 staging dead after this
+  {
+    float* gp = gtable_part + ((size_t)bw * g.heads + h) * g.T2;
+    for (int t = threadIdx.x; t < g.T2; t += blockDim.x) {
+      const int ra = t / R, pb = kZ + ra * P + (t - ra * R);
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT; ++w) a += (float)sBins[pb + w * kBinW] * sQuant[w];
+      gp[t] = a;
+    }
+  }
+  if (DBG & 2) return;
+  // ---- phase 2 staging: Q, dO natural (swizzled)
+  short* sQ = sU;
+  short* sDo = sU + kImg;
+  short* sQq = sU + 2 * kImg;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
+    *reinterpret_cast<bf16x8_t*>(sQ + swz64(t, c)) = cq[it];
+    *reinterpret_cast<bf16x8_t*>(sDo + swz64(t, c)) = cd[it];
+    if (F8) *reinterpret_cast<bf16x8_t*>(sQq + swz64(t, c)) = fp8_token_chunk(cq[it]);
+  }
+  bf16x8_t ks8[2] = {kb[0], kb[1]};
+  if (F8) fp8_token_lane(ks8);
+  const short* sQl = F8 ? sQq : sQ;
+  const int tkey = sTok[key];
+  const int ko4 = (tkey >> 16) - c04, rk = tkey & 0xffff;
+  __syncthreads();
+  f32x16_t dv, dk;
+  zero16(dv);
+  zero16(dk);
+  for (int qq = 0; qq < NT; ++qq) {
+    f32x16_t s, dp;
+    zero16(s);
+    zero16(dp);
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int t = 32 * qq + r, c = 2 * st + hh;
+      s = mfma16(*reinterpret_cast<const bf16x8_t*>(sQl + swz64(t, c)), ks8[st], s);
+      dp = mfma16(*reinterpret_cast<const bf16x8_t*>(sDo + swz64(t, c)), vb[st], dp);
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int4 t4 = *reinterpret_cast<const int4*>(sTok + 32 * qq + 8 * g4 + 4 * hh);
+      const int tq[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4)
+        s[4 * g4 + e4] = fmaf(s[4 * g4 + e4], scale2, *reinterpret_cast<const float*>(biasb + ((tq[e4] >> 16) - ko4)));
+    }
+    if (mixed) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int4 t4 = *reinterpret_cast<const int4*>(sTok + 32 * qq + 8 * g4 + 4 * hh);
+        const int tq[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4)
+          if ((tq[e4] & 0xffff) != rk) s[4 * g4 + e4] += kMaskLog2;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qi = 32 * qq + crow(i, hh);
+      const float p = exp2_fast(s[i] - sL[qi]);
+      s[i] = p;
+      dp[i] = p * (dp[i] - sD[qi]);
+    }
+#pragma unroll
+    for (int th = 0; th < 2; ++th) {
+      const int base = 32 * qq + 16 * th;
+      dv = mfma16(tr_perm64(sDo, base, l), pack8(s, 8 * th), dv);
+      dk = mfma16(tr_perm64(sQ, base, l), pack8(dp, 8 * th), dk);
+    }
+  }
+  if (key < N) {
+    bf16* dst = gw + (size_t)key * C3;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      bf16x4_t a, b;
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        a[e4] = bf16_bits(dk[4 * grp + e4] * g.scale);
+        b[e4] = bf16_bits(dv[4 * grp + e4]);
       }
       *reinterpret_cast<bf16x4_t*>(dst + C + 8 * grp + 4 * hh) = a;
       *reinterpret_cast<bf16x4_t*>(dst + 2 * C + 8 * grp + 4 * hh) = b;
@@ -1426,6 +1791,16 @@ static void launch_fwd_blk(const WinGeom& g, dim3 grid, hipStream_t st, const vo
 #undef VS_FWD_BLK
 }
 
+// The round-5 backward (win_attn_bwd_fb) runs the bf16 windows of 64 < N <= 160 (Swin-B/L ws 12,
+// C3 / C5): -12 % at C5 (profiles/r5_win_bwd_ab.txt).  At N <= 64 (Swin-T ws 7, C2) and on the
+// fp8 path (a third staged image costs a workgroup per CU) the round-4 kernel stays faster.
+// VS_WIN_BWD_FB=0: the round-4 kernel everywhere; 2: the round-5 one everywhere (A/B)
+static bool bwd_fb(bool f8, int N) {
+  const char* e = getenv("VS_WIN_BWD_FB");
+  const int v = e ? atoi(e) : 1;
+  return v == 2 || (v == 1 && !f8 && N > 64);
+}
+
 template <bool F8>
 static void launch_bwd_fa(const WinGeom& g, dim3 grid, hipStream_t st, const void* qkv, const float* table,
                           const void* out, const float* lse, const void* grad_out, void* grad_qkv, float* gpart) {
@@ -1433,6 +1808,45 @@ static void launch_bwd_fa(const WinGeom& g, dim3 grid, hipStream_t st, const voi
 #define VS_BWD_FA(NT_)                                                                                      \
   hipLaunchKernelGGL((win_attn_bwd_fa<NT_, F8>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,       \
                      (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g)
+  const char* dv = getenv("VS_WIN_BWD_VAR");
+  const int dbg = dv ? atoi(dv) : 0;
+  if (bwd_fb(F8, g.N)) {
+    const char* fv = getenv("VS_WIN_BWD_VAR");
+    const int fdbg = fv ? atoi(fv) : 0;
+    if (fdbg > 0 && (g.N + 31) / 32 == 5) {
+#define VS_FB_DBG(D)                                                                                        \
+  case D:                                                                                                   \
+    hipLaunchKernelGGL((win_attn_bwd_fb<5, F8, 4, D>), grid, dim3(64 * 5), 0, st, (const bf16*)qkv, table,  \
+                       (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g);            \
+    return;
+      switch (fdbg) { VS_FB_DBG(1) VS_FB_DBG(2) VS_FB_DBG(3) VS_FB_DBG(4) VS_FB_DBG(6) default: break; }
+#undef VS_FB_DBG
+    }
+    const char* we = getenv("VS_WIN_BWD_WPE");
+    if (we && atoi(we) == 3 && (g.N + 31) / 32 == 5) {
+      hipLaunchKernelGGL((win_attn_bwd_fb<5, F8, 3>), grid, dim3(64 * 5), 0, st, (const bf16*)qkv, table,
+                         (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g);
+      return;
+    }
+#define VS_BWD_FB(NT_)                                                                                      \
+  hipLaunchKernelGGL((win_attn_bwd_fb<NT_, F8>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,       \
+                     (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g)
+    VS_NT_SWITCH((g.N + 31) / 32, VS_BWD_FB)
+#undef VS_BWD_FB
+    return;
+  }
+#define VS_BWD_DBG(D)                                                                                       \
+  case D:                                                                                                   \
+    hipLaunchKernelGGL((win_attn_bwd_fa<5, F8, D>), grid, dim3(64 * 5), 0, st, (const bf16*)qkv, table,     \
+                       (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g);            \
+    return;
+  if (dbg > 0 && (g.N + 31) / 32 == 5) {
+    switch (dbg) {
+      VS_BWD_DBG(1) VS_BWD_DBG(2) VS_BWD_DBG(3) VS_BWD_DBG(4) VS_BWD_DBG(8) VS_BWD_DBG(9) VS_BWD_DBG(6)
+      default: break;
+    }
+  }
+#undef VS_BWD_DBG
   VS_NT_SWITCH((g.N + 31) / 32, VS_BWD_FA)
 #undef VS_BWD_FA
 }
