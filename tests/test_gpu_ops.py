@@ -891,6 +891,36 @@ def test_masked_attention_bf16_fwd_bwd_vs_oracle(monkeypatch, kernel, B, Q, S):
         assert e <= 2e-2 * float(exp.abs().max()) + 1e-4, (e, float(exp.abs().max()))
 
 
+@pytest.mark.parametrize("blocks", ["auto", "1", "3"])
+@pytest.mark.parametrize("B,Q,S", [(2, 100, 4096), (1, 100, 1000), (2, 7, 300), (1, 128, 16384), (4, 100, 16384)])
+def test_masked_attention_v2_equals_v1(monkeypatch, blocks, B, Q, S):
+    """The round-5 MFMA kernels (xattn_fwd_mfma2 / xattn_bwd_mfma2: operands staged in LDS
+    once, transposed dS) against the round-4 ones on the same inputs: the output, dK and dV
+    are the same products in the same order (bit-equal); dQ^T = K^T dS^T takes the MFMA's
+    operands the other way round, so dQ agrees to bf16 rounding (one ulp of the larger
+    value)."""
+    if blocks != "auto":
+        monkeypatch.setenv("VS_XATTN_BLOCKS", blocks)
+    ops = _ops()
+    heads = 8
+    q, k, v, blocked, words = _xattn_case(B, Q, S, heads, seed=Q + S + 1, dtype=torch.bfloat16)
+    go = torch.randn(B, Q, heads * 32, generator=torch.Generator().manual_seed(7)).to(torch.bfloat16)
+    res = []
+    for ver in ("1", "2"):
+        monkeypatch.setenv("VS_XATTN_BWD", ver)
+        monkeypatch.setenv("VS_XATTN_FWD", ver)
+        qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
+        out = ops.masked_attention(qd, kd, vd, words.to(DEV), heads)
+        out.backward(go.to(DEV))
+        torch.cuda.synchronize()
+        res.append([t.grad.float().cpu() for t in (qd, kd, vd)] + [out.detach().float().cpu()])
+    (q1, k1, v1, o1), (q2, k2, v2, o2) = res
+    assert torch.equal(o1, o2)
+    assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    assert bool(((q1 - q2).abs() <= 2 ** -7 * torch.maximum(q1.abs(), q2.abs()) + 1e-6).all()), \
+        float((q1 - q2).abs().max())
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("shape,groups,cl", [((2, 256, 64, 64), 32, True), ((2, 256, 17, 23), 32, True),

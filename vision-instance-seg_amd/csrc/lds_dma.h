@@ -92,5 +92,37 @@ __device__ __forceinline__ void lgkm_wait(bf16x8_t& v) {
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N) : "memory");
 }
 
+// ---- 64-B-row images ([token][32 x bf16], one attention head's rows): the 16-B chunk c of
+// row t sits at chunk c ^ ((t >> 2) & 3), so a row-major read of one chunk column by 16
+// lanes and a 4-row transposed read both cover all 64 banks.  Offsets in shorts.
+__device__ __forceinline__ int swz64(int t, int c) { return 32 * t + 8 * (c ^ ((t >> 2) & 3)); }
+
+// MFMA operand m = channel lane & 31, k = 8hh + j from rows t_lo + e (j = e < 4) and
+// t_hi + e (j = 4 + e), e = (lane & 15) >> 2 chosen by the caller per lane half
+__device__ __forceinline__ bf16x8_t tr64_rows(const short* img, int t_lo, int t_hi, int lane) {
+  typedef __attribute__((address_space(3))) bf16x4v_t lds_v4;
+  const int col = (lane & 16) + 4 * (lane & 3);
+  const bf16x4v_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + 32 * t_lo + 8 * ((col >> 3) ^ ((t_lo >> 2) & 3)) + (col & 7)));
+  const bf16x4v_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + 32 * t_hi + 8 * ((col >> 3) ^ ((t_hi >> 2) & 3)) + (col & 7)));
+  bf16x8_t v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+// permuted token order (k = 8hh + j <-> token base + (j&3) + 8(j>>2) + 4hh: a C tile's rows)
+__device__ __forceinline__ bf16x8_t tr_perm64(const short* img, int base, int lane) {
+  const int t0 = base + 4 * (lane >> 5) + ((lane & 15) >> 2);
+  return tr64_rows(img, t0, t0 + 8, lane);
+}
+
+// natural token order (k = 8hh + j <-> token base + 8hh + j)
+__device__ __forceinline__ bf16x8_t tr_nat64(const short* img, int base, int lane) {
+  const int t0 = base + 8 * (lane >> 5) + ((lane & 15) >> 2);
+  return tr64_rows(img, t0, t0 + 4, lane);
+}
+
 }  // namespace
 }  // namespace vs

@@ -17,6 +17,7 @@
 // query, P recomputed from the saved lse, partials summed over chunks by a combine
 // kernel — deterministic) and dK/dV with one lane per key over all queries staged in
 // LDS.  Those are the f32 (parity) kernels; bf16 runs the MFMA kernels further below.
+#include "lds_dma.h"
 #include "mfma_util.h"
 
 #include <algorithm>
@@ -447,6 +448,101 @@ __global__ void __launch_bounds__(256) xattn_fwd_mfma(const bf16* __restrict__ q
   }
 }
 
+// Forward, round 5 (xattn_fwd_mfma2): the same split as xattn_fwd_mfma with K and V staged
+// once in their natural layout (64-B rows, lds_dma.h swz64: 16-B chunk stores, no
+// transposing two-byte stores) -- the round-4 kernel read every 32-key tile's K fragment and
+// blocked-bits word from global memory inside the tile loop, one L2 round trip per tile with
+// nothing else in flight.  V^T in the permuted key order comes from the transposed LDS read;
+// a lane's blocked bits for the chunk (8 words) are requested with the staging loads.
+__global__ void __launch_bounds__(256) xattn_fwd_mfma2(const bf16* __restrict__ q, const bf16* __restrict__ k,
+                                                       const bf16* __restrict__ v, const uint32_t* __restrict__ words,
+                                                       float* __restrict__ po, float* __restrict__ pml, XGeom g) {
+  __shared__ __attribute__((aligned(16))) short sK[kFChunk * 32];
+  __shared__ __attribute__((aligned(16))) short sV[kFChunk * 32];
+  const int chunk = blockIdx.x, h = blockIdx.y;
+  const int nqg = (g.Q + 127) / 128;
+  const int qg = blockIdx.z % nqg, b = blockIdx.z / nqg;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int C = g.heads * kD;
+  const int jbeg = chunk * kFChunk;
+  const int n = min(kFChunk, g.S - jbeg);
+  const bf16* kb = k + ((size_t)b * g.S + jbeg) * C + h * kD;
+  const bf16* vb = v + ((size_t)b * g.S + jbeg) * C + h * kD;
+  constexpr int kIt = kFChunk * 4 / 256;        // 16-B chunks per thread and tensor
+  bf16x8_t kc[kIt], vc[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int p = threadIdx.x + 256 * it, t = p >> 2, c = p & 3;
+    kc[it] = t < n ? ld8(kb + (size_t)t * C + 8 * c) : zero8();
+    vc[it] = t < n ? ld8(vb + (size_t)t * C + 8 * c) : zero8();
+  }
+  const int qi = qg * 128 + wave * 32 + r;
+  const bool qok = qi < g.Q;
+  bf16x8_t qf[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) qf[st] = qok ? ld8(q + ((size_t)b * g.Q + qi) * C + h * kD + 16 * st + 8 * hh) : zero8();
+  const int ntiles = (n + 31) / 32;
+  const uint32_t* wrow = words + ((size_t)b * g.Q + (qok ? qi : 0)) * g.nw + (jbeg >> 5);
+  uint32_t wv[kFChunk / 32];
+#pragma unroll
+  for (int kt = 0; kt < kFChunk / 32; ++kt) wv[kt] = (qok && kt < ntiles) ? wrow[kt] : 0xffffffffu;
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int p = threadIdx.x + 256 * it, t = p >> 2, c = p & 3;
+    *reinterpret_cast<bf16x8_t*>(sK + swz64(t, c)) = kc[it];
+    *reinterpret_cast<bf16x8_t*>(sV + swz64(t, c)) = vc[it];
+  }
+  __syncthreads();
+  float m = -INFINITY, lsum = 0.f;
+  f32x16_t o;
+  zero16(o);
+#pragma unroll
+  for (int kt = 0; kt < kFChunk / 32; ++kt) {
+    if (kt >= ntiles) break;
+    f32x16_t sc;
+    zero16(sc);
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+      sc = mfma16(*reinterpret_cast<const bf16x8_t*>(sK + swz64(32 * kt + r, 2 * st + hh)), qf[st], sc);
+    const uint32_t w = wv[kt];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kl = crow(i, hh);
+      const bool blocked = (kt * 32 + kl >= n) || ((w >> kl) & 1u);
+      sc[i] = blocked ? -INFINITY : sc[i] * g.scale;
+      mt = fmaxf(mt, sc[i]);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float safe = mn == -INFINITY ? 0.f : mn;
+    const float alpha = __expf(m - safe);
+    lsum *= alpha;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[i] *= alpha;
+      sc[i] = __expf(sc[i] - safe);
+      lsum += sc[i];
+    }
+    m = mn;
+#pragma unroll
+    for (int th = 0; th < 2; ++th) o = mfma16(tr_perm64(sV, kt * 32 + 16 * th, l), pack8(sc, 8 * th), o);
+  }
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (qok) {
+    const size_t prow = (((size_t)b * g.heads + h) * g.nchunk + chunk) * g.Q + qi;
+    float* dst = po + prow * kD;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp)
+      *reinterpret_cast<float4*>(dst + 8 * grp + 4 * hh) =
+          make_float4(o[4 * grp], o[4 * grp + 1], o[4 * grp + 2], o[4 * grp + 3]);
+    if (hh == 0) {
+      pml[prow * 2 + 0] = m;
+      pml[prow * 2 + 1] = lsum;
+    }
+  }
+}
+
 // D_i = dO_i . O_i per (b, h, q)
 template <typename T>
 __global__ void __launch_bounds__(256) xattn_bwd_prep(const T* __restrict__ out, const T* __restrict__ gout,
@@ -600,6 +696,167 @@ __global__ void __launch_bounds__(256) xattn_bwd_mfma(const bf16* __restrict__ q
   }
 }
 
+// Backward, round 5 (xattn_bwd_mfma2): the same workgroup / wave split as xattn_bwd_mfma with
+// every operand read from LDS, staged once in its natural layout:
+//  * Q and dO of the (image, head) -- the round-4 kernel re-read their fragments from global
+//    memory inside the query-tile loop of every key block, a round trip to L2 per tile with
+//    nothing else in flight (the finest level ran at ~14 % of HBM rate); Q^T / dO^T for
+//    dK / dV now come from the transposed LDS read of the same natural copies;
+//  * the blocked-key bits transposed to [key group][query], so a lane's 4 consecutive query
+//    rows are one 16-B read (16 scalar reads before);
+//  * dS stored transposed, [key][query] (256-B rows, lds_dma.h image b): a lane writes its 4
+//    consecutive queries as one 8-B store (16 two-byte stores before), and dQ^T = K^T dS^T
+//    takes both operands by transposed reads; a lane's dQ partial is then 16 channels of
+//    ONE query (4 x 16-B stores).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) xattn_bwd_mfma2(const bf16* __restrict__ q, const bf16* __restrict__ k,
+                                                       const bf16* __restrict__ v, const uint32_t* __restrict__ words,
+                                                       const float* __restrict__ lse, const float* __restrict__ Dbuf,
+                                                       const bf16* __restrict__ gout, bf16* __restrict__ gk,
+                                                       bf16* __restrict__ gv, float* __restrict__ pdq, XGeom g) {
+  __shared__ __attribute__((aligned(16))) short sQ[kBQ * 32];         // Q [q][d], 64-B rows (swz64)
+  __shared__ __attribute__((aligned(16))) short sDo[kBQ * 32];        // dO [q][d]
+  __shared__ __attribute__((aligned(16))) short sK[kBChunk * 32];     // K [key][d] of the block
+  __shared__ __attribute__((aligned(16))) unsigned char sDSt[kBChunk * kBQ * 2];   // dS^T [key][q]
+  __shared__ __attribute__((aligned(16))) uint32_t sWt[kBChunk / 32][kBQ];       // blocked bits
+  __shared__ __attribute__((aligned(16))) float sL[kBQ], sD[kBQ];
+  const int chunk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  const int C = g.heads * kD, Q = g.Q;
+  const bf16* qb = q + (size_t)b * Q * C + h * kD;
+  const bf16* ob = gout + (size_t)b * Q * C + h * kD;
+  // Q, dO natural (4 chunks of 16 B a row): 1024 chunks over 256 threads; lse and D rows
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int p = threadIdx.x + 256 * it, part = p >> 9, t = (p >> 2) & 127, c = p & 3;
+    const bf16* src = part ? ob : qb;
+    const bf16x8_t x = t < Q ? ld8(src + (size_t)t * C + 8 * c) : zero8();
+    *reinterpret_cast<bf16x8_t*>((part ? sDo : sQ) + swz64(t, c)) = x;
+  }
+  if (threadIdx.x < kBQ) {
+    const int t = threadIdx.x;
+    sL[t] = t < Q ? lse[((size_t)b * g.heads + h) * Q + t] : 0.f;
+    sD[t] = t < Q ? Dbuf[((size_t)b * g.heads + h) * Q + t] : 0.f;
+  }
+  f32x16_t dq;                                 // dQ^T of query tile `wave`: rows d, column q
+  zero16(dq);
+  const int nblk = g.chunk / kBChunk;
+  const int kl = wave * 32 + r;                 // key within a block (this lane's column)
+  // a block's global operands: this lane's K / V row slices, the K staging chunks and the
+  // blocked bits -- requested one block ahead, so their latency hides behind a block's work
+  bf16x8_t kf[2], vf[2], kst[2];
+  uint32_t wst[2];
+  auto load_block = [&](int kb) {
+    const int jbeg = chunk * g.chunk + kb * kBChunk;
+    const int n = min(kBChunk, g.S - jbeg);     // <= 0 past the end: everything zero
+    const bf16* kb_ = k + ((size_t)b * g.S + jbeg) * C + h * kD;
+    const bf16* vb = v + ((size_t)b * g.S + jbeg) * C + h * kD;
+    const bool kok = kl < n;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      kf[st] = kok ? ld8(kb_ + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
+      vf[st] = kok ? ld8(vb + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
+    }
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int p = threadIdx.x + 256 * it, t = p >> 2, c = p & 3;
+      kst[it] = t < n ? ld8(kb_ + (size_t)t * C + 8 * c) : zero8();
+      const int qq = p & 127, wg = p >> 7, wi = (jbeg >> 5) + wg;
+      wst[it] = (n > 0 && qq < Q && wi < g.nw) ? words[((size_t)b * Q + qq) * g.nw + wi] : 0xffffffffu;
+    }
+  };
+  load_block(0);
+  for (int kb = 0; kb < nblk; ++kb) {
+    const int jbeg = chunk * g.chunk + kb * kBChunk;
+    if (jbeg >= g.S) break;                     // uniform over the workgroup
+    const int n = min(kBChunk, g.S - jbeg);
+    const bool kok = kl < n;
+    const bf16x8_t kfc[2] = {kf[0], kf[1]}, vfc[2] = {vf[0], vf[1]};
+    __syncthreads();                            // the previous block's K / dS^T / bits are read
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int p = threadIdx.x + 256 * it, t = p >> 2, c = p & 3;
+      *reinterpret_cast<bf16x8_t*>(sK + swz64(t, c)) = kst[it];
+      sWt[p >> 7][p & 127] = wst[it];
+    }
+    if (kb + 1 < nblk) load_block(kb + 1);
+    __syncthreads();
+    f32x16_t dv, dk;
+    zero16(dv);
+    zero16(dk);
+#pragma unroll 1
+    for (int qt = 0; qt < 4; ++qt) {
+      f32x16_t sacc, dacc;
+      zero16(sacc);
+      zero16(dacc);
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const int t = 32 * qt + r, c = 2 * st + hh;
+        sacc = mfma16(*reinterpret_cast<const bf16x8_t*>(sQ + swz64(t, c)), kfc[st], sacc);
+        dacc = mfma16(*reinterpret_cast<const bf16x8_t*>(sDo + swz64(t, c)), vfc[st], dacc);
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int q0 = 32 * qt + 8 * g4 + 4 * hh;
+        const uint4 w4 = *reinterpret_cast<const uint4*>(&sWt[wave][q0]);
+        const float4 L4 = *reinterpret_cast<const float4*>(sL + q0);
+        const float4 D4 = *reinterpret_cast<const float4*>(sD + q0);
+        const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+        bf16x4_t ds4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          const bool ok = kok && q0 + e < Q && !((wv[e] >> r) & 1u);
+          const float p = ok ? __expf(sacc[i] * g.scale - Lv[e]) : 0.f;
+          sacc[i] = p;
+          dacc[i] = p * (dacc[i] - Dv[e]);
+          ds4[e] = bf16_bits(dacc[i]);
+        }
+        *reinterpret_cast<bf16x4_t*>(sDSt + woff(kl, q0 >> 3) + 8 * hh) = ds4;
+      }
+#pragma unroll
+      for (int th = 0; th < 2; ++th) {           // k over the tile's queries, permuted order
+        const int base = 32 * qt + 16 * th;
+        dv = mfma16(tr_perm64(sDo, base, l), pack8(sacc, 8 * th), dv);
+        dk = mfma16(tr_perm64(sQ, base, l), pack8(dacc, 8 * th), dk);
+      }
+    }
+    if (kok) {
+      bf16* gvr = gv + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
+      bf16* gkr = gk + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        bf16x4_t av, ck;
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          av[e2] = bf16_bits(dv[4 * grp + e2]);
+          ck[e2] = bf16_bits(dk[4 * grp + e2] * g.scale);
+        }
+        *reinterpret_cast<bf16x4_t*>(gvr + 8 * grp + 4 * hh) = av;
+        *reinterpret_cast<bf16x4_t*>(gkr + 8 * grp + 4 * hh) = ck;
+      }
+    }
+    __syncthreads();                            // every wave's dS^T is in LDS
+    // dQ^T of query tile `wave` += K^T dS^T over the block's keys
+#pragma unroll
+    for (int tt = 0; tt < kBChunk / 16; ++tt)
+      dq = mfma16(tr_nat64(sK, 16 * tt, l), tr_frag(sDSt, 16 * tt, 32 * wave, l), dq);
+  }
+  const int qr = 32 * wave + r;
+  if (qr < Q) {
+    float* dst = pdq + ((((size_t)b * g.heads + h) * g.nchunk + chunk) * Q + qr) * kD;
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      float4 o;
+      o.x = dq[4 * grp + 0] * g.scale;
+      o.y = dq[4 * grp + 1] * g.scale;
+      o.z = dq[4 * grp + 2] * g.scale;
+      o.w = dq[4 * grp + 3] * g.scale;
+      *reinterpret_cast<float4*>(dst + 8 * grp + 4 * hh) = o;
+    }
+  }
+}
+
 XGeom make_geom(int B, int Q, int S, int heads, float scale) {
   XGeom g;
   g.B = B; g.Q = Q; g.S = S; g.heads = heads; g.scale = scale;
@@ -626,6 +883,18 @@ static XGeom mfma_geom(int B, int Q, int S, int heads, float scale, int chunk) {
   return g;
 }
 
+// VS_XATTN_FWD=1: the round-4 MFMA forward (A/B)
+static bool xattn_fwd_v2() {
+  const char* e = getenv("VS_XATTN_FWD");
+  return !(e && atoi(e) == 1);
+}
+
+// VS_XATTN_BWD=1: the round-4 MFMA backward (A/B)
+static bool xattn_bwd_v2() {
+  const char* e = getenv("VS_XATTN_BWD");
+  return !(e && atoi(e) == 1);
+}
+
 // VS_XATTN_SCALAR=1 selects the scalar-FMA kernels for bf16 too
 static bool xattn_use_mfma() {
   const char* e = getenv("VS_XATTN_SCALAR");
@@ -650,8 +919,12 @@ extern "C" int vs_masked_attn_forward(int dtype, const void* q, const void* k, c
     float* pml = po + (size_t)B * heads * g.nchunk * Q * kD;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid(g.nchunk, heads, B * ((Q + 127) / 128));
-    hipLaunchKernelGGL(xattn_fwd_mfma, grid, dim3(256), 0, st, (const bf16*)q, (const bf16*)k, (const bf16*)v, words,
-                       po, pml, g);
+    if (xattn_fwd_v2())
+      hipLaunchKernelGGL(xattn_fwd_mfma2, grid, dim3(256), 0, st, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                         words, po, pml, g);
+    else
+      hipLaunchKernelGGL(xattn_fwd_mfma, grid, dim3(256), 0, st, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                         words, po, pml, g);
     const long long crows = (long long)B * heads * Q * 32;
     hipLaunchKernelGGL(xattn_fwd_combine<bf16>, dim3((int)((crows + 255) / 256)), dim3(256), 0, st, po, pml,
                        (bf16*)out, lse, g);
@@ -704,8 +977,12 @@ extern "C" int vs_masked_attn_backward(int dtype, const void* q, const void* k, 
     const long long rows = (long long)B * heads * Q;
     hipLaunchKernelGGL(xattn_bwd_prep<bf16>, dim3((int)((rows + 255) / 256)), dim3(256), 0, st, (const bf16*)out,
                        (const bf16*)grad_out, Dbuf, g);
-    hipLaunchKernelGGL(xattn_bwd_mfma, dim3(g.nchunk, heads, B), dim3(256), 0, st, (const bf16*)q, (const bf16*)k,
-                       (const bf16*)v, words, lse, Dbuf, (const bf16*)grad_out, (bf16*)grad_k, (bf16*)grad_v, pdq, g);
+    if (xattn_bwd_v2())
+      hipLaunchKernelGGL(xattn_bwd_mfma2, dim3(g.nchunk, heads, B), dim3(256), 0, st, (const bf16*)q, (const bf16*)k,
+                         (const bf16*)v, words, lse, Dbuf, (const bf16*)grad_out, (bf16*)grad_k, (bf16*)grad_v, pdq, g);
+    else
+      hipLaunchKernelGGL(xattn_bwd_mfma, dim3(g.nchunk, heads, B), dim3(256), 0, st, (const bf16*)q, (const bf16*)k,
+                         (const bf16*)v, words, lse, Dbuf, (const bf16*)grad_out, (bf16*)grad_k, (bf16*)grad_v, pdq, g);
     const long long total = rows * kD;
     hipLaunchKernelGGL(xattn_bwd_dq_combine<bf16>, dim3((int)((total + 255) / 256)), dim3(256), 0, st, pdq,
                        (bf16*)grad_q, g);

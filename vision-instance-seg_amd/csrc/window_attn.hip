@@ -21,6 +21,7 @@
 // pass for dK/dV, recomputing P from the saved log-sum-exp.  The per-window bias
 // gradient partials are written to [Bw, heads, (2ws-1)^2] and summed by the caller
 // (deterministic, no cross-workgroup atomics on a 169-entry table).
+#include "lds_dma.h"
 #include "mfma_util.h"
 #include "mx_util.h"
 
@@ -1384,27 +1385,6 @@ __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_at
 //    B < 2^e / 1.02 keeps every partial sum inside int32 (the 2 % covers the rounding of the
 //    <= 160 terms).  Each term is rounded once, to 2^-32 B: the bins agree with f32 sums to
 //    a few 1e-6 of the gradient's range (tests/test_gpu_ops.py).
-__device__ __forceinline__ int swz64(int t, int c) { return 32 * t + 8 * (c ^ ((t >> 2) & 3)); }
-
-// MFMA operand in the permuted token order (k = 8hh + j <-> token base + (j&3) + 8(j>>2) + 4hh,
-// m = channel lane & 31) from a swizzled [token][32] image: two transposed reads
-typedef short bf16x4tr_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ bf16x8_t tr_perm64(const short* img, int base, int lane) {
-  typedef __attribute__((address_space(3))) bf16x4tr_t lds_v4;
-  const int hh = lane >> 5, e = (lane & 15) >> 2;
-  const int col = (lane & 16) + 4 * (lane & 3);
-  const int t0 = base + 4 * hh + e, t1 = t0 + 8;
-  const bf16x4tr_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_v4*)(img + 32 * t0 + 8 * ((col >> 3) ^ ((t0 >> 2) & 3)) + (col & 7)));
-  const bf16x4tr_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_v4*)(img + 32 * t1 + 8 * ((col >> 3) ^ ((t1 >> 2) & 3)) + (col & 7)));
-  bf16x8_t v;
-  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-  return v;
-}
-
 __device__ __forceinline__ float sumsq8(bf16x8_t c) {
   float a = 0.f;
 #pragma unroll
@@ -1448,7 +1428,7 @@ __device__ __forceinline__ int cvt_rpi(float x) {
 // neighbouring waves or the margins around them, where adding 0 changes nothing.
 // DBG (timing-split instances, VS_WIN_BWD_VAR with VS_WIN_BWD_FB=1): 1 no bins, 2 no phase 2,
 // 4 no phase-1 tile loop
-template <int NT, bool F8, int WPE = 4, int DBG = 0>
+template <int NT, bool F8, int WPE = F8 ? 3 : 4, int DBG = 0>
 __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(WPE))) win_attn_bwd_fb(
     const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
     const float* __restrict__ lse, const bf16* __restrict__ gout, bf16* __restrict__ gqkv,
@@ -1816,7 +1796,7 @@ static void launch_bwd_fa(const WinGeom& g, dim3 grid, hipStream_t st, const voi
     if (fdbg > 0 && (g.N + 31) / 32 == 5) {
 #define VS_FB_DBG(D)                                                                                        \
   case D:                                                                                                   \
-    hipLaunchKernelGGL((win_attn_bwd_fb<5, F8, 4, D>), grid, dim3(64 * 5), 0, st, (const bf16*)qkv, table,  \
+    hipLaunchKernelGGL((win_attn_bwd_fb<5, F8, F8 ? 3 : 4, D>), grid, dim3(64 * 5), 0, st, (const bf16*)qkv, table,  \
                        (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g);            \
     return;
       switch (fdbg) { VS_FB_DBG(1) VS_FB_DBG(2) VS_FB_DBG(3) VS_FB_DBG(4) VS_FB_DBG(6) default: break; }
