@@ -968,7 +968,9 @@ extern "C" int vs_masked_attn_backward(int dtype, const void* q, const void* k, 
     // (the Q^T / dO^T staging and the dQ partial are per workgroup; VS_XATTN_BLOCKS=n
     // forces n blocks per workgroup, for tests)
     const long long nb128 = (long long)B * heads * ((S + kBChunk - 1) / kBChunk);
-    int per = nb128 >= 4096 ? 4 : nb128 >= 2048 ? 2 : 1;     // C2's 128^2 level: 4 (kbench 0.174 -> 0.135 ms)
+    // C2's 128^2 level: 8 (one round of 2 workgroups per CU; kbench op 0.088 -> 0.085 ms with the
+    // round-5 kernel, profiles/r5_xattn_ab.txt; 4 with the round-4 one: 0.174 -> 0.135 ms)
+    int per = nb128 >= 4096 ? (xattn_bwd_v2() ? 8 : 4) : nb128 >= 2048 ? 2 : 1;
     if (const char* e = getenv("VS_XATTN_BLOCKS")) per = std::max(1, std::min(16, atoi(e)));
     XGeom g = mfma_geom(B, Q, S, heads, scale, kBChunk * per);
     float* pdq = (float*)workspace;

@@ -34,7 +34,20 @@ struct WinGeom {
   int heads, ws, shift, nWh, nWw, N, T2;  // T2 = (2ws-1)^2
   float scale;
   int H, W, nat;                           // nat: out / grad_out in the image layout [B, H, W, C]
+  // division by multiply-high (check_geom): a window's token / ws for t < 2^16 / ws, and the
+  // window index / (nWh nWw) and / nWw (exact while the dividend times the divisor < 2^32).
+  // Each integer division was ~30 VALU, and the index arithmetic of the staging and of the
+  // image-layout rows had grown to about half of the backward kernels' VALU instructions
+  unsigned m_ws, m_nw, m_nWw;
 };
+
+__device__ __forceinline__ int div_ws(const WinGeom& g, int t) { return (int)(__umul24((unsigned)t, g.m_ws) >> 16); }
+__device__ __forceinline__ int div_nw(const WinGeom& g, int bw) {
+  return g.m_nw ? (int)__umulhi((unsigned)bw, g.m_nw) : bw;            // m 0: divisor 1
+}
+__device__ __forceinline__ int div_nWw(const WinGeom& g, int wl) {
+  return g.m_nWw ? (int)__umulhi((unsigned)wl, g.m_nWw) : wl;
+}
 
 // Row of window token t of window bw in the output / output-gradient layout: the window
 // layout (bw N + t), or -- nat, the window reverse folded into the kernel -- the token's
@@ -42,9 +55,9 @@ struct WinGeom {
 // which the reverse crops: its output is not stored and its output gradient is zero)
 __device__ __forceinline__ long long out_row(const WinGeom& g, int bw, int t) {
   if (!g.nat) return (long long)bw * g.N + t;
-  const int nw = g.nWh * g.nWw, b = bw / nw, wl = bw - b * nw;
-  const int wy = wl / g.nWw, wx = wl - wy * g.nWw;
-  const int ty = t / g.ws, tx = t - ty * g.ws;
+  const int nw = g.nWh * g.nWw, b = div_nw(g, bw), wl = bw - b * nw;
+  const int wy = div_nWw(g, wl), wx = wl - wy * g.nWw;
+  const int ty = div_ws(g, t), tx = t - ty * g.ws;
   int y = wy * g.ws + ty + g.shift, x = wx * g.ws + tx + g.shift;
   if (y >= g.nWh * g.ws) y -= g.nWh * g.ws;
   if (x >= g.nWw * g.ws) x -= g.nWw * g.ws;
@@ -326,9 +339,9 @@ __device__ __forceinline__ int rel_c0(const WinGeom& g) { return (g.ws - 1) * 2 
 __device__ __forceinline__ int token_meta(const WinGeom& g, int bw, int t) {
   if (t >= g.N) return (int)((unsigned)(rel_c0(g) - g.T2) << 16);
   const int ws = g.ws;
-  const int wl = bw % (g.nWh * g.nWw);
-  const int wy = wl / g.nWw, wx = wl % g.nWw;
-  const int ty = t / ws, tx = t % ws;
+  const int wl = bw - div_nw(g, bw) * (g.nWh * g.nWw);
+  const int wy = div_nWw(g, wl), wx = wl - wy * g.nWw;
+  const int ty = div_ws(g, t), tx = t - ty * ws;
   const int reg = g.shift > 0 ? region_of(wy * ws + ty, g.nWh * ws, ws, g.shift) * 3 +
                                     region_of(wx * ws + tx, g.nWw * ws, ws, g.shift)
                               : 0;
@@ -338,8 +351,9 @@ __device__ __forceinline__ int token_meta(const WinGeom& g, int bw, int t) {
 // Only windows of the last window row / column of a shifted block mix regions (the roll
 // wraps there); every other window skips the mask with a uniform branch.
 __device__ __forceinline__ bool window_mixed(const WinGeom& g, int bw) {
-  const int wl = bw % (g.nWh * g.nWw);
-  return g.shift > 0 && (wl / g.nWw == g.nWh - 1 || wl % g.nWw == g.nWw - 1);
+  const int wl = bw - div_nw(g, bw) * (g.nWh * g.nWw);
+  const int wy = div_nWw(g, wl);
+  return g.shift > 0 && (wy == g.nWh - 1 || wl - wy * g.nWw == g.nWw - 1);
 }
 
 __device__ __forceinline__ void window_tokens(const WinGeom& g, int bw, int lane, int* tok) {
@@ -1703,8 +1717,12 @@ int check_geom(WinGeom& g, int Bw, int heads, int ws, int shift, int nWh, int nW
   g.N = ws * ws;
   g.T2 = (2 * ws - 1) * (2 * ws - 1);
   g.H = nWh * ws; g.W = nWw * ws; g.nat = 0;
+  g.m_ws = ws > 0 ? (65536u + (unsigned)ws - 1u) / (unsigned)ws : 0u;
+  const unsigned long long nw = (unsigned long long)nWh * (unsigned long long)nWw;
+  g.m_nw = nw > 1 ? (unsigned)(((1ull << 32) + nw - 1) / nw) : 0u;     // 1: see div_nw
+  g.m_nWw = nWw > 1 ? (unsigned)(((1ull << 32) + (unsigned long long)nWw - 1) / (unsigned long long)nWw) : 0u;
   return Bw > 0 && heads > 0 && ws > 0 && ws <= 16 && shift >= 0 && shift < ws && nWh > 0 && nWw > 0 &&
-         Bw % (nWh * nWw) == 0;
+         Bw % (nWh * nWw) == 0 && (unsigned long long)Bw * nw < (1ull << 32);
 }
 
 }  // namespace
