@@ -69,6 +69,35 @@ def test_token_gemm_gelu_epilogue(M, N, K):
     assert bool((e2 <= gel.abs() * 2 ** -8 + 1e-6).all()), float(e2.max())
 
 
+@pytest.mark.parametrize("M,N,K,bias,gelu", [(40000, 288, 96, True, False), (33000, 96, 96, False, False),
+                                             (65555, 384, 96, True, True), (40000, 576, 192, True, False),
+                                             (32768, 200, 136, True, False), (50000, 192, 192, True, True),
+                                             (1000, 384, 96, True, False), (70, 128, 64, False, True)])
+def test_token_gemm_stream_equals_tile_kernel(monkeypatch, M, N, K, bias, gelu):
+    """The streaming kernel for short rows (K <= 192, many tokens; W slice resident, token
+    tiles streamed) against the tile kernel on the same operands -- the same products in
+    the same K order, so bit-equal outputs -- and against the f64 product.  Ragged token
+    tiles, N not a multiple of the 128-feature slice, K tails inside a 128-byte step; the
+    last two shapes force the streaming kernel below its row threshold."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + N + K)
+    x, w = _rand((M, K), g), _rand((N, K), g, 1 / math.sqrt(K))
+    b = _rand((N,), g) if bias else None
+    xd, wd, bd = x.to(DEV), w.to(DEV), (b.to(DEV) if b is not None else None)
+    res = []
+    for rows in ("0", "1"):                  # 0: the tile kernel; 1: streaming for any M
+        monkeypatch.setenv("VS_TGEMM_STREAM_ROWS", rows)
+        out = ops.token_gemm(xd, wd, bd, gelu=gelu)
+        torch.cuda.synchronize()
+        res.append([t.cpu() for t in (out if gelu else (out,))])
+    for a, s in zip(*res):
+        assert torch.equal(a, s), float((a.double() - s.double()).abs().max())
+    y = res[1][-1 if gelu else 0].double()   # the pre-activation (gelu) or the output
+    ref = _ref(x, w, b)
+    err = (y - ref).abs()
+    assert bool((err <= ref.abs() * 2 ** -7 + 1e-3 * float(ref.abs().max())).all()), float(err.max())
+
+
 def _mx_emulate(x):
     """The quantiser's rule in torch: (e4m3 bytes, scale bytes, dequantised f64)."""
     rows, K = x.shape

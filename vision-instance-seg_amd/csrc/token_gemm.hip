@@ -24,6 +24,8 @@
 // fp8: the per-row block scales of the K-step (4 bytes a row) are staged by 4-byte DMA.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "gelu_table.h"
 #include "mfma_util.h"
 #include "mx_util.h"
@@ -320,6 +322,151 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Streaming token GEMM for short rows (K <= 192: Swin-T stages 1-2, the C2 step's largest
+// Linears by bytes).  There a 128 x 128 tile is 2-3 K-steps of work behind one DMA round trip
+// and the store tail, so the tile kernel above ran these at 2-3 TB/s (the Linears are
+// HBM-bound: 2 N + 2 K bytes per token for 2 N K flops).  Here a workgroup owns a 128-feature
+// slice of W -- resident in LDS for the whole launch -- and STREAMS token tiles of BM rows
+// through a ring of NBUF X buffers: the X rows of the next NBUF - 1 tiles are in flight
+// (LDS-DMA) while the current tile is multiplied and its outputs are staged and stored, so
+// HBM sees one continuous stream (one tile of prefetch was ~0.5 us of cover for ~1-2 us of
+// latency).
+//   * 4 waves, wave w = features 32w..32w+31 of the slice, all BM tokens (BM / 32 MFMA tiles);
+//   * images as the tile kernel's (128-B K-steps, chunks XOR-swizzled by (row >> 1) & 7);
+//     padding chunks past K are zeroed once and never loaded, sub-steps past K are skipped;
+//   * epilogue as the tile kernel's: bias (+ GELU), staged as the [BM][128] bf16 tile, 16-B
+//     row stores; a ring buffer is re-filled only after every wave has passed the barrier
+//     that follows the last read of it.
+// Counted waits: VMEM operations complete in issue order.  Tile j >= NBUF - 1 was requested in
+// iteration j - NBUF + 1, so at the top of tile j the wait leaves exactly what was issued after
+// it outstanding (NBUF - 1 tiles' stores and NBUF - 2 tiles' DMA); near the end of the
+// sequence, where fewer were issued, it waits for everything; the first NBUF - 1 tiles were
+// waited for after the prologue.
+template <int EPI, int NKS, int TM, int NBUF>
+__global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
+                                                                   const bf16* __restrict__ bias, bf16* __restrict__ Y,
+                                                                   bf16* __restrict__ Y2, int M, int N, int K) {
+  constexpr int BM = 32 * TM, BN = 128, NT = 256;
+  constexpr int WIMG = BN * kRowB, XIMG = BM * kRowB;                 // bytes per K-step image
+  constexpr int WB = NKS * WIMG, XB = NKS * XIMG, OB = BM * BN * 2;
+  constexpr int NCK = BN / 8;                                          // 16-B chunks per output row
+  constexpr int SPT = BM * NCK / NT;                                   // output stores per thread and pass
+  constexpr int XI = BM / 8 * NKS / 4;                                 // X DMA instructions per wave
+  static_assert(SPT * NT == BM * NCK && XI * 4 * 8 == BM * NKS, "tile shape");
+  constexpr int SPASS = (EPI >= 1 ? 2 : 1) * SPT;                     // stores per thread and tile
+  constexpr int WAITN = (NBUF - 1) * SPASS + (NBUF - 2) * XI;         // issued after a tile's DMA
+  static_assert(WAITN <= 63, "vmcnt");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[WB + NBUF * XB + OB + (EPI >= 1 ? kGeluEntries * 2 : 0)];
+  unsigned char* sW = smem;
+  unsigned char* sX = smem + WB;                                       // [NBUF][NKS][BM rows x 128 B]
+  unsigned char* sO = smem + WB + NBUF * XB;
+  unsigned short* sgelu = reinterpret_cast<unsigned short*>(sO + OB);
+  const int rowB = K * 2;
+  const int tilesM = (M + BM - 1) / BM, tilesN = (N + BN - 1) / BN;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int tn = wg % tilesN, g0 = wg / tilesN, G = gridDim.x / tilesN;   // token tiles g0, g0 + G, ...
+  if (g0 >= G || g0 >= tilesM) return;                                 // (uniform)
+  const int ntl = (tilesM - g0 + G - 1) / G;                           // this workgroup's tiles
+  const int n0 = tn * BN;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+  // zero the X ring and W (the chunks past K stay zero), then W by LDS-DMA
+  for (int i = threadIdx.x; i < (WB + NBUF * XB) / 16; i += NT) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
+  if (EPI >= 1)
+    for (int i = threadIdx.x; i < kGeluEntries / 8; i += NT)
+      reinterpret_cast<uint4*>(sgelu)[i] = reinterpret_cast<const uint4*>(kGeluTable)[i];
+  __syncthreads();
+  // W: NKS images of BN rows, 8 rows (1 KB) per wave instruction, lane L -> row 8j + L/8,
+  // physical chunk L%8 (the swizzle applied to the source chunk)
+  for (int blk = w; blk < NKS * BN / 8; blk += 4) {
+    const int ks = blk / (BN / 8), row = (blk % (BN / 8)) * 8 + (l >> 3);
+    const int chunk = (l & 7) ^ ((row >> 1) & 7), kb = ks * kRowB + chunk * 16;
+    if (kb < rowB) glds16(reinterpret_cast<const unsigned char*>(Wt) + (size_t)min(n0 + row, N - 1) * rowB + kb,
+                          sW + ks * WIMG + (blk % (BN / 8)) * 1024);
+  }
+  auto issue_x = [&](int j) {                                          // tile j of this workgroup
+    const int tm = g0 + j * G;
+    unsigned char* base = sX + (j % NBUF) * XB;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int blk = w * XI + i, ks = blk / (BM / 8), rb = blk % (BM / 8);
+      const int row = rb * 8 + (l >> 3);
+      const int chunk = (l & 7) ^ ((row >> 1) & 7), kb = ks * kRowB + chunk * 16;
+      if (kb < rowB)
+        glds16(reinterpret_cast<const unsigned char*>(X) + (size_t)min(tm * BM + row, M - 1) * rowB + kb,
+               base + ks * XIMG + rb * 1024);
+    }
+  };
+  auto so_off = [](int row, int chunk) { return row * (BN * 2) + ((chunk ^ (row & 15)) << 4); };
+  // this lane's bias values (features 32w + 8g + 4hh .. +3), once: a per-tile load from L2
+  // sat in the epilogue's critical path
+  bf16x4_t bvr[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int n = n0 + 32 * w + 8 * g + 4 * hh;
+    bvr[g] = (bias && n < N) ? *reinterpret_cast<const bf16x4_t*>(bias + n) : bf16x4_t{0, 0, 0, 0};
+  }
+  for (int j = 0; j < NBUF - 1 && j < ntl; ++j) issue_x(j);
+  wait_vm<0>();                                                        // W and the first tiles
+  for (int j = 0; j < ntl; ++j) {
+    if (j >= NBUF - 1) {                                               // (tiles < NBUF - 1: the prologue's wait)
+      if (j + NBUF - 2 < ntl) wait_vm<WAITN>();                        // tile j landed; later ops may fly
+      else wait_vm<0>();
+    }
+    raw_barrier();                                                     // every wave's DMA landed; ring slot free
+    if (j + NBUF - 1 < ntl) issue_x(j + NBUF - 1);                     // the slot of tile j - 1
+    // W fragments are re-read from LDS per tile: hoisted out of the tile loop they took the
+    // registers of a second wave per SIMD
+    asm volatile("" ::: "memory");
+    const unsigned char* xs = sX + (j % NBUF) * XB;
+    f32x16_t acc[TM];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) zero16(acc[t]);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        if (ks * 64 + kk * 16 >= K) break;                           // K % 8 == 0: whole 16-steps only
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sW + ks * WIMG + tile_off(32 * w + r, 2 * kk + hh));
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+          acc[t] = mfma16(a, *reinterpret_cast<const bf16x8_t*>(xs + ks * XIMG + tile_off(32 * t + r, 2 * kk + hh)),
+                          acc[t]);
+      }
+    }
+    const int m0 = (g0 + j * G) * BM;
+#pragma unroll
+    for (int pass = 0; pass < (EPI >= 1 ? 2 : 1); ++pass) {
+      if (pass) raw_barrier();                                         // pass 0's rows are stored
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const int row = 32 * t + r;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int f = 32 * w + 8 * g + 4 * hh;
+          const bf16x4_t bv = bvr[g];
+          bf16x4_t o;
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) {
+            const short pre = bf16_bits(acc[t][4 * g + e2] + bf16_bits_to_f32((unsigned short)bv[e2]));
+            o[e2] = (EPI >= 1 && pass == 0) ? (short)gelu_bits((unsigned short)pre, sgelu) : pre;
+          }
+          *reinterpret_cast<bf16x4_t*>(sO + so_off(row, f >> 3) + (f & 7) * 2) = o;
+        }
+      }
+      raw_barrier();
+      bf16* out = pass == 0 ? Y : Y2;
+#pragma unroll
+      for (int i = 0; i < SPT; ++i) {
+        const int idx = threadIdx.x + i * NT, row = idx / NCK, chunk = idx % NCK;
+        const int m = m0 + row, n = n0 + chunk * 8;
+        if (m < M && n < N)
+          *reinterpret_cast<uint4*>(out + (size_t)m * N + n) = *reinterpret_cast<const uint4*>(sO + so_off(row, chunk));
+      }
+    }
+  }
+}
+
 // bf16 rows [rows, K] -> e4m3 rows + one e8m0 scale byte per 32 elements (the largest
 // power of two 2^k with amax 2^k <= 448; scale byte 127 - k), 4 lanes per block
 __global__ void __launch_bounds__(256) mx_quantize_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ q,
@@ -355,6 +502,13 @@ extern "C" int vs_mx_quantize(const void* x, void* q, void* scales, int rows, in
   return VS_OK;
 }
 
+// VS_TGEMM_STREAM_ROWS: the least M for the streaming kernel (0 = never; default 32768)
+static int tgemm_stream_min_rows() {
+  const char* e = getenv("VS_TGEMM_STREAM_ROWS");
+  const int x = e ? atoi(e) : 32768;
+  return x <= 0 ? (1 << 30) : x;
+}
+
 extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, const void* w, const void* w_scales,
                              const void* bias, void* y, void* y_pre, void* y_q, void* y_qscales, int M, int N, int K,
                              void* stream) {
@@ -372,6 +526,31 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
            "alignment: x / w / y / y_pre 16 B, bias 8 B, scales / y_q 4 B");
   const bool qout = (mode & VS_TGEMM_QOUT) != 0;
   VS_CHECK(!qout || (gelu && y_q && y_qscales && N % 32 == 0), "quantised output: with gelu, N % 32 == 0, both buffers");
+  if (!f8 && !qout && N % 8 == 0 && K <= 192 && M >= tgemm_stream_min_rows()) {
+    // short rows, many tokens: the streaming kernel (W slice resident, token tiles streamed)
+    hipStream_t sst = (hipStream_t)stream;
+    // 32-row token tiles through a ring of 4 X buffers (3 tiles of prefetch), 2 workgroups
+    // per CU; K-steps of 3 (K > 128): a ring of 2 keeps 2 workgroups per CU
+    const int nks = (K * 2 + kRowB - 1) / kRowB;
+    const int tilesN = (N + 127) / 128, tilesM = (M + 31) / 32;
+    const int G = std::max(1, std::min(tilesM, 512 / tilesN));     // 2 workgroups per CU
+    const dim3 sgrid((unsigned)(G * tilesN));
+#define VS_TGS(E_, NK_, NB_)                                                                                     \
+  hipLaunchKernelGGL((token_gemm_stream_kernel<E_, NK_, 1, NB_>), sgrid, dim3(256), 0, sst, (const bf16*)x,      \
+                     (const bf16*)w, (const bf16*)bias, (bf16*)y, (bf16*)y_pre, M, N, K)
+    if (gelu) {
+      if (nks == 1) VS_TGS(1, 1, 4);
+      else if (nks == 2) VS_TGS(1, 2, 4);
+      else VS_TGS(1, 3, 2);
+    } else {
+      if (nks == 1) VS_TGS(0, 1, 4);
+      else if (nks == 2) VS_TGS(0, 2, 4);
+      else VS_TGS(0, 3, 2);
+    }
+#undef VS_TGS
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
   // the 256 x 256 tile where the product is MFMA-bound and fills the chip (VS_TGEMM_TILE=128
   // / 256 forces one, for A/B)
   static const int force = [] {

@@ -1214,10 +1214,24 @@ class _LinearFp8Fn(torch.autograd.Function):
 _LinearFp8RowFn.backward = _LinearFp8Fn.backward
 
 
+# fc1 + GELU fused into the STREAMING token GEMM (K <= 128, >= 32768 tokens: Swin-T stage 1):
+# one pass writes the pre-activation and the activation, 158 vs 203 us for the vendor GEMM +
+# ATen GELU at C2 stage 1 (profiles/r5_tgemm_stream_ab.txt); at K = 192 (stage 2) the fused
+# stream kernel's LDS leaves one workgroup per CU and the composition stays faster.
+# VS_TGEMM_STREAM_GELU=0: the composition there too (A/B)
+_STREAM_GELU = os.environ.get("VS_TGEMM_STREAM_GELU", "1") == "1"
+STREAM_MIN_ROWS = int(os.environ.get("VS_TGEMM_STREAM_ROWS", "32768"))
+
+
+def _stream_gelu_ok(x, w) -> bool:
+    return (_STREAM_GELU and STREAM_MIN_ROWS > 0 and w.shape[1] <= 128
+            and x.numel() // max(1, x.shape[-1]) >= STREAM_MIN_ROWS)
+
+
 def linear_gelu_tokens(x, w, b, fp8: bool = False):
     """gelu(F.linear(x, w, b)) with the exact erf GELU: fused into the token GEMM on
     token-heavy bf16 device tensors (_LinearGeluFn), the composition otherwise."""
-    if (_TGEMM_GELU or fp8) and _tgemm_ok(x, w, b):
+    if (_TGEMM_GELU or fp8 or _stream_gelu_ok(x, w)) and _tgemm_ok(x, w, b):
         return _LinearGeluFn.apply(x, w, b, bool(fp8 and w.shape[1] % 128 == 0 and w.shape[1] >= FP8_MIN_K))
     return ops.activation(linear_tokens(x, w, b), "gelu")
 
