@@ -10,6 +10,7 @@ from visionseg import linear as lin, ops  # noqa: E402
 
 DEV = "cuda"
 QUICK = "--quick" in sys.argv
+DGRAD_ONLY = "--dgrad-only" in sys.argv
 SHAPES = [  # (name, tokens, N out, K in)
     ("s1 qkv", 262144, 288, 96), ("s1 proj", 262144, 96, 96), ("s1 fc1", 262144, 384, 96),
     ("s1 fc2", 262144, 96, 384), ("s2 qkv", 65536, 576, 192), ("s2 fc1", 65536, 768, 192),
@@ -61,7 +62,7 @@ def timeit_eager(fn, n=20):
 def main():
     lin.load_gemm_table()
     tot_a = tot_b = 0.0
-    for name, T, N, K in SHAPES:
+    for name, T, N, K in ([] if DGRAD_ONLY else SHAPES):
         gy = torch.randn(T, N, device=DEV).to(torch.bfloat16)
         x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
         ta = timeit(lambda: ops.token_wgrad(gy, x, torch.bfloat16, bias=True))

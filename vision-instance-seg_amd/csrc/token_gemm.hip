@@ -533,7 +533,8 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
     // per CU; K-steps of 3 (K > 128): a ring of 2 keeps 2 workgroups per CU
     const int nks = (K * 2 + kRowB - 1) / kRowB;
     const int tilesN = (N + 127) / 128, tilesM = (M + 31) / 32;
-    const int G = std::max(1, std::min(tilesM, 512 / tilesN));     // 2 workgroups per CU
+    const int per_cu = (gelu && nks == 3) ? 1 : 2;                 // workgroups per CU (LDS)
+    const int G = std::max(1, std::min(tilesM, 256 * per_cu / tilesN));
     const dim3 sgrid((unsigned)(G * tilesN));
 #define VS_TGS(E_, NK_, NB_)                                                                                     \
   hipLaunchKernelGGL((token_gemm_stream_kernel<E_, NK_, 1, NB_>), sgrid, dim3(256), 0, sst, (const bf16*)x,      \
@@ -543,6 +544,8 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
       else if (nks == 2) VS_TGS(1, 2, 4);
       else VS_TGS(1, 3, 2);
     } else {
+      // (K-steps 4-6 with one workgroup per CU were measured slower than the tile kernel:
+      // profiles/r5_tgemm_stream_ab.txt)
       if (nks == 1) VS_TGS(0, 1, 4);
       else if (nks == 2) VS_TGS(0, 2, 4);
       else VS_TGS(0, 3, 2);

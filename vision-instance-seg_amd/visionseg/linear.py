@@ -281,8 +281,18 @@ def _addmm_into(c, a, b):
 _TGEMM_DGRAD = os.environ.get("VS_TGEMM_DGRAD", "1") == "1"
 
 
+# Which dX GEMMs take the token GEMM.  r5a (default): every T <= 300000 except the wide
+# reductions of smaller T.  r5b: only where the isolated dX measured faster than hipBLASLt's
+# dY W (tools/r5/wgrad_ab.py --dgrad-only, profiles/r5_dgrad_ab.txt: Swin-T stage 1 and the
+# wide-output encoder fc2) -- the C2 step measured the same with either (135.2 / 135.4 vs
+# 135.6 img/s on one box, profiles/r5_dgrad_rule_ab.txt), so the earlier rule stays
+_DGRAD_RULE = os.environ.get("VS_TGEMM_DGRAD_RULE", "r5a")
+
+
 def _use_token_gemm_dgrad(T: int, K_out: int, N_red: int) -> bool:
-    return T <= 300_000 and not (N_red >= 4 * K_out and T <= 100_000)
+    if _DGRAD_RULE == "r5a":
+        return T <= 300_000 and not (N_red >= 4 * K_out and T <= 100_000)
+    return T <= 300_000 and (T >= 200_000 or (K_out >= 4 * N_red and K_out >= 1024 and T >= 65536))
 
 
 def _dgrad_gemm(gy2, weight):
