@@ -1,11 +1,12 @@
-#!/bin/bash
-cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/r5
+# msda_bwd column kernel: integer W build vs f32 turns -- tests + kbench A/B
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r5m1
 mkdir -p $O
-timeout -k 10 500 python3 -u -m pytest -v tests/test_gpu_ops.py -k "msda" -s --timeout 250 -x > $O/msda_tests.log 2>&1
-rc=$?
-tail -2 $O/msda_tests.log
-grep -E "FAILED|Error|assert" $O/msda_tests.log | head -20 | cut -c1-300
-[ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python3 tools/kbench.py --only msda --msda-modes dst,col --iters 10 > $O/msda_kbench.log 2>&1
-cat $O/msda_kbench.log | grep -v amdgpu.ids
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_ops.py -k "msda" > $O/tests.log 2>&1; rc=$?
+tail -2 $O/tests.log
+[ $rc -eq 0 ] || exit $rc
+for w in 0 1 0 1; do
+  VS_MSDA_WINT=$w timeout -k 10 300 python3 -u tools/kbench.py --only msda --iters 20 > $O/kb_w$w.log 2>&1 || exit $?
+  echo "wint=$w: $(grep -i 'bwd' $O/kb_w$w.log | head -3 | tr '\n' ' ' | cut -c1-300)"
+done

@@ -1242,7 +1242,13 @@ __device__ __forceinline__ bf16x8_t tr8(const short* img, int pitch, int k0, int
 
 __device__ __forceinline__ int sgpr(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-template <int NCH>
+// WINT (default): W built as FIXED-POINT integers with no-return ds_add_u32 (quantum 2^-30; a
+// cell's W sums at most one level's attention weights times bilinear weights, <= 1, so no
+// partial leaves int32): the four points of a query hit the same cells, and as f32 they had
+// to take turns (4 wave-synchronised rounds of read-modify-write per (band, chunk) pair;
+// ds_add_f32 is 35x slower than the integer add on gfx950).  The product converts each W
+// value back (exact power-of-two scaling) before the bf16 hi / lo split.
+template <int NCH, bool WINT = true>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 3 ? 3 : 2)))
 msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ attw, const bf16* __restrict__ gout,
                     const bf16* __restrict__ value, float* __restrict__ gvalue, float* __restrict__ gloc,
@@ -1393,14 +1399,22 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
               }
             }
           }
+          if (WINT) {
 #pragma unroll
-          for (int pt = 0; pt < P; ++pt) {    // a query's 4 points are lanes of one wave: take turns
-            if (tpt == pt) {
+            for (int k = 0; k < 4; ++k)
+              if (cell[k] >= 0)
+                __hip_atomic_fetch_add(reinterpret_cast<int*>(sW) + cell[k] * kWP8 + tq, __float2int_rn(cw[k] * 0x1p30f),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
 #pragma unroll
-              for (int k = 0; k < 4; ++k)
-                if (cell[k] >= 0) sW[cell[k] * kWP8 + tq] += cw[k];
+            for (int pt = 0; pt < P; ++pt) {  // a query's 4 points are lanes of one wave: take turns
+              if (tpt == pt) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                  if (cell[k] >= 0) sW[cell[k] * kWP8 + tq] += cw[k];
+              }
+              wave_sync();
             }
-            wave_sync();
           }
           lds_barrier();
           if (wave < nmt) {                   // acc[cell][c] += W[cell][q] g[q][c]
@@ -1408,9 +1422,19 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
               const float* wr = sW + (32 * wave + r) * kWP8 + 16 * ks + 8 * hh;
-              const float4 w0 = *reinterpret_cast<const float4*>(wr);
-              const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
-              const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+              float wv[8];
+              if (WINT) {
+                const int4 i0 = *reinterpret_cast<const int4*>(wr);
+                const int4 i1 = *reinterpret_cast<const int4*>(wr + 4);
+                const int iv[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) wv[j] = (float)iv[j] * 0x1p-30f;
+              } else {
+                const float4 w0 = *reinterpret_cast<const float4*>(wr);
+                const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
+                wv[0] = w0.x; wv[1] = w0.y; wv[2] = w0.z; wv[3] = w0.w;
+                wv[4] = w1.x; wv[5] = w1.y; wv[6] = w1.z; wv[7] = w1.w;
+              }
               bf16x8_t ahi, alo;
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
@@ -2040,12 +2064,20 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     const int nch = ccy > 0 && ccx > 0 ? col_geo(lv, L, ccy, ccx, &cg) : 0;
     const long long nbc = nch > 0 ? (long long)B * cg.per_image * Hh : 0;
     if (mfma && fused && bt.mode == 1 && nch > 0 && nbc < (1LL << 31) && (long long)S * Hh * kD < (1LL << 24)) {
-      if (nch <= 3)
-        hipLaunchKernelGGL((msda_bwd_col_kernel<3>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,
-                           (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc);
-      else
-        hipLaunchKernelGGL((msda_bwd_col_kernel<6>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,
-                           (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc);
+      // VS_MSDA_WINT=0: the f32 W build with the points taking turns (A/B)
+      const char* we = getenv("VS_MSDA_WINT");
+      const bool wint = !(we && atoi(we) == 0);
+#define VS_COL(NC_, WI_)                                                                                        \
+  hipLaunchKernelGGL((msda_bwd_col_kernel<NC_, WI_>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,          \
+                     (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc)
+      if (nch <= 3) {
+        if (wint) VS_COL(3, true);
+        else VS_COL(3, false);
+      } else {
+        if (wint) VS_COL(6, true);
+        else VS_COL(6, false);
+      }
+#undef VS_COL
     } else if (mfma && fused && skel == 2)
       hipLaunchKernelGGL((msda_bwd_mfma_wg_kernel<8, 8, true, 2>), dim3((unsigned)nb2), dim3(256), 0, st, loc, attw,
                          (const bf16*)gout, gvalue, lv, bt, S, Hh, Q, L, (int)nb2, (const bf16*)value, gloc, gattw,
