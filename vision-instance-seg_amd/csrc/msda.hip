@@ -1248,7 +1248,8 @@ __device__ __forceinline__ int sgpr(int v) { return __builtin_amdgcn_readfirstla
 // to take turns (4 wave-synchronised rounds of read-modify-write per (band, chunk) pair;
 // ds_add_f32 is 35x slower than the integer add on gfx950).  The product converts each W
 // value back (exact power-of-two scaling) before the bf16 hi / lo split.
-template <int NCH, bool WINT = true>
+// DBG (timing-split instances, VS_MSDA_DBG): 1 no W build, 2 no product, 4 no Dm / dots, 8 no flush
+template <int NCH, bool WINT = true, int DBG = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 3 ? 3 : 2)))
 msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ attw, const bf16* __restrict__ gout,
                     const bf16* __restrict__ value, float* __restrict__ gvalue, float* __restrict__ gloc,
@@ -1399,7 +1400,8 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
               }
             }
           }
-          if (WINT) {
+          if (DBG & 1) {
+          } else if (WINT) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
               if (cell[k] >= 0)
@@ -1417,7 +1419,7 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
             }
           }
           lds_barrier();
-          if (wave < nmt) {                   // acc[cell][c] += W[cell][q] g[q][c]
+          if (!(DBG & 2) && wave < nmt) {     // acc[cell][c] += W[cell][q] g[q][c]
             const short* gs = sg + 64 * s * kD;
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
@@ -1449,7 +1451,7 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
           }
           lds_barrier();                      // W consumed: Dm^T overwrites it
           float* sD = sW;                     // Dm^T[cell][q], W's layout (pitch kWP8)
-          if (wave < nmt) {                   // Dm[q][cell] = g[q] . value[cell], cell tile = wave
+          if (!(DBG & 4) && wave < nmt) {     // Dm[q][cell] = g[q] . value[cell], cell tile = wave
 #pragma unroll
             for (int mq = 0; mq < 2; ++mq) {
               const short* ga = sg + (64 * s + 32 * mq + r) * kD + 8 * hh;
@@ -1476,7 +1478,7 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
           for (int rb = 0; rb < zr; rb += 16)
             *reinterpret_cast<float4*>(sW + (rb + zrow) * kWP8 + 16 * wave + 4 * (lane & 3)) = z4;
         }
-        if (any && wave < nmt) {              // one flush per (band, cell) for the whole column
+        if (!(DBG & 8) && any && wave < nmt) {   // one flush per (band, cell) for the whole column
           // cell -> (row, column) of the band by a multiply-shift (c < 128, bw <= 128: exact
           // with ceil(2^16 / bw)), 32-bit offsets from the (uniform) level base: the integer
           // division and 64-bit address of every flushed row were ~40 VALU per atomic
@@ -2070,7 +2072,17 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
 #define VS_COL(NC_, WI_)                                                                                        \
   hipLaunchKernelGGL((msda_bwd_col_kernel<NC_, WI_>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,          \
                      (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc)
-      if (nch <= 3) {
+      const char* dbe = getenv("VS_MSDA_DBG");
+      const int mdbg = dbe ? atoi(dbe) : 0;
+      if (nch <= 3 && mdbg > 0) {
+#define VS_COLD(D_)                                                                                             \
+  case D_:                                                                                                      \
+    hipLaunchKernelGGL((msda_bwd_col_kernel<3, true, D_>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,    \
+                       (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc); \
+    break;
+        switch (mdbg) { VS_COLD(1) VS_COLD(2) VS_COLD(4) VS_COLD(8) VS_COLD(15) default: break; }
+#undef VS_COLD
+      } else if (nch <= 3) {
         if (wint) VS_COL(3, true);
         else VS_COL(3, false);
       } else {
