@@ -1297,6 +1297,23 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
   const size_t rowstride = (size_t)Hh * kD;
   const size_t vbase = ((size_t)b * S * Hh + h) * kD;
   const int zrow = 4 * ((lane >> 2) & 3) + (lane >> 4);   // W clear: 16 rows x 4 quads per wave
+  // a level's sampling locations / weights are requested one level ahead: loaded at the top
+  // of their level, their round trip sat in front of the box reductions of every level
+  float2 xyn[NCH];
+  float awn[NCH];
+  auto load_level = [&](int l) {
+#pragma unroll
+    for (int s = 0; s < NCH; ++s) {
+      xyn[s] = make_float2(0.f, 0.f);
+      awn[s] = 0.f;
+      if (qid[s] >= 0) {
+        const long long o = (((long long)b * Q + qid[s]) * Hh + h) * LP + l * P + tpt;
+        xyn[s] = *reinterpret_cast<const float2*>(loc + o * 2);
+        awn[s] = attw[o];
+      }
+    }
+  };
+  load_level(0);
   for (int l = 0; l < L; ++l) {
     const int Hl = lv.h[l], Wl = lv.w[l];
     const size_t lbase = vbase + (size_t)lv.start[l] * rowstride;
@@ -1304,15 +1321,11 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
     float aw[NCH], dk[NCH][4];
 #pragma unroll
     for (int s = 0; s < NCH; ++s) {
-      xy[s] = make_float2(0.f, 0.f);
-      aw[s] = 0.f;
+      xy[s] = xyn[s];
+      aw[s] = awn[s];
       dk[s][0] = dk[s][1] = dk[s][2] = dk[s][3] = 0.f;
-      if (qid[s] >= 0) {
-        const long long o = (((long long)b * Q + qid[s]) * Hh + h) * LP + l * P + tpt;
-        xy[s] = *reinterpret_cast<const float2*>(loc + o * 2);
-        aw[s] = attw[o];
-      }
     }
+    if (l + 1 < L) load_level(l + 1);
     // per-chunk boxes of the in-level corners
     const int par = l & 1;
 #pragma unroll
