@@ -144,18 +144,26 @@ def pmc_traffic(op, path):
 
 def kernel_roofline(summary, pmc_path):
     """Pick the hand-written kernel with the largest total time and price it against the
-    roofline of its regime (HBM bytes for gather/copy kernels, matrix FLOP/s otherwise)."""
+    roofline of its regime: HBM bytes for gather/copy kernels and for any kernel whose
+    algorithmic intensity (FLOP per algorithmic byte) sits below the ridge point
+    MFMA peak / HBM peak (312.5 FLOP/B for bf16), matrix FLOP/s otherwise.  The other
+    ceiling's fraction is reported beside it (`frac_other`)."""
     if not summary:
         return None, {}
     name = max(summary, key=lambda k: summary[k]["total_ms"])
     s = summary[name]
     t = s["mean_ms"] / 1e3
     hbm_kernels = {"msda_fwd", "msda_bwd", "window_partition", "window_reverse", "attn_bitmask", "mask_head_fwd"}
-    if name in hbm_kernels:
+    ridge = MFMA_BF16_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    intensity = s["flops"] / s["bytes"] if s["bytes"] and s["flops"] else None
+    if name in hbm_kernels or (intensity is not None and intensity < ridge):
         ach = s["bytes"] / t / 1e9
         traffic, kernels = pmc_traffic(name, pmc_path)
         roof = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, kernel=name,
+                    intensity_flop_per_byte=round(intensity, 1) if intensity else None, ridge=ridge,
+                    frac_other=dict(bound="mfma", achieved=round(s["flops"] / t / 1e12, 2),
+                                    frac=round(s["flops"] / t / 1e12 / MFMA_BF16_PEAK_TFS, 5)) if s["flops"] else None,
                     traffic_source=(f"profiles/{os.path.basename(pmc_path)}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) "
                                     f"+ WRITE_SIZE per launch of {kernels}") if traffic else None,
                     algorithmic_bytes_per_launch=int(s["bytes"]), mean_launch_ms=round(s["mean_ms"], 4),
@@ -165,6 +173,7 @@ def kernel_roofline(summary, pmc_path):
         traffic, kernels = pmc_traffic(name, pmc_path)
         roof = dict(bound="mfma", achieved=round(ach, 2), peak=MFMA_BF16_PEAK_TFS, unit="TFLOP/s",
                     frac=round(ach / MFMA_BF16_PEAK_TFS, 5), traffic=traffic, kernel=name,
+                    intensity_flop_per_byte=round(intensity, 1) if intensity else None, ridge=ridge,
                     traffic_source=(f"profiles/{os.path.basename(pmc_path)}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) "
                                     f"+ WRITE_SIZE per launch of {kernels}") if traffic else None,
                     algorithmic_flops_per_launch=int(s["flops"]), mean_launch_ms=round(s["mean_ms"], 4),

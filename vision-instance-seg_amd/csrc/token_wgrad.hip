@@ -308,14 +308,16 @@ __global__ void __launch_bounds__(64 * WO * WI) token_wgrad_kernel(const WgGroup
 // dW[o][i] = sum_s (fragment-order partial of (o, i) in split s), db[o] = sum_s pbias[s][o],
 // fixed order, for the split Linears of a group.  A thread owns (o, 4 consecutive i): one
 // float4 per split (the 4 registers of a lane's group), consecutive threads take consecutive
-// o (= consecutive lanes: 16-B reads of one 1-KB block).  A 256-thread block = 64 items x 4
-// split groups (g, g + 4, ...), the group sums added in LDS in group order; a block's 64
-// items belong to one Linear (item0 is a multiple of 64).
-template <int BO, int BI, int WO, int WI>
-__global__ void __launch_bounds__(256) token_wgrad_reduce_kernel(const WgGroup grp, const float* __restrict__ part,
-                                                                 const float* __restrict__ pbias) {
+// o (= consecutive lanes: 16-B reads of one 1-KB block).  A block = 64 items x NG split
+// groups (g, g + NG, ...), the group sums added in LDS in group order; a block's 64 items
+// belong to one Linear (item0 is a multiple of 64).  NG = 16 when the items give few blocks
+// (a 96 x 288 Linear: 108 blocks of 4 groups left most CUs idle and each thread ~40
+// dependent-latency loads deep).
+template <int BO, int BI, int WO, int WI, int NG>
+__global__ void __launch_bounds__(64 * NG) token_wgrad_reduce_kernel(const WgGroup grp, const float* __restrict__ part,
+                                                                     const float* __restrict__ pbias) {
   constexpr int TO = BO / WO / 32, TI = BI / WI / 32;
-  __shared__ float4 sp[4][64];
+  __shared__ float4 sp[NG][64];
   const int it = threadIdx.x & 63, gq = threadIdx.x >> 6;
   const int item_blk = blockIdx.x * 64;
   int pi = -1;
@@ -348,17 +350,17 @@ __global__ void __launch_bounds__(256) token_wgrad_reduce_kernel(const WgGroup g
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (isw || isb) {
     int s = gq;
-    for (; s + 12 < S; s += 16) {
+    for (; s + 3 * NG < S; s += 4 * NG) {
       const float4 v0 = *reinterpret_cast<const float4*>(src + s * stride);
-      const float4 v1 = *reinterpret_cast<const float4*>(src + (s + 4) * stride);
-      const float4 v2 = *reinterpret_cast<const float4*>(src + (s + 8) * stride);
-      const float4 v3 = *reinterpret_cast<const float4*>(src + (s + 12) * stride);
+      const float4 v1 = *reinterpret_cast<const float4*>(src + (s + NG) * stride);
+      const float4 v2 = *reinterpret_cast<const float4*>(src + (s + 2 * NG) * stride);
+      const float4 v3 = *reinterpret_cast<const float4*>(src + (s + 3 * NG) * stride);
       a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
       a.x += v1.x; a.y += v1.y; a.z += v1.z; a.w += v1.w;
       a.x += v2.x; a.y += v2.y; a.z += v2.z; a.w += v2.w;
       a.x += v3.x; a.y += v3.y; a.z += v3.z; a.w += v3.w;
     }
-    for (; s < S; s += 4) {
+    for (; s < S; s += NG) {
       const float4 v = *reinterpret_cast<const float4*>(src + s * stride);
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
@@ -366,9 +368,12 @@ __global__ void __launch_bounds__(256) token_wgrad_reduce_kernel(const WgGroup g
   sp[gq][it] = a;
   __syncthreads();
   if (gq == 0 && (isw || isb)) {
-    const float4 b = sp[1][it], c = sp[2][it], d = sp[3][it];
-    const float r0 = ((a.x + b.x) + c.x) + d.x, r1 = ((a.y + b.y) + c.y) + d.y;
-    const float r2 = ((a.z + b.z) + c.z) + d.z, r3 = ((a.w + b.w) + c.w) + d.w;
+    float r0 = a.x, r1 = a.y, r2 = a.z, r3 = a.w;
+#pragma unroll
+    for (int k = 1; k < NG; ++k) {
+      const float4 b = sp[k][it];
+      r0 += b.x; r1 += b.y; r2 += b.z; r3 += b.w;
+    }
     if (isw)
       store4(P.dw, (size_t)o * K + i, grp.f32 != 0, r0, r1, r2, r3);
     else
@@ -567,11 +572,20 @@ extern "C" int vs_token_wgrad_grouped(int dtype, const vs_wgrad_problem* probs, 
     VS_LAUNCH_CHECK();
     if (pl.items > 0) {
       const dim3 gr((unsigned)(pl.items / 64));
-      if (cfg == 0)
-        hipLaunchKernelGGL((token_wgrad_reduce_kernel<256, 128, 4, 2>), gr, dim3(256), 0, st, pl.g,
+      // VS_WGRAD_REDUCE_GROUPS: 4 or 16 split groups per block (default: 16 below 512 blocks)
+      static const int rgroups = env_int("VS_WGRAD_REDUCE_GROUPS", 0);
+      const bool wide = rgroups == 16 || (rgroups != 4 && pl.items / 64 < 512);
+      if (cfg == 0 && wide)
+        hipLaunchKernelGGL((token_wgrad_reduce_kernel<256, 128, 4, 2, 16>), gr, dim3(1024), 0, st, pl.g,
+                           (const float*)part, (const float*)pb);
+      else if (cfg == 0)
+        hipLaunchKernelGGL((token_wgrad_reduce_kernel<256, 128, 4, 2, 4>), gr, dim3(256), 0, st, pl.g,
+                           (const float*)part, (const float*)pb);
+      else if (wide)
+        hipLaunchKernelGGL((token_wgrad_reduce_kernel<128, 128, 4, 2, 16>), gr, dim3(1024), 0, st, pl.g,
                            (const float*)part, (const float*)pb);
       else
-        hipLaunchKernelGGL((token_wgrad_reduce_kernel<128, 128, 4, 2>), gr, dim3(256), 0, st, pl.g,
+        hipLaunchKernelGGL((token_wgrad_reduce_kernel<128, 128, 4, 2, 4>), gr, dim3(256), 0, st, pl.g,
                            (const float*)part, (const float*)pb);
       VS_LAUNCH_CHECK();
     }
