@@ -537,13 +537,17 @@ __global__ void __launch_bounds__(kThreads) act_bwd_colsum_kernel(const T* __res
 }
 
 // out[c] = sum_b part[b][c] (b < nb) in a fixed order; columns [0, split) go to out0,
-// [split, split2) to out1, [split2, N) to out2.  A block = 32 columns x 8 row slices, 4
-// independent accumulators per thread (memory-level parallelism), slices combined in LDS.
+// [split, split2) to out1, [split2, N) to out2.  A block = 32 columns x 32 row slices (1024
+// threads), 4 independent accumulators per thread, slices combined in LDS: 512 partial rows
+// are one batch of 16 loads per thread.  (32 x 8 slices took four dependent batches: ~4.9
+// us per launch, 90 launches per C2 step, for < 2 MB read.)
+constexpr int kCsThreads = 1024, kCsSlices = kCsThreads / 32;
 template <typename T>
-__global__ void __launch_bounds__(kThreads) colsum_partials_kernel(const float* __restrict__ part, T* __restrict__ out0,
-                                                                   T* __restrict__ out1, int nb, int N, int split,
-                                                                   T* __restrict__ out2 = nullptr, int split2 = 1 << 30) {
-  __shared__ float red[8][33];
+__global__ void __launch_bounds__(kCsThreads) colsum_partials_kernel(const float* __restrict__ part, T* __restrict__ out0,
+                                                                     T* __restrict__ out1, int nb, int N, int split,
+                                                                     T* __restrict__ out2 = nullptr, int split2 = 1 << 30) {
+  constexpr int S = kCsSlices;
+  __shared__ float red[S][33];
   const int lane = threadIdx.x & 31;
   const int sl = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + lane;
@@ -552,23 +556,21 @@ __global__ void __launch_bounds__(kThreads) colsum_partials_kernel(const float* 
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (col < N) {
     int r = sl;
-    // unrolled: up to 16 independent loads in flight per thread (512 partials = 16 trips
-    // of 4 at one load batch each were the launch's latency); same summation order
 #pragma unroll 4
-    for (; r + 24 < nb; r += 32) {
+    for (; r + 3 * S < nb; r += 4 * S) {
       a0 += part[(size_t)r * N + col];
-      a1 += part[(size_t)(r + 8) * N + col];
-      a2 += part[(size_t)(r + 16) * N + col];
-      a3 += part[(size_t)(r + 24) * N + col];
+      a1 += part[(size_t)(r + S) * N + col];
+      a2 += part[(size_t)(r + 2 * S) * N + col];
+      a3 += part[(size_t)(r + 3 * S) * N + col];
     }
-    for (; r < nb; r += 8) a0 += part[(size_t)r * N + col];
+    for (; r < nb; r += S) a0 += part[(size_t)r * N + col];
   }
   red[sl][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (sl == 0 && col < N) {
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t += red[i][lane];
+    for (int i = 0; i < S; ++i) t += red[i][lane];
     if (col < split) out0[col] = from_f32<T>(t);
     else if (col < split2) out1[col - split] = from_f32<T>(t);
     else out2[col - split2] = from_f32<T>(t);
@@ -912,10 +914,10 @@ static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, co
   // dw / db (/ dx column sums) = column sums of the partial rows' thirds
   const int rgrid = (NR * C + 31) / 32;
   if (dtype == VS_BF16)
-    hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3(rgrid), dim3(kThreads), 0, st, part, (bf16*)dw, (bf16*)db,
+    hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3(rgrid), dim3(kCsThreads), 0, st, part, (bf16*)dw, (bf16*)db,
                        grid, NR * C, C, (bf16*)dsum, 2 * C);
   else
-    hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3(rgrid), dim3(kThreads), 0, st, part, (float*)dw,
+    hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3(rgrid), dim3(kCsThreads), 0, st, part, (float*)dw,
                        (float*)db, grid, NR * C, C, (float*)dsum, 2 * C);
   VS_LAUNCH_CHECK();
   return VS_OK;
@@ -937,11 +939,11 @@ extern "C" int vs_column_sum(int dtype, const void* x, void* out, void* ws, int 
   const size_t lds = (size_t)rowsets * Nb * sizeof(float);   // >= every column block's rowsets x Nb
   if (dtype == VS_BF16) {
     hipLaunchKernelGGL(colsum_kernel<bf16>, g2, dim3(kThreads), lds, st, (const bf16*)x, part, M, N);
-    hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part, (bf16*)out,
+    hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3((N + 31) / 32), dim3(kCsThreads), 0, st, part, (bf16*)out,
                        (bf16*)nullptr, grid, N, N);
   } else {
     hipLaunchKernelGGL(colsum_kernel<float>, g2, dim3(kThreads), lds, st, (const float*)x, part, M, N);
-    hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part,
+    hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kCsThreads), 0, st, part,
                        (float*)out, (float*)nullptr, grid, N, N);
   }
   VS_LAUNCH_CHECK();
@@ -979,7 +981,7 @@ extern "C" int vs_column_sum_segments(int dtype, const void* x, float* out, void
   else
     hipLaunchKernelGGL(colsum_seg_kernel<float>, dim3(nblk, nseg * B), dim3(kThreads), lds, st, (const float*)x,
                        part, B, S, N, seg);
-  hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32, nseg), dim3(kThreads), 0, st, part, out,
+  hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32, nseg), dim3(kCsThreads), 0, st, part, out,
                      (float*)nullptr, nblk * B, N, N);
   VS_LAUNCH_CHECK();
   return VS_OK;
@@ -1038,11 +1040,11 @@ extern "C" int vs_act_backward_colsum(int dtype, int act, const void* dy, const 
                      (const TT*)x, (TT*)dx, part, M, N)
   if (dtype == VS_BF16) {
     if (act) VS_ACTB(bf16, 1); else VS_ACTB(bf16, 0);
-    hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part,
+    hipLaunchKernelGGL(colsum_partials_kernel<bf16>, dim3((N + 31) / 32), dim3(kCsThreads), 0, st, part,
                        (bf16*)dx_colsum, (bf16*)nullptr, grid, N, N);
   } else {
     if (act) VS_ACTB(float, 1); else VS_ACTB(float, 0);
-    hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kThreads), 0, st, part,
+    hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kCsThreads), 0, st, part,
                        (float*)dx_colsum, (float*)nullptr, grid, N, N);
   }
 #undef VS_ACTB
