@@ -821,6 +821,22 @@ def test_window_attention_bf16_large_windows_vs_oracle(ws, shift, heads, nWh, nW
     assert e <= 2e-2 * float(tr.grad.abs().max()), e
 
 
+@pytest.mark.parametrize("P,H,T", [(5476, 3, 169), (400, 12, 169), (1444, 6, 169), (7, 3, 169), (13, 4, 529),
+                                   (64, 8, 529), (100, 48, 529), (9, 2, 8)])
+def test_window_table_grad_partial_sum(P, H, T):
+    """The relative-position-table gradient: per-window f32 partials summed by the column-sum
+    kernel (8 partial rows folded into one when heads * T % 8 != 0, remainder rows added)
+    against an f64 sum of the same partials; one f32 rounding per partial bounds the error."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(P * 7 + H)
+    part = torch.randn(P, H, T, generator=g)
+    ref = part.double().sum(0)
+    got = ops.table_grad_from_partials(part.to(DEV)).double().cpu()
+    assert got.shape == (H, T)
+    bound = P * 2.0 ** -23 * part.double().abs().sum(0) + 1e-30
+    assert bool(((got - ref).abs() <= bound).all()), float((got - ref).abs().max())
+
+
 @pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("ws,shift,heads,nWh,nWw,amp", [(12, 6, 4, 3, 3, 1.0), (7, 3, 3, 4, 4, 1.0), (12, 0, 2, 2, 2, 12.0),
                                                         (10, 5, 3, 3, 2, 1.0), (12, 6, 6, 4, 4, 0.0)])

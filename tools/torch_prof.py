@@ -33,6 +33,11 @@ def main():
     print("== top ops by device time (2 steps), with input shapes")
     for e in rows[:60]:
         print(f"{e.device_time_total / 1e3:8.2f} ms {e.count:5d}  {e.key[:40]:40s} {str(e.input_shapes)[:110]}")
+    print("\n== copies / sums / clones / casts by input shape")
+    sel = [e for e in rows if e.key in ("aten::copy_", "aten::sum", "aten::clone", "aten::_to_copy", "aten::contiguous",
+                                         "aten::add", "aten::cat", "aten::add_", "aten::fill_", "aten::mul")]
+    for e in sorted(sel, key=lambda e: -e.device_time_total)[:45]:
+        print(f"{e.device_time_total / 1e3:8.2f} ms {e.count:5d}  {e.key:18s} {str(e.input_shapes)[:150]}")
     ks = p.key_averages(group_by_stack_n=6)
     print("\n== copies / adds / sums / cats by stack")
     sel = [e for e in ks if e.key in ("aten::copy_", "aten::add", "aten::add_", "aten::sum", "aten::cat", "aten::mul",

@@ -254,6 +254,31 @@ def window_reverse(windows, batch: int, height: int, width: int, window: int, sh
     return _WindowReverse.apply(windows, int(batch), int(height), int(width), int(window), int(shift))
 
 
+_TABLE_SUM_ATEN = os.environ.get("VS_TABLE_SUM_ATEN", "0") == "1"   # A/B: the ATen dim-0 sum
+
+
+def table_grad_from_partials(part):
+    """f32 partials [P, heads, T] of the relative-position-table gradient (one per window,
+    from the window-attention backward) -> their sum [heads, T] through the column-sum
+    kernel (csrc/norm.hip; ATen's dim-0 sum took 82 us for the 5476 x 507 partials of a C2
+    stage-1 block).  Rows of heads*T % 8 != 0 are summed 8 partial rows at a time as one
+    row of 8 heads*T columns, the remainder rows (< 8) added after."""
+    P, H, T = part.shape
+    R = H * T
+    if _TABLE_SUM_ATEN:
+        return part.sum(0)
+    flat = part.reshape(P, R)
+    if R % 8 == 0 and R <= 16384:
+        return column_sum(flat).view(H, T)
+    q = P // 8
+    if q == 0 or 8 * R > 16384:
+        return part.sum(0)
+    s = column_sum(flat[:8 * q].reshape(q, 8 * R)).view(8, R).sum(0)
+    if P % 8:
+        s = s + flat[8 * q:].sum(0)
+    return s.view(H, T)
+
+
 class WindowAttentionFunction(torch.autograd.Function):
     """Swin window attention core with the relative-position bias and the shifted-window
     mask fused (HF:swin:373-398, 418-468, 584-607).
@@ -294,7 +319,7 @@ class WindowAttentionFunction(torch.autograd.Function):
                    flops=10.0 * Bw * heads * N * N * 32):
             gqkv, part = L.tops().win_attn_bwd(qkv, table, out, lse, g, heads, window, shift, nwin_h, nwin_w,
                                                scale, bool(fp8), True)
-        gtable = part.sum(0).t().contiguous().to(tdtype)
+        gtable = table_grad_from_partials(part).t().contiguous().to(tdtype)
         return gqkv, gtable, None, None, None, None, None, None, None
 
 
@@ -333,7 +358,7 @@ class WindowAttentionImageFunction(torch.autograd.Function):
                    flops=10.0 * Bw * heads * N * N * 32):
             gqkv, part = L.tops().win_attn_bwd_img(qkv, table, out, lse, g, heads, window, shift, nwin_h, nwin_w,
                                                    height, width, scale, bool(fp8))
-        gtable = part.sum(0).t().contiguous().to(tdtype)
+        gtable = table_grad_from_partials(part).t().contiguous().to(tdtype)
         return gqkv, gtable, None, None, None, None, None, None, None, None, None
 
 
