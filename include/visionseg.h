@@ -357,6 +357,26 @@ VS_API int vs_masked_attn_backward(int dtype, const void* q, const void* k, cons
                                    void* workspace, int batch, int num_query, int num_keys,
                                    int heads, float scale, void* stream);
 
+/* ---- a10: decoder self-attention core (csrc/self_attn.hip) ---------------------------
+ * Replaces the F.scaled_dot_product_attention of the decoder layers' self-attention
+ * (HF:m2f:1659-1664, Mask2FormerAttention over the queries; MaskDINO's decoder with its
+ * denoising-group mask, upstream dn_components, reached through training/train_template.py:104).
+ * q [B, Q, heads*32], k / v [B, S, heads*32] bf16, words u32 [Q, ceil(S/32)] (word_bstride = 0:
+ * shared by the batch) or [B, Q, ceil(S/32)] (word_bstride = Q*ceil(S/32)), bit j%32 of word
+ * j/32 = key j blocked, or NULL (no mask); out [B, Q, heads*32] bf16 (+ its f32 copy out_f32, for
+ * the backward; may be NULL), lse f32 [B, heads, Q]
+ * (+inf and a zero output row for a row blocked at every key).  bf16 only (f32 inputs: the
+ * vs_masked_attn_* kernels with explicit words). */
+VS_API int vs_self_attn_forward(int dtype, const void* q, const void* k, const void* v, const uint32_t* words,
+                                long long word_bstride, void* out, float* out_f32, float* lse, int batch,
+                                int num_query, int num_keys, int heads, float scale, void* stream);
+/* grad_out [B, Q, heads*32] -> grad_q, grad_k, grad_v (bf16, overwritten); one launch.  out_f32:
+ * the forward's f32 copy of the output (D = rowsum(grad_out * out) is formed from it). */
+VS_API int vs_self_attn_backward(int dtype, const void* q, const void* k, const void* v, const uint32_t* words,
+                                 long long word_bstride, const float* out_f32, const float* lse, const void* grad_out,
+                                 void* grad_q, void* grad_k, void* grad_v, int batch, int num_query, int num_keys,
+                                 int heads, float scale, void* stream);
+
 /* ---- Token-major LayerNorm and column sums (csrc/norm.hip) --------------------------
  * Replaces torch.nn.LayerNorm on the Swin blocks / patch merging / out-norms
  * (HF modeling_swin SwinLayer.layernorm_before/after, SwinPatchMerging.norm; reference

@@ -27,7 +27,7 @@ def pytest_configure(config):
 # The hot-path oracle files run first (then the f-rows'
 # device criterion and the configs), so that a failure in a "next"-row property test
 # under `-x` can never hide them; within a file pytest's order is kept.
-_FIRST = ("test_abi.py", "test_oracle_golden.py", "test_gpu_ops.py", "test_gpu_model.py",
+_FIRST = ("test_abi.py", "test_oracle_golden.py", "test_gpu_ops.py", "test_gpu_self_attn.py", "test_gpu_model.py",
           "test_gpu_train_parity.py", "test_gpu_match.py", "test_gpu_match_factors.py", "test_gpu_configs.py",
           "test_gpu_optim.py", "test_gpu_point_loss.py", "test_gpu_topk.py", "test_gpu_graphs.py",
           "test_gpu_fp8.py", "test_gpu_tgemm.py")

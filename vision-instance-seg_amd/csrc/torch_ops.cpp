@@ -394,6 +394,72 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> masked_xattn_bwd(const at::Tensor
   return {gq, gk, gv};
 }
 
+
+// ---- a10: decoder self-attention core (words: an empty tensor = no mask, [Q, nw] shared by the
+// batch, or [B, Q, nw])
+long long self_attn_words(const at::Tensor& words, int B, int Q, int S) {
+  if (words.numel() == 0) return -1;
+  const int64_t nw = (S + 31) / 32;
+  TORCH_CHECK(words.scalar_type() == at::kInt && words.is_contiguous(), "words must be contiguous int32");
+  if (words.dim() == 2) {
+    TORCH_CHECK(words.sizes() == at::IntArrayRef({(int64_t)Q, nw}), "words must be [Q, ceil(S/32)]");
+    return 0;
+  }
+  TORCH_CHECK(words.sizes() == at::IntArrayRef({(int64_t)B, (int64_t)Q, nw}), "words must be [B, Q, ceil(S/32)]");
+  return (long long)Q * nw;
+}
+
+void check_self_attn(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t heads) {
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == heads * 32, "q must be [B, Q, heads*32]");
+  TORCH_CHECK(k.sizes() == v.sizes() && k.dim() == 3 && k.size(0) == q.size(0) && k.size(2) == q.size(2),
+              "k / v must be [B, S, heads*32]");
+  TORCH_CHECK(q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 && v.scalar_type() == at::kBFloat16,
+              "self_attn takes bf16 q / k / v");
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> self_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                                 const at::Tensor& words, int64_t heads, double scale) {
+  on_device({&q, &k, &v});
+  check_self_attn(q, k, v, heads);
+  at::Tensor qc = q.contiguous(), kc = k.contiguous(), vc = v.contiguous();
+  const int B = as_int(q.size(0), "batch"), Q = as_int(q.size(1), "queries"), S = as_int(k.size(1), "keys");
+  const long long wbs = self_attn_words(words, B, Q, S);
+  if (wbs >= 0) on_device({&words});
+  at::Tensor out = at::empty_like(qc);
+  at::Tensor out32 = at::empty(qc.sizes(), qc.options().dtype(at::kFloat));
+  at::Tensor lse = at::empty({B, heads, Q}, qc.options().dtype(at::kFloat));
+  vs_ok(vs_self_attn_forward(VS_BF16, qc.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                             wbs >= 0 ? (const uint32_t*)words.data_ptr() : nullptr, wbs >= 0 ? wbs : 0,
+                             out.data_ptr(), out32.data_ptr<float>(), lse.data_ptr<float>(), B, Q, S, (int)heads,
+                             (float)scale, cur_stream(qc)),
+        "self_attn_fwd");
+  return {out, out32, lse};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> self_attn_bwd(const at::Tensor& q, const at::Tensor& k,
+                                                             const at::Tensor& v, const at::Tensor& words,
+                                                             const at::Tensor& out, const at::Tensor& lse,
+                                                             const at::Tensor& grad_out, int64_t heads, double scale) {
+  on_device({&q, &k, &v, &out, &lse, &grad_out});
+  check_self_attn(q, k, v, heads);
+  at::Tensor qc = q.contiguous(), kc = k.contiguous(), vc = v.contiguous();
+  at::Tensor oc = out.contiguous(), lc = lse.contiguous(), g = grad_out.to(at::kBFloat16).contiguous();
+  const int B = as_int(q.size(0), "batch"), Q = as_int(q.size(1), "queries"), S = as_int(k.size(1), "keys");
+  TORCH_CHECK(oc.sizes() == qc.sizes() && g.sizes() == qc.sizes() && oc.scalar_type() == at::kFloat,
+              "out (the forward's f32 copy) / grad_out must be shaped like q");
+  TORCH_CHECK(lc.scalar_type() == at::kFloat && lc.sizes() == at::IntArrayRef({(int64_t)B, heads, (int64_t)Q}),
+              "lse must be float32 [B, heads, Q]");
+  const long long wbs = self_attn_words(words, B, Q, S);
+  if (wbs >= 0) on_device({&words});
+  at::Tensor gq = at::empty_like(qc), gk = at::empty_like(kc), gv = at::empty_like(vc);
+  vs_ok(vs_self_attn_backward(VS_BF16, qc.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                              wbs >= 0 ? (const uint32_t*)words.data_ptr() : nullptr, wbs >= 0 ? wbs : 0,
+                              oc.data_ptr<float>(), lc.data_ptr<float>(), g.data_ptr(), gq.data_ptr(), gk.data_ptr(),
+                              gv.data_ptr(), B, Q, S, (int)heads, (float)scale, cur_stream(qc)),
+        "self_attn_bwd");
+  return {gq, gk, gv};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(visionseg, m) {
@@ -419,6 +485,9 @@ TORCH_LIBRARY(visionseg, m) {
   m.def("masked_xattn_fwd(Tensor q, Tensor k, Tensor v, Tensor words, int heads, float scale) -> (Tensor, Tensor)");
   m.def("masked_xattn_bwd(Tensor q, Tensor k, Tensor v, Tensor words, Tensor out, Tensor lse, Tensor grad_out, "
         "int heads, float scale) -> (Tensor, Tensor, Tensor)");
+  m.def("self_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor words, int heads, float scale) -> (Tensor, Tensor, Tensor)");
+  m.def("self_attn_bwd(Tensor q, Tensor k, Tensor v, Tensor words, Tensor out, Tensor lse, Tensor grad_out, "
+        "int heads, float scale) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(visionseg, CUDA, m) {
@@ -435,4 +504,6 @@ TORCH_LIBRARY_IMPL(visionseg, CUDA, m) {
   m.impl("attn_bitmask", attn_bitmask);
   m.impl("masked_xattn_fwd", masked_xattn_fwd);
   m.impl("masked_xattn_bwd", masked_xattn_bwd);
+  m.impl("self_attn_fwd", self_attn_fwd);
+  m.impl("self_attn_bwd", self_attn_bwd);
 }

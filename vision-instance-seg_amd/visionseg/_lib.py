@@ -67,6 +67,8 @@ SIGNATURES = {
     "vs_masked_attn_workspace_bytes": [_c_int] * 4,
     "vs_masked_attn_forward": [_c_int, _P, _P, _P, _P, _P, _P, _P] + [_c_int] * 4 + [_c_float, _P],
     "vs_masked_attn_backward": [_c_int] + [_P] * 11 + [_c_int] * 4 + [_c_float, _P],
+    "vs_self_attn_forward": [_c_int, _P, _P, _P, _P, ctypes.c_longlong, _P, _P, _P] + [_c_int] * 4 + [_c_float, _P],
+    "vs_self_attn_backward": [_c_int, _P, _P, _P, _P, ctypes.c_longlong] + [_P] * 6 + [_c_int] * 4 + [_c_float, _P],
     "vs_layer_norm_forward": [_c_int] + [_P] * 6 + [_c_int] * 2 + [_c_float, _P],
     "vs_layer_norm_backward_workspace_bytes": [_c_int] * 2,
     "vs_layer_norm_backward": [_c_int] + [_P] * 9 + [_c_int] * 2 + [_P],

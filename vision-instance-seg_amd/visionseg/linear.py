@@ -70,108 +70,8 @@ def _token_wgrad_ok(gy, x, out_dtype) -> bool:
             and x.data_ptr() % 16 == 0)
 
 
-class _DeferredWgrads:
-    """Token-Linear weight gradients collected during one backward and computed together by
-    ops.token_wgrad_grouped when the backward ends (deferred_weight_grads): with the tiles of
-    all the Linears filling the CUs, most run unsplit -- no f32 partials, no reduction -- and
-    ~90 launches become a few.  A Linear's backward returns its (not yet written) dW / db
-    tensors; autograd's AccumulateGrad adopts them as the parameters' .grad without a copy
-    (the step's gradients start as None, each weight is used once), and the flush fills them.
-    The flush verifies that every deferred parameter's .grad IS the returned tensor; a weight
-    used twice in one backward is computed immediately (the queue is flushed first)."""
-
-    def __init__(self):
-        self.items = {}        # out dtype -> [(gy, x, dw, db)]
-        self.checks = []       # (parameter, data_ptr its .grad must have)
-        self.seen = {}         # id(parameter) -> id(owner) that deferred it
-        self.refreshed = 0     # parameters whose .grad was a copy, refreshed after the flush
-        self.keep = []         # storages of the deferred outputs (alive until the flush)
-
-    def wants(self, params, owner=None) -> bool:
-        """False (after flushing) when a parameter was already deferred by another backward
-        call of this pass (a shared weight); `owner`: the backward call pushing several row
-        blocks of one fused parameter."""
-        keys = [id(p) for p in params if p is not None]
-        tag = id(owner) if owner is not None else None
-        if any(k in self.seen and (tag is None or self.seen[k] != tag) for k in keys):
-            self.flush()
-            return False
-        for k in keys:
-            self.seen[k] = tag
-        return True
-
-    def add(self, gy, x, dw, db, checks):
-        # addresses + storages only: a tensor reference here would make autograd copy the
-        # returned gradient instead of adopting it
-        self.keep.append(dw.untyped_storage())
-        if db is not None:
-            self.keep.append(db.untyped_storage())
-        self.items.setdefault(dw.dtype, []).append((gy, x, dw.data_ptr(), db.data_ptr() if db is not None else None))
-        self.checks.extend(checks)
-
-    def flush(self):
-        items, self.items = self.items, {}
-        keep, self.keep = self.keep, []
-        for dt, lst in items.items():
-            for k in range(0, len(lst), 64):
-                ops.token_wgrad_grouped(lst[k:k + 64], dt)
-        checks, self.checks = self.checks, []
-        for p, ptr, ref in checks:
-            if p.grad is None:
-                raise RuntimeError("deferred weight gradient: the parameter got no .grad")
-            if p.grad.data_ptr() != ptr:
-                # autograd copied the (still unwritten) returned tensor instead of adopting it
-                # (e.g. a gradient reaching the parameter through a view): refresh the copy
-                storage, off, size, stride = ref
-                src = torch.empty(0, device=p.grad.device, dtype=p.grad.dtype).set_(storage, off, size, stride)
-                if src.numel() != p.grad.numel():
-                    raise RuntimeError("deferred weight gradient: the parameter's .grad is not the tensor the "
-                                       "flush wrote")
-                p.grad.copy_(src.reshape(p.grad.shape))
-                self.refreshed += 1
-
-
-_DEFER = None
-
-
-class deferred_weight_grads:
-    """Context for a backward pass whose token-Linear weight gradients are batched into grouped
-    launches at its end (single-rank training: a DDP reducer's hooks would read the gradients
-    before the flush).  enabled=False: a no-op."""
-
-    def __init__(self, enabled: bool = True):
-        self.enabled = bool(enabled) and _TOKEN_WGRAD and _DEFER_WGRAD
-
-    def __enter__(self):
-        global _DEFER
-        self.prev = _DEFER
-        if self.enabled:
-            _DEFER = _DeferredWgrads()
-        return self
-
-    def __exit__(self, exc_type, exc, tb):
-        global _DEFER
-        q, _DEFER = _DEFER, self.prev
-        if self.enabled and exc_type is None:
-            q.flush()
-        return False
-
-
-# VS_DEFER_WGRAD=1: the Trainer's single-rank backward defers the token-Linear weight gradients
-# into grouped launches.  Off by default: 1370 instead of 1558 launches per C2 step, but the
-# same step time on the box (30.16 / 30.18 vs 30.13 ms, profiles/r5_defer_ab.txt) -- the chunk
-# loop, not the per-launch overhead, bounds these kernels
-_DEFER_WGRAD = os.environ.get("VS_DEFER_WGRAD", "0") == "1"
-
-
-def _leaf(t):
-    while t is not None and t._base is not None:
-        t = t._base
-    return t
-
-
 def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype, out: torch.Tensor | None = None,
-                bias: bool = False, params=None, ret=None, bias_out=None, owner=None):
+                bias: bool = False, bias_out=None):
     """dW = gy^T x for gy [K, M], x [K, N] -> [M, N] (out_dtype), f32 accumulation.  bf16
     token-heavy operands: the hand-written token weight-gradient kernel (ops.token_wgrad);
     otherwise a batched GEMM over S token chunks with f32 outputs, then one HIP epilogue
@@ -182,29 +82,6 @@ def weight_grad(gy: torch.Tensor, x: torch.Tensor, out_dtype: torch.dtype, out: 
     if _token_wgrad_ok(gy, x, out_dtype) and (out is None or (out.is_contiguous() and out.dtype == out_dtype
                                                                and out.data_ptr() % 16 == 0)) \
             and (bias_out is None or (bias_out.is_contiguous() and bias_out.data_ptr() % 16 == 0)):
-        q = _DEFER
-        # only for weights that ARE parameters (leaves, or views of one): a weight computed from
-        # parameters (a concatenation, a cast) hands its gradient on through autograd before the
-        # flush could write it
-        leaves = [_leaf(p) for p in params] if params is not None else None
-        if q is not None and leaves is not None and all(p is None or (p.is_leaf and p.requires_grad) for p in leaves) \
-                and q.wants(leaves, owner):
-            # params = (weight, bias or None); ret = the tensors this backward returns for them
-            # (default: dW / db themselves)
-            dw = out if out is not None else torch.empty(gy.shape[1], x.shape[1], device=gy.device, dtype=out_dtype)
-            db = None
-            if bias:
-                db = bias_out if bias_out is not None else torch.empty(gy.shape[1], device=gy.device, dtype=out_dtype)
-            rw, rb = ret if ret is not None else (dw, db)
-            def ref(t):   # enough to rebuild the returned tensor without holding a reference to it
-                return t.untyped_storage(), t.storage_offset(), tuple(t.shape), tuple(t.stride())
-
-            checks = [(_leaf(params[0]), rw.data_ptr(), ref(rw))]
-            if bias and len(params) > 1 and params[1] is not None:
-                checks.append((_leaf(params[1]), rb.data_ptr(), ref(rb)))
-            checks = [c for c in checks if not any(c[0] is p for p, _, _ in q.checks)]
-            q.add(gy, x, dw, db, checks)
-            return (dw, db) if bias else dw
         res = ops.token_wgrad(gy, x, out_dtype, bias=bias, out=out, bias_out=bias_out)
         return res
     gw = _vendor_weight_grad(gy, x, out_dtype, out)
@@ -310,7 +187,6 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, sink=None):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        ctx.bias_param = bias
         ctx.sink = sink
         if sink is not None:
             sink.arm()
@@ -334,9 +210,9 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1]).to(gy2.dtype)
             if want_b and gb is None and _token_wgrad_ok(gy2, x2, weight.dtype):
-                gw, gb = weight_grad(gy2, x2, weight.dtype, bias=True, params=(weight, ctx.bias_param))
+                gw, gb = weight_grad(gy2, x2, weight.dtype, bias=True)
             else:
-                gw = weight_grad(gy2, x2, weight.dtype, params=(weight,) if not want_b or gb is not None else None)
+                gw = weight_grad(gy2, x2, weight.dtype)
         if want_b and gb is None:
             if gy2.shape[1] % 8 == 0 and gy2.shape[1] <= ops.COLSUM_MAX_N:
                 gb = ops.column_sum(gy2).to(weight.dtype)          # HIP column sum, f32 accumulation
@@ -599,7 +475,6 @@ class _InProjFn(torch.autograd.Function):
         # dxv are summed into the sink's buffer by the dX GEMMs themselves (beta = 1), over
         # every layer that reads this level -- no add of the two, no add across layers
         ctx.kv_sink = kv_sink
-        ctx.bias_param = bias
         W = (weight[:D], weight[D:2 * D], weight[2 * D:])
         B = (bias[:D], bias[D:2 * D], bias[2 * D:])
         T = xq.numel() // D
@@ -672,8 +547,7 @@ class _InProjFn(torch.autograd.Function):
                 gx.append(gxi if ctx.needs_input_grad[i] else None)
             x2 = x2.to(g2.dtype)
             if _token_wgrad_ok(g2, x2, weight.dtype) and weight.dtype == g2.dtype:
-                weight_grad(g2, x2, weight.dtype, out=gw[rows], bias=True, bias_out=gb[rows],
-                            params=(weight, ctx.bias_param), ret=(gw, gb), owner=ctx)
+                weight_grad(g2, x2, weight.dtype, out=gw[rows], bias=True, bias_out=gb[rows])
                 continue
             weight_grad(g2, x2, weight.dtype, out=gw[rows])
             if D % 8 == 0 and D <= 2048 and g2.dtype == weight.dtype:
@@ -714,7 +588,6 @@ class _ValueQueryProjFn(torch.autograd.Function):
     def forward(ctx, h, pos, wv, bv, wp, bp, level_embed=None, level_sizes=None, sink=None):
         q = h + pos
         ctx.save_for_backward(h, q, wv, wp)
-        ctx.bv = bv
         ctx.level = (level_embed is not None, tuple(level_sizes or ()),
                      level_embed.dtype if level_embed is not None else None)
         ctx.sink = sink
@@ -741,8 +614,8 @@ class _ValueQueryProjFn(torch.autograd.Function):
             dh = gp2 @ wp_ if gres is None else _addmm_into(gres.reshape(gp2.shape[0], Dh), gp2, wp_)
             dh.addmm_(gv2, wv_)                                       # + value's share, in the GEMM epilogue
         h2, q2 = h.reshape(-1, Dh), q.reshape(-1, Dh)
-        gwv, gbv = weight_grad(gv2, h2.to(gv2.dtype), wv.dtype, bias=True, params=(wv, ctx.bv))
-        gwp = weight_grad(gp2, q2.to(gp2.dtype), wp.dtype, params=(wp,))
+        gwv, gbv = weight_grad(gv2, h2.to(gv2.dtype), wv.dtype, bias=True)
+        gwp = weight_grad(gp2, q2.to(gp2.dtype), wp.dtype)
 
         def bias_grad(g2, dt):
             if g2.shape[1] % 8 == 0 and g2.shape[1] <= ops.COLSUM_MAX_N:
@@ -1000,7 +873,7 @@ class _LinearReluFn(torch.autograd.Function):
             else:
                 gx = _dgrad_gemm(gp, weight).view(x.shape)
         if ctx.needs_input_grad[1]:
-            gw = weight_grad(gp, x.reshape(-1, x.shape[-1]).to(gp.dtype), weight.dtype, params=(weight,))
+            gw = weight_grad(gp, x.reshape(-1, x.shape[-1]).to(gp.dtype), weight.dtype)
         if ctx.needs_input_grad[2]:
             gb = cs.to(weight.dtype)
         return gx, gw, gb, None
@@ -1176,7 +1049,7 @@ class _LinearGeluFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = (_dgrad(gp, weight) if ctx.fp8 else _dgrad_gemm(gp, weight)).view(x.shape)
         if ctx.needs_input_grad[1]:
-            gw = weight_grad(gp, x.reshape(-1, x.shape[-1]), weight.dtype, params=(weight,))
+            gw = weight_grad(gp, x.reshape(-1, x.shape[-1]), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = cs.to(weight.dtype)
         return gx, gw, gb, None, None, None, None
@@ -1209,7 +1082,7 @@ class _LinearFp8Fn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = _dgrad(gy2, weight).view(x.shape)
         if ctx.needs_input_grad[1]:
-            gw = weight_grad(gy2, x.reshape(-1, x.shape[-1]).to(gy2.dtype), weight.dtype, params=(weight,))
+            gw = weight_grad(gy2, x.reshape(-1, x.shape[-1]).to(gy2.dtype), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             cs = ops.take_colsum(gy)
             if cs is not None:

@@ -43,7 +43,7 @@ import torch.nn.functional as F
 
 from . import ops
 from .linear import SmallLinear, TokenLayerNorm, TokenLinear, linear_tokens
-from .model import M2FConfig, PixelDecoder, SwinBackbone, _compute_dtype
+from .model import M2FConfig, PixelDecoder, SwinBackbone, _compute_dtype, self_attention_core
 
 
 @dataclass
@@ -199,15 +199,13 @@ class DINODecoderLayer(nn.Module):
         self.linear2 = SmallLinear(ffn, d)
         self.norm3 = TokenLayerNorm(d)
 
-    def forward(self, tgt, qpos, boxes, memory, shapes, attn_mask):
+    def forward(self, tgt, qpos, boxes, memory, shapes, attn_words):
         B, Q, D = tgt.shape
         H, dh = self.heads, D // self.heads
         qk = tgt + qpos
-        q = self.q_proj(qk).view(B, Q, H, dh).transpose(1, 2)
-        k = self.k_proj(qk).view(B, Q, H, dh).transpose(1, 2)
-        v = self.v_proj(tgt).view(B, Q, H, dh).transpose(1, 2)
-        att = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask)
-        _, tgt = self.norm2.add_forward(tgt, self.out_proj(att.transpose(1, 2).reshape(B, Q, D)))
+        # attn_words: the DN-group mask as bitmask words [Q, ceil(Q/32)] (True = blocked), or None
+        att = self_attention_core(self.q_proj(qk), self.k_proj(qk), self.v_proj(tgt), H, dh ** -0.5, attn_words)
+        _, tgt = self.norm2.add_forward(tgt, self.out_proj(att))
         ca = self.cross_attn(tgt + qpos, boxes, memory, shapes)
         _, tgt = self.norm1.add_forward(tgt, ca)
         _, tgt = self.norm3.add_forward(tgt, self.linear2(F.relu(self.linear1(tgt))))
@@ -336,14 +334,14 @@ class MaskDINODecoder(nn.Module):
         interm = dict(classes=i_cls, masks=i_mask, boxes=ref_undetach.sigmoid())
         tgt = tgt_undetach.detach()
         ref_unsig = ref_undetach.detach()
-        attn_mask, dn = None, None
+        attn_words, dn = None, None
         if c.dn and self.training and targets is not None and targets.kc > 0:
             made = self._dn(targets, boxes, B, dev, dtype)
             if made is not None:
                 emb, dn_unsig, blocked, dn = made
                 tgt = torch.cat((emb, tgt), 1)
                 ref_unsig = torch.cat((dn_unsig.float(), ref_unsig), 1)
-                attn_mask = ~blocked                                                 # SDPA: True = attend
+                attn_words = ops.pack_blocked(blocked)                               # bit set = blocked
         # ---- initial prediction + decoder layers with iterative box refinement
         cls0, mask0 = self.heads(tgt, mf, Hm, Wm, sink)
         classes, masks = [cls0], [mask0]
@@ -352,7 +350,7 @@ class MaskDINODecoder(nn.Module):
         out = tgt
         for layer in self.layers:
             qpos = self.ref_point_head(sine_embed_boxes(ref, c.hidden_dim).to(dtype))
-            out = layer(out, qpos, ref, memory, shapes, attn_mask)
+            out = layer(out, qpos, ref, memory, shapes, attn_words)
             new_ref = (self.bbox_embed(out).float() + inverse_sigmoid(ref)).sigmoid()
             ref = new_ref.detach()
             refs.append(new_ref)

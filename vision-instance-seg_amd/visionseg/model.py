@@ -589,6 +589,23 @@ class PixelDecoder(nn.Module):
 # ----------------------------------------------------------------------------------
 
 
+def self_attention_core(q, k, v, heads, scale, words=None):
+    """softmax(q k^T * scale [+ blocked keys]) v over [B, Q, heads*d] token rows -> [B, Q, heads*d]:
+    the hand-written kernels (ops.self_attention: csrc/self_attn.hip for bf16, the scalar
+    masked-attention kernels for f32) on the device; the plain composition on the CPU."""
+    if q.is_cuda and q.shape[-1] == 32 * heads:
+        return ops.self_attention(q, k, v, heads, scale, words=words)
+    B, Q, D = q.shape
+    S = k.shape[1]
+    d = D // heads
+    s = torch.einsum("bqhd,bkhd->bhqk", q.view(B, Q, heads, d).float(), k.view(B, S, heads, d).float()) * scale
+    if words is not None:
+        blocked = ops.unpack_bitmask(words, S)
+        s = s.masked_fill((blocked if blocked.dim() == 3 else blocked[None])[:, None], float("-inf"))
+    att = torch.einsum("bhqk,bkhd->bqhd", s.softmax(-1), v.view(B, S, heads, d).float())
+    return att.reshape(B, Q, D).to(q.dtype)
+
+
 class CrossAttn(nn.Module):
     def __init__(self, d):
         super().__init__()
@@ -633,11 +650,8 @@ class DecoderLayer(nn.Module):
         _, h = self.norm_cross.add_forward(h, self.cross_attn.out_proj(o), sink=s1)   # post-norm, fused add
         sa = self.self_attn
         q_, k_, v_ = self_attn_in_proj(h, qpos, sa.q_proj, sa.k_proj, sa.v_proj, sink=s2, psink=psink)
-        qs = q_.view(B, Q, H, d).transpose(1, 2)
-        ks = k_.view(B, Q, H, d).transpose(1, 2)
-        vs = v_.view(B, Q, H, d).transpose(1, 2)
-        att = F.scaled_dot_product_attention(qs, ks, vs)
-        _, h = self.norm_self.add_forward(h, sa.out_proj(att.transpose(1, 2).reshape(B, Q, D)), sink=s2)
+        att = self_attention_core(q_, k_, v_, H, d ** -0.5)          # HF:m2f:1659-1664
+        _, h = self.norm_self.add_forward(h, sa.out_proj(att), sink=s2)
         f = small_linear(h, self.fc1.weight, self.fc1.bias, relu=True, sink=s3)
         _, h = self.norm_ffn.add_forward(h, self.fc2(f), sink=s3)
         return h

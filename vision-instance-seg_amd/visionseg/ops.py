@@ -964,7 +964,11 @@ class MaskedAttentionFunction(torch.autograd.Function):
         S = k.shape[1]
         nb = (q.numel() * 4 + 2 * k.numel() + 2 * v.numel()) * q.element_size() + words.numel() * 4
         with timed("masked_attn_bwd", q, bytes_=nb, flops=10.0 * B * heads * Q * S * 32):
-            gq, gk, gv = L.tops().masked_xattn_bwd(q, k, v, words, out, lse, g, heads, scale)
+            try:
+                gq, gk, gv = L.tops().masked_xattn_bwd(q, k, v, words, out, lse, g, heads, scale)
+            except RuntimeError as e:
+                raise RuntimeError(f"{e} (q {q.dtype} {tuple(q.shape)}, k {k.dtype} {tuple(k.shape)}, out "
+                                   f"{out.dtype}, lse {lse.dtype}, grad {g.dtype} {tuple(g.shape)})") from e
         return gq, gk, gv, None, None, None
 
 
@@ -972,6 +976,73 @@ def masked_attention(q, k, v, words, heads: int, scale: float | None = None):
     if scale is None:
         scale = 32 ** -0.5
     return MaskedAttentionFunction.apply(q, k, v, words, int(heads), float(scale))
+
+
+def pack_blocked(blocked):
+    """bool [..., S] (True = blocked) -> int32 words [..., ceil(S/32)], bit j%32 of word j/32
+    set = key j blocked (the layout of attn_bitmask / the self-attention kernels)."""
+    S = blocked.shape[-1]
+    nw = (S + 31) // 32
+    b = F.pad(blocked.to(torch.int64), (0, nw * 32 - S)).view(*blocked.shape[:-1], nw, 32)
+    w = (b << torch.arange(32, device=blocked.device, dtype=torch.int64)).sum(-1)
+    return torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32).contiguous()
+
+
+_NO_WORDS: dict = {}
+
+
+class SelfAttentionFunction(torch.autograd.Function):
+    """Decoder self-attention core (HF:m2f:1659-1664; MaskDINO's DN-masked self-attention):
+    softmax over the unblocked keys of (q.k) * scale, times V.  q / k / v [B, Q, heads*32] bf16;
+    words: None, or int32 [Q, nw] shared by the batch / [B, Q, nw] (pack_blocked).  One
+    forward and one backward launch (csrc/self_attn.hip), f32 softmax and dS, P / dS as
+    exact bf16 hi + lo pairs in the products."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, words, heads, scale):
+        L.require_hip(q, k, v)
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        B, Q, C = q.shape
+        S = k.shape[1]
+        if words is None:
+            key = q.device
+            words = _NO_WORDS.get(key)
+            if words is None:
+                words = _NO_WORDS[key] = torch.empty(0, device=q.device, dtype=torch.int32)
+        nb = (2 * q.numel() + k.numel() + v.numel()) * 2 + q.numel() * 4 + words.numel() * 4
+        with timed("self_attn_fwd", q, bytes_=nb, flops=4.0 * B * heads * Q * S * 32):
+            out, out32, lse = L.tops().self_attn_fwd(q, k, v, words, heads, float(scale))
+        ctx.meta = (heads, float(scale))
+        ctx.save_for_backward(q, k, v, words, out32, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        q, k, v, words, out32, lse = ctx.saved_tensors
+        heads, scale = ctx.meta
+        B, Q, C = q.shape
+        S = k.shape[1]
+        nb = (4 * q.numel() + 2 * k.numel() + 2 * v.numel()) * 2 + out32.numel() * 4 + words.numel() * 4
+        with timed("self_attn_bwd", q, bytes_=nb, flops=10.0 * B * heads * Q * S * 32):
+            gq, gk, gv = L.tops().self_attn_bwd(q, k, v, words, out32, lse, g, heads, scale)
+        return gq, gk, gv, None, None, None
+
+
+def self_attention(q, k, v, heads: int, scale: float | None = None, words=None):
+    """Decoder self-attention core on the HIP kernels: bf16 -> SelfAttentionFunction; f32
+    (the parity kernel mode) -> the scalar masked-attention kernels with explicit words
+    (all-zero when there is no mask).  No SDPA, no fallback."""
+    if scale is None:
+        scale = 32 ** -0.5
+    if q.dtype == torch.bfloat16:
+        return SelfAttentionFunction.apply(q, k.to(q.dtype), v.to(q.dtype), words, int(heads), float(scale))
+    B, Q, _ = q.shape
+    S = k.shape[1]
+    if words is None:
+        words = torch.zeros(B, Q, (S + 31) // 32, device=q.device, dtype=torch.int32)
+    elif words.dim() == 2:
+        words = words.unsqueeze(0).expand(B, -1, -1).contiguous()
+    return masked_attention(q, k, v, words, heads, scale)
 
 
 # ------------------------------------------------------------------ LayerNorm / bias grad

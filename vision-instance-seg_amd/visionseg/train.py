@@ -32,7 +32,6 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
-from . import linear as linear_mod
 from .optim import FlatOptimizer, GradReducer
 
 
@@ -198,11 +197,7 @@ class Trainer:
         if self.reducer is not None:
             self.reducer.begin(reduce_mode)
         loss, parts = self.forward_loss(images, mask_labels, class_labels)
-        # single rank: the token-Linear weight gradients are batched into grouped launches at
-        # the end of the backward (linear.deferred_weight_grads); a reducer's hooks would read
-        # them before that, so with one the gradients are computed in place
-        with linear_mod.deferred_weight_grads(enabled=self.reducer is None):
-            loss.backward()
+        loss.backward()
         if self.reducer is not None:
             self.reducer.finish_backward()
         else:
