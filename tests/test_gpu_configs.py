@@ -1,6 +1,7 @@
 """BASELINE configs C3, C4 and C5 exercised at their own workloads on one GPU (the
-per-GPU share of the 8-GPU runs): Swin-B at 1024^2 against the oracle, one Swin-L
-MaskDINO training step with 300 queries at 1024^2 (eager and graph-replayed), and one
+per-GPU share of the 8-GPU runs): Swin-B at 1024^2 against the oracle, Swin-L MaskDINO
+training steps with 300 queries at 4 x 1024^2 (eager and graph-replayed), Swin-L
+Mask2Former at 1536^2 against the oracle (fp32 kernel mode and the bf16 path), and one
 Swin-L 1536^2 training step with fp8 window attention plus its forward logits against the
 bf16-attention path.  The smaller-shape versions of these checks live in
 test_gpu_model.py, test_gpu_maskdino.py and test_gpu_fp8.py."""
@@ -99,7 +100,7 @@ def test_c4_swin_l_maskdino_300q_1024_step_and_graph_replay():
     from visionseg.train import SolverConfig, Trainer
     cfg = MaskDINOConfig.preset("swin_l", num_queries=300)
     m = MaskDINO(cfg).init_weights(0)
-    batch = synthetic_batch(2, 1024, seed=42, device=DEV)
+    batch = synthetic_batch(4, 1024, seed=42, device=DEV)          # C4's per-GPU batch (32 / 8)
     ta = Trainer(copy.deepcopy(m), MaskDINOCriterion(cfg), SolverConfig(warmup_iters=0), device=DEV)
     tb = Trainer(m, MaskDINOCriterion(cfg), SolverConfig(warmup_iters=0), device=DEV, graphs=True)
     la, lb = [], []
@@ -117,6 +118,38 @@ def test_c4_swin_l_maskdino_300q_1024_step_and_graph_replay():
     assert all(np.isfinite(la + lb))
     for a, b in zip(la, lb):
         assert abs(a - b) <= 3e-2 * max(1.0, abs(a)), (la, lb)
+
+
+def test_c5_swin_l_1536_vs_oracle():
+    """C5's backbone + decoder at C5's own input size (Swin-L + Mask2Former, ws 12, 1536^2) vs
+    the oracle with the oracle's attention masks forced in: fp32 kernel mode within the
+    BASELINE bound 1e-3 (mask and class logits), the bf16 production path (bf16 window
+    attention) within max 0.05 / mean 0.006 of the max |logit| (the C3 bounds).  The fp8
+    attention numerics are checked against this bf16 path in the next test."""
+    from oracle.ref_model import RefConfig, RefMask2Former
+    from visionseg.model import M2FConfig, Mask2Former
+    cfg = M2FConfig.preset("swin_l")
+    m = _perturbed(Mask2Former(cfg).init_weights(0))
+    ref = RefMask2Former(RefConfig.from_dict(cfg.to_dict()))
+    ref.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
+    ref.eval()
+    m = m.to(DEV).eval()
+    px = torch.randn(1, 3, 1536, 1536, generator=torch.Generator().manual_seed(6)).to(torch.bfloat16).float()
+    with torch.no_grad():
+        ref.decoder.record = True
+        rmasks, rclasses = ref(px)
+        m.decoder.mask_override = [rb for rb, _ in ref.decoder.trace]
+        fmasks, fclasses = m(px.to(DEV))
+        f32err = max(float((a.cpu() - b).abs().max()) for a, b in zip(fmasks, rmasks))
+        cerr = max(float((a.cpu() - b).abs().max()) for a, b in zip(fclasses, rclasses))
+        del fmasks
+        m = m.to(torch.bfloat16)
+        bmasks, _ = m(px.to(DEV).to(torch.bfloat16))
+    ours = _rel(bmasks, rmasks)
+    print(f"C5 swin_l@1536: fp32-mode mask-logit max|err| {f32err:.2e} (class {cerr:.2e}); bf16 production "
+          f"max|err|/max|logit| {ours[0]:.2e}, mean {ours[1]:.2e}")
+    assert f32err <= 1e-3 and cerr <= 1e-3
+    assert ours[0] <= 0.05 and ours[1] <= 0.006
 
 
 def test_c5_swin_l_1536_fp8_step_and_logits():

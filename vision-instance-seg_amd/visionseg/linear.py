@@ -21,8 +21,12 @@ from . import ops
 import ctypes
 import os
 
-# split when K is at least this many tokens; chunks never drop below MIN_CHUNK rows
-MIN_TOKENS = int(os.environ.get("VS_SPLITK_MIN_TOKENS", "16384"))
+# Linears over at least this many tokens take the token path (_LinearFn: the token GEMM where
+# its shape rule picks it, token_wgrad with the fused bias column sums, residual sinks).  4096
+# (round 6) takes in Swin-T stage 4 (4 x 32 x 32 tokens), whose bias gradients were ATen
+# reductions (16 launches, 0.30 ms of the C2 step, profiles/r6_step_graph_c2_selfattn.txt);
+# measured +0.4 % img/s against 16384 at the end of round 5 (profiles/r5_min_tokens_ab.txt)
+MIN_TOKENS = int(os.environ.get("VS_SPLITK_MIN_TOKENS", "4096"))
 
 GEMM_TABLE = os.environ.get("VS_GEMM_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                              "tuning", "tunableop_mi355x.csv")
