@@ -312,7 +312,8 @@ VS_API int vs_point_scatter(const float* grad_points, const float* grid, float* 
 
 /* Point gather for the mask losses' labels: out f32 [N, P] = bilinear sample (point_sample
  * = grid_sample, align_corners=False, zero padding; HF:m2f:245-275) of maps f32 [M, H, W]
- * row rows[n] (int64 [N], each in [0, M)) at coords f32 [N, P, 2] in [0, 1] (x, y). */
+ * row rows[n] (int64 [N], each in [0, M); or NULL: set n reads map n, N <= M) at coords f32
+ * [N, P, 2] in [0, 1] (x, y). */
 VS_API int vs_point_sample_rows(const float* maps, const long long* rows, const float* coords, float* out,
                                 int num_maps, int height, int width, int num_sets, int num_points, void* stream);
 

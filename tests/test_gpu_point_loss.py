@@ -109,3 +109,23 @@ def test_point_sample_masks_equals_grid_sample():
                             align_corners=False).view(S * NP, P)
         got = ops.point_sample_masks(masks.view(NP, H, W), coords, rows=rows)
         assert float((got - exp).abs().max()) <= 1e-6
+
+
+def test_point_sample_f32_maps_equals_grid_sample():
+    """ops.point_sample (the criterion's uncertainty / matched-logit points and MaskDINO's, on
+    csrc/mask_head.hip point_sample_rows_kernel with no row map) == grid_sample (HF:m2f:245-275
+    point_sample) on f32 maps, incl. points on the border and outside [0, 1]; autograd inputs
+    keep grid_sample."""
+    import torch.nn.functional as F
+    from visionseg import ops
+    g = torch.Generator(device="cuda").manual_seed(12)
+    for N, H, W, P in ((3, 37, 53, 100), (80, 256, 256, 37632)):
+        maps = torch.randn(N, 1, H, W, device="cuda", generator=g) * 4
+        coords = torch.rand(N, P, 2, device="cuda", generator=g) * 1.2 - 0.1
+        coords[0, :3] = torch.tensor([[0.0, 0.0], [1.0, 1.0], [0.5, 0.5]], device="cuda")
+        exp = F.grid_sample(maps, 2.0 * coords.unsqueeze(2) - 1.0, align_corners=False).view(N, P)
+        got = ops.point_sample(maps, coords)
+        assert float((got - exp).abs().max()) <= 1e-5 * float(maps.abs().max())
+    m = maps[:2].clone().requires_grad_(True)
+    ops.point_sample(m, coords[:2]).sum().backward()
+    assert m.grad is not None

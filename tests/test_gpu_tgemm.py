@@ -152,14 +152,12 @@ def test_token_gemm_fp8_vs_dequantised(M, N, K, gelu):
 
 @pytest.mark.parametrize("fp8", [False, True])
 def test_linear_gelu_autograd_vs_f64(monkeypatch, fp8):
-    """linear.linear_gelu_tokens (fc1 + GELU on the token GEMM, the backward through the
-    fused GELU-derivative + column-sum pass, the vendor dX GEMM and the split-K dW) vs torch
-    autograd in f64 on the same bf16 operands (fp8: the forward on the MX MFMA, the backward
-    straight-through, so the gradients match the bf16 formula up to the fp8 forward's
-    pre-activation error)."""
-    from visionseg import linear
+    """linear.linear_gelu_tokens vs torch autograd in f64 on the same bf16 operands: bf16 at
+    this shape = the GEMM + the GELU pass (ops.activation), the backward through the fused
+    GELU-derivative + column-sum pass; fp8 = the token GEMM with the GELU epilogue on the MX
+    MFMA, the backward straight-through, so the gradients match the bf16 formula up to the fp8
+    forward's pre-activation error."""
     from visionseg.linear import linear_gelu_tokens
-    monkeypatch.setattr(linear, "_TGEMM_GELU", True)
     g = torch.Generator().manual_seed(11)
     M, K, N = 20000, 384, 1536
     x = _rand((M, K), g)

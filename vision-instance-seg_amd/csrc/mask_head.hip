@@ -673,7 +673,11 @@ __global__ void __launch_bounds__(256) point_sample_rows_kernel(const T* __restr
                                                                 const float* __restrict__ coords,
                                                                 float* __restrict__ out, int H, int W, long long total,
                                                                 int P, int sets_per_coord) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  // XCD-aware block order (common.h xcd_swizzle): consecutive points of one map stay on one
+  // XCD, so each XCD's L2 holds only its share of the maps.  Round-robin placement made every
+  // XCD gather from every map (80 x 256^2 f32 = 21 MB against a 4 MB L2): 85 us per call at
+  // the criterion's 37 632 uncertainty points per map, one L2 miss per corner
+  const long long i = (long long)xcd_swizzle(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
   if (i >= total) return;
   const long long n = i / P;
   const T* m = maps + (rows ? rows[n] : n) * (long long)H * W;
@@ -703,7 +707,8 @@ extern "C" int vs_point_sample_rows(const float* maps, const long long* rows, co
   VS_CHECK(num_maps > 0 && height > 0 && width > 0 && num_sets >= 0 && num_points > 0, "bad sizes");
   const long long total = (long long)num_sets * num_points;
   if (total == 0) return VS_OK;
-  VS_CHECK(maps && rows && coords && out, "null pointer");
+  VS_CHECK(maps && coords && out, "null pointer");
+  VS_CHECK(rows || num_sets <= num_maps, "without rows, set n reads map n");
   VS_CHECK(((uintptr_t)coords & 7) == 0, "coords must be 8-B aligned");
   hipLaunchKernelGGL((point_sample_rows_kernel<float, false>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, maps, rows, coords, out, height, width, total, num_points, 1);

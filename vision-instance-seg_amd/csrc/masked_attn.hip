@@ -344,111 +344,30 @@ __global__ void __launch_bounds__(256) xattn_bwd_dkdv(const T* __restrict__ q, c
 }
 
 // ---------------------------------------------------------------------------------------
-// bf16 MFMA path (32x32x16 bf16 tiles, helpers in mfma_util.h).
+// bf16 MFMA path (32x32x16 bf16 tiles, helpers in mfma_util.h, lds_dma.h).
 //
-// Forward: workgroup = (256-key chunk, head, image x 128-query group), 4 waves = 4 query
-// tiles of 32.  V^T of the chunk is staged once in LDS.  Per 32-key tile a wave computes
-// S^T = K Q^T (keys on rows: a lane holds 16 keys of ONE query, the other 16 in lane^32),
-// applies the blocked-key bits (one 32-bit word per lane per tile), runs the online
-// softmax in registers and accumulates O^T += V^T P^T with P^T taken straight from the
-// accumulators (permuted k).  Chunk partials (o, m, l) go to xattn_fwd_combine.
+// Forward (xattn_fwd_mfma2): workgroup = (256-key chunk, head, image x 128-query group), 4 waves
+// = 4 query tiles of 32.  Per 32-key tile a wave computes S^T = K Q^T (keys on rows: a lane
+// holds 16 keys of ONE query, the other 16 in lane^32), applies the blocked-key bits (one
+// 32-bit word per lane per tile), runs the online softmax in registers and accumulates
+// O^T += V^T P^T with P^T taken straight from the accumulators (permuted k).  Chunk partials
+// (o, m, l) go to xattn_fwd_combine.
 //
-// Backward: workgroup = (chunk of 1-4 128-key blocks, head, image), all queries (<= 128,
-// padded) in the workgroup, wave w owns keys 32w..32w+31 of each block; the query tiles
-// are walked one at a time (one tile's S / dP accumulators live: 2 waves/SIMD instead
-// of 1) and the dQ partial accumulates over the chunk's blocks in registers.  S = Q K^T and dP = dO V^T with QUERIES on
-// rows, so dV^T = dO^T P and dK^T = scale Q^T dS take P / dS straight from registers
-// (dO^T, Q^T read from LDS in the permuted query order); dS goes to LDS once so that
-// wave w can form the chunk's dQ partial for query tile w (dQ = scale dS K), summed over
-// chunks by xattn_bwd_dq_combine.
+// Backward (xattn_bwd_mfma2): workgroup = (chunk of 1-8 128-key blocks, head, image), all
+// queries (<= 128, padded) in the workgroup, wave w owns keys 32w..32w+31 of each block; the
+// query tiles are walked one at a time (one tile's S / dP accumulators live: 2 waves/SIMD) and
+// the dQ partial accumulates over the chunk's blocks in registers.  S = Q K^T and dP = dO V^T
+// with QUERIES on rows, so dV^T = dO^T P and dK^T = scale Q^T dS take P / dS straight from
+// registers; dS^T goes to LDS once so that wave w can form the chunk's dQ partial for query
+// tile w, summed over chunks by xattn_bwd_dq_combine.  (The round-4 kernels of the same split,
+// which re-read operand fragments from global memory inside their tile loops, are gone:
+// backward 0.135 -> 0.085 ms, forward 0.068 -> 0.055 ms at the 128^2 level,
+// profiles/r5_xattn_ab.txt.)
 constexpr int kFChunk = 256;
-constexpr int kFPad = kFChunk + 8;
 constexpr int kBChunk = 128;
 constexpr int kBQ = 128;
-constexpr int kBPadQ = kBQ + 8;
-constexpr int kBPadK = kBChunk + 8;
 
-__global__ void __launch_bounds__(256) xattn_fwd_mfma(const bf16* __restrict__ q, const bf16* __restrict__ k,
-                                                      const bf16* __restrict__ v, const uint32_t* __restrict__ words,
-                                                      float* __restrict__ po, float* __restrict__ pml, XGeom g) {
-  __shared__ __attribute__((aligned(16))) short sVt[32 * kFPad];
-  const int chunk = blockIdx.x, h = blockIdx.y;
-  const int nqg = (g.Q + 127) / 128;
-  const int qg = blockIdx.z % nqg, b = blockIdx.z / nqg;
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
-  const int C = g.heads * kD;
-  const int jbeg = chunk * kFChunk;
-  const int n = min(kFChunk, g.S - jbeg);
-  const bf16* kb = k + ((size_t)b * g.S + jbeg) * C + h * kD;
-  const bf16* vb = v + ((size_t)b * g.S + jbeg) * C + h * kD;
-  for (int key = threadIdx.x; key < kFChunk; key += 256) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const bf16x8_t v8 = key < n ? ld8(vb + (size_t)key * C + 8 * c) : zero8();
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sVt[(8 * c + j) * kFPad + key] = v8[j];
-    }
-  }
-  __syncthreads();
-  const int qi = qg * 128 + wave * 32 + r;
-  const bool qok = qi < g.Q;
-  bf16x8_t qf[2];
-#pragma unroll
-  for (int st = 0; st < 2; ++st) qf[st] = qok ? ld8(q + ((size_t)b * g.Q + qi) * C + h * kD + 16 * st + 8 * hh) : zero8();
-  const uint32_t* wrow = words + ((size_t)b * g.Q + (qok ? qi : 0)) * g.nw + (jbeg >> 5);
-  float m = -INFINITY, lsum = 0.f;
-  f32x16_t o;
-  zero16(o);
-  const int ntiles = (n + 31) / 32;
-  for (int kt = 0; kt < ntiles; ++kt) {
-    f32x16_t sc;
-    zero16(sc);
-    const int key = kt * 32 + r;
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const bf16x8_t a = key < n ? ld8(kb + (size_t)key * C + 16 * st + 8 * hh) : zero8();
-      sc = mfma16(a, qf[st], sc);
-    }
-    const uint32_t w = qok ? wrow[kt] : 0xffffffffu;
-    float mt = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kl = crow(i, hh);
-      const bool blocked = (kt * 32 + kl >= n) || ((w >> kl) & 1u);
-      sc[i] = blocked ? -INFINITY : sc[i] * g.scale;
-      mt = fmaxf(mt, sc[i]);
-    }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);
-    const float safe = mn == -INFINITY ? 0.f : mn;
-    const float alpha = __expf(m - safe);
-    lsum *= alpha;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o[i] *= alpha;
-      sc[i] = __expf(sc[i] - safe);
-      lsum += sc[i];
-    }
-    m = mn;
-#pragma unroll
-    for (int th = 0; th < 2; ++th) o = mfma16(ld_perm(sVt + r * kFPad, kt * 32 + 16 * th + 4 * hh), pack8(sc, 8 * th), o);
-  }
-  lsum += __shfl_xor(lsum, 32, 64);
-  if (qok) {
-    const size_t prow = (((size_t)b * g.heads + h) * g.nchunk + chunk) * g.Q + qi;
-    float* dst = po + prow * kD;
-#pragma unroll
-    for (int grp = 0; grp < 4; ++grp)
-      *reinterpret_cast<float4*>(dst + 8 * grp + 4 * hh) =
-          make_float4(o[4 * grp], o[4 * grp + 1], o[4 * grp + 2], o[4 * grp + 3]);
-    if (hh == 0) {
-      pml[prow * 2 + 0] = m;
-      pml[prow * 2 + 1] = lsum;
-    }
-  }
-}
-
-// Forward, round 5 (xattn_fwd_mfma2): the same split as xattn_fwd_mfma with K and V staged
+// Forward (xattn_fwd_mfma2): K and V staged
 // once in their natural layout (64-B rows, lds_dma.h swz64: 16-B chunk stores, no
 // transposing two-byte stores) -- the round-4 kernel read every 32-key tile's K fragment and
 // blocked-bits word from global memory inside the tile loop, one L2 round trip per tile with
@@ -562,141 +481,7 @@ __global__ void __launch_bounds__(256) xattn_bwd_prep(const T* __restrict__ out,
   Dbuf[row] = s;
 }
 
-__global__ void __launch_bounds__(256) xattn_bwd_mfma(const bf16* __restrict__ q, const bf16* __restrict__ k,
-                                                      const bf16* __restrict__ v, const uint32_t* __restrict__ words,
-                                                      const float* __restrict__ lse, const float* __restrict__ Dbuf,
-                                                      const bf16* __restrict__ gout, bf16* __restrict__ gk,
-                                                      bf16* __restrict__ gv, float* __restrict__ pdq, XGeom g) {
-  __shared__ __attribute__((aligned(16))) short sQT[32 * kBPadQ];    // Q^T [d][q]
-  __shared__ __attribute__((aligned(16))) short sDoT[32 * kBPadQ];   // dO^T [d][q]
-  __shared__ __attribute__((aligned(16))) short sKT[32 * kBPadK];    // K^T [d][key]
-  __shared__ __attribute__((aligned(16))) short sDS[kBQ * kBPadK];   // dS [q][key]
-  __shared__ float sL[kBQ], sD[kBQ];
-  __shared__ uint32_t sW[kBQ][kBChunk / 32];
-  const int chunk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
-  const int C = g.heads * kD, Q = g.Q;
-  const int t = threadIdx.x & 127;
-  const bool second = threadIdx.x >= 128;
-  const bf16* qb = q + (size_t)b * Q * C + h * kD;
-  const bf16* ob = gout + (size_t)b * Q * C + h * kD;
-  {  // Q^T / dO^T (threads 0..127 / 128..255, one query each), lse and D rows: once per chunk
-    const bf16* src = second ? ob : qb;
-    short* dstT = second ? sDoT : sQT;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const bf16x8_t x = t < Q ? ld8(src + (size_t)t * C + 8 * c) : zero8();
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dstT[(8 * c + j) * kBPadQ + t] = x[j];
-    }
-    if (!second) {
-      sL[t] = t < Q ? lse[((size_t)b * g.heads + h) * Q + t] : 0.f;
-      sD[t] = t < Q ? Dbuf[((size_t)b * g.heads + h) * Q + t] : 0.f;
-    }
-  }
-  // the chunk is g.chunk keys = g.chunk / kBChunk blocks of 128; the dQ partial of query
-  // tile `wave` accumulates over the blocks in registers and is written once per chunk
-  f32x16_t dq;
-  zero16(dq);
-  const int nblk = g.chunk / kBChunk;
-  for (int kb = 0; kb < nblk; ++kb) {
-    const int jbeg = chunk * g.chunk + kb * kBChunk;
-    if (jbeg >= g.S) break;                     // uniform over the workgroup
-    const int n = min(kBChunk, g.S - jbeg);
-    const bf16* kb_ = k + ((size_t)b * g.S + jbeg) * C + h * kD;
-    const bf16* vb = v + ((size_t)b * g.S + jbeg) * C + h * kD;
-    __syncthreads();                            // the previous block's K^T / dS / words are read
-    if (!second) {   // K^T, one key each
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const bf16x8_t x = t < n ? ld8(kb_ + (size_t)t * C + 8 * c) : zero8();
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sKT[(8 * c + j) * kBPadK + t] = x[j];
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < kBChunk / 32; ++c) {
-        const int wi = (jbeg >> 5) + c;
-        sW[t][c] = (t < Q && wi < g.nw) ? words[((size_t)b * Q + t) * g.nw + wi] : 0xffffffffu;
-      }
-    }
-    __syncthreads();
-    // per query tile qt (32 rows): S = Q K^T and dP = dO V^T against this wave's 32 keys
-    // (cols), P and dS, then dV^T += dO^T P and dK^T += Q^T dS over the tile's queries --
-    // one tile's S / dP accumulators live at a time (4 at once cost 1 wave per SIMD)
-    const int kl = wave * 32 + r;               // key within the block (this lane's column)
-    const bool kok = kl < n;
-    bf16x8_t kf[2], vf[2];
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      kf[st] = kok ? ld8(kb_ + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
-      vf[st] = kok ? ld8(vb + (size_t)kl * C + 16 * st + 8 * hh) : zero8();
-    }
-    f32x16_t dv, dk;
-    zero16(dv);
-    zero16(dk);
-#pragma unroll 1
-    for (int qt = 0; qt < 4; ++qt) {
-      f32x16_t sacc, dacc;
-      zero16(sacc);
-      zero16(dacc);
-      const int qr0 = 32 * qt + r;
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8_t qa = qr0 < Q ? ld8(qb + (size_t)qr0 * C + 16 * st + 8 * hh) : zero8();
-        const bf16x8_t da = qr0 < Q ? ld8(ob + (size_t)qr0 * C + 16 * st + 8 * hh) : zero8();
-        sacc = mfma16(qa, kf[st], sacc);
-        dacc = mfma16(da, vf[st], dacc);
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qr = 32 * qt + crow(i, hh);
-        const bool ok = kok && qr < Q && !((sW[qr][wave] >> r) & 1u);
-        const float p = ok ? __expf(sacc[i] * g.scale - sL[qr]) : 0.f;
-        sacc[i] = p;
-        dacc[i] = p * (dacc[i] - sD[qr]);
-        sDS[qr * kBPadK + kl] = bf16_bits(dacc[i]);
-      }
-#pragma unroll
-      for (int th = 0; th < 2; ++th) {           // k over the tile's queries, permuted order
-        const int base = 32 * qt + 16 * th + 4 * hh;
-        dv = mfma16(ld_perm(sDoT + r * kBPadQ, base), pack8(sacc, 8 * th), dv);
-        dk = mfma16(ld_perm(sQT + r * kBPadQ, base), pack8(dacc, 8 * th), dk);
-      }
-    }
-    if (kok) {
-      bf16* gvr = gv + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
-      bf16* gkr = gk + ((size_t)b * g.S + jbeg + kl) * C + h * kD;
-#pragma unroll
-      for (int grp = 0; grp < 4; ++grp) {
-        bf16x4_t av, ck;
-#pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) {
-          av[e2] = bf16_bits(dv[4 * grp + e2]);
-          ck[e2] = bf16_bits(dk[4 * grp + e2] * g.scale);
-        }
-        *reinterpret_cast<bf16x4_t*>(gvr + 8 * grp + 4 * hh) = av;
-        *reinterpret_cast<bf16x4_t*>(gkr + 8 * grp + 4 * hh) = ck;
-      }
-    }
-    __syncthreads();                            // every wave's dS is in LDS
-    // dQ of query tile `wave` += dS K over the block's keys
-#pragma unroll
-    for (int tt = 0; tt < kBChunk / 16; ++tt) {
-      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sDS + (wave * 32 + r) * kBPadK + 16 * tt + 8 * hh);
-      const bf16x8_t bb = *reinterpret_cast<const bf16x8_t*>(sKT + r * kBPadK + 16 * tt + 8 * hh);
-      dq = mfma16(a, bb, dq);
-    }
-  }
-  const size_t prow0 = (((size_t)b * g.heads + h) * g.nchunk + chunk) * Q;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int qr = wave * 32 + crow(i, hh);
-    if (qr < Q) pdq[(prow0 + qr) * kD + r] = dq[i] * g.scale;
-  }
-}
-
-// Backward, round 5 (xattn_bwd_mfma2): the same workgroup / wave split as xattn_bwd_mfma with
+// Backward (xattn_bwd_mfma2): the workgroup / wave split above with
 // every operand read from LDS, staged once in its natural layout:
 //  * Q and dO of the (image, head) -- the round-4 kernel re-read their fragments from global
 //    memory inside the query-tile loop of every key block, a round trip to L2 per tile with
@@ -883,18 +668,6 @@ static XGeom mfma_geom(int B, int Q, int S, int heads, float scale, int chunk) {
   return g;
 }
 
-// VS_XATTN_FWD=1: the round-4 MFMA forward (A/B)
-static bool xattn_fwd_v2() {
-  const char* e = getenv("VS_XATTN_FWD");
-  return !(e && atoi(e) == 1);
-}
-
-// VS_XATTN_BWD=1: the round-4 MFMA backward (A/B)
-static bool xattn_bwd_v2() {
-  const char* e = getenv("VS_XATTN_BWD");
-  return !(e && atoi(e) == 1);
-}
-
 // VS_XATTN_SCALAR=1 selects the scalar-FMA kernels for bf16 too
 static bool xattn_use_mfma() {
   const char* e = getenv("VS_XATTN_SCALAR");
@@ -919,12 +692,8 @@ extern "C" int vs_masked_attn_forward(int dtype, const void* q, const void* k, c
     float* pml = po + (size_t)B * heads * g.nchunk * Q * kD;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid(g.nchunk, heads, B * ((Q + 127) / 128));
-    if (xattn_fwd_v2())
-      hipLaunchKernelGGL(xattn_fwd_mfma2, grid, dim3(256), 0, st, (const bf16*)q, (const bf16*)k, (const bf16*)v,
-                         words, po, pml, g);
-    else
-      hipLaunchKernelGGL(xattn_fwd_mfma, grid, dim3(256), 0, st, (const bf16*)q, (const bf16*)k, (const bf16*)v,
-                         words, po, pml, g);
+    hipLaunchKernelGGL(xattn_fwd_mfma2, grid, dim3(256), 0, st, (const bf16*)q, (const bf16*)k, (const bf16*)v,
+                       words, po, pml, g);
     const long long crows = (long long)B * heads * Q * 32;
     hipLaunchKernelGGL(xattn_fwd_combine<bf16>, dim3((int)((crows + 255) / 256)), dim3(256), 0, st, po, pml,
                        (bf16*)out, lse, g);
@@ -970,7 +739,7 @@ extern "C" int vs_masked_attn_backward(int dtype, const void* q, const void* k, 
     const long long nb128 = (long long)B * heads * ((S + kBChunk - 1) / kBChunk);
     // C2's 128^2 level: 8 (one round of 2 workgroups per CU; kbench op 0.088 -> 0.085 ms with the
     // round-5 kernel, profiles/r5_xattn_ab.txt; 4 with the round-4 one: 0.174 -> 0.135 ms)
-    int per = nb128 >= 4096 ? (xattn_bwd_v2() ? 8 : 4) : nb128 >= 2048 ? 2 : 1;
+    int per = nb128 >= 4096 ? 8 : nb128 >= 2048 ? 2 : 1;
     if (const char* e = getenv("VS_XATTN_BLOCKS")) per = std::max(1, std::min(16, atoi(e)));
     XGeom g = mfma_geom(B, Q, S, heads, scale, kBChunk * per);
     float* pdq = (float*)workspace;
@@ -979,12 +748,8 @@ extern "C" int vs_masked_attn_backward(int dtype, const void* q, const void* k, 
     const long long rows = (long long)B * heads * Q;
     hipLaunchKernelGGL(xattn_bwd_prep<bf16>, dim3((int)((rows + 255) / 256)), dim3(256), 0, st, (const bf16*)out,
                        (const bf16*)grad_out, Dbuf, g);
-    if (xattn_bwd_v2())
-      hipLaunchKernelGGL(xattn_bwd_mfma2, dim3(g.nchunk, heads, B), dim3(256), 0, st, (const bf16*)q, (const bf16*)k,
-                         (const bf16*)v, words, lse, Dbuf, (const bf16*)grad_out, (bf16*)grad_k, (bf16*)grad_v, pdq, g);
-    else
-      hipLaunchKernelGGL(xattn_bwd_mfma, dim3(g.nchunk, heads, B), dim3(256), 0, st, (const bf16*)q, (const bf16*)k,
-                         (const bf16*)v, words, lse, Dbuf, (const bf16*)grad_out, (bf16*)grad_k, (bf16*)grad_v, pdq, g);
+    hipLaunchKernelGGL(xattn_bwd_mfma2, dim3(g.nchunk, heads, B), dim3(256), 0, st, (const bf16*)q, (const bf16*)k,
+                       (const bf16*)v, words, lse, Dbuf, (const bf16*)grad_out, (bf16*)grad_k, (bf16*)grad_v, pdq, g);
     const long long total = rows * kD;
     hipLaunchKernelGGL(xattn_bwd_dq_combine<bf16>, dim3((int)((total + 255) / 256)), dim3(256), 0, st, pdq,
                        (bf16*)grad_q, g);

@@ -10,13 +10,17 @@
 // one 16-B load per lane, adjacent lanes read adjacent bytes; the group's loc/attn
 // rows (96 B / 48 B, 16-B aligned) are read as float4.  Accumulation in f32.
 //
-// Backward: grad_loc / grad_attn from a gather kernel (msda_bwd_geom_kernel); grad_value
-// (f32, then cast) by f32 global atomics, bound by their rate (~1.1 TB/s of added bytes
-// on gfx950, MI355X_MICROARCH §Global float atomics), so the kernels cut the added bytes:
-//   * bf16, P == 4, enough queries (default): msda_bwd_mfma_wg_kernel -- per 8 x 8 query
-//     tile (runs of 64 queries when the queries are not the value grid) and level,
-//     grad_value over the tile's box of cells as one MFMA product W[cell][query] x
-//     grad_out[query][c], one atomic row per touched cell;
+// Backward: grad_value (f32, then cast) by f32 global atomics, bound by their rate (~1.1 TB/s
+// of added bytes on gfx950, MI355X_MICROARCH §Global float atomics), so the kernels cut the
+// added bytes; grad_loc / grad_attn ride in the same walk (or a gather kernel,
+// msda_bwd_geom_kernel, for the f32 / small paths):
+//   * bf16, P == 4, encoder problems (queries = the value grid; default):
+//     msda_bwd_col_kernel -- a workgroup owns a PYRAMID COLUMN (8 x 16 finest-level queries
+//     plus the coarser levels' blocks over the same area), grad_value per band of cells as
+//     one MFMA product W[cell][query] x grad_out[query][c] accumulated over the column's
+//     query chunks, one atomic row per (band, cell) for the whole column;
+//   * bf16, P == 4, query subsets (Q != S): msda_bwd_mfma_wg_kernel -- the same product per
+//     8 x 8 query tile (runs of 64 queries) and level, one atomic row per touched cell;
 //   * f32 (parity mode): msda_bwd_binned_kernel -- 4 x 4 tiles, the tile's corners
 //     counting-sorted by cell, register sums in exact f32, one atomic row per cell
 //     (also bf16 with VS_MSDA_MFMA=0, for A/B and the cross-check test);
@@ -42,6 +46,15 @@ struct Levels {
   int h[kMaxLevels];
   int w[kMaxLevels];
   int start[kMaxLevels];
+};
+
+// pyramid columns (column backward, column-ordered forward): see col_geo
+constexpr int kMsdaColDefault[2] = {8, 16};  // VS_MSDA_COL default (CY, CX); {0, 0}: tile kernel
+
+struct ColGeo {
+  int ty[kMaxLevels], tx[kMaxLevels];    // a column's query block per level (rows, cols)
+  int ord[kMaxLevels];                   // levels in enumeration order (largest first)
+  int ncx, per_image;                    // columns per block row / per image
 };
 
 
@@ -140,20 +153,51 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ val
 // (4 VGPRs each) before any is used, so 8 issue back to back instead of one tap's 4
 // (msda_fwd_kernel's runtime-P loop).  Same arithmetic, same order.  T = 4 (a level's 16
 // corner rows in flight) measured slower: 0.167 vs 0.156 ms at the C2 encoder shape.
-template <int L, int T>
+//
+// COL (encoder problems, queries = the value grid, round 6): the queries are visited in
+// PYRAMID-COLUMN order (ColGeo, as the column backward: a column = an 8 x 16 block of the
+// finest level and the blocks over the same image area at the coarser levels, slots padded
+// to the block sizes), columns in raster order, and the blocks of consecutive columns on one
+// XCD (xcd_swizzle).  In query order an XCD working on the coarse levels' queries gathered
+// from the whole image at the finer levels (8 MB of level-0 value per image against a 4 MB
+// L2): PMC reads were 1.63x the compulsory bytes.  Visiting order only: every query is
+// computed exactly as before.  `cq` = slots per column, `ncol` = columns per image.
+template <int L, int T, bool COL = false>
 __global__ void __launch_bounds__(256) msda_fwd4_kernel(const bf16* __restrict__ value,
                                                          const float* __restrict__ loc,
                                                          const float* __restrict__ attw,
                                                          bf16* __restrict__ out, Levels lv, int S,
-                                                         int Hh, int Q, long long groups) {
+                                                         int Hh, int Q, long long groups, ColGeo cg, int cq) {
   constexpr int P = 4, LP = L * P, V = 8, LPG = kD / V;
   long long gid = (long long)xcd_swizzle(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   long long stride = (long long)gridDim.x * blockDim.x;
   for (; gid < groups * LPG; gid += stride) {
-    const long long grp = gid / LPG;
+    long long grp = gid / LPG;
     const int sub = (int)(gid % LPG);
     const int h = (int)(grp % Hh);
-    const long long b = grp / Hh / Q;
+    long long b = grp / Hh / Q;
+    if (COL) {                                // grp = ((b * ncol + col) * cq + slot) * Hh + h
+      const unsigned t = (unsigned)(grp / Hh);
+      unsigned k = t % (unsigned)cq;
+      const unsigned cgl = t / (unsigned)cq;
+      const unsigned col = cgl % (unsigned)cg.per_image;
+      b = cgl / (unsigned)cg.per_image;
+      const int cyy = (int)(col / (unsigned)cg.ncx), cxx = (int)(col % (unsigned)cg.ncx);
+      int q = -1;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const int l = cg.ord[i];
+        const unsigned n = (unsigned)(cg.ty[l] * cg.tx[l]);
+        if (k < n) {
+          const int y = cyy * cg.ty[l] + (int)(k / (unsigned)cg.tx[l]), x = cxx * cg.tx[l] + (int)(k % (unsigned)cg.tx[l]);
+          if (y < lv.h[l] && x < lv.w[l]) q = lv.start[l] + y * lv.w[l] + x;
+          break;
+        }
+        k -= n;
+      }
+      if (q < 0) continue;                    // a padding slot of a border column
+      grp = (b * Q + q) * Hh + h;
+    }
     const float4* lp = reinterpret_cast<const float4*>(loc + grp * LP * 2);
     const float4* wp = reinterpret_cast<const float4*>(attw + grp * LP);
     const size_t rowstride = (size_t)Hh * kD;
@@ -1216,13 +1260,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
 // rows loaded once and reused by every chunk, stored transposed over W: 16-B stores); a
 // tap's corner dots stay in registers across bands (dk[chunk][corner]).  Band / chunk pairs are skipped from per-chunk boxes
 // (no vote barrier).  4 LDS-only barriers per pair (W built -> product -> Dm -> dots).
-constexpr int kMsdaColDefault[2] = {8, 16};  // VS_MSDA_COL default (CY, CX); {0, 0}: tile kernel
-
-struct ColGeo {
-  int ty[kMaxLevels], tx[kMaxLevels];    // a column's query block per level (rows, cols)
-  int ord[kMaxLevels];                   // levels in enumeration order (largest first)
-  int ncx, per_image;                    // columns per block row / per image
-};
 
 // MFMA operand (8 k-values of one column, k = rows k0 + 8hh + j, column lane & 31) from a
 // row-major bf16 LDS image, by the gfx950 transposed read (cdna_hip_programming.md T10;
@@ -1242,13 +1279,17 @@ __device__ __forceinline__ bf16x8_t tr8(const short* img, int pitch, int k0, int
 
 __device__ __forceinline__ int sgpr(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// WINT (default): W built as FIXED-POINT integers with no-return ds_add_u32 (quantum 2^-30; a
-// cell's W sums at most one level's attention weights times bilinear weights, <= 1, so no
-// partial leaves int32): the four points of a query hit the same cells, and as f32 they had
-// to take turns (4 wave-synchronised rounds of read-modify-write per (band, chunk) pair;
-// ds_add_f32 is 35x slower than the integer add on gfx950).  The product converts each W
-// value back (exact power-of-two scaling) before the bf16 hi / lo split.
-// DBG (timing-split instances, VS_MSDA_DBG): 1 no W build, 2 no product, 4 no Dm / dots, 8 no flush
+// WINT (default): W built as FIXED-POINT integers with no-return ds_add_u32: the four points of
+// a query hit the same cells, and as f32 they had to take turns (4 wave-synchronised rounds of
+// read-modify-write per (band, chunk) pair; ds_add_f32 is 35x slower than the integer add on
+// gfx950).  An entry W[cell][q] sums at most q's four points of the level, |W| <= sum_p |aw_p|
+// (bilinear weights <= 1), so the quantum is 2^-e per (workgroup, level) with e = 30 while that
+// bound is <= 1 (softmax-normalised weights, the encoder: every partial sum stays inside int32)
+// and e lowered by ceil(log2(bound)) beyond it -- any attention weights the op is handed stay
+// exact to the quantum (round-5 ADVICE: a fixed 2^-30 wrapped for weights summing past 2).  The
+// product converts each W value back (exact power-of-two scaling) before the bf16 hi / lo split.
+// DBG: the parts switched off in the round-5 timing split (profiles/r5_msda_split.txt; 1 no W
+// build, 2 no product, 4 no Dm / dots, 8 no flush); only DBG = 0 is instantiated
 template <int NCH, bool WINT = true, int DBG = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCH <= 3 ? 3 : 2)))
 msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ attw, const bf16* __restrict__ gout,
@@ -1258,6 +1299,7 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
   __shared__ __attribute__((aligned(16))) short sg[NCH * 64 * kD];   // grad_out rows, column order
   __shared__ __attribute__((aligned(16))) float sW[kWFloats];        // W of a (band, chunk) / Dm overlay
   __shared__ int sBox[2][4][NCH][4];                                 // [level parity][wave][chunk] box
+  __shared__ int sAwm[2][4];                                         // [level parity][wave] max sum_p |aw_p|
   const int blk = xcd_swizzle(blockIdx.x, nblk);                     // the 8 heads of a column: one XCD
   const int h = blk % Hh;
   const int col = (blk / Hh) % cg.per_image;
@@ -1348,7 +1390,25 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
         sBox[par][wave][s][3] = e;
       }
     }
+    if (WINT) {                               // the fixed-point bound: max over queries of sum_p |aw_p|
+      float am = 0.f;
+#pragma unroll
+      for (int s = 0; s < NCH; ++s) {
+        float a = qid[s] >= 0 ? fabsf(aw[s]) : 0.f;
+        a += __shfl_xor(a, 1, 64);                        // a query's 4 points are lanes 4k .. 4k + 3
+        a += __shfl_xor(a, 2, 64);
+        am = fmaxf(am, a);
+      }
+      const int amb = wave_max(__float_as_int(am));      // non-negative floats order as ints
+      if (lane == 0) sAwm[par][wave] = amb;
+    }
     lds_barrier();                            // (sBox is double-buffered by level parity)
+    int qe = 30;                              // W quantum 2^-qe (WINT)
+    if (WINT) {
+      const float bound = __int_as_float(max(max(sAwm[par][0], sAwm[par][1]), max(sAwm[par][2], sAwm[par][3])));
+      if (bound > 1.f) qe = bound < 0x1p20f ? 30 - (int)ceilf(log2f(bound)) : 10;
+      qe = sgpr(qe);
+    }
     int cb[NCH][4];
     int oy = 1 << 30, yh = -1, ox = 1 << 30, xh = -1;
 #pragma unroll
@@ -1418,7 +1478,7 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
 #pragma unroll
             for (int k = 0; k < 4; ++k)
               if (cell[k] >= 0)
-                __hip_atomic_fetch_add(reinterpret_cast<int*>(sW) + cell[k] * kWP8 + tq, __float2int_rn(cw[k] * 0x1p30f),
+                __hip_atomic_fetch_add(reinterpret_cast<int*>(sW) + cell[k] * kWP8 + tq, __float2int_rn(ldexpf(cw[k], qe)),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           } else {
 #pragma unroll
@@ -1443,7 +1503,7 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
                 const int4 i1 = *reinterpret_cast<const int4*>(wr + 4);
                 const int iv[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
 #pragma unroll
-                for (int j = 0; j < 8; ++j) wv[j] = (float)iv[j] * 0x1p-30f;
+                for (int j = 0; j < 8; ++j) wv[j] = ldexpf((float)iv[j], -qe);
               } else {
                 const float4 w0 = *reinterpret_cast<const float4*>(wr);
                 const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
@@ -1877,6 +1937,8 @@ int fill_levels(Levels* lv, const int64_t* shapes, const int64_t* starts, int L,
 
 using namespace vs;
 
+static int col_geo(const Levels& lv, int L, int CY, int CX, ColGeo* cg);
+
 extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shapes,
                                const int64_t* starts, const float* loc, const float* attw,
                                void* out, int B, int S, int Hh, int D, int L, int Q, int P,
@@ -1895,10 +1957,29 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
   bool unrolled = P == 4;                    // VS_MSDA_FWD4=0: the runtime-P kernel
   if (const char* e = getenv("VS_MSDA_FWD4")) unrolled = unrolled && atoi(e) != 0;
   if (dtype == VS_BF16 && unrolled) {
-    int grid = grid_for(groups * 4, block, 256 * 64);
+    // encoder problems (Q == S: the queries are the value grid): pyramid-column visiting order
+    // (msda_fwd4_kernel COL; VS_MSDA_FWD_COL=0: query order, A/B)
+    ColGeo cg;
+    int cq = 0;
+    bool col = Q == S && L >= 2;
+    if (const char* e = getenv("VS_MSDA_FWD_COL")) col = col && atoi(e) != 0;
+    long long slots = groups;
+    if (col && col_geo(lv, L, kMsdaColDefault[0], kMsdaColDefault[1], &cg) > 0) {
+      for (int l = 0; l < L; ++l) cq += cg.ty[l] * cg.tx[l];
+      slots = (long long)B * cg.per_image * cq * Hh;
+      col = slots * 4 < (1LL << 31) && slots >= groups;
+    } else {
+      col = false;
+    }
+    if (!col) slots = groups;
+    int grid = grid_for(slots * 4, block, 256 * 64);
 #define VS_FWD4(LL)                                                                                          \
-  hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc, \
-                     attw, (bf16*)out, lv, S, Hh, Q, groups)
+  if (col)                                                                                                   \
+    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2, true>), dim3(grid), dim3(block), 0, st, (const bf16*)value,   \
+                       loc, attw, (bf16*)out, lv, S, Hh, Q, slots, cg, cq);                                  \
+  else                                                                                                       \
+    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc,    \
+                       attw, (bf16*)out, lv, S, Hh, Q, groups, cg, 0)
     switch (L) {
       case 1: VS_FWD4(1); break;
       case 2: VS_FWD4(2); break;
@@ -2085,17 +2166,7 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
 #define VS_COL(NC_, WI_)                                                                                        \
   hipLaunchKernelGGL((msda_bwd_col_kernel<NC_, WI_>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,          \
                      (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc)
-      const char* dbe = getenv("VS_MSDA_DBG");
-      const int mdbg = dbe ? atoi(dbe) : 0;
-      if (nch <= 3 && mdbg > 0) {
-#define VS_COLD(D_)                                                                                             \
-  case D_:                                                                                                      \
-    hipLaunchKernelGGL((msda_bwd_col_kernel<3, true, D_>), dim3((unsigned)nbc), dim3(256), 0, st, loc, attw,    \
-                       (const bf16*)gout, (const bf16*)value, gvalue, gloc, gattw, lv, cg, S, Hh, Q, L, (int)nbc); \
-    break;
-        switch (mdbg) { VS_COLD(1) VS_COLD(2) VS_COLD(4) VS_COLD(8) VS_COLD(15) default: break; }
-#undef VS_COLD
-      } else if (nch <= 3) {
+      if (nch <= 3) {
         if (wint) VS_COL(3, true);
         else VS_COL(3, false);
       } else {

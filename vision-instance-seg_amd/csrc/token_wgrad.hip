@@ -71,7 +71,8 @@ __device__ __forceinline__ void store4(void* base, size_t idx, bool f32, float a
 // NS-stage ring of 64-token chunk buffers: NS - 1 chunks in flight while one is multiplied
 // (every wave issues the same PW DMA instructions per chunk, so a counted vmcnt wait retires
 // exactly the oldest chunk).
-// DBG (timing experiments only): 1 no MFMA, 2 no DMA, 3 neither and no LDS reads, 4 no chunk loop
+// DBG: the parts switched off in the round-5 timing split (tools/r5/wg4.sh; 1 no MFMA, 2 no DMA,
+// 3 neither and no LDS reads, 4 no chunk loop); only DBG = 0 is instantiated
 template <int BO, int BI, int WO, int WI, int NS, int DBG = 0>
 __global__ void __launch_bounds__(64 * WO * WI) token_wgrad_kernel(const WgGroup grp, float* __restrict__ part,
                                                                    float* __restrict__ pbias, int spread) {
@@ -548,7 +549,6 @@ extern "C" int vs_token_wgrad_grouped(int dtype, const vs_wgrad_problem* probs, 
   VS_CHECK(need <= 256 || (workspace && ((uintptr_t)workspace & 15) == 0), "workspace: 16-B aligned, sized by "
            "vs_token_wgrad_grouped_workspace_bytes");
   hipStream_t st = (hipStream_t)stream;
-  static const int dbg = env_int("VS_WGRAD_DEBUG", 0);
   // VS_WGRAD_SPREAD=1: the next chunk's DMA pieces issued between the MFMA steps instead of
   // all after the barrier
   static const int spread = env_int("VS_WGRAD_SPREAD", 1);
@@ -558,14 +558,7 @@ extern "C" int vs_token_wgrad_grouped(int dtype, const vs_wgrad_problem* probs, 
     float* pb = part ? part + pl.tile_floats : nullptr;
     const dim3 g((unsigned)pl.wgs);
     if (cfg == 0) {
-      if (dbg == 1)
-        hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 4, 2, 3, 1>), g, dim3(512), 0, st, pl.g, part, pb, spread);
-      else if (dbg == 2)
-        hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 4, 2, 3, 2>), g, dim3(512), 0, st, pl.g, part, pb, spread);
-      else if (dbg == 4)
-        hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 4, 2, 3, 4>), g, dim3(512), 0, st, pl.g, part, pb, spread);
-      else
-        hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 4, 2, 3>), g, dim3(512), 0, st, pl.g, part, pb, spread);
+      hipLaunchKernelGGL((token_wgrad_kernel<256, 128, 4, 2, 3>), g, dim3(512), 0, st, pl.g, part, pb, spread);
     } else {
       hipLaunchKernelGGL((token_wgrad_kernel<128, 128, 4, 2, 4>), g, dim3(512), 0, st, pl.g, part, pb, spread);
     }

@@ -1117,8 +1117,8 @@ __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(ON
 //     in the permuted query order).
 // S and dP are formed twice (the MFMA units idle in this kernel); LDS peaks at ~47 KB for
 // N = 144 (3 workgroups/CU).  F8: the logits on the forward's fp8 operands and scales.
-// DBG (timing-split instances, VS_WIN_BWD_VAR): 1 no bias binning, 2 no phase 2, 4 no phase-1
-// tile loop, 8 no bias gather in the logits
+// DBG: the parts switched off in the round-5 timing split (profiles/r5_win_bwd_ab.txt; 1 no bias
+// binning, 2 no phase 2, 4 no phase-1 tile loop, 8 no bias gather); only DBG = 0 is instantiated
 template <int NT, bool F8, int DBG = 0>
 __global__ void __launch_bounds__(64 * NT, NT == 5 ? 4 : NT == 2 ? 3 : 1) win_attn_bwd_fa(
     const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
@@ -1440,8 +1440,8 @@ __device__ __forceinline__ int cvt_rpi(float x) {
 //    every (real query, padded key) pair lands there (P = 0 with no zone rows);
 // Padded queries / keys (dS = 0) index bins outside the wave's [0, T2): the bins of the
 // neighbouring waves or the margins around them, where adding 0 changes nothing.
-// DBG (timing-split instances, VS_WIN_BWD_VAR with VS_WIN_BWD_FB=1): 1 no bins, 2 no phase 2,
-// 4 no phase-1 tile loop
+// DBG: the parts switched off in the round-5 timing split (1 no bins, 2 no phase 2, 4 no phase-1
+// tile loop); only DBG = 0 is instantiated.  WPE 3 (3 waves / SIMD) measured 1.44 vs 1.21 ms at C5
 template <int NT, bool F8, int WPE = F8 ? 3 : 4, int DBG = 0>
 __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(WPE))) win_attn_bwd_fb(
     const bf16* __restrict__ qkv, const float* __restrict__ table, const bf16* __restrict__ out,
@@ -1806,26 +1806,7 @@ static void launch_bwd_fa(const WinGeom& g, dim3 grid, hipStream_t st, const voi
 #define VS_BWD_FA(NT_)                                                                                      \
   hipLaunchKernelGGL((win_attn_bwd_fa<NT_, F8>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,       \
                      (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g)
-  const char* dv = getenv("VS_WIN_BWD_VAR");
-  const int dbg = dv ? atoi(dv) : 0;
   if (bwd_fb(F8, g.N)) {
-    const char* fv = getenv("VS_WIN_BWD_VAR");
-    const int fdbg = fv ? atoi(fv) : 0;
-    if (fdbg > 0 && (g.N + 31) / 32 == 5) {
-#define VS_FB_DBG(D)                                                                                        \
-  case D:                                                                                                   \
-    hipLaunchKernelGGL((win_attn_bwd_fb<5, F8, F8 ? 3 : 4, D>), grid, dim3(64 * 5), 0, st, (const bf16*)qkv, table,  \
-                       (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g);            \
-    return;
-      switch (fdbg) { VS_FB_DBG(1) VS_FB_DBG(2) VS_FB_DBG(3) VS_FB_DBG(4) VS_FB_DBG(6) default: break; }
-#undef VS_FB_DBG
-    }
-    const char* we = getenv("VS_WIN_BWD_WPE");
-    if (we && atoi(we) == 3 && (g.N + 31) / 32 == 5) {
-      hipLaunchKernelGGL((win_attn_bwd_fb<5, F8, 3>), grid, dim3(64 * 5), 0, st, (const bf16*)qkv, table,
-                         (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g);
-      return;
-    }
 #define VS_BWD_FB(NT_)                                                                                      \
   hipLaunchKernelGGL((win_attn_bwd_fb<NT_, F8>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,       \
                      (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g)
@@ -1833,18 +1814,6 @@ static void launch_bwd_fa(const WinGeom& g, dim3 grid, hipStream_t st, const voi
 #undef VS_BWD_FB
     return;
   }
-#define VS_BWD_DBG(D)                                                                                       \
-  case D:                                                                                                   \
-    hipLaunchKernelGGL((win_attn_bwd_fa<5, F8, D>), grid, dim3(64 * 5), 0, st, (const bf16*)qkv, table,     \
-                       (const bf16*)out, lse, (const bf16*)grad_out, (bf16*)grad_qkv, gpart, g);            \
-    return;
-  if (dbg > 0 && (g.N + 31) / 32 == 5) {
-    switch (dbg) {
-      VS_BWD_DBG(1) VS_BWD_DBG(2) VS_BWD_DBG(3) VS_BWD_DBG(4) VS_BWD_DBG(8) VS_BWD_DBG(9) VS_BWD_DBG(6)
-      default: break;
-    }
-  }
-#undef VS_BWD_DBG
   VS_NT_SWITCH((g.N + 31) / 32, VS_BWD_FA)
 #undef VS_BWD_FA
 }

@@ -45,8 +45,9 @@ _MASK_SAMPLE_KERNEL = os.environ.get("VS_MASK_SAMPLE", "1") == "1"
 
 
 def _sample(feat, coords):
-    """point_sample (HF:m2f:245-275): feat [N,1,H,W], coords [N,P,2] in [0,1] -> [N,P]."""
-    return F.grid_sample(feat, 2.0 * coords.unsqueeze(2) - 1.0, align_corners=False).squeeze(3).squeeze(1)
+    """point_sample (HF:m2f:245-275): feat [N,1,H,W], coords [N,P,2] in [0,1] -> [N,P]
+    (ops.point_sample: the HIP point gather on the device)."""
+    return ops.point_sample(feat, coords)
 
 
 def _target_points(tg, grid):

@@ -162,18 +162,12 @@ def _addmm_into(c, a, b):
 _TGEMM_DGRAD = os.environ.get("VS_TGEMM_DGRAD", "1") == "1"
 
 
-# Which dX GEMMs take the token GEMM.  r5a (default): every T <= 300000 except the wide
-# reductions of smaller T.  r5b: only where the isolated dX measured faster than hipBLASLt's
-# dY W (tools/r5/wgrad_ab.py --dgrad-only, profiles/r5_dgrad_ab.txt: Swin-T stage 1 and the
-# wide-output encoder fc2) -- the C2 step measured the same with either (135.2 / 135.4 vs
-# 135.6 img/s on one box, profiles/r5_dgrad_rule_ab.txt), so the earlier rule stays
-_DGRAD_RULE = os.environ.get("VS_TGEMM_DGRAD_RULE", "r5a")
-
-
+# Which dX GEMMs take the token GEMM: every T <= 300000 except the wide reductions of smaller
+# T.  (Only where the isolated dX measured faster than hipBLASLt's dY W -- Swin-T stage 1 and
+# the wide-output encoder fc2, profiles/r5_dgrad_ab.txt -- measured the same C2 step: 135.2 /
+# 135.4 vs 135.6 img/s on one box, profiles/r5_dgrad_rule_ab.txt; that variant is gone.)
 def _use_token_gemm_dgrad(T: int, K_out: int, N_red: int) -> bool:
-    if _DGRAD_RULE == "r5a":
-        return T <= 300_000 and not (N_red >= 4 * K_out and T <= 100_000)
-    return T <= 300_000 and (T >= 200_000 or (K_out >= 4 * N_red and K_out >= 1024 and T >= 65536))
+    return T <= 300_000 and not (N_red >= 4 * K_out and T <= 100_000)
 
 
 def _dgrad_gemm(gy2, weight):
@@ -318,7 +312,10 @@ class _TokenPlaneFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = torch.bmm(g3.transpose(1, 2), weight.view(Co, Ci).to(x.dtype).unsqueeze(0).expand(B, Co, Ci))
         if ctx.needs_input_grad[1]:
-            gw = torch.bmm(g3, x).float().sum(0).to(weight.dtype).view_as(weight)
+            # per-image products in f32 (bmm's f32 output), summed over the batch and rounded
+            # once -- a bf16 product per image rounded each image's dW first (round-5 ADVICE)
+            gw = (torch.bmm(g3, x, out_dtype=torch.float32) if x.dtype != torch.float32 else torch.bmm(g3, x))
+            gw = gw.sum(0).to(weight.dtype).view_as(weight)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = g3.sum((0, 2), dtype=torch.float32).to(weight.dtype)
         return gx, gw, gb, None, None
@@ -906,8 +903,10 @@ class TokenLinear(nn.Linear):
 # ---------------------------------------------------------------------------------------
 # Swin block Linears on the hand-written token GEMM (csrc/token_gemm.hip)
 # ---------------------------------------------------------------------------------------
-# VS_TGEMM_GELU=0: fc1 + GELU as the vendor GEMM + a separate GELU pass (A/B)
-_TGEMM_GELU = os.environ.get("VS_TGEMM_GELU", "0") == "1"
+# bf16 fc1 + GELU: the vendor GEMM + the GELU pass (ops.activation) except on the streaming
+# kernel (stage 1): the token GEMM's GELU epilogue measured slower than vendor + ATen GELU at
+# the C2 shapes (e.g. stage-3 fc1 0.082 vs 0.075 ms, profiles/r4_tgemm_bench3.txt) and is used
+# by the fp8 path only
 # fp8 Linears only where the product is MFMA-bound: the K-deep ones (C5: stages 2-4 and
 # every fc2); the stage-1 qkv / proj / fc1 of Swin-L (K = 192) are HBM-bound
 FP8_MIN_K = int(os.environ.get("VS_FP8_MIN_K", "384"))
@@ -1118,7 +1117,7 @@ def _stream_gelu_ok(x, w) -> bool:
 def linear_gelu_tokens(x, w, b, fp8: bool = False):
     """gelu(F.linear(x, w, b)) with the exact erf GELU: fused into the token GEMM on
     token-heavy bf16 device tensors (_LinearGeluFn), the composition otherwise."""
-    if (_TGEMM_GELU or fp8 or _stream_gelu_ok(x, w)) and _tgemm_ok(x, w, b):
+    if (fp8 or _stream_gelu_ok(x, w)) and _tgemm_ok(x, w, b):
         return _LinearGeluFn.apply(x, w, b, bool(fp8 and w.shape[1] % 128 == 0 and w.shape[1] >= FP8_MIN_K))
     return ops.activation(linear_tokens(x, w, b), "gelu")
 

@@ -428,8 +428,9 @@ def sigmoid_focal_loss(logits, targets, alpha: float = 0.25, gamma: float = 2.0)
 
 
 def _point_sample(feat, coords):
-    """feat [N, 1, H, W], coords [N, P, 2] in [0, 1] -> [N, P] (HF:m2f:245-275)."""
-    return F.grid_sample(feat, 2.0 * coords.unsqueeze(2) - 1.0, align_corners=False).squeeze(3).squeeze(1)
+    """feat [N, 1, H, W], coords [N, P, 2] in [0, 1] -> [N, P] (HF:m2f:245-275; ops.point_sample:
+    the HIP point gather on the device)."""
+    return ops.point_sample(feat, coords)
 
 
 def _point_sample_rows(maps, rows, coords):

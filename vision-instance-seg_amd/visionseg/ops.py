@@ -482,7 +482,7 @@ class MatchedPointLogitsFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, pred, coords, qsel, E, P):
         grid = 2.0 * coords.unsqueeze(2) - 1.0
-        out = F.grid_sample(pred, grid, align_corners=False).squeeze(3).squeeze(1)
+        out = point_sample(pred, coords)
         ctx.save_for_backward(grid, qsel, E, P)
         ctx.map_shape = tuple(pred.shape)
         return out
@@ -797,20 +797,34 @@ def row_point_logits(logits, rows, coords, Esel, P, sink=None):
 
 
 def point_sample_rows(maps, rows, coords):
-    """maps f32 [M, H, W], rows int64 [N], coords f32 [N, P, 2] in [0, 1] -> [N, P]: the
-    bilinear sample (grid_sample, align_corners=False, zeros) of map rows[n] at each of its
-    points (csrc/mask_head.hip point_sample_rows_kernel)."""
-    L.require_hip(maps, rows, coords)
+    """maps f32 [M, H, W], rows int64 [N] (or None: set n reads map n), coords f32 [N, P, 2]
+    in [0, 1] -> [N, P]: the bilinear sample (grid_sample, align_corners=False, zeros) of map
+    rows[n] at each of its points (csrc/mask_head.hip point_sample_rows_kernel)."""
+    L.require_hip(maps, coords)
     M, H, W = maps.shape
     N, P = coords.shape[:2]
-    mc = maps.float().contiguous()
-    rc = rows.to(torch.int64).contiguous()
-    cc = coords.float().contiguous()
+    mc = maps if (maps.dtype == torch.float32 and maps.is_contiguous()) else maps.float().contiguous()
+    rc = rows.to(torch.int64).contiguous() if rows is not None else None
+    if rc is None and N > M:
+        raise ValueError(f"{N} point sets but {M} maps and no rows")
+    cc = coords if (coords.dtype == torch.float32 and coords.is_contiguous()) else coords.float().contiguous()
     out = torch.empty(N, P, device=maps.device, dtype=torch.float32)
     with timed("point_sample_rows", mc, bytes_=cc.numel() * 4 + out.numel() * 4 * 5):
-        L.check(L.lib().vs_point_sample_rows(L.ptr(mc), L.ptr(rc), L.ptr(cc), L.ptr(out), M, H, W, N, P,
-                                             L.stream(mc)), "point_sample_rows")
+        L.check(L.lib().vs_point_sample_rows(L.ptr(mc), L.ptr(rc) if rc is not None else None, L.ptr(cc), L.ptr(out),
+                                             M, H, W, N, P, L.stream(mc)), "point_sample_rows")
     return out
+
+
+def point_sample(feat, coords):
+    """point_sample (HF:m2f:245-275) of one map per point set: feat f32 [N, 1, H, W] (or
+    [N, H, W]), coords [N, P, 2] in [0, 1] -> [N, P] -- grid_sample(align_corners=False,
+    zeros) on the HIP point gather for device tensors (ATen's grid_sampler_2d took 95 us per
+    call at the criterion's 80 x 256^2 maps / 37 632 points), torch on the CPU or where
+    autograd must differentiate through it."""
+    if not feat.is_cuda or (feat.requires_grad and torch.is_grad_enabled()):
+        return F.grid_sample(feat.view(feat.shape[0], 1, *feat.shape[-2:]), 2.0 * coords.unsqueeze(2) - 1.0,
+                             align_corners=False).squeeze(3).squeeze(1)
+    return point_sample_rows(feat.reshape(feat.shape[0], *feat.shape[-2:]), None, coords)
 
 
 def point_sample_masks(masks, coords, grid_space=False, sets_per_coord=1, rows=None):
