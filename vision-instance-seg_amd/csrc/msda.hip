@@ -152,7 +152,11 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ val
 // 32 L and 16 L bytes per group) and the corner rows of two taps at a time are loaded raw
 // (4 VGPRs each) before any is used, so 8 issue back to back instead of one tap's 4
 // (msda_fwd_kernel's runtime-P loop).  Same arithmetic, same order.  T = 4 (a level's 16
-// corner rows in flight) measured slower: 0.167 vs 0.156 ms at the C2 encoder shape.
+// corner rows in flight) measured slower: 0.167 vs 0.156 ms at the C2 encoder shape.  Round 6:
+// T = 1 (4 corner rows in flight, 78 VGPRs, 6 waves / SIMD) beats T = 2 (115 VGPRs, 4 waves /
+// SIMD) in the C2 step, 0.131 vs 0.140 ms per launch (profiles/r6_msda_fwd_t_ab.txt): the gathers'
+// latency is hidden by more resident waves, not by more loads per wave; T = 2 forced to 5 waves
+// spilled (0.295 ms).
 //
 // COL (encoder problems, queries = the value grid, round 6): the queries are visited in
 // PYRAMID-COLUMN order (ColGeo, as the column backward: a column = an 8 x 16 block of the
@@ -1975,10 +1979,10 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
     int grid = grid_for(slots * 4, block, 256 * 64);
 #define VS_FWD4(LL)                                                                                          \
   if (col)                                                                                                   \
-    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2, true>), dim3(grid), dim3(block), 0, st, (const bf16*)value,   \
+    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 1, true>), dim3(grid), dim3(block), 0, st, (const bf16*)value,   \
                        loc, attw, (bf16*)out, lv, S, Hh, Q, slots, cg, cq);                                  \
   else                                                                                                       \
-    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc,    \
+    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 1>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc,    \
                        attw, (bf16*)out, lv, S, Hh, Q, groups, cg, 0)
     switch (L) {
       case 1: VS_FWD4(1); break;
