@@ -565,9 +565,6 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
     the oracle (bf16 output rounding: 2^-8 relative + 1e-4):
       * "col": msda_bwd_col_kernel, pyramid columns of 8 x 16 finest-level queries
         (3 chunks of 64), one flush per (band, cell) per column; "col16": 16 x 16 (6 chunks);
-      * "dst": msda_bwd_dst_kernel, 8 x 16 destination tiles per level, every cell written
-        once, far taps (> 4 cells from the query's reference point: jitter 3 / 12) through the
-        far-tap list and f32 atomics;
       * "tile" / "tile_s": msda_bwd_mfma_wg_kernel (VS_MSDA_COL=0), 8 x 8 query tiles, on its
         two band skeletons (VS_MSDA_SKEL 0 / 2), and "tile_sep" with the separate grad_loc
         gather kernel (VS_MSDA_GEOM=0).
@@ -607,7 +604,6 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
         "tile_s": dict(VS_MSDA_MFMA="1", VS_MSDA_GEOM="1", VS_MSDA_SKEL="2", VS_MSDA_COL="0"),
         "col": dict(VS_MSDA_MFMA="1", VS_MSDA_GEOM="1", VS_MSDA_SKEL="2", VS_MSDA_COL="8x16"),
         "col16": dict(VS_MSDA_MFMA="1", VS_MSDA_GEOM="1", VS_MSDA_SKEL="2", VS_MSDA_COL="16x16"),
-        "dst": dict(VS_MSDA_MFMA="1", VS_MSDA_GEOM="1", VS_MSDA_SKEL="2", VS_MSDA_COL="dst"),
     }
     for name, env in variants.items():
         for k, v in env.items():
@@ -623,7 +619,7 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
         geo[name] = (ld.grad.cpu(), wd.grad.cpu())
     # grad_loc / grad_attn fused into the band walk vs the separate gather kernel: the same
     # bf16 x bf16 products summed in f32 in another order
-    for name in ("tile", "col", "col16", "dst"):
+    for name in ("tile", "col", "col16"):
         for a, b in zip(geo[name], geo["tile_sep"]):
             sc = float(b.abs().max())
             assert float((a - b).abs().max()) <= 1e-4 * sc, (name, float((a - b).abs().max()) / sc)
@@ -639,7 +635,7 @@ def test_msda_mfma_backward_vs_binned_and_oracle(monkeypatch, win, jitter):
         bad = err > vr.grad.abs() * 2 ** -8 + 1e-4
         assert not bool(bad.any()), (name, float(err.max()), int(bad.sum()), float(vr.grad[bad][0]),
                                      float(gv[bad][0]))
-    for name in ("tile", "tile_s", "col", "col16", "dst"):
+    for name in ("tile", "tile_s", "col", "col16"):
         d = (grads[name] - grads["binned"]).abs()
         # all f32 sums, rounded to bf16 once: within two bf16 ulps, plus f32 summation-order
         # noise (~1e-7 of the summed magnitudes) where contributions cancel to ~0

@@ -153,10 +153,9 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T* __restrict__ val
 // (4 VGPRs each) before any is used, so 8 issue back to back instead of one tap's 4
 // (msda_fwd_kernel's runtime-P loop).  Same arithmetic, same order.  T = 4 (a level's 16
 // corner rows in flight) measured slower: 0.167 vs 0.156 ms at the C2 encoder shape.  Round 6:
-// T = 1 (4 corner rows in flight, 78 VGPRs, 6 waves / SIMD) beats T = 2 (115 VGPRs, 4 waves /
-// SIMD) in the C2 step, 0.131 vs 0.140 ms per launch (profiles/r6_msda_fwd_t_ab.txt): the gathers'
-// latency is hidden by more resident waves, not by more loads per wave; T = 2 forced to 5 waves
-// spilled (0.295 ms).
+// T = 1 (4 corner rows in flight, 84 VGPRs, 5 waves / SIMD) ties T = 2 (116 VGPRs, 4 waves /
+// SIMD) in the C2 step, 0.142 vs 0.140 ms per launch (profiles/r6_msda_fwd_t_ab.txt), so T = 2
+// stays; T = 2 forced to 5 waves spilled (0.295 ms).
 //
 // COL (encoder problems, queries = the value grid, round 6): the queries are visited in
 // PYRAMID-COLUMN order (ColGeo, as the column backward: a column = an 8 x 16 block of the
@@ -222,10 +221,17 @@ __global__ void __launch_bounds__(256) msda_fwd4_kernel(const bf16* __restrict__
       for (int hf = 0; hf < P / T; ++hf) {    // T taps (4T corner rows) in flight at a time
         float xs[T], ys[T], as[T];
 #pragma unroll
-        for (int p = 0; p < T; ++p) {
-          xs[p] = T == P ? xa[p] : (hf ? xa[T + p] : xa[p]);
-          ys[p] = T == P ? ya[p] : (hf ? ya[T + p] : ya[p]);
-          as[p] = T == P ? aa[p] : (hf ? aa[T + p] : aa[p]);
+        for (int p = 0; p < T; ++p) {          // select chain: keeps the loop rolled (VGPRs)
+          xs[p] = xa[p];
+          ys[p] = ya[p];
+          as[p] = aa[p];
+#pragma unroll
+          for (int h = 1; h < P / T; ++h)
+            if (hf == h) {
+              xs[p] = xa[h * T + p];
+              ys[p] = ya[h * T + p];
+              as[p] = aa[h * T + p];
+            }
         }
         uint4 raw[T][4];
         float cw[T][4];
@@ -1593,336 +1599,6 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
   }
 }
 
-// ---------------------------------------------------------------------------------
-// grad_value + grad_loc / grad_attn by DESTINATION TILES (default for bf16 encoder problems,
-// round 5).  The pyramid-column kernel above is query-driven: a column's taps reach a union
-// box that its neighbours' boxes overlap (offsets widen them), so every grad_value cell was
-// flushed ~2.5 times as 128-B f32 atomic rows (PMC: 320 MB written for 187 MB of outputs),
-// behind a memset of the f32 buffer, with 4 barriers per (band, chunk) pair.  Here a
-// workgroup OWNS an 8 x 16 tile T of one sampled level l: it enumerates the queries whose
-// taps can land in T, accumulates T's grad_value in the MFMA accumulators and writes every
-// cell of T exactly once with plain stores (no atomics, no memset, deterministic).
-//   * near / far: a query (m, y, x) has the anchor a = floor((y + 0.5) H_l / H_m - 0.5) (and
-//     the same in x) on level l -- its reference point there.  A tap is NEAR when its
-//     top-left corner, clamped to [-1, H_l - 1] x [-1, W_l - 1], lies within kDstR cells of
-//     the anchor (the encoder's sampling offsets are a few cells: with the Deformable-DETR
-//     init they are exactly <= 4).  Near taps are handled here; a FAR tap is appended by
-//     its anchor's home tile to a list that msda_bwd_far_kernel processes afterwards with
-//     f32 atomics (stream order puts them after these plain stores), so any offsets are
-//     correct and only their speed depends on the window.
-//   * candidates: for every query level m the rectangle of queries whose anchor lies within
-//     T dilated by kDstR + 1; a scan tests each candidate's 4 taps and compacts the queries
-//     with a near tap that touches T (a corner in T) or that T owns into an LDS list.
-//   * ownership: the tile containing the clamped top-left corner max(., 0) owns a near tap
-//     and writes its grad_loc / grad_attn (each tap exactly once; taps outside the level
-//     get zeros).  Its 4 corner dots d_k = g[q] . value[corner] read the tile's value rows
-//     staged in LDS with a 1-cell halo (rows / columns ty1, tx1).
-//   * per chunk of 64 listed queries (thread = query slot, point): the g rows staged, W[cell]
-//     [query] built with the points taking turns (as in the column kernel), ONE barrier, the
-//     product acc[cell][c] += W x g on MFMA (W in bf16 hi + lo) while every thread does its
-//     owned taps' dots (v_dot2 on bf16 pairs), one barrier, W cleared per wave.
-constexpr int kDstTY = 8, kDstTX = 16;       // destination tile (128 cells = 4 waves x 32)
-constexpr int kDstR = 4;                     // near window, cells of the sampled level
-constexpr int kDstList = 512;                // compacted query list (LDS)
-constexpr int kDstVRows = (kDstTY + 1) * (kDstTX + 1);
-
-struct DstGeo {
-  int ntx[kMaxLevels], nty[kMaxLevels];
-  int tile0[kMaxLevels + 1];                 // tile prefix in launch order
-  int lev[kMaxLevels];                       // sampled level of each segment (coarsest first)
-  int per_image;                             // tiles per image
-};
-
-__device__ __forceinline__ int dst_anchor(int y, int Hl, int Hm) {
-  return (int)floorf(((float)y + 0.5f) * ((float)Hl / (float)Hm) - 0.5f);
-}
-
-__device__ __forceinline__ float dot32_bf16(const short* a, const short* b) {
-  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint4 u = *reinterpret_cast<const uint4*>(a + 8 * i);
-    const uint4 v = *reinterpret_cast<const uint4*>(b + 8 * i);
-    s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, u.x), __builtin_bit_cast(bf2, v.x), s, false);
-    s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, u.y), __builtin_bit_cast(bf2, v.y), s, false);
-    s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, u.z), __builtin_bit_cast(bf2, v.z), s, false);
-    s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, u.w), __builtin_bit_cast(bf2, v.w), s, false);
-  }
-  return s;
-}
-
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-msda_bwd_dst_kernel(const float* __restrict__ loc, const float* __restrict__ attw, const bf16* __restrict__ gout,
-                    const bf16* __restrict__ value, float* __restrict__ gvalue, float* __restrict__ gloc,
-                    float* __restrict__ gattw, Levels lv, DstGeo dg, int S, int Hh, int L, int nblk,
-                    int* __restrict__ far_list, int* __restrict__ far_count) {
-  constexpr int P = 4;
-  __shared__ __attribute__((aligned(16))) float sW[kWFloats];          // W[cell][query slot]
-  __shared__ __attribute__((aligned(16))) short sg[64 * kD];           // g rows of the chunk
-  __shared__ __attribute__((aligned(16))) short sV[kDstVRows * kD];    // value rows, tile + halo
-  __shared__ int sList[kDstList];
-  __shared__ int sWave[4];
-  __shared__ int sCount;
-  const int blk = xcd_swizzle(blockIdx.x, nblk);                       // a tile's 8 heads: one XCD
-  const int h = blk % Hh;
-  const int t = (blk / Hh) % dg.per_image;
-  const int b = blk / Hh / dg.per_image;
-  int seg = 0;
-  while (seg + 1 < L && t >= dg.tile0[seg + 1]) ++seg;
-  const int l = dg.lev[seg];
-  const int tt = t - dg.tile0[seg];
-  const int Hl = lv.h[l], Wl = lv.w[l];
-  const int ty0 = (tt / dg.ntx[l]) * kDstTY, tx0 = (tt % dg.ntx[l]) * kDstTX;
-  const int ty1 = min(ty0 + kDstTY, Hl), tx1 = min(tx0 + kDstTX, Wl);
-  const int bh = ty1 - ty0, bw = tx1 - tx0, ncell = bh * bw, nmt = (ncell + 31) >> 5;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int tq = tid >> 2, tpt = tid & 3;
-  const int LP = L * P;
-  const size_t rowstride = (size_t)Hh * kD;
-  const size_t lbase = ((size_t)b * S * Hh + h) * kD + (size_t)lv.start[l] * rowstride;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  // value rows of the tile and its halo (rows ty0..ty1, columns tx0..tx1; zero outside the level)
-  const int vw = bw + 1, nv = (bh + 1) * vw;
-  for (int i = tid; i < nv * 4; i += 256) {
-    const int c = i >> 2, part = i & 3;
-    const int yy = ty0 + c / vw, xx = tx0 + c % vw;
-    bf16x8_t v = zero8();
-    if (yy < Hl && xx < Wl) v = ld8(value + lbase + (size_t)(yy * Wl + xx) * rowstride + 8 * part);
-    *reinterpret_cast<bf16x8_t*>(sV + c * kD + 8 * part) = v;
-  }
-  for (int i = tid; i < kWFloats / 4; i += 256) reinterpret_cast<float4*>(sW)[i] = z4;
-  if (tid == 0) sCount = 0;
-  f32x16_t acc;
-  zero16(acc);
-  const int zrow = 4 * ((lane >> 2) & 3) + (lane >> 4);   // W clear: 16 rows x 4 quads per wave
-  const int zr = nmt * 32;
-  __syncthreads();
-
-  // one chunk of (up to) 64 listed queries: W build, product, owned taps' grad_loc / grad_attn
-  auto run_chunk = [&](int base, int n) {
-    const int qslot = base + tq;
-    const int ent = tq < n ? sList[qslot] : -1;
-    const int q = ent >= 0 ? (ent & 0x0fffffff) : -1, m = ent >= 0 ? (ent >> 28) : 0;
-    int cell[4] = {-1, -1, -1, -1};
-    float cw[4] = {0.f, 0.f, 0.f, 0.f};
-    bool owned = false;
-    Tap tp;
-    float aw = 0.f;
-    long long o = 0;
-    if (q >= 0) {
-      const int lq = q - lv.start[m];
-      const int yq = lq / lv.w[m], xq = lq - yq * lv.w[m];
-      o = (((long long)b * S + q) * Hh + h) * LP + l * P + tpt;
-      const float2 xy = *reinterpret_cast<const float2*>(loc + o * 2);
-      aw = attw[o];
-      tp = tap_geom(xy.x, xy.y, Hl, Wl);
-      const int hc = min(max(tp.h0, -1), Hl - 1), wc = min(max(tp.w0, -1), Wl - 1);
-      const int ay = dst_anchor(yq, Hl, lv.h[m]), ax = dst_anchor(xq, Wl, lv.w[m]);
-      if (abs(hc - ay) <= kDstR && abs(wc - ax) <= kDstR) {
-        const int oy = max(hc, 0), ox = max(wc, 0);
-        owned = oy >= ty0 && oy < ty1 && ox >= tx0 && ox < tx1;
-        if (tp.inside) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int yy = tp.h0 + (k >> 1) - ty0, xx = tp.w0 + (k & 1) - tx0;
-            if ((unsigned)yy < (unsigned)bh && (unsigned)xx < (unsigned)bw) cell[k] = yy * bw + xx;
-            cw[k] = ((k >> 1) ? tp.lh : tp.hh) * ((k & 1) ? tp.lw : tp.hw) * aw;
-          }
-        }
-      }
-    }
-    // g row of the slot's query (thread = (slot, 16-B part))
-    {
-      bf16x8_t v = zero8();
-      if (q >= 0) v = ld8(gout + (((long long)b * S + q) * Hh + h) * kD + tpt * 8);
-      *reinterpret_cast<bf16x8_t*>(sg + tq * kD + tpt * 8) = v;
-    }
-#pragma unroll
-    for (int pt = 0; pt < P; ++pt) {          // a query's 4 points are lanes of one wave: take turns
-      if (tpt == pt) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (cell[k] >= 0) sW[cell[k] * kWP8 + tq] += cw[k];
-      }
-      wave_sync();
-    }
-    lds_barrier();
-    if (wave < nmt) {                         // acc[cell][c] += W[cell][q] g[q][c]
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const float* wr = sW + (32 * wave + r) * kWP8 + 16 * ks + 8 * hh;
-        const float4 w0 = *reinterpret_cast<const float4*>(wr);
-        const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
-        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        bf16x8_t ahi, alo;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const short hb = bf16_bits(wv[j]);
-          ahi[j] = hb;
-          alo[j] = bf16_bits(wv[j] - bf16_bits_to_f32((unsigned short)hb));
-        }
-        const bf16x8_t bq = tr8(sg, kD, 16 * ks, lane);
-        acc = mfma16(ahi, bq, acc);
-        acc = mfma16(alo, bq, acc);
-      }
-    }
-    if (owned) {                              // same formulas as msda_bwd_geom_kernel
-      float r_w = 0.f, r_x = 0.f, r_y = 0.f;
-      if (tp.inside) {
-        float d[4];
-        const short* gq = sg + tq * kD;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {         // corners in the staged rows ty0 - 1 .. ty1 (row -1: outside)
-          const int yy = tp.h0 + (k >> 1) - ty0, xx = tp.w0 + (k & 1) - tx0;
-          const bool in = yy >= 0 && xx >= 0 && tp.h0 + (k >> 1) < Hl && tp.w0 + (k & 1) < Wl;
-          d[k] = in ? dot32_bf16(sV + (yy * vw + xx) * kD, gq) : 0.f;
-        }
-        r_w = tp.hh * tp.hw * d[0] + tp.hh * tp.lw * d[1] + tp.lh * tp.hw * d[2] + tp.lh * tp.lw * d[3];
-        r_x = (float)Wl * aw * (-tp.hh * d[0] + tp.hh * d[1] - tp.lh * d[2] + tp.lh * d[3]);
-        r_y = (float)Hl * aw * (-tp.hw * d[0] - tp.lw * d[1] + tp.hw * d[2] + tp.lw * d[3]);
-      }
-      gattw[o] = r_w;
-      *reinterpret_cast<float2*>(gloc + o * 2) = make_float2(r_x, r_y);
-    }
-    lds_barrier();                            // W and g consumed
-    for (int rb = 0; rb < zr; rb += 16)
-      *reinterpret_cast<float4*>(sW + (rb + zrow) * kWP8 + 16 * wave + 4 * (lane & 3)) = z4;
-  };
-
-  for (int m = 0; m < L; ++m) {
-    const int Hm = lv.h[m], Wm = lv.w[m];
-    const float ry = (float)Hm / (float)Hl, rx = (float)Wm / (float)Wl;
-    const int ylo = max(0, (int)floorf((float)(ty0 - 1 - kDstR) * ry + 0.5f * ry - 0.5f) - 1);
-    const int yhi = min(Hm - 1, (int)ceilf((float)(ty1 - 1 + kDstR) * ry + 1.5f * ry - 0.5f) + 1);
-    const int xlo = max(0, (int)floorf((float)(tx0 - 1 - kDstR) * rx + 0.5f * rx - 0.5f) - 1);
-    const int xhi = min(Wm - 1, (int)ceilf((float)(tx1 - 1 + kDstR) * rx + 1.5f * rx - 0.5f) + 1);
-    const int ny = yhi - ylo + 1, nx = xhi - xlo + 1;
-    const int ncand = (ny > 0 && nx > 0) ? ny * nx : 0;
-    for (int c0 = 0; c0 < ncand; c0 += 256) {
-      // scan: one candidate query per thread, its 4 taps on level l
-      const int k = c0 + tid;
-      bool keep = false;
-      if (k < ncand) {
-        const int yq = ylo + k / nx, xq = xlo + k % nx;
-        const int q = lv.start[m] + yq * Wm + xq;
-        const int ay = dst_anchor(yq, Hl, Hm), ax = dst_anchor(xq, Wl, Wm);
-        const bool home = min(max(ay, 0), Hl - 1) >= ty0 && min(max(ay, 0), Hl - 1) < ty1 &&
-                          min(max(ax, 0), Wl - 1) >= tx0 && min(max(ax, 0), Wl - 1) < tx1;
-        const long long o0 = (((long long)b * S + q) * Hh + h) * LP + l * P;
-        const float4 l01 = *reinterpret_cast<const float4*>(loc + o0 * 2);
-        const float4 l23 = *reinterpret_cast<const float4*>(loc + o0 * 2 + 4);
-        const float px[4] = {l01.x, l01.z, l23.x, l23.z}, py[4] = {l01.y, l01.w, l23.y, l23.w};
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-          const Tap u = tap_geom(px[p], py[p], Hl, Wl);
-          const int hc = min(max(u.h0, -1), Hl - 1), wc = min(max(u.w0, -1), Wl - 1);
-          if (abs(hc - ay) <= kDstR && abs(wc - ax) <= kDstR) {
-            // touches T (a corner inside T) or owned by T
-            const bool touch = u.inside && hc + 1 >= ty0 && hc < ty1 && wc + 1 >= tx0 && wc < tx1;
-            const int oy = max(hc, 0), ox = max(wc, 0);
-            keep = keep || touch || (oy >= ty0 && oy < ty1 && ox >= tx0 && ox < tx1);
-          } else if (home) {
-            far_list[atomicAdd(far_count, 1)] = (int)(o0 + p);
-          }
-        }
-      }
-      // compaction: a wave ballot, then the waves' offsets
-      const unsigned long long bal = __ballot(keep);
-      const int wcount = __popcll(bal);
-      const int rank = __popcll(bal & ((1ull << lane) - 1ull));
-      if (lane == 0) sWave[wave] = wcount;
-      lds_barrier();
-      int off = sCount;
-      for (int w = 0; w < wave; ++w) off += sWave[w];
-      const int total = sCount + sWave[0] + sWave[1] + sWave[2] + sWave[3];
-      if (keep) {
-        const int yq = ylo + k / nx, xq = xlo + k % nx;
-        sList[off + rank] = (m << 28) | (lv.start[m] + yq * Wm + xq);
-      }
-      lds_barrier();
-      // process full chunks; keep the remainder at the front of the list
-      int done = 0;
-      while (total - done >= 64) {
-        run_chunk(done, 64);
-        done += 64;
-      }
-      const int rest = total - done;
-      if (done > 0 && rest > 0) {
-        const int v = tid < rest ? sList[done + tid] : 0;
-        lds_barrier();
-        if (tid < rest) sList[tid] = v;
-      }
-      if (tid == 0) sCount = rest;
-      lds_barrier();
-    }
-  }
-  if (sCount > 0) run_chunk(0, sCount);
-  // every cell of the tile, once
-  if (wave < nmt) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c = 32 * wave + crow(i, hh);
-      if (c < ncell) gvalue[lbase + (size_t)((ty0 + c / bw) * Wl + tx0 + c % bw) * rowstride + r] = acc[i];
-    }
-  }
-}
-
-// The far taps of msda_bwd_dst_kernel: grad_value by f32 atomics (after the tiles' plain
-// stores, stream order), grad_loc / grad_attn by gathers.  One thread per far tap.
-__global__ void __launch_bounds__(256) msda_bwd_far_kernel(const float* __restrict__ loc,
-                                                           const float* __restrict__ attw,
-                                                           const bf16* __restrict__ gout,
-                                                           const bf16* __restrict__ value,
-                                                           float* __restrict__ gvalue, float* __restrict__ gloc,
-                                                           float* __restrict__ gattw, Levels lv, int S, int Hh, int L,
-                                                           const int* __restrict__ far_list,
-                                                           const int* __restrict__ far_count) {
-  constexpr int P = 4;
-  const int n = *far_count;
-  const int LP = L * P;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const long long o = far_list[i];
-    const int lp = (int)(o % LP), l = lp / P;
-    const long long bqh = o / LP;
-    const int h = (int)(bqh % Hh);
-    const long long bq = bqh / Hh;
-    const int b = (int)(bq / S);
-    const int Hl = lv.h[l], Wl = lv.w[l];
-    const float2 xy = *reinterpret_cast<const float2*>(loc + o * 2);
-    const float aw = attw[o];
-    const Tap t = tap_geom(xy.x, xy.y, Hl, Wl);
-    float d[4] = {0.f, 0.f, 0.f, 0.f};
-    if (t.inside) {
-      const size_t rowstride = (size_t)Hh * kD;
-      const size_t lbase = ((size_t)b * S * Hh + h) * kD + (size_t)lv.start[l] * rowstride;
-      const bf16* g = gout + bqh * kD;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int yy = t.h0 + (k >> 1), xx = t.w0 + (k & 1);
-        if (yy < 0 || xx < 0 || yy >= Hl || xx >= Wl) continue;
-        const float cw = ((k >> 1) ? t.lh : t.hh) * ((k & 1) ? t.lw : t.hw) * aw;
-        const bf16* vr = value + lbase + (size_t)(yy * Wl + xx) * rowstride;
-        float* gv = gvalue + lbase + (size_t)(yy * Wl + xx) * rowstride;
-        float s = 0.f;
-        for (int c = 0; c < kD; ++c) {
-          const float gc = __bfloat162float(g[c]);
-          s += __bfloat162float(vr[c]) * gc;
-          atomicAdd(gv + c, cw * gc);
-        }
-        d[k] = s;
-      }
-    }
-    float r_w = 0.f, r_x = 0.f, r_y = 0.f;
-    if (t.inside) {
-      r_w = t.hh * t.hw * d[0] + t.hh * t.lw * d[1] + t.lh * t.hw * d[2] + t.lh * t.lw * d[3];
-      r_x = (float)Wl * aw * (-t.hh * d[0] + t.hh * d[1] - t.lh * d[2] + t.lh * d[3]);
-      r_y = (float)Hl * aw * (-t.hw * d[0] - t.lw * d[1] + t.hw * d[2] + t.lw * d[3]);
-    }
-    gattw[o] = r_w;
-    *reinterpret_cast<float2*>(gloc + o * 2) = make_float2(r_x, r_y);
-  }
-}
 
 int fill_levels(Levels* lv, const int64_t* shapes, const int64_t* starts, int L, int S) {
   long long tot = 0;
@@ -1979,10 +1655,10 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
     int grid = grid_for(slots * 4, block, 256 * 64);
 #define VS_FWD4(LL)                                                                                          \
   if (col)                                                                                                   \
-    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 1, true>), dim3(grid), dim3(block), 0, st, (const bf16*)value,   \
+    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2, true>), dim3(grid), dim3(block), 0, st, (const bf16*)value,   \
                        loc, attw, (bf16*)out, lv, S, Hh, Q, slots, cg, cq);                                  \
   else                                                                                                       \
-    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 1>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc,    \
+    hipLaunchKernelGGL((msda_fwd4_kernel<LL, 2>), dim3(grid), dim3(block), 0, st, (const bf16*)value, loc,    \
                        attw, (bf16*)out, lv, S, Hh, Q, groups, cg, 0)
     switch (L) {
       case 1: VS_FWD4(1); break;
@@ -2053,32 +1729,6 @@ static int col_geo(const Levels& lv, int L, int CY, int CX, ColGeo* cg) {
   return nch <= 6 ? nch : 0;
 }
 
-// destination-tile geometry (msda_bwd_dst_kernel): 8 x 16 tiles of every level, the
-// coarsest level's tiles first (they take the most queries: launched first, they finish
-// with the rest)
-static void dst_geo(const Levels& lv, int L, DstGeo* dg) {
-  int order[kMaxLevels];
-  for (int l = 0; l < L; ++l) order[l] = l;
-  for (int i = 1; i < L; ++i)
-    for (int j = i; j > 0; --j) {
-      const int a = order[j - 1], c = order[j];
-      if ((long long)lv.h[c] * lv.w[c] < (long long)lv.h[a] * lv.w[a]) std::swap(order[j - 1], order[j]);
-      else break;
-    }
-  int tot = 0;
-  for (int l = 0; l < kMaxLevels; ++l) dg->ntx[l] = dg->nty[l] = 1;
-  for (int i = 0; i < L; ++i) {
-    const int l = order[i];
-    dg->lev[i] = l;
-    dg->nty[l] = (lv.h[l] + kDstTY - 1) / kDstTY;
-    dg->ntx[l] = (lv.w[l] + kDstTX - 1) / kDstTX;
-    dg->tile0[i] = tot;
-    tot += dg->nty[l] * dg->ntx[l];
-  }
-  for (int i = L; i <= kMaxLevels; ++i) dg->tile0[i] = tot;
-  for (int i = L; i < kMaxLevels; ++i) dg->lev[i] = 0;
-  dg->per_image = tot;
-}
 
 static int msda_backward_impl(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,
                               const float* loc, const float* attw, const void* gout, float* gvalue, float* gloc,
@@ -2089,6 +1739,7 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   VS_CHECK(B > 0 && S > 0 && Hh > 0 && Q >= 0 && P > 0, "bad sizes");
   VS_CHECK(value && loc && attw && gout && gvalue && gloc && gattw && shapes && starts, "null pointer");
   VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  (void)ws;                                  // reserved (the destination-tile backward's far-tap list)
   Levels lv;
   VS_CHECK(fill_levels(&lv, shapes, starts, L, S), "spatial shapes / level starts inconsistent with S");
   hipStream_t st = (hipStream_t)stream;
@@ -2098,34 +1749,6 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
   bool split = groups >= kSplitMin;
   if (const char* e = getenv("VS_MSDA_RUN")) split = atoi(e) >= 1;   // tests: force either path
   split = split && P == 4;
-  // destination tiles (default for bf16 encoder problems with a workspace; VS_MSDA_DST=0:
-  // the pyramid-column kernel): every grad_value cell written once, no memset
-  // Opt-in (VS_MSDA_COL=dst or VS_MSDA_DST=1): measured SLOWER than the column kernel at
-  // the C2 encoder shapes (tools/kbench.py: 0.69 vs 0.39 ms, init offsets) -- a query's 4
-  // points land in 2-4 tiles per level, so each query is built into W about twice as often
-  // as in the column walk -- but every cell is written once, deterministic for near taps.
-  bool dst = ws != nullptr && split && dtype == VS_BF16 && Q == S && Q > 0 &&
-             (long long)B * Q * Hh * L * P < (1LL << 31);
-  bool want = false;
-  if (const char* e = getenv("VS_MSDA_DST")) want = atoi(e) != 0;
-  if (const char* e = getenv("VS_MSDA_COL")) want = want || strcmp(e, "dst") == 0;
-  dst = dst && want;
-  if (dst) {
-    DstGeo dg;
-    dst_geo(lv, L, &dg);
-    const long long nb = (long long)B * dg.per_image * Hh;
-    VS_CHECK(nb < (1LL << 31), "too many destination tiles");
-    int* far_count = (int*)ws;
-    int* far_list = far_count + 4;
-    VS_HIP(hipMemsetAsync(far_count, 0, sizeof(int), st));
-    hipLaunchKernelGGL(msda_bwd_dst_kernel, dim3((unsigned)nb), dim3(256), 0, st, loc, attw, (const bf16*)gout,
-                       (const bf16*)value, gvalue, gloc, gattw, lv, dg, S, Hh, L, (int)nb, far_list, far_count);
-    hipLaunchKernelGGL(msda_bwd_far_kernel, dim3(64), dim3(256), 0, st, loc, attw, (const bf16*)gout,
-                       (const bf16*)value, gvalue, gloc, gattw, lv, S, Hh, L, (const int*)far_list,
-                       (const int*)far_count);
-    VS_LAUNCH_CHECK();
-    return VS_OK;
-  }
   VS_HIP(hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * Hh * kD, st));
   if (Q == 0) return VS_OK;
   if (split) {
@@ -2146,10 +1769,9 @@ static int msda_backward_impl(int dtype, const void* value, const int64_t* shape
     bt.per_image = bt.mode == 1 ? bt.prefix[L] : (Q + te * te - 1) / (te * te);
     const long long nb2 = (long long)B * bt.per_image * Hh;
     VS_CHECK(nb2 < (1LL << 31), "too many query tiles");
-    // VS_MSDA_LDSBAR: mask of the band walk's barriers that order LDS only (bits of
-    // msda_bwd_mfma_wg_kernel's bar(); default all; 0 = __syncthreads everywhere)
-    int lbmask = 127;
-    if (const char* e = getenv("VS_MSDA_LDSBAR")) lbmask = atoi(e);
+    // every barrier of the tile kernel's band walk orders LDS only (msda_bwd_mfma_wg_kernel's
+    // bar() mask: the band's fire-and-forget atomics stay in flight across them)
+    const int lbmask = 127;
     // VS_MSDA_SKEL: band skeleton variant (2, default: clear-after; 0: zero-fill + barrier
     // at every band start)
     int skel = kMsdaSkelDefault;
@@ -2217,9 +1839,11 @@ extern "C" int vs_msda_backward(int dtype, const void* value, const int64_t* sha
                             P, stream);
 }
 
+// The destination-tile backward that used this workspace (its far-tap list) measured slower
+// than the column kernel and is gone (round 6); the entry point stays for ABI stability.
 extern "C" long long vs_msda_backward_workspace_bytes(int B, int Q, int Hh, int L, int P) {
   if (B < 0 || Q < 0 || Hh < 0 || L < 0 || P < 0) return -1;
-  return ((long long)B * Q * Hh * L * P + 4) * (long long)sizeof(int);
+  return 0;
 }
 
 extern "C" int vs_msda_backward_ex(int dtype, const void* value, const int64_t* shapes, const int64_t* starts,

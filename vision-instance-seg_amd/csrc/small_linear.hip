@@ -520,12 +520,8 @@ extern "C" int vs_small_linear_wgrad(int dtype, const void* grad_y, const void* 
     return VS_OK;
   }
   VS_CHECK(grad_y && x, "null pointer");
-  // token split over the waves from 2 chunks up (VS_SMALL_WGRAD_SPLIT=0: the chunk-serial kernel, A/B)
-  static const int split = [] {
-    const char* e = getenv("VS_SMALL_WGRAD_SPLIT");
-    return e ? atoi(e) : 1;
-  }();
-  if (split && tokens > kTC)
+  // token split over the waves from 2 chunks up (the chunk-serial kernel for one chunk)
+  if (tokens > kTC)
     hipLaunchKernelGGL(small_wgrad_split_kernel, dim3(in_features / kBlk, out_features / kBlk), dim3(256), 0,
                        (hipStream_t)stream, (const bf16*)grad_y, (const bf16*)x, (bf16*)grad_w, (bf16*)grad_b, tokens,
                        out_features, in_features);

@@ -382,10 +382,6 @@ __global__ void __launch_bounds__(64 * NG) token_wgrad_reduce_kernel(const WgGro
   }
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 
 // Plan one launch: the Linears share BO.  Every workgroup gets about the same number of
 // chunks C: C = max(8, total chunk-tiles / 256) (one workgroup per CU with 144 KB of LDS);
@@ -397,8 +393,7 @@ struct Plan {
 };
 
 void plan_group(const vs_wgrad_problem* probs, const int* idx, int n, int BO, int BI, int f32, Plan& pl) {
-  static const int target = env_int("VS_WGRAD_WGS", 256);
-  static const int minc = env_int("VS_WGRAD_MIN_CHUNKS", 8);
+  constexpr int target = 256, minc = 8;        // one workgroup per CU; >= 8 chunks a workgroup
   long long total = 0;
   for (int k = 0; k < n; ++k) {
     const vs_wgrad_problem& q = probs[idx[k]];
@@ -549,9 +544,9 @@ extern "C" int vs_token_wgrad_grouped(int dtype, const vs_wgrad_problem* probs, 
   VS_CHECK(need <= 256 || (workspace && ((uintptr_t)workspace & 15) == 0), "workspace: 16-B aligned, sized by "
            "vs_token_wgrad_grouped_workspace_bytes");
   hipStream_t st = (hipStream_t)stream;
-  // VS_WGRAD_SPREAD=1: the next chunk's DMA pieces issued between the MFMA steps instead of
-  // all after the barrier
-  static const int spread = env_int("VS_WGRAD_SPREAD", 1);
+  // the next chunk's DMA pieces are issued between the MFMA steps (all at once after the
+  // barrier, every wave at the same time, they idled the MFMA pipe: round 5)
+  const int spread = 1;
   return for_each_launch(probs, n, dtype == VS_F32, [&](int cfg, const Plan& pl) -> int {
     VS_CHECK(pl.wgs > 0 && pl.wgs < (1ll << 31), "bad workgroup count");
     float* part = (float*)workspace;
@@ -565,9 +560,8 @@ extern "C" int vs_token_wgrad_grouped(int dtype, const vs_wgrad_problem* probs, 
     VS_LAUNCH_CHECK();
     if (pl.items > 0) {
       const dim3 gr((unsigned)(pl.items / 64));
-      // VS_WGRAD_REDUCE_GROUPS: 4 or 16 split groups per block (default: 16 below 512 blocks)
-      static const int rgroups = env_int("VS_WGRAD_REDUCE_GROUPS", 0);
-      const bool wide = rgroups == 16 || (rgroups != 4 && pl.items / 64 < 512);
+      // 16 split groups per block below 512 blocks, else 4 (profiles/r5_wgrad_reduce_ab.txt)
+      const bool wide = pl.items / 64 < 512;
       if (cfg == 0 && wide)
         hipLaunchKernelGGL((token_wgrad_reduce_kernel<256, 128, 4, 2, 16>), gr, dim3(1024), 0, st, pl.g,
                            (const float*)part, (const float*)pb);

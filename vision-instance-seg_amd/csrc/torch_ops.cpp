@@ -114,7 +114,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> msda_bwd(const at::Tensor& value,
   // grad_value accumulates in f32 (float atomics), then takes value's dtype
   at::Tensor gv = at::empty({d.B, d.S, d.H, d.D}, v.options().dtype(at::kFloat));
   at::Tensor gl = at::empty_like(loc), ga = at::empty_like(aw);
-  // workspace of the destination-tile backward (its far-tap list; csrc/msda.hip)
+  // workspace: reserved by the C ABI (0 bytes since round 6; csrc/msda.hip)
   const long long wsb = vs_msda_backward_workspace_bytes(as_int(d.B, "batch"), as_int(d.Q, "queries"),
                                                          as_int(d.H, "heads"), as_int(d.L, "levels"),
                                                          as_int(d.P, "points"));

@@ -700,111 +700,13 @@ __device__ __forceinline__ void window_tokens_blk(const WinGeom& g, int bw, int*
   for (int t = threadIdx.x; t < 32 * NT; t += blockDim.x) tok[t] = token_meta(g, bw, t);
 }
 
-template <int NT, bool F8>
-__global__ void __launch_bounds__(64 * NT) win_attn_fwd_mfma_big(const bf16* __restrict__ qkv,
-                                                                 const float* __restrict__ table,
-                                                                 bf16* __restrict__ out, float* __restrict__ lse,
-                                                                 WinGeom g) {
-  constexpr int NP = 32 * NT, PT = NP + 8, PK = 40;
-  __shared__ __attribute__((aligned(16))) short sK[NP * PK];   // K [key][d]
-  __shared__ __attribute__((aligned(16))) short sVt[32 * PT];  // V^T [d][key]
-  __shared__ float sBias[kMaxT2Big + 2 * kZoneBig];
-  __shared__ __attribute__((aligned(16))) int sTok[NP];
-  int bw, h;
-  win_block(g, bw, h);
-  const int qt = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
-  const int N = g.N, C = g.heads * kD, C3 = 3 * C;
-  const bf16* win = qkv + (size_t)bw * N * C3;
-  // all global operands requested up front: two 16-B K / V chunks per thread (NP x 4
-  // chunks, 64 NT threads) and this lane's query row slices
-  bf16x8_t ck[2], cv[2], qb[2];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
-    const bf16* row = win + (size_t)t * C3 + h * kD + 8 * c;
-    ck[it] = t < N ? ld8(row + C) : zero8();
-    cv[it] = t < N ? ld8(row + 2 * C) : zero8();
-  }
-  static_assert(!F8, "fp8: win_attn_fwd_mx");
-  const int qrow = 32 * qt + r;
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-    qb[st] = qrow < N ? ld8(win + (size_t)qrow * C3 + h * kD + 16 * st + 8 * hh) : zero8();
-  window_tokens_blk<NT>(g, bw, sTok);
-  const float* bias = stage_bias(sBias, table, g, h, threadIdx.x, blockDim.x);
-  const bool mixed = window_mixed(g, bw);
-  const float scale2 = g.scale * kLog2e;
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int p = threadIdx.x + it * 64 * NT, t = p >> 2, c = p & 3;
-    *reinterpret_cast<bf16x8_t*>(sK + t * PK + 8 * c) = ck[it];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sVt[(8 * c + j) * PT + t] = cv[it][j];
-  }
-  __syncthreads();
-  const WinGeom& gl = g;
-  // S^T = K Q^T for every key tile of this wave's queries
-  f32x16_t acc[NT];
-#pragma unroll
-  for (int kt = 0; kt < NT; ++kt) zero16(acc[kt]);
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
-      const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(sK + (32 * kt + r) * PK + 16 * st + 8 * hh);
-      acc[kt] = mfma16(ka, qb[st], acc[kt]);
-    }
-  float m = -INFINITY;
-#pragma unroll
-  for (int kt = 0; kt < NT; ++kt) {
-    logits_tile(acc[kt], gl, scale2, mixed, sTok, bias, kt, qt, r, hh);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) m = fmaxf(m, acc[kt][i]);
-  }
-  m = fmaxf(m, __shfl_xor(m, 32, 64));
-  float sum = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < NT; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      acc[kt][i] = exp2_fast(acc[kt][i] - m);
-      sum += acc[kt][i];
-    }
-  sum += __shfl_xor(sum, 32, 64);
-  const float lq = (m + __log2f(sum)) * (1.f / kLog2e);
-  const float inv = 1.f / sum;
-  // O^T = V^T P^T
-  f32x16_t o;
-  zero16(o);
-  {
-#pragma unroll
-    for (int t = 0; t < 2 * NT; ++t) {
-      const int kt = t >> 1, th = t & 1;
-      const bf16x8_t a = ld_perm(sVt + r * PT, 32 * kt + 16 * th + 4 * hh);
-      o = mfma16(a, pack8(acc[kt], 8 * th), o);
-    }
-  }
-  const int q = qrow;
-  const long long orow = q < N ? out_row(g, bw, q) : -1;
-  if (q < N && hh == 0) lse[((size_t)bw * g.heads + h) * N + q] = lq;   // every token: the backward reads it
-  if (orow >= 0) {
-    bf16* dst = out + orow * C + h * kD;
-#pragma unroll
-    for (int grp = 0; grp < 4; ++grp) {
-      bf16x4_t v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = bf16_bits(o[4 * grp + e] * inv);
-      *reinterpret_cast<bf16x4_t*>(dst + 8 * grp + 4 * hh) = v;
-    }
-  }
-}
-
-// The same forward with an ONLINE softmax: a wave walks its key tiles keeping one S^T tile,
-// the running max / sum and the O^T accumulator live (rescaled by exp2(m_old - m_new) per
-// tile): 80 VGPRs instead of 120 (NT x 16 accumulators).  The kernel is latency-bound (SQ
-// counters at C5, profiles/r3_win_pmc.txt: waves parked at waitcnt / barrier ~45-50 % of
-// their cycles with 3 workgroups per CU), so the registers buy resident workgroups: 4 per
-// CU at NT = 5 (6 waves / SIMD) instead of 3.  The tile loop stays rolled: unrolled, the
+// Forward for 64 < N <= 160 (one workgroup per (window, head)) with an ONLINE softmax: a wave
+// walks its key tiles keeping one S^T tile, the running max / sum and the O^T accumulator live
+// (rescaled by exp2(m_old - m_new) per tile): 80 VGPRs instead of 120 for the two-pass form
+// (all NT S^T tiles live; removed in round 6).  The kernel is latency-bound (SQ counters at C5,
+// profiles/r3_win_pmc.txt: waves parked at waitcnt / barrier ~45-50 % of their cycles with 3
+// workgroups per CU), so the registers buy resident workgroups: 4 per CU at NT = 5 (6 waves /
+// SIMD) instead of 3 (C5 forward 0.88 -> 0.79 ms).  The tile loop stays rolled: unrolled, the
 // scheduler hoists every tile's QK^T MFMAs and all S^T tiles are live again.
 template <int NT>
 __global__ void __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(6))) win_attn_fwd_online(const bf16* __restrict__ qkv,
@@ -1736,29 +1638,9 @@ static bool use_mfma() {
   return !(e && atoi(e) != 0);
 }
 
-// VS_WIN_FWD_BLK=1: the one-workgroup-per-(window, head) forward also for N <= 64 (A/B)
-static bool fwd_blk_small() {
-  const char* e = getenv("VS_WIN_FWD_BLK");
-  return e && atoi(e) != 0;
-}
-
-// VS_WIN_FWD_ONLINE=0: the two-pass forward (all NT S^T tiles live) instead of the online one (A/B)
-static bool fwd_online() {
-  static const int v = [] {
-    const char* e = getenv("VS_WIN_FWD_ONLINE");
-    return e ? atoi(e) : 1;
-  }();
-  return v != 0;
-}
-
-// VS_WIN_XCD=0: the 2-D (window, head) grid instead of the XCD-grouped 1-D one (A/B)
-static dim3 blk_grid(dim3 g2) {
-  static const int v = [] {
-    const char* e = getenv("VS_WIN_XCD");
-    return e ? atoi(e) : 1;
-  }();
-  return v ? dim3(g2.x * g2.y) : g2;
-}
+// (window, head) workgroups as one XCD-grouped 1-D grid: a window's heads share L2 lines (round 4:
+// C5 backward -6.6 %, forward -16 %, C2 backward -12 % against the 2-D grid, profiles/r4_winbench_xcd.txt)
+static dim3 blk_grid(dim3 g2) { return dim3(g2.x * g2.y); }
 
 #define VS_NT_SWITCH(nt, M)            \
   switch (nt) {                        \
@@ -1773,18 +1655,12 @@ static void launch_fwd_blk(const WinGeom& g, dim3 grid, hipStream_t st, const vo
                            void* out, float* lse) {
   grid = blk_grid(grid);
 #define VS_FWD_BLK(NT_)                                                                                     \
-  if (F8 && fwd_online())                                                                                   \
+  if (F8)                                                                                                   \
     hipLaunchKernelGGL((win_attn_fwd_mx<NT_, true>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,   \
                        (bf16*)out, lse, g);                                                                 \
-  else if (F8)                                                                                              \
-    hipLaunchKernelGGL((win_attn_fwd_mx<NT_, false>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,  \
-                       (bf16*)out, lse, g);                                                                 \
-  else if (fwd_online())                                                                                    \
-    hipLaunchKernelGGL((win_attn_fwd_online<NT_>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,     \
-                       (bf16*)out, lse, g);                                                                 \
   else                                                                                                      \
-    hipLaunchKernelGGL((win_attn_fwd_mfma_big<NT_, false>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv,   \
-                       table, (bf16*)out, lse, g)
+    hipLaunchKernelGGL((win_attn_fwd_online<NT_>), grid, dim3(64 * NT_), 0, st, (const bf16*)qkv, table,     \
+                       (bf16*)out, lse, g)
   VS_NT_SWITCH((g.N + 31) / 32, VS_FWD_BLK)
 #undef VS_FWD_BLK
 }
@@ -1829,7 +1705,7 @@ extern "C" int vs_window_attn_forward(int dtype, const void* qkv, const float* t
   const size_t lds = sizeof(float) * (2 * g.N * kD + g.T2);
   dim3 grid(Bw, heads);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VS_BF16 && g.N <= 64 && use_mfma() && !fwd_blk_small()) {
+  if (dtype == VS_BF16 && g.N <= 64 && use_mfma()) {
     const int items = Bw * heads;
     hipLaunchKernelGGL(win_attn_fwd_mfma, dim3((items + kFwdWaves - 1) / kFwdWaves), dim3(64 * kFwdWaves), 0, st,
                        (const bf16*)qkv, table, (bf16*)out, lse, g, items);
@@ -1928,7 +1804,7 @@ extern "C" int vs_window_attn_forward_image(int dtype, int fp8, const void* qkv,
   hipStream_t st = (hipStream_t)stream;
   if (fp8) {
     launch_fwd_blk<true>(g, dim3(Bw, heads), st, qkv, table, out, lse);
-  } else if (g.N <= 64 && !fwd_blk_small()) {
+  } else if (g.N <= 64) {
     const int items = Bw * heads;
     hipLaunchKernelGGL(win_attn_fwd_mfma, dim3((items + kFwdWaves - 1) / kFwdWaves), dim3(64 * kFwdWaves), 0, st,
                        (const bf16*)qkv, table, (bf16*)out, lse, g, items);

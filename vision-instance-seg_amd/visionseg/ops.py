@@ -254,9 +254,6 @@ def window_reverse(windows, batch: int, height: int, width: int, window: int, sh
     return _WindowReverse.apply(windows, int(batch), int(height), int(width), int(window), int(shift))
 
 
-_TABLE_SUM_ATEN = os.environ.get("VS_TABLE_SUM_ATEN", "0") == "1"   # A/B: the ATen dim-0 sum
-
-
 def table_grad_from_partials(part):
     """f32 partials [P, heads, T] of the relative-position-table gradient (one per window,
     from the window-attention backward) -> their sum [heads, T] through the column-sum
@@ -265,8 +262,6 @@ def table_grad_from_partials(part):
     row of 8 heads*T columns, the remainder rows (< 8) added after."""
     P, H, T = part.shape
     R = H * T
-    if _TABLE_SUM_ATEN:
-        return part.sum(0)
     flat = part.reshape(P, R)
     if R % 8 == 0 and R <= 16384:
         return column_sum(flat).view(H, T)
