@@ -697,6 +697,19 @@ VS_API int vs_token_wgrad_grouped(int dtype, const vs_wgrad_problem* probs, int 
 VS_API int vs_token_wgrad(int dtype, const void* grad_y, long long ld_grad_y, const void* x, long long ld_x, void* dw,
                           void* db, void* workspace, long long tokens, int N, int K, void* stream);
 
+/* ---- a5-a7: W^T copies for the token Linears' input gradient -------------------------
+ * dst [cols, rows] = src [rows, cols]^T for a LIST of bf16 matrices (dtype VS_BF16) in one
+ * launch per 64 matrices; rows % 8 == 0, cols % 8 == 0, src / dst contiguous and 16-B
+ * aligned.  The dX = dY W GEMM of a token Linear (autograd's backward of F.linear, HF:swin /
+ * HF:m2f) runs on vs_token_gemm with W^T as its K-contiguous operand; this replaces one
+ * strided-copy launch per Linear. */
+typedef struct {
+  const void* src;
+  void* dst;
+  int rows, cols;
+} vs_transpose_item;
+VS_API int vs_transpose_batched(int dtype, const vs_transpose_item* items, int n, void* stream);
+
 /* ---- a9: the FPN's 3 x 3 output conv on NHWC planes (replaces MIOpen's conv + layout
  * transposes under nn.Conv2d(256, 256, 3, padding=1, bias=False), HF:m2f:1394-1419).
  * Stride 1, padding 1, bf16, channels-last x [B, H, W, Ci], y [B, H, W, Co].

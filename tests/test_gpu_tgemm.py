@@ -503,3 +503,44 @@ def test_token_wgrad_grouped_vs_f64():
             assert bool((err <= 2.0 ** -8 * r.abs() + 1e-5 * r.abs().max()).all()), (tuple(gy.shape), float(err.max()))
 
 
+
+def test_transpose_batched_bit_exact():
+    """ops.transpose_batched: one launch for matrices of different shapes (edge tiles, a
+    64-divisible one, the Swin-T weight shapes) equals src.t() bit for bit."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(5)
+    shapes = [(288, 96), (96, 384), (1536, 384), (8, 8), (72, 200), (384, 1536), (64, 128), (3072, 768)]
+    pairs = []
+    for R, C in shapes:
+        src = _rand((R, C), g).to(DEV)
+        pairs.append((src, torch.full((C, R), float("nan"), device=DEV, dtype=torch.bfloat16)))
+    ops.transpose_batched(pairs)
+    for src, dst in pairs:
+        assert torch.equal(dst, src.t().contiguous()), tuple(src.shape)
+
+
+def test_linear_dgrad_weight_transposes_bit_exact(monkeypatch):
+    """The dX GEMMs of a stack of token Linears read the W^T copies written by ONE batched
+    launch at the first backward use (linear._WT): dX equals the per-call weight.t().contiguous()
+    path bit for bit, and nothing stays pending after the backward."""
+    from visionseg import linear as lin
+    g = torch.Generator().manual_seed(9)
+    x = _rand((4, 4096, 192), g).to(DEV)
+    w1, b1 = _rand((576, 192), g, 0.05).to(DEV), _rand((576,), g).to(DEV)
+    w2, b2 = _rand((192, 576), g, 0.05).to(DEV), _rand((192,), g).to(DEV)
+    gy = _rand((4, 4096, 192), g).to(DEV)
+    assert lin._dgrad_on_token_gemm(4 * 4096, w2, torch.bfloat16)
+
+    def run(batched):
+        if not batched:
+            monkeypatch.setattr(lin._WT, "request", lambda w: None)
+        ps = [t.clone().requires_grad_() for t in (x, w1, b1, w2, b2)]
+        xs, a1, c1, a2, c2 = ps
+        lin.linear_tokens(lin.linear_tokens(xs, a1, c1), a2, c2).backward(gy)
+        monkeypatch.undo()
+        return [p.grad for p in ps]
+
+    a, b = run(True), run(False)
+    assert not lin._WT.pending
+    for p, q in zip(a, b):
+        assert torch.equal(p, q)

@@ -120,6 +120,7 @@ SIGNATURES = {
     "vs_token_wgrad_workspace_bytes": [ctypes.c_longlong, _c_int, _c_int],
     "vs_token_wgrad_grouped_workspace_bytes": [_P, _c_int],
     "vs_token_wgrad_grouped": [_c_int, _P, _c_int, _P, _P],
+    "vs_transpose_batched": [_c_int, _P, _c_int, _P],
     "vs_token_wgrad": [_c_int, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P, _P, _P, ctypes.c_longlong, _c_int,
                        _c_int, _P],
     "vs_conv3x3_forward": [_P, _P, _P, _P] + [_c_int] * 5 + [_P],

@@ -170,13 +170,60 @@ def _use_token_gemm_dgrad(T: int, K_out: int, N_red: int) -> bool:
     return T <= 300_000 and not (N_red >= 4 * K_out and T <= 100_000)
 
 
-def _dgrad_gemm(gy2, weight):
-    """dX = dY W for dY [T, N] and W [N, K] (no residual term)."""
+def _dgrad_on_token_gemm(T: int, weight, dtype) -> bool:
     N, K = weight.shape
-    T = gy2.shape[0]
-    if (_TGEMM_DGRAD and gy2.is_cuda and gy2.dtype == weight.dtype == torch.bfloat16 and K % 8 == 0 and N % 8 == 0
-            and T >= MIN_TOKENS and _use_token_gemm_dgrad(T, K, N)):
-        return ops.token_gemm(gy2.contiguous(), weight.t().contiguous())
+    return (_TGEMM_DGRAD and weight.is_cuda and dtype == weight.dtype == torch.bfloat16 and K % 8 == 0
+            and N % 8 == 0 and T >= MIN_TOKENS and _use_token_gemm_dgrad(T, K, N))
+
+
+class _WeightTransposes:
+    """W^T [K, N] copies of the token Linears' weights for the dX GEMM on the token GEMM
+    (whose operands are both K-contiguous rows): requested in the forward (request), all
+    written by ONE batched launch (ops.transpose_batched) at the first use in the backward
+    (get).  Before, each dX GEMM made its own weight.t().contiguous(): 53 strided-copy
+    launches per C2 step (0.33 ms, profiles/r6_glue_c2.txt).  The weights do not change
+    between a forward and its backward (the optimizer steps after).  A request never used
+    (a forward without backward) is dropped after `cap` newer ones; get() then falls back to
+    its own copy."""
+
+    def __init__(self, cap: int = 1024):
+        self.pending = []
+        self.cap = cap
+
+    def request(self, weight):
+        h = [weight, torch.empty(weight.shape[1], weight.shape[0], device=weight.device, dtype=weight.dtype), False]
+        self.pending.append(h)
+        if len(self.pending) > self.cap:
+            self.pending.pop(0)
+        return h
+
+    def flush(self):
+        by_dev = {}
+        for h in self.pending:
+            by_dev.setdefault(h[0].device, []).append(h)
+        for hs in by_dev.values():
+            ops.transpose_batched([(h[0].detach().contiguous(), h[1]) for h in hs])
+            for h in hs:
+                h[2] = True
+        self.pending = []
+
+    def get(self, h):
+        if not h[2]:
+            if any(p is h for p in self.pending):
+                self.flush()
+            else:                     # dropped: a copy of its own
+                return h[0].t().contiguous()
+        return h[1]
+
+
+_WT = _WeightTransposes()
+
+
+def _dgrad_gemm(gy2, weight, wt=None):
+    """dX = dY W for dY [T, N] and W [N, K] (no residual term); wt: the _WT request made in
+    the forward when this GEMM was known to run on the token GEMM."""
+    if _dgrad_on_token_gemm(gy2.shape[0], weight, gy2.dtype) and gy2.is_cuda:
+        return ops.token_gemm(gy2.contiguous(), _WT.get(wt) if wt is not None else weight.t().contiguous())
     return gy2 @ weight.to(gy2.dtype)
 
 
@@ -188,6 +235,9 @@ class _LinearFn(torch.autograd.Function):
         ctx.sink = sink
         if sink is not None:
             sink.arm()
+        # the dX GEMM's W^T (only where it runs without the residual term, on the token GEMM)
+        T = x.numel() // max(1, x.shape[-1])
+        ctx.wt = (_WT.request(weight) if sink is None and _dgrad_on_token_gemm(T, weight, x.dtype) else None)
         return _forward_gemm(x, weight, bias)
 
     @staticmethod
@@ -200,7 +250,8 @@ class _LinearFn(torch.autograd.Function):
             if gres is not None:       # the residual path's gradient of x, added by the GEMM (beta = 1)
                 gx = _addmm_into(gres.reshape(gy2.shape[0], -1), gy2, weight.to(gy2.dtype)).view(x.shape)
             else:
-                gx = _dgrad_gemm(gy2, weight).view(x.shape)
+                gx = _dgrad_gemm(gy2, weight, ctx.wt).view(x.shape)
+        ctx.wt = None
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         cs = ops.take_colsum(gy) if want_b else None               # from the LayerNorm backward's pass
         if cs is not None:
@@ -1028,6 +1079,7 @@ class _LinearGeluFn(torch.autograd.Function):
             y, pre, q = out
         else:
             y, pre = out
+        ctx.wt = _WT.request(weight) if not fp8 and _dgrad_on_token_gemm(x2.shape[0], weight, x.dtype) else None
         ctx.save_for_backward(x, weight, pre)
         ctx.has_bias = bias is not None
         ctx.fp8 = bool(fp8)
@@ -1050,7 +1102,8 @@ class _LinearGeluFn(torch.autograd.Function):
                                                    L.ptr(ws), M, N, L.stream(pre)), "act_backward_colsum")
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = (_dgrad(gp, weight) if ctx.fp8 else _dgrad_gemm(gp, weight)).view(x.shape)
+            gx = (_dgrad(gp, weight) if ctx.fp8 else _dgrad_gemm(gp, weight, ctx.wt)).view(x.shape)
+        ctx.wt = None
         if ctx.needs_input_grad[1]:
             gw = weight_grad(gp, x.reshape(-1, x.shape[-1]), weight.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:

@@ -1800,10 +1800,8 @@ def token_wgrad_grouped(items, out_dtype):
     arr = (WgradProblem * n)()
     flops = 0.0
     for k, (gy, x, dw, db) in enumerate(items):
-        # dw / db: tensors, or raw device addresses (linear._DeferredWgrads holds no tensor
-        # reference to them, so that autograd adopts them as .grad without a copy)
-        pw = dw.data_ptr() if torch.is_tensor(dw) else int(dw)
-        pb = (db.data_ptr() if torch.is_tensor(db) else int(db)) if db is not None else None
+        pw = dw.data_ptr()
+        pb = db.data_ptr() if db is not None else None
         arr[k] = WgradProblem(gy.data_ptr(), x.data_ptr(), pw, pb, gy.stride(0), x.stride(0), gy.shape[0],
                               gy.shape[1], x.shape[1])
         flops += 2.0 * gy.shape[0] * gy.shape[1] * x.shape[1]
@@ -1814,6 +1812,24 @@ def token_wgrad_grouped(items, out_dtype):
     with timed("token_wgrad", gy0, flops=flops, bytes_=sum(it[0].shape[0] * (it[0].shape[1] + it[1].shape[1]) * 2
                                                            for it in items)):
         L.check(L.lib().vs_token_wgrad_grouped(code, arr, n, L.ptr(ws), L.stream(gy0)), "token_wgrad_grouped")
+
+
+class TransposeItem(ctypes.Structure):
+    """vs_transpose_item (include/visionseg.h)."""
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int), ("cols", ctypes.c_int)]
+
+
+def transpose_batched(pairs):
+    """dst.copy_(src.t()) for every (src [R, C], dst [C, R]) pair -- contiguous bf16 device
+    tensors, R % 8 == 0, C % 8 == 0 -- in one launch (vs_transpose_batched)."""
+    if not pairs:
+        return
+    L.require_hip(pairs[0][0])
+    arr = (TransposeItem * len(pairs))()
+    for k, (src, dst) in enumerate(pairs):
+        assert src.is_contiguous() and dst.is_contiguous() and dst.shape == (src.shape[1], src.shape[0])
+        arr[k] = TransposeItem(src.data_ptr(), dst.data_ptr(), src.shape[0], src.shape[1])
+    L.check(L.lib().vs_transpose_batched(L.VS_BF16, arr, len(pairs), L.stream(pairs[0][0])), "transpose_batched")
 
 
 # ------------------------------------------------------------------ 3 x 3 conv (channels-last)
