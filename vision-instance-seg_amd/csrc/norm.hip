@@ -376,159 +376,6 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(const T* __restrict__ 
   }
 }
 
-// the register image of a chunk made opaque to the compiler: the values derived from it
-// (xhat, dy * w) are recomputed in the second pass instead of being kept live across the
-// row's reductions
-__device__ __forceinline__ void opaque(RawChunk<bf16>& c) {
-  asm volatile("" : "+v"(c.a.x), "+v"(c.a.y), "+v"(c.a.z), "+v"(c.a.w));
-}
-__device__ __forceinline__ void opaque(RawChunk<float>& c) {
-  asm volatile("" : "+v"(c.a.x), "+v"(c.a.y), "+v"(c.a.z), "+v"(c.a.w));
-  asm volatile("" : "+v"(c.b.x), "+v"(c.b.y), "+v"(c.b.z), "+v"(c.b.w));
-}
-
-// ln_bwd_kernel with two passes over the PACKED row (xhat and dy * w recomputed from the
-// loaded bits in the second pass, gamma held packed): 48-72 fewer VGPRs, so more waves per
-// SIMD keep HBM reads in flight; U rows per iteration.
-template <typename T, int K, bool ADD, bool CS, int U>
-__global__ void __launch_bounds__(kThreads) ln_bwd2_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                           const T* __restrict__ w, const float* __restrict__ mean,
-                                                           const float* __restrict__ rstd, T* __restrict__ dx,
-                                                           float* __restrict__ part, int M, int C, int G,
-                                                           const T* __restrict__ dres = nullptr,
-                                                           const int* __restrict__ dyrows = nullptr) {
-  extern __shared__ float red[];             // [4 waves][NR][C]
-  constexpr int NR = CS ? 3 : 2;
-  const int nch = C >> 3;
-  const int lane = threadIdx.x & (G - 1);
-  const int grp = threadIdx.x / G;
-  const int rows_per_block = kThreads / G;
-  const float invC = 1.f / (float)C;
-  float dw[K][8], db[K][8], ds[CS ? K : 1][8];
-  RawChunk<T> wr[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int j = lane + k * G;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) dw[k][i] = db[k][i] = 0.f;
-    if constexpr (CS) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ds[k][i] = 0.f;
-    }
-    if (j < nch) wr[k].load(w + j * 8);
-    else wr[k].zero();
-  }
-  const long long stride = (long long)gridDim.x * rows_per_block;
-  for (long long row0 = (long long)blockIdx.x * rows_per_block + grp; row0 < M; row0 += U * stride) {
-    RawChunk<T> xr[U][K], dr[U][K], rr[ADD ? U : 1][ADD ? K : 1];
-    float mu[U], rs[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long row = row0 + u * stride;
-      const bool ok = row < M;
-      mu[u] = ok ? mean[row] : 0.f;
-      rs[u] = ok ? rstd[row] : 0.f;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int j = lane + k * G;
-        if (ok && j < nch) {
-          xr[u][k].load(x + row * C + j * 8);
-          dr[u][k].load(dy + (dyrows ? (long long)dyrows[row] : row) * C + j * 8);
-          if constexpr (ADD) rr[u][k].load(dres + row * C + j * 8);
-        } else {
-          xr[u][k].zero();
-          dr[u][k].zero();
-          if constexpr (ADD) rr[u][k].zero();
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long row = row0 + u * stride;
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float xv[8], dv[8], wv[8];
-        xr[u][k].unpack(xv);
-        dr[u][k].unpack(dv);
-        wr[k].unpack(wv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float xh = (xv[i] - mu[u]) * rs[u];      // masked chunks / rows have dv = 0: no effect
-          const float g = dv[i] * wv[i];
-          s1 += g;
-          s2 += g * xh;
-          dw[k][i] += dv[i] * xh;
-          db[k][i] += dv[i];
-        }
-      }
-      s1 = group_sum(s1, G) * invC;
-      s2 = group_sum(s2, G) * invC;
-      if (row < M) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const int j = lane + k * G;
-          if (j < nch) {
-            opaque(xr[u][k]);
-            opaque(dr[u][k]);
-            float xv[8], dv[8], wv[8], o[8];
-            xr[u][k].unpack(xv);
-            dr[u][k].unpack(dv);
-            wr[k].unpack(wv);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const float xh = (xv[i] - mu[u]) * rs[u];
-              o[i] = rs[u] * (dv[i] * wv[i] - s1 - xh * s2);
-            }
-            if constexpr (ADD) {
-              float rv[8];
-              rr[u][k].unpack(rv);
-#pragma unroll
-              for (int i = 0; i < 8; ++i) o[i] += rv[i];
-            }
-            store_chunk(dx + row * C + j * 8, o);
-            if constexpr (CS) {
-#pragma unroll
-              for (int i = 0; i < 8; ++i) ds[k][i] += to_f32(from_f32<T>(o[i]));
-            }
-          }
-        }
-      }
-    }
-  }
-  for (int o = G; o < 64; o <<= 1) {
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        dw[k][i] += __shfl_xor(dw[k][i], o, 64);
-        db[k][i] += __shfl_xor(db[k][i], o, 64);
-        if constexpr (CS) ds[k][i] += __shfl_xor(ds[k][i], o, 64);
-      }
-  }
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) < G) {
-    float* mine = red + (size_t)wave * NR * C;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int j = lane + k * G;
-      if (j < nch) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          mine[j * 8 + i] = dw[k][i];
-          mine[C + j * 8 + i] = db[k][i];
-          if constexpr (CS) mine[2 * C + j * 8 + i] = ds[k][i];
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < NR * C; c += kThreads) {
-    const float acc = (red[c] + red[NR * C + c]) + (red[2 * NR * C + c] + red[3 * NR * C + c]);
-    part[(size_t)blockIdx.x * NR * C + c] = acc;
-  }
-}
-
 // column sums of x [M, N] -> part[blockIdx][N] (f32); a thread owns one 8-column chunk
 // and a subset of rows
 // Row segments of a [B, S, N] tensor (the levels of a multi-scale token sequence):
@@ -988,13 +835,10 @@ static int add_layer_norm_forward_impl(int dtype, const void* x, const void* r, 
   return VS_OK;
 }
 
-// workgroups of the LayerNorm backward sweep: VS_LN_BWD_PARTS (A/B; <= kMaxPartialsLN)
-constexpr int kMaxPartialsLN = 2048;
-static int ln_bwd_parts() {
-  int p = 512;
-  if (const char* e = getenv("VS_LN_BWD_PARTS")) p = atoi(e);
-  return std::min(std::max(p, 1), kMaxPartialsLN);
-}
+// workgroups of the LayerNorm backward sweep (512 vs 256 / 1024 at the C2 shapes:
+// profiles/r6_ln_bwd_ab.txt)
+constexpr int kMaxPartialsLN = 512;
+static int ln_bwd_parts() { return kMaxPartialsLN; }
 
 extern "C" long long vs_layer_norm_backward_workspace_bytes(int M, int C) {
   return (long long)kMaxPartialsLN * 3 * C * sizeof(float);   // dw, db (+ dx column sums)
@@ -1039,26 +883,16 @@ static int layer_norm_backward_impl(int dtype, const void* dy, const void* x, co
   VS_CHECK(M >= 0 && C > 0 && C % 8 == 0, "C must be a positive multiple of 8");
   VS_CHECK(w && dw && db && ws && (M == 0 || (dy && x && mean && rstd && dx)), "null pointer");
   int G, K;
-  static const int bkmax = getenv("VS_LN_BWD_KMAX") ? atoi(getenv("VS_LN_BWD_KMAX")) : 4;
-  if (!pick_gk(C / 8, bkmax, &G, &K))
-    VS_CHECK(pick_gk(C / 8, ln_kmax(dtype), &G, &K), "row too long for the LayerNorm kernel (C <= 2048)");
+  VS_CHECK(pick_gk(C / 8, ln_kmax(dtype), &G, &K), "row too long for the LayerNorm kernel (C <= 2048)");
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   const int grid = blocks_for(M, kThreads / G, ln_bwd_parts());
   const int NR = dsum ? 3 : 2;
   const size_t lds = (size_t)(kThreads / 64) * NR * C * sizeof(float);
   VS_CHECK(lds <= 64 * 1024, "LayerNorm backward LDS budget exceeded");
-  static const int v2 = getenv("VS_LN_BWD2") ? atoi(getenv("VS_LN_BWD2")) : 0;
-#define VS_LNB_T(TT, KK, AD, CS_)                                                                              \
-  if (v2 == 1)                                                                                                  \
-    hipLaunchKernelGGL((ln_bwd2_kernel<TT, KK, AD, CS_, 1>), dim3(grid), dim3(kThreads), lds, st, (const TT*)dy, \
-                       (const TT*)x, (const TT*)w, mean, rstd, (TT*)dx, part, M, C, G, (const TT*)dres, dyrows); \
-  else if (v2 == 2)                                                                                             \
-    hipLaunchKernelGGL((ln_bwd2_kernel<TT, KK, AD, CS_, 2>), dim3(grid), dim3(kThreads), lds, st, (const TT*)dy, \
-                       (const TT*)x, (const TT*)w, mean, rstd, (TT*)dx, part, M, C, G, (const TT*)dres, dyrows); \
-  else                                                                                                          \
-    hipLaunchKernelGGL((ln_bwd_kernel<TT, KK, AD, CS_>), dim3(grid), dim3(kThreads), lds, st, (const TT*)dy,    \
-                       (const TT*)x, (const TT*)w, mean, rstd, (TT*)dx, part, M, C, G, (const TT*)dres, dyrows)
+#define VS_LNB_T(TT, KK, AD, CS_)                                                                            \
+  hipLaunchKernelGGL((ln_bwd_kernel<TT, KK, AD, CS_>), dim3(grid), dim3(kThreads), lds, st, (const TT*)dy,    \
+                     (const TT*)x, (const TT*)w, mean, rstd, (TT*)dx, part, M, C, G, (const TT*)dres, dyrows)
 #define VS_LNB_D(TT, KK)                                        \
   if (dres && dsum) {                                            \
     VS_LNB_T(TT, KK, true, true);                               \
