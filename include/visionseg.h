@@ -431,6 +431,14 @@ VS_API long long vs_column_sum_workspace_bytes(int rows, int cols);
 /* out[n] = sum_m x[m, n] (f32 accumulation, fixed order); N a multiple of 8, <= 2048. */
 VS_API int vs_column_sum(int dtype, const void* x, void* out, void* workspace, int rows, int cols,
                          void* stream);
+/* a4: the relative-position-table gradient from the window-attention backward's per-window
+ * partials part [P, heads, T] (f32, T = (2 ws - 1)^2) -> out [T, heads] (dtype VS_BF16 /
+ * VS_F32: the table's own layout and dtype), summed in a fixed order (deterministic).  The
+ * rows are folded F at a time so the column-sum width is a multiple of 8 (F = 1, 2, 4 or 8
+ * by heads * T): P % F == 0.  Workspace from vs_rel_table_grad_workspace_bytes.  Replaces
+ * the table gradient autograd forms for HF:swin's relative_position_bias_table gather. */
+VS_API long long vs_rel_table_grad_workspace_bytes(int P, int heads, int T);
+VS_API int vs_rel_table_grad(int dtype, const float* part, void* out, void* ws, int P, int heads, int T, void* stream);
 VS_API long long vs_column_sum_segments_workspace_bytes(int batch, int cols, int nseg);
 /* Per-segment column sums of x [B, S, N] (f32 out [nseg, N], fixed order): segment k =
  * rows [seg_start[k], seg_start[k+1]) of every image (host array of nseg + 1 ints,

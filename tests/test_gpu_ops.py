@@ -895,6 +895,25 @@ def test_window_table_grad_partial_sum(P, H, T):
     assert bool(((got - ref).abs() <= bound).all()), float((got - ref).abs().max())
 
 
+@pytest.mark.parametrize("P,H,T", [(5476, 3, 169), (400, 12, 169), (1444, 6, 169), (100, 24, 169), (7, 3, 169),
+                                   (13, 4, 529), (64, 8, 529), (100, 48, 529), (9, 2, 8), (12, 1, 3)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_rel_table_grad_fold(P, H, T, dtype):
+    """ops.rel_table_grad: the partials folded to a multiple-of-8 width, column-summed, folded
+    back, transposed to the table's [T, heads] layout and cast (vs_rel_table_grad; the 4-5
+    launch composition where P does not fold) vs an f64 sum: one f32 rounding per partial,
+    then the output dtype's rounding."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(P * 5 + H)
+    part = torch.randn(P, H, T, generator=g)
+    ref = part.double().sum(0).t()
+    got = ops.rel_table_grad(part.to(DEV), dtype)
+    assert got.shape == (T, H) and got.dtype == dtype
+    got = got.double().cpu()
+    bound = P * 2.0 ** -23 * part.double().abs().sum(0).t() + (2.0 ** -8 * ref.abs() if dtype == torch.bfloat16 else 0)
+    assert bool(((got - ref).abs() <= bound + 1e-30).all()), float((got - ref).abs().max())
+
+
 @pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("ws,shift,heads,nWh,nWw,amp", [(12, 6, 4, 3, 3, 1.0), (7, 3, 3, 4, 4, 1.0), (12, 0, 2, 2, 2, 12.0),
                                                         (10, 5, 3, 3, 2, 1.0), (12, 6, 6, 4, 4, 0.0)])

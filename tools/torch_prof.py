@@ -64,6 +64,12 @@ def main():
             if "visionseg" in fr or "bench.py" in fr:
                 site = fr.split("vision-instance-seg_amd/")[-1][:90]
                 break
+        if site == "?":                  # autograd's C++ backward nodes: the nearest named ancestor
+            par = ev.cpu_parent
+            while par is not None and par.name.startswith("aten::"):
+                par = par.cpu_parent
+            if par is not None:
+                site = par.name[:90]
         s = by_site[(ev.name, site)]
         s[0] += ev.device_time_total / 1e3 / STEPS
         s[1] += 1
@@ -71,7 +77,7 @@ def main():
         total += ev.device_time_total / 1e3 / STEPS
     print(f"\n== glue ops by call site: {total:.3f} ms per step")
     for (name, site), (ms, n, shp) in sorted(by_site.items(), key=lambda kv: -kv[1][0])[:60]:
-        print(f"{ms:8.3f} ms {n // STEPS:4d}  {name:22s} {site:90s} {sorted(shp)[0]}")
+        print(f"{ms:8.3f} ms {n // STEPS:4d}  {name:22s} {site:90s} {' '.join(sorted(shp)[:8])[:400]}")
 
 
 if __name__ == "__main__":

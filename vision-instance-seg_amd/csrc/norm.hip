@@ -577,6 +577,39 @@ __global__ void __launch_bounds__(kCsThreads) colsum_partials_kernel(const float
   }
 }
 
+// Relative-position-table gradient from per-window partials: the partial rows [P, H*T]
+// were column-summed as [P/F, F*H*T] (F folds rows so the width is a multiple of 8: H*T is
+// odd * heads for the (2ws-1)^2 tables) into part[nb][F*H*T]; out[t][h] = sum over b, f of
+// part[b][f*H*T + h*T + t] in a fixed order, written transposed ([T, H]: the table's own
+// layout) in the table's dtype.  Same block shape as colsum_partials_kernel.
+template <typename T>
+__global__ void __launch_bounds__(kCsThreads) table_fold_kernel(const float* __restrict__ part, T* __restrict__ out,
+                                                                int nb, int F, int H, int TT) {
+  constexpr int S = kCsSlices;
+  __shared__ float red[S][33];
+  const int lane = threadIdx.x & 31;
+  const int sl = threadIdx.x >> 5;
+  const int R = H * TT, W = F * R;
+  const int col = blockIdx.x * 32 + lane;      // h * TT + t
+  float a0 = 0.f, a1 = 0.f;
+  if (col < R) {
+    for (int r = sl; r < nb; r += S)
+      for (int f = 0; f < F; ++f) {
+        if (f & 1) a1 += part[(size_t)r * W + f * R + col];
+        else a0 += part[(size_t)r * W + f * R + col];
+      }
+  }
+  red[sl][lane] = a0 + a1;
+  __syncthreads();
+  if (sl == 0 && col < R) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < S; ++i) t += red[i][lane];
+    const int h = col / TT, tt = col - h * TT;
+    out[(size_t)tt * H + h] = from_f32<T>(t);
+  }
+}
+
 // split-K epilogue: out[i] = sum_{s < S} part[s][i] (+ extra[i]), f32 accumulation in a
 // fixed order, written in the output dtype; 4 elements per thread (float4), 4 partial
 // rows in flight
@@ -948,6 +981,43 @@ extern "C" int vs_column_sum(int dtype, const void* x, void* out, void* ws, int 
     hipLaunchKernelGGL(colsum_partials_kernel<float>, dim3((N + 31) / 32), dim3(kCsThreads), 0, st, part,
                        (float*)out, (float*)nullptr, grid, N, N);
   }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+static int table_fold_factor(int R) {
+  for (int f : {1, 2, 4, 8})
+    if ((f * R) % 8 == 0) return f;
+  return 8;
+}
+
+extern "C" long long vs_rel_table_grad_workspace_bytes(int P, int heads, int T) {
+  const long long W = (long long)table_fold_factor(heads * T) * heads * T;
+  return (long long)kMaxPartials * W * sizeof(float);
+}
+
+extern "C" int vs_rel_table_grad(int dtype, const float* part, void* out, void* ws, int P, int heads, int T,
+                                 void* stream) {
+  VS_CHECK(dtype == VS_BF16 || dtype == VS_F32, "dtype must be VS_F32 or VS_BF16");
+  VS_CHECK(P > 0 && heads > 0 && T > 0, "empty partials");
+  VS_CHECK(part && out && ws, "null pointer");
+  const int R = heads * T, F = table_fold_factor(R), W = F * R;
+  VS_CHECK(P % F == 0, "the partial rows must fold into a multiple-of-8 width (P % F == 0)");
+  VS_CHECK(W <= 8 * kColBlock, "table too large");
+  hipStream_t st = (hipStream_t)stream;
+  float* p2 = (float*)ws;
+  const int M = P / F;
+  const int Nb = std::min(W, kColBlock), rowsets = kThreads / (Nb / 8);
+  const int grid = blocks_for(M, rowsets * 16, kMaxPartials);
+  const dim3 g2(grid, (W + kColBlock - 1) / kColBlock);
+  const size_t lds = (size_t)rowsets * Nb * sizeof(float);
+  hipLaunchKernelGGL(colsum_kernel<float>, g2, dim3(kThreads), lds, st, part, p2, M, W);
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(table_fold_kernel<bf16>, dim3((R + 31) / 32), dim3(kCsThreads), 0, st, p2, (bf16*)out, grid, F,
+                       heads, T);
+  else
+    hipLaunchKernelGGL(table_fold_kernel<float>, dim3((R + 31) / 32), dim3(kCsThreads), 0, st, p2, (float*)out, grid,
+                       F, heads, T);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

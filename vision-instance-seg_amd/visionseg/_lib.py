@@ -81,6 +81,8 @@ SIGNATURES = {
     "vs_column_sum_workspace_bytes": [_c_int] * 2,
     "vs_column_sum": [_c_int] + [_P] * 3 + [_c_int] * 2 + [_P],
     "vs_column_sum_segments_workspace_bytes": [_c_int] * 3,
+    "vs_rel_table_grad_workspace_bytes": [_c_int] * 3,
+    "vs_rel_table_grad": [_c_int, _P, _P, _P, _c_int, _c_int, _c_int, _P],
     "vs_column_sum_segments": [_c_int] + [_P] * 3 + [_c_int] * 3 + [_P, _c_int, _P],
     "vs_act_backward_colsum": [_c_int, _c_int] + [_P] * 5 + [_c_int] * 2 + [_P],
     "vs_flat_step_workspace_bytes": [_c_int],
@@ -133,6 +135,7 @@ RESTYPES = {"vs_last_error": ctypes.c_char_p, "vs_masked_attn_workspace_bytes": 
             "vs_layer_norm_backward_workspace_bytes": ctypes.c_longlong,
             "vs_column_sum_workspace_bytes": ctypes.c_longlong,
             "vs_column_sum_segments_workspace_bytes": ctypes.c_longlong,
+            "vs_rel_table_grad_workspace_bytes": ctypes.c_longlong,
             "vs_flat_step_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_workspace_bytes": ctypes.c_longlong,
             "vs_group_norm_nchw_workspace_bytes": ctypes.c_longlong,

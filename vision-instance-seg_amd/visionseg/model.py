@@ -148,10 +148,11 @@ class SwinBlock(nn.Module):
         self.norm2 = TokenLayerNorm(dim)
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
 
-    def forward(self, x, H, W, res=None):
+    def forward(self, x, H, W, res=None, table32=None):
         """x: residual stream; res: the previous block's pending MLP branch (added to x
-        inside this block's first LayerNorm).  Returns (stream, pending MLP branch): the
-        caller adds the branch in the next norm (ops.add_layer_norm)."""
+        inside this block's first LayerNorm); table32: the relative-position table already in
+        f32 (SwinBackbone casts all blocks' at once).  Returns (stream, pending MLP branch):
+        the caller adds the branch in the next norm (ops.add_layer_norm)."""
         B, L, C = x.shape
         ws, shift = self.ws, self.shift
         # the window partition folded into the norm's stores (ops.WindowRows): h comes out
@@ -190,7 +191,7 @@ class SwinBlock(nn.Module):
         # output in the image layout (window reverse folded into the kernel); the per-token
         # proj commutes with the crop
         o = ops.window_attention_image(qkv, self.attn.rel_table, self.attn.heads, ws, shift, B, H, W,
-                                       fp8=self.attn_fp8 and qkv.dtype == torch.bfloat16)
+                                       fp8=self.attn_fp8 and qkv.dtype == torch.bfloat16, table32=table32)
         # proj (C -> C): the MX backend only; on the rowwise backend its input would need a
         # quantisation pass of its own, which costs what the fp8 GEMM saves (Swin-L stage 3:
         # 0.0355 vs 0.0432 ms, tools/r5/scaled_mm_probe.py)
@@ -290,10 +291,22 @@ class SwinBackbone(nn.Module):
         B = x.shape[0]
         x = self.patch_embed.norm(x)
         feats = []
+        # the attention kernels read the relative-position tables in f32: every block's as one
+        # cast (cat + cast: 2 launches where each block's own cast was one launch per block);
+        # the tables' gradients still reach the bf16 parameters (ops.window_attention_image)
+        blocks = [blk for st in self.stages for blk in st.blocks]
+        t32 = None
+        if px.is_cuda and blocks and blocks[0].attn.rel_table.dtype != torch.float32:
+            flat = torch.cat([blk.attn.rel_table.detach().reshape(-1) for blk in blocks]).float()
+            t32, o = {}, 0
+            for blk in blocks:
+                n = blk.attn.rel_table.numel()
+                t32[id(blk)] = flat[o:o + n].view(blk.attn.rel_table.shape)
+                o += n
         for i, st in enumerate(self.stages):
             res = None
             for blk in st.blocks:
-                x, res = blk(x, H, W, res)
+                x, res = blk(x, H, W, res, t32[id(blk)] if t32 is not None else None)
             x, f = self.out_norms[i].add_forward(x, res)     # stream + last MLP branch, stage norm
             feats.append(f.view(B, H, W, -1).permute(0, 3, 1, 2))     # NCHW view, channels-last memory
             if st.merge is not None:

@@ -274,6 +274,25 @@ def table_grad_from_partials(part):
     return s.view(H, T)
 
 
+def rel_table_grad(part, dtype):
+    """f32 partials [P, heads, T] of the relative-position-table gradient -> the table
+    gradient [T, heads] in `dtype` (the table's layout): one column-sum pass over the rows
+    folded to a multiple-of-8 width and one fold / transpose / cast pass
+    (vs_rel_table_grad); table_grad_from_partials + transpose + cast (4-5 launches) where
+    the rows do not fold (P % F != 0)."""
+    P, H, T = part.shape
+    R = H * T
+    F = next(f for f in (1, 2, 4, 8) if (f * R) % 8 == 0)
+    if P % F or F * R > 16384 or dtype not in (torch.float32, torch.bfloat16):
+        return table_grad_from_partials(part).t().contiguous().to(dtype)
+    part = part.contiguous()
+    out = torch.empty(T, H, device=part.device, dtype=dtype)
+    ws = torch.empty(int(L.lib().vs_rel_table_grad_workspace_bytes(P, H, T)), device=part.device, dtype=torch.uint8)
+    L.check(L.lib().vs_rel_table_grad(L.dtype_code(out), L.ptr(part), L.ptr(out), L.ptr(ws), P, H, T,
+                                      L.stream(part)), "rel_table_grad")
+    return out
+
+
 class WindowAttentionFunction(torch.autograd.Function):
     """Swin window attention core with the relative-position bias and the shifted-window
     mask fused (HF:swin:373-398, 418-468, 584-607).
@@ -314,7 +333,7 @@ class WindowAttentionFunction(torch.autograd.Function):
                    flops=10.0 * Bw * heads * N * N * 32):
             gqkv, part = L.tops().win_attn_bwd(qkv, table, out, lse, g, heads, window, shift, nwin_h, nwin_w,
                                                scale, bool(fp8), True)
-        gtable = table_grad_from_partials(part).t().contiguous().to(tdtype)
+        gtable = rel_table_grad(part, tdtype)
         return gqkv, gtable, None, None, None, None, None, None, None
 
 
@@ -326,10 +345,13 @@ class WindowAttentionImageFunction(torch.autograd.Function):
     kernels; qkv and lse stay in the window layout."""
 
     @staticmethod
-    def forward(ctx, qkv, rel_table, heads, window, shift, nwin_h, nwin_w, height, width, scale, fp8=False):
+    def forward(ctx, qkv, rel_table, heads, window, shift, nwin_h, nwin_w, height, width, scale, fp8=False,
+                table32=None):
+        """table32: rel_table's values already in f32 (not differentiated: the gradient goes to
+        rel_table)."""
         L.require_hip(qkv, rel_table)
         qkv = qkv.contiguous()
-        table = rel_table.float().contiguous()
+        table = table32.contiguous() if table32 is not None else rel_table.float().contiguous()
         Bw, N, C3 = qkv.shape
         if C3 != 3 * heads * 32 or N != window * window:
             raise ValueError(f"qkv {tuple(qkv.shape)} does not match heads={heads} (x32) window={window}")
@@ -353,12 +375,12 @@ class WindowAttentionImageFunction(torch.autograd.Function):
                    flops=10.0 * Bw * heads * N * N * 32):
             gqkv, part = L.tops().win_attn_bwd_img(qkv, table, out, lse, g, heads, window, shift, nwin_h, nwin_w,
                                                    height, width, scale, bool(fp8))
-        gtable = table_grad_from_partials(part).t().contiguous().to(tdtype)
-        return gqkv, gtable, None, None, None, None, None, None, None, None, None
+        gtable = rel_table_grad(part, tdtype)
+        return gqkv, gtable, None, None, None, None, None, None, None, None, None, None
 
 
 def window_attention_image(qkv, rel_table, heads: int, window: int, shift: int, batch: int, height: int,
-                           width: int, scale: float | None = None, fp8: bool = False):
+                           width: int, scale: float | None = None, fp8: bool = False, table32=None):
     """Window attention of the partitioned qkv [B*nW, ws^2, 3C] with the output in the image
     layout [B, H, W, C] (= window_reverse(window_attention(...))): the reverse folded into
     the bf16 kernels; the f32 parity mode (and VS_WIN_ATTN_SCALAR) keeps the separate
@@ -369,7 +391,7 @@ def window_attention_image(qkv, rel_table, heads: int, window: int, shift: int, 
     if (qkv.is_cuda and qkv.dtype == torch.bfloat16 and window * window <= 160
             and os.environ.get("VS_WIN_ATTN_SCALAR", "0") == "0" and os.environ.get("VS_WIN_IMAGE", "1") != "0"):
         return WindowAttentionImageFunction.apply(qkv, rel_table, int(heads), int(window), int(shift), nwin_h, nwin_w,
-                                                  int(height), int(width), float(scale), bool(fp8))
+                                                  int(height), int(width), float(scale), bool(fp8), table32)
     o = window_attention(qkv, rel_table, heads, window, shift, nwin_h, nwin_w, scale, fp8)
     return window_reverse(o, batch, height, width, window, shift)
 
@@ -1207,9 +1229,15 @@ def attach_colsum(g: torch.Tensor, colsum: torch.Tensor) -> None:
 
 
 def take_colsum(g: torch.Tensor):
-    """The column sums recorded by attach_colsum if still valid for g, else None."""
+    """The column sums recorded by attach_colsum if still valid for g, else None.  The record
+    is removed: the caller returns the sums as a bias gradient, and a second reference to them
+    makes autograd's AccumulateGrad copy them instead of adopting them as .grad (36 copy
+    launches per C2 step)."""
     rec = getattr(g, "_vs_colsum", None)
-    if rec is None or rec[1] != g._version or rec[0].shape[0] != g.shape[-1]:
+    if rec is None:
+        return None
+    del g._vs_colsum
+    if rec[1] != g._version or rec[0].shape[0] != g.shape[-1]:
         return None
     return rec[0]
 
