@@ -465,10 +465,22 @@ class ConvGN(nn.Module):
         gn = self.gn
         hip = (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and gn.weight.dtype == x.dtype
                and not torch.is_autocast_enabled() and not _TORCH_GN)
+        conv = self.conv
         if hip and self.nchw and _PIXDEC_NCHW:
             y = self.conv(x.contiguous())
             if y.is_contiguous():
                 return ops.group_norm_nchw(y, gn.weight, gn.bias, gn.num_groups, gn.eps, self.relu)
+        elif (hip and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and x.dim() == 4
+              and x.dtype == torch.bfloat16 == conv.weight.dtype and torch.is_grad_enabled()
+              and x.is_contiguous(memory_format=torch.channels_last)):
+            # the input projections' 1x1 convs on the channels-last Swin features as token
+            # Linears: the bias in the GEMM epilogue and its gradient in the split-K weight
+            # gradient (MIOpen's conv + an ATen bias add forward, an ATen sum backward: 6 launches
+            # per step).  Training only, like PatchEmbed (the inference graphs keep the conv)
+            B, Ci, H, W = x.shape
+            Co = conv.weight.shape[0]
+            y = linear_tokens(x.permute(0, 2, 3, 1).reshape(B * H * W, Ci), conv.weight.view(Co, Ci), conv.bias)
+            y = y.view(B, H, W, Co).permute(0, 3, 1, 2)       # NCHW view, channels-last memory
         else:
             y = self.conv(x)
         if hip and y.shape[1] == 8 * gn.num_groups and y.is_contiguous(memory_format=torch.channels_last):
@@ -501,6 +513,7 @@ class PixelDecoder(nn.Module):
         self.mask_proj = nn.Conv2d(Fd, cfg.mask_feature_size, kernel_size=1)
         self._norm_cache = {}
         self._ref_cache = {}
+        self._pos_cache = {}
 
     def forward(self, feats):
         Fd = self.cfg.feature_size
@@ -517,8 +530,17 @@ class PixelDecoder(nn.Module):
         # position term with detached level-embedding rows: the layers route the level
         # embedding's gradient themselves (per-level column sums, linear.value_query_projection)
         lvl = self.level_embed.detach()
-        p = torch.cat([q + lvl[i].view(1, 1, -1).to(q.dtype) for i, q in enumerate(pos)], 1)
-        level = (self.level_embed, [Hl * Wl for (Hl, Wl) in shapes])
+        sizes = [Hl * Wl for (Hl, Wl) in shapes]
+        pkey = (tuple(shapes), B, str(dev), pos[0].dtype)
+        sine = self._pos_cache.get(pkey)
+        if sine is None:      # the levels' sine embeddings concatenated: constant per shape set
+            sine = torch.cat(pos, 1)
+            if not (sine.is_cuda and torch.cuda.is_current_stream_capturing()):
+                self._pos_cache[pkey] = sine
+        # + the level-embedding rows: one broadcast add (was an add per level and a cat)
+        rows = torch.cat([lvl[i].to(sine.dtype).expand(n, Fd) for i, n in enumerate(sizes)], 0)
+        p = sine + rows
+        level = (self.level_embed, sizes)
         ref = self._ref_cache.get((tuple(shapes), B, str(dev)))
         if ref is None:       # constant per shape set, like the sine embedding (sine_pos_tokens)
             ref = reference_points(shapes, B, dev)
