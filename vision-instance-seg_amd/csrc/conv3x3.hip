@@ -342,11 +342,7 @@ __global__ void __launch_bounds__(256) conv3x3_weight_layouts_kernel(const bf16*
 int wgrad_splits(int B, int H, int Wd, int Ci, int Co) {
   const long long tiles = (long long)(Co / kWBlk) * (Ci / kWBlk) * 3;
   const long long nseg = (long long)B * H * ((Wd + kSeg - 1) / kSeg);
-  static const int force = [] {
-    const char* e = getenv("VS_CONV_WGRAD_SPLITS");
-    return e ? atoi(e) : 0;
-  }();
-  long long S = force > 0 ? force : 256 / tiles;                 // one workgroup per CU (196 VGPRs: 8 waves)
+  long long S = 256 / tiles;                                      // one workgroup per CU (196 VGPRs: 8 waves)
   if (S > nseg) S = nseg;
   if (S < 1) S = 1;
   return (int)S;

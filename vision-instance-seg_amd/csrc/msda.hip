@@ -1634,8 +1634,7 @@ extern "C" int vs_msda_forward(int dtype, const void* value, const int64_t* shap
   hipStream_t st = (hipStream_t)stream;
   const long long groups = (long long)B * Q * Hh;
   const int block = 256;
-  bool unrolled = P == 4;                    // VS_MSDA_FWD4=0: the runtime-P kernel
-  if (const char* e = getenv("VS_MSDA_FWD4")) unrolled = unrolled && atoi(e) != 0;
+  const bool unrolled = P == 4;              // else the runtime-P kernel
   if (dtype == VS_BF16 && unrolled) {
     // encoder problems (Q == S: the queries are the value grid): pyramid-column visiting order
     // (msda_fwd4_kernel COL; VS_MSDA_FWD_COL=0: query order, A/B)

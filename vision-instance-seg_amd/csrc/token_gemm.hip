@@ -554,13 +554,8 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
-  // the 256 x 256 tile where the product is MFMA-bound and fills the chip (VS_TGEMM_TILE=128
-  // / 256 forces one, for A/B)
-  static const int force = [] {
-    const char* e = getenv("VS_TGEMM_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  const bool big = force ? force == 256 : (N >= 512 && K >= 256 && (long long)((M + 255) / 256) * ((N + 255) / 256) >= 256);
+  // the 256 x 256 tile where the product is MFMA-bound and fills the chip
+  const bool big = N >= 512 && K >= 256 && (long long)((M + 255) / 256) * ((N + 255) / 256) >= 256;
   const int bm = big ? 256 : 128, bn = big ? 256 : 128;
   const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   VS_CHECK(tiles < (1ll << 31), "too many tiles");

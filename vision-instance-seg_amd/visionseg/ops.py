@@ -389,7 +389,7 @@ def window_attention_image(qkv, rel_table, heads: int, window: int, shift: int, 
         scale = 32 ** -0.5
     nwin_h, nwin_w = -(-height // window), -(-width // window)
     if (qkv.is_cuda and qkv.dtype == torch.bfloat16 and window * window <= 160
-            and os.environ.get("VS_WIN_ATTN_SCALAR", "0") == "0" and os.environ.get("VS_WIN_IMAGE", "1") != "0"):
+            and os.environ.get("VS_WIN_ATTN_SCALAR", "0") == "0"):
         return WindowAttentionImageFunction.apply(qkv, rel_table, int(heads), int(window), int(shift), nwin_h, nwin_w,
                                                   int(height), int(width), float(scale), bool(fp8), table32)
     o = window_attention(qkv, rel_table, heads, window, shift, nwin_h, nwin_w, scale, fp8)
