@@ -244,10 +244,16 @@ VS_API int vs_add_layer_norm_forward_qr(const void* x, const void* r, const void
  *   VS_TGEMM_QOUT : (with GELU) y also as MX fp8: y_q e4m3 [M, N] + y_qscales e8m0
  *                   [M, N/32], the same bytes as vs_mx_quantize(y) (the next GEMM's operand
  *                   without a quantisation pass); N % 32 == 0.
+ *   VS_TGEMM_GELU_BWD : the MLP's GELU backward in the epilogue of fc2's input gradient
+ *                   (x = dY, w = W2^T): y = bf16(x w^T) * gelu'(y_pre), each product rounded
+ *                   once, y_pre the saved bf16 pre-activation (READ); bf16, no bias, N % 8 == 0.
+ *                   Replaces the stored dH plus the activation backward's pass over it
+ *                   (autograd's GeluBackward of HF:swin:511-536).
  * bias may be NULL.  N % 4 == 0. */
 #define VS_TGEMM_FP8 1
 #define VS_TGEMM_GELU 2
 #define VS_TGEMM_QOUT 4
+#define VS_TGEMM_GELU_BWD 8
 VS_API int vs_token_gemm(int mode, const void* x, const void* x_scales, const void* w, const void* w_scales,
                          const void* bias, void* y, void* y_pre, void* y_q, void* y_qscales, int M, int N, int K,
                          void* stream);

@@ -544,3 +544,64 @@ def test_linear_dgrad_weight_transposes_bit_exact(monkeypatch):
     assert not lin._WT.pending
     for p, q in zip(a, b):
         assert torch.equal(p, q)
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 384, 96), (40000, 768, 192), (16384, 1536, 384), (4096, 3072, 768),
+                                   (1000, 256, 64)])
+def test_token_gemm_gelu_backward_epilogue(M, N, K):
+    """token_gemm(dY, W2^T, gelu_pre=pre) -- the MLP's GELU backward in fc2's dX epilogue (stream
+    kernel at K <= 192 and >= 32768 rows, tile kernel otherwise) -- equals the composition it
+    replaces: dH = token_gemm(dY, W2^T) stored in bf16, then the activation backward kernel
+    (vs_act_backward_colsum) on (dH, pre).  Same formula, each product rounded once: at most
+    1 bf16 ulp apart (FMA contraction may differ) and identical almost everywhere."""
+    from visionseg import _lib as L
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + N)
+    gy = _rand((M, K), g).to(DEV)
+    wt = _rand((N, K), g, K ** -0.5).to(DEV)               # W2^T: [hidden, C]
+    pre = _rand((M, N), g, 2.0).to(DEV)
+    got = ops.token_gemm(gy, wt, gelu_pre=pre)
+    dh = ops.token_gemm(gy, wt)
+    ref = torch.empty_like(dh)
+    cs = torch.empty(N, device=DEV, dtype=torch.bfloat16)
+    ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=DEV, dtype=torch.uint8)
+    L.check(L.lib().vs_act_backward_colsum(L.VS_BF16, 1, L.ptr(dh), L.ptr(pre), L.ptr(ref), L.ptr(cs), L.ptr(ws), M, N,
+                                           L.stream(dh)), "act_backward_colsum")
+    torch.cuda.synchronize()
+    a = got.view(torch.int16).int()
+    b = ref.view(torch.int16).int()
+    ulp = (a - b).abs()
+    same_sign = (a >= 0) == (b >= 0)
+    assert bool((ulp[same_sign] <= 1).all()), int(ulp[same_sign].max())
+    assert bool(((got.float() - ref.float()).abs()[~same_sign] <= 1e-30).all())    # +-0
+    assert float((ulp == 0).float().mean()) > 0.99
+
+
+@pytest.mark.parametrize("stage", [1, 3])
+def test_mlp_gelu_backward_sink_vs_composition(stage):
+    """Swin MLP fc1 -> GELU -> fc2 with the GELU backward folded into fc2's dX GEMM
+    (ops.GeluBackwardSink; stage 1: fc1 + GELU on the streaming kernel, stage 3: vendor fc1 +
+    the activation node) vs the same MLP without the sink: every gradient within bf16 summation
+    order (fc1's bias gradient now comes from the split-K kernel's column sums)."""
+    from visionseg import linear as lin
+    ops = _ops()
+    C, T = (96, 4 * 128 * 128) if stage == 1 else (384, 4 * 64 * 64)
+    g = torch.Generator().manual_seed(stage)
+    x = _rand((T, C), g).to(DEV)
+    w1, b1 = _rand((4 * C, C), g, C ** -0.5).to(DEV), _rand((4 * C,), g, 0.1).to(DEV)
+    w2, b2 = _rand((C, 4 * C), g, (4 * C) ** -0.5).to(DEV), _rand((C,), g, 0.1).to(DEV)
+    gy = _rand((T, C), g).to(DEV)
+
+    def run(fused):
+        ps = [t.clone().requires_grad_() for t in (x, w1, b1, w2, b2)]
+        xs, a1, c1, a2, c2 = ps
+        gs = ops.GeluBackwardSink() if fused else None
+        h = lin.linear_gelu_tokens(xs, a1, c1, gelu_sink=gs)
+        lin.linear_tokens(h, a2, c2, gelu_sink=gs).backward(gy)
+        if fused:
+            assert gs.pre is not None and not gs.done
+        return [p.grad.float() for p in ps]
+
+    a, b = run(True), run(False)
+    for name, p, q in zip(("x", "w1", "b1", "w2", "b2"), a, b):
+        assert float((p - q).norm() / q.norm()) < 1e-2, name

@@ -37,6 +37,22 @@ void set_error(const std::string& msg);
 
 using bf16 = __hip_bfloat16;
 
+// d/dx of torch's exact GELU 0.5 x (1 + erf(x / sqrt2)): 0.5 (1 + erf(x / sqrt2)) + x
+// exp(-x^2 / 2) / sqrt(2 pi), with erf(|x| / sqrt2) = 1 - t poly(t) e^{-x^2/2}, t = 1 / (1 +
+// p |x| / sqrt2) (Abramowitz-Stegun 7.1.26, |error| <= 1.5e-7): the exponential is the one
+// the density term needs anyway, so one exp + one reciprocal per element.  Shared by the
+// activation backward (norm.hip) and the dX GEMM's fused GELU-backward epilogue
+// (token_gemm.hip), so both produce the same bits.
+__device__ __forceinline__ float gelu_grad_erf(float xv) {
+  const float e = __expf(-0.5f * xv * xv);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, fabsf(xv), 1.f));
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+  const float erf_abs = fmaf(-poly, e, 1.f);
+  const float erf_v = xv < 0.f ? -erf_abs : erf_abs;
+  return fmaf(0.5f, erf_v, 0.5f) + xv * 0.39894228040143268f * e;
+}
+
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(bf16 x) { return __bfloat162float(x); }
 template <typename T> __device__ __forceinline__ T from_f32(float x);

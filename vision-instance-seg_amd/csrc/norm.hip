@@ -503,19 +503,9 @@ __global__ void __launch_bounds__(kThreads) act_bwd_colsum_kernel(const T* __res
             if (ACT == 0) {
               d = xv > 0.f ? 1.f : 0.f;
             } else {
-              // erf(|x|/sqrt2) = 1 - t poly(t) e^{-x^2/2}, t = 1 / (1 + p |x|/sqrt2)
-              // (Abramowitz-Stegun 7.1.26, |error| <= 1.5e-7): the exponential is the one the
-              // density term needs anyway, so one exp + one reciprocal per element instead
-              // of erff's branches + an exp (the kernel was VALU-bound at GELU, 4.5 vs 5.9
-              // TB/s at ReLU on the C2 shapes)
-              const float e = __expf(-0.5f * xv * xv);
-              const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, fabsf(xv), 1.f));
-              const float poly =
-                  t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
-                           0.254829592f);
-              const float erf_abs = fmaf(-poly, e, 1.f);
-              const float erf_v = xv < 0.f ? -erf_abs : erf_abs;
-              d = fmaf(0.5f, erf_v, 0.5f) + xv * 0.39894228040143268f * e;
+              // (common.h: one exp + one reciprocal per element instead of erff's branches +
+              // an exp -- the kernel was VALU-bound at GELU, 4.5 vs 5.9 TB/s at ReLU)
+              d = gelu_grad_erf(xv);
             }
             o[i] = g[u][i] * d;
           }

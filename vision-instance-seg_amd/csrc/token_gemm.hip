@@ -71,13 +71,29 @@ __device__ __forceinline__ unsigned short gelu_bits(unsigned short pb, const uns
   return e < (unsigned)kGeluE0 ? small : (e >= (unsigned)(kGeluE0 + kGeluNE) ? big : tv);
 }
 
+// 8 bf16 of dH (the GEMM output, already rounded) times gelu'(8 bf16 pre-activations), each
+// product rounded once: what the activation backward computes from the stored dH
+__device__ __forceinline__ uint4 gelu_bwd8(uint4 d, uint4 p) {
+  const unsigned dw[4] = {d.x, d.y, d.z, d.w}, pw[4] = {p.x, p.y, p.z, p.w};
+  unsigned o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = __uint_as_float(dw[i] << 16) * gelu_grad_erf(__uint_as_float(pw[i] << 16));
+    const float hi = __uint_as_float(dw[i] & 0xffff0000u) * gelu_grad_erf(__uint_as_float(pw[i] & 0xffff0000u));
+    o[i] = (unsigned)(unsigned short)bf16_bits(lo) | ((unsigned)(unsigned short)bf16_bits(hi) << 16);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // Tile shapes: GM x GN waves, each TM x TN MFMA tiles of 32 x 32 (tokens x features):
 //   <2, 2, 2, 2>: 128 x 128, 256 threads, 2 workgroups / CU (64 KB of staging);
 //   <2, 4, 4, 2>: 256 x 256, 512 threads, 1 workgroup / CU (128 KB): half the L2 -> LDS
 //   bytes per flop, for the MFMA-bound shapes.
 // EPI: 0 = bias, 1 = bias + GELU (y2 = pre-activation, y = gelu), 2 = as 1 and the GELU
 // output also as MX fp8 (yq e4m3 [M, N] + yqs e8m0 [M, N/32]: the next GEMM's operand,
-// bit-identical to vs_mx_quantize of y)
+// bit-identical to vs_mx_quantize of y), 3 = GELU BACKWARD (the MLP's fc2 dX: y = bf16(x w^T)
+// * gelu'(y2), y2 the saved pre-activation READ in the store loop; no bias): the activation
+// backward's pass over dH (written, then read back with the pre-activation) is gone
 template <bool F8, int EPI, int GM, int GN, int TM, int TN>
 __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned char* __restrict__ X,
                                                                   const unsigned char* __restrict__ Xs,
@@ -89,8 +105,10 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
   constexpr int BM = GM * TM * 32, BN = GN * TN * 32, NW = GM * GN, NT = 64 * NW;
   constexpr int XB = BM * kRowB, WB = BN * kRowB, STB = XB + WB;      // staged bytes per K-step
   constexpr int SCB = F8 ? (BM + BN) * 4 : 0;                         // staged scale bytes per K-step
+  constexpr bool GF = EPI == 1 || EPI == 2, GB = EPI == 3;             // GELU forward / backward epilogue
+  static_assert(!(GB && F8), "GELU backward: bf16");
   // [stage][X tile | W tile] then (fp8) [stage][X scales | W scales] then the GELU table
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STB + 2 * SCB + (EPI >= 1 ? kGeluEntries * 2 : 0)];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STB + 2 * SCB + (GF ? kGeluEntries * 2 : 0)];
   unsigned short* sgelu = reinterpret_cast<unsigned short*>(smem + 2 * STB + 2 * SCB);
   constexpr int ESZ = F8 ? 1 : 2;                      // bytes per element
   const int rowB = K * ESZ;                            // bytes per operand row
@@ -141,7 +159,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
   auto xrow = [&](int t) { return wm * TM * 32 + t * 32 + r; };
   auto wrow = [&](int t) { return wn * TN * 32 + t * 32 + r; };
   issue(0, 0);
-  if (EPI >= 1) {                                     // GELU table: read at the epilogue, after the loop's barriers
+  if (GF) {                                           // GELU table: read at the epilogue, after the loop's barriers
     for (int i = threadIdx.x; i < kGeluEntries / 8; i += NT)
       reinterpret_cast<uint4*>(sgelu)[i] = reinterpret_cast<const uint4*>(kGeluTable)[i];
   }
@@ -213,7 +231,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
     }
   }
 
-  if (EPI < 2 && N % 8 == 0) {
+  if ((EPI < 2 || GB) && N % 8 == 0) {
     // ---- epilogue through LDS: the accumulators are 8-byte pieces of 32 token rows per
     // store instruction (32 lines touched for 512 B); staged in LDS as the [BM][BN] bf16
     // output tile (16-B chunks XOR-swizzled by row & 15: the 8-B writes of 16 rows and the
@@ -223,7 +241,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
     auto so_off = [](int row, int chunk) { return row * (BN * 2) + ((chunk ^ (row & 15)) << 4); };
     raw_barrier();                                     // every wave is done with the staging buffers
 #pragma unroll 1
-    for (int pass = 0; pass < (EPI >= 1 ? 2 : 1); ++pass) {
+    for (int pass = 0; pass < (GF ? 2 : 1); ++pass) {
 #pragma unroll
       for (int b = 0; b < TM; ++b) {
         const int row = xrow(b);
@@ -239,11 +257,34 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
               const short pre = bf16_bits(acc[a][b][4 * g + e] + bf16_bits_to_f32((unsigned short)bv[e]));
               // GELU of the ROUNDED pre-activation: the value the backward (and an unfused
               // bf16 F.gelu) sees
-              o[e] = (EPI >= 1 && pass == 0) ? (short)gelu_bits((unsigned short)pre, sgelu) : pre;
+              o[e] = (GF && pass == 0) ? (short)gelu_bits((unsigned short)pre, sgelu) : pre;
             }
             *reinterpret_cast<bf16x4_t*>(smem + so_off(row, f >> 3) + (f & 7) * 2) = o;
           }
         }
+      }
+      if (GB) {
+        // GELU backward: this thread's pre-activation chunks, requested before the barrier
+        constexpr int SPL = BM * NCK / NT;
+        static_assert(SPL * NT == BM * NCK, "store split");
+        uint4 pv[SPL];
+#pragma unroll
+        for (int i = 0; i < SPL; ++i) {
+          const int idx = threadIdx.x + i * NT, row = idx / NCK, chunk = idx - (idx / NCK) * NCK;
+          const int m = m0 + row, n = n0 + chunk * 8;
+          pv[i] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(Y2 + (size_t)m * N + n) : make_uint4(0, 0, 0, 0);
+        }
+        raw_barrier();
+#pragma unroll
+        for (int i = 0; i < SPL; ++i) {
+          const int idx = threadIdx.x + i * NT, row = idx / NCK, chunk = idx - (idx / NCK) * NCK;
+          const int m = m0 + row, n = n0 + chunk * 8;
+          if (m < M && n < N) {
+            const uint4 dv = *reinterpret_cast<const uint4*>(smem + so_off(row, chunk));
+            *reinterpret_cast<uint4*>(Y + (size_t)m * N + n) = gelu_bwd8(dv, pv[i]);
+          }
+        }
+        return;
       }
       raw_barrier();
       bf16* out = pass == 0 ? Y : Y2;
@@ -253,7 +294,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
         if (m < M && n < N)
           *reinterpret_cast<uint4*>(out + (size_t)m * N + n) = *reinterpret_cast<const uint4*>(smem + so_off(row, chunk));
       }
-      if (EPI >= 1 && pass == 0) raw_barrier();      // the tile is rewritten by pass 1
+      if (GF && pass == 0) raw_barrier();            // the tile is rewritten by pass 1
     }
     return;
   }
@@ -354,10 +395,13 @@ __global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* _
   constexpr int SPT = BM * NCK / NT;                                   // output stores per thread and pass
   constexpr int XI = BM / 8 * NKS / 4;                                 // X DMA instructions per wave
   static_assert(SPT * NT == BM * NCK && XI * 4 * 8 == BM * NKS, "tile shape");
-  constexpr int SPASS = (EPI >= 1 ? 2 : 1) * SPT;                     // stores per thread and tile
-  constexpr int WAITN = (NBUF - 1) * SPASS + (NBUF - 2) * XI;         // issued after a tile's DMA
+  constexpr bool GF = EPI == 1 || EPI == 2, GB = EPI == 3;             // GELU forward / backward epilogue
+  constexpr int SPASS = (GF ? 2 : 1) * SPT;                            // stores per thread and tile
+  constexpr int PL = GB ? SPT : 0;                                     // pre-activation loads per thread and tile
+  // per tile, in issue order: PL pre loads, the DMA of a later tile (XI), SPASS stores
+  constexpr int WAITN = (NBUF - 1) * SPASS + (NBUF - 2) * (XI + PL);  // issued after a tile's DMA
   static_assert(WAITN <= 63, "vmcnt");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[WB + NBUF * XB + OB + (EPI >= 1 ? kGeluEntries * 2 : 0)];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[WB + NBUF * XB + OB + (GF ? kGeluEntries * 2 : 0)];
   unsigned char* sW = smem;
   unsigned char* sX = smem + WB;                                       // [NBUF][NKS][BM rows x 128 B]
   unsigned char* sO = smem + WB + NBUF * XB;
@@ -372,7 +416,7 @@ __global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* _
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
   // zero the X ring and W (the chunks past K stay zero), then W by LDS-DMA
   for (int i = threadIdx.x; i < (WB + NBUF * XB) / 16; i += NT) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
-  if (EPI >= 1)
+  if (GF)
     for (int i = threadIdx.x; i < kGeluEntries / 8; i += NT)
       reinterpret_cast<uint4*>(sgelu)[i] = reinterpret_cast<const uint4*>(kGeluTable)[i];
   __syncthreads();
@@ -414,6 +458,16 @@ __global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* _
       else wait_vm<0>();
     }
     raw_barrier();                                                     // every wave's DMA landed; ring slot free
+    const int m0 = (g0 + j * G) * BM;
+    uint4 pv[GB ? SPT : 1];                                            // GELU backward: this tile's pre-activations
+    if (GB) {
+#pragma unroll
+      for (int i = 0; i < SPT; ++i) {
+        const int idx = threadIdx.x + i * NT, row = idx / NCK, chunk = idx % NCK;
+        const int m = min(m0 + row, M - 1), n = min(n0 + chunk * 8, N - 8);   // always a load: counted waits
+        pv[i] = *reinterpret_cast<const uint4*>(Y2 + (size_t)m * N + n);
+      }
+    }
     if (j + NBUF - 1 < ntl) issue_x(j + NBUF - 1);                     // the slot of tile j - 1
     // W fragments are re-read from LDS per tile: hoisted out of the tile loop they took the
     // registers of a second wave per SIMD
@@ -434,9 +488,8 @@ __global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* _
                           acc[t]);
       }
     }
-    const int m0 = (g0 + j * G) * BM;
 #pragma unroll
-    for (int pass = 0; pass < (EPI >= 1 ? 2 : 1); ++pass) {
+    for (int pass = 0; pass < (GF ? 2 : 1); ++pass) {
       if (pass) raw_barrier();                                         // pass 0's rows are stored
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
@@ -449,12 +502,25 @@ __global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* _
 #pragma unroll
           for (int e2 = 0; e2 < 4; ++e2) {
             const short pre = bf16_bits(acc[t][4 * g + e2] + bf16_bits_to_f32((unsigned short)bv[e2]));
-            o[e2] = (EPI >= 1 && pass == 0) ? (short)gelu_bits((unsigned short)pre, sgelu) : pre;
+            o[e2] = (GF && pass == 0) ? (short)gelu_bits((unsigned short)pre, sgelu) : pre;
           }
           *reinterpret_cast<bf16x4_t*>(sO + so_off(row, f >> 3) + (f & 7) * 2) = o;
         }
       }
       raw_barrier();
+      if (GB) {
+        // the pre loads were issued before tile j + NBUF - 1's DMA: only that DMA may fly on
+        if (j + NBUF - 1 < ntl) wait_vm<XI>();
+        else wait_vm<0>();
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+          const int idx = threadIdx.x + i * NT, row = idx / NCK, chunk = idx % NCK;
+          const int m = m0 + row, n = n0 + chunk * 8;
+          if (m < M && n < N)
+            *reinterpret_cast<uint4*>(Y + (size_t)m * N + n) = gelu_bwd8(*reinterpret_cast<const uint4*>(sO + so_off(row, chunk)), pv[i]);
+        }
+        continue;
+      }
       bf16* out = pass == 0 ? Y : Y2;
 #pragma unroll
       for (int i = 0; i < SPT; ++i) {
@@ -513,7 +579,10 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
                              const void* bias, void* y, void* y_pre, void* y_q, void* y_qscales, int M, int N, int K,
                              void* stream) {
   const bool f8 = (mode & VS_TGEMM_FP8) != 0, gelu = (mode & VS_TGEMM_GELU) != 0;
+  const bool gbwd = (mode & VS_TGEMM_GELU_BWD) != 0;
   VS_CHECK(x && w && y, "null pointer");
+  VS_CHECK(!gbwd || (!f8 && !gelu && !(mode & VS_TGEMM_QOUT) && !bias && y_pre && N % 8 == 0),
+           "GELU backward: bf16, no bias / GELU / quantised output, y_pre (read) given, N % 8 == 0");
   VS_CHECK(M > 0 && N > 0 && K > 0, "empty GEMM");
   VS_CHECK(N % 4 == 0, "N must be a multiple of 4");
   VS_CHECK(f8 ? (K % 128 == 0 && x_scales && w_scales) : (K % 8 == 0), "fp8: K % 128 == 0 and scales; bf16: K % 8 == 0");
@@ -543,6 +612,10 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
       if (nks == 1) VS_TGS(1, 1, 4);
       else if (nks == 2) VS_TGS(1, 2, 4);
       else VS_TGS(1, 3, 2);
+    } else if (gbwd) {
+      if (nks == 1) VS_TGS(3, 1, 4);
+      else if (nks == 2) VS_TGS(3, 2, 4);
+      else VS_TGS(3, 3, 2);
     } else {
       // (K-steps 4-6 with one workgroup per CU were measured slower than the tile kernel:
       // profiles/r5_tgemm_stream_ab.txt)
@@ -577,6 +650,7 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
   else if (f8) VS_TG(true, 0);
   else if (qout) VS_TG(false, 2);
   else if (gelu) VS_TG(false, 1);
+  else if (gbwd) VS_TG(false, 3);
   else VS_TG(false, 0);
 #undef VS_TG
   VS_LAUNCH_CHECK();

@@ -229,7 +229,7 @@ def _dgrad_gemm(gy2, weight, wt=None):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, sink=None):
+    def forward(ctx, x, weight, bias, sink=None, gelu_sink=None):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.sink = sink
@@ -237,7 +237,11 @@ class _LinearFn(torch.autograd.Function):
             sink.arm()
         # the dX GEMM's W^T (only where it runs without the residual term, on the token GEMM)
         T = x.numel() // max(1, x.shape[-1])
-        ctx.wt = (_WT.request(weight) if sink is None and _dgrad_on_token_gemm(T, weight, x.dtype) else None)
+        tok = sink is None and _dgrad_on_token_gemm(T, weight, x.dtype)
+        ctx.wt = _WT.request(weight) if tok else None
+        # x = gelu(pre) of an MLP: the GELU backward rides in the dX GEMM (ops.GeluBackwardSink)
+        ctx.gs = (gelu_sink if tok and gelu_sink is not None and gelu_sink.pre is not None
+                  and gelu_sink.pre.shape == x.shape and gelu_sink.pre.dtype == x.dtype else None)
         return _forward_gemm(x, weight, bias)
 
     @staticmethod
@@ -249,9 +253,12 @@ class _LinearFn(torch.autograd.Function):
             gres = ctx.sink.take() if ctx.sink is not None else None
             if gres is not None:       # the residual path's gradient of x, added by the GEMM (beta = 1)
                 gx = _addmm_into(gres.reshape(gy2.shape[0], -1), gy2, weight.to(gy2.dtype)).view(x.shape)
+            elif ctx.gs is not None and _dgrad_on_token_gemm(gy2.shape[0], weight, gy2.dtype):
+                gx = ops.token_gemm(gy2.contiguous(), _WT.get(ctx.wt), gelu_pre=ctx.gs.pre).view(x.shape)
+                ctx.gs.done = True
             else:
                 gx = _dgrad_gemm(gy2, weight, ctx.wt).view(x.shape)
-        ctx.wt = None
+        ctx.wt = ctx.gs = None
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         cs = ops.take_colsum(gy) if want_b else None               # from the LayerNorm backward's pass
         if cs is not None:
@@ -267,7 +274,7 @@ class _LinearFn(torch.autograd.Function):
                 gb = ops.column_sum(gy2).to(weight.dtype)          # HIP column sum, f32 accumulation
             else:
                 gb = gy2.sum(0, dtype=torch.float32).to(weight.dtype)
-        return gx, gw, gb, None
+        return gx, gw, gb, None, None
 
 
 class _PlaneProjectionFn(torch.autograd.Function):
@@ -875,9 +882,10 @@ class TokenLayerNorm(nn.LayerNorm):
         return (s, self(s), None) if quant else (s, self(s))
 
 
-def linear_tokens(x, w, b=None, sink=None):
+def linear_tokens(x, w, b=None, sink=None, gelu_sink=None):
     """F.linear with the split-K weight gradient when x carries many tokens (`sink`: see
-    ops.ResidualSink; armed only on that path)."""
+    ops.ResidualSink; armed only on that path; `gelu_sink`: ops.GeluBackwardSink when x is
+    the GELU output of an MLP feeding only this Linear)."""
     tokens = x.numel() // max(1, x.shape[-1])
     if not (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and tokens >= MIN_TOKENS):
         return F.linear(x, w, b)
@@ -885,7 +893,7 @@ def linear_tokens(x, w, b=None, sink=None):
         dt = torch.get_autocast_dtype("cuda")
         with torch.autocast("cuda", enabled=False):
             return _LinearFn.apply(x.to(dt), w.to(dt), None if b is None else b.to(dt))
-    return _LinearFn.apply(x, w, b, sink)
+    return _LinearFn.apply(x, w, b, sink, gelu_sink)
 
 
 class _LinearReluFn(torch.autograd.Function):
@@ -1061,7 +1069,7 @@ class _LinearGeluFn(torch.autograd.Function):
     bias gradient) in one HIP pass, then the vendor dX GEMM and the split-K dW."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, fp8=False, quant_out=False, xq=None, xs=None):
+    def forward(ctx, x, weight, bias, fp8=False, quant_out=False, xq=None, xs=None, gelu_sink=None):
         K = x.shape[-1]
         N = weight.shape[0]
         x2 = x.reshape(-1, K)
@@ -1080,6 +1088,9 @@ class _LinearGeluFn(torch.autograd.Function):
         else:
             y, pre = out
         ctx.wt = _WT.request(weight) if not fp8 and _dgrad_on_token_gemm(x2.shape[0], weight, x.dtype) else None
+        ctx.gs = gelu_sink if not quant_out else None          # ops.GeluBackwardSink: pre offered to fc2
+        if ctx.gs is not None:
+            ctx.gs.pre = pre.view(*x.shape[:-1], N)
         ctx.save_for_backward(x, weight, pre)
         ctx.has_bias = bias is not None
         ctx.fp8 = bool(fp8)
@@ -1094,21 +1105,34 @@ class _LinearGeluFn(torch.autograd.Function):
         x, weight, pre = ctx.saved_tensors
         M, N = pre.shape
         gy2 = gy.reshape(M, N).to(pre.dtype).contiguous()
-        gp = torch.empty_like(pre)
-        cs = torch.empty(N, device=pre.device, dtype=pre.dtype)
-        ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=pre.device, dtype=torch.uint8)
-        with ops.timed("act_bwd_colsum", pre, bytes_=3 * pre.numel() * pre.element_size()):
-            L.check(L.lib().vs_act_backward_colsum(L.dtype_code(pre), 1, L.ptr(gy2), L.ptr(pre), L.ptr(gp), L.ptr(cs),
-                                                   L.ptr(ws), M, N, L.stream(pre)), "act_backward_colsum")
+        if ctx.gs is not None and ctx.gs.done:
+            # fc2's dX GEMM already applied the GELU derivative: gy IS the pre-activation's gradient
+            ctx.gs.done = False
+            gp, cs = gy2, None
+        else:
+            gp = torch.empty_like(pre)
+            cs = torch.empty(N, device=pre.device, dtype=pre.dtype)
+            ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=pre.device, dtype=torch.uint8)
+            with ops.timed("act_bwd_colsum", pre, bytes_=3 * pre.numel() * pre.element_size()):
+                L.check(L.lib().vs_act_backward_colsum(L.dtype_code(pre), 1, L.ptr(gy2), L.ptr(pre), L.ptr(gp),
+                                                       L.ptr(cs), L.ptr(ws), M, N, L.stream(pre)), "act_backward_colsum")
+        ctx.gs = None
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = (_dgrad(gp, weight) if ctx.fp8 else _dgrad_gemm(gp, weight, ctx.wt)).view(x.shape)
         ctx.wt = None
-        if ctx.needs_input_grad[1]:
-            gw = weight_grad(gp, x.reshape(-1, x.shape[-1]), weight.dtype)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        x2 = x.reshape(-1, x.shape[-1])
+        if want_b and cs is None:
+            if ctx.needs_input_grad[1] and _token_wgrad_ok(gp, x2, weight.dtype):
+                gw, gb = weight_grad(gp, x2, weight.dtype, bias=True)
+            else:
+                gb = ops.column_sum(gp).to(weight.dtype)
+        elif want_b:
             gb = cs.to(weight.dtype)
-        return gx, gw, gb, None, None, None, None
+        if ctx.needs_input_grad[1] and gw is None:
+            gw = weight_grad(gp, x2, weight.dtype)
+        return gx, gw, gb, None, None, None, None, None
 
 
 class _LinearFp8Fn(torch.autograd.Function):
@@ -1167,12 +1191,15 @@ def _stream_gelu_ok(x, w) -> bool:
             and x.numel() // max(1, x.shape[-1]) >= STREAM_MIN_ROWS)
 
 
-def linear_gelu_tokens(x, w, b, fp8: bool = False):
+def linear_gelu_tokens(x, w, b, fp8: bool = False, gelu_sink=None):
     """gelu(F.linear(x, w, b)) with the exact erf GELU: fused into the token GEMM on
-    token-heavy bf16 device tensors (_LinearGeluFn), the composition otherwise."""
+    token-heavy bf16 device tensors (_LinearGeluFn), the composition otherwise.  gelu_sink:
+    ops.GeluBackwardSink when the output feeds only the MLP's fc2 (linear_tokens with the same
+    sink), which then folds the GELU backward into its dX GEMM."""
     if (fp8 or _stream_gelu_ok(x, w)) and _tgemm_ok(x, w, b):
-        return _LinearGeluFn.apply(x, w, b, bool(fp8 and w.shape[1] % 128 == 0 and w.shape[1] >= FP8_MIN_K))
-    return ops.activation(linear_tokens(x, w, b), "gelu")
+        return _LinearGeluFn.apply(x, w, b, bool(fp8 and w.shape[1] % 128 == 0 and w.shape[1] >= FP8_MIN_K), False,
+                                   None, None, gelu_sink)
+    return ops.activation(linear_tokens(x, w, b), "gelu", gelu_sink)
 
 
 def linear_fp8_tokens(x, w, b, xq=None):

@@ -134,7 +134,10 @@ class Mlp(nn.Module):
     def forward(self, x, xq=None):
         if self.fp8:
             return mlp_fp8(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, xq)
-        return self.fc2(linear_gelu_tokens(x, self.fc1.weight, self.fc1.bias))
+        # the GELU output feeds fc2 only: its backward rides in fc2's dX GEMM (ops.GeluBackwardSink)
+        gs = ops.GeluBackwardSink()
+        h = linear_gelu_tokens(x, self.fc1.weight, self.fc1.bias, gelu_sink=gs)
+        return linear_tokens(h, self.fc2.weight, self.fc2.bias, gelu_sink=gs)
 
 
 class SwinBlock(nn.Module):

@@ -1444,19 +1444,46 @@ class ResidualSink:
         return g
 
 
+class GeluBackwardSink:
+    """The GELU backward of one MLP (fc1 -> GELU -> fc2) folded into fc2's dX GEMM
+    (token_gemm gelu_pre: the epilogue reads the saved pre-activation), so dH is never written
+    and read back by a separate activation pass.  Protocol (one object per MLP call, owned by
+    the caller, whose GELU output feeds fc2 ONLY): the GELU producer records its saved
+    pre-activation (`pre`); fc2's Linear takes the sink in its forward when its dX runs on the
+    token GEMM and, in its backward (which runs first), returns dpre = (dY W2) * gelu'(pre) and
+    sets `done`; the GELU's backward then passes that gradient through unchanged.  Either side
+    on another path leaves the sink unused and autograd runs the plain composition."""
+
+    __slots__ = ("pre", "done")
+
+    def __init__(self):
+        self.pre = None
+        self.done = False
+
+
 class _ActColsumFunction(torch.autograd.Function):
     """y = act(x) (torch's ReLU / exact GELU forward); the backward is one HIP pass
     (vs_act_backward_colsum) that also records the column sums of dx (attach_colsum): the
-    bias gradient of the Linear that produced x, which then reads no dY for it."""
+    bias gradient of the Linear that produced x, which then reads no dY for it.  gelu_sink
+    (GeluBackwardSink): x is offered to the consumer; when it folded the derivative into its
+    dX GEMM the incoming gradient IS dx (passed through; the producing Linear then takes its
+    bias gradient from the split-K kernel)."""
 
     @staticmethod
-    def forward(ctx, x, act):
+    def forward(ctx, x, act, gelu_sink=None):
         ctx.act = act
+        ctx.gs = gelu_sink if act == 1 else None
+        if ctx.gs is not None:
+            ctx.gs.pre = x
         ctx.save_for_backward(x)
         return F.gelu(x) if act == 1 else F.relu(x)
 
     @staticmethod
     def backward(ctx, gy):
+        gs = getattr(ctx, "gs", None)            # (shared with _GeluRowQuantFunction: no sink there)
+        if gs is not None and gs.done:
+            gs.done = False
+            return gy, None, None
         (x,) = ctx.saved_tensors
         N = x.shape[-1]
         M = x.numel() // N
@@ -1468,7 +1495,7 @@ class _ActColsumFunction(torch.autograd.Function):
             L.check(L.lib().vs_act_backward_colsum(L.dtype_code(x), int(ctx.act), L.ptr(gy), L.ptr(x), L.ptr(gx),
                                                    L.ptr(cs), L.ptr(ws), M, N, L.stream(x)), "act_backward_colsum")
         attach_colsum(gx, cs)
-        return gx, None
+        return gx, None, None
 
 
 class _GeluRowQuantFunction(torch.autograd.Function):
@@ -1496,14 +1523,15 @@ def gelu_row_quant(x):
     return _GeluRowQuantFunction.apply(x)
 
 
-def activation(x, kind: str):
+def activation(x, kind: str, gelu_sink=None):
     """F.gelu / F.relu whose backward feeds the preceding Linear's bias gradient (see
-    _ActColsumFunction) on contiguous f32 / bf16 device tensors with N % 8 == 0."""
+    _ActColsumFunction) on contiguous f32 / bf16 device tensors with N % 8 == 0 (gelu_sink:
+    see GeluBackwardSink)."""
     act = {"relu": 0, "gelu": 1}[kind]
     N = x.shape[-1]
     if (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and N % 8 == 0 and N <= COLSUM_MAX_N
             and x.is_contiguous() and torch.is_grad_enabled() and x.requires_grad and not torch.is_autocast_enabled()):
-        return _ActColsumFunction.apply(x, act)
+        return _ActColsumFunction.apply(x, act, gelu_sink)
     return F.gelu(x) if act == 1 else F.relu(x)
 
 
@@ -1955,7 +1983,7 @@ def conv3x3_nhwc(x, weight, bias=None):
 # ---------------------------------------------------------------------------------------
 # token GEMM (csrc/token_gemm.hip): the Swin blocks' Linears, bf16 or block-scaled MX fp8
 # ---------------------------------------------------------------------------------------
-TGEMM_FP8, TGEMM_GELU, TGEMM_QOUT = 1, 2, 4
+TGEMM_FP8, TGEMM_GELU, TGEMM_QOUT, TGEMM_GELU_BWD = 1, 2, 4, 8
 
 
 def mx_quantize(x: torch.Tensor):
@@ -1998,17 +2026,22 @@ def row_quantize_fp8(x: torch.Tensor, gelu: bool = False):
     return q, sc
 
 
-def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None, quant_out: bool = False):
+def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None, quant_out: bool = False,
+               gelu_pre=None):
     """y = x w^T + bias over token rows (x [..., K], w [N, K]; bf16, or -- with scales --
     e4m3 bytes from mx_quantize) -> bf16 [..., N]; gelu=True -> (gelu(y), y) with the exact
     erf GELU in the epilogue (y = the bf16 pre-activation); quant_out=True (with gelu) ->
-    (gelu(y), y, (e4m3 bytes, e8m0 scales) of gelu(y), as mx_quantize would make them)."""
+    (gelu(y), y, (e4m3 bytes, e8m0 scales) of gelu(y), as mx_quantize would make them).
+    gelu_pre ([..., N] bf16, no bias): the GELU BACKWARD in the epilogue -> bf16(x w^T) *
+    gelu'(gelu_pre), each product rounded once (VS_TGEMM_GELU_BWD: fc2's dX of an MLP)."""
     fp8 = x_scales is not None
     L.require_hip(x, w)
     K = x.shape[-1]
     N = w.shape[0]
     if w.shape[1] != K or N % 4 or (fp8 and (w_scales is None or K % 128)) or (not fp8 and K % 8) \
-            or (quant_out and (not gelu or N % 32)):
+            or (quant_out and (not gelu or N % 32)) \
+            or (gelu_pre is not None and (fp8 or gelu or bias is not None or N % 8 or gelu_pre.dtype != torch.bfloat16
+                                          or gelu_pre.numel() != x.numel() // K * N)):
         raise ValueError(f"token_gemm: bad shapes x {tuple(x.shape)} w {tuple(w.shape)} fp8={fp8}")
     x2 = x.reshape(-1, K).contiguous()
     w = w.contiguous()
@@ -2028,13 +2061,20 @@ def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None
     yq = torch.empty(M, N, device=x.device, dtype=torch.uint8) if quant_out else None
     yqs = torch.empty(M, N // 32, device=x.device, dtype=torch.uint8) if quant_out else None
     mode = (TGEMM_FP8 if fp8 else 0) | (TGEMM_GELU if gelu else 0) | (TGEMM_QOUT if quant_out else 0)
+    if gelu_pre is not None:
+        mode |= TGEMM_GELU_BWD
+        pre = gelu_pre.reshape(M, N).contiguous()
+        if pre.data_ptr() % 16:
+            pre = pre.clone()
     esz = 1 if fp8 else 2
-    nb = (M * K + N * K) * esz + M * N * 2 * (2 if gelu else 1) + (M * N * 33 // 32 if quant_out else 0)
+    nb = (M * K + N * K) * esz + M * N * 2 * (2 if gelu or gelu_pre is not None else 1) + \
+        (M * N * 33 // 32 if quant_out else 0)
     with timed("token_gemm_fp8" if fp8 else "token_gemm", x2, bytes_=nb, flops=2.0 * M * N * K):
         L.check(L.lib().vs_token_gemm(mode, L.ptr(x2), L.ptr(x_scales.contiguous()) if fp8 else None,
                                       L.ptr(w), L.ptr(w_scales.contiguous()) if fp8 else None,
                                       L.ptr(bias) if bias is not None else None, L.ptr(y),
-                                      L.ptr(pre) if gelu else None, L.ptr(yq) if quant_out else None,
+                                      L.ptr(pre) if gelu or gelu_pre is not None else None,
+                                      L.ptr(yq) if quant_out else None,
                                       L.ptr(yqs) if quant_out else None, M, N, K, L.stream(x2)), "token_gemm")
     shape = (*x.shape[:-1], N)
     if quant_out:
