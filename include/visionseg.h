@@ -249,11 +249,14 @@ VS_API int vs_add_layer_norm_forward_qr(const void* x, const void* r, const void
  *                   once, y_pre the saved bf16 pre-activation (READ); bf16, no bias, N % 8 == 0.
  *                   Replaces the stored dH plus the activation backward's pass over it
  *                   (autograd's GeluBackward of HF:swin:511-536).
+ *   VS_TGEMM_RELU_BWD : the same for a ReLU FFN (the pixel decoder's encoder layers,
+ *                   HF:m2f:1080-1082): y_pre = the ReLU OUTPUT, y = bf16(x w^T) * [y_pre > 0].
  * bias may be NULL.  N % 4 == 0. */
 #define VS_TGEMM_FP8 1
 #define VS_TGEMM_GELU 2
 #define VS_TGEMM_QOUT 4
 #define VS_TGEMM_GELU_BWD 8
+#define VS_TGEMM_RELU_BWD 16
 VS_API int vs_token_gemm(int mode, const void* x, const void* x_scales, const void* w, const void* w_scales,
                          const void* bias, void* y, void* y_pre, void* y_q, void* y_qscales, int M, int N, int K,
                          void* stream);

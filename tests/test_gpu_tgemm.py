@@ -546,12 +546,14 @@ def test_linear_dgrad_weight_transposes_bit_exact(monkeypatch):
         assert torch.equal(p, q)
 
 
+@pytest.mark.parametrize("act", ["gelu", "relu"])
 @pytest.mark.parametrize("M,N,K", [(32768, 384, 96), (40000, 768, 192), (16384, 1536, 384), (4096, 3072, 768),
-                                   (1000, 256, 64)])
-def test_token_gemm_gelu_backward_epilogue(M, N, K):
-    """token_gemm(dY, W2^T, gelu_pre=pre) -- the MLP's GELU backward in fc2's dX epilogue (stream
-    kernel at K <= 192 and >= 32768 rows, tile kernel otherwise) -- equals the composition it
-    replaces: dH = token_gemm(dY, W2^T) stored in bf16, then the activation backward kernel
+                                   (86016, 1024, 256), (1000, 256, 64)])
+def test_token_gemm_act_backward_epilogue(M, N, K, act):
+    """token_gemm(dY, W2^T, gelu_pre=pre / relu_out=y) -- an MLP's activation backward in fc2's
+    dX epilogue (stream kernel at K <= 192 and >= 32768 rows, tile kernels otherwise, the
+    256 x 256 one at the encoder FFN shape) -- equals the composition it replaces: dH =
+    token_gemm(dY, W2^T) stored in bf16, then the activation backward kernel
     (vs_act_backward_colsum) on (dH, pre).  Same formula, each product rounded once: at most
     1 bf16 ulp apart (FMA contraction may differ) and identical almost everywhere."""
     from visionseg import _lib as L
@@ -560,13 +562,15 @@ def test_token_gemm_gelu_backward_epilogue(M, N, K):
     gy = _rand((M, K), g).to(DEV)
     wt = _rand((N, K), g, K ** -0.5).to(DEV)               # W2^T: [hidden, C]
     pre = _rand((M, N), g, 2.0).to(DEV)
-    got = ops.token_gemm(gy, wt, gelu_pre=pre)
+    if act == "relu":
+        pre = pre.clamp_min(0)                             # a ReLU output (exact zeros where masked)
+    got = ops.token_gemm(gy, wt, **({"gelu_pre": pre} if act == "gelu" else {"relu_out": pre}))
     dh = ops.token_gemm(gy, wt)
     ref = torch.empty_like(dh)
     cs = torch.empty(N, device=DEV, dtype=torch.bfloat16)
     ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=DEV, dtype=torch.uint8)
-    L.check(L.lib().vs_act_backward_colsum(L.VS_BF16, 1, L.ptr(dh), L.ptr(pre), L.ptr(ref), L.ptr(cs), L.ptr(ws), M, N,
-                                           L.stream(dh)), "act_backward_colsum")
+    L.check(L.lib().vs_act_backward_colsum(L.VS_BF16, 1 if act == "gelu" else 0, L.ptr(dh), L.ptr(pre), L.ptr(ref),
+                                           L.ptr(cs), L.ptr(ws), M, N, L.stream(dh)), "act_backward_colsum")
     torch.cuda.synchronize()
     a = got.view(torch.int16).int()
     b = ref.view(torch.int16).int()
@@ -600,6 +604,34 @@ def test_mlp_gelu_backward_sink_vs_composition(stage):
         lin.linear_tokens(h, a2, c2, gelu_sink=gs).backward(gy)
         if fused:
             assert gs.pre is not None and not gs.done
+        return [p.grad.float() for p in ps]
+
+    a, b = run(True), run(False)
+    for name, p, q in zip(("x", "w1", "b1", "w2", "b2"), a, b):
+        assert float((p - q).norm() / q.norm()) < 1e-2, name
+
+
+def test_ffn_relu_backward_sink_vs_composition():
+    """The encoder FFN (fc1 + bias + ReLU in the GEMM epilogue, fc2) with the ReLU backward
+    folded into fc2's dX GEMM (ops.ActBackwardSink("relu")) vs without: every gradient within
+    bf16 summation order."""
+    from visionseg import linear as lin
+    ops = _ops()
+    T, C, F = 4 * 5376, 256, 1024
+    g = torch.Generator().manual_seed(7)
+    x = _rand((T, C), g).to(DEV)
+    w1, b1 = _rand((F, C), g, C ** -0.5).to(DEV), _rand((F,), g, 0.1).to(DEV)
+    w2, b2 = _rand((C, F), g, F ** -0.5).to(DEV), _rand((C,), g, 0.1).to(DEV)
+    gy = _rand((T, C), g).to(DEV)
+
+    def run(fused):
+        ps = [t.clone().requires_grad_() for t in (x, w1, b1, w2, b2)]
+        xs, a1, c1, a2, c2 = ps
+        rs = ops.ActBackwardSink("relu") if fused else None
+        f = lin.linear_relu_tokens(xs, a1, c1, act_sink=rs)
+        lin.linear_tokens(f, a2, c2, gelu_sink=rs).backward(gy)
+        if fused:
+            assert rs.pre is not None and not rs.done
         return [p.grad.float() for p in ps]
 
     a, b = run(True), run(False)

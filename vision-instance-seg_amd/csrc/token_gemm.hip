@@ -71,15 +71,22 @@ __device__ __forceinline__ unsigned short gelu_bits(unsigned short pb, const uns
   return e < (unsigned)kGeluE0 ? small : (e >= (unsigned)(kGeluE0 + kGeluNE) ? big : tv);
 }
 
-// 8 bf16 of dH (the GEMM output, already rounded) times gelu'(8 bf16 pre-activations), each
-// product rounded once: what the activation backward computes from the stored dH
-__device__ __forceinline__ uint4 gelu_bwd8(uint4 d, uint4 p) {
+// 8 bf16 of dH (the GEMM output, already rounded) times act'(8 bf16 activation inputs /
+// outputs), each product rounded once: what the activation backward (norm.hip
+// act_bwd_colsum_kernel) computes from the stored dH.  RELU: p is the ReLU's output (> 0
+// exactly where its input is), else GELU's pre-activation.
+template <bool RELU>
+__device__ __forceinline__ float act_grad(float p) {
+  return RELU ? (p > 0.f ? 1.f : 0.f) : gelu_grad_erf(p);
+}
+template <bool RELU>
+__device__ __forceinline__ uint4 act_bwd8(uint4 d, uint4 p) {
   const unsigned dw[4] = {d.x, d.y, d.z, d.w}, pw[4] = {p.x, p.y, p.z, p.w};
   unsigned o[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float lo = __uint_as_float(dw[i] << 16) * gelu_grad_erf(__uint_as_float(pw[i] << 16));
-    const float hi = __uint_as_float(dw[i] & 0xffff0000u) * gelu_grad_erf(__uint_as_float(pw[i] & 0xffff0000u));
+    const float lo = __uint_as_float(dw[i] << 16) * act_grad<RELU>(__uint_as_float(pw[i] << 16));
+    const float hi = __uint_as_float(dw[i] & 0xffff0000u) * act_grad<RELU>(__uint_as_float(pw[i] & 0xffff0000u));
     o[i] = (unsigned)(unsigned short)bf16_bits(lo) | ((unsigned)(unsigned short)bf16_bits(hi) << 16);
   }
   return make_uint4(o[0], o[1], o[2], o[3]);
@@ -93,7 +100,8 @@ __device__ __forceinline__ uint4 gelu_bwd8(uint4 d, uint4 p) {
 // output also as MX fp8 (yq e4m3 [M, N] + yqs e8m0 [M, N/32]: the next GEMM's operand,
 // bit-identical to vs_mx_quantize of y), 3 = GELU BACKWARD (the MLP's fc2 dX: y = bf16(x w^T)
 // * gelu'(y2), y2 the saved pre-activation READ in the store loop; no bias): the activation
-// backward's pass over dH (written, then read back with the pre-activation) is gone
+// backward's pass over dH (written, then read back with the pre-activation) is gone;
+// 4 = ReLU backward (the encoder FFN: y2 = the ReLU output, y = bf16(x w^T) * [y2 > 0])
 template <bool F8, int EPI, int GM, int GN, int TM, int TN>
 __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned char* __restrict__ X,
                                                                   const unsigned char* __restrict__ Xs,
@@ -105,8 +113,8 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
   constexpr int BM = GM * TM * 32, BN = GN * TN * 32, NW = GM * GN, NT = 64 * NW;
   constexpr int XB = BM * kRowB, WB = BN * kRowB, STB = XB + WB;      // staged bytes per K-step
   constexpr int SCB = F8 ? (BM + BN) * 4 : 0;                         // staged scale bytes per K-step
-  constexpr bool GF = EPI == 1 || EPI == 2, GB = EPI == 3;             // GELU forward / backward epilogue
-  static_assert(!(GB && F8), "GELU backward: bf16");
+  constexpr bool GF = EPI == 1 || EPI == 2, GB = EPI == 3 || EPI == 4;   // GELU forward / act backward
+  static_assert(!(GB && F8), "activation backward: bf16");
   // [stage][X tile | W tile] then (fp8) [stage][X scales | W scales] then the GELU table
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STB + 2 * SCB + (GF ? kGeluEntries * 2 : 0)];
   unsigned short* sgelu = reinterpret_cast<unsigned short*>(smem + 2 * STB + 2 * SCB);
@@ -281,7 +289,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
           const int m = m0 + row, n = n0 + chunk * 8;
           if (m < M && n < N) {
             const uint4 dv = *reinterpret_cast<const uint4*>(smem + so_off(row, chunk));
-            *reinterpret_cast<uint4*>(Y + (size_t)m * N + n) = gelu_bwd8(dv, pv[i]);
+            *reinterpret_cast<uint4*>(Y + (size_t)m * N + n) = act_bwd8<EPI == 4>(dv, pv[i]);
           }
         }
         return;
@@ -395,7 +403,7 @@ __global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* _
   constexpr int SPT = BM * NCK / NT;                                   // output stores per thread and pass
   constexpr int XI = BM / 8 * NKS / 4;                                 // X DMA instructions per wave
   static_assert(SPT * NT == BM * NCK && XI * 4 * 8 == BM * NKS, "tile shape");
-  constexpr bool GF = EPI == 1 || EPI == 2, GB = EPI == 3;             // GELU forward / backward epilogue
+  constexpr bool GF = EPI == 1 || EPI == 2, GB = EPI == 3 || EPI == 4;   // GELU forward / act backward
   constexpr int SPASS = (GF ? 2 : 1) * SPT;                            // stores per thread and tile
   constexpr int PL = GB ? SPT : 0;                                     // pre-activation loads per thread and tile
   // per tile, in issue order: PL pre loads, the DMA of a later tile (XI), SPASS stores
@@ -517,7 +525,8 @@ __global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* _
           const int idx = threadIdx.x + i * NT, row = idx / NCK, chunk = idx % NCK;
           const int m = m0 + row, n = n0 + chunk * 8;
           if (m < M && n < N)
-            *reinterpret_cast<uint4*>(Y + (size_t)m * N + n) = gelu_bwd8(*reinterpret_cast<const uint4*>(sO + so_off(row, chunk)), pv[i]);
+            *reinterpret_cast<uint4*>(Y + (size_t)m * N + n) =
+                act_bwd8<EPI == 4>(*reinterpret_cast<const uint4*>(sO + so_off(row, chunk)), pv[i]);
         }
         continue;
       }
@@ -579,10 +588,11 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
                              const void* bias, void* y, void* y_pre, void* y_q, void* y_qscales, int M, int N, int K,
                              void* stream) {
   const bool f8 = (mode & VS_TGEMM_FP8) != 0, gelu = (mode & VS_TGEMM_GELU) != 0;
-  const bool gbwd = (mode & VS_TGEMM_GELU_BWD) != 0;
+  const bool gbwd = (mode & VS_TGEMM_GELU_BWD) != 0, rbwd = (mode & VS_TGEMM_RELU_BWD) != 0;
   VS_CHECK(x && w && y, "null pointer");
-  VS_CHECK(!gbwd || (!f8 && !gelu && !(mode & VS_TGEMM_QOUT) && !bias && y_pre && N % 8 == 0),
-           "GELU backward: bf16, no bias / GELU / quantised output, y_pre (read) given, N % 8 == 0");
+  VS_CHECK(!(gbwd && rbwd), "one activation backward");
+  VS_CHECK(!(gbwd || rbwd) || (!f8 && !gelu && !(mode & VS_TGEMM_QOUT) && !bias && y_pre && N % 8 == 0),
+           "activation backward: bf16, no bias / GELU / quantised output, y_pre (read) given, N % 8 == 0");
   VS_CHECK(M > 0 && N > 0 && K > 0, "empty GEMM");
   VS_CHECK(N % 4 == 0, "N must be a multiple of 4");
   VS_CHECK(f8 ? (K % 128 == 0 && x_scales && w_scales) : (K % 8 == 0), "fp8: K % 128 == 0 and scales; bf16: K % 8 == 0");
@@ -616,6 +626,10 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
       if (nks == 1) VS_TGS(3, 1, 4);
       else if (nks == 2) VS_TGS(3, 2, 4);
       else VS_TGS(3, 3, 2);
+    } else if (rbwd) {
+      if (nks == 1) VS_TGS(4, 1, 4);
+      else if (nks == 2) VS_TGS(4, 2, 4);
+      else VS_TGS(4, 3, 2);
     } else {
       // (K-steps 4-6 with one workgroup per CU were measured slower than the tile kernel:
       // profiles/r5_tgemm_stream_ab.txt)
@@ -651,6 +665,7 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
   else if (qout) VS_TG(false, 2);
   else if (gelu) VS_TG(false, 1);
   else if (gbwd) VS_TG(false, 3);
+  else if (rbwd) VS_TG(false, 4);
   else VS_TG(false, 0);
 #undef VS_TG
   VS_LAUNCH_CHECK();

@@ -239,7 +239,7 @@ class _LinearFn(torch.autograd.Function):
         T = x.numel() // max(1, x.shape[-1])
         tok = sink is None and _dgrad_on_token_gemm(T, weight, x.dtype)
         ctx.wt = _WT.request(weight) if tok else None
-        # x = gelu(pre) of an MLP: the GELU backward rides in the dX GEMM (ops.GeluBackwardSink)
+        # x = act(pre) of an MLP: the activation backward rides in the dX GEMM (ops.ActBackwardSink)
         ctx.gs = (gelu_sink if tok and gelu_sink is not None and gelu_sink.pre is not None
                   and gelu_sink.pre.shape == x.shape and gelu_sink.pre.dtype == x.dtype else None)
         return _forward_gemm(x, weight, bias)
@@ -254,7 +254,8 @@ class _LinearFn(torch.autograd.Function):
             if gres is not None:       # the residual path's gradient of x, added by the GEMM (beta = 1)
                 gx = _addmm_into(gres.reshape(gy2.shape[0], -1), gy2, weight.to(gy2.dtype)).view(x.shape)
             elif ctx.gs is not None and _dgrad_on_token_gemm(gy2.shape[0], weight, gy2.dtype):
-                gx = ops.token_gemm(gy2.contiguous(), _WT.get(ctx.wt), gelu_pre=ctx.gs.pre).view(x.shape)
+                act = {"gelu_pre" if ctx.gs.kind == "gelu" else "relu_out": ctx.gs.pre}
+                gx = ops.token_gemm(gy2.contiguous(), _WT.get(ctx.wt), **act).view(x.shape)
                 ctx.gs.done = True
             else:
                 gx = _dgrad_gemm(gy2, weight, ctx.wt).view(x.shape)
@@ -884,8 +885,8 @@ class TokenLayerNorm(nn.LayerNorm):
 
 def linear_tokens(x, w, b=None, sink=None, gelu_sink=None):
     """F.linear with the split-K weight gradient when x carries many tokens (`sink`: see
-    ops.ResidualSink; armed only on that path; `gelu_sink`: ops.GeluBackwardSink when x is
-    the GELU output of an MLP feeding only this Linear)."""
+    ops.ResidualSink; armed only on that path; `gelu_sink`: ops.ActBackwardSink when x is
+    the GELU / ReLU output of an MLP feeding only this Linear)."""
     tokens = x.numel() // max(1, x.shape[-1])
     if not (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and tokens >= MIN_TOKENS):
         return F.linear(x, w, b)
@@ -905,14 +906,18 @@ class _LinearReluFn(torch.autograd.Function):
     (with the residual sink's gradient, beta = 1) and the split-K weight gradient."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, sink=None):
+    def forward(ctx, x, weight, bias, sink=None, act_sink=None):
         x2 = x.reshape(-1, x.shape[-1])
         y = torch._addmm_activation(bias, x2, weight.t(), use_gelu=False)
         ctx.save_for_backward(x, weight, y)
         ctx.sink = sink
         if sink is not None:
             sink.arm()
-        return y.view(*x.shape[:-1], weight.shape[0])
+        out = y.view(*x.shape[:-1], weight.shape[0])
+        ctx.gs = act_sink if act_sink is not None and act_sink.kind == "relu" else None
+        if ctx.gs is not None:            # fc2 reads y's sign in its dX epilogue (ops.ActBackwardSink)
+            ctx.gs.pre = out
+        return out
 
     @staticmethod
     def backward(ctx, gy):
@@ -920,11 +925,17 @@ class _LinearReluFn(torch.autograd.Function):
         N = y.shape[-1]
         M = y.shape[0]
         gy2 = gy.reshape(M, N).to(y.dtype).contiguous()
-        gp = torch.empty_like(y)
-        cs = torch.empty(N, device=y.device, dtype=y.dtype)
-        ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=y.device, dtype=torch.uint8)
-        L.check(L.lib().vs_act_backward_colsum(L.dtype_code(y), 0, L.ptr(gy2), L.ptr(y), L.ptr(gp), L.ptr(cs),
-                                               L.ptr(ws), M, N, L.stream(y)), "act_backward_colsum")
+        if ctx.gs is not None and ctx.gs.done:
+            # fc2's dX GEMM already applied the ReLU mask: gy IS the pre-activation's gradient
+            ctx.gs.done = False
+            gp, cs = gy2, None
+        else:
+            gp = torch.empty_like(y)
+            cs = torch.empty(N, device=y.device, dtype=y.dtype)
+            ws = torch.empty(int(L.lib().vs_column_sum_workspace_bytes(M, N)), device=y.device, dtype=torch.uint8)
+            L.check(L.lib().vs_act_backward_colsum(L.dtype_code(y), 0, L.ptr(gy2), L.ptr(y), L.ptr(gp), L.ptr(cs),
+                                                   L.ptr(ws), M, N, L.stream(y)), "act_backward_colsum")
+        ctx.gs = None
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gres = ctx.sink.take() if ctx.sink is not None else None
@@ -932,23 +943,30 @@ class _LinearReluFn(torch.autograd.Function):
                 gx = _addmm_into(gres.reshape(M, -1), gp, weight.to(gp.dtype)).view(x.shape)
             else:
                 gx = _dgrad_gemm(gp, weight).view(x.shape)
-        if ctx.needs_input_grad[1]:
-            gw = weight_grad(gp, x.reshape(-1, x.shape[-1]).to(gp.dtype), weight.dtype)
-        if ctx.needs_input_grad[2]:
+        x2 = x.reshape(-1, x.shape[-1]).to(gp.dtype)
+        if ctx.needs_input_grad[2] and cs is None:
+            if ctx.needs_input_grad[1] and _token_wgrad_ok(gp, x2, weight.dtype):
+                gw, gb = weight_grad(gp, x2, weight.dtype, bias=True)
+            else:
+                gb = ops.column_sum(gp).to(weight.dtype)
+        elif ctx.needs_input_grad[2]:
             gb = cs.to(weight.dtype)
-        return gx, gw, gb, None
+        if ctx.needs_input_grad[1] and gw is None:
+            gw = weight_grad(gp, x2, weight.dtype)
+        return gx, gw, gb, None, None
 
 
-def linear_relu_tokens(x, w, b, sink=None):
+def linear_relu_tokens(x, w, b, sink=None, act_sink=None):
     """relu(F.linear(x, w, b)) -- fused on token-heavy device tensors (see _LinearReluFn);
-    the unfused composition otherwise (`sink`: ops.ResidualSink, armed only when fused)."""
+    the unfused composition otherwise (`sink`: ops.ResidualSink, armed only when fused;
+    `act_sink`: ops.ActBackwardSink("relu") when the output feeds only the FFN's fc2)."""
     from . import ops
     tokens = x.numel() // max(1, x.shape[-1])
     N = w.shape[0]
     if (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and b is not None and tokens >= MIN_TOKENS
             and not torch.is_autocast_enabled() and x.dtype == w.dtype == b.dtype
             and x.dtype in (torch.float32, torch.bfloat16) and N % 8 == 0 and N <= ops.COLSUM_MAX_N and x.is_contiguous()):
-        return _LinearReluFn.apply(x, w, b, sink)
+        return _LinearReluFn.apply(x, w, b, sink, act_sink)
     return ops.activation(linear_tokens(x, w, b, sink), "relu")
 
 

@@ -438,8 +438,10 @@ class EncoderLayer(nn.Module):
         # the dX GEMM of the branch's first op (ops.ResidualSink), not by autograd
         s1, s2 = ops.ResidualSink(), ops.ResidualSink()
         _, h = self.norm1.add_forward(h, self.attn(h, pos, ref, shapes, norm, level, s1), s1)
-        f = linear_relu_tokens(h, self.fc1.weight, self.fc1.bias, s2)                # bias + ReLU in the GEMM
-        _, h = self.norm2.add_forward(h, self.fc2(f), s2)
+        # bias + ReLU in the GEMM; the ReLU's backward in fc2's dX epilogue (ops.ActBackwardSink)
+        rs = ops.ActBackwardSink("relu")
+        f = linear_relu_tokens(h, self.fc1.weight, self.fc1.bias, s2, act_sink=rs)
+        _, h = self.norm2.add_forward(h, linear_tokens(f, self.fc2.weight, self.fc2.bias, gelu_sink=rs), s2)
         return h
 
 

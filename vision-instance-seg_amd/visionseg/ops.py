@@ -1444,21 +1444,27 @@ class ResidualSink:
         return g
 
 
-class GeluBackwardSink:
-    """The GELU backward of one MLP (fc1 -> GELU -> fc2) folded into fc2's dX GEMM
-    (token_gemm gelu_pre: the epilogue reads the saved pre-activation), so dH is never written
-    and read back by a separate activation pass.  Protocol (one object per MLP call, owned by
-    the caller, whose GELU output feeds fc2 ONLY): the GELU producer records its saved
-    pre-activation (`pre`); fc2's Linear takes the sink in its forward when its dX runs on the
-    token GEMM and, in its backward (which runs first), returns dpre = (dY W2) * gelu'(pre) and
-    sets `done`; the GELU's backward then passes that gradient through unchanged.  Either side
-    on another path leaves the sink unused and autograd runs the plain composition."""
+class ActBackwardSink:
+    """The activation backward of one MLP (fc1 -> GELU / ReLU -> fc2) folded into fc2's dX
+    GEMM (token_gemm gelu_pre / relu_out: the epilogue reads the saved pre-activation, resp.
+    the ReLU output = fc2's own input), so dH is never written and read back by a separate
+    activation pass.  Protocol (one object per MLP call, owned by the caller, whose activation
+    output feeds fc2 ONLY): the activation's producer records the tensor (`pre`); fc2's Linear
+    takes the sink in its forward when its dX runs on the token GEMM and, in its backward
+    (which runs first), returns dpre = (dY W2) * act'(pre) and sets `done`; the activation's
+    backward then passes that gradient through unchanged.  Either side on another path leaves
+    the sink unused and autograd runs the plain composition."""
 
-    __slots__ = ("pre", "done")
+    __slots__ = ("kind", "pre", "done")
 
-    def __init__(self):
+    def __init__(self, kind: str = "gelu"):
+        assert kind in ("gelu", "relu")
+        self.kind = kind
         self.pre = None
         self.done = False
+
+
+GeluBackwardSink = ActBackwardSink
 
 
 class _ActColsumFunction(torch.autograd.Function):
@@ -1472,7 +1478,7 @@ class _ActColsumFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, act, gelu_sink=None):
         ctx.act = act
-        ctx.gs = gelu_sink if act == 1 else None
+        ctx.gs = gelu_sink if act == 1 and gelu_sink is not None and gelu_sink.kind == "gelu" else None
         if ctx.gs is not None:
             ctx.gs.pre = x
         ctx.save_for_backward(x)
@@ -1983,7 +1989,7 @@ def conv3x3_nhwc(x, weight, bias=None):
 # ---------------------------------------------------------------------------------------
 # token GEMM (csrc/token_gemm.hip): the Swin blocks' Linears, bf16 or block-scaled MX fp8
 # ---------------------------------------------------------------------------------------
-TGEMM_FP8, TGEMM_GELU, TGEMM_QOUT, TGEMM_GELU_BWD = 1, 2, 4, 8
+TGEMM_FP8, TGEMM_GELU, TGEMM_QOUT, TGEMM_GELU_BWD, TGEMM_RELU_BWD = 1, 2, 4, 8, 16
 
 
 def mx_quantize(x: torch.Tensor):
@@ -2027,14 +2033,21 @@ def row_quantize_fp8(x: torch.Tensor, gelu: bool = False):
 
 
 def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None, quant_out: bool = False,
-               gelu_pre=None):
+               gelu_pre=None, relu_out=None):
     """y = x w^T + bias over token rows (x [..., K], w [N, K]; bf16, or -- with scales --
     e4m3 bytes from mx_quantize) -> bf16 [..., N]; gelu=True -> (gelu(y), y) with the exact
     erf GELU in the epilogue (y = the bf16 pre-activation); quant_out=True (with gelu) ->
     (gelu(y), y, (e4m3 bytes, e8m0 scales) of gelu(y), as mx_quantize would make them).
     gelu_pre ([..., N] bf16, no bias): the GELU BACKWARD in the epilogue -> bf16(x w^T) *
-    gelu'(gelu_pre), each product rounded once (VS_TGEMM_GELU_BWD: fc2's dX of an MLP)."""
+    gelu'(gelu_pre), each product rounded once (VS_TGEMM_GELU_BWD: fc2's dX of an MLP);
+    relu_out (the same for a ReLU, given its OUTPUT): bf16(x w^T) * [relu_out > 0]."""
     fp8 = x_scales is not None
+    if relu_out is not None:
+        if gelu_pre is not None:
+            raise ValueError("token_gemm: one activation backward")
+        gelu_pre, act_mode = relu_out, TGEMM_RELU_BWD
+    else:
+        act_mode = TGEMM_GELU_BWD
     L.require_hip(x, w)
     K = x.shape[-1]
     N = w.shape[0]
@@ -2062,7 +2075,7 @@ def token_gemm(x, w, bias=None, gelu: bool = False, x_scales=None, w_scales=None
     yqs = torch.empty(M, N // 32, device=x.device, dtype=torch.uint8) if quant_out else None
     mode = (TGEMM_FP8 if fp8 else 0) | (TGEMM_GELU if gelu else 0) | (TGEMM_QOUT if quant_out else 0)
     if gelu_pre is not None:
-        mode |= TGEMM_GELU_BWD
+        mode |= act_mode
         pre = gelu_pre.reshape(M, N).contiguous()
         if pre.data_ptr() % 16:
             pre = pre.clone()
