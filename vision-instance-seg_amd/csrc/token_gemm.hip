@@ -171,6 +171,20 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
     for (int i = threadIdx.x; i < kGeluEntries / 8; i += NT)
       reinterpret_cast<uint4*>(sgelu)[i] = reinterpret_cast<const uint4*>(kGeluTable)[i];
   }
+  // activation backward: this thread's pre-activation chunks of the output tile, requested
+  // with the last K-step's operands (the 128 x 128 tile: 8 registers x 4; the 256 x 256
+  // tile's 16 would not fit beside its accumulators -- it loads them after the staging)
+  constexpr int SPL = (EPI < 2 || GB) ? BM * (BN / 8) / NT : 1;
+  constexpr bool PEARLY = GB && SPL <= 8;
+  uint4 pv[GB ? SPL : 1];
+  auto load_pre = [&]() {
+#pragma unroll
+    for (int i = 0; i < SPL; ++i) {
+      const int idx = threadIdx.x + i * NT, row = idx / (BN / 8), chunk = idx - (idx / (BN / 8)) * (BN / 8);
+      const int m = m0 + row, n = n0 + chunk * 8;
+      pv[i] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(Y2 + (size_t)m * N + n) : make_uint4(0, 0, 0, 0);
+    }
+  };
   for (int ks = 0; ks < nks; ++ks) {
     const int st = ks & 1;
     wait_vm<0>();                                     // this wave's DMA of step ks landed
@@ -187,6 +201,7 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
       raw_barrier();
     }
     if (ks + 1 < nks) issue(ks + 1, st ^ 1);          // the other buffer: last read in step ks - 1
+    else if (PEARLY) load_pre();
     if (F8) {
       const unsigned* ss = reinterpret_cast<const unsigned*>(smem + 2 * STB + st * SCB);
       unsigned xsc[TM], wsc[TN];
@@ -272,16 +287,8 @@ __global__ void __launch_bounds__(64 * GM * GN) token_gemm_kernel(const unsigned
         }
       }
       if (GB) {
-        // GELU backward: this thread's pre-activation chunks, requested before the barrier
-        constexpr int SPL = BM * NCK / NT;
-        static_assert(SPL * NT == BM * NCK, "store split");
-        uint4 pv[SPL];
-#pragma unroll
-        for (int i = 0; i < SPL; ++i) {
-          const int idx = threadIdx.x + i * NT, row = idx / NCK, chunk = idx - (idx / NCK) * NCK;
-          const int m = m0 + row, n = n0 + chunk * 8;
-          pv[i] = (m < M && n < N) ? *reinterpret_cast<const uint4*>(Y2 + (size_t)m * N + n) : make_uint4(0, 0, 0, 0);
-        }
+        static_assert(!GB || SPL * NT == BM * NCK, "store split");
+        if (!PEARLY) load_pre();                       // requested before the barrier
         raw_barrier();
 #pragma unroll
         for (int i = 0; i < SPL; ++i) {
@@ -458,6 +465,19 @@ __global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* _
     const int n = n0 + 32 * w + 8 * g + 4 * hh;
     bvr[g] = (bias && n < N) ? *reinterpret_cast<const bf16x4_t*>(bias + n) : bf16x4_t{0, 0, 0, 0};
   }
+  // activation backward: the pre-activation (ReLU output) chunks of this thread's stores, one
+  // tile AHEAD (tile j's in ring slot j & 1): requested in the same position as the tile's
+  // own loads would be, so each tile finds them landed instead of waiting a round trip
+  uint4 pv0[GB ? SPT : 1], pv1[GB ? SPT : 1];
+  auto load_pre = [&](int j, uint4* pv) {
+    const int m0 = (g0 + j * G) * BM;
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) {
+      const int idx = threadIdx.x + i * NT, row = idx / NCK, chunk = idx % NCK;
+      const int m = min(m0 + row, M - 1), n = min(n0 + chunk * 8, N - 8);   // always a load: counted waits
+      pv[i] = *reinterpret_cast<const uint4*>(Y2 + (size_t)m * N + n);
+    }
+  };
   for (int j = 0; j < NBUF - 1 && j < ntl; ++j) issue_x(j);
   wait_vm<0>();                                                        // W and the first tiles
   for (int j = 0; j < ntl; ++j) {
@@ -642,7 +662,12 @@ extern "C" int vs_token_gemm(int mode, const void* x, const void* x_scales, cons
     return VS_OK;
   }
   // the 256 x 256 tile where the product is MFMA-bound and fills the chip
-  const bool big = N >= 512 && K >= 256 && (long long)((M + 255) / 256) * ((N + 255) / 256) >= 256;
+  // (the activation-backward epilogues take the 128 x 128 tile: its pre-activation loads ride
+  // with the last K-step, and two workgroups per CU overlap one's epilogue with the other's
+  // loop -- 56.5 vs 66.6 us at the stage-3 fc2 dX, 135.7 vs 144.0 at the encoder FFN's,
+  // profiles/r6_act_bwd_epilogue_ab.txt)
+  const bool big = N >= 512 && K >= 256 && (long long)((M + 255) / 256) * ((N + 255) / 256) >= 256 &&
+                   !(gbwd || rbwd);
   const int bm = big ? 256 : 128, bn = big ? 256 : 128;
   const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   VS_CHECK(tiles < (1ll << 31), "too many tiles");
