@@ -1259,7 +1259,9 @@ def _prep_ref(off, lg, ref, shapes, H, P):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", [(2, 37, 8, [(4, 5), (2, 3), (1, 1)], 4, "fused"), (1, 300, 8, [(10, 30)] * 4, 4, "plain"),
                                   (3, 5, 2, [(7, 3)], 1, "plain"), (2, 0, 8, [(2, 2)] * 3, 4, "plain"),
-                                  (1, 64, 3, [(8, 8), (4, 4)], 8, "fused")])
+                                  (1, 64, 3, [(8, 8), (4, 4)], 8, "fused"),
+                                  (2, 37, 8, [(4, 5), (2, 3), (1, 1)], 4, "packed"),
+                                  (4, 300, 8, [(10, 20), (5, 10), (3, 5)], 4, "packed")])
 def test_msda_prep_vs_torch(case, dtype):
     """csrc/msda_prep.hip (sampling locations + softmax weights and their adjoint) vs the
     f32 torch composition: loc / weights <= 1e-6 abs (f32 math on identical inputs), input
@@ -1270,8 +1272,8 @@ def test_msda_prep_vs_torch(case, dtype):
     B, Q, H, shapes, P, layout = case
     nl = len(shapes)
     g = torch.Generator().manual_seed(Q + H)
-    if layout == "fused":
-        proj = (torch.randn(B, Q, H * nl * P * 3 + 5, generator=g) * 3).to(dtype).to(DEV)
+    if layout in ("fused", "packed"):   # packed: the production row (offsets then logits, P = 4: vector kernels)
+        proj = (torch.randn(B, Q, H * nl * P * 3 + (5 if layout == "fused" else 0), generator=g) * 3).to(dtype).to(DEV)
         off, lg = proj[..., :H * nl * P * 2], proj[..., H * nl * P * 2:H * nl * P * 3]
     else:
         off = (torch.randn(B, Q, H * nl * P * 2, generator=g) * 3).to(dtype).to(DEV)

@@ -10,6 +10,7 @@
 //   backward: grad_offsets = grad_loc / (W_l, H_l), grad_logits = a * (g - <g, a>),
 //             rounded to the projections' dtype (as the cast's backward)
 #include "common.h"
+#include "mfma_util.h"
 
 namespace vs {
 namespace {
@@ -129,6 +130,126 @@ __global__ void __launch_bounds__(256) msda_prep_bwd_kernel(const float* __restr
   }
 }
 
+// P = 4 (the production configuration), bf16 projections: every access a whole 8-, 16- or
+// 32-byte vector.  The general kernels above move 2-byte projection elements one at a time
+// and pay integer divisions per element (2.7-3.2 TB/s at the C2 encoder shape).
+//   locations: one thread per (group, level): the level's 4 (x, y) offsets are one 16-B row
+//              piece, its 4 locations two 16-B stores;
+//   weights:   one thread per group: its L*4 logits (3 x 8 B at L = 3), softmax in registers,
+//              L*4 f32 weights as 16-B stores (no LDS).
+// Same arithmetic, same order as the general kernels (x / W_l, f32 softmax).
+__device__ __forceinline__ void bf16x4_to_f32(uint2 v, float* o) {
+  o[0] = __uint_as_float(v.x << 16);
+  o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16);
+  o[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
+template <int L>
+__global__ void __launch_bounds__(256) msda_prep_fwd4_kernel(const bf16* __restrict__ off, const bf16* __restrict__ logit,
+                                                             const float* __restrict__ ref, float* __restrict__ loc,
+                                                             float* __restrict__ aw, PrepGeom gm, int Q, int Hh,
+                                                             long long off_rs, long long logit_rs, long long ref_bs,
+                                                             long long groups) {
+  constexpr int LP = L * 4;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t < groups * L) {                                   // locations: item (group, level)
+    const long long g = t / L;
+    const int l = (int)(t - g * L);
+    const long long bq = g / Hh;
+    const int h = (int)(g - bq * Hh);
+    const long long b = bq / Q;
+    const int q = (int)(bq - b * Q);
+    const uint4 o = *reinterpret_cast<const uint4*>(off + bq * off_rs + (h * L + l) * 8);
+    const float2 r = *reinterpret_cast<const float2*>(ref + b * ref_bs + ((long long)q * L + l) * 2);
+    float v[8];
+    bf16x4_to_f32(make_uint2(o.x, o.y), v);
+    bf16x4_to_f32(make_uint2(o.z, o.w), v + 4);
+    const float w = gm.w[l], hgt = gm.h[l];
+    float4* dst = reinterpret_cast<float4*>(loc + g * LP * 2 + l * 8);
+    dst[0] = make_float4(r.x + v[0] / w, r.y + v[1] / hgt, r.x + v[2] / w, r.y + v[3] / hgt);
+    dst[1] = make_float4(r.x + v[4] / w, r.y + v[5] / hgt, r.x + v[6] / w, r.y + v[7] / hgt);
+  }
+  if (t < groups) {                                       // weights: one group
+    const long long g = t;
+    const long long bq = g / Hh;
+    const int h = (int)(g - bq * Hh);
+    const uint2* src = reinterpret_cast<const uint2*>(logit + bq * logit_rs + h * LP);
+    float v[LP];
+#pragma unroll
+    for (int k = 0; k < L; ++k) bf16x4_to_f32(src[k], v + 4 * k);
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < LP; ++i) m = fmaxf(m, v[i]);
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < LP; ++i) {
+      v[i] = expf(v[i] - m);
+      sum += v[i];
+    }
+    float4* dst = reinterpret_cast<float4*>(aw + g * LP);
+#pragma unroll
+    for (int k = 0; k < L; ++k) dst[k] = make_float4(v[4 * k] / sum, v[4 * k + 1] / sum, v[4 * k + 2] / sum, v[4 * k + 3] / sum);
+  }
+}
+
+template <int L>
+__global__ void __launch_bounds__(256) msda_prep_bwd4_kernel(const float* __restrict__ gloc,
+                                                             const float* __restrict__ gaw,
+                                                             const float* __restrict__ aw, bf16* __restrict__ goff,
+                                                             bf16* __restrict__ glogit, PrepGeom gm, int Hh,
+                                                             long long goff_rs, long long glogit_rs, long long groups) {
+  constexpr int LP = L * 4;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t < groups * L) {                                   // offsets' gradient: item (group, level)
+    const long long g = t / L;
+    const int l = (int)(t - g * L);
+    const long long bq = g / Hh;
+    const int h = (int)(g - bq * Hh);
+    const float4* src = reinterpret_cast<const float4*>(gloc + g * LP * 2 + l * 8);
+    const float4 a = src[0], c = src[1];
+    const float w = gm.w[l], hgt = gm.h[l];
+    uint4 o;
+    o.x = (unsigned)(unsigned short)bf16_bits(a.x / w) | ((unsigned)(unsigned short)bf16_bits(a.y / hgt) << 16);
+    o.y = (unsigned)(unsigned short)bf16_bits(a.z / w) | ((unsigned)(unsigned short)bf16_bits(a.w / hgt) << 16);
+    o.z = (unsigned)(unsigned short)bf16_bits(c.x / w) | ((unsigned)(unsigned short)bf16_bits(c.y / hgt) << 16);
+    o.w = (unsigned)(unsigned short)bf16_bits(c.z / w) | ((unsigned)(unsigned short)bf16_bits(c.w / hgt) << 16);
+    *reinterpret_cast<uint4*>(goff + bq * goff_rs + (h * L + l) * 8) = o;
+  }
+  if (t < groups) {                                       // logits' gradient: one group
+    const long long g = t;
+    const long long bq = g / Hh;
+    const int h = (int)(g - bq * Hh);
+    float a[LP], gg[LP];
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      const float4 x = reinterpret_cast<const float4*>(aw + g * LP)[k];
+      const float4 y = reinterpret_cast<const float4*>(gaw + g * LP)[k];
+      a[4 * k] = x.x; a[4 * k + 1] = x.y; a[4 * k + 2] = x.z; a[4 * k + 3] = x.w;
+      gg[4 * k] = y.x; gg[4 * k + 1] = y.y; gg[4 * k + 2] = y.z; gg[4 * k + 3] = y.w;
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < LP; ++i) dot += gg[i] * a[i];
+    uint2* dst = reinterpret_cast<uint2*>(glogit + bq * glogit_rs + h * LP);
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      float r[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = a[4 * k + e] * (gg[4 * k + e] - dot);
+      dst[k] = make_uint2((unsigned)(unsigned short)bf16_bits(r[0]) | ((unsigned)(unsigned short)bf16_bits(r[1]) << 16),
+                          (unsigned)(unsigned short)bf16_bits(r[2]) | ((unsigned)(unsigned short)bf16_bits(r[3]) << 16));
+    }
+  }
+}
+
+// the vector kernels' alignment: 16-B offset rows, 8-B logit pieces, 16-B f32 outputs
+bool prep4_ok(int dtype, int P, int L, const void* off, long long off_rs, const void* logit, long long logit_rs,
+              const void* f1, const void* f2) {
+  return dtype == VS_BF16 && P == 4 && L >= 1 && L <= 4 && ((uintptr_t)off & 15) == 0 && off_rs % 8 == 0 &&
+         ((uintptr_t)logit & 7) == 0 && logit_rs % 4 == 0 && ((uintptr_t)f1 & 15) == 0 && ((uintptr_t)f2 & 15) == 0;
+}
+
 int fill_geom(PrepGeom* gm, const int64_t* shapes, int L) {
   for (int l = 0; l < 4; ++l) gm->w[l] = gm->h[l] = 1.f;
   for (int l = 0; l < L; ++l) {
@@ -160,6 +281,21 @@ extern "C" int vs_msda_prep_forward(int dtype, const void* offsets, long long of
   VS_CHECK(((uintptr_t)ref & 7) == 0 && ref_batch_stride % 2 == 0 && ((uintptr_t)loc & 7) == 0,
            "ref / loc must be 8-byte aligned with an even batch stride");
   hipStream_t st = (hipStream_t)stream;
+  if (prep4_ok(dtype, P, L, offsets, offsets_row_stride, logits, logits_row_stride, loc, attw)) {
+    const dim3 g4((unsigned)((groups * L + 255) / 256));
+#define VS_PF4(LL)                                                                                                  \
+  hipLaunchKernelGGL((msda_prep_fwd4_kernel<LL>), g4, dim3(256), 0, st, (const bf16*)offsets, (const bf16*)logits, \
+                     ref, loc, attw, gm, Q, Hh, offsets_row_stride, logits_row_stride, ref_batch_stride, groups)
+    switch (L) {
+      case 1: VS_PF4(1); break;
+      case 2: VS_PF4(2); break;
+      case 3: VS_PF4(3); break;
+      default: VS_PF4(4); break;
+    }
+#undef VS_PF4
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
   const int grid = (int)((groups + kGroups - 1) / kGroups);
   if (dtype == VS_BF16)
     hipLaunchKernelGGL(msda_prep_fwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)offsets,
@@ -190,6 +326,23 @@ extern "C" int vs_msda_prep_backward(int dtype, const float* grad_loc, const flo
   VS_CHECK(grad_loc && grad_attw && attw && grad_offsets && grad_logits, "null pointer");
   VS_CHECK(((uintptr_t)grad_loc & 7) == 0, "grad_loc must be 8-byte aligned");
   hipStream_t st = (hipStream_t)stream;
+  if (prep4_ok(dtype, P, L, grad_offsets, grad_offsets_row_stride, grad_logits, grad_logits_row_stride, grad_loc,
+               grad_attw) && ((uintptr_t)attw & 15) == 0) {
+    const dim3 g4((unsigned)((groups * L + 255) / 256));
+#define VS_PB4(LL)                                                                                                \
+  hipLaunchKernelGGL((msda_prep_bwd4_kernel<LL>), g4, dim3(256), 0, st, grad_loc, grad_attw, attw,                \
+                     (bf16*)grad_offsets, (bf16*)grad_logits, gm, Hh, grad_offsets_row_stride,                    \
+                     grad_logits_row_stride, groups)
+    switch (L) {
+      case 1: VS_PB4(1); break;
+      case 2: VS_PB4(2); break;
+      case 3: VS_PB4(3); break;
+      default: VS_PB4(4); break;
+    }
+#undef VS_PB4
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
   const int grid = (int)((groups + kGroups - 1) / kGroups);
   if (dtype == VS_BF16)
     hipLaunchKernelGGL(msda_prep_bwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, grad_loc, grad_attw, attw,
