@@ -987,9 +987,13 @@ def test_masked_attention_bf16_fwd_bwd_vs_oracle(monkeypatch, kernel, B, Q, S):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("shape,groups,cl", [((2, 256, 64, 64), 32, True), ((2, 256, 17, 23), 32, True),
-                                             ((1, 64, 5, 7), 8, False), ((1, 256, 256, 256), 32, True)])
+                                             ((1, 64, 5, 7), 8, False), ((1, 256, 256, 256), 32, True),
+                                             ((4, 256, 128, 128), 32, True), ((9, 512, 33, 31), 64, True),
+                                             ((3, 16, 9, 11), 2, True), ((8, 256, 128, 128), 32, True)])
 def test_group_norm_nhwc_vs_torch(dtype, relu, shape, groups, cl):
     """Channels-last GroupNorm (+ReLU) forward/backward (csrc/groupnorm.hip) vs torch f64.
+    Shapes cover 1..256 row chunks per image and 1..64 dw/db slices (B = 8 at 128^2:
+    2048 channel partials), a column count below one 64-lane block (C = 16).
     With the ReLU, a pre-activation within rounding of 0 may be masked differently by
     the kernel (f32 statistics) and the f64 reference: every such disagreement must sit at
     |pre-activation| < 1e-4, and the gradients are compared against the reference using

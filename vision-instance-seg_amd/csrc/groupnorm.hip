@@ -22,8 +22,13 @@ namespace vs {
 namespace {
 
 constexpr int kT = 256;
-constexpr int kMinRows = 256;      // rows per chunk: max(kMinRows, HW / kMaxChunks)
-constexpr int kMaxChunks = 64;
+// rows per chunk: max(kMinRows, HW / kMaxChunks).  Up to 256 chunks per image so the
+// statistics passes launch ~1024 blocks at B = 4 (16 KB of loads in flight per block;
+// 64 chunks left them at 1.2-2.2 TB/s, profiles/r6_gn_parallel_ab.txt).
+constexpr int kMinRows = 32;
+constexpr int kMaxChunks = 256;
+constexpr int kPartsPerSlice = 32;  // dw / db level-1 slices: >= 32 parts each, <= 64 slices
+constexpr int kMaxSlices = 64;
 
 template <typename T>
 __device__ __forceinline__ void ld8f(const T* p, float* v) {
@@ -85,18 +90,38 @@ __global__ void __launch_bounds__(kT) gn_stats_kernel(const T* __restrict__ x, f
   }
 }
 
+// butterfly over the 64 lanes: every pair adds the same two operands, so all lanes end with
+// the same, schedule-independent value
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// one wave per (b, g): lane l sums chunks l, l + 64, ... in f64, then a wave butterfly
+__device__ __forceinline__ bool group_sums(const float* __restrict__ part, int i, int G, int nchunk, double& s,
+                                          double& q) {
+  const int l = threadIdx.x & 63;
+  const int b = i / G, g = i % G;
+  s = 0.0;
+  q = 0.0;
+  for (int c = l; c < nchunk; c += 64) {
+    const float2 p = *reinterpret_cast<const float2*>(part + (((size_t)b * nchunk + c) * G + g) * 2);
+    s += p.x;
+    q += p.y;
+  }
+  s = wave_sum_f64(s);
+  q = wave_sum_f64(q);
+  return l == 0;
+}
+
 __global__ void __launch_bounds__(kT) gn_finalize_kernel(const float* __restrict__ part, float* __restrict__ mean,
                                                          float* __restrict__ rstd, int B, int HW, int G, int nchunk,
                                                          float eps) {
-  const int i = blockIdx.x * kT + threadIdx.x;   // (b, g)
+  const int i = blockIdx.x * (kT / 64) + (threadIdx.x >> 6);   // (b, g), wave-uniform
   if (i >= B * G) return;
-  const int b = i / G, g = i % G;
-  double s = 0.0, q = 0.0;
-  for (int c = 0; c < nchunk; ++c) {
-    const float* p = part + (((size_t)b * nchunk + c) * G + g) * 2;
-    s += p[0];
-    q += p[1];
-  }
+  double s, q;
+  if (!group_sums(part, i, G, nchunk, s, q)) return;
   const double n = (double)HW * 8.0;
   const double m = s / n;
   const double var = fmax(q / n - m * m, 0.0);
@@ -203,50 +228,43 @@ __global__ void __launch_bounds__(kT) gn_bwd_stats_kernel(const T* __restrict__ 
   }
 }
 
-// group coefficients c1 = mean(g), c2 = mean(g xhat) per (b, g)
+// Blocks [0, nfin): group coefficients c1 = mean(g), c2 = mean(g xhat), one wave per (b, g).
+// Blocks [nfin, ...): level 1 of dw / db -- a block sums one slice of pps consecutive parts
+// for 64 (channel, which) columns (lane = column, 4 waves interleaved over the slice) into
+// wpart[slice][2C]; gn_bwd_apply_kernel adds the slices in order.  Fixed order throughout.
 __global__ void __launch_bounds__(kT) gn_bwd_finalize_kernel(const float* __restrict__ gpart, float* __restrict__ c12,
-                                                             int B, int HW, int G, int nchunk) {
-  const int i = blockIdx.x * kT + threadIdx.x;
-  if (i >= B * G) return;
-  const int b = i / G, g = i % G;
-  double a = 0.0, c = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
-    const float* p = gpart + (((size_t)b * nchunk + k) * G + g) * 2;
-    a += p[0];
-    c += p[1];
+                                                             const float* __restrict__ cpart,
+                                                             float* __restrict__ wpart, int B, int HW, int G,
+                                                             int nchunk, int nfin, int pps) {
+  if ((int)blockIdx.x < nfin) {
+    const int i = blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+    if (i >= B * G) return;
+    double a, c;
+    if (!group_sums(gpart, i, G, nchunk, a, c)) return;
+    const double n = (double)HW * 8.0;
+    c12[i * 2 + 0] = (float)(a / n);
+    c12[i * 2 + 1] = (float)(c / n);
+    return;
   }
-  const double n = (double)HW * 8.0;
-  c12[i * 2 + 0] = (float)(a / n);
-  c12[i * 2 + 1] = (float)(c / n);
-}
-
-// dw / db: sum of the per-chunk channel partials in a fixed order; a block = 32 (channel,
-// which) columns x 8 part slices, 4 independent accumulators, slices combined in LDS
-template <typename T>
-__global__ void __launch_bounds__(kT) gn_bwd_wb_kernel(const float* __restrict__ cpart, T* __restrict__ dw,
-                                                       T* __restrict__ db, int nparts, int C) {
-  __shared__ float red[8][33];
-  const int lane = threadIdx.x & 31, sl = threadIdx.x >> 5;
-  const int j = blockIdx.x * 32 + lane;          // (channel, which) = cpart column
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (j < 2 * C) {
-    int k = sl;
-    for (; k + 24 < nparts; k += 32) {
-      a0 += cpart[(size_t)k * 2 * C + j];
-      a1 += cpart[(size_t)(k + 8) * 2 * C + j];
-      a2 += cpart[(size_t)(k + 16) * 2 * C + j];
-      a3 += cpart[(size_t)(k + 24) * 2 * C + j];
+  __shared__ float red[4][64];
+  const int C2 = 16 * G;                         // (channel, which) columns
+  const int ncb = (C2 + 63) / 64;
+  const int nb = blockIdx.x - nfin, cb = nb % ncb, sl = nb / ncb;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = cb * 64 + lane;
+  const int k1 = min(B * nchunk, (sl + 1) * pps);
+  float a0 = 0.f, a1 = 0.f;
+  if (col < C2) {
+    int k = sl * pps + w;
+    for (; k + 4 < k1; k += 8) {
+      a0 += cpart[(size_t)k * C2 + col];
+      a1 += cpart[(size_t)(k + 4) * C2 + col];
     }
-    for (; k < nparts; k += 8) a0 += cpart[(size_t)k * 2 * C + j];
+    if (k < k1) a0 += cpart[(size_t)k * C2 + col];
   }
-  red[sl][lane] = (a0 + a1) + (a2 + a3);
+  red[w][lane] = a0 + a1;
   __syncthreads();
-  if (sl == 0 && j < 2 * C) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) t += red[i][lane];
-    ((j & 1) ? db : dw)[j >> 1] = from_f32<T>(t);
-  }
+  if (w == 0 && col < C2) wpart[(size_t)sl * C2 + col] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 template <typename T, bool RELU>
@@ -255,7 +273,16 @@ __global__ void __launch_bounds__(kT) gn_bwd_apply_kernel(const T* __restrict__ 
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ rstd,
                                                           const float* __restrict__ c12, T* __restrict__ dx, int B,
-                                                          int HW, int G) {
+                                                          int HW, int G, const float* __restrict__ wpart, int nslice,
+                                                          T* __restrict__ dw, T* __restrict__ db) {
+  if ((int)blockIdx.x * kT < 16 * G) {           // level 2 of dw / db: slices in order
+    const int col = blockIdx.x * kT + threadIdx.x;
+    if (col < 16 * G) {
+      float t = 0.f;
+      for (int s = 0; s < nslice; ++s) t += wpart[(size_t)s * 16 * G + col];
+      ((col & 1) ? db : dw)[col >> 1] = from_f32<T>(t);
+    }
+  }
   const long long n = (long long)B * HW * G;
   for (long long i = (long long)blockIdx.x * kT + threadIdx.x; i < n; i += (long long)gridDim.x * kT) {
     const int g = (int)(i % G);
@@ -548,6 +575,9 @@ int chunks_for(int HW) { return (HW + rows_per_chunk(HW) - 1) / rows_per_chunk(H
 
 int apply_grid(long long n) { return (int)std::min<long long>((n + kT - 1) / kT, 256 * 32); }
 
+// dw / db level-1 slicing of the B * nchunk channel partials
+int parts_per_slice(int nparts) { return std::max(kPartsPerSlice, (nparts + kMaxSlices - 1) / kMaxSlices); }
+
 }  // namespace
 }  // namespace vs
 
@@ -555,8 +585,9 @@ using namespace vs;
 
 extern "C" long long vs_group_norm_workspace_bytes(int B, int HW, int C, int G) {
   const long long nchunk = chunks_for(HW);
-  // forward: group partials; backward: group partials + channel partials + c12
-  return (long long)B * nchunk * G * 2 * 4 + (long long)B * nchunk * C * 2 * 4 + (long long)B * G * 2 * 4 + 256;
+  // forward: group partials; backward: group partials + channel partials + c12 + dw/db slices
+  return (long long)B * nchunk * G * 2 * 4 + (long long)B * nchunk * C * 2 * 4 + (long long)B * G * 2 * 4 +
+         (long long)kMaxSlices * C * 2 * 4 + 256;
 }
 
 #define VS_GN_CHECK()                                                                           \
@@ -580,8 +611,8 @@ extern "C" int vs_group_norm_forward(int dtype, const void* x, const void* weigh
   else
     hipLaunchKernelGGL(gn_stats_kernel<float>, dim3(nchunk, B), dim3(kT), lds, st, (const float*)x, part, HW, G,
                        nchunk, rows_per_chunk(HW));
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * G + kT - 1) / kT), dim3(kT), 0, st, part, mean, rstd, B, HW, G,
-                     nchunk, eps);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * G + 3) / 4), dim3(kT), 0, st, part, mean, rstd, B, HW, G, nchunk,
+                     eps);
 #define VS_GN_APPLY(TT, R)                                                                                    \
   hipLaunchKernelGGL((gn_apply_kernel<TT, R>), dim3(apply_grid(n)), dim3(kT), 0, st, (const TT*)x,           \
                      (const TT*)weight, (const TT*)bias, mean, rstd, (TT*)y, B, HW, G)
@@ -607,18 +638,23 @@ extern "C" int vs_group_norm_backward(int dtype, const void* grad_y, const void*
   float* gpart = (float*)workspace;
   float* cpart = gpart + (size_t)B * nchunk * G * 2;
   float* c12 = cpart + (size_t)B * nchunk * C * 2;
+  float* wpart = c12 + (size_t)B * G * 2;
   const size_t lds = (size_t)kT * 18 * sizeof(float);
   const long long n = (long long)B * HW * G;
+  const int nfin = (B * G + 3) / 4;
+  const int pps = parts_per_slice(B * nchunk);
+  const int nslice = (B * nchunk + pps - 1) / pps;
+  const int nwb = ((2 * C + 63) / 64) * nslice;
+  const int agrid = std::max(apply_grid(n), (2 * C + kT - 1) / kT);
 #define VS_GN_BWD(TT, R)                                                                                          \
   hipLaunchKernelGGL((gn_bwd_stats_kernel<TT, R>), dim3(nchunk, B), dim3(kT), lds, st, (const TT*)grad_y,         \
                      (const TT*)x, (const TT*)weight, (const TT*)bias, mean, rstd, gpart, cpart, HW, G, nchunk,    \
                      rows_per_chunk(HW));                                                                         \
-  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3((B * G + kT - 1) / kT), dim3(kT), 0, st, gpart, c12, B, HW, G,   \
-                     nchunk);                                                                                     \
-  hipLaunchKernelGGL((gn_bwd_wb_kernel<TT>), dim3((2 * C + 31) / 32), dim3(kT), 0, st, cpart, (TT*)grad_weight,    \
-                     (TT*)grad_bias, B * nchunk, C);                                                              \
-  hipLaunchKernelGGL((gn_bwd_apply_kernel<TT, R>), dim3(apply_grid(n)), dim3(kT), 0, st, (const TT*)grad_y,       \
-                     (const TT*)x, (const TT*)weight, (const TT*)bias, mean, rstd, c12, (TT*)grad_x, B, HW, G)
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(nfin + nwb), dim3(kT), 0, st, gpart, c12, cpart, wpart, B, HW, G, \
+                     nchunk, nfin, pps);                                                                          \
+  hipLaunchKernelGGL((gn_bwd_apply_kernel<TT, R>), dim3(agrid), dim3(kT), 0, st, (const TT*)grad_y, (const TT*)x, \
+                     (const TT*)weight, (const TT*)bias, mean, rstd, c12, (TT*)grad_x, B, HW, G, wpart, nslice,   \
+                     (TT*)grad_weight, (TT*)grad_bias)
   if (dtype == VS_BF16) {
     if (relu) { VS_GN_BWD(bf16, true); } else { VS_GN_BWD(bf16, false); }
   } else {
