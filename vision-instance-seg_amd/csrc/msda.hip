@@ -1269,7 +1269,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
 // the tile kernel (Dm[q][cell] = g[q] . value[cell] per (band, chunk), the band's value
 // rows loaded once and reused by every chunk, stored transposed over W: 16-B stores); a
 // tap's corner dots stay in registers across bands (dk[chunk][corner]).  Band / chunk pairs are skipped from per-chunk boxes
-// (no vote barrier).  4 LDS-only barriers per pair (W built -> product -> Dm -> dots).
+// (no vote barrier).  2 LDS-only barriers per pair (W built -> product + Dm; Dm stored -> dots):
+// the product / Dm^T overlay and the dots / W clear touch one wave's own rows / columns only
+// (round 6; the round-5 kernel had a barrier after each of the four phases).
 
 // MFMA operand (8 k-values of one column, k = rows k0 + 8hh + j, column lane & 31) from a
 // row-major bf16 LDS image, by the gfx950 transposed read (cdna_hip_programming.md T10;
@@ -1532,7 +1534,10 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
               acc = mfma16(alo, bq, acc);
             }
           }
-          lds_barrier();                      // W consumed: Dm^T overwrites it
+          // W consumed: Dm^T overwrites it.  A wave's product reads only its own cell rows
+          // (32 wave .. + 31) and its Dm^T store writes only those rows, so program order within
+          // the wave suffices (wave_sync: a compiler fence across its lanes, no instruction)
+          wave_sync();
           float* sD = sW;                     // Dm^T[cell][q], W's layout (pitch kWP8)
           if (!(DBG & 4) && wave < nmt) {     // Dm[q][cell] = g[q] . value[cell], cell tile = wave
 #pragma unroll
@@ -1555,9 +1560,11 @@ msda_bwd_col_kernel(const float* __restrict__ loc, const float* __restrict__ att
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (cell[k] >= 0) dk[s][k] += sD[cell[k] * kWP8 + tq];
-          lds_barrier();                      // Dm read: clear W for the next pair
-          // each wave clears only the W columns it writes (its 16 queries) over every row W
-          // or Dm^T touched; no other wave's next build touches them (no barrier needed)
+          // Dm read: clear W for the next pair.  A wave's dots read only its own query columns
+          // (tq = 16 wave .. + 15), and it clears only those columns over every row W or Dm^T
+          // touched -- the columns its next build writes, so no other wave's access meets them
+          // before the next pair's first barrier: program order within the wave suffices
+          wave_sync();
           for (int rb = 0; rb < zr; rb += 16)
             *reinterpret_cast<float4*>(sW + (rb + zrow) * kWP8 + 16 * wave + 4 * (lane & 3)) = z4;
         }
