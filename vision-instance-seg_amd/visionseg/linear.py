@@ -653,7 +653,10 @@ class _ValueQueryProjFn(torch.autograd.Function):
         ctx.sink = sink
         if sink is not None:
             sink.arm()
-        return F.linear(h, wv, bv), F.linear(q, wp, bp)
+        # proj (256 -> 288 at the C2 encoder) on the token GEMM by the forward rule: 36.9 vs 44.3
+        # us per call; value (256 -> 256) ties (29.8 vs 28.9 us) and stays on the vendor GEMM
+        # (tools/r6/enc_gemm_bench.py, profiles/r6_enc_gemm_bench.txt)
+        return F.linear(h, wv, bv), _forward_gemm(q, wp, bp)
 
     @staticmethod
     def backward(ctx, gv, gp):
