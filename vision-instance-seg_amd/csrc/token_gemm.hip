@@ -465,19 +465,6 @@ __global__ void __launch_bounds__(256, 2) token_gemm_stream_kernel(const bf16* _
     const int n = n0 + 32 * w + 8 * g + 4 * hh;
     bvr[g] = (bias && n < N) ? *reinterpret_cast<const bf16x4_t*>(bias + n) : bf16x4_t{0, 0, 0, 0};
   }
-  // activation backward: the pre-activation (ReLU output) chunks of this thread's stores, one
-  // tile AHEAD (tile j's in ring slot j & 1): requested in the same position as the tile's
-  // own loads would be, so each tile finds them landed instead of waiting a round trip
-  uint4 pv0[GB ? SPT : 1], pv1[GB ? SPT : 1];
-  auto load_pre = [&](int j, uint4* pv) {
-    const int m0 = (g0 + j * G) * BM;
-#pragma unroll
-    for (int i = 0; i < SPT; ++i) {
-      const int idx = threadIdx.x + i * NT, row = idx / NCK, chunk = idx % NCK;
-      const int m = min(m0 + row, M - 1), n = min(n0 + chunk * 8, N - 8);   // always a load: counted waits
-      pv[i] = *reinterpret_cast<const uint4*>(Y2 + (size_t)m * N + n);
-    }
-  };
   for (int j = 0; j < NBUF - 1 && j < ntl; ++j) issue_x(j);
   wait_vm<0>();                                                        // W and the first tiles
   for (int j = 0; j < ntl; ++j) {
