@@ -3,7 +3,7 @@ GEMM + the activation backward kernel, HIP events (median of 20)."""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.environ.get("VS_ROOT") or os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "vision-instance-seg_amd")]
 import torch  # noqa: E402
 from visionseg import ops, _lib as L  # noqa: E402
