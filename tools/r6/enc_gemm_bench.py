@@ -48,6 +48,13 @@ def main():
         by = M * (N + K) * 2
         print(f"{name:10s} M={M} N={N:5d} K={K:5d}: vendor {tv:6.1f} us  token_gemm {tt:6.1f} us "
               f"({by / tt / 1e3:5.0f} GB/s)  max|diff| {e:.3g}", flush=True)
+    # fc1 + bias + ReLU: hipBLASLt RELU_BIAS epilogue vs the token GEMM's (VS_TGEMM_RELU)
+    x = torch.randn(M, 256, device=dev).to(bf)
+    w = (torch.randn(1024, 256, device=dev) * 256 ** -0.5).to(bf)
+    b = torch.randn(1024, device=dev).to(bf)
+    tv = timeit(lambda: torch._addmm_activation(b, x, w.t(), use_gelu=False))
+    tt = timeit(lambda: ops.token_gemm(x, w, b, relu=True))
+    print(f"fc1+relu   M={M} N= 1024 K=  256: vendor {tv:6.1f} us  token_gemm(relu) {tt:6.1f} us", flush=True)
     # dX: dh = gp Wp + gv Wv (K = 288 / 256 -> 256)
     for name, Nred in (("proj dX", 288), ("value dX", 256), ("fc2 dX", 1024)):
         g = torch.randn(M, Nred, device=dev).to(bf)
