@@ -4,7 +4,8 @@ operands in the Infinity Cache from the previous one.  GB/s = algorithmic bytes 
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "vision-instance-seg_amd"))
+sys.path.insert(0, os.path.join(os.environ.get("VS_ROOT") or os.path.join(os.path.dirname(__file__), "..", ".."),
+                                "vision-instance-seg_amd"))
 import torch
 from visionseg import _lib as L
 
